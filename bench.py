@@ -1,0 +1,176 @@
+"""bench.py -- SVGD particle-updates/s at n=65536, d=256 (BASELINE.json metric).
+
+Workload (BASELINE.json configs[3]): dist-logreg via
+DistSampler, exchange=all_scores (all-gather of particles + all-reduce of the
+shard-local scores of all n particles), median-heuristic bandwidth, Jacobi
+order, n = 65536 particles of d = 256 (p = 255 weights), N_global = 16384
+synthetic data rows sharded N/S, the n particles sharded n/S per GPU.
+One step = exchange + scores + median (exact radix select over n^2 distances)
++ phi (K.[X|S] on MFMA) + x += eps*phi for all n particles.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU, RCCL)
+
+Prints ONE JSON line (rank 0).  value = n*K / max-over-ranks wall time of the K
+timed steps (whole job).  roofline: the dominant kernel (phi_mm, the fused
+exp + K.[Xc|S] MFMA GEMM) -- algorithmic 4*m*n*d flop per launch / its mean
+HIP-event duration, against the 157.3 TF fp32 MFMA peak.  cpu_baseline: the
+reference algorithm's per-pair autograd loop (oracle/loop_baseline.py, a port)
+timed on this host on a bounded sample, rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "dist-svgd_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_FP32_MFMA_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, spec
+PEAK_HBM_GBS = 8000.0
+
+
+def synthetic_data(N, p, seed=0):
+    rs = np.random.RandomState(seed)
+    x = rs.randn(N, p).astype(np.float32) / np.sqrt(p)
+    w = np.random.RandomState(seed + 1).randn(p)
+    z = x @ w + np.random.RandomState(seed + 2).logistic(size=N)
+    t = np.where(z > 0, 1.0, -1.0).astype(np.float32)
+    return x, t
+
+
+def cpu_baseline(n, d, x_local, t_local, budget_s):
+    """Reference-algorithm per-pair loop (port) on a bounded sample."""
+    from oracle import loop_baseline as L
+    from oracle import cpu_vectorized as V
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(1)
+    rs = np.random.RandomState(1)
+    X = rs.randn(n, d).astype(np.float32) * 0.1
+    logp = L.logreg_logp(x_local, t_local)
+    sec_per_update, updates, pairs = L.time_particle_updates(X, logp, h=float(d), m=1,
+                                                             budget_s=budget_s)
+    out = {"value": 1.0 / sec_per_update, "unit": "particle-updates/s", "cores": 1,
+           "kind": "port",
+           "sample": "reference per-pair autograd loop (kernel, grad kernel, grad logp per pair; "
+                     "oracle/loop_baseline.py), %d pair terms of one n=%d particle update timed, "
+                     "extrapolated x n; logreg target N_local=%d" % (pairs, n, x_local.shape[0])}
+    # vectorised torch-CPU restatement on all host cores (extra, for scale)
+    nt = min(cores, 64)
+    torch.set_num_threads(nt)
+    S = rs.randn(n, d).astype(np.float32)
+    spu, rows = V.time_rows(X, S, float(d), rows=4096, chunk=512, budget_s=budget_s / 2)
+    out["vectorized_value"] = 1.0 / spu
+    out["vectorized_cores"] = nt
+    out["vectorized_sample"] = "torch-CPU fp32 phi for %d rows against all n=%d (oracle/cpu_vectorized.py)" % (rows, n)
+    out["host_cores_available"] = cores
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--d", type=int, default=256)
+    ap.add_argument("--N", type=int, default=16384, help="global data rows")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import dsvgd
+    from dsvgd.engine import StageTimer
+
+    n, d, Ng = args.n, args.d, args.N
+    p = d - 1
+    per_data = Ng // world
+    x, t = synthetic_data(Ng, p)
+    xl, tl = x[rank * per_data:(rank + 1) * per_data], t[rank * per_data:(rank + 1) * per_data]
+    gen = torch.Generator(device="cpu").manual_seed(0)
+    parts = (0.1 * torch.randn(n, d, generator=gen)).to(dev)
+    sampler = dsvgd.DistSampler(rank, world, dsvgd.targets.LogisticRegression(xl, tl),
+                                dsvgd.RBF("median"), parts, per_data, per_data * world,
+                                exchange_particles=True, exchange_scores=True,
+                                include_wasserstein=False, order="jacobi")
+    eps = 1e-4
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        sampler.make_step(eps)
+    torch.cuda.synchronize()
+    # per-stage HIP events ride along the timed steps (same stream as the kernels)
+    timer = StageTimer()
+    sampler.timer = timer
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sampler.make_step(eps)
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    sampler.timer = None
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    stages = {k: float(np.mean(v)) for k, v in timer.summary().items()}
+    assert bool(torch.isfinite(sampler._work).all()), "non-finite particles"
+
+    m = n // world
+    phi_ms = stages["phi_mm"]
+    flops = 4.0 * m * n * d
+    achieved = flops / (phi_ms * 1e-3) / 1e12
+    out = {
+        "metric": "SVGD particle-updates/sec (n=65536,d=256) at 1/2/4/8 GPUs + % MFMA/HBM roofline",
+        "value": n * args.steps / el,
+        "unit": "particle-updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * el / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (logreg data N(0,1/p), labels from a random w + logistic noise; "
+                "particles 0.1*N(0,1))",
+        "config": {"workload": "dist-logreg DistSampler all_scores, Jacobi, median bandwidth",
+                   "n": n, "d": d, "N_global": Ng, "parallelism": "dp%d" % world,
+                   "particles_per_gpu": m},
+        "roofline": {"bound": "mfma", "kernel": "phi_mm (nn_kernel<4,true>)",
+                     "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
+                     "flop_per_launch": flops, "avg_launch_ms": phi_ms},
+        "stages_ms": stages,
+        "step_flop_6n2d_frac": (6.0 * m * n * d) / (1e-3 * el / args.steps) / 1e12 / PEAK_FP32_MFMA_TFLOPS,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(n, d, xl, tl, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,51 @@
+// common.hpp -- shared helpers for the gfx950 SVGD kernels (libdsvgd_hip.so).
+//
+// Written for CDNA4 only: 64-lane waves, fp32-input MFMA
+// (v_mfma_f32_32x32x2_f32), 160 KiB LDS per CU.  No CUDA / hipify layer.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdio>
+#include <string>
+
+#include "../../include/dsvgd.h"
+
+namespace dsvgd {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+constexpr float kLog2e = 1.4426950408889634f;
+
+// ---- error plumbing (thread-local message, negative return codes) --------
+void set_error(const char* fmt, ...);
+int fail_arg(const char* what);
+int check_launch(const char* kernel);
+
+inline int64_t roundup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+// 32x32x2 f32 MFMA: lane l holds A[l&31][l>>5], B[l>>5][l&31]; the 16 result
+// registers hold C[(r&3) + 8*(r>>2) + 4*(l>>5)][l&31]  (r = register index).
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int c_row(int reg, int lane) {
+  return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace dsvgd
+
+#define DSVGD_REQUIRE(cond, msg)          \
+  do {                                    \
+    if (!(cond)) return dsvgd::fail_arg(msg); \
+  } while (0)

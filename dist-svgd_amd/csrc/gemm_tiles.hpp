@@ -1,0 +1,238 @@
+// gemm_tiles.hpp -- the two fp32 MFMA tile engines every contraction of the
+// SVGD step runs on (v_mfma_f32_32x32x2_f32, exact fp32: a k-ordered fmaf
+// chain per output, MI355X_MICROARCH.md "Matrix cores").
+//
+//  * NT engine  C[BM x BN] = A[BM x K] . B[BN x K]^T, A and B row-major
+//    (both operands are rows of the particle matrix: the Gram X X^T, and the
+//    logistic-regression Z = W Xd^T).  Register-staged single LDS buffer, the
+//    next K-tile in flight during the MFMAs (2 barriers per K-step; 3 blocks
+//    per CU cover the barrier gaps).
+//  * NN engine  C[BM x BC] = f(A)[BM x K] . B[K x BC], A in the "panel"
+//    layout below, f = exp2(scale * a) (the fused RBF kernel) or identity.
+//    Double-buffered LDS, one barrier per K-step, one 256-thread block per CU
+//    holding a 128 x 512 fp32 accumulator (256 AGPRs per lane).
+//
+// Both read fragments with ds_read_b128: within a group of 4 consecutive
+// MFMAs, lane (r = l&31, h = l>>5) feeds k = 8g + 4h + t to MFMA t, so one
+// 16-byte LDS read serves 4 MFMAs (the k order inside a 8-wide group is
+// permuted identically for A and B, which leaves every dot product intact).
+//
+// Panel layout of an M x N matrix produced by the NT engine and consumed by
+// the NN engine (D and the logreg G): 128-row x 16-column panels, each a
+// contiguous row-major [128][16] block, panels ordered row-panel-major:
+//     off(i, j) = ((i/128) * (Npad/16) + j/16) * 2048 + (i%128) * 16 + j%16.
+// One NN K-step then streams exactly one contiguous 8 KiB panel.
+#pragma once
+#include "common.hpp"
+
+namespace dsvgd {
+
+constexpr int kPanelRows = 128;
+constexpr int kPanelCols = 16;
+constexpr int kPanelElems = kPanelRows * kPanelCols;
+
+__host__ __device__ inline int64_t panel_off(int64_t i, int64_t j, int64_t npad) {
+  return ((i >> 7) * (npad >> 4) + (j >> 4)) * kPanelElems + (i & 127) * 16 + (j & 15);
+}
+
+// ------------------------------------------------------------ NT engine ----
+// Block = WM x WN waves, each wave TM x TN tiles of 32x32; BK = 32.
+template <int TM, int TN, int WM, int WN>
+struct NTTile {
+  static constexpr int kThreads = 64 * WM * WN;
+  static constexpr int BM = 32 * TM * WM;
+  static constexpr int BN = 32 * TN * WN;
+  static constexpr int BK = 32;
+  static constexpr int LDK = BK + 4;  // 144-B rows: 16 consecutive rows hit 16 distinct 16-B slots
+  static constexpr int LA = BM * BK / 4 / kThreads;  // float4 loads per thread (A)
+  static constexpr int LB = BN * BK / 4 / kThreads;
+  static constexpr int kSmemFloats = (BM + BN) * LDK;
+
+  f32x16 acc[TM][TN];
+  f32x4 ra[LA], rb[LB];
+
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+  }
+
+  __device__ __forceinline__ void load(const float* __restrict__ A, int64_t lda,
+                                       const float* __restrict__ B, int64_t ldb, int k0) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < LA; ++u) {
+      const int f = t + u * kThreads, row = f >> 3, c4 = f & 7;
+      ra[u] = *reinterpret_cast<const f32x4*>(A + (int64_t)row * lda + k0 + 4 * c4);
+    }
+#pragma unroll
+    for (int u = 0; u < LB; ++u) {
+      const int f = t + u * kThreads, row = f >> 3, c4 = f & 7;
+      rb[u] = *reinterpret_cast<const f32x4*>(B + (int64_t)row * ldb + k0 + 4 * c4);
+    }
+  }
+
+  __device__ __forceinline__ void store(float* sA, float* sB) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < LA; ++u) {
+      const int f = t + u * kThreads, row = f >> 3, c4 = f & 7;
+      *reinterpret_cast<f32x4*>(sA + row * LDK + 4 * c4) = ra[u];
+    }
+#pragma unroll
+    for (int u = 0; u < LB; ++u) {
+      const int f = t + u * kThreads, row = f >> 3, c4 = f & 7;
+      *reinterpret_cast<f32x4*>(sB + row * LDK + 4 * c4) = rb[u];
+    }
+  }
+
+  __device__ __forceinline__ void compute(const float* sA, const float* sB, int wm, int wn) {
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int g = 0; g < BK / 8; ++g) {
+      f32x4 a[TM], b[TN];
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+        a[mi] = *reinterpret_cast<const f32x4*>(sA + (wm * 32 * TM + mi * 32 + r) * LDK + 8 * g +
+                                                4 * h);
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+        b[ni] = *reinterpret_cast<const f32x4*>(sB + (wn * 32 * TN + ni * 32 + r) * LDK + 8 * g +
+                                                4 * h);
+#pragma unroll
+      for (int t4 = 0; t4 < 4; ++t4)
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = mfma32(a[mi][t4], b[ni][t4], acc[mi][ni]);
+    }
+  }
+
+  // Full K loop: A, B point at the block's first row; K % BK == 0.
+  __device__ __forceinline__ void run(const float* __restrict__ A, int64_t lda,
+                                      const float* __restrict__ B, int64_t ldb, int K, float* smem) {
+    float* sA = smem;
+    float* sB = smem + BM * LDK;
+    const int w = threadIdx.x >> 6, wm = w / WN, wn = w % WN;
+    zero();
+    load(A, lda, B, ldb, 0);
+    for (int k0 = 0; k0 < K; k0 += BK) {
+      __syncthreads();
+      store(sA, sB);
+      __syncthreads();
+      if (k0 + BK < K) load(A, lda, B, ldb, k0 + BK);
+      compute(sA, sB, wm, wn);
+    }
+  }
+};
+
+// ------------------------------------------------------------ NN engine ----
+// BM = 128 rows (TM = 4), 4 waves side by side along the columns, each
+// 128 x 32*TN; K-step = one 16-column panel of A and 16 rows of B.
+template <int TN, bool EXP>
+struct NNTile {
+  static constexpr int kThreads = 256;
+  static constexpr int TM = 4;
+  static constexpr int BM = 128;
+  static constexpr int BC = 128 * TN;
+  static constexpr int BJ = 16;
+  static constexpr int LDA = BJ + 4;  // 80-B rows: conflict-free ds_read_b128
+  static constexpr int SA = BM * LDA;
+  static constexpr int SB = BJ * BC;
+  static constexpr int kStage = SA + SB;
+  static constexpr int kSmemFloats = 2 * kStage;
+  static constexpr int LA = BM * BJ / 4 / kThreads;  // 2
+  static constexpr int LB = BJ * BC / 4 / kThreads;  // 2*TN
+
+  f32x16 acc[TM][TN];
+  f32x4 ra[LA], rb[LB];
+  float rsum[TM];
+
+  __device__ __forceinline__ void load(const float* __restrict__ Apanels, const float* __restrict__ B,
+                                       int64_t ldb, int64_t j0) {
+    const int t = threadIdx.x;
+    const float* ap = Apanels + (j0 >> 4) * kPanelElems;  // contiguous 8 KiB panel
+#pragma unroll
+    for (int u = 0; u < LA; ++u) ra[u] = *reinterpret_cast<const f32x4*>(ap + 4 * (t + u * kThreads));
+#pragma unroll
+    for (int u = 0; u < LB; ++u) {
+      const int f = t + u * kThreads, row = f / (BC / 4), c4 = f % (BC / 4);
+      rb[u] = *reinterpret_cast<const f32x4*>(B + (j0 + row) * ldb + 4 * c4);
+    }
+  }
+
+  __device__ __forceinline__ void store(float* st) {
+    const int t = threadIdx.x;
+    float* sA = st;
+    float* sB = st + SA;
+#pragma unroll
+    for (int u = 0; u < LA; ++u) {
+      const int f = t + u * kThreads, row = f >> 2, c4 = f & 3;
+      *reinterpret_cast<f32x4*>(sA + row * LDA + 4 * c4) = ra[u];
+    }
+#pragma unroll
+    for (int u = 0; u < LB; ++u) *reinterpret_cast<f32x4*>(sB + 4 * (t + u * kThreads)) = rb[u];
+  }
+
+  __device__ __forceinline__ void compute(const float* st, int wc, float scale) {
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+    const float* sA = st;
+    const float* sB = st + SA;
+#pragma unroll
+    for (int g = 0; g < BJ / 8; ++g) {
+      f32x4 a[TM];
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        a[mi] = *reinterpret_cast<const f32x4*>(sA + (mi * 32 + r) * LDA + 8 * g + 4 * h);
+        if (EXP) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) a[mi][q] = __builtin_amdgcn_exp2f(a[mi][q] * scale);
+          rsum[mi] += (a[mi][0] + a[mi][1]) + (a[mi][2] + a[mi][3]);
+        }
+      }
+#pragma unroll
+      for (int t4 = 0; t4 < 4; ++t4) {
+        float b[TN];
+        const float* brow = sB + (8 * g + 4 * h + t4) * BC + wc * 32 * TN + r;
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni) b[ni] = brow[ni * 32];
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = mfma32(a[mi][t4], b[ni], acc[mi][ni]);
+      }
+    }
+  }
+
+  // Apanels: the block's row-panel (128 rows x K, panel layout); B: K x BC
+  // (row-major, ldb, already offset to the block's first column).
+  __device__ __forceinline__ void run(const float* __restrict__ Apanels, const float* __restrict__ B,
+                                      int64_t ldb, int64_t K, float scale, float* smem) {
+    const int wc = threadIdx.x >> 6;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      rsum[mi] = 0.f;
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[mi][ni][q] = 0.f;
+    }
+    load(Apanels, B, ldb, 0);
+    store(smem);
+    __syncthreads();
+    int cur = 0;
+    for (int64_t j0 = 0; j0 < K; j0 += BJ) {
+      const bool more = j0 + BJ < K;
+      if (more) load(Apanels, B, ldb, j0 + BJ);
+      compute(smem + cur * kStage, wc, scale);
+      if (more) store(smem + (cur ^ 1) * kStage);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+};
+
+}  // namespace dsvgd

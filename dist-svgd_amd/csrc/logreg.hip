@@ -1,0 +1,163 @@
+// logreg.hip -- batched score of the Bayesian logistic-regression posterior
+// of experiments/logreg.py:45-58 for ALL n particles at once, replacing the
+// per-particle autograd _dlogp (dsvgd/sampler.py:28-33, distsampler.py:77-82):
+//
+//   x = [log a, w],  log p = log Gamma(1,1)(a) + log N(w; 0, I/a) - sum_q log(1+exp(-t_q xd_q.w))
+//   d/dx0 = -a + p/2 - (a/2)|w|^2          d/dw = -a w + sum_q t_q xd_q sigma(-t_q xd_q.w)
+//
+// as Z = W Xd^T (NT MFMA engine, sigmoid epilogue -> G in panel layout) and
+// G Xd (NN MFMA engine); 4 n N p flop, MFMA-bound.
+#include <cmath>
+
+#include "gemm_tiles.hpp"
+
+namespace dsvgd {
+
+int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, int64_t cols,
+            const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
+            hipStream_t s);
+
+static int64_t nn_cols(int64_t w) {
+  if (w <= 128) return 128;
+  if (w <= 256) return 256;
+  return roundup(w, 512);
+}
+
+struct LogregWs {
+  int64_t n_pad, N_pad, pp, ldb;
+  size_t off_w, off_xd, off_t, off_g, off_gw, total;
+};
+
+static LogregWs logreg_ws(int64_t n, int64_t N, int64_t p) {
+  LogregWs w;
+  w.n_pad = roundup(n, 128);
+  w.N_pad = roundup(N, 128);
+  w.pp = roundup(p < 1 ? 1 : p, 32);
+  w.ldb = nn_cols(w.pp);
+  size_t o = 0;
+  auto take = [&](size_t floats) {
+    size_t at = o;
+    o += roundup((int64_t)(floats * sizeof(float)), 256);
+    return at;
+  };
+  w.off_w = take((size_t)w.n_pad * w.ldb);
+  w.off_xd = take((size_t)w.N_pad * w.ldb);
+  w.off_t = take((size_t)w.N_pad);
+  w.off_g = take((size_t)w.n_pad * w.N_pad);
+  w.off_gw = take((size_t)w.n_pad * w.ldb);
+  w.total = o;
+  return w;
+}
+
+// dst[r][c] = src[r][c0 + c] for r < rows, c < cols; zero elsewhere (rows_pad x ldd)
+__global__ __launch_bounds__(256) void pad_copy_kernel(const float* __restrict__ src, int64_t lds,
+                                                       int64_t c0, int64_t rows, int64_t cols,
+                                                       int64_t rows_pad, float* __restrict__ dst,
+                                                       int64_t ldd) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= rows_pad * ldd) return;
+  const int64_t r = t / ldd, c = t % ldd;
+  dst[t] = (r < rows && c < cols) ? src[r * lds + c0 + c] : 0.f;
+}
+
+using ZTile = NTTile<2, 2, 2, 2>;
+
+__device__ __forceinline__ float sigmoidf_stable(float u) {
+  if (u >= 0.f) return 1.f / (1.f + expf(-u));
+  const float e = expf(u);
+  return e / (1.f + e);
+}
+
+// G[j][q] = t_q sigma(-t_q (w_j . xd_q)), zero for padded q; panel layout.
+__global__ __launch_bounds__(256) void logreg_z_kernel(const float* __restrict__ W,
+                                                       const float* __restrict__ Xd, int64_t ldb,
+                                                       int pp, const float* __restrict__ tp,
+                                                       int64_t N, int64_t N_pad,
+                                                       float* __restrict__ G) {
+  __shared__ __attribute__((aligned(16))) float smem[ZTile::kSmemFloats];
+  const int64_t i0 = (int64_t)blockIdx.y * ZTile::BM, q0 = (int64_t)blockIdx.x * ZTile::BN;
+  ZTile tile;
+  tile.run(W + i0 * ldb, ldb, Xd + q0 * ldb, ldb, pp, smem);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int64_t q = q0 + wn * 64 + ni * 32 + (lane & 31);
+      const float tq = tp[q];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t i = i0 + wm * 64 + mi * 32 + c_row(r, lane);
+        const float z = tile.acc[mi][ni][r];
+        G[panel_off(i, q, N_pad)] = (q < N) ? tq * sigmoidf_stable(-tq * z) : 0.f;
+      }
+    }
+}
+
+// one wave per particle row
+__global__ __launch_bounds__(256) void logreg_finish_kernel(const float* __restrict__ X,
+                                                            int64_t ldx, int64_t n, int64_t p,
+                                                            const float* __restrict__ GW,
+                                                            int64_t ldg, float scale,
+                                                            float* __restrict__ S, int64_t lds) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= n) return;
+  const float* x = X + j * ldx;
+  const float a = expf(x[0]);
+  float w2 = 0.f;
+  for (int64_t c = lane; c < p; c += 64) w2 = fmaf(x[1 + c], x[1 + c], w2);
+  w2 = warp_sum(w2);
+  for (int64_t c = lane; c < p; c += 64) S[j * lds + 1 + c] = scale * (GW[j * ldg + c] - a * x[1 + c]);
+  if (lane == 0) S[j * lds] = scale * (-a + 0.5f * (float)p - 0.5f * a * w2);
+}
+
+}  // namespace dsvgd
+
+using namespace dsvgd;
+
+extern "C" {
+
+size_t dsvgd_logreg_workspace_bytes(int64_t n, int64_t N, int64_t p) {
+  return logreg_ws(n, N, p).total;
+}
+
+int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const float* Xd,
+                       int64_t ldxd, const float* t, int64_t N, float scale, float* S, int64_t lds,
+                       void* workspace, void* stream) {
+  DSVGD_REQUIRE(X && Xd && t && S && workspace, "null pointer");
+  DSVGD_REQUIRE(n > 0 && d >= 2 && N > 0 && ldx >= d && lds >= d && ldxd >= d - 1, "sizes");
+  DSVGD_REQUIRE(((uintptr_t)workspace & 255) == 0, "workspace must be 256-byte aligned");
+  const int64_t p = d - 1;
+  const LogregWs w = logreg_ws(n, N, p);
+  DSVGD_REQUIRE(w.n_pad / 128 <= 65535, "too many row tiles");
+  char* base = (char*)workspace;
+  float* Wp = (float*)(base + w.off_w);
+  float* Xdp = (float*)(base + w.off_xd);
+  float* tp = (float*)(base + w.off_t);
+  float* G = (float*)(base + w.off_g);
+  float* GW = (float*)(base + w.off_gw);
+  hipStream_t s = (hipStream_t)stream;
+  int64_t tot = w.n_pad * w.ldb;
+  hipLaunchKernelGGL(pad_copy_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, X, ldx, 1, n, p,
+                     w.n_pad, Wp, w.ldb);
+  int rc = check_launch("pad_copy(W)");
+  if (rc) return rc;
+  tot = w.N_pad * w.ldb;
+  hipLaunchKernelGGL(pad_copy_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Xd, ldxd, 0, N, p,
+                     w.N_pad, Xdp, w.ldb);
+  if ((rc = check_launch("pad_copy(Xd)"))) return rc;
+  hipLaunchKernelGGL(pad_copy_kernel, dim3((w.N_pad + 255) / 256), dim3(256), 0, s, t, 1, 0, N, 1,
+                     w.N_pad, tp, 1);
+  if ((rc = check_launch("pad_copy(t)"))) return rc;
+  hipLaunchKernelGGL(logreg_z_kernel, dim3(w.N_pad / 128, w.n_pad / 128), dim3(256), 0, s, Wp, Xdp,
+                     w.ldb, (int)w.pp, tp, N, w.N_pad, G);
+  if ((rc = check_launch("logreg_z"))) return rc;
+  if ((rc = nn_gemm(false, G, w.N_pad, Xdp, w.ldb, w.ldb, nullptr, GW, w.ldb, nullptr, n, s)))
+    return rc;
+  hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,
+                     w.ldb, scale, S, lds);
+  return check_launch("logreg_finish");
+}
+
+}  // extern "C"

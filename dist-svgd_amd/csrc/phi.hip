@@ -1,0 +1,189 @@
+// phi.hip -- the SVGD direction
+//     phi_i = 1/n sum_j [ k_ij s_j + (2/h) k_ij (x_i - x_j) ],  k_ij = exp(-D_ij / h)
+//           = 1/n [ (K S)_i + (2/h) (r_i x_i - (K X)_i) ],          r_i = sum_j k_ij
+// (dsvgd/sampler.py:35-40, dsvgd/distsampler.py:84-101 with the RBF kernel of
+// experiments/logreg.py:60-61 and its autograd gradient folded in closed form).
+//
+// phi_mm: K [Xc | S] on the NN MFMA engine with the exp fused into the A
+// operand; D streams from HBM once (panel layout), [Xc|S] re-reads hit L2/MALL.
+// Roofline: 2 * 128 * BC flop per 8 KiB D panel -> MFMA-bound for d >= 64.
+#include <cmath>
+
+#include "gemm_tiles.hpp"
+
+namespace dsvgd {
+
+template <int TN, bool EXP>
+__global__ __launch_bounds__(256) void nn_kernel(const float* __restrict__ A, int64_t a_npad,
+                                                 const float* __restrict__ B, int64_t ldb,
+                                                 int64_t K, const dsvgd_select_state* __restrict__ st,
+                                                 float* __restrict__ C, int64_t ldc,
+                                                 float* __restrict__ rowsum, int64_t m) {
+  using Tile = NNTile<TN, EXP>;
+  __shared__ __attribute__((aligned(16))) float smem[Tile::kSmemFloats];
+  const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
+  const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
+  float scale = 0.f;
+  if (EXP) scale = -st->inv_h * kLog2e;
+  Tile tile;
+  tile.run(A + (i0 >> 7) * (a_npad >> 4) * kPanelElems, B + c0, ldb, K, scale, smem);
+
+  const int lane = threadIdx.x & 63, wc = threadIdx.x >> 6;
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+      const int64_t col = c0 + wc * 32 * TN + ni * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = i0 + mi * 32 + c_row(r, lane);
+        if (row < m) C[row * ldc + col] = tile.acc[mi][ni][r];
+      }
+    }
+  if (EXP && rowsum && blockIdx.x == 0 && wc == 0) {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const float v = tile.rsum[mi] + __shfl_xor(tile.rsum[mi], 32, 64);
+      const int64_t row = i0 + mi * 32 + lane;
+      if (lane < 32 && row < m) rowsum[row] = v;
+    }
+  }
+}
+
+// phi[i][c] = inv_n (KS[i][c] + (2/h)(r_i xc[i][c] - KX[i][c])); X[i][c] += step phi.
+__global__ __launch_bounds__(256) void phi_finish_kernel(
+    const float* __restrict__ KY, int64_t ldk, const float* __restrict__ rowsum,
+    const float* __restrict__ Y, int64_t ldy, int64_t row0, int64_t m, int64_t d, int64_t dp,
+    const dsvgd_select_state* __restrict__ st, float inv_n, float step, float* __restrict__ phi,
+    int64_t ldphi, float* __restrict__ X, int64_t ldx) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= m * d) return;
+  const int64_t i = t / d, c = t % d;
+  const float two_inv_h = 2.f * st->inv_h;
+  const float kx = KY[i * ldk + c], ks = KY[i * ldk + dp + c];
+  const float xc = Y[(row0 + i) * ldy + c];
+  const float p = inv_n * (ks + two_inv_h * (rowsum[i] * xc - kx));
+  if (phi) phi[i * ldphi + c] = p;
+  if (X) X[i * ldx + c] += step * p;
+}
+
+// Gauss-Seidel row update (reference order, exact differences, no Gram):
+// one block; j in chunks of 256 (one per thread) -> k_j in LDS -> columns.
+__global__ __launch_bounds__(256) void phi_row_kernel(float* __restrict__ X, int64_t ldx,
+                                                      const float* __restrict__ S, int64_t lds,
+                                                      int64_t n, int64_t d, int64_t i,
+                                                      const dsvgd_select_state* __restrict__ st,
+                                                      float step, float* __restrict__ phi_out) {
+  extern __shared__ __attribute__((aligned(16))) float dyn[];
+  float* xi = dyn;            // d
+  float* acc = dyn + d;       // d
+  float* kb = dyn + 2 * d;    // 256
+  const int t = threadIdx.x;
+  const float inv_h = st->inv_h;
+  for (int64_t c = t; c < d; c += 256) {
+    xi[c] = X[i * ldx + c];
+    acc[c] = 0.f;
+  }
+  __syncthreads();
+  for (int64_t j0 = 0; j0 < n; j0 += 256) {
+    const int64_t j = j0 + t;
+    float k = 0.f;
+    if (j < n) {
+      float s2 = 0.f;
+      for (int64_t c = 0; c < d; ++c) {
+        const float df = X[j * ldx + c] - xi[c];
+        s2 = fmaf(df, df, s2);
+      }
+      k = expf(-s2 * inv_h);
+    }
+    kb[t] = k;
+    __syncthreads();
+    const int64_t nj = min((int64_t)256, n - j0);
+    for (int64_t c = t; c < d; c += 256) {
+      float a = acc[c];
+      const float x = xi[c];
+      for (int64_t q = 0; q < nj; ++q) {
+        const int64_t jj = j0 + q;
+        a += kb[q] * S[jj * lds + c] + (2.f * inv_h) * kb[q] * (x - X[jj * ldx + c]);
+      }
+      acc[c] = a;
+    }
+    __syncthreads();
+  }
+  const float inv_n = 1.f / (float)n;
+  for (int64_t c = t; c < d; c += 256) {
+    const float p = inv_n * acc[c];
+    if (phi_out) phi_out[c] = p;
+    X[i * ldx + c] = xi[c] + step * p;
+  }
+}
+
+template <int TN>
+int launch_nn(bool exp_, const float* A, int64_t a_npad, const float* B, int64_t ldb, int64_t K,
+              const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
+              int64_t cols, hipStream_t s) {
+  const dim3 grid(cols / (128 * TN), roundup(m, 128) / 128);
+  if (exp_)
+    hipLaunchKernelGGL((nn_kernel<TN, true>), grid, dim3(256), 0, s, A, a_npad, B, ldb, K, st, C,
+                       ldc, rowsum, m);
+  else
+    hipLaunchKernelGGL((nn_kernel<TN, false>), grid, dim3(256), 0, s, A, a_npad, B, ldb, K, st, C,
+                       ldc, rowsum, m);
+  return check_launch("nn_kernel");
+}
+
+// C[m x cols] = f(A) B with A in panel layout (m_pad x K), B row-major K x cols.
+int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, int64_t cols,
+            const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
+            hipStream_t s) {
+  if (cols % 512 == 0) return launch_nn<4>(exp_, A, K, B, ldb, K, st, C, ldc, rowsum, m, cols, s);
+  if (cols % 256 == 0) return launch_nn<2>(exp_, A, K, B, ldb, K, st, C, ldc, rowsum, m, cols, s);
+  return launch_nn<1>(exp_, A, K, B, ldb, K, st, C, ldc, rowsum, m, cols, s);
+}
+
+}  // namespace dsvgd
+
+using namespace dsvgd;
+
+extern "C" {
+
+int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t m, int64_t n,
+                 const dsvgd_select_state* st, float* KY, int64_t ldk, float* rowsum,
+                 void* stream) {
+  DSVGD_REQUIRE(D && Y && st && KY && rowsum, "null pointer");
+  DSVGD_REQUIRE(m > 0 && n > 0, "sizes");
+  const int64_t n_pad = roundup(n, 128);
+  DSVGD_REQUIRE(ldd == n_pad, "ldd must equal roundup(n,128) (panel layout)");
+  DSVGD_REQUIRE(ldy % 128 == 0 && ldk >= ldy, "ldy must be a multiple of 128, ldk >= ldy");
+  DSVGD_REQUIRE(((uintptr_t)Y & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
+  DSVGD_REQUIRE(roundup(m, 128) / 128 <= 65535, "too many row tiles");
+  return nn_gemm(true, D, n_pad, Y, ldy, ldy, st, KY, ldk, rowsum, m, (hipStream_t)stream);
+}
+
+int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, const float* Y,
+                     int64_t ldy, int64_t row0, int64_t m, int64_t d, int64_t dp,
+                     const dsvgd_select_state* st, float inv_n, float step, float* phi,
+                     int64_t ldphi, float* X, int64_t ldx, void* stream) {
+  DSVGD_REQUIRE(KY && rowsum && Y && st, "null pointer");
+  DSVGD_REQUIRE(m > 0 && d > 0 && dp >= d && ldk >= 2 * dp && ldy >= 2 * dp, "sizes");
+  DSVGD_REQUIRE(!phi || ldphi >= d, "ldphi");
+  DSVGD_REQUIRE(!X || ldx >= d, "ldx");
+  hipLaunchKernelGGL(phi_finish_kernel, dim3((m * d + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, KY, ldk, rowsum, Y, ldy, row0, m, d, dp, st, inv_n,
+                     step, phi, ldphi, X, ldx);
+  return check_launch("phi_finish");
+}
+
+int dsvgd_phi_row(float* X, int64_t ldx, const float* S, int64_t lds, int64_t n_int, int64_t d,
+                  int64_t i, const dsvgd_select_state* st, float step, float* phi_out,
+                  void* stream) {
+  DSVGD_REQUIRE(X && S && st, "null pointer");
+  DSVGD_REQUIRE(n_int > 0 && d > 0 && i >= 0 && i < n_int && ldx >= d && lds >= d, "sizes");
+  DSVGD_REQUIRE(d <= 8064, "phi_row supports d <= 8064 (64 KiB LDS)");
+  const size_t shm = (size_t)(2 * d + 256) * sizeof(float);
+  hipLaunchKernelGGL(phi_row_kernel, dim3(1), dim3(256), shm, (hipStream_t)stream, X, ldx, S, lds,
+                     n_int, d, i, st, step, phi_out);
+  return check_launch("phi_row");
+}
+
+}  // extern "C"

@@ -1,0 +1,211 @@
+// prep.hip -- ABI meta, error plumbing, particle preparation (mean, pack),
+// elementwise target scores.  Bandwidth: HBM (all O(n d) streams).
+#include <cstdarg>
+#include <cmath>
+
+#include "common.hpp"
+
+namespace dsvgd {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int fail_arg(const char* what) {
+  set_error("invalid argument: %s", what);
+  return DSVGD_E_ARG;
+}
+
+int check_launch(const char* kernel) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s launch failed: %s", kernel, hipGetErrorString(e));
+    return DSVGD_E_LAUNCH;
+  }
+  return DSVGD_OK;
+}
+
+// ---------------------------------------------------------------- mean ----
+// Deterministic two-level column sum: block b sums rows [b*R, (b+1)*R) of a
+// 64-column stripe into partial[b][c]; the second kernel sums the partials in
+// block order.  (Float atomics would make the centring -- and so the median
+// bits -- vary from run to run.)
+constexpr int kMeanRows = 512;
+
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ X,
+                                                             int64_t ldx, int64_t n, int64_t d,
+                                                             float* __restrict__ partial) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;  // 4 row groups
+  const int64_t r0 = (int64_t)blockIdx.x * kMeanRows;
+  const int64_t r1 = min(r0 + kMeanRows, n);
+  float s = 0.f;
+  if (c < d)
+    for (int64_t r = r0 + rg; r < r1; r += 4) s += X[r * ldx + c];
+  red[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && c < d)
+    partial[(int64_t)blockIdx.x * d + c] =
+        ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ partial,
+                                                           int64_t nb, int64_t n, int64_t d,
+                                                           float* __restrict__ mean) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= d) return;
+  float s = 0.f;
+  for (int64_t b = 0; b < nb; ++b) s += partial[b * d + c];
+  mean[c] = s / (float)n;
+}
+
+// ---------------------------------------------------------------- pack ----
+// One wave per row: Y[j] = [X[j]-mean (dp cols) | scale*S[j] (dp cols) | 0],
+// norms[j] = |X[j]-mean|^2.  Rows j >= n are zero.
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ X, int64_t ldx,
+                                                   const float* __restrict__ S, int64_t lds,
+                                                   float scale, const float* __restrict__ mean,
+                                                   int64_t n, int64_t d, int64_t rows_pad,
+                                                   int64_t dp, float* __restrict__ Y, int64_t ldy,
+                                                   float* __restrict__ norms) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= rows_pad) return;
+  float* y = Y + j * ldy;
+  float nrm = 0.f;
+  if (j < n) {
+    for (int64_t c = lane; c < ldy; c += 64) {
+      float v = 0.f;
+      if (c < d) {
+        v = X[j * ldx + c] - mean[c];
+        nrm = fmaf(v, v, nrm);
+      } else if (c >= dp && c < dp + d && S != nullptr) {
+        v = scale * S[j * lds + (c - dp)];
+      }
+      y[c] = v;
+    }
+  } else {
+    for (int64_t c = lane; c < ldy; c += 64) y[c] = 0.f;
+  }
+  nrm = warp_sum(nrm);
+  if (lane == 0) norms[j] = nrm;
+}
+
+// -------------------------------------------------------------- scores ----
+__global__ __launch_bounds__(256) void score_gaussian_kernel(const float* __restrict__ X,
+                                                             int64_t ldx, int64_t n, int64_t d,
+                                                             const float* __restrict__ mu,
+                                                             const float* __restrict__ lam,
+                                                             float scale, float* __restrict__ S,
+                                                             int64_t lds) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n * d) return;
+  const int64_t j = t / d, c = t % d;
+  S[j * lds + c] = scale * (-lam[c] * (X[j * ldx + c] - mu[c]));
+}
+
+// d/dx log(1/3 N(x;-2,1) + 1/3 N(x;2,1)) = -(w1 (x+2) + w2 (x-2)),  with
+// (w1, w2) the softmax of (-(x+2)^2/2, -(x-2)^2/2): stable for any x.
+__global__ __launch_bounds__(256) void score_gmm_kernel(const float* __restrict__ X, int64_t ldx,
+                                                        int64_t n, int64_t d, float scale,
+                                                        float* __restrict__ S, int64_t lds) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n * d) return;
+  const int64_t j = t / d, c = t % d;
+  const float x = X[j * ldx + c];
+  const float a = -0.5f * (x + 2.f) * (x + 2.f), b = -0.5f * (x - 2.f) * (x - 2.f);
+  const float m = fmaxf(a, b);
+  const float ea = __expf(a - m), eb = __expf(b - m);
+  const float s = -(ea * (x + 2.f) + eb * (x - 2.f)) / (ea + eb);
+  S[j * lds + c] = scale * s;
+}
+
+__global__ void set_bandwidth_kernel(dsvgd_select_state* st, float h) {
+  st->h = h;
+  st->inv_h = 1.f / h;
+  st->median = NAN;
+}
+
+}  // namespace dsvgd
+
+using namespace dsvgd;
+
+extern "C" {
+
+int dsvgd_abi_version(void) { return DSVGD_ABI_VERSION; }
+const char* dsvgd_last_error(void) { return g_err; }
+size_t dsvgd_select_state_bytes(void) { return sizeof(dsvgd_select_state); }
+int64_t dsvgd_pad128(int64_t n) { return roundup(n < 1 ? 1 : n, 128); }
+int64_t dsvgd_dp(int64_t d) { return roundup(d < 1 ? 1 : d, 32); }
+int64_t dsvgd_ldy(int64_t dp) {
+  // phi column tile: 128 (2dp<=128), 256 (<=256), else multiples of 512
+  const int64_t w = 2 * dp;
+  if (w <= 128) return 128;
+  if (w <= 256) return 256;
+  return roundup(w, 512);
+}
+
+size_t dsvgd_colmean_workspace_floats(int64_t n, int64_t d) {
+  return (size_t)((n + kMeanRows - 1) / kMeanRows) * (size_t)d;
+}
+
+int dsvgd_colmean(const float* X, int64_t ldx, int64_t n, int64_t d, float* partial, float* mean,
+                  void* stream) {
+  DSVGD_REQUIRE(X && partial && mean, "null pointer");
+  DSVGD_REQUIRE(n > 0 && d > 0 && ldx >= d, "sizes");
+  const int64_t nb = (n + kMeanRows - 1) / kMeanRows;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb, (d + 63) / 64), dim3(256), 0, s, X, ldx, n,
+                     d, partial);
+  int rc = check_launch("colsum_partial");
+  if (rc) return rc;
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((d + 255) / 256), dim3(256), 0, s, partial, nb, n,
+                     d, mean);
+  return check_launch("colsum_final");
+}
+
+int dsvgd_pack(const float* X, int64_t ldx, const float* S, int64_t lds, float score_scale,
+               const float* mean, int64_t n, int64_t d, int64_t rows_pad, float* Y, int64_t ldy,
+               float* norms, void* stream) {
+  DSVGD_REQUIRE(X && mean && Y && norms, "null pointer");
+  DSVGD_REQUIRE(n > 0 && d > 0 && ldx >= d && rows_pad >= n, "sizes");
+  const int64_t dp = dsvgd_dp(d);
+  DSVGD_REQUIRE(ldy >= 2 * dp, "ldy < 2*dp");
+  DSVGD_REQUIRE(S == nullptr || lds >= d, "lds");
+  hipLaunchKernelGGL(pack_kernel, dim3((rows_pad + 3) / 4), dim3(256), 0, (hipStream_t)stream, X,
+                     ldx, S, lds, score_scale, mean, n, d, rows_pad, dp, Y, ldy, norms);
+  return check_launch("pack");
+}
+
+int dsvgd_score_gaussian(const float* X, int64_t ldx, int64_t n, int64_t d, const float* mu,
+                         const float* lam, float scale, float* S, int64_t lds, void* stream) {
+  DSVGD_REQUIRE(X && mu && lam && S, "null pointer");
+  DSVGD_REQUIRE(n > 0 && d > 0 && ldx >= d && lds >= d, "sizes");
+  hipLaunchKernelGGL(score_gaussian_kernel, dim3((n * d + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, X, ldx, n, d, mu, lam, scale, S, lds);
+  return check_launch("score_gaussian");
+}
+
+int dsvgd_score_gmm(const float* X, int64_t ldx, int64_t n, int64_t d, float scale, float* S,
+                    int64_t lds, void* stream) {
+  DSVGD_REQUIRE(X && S, "null pointer");
+  DSVGD_REQUIRE(n > 0 && d > 0 && ldx >= d && lds >= d, "sizes");
+  hipLaunchKernelGGL(score_gmm_kernel, dim3((n * d + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, X, ldx, n, d, scale, S, lds);
+  return check_launch("score_gmm");
+}
+
+int dsvgd_set_bandwidth(dsvgd_select_state* st, float h, void* stream) {
+  DSVGD_REQUIRE(st, "null state");
+  DSVGD_REQUIRE(h > 0.f && std::isfinite(h), "bandwidth must be finite and > 0");
+  hipLaunchKernelGGL(set_bandwidth_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, st, h);
+  return check_launch("set_bandwidth");
+}
+
+}  // extern "C"

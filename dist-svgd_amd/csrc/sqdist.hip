@@ -1,0 +1,230 @@
+// sqdist.hip -- pairwise squared distances on MFMA + the exact radix select
+// that turns them into the median-heuristic bandwidth.
+//
+// Roofline (per 128x128 output tile, d = dp): 2*128*128*dp MFMA flop against
+// 64 KiB of D written -- MFMA-bound for dp >= 64 (2 dp flop per byte written
+// vs 157 TF / 8 TB/s ~ 20 flop/B); the radix passes are pure HBM streams of D.
+#include <cmath>
+
+#include "gemm_tiles.hpp"
+
+namespace dsvgd {
+
+using GramTile = NTTile<2, 2, 2, 2>;  // 128 x 128 block, 4 waves of 64 x 64
+
+// D (panel layout, m_pad x n_pad) for rows [row0, row0+m) of Y against rows [0,n).
+__global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y, int64_t ldy,
+                                                     const float* __restrict__ norms, int64_t row0,
+                                                     int64_t m, int64_t n, int64_t n_pad, int dp,
+                                                     float* __restrict__ D,
+                                                     dsvgd_select_state* __restrict__ st) {
+  __shared__ __attribute__((aligned(16))) float smem[GramTile::kSmemFloats];
+  __shared__ uint32_t shist[DSVGD_RADIX_BINS];
+  __shared__ float snorm[GramTile::BM + GramTile::BN];
+
+  const int bi = blockIdx.y, bj = blockIdx.x;
+  const int64_t i0 = (int64_t)bi * GramTile::BM;  // within the owned block
+  const int64_t j0 = (int64_t)bj * GramTile::BN;
+  if (st)
+    for (int b = threadIdx.x; b < DSVGD_RADIX_BINS; b += 256) shist[b] = 0u;
+
+  GramTile tile;
+  tile.run(Y + (row0 + i0) * ldy, ldy, Y + j0 * ldy, ldy, dp, smem);
+
+  for (int t = threadIdx.x; t < GramTile::BM + GramTile::BN; t += 256)
+    snorm[t] = t < GramTile::BM ? norms[row0 + i0 + t] : norms[j0 + t - GramTile::BM];
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int cl = wn * 64 + ni * 32 + (lane & 31);
+      const int64_t gj = j0 + cl;
+      const float nj = snorm[GramTile::BM + cl];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rl = wm * 64 + mi * 32 + c_row(r, lane);
+        const int64_t gi = i0 + rl;
+        float v;
+        if (gi < m && gj < n) {
+          v = (row0 + gi == gj) ? 0.f : fmaxf(0.f, (snorm[rl] + nj) - 2.f * tile.acc[mi][ni][r]);
+          if (st) atomicAdd(&shist[__float_as_uint(v) >> 21], 1u);
+        } else {
+          v = INFINITY;
+        }
+        D[panel_off(gi, gj, n_pad)] = v;
+      }
+    }
+  if (st) {
+    __syncthreads();
+    for (int b = threadIdx.x; b < DSVGD_RADIX_BINS; b += 256) {
+      const uint32_t c = shist[b];
+      if (c) atomicAdd((unsigned long long*)&st->hist[b], (unsigned long long)c);
+    }
+  }
+}
+
+// ---------------------------------------------------------- radix select --
+// keys: the fp32 bit patterns of D >= 0 (monotone as uint32).  +inf pads and
+// NaN are never counted.  digit 1 = bits 31..21, 2 = 20..10, 3 = 9..0.
+__device__ __forceinline__ void digit_of(int pass, uint32_t& shift, uint32_t& mask,
+                                         uint32_t& hishift) {
+  if (pass == 1) {
+    shift = 21; mask = 0x7FFu; hishift = 32;
+  } else if (pass == 2) {
+    shift = 10; mask = 0x7FFu; hishift = 21;
+  } else {
+    shift = 0; mask = 0x3FFu; hishift = 10;
+  }
+}
+
+__global__ __launch_bounds__(256) void radix_hist_kernel(const float* __restrict__ D, int64_t count4,
+                                                         int pass,
+                                                         dsvgd_select_state* __restrict__ st) {
+  __shared__ uint32_t shist[DSVGD_RADIX_BINS];
+  for (int b = threadIdx.x; b < DSVGD_RADIX_BINS; b += 256) shist[b] = 0u;
+  uint32_t shift, mask, hishift;
+  digit_of(pass, shift, mask, hishift);
+  const uint32_t prefix = st->prefix;
+  const uint32_t want = hishift >= 32 ? 0u : (prefix >> hishift);
+  __syncthreads();
+  const f32x4* D4 = reinterpret_cast<const f32x4*>(D);
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < count4;
+       q += (int64_t)gridDim.x * 256) {
+    const f32x4 v = D4[q];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t key = __float_as_uint(v[e]);
+      if (key >= 0x7F800000u) continue;  // +inf pad / NaN
+      const uint32_t hi = hishift >= 32 ? 0u : (key >> hishift);
+      if (hi == want) atomicAdd(&shist[(key >> shift) & mask], 1u);
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < DSVGD_RADIX_BINS; b += 256) {
+    const uint32_t c = shist[b];
+    if (c) atomicAdd((unsigned long long*)&st->hist[b], (unsigned long long)c);
+  }
+}
+
+// One block: find the bin that holds rank k, fix its digit, clear the bins.
+__global__ __launch_bounds__(256) void radix_pick_kernel(dsvgd_select_state* __restrict__ st,
+                                                         int pass) {
+  __shared__ unsigned long long part[256];
+  __shared__ unsigned long long excl[256];
+  const int t = threadIdx.x;
+  uint32_t shift, mask, hishift;
+  digit_of(pass, shift, mask, hishift);
+  const int nb = (int)mask + 1;            // 2048 or 1024 bins
+  const int per = nb / 256;                // 8 or 4 bins per thread
+  unsigned long long loc[8];
+  unsigned long long s = 0;
+  for (int u = 0; u < per; ++u) {
+    loc[u] = st->hist[t * per + u];
+    s += loc[u];
+  }
+  part[t] = s;
+  __syncthreads();
+  if (t == 0) {
+    unsigned long long run = 0;
+    for (int q = 0; q < 256; ++q) {
+      excl[q] = run;
+      run += part[q];
+    }
+  }
+  __syncthreads();
+  const unsigned long long k = st->k;
+  const unsigned long long lo = excl[t];
+  __syncthreads();
+  if (k >= lo && k < lo + part[t]) {
+    unsigned long long run = lo;
+    for (int u = 0; u < per; ++u) {
+      if (k < run + loc[u]) {
+        const uint32_t digit = (uint32_t)(t * per + u);
+        const uint32_t prefix = st->prefix | (digit << shift);
+        st->prefix = prefix;
+        st->k = k - run;
+        st->passes_done = (uint32_t)pass;
+        if (pass == 3) {
+          const float med = __uint_as_float(prefix);
+          const double nt = (double)st->n_total;
+          float h = 1.f;
+          if (med > 0.f && nt > 1.0) h = (float)((double)med / log(nt));
+          st->median = med;
+          st->h = h;
+          st->inv_h = 1.f / h;
+        }
+        break;
+      }
+      run += loc[u];
+    }
+  }
+  for (int u = 0; u < 8; ++u) st->hist[t * 8 + u] = 0ull;  // clear all 2048 bins
+}
+
+__global__ void select_init_kernel(dsvgd_select_state* st, int64_t n_total) {
+  const int t = threadIdx.x;
+  for (int b = t; b < DSVGD_RADIX_BINS; b += blockDim.x) st->hist[b] = 0ull;
+  if (t == 0) {
+    const unsigned long long nn = (unsigned long long)n_total * (unsigned long long)n_total;
+    st->k = (nn - 1ull) / 2ull;
+    st->n_total = (unsigned long long)n_total;
+    st->prefix = 0u;
+    st->passes_done = 0u;
+    st->median = NAN;
+    st->h = NAN;
+    st->inv_h = NAN;
+  }
+}
+
+}  // namespace dsvgd
+
+using namespace dsvgd;
+
+extern "C" {
+
+int dsvgd_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0, int64_t m,
+                 int64_t n, int64_t dp, float* D, int64_t ldd, dsvgd_select_state* st,
+                 void* stream) {
+  DSVGD_REQUIRE(Y && norms && D, "null pointer");
+  DSVGD_REQUIRE(m > 0 && n > 0 && row0 >= 0, "sizes");
+  DSVGD_REQUIRE(dp % 32 == 0 && dp > 0 && ldy >= dp && ldy % 4 == 0, "dp must be a multiple of 32");
+  const int64_t m_pad = roundup(m, 128), n_pad = roundup(n, 128);
+  DSVGD_REQUIRE(ldd == n_pad, "ldd must equal roundup(n,128) (panel layout)");
+  DSVGD_REQUIRE(((uintptr_t)Y & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
+  DSVGD_REQUIRE(m_pad / 128 <= 65535, "too many row tiles");
+  hipLaunchKernelGGL(sqdist_kernel, dim3(n_pad / 128, m_pad / 128), dim3(256), 0,
+                     (hipStream_t)stream, Y, ldy, norms, row0, m, n, n_pad, (int)dp, D, st);
+  return check_launch("sqdist");
+}
+
+int dsvgd_select_init(dsvgd_select_state* st, int64_t n_total, void* stream) {
+  DSVGD_REQUIRE(st && n_total > 0, "args");
+  hipLaunchKernelGGL(select_init_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, st, n_total);
+  return check_launch("select_init");
+}
+
+int dsvgd_radix_hist(const float* D, int64_t ldd, int64_t m, int64_t n, int pass,
+                     dsvgd_select_state* st, void* stream) {
+  DSVGD_REQUIRE(D && st, "null pointer");
+  DSVGD_REQUIRE(pass >= 1 && pass <= 3, "pass must be 1..3");
+  const int64_t m_pad = roundup(m, 128), n_pad = roundup(n, 128);
+  DSVGD_REQUIRE(ldd == n_pad, "ldd must equal roundup(n,128) (panel layout)");
+  const int64_t count4 = m_pad * n_pad / 4;
+  int64_t blocks = (count4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(radix_hist_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, D, count4,
+                     pass, st);
+  return check_launch("radix_hist");
+}
+
+int dsvgd_radix_pick(dsvgd_select_state* st, int pass, void* stream) {
+  DSVGD_REQUIRE(st, "null state");
+  DSVGD_REQUIRE(pass >= 1 && pass <= 3, "pass must be 1..3");
+  hipLaunchKernelGGL(radix_pick_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, st, pass);
+  return check_launch("radix_pick");
+}
+
+}  // extern "C"

@@ -1,0 +1,110 @@
+"""ctypes binding of libdsvgd_hip.so (the C ABI declared in include/dsvgd.h).
+
+There is deliberately no fallback: if the HIP library is missing or cannot be
+loaded, every compute entry point raises :class:`NativeUnavailable`.  The
+SVGD math runs only in the gfx950 kernels.
+"""
+import ctypes
+import os
+
+import torch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libdsvgd_hip.so")
+
+_c = ctypes
+_p = _c.c_void_p
+_i64 = _c.c_int64
+_f = _c.c_float
+_int = _c.c_int
+
+# name -> (restype, argtypes); must mirror include/dsvgd.h exactly
+SIGNATURES = {
+    "dsvgd_abi_version": (_int, []),
+    "dsvgd_last_error": (_c.c_char_p, []),
+    "dsvgd_select_state_bytes": (_c.c_size_t, []),
+    "dsvgd_pad128": (_i64, [_i64]),
+    "dsvgd_dp": (_i64, [_i64]),
+    "dsvgd_ldy": (_i64, [_i64]),
+    "dsvgd_colmean_workspace_floats": (_c.c_size_t, [_i64, _i64]),
+    "dsvgd_colmean": (_int, [_p, _i64, _i64, _i64, _p, _p, _p]),
+    "dsvgd_pack": (_int, [_p, _i64, _p, _i64, _f, _p, _i64, _i64, _i64, _p, _i64, _p, _p]),
+    "dsvgd_sqdist": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _p]),
+    "dsvgd_select_init": (_int, [_p, _i64, _p]),
+    "dsvgd_radix_hist": (_int, [_p, _i64, _i64, _i64, _int, _p, _p]),
+    "dsvgd_radix_pick": (_int, [_p, _int, _p]),
+    "dsvgd_set_bandwidth": (_int, [_p, _f, _p]),
+    "dsvgd_phi_mm": (_int, [_p, _i64, _p, _i64, _i64, _i64, _p, _p, _i64, _p, _p]),
+    "dsvgd_phi_finish": (_int, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _p, _f, _f,
+                                _p, _i64, _p, _i64, _p]),
+    "dsvgd_phi_row": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _f, _p, _p]),
+    "dsvgd_score_gaussian": (_int, [_p, _i64, _i64, _i64, _p, _p, _f, _p, _i64, _p]),
+    "dsvgd_score_gmm": (_int, [_p, _i64, _i64, _i64, _f, _p, _i64, _p]),
+    "dsvgd_logreg_workspace_bytes": (_c.c_size_t, [_i64, _i64, _i64]),
+    "dsvgd_score_logreg": (_int, [_p, _i64, _i64, _i64, _p, _i64, _p, _i64, _f, _p, _i64, _p,
+                                  _p]),
+}
+
+
+class NativeUnavailable(RuntimeError):
+    """libdsvgd_hip.so is missing or unusable (no silent fallback exists)."""
+
+
+class NativeError(RuntimeError):
+    """A libdsvgd_hip.so entry point returned an error code."""
+
+
+_lib = None
+
+
+def load():
+    """Load (once) and return the ctypes library with typed entry points."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeUnavailable(
+            "libdsvgd_hip.so not found at %s -- build it with `make -C dist-svgd_amd` "
+            "(or __graft_entry__.build()); dsvgd has no non-HIP compute path" % LIB_PATH)
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover - environment specific
+        raise NativeUnavailable("cannot load %s: %s" % (LIB_PATH, e))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.dsvgd_abi_version() != 1:
+        raise NativeUnavailable("ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Invoke entry point `name`; raise NativeError on a nonzero return code."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise NativeError("%s failed (%d): %s" % (name, rc, lib.dsvgd_last_error().decode()))
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("dsvgd kernels need device (HIP) tensors, got %s" % t.device)
+    return t.data_ptr()
+
+
+def stream(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_gpu(device):
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise NativeUnavailable("dsvgd runs on MI355X (HIP) devices only; got device %s" % dev)
+    if not torch.cuda.is_available():
+        raise NativeUnavailable("no HIP device visible; dsvgd has no CPU compute path")
+    load()
+    return dev

@@ -1,0 +1,215 @@
+"""Drop-in `dsvgd.DistSampler` (reference: dsvgd/distsampler.py:8-205) on MI355X.
+
+Constructor, `particles` property (owned row-block view; setter asserts the
+shape, distsampler.py:53-62), `make_step(step_size, h=1.0) -> None` and the
+three exchange modes keep the reference semantics:
+
+  partitions     (exchange_particles=False): ring shift of the owned block to
+                 rank+1, receive into rank-1's rows, which become the owned rows
+                 from then on (distsampler.py:131-150); interactions and the
+                 median are local to the block; score = N_global/N_local *
+                 grad log p_local (:97-99).
+  all_particles  all-gather of the owned blocks; owned rows interact with all n;
+                 score = N_global/N_local * grad log p_local.
+  all_scores     all-gather, then the local-data scores of ALL n particles are
+                 all-reduced (SUM) and frozen for the step (:160-170); like the
+                 reference the prior is summed S times.
+
+Device model: one process per GPU; the process group (nccl = RCCL) must be
+initialised before make_step when num_shards > 1.  A device `particles`
+tensor is updated in place (the reference mutates the caller's tensor, a7);
+a CPU tensor is copied to the GPU and mirrored back after every make_step.
+
+Extensions (keyword-only): order="sequential" (reference in-place
+Gauss-Seidel over the owned rows) | "jacobi" (MFMA fast path); device; group.
+Deviations: exchange_scores with num_shards == 1 uses the local scores (the
+reference reads an uninitialised buffer there); include_wasserstein's W2/JKO
+term (distsampler.py:103-129) is not implemented yet and raises
+NotImplementedError when it would be applied (from the second step on).
+"""
+import torch
+
+from . import _native as N
+from . import exchange
+from .engine import PhiEngine, SelectState, sequential_sweep, span
+from .kernels import resolve_kernel
+from .targets import resolve_target
+
+
+class DistSampler(object):
+    timer = None   # optional engine.StageTimer (bench instrumentation)
+
+    def __init__(self, rank, num_shards, logp, kernel, particles,
+                 N_local, N_global,
+                 exchange_particles=True, exchange_scores=True, include_wasserstein=True,
+                 *, order="sequential", device=None, group=None):
+        """Initializes a distributed SVGD sampler (distsampler.py:9-51)."""
+        assert not (exchange_scores and not exchange_particles), \
+            "must exchange particles to also exchange scores"
+        if order not in ("sequential", "jacobi"):
+            raise ValueError("order must be 'sequential' or 'jacobi'")
+        self._rank = rank
+        self._num_shards = num_shards
+        self._logp = logp
+        self._kernel = kernel
+        self._N_local = N_local
+        self._N_global = N_global
+        self._d = particles.shape[1]
+        self._exchange_particles = exchange_particles
+        self._exchange_scores = exchange_scores
+        self._include_wasserstein = include_wasserstein
+        self._order = order
+        self._group = group
+        self._target = resolve_target(logp)
+        self._rbf = resolve_kernel(kernel, self._d)
+
+        # NOTE: drops particles if not divisible by num_shards (as the reference)
+        self._particles_per_shard = int(particles.shape[0] / self._num_shards)
+        self._num_particles = self._particles_per_shard * self._num_shards
+        self._particles = particles[:self._num_particles]
+        if particles.is_cuda:
+            self._device = N.require_gpu(particles.device)
+            assert self._particles.stride(1) == 1, "device particles must be row-major"
+            self._work = self._particles          # updated in place
+        else:
+            self._device = N.require_gpu(device if device is not None else "cuda")
+            self._work = self._particles.detach().to(self._device, torch.float32).contiguous()
+        self._scores = None
+        if exchange_scores:
+            self._scores = torch.empty(self._work.shape, dtype=torch.float32, device=self._device)
+
+        (start, end) = self._particle_idx_range(rank)
+        self._particle_start_idx = start
+        self._particle_end_idx = end
+        self._previous_particles = None
+        self._engines = {}
+        self._state = None
+
+    # ---------------------------------------------------- reference API --
+    @property
+    def particles(self):
+        "Returns particles currently being updated on this sampler"
+        return self._particles[self._particle_start_idx:self._particle_end_idx, :]
+
+    @particles.setter
+    def particles(self, value):
+        "Sets value of particles currently being updated on this sampler"
+        assert value.shape == self.particles.shape
+        s, e = self._particle_start_idx, self._particle_end_idx
+        self._particles[s:e, :] = value
+        if self._work is not self._particles:
+            self._work[s:e, :] = value.to(self._device)
+
+    def _particle_idx_range(self, rank):
+        assert rank >= 0 and rank < self._num_shards
+        return (self._particles_per_shard * rank, self._particles_per_shard * (rank + 1))
+
+    # -------------------------------------------------------- exchange --
+    def _exchange_round_robin(self):
+        "Exchanges single particle partitions round robin (distsampler.py:131-150)."
+        s, e = self._particle_start_idx, self._particle_end_idx
+        send = self._work[s:e].clone()
+        src = (self._rank - 1 + self._num_shards) % self._num_shards
+        start, end = self._particle_idx_range(src)
+        recv = torch.empty_like(send)
+        exchange.ring_shift(send, recv, self._rank, self._num_shards, self._group)
+        self._work[start:end] = recv
+        self._particle_start_idx = start
+        self._particle_end_idx = end
+
+    def _exchange_all_particles(self):
+        "Gathers all particles to all shards (distsampler.py:152-158)."
+        s, e = self._particle_start_idx, self._particle_end_idx
+        out = torch.empty_like(self._work)
+        exchange.all_gather_blocks(self._work[s:e], out, self._group)
+        self._work.copy_(out)
+
+    def _local_scores(self, X, out, scale=1.0):
+        self._target.score(X, out, scale)
+
+    def _exchange_all_scores(self):
+        "Sum of every shard's local-data scores of all particles (distsampler.py:160-170)."
+        with span(self.timer, "scores"):
+            self._local_scores(self._work, self._scores)
+        with span(self.timer, "allreduce_scores"):
+            exchange.all_reduce_sum(self._scores, self._group)
+
+    # ------------------------------------------------------------ step --
+    def _engine(self, n_int, m, row0):
+        key = (n_int, m, row0)
+        if key not in self._engines:
+            self._engines = {key: PhiEngine(n_int, self._d, m=m, row0=row0, device=self._device)}
+        eng = self._engines[key]
+        eng.timer = self.timer
+        return eng
+
+    def make_step(self, step_size, h=1.0):
+        """Performs one step of SVGD (distsampler.py:172-205).
+
+        Params:
+            step_size - step size
+            h - discretization size for the JKO (W2) term
+        """
+        S = self._num_shards
+        if S > 1:
+            if self._exchange_particles:
+                with span(self.timer, "allgather_x"):
+                    self._exchange_all_particles()
+                if self._exchange_scores:
+                    self._exchange_all_scores()
+            else:
+                with span(self.timer, "ring_shift"):
+                    self._exchange_round_robin()
+        elif self._exchange_scores:
+            with span(self.timer, "scores"):
+                self._local_scores(self._work, self._scores)
+
+        if self._include_wasserstein and self._previous_particles is not None:
+            raise NotImplementedError(
+                "include_wasserstein=True: the W2/JKO term (distsampler.py:103-129) is not "
+                "implemented on MI355X yet; construct with include_wasserstein=False")
+
+        s, e = self._particle_start_idx, self._particle_end_idx
+        X = self._work
+        if self._exchange_particles:
+            Xi, lo = X, 0
+        else:
+            Xi, lo = X[s:e], s
+        n_int = Xi.shape[0]
+        scale = 1.0 if self._exchange_scores else self._N_global / self._N_local
+        if self._exchange_scores:
+            Si = self._scores
+        else:
+            Si = torch.empty(Xi.shape, dtype=torch.float32, device=self._device)
+            with span(self.timer, "scores"):
+                self._local_scores(Xi, Si, scale)
+        median = self._rbf.median
+        share = self._exchange_particles and S > 1
+        hook = (lambda t: exchange.all_reduce_sum(t, self._group)) if share else None
+
+        if self._order == "jacobi":
+            eng = self._engine(n_int, e - s, s - lo)
+            eng.step(Xi, Si, X_own=X[s:e], step=step_size, h=None if median else self._rbf.h,
+                     allreduce=hook, write_phi=False)
+        else:
+            if median:
+                eng = self._engine(n_int, e - s, s - lo)
+                eng.pack(Xi)
+                eng.distances(histogram=True)
+                eng.median_bandwidth(hook)
+                state = eng.state
+            else:
+                if self._state is None:
+                    self._state = SelectState(self._device)
+                state = self._state
+                N.call("dsvgd_set_bandwidth", state.ptr, float(self._rbf.h),
+                       N.stream(self._device))
+            tgt = None if self._exchange_scores else self._target
+            sequential_sweep(Xi, Si, range(s - lo, e - lo), state, step_size, target=tgt,
+                             score_scale=scale)
+
+        if self._include_wasserstein:
+            src = X if self._exchange_particles else X[s:e]
+            self._previous_particles = src.clone()
+        if self._work is not self._particles:
+            self._particles.copy_(self._work)

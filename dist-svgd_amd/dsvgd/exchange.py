@@ -1,0 +1,53 @@
+"""DistSampler's particle / score exchange on torch.distributed.
+
+On MI355X the process group is `nccl` (= RCCL over xGMI) and every buffer is
+a device tensor, so the collectives run stream-ordered on the GPU.  The same
+functions accept a `gloo` group (CPU rehearsal / tests); gloo is given host
+copies.  Reference call sites: dist.isend/irecv (dsvgd/distsampler.py:136,143),
+dist.all_gather (:156), dist.all_reduce SUM (:170).
+"""
+import torch
+import torch.distributed as dist
+
+
+def _is_gloo(group=None):
+    return dist.get_backend(group) == "gloo"
+
+
+def all_gather_blocks(own, out, group=None):
+    """out (S*m, d) <- concat over ranks of `own` (m, d)   [distsampler.py:152-158]."""
+    if own.is_cuda and not _is_gloo(group):
+        dist.all_gather_into_tensor(out, own.contiguous(), group=group)
+        return
+    src = own.detach().cpu().contiguous()
+    parts = [torch.empty_like(src) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, src, group=group)
+    out.copy_(torch.cat(parts).to(out.device))
+
+
+def all_reduce_sum(t, group=None):
+    """In-place SUM over ranks   [distsampler.py:170]."""
+    if t.is_cuda and not _is_gloo(group):
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        return
+    h = t.detach().cpu()
+    dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+    t.copy_(h.to(t.device))
+
+
+def ring_shift(send, recv, rank, size, group=None):
+    """send -> rank+1, recv <- rank-1   [distsampler.py:131-150]."""
+    dst, src = (rank + 1) % size, (rank - 1 + size) % size
+    if send.is_cuda and not _is_gloo(group):
+        ops = [dist.P2POp(dist.isend, send.contiguous(), dst, group=group),
+               dist.P2POp(dist.irecv, recv, src, group=group)]
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+        return
+    hs = send.detach().cpu().contiguous()
+    hr = torch.empty(recv.shape, dtype=recv.dtype)
+    r1 = dist.isend(hs, dst, group=group)
+    r2 = dist.irecv(hr, src, group=group)
+    r1.wait()
+    r2.wait()
+    recv.copy_(hr.to(recv.device))

@@ -1,0 +1,157 @@
+/*
+ * dsvgd.h -- C ABI of libdsvgd_hip.so, the MI355X (gfx950) SVGD particle-update
+ * engine behind the drop-in `dsvgd.Sampler` / `dsvgd.DistSampler` Python API.
+ *
+ * Conventions (every entry point):
+ *   - plain pointers + int64 sizes; every float buffer is caller-owned DEVICE
+ *     memory, row-major fp32, with an explicit leading dimension (elements);
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream); every
+ *     call only ENQUEUES work on it (no host sync, no allocation), so the whole
+ *     SVGD step can be captured into a hipGraph;
+ *   - return 0 on success, a negative DSVGD_E* code otherwise; the message is
+ *     in dsvgd_last_error() (thread-local).  No C++ exception crosses the ABI.
+ *
+ * Padding contract ("padded shapes"): n_pad = roundup(n,128), m_pad =
+ * roundup(m,128), dp = roundup(d,32); Y has >= n_pad+128 rows and ldy =
+ * dsvgd_ldy(dp) columns; D is m_pad x n_pad (ldd >= n_pad).  The helpers
+ * dsvgd_dp / dsvgd_ldy / dsvgd_pad128 compute these.
+ *
+ * The reference interface each call replaces is cited beside it
+ * (paths relative to the Sandy4321/dist-svgd tree).
+ */
+#ifndef DSVGD_H_
+#define DSVGD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSVGD_ABI_VERSION 1
+
+enum {
+  DSVGD_OK = 0,
+  DSVGD_E_ARG = -1,    /* bad size / pointer / alignment                    */
+  DSVGD_E_LAUNCH = -2, /* hipLaunchKernel (or a HIP runtime call) failed     */
+  DSVGD_E_UNSUPPORTED = -3
+};
+
+/* number of histogram bins of one radix-select pass (11-bit digits) */
+#define DSVGD_RADIX_BINS 2048
+
+/* Device-resident state of the median-bandwidth radix select.  Allocate
+ * dsvgd_select_state_bytes() of device memory; the histogram is the first
+ * member so a distributed caller can all-reduce it in place (int64 SUM). */
+typedef struct dsvgd_select_state {
+  uint64_t hist[DSVGD_RADIX_BINS]; /* per-pass counts (u64: n^2 may be 2^32)  */
+  uint64_t k;                      /* rank still to find inside the prefix    */
+  uint64_t n_total;                /* global particle count n (matrix n x n)  */
+  uint32_t prefix;                 /* key bits fixed by the passes so far     */
+  uint32_t passes_done;
+  float median;                    /* k-th smallest squared distance          */
+  float h;                         /* bandwidth  h = median / log(n)          */
+  float inv_h;                     /* 1 / h (read by the phi kernels)         */
+  float pad_;
+} dsvgd_select_state;
+
+/* ---- meta ------------------------------------------------------------- */
+int dsvgd_abi_version(void);
+const char* dsvgd_last_error(void);
+size_t dsvgd_select_state_bytes(void);
+int64_t dsvgd_pad128(int64_t n);
+int64_t dsvgd_dp(int64_t d);   /* padded feature width: roundup(d, 32)     */
+int64_t dsvgd_ldy(int64_t dp); /* row stride of Y = [Xc | S] (phi col tile) */
+
+/* ---- particle preparation ---------------------------------------------- */
+/* mean[c] = (1/n) sum_j X[j][c]  (deterministic two-level sum; `partial`
+ * is workspace of dsvgd_colmean_workspace_floats(n, d) floats).
+ * Centering is exact algebra for phi (sum_j k_ij (x_i - x_j) is translation
+ * invariant) and keeps ||x||^2 - 2 x.y well conditioned. */
+size_t dsvgd_colmean_workspace_floats(int64_t n, int64_t d);
+int dsvgd_colmean(const float* X, int64_t ldx, int64_t n, int64_t d, float* partial, float* mean,
+                  void* stream);
+
+/* Y[j] = [X[j]-mean | score_scale*S[j]] zero padded to (rows_pad x ldy);
+ * norms[j] = ||X[j]-mean||^2.  Replaces the per-pair operand gathering of
+ * dsvgd/sampler.py:37-39 and dsvgd/distsampler.py:90-99.  S may be NULL
+ * (S half left zero). */
+int dsvgd_pack(const float* X, int64_t ldx, const float* S, int64_t lds, float score_scale,
+               const float* mean, int64_t n, int64_t d, int64_t rows_pad, float* Y, int64_t ldy,
+               float* norms, void* stream);
+
+/* ---- pairwise squared distances (MFMA fp32) ---------------------------- */
+/* D[i][j] = max(0, |y_i|^2 + |y_j|^2 - 2 y_i.y_j) for the owned row block
+ * i in [row0, row0+m) against all j < n (D[i][i]=0 exactly, pads = +inf),
+ * computed on v_mfma_f32_32x32x2_f32; if hist != NULL also accumulates the
+ * first radix-select histogram (key bits 31..21) of the valid entries.
+ * Replaces torch.dist(x, y, p=2)**2 inside kernel(...) at
+ * experiments/logreg.py:60-61 / experiments/gmm.py:23-24 as called per pair
+ * from dsvgd/sampler.py:38 and dsvgd/distsampler.py:91-97. */
+int dsvgd_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0, int64_t m,
+                 int64_t n, int64_t dp, float* D, int64_t ldd, dsvgd_select_state* st,
+                 void* stream);
+
+/* ---- median bandwidth: exact radix select over the n x n distances ----- */
+/* (absent in the reference, whose kernel bandwidth is fixed at h=1; the
+ * median heuristic is pinned in SURVEY.md a18: lower median, k=(n^2-1)//2
+ * over the full matrix incl. the diagonal, h = median / log n.)            */
+int dsvgd_select_init(dsvgd_select_state* st, int64_t n_total, void* stream);
+/* histogram of key digit `pass` (1: bits 31..21, 2: 20..10, 3: 9..0) of the
+ * entries of D[0:m, 0:n] whose higher digits equal st->prefix. */
+int dsvgd_radix_hist(const float* D, int64_t ldd, int64_t m, int64_t n, int pass,
+                     dsvgd_select_state* st, void* stream);
+/* pick the bin holding rank k, fix its digit, clear hist; after pass 3
+ * writes median, h, inv_h. */
+int dsvgd_radix_pick(dsvgd_select_state* st, int pass, void* stream);
+/* fixed-bandwidth mode: st->h = h, st->inv_h = 1/h */
+int dsvgd_set_bandwidth(dsvgd_select_state* st, float h, void* stream);
+
+/* ---- phi: K.[Xc | S] on MFMA with the fused RBF exp -------------------- */
+/* KY[i][:] = sum_j exp(-D[i][j]/h) Y[j][:],  rowsum[i] = sum_j exp(-D[i][j]/h)
+ * (h read from st on device).  Replaces the inner loop of
+ * dsvgd/sampler.py:35-40 (_phi_hat) and dsvgd/distsampler.py:84-101. */
+int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t m,
+                 int64_t n, const dsvgd_select_state* st, float* KY, int64_t ldk,
+                 float* rowsum, void* stream);
+
+/* phi[i] = inv_n * (KS[i] + (2/h) (rowsum[i] xc[i] - KXc[i]))  and, if X != NULL,
+ * X[i] += step * phi[i]  (the update of dsvgd/sampler.py:68 /
+ * dsvgd/distsampler.py:200, Jacobi order).  phi may be NULL. */
+int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, const float* Y,
+                     int64_t ldy, int64_t row0, int64_t m, int64_t d, int64_t dp,
+                     const dsvgd_select_state* st, float inv_n, float step, float* phi,
+                     int64_t ldphi, float* X, int64_t ldx, void* stream);
+
+/* Gauss-Seidel single-row update (reference order): for particle i, phi_i
+ * from exact differences against the CURRENT X (rows < i already moved),
+ * X[i] += step * phi_i.  Reproduces dsvgd/sampler.py:64-68 and
+ * dsvgd/distsampler.py:194-200 one row at a time.  n_int interacting rows
+ * start at X (row i is X + i*ldx). */
+int dsvgd_phi_row(float* X, int64_t ldx, const float* S, int64_t lds, int64_t n_int, int64_t d,
+                  int64_t i, const dsvgd_select_state* st, float step, float* phi_out,
+                  void* stream);
+
+/* ---- target scores grad log p (replace the autograd _dlogp calls) ------ */
+/* S = scale * (-lam * (X - mu))      (synthetic Gaussian target)            */
+int dsvgd_score_gaussian(const float* X, int64_t ldx, int64_t n, int64_t d, const float* mu,
+                         const float* lam, float scale, float* S, int64_t lds, void* stream);
+/* S = scale * d/dx log(1/3 N(x;-2,1) + 1/3 N(x;2,1)), elementwise
+ * (experiments/gmm.py:16-21) */
+int dsvgd_score_gmm(const float* X, int64_t ldx, int64_t n, int64_t d, float scale, float* S,
+                    int64_t lds, void* stream);
+/* Bayesian logistic regression (experiments/logreg.py:45-58), x = [log a, w]:
+ *   s_0 = scale*(-a + p/2 - a/2 |w|^2),  s_w = scale*(-a w + Xd^T (t * sigma(-t * Xd w)))
+ * as two MFMA GEMMs (Z = W Xd^T with the sigmoid epilogue, G Xd).
+ * Xd: N x p data rows (ldxd), t: N labels (+-1).  Workspace:
+ * dsvgd_logreg_workspace_bytes(n, N, p). */
+size_t dsvgd_logreg_workspace_bytes(int64_t n, int64_t N, int64_t p);
+int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const float* Xd,
+                       int64_t ldxd, const float* t, int64_t N, float scale, float* S, int64_t lds,
+                       void* workspace, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DSVGD_H_ */

@@ -1,0 +1,234 @@
+"""CPU ORACLE for the SVGD particle update -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker / the timed CPU baseline.  The product
+path (dist-svgd_amd/dsvgd) never imports it and has no CPU compute path.
+
+An independent numpy restatement (fp64 by default) of the reference algorithm
+(Sandy4321/dist-svgd, paths relative to that tree):
+
+  * phi on frozen particles ............ dsvgd/sampler.py:35-40, dsvgd/distsampler.py:84-101
+      phi_i = 1/n sum_j [ k(x_j,x_i) s_j + grad_{x_j} k(x_j,x_i) ],  k = exp(-|x-y|^2/h)
+      grad_{x_j} k(x_j, x_i) = (2/h) (x_i - x_j) k  (autograd of experiments/logreg.py:60-61)
+  * Gauss-Seidel sweeps ................ dsvgd/sampler.py:62-74 (in-place row update, :68)
+  * DistSampler.make_step .............. dsvgd/distsampler.py:172-205 for S simulated
+    ranks: partitions ring shift (:131-150), all_particles all_gather (:152-158),
+    all_scores all_reduce (:160-170), N_global/N_local score scaling (:97-99)
+  * target scores (closed-form autograd of) experiments/gmm.py:16-21,
+    experiments/logreg.py:45-58 and the synthetic Gaussian N(mu, diag(1/lam))
+  * median bandwidth (absent from the reference): lower median
+    k=(n^2-1)//2 of the full n x n squared-distance matrix, h = median / log n.
+
+Parity pinning: checked against the golden vectors in tests/golden/*.npz, which
+tests/golden/make_golden.py produced by running the reference itself.
+"""
+import math
+
+import numpy as np
+
+
+# ------------------------------------------------------------------ scores --
+def score_gaussian(X, mu, lam):
+    X = np.asarray(X, np.float64)
+    return -np.asarray(lam, np.float64) * (X - np.asarray(mu, np.float64))
+
+
+def score_gmm(X):
+    """d/dx log(1/3 N(x;-2,1) + 1/3 N(x;2,1)) per coordinate (gmm.py:19-21)."""
+    X = np.asarray(X, np.float64)
+    a = -0.5 * (X + 2.0) ** 2
+    b = -0.5 * (X - 2.0) ** 2
+    m = np.maximum(a, b)
+    ea, eb = np.exp(a - m), np.exp(b - m)
+    return -(ea * (X + 2.0) + eb * (X - 2.0)) / (ea + eb)
+
+
+def score_logreg(X, x_train, t_train):
+    """grad of logreg.py:45-58: x = [log alpha, w]; Gamma(1,1) prior on alpha
+    (no log-Jacobian), N(0, I/alpha) prior on w, logistic likelihood."""
+    X = np.asarray(X, np.float64)
+    xd = np.asarray(x_train, np.float64)
+    t = np.asarray(t_train, np.float64).reshape(-1)
+    a = np.exp(X[:, 0])
+    W = X[:, 1:]
+    p = W.shape[1]
+    Z = W @ xd.T                              # (n, N)
+    G = t[None, :] * _sigmoid(-t[None, :] * Z)
+    S = np.empty_like(X)
+    S[:, 0] = -a + 0.5 * p - 0.5 * a * (W * W).sum(1)
+    S[:, 1:] = G @ xd - a[:, None] * W
+    return S
+
+
+def _sigmoid(u):
+    out = np.empty_like(u)
+    pos = u >= 0
+    out[pos] = 1.0 / (1.0 + np.exp(-u[pos]))
+    e = np.exp(u[~pos])
+    out[~pos] = e / (1.0 + e)
+    return out
+
+
+# ------------------------------------------------------------- bandwidth --
+def sqdist(Xr, X):
+    """||x_i - x_j||^2 from explicit differences (as torch.dist**2 per pair),
+    chunked over rows to bound memory."""
+    Xr = np.asarray(Xr, np.float64)
+    X = np.asarray(X, np.float64)
+    out = np.empty((Xr.shape[0], X.shape[0]))
+    step = max(1, (1 << 24) // max(1, X.size))
+    for s in range(0, Xr.shape[0], step):
+        out[s:s + step] = ((Xr[s:s + step, None, :] - X[None, :, :]) ** 2).sum(-1)
+    return out
+
+
+def lower_median(values):
+    """k-th smallest, k = (N-1)//2 (== torch.median semantics on a flat tensor)."""
+    v = np.asarray(values).ravel()
+    k = (v.size - 1) // 2
+    return np.partition(v, k)[k]
+
+
+def median_bandwidth(X):
+    """h = lower_median(D) / log(n) over the full n x n matrix (diag included);
+    h = 1 when n <= 1 or the median is 0 (all particles coincide)."""
+    X = np.asarray(X, np.float64)
+    n = X.shape[0]
+    med = float(lower_median(sqdist(X, X)))
+    if n <= 1 or med <= 0.0:
+        return 1.0, med
+    return med / math.log(n), med
+
+
+# ------------------------------------------------------------------- phi --
+def phi(X, S, h, rows=None):
+    """Jacobi phi for `rows` (default all) against the frozen set X (n x d)."""
+    X = np.asarray(X, np.float64)
+    S = np.asarray(S, np.float64)
+    Xr = X if rows is None else X[rows]
+    K = np.exp(-sqdist(Xr, X) / h)             # K[i, j] = k(x_j, x_i)
+    n = X.shape[0]
+    rep = (2.0 / h) * (K.sum(1)[:, None] * Xr - K @ X)
+    return (K @ S + rep) / n
+
+
+def phi_pairloop_row(i, X, score_fn, h):
+    """Literal restatement of the per-pair loop (sampler.py:36-40), one row."""
+    X = np.asarray(X, np.float64)
+    x = X[i]
+    total = np.zeros_like(x)
+    for xj in X:
+        k = math.exp(-float(((xj - x) ** 2).sum()) / h)
+        total += k * score_fn(xj[None, :])[0] + (2.0 / h) * (x - xj) * k
+    return total / X.shape[0]
+
+
+# ----------------------------------------------- Sampler (Gauss-Seidel) --
+def sampler_sequential(X0, score_fn, h, num_iter, step_size, dtype=np.float64):
+    """sampler.py:62-74: returns the history (num_iter+1, n, d); history[l] is
+    the particle set at the start of sweep l (== what the reference records
+    for every particle right before its own update)."""
+    X = np.array(X0, dtype=dtype)
+    n = X.shape[0]
+    hist = [X.copy()]
+    for _ in range(num_iter):
+        for i in range(n):
+            S = score_fn(X)
+            p = phi(X, S, h, rows=[i])[0]
+            X[i] = X[i] + step_size * p
+        hist.append(X.copy())
+    return np.stack(hist)
+
+
+def sampler_jacobi(X0, score_fn, h, num_iter, step_size, median=False):
+    X = np.array(X0, np.float64)
+    hist = [X.copy()]
+    for _ in range(num_iter):
+        hh = median_bandwidth(X)[0] if median else h
+        X = X + step_size * phi(X, score_fn(X), hh)
+        hist.append(X.copy())
+    return np.stack(hist)
+
+
+# ----------------------------------------------------- DistSampler (S ranks) --
+class DistOracle:
+    """All S ranks of DistSampler simulated in one process (distsampler.py:9-205).
+
+    `particles[r]` is rank r's (n, d) copy; `score_fns[r](X)` the rank-local
+    score grad log p_r (prior + local likelihood).  sequential=True follows the
+    reference's in-place Gauss-Seidel order; False is the Jacobi variant.
+    """
+
+    def __init__(self, particles, score_fns, N_local, N_global, exchange_particles,
+                 exchange_scores, h=1.0, sequential=True):
+        assert not (exchange_scores and not exchange_particles)
+        self.S = len(particles)
+        n = np.asarray(particles[0]).shape[0]
+        self.per = int(n / self.S)
+        self.n = self.per * self.S
+        self.X = [np.array(p, np.float64)[:self.n].copy() for p in particles]
+        self.score_fns = score_fns
+        self.N_local, self.N_global = N_local, N_global
+        self.xp, self.xs = exchange_particles, exchange_scores
+        self.h = h
+        self.sequential = sequential
+        self.start = [r * self.per for r in range(self.S)]
+
+    def own(self, r):
+        return self.X[r][self.start[r]:self.start[r] + self.per]
+
+    def _exchange(self):
+        S = self.S
+        if S <= 1:
+            return None
+        if self.xp:
+            full = np.concatenate([self.own(r) for r in range(S)])
+            for r in range(S):
+                self.X[r][:] = full
+            if self.xs:
+                tot = sum(self.score_fns[r](full) for r in range(S))
+                return [tot.copy() for _ in range(S)]
+            return None
+        blocks = [self.own(r).copy() for r in range(S)]
+        for r in range(S):
+            src = (r - 1 + S) % S
+            s0 = src * self.per
+            self.X[r][s0:s0 + self.per] = blocks[src]
+            self.start[r] = s0
+        return None
+
+    def step(self, step_size):
+        scores = self._exchange()
+        if scores is None and self.xs:      # S == 1 with exchange_scores: local scores
+            scores = [self.score_fns[r](self.X[r]) for r in range(self.S)]
+        for r in range(self.S):
+            Xr = self.X[r]
+            s0, s1 = self.start[r], self.start[r] + self.per
+            lo, hi = (0, self.n) if self.xp else (s0, s1)
+            scale = 1.0 if self.xs else self.N_global / self.N_local
+            if self.sequential:
+                for i in range(s0, s1):
+                    Xi = Xr[lo:hi]
+                    Sj = scores[r][lo:hi] if self.xs else scale * self.score_fns[r](Xi)
+                    Xr[i] += step_size * phi(Xi, Sj, self.h, rows=[i - lo])[0]
+            else:
+                Xi = Xr[lo:hi].copy()
+                Sj = scores[r][lo:hi] if self.xs else scale * self.score_fns[r](Xi)
+                Xr[s0:s1] += step_size * phi(Xi, Sj, self.h, rows=np.arange(s0 - lo, s1 - lo))
+
+
+# --------------------------------------------------------------- metric --
+def test_accuracy(particles, x_test, t_test):
+    """logreg_plots.py:42-50: posterior-predictive ensemble accuracy."""
+    P = np.asarray(particles, np.float64)
+    w = P[:, 1:]
+    prob = _sigmoid(np.asarray(x_test, np.float64) @ w.T).mean(1)
+    return float(((prob > 0.5) == (np.asarray(t_test).reshape(-1) > 0)).mean())
+
+
+def ref_init(n, d, seed):
+    """Reference init (sampler.py:58-60): n successive Normal(0,1).sample((d,1))
+    draws from torch's global CPU generator (== n successive torch.randn(d,1))."""
+    import torch
+    torch.manual_seed(seed)
+    return torch.cat([torch.randn(d, 1) for _ in range(n)], dim=1).t().contiguous().numpy()

@@ -1,0 +1,144 @@
+"""CPU-only tests: the C ABI library loads and exports every symbol the header
+declares, host-side logic (kernel probing, padding helpers), the gloo exchange
+layer at world_size 2, and that the product path refuses to run without a GPU."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "dsvgd.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dsvgd_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from dsvgd import _native
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    names = header_functions()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # the ctypes table mirrors the header exactly
+    assert sorted(_native.SIGNATURES) == names
+
+
+def test_meta_calls_without_gpu():
+    from dsvgd import _native
+    from dsvgd.engine import _SelectState
+    lib = _native.load()
+    assert lib.dsvgd_abi_version() == 1
+    assert lib.dsvgd_select_state_bytes() == ctypes.sizeof(_SelectState)
+    assert lib.dsvgd_pad128(1) == 128 and lib.dsvgd_pad128(129) == 256
+    assert lib.dsvgd_dp(1) == 32 and lib.dsvgd_dp(256) == 256 and lib.dsvgd_dp(255) == 256
+    assert lib.dsvgd_ldy(32) == 128 and lib.dsvgd_ldy(128) == 256 and lib.dsvgd_ldy(256) == 512
+    assert lib.dsvgd_ldy(1024) == 2048
+    assert lib.dsvgd_logreg_workspace_bytes(100, 400, 2) % 256 == 0
+    # argument validation returns an error code (no GPU work is enqueued)
+    rc = lib.dsvgd_sqdist(None, 0, None, 0, 0, 0, 32, None, 128, None, None)
+    assert rc == -1 and b"null" in lib.dsvgd_last_error()
+
+
+def test_kernel_probe_accepts_reference_kernels():
+    from dsvgd.kernels import RBF, resolve_kernel
+
+    def ref_kernel(x, y):                  # experiments/logreg.py:60-61
+        return torch.exp(-1. * torch.dist(x, y, p=2) ** 2)
+    assert resolve_kernel(ref_kernel, 3).h == 1.0
+    assert resolve_kernel(lambda x, y: torch.exp(-torch.dist(x, y) ** 2 / 3.7), 5).h == \
+        pytest.approx(3.7, rel=1e-5)
+    assert resolve_kernel(RBF("median"), 4).median
+    with pytest.raises(ValueError):
+        resolve_kernel(lambda x, y: torch.exp(-torch.dist(x, y)), 3)   # Laplace kernel
+    with pytest.raises(ValueError):
+        resolve_kernel(lambda x, y: (x * y).sum(), 3)
+
+
+def test_product_path_fails_loudly_without_gpu():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import dsvgd
+    from dsvgd._native import NativeUnavailable
+    s = dsvgd.Sampler(2, dsvgd.targets.Gaussian([0, 0], [1, 1]), dsvgd.RBF(1.0))
+    with pytest.raises(NativeUnavailable):
+        s.sample(8, 1, 0.1, verbose=False)
+    with pytest.raises(NativeUnavailable):
+        dsvgd.DistSampler(0, 1, dsvgd.targets.Gaussian([0, 0], [1, 1]), dsvgd.RBF(1.0),
+                          torch.zeros(8, 2), 1, 1, False, False, False)
+
+
+def test_reference_targets_are_callables():
+    import dsvgd
+    from oracle import svgd_oracle as O
+    rs = np.random.RandomState(0)
+    x, t = rs.randn(40, 3).astype(np.float32), np.sign(rs.randn(40)).astype(np.float32)
+    tgt = dsvgd.targets.LogisticRegression(x, t)
+    X = rs.randn(5, 4).astype(np.float32)
+    for i in range(5):
+        xi = torch.tensor(X[i], requires_grad=True)
+        tgt(xi).backward()
+        ref = O.score_logreg(X[i:i + 1], x, t)[0]
+        assert np.abs(xi.grad.numpy() - ref).max() < 1e-4 * max(1, np.abs(ref).max())
+    g = dsvgd.targets.GaussianMixture1D()
+    xi = torch.tensor([0.7], requires_grad=True)
+    g(xi).backward()
+    assert abs(float(xi.grad[0]) - float(O.score_gmm(np.array([[0.7]]))[0, 0])) < 1e-6
+
+
+# ---------------------------------------------------------- gloo, 2 ranks --
+def _gloo_worker(rank, port, q):
+    import torch.distributed as dist
+    from dsvgd import exchange
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    own = torch.full((3, 2), float(rank + 1))
+    out = torch.empty(6, 2)
+    exchange.all_gather_blocks(own, out)
+    red = torch.arange(4, dtype=torch.int64) * (rank + 1)
+    exchange.all_reduce_sum(red)
+    recv = torch.empty(3, 2)
+    exchange.ring_shift(own, recv, rank, 2)
+    q.put((rank, out.numpy(), red.numpy(), recv.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_exchange_gloo_world2():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gloo_worker, args=(r, 29751, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, out, red, recv in res:
+        np.testing.assert_array_equal(out, np.concatenate([np.full((3, 2), 1.), np.full((3, 2), 2.)]))
+        np.testing.assert_array_equal(red, np.arange(4) * 3)
+        np.testing.assert_array_equal(recv, np.full((3, 2), float((rank - 1) % 2 + 1)))
+
+
+def test_dist_oracle_jacobi_equals_sequential_at_tiny_step(golden):
+    """Host logic check of the oracle's two orders on the golden S=2 inputs."""
+    from oracle import svgd_oracle as O
+    g = golden("g4_dist_s2_all_scores")
+    x, t = g["x_train"], g["t_train"]
+    per = x.shape[0] // 2
+    fns = [(lambda X, r=r: O.score_logreg(X, x[r * per:(r + 1) * per], t[r * per:(r + 1) * per]))
+           for r in range(2)]
+    a = O.DistOracle(list(g["init"]), fns, per, 2 * per, True, True, sequential=True)
+    b = O.DistOracle(list(g["init"]), fns, per, 2 * per, True, True, sequential=False)
+    a.step(1e-7)
+    b.step(1e-7)
+    assert np.abs(a.X[0] - b.X[0]).max() < 1e-9

@@ -1,0 +1,97 @@
+"""Pin the CPU oracle to the reference: every golden vector in tests/golden/
+(produced by running the reference itself, see tests/golden/make_golden.py)."""
+import numpy as np
+import pytest
+
+from oracle import svgd_oracle as O
+
+PHI_TOL = 1e-5      # north_star: 1e-5 relative per step on phi (max-normalised)
+TRAJ_TOL = 1e-4     # Gauss-Seidel trajectory, fp64 oracle vs fp32 reference
+
+
+def score_fn_for(g):
+    tgt = str(g["target"])
+    if tgt == "gmm":
+        return O.score_gmm
+    if tgt == "gaussian":
+        return lambda X: O.score_gaussian(X, g["mu"], g["lam"])
+    if tgt == "logreg":
+        return lambda X: O.score_logreg(X, g["x_train"], g["t_train"])
+    raise KeyError(tgt)
+
+
+@pytest.mark.parametrize("name", ["g1_gmm_n64", "g1_gauss_n128_d8_medh", "g1_gauss_n64_d64_h1",
+                                  "g1_logreg_n100"])
+def test_phi_matches_reference(golden, name):
+    g = golden(name)
+    X, ref = g["X"], g["phi"]
+    got = O.phi(X, score_fn_for(g)(X), float(g["h"]))
+    err = np.abs(got - ref).max() / np.abs(ref).max()
+    assert err < PHI_TOL, err
+
+
+def test_median_h_fixture_definition(golden):
+    g = golden("g1_gauss_n128_d8_medh")
+    h, med = O.median_bandwidth(g["X"])
+    assert abs(h - float(g["h"])) <= 1e-12 * h
+
+
+def test_pairloop_matches_vectorised(golden):
+    g = golden("g1_logreg_n100")
+    X = g["X"].astype(np.float64)
+    fn = score_fn_for(g)
+    full = O.phi(X, fn(X), 1.0)
+    for i in (0, 17, 99):
+        row = O.phi_pairloop_row(i, X, fn, 1.0)
+        assert np.abs(row - full[i]).max() <= 1e-12 * np.abs(full).max()
+
+
+@pytest.mark.parametrize("name", ["g2_sample_gauss_n32_d2", "g2_sample_gmm_n50"])
+def test_sampler_trajectory(golden, name):
+    g = golden(name)
+    n, d, T = int(g["n"]), int(g["d"]), int(g["T"])
+    X0 = O.ref_init(n, d, int(g["seed"]))
+    np.testing.assert_array_equal(X0, g["values"][0])     # bit-exact reference init
+    hist = O.sampler_sequential(X0, score_fn_for(g), float(g["h"]), T, float(g["eps"]))
+    assert np.abs(hist - g["values"]).max() < TRAJ_TOL
+    # history layout of sampler.py:66,73: rows ordered (timestep, particle)
+    np.testing.assert_array_equal(g["timestep"], np.repeat(np.arange(T + 1), n))
+    np.testing.assert_array_equal(g["particle"], np.tile(np.arange(n), T + 1))
+
+
+def _dist_oracle(g, sequential=True):
+    S, n = int(g["S"]), int(g["n"])
+    mode = str(g["mode"])
+    x, t = g["x_train"], g["t_train"]
+    per = x.shape[0] // S
+    fns = [(lambda X, r=r: O.score_logreg(X, x[r * per:(r + 1) * per], t[r * per:(r + 1) * per]))
+           for r in range(S)]
+    return O.DistOracle(list(g["init"]), fns, per, per * S,
+                        exchange_particles=mode in ("all_particles", "all_scores"),
+                        exchange_scores=mode == "all_scores", h=1.0, sequential=sequential)
+
+
+@pytest.mark.parametrize("name", ["g3_dist_s1_partitions"] + [
+    "g4_dist_s%d_%s" % (S, m) for S in (2, 4) for m in ("partitions", "all_particles", "all_scores")])
+def test_distsampler_steps(golden, name):
+    g = golden(name)
+    D = _dist_oracle(g)
+    for step in range(int(g["steps"])):
+        D.step(float(g["eps"]))
+        for r in range(D.S):
+            assert D.start[r] == int(g["start"][r][step])
+            assert np.abs(D.own(r) - g["own"][r][step]).max() < TRAJ_TOL
+            assert np.abs(D.X[r] - g["full"][r][step]).max() < TRAJ_TOL
+
+
+def test_scores_match_autograd():
+    """Closed-form scores == torch autograd of the reference closures."""
+    import torch
+    from oracle.loop_baseline import logreg_logp, _dlogp
+    rs = np.random.RandomState(0)
+    x, t = rs.randn(50, 3).astype(np.float32), np.sign(rs.randn(50)).astype(np.float32)
+    X = rs.randn(7, 4).astype(np.float32)
+    lp = logreg_logp(x, t)
+    ref = np.stack([_dlogp(lp, torch.tensor(X[i])).numpy() for i in range(7)])
+    got = O.score_logreg(X, x, t)
+    assert np.abs(got - ref).max() < 1e-4 * max(1.0, np.abs(ref).max())
