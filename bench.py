@@ -162,7 +162,8 @@ def main():
                      "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
                      "flop_per_launch": flops, "avg_launch_ms": phi_ms},
         "stages_ms": stages,
-        "step_flop_6n2d_frac": (6.0 * m * n * d) / (1e-3 * el / args.steps) / 1e12 / PEAK_FP32_MFMA_TFLOPS,
+        "step_6n2d_mfma_frac": (6.0 * m * n * d) / (el / args.steps) / 1e12 / PEAK_FP32_MFMA_TFLOPS,
+        "phi_splits": int(sampler._engines[next(iter(sampler._engines))].splits),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, d, xl, tl, args.cpu_budget)

@@ -26,6 +26,7 @@ int fail_arg(const char* what);
 int check_launch(const char* kernel);
 
 inline int64_t roundup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+__host__ __device__ inline int64_t roundup128(int64_t x) { return (x + 127) & ~(int64_t)127; }
 
 // 32x32x2 f32 MFMA: lane l holds A[l&31][l>>5], B[l>>5][l&31]; the 16 result
 // registers hold C[(r&3) + 8*(r>>2) + 4*(l>>5)][l&31]  (r = register index).

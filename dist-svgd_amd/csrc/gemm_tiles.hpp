@@ -208,9 +208,11 @@ struct NNTile {
   }
 
   // Apanels: the block's row-panel (128 rows x K, panel layout); B: K x BC
-  // (row-major, ldb, already offset to the block's first column).
+  // (row-major, ldb, already offset to the block's first column); the K range
+  // [k0, k1) (multiples of 16) is this block's split-K slice.
   __device__ __forceinline__ void run(const float* __restrict__ Apanels, const float* __restrict__ B,
-                                      int64_t ldb, int64_t K, float scale, float* smem) {
+                                      int64_t ldb, int64_t k0, int64_t k1, float scale,
+                                      float* smem) {
     const int wc = threadIdx.x >> 6;
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
@@ -220,12 +222,13 @@ struct NNTile {
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[mi][ni][q] = 0.f;
     }
-    load(Apanels, B, ldb, 0);
+    if (k0 >= k1) return;
+    load(Apanels, B, ldb, k0);
     store(smem);
     __syncthreads();
     int cur = 0;
-    for (int64_t j0 = 0; j0 < K; j0 += BJ) {
-      const bool more = j0 + BJ < K;
+    for (int64_t j0 = k0; j0 < k1; j0 += BJ) {
+      const bool more = j0 + BJ < k1;
       if (more) load(Apanels, B, ldb, j0 + BJ);
       compute(smem + cur * kStage, wc, scale);
       if (more) store(smem + (cur ^ 1) * kStage);

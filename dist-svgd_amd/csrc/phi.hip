@@ -13,20 +13,28 @@
 
 namespace dsvgd {
 
+// blockIdx.z = split-K slice z: K columns [z*kchunk, min(K,(z+1)*kchunk)) into
+// the partial C + z*m*ldc (and rowsum + z*m_pad); phi_finish sums the slices
+// in order (deterministic, no atomics).
 template <int TN, bool EXP>
 __global__ __launch_bounds__(256) void nn_kernel(const float* __restrict__ A, int64_t a_npad,
                                                  const float* __restrict__ B, int64_t ldb,
-                                                 int64_t K, const dsvgd_select_state* __restrict__ st,
+                                                 int64_t K, int64_t kchunk,
+                                                 const dsvgd_select_state* __restrict__ st,
                                                  float* __restrict__ C, int64_t ldc,
                                                  float* __restrict__ rowsum, int64_t m) {
   using Tile = NNTile<TN, EXP>;
   __shared__ __attribute__((aligned(16))) float smem[Tile::kSmemFloats];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
+  const int64_t k0 = (int64_t)blockIdx.z * kchunk;
+  const int64_t k1 = min(K, k0 + kchunk);
+  C += (int64_t)blockIdx.z * m * ldc;
+  if (rowsum) rowsum += (int64_t)blockIdx.z * roundup128(m);
   float scale = 0.f;
   if (EXP) scale = -st->inv_h * kLog2e;
   Tile tile;
-  tile.run(A + (i0 >> 7) * (a_npad >> 4) * kPanelElems, B + c0, ldb, K, scale, smem);
+  tile.run(A + (i0 >> 7) * (a_npad >> 4) * kPanelElems, B + c0, ldb, k0, k1, scale, smem);
 
   const int lane = threadIdx.x & 63, wc = threadIdx.x >> 6;
 #pragma unroll
@@ -51,8 +59,9 @@ __global__ __launch_bounds__(256) void nn_kernel(const float* __restrict__ A, in
 }
 
 // phi[i][c] = inv_n (KS[i][c] + (2/h)(r_i xc[i][c] - KX[i][c])); X[i][c] += step phi.
+// KY / rowsum hold `splits` split-K partials, summed here in slice order.
 __global__ __launch_bounds__(256) void phi_finish_kernel(
-    const float* __restrict__ KY, int64_t ldk, const float* __restrict__ rowsum,
+    const float* __restrict__ KY, int64_t ldk, const float* __restrict__ rowsum, int splits,
     const float* __restrict__ Y, int64_t ldy, int64_t row0, int64_t m, int64_t d, int64_t dp,
     const dsvgd_select_state* __restrict__ st, float inv_n, float step, float* __restrict__ phi,
     int64_t ldphi, float* __restrict__ X, int64_t ldx) {
@@ -60,9 +69,16 @@ __global__ __launch_bounds__(256) void phi_finish_kernel(
   if (t >= m * d) return;
   const int64_t i = t / d, c = t % d;
   const float two_inv_h = 2.f * st->inv_h;
-  const float kx = KY[i * ldk + c], ks = KY[i * ldk + dp + c];
+  const int64_t mp = roundup128(m);
+  float kx = 0.f, ks = 0.f, r = 0.f;
+  for (int z = 0; z < splits; ++z) {
+    const float* ky = KY + (int64_t)z * m * ldk + i * ldk;
+    kx += ky[c];
+    ks += ky[dp + c];
+    r += rowsum[(int64_t)z * mp + i];
+  }
   const float xc = Y[(row0 + i) * ldy + c];
-  const float p = inv_n * (ks + two_inv_h * (rowsum[i] * xc - kx));
+  const float p = inv_n * (ks + two_inv_h * (r * xc - kx));
   if (phi) phi[i * ldphi + c] = p;
   if (X) X[i * ldx + c] += step * p;
 }
@@ -119,26 +135,37 @@ __global__ __launch_bounds__(256) void phi_row_kernel(float* __restrict__ X, int
 }
 
 template <int TN>
-int launch_nn(bool exp_, const float* A, int64_t a_npad, const float* B, int64_t ldb, int64_t K,
+int launch_nn(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
               const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
               int64_t cols, hipStream_t s) {
-  const dim3 grid(cols / (128 * TN), roundup(m, 128) / 128);
+  const int64_t kchunk = roundup((K + splits - 1) / splits, 16);
+  const dim3 grid(cols / (128 * TN), roundup(m, 128) / 128, splits);
   if (exp_)
-    hipLaunchKernelGGL((nn_kernel<TN, true>), grid, dim3(256), 0, s, A, a_npad, B, ldb, K, st, C,
-                       ldc, rowsum, m);
+    hipLaunchKernelGGL((nn_kernel<TN, true>), grid, dim3(256), 0, s, A, K, B, ldb, K, kchunk, st,
+                       C, ldc, rowsum, m);
   else
-    hipLaunchKernelGGL((nn_kernel<TN, false>), grid, dim3(256), 0, s, A, a_npad, B, ldb, K, st, C,
-                       ldc, rowsum, m);
+    hipLaunchKernelGGL((nn_kernel<TN, false>), grid, dim3(256), 0, s, A, K, B, ldb, K, kchunk, st,
+                       C, ldc, rowsum, m);
   return check_launch("nn_kernel");
 }
 
-// C[m x cols] = f(A) B with A in panel layout (m_pad x K), B row-major K x cols.
+// C[splits x m x cols] = f(A) B with A in panel layout (m_pad x K), B row-major K x cols.
 int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, int64_t cols,
-            const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-            hipStream_t s) {
-  if (cols % 512 == 0) return launch_nn<4>(exp_, A, K, B, ldb, K, st, C, ldc, rowsum, m, cols, s);
-  if (cols % 256 == 0) return launch_nn<2>(exp_, A, K, B, ldb, K, st, C, ldc, rowsum, m, cols, s);
-  return launch_nn<1>(exp_, A, K, B, ldb, K, st, C, ldc, rowsum, m, cols, s);
+            int splits, const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum,
+            int64_t m, hipStream_t s) {
+  if (cols % 512 == 0) return launch_nn<4>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, s);
+  if (cols % 256 == 0) return launch_nn<2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, s);
+  return launch_nn<1>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, s);
+}
+
+// split-K slices so that a phi_mm launch has >= 2 blocks per CU (256 CUs),
+// each slice keeping >= 64 K-steps (1024 columns) of its own.
+int64_t phi_splits(int64_t m, int64_t n, int64_t ldy) {
+  const int64_t cols = ldy % 512 == 0 ? 512 : (ldy % 256 == 0 ? 256 : 128);
+  const int64_t blocks = (roundup(m, 128) / 128) * (ldy / cols);
+  int64_t s = 1;
+  while (blocks * s < 512 && roundup(n, 128) / (2 * s) >= 1024) s *= 2;
+  return s;
 }
 
 }  // namespace dsvgd
@@ -147,9 +174,11 @@ using namespace dsvgd;
 
 extern "C" {
 
+int64_t dsvgd_phi_splits(int64_t m, int64_t n, int64_t ldy) { return phi_splits(m, n, ldy); }
+
 int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t m, int64_t n,
-                 const dsvgd_select_state* st, float* KY, int64_t ldk, float* rowsum,
-                 void* stream) {
+                 const dsvgd_select_state* st, int64_t splits, float* KY, int64_t ldk,
+                 float* rowsum, void* stream) {
   DSVGD_REQUIRE(D && Y && st && KY && rowsum, "null pointer");
   DSVGD_REQUIRE(m > 0 && n > 0, "sizes");
   const int64_t n_pad = roundup(n, 128);
@@ -157,19 +186,23 @@ int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64
   DSVGD_REQUIRE(ldy % 128 == 0 && ldk >= ldy, "ldy must be a multiple of 128, ldk >= ldy");
   DSVGD_REQUIRE(((uintptr_t)Y & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
   DSVGD_REQUIRE(roundup(m, 128) / 128 <= 65535, "too many row tiles");
-  return nn_gemm(true, D, n_pad, Y, ldy, ldy, st, KY, ldk, rowsum, m, (hipStream_t)stream);
+  DSVGD_REQUIRE(splits >= 1 && splits <= 1024, "splits must be in [1, 1024]");
+  return nn_gemm(true, D, n_pad, Y, ldy, ldy, (int)splits, st, KY, ldk, rowsum, m,
+                 (hipStream_t)stream);
 }
 
-int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, const float* Y,
-                     int64_t ldy, int64_t row0, int64_t m, int64_t d, int64_t dp,
+int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t splits,
+                     const float* Y, int64_t ldy, int64_t row0, int64_t m, int64_t d, int64_t dp,
                      const dsvgd_select_state* st, float inv_n, float step, float* phi,
                      int64_t ldphi, float* X, int64_t ldx, void* stream) {
   DSVGD_REQUIRE(KY && rowsum && Y && st, "null pointer");
+  DSVGD_REQUIRE(splits >= 1 && splits <= 1024, "splits must be in [1, 1024]");
   DSVGD_REQUIRE(m > 0 && d > 0 && dp >= d && ldk >= 2 * dp && ldy >= 2 * dp, "sizes");
   DSVGD_REQUIRE(!phi || ldphi >= d, "ldphi");
   DSVGD_REQUIRE(!X || ldx >= d, "ldx");
   hipLaunchKernelGGL(phi_finish_kernel, dim3((m * d + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, KY, ldk, rowsum, Y, ldy, row0, m, d, dp, st, inv_n,
+                     (hipStream_t)stream, KY, ldk, rowsum, (int)splits, Y, ldy, row0, m, d, dp,
+                     st, inv_n,
                      step, phi, ldphi, X, ldx);
   return check_launch("phi_finish");
 }

@@ -33,9 +33,10 @@ SIGNATURES = {
     "dsvgd_radix_hist": (_int, [_p, _i64, _i64, _i64, _int, _p, _p]),
     "dsvgd_radix_pick": (_int, [_p, _int, _p]),
     "dsvgd_set_bandwidth": (_int, [_p, _f, _p]),
-    "dsvgd_phi_mm": (_int, [_p, _i64, _p, _i64, _i64, _i64, _p, _p, _i64, _p, _p]),
-    "dsvgd_phi_finish": (_int, [_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64, _p, _f, _f,
-                                _p, _i64, _p, _i64, _p]),
+    "dsvgd_phi_splits": (_i64, [_i64, _i64, _i64]),
+    "dsvgd_phi_mm": (_int, [_p, _i64, _p, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p]),
+    "dsvgd_phi_finish": (_int, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _f,
+                                _f, _p, _i64, _p, _i64, _p]),
     "dsvgd_phi_row": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _f, _p, _p]),
     "dsvgd_score_gaussian": (_int, [_p, _i64, _i64, _i64, _p, _p, _f, _p, _i64, _p]),
     "dsvgd_score_gmm": (_int, [_p, _i64, _i64, _i64, _f, _p, _i64, _p]),
@@ -94,6 +95,19 @@ def ptr(t):
     if not t.is_cuda:
         raise ValueError("dsvgd kernels need device (HIP) tensors, got %s" % t.device)
     return t.data_ptr()
+
+
+def ld(t):
+    """Leading dimension (row stride, elements) of a row-major 2-D tensor; a
+    (n, 1) tensor is row-major whatever its column stride says."""
+    if t.dim() != 2:
+        raise ValueError("expected a 2-D tensor, got shape %s" % (tuple(t.shape),))
+    if t.shape[1] != 1 and t.stride(1) != 1:
+        raise ValueError("tensor must be row-major (stride(1) == 1), got strides %s"
+                         % (t.stride(),))
+    if t.dtype != torch.float32:
+        raise ValueError("dsvgd kernels take float32 tensors, got %s" % t.dtype)
+    return max(t.stride(0), t.shape[1]) if t.shape[0] == 1 else t.stride(0)
 
 
 def stream(device=None):

@@ -69,11 +69,13 @@ class DistSampler(object):
         self._particles = particles[:self._num_particles]
         if particles.is_cuda:
             self._device = N.require_gpu(particles.device)
-            assert self._particles.stride(1) == 1, "device particles must be row-major"
+            N.ld(self._particles)                 # row-major fp32 or ValueError
             self._work = self._particles          # updated in place
         else:
             self._device = N.require_gpu(device if device is not None else "cuda")
-            self._work = self._particles.detach().to(self._device, torch.float32).contiguous()
+            self._work = torch.empty(self._particles.shape, dtype=torch.float32,
+                                     device=self._device)
+            self._work.copy_(self._particles)
         self._scores = None
         if exchange_scores:
             self._scores = torch.empty(self._work.shape, dtype=torch.float32, device=self._device)

@@ -124,8 +124,9 @@ class PhiEngine(object):
         self.Y = torch.zeros(rows, self.ldy, **f32)
         self.norms = torch.zeros(rows, **f32)
         self.D = torch.empty(self.m_pad * self.n_pad, **f32)
-        self.KY = torch.empty(m, self.ldy, **f32)
-        self.rowsum = torch.empty(self.m_pad, **f32)
+        self.splits = lib.dsvgd_phi_splits(m, n, self.ldy)
+        self.KY = torch.empty(self.splits * m, self.ldy, **f32)
+        self.rowsum = torch.empty(self.splits * self.m_pad, **f32)
         self.mean = torch.empty(d, **f32)
         self.mean_ws = torch.empty(max(1, lib.dsvgd_colmean_workspace_floats(n, d)), **f32)
         self.phi = torch.empty(m, d, **f32)
@@ -134,18 +135,18 @@ class PhiEngine(object):
     # ------------------------------------------------------------ stages --
     def pack(self, X, S=None, score_scale=1.0):
         """X, S: (n, d) device tensors (row stride may exceed d)."""
-        assert X.shape == (self.n, self.d) and X.stride(1) == 1
+        assert X.shape == (self.n, self.d)
         s = N.stream(self.device)
         with span(self.timer, "pack"):
             self._pack(X, S, score_scale, s)
 
     def _pack(self, X, S, score_scale, s):
-        N.call("dsvgd_colmean", N.ptr(X), X.stride(0), self.n, self.d, N.ptr(self.mean_ws),
+        N.call("dsvgd_colmean", N.ptr(X), N.ld(X), self.n, self.d, N.ptr(self.mean_ws),
                N.ptr(self.mean), s)
-        lds = S.stride(0) if S is not None else self.d
+        lds = N.ld(S) if S is not None else self.d
         if S is not None:
-            assert S.shape == (self.n, self.d) and S.stride(1) == 1
-        N.call("dsvgd_pack", N.ptr(X), X.stride(0), N.ptr(S), lds, float(score_scale),
+            assert S.shape == (self.n, self.d)
+        N.call("dsvgd_pack", N.ptr(X), N.ld(X), N.ptr(S), lds, float(score_scale),
                N.ptr(self.mean), self.n, self.d, self.Y.shape[0], N.ptr(self.Y), self.ldy,
                N.ptr(self.norms), s)
 
@@ -157,7 +158,7 @@ class PhiEngine(object):
             st = self.state.ptr
         with span(self.timer, "sqdist"):
             N.call("dsvgd_sqdist", N.ptr(self.Y), self.ldy, N.ptr(self.norms), self.row0, self.m,
-                   self.n, self.dp, N.ptr(self.D), self.n_pad, st, s)
+                   self.n, self.d, N.ptr(self.D), self.n_pad, st, s)
 
     def median_bandwidth(self, allreduce=None):
         """Radix select over D (after distances(histogram=True))."""
@@ -180,14 +181,15 @@ class PhiEngine(object):
         s = N.stream(self.device)
         with span(self.timer, "phi_mm"):
             N.call("dsvgd_phi_mm", N.ptr(self.D), self.n_pad, N.ptr(self.Y), self.ldy, self.m,
-                   self.n, self.state.ptr, N.ptr(self.KY), self.ldy, N.ptr(self.rowsum), s)
+                   self.n, self.state.ptr, self.splits, N.ptr(self.KY), self.ldy,
+                   N.ptr(self.rowsum), s)
         if X_own is not None:
-            assert X_own.shape == (self.m, self.d) and X_own.stride(1) == 1
+            assert X_own.shape == (self.m, self.d)
         inv_n = 1.0 / self.n if inv_n is None else inv_n
-        N.call("dsvgd_phi_finish", N.ptr(self.KY), self.ldy, N.ptr(self.rowsum), N.ptr(self.Y),
-               self.ldy, self.row0, self.m, self.d, self.dp, self.state.ptr, float(inv_n),
+        N.call("dsvgd_phi_finish", N.ptr(self.KY), self.ldy, N.ptr(self.rowsum), self.splits,
+               N.ptr(self.Y), self.ldy, self.row0, self.m, self.d, self.dp, self.state.ptr, float(inv_n),
                float(step), N.ptr(self.phi) if write_phi else None, self.d,
-               N.ptr(X_own), X_own.stride(0) if X_own is not None else self.d, s)
+               N.ptr(X_own), N.ld(X_own) if X_own is not None else self.d, s)
 
     # ------------------------------------------------------------ helpers --
     def step(self, X, S, X_own=None, step=0.0, h=None, score_scale=1.0, allreduce=None,
@@ -218,7 +220,7 @@ def sequential_sweep(X, S, rows, h_state, step, target=None, score_scale=1.0, ph
     n, d = X.shape
     s = N.stream(X.device)
     for k, i in enumerate(rows):
-        N.call("dsvgd_phi_row", N.ptr(X), X.stride(0), N.ptr(S), S.stride(0), n, d, int(i),
+        N.call("dsvgd_phi_row", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), n, d, int(i),
                h_state.ptr, float(step), N.ptr(phi_out[k]) if phi_out is not None else None, s)
         if target is not None:
             target.score(X[i:i + 1], S[i:i + 1], score_scale)

@@ -49,7 +49,8 @@ class Sampler(object):
         q = Normal(0, 1)
         make_sample = lambda: q.sample((self._d, 1))  # noqa: E731  (sampler.py:58-60)
         particles = torch.cat([make_sample() for _ in range(n)], dim=1).t()
-        X = particles.contiguous().to(dev)
+        X = torch.empty(n, self._d, dtype=torch.float32, device=dev)
+        X.copy_(particles)
         d = self._d
         hist = torch.empty(num_iter + 1, n, d, dtype=torch.float32, device=dev)
         S = torch.empty(n, d, dtype=torch.float32, device=dev)

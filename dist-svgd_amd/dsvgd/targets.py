@@ -52,8 +52,8 @@ class Gaussian(Target):
         n, d = X.shape
         assert d == self.mu.numel(), "Gaussian target has d=%d" % self.mu.numel()
         mu, lam = self._params(X.device)
-        N.call("dsvgd_score_gaussian", N.ptr(X), X.stride(0), n, d, N.ptr(mu), N.ptr(lam),
-               float(scale), N.ptr(out), out.stride(0), N.stream(X.device))
+        N.call("dsvgd_score_gaussian", N.ptr(X), N.ld(X), n, d, N.ptr(mu), N.ptr(lam),
+               float(scale), N.ptr(out), N.ld(out), N.stream(X.device))
 
 
 class GaussianMixture1D(Target):
@@ -67,8 +67,8 @@ class GaussianMixture1D(Target):
 
     def score(self, X, out, scale=1.0):
         n, d = X.shape
-        N.call("dsvgd_score_gmm", N.ptr(X), X.stride(0), n, d, float(scale), N.ptr(out),
-               out.stride(0), N.stream(X.device))
+        N.call("dsvgd_score_gmm", N.ptr(X), N.ld(X), n, d, float(scale), N.ptr(out),
+               N.ld(out), N.stream(X.device))
 
 
 class LogisticRegression(Target):
@@ -121,8 +121,8 @@ class LogisticRegression(Target):
             self._ws[key] = ws
         base = ws.data_ptr()
         aligned = (base + 255) // 256 * 256
-        N.call("dsvgd_score_logreg", N.ptr(X), X.stride(0), n, d, N.ptr(xd), xd.stride(0),
-               N.ptr(t), self.N, float(scale), N.ptr(out), out.stride(0), aligned,
+        N.call("dsvgd_score_logreg", N.ptr(X), N.ld(X), n, d, N.ptr(xd), N.ld(xd),
+               N.ptr(t), self.N, float(scale), N.ptr(out), N.ld(out), aligned,
                N.stream(X.device))
 
 

@@ -81,16 +81,20 @@ int dsvgd_pack(const float* X, int64_t ldx, const float* S, int64_t lds, float s
                const float* mean, int64_t n, int64_t d, int64_t rows_pad, float* Y, int64_t ldy,
                float* norms, void* stream);
 
-/* ---- pairwise squared distances (MFMA fp32) ---------------------------- */
-/* D[i][j] = max(0, |y_i|^2 + |y_j|^2 - 2 y_i.y_j) for the owned row block
- * i in [row0, row0+m) against all j < n (D[i][i]=0 exactly, pads = +inf),
- * computed on v_mfma_f32_32x32x2_f32; if hist != NULL also accumulates the
- * first radix-select histogram (key bits 31..21) of the valid entries.
+/* ---- pairwise squared distances ---------------------------------------- */
+/* D[i][j] = ||y_i - y_j||^2 for the owned row block i in [row0, row0+m) of Y
+ * against all j < n, y = the first d columns of Y (centred particles).
+ * d <= 64: explicit differences on the VALU (exact like the reference);
+ * d > 64: max(0, |y_i|^2 + |y_j|^2 - 2 y_i.y_j) on v_mfma_f32_32x32x2_f32,
+ * upper-triangle tiles only when m == n and row0 == 0 (the transpose is
+ * stored too).  D[i][i] = 0 exactly, pads = +inf, panel layout (ldd = n_pad).
+ * If st != NULL also accumulates the first radix-select histogram (key bits
+ * 31..21) of the valid entries into st->hist.
  * Replaces torch.dist(x, y, p=2)**2 inside kernel(...) at
  * experiments/logreg.py:60-61 / experiments/gmm.py:23-24 as called per pair
  * from dsvgd/sampler.py:38 and dsvgd/distsampler.py:91-97. */
 int dsvgd_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0, int64_t m,
-                 int64_t n, int64_t dp, float* D, int64_t ldd, dsvgd_select_state* st,
+                 int64_t n, int64_t d, float* D, int64_t ldd, dsvgd_select_state* st,
                  void* stream);
 
 /* ---- median bandwidth: exact radix select over the n x n distances ----- */
@@ -99,7 +103,8 @@ int dsvgd_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0, 
  * over the full matrix incl. the diagonal, h = median / log n.)            */
 int dsvgd_select_init(dsvgd_select_state* st, int64_t n_total, void* stream);
 /* histogram of key digit `pass` (1: bits 31..21, 2: 20..10, 3: 9..0) of the
- * entries of D[0:m, 0:n] whose higher digits equal st->prefix. */
+ * finite entries of the m_pad x n_pad panel buffer D (pads are +inf and never
+ * counted) whose higher digits equal st->prefix. */
 int dsvgd_radix_hist(const float* D, int64_t ldd, int64_t m, int64_t n, int pass,
                      dsvgd_select_state* st, void* stream);
 /* pick the bin holding rank k, fix its digit, clear hist; after pass 3
@@ -109,18 +114,24 @@ int dsvgd_radix_pick(dsvgd_select_state* st, int pass, void* stream);
 int dsvgd_set_bandwidth(dsvgd_select_state* st, float h, void* stream);
 
 /* ---- phi: K.[Xc | S] on MFMA with the fused RBF exp -------------------- */
-/* KY[i][:] = sum_j exp(-D[i][j]/h) Y[j][:],  rowsum[i] = sum_j exp(-D[i][j]/h)
- * (h read from st on device).  Replaces the inner loop of
- * dsvgd/sampler.py:35-40 (_phi_hat) and dsvgd/distsampler.py:84-101. */
+/* KY_z[i][:] = sum_{j in slice z} exp(-D[i][j]/h) Y[j][:] and rowsum_z[i] =
+ * sum_{j in slice z} exp(-D[i][j]/h) for split-K slices z < splits of the
+ * columns (h read from st on device).  KY holds splits x m rows (ldk >= ldy,
+ * slice z at KY + z*m*ldk), rowsum splits x roundup(m,128) floats.
+ * Replaces the inner loop of dsvgd/sampler.py:35-40 (_phi_hat) and
+ * dsvgd/distsampler.py:84-101.  dsvgd_phi_splits gives a slice count that
+ * fills the 256 CUs (>= 2 blocks per CU) for an m-row block. */
+int64_t dsvgd_phi_splits(int64_t m, int64_t n, int64_t ldy);
 int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t m,
-                 int64_t n, const dsvgd_select_state* st, float* KY, int64_t ldk,
-                 float* rowsum, void* stream);
+                 int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
+                 int64_t ldk, float* rowsum, void* stream);
 
-/* phi[i] = inv_n * (KS[i] + (2/h) (rowsum[i] xc[i] - KXc[i]))  and, if X != NULL,
- * X[i] += step * phi[i]  (the update of dsvgd/sampler.py:68 /
- * dsvgd/distsampler.py:200, Jacobi order).  phi may be NULL. */
-int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, const float* Y,
-                     int64_t ldy, int64_t row0, int64_t m, int64_t d, int64_t dp,
+/* phi[i] = inv_n * (KS[i] + (2/h) (rowsum[i] xc[i] - KXc[i])) with the split-K
+ * partials summed in slice order, and, if X != NULL, X[i] += step * phi[i]
+ * (the update of dsvgd/sampler.py:68 / dsvgd/distsampler.py:200, Jacobi
+ * order).  phi may be NULL. */
+int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t splits,
+                     const float* Y, int64_t ldy, int64_t row0, int64_t m, int64_t d, int64_t dp,
                      const dsvgd_select_state* st, float inv_n, float step, float* phi,
                      int64_t ldphi, float* X, int64_t ldx, void* stream);
 

@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU-box session: smoke -> gpu tests -> bench -> rocprof kernel stats.
+# Stops at the first GPU fault / abort / timeout (exit 124,134,137,139 or >128).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-run}
+mkdir -p "$OUT"
+fatal() { local rc=$1; [ "$rc" -eq 124 ] || [ "$rc" -eq 134 ] || [ "$rc" -eq 137 ] || [ "$rc" -eq 139 ] || [ "$rc" -gt 128 ]; }
+step() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*" | tee -a "$OUT/steps.log"
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name exit $rc" | tee -a "$OUT/steps.log"
+  tail -5 "$OUT/$name.log"
+  if fatal $rc; then echo "FATAL in $name ($rc): stopping"; exit $rc; fi
+  return 0
+}
+for s in ${STEPS:-smoke tests bench prof}; do
+  case $s in
+    smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) step tests 1500 python -m pytest tests -m gpu -q ${PYTEST_ARGS:-} ;;
+    bench) step bench 900 python bench.py --steps ${BSTEPS:-10} --warmup 3 ${BENCH_ARGS:-} ;;
+    prof)  step prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    pmc)   step pmc 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmcw)  step pmcw 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+  esac
+done
+echo ALL DONE

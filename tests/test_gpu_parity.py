@@ -54,7 +54,7 @@ def engine_phi(X, S, h):
 
 
 # ----------------------------------------------------------- distances --
-@pytest.mark.parametrize("n,d", [(1, 1), (2, 3), (129, 37), (300, 64), (513, 256)])
+@pytest.mark.parametrize("n,d", [(1, 1), (2, 3), (129, 37), (300, 64), (513, 256), (1000, 100)])
 def test_sqdist_matches_oracle(n, d):
     rs = np.random.RandomState(n + d)
     X = (rs.randn(n, d) * 1.5 + 3.0).astype(np.float32)
@@ -148,6 +148,26 @@ def test_phi_matches_oracle(n, d, median):
     hh = eng.state.read()[1] if median else h
     ref = O.phi(X, S, hh)
     assert rel_err(phi, ref) < PHI_TOL
+
+
+@pytest.mark.parametrize("n,d,m,row0", [(4096, 256, 1024, 1024), (16384, 96, 2048, 14336),
+                                        (3000, 40, 1000, 1500)])
+def test_phi_row_block_split_k(n, d, m, row0):
+    """A DistSampler rank's row block (non-symmetric D, split-K phi_mm)."""
+    rs = np.random.RandomState(m)
+    X = rs.randn(n, d).astype(np.float32)
+    S = rs.randn(n, d).astype(np.float32)
+    eng = dsvgd().PhiEngine(n, d, m=m, row0=row0, device=DEV)
+    if n >= 4096:
+        assert eng.splits > 1
+    eng.step(gpu(X), gpu(S), h=None)
+    _, h, _ = eng.state.read()
+    # h: the k=(n^2-1)//2 rank searched over this m x n block alone (no
+    # all-reduce in one process) -- phi is checked for that h
+    sample = np.arange(0, m, max(1, m // 64))
+    ref = O.phi(X, S, h, rows=row0 + sample)
+    got = eng.phi.cpu().numpy()[sample]
+    assert rel_err(got, ref) < PHI_TOL
 
 
 def test_phi_full_size_sampled_rows():
