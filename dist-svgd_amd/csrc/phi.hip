@@ -83,6 +83,72 @@ __global__ __launch_bounds__(256) void phi_finish_kernel(
   if (X) X[i * ldx + c] += step * p;
 }
 
+// d <= 64: phi from explicit differences, the reference's own pairwise form
+//   phi_i = inv_n sum_j k_ij (s_j + (2/h)(x_i - x_j))
+// (no r_i x_i - (K X)_i cancellation, which at small d and a narrow bandwidth
+// exceeds the 1e-5 tolerance).  Block: 64 rows x 64 columns; thread (rq, cq)
+// owns rows 4rq..+3 x columns 4cq..+3; j streams in chunks of 64 through LDS
+// (K chunk transposed [j][i], x_j and s_j [j][c]).  VALU: 3 ops per (i,j,c).
+constexpr int kPhiDirectMaxD = 64;
+
+__global__ __launch_bounds__(256) void phi_direct_kernel(
+    const float* __restrict__ D, int64_t n_pad, const float* __restrict__ Y, int64_t ldy,
+    int64_t row0, int64_t m, int64_t n, int d, int64_t dp,
+    const dsvgd_select_state* __restrict__ st, float inv_n, float step, float* __restrict__ phi,
+    int64_t ldphi, float* __restrict__ X, int64_t ldx) {
+  __shared__ __attribute__((aligned(16))) float kT[64][64];
+  __shared__ __attribute__((aligned(16))) float xs[64][64];
+  __shared__ __attribute__((aligned(16))) float ss[64][64];
+  const int t = threadIdx.x, rq = t >> 4, cq = t & 15;
+  const int64_t i0 = (int64_t)blockIdx.x * 64;
+  const float inv_h = st->inv_h;
+  const float scale = -inv_h * kLog2e, g = 2.f * inv_h;
+  float xi[4][4], acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int64_t i = i0 + 4 * rq + a;
+      const int col = 4 * cq + c;
+      xi[a][c] = (i < m && col < d) ? Y[(row0 + i) * ldy + col] : 0.f;
+      acc[a][c] = 0.f;
+    }
+  for (int64_t j0 = 0; j0 < n; j0 += 64) {
+    for (int e = t; e < 64 * 64; e += 256) {
+      const int r = e >> 6, q = e & 63;  // kT[q][r]: row i0+r, column j0+q
+      const int64_t i = i0 + r, j = j0 + q;
+      kT[q][r] = (i < m && j < n) ? __builtin_amdgcn_exp2f(D[panel_off(i, j, n_pad)] * scale) : 0.f;
+      const int64_t jr = j0 + r;
+      xs[r][q] = (jr < n && q < d) ? Y[jr * ldy + q] : 0.f;
+      ss[r][q] = (jr < n && q < d) ? Y[jr * ldy + dp + q] : 0.f;
+    }
+    __syncthreads();
+    const int jn = (int)min((int64_t)64, n - j0);
+    for (int q = 0; q < jn; ++q) {
+      const f32x4 k4 = *reinterpret_cast<const f32x4*>(&kT[q][4 * rq]);
+      const f32x4 x4 = *reinterpret_cast<const f32x4*>(&xs[q][4 * cq]);
+      const f32x4 s4 = *reinterpret_cast<const f32x4*>(&ss[q][4 * cq]);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[a][c] = fmaf(k4[a], fmaf(g, xi[a][c] - x4[c], s4[c]), acc[a][c]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int64_t i = i0 + 4 * rq + a;
+      const int col = 4 * cq + c;
+      if (i < m && col < d) {
+        const float p = inv_n * acc[a][c];
+        if (phi) phi[i * ldphi + col] = p;
+        if (X) X[i * ldx + col] += step * p;
+      }
+    }
+}
+
 // Gauss-Seidel row update (reference order, exact differences, no Gram):
 // one block; j in chunks of 256 (one per thread) -> k_j in LDS -> columns.
 __global__ __launch_bounds__(256) void phi_row_kernel(float* __restrict__ X, int64_t ldx,
@@ -205,6 +271,22 @@ int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t 
                      st, inv_n,
                      step, phi, ldphi, X, ldx);
   return check_launch("phi_finish");
+}
+
+int dsvgd_phi_direct(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t row0,
+                     int64_t m, int64_t n, int64_t d, const dsvgd_select_state* st, float inv_n,
+                     float step, float* phi, int64_t ldphi, float* X, int64_t ldx, void* stream) {
+  DSVGD_REQUIRE(D && Y && st, "null pointer");
+  DSVGD_REQUIRE(m > 0 && n > 0 && d > 0 && row0 >= 0, "sizes");
+  DSVGD_REQUIRE(d <= kPhiDirectMaxD, "phi_direct supports d <= 64");
+  const int64_t n_pad = roundup(n, 128), dp = roundup(d, 32);
+  DSVGD_REQUIRE(ldd == n_pad, "ldd must equal roundup(n,128) (panel layout)");
+  DSVGD_REQUIRE(ldy >= 2 * dp, "ldy");
+  DSVGD_REQUIRE(!phi || ldphi >= d, "ldphi");
+  DSVGD_REQUIRE(!X || ldx >= d, "ldx");
+  hipLaunchKernelGGL(phi_direct_kernel, dim3((m + 63) / 64), dim3(256), 0, (hipStream_t)stream, D,
+                     n_pad, Y, ldy, row0, m, n, (int)d, dp, st, inv_n, step, phi, ldphi, X, ldx);
+  return check_launch("phi_direct");
 }
 
 int dsvgd_phi_row(float* X, int64_t ldx, const float* S, int64_t lds, int64_t n_int, int64_t d,

@@ -176,20 +176,31 @@ class PhiEngine(object):
     def fixed_bandwidth(self, h):
         N.call("dsvgd_set_bandwidth", self.state.ptr, float(h), N.stream(self.device))
 
+    DIRECT_MAX_D = 64
+
     def direction(self, X_own=None, step=0.0, write_phi=True, inv_n=None):
-        """phi for the owned rows; optionally X_own += step * phi (in place)."""
+        """phi for the owned rows; optionally X_own += step * phi (in place).
+        d <= 64: pairwise VALU form (dsvgd_phi_direct); else K.[Xc|S] on MFMA."""
         s = N.stream(self.device)
+        if X_own is not None:
+            assert X_own.shape == (self.m, self.d)
+        inv_n = 1.0 / self.n if inv_n is None else inv_n
+        phi = N.ptr(self.phi) if write_phi else None
+        xo = N.ptr(X_own)
+        ldx = N.ld(X_own) if X_own is not None else self.d
+        if self.d <= self.DIRECT_MAX_D:
+            with span(self.timer, "phi_direct"):
+                N.call("dsvgd_phi_direct", N.ptr(self.D), self.n_pad, N.ptr(self.Y), self.ldy,
+                       self.row0, self.m, self.n, self.d, self.state.ptr, float(inv_n),
+                       float(step), phi, self.d, xo, ldx, s)
+            return
         with span(self.timer, "phi_mm"):
             N.call("dsvgd_phi_mm", N.ptr(self.D), self.n_pad, N.ptr(self.Y), self.ldy, self.m,
                    self.n, self.state.ptr, self.splits, N.ptr(self.KY), self.ldy,
                    N.ptr(self.rowsum), s)
-        if X_own is not None:
-            assert X_own.shape == (self.m, self.d)
-        inv_n = 1.0 / self.n if inv_n is None else inv_n
         N.call("dsvgd_phi_finish", N.ptr(self.KY), self.ldy, N.ptr(self.rowsum), self.splits,
-               N.ptr(self.Y), self.ldy, self.row0, self.m, self.d, self.dp, self.state.ptr, float(inv_n),
-               float(step), N.ptr(self.phi) if write_phi else None, self.d,
-               N.ptr(X_own), N.ld(X_own) if X_own is not None else self.d, s)
+               N.ptr(self.Y), self.ldy, self.row0, self.m, self.d, self.dp, self.state.ptr,
+               float(inv_n), float(step), phi, self.d, xo, ldx, s)
 
     # ------------------------------------------------------------ helpers --
     def step(self, X, S, X_own=None, step=0.0, h=None, score_scale=1.0, allreduce=None,

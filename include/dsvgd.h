@@ -135,6 +135,15 @@ int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t 
                      const dsvgd_select_state* st, float inv_n, float step, float* phi,
                      int64_t ldphi, float* X, int64_t ldx, void* stream);
 
+/* d <= 64: phi (and the optional X update) straight from the pairwise form
+ * phi_i = inv_n sum_j k_ij (s_j + (2/h)(x_i - x_j)) on the VALU -- the
+ * reference's own per-pair expression (dsvgd/sampler.py:38-40), which avoids
+ * the r x - K X cancellation of the GEMM form at small d.  Replaces
+ * dsvgd_phi_mm + dsvgd_phi_finish for small d. */
+int dsvgd_phi_direct(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t row0,
+                     int64_t m, int64_t n, int64_t d, const dsvgd_select_state* st, float inv_n,
+                     float step, float* phi, int64_t ldphi, float* X, int64_t ldx, void* stream);
+
 /* Gauss-Seidel single-row update (reference order): for particle i, phi_i
  * from exact differences against the CURRENT X (rows < i already moved),
  * X[i] += step * phi_i.  Reproduces dsvgd/sampler.py:64-68 and

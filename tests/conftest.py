@@ -12,6 +12,29 @@ for p in (ROOT, PKG):
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
+# worst parity error seen per test (tests record into it; written at session end)
+PARITY = {}
+
+
+def record_parity(err):
+    key = os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0]
+    PARITY[key] = max(PARITY.get(key, 0.0), float(err))
+
+
+def pytest_sessionfinish(session, exitstatus):
+    if not PARITY:
+        return
+    import json
+    import time
+    out = os.path.join(ROOT, "gpurun_out")
+    try:
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, "parity_%d.json" % int(time.time())), "w") as f:
+            json.dump(dict(sorted(PARITY.items())), f, indent=1)
+    except OSError:
+        pass
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP) device")
 
