@@ -1,0 +1,272 @@
+// select.hip -- exact k-th order statistic of the squared distances (the
+// median-heuristic bandwidth; absent from the reference, pinned in SURVEY.md
+// a18) as an LSD-free radix select over the fp32 key bits (monotone as uint32
+// for D >= 0): digit 1 = bits 31..21, 2 = 20..10, 3 = 9..0.  Each pass is a
+// histogram (LDS per block, u64 global bins, all-reducible across ranks)
+// followed by a one-block pick; no host synchronisation anywhere.
+//
+// Sources of a pass: the D panel buffer (HBM stream, 4 B per entry per pass)
+// or, in bracketed mode, the candidate buffer the distance epilogue compacted
+// (~1 % of D).  The choice is made on device (st->fallback).
+#include <cmath>
+
+#include "select.hpp"
+
+namespace dsvgd {
+
+__device__ __forceinline__ void digit_of(int pass, uint32_t& shift, uint32_t& mask,
+                                         uint32_t& hishift) {
+  if (pass == 1) {
+    shift = 21; mask = 0x7FFu; hishift = 32;
+  } else if (pass == 2) {
+    shift = 10; mask = 0x7FFu; hishift = 21;
+  } else {
+    shift = 0; mask = 0x3FFu; hishift = 10;
+  }
+}
+
+__device__ __forceinline__ void hist_key(uint32_t key, uint32_t want, uint32_t shift,
+                                         uint32_t mask, uint32_t hishift, uint32_t* shist) {
+  if (key >= 0x7F800000u) return;  // +inf pad / NaN
+  const uint32_t hi = hishift >= 32 ? 0u : (key >> hishift);
+  if (hi == want) atomicAdd(&shist[(key >> shift) & mask], 1u);
+}
+
+// count: entries of D (any order); cand: optional candidate buffer used
+// instead of D when st->fallback == 0 (bracketed mode).
+__global__ __launch_bounds__(256) void radix_hist_kernel(const float* __restrict__ D, int64_t count,
+                                                         const float* __restrict__ cand, int pass,
+                                                         dsvgd_select_state* __restrict__ st) {
+  __shared__ uint32_t shist[DSVGD_RADIX_BINS];
+  for (int b = threadIdx.x; b < DSVGD_RADIX_BINS; b += 256) shist[b] = 0u;
+  uint32_t shift, mask, hishift;
+  digit_of(pass, shift, mask, hishift);
+  const uint32_t prefix = st->prefix;
+  const uint32_t want = hishift >= 32 ? 0u : (prefix >> hishift);
+  const bool use_cand = cand != nullptr && st->fallback == 0u;
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (use_cand) {
+    const int64_t nc = (int64_t)min(st->ncand, st->cand_cap);
+    for (int64_t q = t0; q < nc; q += stride)
+      hist_key(__float_as_uint(cand[q]), want, shift, mask, hishift, shist);
+  } else {
+    const int64_t c4 = count >> 2;
+    const f32x4* D4 = reinterpret_cast<const f32x4*>(D);
+    for (int64_t q = t0; q < c4; q += stride) {
+      const f32x4 v = D4[q];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        hist_key(__float_as_uint(v[e]), want, shift, mask, hishift, shist);
+    }
+    for (int64_t q = 4 * c4 + t0; q < count; q += stride)
+      hist_key(__float_as_uint(D[q]), want, shift, mask, hishift, shist);
+  }
+  __syncthreads();
+  flush_block_hist(shist, st);
+}
+
+// One block: find the bin that holds rank k, fix its digit, clear the bins.
+__global__ __launch_bounds__(256) void radix_pick_kernel(dsvgd_select_state* __restrict__ st,
+                                                         int pass) {
+  __shared__ unsigned long long part[256];
+  __shared__ unsigned long long excl[256];
+  const int t = threadIdx.x;
+  uint32_t shift, mask, hishift;
+  digit_of(pass, shift, mask, hishift);
+  const int nb = (int)mask + 1;  // 2048 or 1024 bins
+  const int per = nb / 256;      // 8 or 4 bins per thread
+  unsigned long long loc[8];
+  unsigned long long s = 0;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    loc[u] = u < per ? st->hist[t * per + u] : 0ull;
+    s += loc[u];
+  }
+  part[t] = s;
+  __syncthreads();
+  if (t == 0) {
+    unsigned long long run = 0;
+    for (int q = 0; q < 256; ++q) {
+      excl[q] = run;
+      run += part[q];
+    }
+  }
+  __syncthreads();
+  const unsigned long long k = st->k;
+  const unsigned long long lo = excl[t];
+  __syncthreads();
+  if (k >= lo && k < lo + part[t]) {
+    unsigned long long run = lo;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (u < per && k < run + loc[u]) {
+        const uint32_t digit = (uint32_t)(t * per + u);
+        const uint32_t prefix = st->prefix | (digit << shift);
+        st->prefix = prefix;
+        st->k = k - run;
+        st->passes_done = (uint32_t)pass;
+        if (pass == 3) {
+          const float med = __uint_as_float(prefix);
+          const double nt = (double)st->n_total;
+          float h = 1.f;
+          if (med > 0.f && nt > 1.0) h = (float)((double)med / log(nt));
+          st->median = med;
+          st->h = h;
+          st->inv_h = 1.f / h;
+        }
+        break;
+      }
+      run += u < per ? loc[u] : 0ull;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) st->hist[t * 8 + u] = 0ull;  // clear all 2048 bins
+}
+
+__device__ void reset_state(dsvgd_select_state* st, unsigned long long k,
+                            unsigned long long n_total) {
+  st->k = k;
+  st->n_total = n_total;
+  st->prefix = 0u;
+  st->passes_done = 0u;
+  st->median = NAN;
+  st->h = NAN;
+  st->inv_h = NAN;
+  st->fallback = 1u;
+  st->below = 0ull;
+  st->ncand = 0ull;
+}
+
+__global__ void select_init_kernel(dsvgd_select_state* st, int64_t n_total, int64_t k_rank) {
+  const int t = threadIdx.x;
+  for (int b = t; b < DSVGD_RADIX_BINS; b += blockDim.x) st->hist[b] = 0ull;
+  if (t == 0) {
+    const unsigned long long nn = (unsigned long long)n_total * (unsigned long long)n_total;
+    reset_state(st, k_rank >= 0 ? (unsigned long long)k_rank : (nn - 1ull) / 2ull,
+                (unsigned long long)n_total);
+  }
+}
+
+// bracket [lo, hi] = the medians the two sample selects found
+__global__ void bracket_init_kernel(dsvgd_select_state* st, int64_t n_total,
+                                    const dsvgd_select_state* lo_st,
+                                    const dsvgd_select_state* hi_st, int64_t cap) {
+  const int t = threadIdx.x;
+  for (int b = t; b < DSVGD_RADIX_BINS; b += blockDim.x) st->hist[b] = 0ull;
+  if (t == 0) {
+    const unsigned long long nn = (unsigned long long)n_total * (unsigned long long)n_total;
+    reset_state(st, (nn - 1ull) / 2ull, (unsigned long long)n_total);
+    st->fallback = 0u;
+    st->lo = lo_st->median;
+    st->hi = hi_st->median;
+    st->cand_cap = (unsigned long long)cap;
+  }
+}
+
+// After the distance pass (and the all-reduce of below/ncand): does the
+// bracket provably hold rank k?  Yes -> select rank k - below among the
+// candidates; no (or overflow) -> select rank k over D itself.
+__global__ void bracket_check_kernel(dsvgd_select_state* st) {
+  const unsigned long long k = st->k, below = st->below, nc = st->ncand;
+  if (below <= k && k < below + nc && nc <= st->cand_cap) {
+    st->k = k - below;
+    st->fallback = 0u;
+  } else {
+    st->fallback = 1u;
+  }
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
+// out[p] = ||y_i - y_j||^2 (explicit differences) for s hash-chosen pairs
+// (i, j) in [0,n)^2; one wave per pair, deterministic for a given seed.
+__global__ __launch_bounds__(256) void sample_sqdist_kernel(const float* __restrict__ Y,
+                                                            int64_t ldy, int64_t n, int d,
+                                                            int64_t s, uint64_t seed,
+                                                            float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < s;
+       p += (int64_t)gridDim.x * 4) {
+    const uint64_t h = mix64(seed ^ (0x9e3779b97f4a7c15ull * (uint64_t)(p + 1)));
+    const int64_t i = (int64_t)((h & 0xffffffffull) % (uint64_t)n);
+    const int64_t j = (int64_t)((h >> 32) % (uint64_t)n);
+    const float* yi = Y + i * ldy;
+    const float* yj = Y + j * ldy;
+    float acc = 0.f;
+    for (int c = lane; c < d; c += 64) {
+      const float df = yi[c] - yj[c];
+      acc = fmaf(df, df, acc);
+    }
+    acc = warp_sum(acc);
+    if (lane == 0) out[p] = acc;
+  }
+}
+
+}  // namespace dsvgd
+
+using namespace dsvgd;
+
+extern "C" {
+
+int dsvgd_select_init(dsvgd_select_state* st, int64_t n_total, int64_t k_rank, void* stream) {
+  DSVGD_REQUIRE(st && n_total > 0, "args");
+  hipLaunchKernelGGL(select_init_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, st, n_total,
+                     k_rank);
+  return check_launch("select_init");
+}
+
+int dsvgd_radix_hist(const float* D, int64_t count, const float* cand, int pass,
+                     dsvgd_select_state* st, void* stream) {
+  DSVGD_REQUIRE(D && st, "null pointer");
+  DSVGD_REQUIRE(pass >= 1 && pass <= 3, "pass must be 1..3");
+  DSVGD_REQUIRE(count >= 0 && ((uintptr_t)D & 15) == 0, "count / alignment");
+  int64_t blocks = (count / 4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 64) blocks = 64;  // the candidate count is only known on device
+  hipLaunchKernelGGL(radix_hist_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, D, count,
+                     cand, pass, st);
+  return check_launch("radix_hist");
+}
+
+int dsvgd_radix_pick(dsvgd_select_state* st, int pass, void* stream) {
+  DSVGD_REQUIRE(st, "null state");
+  DSVGD_REQUIRE(pass >= 1 && pass <= 3, "pass must be 1..3");
+  hipLaunchKernelGGL(radix_pick_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, st, pass);
+  return check_launch("radix_pick");
+}
+
+int dsvgd_sample_sqdist(const float* Y, int64_t ldy, int64_t n, int64_t d, int64_t s,
+                        uint64_t seed, float* out, void* stream) {
+  DSVGD_REQUIRE(Y && out, "null pointer");
+  DSVGD_REQUIRE(n > 0 && d > 0 && s > 0 && ldy >= d, "sizes");
+  int64_t blocks = (s + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(sample_sqdist_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, Y, ldy,
+                     n, (int)d, s, seed, out);
+  return check_launch("sample_sqdist");
+}
+
+int dsvgd_bracket_init(dsvgd_select_state* st, int64_t n_total, const dsvgd_select_state* lo_st,
+                       const dsvgd_select_state* hi_st, int64_t cand_cap, void* stream) {
+  DSVGD_REQUIRE(st && lo_st && hi_st && n_total > 0 && cand_cap > 0, "args");
+  hipLaunchKernelGGL(bracket_init_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, st, n_total,
+                     lo_st, hi_st, cand_cap);
+  return check_launch("bracket_init");
+}
+
+int dsvgd_bracket_check(dsvgd_select_state* st, void* stream) {
+  DSVGD_REQUIRE(st, "null state");
+  hipLaunchKernelGGL(bracket_check_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, st);
+  return check_launch("bracket_check");
+}
+
+}  // extern "C"

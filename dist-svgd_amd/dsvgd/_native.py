@@ -28,10 +28,13 @@ SIGNATURES = {
     "dsvgd_colmean_workspace_floats": (_c.c_size_t, [_i64, _i64]),
     "dsvgd_colmean": (_int, [_p, _i64, _i64, _i64, _p, _p, _p]),
     "dsvgd_pack": (_int, [_p, _i64, _p, _i64, _f, _p, _i64, _i64, _i64, _p, _i64, _p, _p]),
-    "dsvgd_sqdist": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _p]),
-    "dsvgd_select_init": (_int, [_p, _i64, _p]),
-    "dsvgd_radix_hist": (_int, [_p, _i64, _i64, _i64, _int, _p, _p]),
+    "dsvgd_sqdist": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p]),
+    "dsvgd_select_init": (_int, [_p, _i64, _i64, _p]),
+    "dsvgd_radix_hist": (_int, [_p, _i64, _p, _int, _p, _p]),
     "dsvgd_radix_pick": (_int, [_p, _int, _p]),
+    "dsvgd_sample_sqdist": (_int, [_p, _i64, _i64, _i64, _i64, _c.c_uint64, _p, _p]),
+    "dsvgd_bracket_init": (_int, [_p, _i64, _p, _p, _i64, _p]),
+    "dsvgd_bracket_check": (_int, [_p, _p]),
     "dsvgd_set_bandwidth": (_int, [_p, _f, _p]),
     "dsvgd_phi_splits": (_i64, [_i64, _i64, _i64]),
     "dsvgd_phi_mm": (_int, [_p, _i64, _p, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p]),

@@ -197,7 +197,7 @@ class DistSampler(object):
             if median:
                 eng = self._engine(n_int, e - s, s - lo)
                 eng.pack(Xi)
-                eng.distances(histogram=True)
+                eng.distances(median=True)
                 eng.median_bandwidth(hook)
                 state = eng.state
             else:

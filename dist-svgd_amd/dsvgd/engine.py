@@ -16,6 +16,7 @@ The hist all-reduce hook is where a DistSampler with a row-sharded D makes the
 median global (RCCL all_reduce of 2048 int64 counts per pass).
 """
 import ctypes
+import math
 
 import torch
 
@@ -25,10 +26,15 @@ NBINS = 2048
 
 
 class _SelectState(ctypes.Structure):
+    """Mirror of dsvgd_select_state (include/dsvgd.h)."""
     _fields_ = [("hist", ctypes.c_uint64 * NBINS), ("k", ctypes.c_uint64),
                 ("n_total", ctypes.c_uint64), ("prefix", ctypes.c_uint32),
                 ("passes_done", ctypes.c_uint32), ("median", ctypes.c_float),
-                ("h", ctypes.c_float), ("inv_h", ctypes.c_float), ("pad_", ctypes.c_float)]
+                ("h", ctypes.c_float), ("inv_h", ctypes.c_float), ("fallback", ctypes.c_uint32),
+                ("below", ctypes.c_uint64), ("ncand", ctypes.c_uint64), ("lo", ctypes.c_float),
+                ("hi", ctypes.c_float), ("cand_cap", ctypes.c_uint64)]
+
+SEL_NONE, SEL_HIST, SEL_BRACKET = 0, 1, 2
 
 
 _OFF_MEDIAN = _SelectState.median.offset
@@ -51,6 +57,22 @@ class SelectState(object):
     @property
     def hist(self):
         return self.buf[:NBINS]
+
+    @property
+    def counts(self):
+        """int64[2] view of (below, ncand) -- all-reduced in bracketed mode."""
+        o = _SelectState.below.offset // 8
+        return self.buf[o:o + 2]
+
+    def bracket(self):
+        """(lo, hi, below, ncand, fallback) -- synchronises with the device."""
+        raw = self.buf.cpu()
+        u8 = raw.view(torch.uint8)
+        lo, hi = u8[_SelectState.lo.offset:_SelectState.lo.offset + 8].view(torch.float32).tolist()
+        fb = int(u8[_SelectState.fallback.offset:_SelectState.fallback.offset + 4]
+                 .view(torch.int32)[0])
+        b, c = raw[_SelectState.below.offset // 8:_SelectState.below.offset // 8 + 2].tolist()
+        return lo, hi, b, c, fb
 
     def read(self):
         """(median, h, inv_h) -- synchronises with the device."""
@@ -108,6 +130,12 @@ def span(timer, name):
 
 class PhiEngine(object):
     timer = None
+    # median select: bracketed (sample -> [lo, hi] -> candidates) when the
+    # owned block has at least this many entries, plain radix passes over D below
+    BRACKET_MIN_ENTRIES = 1 << 24
+    SAMPLE = 1 << 18            # sampled pairs that fix the bracket
+    SIGMAS = 6.0                # bracket half-width in sample-rank standard deviations
+    SEED = 0x5EED5EED
 
     def __init__(self, n, d, m=None, row0=0, device=None):
         dev = N.require_gpu(device if device is not None else "cuda")
@@ -131,6 +159,17 @@ class PhiEngine(object):
         self.mean_ws = torch.empty(max(1, lib.dsvgd_colmean_workspace_floats(n, d)), **f32)
         self.phi = torch.empty(m, d, **f32)
         self.state = SelectState(dev)
+        self.bracketed = m * n >= self.BRACKET_MIN_ENTRIES
+        if self.bracketed:
+            s = self.SAMPLE
+            half = 0.5 * s
+            dk = self.SIGMAS * math.sqrt(s) / 2.0
+            self.k_lo = max(0, int(math.floor(half - dk)))
+            self.k_hi = min(s - 1, int(math.ceil(half + dk)))
+            self.sample = torch.empty(s, **f32)
+            self.st_lo, self.st_hi = SelectState(dev), SelectState(dev)
+            self.cand_cap = max(1 << 22, (m * n) // 16)
+            self.cand = torch.empty(self.cand_cap, **f32)
 
     # ------------------------------------------------------------ stages --
     def pack(self, X, S=None, score_scale=1.0):
@@ -150,24 +189,49 @@ class PhiEngine(object):
                N.ptr(self.mean), self.n, self.d, self.Y.shape[0], N.ptr(self.Y), self.ldy,
                N.ptr(self.norms), s)
 
-    def distances(self, histogram=True):
+    def distances(self, median=False):
+        """D for the owned rows.  median=True also does the select's first
+        stage: the fused digit-1 histogram, or (bracketed) the sample bracket +
+        the below-count / candidate compaction."""
         s = N.stream(self.device)
-        st = None
-        if histogram:
-            N.call("dsvgd_select_init", self.state.ptr, self.n, s)
-            st = self.state.ptr
+        st, cand, mode = None, None, SEL_NONE
+        if median and self.bracketed:
+            with span(self.timer, "bracket"):
+                self._bracket(s)
+            st, cand, mode = self.state.ptr, N.ptr(self.cand), SEL_BRACKET
+        elif median:
+            N.call("dsvgd_select_init", self.state.ptr, self.n, -1, s)
+            st, mode = self.state.ptr, SEL_HIST
         with span(self.timer, "sqdist"):
             N.call("dsvgd_sqdist", N.ptr(self.Y), self.ldy, N.ptr(self.norms), self.row0, self.m,
-                   self.n, self.d, N.ptr(self.D), self.n_pad, st, s)
+                   self.n, self.d, N.ptr(self.D), self.n_pad, mode, st, cand, s)
+
+    def _bracket(self, s):
+        N.call("dsvgd_sample_sqdist", N.ptr(self.Y), self.ldy, self.n, self.d, self.SAMPLE,
+               self.SEED, N.ptr(self.sample), s)
+        for sub, k in ((self.st_lo, self.k_lo), (self.st_hi, self.k_hi)):
+            N.call("dsvgd_select_init", sub.ptr, self.SAMPLE, k, s)
+            for p in (1, 2, 3):
+                N.call("dsvgd_radix_hist", N.ptr(self.sample), self.SAMPLE, None, p, sub.ptr, s)
+                N.call("dsvgd_radix_pick", sub.ptr, p, s)
+        N.call("dsvgd_bracket_init", self.state.ptr, self.n, self.st_lo.ptr, self.st_hi.ptr,
+               self.cand_cap, s)
 
     def median_bandwidth(self, allreduce=None):
-        """Radix select over D (after distances(histogram=True))."""
+        """Exact radix select (after distances(median=True)); `allreduce` sums
+        an int64 device tensor over the ranks that share the n x n matrix."""
         s = N.stream(self.device)
+        count = self.m_pad * self.n_pad
+        cand = None
+        if self.bracketed:
+            if allreduce is not None:
+                allreduce(self.state.counts)
+            N.call("dsvgd_bracket_check", self.state.ptr, s)
+            cand = N.ptr(self.cand)
         for p in (1, 2, 3):
-            if p > 1:
+            if p > 1 or self.bracketed:
                 with span(self.timer, "radix_hist"):
-                    N.call("dsvgd_radix_hist", N.ptr(self.D), self.n_pad, self.m, self.n, p,
-                           self.state.ptr, s)
+                    N.call("dsvgd_radix_hist", N.ptr(self.D), count, cand, p, self.state.ptr, s)
             if allreduce is not None:
                 with span(self.timer, "hist_allreduce"):
                     allreduce(self.state.hist)
@@ -208,7 +272,7 @@ class PhiEngine(object):
         """One Jacobi step: h=None -> median bandwidth, else fixed h."""
         self.pack(X, S, score_scale)
         median = h is None
-        self.distances(histogram=median)
+        self.distances(median=median)
         if median:
             self.median_bandwidth(allreduce)
         else:

@@ -70,7 +70,7 @@ class Sampler(object):
             else:
                 if median:
                     engine.pack(X)
-                    engine.distances(histogram=True)
+                    engine.distances(median=True)
                     engine.median_bandwidth()
                 sequential_sweep(X, S, range(n), state, step_size, target=self._target)
             if verbose:

@@ -43,7 +43,8 @@ enum {
 
 /* Device-resident state of the median-bandwidth radix select.  Allocate
  * dsvgd_select_state_bytes() of device memory; the histogram is the first
- * member so a distributed caller can all-reduce it in place (int64 SUM). */
+ * member so a distributed caller can all-reduce it in place (int64 SUM), and
+ * `below`/`ncand` are adjacent for one int64[2] all-reduce. */
 typedef struct dsvgd_select_state {
   uint64_t hist[DSVGD_RADIX_BINS]; /* per-pass counts (u64: n^2 may be 2^32)  */
   uint64_t k;                      /* rank still to find inside the prefix    */
@@ -53,8 +54,17 @@ typedef struct dsvgd_select_state {
   float median;                    /* k-th smallest squared distance          */
   float h;                         /* bandwidth  h = median / log(n)          */
   float inv_h;                     /* 1 / h (read by the phi kernels)         */
-  float pad_;
+  uint32_t fallback;               /* bracketed: 1 = select over D itself     */
+  uint64_t below;                  /* bracketed: # entries < lo               */
+  uint64_t ncand;                  /* bracketed: # entries in [lo, hi]        */
+  float lo, hi;                    /* bracketed: the sample bracket           */
+  uint64_t cand_cap;               /* bracketed: candidate buffer capacity    */
 } dsvgd_select_state;
+
+/* select_mode of dsvgd_sqdist */
+#define DSVGD_SEL_NONE 0    /* fixed bandwidth: distances only                 */
+#define DSVGD_SEL_HIST 1    /* fused radix digit-1 histogram                   */
+#define DSVGD_SEL_BRACKET 2 /* count < lo, compact [lo, hi] into candidates    */
 
 /* ---- meta ------------------------------------------------------------- */
 int dsvgd_abi_version(void);
@@ -88,28 +98,44 @@ int dsvgd_pack(const float* X, int64_t ldx, const float* S, int64_t lds, float s
  * d > 64: max(0, |y_i|^2 + |y_j|^2 - 2 y_i.y_j) on v_mfma_f32_32x32x2_f32,
  * upper-triangle tiles only when m == n and row0 == 0 (the transpose is
  * stored too).  D[i][i] = 0 exactly, pads = +inf, panel layout (ldd = n_pad).
- * If st != NULL also accumulates the first radix-select histogram (key bits
- * 31..21) of the valid entries into st->hist.
+ * select_mode (DSVGD_SEL_*): HIST accumulates radix digit 1 of the valid
+ * entries into st->hist; BRACKET counts entries < st->lo into st->below and
+ * appends the entries in [st->lo, st->hi] to cand (capacity st->cand_cap,
+ * count st->ncand).
  * Replaces torch.dist(x, y, p=2)**2 inside kernel(...) at
  * experiments/logreg.py:60-61 / experiments/gmm.py:23-24 as called per pair
  * from dsvgd/sampler.py:38 and dsvgd/distsampler.py:91-97. */
 int dsvgd_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0, int64_t m,
-                 int64_t n, int64_t d, float* D, int64_t ldd, dsvgd_select_state* st,
-                 void* stream);
+                 int64_t n, int64_t d, float* D, int64_t ldd, int select_mode,
+                 dsvgd_select_state* st, float* cand, void* stream);
 
 /* ---- median bandwidth: exact radix select over the n x n distances ----- */
 /* (absent in the reference, whose kernel bandwidth is fixed at h=1; the
  * median heuristic is pinned in SURVEY.md a18: lower median, k=(n^2-1)//2
- * over the full matrix incl. the diagonal, h = median / log n.)            */
-int dsvgd_select_init(dsvgd_select_state* st, int64_t n_total, void* stream);
+ * over the full matrix incl. the diagonal, h = median / log n.)
+ * select_init: k = k_rank if k_rank >= 0 else (n_total^2-1)/2, prefix 0. */
+int dsvgd_select_init(dsvgd_select_state* st, int64_t n_total, int64_t k_rank, void* stream);
 /* histogram of key digit `pass` (1: bits 31..21, 2: 20..10, 3: 9..0) of the
- * finite entries of the m_pad x n_pad panel buffer D (pads are +inf and never
- * counted) whose higher digits equal st->prefix. */
-int dsvgd_radix_hist(const float* D, int64_t ldd, int64_t m, int64_t n, int pass,
+ * finite entries (pads +inf / NaN skipped) whose higher digits equal
+ * st->prefix, over D[0:count) -- or, when cand != NULL and the bracket holds
+ * (st->fallback == 0), over the st->ncand candidates instead. */
+int dsvgd_radix_hist(const float* D, int64_t count, const float* cand, int pass,
                      dsvgd_select_state* st, void* stream);
 /* pick the bin holding rank k, fix its digit, clear hist; after pass 3
- * writes median, h, inv_h. */
+ * writes median, h = median/log(n_total) (1 if median == 0 or n == 1), inv_h. */
 int dsvgd_radix_pick(dsvgd_select_state* st, int pass, void* stream);
+/* bracketed select: out[p] = ||y_i - y_j||^2 for s pairs (i,j) drawn by a
+ * seeded hash (identical on every rank for the same Y) ... */
+int dsvgd_sample_sqdist(const float* Y, int64_t ldy, int64_t n, int64_t d, int64_t s,
+                        uint64_t seed, float* out, void* stream);
+/* ... whose k_lo-th / k_hi-th order statistics (two select states run over
+ * `out`) become the bracket [lo, hi] of st (k = (n_total^2-1)/2) ... */
+int dsvgd_bracket_init(dsvgd_select_state* st, int64_t n_total, const dsvgd_select_state* lo_st,
+                       const dsvgd_select_state* hi_st, int64_t cand_cap, void* stream);
+/* ... and, after dsvgd_sqdist(BRACKET) (+ an all-reduce of below/ncand), the
+ * exact check below <= k < below + ncand (no overflow): k -= below and the
+ * passes read the candidates; otherwise they read D (fallback). */
+int dsvgd_bracket_check(dsvgd_select_state* st, void* stream);
 /* fixed-bandwidth mode: st->h = h, st->inv_h = 1/h */
 int dsvgd_set_bandwidth(dsvgd_select_state* st, float h, void* stream);
 

@@ -70,7 +70,7 @@ def test_sqdist_matches_oracle(n, d):
     X = (rs.randn(n, d) * 1.5 + 3.0).astype(np.float32)
     eng = dsvgd().PhiEngine(n, d, device=DEV)
     eng.pack(gpu(X))
-    eng.distances(histogram=True)
+    eng.distances(median=True)
     D = eng.dense_D().cpu().numpy().astype(np.float64)
     ref = O.sqdist(X, X)
     nrm = ((X - X.mean(0)) ** 2).sum(1).astype(np.float64)
@@ -90,7 +90,7 @@ def test_median_select_bit_exact(n, d):
     X = rs.randn(n, d).astype(np.float32)
     eng = dsvgd().PhiEngine(n, d, device=DEV)
     eng.pack(gpu(X))
-    eng.distances(histogram=True)
+    eng.distances(median=True)
     eng.median_bandwidth()
     med, h, inv_h = eng.state.read()
     D = eng.dense_D().cpu().numpy()
@@ -105,14 +105,44 @@ def test_median_select_bit_exact(n, d):
         assert h == 1.0
 
 
-def test_median_all_identical_particles():
-    X = np.ones((100, 4), np.float32)
-    eng = dsvgd().PhiEngine(100, 4, device=DEV)
+@pytest.mark.parametrize("n,d,force_miss", [(4200, 100, False), (4200, 8, False),
+                                             (4200, 100, True)])
+def test_bracketed_median_bit_exact(n, d, force_miss):
+    """Bracketed select (sample -> [lo, hi] -> candidates): bit-exact median,
+    and the exact fallback to the passes over D when the bracket misses."""
+    rs = np.random.RandomState(n + d)
+    X = rs.randn(n, d).astype(np.float32)
+    eng = dsvgd().PhiEngine(n, d, device=DEV)
+    assert eng.bracketed
+    if force_miss:
+        eng.k_lo = eng.k_hi = 0          # bracket [min, min] cannot hold the median
     eng.pack(gpu(X))
-    eng.distances(histogram=True)
+    eng.distances(median=True)
+    eng.median_bandwidth()
+    med, h, _ = eng.state.read()
+    lo, hi, below, ncand, fallback = eng.state.bracket()
+    D = eng.dense_D().cpu().numpy()
+    k = (n * n - 1) // 2
+    exact = np.partition(D.ravel(), k)[k]
+    assert np.float32(med).view(np.uint32) == np.float32(exact).view(np.uint32)
+    assert fallback == (1 if force_miss else 0)
+    if not force_miss:
+        assert lo <= med <= hi
+        assert below == int((D < lo).sum()) and ncand == int(((D >= lo) & (D <= hi)).sum())
+        assert ncand < 0.05 * n * n
+
+
+@pytest.mark.parametrize("n", [100, 4200])
+def test_median_all_identical_particles(n):
+    X = np.ones((n, 4), np.float32)
+    eng = dsvgd().PhiEngine(n, 4, device=DEV)
+    eng.pack(gpu(X))
+    eng.distances(median=True)
     eng.median_bandwidth()
     med, h, _ = eng.state.read()
     assert med == 0.0 and h == 1.0
+    if eng.bracketed:                    # every entry in [0, 0]: overflow -> fallback
+        assert eng.state.bracket()[4] == 1
 
 
 def test_fused_histogram_equals_standalone_pass1():
@@ -121,12 +151,12 @@ def test_fused_histogram_equals_standalone_pass1():
     X = np.random.RandomState(3).randn(n, d).astype(np.float32)
     eng = dsvgd().PhiEngine(n, d, device=DEV)
     eng.pack(gpu(X))
-    eng.distances(histogram=True)
+    eng.distances(median=True)
     fused = eng.state.hist.clone()
     st2 = dsvgd().engine.SelectState(DEV)
     s = N.stream(DEV)
-    N.call("dsvgd_select_init", st2.ptr, n, s)
-    N.call("dsvgd_radix_hist", N.ptr(eng.D), eng.n_pad, n, n, 1, st2.ptr, s)
+    N.call("dsvgd_select_init", st2.ptr, n, -1, s)
+    N.call("dsvgd_radix_hist", N.ptr(eng.D), eng.m_pad * eng.n_pad, None, 1, st2.ptr, s)
     assert torch.equal(fused, st2.hist)
     assert int(fused.sum()) == n * n
 
@@ -368,3 +398,58 @@ def test_distsampler_two_ranks_match_reference(golden, mode):
             assert start == int(g["start"][rank][step])
             assert abs_err(own, g["own"][rank][step]) < TRAJ_TOL
             assert abs_err(full, g["full"][rank][step]) < TRAJ_TOL
+
+
+def _dist_median_worker(rank, S, port, X, d, steps, eps, q):
+    import os
+    import sys
+    import torch.distributed as dist
+    from conftest import PKG, ROOT
+    for p in (ROOT, PKG):
+        sys.path.insert(0, p)
+    import dsvgd as m
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=S)
+    mu = np.zeros(d, np.float32)
+    lam = np.ones(d, np.float32)
+    parts = torch.tensor(X, device=DEV)
+    ds = m.DistSampler(rank, S, m.targets.Gaussian(mu, lam), m.RBF("median"), parts,
+                       1, 1, exchange_particles=True, exchange_scores=False,
+                       include_wasserstein=False, order="jacobi")
+    hs = []
+    for _ in range(steps):
+        ds.make_step(eps)
+        eng = next(iter(ds._engines.values()))
+        hs.append((eng.bracketed, eng.state.read()[1], eng.state.bracket()[4]))
+    q.put((rank, ds.particles.cpu().numpy(), hs))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("d", [16, 80])
+def test_distsampler_median_two_ranks_jacobi(d):
+    """Row-sharded D over 2 ranks (bracketed select, all-reduced counts and
+    histograms) vs the oracle's global-median Jacobi step."""
+    import torch.multiprocessing as mp
+    n, S, steps, eps = 6000, 2, 2, 0.05
+    X = np.random.RandomState(d).randn(n, d).astype(np.float32)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_dist_median_worker, args=(r, S, 29830 + d, X, d, steps, eps, q))
+          for r in range(S)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in range(S)], key=lambda r: r[0])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    ref = np.array(X, np.float64)
+    for _ in range(steps):
+        ref = ref + eps * O.phi(ref, -ref, O.median_bandwidth(ref)[0])
+    got = np.concatenate([r[1] for r in res])
+    assert abs_err(got, ref) < TRAJ_TOL
+    for _, _, hs in res:
+        for bracketed, h, fallback in hs:
+            assert bracketed and fallback == 0
+    assert res[0][2] == res[1][2]            # identical h on both ranks

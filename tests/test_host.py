@@ -43,7 +43,7 @@ def test_meta_calls_without_gpu():
     assert lib.dsvgd_ldy(1024) == 2048
     assert lib.dsvgd_logreg_workspace_bytes(100, 400, 2) % 256 == 0
     # argument validation returns an error code (no GPU work is enqueued)
-    rc = lib.dsvgd_sqdist(None, 0, None, 0, 0, 0, 32, None, 128, None, None)
+    rc = lib.dsvgd_sqdist(None, 0, None, 0, 0, 0, 32, None, 128, 0, None, None, None)
     assert rc == -1 and b"null" in lib.dsvgd_last_error()
 
 
