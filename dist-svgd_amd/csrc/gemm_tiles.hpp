@@ -130,12 +130,15 @@ struct NTTile {
 };
 
 // ------------------------------------------------------------ NN engine ----
-// BM = 128 rows (TM = 4), 4 waves side by side along the columns, each
-// 128 x 32*TN; K-step = one 16-column panel of A and 16 rows of B.
-template <int TN, bool EXP>
+// BM = 128 rows; WM x 4 waves (256*WM threads): wave (wr, wc) owns rows
+// [wr*128/WM, +128/WM) x columns [wc*32*TN, +32*TN) -- TM = 4/WM row tiles,
+// i.e. 16*TM*TN accumulator registers (WM = 2: two waves per SIMD, 128 AGPRs
+// each, so one wave's barrier / LDS waits hide under the other's MFMAs).
+// K-step = one 16-column panel of A and 16 rows of B.
+template <int TN, bool EXP, int WM = 1>
 struct NNTile {
-  static constexpr int kThreads = 256;
-  static constexpr int TM = 4;
+  static constexpr int kThreads = 256 * WM;
+  static constexpr int TM = 4 / WM;
   static constexpr int BM = 128;
   static constexpr int BC = 128 * TN;
   static constexpr int BJ = 16;
@@ -144,8 +147,9 @@ struct NNTile {
   static constexpr int SB = BJ * BC;
   static constexpr int kStage = SA + SB;
   static constexpr int kSmemFloats = 2 * kStage;
-  static constexpr int LA = BM * BJ / 4 / kThreads;  // 2
-  static constexpr int LB = BJ * BC / 4 / kThreads;  // 2*TN
+  static constexpr int LA = BM * BJ / 4 / kThreads;
+  static constexpr int LB = BJ * BC / 4 / kThreads;
+  static_assert(LA >= 1 && LB >= 1, "tile too small for the block");
 
   f32x16 acc[TM][TN];
   f32x4 ra[LA], rb[LB];
@@ -177,9 +181,9 @@ struct NNTile {
     for (int u = 0; u < LB; ++u) *reinterpret_cast<f32x4*>(sB + 4 * (t + u * kThreads)) = rb[u];
   }
 
-  __device__ __forceinline__ void compute(const float* st, int wc, float scale) {
+  __device__ __forceinline__ void compute(const float* st, int wr, int wc, float scale) {
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-    const float* sA = st;
+    const float* sA = st + (wr * 32 * TM) * LDA;
     const float* sB = st + SA;
 #pragma unroll
     for (int g = 0; g < BJ / 8; ++g) {
@@ -213,7 +217,7 @@ struct NNTile {
   __device__ __forceinline__ void run(const float* __restrict__ Apanels, const float* __restrict__ B,
                                       int64_t ldb, int64_t k0, int64_t k1, float scale,
                                       float* smem) {
-    const int wc = threadIdx.x >> 6;
+    const int w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
       rsum[mi] = 0.f;
@@ -230,7 +234,7 @@ struct NNTile {
     for (int64_t j0 = k0; j0 < k1; j0 += BJ) {
       const bool more = j0 + BJ < k1;
       if (more) load(Apanels, B, ldb, j0 + BJ);
-      compute(smem + cur * kStage, wc, scale);
+      compute(smem + cur * kStage, wr, wc, scale);
       if (more) store(smem + (cur ^ 1) * kStage);
       __syncthreads();
       cur ^= 1;

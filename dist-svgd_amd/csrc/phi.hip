@@ -8,6 +8,7 @@
 // operand; D streams from HBM once (panel layout), [Xc|S] re-reads hit L2/MALL.
 // Roofline: 2 * 128 * BC flop per 8 KiB D panel -> MFMA-bound for d >= 64.
 #include <cmath>
+#include <cstdlib>
 
 #include "gemm_tiles.hpp"
 
@@ -16,14 +17,14 @@ namespace dsvgd {
 // blockIdx.z = split-K slice z: K columns [z*kchunk, min(K,(z+1)*kchunk)) into
 // the partial C + z*m*ldc (and rowsum + z*m_pad); phi_finish sums the slices
 // in order (deterministic, no atomics).
-template <int TN, bool EXP>
-__global__ __launch_bounds__(256) void nn_kernel(const float* __restrict__ A, int64_t a_npad,
-                                                 const float* __restrict__ B, int64_t ldb,
-                                                 int64_t K, int64_t kchunk,
-                                                 const dsvgd_select_state* __restrict__ st,
-                                                 float* __restrict__ C, int64_t ldc,
-                                                 float* __restrict__ rowsum, int64_t m) {
-  using Tile = NNTile<TN, EXP>;
+template <int TN, bool EXP, int WM>
+__global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ A, int64_t a_npad,
+                                                      const float* __restrict__ B, int64_t ldb,
+                                                      int64_t K, int64_t kchunk,
+                                                      const dsvgd_select_state* __restrict__ st,
+                                                      float* __restrict__ C, int64_t ldc,
+                                                      float* __restrict__ rowsum, int64_t m) {
+  using Tile = NNTile<TN, EXP, WM>;
   __shared__ __attribute__((aligned(16))) float smem[Tile::kSmemFloats];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
@@ -36,23 +37,24 @@ __global__ __launch_bounds__(256) void nn_kernel(const float* __restrict__ A, in
   Tile tile;
   tile.run(A + (i0 >> 7) * (a_npad >> 4) * kPanelElems, B + c0, ldb, k0, k1, scale, smem);
 
-  const int lane = threadIdx.x & 63, wc = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
+  const int64_t r0 = i0 + wr * 32 * Tile::TM;
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
+  for (int mi = 0; mi < Tile::TM; ++mi)
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
       const int64_t col = c0 + wc * 32 * TN + ni * 32 + (lane & 31);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int64_t row = i0 + mi * 32 + c_row(r, lane);
+        const int64_t row = r0 + mi * 32 + c_row(r, lane);
         if (row < m) C[row * ldc + col] = tile.acc[mi][ni][r];
       }
     }
   if (EXP && rowsum && blockIdx.x == 0 && wc == 0) {
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
+    for (int mi = 0; mi < Tile::TM; ++mi) {
       const float v = tile.rsum[mi] + __shfl_xor(tile.rsum[mi], 32, 64);
-      const int64_t row = i0 + mi * 32 + lane;
+      const int64_t row = r0 + mi * 32 + lane;
       if (lane < 32 && row < m) rowsum[row] = v;
     }
   }
@@ -200,19 +202,34 @@ __global__ __launch_bounds__(256) void phi_row_kernel(float* __restrict__ X, int
   }
 }
 
+// NN block shape: 1 or 2 waves per SIMD (DSVGD_NN_WAVES=1|2 overrides, for A/B runs)
+static int nn_waves_per_simd() {
+  const char* e = getenv("DSVGD_NN_WAVES");
+  return (e && e[0] == '1') ? 1 : 2;
+}
+
+template <int TN, int WM>
+int launch_nn_wm(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
+                 const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
+                 int64_t cols, hipStream_t s) {
+  const int64_t kchunk = roundup((K + splits - 1) / splits, 16);
+  const dim3 grid(cols / (128 * TN), roundup(m, 128) / 128, splits);
+  if (exp_)
+    hipLaunchKernelGGL((nn_kernel<TN, true, WM>), grid, dim3(256 * WM), 0, s, A, K, B, ldb, K,
+                       kchunk, st, C, ldc, rowsum, m);
+  else
+    hipLaunchKernelGGL((nn_kernel<TN, false, WM>), grid, dim3(256 * WM), 0, s, A, K, B, ldb, K,
+                       kchunk, st, C, ldc, rowsum, m);
+  return check_launch("nn_kernel");
+}
+
 template <int TN>
 int launch_nn(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
               const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
               int64_t cols, hipStream_t s) {
-  const int64_t kchunk = roundup((K + splits - 1) / splits, 16);
-  const dim3 grid(cols / (128 * TN), roundup(m, 128) / 128, splits);
-  if (exp_)
-    hipLaunchKernelGGL((nn_kernel<TN, true>), grid, dim3(256), 0, s, A, K, B, ldb, K, kchunk, st,
-                       C, ldc, rowsum, m);
-  else
-    hipLaunchKernelGGL((nn_kernel<TN, false>), grid, dim3(256), 0, s, A, K, B, ldb, K, kchunk, st,
-                       C, ldc, rowsum, m);
-  return check_launch("nn_kernel");
+  if (nn_waves_per_simd() == 2)
+    return launch_nn_wm<TN, 2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, s);
+  return launch_nn_wm<TN, 1>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, s);
 }
 
 // C[splits x m x cols] = f(A) B with A in panel layout (m_pad x K), B row-major K x cols.

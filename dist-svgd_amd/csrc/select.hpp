@@ -57,13 +57,11 @@ __device__ __forceinline__ void flush_block_hist(const uint32_t* shist, dsvgd_se
 
 // histogram of a lane's NV values (+inf = invalid, skipped), weight w
 template <int NV>
-__device__ __forceinline__ void hist_account(const float (&v)[NV], uint32_t w, uint32_t* shist) {
-  WindowHist wh;
-  wh.init(v[0]);
+__device__ __forceinline__ void hist_account(WindowHist& wh, const float (&v)[NV], uint32_t w,
+                                             uint32_t* shist) {
 #pragma unroll
   for (int i = 0; i < NV; ++i)
     if (v[i] != INFINITY) wh.add(v[i], w, shist);
-  wh.flush(shist);
 }
 
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t& total) {

@@ -28,11 +28,11 @@ __device__ __forceinline__ void tri_decode(int64_t b, int T, int& bi, int& bj) {
 // Rows [row0, row0+m) of Y against rows [0,n).  SYM (m == n, row0 == 0): only
 // tiles bi <= bj, the off-diagonal ones stored twice (tile + transpose) and
 // accounted with weight 2.
-template <bool SYM>
+template <bool SYM, int smode>
 __global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y, int64_t ldy,
                                                      const float* __restrict__ norms, int64_t row0,
                                                      int64_t m, int64_t n, int64_t n_pad, int dp,
-                                                     float* __restrict__ D, int smode,
+                                                     float* __restrict__ D,
                                                      dsvgd_select_state* __restrict__ st,
                                                      float* __restrict__ cand) {
   __shared__ __attribute__((aligned(16))) float smem[GramTile::kSmemFloats];
@@ -60,42 +60,54 @@ __global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y
   __syncthreads();
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
-  float v[64];
+  const uint32_t weight = mirror ? 2u : 1u;
+  WindowHist wh;
+  // epilogue one 32x32 sub-tile (16 values per lane) at a time.  Panel-layout
+  // addresses: per lane one base pointer per sub-tile, the per-register part
+  // ((r&3)*16 + (r>>2)*128 floats) is a compile-time immediate.
+  const int h4 = 4 * (lane >> 5);
+  float* const Dtile = D + ((int64_t)bi * (n_pad >> 4) + (int64_t)bj * 8) * kPanelElems;
+  float* const Dmir = D + ((int64_t)bj * (n_pad >> 4) + (int64_t)bi * 8) * kPanelElems;
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
       const int cl = wn * 64 + ni * 32 + (lane & 31);
-      const int64_t gj = j0 + cl;
+      const int rb = wm * 64 + mi * 32 + h4;  // this lane's first row in the sub-tile
+      const bool colok = j0 + cl < n;
       const float nj = snorm[GramTile::BM + cl];
+      float* const dp0 = Dtile + (cl >> 4) * kPanelElems + (cl & 15) + rb * 16;
+      float v[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int rl = wm * 64 + mi * 32 + c_row(r, lane);
-        const int64_t gi = i0 + rl;
+        const int rl = rb + (r & 3) + 8 * (r >> 2);
         float x;
-        if (gi < m && gj < n)
-          x = (row0 + gi == gj) ? 0.f : fmaxf(0.f, (snorm[rl] + nj) - 2.f * tile.acc[mi][ni][r]);
+        if (colok && i0 + rl < m)
+          x = (row0 + i0 + rl == j0 + cl) ? 0.f
+                                          : fmaxf(0.f, (snorm[rl] + nj) - 2.f * tile.acc[mi][ni][r]);
         else
           x = INFINITY;
-        v[(mi * 2 + ni) * 16 + r] = x;
-        D[panel_off(gi, gj, n_pad)] = x;
+        v[r] = x;
+        dp0[(r & 3) * 16 + (r >> 2) * 128] = x;
       }
       if (mirror) {  // D[j][i]: 4 consecutive i per register quad -> 16-byte stores
+        float* const mp0 = Dmir + (int64_t)cl * 16 + (wm * 4 + mi * 2) * kPanelElems + h4;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int64_t ci = i0 + wm * 64 + mi * 32 + 8 * q + 4 * (lane >> 5);
-          const float* p = &v[(mi * 2 + ni) * 16 + 4 * q];
-          *reinterpret_cast<f32x4*>(D + panel_off(gj, ci, n_pad)) = f32x4{p[0], p[1], p[2], p[3]};
-        }
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<f32x4*>(mp0 + (q >> 1) * kPanelElems + 8 * (q & 1)) =
+              f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+      }
+      if (smode == kSelHist) {
+        if (mi == 0 && ni == 0) wh.init(v[0]);
+        hist_account(wh, v, weight, shist);
+      } else if (smode == kSelBracket) {
+        bracket_account(v, weight, st, cand);
       }
     }
-  const uint32_t weight = mirror ? 2u : 1u;
   if (smode == kSelHist) {
-    hist_account(v, weight, shist);
+    wh.flush(shist);
     __syncthreads();
     flush_block_hist(shist, st);
-  } else if (smode == kSelBracket) {
-    bracket_account(v, weight, st, cand);
   }
 }
 
@@ -106,10 +118,11 @@ __global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y
 // 8 x 8 outputs per thread, both operand tiles transposed in LDS.
 constexpr int kDirectMaxD = 64;
 
+template <int smode>
 __global__ __launch_bounds__(256) void sqdist_direct_kernel(const float* __restrict__ Y,
                                                             int64_t ldy, int64_t row0, int64_t m,
                                                             int64_t n, int64_t n_pad, int d,
-                                                            float* __restrict__ D, int smode,
+                                                            float* __restrict__ D,
                                                             dsvgd_select_state* __restrict__ st,
                                                             float* __restrict__ cand) {
   __shared__ __attribute__((aligned(16))) float sA[kDirectMaxD][128];
@@ -146,27 +159,52 @@ __global__ __launch_bounds__(256) void sqdist_direct_kernel(const float* __restr
         acc[a][b] = fmaf(df, df, acc[a][b]);
       }
   }
-  float v[64];
+  WindowHist wh;
+  if (smode == kSelHist)
+    wh.init((i0 + ty * 8 < m && j0 + tx * 8 < n) ? acc[0][0] : INFINITY);
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
     const int64_t gi = i0 + ty * 8 + a;
+    float v[8];
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       const int64_t gj = j0 + tx * 8 + b;
-      v[a * 8 + b] = (gi < m && gj < n) ? acc[a][b] : INFINITY;
+      v[b] = (gi < m && gj < n) ? acc[a][b] : INFINITY;
     }
     float* dst = D + panel_off(gi, j0 + tx * 8, n_pad);
-    const float* p = &v[a * 8];
-    *reinterpret_cast<f32x4*>(dst) = f32x4{p[0], p[1], p[2], p[3]};
-    *reinterpret_cast<f32x4*>(dst + 4) = f32x4{p[4], p[5], p[6], p[7]};
+    *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4*>(dst + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    if (smode == kSelHist)
+      hist_account(wh, v, 1u, shist);
+    else if (smode == kSelBracket)
+      bracket_account(v, 1u, st, cand);
   }
   if (smode == kSelHist) {
-    hist_account(v, 1u, shist);
+    wh.flush(shist);
     __syncthreads();
     flush_block_hist(shist, st);
-  } else if (smode == kSelBracket) {
-    bracket_account(v, 1u, st, cand);
   }
+}
+
+template <int SM>
+int launch_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0, int64_t m,
+                  int64_t n, int64_t d, float* D, dsvgd_select_state* st, float* cand,
+                  hipStream_t s) {
+  const int64_t dp = roundup(d, 32), m_pad = roundup(m, 128), n_pad = roundup(n, 128);
+  if (d <= kDirectMaxD) {
+    hipLaunchKernelGGL((sqdist_direct_kernel<SM>), dim3(n_pad / 128, m_pad / 128), dim3(256), 0, s,
+                       Y, ldy, row0, m, n, n_pad, (int)d, D, st, cand);
+    return check_launch("sqdist_direct");
+  }
+  if (m == n && row0 == 0) {
+    const int64_t T = n_pad / 128;
+    hipLaunchKernelGGL((sqdist_kernel<true, SM>), dim3(T * (T + 1) / 2), dim3(256), 0, s, Y, ldy,
+                       norms, row0, m, n, n_pad, (int)dp, D, st, cand);
+  } else {
+    hipLaunchKernelGGL((sqdist_kernel<false, SM>), dim3(n_pad / 128, m_pad / 128), dim3(256), 0, s,
+                       Y, ldy, norms, row0, m, n, n_pad, (int)dp, D, st, cand);
+  }
+  return check_launch("sqdist");
 }
 
 }  // namespace dsvgd
@@ -190,20 +228,11 @@ int dsvgd_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0, 
   DSVGD_REQUIRE(((uintptr_t)Y & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
   DSVGD_REQUIRE(m_pad / 128 <= 65535, "too many row tiles");
   hipStream_t s = (hipStream_t)stream;
-  if (d <= kDirectMaxD) {
-    hipLaunchKernelGGL(sqdist_direct_kernel, dim3(n_pad / 128, m_pad / 128), dim3(256), 0, s, Y,
-                       ldy, row0, m, n, n_pad, (int)d, D, select_mode, st, cand);
-    return check_launch("sqdist_direct");
+  switch (select_mode) {
+    case kSelNone: return launch_sqdist<kSelNone>(Y, ldy, norms, row0, m, n, d, D, st, cand, s);
+    case kSelHist: return launch_sqdist<kSelHist>(Y, ldy, norms, row0, m, n, d, D, st, cand, s);
+    default: return launch_sqdist<kSelBracket>(Y, ldy, norms, row0, m, n, d, D, st, cand, s);
   }
-  if (m == n && row0 == 0) {
-    const int64_t T = n_pad / 128;
-    hipLaunchKernelGGL((sqdist_kernel<true>), dim3(T * (T + 1) / 2), dim3(256), 0, s, Y, ldy,
-                       norms, row0, m, n, n_pad, (int)dp, D, select_mode, st, cand);
-  } else {
-    hipLaunchKernelGGL((sqdist_kernel<false>), dim3(n_pad / 128, m_pad / 128), dim3(256), 0, s, Y,
-                       ldy, norms, row0, m, n, n_pad, (int)dp, D, select_mode, st, cand);
-  }
-  return check_launch("sqdist");
 }
 
 }  // extern "C"

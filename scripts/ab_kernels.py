@@ -1,0 +1,69 @@
+"""Interleaved in-process A/B timing of kernel variants at the headline shape
+(cdna_hip_programming.md rule 24: rounds interleaved in ONE process).
+
+    python scripts/ab_kernels.py [--n 65536 --d 256 --rounds 5]
+
+Variants are switched through environment variables the launchers read on
+every call (DSVGD_NN_WAVES=1|2 for the NN MFMA engine).
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dist-svgd_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def timed(fn, reps=3):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--d", type=int, default=256)
+    ap.add_argument("--rounds", type=int, default=5)
+    args = ap.parse_args()
+    import dsvgd
+    n, d = args.n, args.d
+    g = torch.Generator(device="cpu").manual_seed(0)
+    X = torch.randn(n, d, generator=g).cuda()
+    S = torch.randn(n, d, generator=g).cuda()
+    eng = dsvgd.PhiEngine(n, d, device="cuda:0")
+    eng.pack(X, S)
+    eng.distances(median=True)
+    eng.median_bandwidth()
+    variants = {"nn_waves=1": {"DSVGD_NN_WAVES": "1"}, "nn_waves=2": {"DSVGD_NN_WAVES": "2"}}
+    res = {k: [] for k in variants}
+    ref = None
+    for _ in range(args.rounds):
+        for name, env in variants.items():
+            os.environ.update(env)
+            res[name].append(timed(lambda: eng.direction(write_phi=True)))
+            if ref is None:
+                ref = eng.phi.clone()
+            else:
+                err = float((eng.phi - ref).abs().max() / ref.abs().max())
+                assert err < 1e-5, (name, err)
+    flops = 4.0 * n * n * d
+    out = {k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v)),
+               "tflops": flops / (np.median(v) * 1e-3) / 1e12} for k, v in res.items()}
+    out["sqdist_ms"] = timed(lambda: eng.distances(median=False))
+    out["sqdist_select_ms"] = timed(lambda: (eng.distances(median=True), eng.median_bandwidth()))
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
