@@ -47,10 +47,16 @@ __global__ __launch_bounds__(256) void radix_hist_kernel(const float* __restrict
   __syncthreads();
   const int64_t stride = (int64_t)gridDim.x * 256;
   const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (use_cand) {
-    const int64_t nc = (int64_t)min(st->ncand, st->cand_cap);
-    for (int64_t q = t0; q < nc; q += stride)
-      hist_key(__float_as_uint(cand[q]), want, shift, mask, hishift, shist);
+  if (use_cand) {  // lists l = block % 256, each swept by gridDim/256 blocks
+    const unsigned long long capl = st->cand_cap / kCandLists;
+    const int per = max(1, (int)(gridDim.x / kCandLists));
+    for (int l = blockIdx.x % kCandLists; l < kCandLists; l += (int)min(gridDim.x, (unsigned)kCandLists)) {
+      const int64_t nl = (int64_t)min(st->list_cnt[l], capl);
+      const float* c = cand + (unsigned long long)l * capl;
+      for (int64_t q = (int64_t)(blockIdx.x / kCandLists) * 256 + threadIdx.x; q < nl;
+           q += (int64_t)per * 256)
+        hist_key(__float_as_uint(c[q]), want, shift, mask, hishift, shist);
+    }
   } else {
     const int64_t c4 = count >> 2;
     const f32x4* D4 = reinterpret_cast<const f32x4*>(D);
@@ -135,8 +141,9 @@ __device__ void reset_state(dsvgd_select_state* st, unsigned long long k,
   st->h = NAN;
   st->inv_h = NAN;
   st->fallback = 1u;
-  st->below = 0ull;
-  st->ncand = 0ull;
+  st->below_total = 0ull;
+  st->ncand_total = 0ull;
+  st->overflow = 0ull;
 }
 
 __global__ void select_init_kernel(dsvgd_select_state* st, int64_t n_total, int64_t k_rank) {
@@ -155,6 +162,10 @@ __global__ void bracket_init_kernel(dsvgd_select_state* st, int64_t n_total,
                                     const dsvgd_select_state* hi_st, int64_t cap) {
   const int t = threadIdx.x;
   for (int b = t; b < DSVGD_RADIX_BINS; b += blockDim.x) st->hist[b] = 0ull;
+  for (int l = t; l < kCandLists; l += blockDim.x) {
+    st->list_cnt[l] = 0ull;
+    st->list_below[l] = 0ull;
+  }
   if (t == 0) {
     const unsigned long long nn = (unsigned long long)n_total * (unsigned long long)n_total;
     reset_state(st, (nn - 1ull) / 2ull, (unsigned long long)n_total);
@@ -165,12 +176,38 @@ __global__ void bracket_init_kernel(dsvgd_select_state* st, int64_t n_total,
   }
 }
 
-// After the distance pass (and the all-reduce of below/ncand): does the
-// bracket provably hold rank k?  Yes -> select rank k - below among the
-// candidates; no (or overflow) -> select rank k over D itself.
+// Sum the local candidate lists: (below_total, ncand_total, overflow), the
+// int64[3] a distributed caller all-reduces before bracket_check.
+__global__ __launch_bounds__(256) void bracket_totals_kernel(dsvgd_select_state* st) {
+  __shared__ unsigned long long sb[256], sc[256], so[256];
+  const int l = threadIdx.x;
+  const unsigned long long capl = st->cand_cap / kCandLists;
+  const unsigned long long c = st->list_cnt[l];
+  sb[l] = st->list_below[l];
+  sc[l] = c;
+  so[l] = c > capl ? 1ull : 0ull;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (l < o) {
+      sb[l] += sb[l + o];
+      sc[l] += sc[l + o];
+      so[l] += so[l + o];
+    }
+    __syncthreads();
+  }
+  if (l == 0) {
+    st->below_total = sb[0];
+    st->ncand_total = sc[0];
+    st->overflow = so[0];
+  }
+}
+
+// Does the bracket provably hold rank k (global totals)?  Yes -> select rank
+// k - below among the candidates; no (or a list overflowed on any rank) ->
+// select rank k over D itself.
 __global__ void bracket_check_kernel(dsvgd_select_state* st) {
-  const unsigned long long k = st->k, below = st->below, nc = st->ncand;
-  if (below <= k && k < below + nc && nc <= st->cand_cap) {
+  const unsigned long long k = st->k, below = st->below_total, nc = st->ncand_total;
+  if (st->overflow == 0ull && below <= k && k < below + nc) {
     st->k = k - below;
     st->fallback = 0u;
   } else {
@@ -231,7 +268,7 @@ int dsvgd_radix_hist(const float* D, int64_t count, const float* cand, int pass,
   DSVGD_REQUIRE(count >= 0 && ((uintptr_t)D & 15) == 0, "count / alignment");
   int64_t blocks = (count / 4 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  if (blocks < 64) blocks = 64;  // the candidate count is only known on device
+  if (cand && blocks < 1024) blocks = 1024;  // >= 4 blocks per candidate list
   hipLaunchKernelGGL(radix_hist_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, D, count,
                      cand, pass, st);
   return check_launch("radix_hist");
@@ -257,10 +294,18 @@ int dsvgd_sample_sqdist(const float* Y, int64_t ldy, int64_t n, int64_t d, int64
 
 int dsvgd_bracket_init(dsvgd_select_state* st, int64_t n_total, const dsvgd_select_state* lo_st,
                        const dsvgd_select_state* hi_st, int64_t cand_cap, void* stream) {
-  DSVGD_REQUIRE(st && lo_st && hi_st && n_total > 0 && cand_cap > 0, "args");
+  DSVGD_REQUIRE(st && lo_st && hi_st && n_total > 0, "args");
+  DSVGD_REQUIRE(cand_cap >= DSVGD_CAND_LISTS && cand_cap % DSVGD_CAND_LISTS == 0,
+                "cand_cap must be a positive multiple of DSVGD_CAND_LISTS");
   hipLaunchKernelGGL(bracket_init_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, st, n_total,
                      lo_st, hi_st, cand_cap);
   return check_launch("bracket_init");
+}
+
+int dsvgd_bracket_totals(dsvgd_select_state* st, void* stream) {
+  DSVGD_REQUIRE(st, "null state");
+  hipLaunchKernelGGL(bracket_totals_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, st);
+  return check_launch("bracket_totals");
 }
 
 int dsvgd_bracket_check(dsvgd_select_state* st, void* stream) {

@@ -76,39 +76,82 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t& total) 
   return inc - x;
 }
 
-// bracket accounting of a lane's NV values (+inf = invalid), each of weight w
-// (w = 2 for the mirrored tiles of the symmetric Gram): one atomic per wave.
-template <int NV>
-__device__ __forceinline__ void bracket_account(const float (&v)[NV], uint32_t w,
-                                                dsvgd_select_state* __restrict__ st,
-                                                float* __restrict__ cand) {
-  const float lo = st->lo, hi = st->hi;
+// ---- bracketed mode --------------------------------------------------------
+// Phase 1 (while storing D): each lane counts its values < lo and in [lo, hi].
+// Phase 2 (block-collective): one returning atomic per BLOCK on the list
+// counter of the block's candidate list (256 lists: no counter sees more than
+// a few hundred atomics per launch -- same-address float/int atomics from every
+// CU serialise, MI355X_MICROARCH.md "Global float atomics", contention row).
+// Phase 3: each lane re-derives its values (deterministic) and writes the
+// in-bracket ones at its reserved positions.
+struct BracketCounter {
   uint32_t below = 0, inb = 0;
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    below += (v[i] < lo) ? w : 0u;
-    inb += (v[i] >= lo && v[i] <= hi) ? w : 0u;
+  float lo = 0.f, hi = -1.f;
+  __device__ __forceinline__ void load(const dsvgd_select_state* st) {
+    lo = st->lo;
+    hi = st->hi;
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) below += __shfl_xor(below, o, 64);
-  uint32_t total;
-  const uint32_t off = wave_excl_scan(inb, total);
-  const int lane = threadIdx.x & 63;
-  if (lane == 0 && below)
-    atomicAdd((unsigned long long*)&st->below, (unsigned long long)below);
-  if (total == 0) return;
-  unsigned long long base = 0;
-  if (lane == 0) base = atomicAdd((unsigned long long*)&st->ncand, (unsigned long long)total);
-  base = __shfl(base, 0, 64);
-  const unsigned long long cap = st->cand_cap;
-  unsigned long long pos = base + off;
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    if (v[i] >= lo && v[i] <= hi) {
+  __device__ __forceinline__ void count(float v, uint32_t w) {
+    below += (v < lo) ? w : 0u;
+    inb += (v >= lo && v <= hi) ? w : 0u;
+  }
+};
+
+struct BracketWriter {
+  float* dst = nullptr;
+  unsigned long long pos = 0, cap = 0;
+  float lo = 0.f, hi = -1.f;
+  __device__ __forceinline__ void put(float v, uint32_t w) {
+    if (v >= lo && v <= hi) {
       for (uint32_t r = 0; r < w; ++r, ++pos)
-        if (pos < cap) cand[pos] = v[i];
+        if (pos < cap) dst[pos] = v;
     }
   }
+};
+
+constexpr int kCandLists = DSVGD_CAND_LISTS;
+
+// sred: LDS scratch of >= 2*NW + 4 u32 (NW = waves per block).  Every thread
+// of the block must call it.
+template <int NW>
+__device__ __forceinline__ BracketWriter bracket_reserve(const BracketCounter& bc,
+                                                         dsvgd_select_state* __restrict__ st,
+                                                         float* __restrict__ cand, int list,
+                                                         uint32_t* sred) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t below = bc.below;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) below += __shfl_xor(below, o, 64);
+  uint32_t wtotal;
+  const uint32_t off = wave_excl_scan(bc.inb, wtotal);
+  if (lane == 0) {
+    sred[wave] = wtotal;
+    sred[NW + wave] = below;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0, bsum = 0;
+    for (int w = 0; w < NW; ++w) {
+      const uint32_t t = sred[w];
+      sred[w] = run;
+      run += t;
+      bsum += sred[NW + w];
+    }
+    unsigned long long base = 0;
+    if (run) base = atomicAdd((unsigned long long*)&st->list_cnt[list], (unsigned long long)run);
+    if (bsum) atomicAdd((unsigned long long*)&st->list_below[list], (unsigned long long)bsum);
+    sred[2 * NW] = (uint32_t)(base & 0xffffffffull);
+    sred[2 * NW + 1] = (uint32_t)(base >> 32);
+  }
+  __syncthreads();
+  BracketWriter bw;
+  const unsigned long long cap = st->cand_cap / kCandLists;
+  bw.dst = cand + (unsigned long long)list * cap;
+  bw.cap = cap;
+  bw.pos = (((unsigned long long)sred[2 * NW + 1] << 32) | sred[2 * NW]) + sred[wave] + off;
+  bw.lo = bc.lo;
+  bw.hi = bc.hi;
+  return bw;
 }
 
 }  // namespace dsvgd

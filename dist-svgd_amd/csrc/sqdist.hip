@@ -38,6 +38,7 @@ __global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y
   __shared__ __attribute__((aligned(16))) float smem[GramTile::kSmemFloats];
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
   __shared__ float snorm[GramTile::BM + GramTile::BN];
+  __shared__ uint32_t sred[16];
 
   int bi, bj;
   if (SYM) {
@@ -62,6 +63,8 @@ __global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
   const uint32_t weight = mirror ? 2u : 1u;
   WindowHist wh;
+  BracketCounter bc;
+  if (smode == kSelBracket) bc.load(st);
   // epilogue one 32x32 sub-tile (16 values per lane) at a time.  Panel-layout
   // addresses: per lane one base pointer per sub-tile, the per-register part
   // ((r&3)*16 + (r>>2)*128 floats) is a compile-time immediate.
@@ -101,9 +104,25 @@ __global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y
         if (mi == 0 && ni == 0) wh.init(v[0]);
         hist_account(wh, v, weight, shist);
       } else if (smode == kSelBracket) {
-        bracket_account(v, weight, st, cand);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bc.count(v[r], weight);
       }
     }
+  if (smode == kSelBracket) {
+    BracketWriter bw = bracket_reserve<4>(bc, st, cand, (int)(blockIdx.x & (kCandLists - 1)), sred);
+    // phase 3 re-reads this lane's own just-written D entries (L2-hot) rather
+    // than keeping the accumulators live across the block-wide reservation
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int cl = wn * 64 + ni * 32 + (lane & 31);
+        const int rb = wm * 64 + mi * 32 + h4;
+        const float* dp0 = Dtile + (cl >> 4) * kPanelElems + (cl & 15) + rb * 16;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bw.put(dp0[(r & 3) * 16 + (r >> 2) * 128], weight);
+      }
+  }
   if (smode == kSelHist) {
     wh.flush(shist);
     __syncthreads();
@@ -128,6 +147,7 @@ __global__ __launch_bounds__(256) void sqdist_direct_kernel(const float* __restr
   __shared__ __attribute__((aligned(16))) float sA[kDirectMaxD][128];
   __shared__ __attribute__((aligned(16))) float sB[kDirectMaxD][128];
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
+  __shared__ uint32_t sred[16];
   const int t = threadIdx.x;
   const int64_t i0 = (int64_t)blockIdx.y * 128, j0 = (int64_t)blockIdx.x * 128;
   if (smode == kSelHist)
@@ -162,6 +182,8 @@ __global__ __launch_bounds__(256) void sqdist_direct_kernel(const float* __restr
   WindowHist wh;
   if (smode == kSelHist)
     wh.init((i0 + ty * 8 < m && j0 + tx * 8 < n) ? acc[0][0] : INFINITY);
+  BracketCounter bc;
+  if (smode == kSelBracket) bc.load(st);
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
     const int64_t gi = i0 + ty * 8 + a;
@@ -174,10 +196,22 @@ __global__ __launch_bounds__(256) void sqdist_direct_kernel(const float* __restr
     float* dst = D + panel_off(gi, j0 + tx * 8, n_pad);
     *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
     *reinterpret_cast<f32x4*>(dst + 4) = f32x4{v[4], v[5], v[6], v[7]};
-    if (smode == kSelHist)
+    if (smode == kSelHist) {
       hist_account(wh, v, 1u, shist);
-    else if (smode == kSelBracket)
-      bracket_account(v, 1u, st, cand);
+    } else if (smode == kSelBracket) {
+#pragma unroll
+      for (int b = 0; b < 8; ++b) bc.count(v[b], 1u);
+    }
+  }
+  if (smode == kSelBracket) {
+    const int list = (int)((blockIdx.x + blockIdx.y * gridDim.x) & (kCandLists - 1));
+    BracketWriter bw = bracket_reserve<4>(bc, st, cand, list, sred);
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      const float* src = D + panel_off(i0 + ty * 8 + a, j0 + tx * 8, n_pad);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) bw.put(src[b], 1u);  // pads are +inf: never in the bracket
+    }
   }
   if (smode == kSelHist) {
     wh.flush(shist);

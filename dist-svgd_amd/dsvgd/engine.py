@@ -23,6 +23,7 @@ import torch
 from . import _native as N
 
 NBINS = 2048
+NLISTS = 256
 
 
 class _SelectState(ctypes.Structure):
@@ -31,8 +32,10 @@ class _SelectState(ctypes.Structure):
                 ("n_total", ctypes.c_uint64), ("prefix", ctypes.c_uint32),
                 ("passes_done", ctypes.c_uint32), ("median", ctypes.c_float),
                 ("h", ctypes.c_float), ("inv_h", ctypes.c_float), ("fallback", ctypes.c_uint32),
-                ("below", ctypes.c_uint64), ("ncand", ctypes.c_uint64), ("lo", ctypes.c_float),
-                ("hi", ctypes.c_float), ("cand_cap", ctypes.c_uint64)]
+                ("below_total", ctypes.c_uint64), ("ncand_total", ctypes.c_uint64),
+                ("overflow", ctypes.c_uint64), ("lo", ctypes.c_float), ("hi", ctypes.c_float),
+                ("cand_cap", ctypes.c_uint64), ("list_cnt", ctypes.c_uint64 * NLISTS),
+                ("list_below", ctypes.c_uint64 * NLISTS)]
 
 SEL_NONE, SEL_HIST, SEL_BRACKET = 0, 1, 2
 
@@ -59,19 +62,21 @@ class SelectState(object):
         return self.buf[:NBINS]
 
     @property
-    def counts(self):
-        """int64[2] view of (below, ncand) -- all-reduced in bracketed mode."""
-        o = _SelectState.below.offset // 8
-        return self.buf[o:o + 2]
+    def totals(self):
+        """int64[3] view of (below_total, ncand_total, overflow) -- all-reduced
+        between dsvgd_bracket_totals and dsvgd_bracket_check."""
+        o = _SelectState.below_total.offset // 8
+        return self.buf[o:o + 3]
 
     def bracket(self):
-        """(lo, hi, below, ncand, fallback) -- synchronises with the device."""
+        """(lo, hi, below_total, ncand_total, fallback) -- synchronises."""
         raw = self.buf.cpu()
         u8 = raw.view(torch.uint8)
         lo, hi = u8[_SelectState.lo.offset:_SelectState.lo.offset + 8].view(torch.float32).tolist()
         fb = int(u8[_SelectState.fallback.offset:_SelectState.fallback.offset + 4]
                  .view(torch.int32)[0])
-        b, c = raw[_SelectState.below.offset // 8:_SelectState.below.offset // 8 + 2].tolist()
+        o = _SelectState.below_total.offset // 8
+        b, c = raw[o:o + 2].tolist()
         return lo, hi, b, c, fb
 
     def read(self):
@@ -168,7 +173,7 @@ class PhiEngine(object):
             self.k_hi = min(s - 1, int(math.ceil(half + dk)))
             self.sample = torch.empty(s, **f32)
             self.st_lo, self.st_hi = SelectState(dev), SelectState(dev)
-            self.cand_cap = max(1 << 22, (m * n) // 16)
+            self.cand_cap = max(1 << 22, (m * n) // 16) // NLISTS * NLISTS
             self.cand = torch.empty(self.cand_cap, **f32)
 
     # ------------------------------------------------------------ stages --
@@ -224,8 +229,9 @@ class PhiEngine(object):
         count = self.m_pad * self.n_pad
         cand = None
         if self.bracketed:
+            N.call("dsvgd_bracket_totals", self.state.ptr, s)
             if allreduce is not None:
-                allreduce(self.state.counts)
+                allreduce(self.state.totals)
             N.call("dsvgd_bracket_check", self.state.ptr, s)
             cand = N.ptr(self.cand)
         for p in (1, 2, 3):
