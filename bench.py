@@ -74,6 +74,22 @@ def cpu_baseline(n, d, x_local, t_local, budget_s):
     return out
 
 
+def pmc_traffic(kernel_prefix):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
+    --pmc summary (FETCH_SIZE x2 [gfx950 half-count] + WRITE_SIZE, separate
+    passes; scripts/pmc_summary.py) -- None if no summary is present."""
+    path = os.path.join(ROOT, "profiles", "latest_summary.json")
+    try:
+        with open(path) as f:
+            ks = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None, None
+    for name, v in ks.items():
+        if name.startswith(kernel_prefix) and "hbm_bytes_per_launch" in v:
+            return v["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -138,6 +154,7 @@ def main():
 
     m = n // world
     phi_ms = stages["phi_mm"]
+    traffic, traffic_src = pmc_traffic("void dsvgd::nn_kernel<4, true")
     flops = 4.0 * m * n * d
     achieved = flops / (phi_ms * 1e-3) / 1e12
     out = {
@@ -159,7 +176,9 @@ def main():
                    "particles_per_gpu": m},
         "roofline": {"bound": "mfma", "kernel": "phi_mm (nn_kernel<4,true>)",
                      "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
+                     "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
+                     "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                     "algorithmic_bytes": 4.0 * m * n + 4.0 * (n + 128) * 512,
                      "flop_per_launch": flops, "avg_launch_ms": phi_ms},
         "stages_ms": stages,
         "step_6n2d_mfma_frac": (6.0 * m * n * d) / (el / args.steps) / 1e12 / PEAK_FP32_MFMA_TFLOPS,

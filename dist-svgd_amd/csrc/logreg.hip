@@ -15,7 +15,7 @@ namespace dsvgd {
 
 int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, int64_t cols,
             int splits, const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum,
-            int64_t m, hipStream_t s);
+            int64_t m, int64_t row0, hipStream_t s);
 
 static int64_t nn_cols(int64_t w) {
   if (w <= 128) return 128;
@@ -153,7 +153,7 @@ int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const 
   hipLaunchKernelGGL(logreg_z_kernel, dim3(w.N_pad / 128, w.n_pad / 128), dim3(256), 0, s, Wp, Xdp,
                      w.ldb, (int)w.pp, tp, N, w.N_pad, G);
   if ((rc = check_launch("logreg_z"))) return rc;
-  if ((rc = nn_gemm(false, G, w.N_pad, Xdp, w.ldb, w.ldb, 1, nullptr, GW, w.ldb, nullptr, n, s)))
+  if ((rc = nn_gemm(false, G, w.N_pad, Xdp, w.ldb, w.ldb, 1, nullptr, GW, w.ldb, nullptr, n, 0, s)))
     return rc;
   hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,
                      w.ldb, scale, S, lds);

@@ -17,13 +17,16 @@ namespace dsvgd {
 // blockIdx.z = split-K slice z: K columns [z*kchunk, min(K,(z+1)*kchunk)) into
 // the partial C + z*m*ldc (and rowsum + z*m_pad); phi_finish sums the slices
 // in order (deterministic, no atomics).
+// row0: interacting-set index of A's row 0 (EXP: the diagonal j == row0 + i
+// is skipped, see NNTile::compute).
 template <int TN, bool EXP, int WM>
 __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ A, int64_t a_npad,
                                                       const float* __restrict__ B, int64_t ldb,
                                                       int64_t K, int64_t kchunk,
                                                       const dsvgd_select_state* __restrict__ st,
                                                       float* __restrict__ C, int64_t ldc,
-                                                      float* __restrict__ rowsum, int64_t m) {
+                                                      float* __restrict__ rowsum, int64_t m,
+                                                      int64_t row0) {
   using Tile = NNTile<TN, EXP, WM>;
   __shared__ __attribute__((aligned(16))) float smem[Tile::kSmemFloats];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
@@ -35,7 +38,8 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
   float scale = 0.f;
   if (EXP) scale = -st->inv_h * kLog2e;
   Tile tile;
-  tile.run(A + (i0 >> 7) * (a_npad >> 4) * kPanelElems, B + c0, ldb, k0, k1, scale, smem);
+  tile.run(A + (i0 >> 7) * (a_npad >> 4) * kPanelElems, B + c0, ldb, k0, k1, scale, smem,
+           row0 + i0);
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
   const int64_t r0 = i0 + wr * 32 * Tile::TM;
@@ -79,8 +83,9 @@ __global__ __launch_bounds__(256) void phi_finish_kernel(
     ks += ky[dp + c];
     r += rowsum[(int64_t)z * mp + i];
   }
-  const float xc = Y[(row0 + i) * ldy + c];
-  const float p = inv_n * (ks + two_inv_h * (r * xc - kx));
+  const float* yi = Y + (row0 + i) * ldy;
+  // + the self term k_ii (s_i + 2/h (x_i - x_i)) = s_i, excluded from phi_mm
+  const float p = inv_n * ((yi[dp + c] + ks) + two_inv_h * (r * yi[c] - kx));
   if (phi) phi[i * ldphi + c] = p;
   if (X) X[i * ldx + c] += step * p;
 }
@@ -211,34 +216,37 @@ static int nn_waves_per_simd() {
 template <int TN, int WM>
 int launch_nn_wm(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
                  const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-                 int64_t cols, hipStream_t s) {
+                 int64_t cols, int64_t row0, hipStream_t s) {
   const int64_t kchunk = roundup((K + splits - 1) / splits, 16);
   const dim3 grid(cols / (128 * TN), roundup(m, 128) / 128, splits);
   if (exp_)
     hipLaunchKernelGGL((nn_kernel<TN, true, WM>), grid, dim3(256 * WM), 0, s, A, K, B, ldb, K,
-                       kchunk, st, C, ldc, rowsum, m);
+                       kchunk, st, C, ldc, rowsum, m, row0);
   else
     hipLaunchKernelGGL((nn_kernel<TN, false, WM>), grid, dim3(256 * WM), 0, s, A, K, B, ldb, K,
-                       kchunk, st, C, ldc, rowsum, m);
+                       kchunk, st, C, ldc, rowsum, m, row0);
   return check_launch("nn_kernel");
 }
 
 template <int TN>
 int launch_nn(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
               const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-              int64_t cols, hipStream_t s) {
+              int64_t cols, int64_t row0, hipStream_t s) {
   if (nn_waves_per_simd() == 2)
-    return launch_nn_wm<TN, 2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, s);
-  return launch_nn_wm<TN, 1>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, s);
+    return launch_nn_wm<TN, 2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s);
+  return launch_nn_wm<TN, 1>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s);
 }
 
 // C[splits x m x cols] = f(A) B with A in panel layout (m_pad x K), B row-major K x cols.
+// exp_: f = exp2(-inv_h log2e a) with the diagonal (column row0 + i) skipped.
 int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, int64_t cols,
             int splits, const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum,
-            int64_t m, hipStream_t s) {
-  if (cols % 512 == 0) return launch_nn<4>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, s);
-  if (cols % 256 == 0) return launch_nn<2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, s);
-  return launch_nn<1>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, s);
+            int64_t m, int64_t row0, hipStream_t s) {
+  if (cols % 512 == 0)
+    return launch_nn<4>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s);
+  if (cols % 256 == 0)
+    return launch_nn<2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s);
+  return launch_nn<1>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s);
 }
 
 // split-K slices so that a phi_mm launch has >= 2 blocks per CU (256 CUs),
@@ -259,9 +267,9 @@ extern "C" {
 
 int64_t dsvgd_phi_splits(int64_t m, int64_t n, int64_t ldy) { return phi_splits(m, n, ldy); }
 
-int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t m, int64_t n,
-                 const dsvgd_select_state* st, int64_t splits, float* KY, int64_t ldk,
-                 float* rowsum, void* stream) {
+int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t row0,
+                 int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
+                 int64_t ldk, float* rowsum, void* stream) {
   DSVGD_REQUIRE(D && Y && st && KY && rowsum, "null pointer");
   DSVGD_REQUIRE(m > 0 && n > 0, "sizes");
   const int64_t n_pad = roundup(n, 128);
@@ -270,7 +278,8 @@ int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64
   DSVGD_REQUIRE(((uintptr_t)Y & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
   DSVGD_REQUIRE(roundup(m, 128) / 128 <= 65535, "too many row tiles");
   DSVGD_REQUIRE(splits >= 1 && splits <= 1024, "splits must be in [1, 1024]");
-  return nn_gemm(true, D, n_pad, Y, ldy, ldy, (int)splits, st, KY, ldk, rowsum, m,
+  DSVGD_REQUIRE(row0 >= 0 && row0 + m <= n, "row block outside [0, n)");
+  return nn_gemm(true, D, n_pad, Y, ldy, ldy, (int)splits, st, KY, ldk, rowsum, m, row0,
                  (hipStream_t)stream);
 }
 

@@ -86,14 +86,17 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t& total) 
 // in-bracket ones at its reserved positions.
 struct BracketCounter {
   uint32_t below = 0, inb = 0;
+  uint64_t mask = 0;  // bit i: value i of this lane is in [lo, hi]
   float lo = 0.f, hi = -1.f;
   __device__ __forceinline__ void load(const dsvgd_select_state* st) {
     lo = st->lo;
     hi = st->hi;
   }
-  __device__ __forceinline__ void count(float v, uint32_t w) {
+  __device__ __forceinline__ void count(float v, uint32_t w, int idx) {
+    const bool in = v >= lo && v <= hi;
     below += (v < lo) ? w : 0u;
-    inb += (v >= lo && v <= hi) ? w : 0u;
+    inb += in ? w : 0u;
+    mask |= (uint64_t)in << idx;
   }
 };
 
@@ -102,10 +105,8 @@ struct BracketWriter {
   unsigned long long pos = 0, cap = 0;
   float lo = 0.f, hi = -1.f;
   __device__ __forceinline__ void put(float v, uint32_t w) {
-    if (v >= lo && v <= hi) {
-      for (uint32_t r = 0; r < w; ++r, ++pos)
-        if (pos < cap) dst[pos] = v;
-    }
+    for (uint32_t r = 0; r < w; ++r, ++pos)
+      if (pos < cap) dst[pos] = v;
   }
 };
 

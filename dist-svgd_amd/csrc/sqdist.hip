@@ -105,23 +105,19 @@ __global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y
         hist_account(wh, v, weight, shist);
       } else if (smode == kSelBracket) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) bc.count(v[r], weight);
+        for (int r = 0; r < 16; ++r) bc.count(v[r], weight, (mi * 2 + ni) * 16 + r);
       }
     }
   if (smode == kSelBracket) {
     BracketWriter bw = bracket_reserve<4>(bc, st, cand, (int)(blockIdx.x & (kCandLists - 1)), sred);
-    // phase 3 re-reads this lane's own just-written D entries (L2-hot) rather
-    // than keeping the accumulators live across the block-wide reservation
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni) {
-        const int cl = wn * 64 + ni * 32 + (lane & 31);
-        const int rb = wm * 64 + mi * 32 + h4;
-        const float* dp0 = Dtile + (cl >> 4) * kPanelElems + (cl & 15) + rb * 16;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) bw.put(dp0[(r & 3) * 16 + (r >> 2) * 128], weight);
-      }
+    // phase 3 re-reads only this lane's in-bracket entries (~1 %, L2-hot)
+    // instead of keeping the accumulators live across the block reservation
+    for (uint64_t msk = bc.mask; msk; msk &= msk - 1) {
+      const int idx = __builtin_ctzll(msk), sub = idx >> 4, r = idx & 15;
+      const int cl = wn * 64 + (sub & 1) * 32 + (lane & 31);
+      const int rl = wm * 64 + (sub >> 1) * 32 + h4 + (r & 3) + 8 * (r >> 2);
+      bw.put(Dtile[(cl >> 4) * kPanelElems + (cl & 15) + rl * 16], weight);
+    }
   }
   if (smode == kSelHist) {
     wh.flush(shist);
@@ -200,17 +196,15 @@ __global__ __launch_bounds__(256) void sqdist_direct_kernel(const float* __restr
       hist_account(wh, v, 1u, shist);
     } else if (smode == kSelBracket) {
 #pragma unroll
-      for (int b = 0; b < 8; ++b) bc.count(v[b], 1u);
+      for (int b = 0; b < 8; ++b) bc.count(v[b], 1u, a * 8 + b);
     }
   }
   if (smode == kSelBracket) {
     const int list = (int)((blockIdx.x + blockIdx.y * gridDim.x) & (kCandLists - 1));
     BracketWriter bw = bracket_reserve<4>(bc, st, cand, list, sred);
-#pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      const float* src = D + panel_off(i0 + ty * 8 + a, j0 + tx * 8, n_pad);
-#pragma unroll
-      for (int b = 0; b < 8; ++b) bw.put(src[b], 1u);  // pads are +inf: never in the bracket
+    for (uint64_t msk = bc.mask; msk; msk &= msk - 1) {
+      const int idx = __builtin_ctzll(msk);
+      bw.put(D[panel_off(i0 + ty * 8 + (idx >> 3), j0 + tx * 8 + (idx & 7), n_pad)], 1u);
     }
   }
   if (smode == kSelHist) {

@@ -265,8 +265,8 @@ class PhiEngine(object):
                        float(step), phi, self.d, xo, ldx, s)
             return
         with span(self.timer, "phi_mm"):
-            N.call("dsvgd_phi_mm", N.ptr(self.D), self.n_pad, N.ptr(self.Y), self.ldy, self.m,
-                   self.n, self.state.ptr, self.splits, N.ptr(self.KY), self.ldy,
+            N.call("dsvgd_phi_mm", N.ptr(self.D), self.n_pad, N.ptr(self.Y), self.ldy, self.row0,
+                   self.m, self.n, self.state.ptr, self.splits, N.ptr(self.KY), self.ldy,
                    N.ptr(self.rowsum), s)
         N.call("dsvgd_phi_finish", N.ptr(self.KY), self.ldy, N.ptr(self.rowsum), self.splits,
                N.ptr(self.Y), self.ldy, self.row0, self.m, self.d, self.dp, self.state.ptr,

@@ -151,20 +151,22 @@ int dsvgd_bracket_check(dsvgd_select_state* st, void* stream);
 int dsvgd_set_bandwidth(dsvgd_select_state* st, float h, void* stream);
 
 /* ---- phi: K.[Xc | S] on MFMA with the fused RBF exp -------------------- */
-/* KY_z[i][:] = sum_{j in slice z} exp(-D[i][j]/h) Y[j][:] and rowsum_z[i] =
- * sum_{j in slice z} exp(-D[i][j]/h) for split-K slices z < splits of the
- * columns (h read from st on device).  KY holds splits x m rows (ldk >= ldy,
+/* KY_z[i][:] = sum_{j in slice z, j != row0+i} exp(-D[i][j]/h) Y[j][:] and
+ * rowsum_z[i] = the same sum of exp(-D[i][j]/h), for split-K slices z < splits
+ * of the columns (h read from st on device; row0 = index of the block's first
+ * row in the interacting set; the diagonal self term is added exactly by
+ * dsvgd_phi_finish instead of being summed among ~n tiny terms).  KY holds splits x m rows (ldk >= ldy,
  * slice z at KY + z*m*ldk), rowsum splits x roundup(m,128) floats.
  * Replaces the inner loop of dsvgd/sampler.py:35-40 (_phi_hat) and
  * dsvgd/distsampler.py:84-101.  dsvgd_phi_splits gives a slice count that
  * fills the 256 CUs (>= 2 blocks per CU) for an m-row block. */
 int64_t dsvgd_phi_splits(int64_t m, int64_t n, int64_t ldy);
-int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t m,
-                 int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
+int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t row0,
+                 int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
                  int64_t ldk, float* rowsum, void* stream);
 
-/* phi[i] = inv_n * (KS[i] + (2/h) (rowsum[i] xc[i] - KXc[i])) with the split-K
- * partials summed in slice order, and, if X != NULL, X[i] += step * phi[i]
+/* phi[i] = inv_n * (s_i + KS[i] + (2/h) (rowsum[i] xc[i] - KXc[i])) with the
+ * split-K partials summed in slice order (s_i: the self term k_ii s_i), and, if X != NULL, X[i] += step * phi[i]
  * (the update of dsvgd/sampler.py:68 / dsvgd/distsampler.py:200, Jacobi
  * order).  phi may be NULL. */
 int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t splits,

@@ -40,6 +40,9 @@ def main(run, tag):
             v["hbm_bytes_per_launch"] = v.get("fetch_bytes_corrected", 0) + v.get("write_bytes", 0)
     with open(os.path.join("profiles", "%s_summary.json" % tag), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
+    if any("hbm_bytes_per_launch" in v for v in out["kernels"].values()):
+        shutil.copy(os.path.join("profiles", "%s_summary.json" % tag),
+                    os.path.join("profiles", "latest_summary.json"))
     for k, v in sorted(out["kernels"].items(), key=lambda kv: -kv[1].get("avg_ms", 0)):
         print("%-70s %8.3f ms  %s" % (k[:70], v.get("avg_ms", float("nan")),
               "%.2f GB" % (v["hbm_bytes_per_launch"] / 1e9) if "hbm_bytes_per_launch" in v else ""))
