@@ -249,13 +249,21 @@ int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, i
   return launch_nn<1>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s);
 }
 
-// split-K slices so that a phi_mm launch has >= 2 blocks per CU (256 CUs),
-// each slice keeping >= 64 K-steps (1024 columns) of its own.
+// split-K slices: (1) enough for >= 2 blocks per CU (256 CUs) when the owned
+// row block is small (S ranks), (2) at most kMaxChain columns per fp32
+// accumulation chain.  (2) is precision: K.S is a coherent sum (|sum| grows
+// linearly), so one n-long fma chain loses ~sqrt(n) eps |sum| -- 8.7e-6 of
+// max|phi| at n = 65536, d = 256 (scripts/diag_precision.py); slices of 8192
+// summed in slice order by phi_finish cut that ~8x.
+constexpr int64_t kMaxChain = 8192;
+
 int64_t phi_splits(int64_t m, int64_t n, int64_t ldy) {
   const int64_t cols = ldy % 512 == 0 ? 512 : (ldy % 256 == 0 ? 256 : 128);
   const int64_t blocks = (roundup(m, 128) / 128) * (ldy / cols);
+  const int64_t n_pad = roundup(n, 128);
   int64_t s = 1;
-  while (blocks * s < 512 && roundup(n, 128) / (2 * s) >= 1024) s *= 2;
+  while (blocks * s < 512 && n_pad / (2 * s) >= 1024) s *= 2;
+  while (n_pad / s > kMaxChain && s < 64) s *= 2;
   return s;
 }
 

@@ -129,12 +129,15 @@ class DistSampler(object):
     def _local_scores(self, X, out, scale=1.0):
         self._target.score(X, out, scale)
 
-    def _exchange_all_scores(self):
+    def _exchange_all_scores(self, async_op=False):
         "Sum of every shard's local-data scores of all particles (distsampler.py:160-170)."
         with span(self.timer, "scores"):
             self._local_scores(self._work, self._scores)
+        if async_op:
+            return exchange.all_reduce_sum_async(self._scores, self._group)
         with span(self.timer, "allreduce_scores"):
             exchange.all_reduce_sum(self._scores, self._group)
+        return None
 
     # ------------------------------------------------------------ step --
     def _engine(self, n_int, m, row0):
@@ -153,12 +156,16 @@ class DistSampler(object):
             h - discretization size for the JKO (W2) term
         """
         S = self._num_shards
+        # Jacobi + all_scores: the score all-reduce (n x d) overlaps the
+        # distance / median stage, which needs the particles only
+        overlap = self._order == "jacobi" and self._exchange_scores and S > 1
+        pending = None
         if S > 1:
             if self._exchange_particles:
                 with span(self.timer, "allgather_x"):
                     self._exchange_all_particles()
                 if self._exchange_scores:
-                    self._exchange_all_scores()
+                    pending = self._exchange_all_scores(async_op=overlap)
             else:
                 with span(self.timer, "ring_shift"):
                     self._exchange_round_robin()
@@ -191,8 +198,20 @@ class DistSampler(object):
 
         if self._order == "jacobi":
             eng = self._engine(n_int, e - s, s - lo)
-            eng.step(Xi, Si, X_own=X[s:e], step=step_size, h=None if median else self._rbf.h,
-                     allreduce=hook, write_phi=False)
+            if pending is not None:
+                eng.pack(Xi)                       # X half only: the scores are in flight
+                eng.distances(median=median)
+                if median:
+                    eng.median_bandwidth(hook)
+                else:
+                    eng.fixed_bandwidth(self._rbf.h)
+                with span(self.timer, "allreduce_scores_wait"):
+                    pending.wait()
+                eng.pack(Xi, Si)                   # Si already carries the score scale
+                eng.direction(X[s:e], step_size, write_phi=False)
+            else:
+                eng.step(Xi, Si, X_own=X[s:e], step=step_size, h=None if median else self._rbf.h,
+                         allreduce=hook, write_phi=False)
         else:
             if median:
                 eng = self._engine(n_int, e - s, s - lo)

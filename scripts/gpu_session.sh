@@ -25,6 +25,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     prof)  step prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     ab)    step ab 600 python scripts/ab_kernels.py ;;
     dbg)   step dbg 600 python scripts/debug_dist.py 6000 16 ;;
+    diag)  step diag 600 python scripts/diag_precision.py ;;
     pmc)   step pmc 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmcw)  step pmcw 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
   esac
