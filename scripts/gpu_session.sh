@@ -27,6 +27,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     dbg)   step dbg 600 python scripts/debug_dist.py 6000 16 ;;
     diag)  step diag 600 python scripts/diag_precision.py ;;
     pmc)   step pmc 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmcclk) step pmcclk 900 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 --kernel-trace -d "$OUT/pmcclk" -o run --output-format csv -- python3 scripts/ab_kernels.py --rounds 1 ;;
     pmcw)  step pmcw 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
   esac
 done

@@ -346,7 +346,7 @@ def test_wasserstein_flag_raises_from_second_step():
 
 
 # ------------------------------------------ DistSampler, 2 ranks, 1 GPU --
-def _dist_gpu_worker(rank, S, port, name, order, q):
+def _dist_gpu_worker(rank, S, port, name, order, q, median=False):
     import os
     import sys
     import torch.distributed as dist
@@ -363,7 +363,7 @@ def _dist_gpu_worker(rank, S, port, name, order, q):
     mode = str(g["mode"])
     tgt = m.targets.LogisticRegression(x[rank * per:(rank + 1) * per], t[rank * per:(rank + 1) * per])
     parts = torch.tensor(g["init"][rank], device=DEV)
-    ds = m.DistSampler(rank, S, tgt, m.RBF(1.0), parts, per, per * S,
+    ds = m.DistSampler(rank, S, tgt, m.RBF("median" if median else 1.0), parts, per, per * S,
                        exchange_particles=mode in ("all_particles", "all_scores"),
                        exchange_scores=mode == "all_scores", include_wasserstein=False,
                        order=order)
@@ -453,3 +453,36 @@ def test_distsampler_median_two_ranks_jacobi(d):
         for bracketed, h, fallback in hs:
             assert bracketed and fallback == 0
     assert res[0][2] == res[1][2]            # identical h on both ranks
+
+
+@pytest.mark.parametrize("mode", ["all_scores", "all_particles", "partitions"])
+def test_distsampler_two_ranks_jacobi_vs_oracle(golden, mode):
+    """Jacobi DistSampler over 2 ranks (the all_scores path overlaps the score
+    all-reduce with the distance stage) vs the oracle's Jacobi DistSampler."""
+    import torch.multiprocessing as mp
+    name = "g4_dist_s2_" + mode
+    g = golden(name)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29860 + ["partitions", "all_particles", "all_scores"].index(mode)
+    ps = [ctx.Process(target=_dist_gpu_worker, args=(r, 2, port, name, "jacobi", q))
+          for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda r: r[0])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    x, t = g["x_train"], g["t_train"]
+    per = x.shape[0] // 2
+    fns = [(lambda X, r=r: O.score_logreg(X, x[r * per:(r + 1) * per], t[r * per:(r + 1) * per]))
+           for r in range(2)]
+    D = O.DistOracle(list(g["init"]), fns, per, 2 * per,
+                     exchange_particles=mode != "partitions", exchange_scores=mode == "all_scores",
+                     h=1.0, sequential=False)
+    for step in range(int(g["steps"])):
+        D.step(float(g["eps"]))
+        for rank, out in res:
+            own, full, start = out[step]
+            assert start == D.start[rank]
+            assert abs_err(own, D.own(rank)) < TRAJ_TOL
