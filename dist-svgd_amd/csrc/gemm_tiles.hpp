@@ -130,16 +130,18 @@ struct NTTile {
 };
 
 // ------------------------------------------------------------ NN engine ----
-// BM = 128 rows; WM x 4 waves (256*WM threads): wave (wr, wc) owns rows
-// [wr*128/WM, +128/WM) x columns [wc*32*TN, +32*TN) -- TM = 4/WM row tiles,
-// i.e. 16*TM*TN accumulator registers (WM = 2: two waves per SIMD, 128 AGPRs
-// each, so one wave's barrier / LDS waits hide under the other's MFMAs).
-// K-step = one 16-column panel of A and 16 rows of B.
-template <int TN, bool EXP, int WM = 1>
+// Block = WM x 4 waves (256*WM threads): wave (wr, wc) owns rows
+// [wr*32*TM, +32*TM) x columns [wc*32*TN, +32*TN), i.e. 16*TM*TN accumulator
+// registers; BM = 32*TM*WM rows (64 or 128) per block.  Shapes in use:
+//   WM=1 TM=4 (128 rows, 256 AGPRs, 1 wave/SIMD), WM=2 TM=2 (128 rows, two
+//   waves per SIMD in one block), WM=1 TM=2 (64 rows, two blocks per CU: one
+//   block's barrier wait hides under the other block's MFMAs).
+// K-step = one 16-column panel slice of A (BM rows) and 16 rows of B.
+template <int TN, bool EXP, int WM = 1, int TM_ = 4 / WM>
 struct NNTile {
   static constexpr int kThreads = 256 * WM;
-  static constexpr int TM = 4 / WM;
-  static constexpr int BM = 128;
+  static constexpr int TM = TM_;
+  static constexpr int BM = 32 * TM * WM;
   static constexpr int BC = 128 * TN;
   static constexpr int BJ = 16;
   static constexpr int LDA = BJ + 4;  // 80-B rows: conflict-free ds_read_b128
@@ -150,6 +152,7 @@ struct NNTile {
   static constexpr int LA = BM * BJ / 4 / kThreads;
   static constexpr int LB = BJ * BC / 4 / kThreads;
   static_assert(LA >= 1 && LB >= 1, "tile too small for the block");
+  static_assert(BM == 64 || BM == 128, "BM must divide the 128-row panel");
 
   f32x16 acc[TM][TN];
   f32x4 ra[LA], rb[LB];

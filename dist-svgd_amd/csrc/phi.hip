@@ -19,7 +19,7 @@ namespace dsvgd {
 // in order (deterministic, no atomics).
 // row0: interacting-set index of A's row 0 (EXP: the diagonal j == row0 + i
 // is skipped, see NNTile::compute).
-template <int TN, bool EXP, int WM>
+template <int TN, bool EXP, int WM, int TM>
 __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ A, int64_t a_npad,
                                                       const float* __restrict__ B, int64_t ldb,
                                                       int64_t K, int64_t kchunk,
@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
                                                       float* __restrict__ C, int64_t ldc,
                                                       float* __restrict__ rowsum, int64_t m,
                                                       int64_t row0) {
-  using Tile = NNTile<TN, EXP, WM>;
+  using Tile = NNTile<TN, EXP, WM, TM>;
   __shared__ __attribute__((aligned(16))) float smem[Tile::kSmemFloats];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
@@ -38,8 +38,8 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
   float scale = 0.f;
   if (EXP) scale = -st->inv_h * kLog2e;
   Tile tile;
-  tile.run(A + (i0 >> 7) * (a_npad >> 4) * kPanelElems, B + c0, ldb, k0, k1, scale, smem,
-           row0 + i0);
+  tile.run(A + (i0 >> 7) * (a_npad >> 4) * kPanelElems + (i0 & 127) * 16, B + c0, ldb, k0, k1,
+           scale, smem, row0 + i0);
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
   const int64_t r0 = i0 + wr * 32 * Tile::TM;
@@ -207,24 +207,31 @@ __global__ __launch_bounds__(256) void phi_row_kernel(float* __restrict__ X, int
   }
 }
 
-// NN block shape: 1 or 2 waves per SIMD (DSVGD_NN_WAVES=1|2 overrides, for A/B runs)
-static int nn_waves_per_simd() {
-  const char* e = getenv("DSVGD_NN_WAVES");
-  return (e && e[0] == '1') ? 1 : 2;
+// NN block shape (DSVGD_NN_SHAPE overrides, for in-process A/B runs):
+//   "w1"  128 rows, 4 waves x 256 AGPRs        (1 block/CU, 1 wave/SIMD)
+//   "w2"  128 rows, 8 waves x 128 accumulators (1 block/CU, 2 waves/SIMD)
+//   "b64"  64 rows, 4 waves x 128 accumulators (2 blocks/CU)
+enum NNShape { kW1, kW2, kB64 };
+static NNShape nn_shape() {
+  const char* e = getenv("DSVGD_NN_SHAPE");
+  if (e && e[0] == 'w' && e[1] == '1') return kW1;
+  if (e && e[0] == 'b') return kB64;
+  return kW2;
 }
 
-template <int TN, int WM>
-int launch_nn_wm(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
-                 const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-                 int64_t cols, int64_t row0, hipStream_t s) {
+template <int TN, int WM, int TM>
+int launch_nn_shape(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
+                    const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
+                    int64_t cols, int64_t row0, hipStream_t s) {
+  constexpr int BM = 32 * TM * WM;
   const int64_t kchunk = roundup((K + splits - 1) / splits, 16);
-  const dim3 grid(cols / (128 * TN), roundup(m, 128) / 128, splits);
+  const dim3 grid(cols / (128 * TN), roundup(m, BM) / BM, splits);
   if (exp_)
-    hipLaunchKernelGGL((nn_kernel<TN, true, WM>), grid, dim3(256 * WM), 0, s, A, K, B, ldb, K,
-                       kchunk, st, C, ldc, rowsum, m, row0);
+    hipLaunchKernelGGL((nn_kernel<TN, true, WM, TM>), grid, dim3(256 * WM), 0, s, A, K, B, ldb,
+                       K, kchunk, st, C, ldc, rowsum, m, row0);
   else
-    hipLaunchKernelGGL((nn_kernel<TN, false, WM>), grid, dim3(256 * WM), 0, s, A, K, B, ldb, K,
-                       kchunk, st, C, ldc, rowsum, m, row0);
+    hipLaunchKernelGGL((nn_kernel<TN, false, WM, TM>), grid, dim3(256 * WM), 0, s, A, K, B, ldb,
+                       K, kchunk, st, C, ldc, rowsum, m, row0);
   return check_launch("nn_kernel");
 }
 
@@ -232,9 +239,17 @@ template <int TN>
 int launch_nn(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
               const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
               int64_t cols, int64_t row0, hipStream_t s) {
-  if (nn_waves_per_simd() == 2)
-    return launch_nn_wm<TN, 2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s);
-  return launch_nn_wm<TN, 1>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s);
+  switch (nn_shape()) {
+    case kW1:
+      return launch_nn_shape<TN, 1, 4>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols,
+                                       row0, s);
+    case kB64:
+      return launch_nn_shape<TN, 1, 2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols,
+                                       row0, s);
+    default:
+      return launch_nn_shape<TN, 2, 2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols,
+                                       row0, s);
+  }
 }
 
 // C[splits x m x cols] = f(A) B with A in panel layout (m_pad x K), B row-major K x cols.

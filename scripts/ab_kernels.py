@@ -4,7 +4,7 @@
     python scripts/ab_kernels.py [--n 65536 --d 256 --rounds 5]
 
 Variants are switched through environment variables the launchers read on
-every call (DSVGD_NN_WAVES=1|2 for the NN MFMA engine).
+every call (DSVGD_NN_SHAPE=w1|w2|b64 for the NN MFMA engine).
 """
 import argparse
 import json
@@ -45,7 +45,8 @@ def main():
     eng.pack(X, S)
     eng.distances(median=True)
     eng.median_bandwidth()
-    variants = {"nn_waves=1": {"DSVGD_NN_WAVES": "1"}, "nn_waves=2": {"DSVGD_NN_WAVES": "2"}}
+    variants = {"nn=w1": {"DSVGD_NN_SHAPE": "w1"}, "nn=w2": {"DSVGD_NN_SHAPE": "w2"},
+                "nn=b64": {"DSVGD_NN_SHAPE": "b64"}}
     res = {k: [] for k in variants}
     ref = None
     for _ in range(args.rounds):
