@@ -137,7 +137,12 @@ struct NTTile {
 //   waves per SIMD in one block), WM=1 TM=2 (64 rows, two blocks per CU: one
 //   block's barrier wait hides under the other block's MFMAs).
 // K-step = one 16-column panel slice of A (BM rows) and 16 rows of B.
-template <int TN, bool EXP, int WM = 1, int TM_ = 4 / WM>
+//
+// BT (transposed B image): the B tile is stored column-major [BC][BJ+4] so a
+// lane's 4 k-values of one column are one ds_read_b128 (8 per K-step instead
+// of 16 ds_read2_b32); each thread loads 4x4 blocks (4 rows x float4) and
+// writes their columns as float4s.
+template <int TN, bool EXP, int WM = 1, int TM_ = 4 / WM, bool BT = false>
 struct NNTile {
   static constexpr int kThreads = 256 * WM;
   static constexpr int TM = TM_;
@@ -145,12 +150,14 @@ struct NNTile {
   static constexpr int BC = 128 * TN;
   static constexpr int BJ = 16;
   static constexpr int LDA = BJ + 4;  // 80-B rows: conflict-free ds_read_b128
+  static constexpr int LDBT = BJ + 4;
   static constexpr int SA = BM * LDA;
-  static constexpr int SB = BJ * BC;
+  static constexpr int SB = BT ? BC * LDBT : BJ * BC;
   static constexpr int kStage = SA + SB;
   static constexpr int kSmemFloats = 2 * kStage;
   static constexpr int LA = BM * BJ / 4 / kThreads;
-  static constexpr int LB = BJ * BC / 4 / kThreads;
+  static constexpr int NB4 = BC;  // 4x4 blocks of a BJ x BC tile (BT)
+  static constexpr int LB = BT ? 4 * ((NB4 + kThreads - 1) / kThreads) : BJ * BC / 4 / kThreads;
   static_assert(LA >= 1 && LB >= 1, "tile too small for the block");
   static_assert(BM == 64 || BM == 128, "BM must divide the 128-row panel");
 
@@ -164,10 +171,23 @@ struct NNTile {
     const float* ap = Apanels + (j0 >> 4) * kPanelElems;  // contiguous 8 KiB panel
 #pragma unroll
     for (int u = 0; u < LA; ++u) ra[u] = *reinterpret_cast<const f32x4*>(ap + 4 * (t + u * kThreads));
+    if (BT) {
 #pragma unroll
-    for (int u = 0; u < LB; ++u) {
-      const int f = t + u * kThreads, row = f / (BC / 4), c4 = f % (BC / 4);
-      rb[u] = *reinterpret_cast<const f32x4*>(B + (j0 + row) * ldb + 4 * c4);
+      for (int u = 0; u < LB / 4; ++u) {
+        const int blk = t + u * kThreads;  // 4x4 block: rows 4*rg.., cols 4*cg..
+        if (blk < NB4) {
+          const int rg = blk / (BC / 4), cg = blk % (BC / 4);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            rb[4 * u + i] = *reinterpret_cast<const f32x4*>(B + (j0 + 4 * rg + i) * ldb + 4 * cg);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < LB; ++u) {
+        const int f = t + u * kThreads, row = f / (BC / 4), c4 = f % (BC / 4);
+        rb[u] = *reinterpret_cast<const f32x4*>(B + (j0 + row) * ldb + 4 * c4);
+      }
     }
   }
 
@@ -180,8 +200,22 @@ struct NNTile {
       const int f = t + u * kThreads, row = f >> 2, c4 = f & 3;
       *reinterpret_cast<f32x4*>(sA + row * LDA + 4 * c4) = ra[u];
     }
+    if (BT) {
 #pragma unroll
-    for (int u = 0; u < LB; ++u) *reinterpret_cast<f32x4*>(sB + 4 * (t + u * kThreads)) = rb[u];
+      for (int u = 0; u < LB / 4; ++u) {
+        const int blk = t + u * kThreads;
+        if (blk < NB4) {
+          const int rg = blk / (BC / 4), cg = blk % (BC / 4);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            *reinterpret_cast<f32x4*>(sB + (4 * cg + i) * LDBT + 4 * rg) =
+                f32x4{rb[4 * u][i], rb[4 * u + 1][i], rb[4 * u + 2][i], rb[4 * u + 3][i]};
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < LB; ++u) *reinterpret_cast<f32x4*>(sB + 4 * (t + u * kThreads)) = rb[u];
+    }
   }
 
   // dgl = (global row of this block's row 0) - (global column of this K-step's
@@ -207,16 +241,31 @@ struct NNTile {
           rsum[mi] += (a[mi][0] + a[mi][1]) + (a[mi][2] + a[mi][3]);
         }
       }
+      if (BT) {
+        f32x4 b4[TN];
 #pragma unroll
-      for (int t4 = 0; t4 < 4; ++t4) {
-        float b[TN];
-        const float* brow = sB + (8 * g + 4 * h + t4) * BC + wc * 32 * TN + r;
+        for (int ni = 0; ni < TN; ++ni)
+          b4[ni] = *reinterpret_cast<const f32x4*>(sB + (wc * 32 * TN + ni * 32 + r) * LDBT +
+                                                   8 * g + 4 * h);
 #pragma unroll
-        for (int ni = 0; ni < TN; ++ni) b[ni] = brow[ni * 32];
+        for (int t4 = 0; t4 < 4; ++t4)
 #pragma unroll
-        for (int mi = 0; mi < TM; ++mi)
+          for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = mfma32(a[mi][t4], b[ni], acc[mi][ni]);
+            for (int ni = 0; ni < TN; ++ni)
+              acc[mi][ni] = mfma32(a[mi][t4], b4[ni][t4], acc[mi][ni]);
+      } else {
+#pragma unroll
+        for (int t4 = 0; t4 < 4; ++t4) {
+          float b[TN];
+          const float* brow = sB + (8 * g + 4 * h + t4) * BC + wc * 32 * TN + r;
+#pragma unroll
+          for (int ni = 0; ni < TN; ++ni) b[ni] = brow[ni * 32];
+#pragma unroll
+          for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = mfma32(a[mi][t4], b[ni], acc[mi][ni]);
+        }
       }
     }
   }

@@ -19,7 +19,7 @@ namespace dsvgd {
 // in order (deterministic, no atomics).
 // row0: interacting-set index of A's row 0 (EXP: the diagonal j == row0 + i
 // is skipped, see NNTile::compute).
-template <int TN, bool EXP, int WM, int TM>
+template <int TN, bool EXP, int WM, int TM, bool BT>
 __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ A, int64_t a_npad,
                                                       const float* __restrict__ B, int64_t ldb,
                                                       int64_t K, int64_t kchunk,
@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
                                                       float* __restrict__ C, int64_t ldc,
                                                       float* __restrict__ rowsum, int64_t m,
                                                       int64_t row0) {
-  using Tile = NNTile<TN, EXP, WM, TM>;
+  using Tile = NNTile<TN, EXP, WM, TM, BT>;
   __shared__ __attribute__((aligned(16))) float smem[Tile::kSmemFloats];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
@@ -64,13 +64,16 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
   }
 }
 
-// phi[i][c] = inv_n (KS[i][c] + (2/h)(r_i xc[i][c] - KX[i][c])); X[i][c] += step phi.
-// KY / rowsum hold `splits` split-K partials, summed here in slice order.
+// phi[i][c] = inv_n (KS[i][c] + (2/h)(r_i xc[i][c] - KX[i][c])) [+ extra[i][c]];
+// X[i][c] += step phi.  KY / rowsum hold `splits` split-K partials, summed
+// here in slice order.  extra (nullable): the h * W2-gradient rows, added to
+// phi before the step as in distsampler.py:196-200.
 __global__ __launch_bounds__(256) void phi_finish_kernel(
     const float* __restrict__ KY, int64_t ldk, const float* __restrict__ rowsum, int splits,
     const float* __restrict__ Y, int64_t ldy, int64_t row0, int64_t m, int64_t d, int64_t dp,
-    const dsvgd_select_state* __restrict__ st, float inv_n, float step, float* __restrict__ phi,
-    int64_t ldphi, float* __restrict__ X, int64_t ldx) {
+    const dsvgd_select_state* __restrict__ st, float inv_n, float step,
+    const float* __restrict__ extra, int64_t lde, float* __restrict__ phi, int64_t ldphi,
+    float* __restrict__ X, int64_t ldx) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= m * d) return;
   const int64_t i = t / d, c = t % d;
@@ -85,7 +88,8 @@ __global__ __launch_bounds__(256) void phi_finish_kernel(
   }
   const float* yi = Y + (row0 + i) * ldy;
   // + the self term k_ii (s_i + 2/h (x_i - x_i)) = s_i, excluded from phi_mm
-  const float p = inv_n * ((yi[dp + c] + ks) + two_inv_h * (r * yi[c] - kx));
+  float p = inv_n * ((yi[dp + c] + ks) + two_inv_h * (r * yi[c] - kx));
+  if (extra) p += extra[i * lde + c];
   if (phi) phi[i * ldphi + c] = p;
   if (X) X[i * ldx + c] += step * p;
 }
@@ -101,8 +105,9 @@ constexpr int kPhiDirectMaxD = 64;
 __global__ __launch_bounds__(256) void phi_direct_kernel(
     const float* __restrict__ D, int64_t n_pad, const float* __restrict__ Y, int64_t ldy,
     int64_t row0, int64_t m, int64_t n, int d, int64_t dp,
-    const dsvgd_select_state* __restrict__ st, float inv_n, float step, float* __restrict__ phi,
-    int64_t ldphi, float* __restrict__ X, int64_t ldx) {
+    const dsvgd_select_state* __restrict__ st, float inv_n, float step,
+    const float* __restrict__ extra, int64_t lde, float* __restrict__ phi, int64_t ldphi,
+    float* __restrict__ X, int64_t ldx) {
   __shared__ __attribute__((aligned(16))) float kT[64][64];
   __shared__ __attribute__((aligned(16))) float xs[64][64];
   __shared__ __attribute__((aligned(16))) float ss[64][64];
@@ -149,7 +154,8 @@ __global__ __launch_bounds__(256) void phi_direct_kernel(
       const int64_t i = i0 + 4 * rq + a;
       const int col = 4 * cq + c;
       if (i < m && col < d) {
-        const float p = inv_n * acc[a][c];
+        float p = inv_n * acc[a][c];
+        if (extra) p += extra[i * lde + col];
         if (phi) phi[i * ldphi + col] = p;
         if (X) X[i * ldx + col] += step * p;
       }
@@ -162,7 +168,9 @@ __global__ __launch_bounds__(256) void phi_row_kernel(float* __restrict__ X, int
                                                       const float* __restrict__ S, int64_t lds,
                                                       int64_t n, int64_t d, int64_t i,
                                                       const dsvgd_select_state* __restrict__ st,
-                                                      float step, float* __restrict__ phi_out) {
+                                                      float step,
+                                                      const float* __restrict__ extra,
+                                                      float* __restrict__ phi_out) {
   extern __shared__ __attribute__((aligned(16))) float dyn[];
   float* xi = dyn;            // d
   float* acc = dyn + d;       // d
@@ -201,7 +209,8 @@ __global__ __launch_bounds__(256) void phi_row_kernel(float* __restrict__ X, int
   }
   const float inv_n = 1.f / (float)n;
   for (int64_t c = t; c < d; c += 256) {
-    const float p = inv_n * acc[c];
+    float p = inv_n * acc[c];
+    if (extra) p += extra[c];
     if (phi_out) phi_out[c] = p;
     X[i * ldx + c] = xi[c] + step * p;
   }
@@ -211,15 +220,17 @@ __global__ __launch_bounds__(256) void phi_row_kernel(float* __restrict__ X, int
 //   "w1"  128 rows, 4 waves x 256 AGPRs        (1 block/CU, 1 wave/SIMD)
 //   "w2"  128 rows, 8 waves x 128 accumulators (1 block/CU, 2 waves/SIMD)
 //   "b64"  64 rows, 4 waves x 128 accumulators (2 blocks/CU)
-enum NNShape { kW1, kW2, kB64 };
+//   "w2t"  as w2 with the transposed B image (b128 B-fragment reads)
+enum NNShape { kW1, kW2, kB64, kW2T };
 static NNShape nn_shape() {
   const char* e = getenv("DSVGD_NN_SHAPE");
   if (e && e[0] == 'w' && e[1] == '1') return kW1;
   if (e && e[0] == 'b') return kB64;
+  if (e && e[0] == 'w' && e[1] == '2' && e[2] == 't') return kW2T;
   return kW2;
 }
 
-template <int TN, int WM, int TM>
+template <int TN, int WM, int TM, bool BT = false>
 int launch_nn_shape(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
                     const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
                     int64_t cols, int64_t row0, hipStream_t s) {
@@ -227,11 +238,11 @@ int launch_nn_shape(bool exp_, const float* A, const float* B, int64_t ldb, int6
   const int64_t kchunk = roundup((K + splits - 1) / splits, 16);
   const dim3 grid(cols / (128 * TN), roundup(m, BM) / BM, splits);
   if (exp_)
-    hipLaunchKernelGGL((nn_kernel<TN, true, WM, TM>), grid, dim3(256 * WM), 0, s, A, K, B, ldb,
-                       K, kchunk, st, C, ldc, rowsum, m, row0);
+    hipLaunchKernelGGL((nn_kernel<TN, true, WM, TM, BT>), grid, dim3(256 * WM), 0, s, A, K, B,
+                       ldb, K, kchunk, st, C, ldc, rowsum, m, row0);
   else
-    hipLaunchKernelGGL((nn_kernel<TN, false, WM, TM>), grid, dim3(256 * WM), 0, s, A, K, B, ldb,
-                       K, kchunk, st, C, ldc, rowsum, m, row0);
+    hipLaunchKernelGGL((nn_kernel<TN, false, WM, TM, BT>), grid, dim3(256 * WM), 0, s, A, K, B,
+                       ldb, K, kchunk, st, C, ldc, rowsum, m, row0);
   return check_launch("nn_kernel");
 }
 
@@ -246,6 +257,9 @@ int launch_nn(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K,
     case kB64:
       return launch_nn_shape<TN, 1, 2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols,
                                        row0, s);
+    case kW2T:
+      return launch_nn_shape<TN, 2, 2, true>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m,
+                                             cols, row0, s);
     default:
       return launch_nn_shape<TN, 2, 2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols,
                                        row0, s);
@@ -308,24 +322,27 @@ int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64
 
 int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t splits,
                      const float* Y, int64_t ldy, int64_t row0, int64_t m, int64_t d, int64_t dp,
-                     const dsvgd_select_state* st, float inv_n, float step, float* phi,
-                     int64_t ldphi, float* X, int64_t ldx, void* stream) {
+                     const dsvgd_select_state* st, float inv_n, float step, const float* extra,
+                     int64_t lde, float* phi, int64_t ldphi, float* X, int64_t ldx,
+                     void* stream) {
   DSVGD_REQUIRE(KY && rowsum && Y && st, "null pointer");
+  DSVGD_REQUIRE(!extra || lde >= d, "lde");
   DSVGD_REQUIRE(splits >= 1 && splits <= 1024, "splits must be in [1, 1024]");
   DSVGD_REQUIRE(m > 0 && d > 0 && dp >= d && ldk >= 2 * dp && ldy >= 2 * dp, "sizes");
   DSVGD_REQUIRE(!phi || ldphi >= d, "ldphi");
   DSVGD_REQUIRE(!X || ldx >= d, "ldx");
   hipLaunchKernelGGL(phi_finish_kernel, dim3((m * d + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, KY, ldk, rowsum, (int)splits, Y, ldy, row0, m, d, dp,
-                     st, inv_n,
-                     step, phi, ldphi, X, ldx);
+                     st, inv_n, step, extra, lde, phi, ldphi, X, ldx);
   return check_launch("phi_finish");
 }
 
 int dsvgd_phi_direct(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t row0,
                      int64_t m, int64_t n, int64_t d, const dsvgd_select_state* st, float inv_n,
-                     float step, float* phi, int64_t ldphi, float* X, int64_t ldx, void* stream) {
+                     float step, const float* extra, int64_t lde, float* phi, int64_t ldphi,
+                     float* X, int64_t ldx, void* stream) {
   DSVGD_REQUIRE(D && Y && st, "null pointer");
+  DSVGD_REQUIRE(!extra || lde >= d, "lde");
   DSVGD_REQUIRE(m > 0 && n > 0 && d > 0 && row0 >= 0, "sizes");
   DSVGD_REQUIRE(d <= kPhiDirectMaxD, "phi_direct supports d <= 64");
   const int64_t n_pad = roundup(n, 128), dp = roundup(d, 32);
@@ -334,19 +351,20 @@ int dsvgd_phi_direct(const float* D, int64_t ldd, const float* Y, int64_t ldy, i
   DSVGD_REQUIRE(!phi || ldphi >= d, "ldphi");
   DSVGD_REQUIRE(!X || ldx >= d, "ldx");
   hipLaunchKernelGGL(phi_direct_kernel, dim3((m + 63) / 64), dim3(256), 0, (hipStream_t)stream, D,
-                     n_pad, Y, ldy, row0, m, n, (int)d, dp, st, inv_n, step, phi, ldphi, X, ldx);
+                     n_pad, Y, ldy, row0, m, n, (int)d, dp, st, inv_n, step, extra, lde, phi, ldphi, X,
+                     ldx);
   return check_launch("phi_direct");
 }
 
 int dsvgd_phi_row(float* X, int64_t ldx, const float* S, int64_t lds, int64_t n_int, int64_t d,
-                  int64_t i, const dsvgd_select_state* st, float step, float* phi_out,
-                  void* stream) {
+                  int64_t i, const dsvgd_select_state* st, float step, const float* extra,
+                  float* phi_out, void* stream) {
   DSVGD_REQUIRE(X && S && st, "null pointer");
   DSVGD_REQUIRE(n_int > 0 && d > 0 && i >= 0 && i < n_int && ldx >= d && lds >= d, "sizes");
   DSVGD_REQUIRE(d <= 8064, "phi_row supports d <= 8064 (64 KiB LDS)");
   const size_t shm = (size_t)(2 * d + 256) * sizeof(float);
   hipLaunchKernelGGL(phi_row_kernel, dim3(1), dim3(256), shm, (hipStream_t)stream, X, ldx, S, lds,
-                     n_int, d, i, st, step, phi_out);
+                     n_int, d, i, st, step, extra, phi_out);
   return check_launch("phi_row");
 }
 

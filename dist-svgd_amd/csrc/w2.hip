@@ -1,0 +1,334 @@
+// w2.hip -- the W2 / JKO term of DistSampler.make_step
+// (reference dsvgd/distsampler.py:103-129, applied at :190-198).
+//
+// The reference solves  min <P, C>  s.t.  P >= 0, P 1 = 1/m, P^T 1 = 1/n  with
+// C_ij = ||x_i - y_j||^2 (x: the m owned particles, y: the n previous ones)
+// by scipy linprog and returns  sum_j P_ij (x_i - y_j).  In every DistSampler
+// mode n = R m (R = 1 for partitions, R = num_shards when particles are
+// exchanged), and after scaling by n the supplies are R and the demands 1, so
+// the LP's vertices are integral: the optimum is an assignment of n "slots"
+// (slot s belongs to row s / R) to the n columns, each carrying mass 1/n.
+//
+// Solver: forward auction (Bertsekas) with epsilon scaling, Jacobi bidding.
+//   * one wave per unassigned slot scans its cost row: best / second-best of
+//     -C_sj - p_j (prices in fp64), bids  p_j + (v1 - v2 + eps)  on the best;
+//   * bids are resolved with one 64-bit atomicMax per bid, key =
+//     (fp32 increment rounded down) << 32 | slot, so a round's outcome does
+//     not depend on scheduling (ties go to the higher slot id);
+//   * a one-thread control kernel ends a phase when every slot is assigned,
+//     divides eps by kTheta and starts the next phase by bumping an epoch
+//     counter (assignments of older epochs read as unassigned -- no reset
+//     pass over n); prices carry over between phases.
+// With eps_final = cmax * 2^-24 / n the final assignment is within cmax *
+// 2^-24 (one fp32 ulp of the largest cost) of the optimum.  The host wrapper
+// enqueues rounds in batches and polls the control block between batches.
+#include <float.h>
+
+#include <algorithm>
+
+#include "common.hpp"
+
+namespace dsvgd {
+
+struct W2Ctl {
+  double eps, eps_final;
+  float cmax;
+  int32_t epoch;
+  int32_t done;  // 0 running, 1 converged, 2 degenerate (all costs 0), 3 bad input
+  int32_t pad_;
+  unsigned long long unassigned;
+  long long rounds, phases;
+};
+
+constexpr size_t kW2CtlBytes = 256;
+constexpr double kTheta = 8.0;
+constexpr int kRoundBatch = 16;
+
+struct W2Ws {
+  W2Ctl* ctl;
+  double* price;
+  unsigned long long* bid;
+  int32_t *owner, *owner_ep, *assigned, *assigned_ep;
+  W2Ws(void* ws, int64_t n) {
+    char* p = (char*)ws;
+    ctl = (W2Ctl*)p;
+    price = (double*)(p + kW2CtlBytes);
+    bid = (unsigned long long*)(price + n);
+    owner = (int32_t*)(bid + n);
+    owner_ep = owner + n;
+    assigned = owner_ep + n;
+    assigned_ep = assigned + n;
+  }
+};
+
+// C[i][j] = ||x_i - y_j||^2 from explicit fp32 differences (the reference's
+// diffs / norm, distsampler.py:107-114).  64 x 64 tile per block, each thread
+// 4 x 4; 32-dim chunks of both operands transposed into LDS ([k][row]) so a
+// thread's 4 rows / 4 columns are one ds_read_b128 each.
+__global__ __launch_bounds__(256) void w2_cost_kernel(const float* __restrict__ X, int64_t ldx,
+                                                      int64_t m, const float* __restrict__ Y,
+                                                      int64_t ldy, int64_t n, int64_t d,
+                                                      float* __restrict__ C, int64_t ldc) {
+  __shared__ __attribute__((aligned(16))) float xs[32][68];
+  __shared__ __attribute__((aligned(16))) float ys[32][68];
+  const int t = threadIdx.x, rq = t >> 4, cq = t & 15;
+  const int64_t i0 = (int64_t)blockIdx.y * 64, j0 = (int64_t)blockIdx.x * 64;
+  float acc[4][4] = {};
+  for (int64_t k0 = 0; k0 < d; k0 += 32) {
+    for (int e = t; e < 64 * 32; e += 256) {
+      const int r = e >> 5, k = e & 31;
+      const int64_t i = i0 + r, j = j0 + r, kk = k0 + k;
+      xs[k][r] = (i < m && kk < d) ? X[i * ldx + kk] : 0.f;
+      ys[k][r] = (j < n && kk < d) ? Y[j * ldy + kk] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int k = 0; k < 32; ++k) {
+      const f32x4 x4 = *reinterpret_cast<const f32x4*>(&xs[k][4 * rq]);
+      const f32x4 y4 = *reinterpret_cast<const f32x4*>(&ys[k][4 * cq]);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const float df = x4[a] - y4[b];
+          acc[a][b] = fmaf(df, df, acc[a][b]);
+        }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int64_t i = i0 + 4 * rq + a;
+    if (i >= m) continue;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int64_t j = j0 + 4 * cq + b;
+      if (j < n) C[i * ldc + j] = acc[a][b];
+    }
+  }
+}
+
+// cmax = max C (C >= 0: the fp32 bit patterns order like the values); any
+// non-finite cost marks the control block invalid.
+__global__ __launch_bounds__(256) void w2_cmax_kernel(const float* __restrict__ C, int64_t ldc,
+                                                      int64_t m, int64_t n, W2Ctl* ctl) {
+  uint32_t mx = 0;
+  bool bad = false;
+  const int64_t total = m * n;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * 256) {
+    const float v = C[(e / n) * ldc + e % n];
+    bad |= !(v >= 0.f && v <= FLT_MAX);
+    mx = max(mx, __float_as_uint(v));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax((unsigned int*)&ctl->cmax, mx);
+  if (bad) atomicExch(&ctl->done, 3);
+}
+
+__global__ void w2_start_kernel(W2Ctl* ctl, int64_t n) {
+  const double cmax = (double)ctl->cmax;
+  ctl->eps_final = fmax(cmax * 0x1p-24 / (double)n, cmax * 1e-13);
+  ctl->eps = fmax(cmax / kTheta, ctl->eps_final);
+  ctl->epoch = 1;
+  ctl->unassigned = (unsigned long long)n;
+  ctl->rounds = 0;
+  ctl->phases = 1;
+  if (ctl->done == 0 && !(cmax > 0.0)) ctl->done = 2;
+}
+
+// One wave per slot; only slots unassigned in the current epoch bid.
+__global__ __launch_bounds__(256) void w2_bid_kernel(const float* __restrict__ C, int64_t ldc,
+                                                     int64_t n, int64_t R, W2Ws w) {
+  const W2Ctl* ctl = w.ctl;
+  if (ctl->done) return;
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (s >= n) return;
+  const int ep = ctl->epoch;
+  if (w.assigned_ep[s] == ep && w.assigned[s] >= 0) return;
+  const float* row = C + (s / R) * ldc;
+  double v1 = -DBL_MAX, v2 = -DBL_MAX;
+  int j1 = INT32_MAX;
+  for (int64_t j = lane; j < n; j += 64) {
+    const double v = -(double)row[j] - w.price[j];
+    if (v > v1) {
+      v2 = v1;
+      v1 = v;
+      j1 = (int)j;
+    } else if (v > v2) {
+      v2 = v;
+    }
+  }
+  // wave top-2 (ties in v1 resolved to the lower column; then v2 == v1)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov1 = __shfl_xor(v1, o, 64), ov2 = __shfl_xor(v2, o, 64);
+    const int oj1 = __shfl_xor(j1, o, 64);
+    if (ov1 > v1 || (ov1 == v1 && oj1 < j1)) {
+      v2 = fmax(v1, ov2);
+      v1 = ov1;
+      j1 = oj1;
+    } else {
+      v2 = fmax(v2, ov1);
+    }
+  }
+  if (lane == 0) {
+    const double eps = ctl->eps;
+    const double inc = (n > 1 ? v1 - v2 : 0.0) + eps;
+    float f = (float)inc;
+    if ((double)f > inc) f = nextafterf(f, 0.f);  // round down: keeps eps-CS
+    if (!(f > 0.f)) f = FLT_MIN;
+    const unsigned long long key =
+        ((unsigned long long)__float_as_uint(f) << 32) | (unsigned long long)(uint32_t)s;
+    atomicMax(&w.bid[j1], key);
+  }
+}
+
+// One thread per column: award the column to its highest bidder.
+__global__ __launch_bounds__(256) void w2_resolve_kernel(int64_t n, W2Ws w) {
+  W2Ctl* ctl = w.ctl;
+  if (ctl->done) return;
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  unsigned long long gained = 0;
+  if (j < n) {
+    const unsigned long long b = w.bid[j];
+    if (b) {
+      w.bid[j] = 0;
+      const int s = (int)(uint32_t)b;
+      const float inc = __uint_as_float((uint32_t)(b >> 32));
+      const int ep = ctl->epoch;
+      w.price[j] += (double)inc;
+      const int old = (w.owner_ep[j] == ep) ? w.owner[j] : -1;
+      if (old >= 0)
+        w.assigned[old] = -1;  // displaced: bids again next round
+      else
+        gained = 1;
+      w.owner[j] = s;
+      w.owner_ep[j] = ep;
+      w.assigned[s] = (int)j;
+      w.assigned_ep[s] = ep;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) gained += __shfl_xor(gained, o, 64);
+  if ((threadIdx.x & 63) == 0 && gained) atomicAdd(&ctl->unassigned, (unsigned long long)(-(long long)gained));
+}
+
+__global__ void w2_control_kernel(W2Ctl* ctl, int64_t n) {
+  if (ctl->done) return;
+  ctl->rounds += 1;
+  if (ctl->unassigned != 0) return;
+  if (ctl->eps <= ctl->eps_final) {
+    ctl->done = 1;
+    return;
+  }
+  ctl->eps = fmax(ctl->eps / kTheta, ctl->eps_final);
+  ctl->epoch += 1;
+  ctl->phases += 1;
+  ctl->unassigned = (unsigned long long)n;
+}
+
+__global__ __launch_bounds__(256) void w2_emit_kernel(int64_t n, W2Ws w, int32_t* assign) {
+  const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (s >= n) return;
+  assign[s] = (w.ctl->done == 2) ? (int32_t)s : w.assigned[s];
+}
+
+// G[i][c] = h/n * sum_{r<R} (x_i - y_{assign[iR+r]})[c]   (distsampler.py:128
+// times the JKO step h of :198)
+__global__ __launch_bounds__(256) void w2_grad_kernel(const float* __restrict__ X, int64_t ldx,
+                                                      int64_t m, const float* __restrict__ Y,
+                                                      int64_t ldy, int64_t n, int64_t d,
+                                                      const int32_t* __restrict__ assign,
+                                                      float h, float* __restrict__ G,
+                                                      int64_t ldg) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= m * d) return;
+  const int64_t i = t / d, c = t % d, R = n / m;
+  const float x = X[i * ldx + c];
+  float acc = 0.f;
+  for (int64_t r = 0; r < R; ++r) acc += x - Y[(int64_t)assign[i * R + r] * ldy + c];
+  G[i * ldg + c] = h * (acc / (float)n);
+}
+
+}  // namespace dsvgd
+
+using namespace dsvgd;
+
+extern "C" {
+
+size_t dsvgd_w2_workspace_bytes(int64_t m, int64_t n) {
+  (void)m;
+  return kW2CtlBytes + (size_t)n * (sizeof(double) + sizeof(unsigned long long) + 4 * sizeof(int32_t));
+}
+
+int dsvgd_w2_cost(const float* X, int64_t ldx, int64_t m, const float* Y, int64_t ldy, int64_t n,
+                  int64_t d, float* C, int64_t ldc, void* stream) {
+  DSVGD_REQUIRE(X && Y && C, "null pointer");
+  DSVGD_REQUIRE(m > 0 && n > 0 && d > 0 && ldx >= d && ldy >= d && ldc >= n, "sizes");
+  DSVGD_REQUIRE((n + 63) / 64 <= INT32_MAX && (m + 63) / 64 <= 65535, "grid too large");
+  hipLaunchKernelGGL(w2_cost_kernel, dim3((n + 63) / 64, (m + 63) / 64), dim3(256), 0,
+                     (hipStream_t)stream, X, ldx, m, Y, ldy, n, d, C, ldc);
+  return check_launch("w2_cost");
+}
+
+int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
+                    int64_t max_rounds, int32_t* assign, int64_t* rounds_out, void* stream) {
+  DSVGD_REQUIRE(C && ws && assign, "null pointer");
+  DSVGD_REQUIRE(m > 0 && n > 0 && ldc >= n, "sizes");
+  DSVGD_REQUIRE(n % m == 0, "n must be a multiple of m (n = R m slots)");
+  DSVGD_REQUIRE(n <= INT32_MAX - 1, "n too large for 32-bit slot ids");
+  DSVGD_REQUIRE(max_rounds > 0, "max_rounds");
+  hipStream_t s = (hipStream_t)stream;
+  W2Ws w(ws, n);
+  const int64_t R = n / m;
+  if (hipMemsetAsync(ws, 0, dsvgd_w2_workspace_bytes(m, n), s) != hipSuccess)
+    return check_launch("w2 workspace memset");
+  const int64_t total = m * n;
+  const int cblocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
+  hipLaunchKernelGGL(w2_cmax_kernel, dim3(cblocks), dim3(256), 0, s, C, ldc, m, n, w.ctl);
+  hipLaunchKernelGGL(w2_start_kernel, dim3(1), dim3(1), 0, s, w.ctl, n);
+  int rc = check_launch("w2_start");
+  if (rc) return rc;
+  const dim3 gb((unsigned)((n + 3) / 4)), gr((unsigned)((n + 255) / 256));
+  W2Ctl h{};
+  for (int64_t launched = 0;;) {
+    for (int b = 0; b < kRoundBatch; ++b) {
+      hipLaunchKernelGGL(w2_bid_kernel, gb, dim3(256), 0, s, C, ldc, n, R, w);
+      hipLaunchKernelGGL(w2_resolve_kernel, gr, dim3(256), 0, s, n, w);
+      hipLaunchKernelGGL(w2_control_kernel, dim3(1), dim3(1), 0, s, w.ctl, n);
+    }
+    launched += kRoundBatch;
+    if ((rc = check_launch("w2 auction round"))) return rc;
+    if (hipMemcpyAsync(&h, w.ctl, sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return check_launch("w2 control readback");
+    if (h.done) break;
+    if (launched >= max_rounds) {
+      set_error("dsvgd_w2_assign: no convergence after %lld rounds (%lld phases, %llu unassigned)",
+                (long long)launched, (long long)h.phases, (unsigned long long)h.unassigned);
+      return -3;
+    }
+  }
+  if (h.done == 3) {
+    set_error("dsvgd_w2_assign: non-finite or negative cost");
+    return -2;
+  }
+  if (rounds_out) *rounds_out = h.rounds;
+  hipLaunchKernelGGL(w2_emit_kernel, gr, dim3(256), 0, s, n, w, assign);
+  return check_launch("w2_emit");
+}
+
+int dsvgd_w2_grad(const float* X, int64_t ldx, int64_t m, const float* Y, int64_t ldy, int64_t n,
+                  int64_t d, const int32_t* assign, float h, float* G, int64_t ldg, void* stream) {
+  DSVGD_REQUIRE(X && Y && assign && G, "null pointer");
+  DSVGD_REQUIRE(m > 0 && n > 0 && d > 0 && ldx >= d && ldy >= d && ldg >= d, "sizes");
+  DSVGD_REQUIRE(n % m == 0, "n must be a multiple of m");
+  hipLaunchKernelGGL(w2_grad_kernel, dim3((unsigned)((m * d + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, X, ldx, m, Y, ldy, n, d, assign, h, G, ldg);
+  return check_launch("w2_grad");
+}
+
+}  // extern "C"

@@ -22,10 +22,14 @@ a CPU tensor is copied to the GPU and mirrored back after every make_step.
 
 Extensions (keyword-only): order="sequential" (reference in-place
 Gauss-Seidel over the owned rows) | "jacobi" (MFMA fast path); device; group.
-Deviations: exchange_scores with num_shards == 1 uses the local scores (the
-reference reads an uninitialised buffer there); include_wasserstein's W2/JKO
-term (distsampler.py:103-129) is not implemented yet and raises
-NotImplementedError when it would be applied (from the second step on).
+include_wasserstein (the reference default) adds the W2/JKO term from the
+second step on (distsampler.py:103-129, 190-198): the reference's LP is solved
+exactly as an assignment on the GPU (dsvgd.w2), and h * grad is added to every
+owned row's direction before the update.  previous particles = all n rows
+after the step when particles are exchanged, else the owned block (:202-205).
+
+Deviation: exchange_scores with num_shards == 1 uses the local scores (the
+reference reads an uninitialised buffer there).
 """
 import torch
 
@@ -34,6 +38,7 @@ from . import exchange
 from .engine import PhiEngine, SelectState, sequential_sweep, span
 from .kernels import resolve_kernel
 from .targets import resolve_target
+from .w2 import W2Term
 
 
 class DistSampler(object):
@@ -86,6 +91,7 @@ class DistSampler(object):
         self._previous_particles = None
         self._engines = {}
         self._state = None
+        self._w2 = None
 
     # ---------------------------------------------------- reference API --
     @property
@@ -139,6 +145,14 @@ class DistSampler(object):
             exchange.all_reduce_sum(self._scores, self._group)
         return None
 
+    def _wasserstein_grad(self, particles, previous_particles, h):
+        """h * W2 gradient (distsampler.py:103-129 times h, :198) of the owned
+        rows against the previous particles, on the GPU (dsvgd.w2)."""
+        key = (particles.shape[0], previous_particles.shape[0], self._d)
+        if self._w2 is None or (self._w2.m, self._w2.n, self._w2.d) != key:
+            self._w2 = W2Term(*key, device=self._device)
+        return self._w2.grad(particles, previous_particles, h)
+
     # ------------------------------------------------------------ step --
     def _engine(self, n_int, m, row0):
         key = (n_int, m, row0)
@@ -173,13 +187,12 @@ class DistSampler(object):
             with span(self.timer, "scores"):
                 self._local_scores(self._work, self._scores)
 
-        if self._include_wasserstein and self._previous_particles is not None:
-            raise NotImplementedError(
-                "include_wasserstein=True: the W2/JKO term (distsampler.py:103-129) is not "
-                "implemented on MI355X yet; construct with include_wasserstein=False")
-
         s, e = self._particle_start_idx, self._particle_end_idx
         X = self._work
+        w2g = None
+        if self._include_wasserstein and self._previous_particles is not None:
+            with span(self.timer, "w2"):
+                w2g = self._wasserstein_grad(X[s:e], self._previous_particles, h)
         if self._exchange_particles:
             Xi, lo = X, 0
         else:
@@ -208,10 +221,10 @@ class DistSampler(object):
                 with span(self.timer, "allreduce_scores_wait"):
                     pending.wait()
                 eng.pack(Xi, Si)                   # Si already carries the score scale
-                eng.direction(X[s:e], step_size, write_phi=False)
+                eng.direction(X[s:e], step_size, write_phi=False, extra=w2g)
             else:
                 eng.step(Xi, Si, X_own=X[s:e], step=step_size, h=None if median else self._rbf.h,
-                         allreduce=hook, write_phi=False)
+                         allreduce=hook, write_phi=False, extra=w2g)
         else:
             if median:
                 eng = self._engine(n_int, e - s, s - lo)
@@ -227,7 +240,7 @@ class DistSampler(object):
                        N.stream(self._device))
             tgt = None if self._exchange_scores else self._target
             sequential_sweep(Xi, Si, range(s - lo, e - lo), state, step_size, target=tgt,
-                             score_scale=scale)
+                             score_scale=scale, extra=w2g)
 
         if self._include_wasserstein:
             src = X if self._exchange_particles else X[s:e]

@@ -248,12 +248,16 @@ class PhiEngine(object):
 
     DIRECT_MAX_D = 64
 
-    def direction(self, X_own=None, step=0.0, write_phi=True, inv_n=None):
-        """phi for the owned rows; optionally X_own += step * phi (in place).
+    def direction(self, X_own=None, step=0.0, write_phi=True, inv_n=None, extra=None):
+        """phi for the owned rows (+ `extra`, e.g. the h * W2 gradient rows);
+        optionally X_own += step * phi (in place).
         d <= 64: pairwise VALU form (dsvgd_phi_direct); else K.[Xc|S] on MFMA."""
         s = N.stream(self.device)
         if X_own is not None:
             assert X_own.shape == (self.m, self.d)
+        if extra is not None:
+            assert extra.shape == (self.m, self.d) and extra.dtype == torch.float32
+        ex, lde = (N.ptr(extra), N.ld(extra)) if extra is not None else (None, self.d)
         inv_n = 1.0 / self.n if inv_n is None else inv_n
         phi = N.ptr(self.phi) if write_phi else None
         xo = N.ptr(X_own)
@@ -262,7 +266,7 @@ class PhiEngine(object):
             with span(self.timer, "phi_direct"):
                 N.call("dsvgd_phi_direct", N.ptr(self.D), self.n_pad, N.ptr(self.Y), self.ldy,
                        self.row0, self.m, self.n, self.d, self.state.ptr, float(inv_n),
-                       float(step), phi, self.d, xo, ldx, s)
+                       float(step), ex, lde, phi, self.d, xo, ldx, s)
             return
         with span(self.timer, "phi_mm"):
             N.call("dsvgd_phi_mm", N.ptr(self.D), self.n_pad, N.ptr(self.Y), self.ldy, self.row0,
@@ -270,11 +274,11 @@ class PhiEngine(object):
                    N.ptr(self.rowsum), s)
         N.call("dsvgd_phi_finish", N.ptr(self.KY), self.ldy, N.ptr(self.rowsum), self.splits,
                N.ptr(self.Y), self.ldy, self.row0, self.m, self.d, self.dp, self.state.ptr,
-               float(inv_n), float(step), phi, self.d, xo, ldx, s)
+               float(inv_n), float(step), ex, lde, phi, self.d, xo, ldx, s)
 
     # ------------------------------------------------------------ helpers --
     def step(self, X, S, X_own=None, step=0.0, h=None, score_scale=1.0, allreduce=None,
-             write_phi=True):
+             write_phi=True, extra=None):
         """One Jacobi step: h=None -> median bandwidth, else fixed h."""
         self.pack(X, S, score_scale)
         median = h is None
@@ -283,7 +287,7 @@ class PhiEngine(object):
             self.median_bandwidth(allreduce)
         else:
             self.fixed_bandwidth(h)
-        self.direction(X_own, step, write_phi)
+        self.direction(X_own, step, write_phi, extra=extra)
 
     def dense_D(self):
         """D as a dense (m, n) tensor (tests/inspection; un-does the panel layout)."""
@@ -292,16 +296,21 @@ class PhiEngine(object):
         return Dd[:self.m, :self.n]
 
 
-def sequential_sweep(X, S, rows, h_state, step, target=None, score_scale=1.0, phi_out=None):
+def sequential_sweep(X, S, rows, h_state, step, target=None, score_scale=1.0, phi_out=None,
+                     extra=None):
     """Gauss-Seidel sweep in the reference order over `rows` of the interacting
     set X (n, d): for each i, phi_i from the CURRENT X (earlier rows already
-    moved), X[i] += step * phi_i, then (if `target`) S[i] is recomputed for the
-    moved particle, which is what re-running _dlogp per pair amounts to
-    (dsvgd/sampler.py:64-68, dsvgd/distsampler.py:194-200)."""
+    moved), X[i] += step * (phi_i + extra[k]), then (if `target`) S[i] is
+    recomputed for the moved particle, which is what re-running _dlogp per
+    pair amounts to (dsvgd/sampler.py:64-68, dsvgd/distsampler.py:194-200).
+    extra: optional (len(rows), d) contiguous rows (the h * W2 gradient)."""
     n, d = X.shape
     s = N.stream(X.device)
+    if extra is not None:
+        assert extra.is_contiguous() and extra.shape == (len(rows), d)
     for k, i in enumerate(rows):
         N.call("dsvgd_phi_row", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), n, d, int(i),
-               h_state.ptr, float(step), N.ptr(phi_out[k]) if phi_out is not None else None, s)
+               h_state.ptr, float(step), N.ptr(extra[k]) if extra is not None else None,
+               N.ptr(phi_out[k]) if phi_out is not None else None, s)
         if target is not None:
             target.score(X[i:i + 1], S[i:i + 1], score_scale)

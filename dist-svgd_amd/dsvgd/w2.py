@@ -1,0 +1,55 @@
+"""The W2 / JKO term of DistSampler.make_step on the GPU
+(reference dsvgd/distsampler.py:103-129, applied at :190-198).
+
+    G = h * sum_j P_ij (x_i - y_j)
+
+with P the optimal plan of the reference LP (uniform marginals 1/m, 1/n).
+For n = R m the plan is an assignment of n slots to n columns (include/dsvgd.h,
+dsvgd_w2_*): cost tiles (dsvgd_w2_cost) -> epsilon-scaling auction
+(dsvgd_w2_assign) -> dsvgd_w2_grad, all on device.  G is handed to the phi
+epilogue as `extra`, so the update is x_i += step * (phi_i + G_i) as at
+distsampler.py:196-200.
+"""
+import ctypes
+
+import torch
+
+from . import _native as N
+
+
+class W2Term(object):
+    """Buffers for one (m, n, d) shape: cost C (m x n fp32), auction workspace,
+    slot assignment (n int32) and G (m x d)."""
+
+    MAX_ROUNDS = 1 << 18
+
+    def __init__(self, m, n, d, device):
+        if n % m:
+            raise ValueError("W2 term needs n to be a multiple of m (n = R m)")
+        self.m, self.n, self.d = m, n, d
+        self.device = torch.device(device)
+        self.C = torch.empty((m, n), dtype=torch.float32, device=self.device)
+        nbytes = int(N.load().dsvgd_w2_workspace_bytes(m, n))
+        self.ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        self.assign = torch.empty(n, dtype=torch.int32, device=self.device)
+        self.G = torch.empty((m, d), dtype=torch.float32, device=self.device)
+        self.rounds = 0
+
+    def grad(self, X, Y, h):
+        """G (m, d) = h * W2 gradient of the owned rows X (m, d) against the
+        previous particles Y (n, d).  Blocks until the auction has converged."""
+        assert X.shape == (self.m, self.d) and Y.shape == (self.n, self.d)
+        s = N.stream(self.device)
+        N.call("dsvgd_w2_cost", N.ptr(X), N.ld(X), self.m, N.ptr(Y), N.ld(Y), self.n, self.d,
+               N.ptr(self.C), self.n, s)
+        rounds = ctypes.c_int64(0)
+        N.call("dsvgd_w2_assign", N.ptr(self.C), self.n, self.m, self.n, N.ptr(self.ws),
+               self.MAX_ROUNDS, N.ptr(self.assign), ctypes.addressof(rounds), s)
+        self.rounds = int(rounds.value)
+        N.call("dsvgd_w2_grad", N.ptr(X), N.ld(X), self.m, N.ptr(Y), N.ld(Y), self.n, self.d,
+               N.ptr(self.assign), float(h), N.ptr(self.G), self.d, s)
+        return self.G
+
+    def plan(self):
+        """The last slot -> column assignment as a host int64 array."""
+        return self.assign.cpu().numpy().astype("int64")

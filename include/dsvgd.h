@@ -166,31 +166,62 @@ int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64
                  int64_t ldk, float* rowsum, void* stream);
 
 /* phi[i] = inv_n * (s_i + KS[i] + (2/h) (rowsum[i] xc[i] - KXc[i])) with the
- * split-K partials summed in slice order (s_i: the self term k_ii s_i), and, if X != NULL, X[i] += step * phi[i]
- * (the update of dsvgd/sampler.py:68 / dsvgd/distsampler.py:200, Jacobi
- * order).  phi may be NULL. */
+ * split-K partials summed in slice order (s_i: the self term k_ii s_i), plus
+ * extra[i] if extra != NULL (the h * W2-gradient row of dsvgd_w2_grad:
+ * delta = phi_hat + h W, dsvgd/distsampler.py:194-198), and, if X != NULL,
+ * X[i] += step * phi[i] (the update of dsvgd/sampler.py:68 /
+ * dsvgd/distsampler.py:200, Jacobi order).  phi and extra may be NULL. */
 int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t splits,
                      const float* Y, int64_t ldy, int64_t row0, int64_t m, int64_t d, int64_t dp,
-                     const dsvgd_select_state* st, float inv_n, float step, float* phi,
-                     int64_t ldphi, float* X, int64_t ldx, void* stream);
+                     const dsvgd_select_state* st, float inv_n, float step, const float* extra,
+                     int64_t lde, float* phi, int64_t ldphi, float* X, int64_t ldx,
+                     void* stream);
 
 /* d <= 64: phi (and the optional X update) straight from the pairwise form
  * phi_i = inv_n sum_j k_ij (s_j + (2/h)(x_i - x_j)) on the VALU -- the
  * reference's own per-pair expression (dsvgd/sampler.py:38-40), which avoids
  * the r x - K X cancellation of the GEMM form at small d.  Replaces
- * dsvgd_phi_mm + dsvgd_phi_finish for small d. */
+ * dsvgd_phi_mm + dsvgd_phi_finish for small d (extra as in dsvgd_phi_finish). */
 int dsvgd_phi_direct(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t row0,
                      int64_t m, int64_t n, int64_t d, const dsvgd_select_state* st, float inv_n,
-                     float step, float* phi, int64_t ldphi, float* X, int64_t ldx, void* stream);
+                     float step, const float* extra, int64_t lde, float* phi, int64_t ldphi,
+                     float* X, int64_t ldx, void* stream);
 
 /* Gauss-Seidel single-row update (reference order): for particle i, phi_i
  * from exact differences against the CURRENT X (rows < i already moved),
  * X[i] += step * phi_i.  Reproduces dsvgd/sampler.py:64-68 and
  * dsvgd/distsampler.py:194-200 one row at a time.  n_int interacting rows
- * start at X (row i is X + i*ldx). */
+ * start at X (row i is X + i*ldx).  extra (nullable, d floats) is added to
+ * phi_i before the step (the row's h * W2 gradient, distsampler.py:196-198). */
 int dsvgd_phi_row(float* X, int64_t ldx, const float* S, int64_t lds, int64_t n_int, int64_t d,
-                  int64_t i, const dsvgd_select_state* st, float step, float* phi_out,
-                  void* stream);
+                  int64_t i, const dsvgd_select_state* st, float step, const float* extra,
+                  float* phi_out, void* stream);
+
+/* ---- W2 / JKO term (dsvgd/distsampler.py:103-129, used at :190-198) ---- */
+/* The reference LP  min <P,C>, P >= 0, row sums 1/m, column sums 1/n  over
+ * C_ij = ||x_i - y_j||^2 (x: m owned particles, y: n previous particles) has
+ * an integral optimum when n = R m: an assignment of n slots (slot s belongs
+ * to row s / R) to the n columns, each of mass 1/n.
+ *
+ * C[i][j] (m x n, ldc >= n) from explicit fp32 differences
+ * (distsampler.py:107-114). */
+int dsvgd_w2_cost(const float* X, int64_t ldx, int64_t m, const float* Y, int64_t ldy, int64_t n,
+                  int64_t d, float* C, int64_t ldc, void* stream);
+/* Device workspace of dsvgd_w2_assign (32 n + 256 bytes). */
+size_t dsvgd_w2_workspace_bytes(int64_t m, int64_t n);
+/* assign[s] = column of slot s in an optimal plan (replaces scipy linprog,
+ * distsampler.py:115-126): epsilon-scaling auction on the GPU, final
+ * eps = max C * 2^-24 / n (within one fp32 ulp of max C of the optimum).
+ * BLOCKS the calling thread (polls the device between batches of rounds);
+ * fails with -3 after max_rounds.  rounds_out (host, nullable) gets the
+ * number of bidding rounds. */
+int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
+                    int64_t max_rounds, int32_t* assign, int64_t* rounds_out, void* stream);
+/* G[i] = h * sum_j P_ij (x_i - y_j) = h/n * sum_{slots s of i} (x_i - y_assign[s])
+ * (distsampler.py:128 scaled by the JKO step h of :198); pass G as `extra`
+ * to dsvgd_phi_finish / dsvgd_phi_direct / dsvgd_phi_row. */
+int dsvgd_w2_grad(const float* X, int64_t ldx, int64_t m, const float* Y, int64_t ldy, int64_t n,
+                  int64_t d, const int32_t* assign, float h, float* G, int64_t ldg, void* stream);
 
 /* ---- target scores grad log p (replace the autograd _dlogp calls) ------ */
 /* S = scale * (-lam * (X - mu))      (synthetic Gaussian target)            */

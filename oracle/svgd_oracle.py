@@ -151,16 +151,61 @@ def sampler_jacobi(X0, score_fn, h, num_iter, step_size, median=False):
 
 
 # ----------------------------------------------------- DistSampler (S ranks) --
+# ------------------------------------------------------------ W2 / JKO --
+def w2_cost(X, P):
+    """C[i][j] = ||x_i - p_j||^2 in fp64 from explicit differences, as the
+    reference builds `diffs` and `c` (distsampler.py:107-114)."""
+    X = np.asarray(X, np.float64)
+    P = np.asarray(P, np.float64)
+    if X.shape[0] * P.shape[0] * X.shape[1] <= 1 << 26:
+        return ((X[:, None, :] - P[None, :, :]) ** 2).sum(-1)
+    return np.maximum(sqdist(X, P), 0.0)
+
+
+def w2_plan(C):
+    """Optimal plan of the reference LP (distsampler.py:115-126): minimise
+    <P, C> over P >= 0 with row sums 1/m and column sums 1/n.  For n = R m the
+    vertices are integral after replicating each row R times (supplies R,
+    demands 1, scaled by n), so the LP optimum is an exact assignment of
+    n slots (slot s -> row s // R) to n columns, each carrying mass 1/n.
+    Returns the column of every slot (scipy's exact Hungarian solver)."""
+    from scipy.optimize import linear_sum_assignment
+    m, n = C.shape
+    assert n % m == 0, "the reference LP is integral here only for n = R m"
+    R = n // m
+    rows, cols = linear_sum_assignment(np.repeat(C, R, axis=0))
+    out = np.empty(n, np.int64)
+    out[rows] = cols
+    return out
+
+
+def w2_grad(X, P, plan=None):
+    """sum_j P_ij (x_i - p_j) (distsampler.py:128), P_ij = 1/n on the slots of
+    row i.  Returns (grad (m, d) fp64, plan)."""
+    X = np.asarray(X, np.float64)
+    P = np.asarray(P, np.float64)
+    m, n = X.shape[0], P.shape[0]
+    if plan is None:
+        plan = w2_plan(w2_cost(X, P))
+    R = n // m
+    g = (X[:, None, :] - P[plan].reshape(m, R, -1)).sum(1) / n
+    return g, plan
+
+
 class DistOracle:
     """All S ranks of DistSampler simulated in one process (distsampler.py:9-205).
 
     `particles[r]` is rank r's (n, d) copy; `score_fns[r](X)` the rank-local
     score grad log p_r (prior + local likelihood).  sequential=True follows the
     reference's in-place Gauss-Seidel order; False is the Jacobi variant.
+    include_wasserstein adds the JKO term h_jko * w2_grad(own, previous) to
+    every owned row's direction (distsampler.py:190-198) from the second step
+    on; previous = all n rows after the sweep when particles are exchanged,
+    else the owned block (:202-205).
     """
 
     def __init__(self, particles, score_fns, N_local, N_global, exchange_particles,
-                 exchange_scores, h=1.0, sequential=True):
+                 exchange_scores, h=1.0, sequential=True, include_wasserstein=False):
         assert not (exchange_scores and not exchange_particles)
         self.S = len(particles)
         n = np.asarray(particles[0]).shape[0]
@@ -173,6 +218,8 @@ class DistOracle:
         self.h = h
         self.sequential = sequential
         self.start = [r * self.per for r in range(self.S)]
+        self.w2 = include_wasserstein
+        self.prev = [None] * self.S
 
     def own(self, r):
         return self.X[r][self.start[r]:self.start[r] + self.per]
@@ -197,7 +244,7 @@ class DistOracle:
             self.start[r] = s0
         return None
 
-    def step(self, step_size):
+    def step(self, step_size, h_jko=1.0):
         scores = self._exchange()
         if scores is None and self.xs:      # S == 1 with exchange_scores: local scores
             scores = [self.score_fns[r](self.X[r]) for r in range(self.S)]
@@ -206,15 +253,21 @@ class DistOracle:
             s0, s1 = self.start[r], self.start[r] + self.per
             lo, hi = (0, self.n) if self.xp else (s0, s1)
             scale = 1.0 if self.xs else self.N_global / self.N_local
+            extra = np.zeros((s1 - s0, Xr.shape[1]))
+            if self.w2 and self.prev[r] is not None:
+                extra = h_jko * w2_grad(Xr[s0:s1], self.prev[r])[0]
             if self.sequential:
                 for i in range(s0, s1):
                     Xi = Xr[lo:hi]
                     Sj = scores[r][lo:hi] if self.xs else scale * self.score_fns[r](Xi)
-                    Xr[i] += step_size * phi(Xi, Sj, self.h, rows=[i - lo])[0]
+                    Xr[i] += step_size * (phi(Xi, Sj, self.h, rows=[i - lo])[0] + extra[i - s0])
             else:
                 Xi = Xr[lo:hi].copy()
                 Sj = scores[r][lo:hi] if self.xs else scale * self.score_fns[r](Xi)
-                Xr[s0:s1] += step_size * phi(Xi, Sj, self.h, rows=np.arange(s0 - lo, s1 - lo))
+                Xr[s0:s1] += step_size * (phi(Xi, Sj, self.h, rows=np.arange(s0 - lo, s1 - lo))
+                                          + extra)
+            if self.w2:
+                self.prev[r] = (Xr if self.xp else Xr[s0:s1]).copy()
 
 
 # --------------------------------------------------------------- metric --

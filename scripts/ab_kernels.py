@@ -46,7 +46,7 @@ def main():
     eng.distances(median=True)
     eng.median_bandwidth()
     variants = {"nn=w1": {"DSVGD_NN_SHAPE": "w1"}, "nn=w2": {"DSVGD_NN_SHAPE": "w2"},
-                "nn=b64": {"DSVGD_NN_SHAPE": "b64"}}
+                "nn=b64": {"DSVGD_NN_SHAPE": "b64"}, "nn=w2t": {"DSVGD_NN_SHAPE": "w2t"}}
     res = {k: [] for k in variants}
     ref = None
     for _ in range(args.rounds):

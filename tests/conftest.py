@@ -14,11 +14,16 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 # worst parity error seen per test (tests record into it; written at session end)
 PARITY = {}
+INFO = {}
 
 
-def record_parity(err):
+def record_parity(err, **info):
+    """Keep the worst error of the running test; optional counters (e.g. the
+    auction's round count) go to the "info" section of the dump."""
     key = os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0]
     PARITY[key] = max(PARITY.get(key, 0.0), float(err))
+    if info:
+        INFO[key] = info
 
 
 def pytest_sessionfinish(session, exitstatus):
@@ -30,7 +35,10 @@ def pytest_sessionfinish(session, exitstatus):
     try:
         os.makedirs(out, exist_ok=True)
         with open(os.path.join(out, "parity_%d.json" % int(time.time())), "w") as f:
-            json.dump(dict(sorted(PARITY.items())), f, indent=1)
+            doc = dict(sorted(PARITY.items()))
+            if INFO:
+                doc["info"] = dict(sorted(INFO.items()))
+            json.dump(doc, f, indent=1)
     except OSError:
         pass
 

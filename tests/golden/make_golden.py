@@ -16,8 +16,11 @@ Targets and kernels below restate the reference experiments' closures:
                           at logreg.py:57 raises TypeError on torch 2.10)
   * Gaussian              N(mu, diag(1/lam)), the survey's synthetic target
 The golden outputs are the reference's own Sampler._phi_hat (sampler.py:35-40),
-Sampler.sample (sampler.py:42-74) and DistSampler.make_step
-(distsampler.py:172-205, S = 1, 2, 4 under gloo, all three exchange modes).
+Sampler.sample (sampler.py:42-74), DistSampler.make_step
+(distsampler.py:172-205, S = 1, 2, 4 under gloo, all three exchange modes) and
+DistSampler._wasserstein_grad (distsampler.py:103-129, the W2/JKO LP; called
+unbound with self=None -- it reads nothing from self -- and through make_step
+with include_wasserstein=True).
 """
 import contextlib
 import io
@@ -144,7 +147,24 @@ def sample_case(name, d, n, T, eps, logp, h, seed, extra):
     print(name, vals.shape)
 
 
-def _dist_worker(rank, S, port, n, steps, eps, hjko, mode, x, t, q):
+def w2_case(name, m, n, d, seed, near=None):
+    """_wasserstein_grad(particles (m,d), previous (n,d)) -> (m,d) float64.
+    near: previous = particles (tiled n/m times) + near * noise, the shape the
+    JKO term sees between consecutive SVGD steps."""
+    dsvgd = _ref()
+    import torch
+    rs = np.random.RandomState(seed)
+    X = rs.randn(m, d).astype(np.float32)
+    if near is None:
+        P = rs.randn(n, d).astype(np.float32)
+    else:
+        P = (np.tile(X, (n // m, 1)) + near * rs.randn(n, d)).astype(np.float32)
+    g = dsvgd.DistSampler._wasserstein_grad(None, torch.tensor(X), torch.tensor(P))
+    np.savez(os.path.join(OUT, name + ".npz"), X=X, P=P, grad=np.asarray(g, np.float64))
+    print(name, (m, n, d), "max|grad|", np.abs(g).max())
+
+
+def _dist_worker(rank, S, port, n, steps, eps, hjko, mode, x, t, q, w2=False):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -162,7 +182,7 @@ def _dist_worker(rank, S, port, n, steps, eps, hjko, mode, x, t, q):
     ds = dsvgd.DistSampler(rank, S, logp, rbf(1.0), parts, per, per * S,
                            exchange_particles=mode in ("all_particles", "all_scores"),
                            exchange_scores=mode == "all_scores",
-                           include_wasserstein=False)
+                           include_wasserstein=w2)
     own, full, start = [], [], []
     for _ in range(steps):
         ds.make_step(eps, h=hjko)
@@ -174,13 +194,14 @@ def _dist_worker(rank, S, port, n, steps, eps, hjko, mode, x, t, q):
     dist.destroy_process_group()
 
 
-def dist_case(name, S, n, steps, eps, mode, port):
+def dist_case(name, S, n, steps, eps, mode, port, w2=False, hjko=10.0):
     import torch.multiprocessing as mp
     x, t = banana_like(N=400)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_dist_worker,
-                         args=(r, S, port, n, steps, eps, 10.0, mode, x, t, q)) for r in range(S)]
+                         args=(r, S, port, n, steps, eps, hjko, mode, x, t, q, w2))
+             for r in range(S)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=600) for _ in range(S)], key=lambda r: r[0])
@@ -189,6 +210,7 @@ def dist_case(name, S, n, steps, eps, mode, port):
         assert p.exitcode == 0
     np.savez(os.path.join(OUT, name + ".npz"), S=np.int64(S), n=np.int64(n),
              steps=np.int64(steps), eps=np.float64(eps), mode=np.array(mode),
+             w2=np.bool_(w2), hjko=np.float64(hjko),
              x_train=x, t_train=t,
              init=np.stack([r[1] for r in res]), own=np.stack([r[2] for r in res]),
              full=np.stack([r[3] for r in res]), start=np.stack([r[4] for r in res]))
@@ -246,6 +268,20 @@ def main(which=None):
             cases.append((nm, (lambda nm=nm, S=S, n=n, mode=mode, port=port:
                                dist_case(nm, S, n, 3, 0.05, mode, port))))
             port += 1
+    # G5 -- the W2/JKO term (distsampler.py:103-129, 190-198)
+    for nm, m, n, d, seed, near in (("g5_w2_m8_n8_d2", 8, 8, 2, 5, None),
+                                    ("g5_w2_m12_n12_d3", 12, 12, 3, 6, None),
+                                    ("g5_w2_m8_n16_d3", 8, 16, 3, 7, None),
+                                    ("g5_w2_m6_n24_d5", 6, 24, 5, 8, None),
+                                    ("g5_w2_m16_n32_d4_near", 16, 32, 4, 9, 0.05),
+                                    ("g5_w2_m24_n24_d3_near", 24, 24, 3, 10, 0.02)):
+        cases.append((nm, (lambda nm=nm, m=m, n=n, d=d, seed=seed, near=near:
+                           w2_case(nm, m, n, d, seed, near))))
+    for mode in ("partitions", "all_particles", "all_scores"):
+        nm = "g5_dist_s2_%s_w2" % mode
+        cases.append((nm, (lambda nm=nm, mode=mode, port=port:
+                           dist_case(nm, 2, 16, 3, 0.05, mode, port, w2=True))))
+        port += 1
     for nm, fn in cases:
         if which and nm not in which:
             continue

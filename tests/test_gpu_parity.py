@@ -335,14 +335,91 @@ def test_distsampler_s1_matches_reference(golden, order):
     np.testing.assert_array_equal(parts.numpy(), ds._particles.numpy())
 
 
-def test_wasserstein_flag_raises_from_second_step():
-    x = np.random.RandomState(0).randn(50, 2).astype(np.float32)
-    t = np.sign(x[:, 0]).astype(np.float32)
-    ds = dsvgd().DistSampler(0, 1, dsvgd().targets.LogisticRegression(x, t), dsvgd().RBF(1.0),
-                             torch.randn(16, 3), 50, 50, False, False, True)
-    ds.make_step(1e-3)
-    with pytest.raises(NotImplementedError):
-        ds.make_step(1e-3)
+# ----------------------------------------------------- W2 / JKO term --
+W2_GOLDEN = ["g5_w2_m8_n8_d2", "g5_w2_m12_n12_d3", "g5_w2_m8_n16_d3", "g5_w2_m6_n24_d5",
+             "g5_w2_m16_n32_d4_near", "g5_w2_m24_n24_d3_near"]
+
+
+def _w2_gpu(X, P, h=1.0):
+    X = torch.tensor(np.ascontiguousarray(X, np.float32), device=DEV)
+    P = torch.tensor(np.ascontiguousarray(P, np.float32), device=DEV)
+    w = dsvgd().w2.W2Term(X.shape[0], P.shape[0], X.shape[1], DEV)
+    G = w.grad(X, P, h).cpu().numpy().astype(np.float64)
+    return G, w.plan(), w
+
+
+@pytest.mark.parametrize("name", W2_GOLDEN)
+def test_w2_grad_matches_reference_lp(golden, name):
+    """GPU auction + gradient == the reference's linprog plan (golden)."""
+    g = golden(name)
+    G, plan, _ = _w2_gpu(g["X"], g["P"], h=1.0)
+    err = abs_err(G, g["grad"]) / max(np.abs(g["grad"]).max(), 1e-30)
+    record_parity(err)
+    assert err < PHI_TOL, err
+    np.testing.assert_array_equal(plan, O.w2_plan(O.w2_cost(g["X"], g["P"])))
+
+
+@pytest.mark.parametrize("m,n,d,near", [(256, 256, 16, None), (512, 1024, 8, None),
+                                        (500, 4000, 3, None), (2048, 2048, 64, None),
+                                        (1024, 1024, 32, 0.05), (1024, 4096, 8, 0.01),
+                                        (3000, 3000, 2, 0.2)])
+def test_w2_assignment_optimal(m, n, d, near):
+    """Plan == scipy's exact assignment on the fp64 costs (random inputs: no
+    near-ties at these sizes), and the gradient within PHI_TOL."""
+    rs = np.random.RandomState(m + n + d)
+    X = rs.randn(m, d).astype(np.float32)
+    if near is None:
+        P = rs.randn(n, d).astype(np.float32)
+    else:
+        P = (np.tile(X, (n // m, 1)) + near * rs.randn(n, d)).astype(np.float32)
+    G, plan, w = _w2_gpu(X, P, h=2.5)
+    C = O.w2_cost(X, P)
+    ref_plan = O.w2_plan(C)
+    R = n // m
+    rows = np.arange(n) // R
+    got_cost, opt_cost = C[rows, plan].sum(), C[rows, ref_plan].sum()
+    assert sorted(plan.tolist()) == list(range(n))
+    assert got_cost <= opt_cost * (1 + 1e-6) + 1e-9, (got_cost, opt_cost)
+    same = float((plan == ref_plan).mean())
+    ref = 2.5 * O.w2_grad(X, P, ref_plan)[0]
+    err = abs_err(G, ref) / np.abs(ref).max()
+    record_parity(err, rounds=w.rounds, same_plan=same)
+    assert same == 1.0, same
+    assert err < PHI_TOL, err
+
+
+def test_w2_degenerate_and_identity():
+    """All-equal particles (every cost 0) -> zero gradient; previous ==
+    current (S = 1 consecutive steps) -> identity plan, zero gradient."""
+    X = np.ones((64, 5), np.float32)
+    G, plan, _ = _w2_gpu(X, np.ones((128, 5), np.float32))
+    assert np.all(G == 0)
+    Y = np.random.RandomState(3).randn(300, 7).astype(np.float32)
+    G, plan, _ = _w2_gpu(Y, Y)
+    np.testing.assert_array_equal(plan, np.arange(300))
+    assert np.all(G == 0)
+
+
+def test_w2_ties_reach_optimal_cost():
+    """Duplicated previous particles make the plan non-unique (the LP may
+    return any vertex): the cost must still be optimal."""
+    rs = np.random.RandomState(7)
+    X = rs.randn(200, 3).astype(np.float32)
+    P = np.repeat(rs.randn(100, 3).astype(np.float32), 2, axis=0)
+    _, plan, _ = _w2_gpu(X, P)
+    C = O.w2_cost(X, P)
+    opt = C[np.arange(200), O.w2_plan(C)].sum()
+    assert C[np.arange(200), plan].sum() <= opt * (1 + 1e-6)
+
+
+def test_w2_errors():
+    X = torch.zeros((3, 2), device=DEV)
+    with pytest.raises(ValueError):
+        dsvgd().w2.W2Term(3, 4, 2, DEV)
+    w = dsvgd().w2.W2Term(3, 3, 2, DEV)
+    bad = torch.full((3, 2), float("nan"), device=DEV)
+    with pytest.raises(dsvgd()._native.NativeError):
+        w.grad(X, bad, 1.0)
 
 
 # ------------------------------------------ DistSampler, 2 ranks, 1 GPU --
@@ -363,28 +440,34 @@ def _dist_gpu_worker(rank, S, port, name, order, q, median=False):
     mode = str(g["mode"])
     tgt = m.targets.LogisticRegression(x[rank * per:(rank + 1) * per], t[rank * per:(rank + 1) * per])
     parts = torch.tensor(g["init"][rank], device=DEV)
+    w2 = bool(g["w2"]) if "w2" in g else False
+    hjko = float(g["hjko"]) if "hjko" in g else 10.0
     ds = m.DistSampler(rank, S, tgt, m.RBF("median" if median else 1.0), parts, per, per * S,
                        exchange_particles=mode in ("all_particles", "all_scores"),
-                       exchange_scores=mode == "all_scores", include_wasserstein=False,
+                       exchange_scores=mode == "all_scores", include_wasserstein=w2,
                        order=order)
     out = []
     for _ in range(int(g["steps"])):
-        ds.make_step(float(g["eps"]), h=10.0)
+        ds.make_step(float(g["eps"]), h=hjko)
         out.append((ds.particles.cpu().numpy(), ds._particles.cpu().numpy(), ds._particle_start_idx))
     q.put((rank, out))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["partitions", "all_particles", "all_scores"])
-def test_distsampler_two_ranks_match_reference(golden, mode):
-    """Two ranks share cuda:0 (gloo for the exchange; kernels on the GPU)."""
+DIST_S2 = (["g4_dist_s2_" + m for m in ("partitions", "all_particles", "all_scores")]
+           + ["g5_dist_s2_%s_w2" % m for m in ("partitions", "all_particles", "all_scores")])
+
+
+@pytest.mark.parametrize("name", DIST_S2)
+def test_distsampler_two_ranks_match_reference(golden, name):
+    """Two ranks share cuda:0 (gloo for the exchange; kernels on the GPU);
+    g5_*: include_wasserstein=True, the W2/JKO term from the second step."""
     import torch.multiprocessing as mp
-    name = "g4_dist_s2_" + mode
     g = golden(name)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29800 + ["partitions", "all_particles", "all_scores"].index(mode)
+    port = 29800 + DIST_S2.index(name)
     ps = [ctx.Process(target=_dist_gpu_worker, args=(r, 2, port, name, "sequential", q))
           for r in range(2)]
     for p in ps:
@@ -455,16 +538,17 @@ def test_distsampler_median_two_ranks_jacobi(d):
     assert res[0][2] == res[1][2]            # identical h on both ranks
 
 
-@pytest.mark.parametrize("mode", ["all_scores", "all_particles", "partitions"])
-def test_distsampler_two_ranks_jacobi_vs_oracle(golden, mode):
+@pytest.mark.parametrize("name", DIST_S2)
+def test_distsampler_two_ranks_jacobi_vs_oracle(golden, name):
     """Jacobi DistSampler over 2 ranks (the all_scores path overlaps the score
     all-reduce with the distance stage) vs the oracle's Jacobi DistSampler."""
     import torch.multiprocessing as mp
-    name = "g4_dist_s2_" + mode
     g = golden(name)
+    mode = str(g["mode"])
+    w2 = bool(g["w2"]) if "w2" in g else False
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29860 + ["partitions", "all_particles", "all_scores"].index(mode)
+    port = 29860 + DIST_S2.index(name)
     ps = [ctx.Process(target=_dist_gpu_worker, args=(r, 2, port, name, "jacobi", q))
           for r in range(2)]
     for p in ps:
@@ -479,9 +563,9 @@ def test_distsampler_two_ranks_jacobi_vs_oracle(golden, mode):
            for r in range(2)]
     D = O.DistOracle(list(g["init"]), fns, per, 2 * per,
                      exchange_particles=mode != "partitions", exchange_scores=mode == "all_scores",
-                     h=1.0, sequential=False)
+                     h=1.0, sequential=False, include_wasserstein=w2)
     for step in range(int(g["steps"])):
-        D.step(float(g["eps"]))
+        D.step(float(g["eps"]), float(g["hjko"]) if "hjko" in g else 10.0)
         for rank, out in res:
             own, full, start = out[step]
             assert start == D.start[rank]

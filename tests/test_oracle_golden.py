@@ -68,16 +68,39 @@ def _dist_oracle(g, sequential=True):
            for r in range(S)]
     return O.DistOracle(list(g["init"]), fns, per, per * S,
                         exchange_particles=mode in ("all_particles", "all_scores"),
-                        exchange_scores=mode == "all_scores", h=1.0, sequential=sequential)
+                        exchange_scores=mode == "all_scores", h=1.0, sequential=sequential,
+                        include_wasserstein=bool(g["w2"]) if "w2" in g else False)
+
+
+W2_DIRECT = ["g5_w2_m8_n8_d2", "g5_w2_m12_n12_d3", "g5_w2_m8_n16_d3", "g5_w2_m6_n24_d5",
+             "g5_w2_m16_n32_d4_near", "g5_w2_m24_n24_d3_near"]
+W2_DIST = ["g5_dist_s2_%s_w2" % m for m in ("partitions", "all_particles", "all_scores")]
+
+
+@pytest.mark.parametrize("name", W2_DIRECT)
+def test_w2_grad_matches_reference_lp(golden, name):
+    """The exact-assignment restatement == the reference's linprog plan
+    (distsampler.py:103-129), including replicated rows (n = R m)."""
+    g = golden(name)
+    got, plan = O.w2_grad(g["X"], g["P"])
+    ref = g["grad"]
+    # HiGHS returns the vertex to its ~1e-9 feasibility tolerance; a different
+    # assignment would move a row by |x - y| / n ~ 1e-2
+    assert np.abs(got - ref).max() <= 1e-7 * max(1.0, np.abs(ref).max())
+    n, m = g["P"].shape[0], g["X"].shape[0]
+    assert sorted(plan.tolist()) == list(range(n))           # a permutation of the columns
+    C = O.w2_cost(g["X"], g["P"])
+    assert C.shape == (m, n)
 
 
 @pytest.mark.parametrize("name", ["g3_dist_s1_partitions"] + [
-    "g4_dist_s%d_%s" % (S, m) for S in (2, 4) for m in ("partitions", "all_particles", "all_scores")])
+    "g4_dist_s%d_%s" % (S, m) for S in (2, 4) for m in ("partitions", "all_particles", "all_scores")]
+    + W2_DIST)
 def test_distsampler_steps(golden, name):
     g = golden(name)
     D = _dist_oracle(g)
     for step in range(int(g["steps"])):
-        D.step(float(g["eps"]))
+        D.step(float(g["eps"]), float(g["hjko"]) if "hjko" in g else 1.0)
         for r in range(D.S):
             assert D.start[r] == int(g["start"][r][step])
             assert np.abs(D.own(r) - g["own"][r][step]).max() < TRAJ_TOL
