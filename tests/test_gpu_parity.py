@@ -340,6 +340,11 @@ W2_GOLDEN = ["g5_w2_m8_n8_d2", "g5_w2_m12_n12_d3", "g5_w2_m8_n16_d3", "g5_w2_m6_
              "g5_w2_m16_n32_d4_near", "g5_w2_m24_n24_d3_near"]
 
 
+def _row_sets(plan, m):
+    """The plan as per-row column sets (slots of one row are interchangeable)."""
+    return np.sort(np.asarray(plan).reshape(m, -1), axis=1)
+
+
 def _w2_gpu(X, P, h=1.0):
     X = torch.tensor(np.ascontiguousarray(X, np.float32), device=DEV)
     P = torch.tensor(np.ascontiguousarray(P, np.float32), device=DEV)
@@ -356,7 +361,8 @@ def test_w2_grad_matches_reference_lp(golden, name):
     err = abs_err(G, g["grad"]) / max(np.abs(g["grad"]).max(), 1e-30)
     record_parity(err)
     assert err < PHI_TOL, err
-    np.testing.assert_array_equal(plan, O.w2_plan(O.w2_cost(g["X"], g["P"])))
+    m = g["X"].shape[0]
+    np.testing.assert_array_equal(_row_sets(plan, m), _row_sets(O.w2_plan(O.w2_cost(g["X"], g["P"])), m))
 
 
 @pytest.mark.parametrize("m,n,d,near", [(256, 256, 16, None), (512, 1024, 8, None),
@@ -380,7 +386,7 @@ def test_w2_assignment_optimal(m, n, d, near):
     got_cost, opt_cost = C[rows, plan].sum(), C[rows, ref_plan].sum()
     assert sorted(plan.tolist()) == list(range(n))
     assert got_cost <= opt_cost * (1 + 1e-6) + 1e-9, (got_cost, opt_cost)
-    same = float((plan == ref_plan).mean())
+    same = float((_row_sets(plan, m) == _row_sets(ref_plan, m)).all(1).mean())
     ref = 2.5 * O.w2_grad(X, P, ref_plan)[0]
     err = abs_err(G, ref) / np.abs(ref).max()
     record_parity(err, rounds=w.rounds, same_plan=same)
