@@ -175,7 +175,7 @@ struct NNTile {
 #pragma unroll
       for (int u = 0; u < LB / 4; ++u) {
         const int blk = t + u * kThreads;  // 4x4 block: rows 4*rg.., cols 4*cg..
-        if (blk < NB4) {
+        if (NB4 % kThreads == 0 || blk < NB4) {
           const int rg = blk / (BC / 4), cg = blk % (BC / 4);
 #pragma unroll
           for (int i = 0; i < 4; ++i)
@@ -204,7 +204,7 @@ struct NNTile {
 #pragma unroll
       for (int u = 0; u < LB / 4; ++u) {
         const int blk = t + u * kThreads;
-        if (blk < NB4) {
+        if (NB4 % kThreads == 0 || blk < NB4) {
           const int rg = blk / (BC / 4), cg = blk % (BC / 4);
 #pragma unroll
           for (int i = 0; i < 4; ++i)

@@ -271,6 +271,10 @@ int launch_nn(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K,
 int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, int64_t cols,
             int splits, const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum,
             int64_t m, int64_t row0, hipStream_t s) {
+  // DSVGD_NN_NOEXP=1: TIMING EXPERIMENTS ONLY (wrong phi) -- the same engine
+  // without the fused exp / row sums, to price the VALU work between MFMAs.
+  const char* noexp = getenv("DSVGD_NN_NOEXP");
+  if (noexp && noexp[0] == '1') exp_ = false;
   if (cols % 512 == 0)
     return launch_nn<4>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s);
   if (cols % 256 == 0)

@@ -15,13 +15,15 @@
 //   * bids are resolved with one 64-bit atomicMax per bid, key =
 //     (fp32 increment rounded down) << 32 | slot, so a round's outcome does
 //     not depend on scheduling (ties go to the higher slot id);
-//   * a one-thread control kernel ends a phase when every slot is assigned,
-//     divides eps by kTheta and starts the next phase by bumping an epoch
-//     counter (assignments of older epochs read as unassigned -- no reset
-//     pass over n); prices carry over between phases.
+//   * the last resolve block (agent-scope release/acquire ticket) runs the
+//     control step: it ends a phase when every slot is assigned, divides eps
+//     by kTheta and starts the next phase by bumping an epoch counter
+//     (assignments of older epochs read as unassigned -- no reset pass over
+//     n); prices carry over between phases.  A round = 2 launches.
 // With eps_final = cmax * 2^-24 / n the final assignment is within cmax *
 // 2^-24 (one fp32 ulp of the largest cost) of the optimum.  The host wrapper
-// enqueues rounds in batches and polls the control block between batches.
+// enqueues rounds in batches and polls the control block (pinned, double
+// buffered: batch k+1 is queued before batch k's state is waited for).
 #include <float.h>
 
 #include <algorithm>
@@ -38,11 +40,13 @@ struct W2Ctl {
   int32_t pad_;
   unsigned long long unassigned;
   long long rounds, phases;
+  unsigned int ticket;  // resolve-kernel arrival counter (last arriver resets it)
 };
 
 constexpr size_t kW2CtlBytes = 256;
 constexpr double kTheta = 8.0;
 constexpr int kRoundBatch = 16;
+constexpr int kBidBlocks = 1024;  // grid-stride bid kernel: 4096 waves
 
 struct W2Ws {
   W2Ctl* ctl;
@@ -138,17 +142,9 @@ __global__ void w2_start_kernel(W2Ctl* ctl, int64_t n) {
   if (ctl->done == 0 && !(cmax > 0.0)) ctl->done = 2;
 }
 
-// One wave per slot; only slots unassigned in the current epoch bid.
-__global__ __launch_bounds__(256) void w2_bid_kernel(const float* __restrict__ C, int64_t ldc,
-                                                     int64_t n, int64_t R, W2Ws w) {
-  const W2Ctl* ctl = w.ctl;
-  if (ctl->done) return;
-  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (s >= n) return;
-  const int ep = ctl->epoch;
-  if (w.assigned_ep[s] == ep && w.assigned[s] >= 0) return;
-  const float* row = C + (s / R) * ldc;
+// One slot's bid: best / second-best of -C_sj - p_j over its cost row.
+__device__ __forceinline__ void bid_slot(const float* __restrict__ row, int64_t n, int64_t s,
+                                         int lane, double eps, const W2Ws& w) {
   double v1 = -DBL_MAX, v2 = -DBL_MAX;
   int j1 = INT32_MAX;
   for (int64_t j = lane; j < n; j += 64) {
@@ -175,7 +171,6 @@ __global__ __launch_bounds__(256) void w2_bid_kernel(const float* __restrict__ C
     }
   }
   if (lane == 0) {
-    const double eps = ctl->eps;
     const double inc = (n > 1 ? v1 - v2 : 0.0) + eps;
     float f = (float)inc;
     if ((double)f > inc) f = nextafterf(f, 0.f);  // round down: keeps eps-CS
@@ -186,7 +181,38 @@ __global__ __launch_bounds__(256) void w2_bid_kernel(const float* __restrict__ C
   }
 }
 
-// One thread per column: award the column to its highest bidder.
+// Waves stride over the slots; only slots unassigned in the current epoch bid.
+__global__ __launch_bounds__(256) void w2_bid_kernel(const float* __restrict__ C, int64_t ldc,
+                                                     int64_t n, int64_t R, W2Ws w) {
+  const W2Ctl* ctl = w.ctl;
+  if (ctl->done) return;
+  const int lane = threadIdx.x & 63;
+  const int ep = ctl->epoch;
+  const double eps = ctl->eps;
+  for (int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); s < n;
+       s += (int64_t)gridDim.x * 4) {
+    if (w.assigned_ep[s] == ep && w.assigned[s] >= 0) continue;
+    bid_slot(C + (s / R) * ldc, n, s, lane, eps, w);
+  }
+}
+
+__device__ void w2_control(W2Ctl* ctl, int64_t n) {
+  ctl->rounds += 1;
+  if (__hip_atomic_load(&ctl->unassigned, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  if (ctl->eps <= ctl->eps_final) {
+    ctl->done = 1;
+    return;
+  }
+  ctl->eps = fmax(ctl->eps / kTheta, ctl->eps_final);
+  ctl->epoch += 1;
+  ctl->phases += 1;
+  ctl->unassigned = (unsigned long long)n;
+}
+
+// One thread per column: award the column to its highest bidder; the last
+// block to arrive runs the control step (release/acquire ticket,
+// cdna_hip_programming.md Guideline 16).  `done` is uniform over the grid:
+// only the last arriver writes it, after every block has read it.
 __global__ __launch_bounds__(256) void w2_resolve_kernel(int64_t n, W2Ws w) {
   W2Ctl* ctl = w.ctl;
   if (ctl->done) return;
@@ -213,21 +239,22 @@ __global__ __launch_bounds__(256) void w2_resolve_kernel(int64_t n, W2Ws w) {
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) gained += __shfl_xor(gained, o, 64);
-  if ((threadIdx.x & 63) == 0 && gained) atomicAdd(&ctl->unassigned, (unsigned long long)(-(long long)gained));
-}
-
-__global__ void w2_control_kernel(W2Ctl* ctl, int64_t n) {
-  if (ctl->done) return;
-  ctl->rounds += 1;
-  if (ctl->unassigned != 0) return;
-  if (ctl->eps <= ctl->eps_final) {
-    ctl->done = 1;
-    return;
+  if ((threadIdx.x & 63) == 0 && gained)
+    atomicAdd(&ctl->unassigned, (unsigned long long)(-(long long)gained));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t =
+        __hip_atomic_fetch_add(&ctl->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == gridDim.x - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ctl->ticket = 0;
+      w2_control(ctl, n);
+    }
   }
-  ctl->eps = fmax(ctl->eps / kTheta, ctl->eps_final);
-  ctl->epoch += 1;
-  ctl->phases += 1;
-  ctl->unassigned = (unsigned long long)n;
 }
 
 __global__ __launch_bounds__(256) void w2_emit_kernel(int64_t n, W2Ws w, int32_t* assign) {
@@ -292,26 +319,52 @@ int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
   hipLaunchKernelGGL(w2_start_kernel, dim3(1), dim3(1), 0, s, w.ctl, n);
   int rc = check_launch("w2_start");
   if (rc) return rc;
-  const dim3 gb((unsigned)((n + 3) / 4)), gr((unsigned)((n + 255) / 256));
+  const dim3 gb((unsigned)std::min<int64_t>(kBidBlocks, (n + 3) / 4));
+  const dim3 gr((unsigned)((n + 255) / 256));
+  // pinned, double-buffered control readback (one pair per host thread)
+  static thread_local W2Ctl* hbuf = nullptr;
+  if (!hbuf && hipHostMalloc((void**)&hbuf, 2 * sizeof(W2Ctl), hipHostMallocDefault) != hipSuccess) {
+    hbuf = nullptr;
+    return check_launch("w2 pinned control buffer");
+  }
+  hipEvent_t ev[2];
+  if (hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) != hipSuccess)
+    return check_launch("w2 events");
   W2Ctl h{};
-  for (int64_t launched = 0;;) {
+  rc = 0;
+  for (int64_t batch = 0;; ++batch) {
     for (int b = 0; b < kRoundBatch; ++b) {
       hipLaunchKernelGGL(w2_bid_kernel, gb, dim3(256), 0, s, C, ldc, n, R, w);
       hipLaunchKernelGGL(w2_resolve_kernel, gr, dim3(256), 0, s, n, w);
-      hipLaunchKernelGGL(w2_control_kernel, dim3(1), dim3(1), 0, s, w.ctl, n);
     }
-    launched += kRoundBatch;
-    if ((rc = check_launch("w2 auction round"))) return rc;
-    if (hipMemcpyAsync(&h, w.ctl, sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-      return check_launch("w2 control readback");
+    W2Ctl* slot = hbuf + (batch & 1);
+    if ((rc = check_launch("w2 auction round")) ||
+        hipMemcpyAsync(slot, w.ctl, sizeof(W2Ctl), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipEventRecord(ev[batch & 1], s) != hipSuccess) {
+      rc = rc ? rc : check_launch("w2 control readback");
+      break;
+    }
+    if (batch == 0) continue;  // keep one batch queued ahead of the poll
+    if (hipEventSynchronize(ev[(batch - 1) & 1]) != hipSuccess) {
+      rc = check_launch("w2 control readback");
+      break;
+    }
+    h = hbuf[(batch - 1) & 1];
     if (h.done) break;
-    if (launched >= max_rounds) {
+    if ((batch - 1) * kRoundBatch >= max_rounds) {
       set_error("dsvgd_w2_assign: no convergence after %lld rounds (%lld phases, %llu unassigned)",
-                (long long)launched, (long long)h.phases, (unsigned long long)h.unassigned);
-      return -3;
+                (long long)h.rounds, (long long)h.phases, (unsigned long long)h.unassigned);
+      rc = -3;
+      break;
     }
   }
+  // the batch queued after the poll is a no-op once done is set; make the
+  // pinned slots quiescent before the next call reuses them
+  if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = check_launch("w2 drain");
+  (void)hipEventDestroy(ev[0]);
+  (void)hipEventDestroy(ev[1]);
+  if (rc) return rc;
   if (h.done == 3) {
     set_error("dsvgd_w2_assign: non-finite or negative cost");
     return -2;

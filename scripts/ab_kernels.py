@@ -45,8 +45,9 @@ def main():
     eng.pack(X, S)
     eng.distances(median=True)
     eng.median_bandwidth()
-    variants = {"nn=w1": {"DSVGD_NN_SHAPE": "w1"}, "nn=w2": {"DSVGD_NN_SHAPE": "w2"},
-                "nn=b64": {"DSVGD_NN_SHAPE": "b64"}, "nn=w2t": {"DSVGD_NN_SHAPE": "w2t"}}
+    variants = json.loads(os.environ.get("AB_VARIANTS", "null")) or {
+        "nn=w1": {"DSVGD_NN_SHAPE": "w1"}, "nn=w2": {"DSVGD_NN_SHAPE": "w2"},
+        "nn=b64": {"DSVGD_NN_SHAPE": "b64"}, "nn=w2t": {"DSVGD_NN_SHAPE": "w2t"}}
     res = {k: [] for k in variants}
     ref = None
     for _ in range(args.rounds):
@@ -55,7 +56,7 @@ def main():
             res[name].append(timed(lambda: eng.direction(write_phi=True)))
             if ref is None:
                 ref = eng.phi.clone()
-            else:
+            elif not env.get("NOCHECK"):
                 err = float((eng.phi - ref).abs().max() / ref.abs().max())
                 assert err < 1e-5, (name, err)
     flops = 4.0 * n * n * d

@@ -1,0 +1,57 @@
+"""Time the GPU W2/JKO term (dsvgd.w2.W2Term.grad: cost + auction + gradient)
+on random and SVGD-shaped inputs.
+
+    python scripts/w2_timing.py [--big]
+
+SVGD shape: the owned block X (m rows) against previous particles of which
+the first m rows are X before a small step (all_particles / all_scores mode
+with R = n/m ranks) -- the structure make_step hands to the term.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dist-svgd_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def case(m, n, d, kind, seed=0):
+    import dsvgd
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    X = torch.randn(m, d, generator=g)
+    if kind == "random":
+        P = torch.randn(n, d, generator=g)
+    else:   # svgd: own rows moved by a small step, other rows other ranks' particles
+        P = torch.randn(n, d, generator=g)
+        P[:m] = X - 1e-3 * torch.randn(m, d, generator=g)
+    X, P = X.cuda(), P.cuda()
+    w = dsvgd.w2.W2Term(m, n, d, "cuda:0")
+    w.grad(X, P, 1.0)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    w.grad(X, P, 1.0)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) * 1e3
+    return {"m": m, "n": n, "d": d, "kind": kind, "ms": round(ms, 3), "rounds": w.rounds,
+            "us_per_round": round(ms * 1e3 / max(w.rounds, 1), 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--big", action="store_true")
+    args = ap.parse_args()
+    shapes = [(256, 256, 16, "random"), (2048, 2048, 64, "random"), (500, 4000, 3, "random"),
+              (1024, 8192, 16, "svgd"), (4096, 4096, 256, "svgd"), (2048, 16384, 256, "svgd")]
+    if args.big:
+        shapes += [(8192, 65536, 256, "svgd"), (65536, 65536, 256, "svgd")]
+    for s in shapes:
+        print(json.dumps(case(*s)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
