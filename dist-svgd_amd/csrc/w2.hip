@@ -9,9 +9,15 @@
 // the LP's vertices are integral: the optimum is an assignment of n "slots"
 // (slot s belongs to row s / R) to the n columns, each carrying mass 1/n.
 //
-// Solver: forward auction (Bertsekas) with epsilon scaling, Jacobi bidding.
-//   * one wave per unassigned slot scans its cost row: best / second-best of
-//     -C_sj - p_j (prices in fp64), bids  p_j + (v1 - v2 + eps)  on the best;
+// Solver: forward auction (Bertsekas) with epsilon scaling, Jacobi bidding,
+// rows bidding as classes of R identical "similar persons":
+//   * one wave per row with u > 0 free slots scans its cost row for the
+//     u + 1 best values v_k of -C_ij - p_j (prices in fp64) over the columns
+//     the row does not already hold, and its free slots bid
+//     p_jk + (v_k - v_{u+1} + eps) on the u best.  Excluding the row's own
+//     columns is what stops sibling slots (identical cost rows) from
+//     outbidding each other by eps -- the price war that makes slot-level
+//     bidding take 5-50x more rounds when R > 1;
 //   * bids are resolved with one 64-bit atomicMax per bid, key =
 //     (fp32 increment rounded down) << 32 | slot, so a round's outcome does
 //     not depend on scheduling (ties go to the higher slot id);
@@ -48,19 +54,28 @@ constexpr double kTheta = 8.0;
 constexpr int kRoundBatch = 16;
 constexpr int kBidBlocks = 1024;  // grid-stride bid kernel: 4096 waves
 
+// holder[j] = epoch tag << 21 | row holding column j (tag = epoch & 0x7ff,
+// never 0: stale entries of earlier phases and the zeroed workspace read as
+// "not held"); owner[j] = the holding slot.
+constexpr int kRowBits = 21;
+constexpr int64_t kMaxRows = (int64_t)1 << kRowBits;
+constexpr int kMaxR = 32;
+__device__ __forceinline__ uint32_t w2_tag(int ep) { return (uint32_t)(ep & 0x7ff) << kRowBits; }
+
 struct W2Ws {
   W2Ctl* ctl;
   double* price;
   unsigned long long* bid;
-  int32_t *owner, *owner_ep, *assigned, *assigned_ep;
+  int32_t *owner, *assigned, *assigned_ep;
+  uint32_t* holder;
   W2Ws(void* ws, int64_t n) {
     char* p = (char*)ws;
     ctl = (W2Ctl*)p;
     price = (double*)(p + kW2CtlBytes);
     bid = (unsigned long long*)(price + n);
     owner = (int32_t*)(bid + n);
-    owner_ep = owner + n;
-    assigned = owner_ep + n;
+    holder = (uint32_t*)(owner + n);
+    assigned = (int32_t*)(holder + n);
     assigned_ep = assigned + n;
   }
 };
@@ -142,57 +157,117 @@ __global__ void w2_start_kernel(W2Ctl* ctl, int64_t n) {
   if (ctl->done == 0 && !(cmax > 0.0)) ctl->done = 2;
 }
 
-// One slot's bid: best / second-best of -C_sj - p_j over its cost row.
-__device__ __forceinline__ void bid_slot(const float* __restrict__ row, int64_t n, int64_t s,
-                                         int lane, double eps, const W2Ws& w) {
-  double v1 = -DBL_MAX, v2 = -DBL_MAX;
-  int j1 = INT32_MAX;
-  for (int64_t j = lane; j < n; j += 64) {
-    const double v = -(double)row[j] - w.price[j];
-    if (v > v1) {
-      v2 = v1;
-      v1 = v;
-      j1 = (int)j;
-    } else if (v > v2) {
-      v2 = v;
-    }
-  }
-  // wave top-2 (ties in v1 resolved to the lower column; then v2 == v1)
+// A lane's K best (value, column) pairs, sorted descending; ties keep the
+// lower column (a lane sees its columns in increasing order).
+template <int K>
+struct TopK {
+  double v[K];
+  int j[K];
+  __device__ __forceinline__ void init() {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double ov1 = __shfl_xor(v1, o, 64), ov2 = __shfl_xor(v2, o, 64);
-    const int oj1 = __shfl_xor(j1, o, 64);
-    if (ov1 > v1 || (ov1 == v1 && oj1 < j1)) {
-      v2 = fmax(v1, ov2);
-      v1 = ov1;
-      j1 = oj1;
-    } else {
-      v2 = fmax(v2, ov1);
+    for (int k = 0; k < K; ++k) {
+      v[k] = -DBL_MAX;
+      j[k] = INT32_MAX;
     }
   }
-  if (lane == 0) {
-    const double inc = (n > 1 ? v1 - v2 : 0.0) + eps;
-    float f = (float)inc;
-    if ((double)f > inc) f = nextafterf(f, 0.f);  // round down: keeps eps-CS
-    if (!(f > 0.f)) f = FLT_MIN;
-    const unsigned long long key =
-        ((unsigned long long)__float_as_uint(f) << 32) | (unsigned long long)(uint32_t)s;
-    atomicMax(&w.bid[j1], key);
+  __device__ __forceinline__ void push(double x, int c) {
+    if (!(x > v[K - 1])) return;
+#pragma unroll
+    for (int k = K - 1; k > 0; --k) {
+      const bool up = x > v[k - 1];
+      const bool here = x > v[k];
+      j[k] = up ? j[k - 1] : (here ? c : j[k]);
+      v[k] = up ? v[k - 1] : (here ? x : v[k]);
+    }
+    if (x > v[0]) {
+      v[0] = x;
+      j[0] = c;
+    }
   }
+  __device__ __forceinline__ void pop() {
+#pragma unroll
+    for (int k = 0; k < K - 1; ++k) {
+      v[k] = v[k + 1];
+      j[k] = j[k + 1];
+    }
+    v[K - 1] = -DBL_MAX;
+    j[K - 1] = INT32_MAX;
+  }
+};
+
+// Row i's bid: its u free slots (bit r of `free` = slot iR + r) bid on the
+// u best columns the row does not hold, each at v_k - v_{u+1} + eps.
+template <int K>
+__device__ __forceinline__ void bid_row(const float* __restrict__ row, int64_t n, int64_t i,
+                                        int64_t R, unsigned long long free, int lane, double eps,
+                                        uint32_t tag, const W2Ws& w) {
+  const int u = __popcll(free);
+  TopK<K> t;
+  t.init();
+  const uint32_t mine = tag | (uint32_t)i;
+  for (int64_t j = lane; j < n; j += 64) {
+    if (w.holder[j] == mine) continue;
+    t.push(-(double)row[j] - w.price[j], (int)j);
+  }
+  // wave merge: extract the u + 1 best in order (ties -> lower column); the
+  // k-th lands in lane k's (kv, kj)
+  double kv = -DBL_MAX;
+  int kj = INT32_MAX;
+  for (int k = 0; k <= u; ++k) {
+    double bv = t.v[0];
+    int bj = t.j[0];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ov = __shfl_xor(bv, o, 64);
+      const int oj = __shfl_xor(bj, o, 64);
+      if (ov > bv || (ov == bv && oj < bj)) {
+        bv = ov;
+        bj = oj;
+      }
+    }
+    if (lane == k) {
+      kv = bv;
+      kj = bj;
+    }
+    if (t.j[0] == bj) t.pop();
+  }
+  // v_{u+1}; if the row has no (u+1)-th alternative, price against the u-th
+  const double vu1 = __shfl(kv, u, 64), vu = __shfl(kv, u - 1, 64);
+  const double vref = (vu1 > -DBL_MAX) ? vu1 : vu;
+  if (lane >= u || kj == INT32_MAX) return;
+  // lane k bids for the k-th free slot of the row
+  unsigned long long rest = free;
+  for (int k = 0; k < lane; ++k) rest &= rest - 1;
+  const int64_t s = i * R + (__ffsll((long long)rest) - 1);
+  const double inc = kv - vref + eps;
+  float f = (float)inc;
+  if ((double)f > inc) f = nextafterf(f, 0.f);  // round down: keeps eps-CS
+  if (!(f > 0.f)) f = FLT_MIN;
+  const unsigned long long key =
+      ((unsigned long long)__float_as_uint(f) << 32) | (unsigned long long)(uint32_t)s;
+  atomicMax(&w.bid[kj], key);
 }
 
-// Waves stride over the slots; only slots unassigned in the current epoch bid.
+// Waves stride over the rows; rows with free slots in this epoch bid.
+template <int K>
 __global__ __launch_bounds__(256) void w2_bid_kernel(const float* __restrict__ C, int64_t ldc,
-                                                     int64_t n, int64_t R, W2Ws w) {
+                                                     int64_t m, int64_t n, int64_t R, W2Ws w) {
   const W2Ctl* ctl = w.ctl;
   if (ctl->done) return;
   const int lane = threadIdx.x & 63;
   const int ep = ctl->epoch;
   const double eps = ctl->eps;
-  for (int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); s < n;
-       s += (int64_t)gridDim.x * 4) {
-    if (w.assigned_ep[s] == ep && w.assigned[s] >= 0) continue;
-    bid_slot(C + (s / R) * ldc, n, s, lane, eps, w);
+  const uint32_t tag = w2_tag(ep);
+  for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < m;
+       i += (int64_t)gridDim.x * 4) {
+    bool fr = false;
+    if (lane < R) {
+      const int64_t s = i * R + lane;
+      fr = !(w.assigned_ep[s] == ep && w.assigned[s] >= 0);
+    }
+    const unsigned long long free = __ballot(fr);
+    if (free == 0) continue;
+    bid_row<K>(C + i * ldc, n, i, R, free, lane, eps, tag, w);
   }
 }
 
@@ -213,7 +288,7 @@ __device__ void w2_control(W2Ctl* ctl, int64_t n) {
 // block to arrive runs the control step (release/acquire ticket,
 // cdna_hip_programming.md Guideline 16).  `done` is uniform over the grid:
 // only the last arriver writes it, after every block has read it.
-__global__ __launch_bounds__(256) void w2_resolve_kernel(int64_t n, W2Ws w) {
+__global__ __launch_bounds__(256) void w2_resolve_kernel(int64_t n, int64_t R, W2Ws w) {
   W2Ctl* ctl = w.ctl;
   if (ctl->done) return;
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -225,14 +300,16 @@ __global__ __launch_bounds__(256) void w2_resolve_kernel(int64_t n, W2Ws w) {
       const int s = (int)(uint32_t)b;
       const float inc = __uint_as_float((uint32_t)(b >> 32));
       const int ep = ctl->epoch;
+      const uint32_t tag = w2_tag(ep);
       w.price[j] += (double)inc;
-      const int old = (w.owner_ep[j] == ep) ? w.owner[j] : -1;
+      const uint32_t h = w.holder[j];
+      const int old = ((h & ~(uint32_t)(kMaxRows - 1)) == tag) ? w.owner[j] : -1;
       if (old >= 0)
         w.assigned[old] = -1;  // displaced: bids again next round
       else
         gained = 1;
       w.owner[j] = s;
-      w.owner_ep[j] = ep;
+      w.holder[j] = tag | (uint32_t)(s / R);
       w.assigned[s] = (int)j;
       w.assigned_ep[s] = ep;
     }
@@ -307,6 +384,8 @@ int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
   DSVGD_REQUIRE(m > 0 && n > 0 && ldc >= n, "sizes");
   DSVGD_REQUIRE(n % m == 0, "n must be a multiple of m (n = R m slots)");
   DSVGD_REQUIRE(n <= INT32_MAX - 1, "n too large for 32-bit slot ids");
+  DSVGD_REQUIRE(m < kMaxRows, "m too large (2^21 rows)");
+  DSVGD_REQUIRE(n / m <= kMaxR, "n / m must be <= 32 (slots per row)");
   DSVGD_REQUIRE(max_rounds > 0, "max_rounds");
   hipStream_t s = (hipStream_t)stream;
   W2Ws w(ws, n);
@@ -319,7 +398,21 @@ int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
   hipLaunchKernelGGL(w2_start_kernel, dim3(1), dim3(1), 0, s, w.ctl, n);
   int rc = check_launch("w2_start");
   if (rc) return rc;
-  const dim3 gb((unsigned)std::min<int64_t>(kBidBlocks, (n + 3) / 4));
+  const dim3 gb((unsigned)std::min<int64_t>(kBidBlocks, (m + 3) / 4));
+  auto bid = [&]() {
+    if (R <= 1)
+      hipLaunchKernelGGL(w2_bid_kernel<2>, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
+    else if (R <= 2)
+      hipLaunchKernelGGL(w2_bid_kernel<3>, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
+    else if (R <= 4)
+      hipLaunchKernelGGL(w2_bid_kernel<5>, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
+    else if (R <= 8)
+      hipLaunchKernelGGL(w2_bid_kernel<9>, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
+    else if (R <= 16)
+      hipLaunchKernelGGL(w2_bid_kernel<17>, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
+    else
+      hipLaunchKernelGGL(w2_bid_kernel<33>, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
+  };
   const dim3 gr((unsigned)((n + 255) / 256));
   // pinned, double-buffered control readback (one pair per host thread)
   static thread_local W2Ctl* hbuf = nullptr;
@@ -335,8 +428,8 @@ int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
   rc = 0;
   for (int64_t batch = 0;; ++batch) {
     for (int b = 0; b < kRoundBatch; ++b) {
-      hipLaunchKernelGGL(w2_bid_kernel, gb, dim3(256), 0, s, C, ldc, n, R, w);
-      hipLaunchKernelGGL(w2_resolve_kernel, gr, dim3(256), 0, s, n, w);
+      bid();
+      hipLaunchKernelGGL(w2_resolve_kernel, gr, dim3(256), 0, s, n, R, w);
     }
     W2Ctl* slot = hbuf + (batch & 1);
     if ((rc = check_launch("w2 auction round")) ||

@@ -50,8 +50,11 @@ def main():
         "nn=b64": {"DSVGD_NN_SHAPE": "b64"}, "nn=w2t": {"DSVGD_NN_SHAPE": "w2t"}}
     res = {k: [] for k in variants}
     ref = None
+    keys = {k for env in variants.values() for k in env}
     for _ in range(args.rounds):
         for name, env in variants.items():
+            for k in keys:               # a variant's knobs must not leak into the next
+                os.environ.pop(k, None)
             os.environ.update(env)
             res[name].append(timed(lambda: eng.direction(write_phi=True)))
             if ref is None:

@@ -46,7 +46,8 @@ def main():
     ap.add_argument("--big", action="store_true")
     args = ap.parse_args()
     shapes = [(256, 256, 16, "random"), (2048, 2048, 64, "random"), (500, 4000, 3, "random"),
-              (1024, 8192, 16, "svgd"), (4096, 4096, 256, "svgd"), (2048, 16384, 256, "svgd")]
+              (1024, 8192, 16, "svgd"), (4096, 4096, 256, "svgd"), (2048, 16384, 256, "svgd"),
+              (4096, 32768, 64, "svgd")]
     if args.big:
         shapes += [(8192, 65536, 256, "svgd"), (65536, 65536, 256, "svgd")]
     for s in shapes:

@@ -368,14 +368,20 @@ def test_w2_grad_matches_reference_lp(golden, name):
 @pytest.mark.parametrize("m,n,d,near", [(256, 256, 16, None), (512, 1024, 8, None),
                                         (500, 4000, 3, None), (2048, 2048, 64, None),
                                         (1024, 1024, 32, 0.05), (1024, 4096, 8, 0.01),
-                                        (3000, 3000, 2, 0.2)])
+                                        (3000, 3000, 2, 0.2), (64, 1024, 8, None),
+                                        (32, 1024, 4, None), (512, 4096, 16, "svgd")])
 def test_w2_assignment_optimal(m, n, d, near):
     """Plan == scipy's exact assignment on the fp64 costs (random inputs: no
-    near-ties at these sizes), and the gradient within PHI_TOL."""
+    near-ties at these sizes), and the gradient within PHI_TOL.  R = n/m up to
+    32; "svgd": the owned rows' previous copies (all_particles mode) plus
+    other ranks' particles."""
     rs = np.random.RandomState(m + n + d)
     X = rs.randn(m, d).astype(np.float32)
     if near is None:
         P = rs.randn(n, d).astype(np.float32)
+    elif near == "svgd":
+        P = rs.randn(n, d).astype(np.float32)
+        P[:m] = X - 1e-3 * rs.randn(m, d).astype(np.float32)
     else:
         P = (np.tile(X, (n // m, 1)) + near * rs.randn(n, d)).astype(np.float32)
     G, plan, w = _w2_gpu(X, P, h=2.5)
@@ -576,3 +582,46 @@ def test_distsampler_two_ranks_jacobi_vs_oracle(golden, name):
             own, full, start = out[step]
             assert start == D.start[rank]
             assert abs_err(own, D.own(rank)) < TRAJ_TOL
+
+
+# ------------------------------------ logreg: test accuracy after T steps --
+def _banana_like(N, p=2, seed=0, w_seed=1, noise_seed=2):
+    """Synthetic stand-in for benchmarks.mat 'banana' (an LFS pointer in the
+    reference): x ~ N(0, I), t = sign(x.w* + logistic noise)."""
+    x = np.random.RandomState(seed).randn(N, p).astype(np.float32)
+    w = np.random.RandomState(w_seed).randn(p)
+    z = x @ w + np.random.RandomState(noise_seed).logistic(size=N)
+    return x, np.where(z > 0, 1.0, -1.0).astype(np.float32)
+
+
+@pytest.mark.parametrize("order,n,T", [("sequential", 100, 100), ("jacobi", 1024, 100)])
+def test_logreg_test_accuracy_after_T_steps(order, n, T):
+    """experiments/logreg.py config A (S = 1, partitions, eps = 1e-3, h = 10,
+    rank-0 reference init) for T steps: particles vs the oracle, then the
+    posterior mean / variance and the posterior-predictive test accuracy of
+    logreg_plots.py:42-50 on 4900 held-out points."""
+    x, t = _banana_like(400)
+    x_test, t_test = _banana_like(4900, seed=10, noise_seed=12)
+    X0 = O.ref_init(n, 3, 0)
+    ds = dsvgd().DistSampler(0, 1, dsvgd().targets.LogisticRegression(x, t), dsvgd().RBF(1.0),
+                             torch.tensor(X0), 400, 400, exchange_particles=False,
+                             exchange_scores=False, include_wasserstein=False, order=order)
+    for _ in range(T):
+        ds.make_step(1e-3, h=10.0)
+    got = ds.particles.numpy().astype(np.float64)
+    fn = lambda X: O.score_logreg(X, x, t)  # noqa: E731
+    D = O.DistOracle([X0], [fn], 400, 400, False, False, sequential=order == "sequential")
+    for _ in range(T):
+        D.step(1e-3)
+    ref = D.own(0)
+    err = abs_err(got, ref)
+    assert err < 1e-3, err
+    # posterior mean / variance of the weights: same algorithm, so far inside MC error
+    se = np.sqrt(ref[:, 1:].var(0) / n)
+    assert np.all(np.abs(got[:, 1:].mean(0) - ref[:, 1:].mean(0)) < 0.01 * se + 1e-5)
+    assert np.all(np.abs(got[:, 1:].var(0) / ref[:, 1:].var(0) - 1) < 1e-3)
+    acc_gpu = O.test_accuracy(got, x_test, t_test)
+    acc_ref = O.test_accuracy(ref, x_test, t_test)
+    record_parity(err, acc_gpu=acc_gpu, acc_oracle=acc_ref)
+    assert abs(acc_gpu - acc_ref) <= 0.01
+    assert acc_gpu > 0.6        # the posterior predicts (chance is ~0.5)
