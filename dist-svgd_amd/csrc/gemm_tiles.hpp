@@ -163,7 +163,7 @@ struct NNTile {
 
   f32x16 acc[TM][TN];
   f32x4 ra[LA], rb[LB];
-  float rsum[TM];
+  float rs[LA];  // EXP: row-sum partials of the rows this thread stages
 
   __device__ __forceinline__ void load(const float* __restrict__ Apanels, const float* __restrict__ B,
                                        int64_t ldb, int64_t j0) {
@@ -191,13 +191,26 @@ struct NNTile {
     }
   }
 
-  __device__ __forceinline__ void store(float* st) {
+  // EXP: the staging thread turns its 4 D values into k = exp2(D * scale)
+  // once (not once per reading wave), skips the diagonal and accumulates the
+  // row-sum partial.  dgl = (global row of the block's row 0) - (global
+  // column of this K-step's column 0): the diagonal k_ii is left out (phi_finish
+  // adds the self term exactly) so no accumulator carries the O(1) self term
+  // while it sums ~n tiny off-diagonal terms.
+  __device__ __forceinline__ void store(float* st, float scale, int64_t dgl) {
     const int t = threadIdx.x;
     float* sA = st;
     float* sB = st + SA;
 #pragma unroll
     for (int u = 0; u < LA; ++u) {
       const int f = t + u * kThreads, row = f >> 2, c4 = f & 3;
+      if (EXP) {
+        const int64_t qd = dgl + row - 4 * c4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          ra[u][q] = (qd == q) ? 0.f : __builtin_amdgcn_exp2f(ra[u][q] * scale);
+        rs[u] += (ra[u][0] + ra[u][1]) + (ra[u][2] + ra[u][3]);
+      }
       *reinterpret_cast<f32x4*>(sA + row * LDA + 4 * c4) = ra[u];
     }
     if (BT) {
@@ -218,12 +231,7 @@ struct NNTile {
     }
   }
 
-  // dgl = (global row of this block's row 0) - (global column of this K-step's
-  // column 0): the diagonal k_ii is skipped (EXP only; phi_finish adds the
-  // self term exactly) so no accumulator carries the O(1) self term while it
-  // sums ~n tiny off-diagonal terms (fp32 rounding at the large magnitude).
-  __device__ __forceinline__ void compute(const float* st, int wr, int wc, float scale,
-                                          int64_t dgl) {
+  __device__ __forceinline__ void compute(const float* st, int wr, int wc) {
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
     const float* sA = st + (wr * 32 * TM) * LDA;
     const float* sB = st + SA;
@@ -231,16 +239,8 @@ struct NNTile {
     for (int g = 0; g < BJ / 8; ++g) {
       f32x4 a[TM];
 #pragma unroll
-      for (int mi = 0; mi < TM; ++mi) {
+      for (int mi = 0; mi < TM; ++mi)
         a[mi] = *reinterpret_cast<const f32x4*>(sA + (mi * 32 + r) * LDA + 8 * g + 4 * h);
-        if (EXP) {
-          const int64_t qd = dgl + wr * 32 * TM + mi * 32 + r - 8 * g - 4 * h;
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            a[mi][q] = (qd == q) ? 0.f : __builtin_amdgcn_exp2f(a[mi][q] * scale);
-          rsum[mi] += (a[mi][0] + a[mi][1]) + (a[mi][2] + a[mi][3]);
-        }
-      }
       if (BT) {
         f32x4 b4[TN];
 #pragma unroll
@@ -278,26 +278,36 @@ struct NNTile {
                                       float* smem, int64_t row_g0 = INT64_MIN / 2) {
     const int w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
 #pragma unroll
-    for (int mi = 0; mi < TM; ++mi) {
-      rsum[mi] = 0.f;
+    for (int u = 0; u < LA; ++u) rs[u] = 0.f;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni)
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[mi][ni][q] = 0.f;
-    }
     if (k0 >= k1) return;
     load(Apanels, B, ldb, k0);
-    store(smem);
+    store(smem, scale, row_g0 - k0);
     __syncthreads();
     int cur = 0;
     for (int64_t j0 = k0; j0 < k1; j0 += BJ) {
       const bool more = j0 + BJ < k1;
       if (more) load(Apanels, B, ldb, j0 + BJ);
-      compute(smem + cur * kStage, wr, wc, scale, row_g0 - j0);
-      if (more) store(smem + (cur ^ 1) * kStage);
+      compute(smem + cur * kStage, wr, wc);
+      if (more) store(smem + (cur ^ 1) * kStage, scale, row_g0 - (j0 + BJ));
       __syncthreads();
       cur ^= 1;
     }
+  }
+
+  // EXP: the full row sum of staged row (f >> 2), f = t + u * kThreads, is the
+  // sum over the 4 consecutive lanes staging that row; returns it on every
+  // lane (valid where (f & 3) == 0 is the writer).
+  __device__ __forceinline__ float row_sum(int u) const {
+    float v = rs[u];
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    return v;
   }
 };
 

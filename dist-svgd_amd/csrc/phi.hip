@@ -18,7 +18,7 @@ namespace dsvgd {
 // the partial C + z*m*ldc (and rowsum + z*m_pad); phi_finish sums the slices
 // in order (deterministic, no atomics).
 // row0: interacting-set index of A's row 0 (EXP: the diagonal j == row0 + i
-// is skipped, see NNTile::compute).
+// is skipped, see NNTile::store).
 template <int TN, bool EXP, int WM, int TM, bool BT>
 __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ A, int64_t a_npad,
                                                       const float* __restrict__ B, int64_t ldb,
@@ -54,12 +54,13 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
         if (row < m) C[row * ldc + col] = tile.acc[mi][ni][r];
       }
     }
-  if (EXP && rowsum && blockIdx.x == 0 && wc == 0) {
+  if (EXP && rowsum && blockIdx.x == 0) {
 #pragma unroll
-    for (int mi = 0; mi < Tile::TM; ++mi) {
-      const float v = tile.rsum[mi] + __shfl_xor(tile.rsum[mi], 32, 64);
-      const int64_t row = r0 + mi * 32 + lane;
-      if (lane < 32 && row < m) rowsum[row] = v;
+    for (int u = 0; u < Tile::LA; ++u) {
+      const int f = threadIdx.x + u * Tile::kThreads;
+      const float v = tile.row_sum(u);
+      const int64_t row = i0 + (f >> 2);
+      if ((f & 3) == 0 && row < m) rowsum[row] = v;
     }
   }
 }
