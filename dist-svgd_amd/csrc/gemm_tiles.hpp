@@ -165,10 +165,12 @@ struct NNTile {
   f32x4 ra[LA], rb[LB];
   float rs[LA];  // EXP: row-sum partials of the rows this thread stages
 
+  int64_t amask = -1;  // timing experiments only: A panel index mask (-1 = off)
+
   __device__ __forceinline__ void load(const float* __restrict__ Apanels, const float* __restrict__ B,
                                        int64_t ldb, int64_t j0) {
     const int t = threadIdx.x;
-    const float* ap = Apanels + (j0 >> 4) * kPanelElems;  // contiguous 8 KiB panel
+    const float* ap = Apanels + ((j0 >> 4) & amask) * kPanelElems;  // contiguous 8 KiB panel
 #pragma unroll
     for (int u = 0; u < LA; ++u) ra[u] = *reinterpret_cast<const f32x4*>(ap + 4 * (t + u * kThreads));
     if (BT) {

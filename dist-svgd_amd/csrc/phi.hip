@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
                                                       const dsvgd_select_state* __restrict__ st,
                                                       float* __restrict__ C, int64_t ldc,
                                                       float* __restrict__ rowsum, int64_t m,
-                                                      int64_t row0) {
+                                                      int64_t row0, int64_t amask) {
   using Tile = NNTile<TN, EXP, WM, TM, BT>;
   __shared__ __attribute__((aligned(16))) float smem[Tile::kSmemFloats];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
@@ -38,6 +38,7 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
   float scale = 0.f;
   if (EXP) scale = -st->inv_h * kLog2e;
   Tile tile;
+  tile.amask = amask;
   tile.run(A + (i0 >> 7) * (a_npad >> 4) * kPanelElems + (i0 & 127) * 16, B + c0, ldb, k0, k1,
            scale, smem, row0 + i0);
 
@@ -238,12 +239,17 @@ int launch_nn_shape(bool exp_, const float* A, const float* B, int64_t ldb, int6
   constexpr int BM = 32 * TM * WM;
   const int64_t kchunk = roundup((K + splits - 1) / splits, 16);
   const dim3 grid(cols / (128 * TN), roundup(m, BM) / BM, splits);
+  // DSVGD_NN_AMASK=<int>: TIMING EXPERIMENTS ONLY (wrong results) -- A panel
+  // index & mask, so blocks re-read a few L2-resident panels instead of
+  // streaming D from HBM (prices the HBM latency of the A operand).
+  const char* am = getenv("DSVGD_NN_AMASK");
+  const int64_t amask = am ? atoll(am) : -1;
   if (exp_)
     hipLaunchKernelGGL((nn_kernel<TN, true, WM, TM, BT>), grid, dim3(256 * WM), 0, s, A, K, B,
-                       ldb, K, kchunk, st, C, ldc, rowsum, m, row0);
+                       ldb, K, kchunk, st, C, ldc, rowsum, m, row0, amask);
   else
     hipLaunchKernelGGL((nn_kernel<TN, false, WM, TM, BT>), grid, dim3(256 * WM), 0, s, A, K, B,
-                       ldb, K, kchunk, st, C, ldc, rowsum, m, row0);
+                       ldb, K, kchunk, st, C, ldc, rowsum, m, row0, amask);
   return check_launch("nn_kernel");
 }
 
