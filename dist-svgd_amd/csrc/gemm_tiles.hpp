@@ -142,37 +142,65 @@ struct NTTile {
 // lane's 4 k-values of one column are one ds_read_b128 (8 per K-step instead
 // of 16 ds_read2_b32); each thread loads 4x4 blocks (4 rows x float4) and
 // writes their columns as float4s.
-template <int TN, bool EXP, int WM = 1, int TM_ = 4 / WM, bool BT = false>
+//
+// BJ_ = 32: 32-deep K-steps (two D panels per step: half the barriers and
+// LDS-read restarts per unit of work).  Double-buffered that is exactly
+// 2 x (16 KiB A + 64 KiB B) = 160 KiB, so the A image drops its row padding
+// and XOR-swizzles its 16-B chunks instead: chunk' = chunk ^ ((row >> 1) & 7)
+// keeps a ds_read_b128 lane group (16 rows, 2 per 64-bank line) conflict-free.
+template <int TN, bool EXP, int WM = 1, int TM_ = 4 / WM, bool BT = false, int BJ_ = 16>
 struct NNTile {
   static constexpr int kThreads = 256 * WM;
   static constexpr int TM = TM_;
   static constexpr int BM = 32 * TM * WM;
   static constexpr int BC = 128 * TN;
-  static constexpr int BJ = 16;
-  static constexpr int LDA = BJ + 4;  // 80-B rows: conflict-free ds_read_b128
+  static constexpr int BJ = BJ_;
+  static constexpr bool kSwz = BJ == 32;
+  static constexpr int LDA = kSwz ? BJ : BJ + 4;  // 16: 80-B rows (conflict-free b128)
   static constexpr int LDBT = BJ + 4;
   static constexpr int SA = BM * LDA;
   static constexpr int SB = BT ? BC * LDBT : BJ * BC;
   static constexpr int kStage = SA + SB;
   static constexpr int kSmemFloats = 2 * kStage;
   static constexpr int LA = BM * BJ / 4 / kThreads;
-  static constexpr int NB4 = BC;  // 4x4 blocks of a BJ x BC tile (BT)
+  static constexpr int RPT = BM * 4 / kThreads > 1 ? BM * 4 / kThreads : 1;  // rows per thread
+  static constexpr int NB4 = BC * BJ / 16;  // 4x4 blocks of a BJ x BC tile (BT)
   static constexpr int LB = BT ? 4 * ((NB4 + kThreads - 1) / kThreads) : BJ * BC / 4 / kThreads;
   static_assert(LA >= 1 && LB >= 1, "tile too small for the block");
   static_assert(BM == 64 || BM == 128, "BM must divide the 128-row panel");
+  static_assert(BJ == 16 || BJ == 32, "BJ is 16 or 32");
+  static_assert(!(kSwz && BT), "BJ = 32 uses the row-major B image");
+  static_assert(kSmemFloats * 4 <= 160 * 1024, "LDS budget");
 
   f32x16 acc[TM][TN];
   f32x4 ra[LA], rb[LB];
-  float rs[LA];  // EXP: row-sum partials of the rows this thread stages
+  float rs[RPT];  // EXP: row-sum partials of the rows this thread stages
+
+  // A image offset of (row, 16-B chunk)
+  __device__ __forceinline__ static int a_off(int row, int chunk) {
+    return row * LDA + 4 * (kSwz ? (chunk ^ ((row >> 1) & 7)) : chunk);
+  }
+  // staged A vector u of thread t: panel p (16 columns each), row, chunk in panel
+  __device__ __forceinline__ static void a_map(int t, int u, int& p, int& row, int& c4) {
+    const int f = t + u * kThreads;
+    p = f / (BM * 4);
+    const int fi = f % (BM * 4);
+    row = fi >> 2;
+    c4 = fi & 3;
+  }
 
   int64_t amask = -1;  // timing experiments only: A panel index mask (-1 = off)
 
   __device__ __forceinline__ void load(const float* __restrict__ Apanels, const float* __restrict__ B,
                                        int64_t ldb, int64_t j0) {
     const int t = threadIdx.x;
-    const float* ap = Apanels + ((j0 >> 4) & amask) * kPanelElems;  // contiguous 8 KiB panel
 #pragma unroll
-    for (int u = 0; u < LA; ++u) ra[u] = *reinterpret_cast<const f32x4*>(ap + 4 * (t + u * kThreads));
+    for (int u = 0; u < LA; ++u) {
+      int p, row, c4;
+      a_map(t, u, p, row, c4);
+      const float* ap = Apanels + (((j0 >> 4) + p) & amask) * kPanelElems;  // 8 KiB panel
+      ra[u] = *reinterpret_cast<const f32x4*>(ap + row * 16 + 4 * c4);
+    }
     if (BT) {
 #pragma unroll
       for (int u = 0; u < LB / 4; ++u) {
@@ -205,15 +233,17 @@ struct NNTile {
     float* sB = st + SA;
 #pragma unroll
     for (int u = 0; u < LA; ++u) {
-      const int f = t + u * kThreads, row = f >> 2, c4 = f & 3;
+      int p, row, c4;
+      a_map(t, u, p, row, c4);
+      const int chunk = 4 * p + c4;
       if (EXP) {
-        const int64_t qd = dgl + row - 4 * c4;
+        const int64_t qd = dgl + row - 4 * chunk;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           ra[u][q] = (qd == q) ? 0.f : __builtin_amdgcn_exp2f(ra[u][q] * scale);
-        rs[u] += (ra[u][0] + ra[u][1]) + (ra[u][2] + ra[u][3]);
+        rs[u % RPT] += (ra[u][0] + ra[u][1]) + (ra[u][2] + ra[u][3]);
       }
-      *reinterpret_cast<f32x4*>(sA + row * LDA + 4 * c4) = ra[u];
+      *reinterpret_cast<f32x4*>(sA + a_off(row, chunk)) = ra[u];
     }
     if (BT) {
 #pragma unroll
@@ -235,14 +265,14 @@ struct NNTile {
 
   __device__ __forceinline__ void compute(const float* st, int wr, int wc) {
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-    const float* sA = st + (wr * 32 * TM) * LDA;
+    const float* sA = st;
     const float* sB = st + SA;
 #pragma unroll
     for (int g = 0; g < BJ / 8; ++g) {
       f32x4 a[TM];
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi)
-        a[mi] = *reinterpret_cast<const f32x4*>(sA + (mi * 32 + r) * LDA + 8 * g + 4 * h);
+        a[mi] = *reinterpret_cast<const f32x4*>(sA + a_off(wr * 32 * TM + mi * 32 + r, 2 * g + h));
       if (BT) {
         f32x4 b4[TN];
 #pragma unroll
@@ -280,7 +310,7 @@ struct NNTile {
                                       float* smem, int64_t row_g0 = INT64_MIN / 2) {
     const int w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
 #pragma unroll
-    for (int u = 0; u < LA; ++u) rs[u] = 0.f;
+    for (int u = 0; u < RPT; ++u) rs[u] = 0.f;
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
@@ -302,9 +332,9 @@ struct NNTile {
     }
   }
 
-  // EXP: the full row sum of staged row (f >> 2), f = t + u * kThreads, is the
-  // sum over the 4 consecutive lanes staging that row; returns it on every
-  // lane (valid where (f & 3) == 0 is the writer).
+  // EXP: the full row sum of staged row a_map(t, u) (u < RPT) is the sum over
+  // the 4 consecutive lanes staging that row; returned on every lane (the
+  // lane with c4 == 0 is the writer).
   __device__ __forceinline__ float row_sum(int u) const {
     float v = rs[u];
     v += __shfl_xor(v, 1, 64);

@@ -9,6 +9,7 @@
 // Roofline: 2 * 128 * BC flop per 8 KiB D panel -> MFMA-bound for d >= 64.
 #include <cmath>
 #include <cstdlib>
+#include <string>
 
 #include "gemm_tiles.hpp"
 
@@ -19,7 +20,7 @@ namespace dsvgd {
 // in order (deterministic, no atomics).
 // row0: interacting-set index of A's row 0 (EXP: the diagonal j == row0 + i
 // is skipped, see NNTile::store).
-template <int TN, bool EXP, int WM, int TM, bool BT>
+template <int TN, bool EXP, int WM, int TM, bool BT, int BJ>
 __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ A, int64_t a_npad,
                                                       const float* __restrict__ B, int64_t ldb,
                                                       int64_t K, int64_t kchunk,
@@ -27,7 +28,7 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
                                                       float* __restrict__ C, int64_t ldc,
                                                       float* __restrict__ rowsum, int64_t m,
                                                       int64_t row0, int64_t amask) {
-  using Tile = NNTile<TN, EXP, WM, TM, BT>;
+  using Tile = NNTile<TN, EXP, WM, TM, BT, BJ>;
   __shared__ __attribute__((aligned(16))) float smem[Tile::kSmemFloats];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
@@ -57,11 +58,12 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
     }
   if (EXP && rowsum && blockIdx.x == 0) {
 #pragma unroll
-    for (int u = 0; u < Tile::LA; ++u) {
-      const int f = threadIdx.x + u * Tile::kThreads;
+    for (int u = 0; u < Tile::RPT; ++u) {
+      int p, rr, c4;
+      Tile::a_map(threadIdx.x, u, p, rr, c4);
       const float v = tile.row_sum(u);
-      const int64_t row = i0 + (f >> 2);
-      if ((f & 3) == 0 && row < m) rowsum[row] = v;
+      const int64_t row = i0 + rr;
+      if (c4 == 0 && row < m) rowsum[row] = v;
     }
   }
 }
@@ -223,21 +225,28 @@ __global__ __launch_bounds__(256) void phi_row_kernel(float* __restrict__ X, int
 //   "w2"  128 rows, 8 waves x 128 accumulators (1 block/CU, 2 waves/SIMD)
 //   "b64"  64 rows, 4 waves x 128 accumulators (2 blocks/CU)
 //   "w2t"  as w2 with the transposed B image (b128 B-fragment reads)
-enum NNShape { kW1, kW2, kB64, kW2T };
+//   "w2k"  as w2 with 32-deep K-steps (160 KiB LDS, swizzled A image)
+//   "w1k"  as w1 with 32-deep K-steps
+enum NNShape { kW1, kW2, kB64, kW2T, kW2K, kW1K };
 static NNShape nn_shape() {
   const char* e = getenv("DSVGD_NN_SHAPE");
-  if (e && e[0] == 'w' && e[1] == '1') return kW1;
-  if (e && e[0] == 'b') return kB64;
-  if (e && e[0] == 'w' && e[1] == '2' && e[2] == 't') return kW2T;
+  if (!e) return kW2;
+  const std::string v(e);
+  if (v == "w1") return kW1;
+  if (v == "b64") return kB64;
+  if (v == "w2t") return kW2T;
+  if (v == "w2k") return kW2K;
+  if (v == "w1k") return kW1K;
   return kW2;
 }
 
-template <int TN, int WM, int TM, bool BT = false>
+template <int TN, int WM, int TM, bool BT = false, int BJ = 16>
 int launch_nn_shape(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
                     const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
                     int64_t cols, int64_t row0, hipStream_t s) {
   constexpr int BM = 32 * TM * WM;
-  const int64_t kchunk = roundup((K + splits - 1) / splits, 16);
+  if (K % BJ != 0) return fail_arg("nn_kernel: K must be a multiple of the K-step");
+  const int64_t kchunk = roundup((K + splits - 1) / splits, BJ);
   const dim3 grid(cols / (128 * TN), roundup(m, BM) / BM, splits);
   // DSVGD_NN_AMASK=<int>: TIMING EXPERIMENTS ONLY (wrong results) -- A panel
   // index & mask, so blocks re-read a few L2-resident panels instead of
@@ -245,10 +254,10 @@ int launch_nn_shape(bool exp_, const float* A, const float* B, int64_t ldb, int6
   const char* am = getenv("DSVGD_NN_AMASK");
   const int64_t amask = am ? atoll(am) : -1;
   if (exp_)
-    hipLaunchKernelGGL((nn_kernel<TN, true, WM, TM, BT>), grid, dim3(256 * WM), 0, s, A, K, B,
+    hipLaunchKernelGGL((nn_kernel<TN, true, WM, TM, BT, BJ>), grid, dim3(256 * WM), 0, s, A, K, B,
                        ldb, K, kchunk, st, C, ldc, rowsum, m, row0, amask);
   else
-    hipLaunchKernelGGL((nn_kernel<TN, false, WM, TM, BT>), grid, dim3(256 * WM), 0, s, A, K, B,
+    hipLaunchKernelGGL((nn_kernel<TN, false, WM, TM, BT, BJ>), grid, dim3(256 * WM), 0, s, A, K, B,
                        ldb, K, kchunk, st, C, ldc, rowsum, m, row0, amask);
   return check_launch("nn_kernel");
 }
@@ -264,13 +273,24 @@ int launch_nn(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K,
     case kB64:
       return launch_nn_shape<TN, 1, 2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols,
                                        row0, s);
+    case kW2K:
+      if (K % 32 == 0)
+        return launch_nn_shape<TN, 2, 2, false, 32>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum,
+                                                    m, cols, row0, s);
+      break;
+    case kW1K:
+      if (K % 32 == 0)
+        return launch_nn_shape<TN, 1, 4, false, 32>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum,
+                                                    m, cols, row0, s);
+      break;
     case kW2T:
       return launch_nn_shape<TN, 2, 2, true>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m,
                                              cols, row0, s);
     default:
-      return launch_nn_shape<TN, 2, 2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols,
-                                       row0, s);
+      break;
   }
+  return launch_nn_shape<TN, 2, 2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0,
+                                   s);
 }
 
 // C[splits x m x cols] = f(A) B with A in panel layout (m_pad x K), B row-major K x cols.
