@@ -148,7 +148,12 @@ struct NTTile {
 // 2 x (16 KiB A + 64 KiB B) = 160 KiB, so the A image drops its row padding
 // and XOR-swizzles its 16-B chunks instead: chunk' = chunk ^ ((row >> 1) & 7)
 // keeps a ds_read_b128 lane group (16 rows, 2 per 64-bank line) conflict-free.
-template <int TN, bool EXP, int WM = 1, int TM_ = 4 / WM, bool BT = false, int BJ_ = 16>
+//
+// PRIO (cdna_hip_programming.md T5): 1 = s_setprio(1) around every MFMA
+// cluster (keeps hipcc from moving MFMAs across the barrier); 2 = the static
+// 2-waves-per-SIMD form, priority 1 for the younger half (threads >= 256).
+template <int TN, bool EXP, int WM = 1, int TM_ = 4 / WM, bool BT = false, int BJ_ = 16,
+          int PRIO = 0>
 struct NNTile {
   static constexpr int kThreads = 256 * WM;
   static constexpr int TM = TM_;
@@ -293,10 +298,12 @@ struct NNTile {
           const float* brow = sB + (8 * g + 4 * h + t4) * BC + wc * 32 * TN + r;
 #pragma unroll
           for (int ni = 0; ni < TN; ++ni) b[ni] = brow[ni * 32];
+          if (PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
             for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = mfma32(a[mi][t4], b[ni], acc[mi][ni]);
+          if (PRIO == 1) __builtin_amdgcn_s_setprio(0);
         }
       }
     }
@@ -318,6 +325,8 @@ struct NNTile {
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[mi][ni][q] = 0.f;
     if (k0 >= k1) return;
+    if (PRIO == 2 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256)
+      __builtin_amdgcn_s_setprio(1);
     load(Apanels, B, ldb, k0);
     store(smem, scale, row_g0 - k0);
     __syncthreads();

@@ -20,7 +20,7 @@ namespace dsvgd {
 // in order (deterministic, no atomics).
 // row0: interacting-set index of A's row 0 (EXP: the diagonal j == row0 + i
 // is skipped, see NNTile::store).
-template <int TN, bool EXP, int WM, int TM, bool BT, int BJ>
+template <int TN, bool EXP, int WM, int TM, bool BT, int BJ, int PRIO>
 __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ A, int64_t a_npad,
                                                       const float* __restrict__ B, int64_t ldb,
                                                       int64_t K, int64_t kchunk,
@@ -28,7 +28,7 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
                                                       float* __restrict__ C, int64_t ldc,
                                                       float* __restrict__ rowsum, int64_t m,
                                                       int64_t row0, int64_t amask) {
-  using Tile = NNTile<TN, EXP, WM, TM, BT, BJ>;
+  using Tile = NNTile<TN, EXP, WM, TM, BT, BJ, PRIO>;
   __shared__ __attribute__((aligned(16))) float smem[Tile::kSmemFloats];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
@@ -227,7 +227,9 @@ __global__ __launch_bounds__(256) void phi_row_kernel(float* __restrict__ X, int
 //   "w2t"  as w2 with the transposed B image (b128 B-fragment reads)
 //   "w2k"  as w2 with 32-deep K-steps (160 KiB LDS, swizzled A image)
 //   "w1k"  as w1 with 32-deep K-steps
-enum NNShape { kW1, kW2, kB64, kW2T, kW2K, kW1K };
+//   "w2p"  as w2 with s_setprio(1) around each MFMA cluster
+//   "w2s"  as w2 with priority 1 for the younger half of the block
+enum NNShape { kW1, kW2, kB64, kW2T, kW2K, kW1K, kW2P, kW2S };
 static NNShape nn_shape() {
   const char* e = getenv("DSVGD_NN_SHAPE");
   if (!e) return kW2;
@@ -237,10 +239,12 @@ static NNShape nn_shape() {
   if (v == "w2t") return kW2T;
   if (v == "w2k") return kW2K;
   if (v == "w1k") return kW1K;
+  if (v == "w2p") return kW2P;
+  if (v == "w2s") return kW2S;
   return kW2;
 }
 
-template <int TN, int WM, int TM, bool BT = false, int BJ = 16>
+template <int TN, int WM, int TM, bool BT = false, int BJ = 16, int PRIO = 0>
 int launch_nn_shape(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
                     const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
                     int64_t cols, int64_t row0, hipStream_t s) {
@@ -254,10 +258,10 @@ int launch_nn_shape(bool exp_, const float* A, const float* B, int64_t ldb, int6
   const char* am = getenv("DSVGD_NN_AMASK");
   const int64_t amask = am ? atoll(am) : -1;
   if (exp_)
-    hipLaunchKernelGGL((nn_kernel<TN, true, WM, TM, BT, BJ>), grid, dim3(256 * WM), 0, s, A, K, B,
+    hipLaunchKernelGGL((nn_kernel<TN, true, WM, TM, BT, BJ, PRIO>), grid, dim3(256 * WM), 0, s, A, K, B,
                        ldb, K, kchunk, st, C, ldc, rowsum, m, row0, amask);
   else
-    hipLaunchKernelGGL((nn_kernel<TN, false, WM, TM, BT, BJ>), grid, dim3(256 * WM), 0, s, A, K, B,
+    hipLaunchKernelGGL((nn_kernel<TN, false, WM, TM, BT, BJ, PRIO>), grid, dim3(256 * WM), 0, s, A, K, B,
                        ldb, K, kchunk, st, C, ldc, rowsum, m, row0, amask);
   return check_launch("nn_kernel");
 }
@@ -283,6 +287,12 @@ int launch_nn(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K,
         return launch_nn_shape<TN, 1, 4, false, 32>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum,
                                                     m, cols, row0, s);
       break;
+    case kW2P:
+      return launch_nn_shape<TN, 2, 2, false, 16, 1>(exp_, A, B, ldb, K, splits, st, C, ldc,
+                                                     rowsum, m, cols, row0, s);
+    case kW2S:
+      return launch_nn_shape<TN, 2, 2, false, 16, 2>(exp_, A, B, ldb, K, splits, st, C, ldc,
+                                                     rowsum, m, cols, row0, s);
     case kW2T:
       return launch_nn_shape<TN, 2, 2, true>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m,
                                              cols, row0, s);
