@@ -25,6 +25,46 @@ __device__ __forceinline__ void tri_decode(int64_t b, int T, int& bi, int& bj) {
   bj = x + (int)(b - off(x));
 }
 
+// XCD-aware, L2-grouped tile order.  Workgroups are dispatched round-robin
+// over the 8 XCDs (block b runs on XCD b % 8), each with its own 4 MiB L2.
+// xcd_linear gives XCD x a contiguous range of logical tiles, and logical
+// tiles run in groups of kGroup x kGroup tiles, so the rows an XCD re-reads
+// (kGroup A + kGroup B blocks of 128 rows x dp, 2 MiB at dp = 256) stay in
+// its L2 instead of re-streaming Y from MALL for every row panel.
+constexpr int kXcds = 8;
+constexpr int kGroup = 8;
+
+__device__ __forceinline__ int64_t xcd_linear(int64_t b, int64_t total) {
+  const int64_t q = total / kXcds, r = total % kXcds, x = b % kXcds;
+  return x * q + min(x, r) + b / kXcds;
+}
+
+// Tile (bi, bj) of block b in a grid of `total` = groups * kGroup^2 blocks
+// over Tm x Tn tiles; SYM: groups over the upper triangle, tiles bi <= bj.
+// Returns false for the padding blocks of diagonal / edge groups.
+__device__ __forceinline__ bool tile_of(int64_t b, int64_t total, int Tm, int Tn, bool sym,
+                                        int& bi, int& bj) {
+  const int64_t L = xcd_linear(b, total);
+  const int64_t g = L / (kGroup * kGroup);
+  const int w = (int)(L % (kGroup * kGroup));
+  int gi, gj;
+  if (sym) {
+    tri_decode(g, (Tn + kGroup - 1) / kGroup, gi, gj);
+  } else {
+    const int ngn = (Tn + kGroup - 1) / kGroup;
+    gi = (int)(g / ngn);
+    gj = (int)(g % ngn);
+  }
+  bi = gi * kGroup + w / kGroup;
+  bj = gj * kGroup + w % kGroup;
+  return bi < Tm && bj < Tn && (!sym || bi <= bj);
+}
+
+__host__ __device__ inline int64_t tile_grid(int64_t Tm, int64_t Tn, bool sym) {
+  const int64_t ngm = (Tm + kGroup - 1) / kGroup, ngn = (Tn + kGroup - 1) / kGroup;
+  return (sym ? ngn * (ngn + 1) / 2 : ngm * ngn) * kGroup * kGroup;
+}
+
 // Rows [row0, row0+m) of Y against rows [0,n).  SYM (m == n, row0 == 0): only
 // tiles bi <= bj, the off-diagonal ones stored twice (tile + transpose) and
 // accounted with weight 2.
@@ -41,12 +81,8 @@ __global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y
   __shared__ uint32_t sred[16];
 
   int bi, bj;
-  if (SYM) {
-    tri_decode(blockIdx.x, (int)(n_pad / 128), bi, bj);
-  } else {
-    bi = blockIdx.y;
-    bj = blockIdx.x;
-  }
+  const int Tm = (int)(roundup128(m) / 128), Tn = (int)(n_pad / 128);
+  if (!tile_of(blockIdx.x, gridDim.x, Tm, Tn, SYM, bi, bj)) return;  // whole block, before any barrier
   const bool mirror = SYM && bi != bj;
   const int64_t i0 = (int64_t)bi * GramTile::BM;  // within the owned block
   const int64_t j0 = (int64_t)bj * GramTile::BN;
@@ -226,10 +262,11 @@ int launch_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0,
   }
   if (m == n && row0 == 0) {
     const int64_t T = n_pad / 128;
-    hipLaunchKernelGGL((sqdist_kernel<true, SM>), dim3(T * (T + 1) / 2), dim3(256), 0, s, Y, ldy,
-                       norms, row0, m, n, n_pad, (int)dp, D, st, cand);
+    hipLaunchKernelGGL((sqdist_kernel<true, SM>), dim3((unsigned)tile_grid(T, T, true)), dim3(256),
+                       0, s, Y, ldy, norms, row0, m, n, n_pad, (int)dp, D, st, cand);
   } else {
-    hipLaunchKernelGGL((sqdist_kernel<false, SM>), dim3(n_pad / 128, m_pad / 128), dim3(256), 0, s,
+    hipLaunchKernelGGL((sqdist_kernel<false, SM>),
+                       dim3((unsigned)tile_grid(m_pad / 128, n_pad / 128, false)), dim3(256), 0, s,
                        Y, ldy, norms, row0, m, n, n_pad, (int)dp, D, st, cand);
   }
   return check_launch("sqdist");
