@@ -69,7 +69,7 @@ __host__ __device__ inline int64_t tile_grid(int64_t Tm, int64_t Tn, bool sym) {
 // tiles bi <= bj, the off-diagonal ones stored twice (tile + transpose) and
 // accounted with weight 2.
 template <bool SYM, int smode>
-__global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y, int64_t ldy,
+__global__ __launch_bounds__(256, 3) void sqdist_kernel(const float* __restrict__ Y, int64_t ldy,
                                                      const float* __restrict__ norms, int64_t row0,
                                                      int64_t m, int64_t n, int64_t n_pad, int dp,
                                                      float* __restrict__ D,
