@@ -6,6 +6,7 @@
 //   128x128 tile: 2*128*128*dp flop vs 64 KiB written -> MFMA-bound for dp >= 64.
 // d <= 64: explicit differences on the VALU (torch.dist semantics).
 #include <cmath>
+#include <cstdlib>
 
 #include "gemm_tiles.hpp"
 #include "select.hpp"
@@ -69,12 +70,12 @@ __host__ __device__ inline int64_t tile_grid(int64_t Tm, int64_t Tn, bool sym) {
 // tiles bi <= bj, the off-diagonal ones stored twice (tile + transpose) and
 // accounted with weight 2.
 template <bool SYM, int smode>
-__global__ __launch_bounds__(256, 3) void sqdist_kernel(const float* __restrict__ Y, int64_t ldy,
+__global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y, int64_t ldy,
                                                      const float* __restrict__ norms, int64_t row0,
                                                      int64_t m, int64_t n, int64_t n_pad, int dp,
                                                      float* __restrict__ D,
                                                      dsvgd_select_state* __restrict__ st,
-                                                     float* __restrict__ cand) {
+                                                     float* __restrict__ cand, int epi) {
   __shared__ __attribute__((aligned(16))) float smem[GramTile::kSmemFloats];
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
   __shared__ float snorm[GramTile::BM + GramTile::BN];
@@ -127,9 +128,9 @@ __global__ __launch_bounds__(256, 3) void sqdist_kernel(const float* __restrict_
         else
           x = INFINITY;
         v[r] = x;
-        dp0[(r & 3) * 16 + (r >> 2) * 128] = x;
+        if (epi < 2 || x != x) dp0[(r & 3) * 16 + (r >> 2) * 128] = x;
       }
-      if (mirror) {  // D[j][i]: 4 consecutive i per register quad -> 16-byte stores
+      if (mirror && (epi == 0 || v[0] != v[0])) {  // D[j][i]: 4 consecutive i per register quad -> 16-byte stores
         float* const mp0 = Dmir + (int64_t)cl * 16 + (wm * 4 + mi * 2) * kPanelElems + h4;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -260,14 +261,18 @@ int launch_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0,
                        Y, ldy, row0, m, n, n_pad, (int)d, D, st, cand);
     return check_launch("sqdist_direct");
   }
+  // DSVGD_SQ_EPI=1|2: TIMING EXPERIMENTS ONLY (D left incomplete) -- skip the
+  // mirror stores (1) or every D store (2), to price the epilogue.
+  const char* ep = getenv("DSVGD_SQ_EPI");
+  const int epi = ep ? atoi(ep) : 0;
   if (m == n && row0 == 0) {
     const int64_t T = n_pad / 128;
     hipLaunchKernelGGL((sqdist_kernel<true, SM>), dim3((unsigned)tile_grid(T, T, true)), dim3(256),
-                       0, s, Y, ldy, norms, row0, m, n, n_pad, (int)dp, D, st, cand);
+                       0, s, Y, ldy, norms, row0, m, n, n_pad, (int)dp, D, st, cand, epi);
   } else {
     hipLaunchKernelGGL((sqdist_kernel<false, SM>),
                        dim3((unsigned)tile_grid(m_pad / 128, n_pad / 128, false)), dim3(256), 0, s,
-                       Y, ldy, norms, row0, m, n, n_pad, (int)dp, D, st, cand);
+                       Y, ldy, norms, row0, m, n, n_pad, (int)dp, D, st, cand, epi);
   }
   return check_launch("sqdist");
 }

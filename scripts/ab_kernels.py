@@ -66,6 +66,11 @@ def main():
     out = {k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v)),
                "tflops": flops / (np.median(v) * 1e-3) / 1e12} for k, v in res.items()}
     out["sqdist_ms"] = timed(lambda: eng.distances(median=False))
+    for k, v in json.loads(os.environ.get("AB_SQ_VARIANTS", "{}")).items():
+        os.environ.update(v)
+        out["sqdist_ms[%s]" % k] = timed(lambda: eng.distances(median=False))
+        for key in v:
+            os.environ.pop(key, None)
     out["sqdist_select_ms"] = timed(lambda: (eng.distances(median=True), eng.median_bandwidth()))
     print(json.dumps(out, indent=1))
 
