@@ -92,6 +92,8 @@ class DistSampler(object):
         self._engines = {}
         self._state = None
         self._w2 = None
+        self._side = None        # score stream (Jacobi)
+        self._sbuf = None
 
     # ---------------------------------------------------- reference API --
     @property
@@ -135,15 +137,15 @@ class DistSampler(object):
     def _local_scores(self, X, out, scale=1.0):
         self._target.score(X, out, scale)
 
-    def _exchange_all_scores(self, async_op=False):
+    def _exchange_all_scores(self):
         "Sum of every shard's local-data scores of all particles (distsampler.py:160-170)."
-        with span(self.timer, "scores"):
-            self._local_scores(self._work, self._scores)
-        if async_op:
-            return exchange.all_reduce_sum_async(self._scores, self._group)
-        with span(self.timer, "allreduce_scores"):
-            exchange.all_reduce_sum(self._scores, self._group)
-        return None
+        self._local_scores(self._work, self._scores)
+        exchange.all_reduce_sum(self._scores, self._group)
+
+    def _score_buffer(self, shape):
+        if self._sbuf is None or tuple(self._sbuf.shape) != tuple(shape):
+            self._sbuf = torch.empty(shape, dtype=torch.float32, device=self._device)
+        return self._sbuf
 
     def _wasserstein_grad(self, particles, previous_particles, h):
         """h * W2 gradient (distsampler.py:103-129 times h, :198) of the owned
@@ -170,61 +172,65 @@ class DistSampler(object):
             h - discretization size for the JKO (W2) term
         """
         S = self._num_shards
-        # Jacobi + all_scores: the score all-reduce (n x d) overlaps the
-        # distance / median stage, which needs the particles only
-        overlap = self._order == "jacobi" and self._exchange_scores and S > 1
-        pending = None
+        jacobi = self._order == "jacobi"
         if S > 1:
             if self._exchange_particles:
                 with span(self.timer, "allgather_x"):
                     self._exchange_all_particles()
-                if self._exchange_scores:
-                    pending = self._exchange_all_scores(async_op=overlap)
             else:
                 with span(self.timer, "ring_shift"):
                     self._exchange_round_robin()
-        elif self._exchange_scores:
-            with span(self.timer, "scores"):
-                self._local_scores(self._work, self._scores)
 
         s, e = self._particle_start_idx, self._particle_end_idx
         X = self._work
-        w2g = None
-        if self._include_wasserstein and self._previous_particles is not None:
-            with span(self.timer, "w2"):
-                w2g = self._wasserstein_grad(X[s:e], self._previous_particles, h)
         if self._exchange_particles:
             Xi, lo = X, 0
         else:
             Xi, lo = X[s:e], s
         n_int = Xi.shape[0]
         scale = 1.0 if self._exchange_scores else self._N_global / self._N_local
-        if self._exchange_scores:
-            Si = self._scores
-        else:
-            Si = torch.empty(Xi.shape, dtype=torch.float32, device=self._device)
-            with span(self.timer, "scores"):
-                self._local_scores(Xi, Si, scale)
+        Si = self._scores if self._exchange_scores else self._score_buffer(Xi.shape)
         median = self._rbf.median
         share = self._exchange_particles and S > 1
         hook = (lambda t: exchange.all_reduce_sum(t, self._group)) if share else None
 
-        if self._order == "jacobi":
-            eng = self._engine(n_int, e - s, s - lo)
-            if pending is not None:
-                eng.pack(Xi)                       # X half only: the scores are in flight
-                eng.distances(median=median)
-                if median:
-                    eng.median_bandwidth(hook)
+        # scores: all n particles' local-data scores, all-reduced over the
+        # shards (all_scores, distsampler.py:160-170), else the interacting
+        # set's scaled local scores (:94-99).  Jacobi: on a side stream,
+        # concurrent with the distance / median stage (which needs X only).
+        main = torch.cuda.current_stream(self._device)
+        side = main
+        if jacobi:
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=self._device)
+            side = self._side
+            side.wait_stream(main)
+        with torch.cuda.stream(side):
+            with span(self.timer, "scores"):
+                if self._exchange_scores:
+                    self._local_scores(X, Si)
                 else:
-                    eng.fixed_bandwidth(self._rbf.h)
-                with span(self.timer, "allreduce_scores_wait"):
-                    pending.wait()
-                eng.pack(Xi, Si)                   # Si already carries the score scale
-                eng.direction(X[s:e], step_size, write_phi=False, extra=w2g)
+                    self._local_scores(Xi, Si, scale)
+            if self._exchange_scores and S > 1:
+                with span(self.timer, "allreduce_scores"):
+                    exchange.all_reduce_sum(Si, self._group)
+
+        w2g = None
+        if self._include_wasserstein and self._previous_particles is not None:
+            with span(self.timer, "w2"):
+                w2g = self._wasserstein_grad(X[s:e], self._previous_particles, h)
+
+        if jacobi:
+            eng = self._engine(n_int, e - s, s - lo)
+            eng.pack(Xi)                           # X half only: the scores are in flight
+            eng.distances(median=median)
+            if median:
+                eng.median_bandwidth(hook)
             else:
-                eng.step(Xi, Si, X_own=X[s:e], step=step_size, h=None if median else self._rbf.h,
-                         allreduce=hook, write_phi=False, extra=w2g)
+                eng.fixed_bandwidth(self._rbf.h)
+            main.wait_stream(side)
+            eng.pack(Xi, Si)                       # Si already carries the score scale
+            eng.direction(X[s:e], step_size, write_phi=False, extra=w2g)
         else:
             if median:
                 eng = self._engine(n_int, e - s, s - lo)

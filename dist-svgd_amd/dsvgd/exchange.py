@@ -35,21 +35,6 @@ def all_reduce_sum(t, group=None):
     t.copy_(h.to(t.device))
 
 
-class _Done(object):
-    def wait(self):
-        return True
-
-
-def all_reduce_sum_async(t, group=None):
-    """Start a SUM all-reduce and return a handle; on nccl the collective runs
-    on RCCL's stream while the caller keeps enqueueing independent kernels,
-    and handle.wait() makes the current stream wait for it."""
-    if t.is_cuda and not _is_gloo(group):
-        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True)
-    all_reduce_sum(t, group)
-    return _Done()
-
-
 def ring_shift(send, recv, rank, size, group=None):
     """send -> rank+1, recv <- rank-1   [distsampler.py:131-150]."""
     dst, src = (rank + 1) % size, (rank - 1 + size) % size
