@@ -92,7 +92,7 @@ class DistSampler(object):
         self._engines = {}
         self._state = None
         self._w2 = None
-        self._side = None        # score stream (Jacobi)
+        self._side = None        # score all-reduce stream (Jacobi, S > 1)
         self._sbuf = None
 
     # ---------------------------------------------------- reference API --
@@ -196,22 +196,25 @@ class DistSampler(object):
 
         # scores: all n particles' local-data scores, all-reduced over the
         # shards (all_scores, distsampler.py:160-170), else the interacting
-        # set's scaled local scores (:94-99).  Jacobi: on a side stream,
-        # concurrent with the distance / median stage (which needs X only).
+        # set's scaled local scores (:94-99).  Jacobi: the all-reduce runs on a
+        # side stream, concurrent with the distance / median stage (which
+        # needs X only).  The score kernels themselves stay on the main
+        # stream: run beside the distance kernel they only time-slice the CUs
+        # (measured: no gain), both being MFMA-bound.
         main = torch.cuda.current_stream(self._device)
+        with span(self.timer, "scores"):
+            if self._exchange_scores:
+                self._local_scores(X, Si)
+            else:
+                self._local_scores(Xi, Si, scale)
         side = main
-        if jacobi:
-            if self._side is None:
-                self._side = torch.cuda.Stream(device=self._device)
-            side = self._side
-            side.wait_stream(main)
-        with torch.cuda.stream(side):
-            with span(self.timer, "scores"):
-                if self._exchange_scores:
-                    self._local_scores(X, Si)
-                else:
-                    self._local_scores(Xi, Si, scale)
-            if self._exchange_scores and S > 1:
+        if self._exchange_scores and S > 1:
+            if jacobi:
+                if self._side is None:
+                    self._side = torch.cuda.Stream(device=self._device)
+                side = self._side
+                side.wait_stream(main)
+            with torch.cuda.stream(side):
                 with span(self.timer, "allreduce_scores"):
                     exchange.all_reduce_sum(Si, self._group)
 
@@ -228,7 +231,8 @@ class DistSampler(object):
                 eng.median_bandwidth(hook)
             else:
                 eng.fixed_bandwidth(self._rbf.h)
-            main.wait_stream(side)
+            if side is not main:
+                main.wait_stream(side)
             eng.pack(Xi, Si)                       # Si already carries the score scale
             eng.direction(X[s:e], step_size, write_phi=False, extra=w2g)
         else:
