@@ -37,7 +37,9 @@ __host__ __device__ inline int64_t panel_off(int64_t i, int64_t j, int64_t npad)
 
 // ------------------------------------------------------------ NT engine ----
 // Block = WM x WN waves, each wave TM x TN tiles of 32x32; BK = 32.
-template <int TM, int TN, int WM, int WN>
+// DB: double-buffered LDS (one barrier per K-step, the next K-tile written
+// behind the MFMAs) instead of one buffer with two barriers per K-step.
+template <int TM, int TN, int WM, int WN, bool DB = false>
 struct NTTile {
   static constexpr int kThreads = 64 * WM * WN;
   static constexpr int BM = 32 * TM * WM;
@@ -46,7 +48,8 @@ struct NTTile {
   static constexpr int LDK = BK + 4;  // 144-B rows: 16 consecutive rows hit 16 distinct 16-B slots
   static constexpr int LA = BM * BK / 4 / kThreads;  // float4 loads per thread (A)
   static constexpr int LB = BN * BK / 4 / kThreads;
-  static constexpr int kSmemFloats = (BM + BN) * LDK;
+  static constexpr int kStage = (BM + BN) * LDK;
+  static constexpr int kSmemFloats = (DB ? 2 : 1) * kStage;
 
   f32x16 acc[TM][TN];
   f32x4 ra[LA], rb[LB];
@@ -114,11 +117,29 @@ struct NTTile {
   // Full K loop: A, B point at the block's first row; K % BK == 0.
   __device__ __forceinline__ void run(const float* __restrict__ A, int64_t lda,
                                       const float* __restrict__ B, int64_t ldb, int K, float* smem) {
-    float* sA = smem;
-    float* sB = smem + BM * LDK;
     const int w = threadIdx.x >> 6, wm = w / WN, wn = w % WN;
     zero();
     load(A, lda, B, ldb, 0);
+    if (DB) {
+      store(smem, smem + BM * LDK);
+      __syncthreads();
+      int cur = 0;
+      for (int k0 = 0; k0 < K; k0 += BK) {
+        const bool more = k0 + BK < K;
+        if (more) load(A, lda, B, ldb, k0 + BK);
+        const float* st = smem + cur * kStage;
+        compute(st, st + BM * LDK, wm, wn);
+        if (more) {
+          float* nx = smem + (cur ^ 1) * kStage;
+          store(nx, nx + BM * LDK);
+        }
+        __syncthreads();
+        cur ^= 1;
+      }
+      return;
+    }
+    float* sA = smem;
+    float* sB = smem + BM * LDK;
     for (int k0 = 0; k0 < K; k0 += BK) {
       __syncthreads();
       store(sA, sB);

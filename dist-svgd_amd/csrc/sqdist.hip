@@ -13,7 +13,8 @@
 
 namespace dsvgd {
 
-using GramTile = NTTile<2, 2, 2, 2>;  // 128 x 128 block, 4 waves of 64 x 64
+template <bool DB>
+using GramTileT = NTTile<2, 2, 2, 2, DB>;  // 128 x 128 block, 4 waves of 64 x 64
 
 // Upper-triangle tile pair (bi <= bj) of linear block id b over T x T tiles.
 __device__ __forceinline__ void tri_decode(int64_t b, int T, int& bi, int& bj) {
@@ -69,13 +70,14 @@ __host__ __device__ inline int64_t tile_grid(int64_t Tm, int64_t Tn, bool sym) {
 // Rows [row0, row0+m) of Y against rows [0,n).  SYM (m == n, row0 == 0): only
 // tiles bi <= bj, the off-diagonal ones stored twice (tile + transpose) and
 // accounted with weight 2.
-template <bool SYM, int smode>
+template <bool SYM, int smode, bool DB>
 __global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y, int64_t ldy,
                                                      const float* __restrict__ norms, int64_t row0,
                                                      int64_t m, int64_t n, int64_t n_pad, int dp,
                                                      float* __restrict__ D,
                                                      dsvgd_select_state* __restrict__ st,
                                                      float* __restrict__ cand, int epi) {
+  using GramTile = GramTileT<DB>;
   __shared__ __attribute__((aligned(16))) float smem[GramTile::kSmemFloats];
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
   __shared__ float snorm[GramTile::BM + GramTile::BN];
@@ -265,15 +267,27 @@ int launch_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0,
   // mirror stores (1) or every D store (2), to price the epilogue.
   const char* ep = getenv("DSVGD_SQ_EPI");
   const int epi = ep ? atoi(ep) : 0;
-  if (m == n && row0 == 0) {
-    const int64_t T = n_pad / 128;
-    hipLaunchKernelGGL((sqdist_kernel<true, SM>), dim3((unsigned)tile_grid(T, T, true)), dim3(256),
-                       0, s, Y, ldy, norms, row0, m, n, n_pad, (int)dp, D, st, cand, epi);
+  // DSVGD_SQ_DB=1: the double-buffered NT mainloop (A/B switch)
+  const char* db = getenv("DSVGD_SQ_DB");
+  const bool dbuf = db && db[0] == '1';
+  const bool sym = m == n && row0 == 0;
+  const int64_t T = n_pad / 128;
+  const dim3 grid((unsigned)(sym ? tile_grid(T, T, true) : tile_grid(m_pad / 128, T, false)));
+#define DSVGD_SQ_LAUNCH(SYMV, DBV)                                                             \
+  hipLaunchKernelGGL((sqdist_kernel<SYMV, SM, DBV>), grid, dim3(256), 0, s, Y, ldy, norms, row0, \
+                     m, n, n_pad, (int)dp, D, st, cand, epi)
+  if (sym) {
+    if (dbuf)
+      DSVGD_SQ_LAUNCH(true, true);
+    else
+      DSVGD_SQ_LAUNCH(true, false);
   } else {
-    hipLaunchKernelGGL((sqdist_kernel<false, SM>),
-                       dim3((unsigned)tile_grid(m_pad / 128, n_pad / 128, false)), dim3(256), 0, s,
-                       Y, ldy, norms, row0, m, n, n_pad, (int)dp, D, st, cand, epi);
+    if (dbuf)
+      DSVGD_SQ_LAUNCH(false, true);
+    else
+      DSVGD_SQ_LAUNCH(false, false);
   }
+#undef DSVGD_SQ_LAUNCH
   return check_launch("sqdist");
 }
 

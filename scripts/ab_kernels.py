@@ -69,6 +69,8 @@ def main():
     for k, v in json.loads(os.environ.get("AB_SQ_VARIANTS", "{}")).items():
         os.environ.update(v)
         out["sqdist_ms[%s]" % k] = timed(lambda: eng.distances(median=False))
+        out["sqdist_select_ms[%s]" % k] = timed(
+            lambda: (eng.distances(median=True), eng.median_bandwidth()))
         for key in v:
             os.environ.pop(key, None)
     out["sqdist_select_ms"] = timed(lambda: (eng.distances(median=True), eng.median_bandwidth()))
