@@ -26,10 +26,11 @@ __device__ __forceinline__ void digit_of(int pass, uint32_t& shift, uint32_t& ma
 }
 
 __device__ __forceinline__ void hist_key(uint32_t key, uint32_t want, uint32_t shift,
-                                         uint32_t mask, uint32_t hishift, uint32_t* shist) {
+                                         uint32_t mask, uint32_t hishift, uint32_t* shist,
+                                         uint32_t w = 1u) {
   if (key >= 0x7F800000u) return;  // +inf pad / NaN
   const uint32_t hi = hishift >= 32 ? 0u : (key >> hishift);
-  if (hi == want) atomicAdd(&shist[(key >> shift) & mask], 1u);
+  if (hi == want) atomicAdd(&shist[(key >> shift) & mask], w);
 }
 
 // count: entries of D (any order); cand: optional candidate buffer used
@@ -47,15 +48,18 @@ __global__ __launch_bounds__(256) void radix_hist_kernel(const float* __restrict
   __syncthreads();
   const int64_t stride = (int64_t)gridDim.x * 256;
   const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (use_cand) {  // lists l = block % 256, each swept by gridDim/256 blocks
-    const unsigned long long capl = st->cand_cap / kCandLists;
-    const int per = max(1, (int)(gridDim.x / kCandLists));
-    for (int l = blockIdx.x % kCandLists; l < kCandLists; l += (int)min(gridDim.x, (unsigned)kCandLists)) {
-      const int64_t nl = (int64_t)min(st->list_cnt[l], capl);
-      const float* c = cand + (unsigned long long)l * capl;
-      for (int64_t q = (int64_t)(blockIdx.x / kCandLists) * 256 + threadIdx.x; q < nl;
-           q += (int64_t)per * 256)
-        hist_key(__float_as_uint(c[q]), want, shift, mask, hishift, shist);
+  if (use_cand) {  // one wave per candidate slot (weight 2: a mirrored tile)
+    const int64_t ns = (int64_t)st->nslots, cap = (int64_t)st->slot_cap;
+    const uint32_t* cnt = reinterpret_cast<const uint32_t*>(cand);
+    const float* data = cand + 2 * ns;
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t sl = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); sl < ns; sl += nw) {
+      const uint32_t c = cnt[sl];
+      const uint32_t w = (c & DSVGD_SLOT_WEIGHT2) ? 2u : 1u;
+      const int64_t nc = min((int64_t)(c & ~DSVGD_SLOT_WEIGHT2), cap);
+      for (int64_t q = lane; q < nc; q += 64)
+        hist_key(__float_as_uint(data[sl * cap + q]), want, shift, mask, hishift, shist, w);
     }
   } else {
     const int64_t c4 = count >> 2;
@@ -162,10 +166,6 @@ __global__ void bracket_init_kernel(dsvgd_select_state* st, int64_t n_total,
                                     const dsvgd_select_state* hi_st, int64_t cap) {
   const int t = threadIdx.x;
   for (int b = t; b < DSVGD_RADIX_BINS; b += blockDim.x) st->hist[b] = 0ull;
-  for (int l = t; l < kCandLists; l += blockDim.x) {
-    st->list_cnt[l] = 0ull;
-    st->list_below[l] = 0ull;
-  }
   if (t == 0) {
     const unsigned long long nn = (unsigned long long)n_total * (unsigned long long)n_total;
     reset_state(st, (nn - 1ull) / 2ull, (unsigned long long)n_total);
@@ -173,32 +173,47 @@ __global__ void bracket_init_kernel(dsvgd_select_state* st, int64_t n_total,
     st->lo = lo_st->median;
     st->hi = hi_st->median;
     st->cand_cap = (unsigned long long)cap;
+    st->nslots = 0ull;
+    st->slot_cap = 0ull;
   }
 }
 
-// Sum the local candidate lists: (below_total, ncand_total, overflow), the
-// int64[3] a distributed caller all-reduces before bracket_check.
-__global__ __launch_bounds__(256) void bracket_totals_kernel(dsvgd_select_state* st) {
+// Sum the local candidate slots into (below_total, ncand_total, overflow),
+// the int64[3] a distributed caller all-reduces before bracket_check
+// (zeroed by bracket_init; integer atomics, so the sums are exact).
+__global__ __launch_bounds__(256) void bracket_totals_kernel(dsvgd_select_state* st,
+                                                             const float* __restrict__ cand) {
   __shared__ unsigned long long sb[256], sc[256], so[256];
-  const int l = threadIdx.x;
-  const unsigned long long capl = st->cand_cap / kCandLists;
-  const unsigned long long c = st->list_cnt[l];
-  sb[l] = st->list_below[l];
-  sc[l] = c;
-  so[l] = c > capl ? 1ull : 0ull;
+  const int t = threadIdx.x;
+  const int64_t ns = (int64_t)st->nslots;
+  const uint64_t cap = st->slot_cap;
+  const uint32_t* cnt = reinterpret_cast<const uint32_t*>(cand);
+  const uint32_t* below = cnt + ns;
+  unsigned long long b = 0, c = 0, o = 0;
+  for (int64_t sl = (int64_t)blockIdx.x * 256 + t; sl < ns; sl += (int64_t)gridDim.x * 256) {
+    const uint32_t x = cnt[sl];
+    const uint64_t w = (x & DSVGD_SLOT_WEIGHT2) ? 2u : 1u;
+    const uint64_t k = x & ~DSVGD_SLOT_WEIGHT2;
+    b += w * below[sl];
+    c += w * k;
+    o += k > cap ? 1u : 0u;
+  }
+  sb[t] = b;
+  sc[t] = c;
+  so[t] = o;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (l < o) {
-      sb[l] += sb[l + o];
-      sc[l] += sc[l + o];
-      so[l] += so[l + o];
+  for (int q = 128; q > 0; q >>= 1) {
+    if (t < q) {
+      sb[t] += sb[t + q];
+      sc[t] += sc[t + q];
+      so[t] += so[t + q];
     }
     __syncthreads();
   }
-  if (l == 0) {
-    st->below_total = sb[0];
-    st->ncand_total = sc[0];
-    st->overflow = so[0];
+  if (t == 0) {
+    if (sb[0]) atomicAdd((unsigned long long*)&st->below_total, sb[0]);
+    if (sc[0]) atomicAdd((unsigned long long*)&st->ncand_total, sc[0]);
+    if (so[0]) atomicAdd((unsigned long long*)&st->overflow, so[0]);
   }
 }
 
@@ -268,7 +283,7 @@ int dsvgd_radix_hist(const float* D, int64_t count, const float* cand, int pass,
   DSVGD_REQUIRE(count >= 0 && ((uintptr_t)D & 15) == 0, "count / alignment");
   int64_t blocks = (count / 4 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  if (cand && blocks < 1024) blocks = 1024;  // >= 4 blocks per candidate list
+  if (cand && blocks < 1024) blocks = 1024;  // candidate slots: one wave each, grid-stride
   hipLaunchKernelGGL(radix_hist_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, D, count,
                      cand, pass, st);
   return check_launch("radix_hist");
@@ -295,16 +310,16 @@ int dsvgd_sample_sqdist(const float* Y, int64_t ldy, int64_t n, int64_t d, int64
 int dsvgd_bracket_init(dsvgd_select_state* st, int64_t n_total, const dsvgd_select_state* lo_st,
                        const dsvgd_select_state* hi_st, int64_t cand_cap, void* stream) {
   DSVGD_REQUIRE(st && lo_st && hi_st && n_total > 0, "args");
-  DSVGD_REQUIRE(cand_cap >= DSVGD_CAND_LISTS && cand_cap % DSVGD_CAND_LISTS == 0,
-                "cand_cap must be a positive multiple of DSVGD_CAND_LISTS");
+  DSVGD_REQUIRE(cand_cap > 0, "cand_cap must be positive");
   hipLaunchKernelGGL(bracket_init_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, st, n_total,
                      lo_st, hi_st, cand_cap);
   return check_launch("bracket_init");
 }
 
-int dsvgd_bracket_totals(dsvgd_select_state* st, void* stream) {
-  DSVGD_REQUIRE(st, "null state");
-  hipLaunchKernelGGL(bracket_totals_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, st);
+int dsvgd_bracket_totals(dsvgd_select_state* st, const float* cand, void* stream) {
+  DSVGD_REQUIRE(st && cand, "null pointer");
+  hipLaunchKernelGGL(bracket_totals_kernel, dim3(256), dim3(256), 0, (hipStream_t)stream, st,
+                     cand);
   return check_launch("bracket_totals");
 }
 

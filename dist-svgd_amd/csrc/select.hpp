@@ -6,8 +6,9 @@
 //               every valid entry; passes 2 and 3 then stream D again.
 //  kSelBracket  a 2^18-pair sample has fixed lo <= median <= hi (6 sigma of
 //               the sample rank); the epilogue counts entries < lo and
-//               compacts the entries in [lo, hi] (~1 %) into a candidate
-//               buffer, so the three radix passes read the candidates, not D.
+//               compacts the entries in [lo, hi] (~1 %) into per-wave
+//               candidate slots, so the three radix passes read the
+//               candidates, not D.
 //               Exactness is checked on device (below <= k < below + ncand);
 //               a miss or an overflow falls back to the passes over D.
 #pragma once
@@ -77,82 +78,80 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t& total) 
 }
 
 // ---- bracketed mode --------------------------------------------------------
-// Phase 1 (while storing D): each lane counts its values < lo and in [lo, hi].
-// Phase 2 (block-collective): one returning atomic per BLOCK on the list
-// counter of the block's candidate list (256 lists: no counter sees more than
-// a few hundred atomics per launch -- same-address float/int atomics from every
-// CU serialise, MI355X_MICROARCH.md "Global float atomics", contention row).
-// Phase 3: each lane re-derives its values (deterministic) and writes the
-// in-bracket ones at its reserved positions.
-struct BracketCounter {
-  uint32_t below = 0, inb = 0;
-  uint64_t mask = 0;  // bit i: value i of this lane is in [lo, hi]
+// Every wave of a distance launch owns one fixed-capacity candidate slot
+// (layout: include/dsvgd.h, DSVGD_SLOT_WEIGHT2).  Per value: the lane counts
+// it if < lo; values in [lo, hi] (~1 %) are compacted into the slot with a
+// wave ballot + mbcnt (no atomics, no block barrier, no re-reads).  finish()
+// writes the slot's counts; a slot that fills up is detected by
+// bracket_totals (count > slot_cap) and the select falls back to D.
+struct SlotLayout {
+  uint32_t* cnt;
+  uint32_t* below;
+  float* data;
+  int64_t nslots, cap;
+  __device__ __forceinline__ SlotLayout(float* cand, int64_t nslots_, uint64_t cand_cap)
+      : nslots(nslots_) {
+    cnt = reinterpret_cast<uint32_t*>(cand);
+    below = cnt + nslots_;
+    data = cand + 2 * nslots_;
+    const int64_t c = ((int64_t)cand_cap - 2 * nslots_) / nslots_;
+    cap = c > 0 ? c : 0;
+  }
+  // block 0 publishes the geometry for the select passes / totals
+  __device__ __forceinline__ void publish(dsvgd_select_state* st, int64_t block) const {
+    if (block == 0 && threadIdx.x == 0) {
+      st->nslots = (uint64_t)nslots;
+      st->slot_cap = (uint64_t)cap;
+    }
+  }
+};
+
+struct SlotWriter {
+  float* dst = nullptr;
+  uint32_t cnt = 0;    // wave-uniform: entries in [lo, hi] so far (may exceed cap)
+  uint32_t below = 0;  // per lane
+  uint32_t cap = 0;
   float lo = 0.f, hi = -1.f;
-  __device__ __forceinline__ void load(const dsvgd_select_state* st) {
+  __device__ __forceinline__ void begin(const dsvgd_select_state* st, const SlotLayout& L,
+                                        int64_t slot) {
     lo = st->lo;
     hi = st->hi;
+    dst = L.data + slot * L.cap;
+    cap = (uint32_t)L.cap;
   }
-  __device__ __forceinline__ void count(float v, uint32_t w, int idx) {
+  // every lane of the wave must call add() for the same value index
+  __device__ __forceinline__ void add(float v) {
+    below += (v < lo) ? 1u : 0u;
     const bool in = v >= lo && v <= hi;
-    below += (v < lo) ? w : 0u;
-    inb += in ? w : 0u;
-    mask |= (uint64_t)in << idx;
-  }
-};
-
-struct BracketWriter {
-  float* dst = nullptr;
-  unsigned long long pos = 0, cap = 0;
-  float lo = 0.f, hi = -1.f;
-  __device__ __forceinline__ void put(float v, uint32_t w) {
-    for (uint32_t r = 0; r < w; ++r, ++pos)
-      if (pos < cap) dst[pos] = v;
-  }
-};
-
-constexpr int kCandLists = DSVGD_CAND_LISTS;
-
-// sred: LDS scratch of >= 2*NW + 4 u32 (NW = waves per block).  Every thread
-// of the block must call it.
-template <int NW>
-__device__ __forceinline__ BracketWriter bracket_reserve(const BracketCounter& bc,
-                                                         dsvgd_select_state* __restrict__ st,
-                                                         float* __restrict__ cand, int list,
-                                                         uint32_t* sred) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t below = bc.below;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) below += __shfl_xor(below, o, 64);
-  uint32_t wtotal;
-  const uint32_t off = wave_excl_scan(bc.inb, wtotal);
-  if (lane == 0) {
-    sred[wave] = wtotal;
-    sred[NW + wave] = below;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t run = 0, bsum = 0;
-    for (int w = 0; w < NW; ++w) {
-      const uint32_t t = sred[w];
-      sred[w] = run;
-      run += t;
-      bsum += sred[NW + w];
+    const uint64_t bal = __ballot(in);
+    if (bal) {
+      if (in) {
+        const uint32_t pos = cnt + __builtin_amdgcn_mbcnt_hi(
+                                       (uint32_t)(bal >> 32),
+                                       __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        if (pos < cap) dst[pos] = v;
+      }
+      cnt += (uint32_t)__popcll(bal);
     }
-    unsigned long long base = 0;
-    if (run) base = atomicAdd((unsigned long long*)&st->list_cnt[list], (unsigned long long)run);
-    if (bsum) atomicAdd((unsigned long long*)&st->list_below[list], (unsigned long long)bsum);
-    sred[2 * NW] = (uint32_t)(base & 0xffffffffull);
-    sred[2 * NW + 1] = (uint32_t)(base >> 32);
   }
-  __syncthreads();
-  BracketWriter bw;
-  const unsigned long long cap = st->cand_cap / kCandLists;
-  bw.dst = cand + (unsigned long long)list * cap;
-  bw.cap = cap;
-  bw.pos = (((unsigned long long)sred[2 * NW + 1] << 32) | sred[2 * NW]) + sred[wave] + off;
-  bw.lo = bc.lo;
-  bw.hi = bc.hi;
-  return bw;
+  __device__ __forceinline__ void finish(const SlotLayout& L, int64_t slot, bool weight2) {
+    uint32_t b = below;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o, 64);
+    if ((threadIdx.x & 63) == 0) {
+      const uint32_t flag = weight2 ? DSVGD_SLOT_WEIGHT2 : 0u;
+      L.cnt[slot] = (cnt < DSVGD_SLOT_WEIGHT2 ? cnt : DSVGD_SLOT_WEIGHT2 - 1u) | flag;
+      L.below[slot] = b;
+    }
+  }
+};
+
+// slots of a wave that has no values (padding blocks): empty counts
+__device__ __forceinline__ void slot_clear(const SlotLayout& L, int64_t slot) {
+  if ((threadIdx.x & 63) == 0) {
+    L.cnt[slot] = 0u;
+    L.below[slot] = 0u;
+  }
 }
 
 }  // namespace dsvgd

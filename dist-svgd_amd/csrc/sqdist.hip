@@ -81,11 +81,15 @@ __global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y
   __shared__ __attribute__((aligned(16))) float smem[GramTile::kSmemFloats];
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
   __shared__ float snorm[GramTile::BM + GramTile::BN];
-  __shared__ uint32_t sred[16];
 
   int bi, bj;
   const int Tm = (int)(roundup128(m) / 128), Tn = (int)(n_pad / 128);
-  if (!tile_of(blockIdx.x, gridDim.x, Tm, Tn, SYM, bi, bj)) return;  // whole block, before any barrier
+  const int w = threadIdx.x >> 6;
+  const int64_t slot = (int64_t)blockIdx.x * 4 + w;
+  if (!tile_of(blockIdx.x, gridDim.x, Tm, Tn, SYM, bi, bj)) {  // whole block, before any barrier
+    if (smode == kSelBracket) slot_clear(SlotLayout(cand, (int64_t)gridDim.x * 4, st->cand_cap), slot);
+    return;
+  }
   const bool mirror = SYM && bi != bj;
   const int64_t i0 = (int64_t)bi * GramTile::BM;  // within the owned block
   const int64_t j0 = (int64_t)bj * GramTile::BN;
@@ -99,11 +103,15 @@ __global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y
     snorm[t] = t < GramTile::BM ? norms[row0 + i0 + t] : norms[j0 + t - GramTile::BM];
   __syncthreads();
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
+  const int lane = threadIdx.x & 63, wm = w >> 1, wn = w & 1;
   const uint32_t weight = mirror ? 2u : 1u;
   WindowHist wh;
-  BracketCounter bc;
-  if (smode == kSelBracket) bc.load(st);
+  SlotWriter sw;
+  SlotLayout sl(cand, (int64_t)gridDim.x * 4, smode == kSelBracket ? st->cand_cap : 0);
+  if (smode == kSelBracket) {
+    sl.publish(st, blockIdx.x);
+    sw.begin(st, sl, slot);
+  }
   // epilogue one 32x32 sub-tile (16 values per lane) at a time.  Panel-layout
   // addresses: per lane one base pointer per sub-tile, the per-register part
   // ((r&3)*16 + (r>>2)*128 floats) is a compile-time immediate.
@@ -144,20 +152,10 @@ __global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y
         hist_account(wh, v, weight, shist);
       } else if (smode == kSelBracket) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) bc.count(v[r], weight, (mi * 2 + ni) * 16 + r);
+        for (int r = 0; r < 16; ++r) sw.add(v[r]);
       }
     }
-  if (smode == kSelBracket) {
-    BracketWriter bw = bracket_reserve<4>(bc, st, cand, (int)(blockIdx.x & (kCandLists - 1)), sred);
-    // phase 3 re-reads only this lane's in-bracket entries (~1 %, L2-hot)
-    // instead of keeping the accumulators live across the block reservation
-    for (uint64_t msk = bc.mask; msk; msk &= msk - 1) {
-      const int idx = __builtin_ctzll(msk), sub = idx >> 4, r = idx & 15;
-      const int cl = wn * 64 + (sub & 1) * 32 + (lane & 31);
-      const int rl = wm * 64 + (sub >> 1) * 32 + h4 + (r & 3) + 8 * (r >> 2);
-      bw.put(Dtile[(cl >> 4) * kPanelElems + (cl & 15) + rl * 16], weight);
-    }
-  }
+  if (smode == kSelBracket) sw.finish(sl, slot, mirror);
   if (smode == kSelHist) {
     wh.flush(shist);
     __syncthreads();
@@ -182,7 +180,6 @@ __global__ __launch_bounds__(256) void sqdist_direct_kernel(const float* __restr
   __shared__ __attribute__((aligned(16))) float sA[kDirectMaxD][128];
   __shared__ __attribute__((aligned(16))) float sB[kDirectMaxD][128];
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
-  __shared__ uint32_t sred[16];
   const int t = threadIdx.x;
   const int64_t i0 = (int64_t)blockIdx.y * 128, j0 = (int64_t)blockIdx.x * 128;
   if (smode == kSelHist)
@@ -217,8 +214,14 @@ __global__ __launch_bounds__(256) void sqdist_direct_kernel(const float* __restr
   WindowHist wh;
   if (smode == kSelHist)
     wh.init((i0 + ty * 8 < m && j0 + tx * 8 < n) ? acc[0][0] : INFINITY);
-  BracketCounter bc;
-  if (smode == kSelBracket) bc.load(st);
+  const int64_t nslots = (int64_t)gridDim.x * gridDim.y * 4;
+  const int64_t slot = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (t >> 6);
+  SlotWriter sw;
+  SlotLayout sl(cand, nslots, smode == kSelBracket ? st->cand_cap : 0);
+  if (smode == kSelBracket) {
+    sl.publish(st, (int64_t)blockIdx.y * gridDim.x + blockIdx.x);
+    sw.begin(st, sl, slot);
+  }
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
     const int64_t gi = i0 + ty * 8 + a;
@@ -235,17 +238,10 @@ __global__ __launch_bounds__(256) void sqdist_direct_kernel(const float* __restr
       hist_account(wh, v, 1u, shist);
     } else if (smode == kSelBracket) {
 #pragma unroll
-      for (int b = 0; b < 8; ++b) bc.count(v[b], 1u, a * 8 + b);
+      for (int b = 0; b < 8; ++b) sw.add(v[b]);
     }
   }
-  if (smode == kSelBracket) {
-    const int list = (int)((blockIdx.x + blockIdx.y * gridDim.x) & (kCandLists - 1));
-    BracketWriter bw = bracket_reserve<4>(bc, st, cand, list, sred);
-    for (uint64_t msk = bc.mask; msk; msk &= msk - 1) {
-      const int idx = __builtin_ctzll(msk);
-      bw.put(D[panel_off(i0 + ty * 8 + (idx >> 3), j0 + tx * 8 + (idx & 7), n_pad)], 1u);
-    }
-  }
+  if (smode == kSelBracket) sw.finish(sl, slot, false);
   if (smode == kSelHist) {
     wh.flush(shist);
     __syncthreads();

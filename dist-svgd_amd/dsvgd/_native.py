@@ -34,7 +34,7 @@ SIGNATURES = {
     "dsvgd_radix_pick": (_int, [_p, _int, _p]),
     "dsvgd_sample_sqdist": (_int, [_p, _i64, _i64, _i64, _i64, _c.c_uint64, _p, _p]),
     "dsvgd_bracket_init": (_int, [_p, _i64, _p, _p, _i64, _p]),
-    "dsvgd_bracket_totals": (_int, [_p, _p]),
+    "dsvgd_bracket_totals": (_int, [_p, _p, _p]),
     "dsvgd_bracket_check": (_int, [_p, _p]),
     "dsvgd_set_bandwidth": (_int, [_p, _f, _p]),
     "dsvgd_phi_splits": (_i64, [_i64, _i64, _i64]),

@@ -23,7 +23,6 @@ import torch
 from . import _native as N
 
 NBINS = 2048
-NLISTS = 256
 
 
 class _SelectState(ctypes.Structure):
@@ -34,8 +33,8 @@ class _SelectState(ctypes.Structure):
                 ("h", ctypes.c_float), ("inv_h", ctypes.c_float), ("fallback", ctypes.c_uint32),
                 ("below_total", ctypes.c_uint64), ("ncand_total", ctypes.c_uint64),
                 ("overflow", ctypes.c_uint64), ("lo", ctypes.c_float), ("hi", ctypes.c_float),
-                ("cand_cap", ctypes.c_uint64), ("list_cnt", ctypes.c_uint64 * NLISTS),
-                ("list_below", ctypes.c_uint64 * NLISTS)]
+                ("cand_cap", ctypes.c_uint64), ("nslots", ctypes.c_uint64),
+                ("slot_cap", ctypes.c_uint64)]
 
 SEL_NONE, SEL_HIST, SEL_BRACKET = 0, 1, 2
 
@@ -173,7 +172,9 @@ class PhiEngine(object):
             self.k_hi = min(s - 1, int(math.ceil(half + dk)))
             self.sample = torch.empty(s, **f32)
             self.st_lo, self.st_hi = SelectState(dev), SelectState(dev)
-            self.cand_cap = max(1 << 22, (m * n) // 16) // NLISTS * NLISTS
+            # one fixed-capacity slot per distance-launch wave (include/dsvgd.h);
+            # 1/16 of the entries leaves ~5x headroom over the ~1.2 % in bracket
+            self.cand_cap = max(1 << 22, (m * n) // 16)
             self.cand = torch.empty(self.cand_cap, **f32)
 
     # ------------------------------------------------------------ stages --
@@ -229,7 +230,7 @@ class PhiEngine(object):
         count = self.m_pad * self.n_pad
         cand = None
         if self.bracketed:
-            N.call("dsvgd_bracket_totals", self.state.ptr, s)
+            N.call("dsvgd_bracket_totals", self.state.ptr, N.ptr(self.cand), s)
             if allreduce is not None:
                 allreduce(self.state.totals)
             N.call("dsvgd_bracket_check", self.state.ptr, s)

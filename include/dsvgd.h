@@ -40,10 +40,16 @@ enum {
 
 /* number of histogram bins of one radix-select pass (11-bit digits) */
 #define DSVGD_RADIX_BINS 2048
-/* bracketed select: the candidate buffer is cand_cap/DSVGD_CAND_LISTS-sized
- * lists, each appended to by one atomic per distance block (sharded so no
- * counter sees more than a few hundred atomics per launch) */
-#define DSVGD_CAND_LISTS 256
+/* bracketed select: the candidate buffer (cand_cap floats) is split into one
+ * fixed-capacity SLOT per wave of the distance launch, written without any
+ * atomic or block barrier:
+ *   cand[0 : nslots)            u32 slot_cnt   (entries in [lo,hi]; bit 31 =
+ *                                               weight 2, a mirrored tile)
+ *   cand[nslots : 2 nslots)     u32 slot_below (entries < lo, same weight)
+ *   cand[2 nslots + s*slot_cap] the slot's values (slot_cap floats each)
+ * with slot_cap = (cand_cap - 2 nslots) / nslots; a slot that fills up sets
+ * `overflow` and the select falls back to the passes over D (still exact). */
+#define DSVGD_SLOT_WEIGHT2 0x80000000u
 
 /* Device-resident state of the median-bandwidth radix select.  Allocate
  * dsvgd_select_state_bytes() of device memory; the histogram is the first
@@ -62,11 +68,11 @@ typedef struct dsvgd_select_state {
   uint32_t fallback;               /* bracketed: 1 = select over D itself     */
   uint64_t below_total;            /* bracketed: # entries < lo      } int64[3], */
   uint64_t ncand_total;            /* bracketed: # entries in [lo,hi] } all-     */
-  uint64_t overflow;               /* bracketed: # overflowed lists  } reduced  */
+  uint64_t overflow;               /* bracketed: # overflowed slots  } reduced  */
   float lo, hi;                    /* bracketed: the sample bracket           */
   uint64_t cand_cap;               /* bracketed: candidate buffer floats      */
-  uint64_t list_cnt[DSVGD_CAND_LISTS];   /* local entries per candidate list  */
-  uint64_t list_below[DSVGD_CAND_LISTS]; /* local entries < lo per list       */
+  uint64_t nslots;                 /* bracketed: slots of the last sqdist     */
+  uint64_t slot_cap;               /* bracketed: floats per slot              */
 } dsvgd_select_state;
 
 /* select_mode of dsvgd_sqdist */
@@ -107,9 +113,9 @@ int dsvgd_pack(const float* X, int64_t ldx, const float* S, int64_t lds, float s
  * upper-triangle tiles only when m == n and row0 == 0 (the transpose is
  * stored too).  D[i][i] = 0 exactly, pads = +inf, panel layout (ldd = n_pad).
  * select_mode (DSVGD_SEL_*): HIST accumulates radix digit 1 of the valid
- * entries into st->hist; BRACKET counts entries < st->lo into st->list_below
- * and appends the entries in [st->lo, st->hi] to the candidate lists in cand
- * (list l = cand + l*cand_cap/DSVGD_CAND_LISTS, length st->list_cnt[l]).
+ * entries into st->hist; BRACKET counts the entries < st->lo and writes the
+ * entries in [st->lo, st->hi] into the wave slots of cand (layout above;
+ * st->nslots / st->slot_cap are set by the launch).
  * Replaces torch.dist(x, y, p=2)**2 inside kernel(...) at
  * experiments/logreg.py:60-61 / experiments/gmm.py:23-24 as called per pair
  * from dsvgd/sampler.py:38 and dsvgd/distsampler.py:91-97. */
@@ -126,7 +132,7 @@ int dsvgd_select_init(dsvgd_select_state* st, int64_t n_total, int64_t k_rank, v
 /* histogram of key digit `pass` (1: bits 31..21, 2: 20..10, 3: 9..0) of the
  * finite entries (pads +inf / NaN skipped) whose higher digits equal
  * st->prefix, over D[0:count) -- or, when cand != NULL and the bracket holds
- * (st->fallback == 0), over the local candidate lists instead. */
+ * (st->fallback == 0), over the local candidate slots instead. */
 int dsvgd_radix_hist(const float* D, int64_t count, const float* cand, int pass,
                      dsvgd_select_state* st, void* stream);
 /* pick the bin holding rank k, fix its digit, clear hist; after pass 3
@@ -140,12 +146,12 @@ int dsvgd_sample_sqdist(const float* Y, int64_t ldy, int64_t n, int64_t d, int64
  * `out`) become the bracket [lo, hi] of st (k = (n_total^2-1)/2) ... */
 int dsvgd_bracket_init(dsvgd_select_state* st, int64_t n_total, const dsvgd_select_state* lo_st,
                        const dsvgd_select_state* hi_st, int64_t cand_cap, void* stream);
-/* ... then, after dsvgd_sqdist(BRACKET): bracket_totals sums the lists into
+/* ... then, after dsvgd_sqdist(BRACKET): bracket_totals sums the slots into
  * below_total / ncand_total / overflow (a distributed caller all-reduces
  * those three int64), and bracket_check decides exactly: below <= k <
- * below + ncand and no list overflowed -> k -= below, the passes read the
- * candidate lists; otherwise they read D (fallback). */
-int dsvgd_bracket_totals(dsvgd_select_state* st, void* stream);
+ * below + ncand and no slot overflowed -> k -= below, the passes read the
+ * candidate slots; otherwise they read D (fallback). */
+int dsvgd_bracket_totals(dsvgd_select_state* st, const float* cand, void* stream);
 int dsvgd_bracket_check(dsvgd_select_state* st, void* stream);
 /* fixed-bandwidth mode: st->h = h, st->inv_h = 1/h */
 int dsvgd_set_bandwidth(dsvgd_select_state* st, float h, void* stream);

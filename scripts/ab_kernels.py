@@ -69,10 +69,12 @@ def main():
     for k, v in json.loads(os.environ.get("AB_SQ_VARIANTS", "{}")).items():
         os.environ.update(v)
         out["sqdist_ms[%s]" % k] = timed(lambda: eng.distances(median=False))
+        out["sqdist_bracket_ms[%s]" % k] = timed(lambda: eng.distances(median=True))
         out["sqdist_select_ms[%s]" % k] = timed(
             lambda: (eng.distances(median=True), eng.median_bandwidth()))
         for key in v:
             os.environ.pop(key, None)
+    out["sqdist_bracket_ms"] = timed(lambda: eng.distances(median=True))
     out["sqdist_select_ms"] = timed(lambda: (eng.distances(median=True), eng.median_bandwidth()))
     print(json.dumps(out, indent=1))
 
