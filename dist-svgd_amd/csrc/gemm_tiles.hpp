@@ -63,19 +63,27 @@ struct NTTile {
         for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
   }
 
+  // Buffer loads: one per-lane byte offset (row t/8, chunk t%8) and scalar
+  // offsets for the u-th 32-row group and the K-step, so the staging needs
+  // no per-load 64-bit address registers (the row-block bases are uniform).
   __device__ __forceinline__ void load(const float* __restrict__ A, int64_t lda,
                                        const float* __restrict__ B, int64_t ldb, int k0) {
     const int t = threadIdx.x;
+    constexpr int kRows = kThreads / 8;  // rows covered by one float4 per thread
+    const __amdgpu_buffer_rsrc_t rA =
+        __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB =
+        __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0x7fffffff, 0x00020000);
+    const int voA = (int)(((t >> 3) * lda + 4 * (t & 7)) * 4);
+    const int voB = (int)(((t >> 3) * ldb + 4 * (t & 7)) * 4);
 #pragma unroll
-    for (int u = 0; u < LA; ++u) {
-      const int f = t + u * kThreads, row = f >> 3, c4 = f & 7;
-      ra[u] = *reinterpret_cast<const f32x4*>(A + (int64_t)row * lda + k0 + 4 * c4);
-    }
+    for (int u = 0; u < LA; ++u)
+      ra[u] = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, voA, (int)((u * kRows * lda + k0) * 4), 0));
 #pragma unroll
-    for (int u = 0; u < LB; ++u) {
-      const int f = t + u * kThreads, row = f >> 3, c4 = f & 7;
-      rb[u] = *reinterpret_cast<const f32x4*>(B + (int64_t)row * ldb + k0 + 4 * c4);
-    }
+    for (int u = 0; u < LB; ++u)
+      rb[u] = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rB, voB, (int)((u * kRows * ldb + k0) * 4), 0));
   }
 
   __device__ __forceinline__ void store(float* sA, float* sB) {

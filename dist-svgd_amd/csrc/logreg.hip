@@ -112,6 +112,76 @@ __global__ __launch_bounds__(256) void logreg_finish_kernel(const float* __restr
   if (lane == 0) S[j * lds] = scale * (-a + 0.5f * (float)p - 0.5f * a * w2);
 }
 
+
+// ---- posterior-predictive test accuracy (experiments/logreg_plots.py:42-50) --
+// prob[q] = (1/n) sum_j sigma(xt_q . w_j) over the particles' weights w_j =
+// x_j[1:] (no bias, alpha unused, as the reference's _test_acc); the caller
+// thresholds prob > 0.5 against t_q > 0.  Z tiles on the NT engine; each
+// block reduces its 128 particle rows per test column into part[block row]
+// and predict_finish sums those partials in row-block order (deterministic).
+__global__ __launch_bounds__(256) void logreg_predict_kernel(const float* __restrict__ W,
+                                                             const float* __restrict__ Xt,
+                                                             int64_t ldb, int pp, int64_t n,
+                                                             int64_t Nt_pad,
+                                                             float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float smem[ZTile::kSmemFloats];
+  __shared__ float scol[2][128];
+  const int64_t i0 = (int64_t)blockIdx.y * ZTile::BM, q0 = (int64_t)blockIdx.x * ZTile::BN;
+  ZTile tile;
+  tile.run(W + i0 * ldb, ldb, Xt + q0 * ldb, ldb, pp, smem);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni) {
+    float s = 0.f;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t i = i0 + wm * 64 + mi * 32 + c_row(r, lane);
+        if (i < n) s += sigmoidf_stable(tile.acc[mi][ni][r]);
+      }
+    s += __shfl_xor(s, 32, 64);  // lanes l, l^32: the same column, the other 4-row half
+    if (lane < 32) scol[wm][wn * 64 + ni * 32 + lane] = s;
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 128; t += 256)
+    part[(int64_t)blockIdx.y * Nt_pad + q0 + t] = scol[0][t] + scol[1][t];
+}
+
+__global__ __launch_bounds__(256) void predict_finish_kernel(const float* __restrict__ part,
+                                                             int64_t nblk, int64_t Nt,
+                                                             int64_t Nt_pad, float inv_n,
+                                                             float* __restrict__ prob) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= Nt) return;
+  float s = 0.f;
+  for (int64_t b = 0; b < nblk; ++b) s += part[b * Nt_pad + q];
+  prob[q] = s * inv_n;
+}
+
+struct PredictWs {
+  int64_t n_pad, Nt_pad, pp;
+  size_t off_w, off_xt, off_part, total;
+};
+
+static PredictWs predict_ws(int64_t n, int64_t Nt, int64_t p) {
+  PredictWs w;
+  w.n_pad = roundup(n, 128);
+  w.Nt_pad = roundup(Nt, 128);
+  w.pp = roundup(p < 1 ? 1 : p, 32);
+  size_t o = 0;
+  auto take = [&](size_t floats) {
+    size_t at = o;
+    o += roundup((int64_t)(floats * sizeof(float)), 256);
+    return at;
+  };
+  w.off_w = take((size_t)w.n_pad * w.pp);
+  w.off_xt = take((size_t)w.Nt_pad * w.pp);
+  w.off_part = take((size_t)(w.n_pad / 128) * w.Nt_pad);
+  w.total = o;
+  return w;
+}
+
 }  // namespace dsvgd
 
 using namespace dsvgd;
@@ -158,6 +228,40 @@ int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const 
   hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,
                      w.ldb, scale, S, lds);
   return check_launch("logreg_finish");
+}
+
+size_t dsvgd_logreg_predict_workspace_bytes(int64_t n, int64_t Nt, int64_t p) {
+  return predict_ws(n, Nt, p).total;
+}
+
+int dsvgd_logreg_predict(const float* X, int64_t ldx, int64_t n, int64_t d, const float* Xt,
+                         int64_t ldxt, int64_t Nt, float* prob, void* workspace, void* stream) {
+  DSVGD_REQUIRE(X && Xt && prob && workspace, "null pointer");
+  DSVGD_REQUIRE(n > 0 && d >= 2 && Nt > 0 && ldx >= d && ldxt >= d - 1, "sizes");
+  DSVGD_REQUIRE(((uintptr_t)workspace & 255) == 0, "workspace must be 256-byte aligned");
+  const int64_t p = d - 1;
+  const PredictWs w = predict_ws(n, Nt, p);
+  DSVGD_REQUIRE(w.n_pad / 128 <= 65535, "too many particle tiles");
+  char* base = (char*)workspace;
+  float* Wp = (float*)(base + w.off_w);
+  float* Xtp = (float*)(base + w.off_xt);
+  float* part = (float*)(base + w.off_part);
+  hipStream_t s = (hipStream_t)stream;
+  int64_t tot = w.n_pad * w.pp;
+  hipLaunchKernelGGL(pad_copy_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, X, ldx, 1, n, p,
+                     w.n_pad, Wp, w.pp);
+  int rc = check_launch("pad_copy(W)");
+  if (rc) return rc;
+  tot = w.Nt_pad * w.pp;
+  hipLaunchKernelGGL(pad_copy_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Xt, ldxt, 0, Nt, p,
+                     w.Nt_pad, Xtp, w.pp);
+  if ((rc = check_launch("pad_copy(Xt)"))) return rc;
+  hipLaunchKernelGGL(logreg_predict_kernel, dim3(w.Nt_pad / 128, w.n_pad / 128), dim3(256), 0, s,
+                     Wp, Xtp, w.pp, (int)w.pp, n, w.Nt_pad, part);
+  if ((rc = check_launch("logreg_predict"))) return rc;
+  hipLaunchKernelGGL(predict_finish_kernel, dim3((Nt + 255) / 256), dim3(256), 0, s, part,
+                     w.n_pad / 128, Nt, w.Nt_pad, 1.f / (float)n, prob);
+  return check_launch("predict_finish");
 }
 
 }  // extern "C"

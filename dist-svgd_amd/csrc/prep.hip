@@ -30,6 +30,36 @@ int check_launch(const char* kernel) {
   return DSVGD_OK;
 }
 
+// Grid of a persistent kernel: resident blocks per CU (occupancy of `fn` at
+// 256 threads, no dynamic LDS) x CUs, a multiple of the 8 XCDs.  Cached per
+// (kernel, device).
+int persistent_blocks(const void* fn, int* blocks) {
+  struct Entry { const void* fn; int dev; int blocks; };
+  static thread_local Entry cache[16];
+  static thread_local int ncache = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    set_error("hipGetDevice failed");
+    return DSVGD_E_LAUNCH;
+  }
+  for (int i = 0; i < ncache; ++i)
+    if (cache[i].fn == fn && cache[i].dev == dev) {
+      *blocks = cache[i].blocks;
+      return DSVGD_OK;
+    }
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    set_error("occupancy query failed");
+    return DSVGD_E_LAUNCH;
+  }
+  int b = (per_cu < 1 ? 1 : per_cu) * cus;
+  b = b >= 8 ? b / 8 * 8 : 8;
+  if (ncache < 16) cache[ncache++] = Entry{fn, dev, b};
+  *blocks = b;
+  return DSVGD_OK;
+}
+
 // ---------------------------------------------------------------- mean ----
 // Deterministic two-level column sum: block b sums rows [b*R, (b+1)*R) of a
 // 64-column stripe into partial[b][c]; the second kernel sums the partials in

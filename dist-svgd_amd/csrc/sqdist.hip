@@ -13,8 +13,7 @@
 
 namespace dsvgd {
 
-template <bool DB>
-using GramTileT = NTTile<2, 2, 2, 2, DB>;  // 128 x 128 block, 4 waves of 64 x 64
+using GramTile = NTTile<2, 2, 2, 2>;  // 128 x 128 block, 4 waves of 64 x 64
 
 // Upper-triangle tile pair (bi <= bj) of linear block id b over T x T tiles.
 __device__ __forceinline__ void tri_decode(int64_t b, int T, int& bi, int& bj) {
@@ -44,9 +43,14 @@ __device__ __forceinline__ int64_t xcd_linear(int64_t b, int64_t total) {
 // Tile (bi, bj) of block b in a grid of `total` = groups * kGroup^2 blocks
 // over Tm x Tn tiles; SYM: groups over the upper triangle, tiles bi <= bj.
 // Returns false for the padding blocks of diagonal / edge groups.
+__device__ __forceinline__ bool tile_at(int64_t L, int Tm, int Tn, bool sym, int& bi, int& bj);
 __device__ __forceinline__ bool tile_of(int64_t b, int64_t total, int Tm, int Tn, bool sym,
                                         int& bi, int& bj) {
-  const int64_t L = xcd_linear(b, total);
+  return tile_at(xcd_linear(b, total), Tm, Tn, sym, bi, bj);
+}
+
+// Logical tile L (after the XCD remap) -> (bi, bj); false for padding tiles.
+__device__ __forceinline__ bool tile_at(int64_t L, int Tm, int Tn, bool sym, int& bi, int& bj) {
   const int64_t g = L / (kGroup * kGroup);
   const int w = (int)(L % (kGroup * kGroup));
   int gi, gj;
@@ -67,52 +71,23 @@ __host__ __device__ inline int64_t tile_grid(int64_t Tm, int64_t Tn, bool sym) {
   return (sym ? ngn * (ngn + 1) / 2 : ngm * ngn) * kGroup * kGroup;
 }
 
-// Rows [row0, row0+m) of Y against rows [0,n).  SYM (m == n, row0 == 0): only
-// tiles bi <= bj, the off-diagonal ones stored twice (tile + transpose) and
-// accounted with weight 2.
-template <bool SYM, int smode, bool DB>
-__global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y, int64_t ldy,
-                                                     const float* __restrict__ norms, int64_t row0,
-                                                     int64_t m, int64_t n, int64_t n_pad, int dp,
-                                                     float* __restrict__ D,
-                                                     dsvgd_select_state* __restrict__ st,
-                                                     float* __restrict__ cand, int epi) {
-  using GramTile = GramTileT<DB>;
-  __shared__ __attribute__((aligned(16))) float smem[GramTile::kSmemFloats];
-  __shared__ uint32_t shist[DSVGD_RADIX_BINS];
-  __shared__ float snorm[GramTile::BM + GramTile::BN];
-
-  int bi, bj;
-  const int Tm = (int)(roundup128(m) / 128), Tn = (int)(n_pad / 128);
-  const int w = threadIdx.x >> 6;
-  const int64_t slot = (int64_t)blockIdx.x * 4 + w;
-  if (!tile_of(blockIdx.x, gridDim.x, Tm, Tn, SYM, bi, bj)) {  // whole block, before any barrier
-    if (smode == kSelBracket) slot_clear(SlotLayout(cand, (int64_t)gridDim.x * 4, st->cand_cap), slot);
-    return;
-  }
+// Epilogue of one 128 x 128 distance tile (bi, bj) from the Gram
+// accumulators: D = max(0, |y_i|^2 + |y_j|^2 - 2 y_i.y_j) (diagonal exactly 0,
+// pads +inf) into the panel layout, the mirror tile for SYM off-diagonal
+// tiles, and the select accounting (weight 2 for mirrored tiles).
+// snorm: [0,128) the tile's row norms, [128,256) its column norms.
+template <bool SYM, int smode, bool ZERO = false>
+__device__ __forceinline__ void sq_epilogue(GramTile& tile, int bi, int bj, int64_t row0,
+                                            int64_t m, int64_t n, int64_t n_pad,
+                                            float* __restrict__ D, const float* snorm,
+                                            WindowHist& wh, uint32_t* shist, SlotWriter& sw,
+                                            const SlotLayout& sl, int64_t slot, int epi) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
   const bool mirror = SYM && bi != bj;
   const int64_t i0 = (int64_t)bi * GramTile::BM;  // within the owned block
   const int64_t j0 = (int64_t)bj * GramTile::BN;
-  if (smode == kSelHist)
-    for (int b = threadIdx.x; b < DSVGD_RADIX_BINS; b += 256) shist[b] = 0u;
-
-  GramTile tile;
-  tile.run(Y + (row0 + i0) * ldy, ldy, Y + j0 * ldy, ldy, dp, smem);
-
-  for (int t = threadIdx.x; t < GramTile::BM + GramTile::BN; t += 256)
-    snorm[t] = t < GramTile::BM ? norms[row0 + i0 + t] : norms[j0 + t - GramTile::BM];
-  __syncthreads();
-
-  const int lane = threadIdx.x & 63, wm = w >> 1, wn = w & 1;
   const uint32_t weight = mirror ? 2u : 1u;
-  WindowHist wh;
-  SlotWriter sw;
-  SlotLayout sl(cand, (int64_t)gridDim.x * 4, smode == kSelBracket ? st->cand_cap : 0);
-  if (smode == kSelBracket) {
-    sl.publish(st, blockIdx.x);
-    sw.begin(st, sl, slot);
-  }
-  // epilogue one 32x32 sub-tile (16 values per lane) at a time.  Panel-layout
+  // one 32x32 sub-tile (16 values per lane) at a time.  Panel-layout
   // addresses: per lane one base pointer per sub-tile, the per-register part
   // ((r&3)*16 + (r>>2)*128 floats) is a compile-time immediate.
   const int h4 = 4 * (lane >> 5);
@@ -154,10 +129,165 @@ __global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y
 #pragma unroll
         for (int r = 0; r < 16; ++r) sw.add(v[r]);
       }
+      if (ZERO) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tile.acc[mi][ni][r] = 0.f;
+      }
     }
   if (smode == kSelBracket) sw.finish(sl, slot, mirror);
+}
+
+// One tile per block.  Rows [row0, row0+m) of Y against rows [0,n).  SYM
+// (m == n, row0 == 0): only tiles bi <= bj, the off-diagonal ones stored
+// twice (tile + transpose) and accounted with weight 2.
+template <bool SYM, int smode>
+__global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y, int64_t ldy,
+                                                     const float* __restrict__ norms, int64_t row0,
+                                                     int64_t m, int64_t n, int64_t n_pad, int dp,
+                                                     float* __restrict__ D,
+                                                     dsvgd_select_state* __restrict__ st,
+                                                     float* __restrict__ cand, int epi) {
+  __shared__ __attribute__((aligned(16))) float smem[GramTile::kSmemFloats];
+  __shared__ uint32_t shist[DSVGD_RADIX_BINS];
+  __shared__ float snorm[GramTile::BM + GramTile::BN];
+
+  int bi, bj;
+  const int Tm = (int)(roundup128(m) / 128), Tn = (int)(n_pad / 128);
+  const int w = threadIdx.x >> 6;
+  const int64_t slot = (int64_t)blockIdx.x * 4 + w;
+  SlotLayout sl(cand, (int64_t)gridDim.x * 4, smode == kSelBracket ? st->cand_cap : 0);
+  if (!tile_of(blockIdx.x, gridDim.x, Tm, Tn, SYM, bi, bj)) {  // whole block, before any barrier
+    if (smode == kSelBracket) slot_clear(sl, slot);
+    return;
+  }
+  const int64_t i0 = (int64_t)bi * GramTile::BM;
+  const int64_t j0 = (int64_t)bj * GramTile::BN;
+  if (smode == kSelHist)
+    for (int b = threadIdx.x; b < DSVGD_RADIX_BINS; b += 256) shist[b] = 0u;
+
+  GramTile tile;
+  tile.run(Y + (row0 + i0) * ldy, ldy, Y + j0 * ldy, ldy, dp, smem);
+
+  for (int t = threadIdx.x; t < GramTile::BM + GramTile::BN; t += 256)
+    snorm[t] = t < GramTile::BM ? norms[row0 + i0 + t] : norms[j0 + t - GramTile::BM];
+  __syncthreads();
+
+  WindowHist wh;
+  SlotWriter sw;
+  if (smode == kSelBracket) {
+    sl.publish(st, blockIdx.x);
+    sw.begin(st, sl, slot);
+  }
+  sq_epilogue<SYM, smode>(tile, bi, bj, row0, m, n, n_pad, D, snorm, wh, shist, sw, sl, slot, epi);
   if (smode == kSelHist) {
     wh.flush(shist);
+    __syncthreads();
+    flush_block_hist(shist, st);
+  }
+}
+
+// Persistent form: a grid of (resident blocks per CU) x CUs; block b (on XCD
+// b % 8 under round-robin dispatch) walks the logical tiles L = lo_x + u,
+// lo_x + u + U, ... of its XCD's contiguous range (same L2-grouped order as
+// above).  The first K-step of the next tile (and its norms) is loaded while
+// the current tile's last K-step computes, so a tile's load latency hides
+// under the previous tile's MFMAs and epilogue -- at dp = 256 a tile is only
+// 8 K-steps, and that per-tile latency is what one-tile blocks lose.
+// Candidate slots are per (logical tile, wave); the digit-1 histogram stays
+// in LDS across a block's tiles (one global flush).
+template <bool SYM, int smode>
+__global__ __launch_bounds__(256, 2) void sqdist_persistent_kernel(
+    const float* __restrict__ Y, int64_t ldy, const float* __restrict__ norms, int64_t row0,
+    int64_t m, int64_t n, int64_t n_pad, int dp, float* __restrict__ D,
+    dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int epi, int64_t total) {
+  __shared__ __attribute__((aligned(16))) float smem[GramTile::kSmemFloats];
+  __shared__ uint32_t shist[DSVGD_RADIX_BINS];
+  __shared__ float snorm[2][GramTile::BM + GramTile::BN];  // current / next tile
+  float* const sA = smem;
+  float* const sB = smem + GramTile::BM * GramTile::LDK;
+
+  const int Tm = (int)(roundup128(m) / 128), Tn = (int)(n_pad / 128);
+  const int t = threadIdx.x, w = t >> 6, wm = w >> 1, wn = w & 1;
+  const int64_t x = blockIdx.x % kXcds, u = blockIdx.x / kXcds, U = gridDim.x / kXcds;
+  const int64_t q = total / kXcds, rr = total % kXcds;
+  const int64_t lo = x * q + min(x, rr);
+  const int64_t hi = (int64_t)__builtin_amdgcn_readfirstlane((int)(lo + q + (x < rr ? 1 : 0)));
+  SlotLayout sl(cand, total * 4, smode == kSelBracket ? st->cand_cap : 0);
+  if (smode == kSelBracket) sl.publish(st, blockIdx.x);
+  if (smode == kSelHist)
+    for (int b = t; b < DSVGD_RADIX_BINS; b += 256) shist[b] = 0u;
+
+  // next valid logical tile at or after L (padding tiles: empty slots)
+  // (tile indices are block-uniform: readfirstlane keeps them -- and every
+  // address derived from them -- in SGPRs)
+  auto next_valid = [&](int64_t L, int& bi, int& bj) -> int64_t {
+    for (; L < hi; L += U) {
+      if (tile_at(L, Tm, Tn, SYM, bi, bj)) {
+        bi = __builtin_amdgcn_readfirstlane(bi);
+        bj = __builtin_amdgcn_readfirstlane(bj);
+        return L;
+      }
+      if (smode == kSelBracket) slot_clear(sl, L * 4 + w);
+    }
+    return L;
+  };
+  auto norm_of = [&](int bi, int bj) -> float {
+    return t < 128 ? norms[row0 + (int64_t)bi * 128 + t] : norms[(int64_t)bj * 128 + t - 128];
+  };
+  int bi, bj;
+  int64_t L = next_valid((int64_t)__builtin_amdgcn_readfirstlane((int)(lo + u)), bi, bj);
+  GramTile tile;
+  tile.zero();  // the epilogue re-zeroes each sub-tile after consuming it
+  const int nk = dp / GramTile::BK;
+  int par = 0;
+  if (L < hi) {  // stage K-step 0 of the first tile
+    tile.load(Y + (row0 + (int64_t)bi * 128) * ldy, ldy, Y + (int64_t)bj * 128 * ldy, ldy, 0);
+    snorm[0][t] = norm_of(bi, bj);
+    tile.store(sA, sB);
+  }
+  __syncthreads();
+  // Per K-step: issue the next stage's loads (the next tile's K-step 0 after
+  // the last one), MFMAs on the staged one, barrier, write the next stage,
+  // barrier.  The staging registers are dead again before the epilogue.
+  while (L < hi) {
+    int bin = 0, bjn = 0;
+    const int64_t Ln = next_valid(L + U, bin, bjn);
+    const bool has_next = Ln < hi;
+    const float* Ab = Y + (row0 + (int64_t)bi * 128) * ldy;
+    const float* Bb = Y + (int64_t)bj * 128 * ldy;
+    const float* An = Y + (row0 + (int64_t)bin * 128) * ldy;
+    const float* Bn = Y + (int64_t)bjn * 128 * ldy;
+#pragma unroll 1
+    for (int ks = 0; ks < nk; ++ks) {
+      const bool last = ks + 1 == nk;
+      // one load site (one register set): this tile's next K-step, or the
+      // next tile's first
+      const bool more = !last || has_next;
+      float nrm = 0.f;
+      if (more)
+        tile.load(last ? An : Ab, ldy, last ? Bn : Bb, ldy, last ? 0 : (ks + 1) * GramTile::BK);
+      if (last && has_next) nrm = norm_of(bin, bjn);
+      tile.compute(sA, sB, wm, wn);
+      __syncthreads();
+      if (more) {
+        tile.store(sA, sB);
+        if (last) snorm[par ^ 1][t] = nrm;
+      }
+      __syncthreads();
+    }
+    const int64_t slot = L * 4 + w;
+    WindowHist wh;
+    SlotWriter sw;
+    if (smode == kSelBracket) sw.begin(st, sl, slot);
+    sq_epilogue<SYM, smode, true>(tile, bi, bj, row0, m, n, n_pad, D, snorm[par], wh, shist, sw, sl,
+                                  slot, epi);
+    if (smode == kSelHist) wh.flush(shist);
+    par ^= 1;
+    L = Ln;
+    bi = bin;
+    bj = bjn;
+  }
+  if (smode == kSelHist) {
     __syncthreads();
     flush_block_hist(shist, st);
   }
@@ -263,27 +393,35 @@ int launch_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0,
   // mirror stores (1) or every D store (2), to price the epilogue.
   const char* ep = getenv("DSVGD_SQ_EPI");
   const int epi = ep ? atoi(ep) : 0;
-  // DSVGD_SQ_DB=1: the double-buffered NT mainloop (A/B switch)
-  const char* db = getenv("DSVGD_SQ_DB");
-  const bool dbuf = db && db[0] == '1';
+  // DSVGD_SQ_PERSIST=0: one tile per block (A/B switch against the persistent form)
+  const char* pe = getenv("DSVGD_SQ_PERSIST");
+  const bool persist = !(pe && pe[0] == '0');
   const bool sym = m == n && row0 == 0;
   const int64_t T = n_pad / 128;
-  const dim3 grid((unsigned)(sym ? tile_grid(T, T, true) : tile_grid(m_pad / 128, T, false)));
-#define DSVGD_SQ_LAUNCH(SYMV, DBV)                                                             \
-  hipLaunchKernelGGL((sqdist_kernel<SYMV, SM, DBV>), grid, dim3(256), 0, s, Y, ldy, norms, row0, \
-                     m, n, n_pad, (int)dp, D, st, cand, epi)
-  if (sym) {
-    if (dbuf)
-      DSVGD_SQ_LAUNCH(true, true);
+  const int64_t total = sym ? tile_grid(T, T, true) : tile_grid(m_pad / 128, T, false);
+  if (persist) {
+    int blocks = 0;
+    int rc = sym ? persistent_blocks(
+                       reinterpret_cast<const void*>(&sqdist_persistent_kernel<true, SM>), &blocks)
+                 : persistent_blocks(
+                       reinterpret_cast<const void*>(&sqdist_persistent_kernel<false, SM>), &blocks);
+    if (rc) return rc;
+    const dim3 grid((unsigned)blocks);
+    if (sym)
+      hipLaunchKernelGGL((sqdist_persistent_kernel<true, SM>), grid, dim3(256), 0, s, Y, ldy, norms,
+                         row0, m, n, n_pad, (int)dp, D, st, cand, epi, total);
     else
-      DSVGD_SQ_LAUNCH(true, false);
-  } else {
-    if (dbuf)
-      DSVGD_SQ_LAUNCH(false, true);
-    else
-      DSVGD_SQ_LAUNCH(false, false);
+      hipLaunchKernelGGL((sqdist_persistent_kernel<false, SM>), grid, dim3(256), 0, s, Y, ldy,
+                         norms, row0, m, n, n_pad, (int)dp, D, st, cand, epi, total);
+    return check_launch("sqdist_persistent");
   }
-#undef DSVGD_SQ_LAUNCH
+  const dim3 grid((unsigned)total);
+  if (sym)
+    hipLaunchKernelGGL((sqdist_kernel<true, SM>), grid, dim3(256), 0, s, Y, ldy, norms, row0, m, n,
+                       n_pad, (int)dp, D, st, cand, epi);
+  else
+    hipLaunchKernelGGL((sqdist_kernel<false, SM>), grid, dim3(256), 0, s, Y, ldy, norms, row0, m,
+                       n, n_pad, (int)dp, D, st, cand, epi);
   return check_launch("sqdist");
 }
 

@@ -7,8 +7,8 @@ C ABI in include/dsvgd.h); there is no CPU compute path.
 name = 'dsvgd'
 from .sampler import Sampler  # noqa: E402
 from .distsampler import DistSampler  # noqa: E402
-from . import kernels, targets  # noqa: E402
+from . import kernels, metrics, targets  # noqa: E402
 from .kernels import RBF  # noqa: E402
 from .engine import PhiEngine  # noqa: E402
 
-__all__ = ["name", "Sampler", "DistSampler", "RBF", "PhiEngine", "kernels", "targets"]
+__all__ = ["name", "Sampler", "DistSampler", "RBF", "PhiEngine", "kernels", "metrics", "targets"]

@@ -53,6 +53,8 @@ SIGNATURES = {
     "dsvgd_logreg_workspace_bytes": (_c.c_size_t, [_i64, _i64, _i64]),
     "dsvgd_score_logreg": (_int, [_p, _i64, _i64, _i64, _p, _i64, _p, _i64, _f, _p, _i64, _p,
                                   _p]),
+    "dsvgd_logreg_predict_workspace_bytes": (_c.c_size_t, [_i64, _i64, _i64]),
+    "dsvgd_logreg_predict": (_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _p, _p]),
 }
 
 

@@ -247,6 +247,17 @@ int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const 
                        int64_t ldxd, const float* t, int64_t N, float scale, float* S, int64_t lds,
                        void* workspace, void* stream);
 
+/* Posterior-predictive probability of the logistic-regression test set:
+ * prob[q] = (1/n) sum_j sigma(xt_q . w_j), w_j = X[j][1:d] (no bias; alpha
+ * unused) -- the ensemble mean of experiments/logreg_plots.py:42-50
+ * (`_test_acc`), which the caller thresholds (prob > 0.5 vs t > 0) for the
+ * test accuracy.  fp32 (the reference evaluates it in fp64 with numpy).
+ * Xt: Nt x (d-1) row-major; workspace of
+ * dsvgd_logreg_predict_workspace_bytes(n, Nt, d-1) bytes, 256-B aligned. */
+size_t dsvgd_logreg_predict_workspace_bytes(int64_t n, int64_t Nt, int64_t p);
+int dsvgd_logreg_predict(const float* X, int64_t ldx, int64_t n, int64_t d, const float* Xt,
+                         int64_t ldxt, int64_t Nt, float* prob, void* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

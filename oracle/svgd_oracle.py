@@ -271,11 +271,15 @@ class DistOracle:
 
 
 # --------------------------------------------------------------- metric --
+def predictive_prob(particles, x_test):
+    """logreg_plots.py:44-48: mean over particles of expit(x_test . w), w = x[1:]."""
+    P = np.asarray(particles, np.float64)
+    return _sigmoid(np.asarray(x_test, np.float64) @ P[:, 1:].T).mean(1)
+
+
 def test_accuracy(particles, x_test, t_test):
     """logreg_plots.py:42-50: posterior-predictive ensemble accuracy."""
-    P = np.asarray(particles, np.float64)
-    w = P[:, 1:]
-    prob = _sigmoid(np.asarray(x_test, np.float64) @ w.T).mean(1)
+    prob = predictive_prob(particles, x_test)
     return float(((prob > 0.5) == (np.asarray(t_test).reshape(-1) > 0)).mean())
 
 

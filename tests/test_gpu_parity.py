@@ -620,8 +620,29 @@ def test_logreg_test_accuracy_after_T_steps(order, n, T):
     se = np.sqrt(ref[:, 1:].var(0) / n)
     assert np.all(np.abs(got[:, 1:].mean(0) - ref[:, 1:].mean(0)) < 0.01 * se + 1e-5)
     assert np.all(np.abs(got[:, 1:].var(0) / ref[:, 1:].var(0) - 1) < 1e-3)
-    acc_gpu = O.test_accuracy(got, x_test, t_test)
+    acc_gpu = dsvgd().metrics.test_accuracy(ds._work, x_test, t_test)   # on the GPU
+    assert acc_gpu == O.test_accuracy(got, x_test, t_test)
     acc_ref = O.test_accuracy(ref, x_test, t_test)
     record_parity(err, acc_gpu=acc_gpu, acc_oracle=acc_ref)
     assert abs(acc_gpu - acc_ref) <= 0.01
     assert acc_gpu > 0.6        # the posterior predicts (chance is ~0.5)
+
+
+@pytest.mark.parametrize("n,d,Nt", [(100, 3, 4900), (1000, 256, 3000), (300, 1024, 129),
+                                    (4200, 33, 1)])
+def test_predictive_prob_and_test_accuracy(n, d, Nt):
+    """dsvgd.metrics (dsvgd_logreg_predict) vs the fp64 restatement of
+    logreg_plots.py:42-50: ensemble-mean probabilities within 2e-6 absolute;
+    the accuracy identical except for test points within 1e-5 of 0.5."""
+    rs = np.random.RandomState(n + d)
+    P = (rs.randn(n, d) * 0.5).astype(np.float32)
+    xt = (rs.randn(Nt, d - 1) / np.sqrt(d)).astype(np.float32)
+    tt = np.where(rs.randn(Nt) > 0, 1.0, -1.0).astype(np.float32)
+    prob = dsvgd().metrics.predictive_prob(gpu(P), xt).cpu().numpy()
+    ref = O.predictive_prob(P, xt)
+    assert abs_err(prob, ref) < 2e-6
+    acc = dsvgd().metrics.test_accuracy(gpu(P), xt, tt)
+    sure = np.abs(ref - 0.5) > 1e-5
+    agree = ((ref > 0.5) == (tt > 0))
+    lo, hi = agree[sure].sum() / Nt, (agree[sure].sum() + (~sure).sum()) / Nt
+    assert lo - 1e-12 <= acc <= hi + 1e-12
