@@ -223,17 +223,26 @@ struct NNTile {
     c4 = fi & 3;
   }
 
-  int64_t amask = -1;  // timing experiments only: A panel index mask (-1 = off)
-
+  // Buffer loads: per-lane byte offsets are loop invariant (one 32-bit VGPR
+  // each, hoisted), the K-step position is a scalar offset, so the K loop
+  // carries no 64-bit address arithmetic on the VALU (every VALU instruction
+  // beside the f32 MFMAs costs MFMA issue time).
   __device__ __forceinline__ void load(const float* __restrict__ Apanels, const float* __restrict__ B,
                                        int64_t ldb, int64_t j0) {
     const int t = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rA =
+        __builtin_amdgcn_make_buffer_rsrc((void*)Apanels, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB =
+        __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, 0x7fffffff, 0x00020000);
+    const int soA = (int)((j0 >> 4) * kPanelElems * 4);
+    const int soB = (int)(j0 * ldb * 4);
 #pragma unroll
     for (int u = 0; u < LA; ++u) {
       int p, row, c4;
       a_map(t, u, p, row, c4);
-      const float* ap = Apanels + (((j0 >> 4) + p) & amask) * kPanelElems;  // 8 KiB panel
-      ra[u] = *reinterpret_cast<const f32x4*>(ap + row * 16 + 4 * c4);
+      ra[u] = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, (p * kPanelElems + row * 16 + 4 * c4) * 4,
+                                                       soA, 0));
     }
     if (BT) {
 #pragma unroll
@@ -243,14 +252,17 @@ struct NNTile {
           const int rg = blk / (BC / 4), cg = blk % (BC / 4);
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            rb[4 * u + i] = *reinterpret_cast<const f32x4*>(B + (j0 + 4 * rg + i) * ldb + 4 * cg);
+            rb[4 * u + i] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                           rB, (int)(((4 * rg + i) * ldb + 4 * cg) * 4), soB, 0));
         }
       }
     } else {
 #pragma unroll
       for (int u = 0; u < LB; ++u) {
         const int f = t + u * kThreads, row = f / (BC / 4), c4 = f % (BC / 4);
-        rb[u] = *reinterpret_cast<const f32x4*>(B + (j0 + row) * ldb + 4 * c4);
+        rb[u] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rB, (int)((row * ldb + 4 * c4) * 4), soB, 0));
       }
     }
   }
@@ -271,7 +283,8 @@ struct NNTile {
       a_map(t, u, p, row, c4);
       const int chunk = 4 * p + c4;
       if (EXP) {
-        const int64_t qd = dgl + row - 4 * chunk;
+        // |dgl| < 2^31 for every launch the ABI accepts (rows, columns < 2^31)
+        const int qd = (int)dgl + row - 4 * chunk;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           ra[u][q] = (qd == q) ? 0.f : __builtin_amdgcn_exp2f(ra[u][q] * scale);
@@ -321,17 +334,22 @@ struct NNTile {
             for (int ni = 0; ni < TN; ++ni)
               acc[mi][ni] = mfma32(a[mi][t4], b4[ni][t4], acc[mi][ni]);
       } else {
+        // all of this group's B fragments are read before its MFMAs (one
+        // LDS wait per group instead of one per 4-MFMA cluster)
+        float b[4][TN];
 #pragma unroll
         for (int t4 = 0; t4 < 4; ++t4) {
-          float b[TN];
           const float* brow = sB + (8 * g + 4 * h + t4) * BC + wc * 32 * TN + r;
 #pragma unroll
-          for (int ni = 0; ni < TN; ++ni) b[ni] = brow[ni * 32];
+          for (int ni = 0; ni < TN; ++ni) b[t4][ni] = brow[ni * 32];
+        }
+#pragma unroll
+        for (int t4 = 0; t4 < 4; ++t4) {
           if (PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = mfma32(a[mi][t4], b[ni], acc[mi][ni]);
+            for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = mfma32(a[mi][t4], b[t4][ni], acc[mi][ni]);
           if (PRIO == 1) __builtin_amdgcn_s_setprio(0);
         }
       }

@@ -68,7 +68,11 @@ __device__ __forceinline__ float sigmoidf_stable(float u) {
   return e / (1.f + e);
 }
 
-// G[j][q] = t_q sigma(-t_q (w_j . xd_q)), zero for padded q; panel layout.
+// G[j][q] = t_q sigma(-t_q (w_j . xd_q)) = t_q / (1 + exp(t_q z)), zero for
+// padded q (t_q = 0 there); panel layout.  The epilogue is VALU work beside
+// the other resident blocks' f32 MFMAs (they share the SIMD's issue), so it
+// is kept short: exp2 + rcp (~1 ulp each) and store addresses that are one
+// per-lane base plus compile-time offsets (as the distance epilogue).
 __global__ __launch_bounds__(256) void logreg_z_kernel(const float* __restrict__ W,
                                                        const float* __restrict__ Xd, int64_t ldb,
                                                        int pp, const float* __restrict__ tp,
@@ -79,19 +83,23 @@ __global__ __launch_bounds__(256) void logreg_z_kernel(const float* __restrict__
   ZTile tile;
   tile.run(W + i0 * ldb, ldb, Xd + q0 * ldb, ldb, pp, smem);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
+  const int h4 = 4 * (lane >> 5);
+  float* const Gt = G + ((int64_t)blockIdx.y * (N_pad >> 4) + (q0 >> 4)) * kPanelElems;
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
+  for (int ni = 0; ni < 2; ++ni) {
+    const int cl = wn * 64 + ni * 32 + (lane & 31);
+    const float tq = tp[q0 + cl];
+    const float sc = tq * kLog2e;
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      const int64_t q = q0 + wn * 64 + ni * 32 + (lane & 31);
-      const float tq = tp[q];
+    for (int mi = 0; mi < 2; ++mi) {
+      float* const g0 = Gt + (cl >> 4) * kPanelElems + (cl & 15) + (wm * 64 + mi * 32 + h4) * 16;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int64_t i = i0 + wm * 64 + mi * 32 + c_row(r, lane);
-        const float z = tile.acc[mi][ni][r];
-        G[panel_off(i, q, N_pad)] = (q < N) ? tq * sigmoidf_stable(-tq * z) : 0.f;
+        const float e = __builtin_amdgcn_exp2f(sc * tile.acc[mi][ni][r]);
+        g0[(r & 3) * 16 + (r >> 2) * 128] = tq * __builtin_amdgcn_rcpf(1.f + e);
       }
     }
+  }
 }
 
 // one wave per particle row

@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
                                                       const dsvgd_select_state* __restrict__ st,
                                                       float* __restrict__ C, int64_t ldc,
                                                       float* __restrict__ rowsum, int64_t m,
-                                                      int64_t row0, int64_t amask) {
+                                                      int64_t row0) {
   using Tile = NNTile<TN, EXP, WM, TM, BT, BJ, PRIO>;
   __shared__ __attribute__((aligned(16))) float smem[Tile::kSmemFloats];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
@@ -39,7 +39,6 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
   float scale = 0.f;
   if (EXP) scale = -st->inv_h * kLog2e;
   Tile tile;
-  tile.amask = amask;
   tile.run(A + (i0 >> 7) * (a_npad >> 4) * kPanelElems + (i0 & 127) * 16, B + c0, ldb, k0, k1,
            scale, smem, row0 + i0);
 
@@ -252,17 +251,12 @@ int launch_nn_shape(bool exp_, const float* A, const float* B, int64_t ldb, int6
   if (K % BJ != 0) return fail_arg("nn_kernel: K must be a multiple of the K-step");
   const int64_t kchunk = roundup((K + splits - 1) / splits, BJ);
   const dim3 grid(cols / (128 * TN), roundup(m, BM) / BM, splits);
-  // DSVGD_NN_AMASK=<int>: TIMING EXPERIMENTS ONLY (wrong results) -- A panel
-  // index & mask, so blocks re-read a few L2-resident panels instead of
-  // streaming D from HBM (prices the HBM latency of the A operand).
-  const char* am = getenv("DSVGD_NN_AMASK");
-  const int64_t amask = am ? atoll(am) : -1;
   if (exp_)
     hipLaunchKernelGGL((nn_kernel<TN, true, WM, TM, BT, BJ, PRIO>), grid, dim3(256 * WM), 0, s, A, K, B,
-                       ldb, K, kchunk, st, C, ldc, rowsum, m, row0, amask);
+                       ldb, K, kchunk, st, C, ldc, rowsum, m, row0);
   else
     hipLaunchKernelGGL((nn_kernel<TN, false, WM, TM, BT, BJ, PRIO>), grid, dim3(256 * WM), 0, s, A, K, B,
-                       ldb, K, kchunk, st, C, ldc, rowsum, m, row0, amask);
+                       ldb, K, kchunk, st, C, ldc, rowsum, m, row0);
   return check_launch("nn_kernel");
 }
 

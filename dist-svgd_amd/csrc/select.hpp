@@ -111,18 +111,25 @@ struct SlotWriter {
   uint32_t cnt = 0;    // wave-uniform: entries in [lo, hi] so far (may exceed cap)
   uint32_t below = 0;  // per lane
   uint32_t cap = 0;
-  float lo = 0.f, hi = -1.f;
+  // keys: fp32 bit patterns, monotone for the values >= 0 (and +inf) this
+  // sees; in-bracket is one unsigned range test, key - klo <= khi - klo
+  uint32_t klo = 1u, kspan = 0u;
   __device__ __forceinline__ void begin(const dsvgd_select_state* st, const SlotLayout& L,
                                         int64_t slot) {
-    lo = st->lo;
-    hi = st->hi;
+    const float lo = st->lo, hi = st->hi;
+    // an unordered bracket (NaN sample) counts everything below and nothing
+    // in range, so bracket_check falls back to the exact passes over D
+    const bool ok = hi >= lo && lo >= 0.f;
+    klo = ok ? __float_as_uint(lo) : 0xFFFFFFFFu;
+    kspan = ok ? __float_as_uint(hi) - klo : 0u;
     dst = L.data + slot * L.cap;
     cap = (uint32_t)L.cap;
   }
   // every lane of the wave must call add() for the same value index
   __device__ __forceinline__ void add(float v) {
-    below += (v < lo) ? 1u : 0u;
-    const bool in = v >= lo && v <= hi;
+    const uint32_t key = __float_as_uint(v);
+    below += key < klo ? 1u : 0u;
+    const bool in = key - klo <= kspan;
     const uint64_t bal = __ballot(in);
     if (bal) {
       if (in) {

@@ -93,28 +93,41 @@ __device__ __forceinline__ void sq_epilogue(GramTile& tile, int bi, int bj, int6
   const int h4 = 4 * (lane >> 5);
   float* const Dtile = D + ((int64_t)bi * (n_pad >> 4) + (int64_t)bj * 8) * kPanelElems;
   float* const Dmir = D + ((int64_t)bj * (n_pad >> 4) + (int64_t)bi * 8) * kPanelElems;
+  // interior tiles (the bulk): no diagonal entry, every row and column valid
+  // -> 3 VALU per value; edge / diagonal tiles take the guarded form
+  const bool interior = (row0 + i0 + 128 <= j0 || j0 + 128 <= row0 + i0) && i0 + 128 <= m &&
+                        j0 + 128 <= n;
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
       const int cl = wn * 64 + ni * 32 + (lane & 31);
       const int rb = wm * 64 + mi * 32 + h4;  // this lane's first row in the sub-tile
-      const bool colok = j0 + cl < n;
       const float nj = snorm[GramTile::BM + cl];
       float* const dp0 = Dtile + (cl >> 4) * kPanelElems + (cl & 15) + rb * 16;
       float v[16];
+      if (interior) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rl = rb + (r & 3) + 8 * (r >> 2);
-        float x;
-        if (colok && i0 + rl < m)
-          x = (row0 + i0 + rl == j0 + cl) ? 0.f
-                                          : fmaxf(0.f, (snorm[rl] + nj) - 2.f * tile.acc[mi][ni][r]);
-        else
-          x = INFINITY;
-        v[r] = x;
-        if (epi < 2 || x != x) dp0[(r & 3) * 16 + (r >> 2) * 128] = x;
+        for (int r = 0; r < 16; ++r)
+          v[r] = fmaxf(0.f, (snorm[rb + (r & 3) + 8 * (r >> 2)] + nj) - 2.f * tile.acc[mi][ni][r]);
+      } else {
+        const bool colok = j0 + cl < n;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = rb + (r & 3) + 8 * (r >> 2);
+          float x;
+          if (colok && i0 + rl < m)
+            x = (row0 + i0 + rl == j0 + cl)
+                    ? 0.f
+                    : fmaxf(0.f, (snorm[rl] + nj) - 2.f * tile.acc[mi][ni][r]);
+          else
+            x = INFINITY;
+          v[r] = x;
+        }
       }
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (epi < 2 || v[r] != v[r]) dp0[(r & 3) * 16 + (r >> 2) * 128] = v[r];
       if (mirror && (epi == 0 || v[0] != v[0])) {  // D[j][i]: 4 consecutive i per register quad -> 16-byte stores
         float* const mp0 = Dmir + (int64_t)cl * 16 + (wm * 4 + mi * 2) * kPanelElems + h4;
 #pragma unroll

@@ -43,4 +43,4 @@ def test_accuracy(particles, x_test, t_test):
     with t_test > 0 (logreg_plots.py:42-50)."""
     prob = predictive_prob(particles, x_test)
     t = _device_f32(t_test, prob.device).reshape(-1)
-    return float(((prob > 0.5) == (t > 0)).float().mean())
+    return int(((prob > 0.5) == (t > 0)).sum()) / prob.numel()
