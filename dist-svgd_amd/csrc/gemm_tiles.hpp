@@ -35,6 +35,63 @@ __host__ __device__ inline int64_t panel_off(int64_t i, int64_t j, int64_t npad)
   return ((i >> 7) * (npad >> 4) + (j >> 4)) * kPanelElems + (i & 127) * 16 + (j & 15);
 }
 
+// ------------------------------------------------------ tile schedules ----
+// Upper-triangle tile pair (bi <= bj) of linear block id b over T x T tiles.
+__device__ __forceinline__ void tri_decode(int64_t b, int T, int& bi, int& bj) {
+  const double A = (double)T + 0.5;
+  int x = (int)(A - sqrt(A * A - 2.0 * (double)b));
+  auto off = [&](int r) { return (int64_t)r * T - (int64_t)r * (r - 1) / 2; };
+  while (x > 0 && off(x) > b) --x;
+  while (x + 1 < T && off(x + 1) <= b) ++x;
+  bi = x;
+  bj = x + (int)(b - off(x));
+}
+
+// XCD-aware, L2-grouped tile order.  Workgroups are dispatched round-robin
+// over the 8 XCDs (block b runs on XCD b % 8), each with its own 4 MiB L2.
+// xcd_linear gives XCD x a contiguous range of logical tiles, and logical
+// tiles run in groups of kGroup x kGroup tiles, so the rows an XCD re-reads
+// (kGroup A + kGroup B blocks of 128 rows x dp, 2 MiB at dp = 256) stay in
+// its L2 instead of re-streaming Y from MALL for every row panel.
+constexpr int kXcds = 8;
+constexpr int kGroup = 8;
+
+__device__ __forceinline__ int64_t xcd_linear(int64_t b, int64_t total) {
+  const int64_t q = total / kXcds, r = total % kXcds, x = b % kXcds;
+  return x * q + min(x, r) + b / kXcds;
+}
+
+// Tile (bi, bj) of block b in a grid of `total` = groups * kGroup^2 blocks
+// over Tm x Tn tiles; SYM: groups over the upper triangle, tiles bi <= bj.
+// Returns false for the padding blocks of diagonal / edge groups.
+__device__ __forceinline__ bool tile_at(int64_t L, int Tm, int Tn, bool sym, int& bi, int& bj);
+__device__ __forceinline__ bool tile_of(int64_t b, int64_t total, int Tm, int Tn, bool sym,
+                                        int& bi, int& bj) {
+  return tile_at(xcd_linear(b, total), Tm, Tn, sym, bi, bj);
+}
+
+// Logical tile L (after the XCD remap) -> (bi, bj); false for padding tiles.
+__device__ __forceinline__ bool tile_at(int64_t L, int Tm, int Tn, bool sym, int& bi, int& bj) {
+  const int64_t g = L / (kGroup * kGroup);
+  const int w = (int)(L % (kGroup * kGroup));
+  int gi, gj;
+  if (sym) {
+    tri_decode(g, (Tn + kGroup - 1) / kGroup, gi, gj);
+  } else {
+    const int ngn = (Tn + kGroup - 1) / kGroup;
+    gi = (int)(g / ngn);
+    gj = (int)(g % ngn);
+  }
+  bi = gi * kGroup + w / kGroup;
+  bj = gj * kGroup + w % kGroup;
+  return bi < Tm && bj < Tn && (!sym || bi <= bj);
+}
+
+__host__ __device__ inline int64_t tile_grid(int64_t Tm, int64_t Tn, bool sym) {
+  const int64_t ngm = (Tm + kGroup - 1) / kGroup, ngn = (Tn + kGroup - 1) / kGroup;
+  return (sym ? ngn * (ngn + 1) / 2 : ngm * ngn) * kGroup * kGroup;
+}
+
 // ------------------------------------------------------------ NT engine ----
 // Block = WM x WN waves, each wave TM x TN tiles of 32x32; BK = 32.
 // DB: double-buffered LDS (one barrier per K-step, the next K-tile written
@@ -161,28 +218,18 @@ struct NTTile {
 // ------------------------------------------------------------ NN engine ----
 // Block = WM x 4 waves (256*WM threads): wave (wr, wc) owns rows
 // [wr*32*TM, +32*TM) x columns [wc*32*TN, +32*TN), i.e. 16*TM*TN accumulator
-// registers; BM = 32*TM*WM rows (64 or 128) per block.  Shapes in use:
-//   WM=1 TM=4 (128 rows, 256 AGPRs, 1 wave/SIMD), WM=2 TM=2 (128 rows, two
-//   waves per SIMD in one block), WM=1 TM=2 (64 rows, two blocks per CU: one
-//   block's barrier wait hides under the other block's MFMAs).
-// K-step = one 16-column panel slice of A (BM rows) and 16 rows of B.
-//
-// BT (transposed B image): the B tile is stored column-major [BC][BJ+4] so a
-// lane's 4 k-values of one column are one ds_read_b128 (8 per K-step instead
-// of 16 ds_read2_b32); each thread loads 4x4 blocks (4 rows x float4) and
-// writes their columns as float4s.
+// registers; BM = 32*TM*WM rows per block.  In use: WM=2 TM=2 (128 rows, two
+// waves per SIMD in one block, 128 accumulators each).  (Measured and
+// dropped: 1 wave/SIMD with 256 accumulators, 64-row blocks at 2 per CU, a
+// transposed B image, s_setprio around the MFMA clusters -- all slower.)
+// K-step = BJ columns of A (one or two 16-column panels) and BJ rows of B.
 //
 // BJ_ = 32: 32-deep K-steps (two D panels per step: half the barriers and
 // LDS-read restarts per unit of work).  Double-buffered that is exactly
 // 2 x (16 KiB A + 64 KiB B) = 160 KiB, so the A image drops its row padding
 // and XOR-swizzles its 16-B chunks instead: chunk' = chunk ^ ((row >> 1) & 7)
 // keeps a ds_read_b128 lane group (16 rows, 2 per 64-bank line) conflict-free.
-//
-// PRIO (cdna_hip_programming.md T5): 1 = s_setprio(1) around every MFMA
-// cluster (keeps hipcc from moving MFMAs across the barrier); 2 = the static
-// 2-waves-per-SIMD form, priority 1 for the younger half (threads >= 256).
-template <int TN, bool EXP, int WM = 1, int TM_ = 4 / WM, bool BT = false, int BJ_ = 16,
-          int PRIO = 0>
+template <int TN, bool EXP, int WM = 2, int TM_ = 4 / WM, int BJ_ = 16>
 struct NNTile {
   static constexpr int kThreads = 256 * WM;
   static constexpr int TM = TM_;
@@ -191,19 +238,16 @@ struct NNTile {
   static constexpr int BJ = BJ_;
   static constexpr bool kSwz = BJ == 32;
   static constexpr int LDA = kSwz ? BJ : BJ + 4;  // 16: 80-B rows (conflict-free b128)
-  static constexpr int LDBT = BJ + 4;
   static constexpr int SA = BM * LDA;
-  static constexpr int SB = BT ? BC * LDBT : BJ * BC;
+  static constexpr int SB = BJ * BC;
   static constexpr int kStage = SA + SB;
   static constexpr int kSmemFloats = 2 * kStage;
   static constexpr int LA = BM * BJ / 4 / kThreads;
   static constexpr int RPT = BM * 4 / kThreads > 1 ? BM * 4 / kThreads : 1;  // rows per thread
-  static constexpr int NB4 = BC * BJ / 16;  // 4x4 blocks of a BJ x BC tile (BT)
-  static constexpr int LB = BT ? 4 * ((NB4 + kThreads - 1) / kThreads) : BJ * BC / 4 / kThreads;
+  static constexpr int LB = BJ * BC / 4 / kThreads;
   static_assert(LA >= 1 && LB >= 1, "tile too small for the block");
   static_assert(BM == 64 || BM == 128, "BM must divide the 128-row panel");
   static_assert(BJ == 16 || BJ == 32, "BJ is 16 or 32");
-  static_assert(!(kSwz && BT), "BJ = 32 uses the row-major B image");
   static_assert(kSmemFloats * 4 <= 160 * 1024, "LDS budget");
 
   f32x16 acc[TM][TN];
@@ -244,26 +288,11 @@ struct NNTile {
           f32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, (p * kPanelElems + row * 16 + 4 * c4) * 4,
                                                        soA, 0));
     }
-    if (BT) {
 #pragma unroll
-      for (int u = 0; u < LB / 4; ++u) {
-        const int blk = t + u * kThreads;  // 4x4 block: rows 4*rg.., cols 4*cg..
-        if (NB4 % kThreads == 0 || blk < NB4) {
-          const int rg = blk / (BC / 4), cg = blk % (BC / 4);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            rb[4 * u + i] = __builtin_bit_cast(
-                f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                           rB, (int)(((4 * rg + i) * ldb + 4 * cg) * 4), soB, 0));
-        }
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < LB; ++u) {
-        const int f = t + u * kThreads, row = f / (BC / 4), c4 = f % (BC / 4);
-        rb[u] = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rB, (int)((row * ldb + 4 * c4) * 4), soB, 0));
-      }
+    for (int u = 0; u < LB; ++u) {
+      const int f = t + u * kThreads, row = f / (BC / 4), c4 = f % (BC / 4);
+      rb[u] = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rB, (int)((row * ldb + 4 * c4) * 4), soB, 0));
     }
   }
 
@@ -283,31 +312,24 @@ struct NNTile {
       a_map(t, u, p, row, c4);
       const int chunk = 4 * p + c4;
       if (EXP) {
-        // |dgl| < 2^31 for every launch the ABI accepts (rows, columns < 2^31)
-        const int qd = (int)dgl + row - 4 * chunk;
+        // Diagonal entry (row i, column c of this K-step) <=> c - i = dgl,
+        // so only K-steps with -BM < dgl < BJ hold one; the rest skip the test.
+        // (|dgl| < 2^31 for every launch the ABI accepts.)
+        if (dgl > -BM && dgl < BJ) {
+          const int qd = (int)dgl + row - 4 * chunk;
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          ra[u][q] = (qd == q) ? 0.f : __builtin_amdgcn_exp2f(ra[u][q] * scale);
+          for (int q = 0; q < 4; ++q)
+            ra[u][q] = (qd == q) ? 0.f : __builtin_amdgcn_exp2f(ra[u][q] * scale);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ra[u][q] = __builtin_amdgcn_exp2f(ra[u][q] * scale);
+        }
         rs[u % RPT] += (ra[u][0] + ra[u][1]) + (ra[u][2] + ra[u][3]);
       }
       *reinterpret_cast<f32x4*>(sA + a_off(row, chunk)) = ra[u];
     }
-    if (BT) {
 #pragma unroll
-      for (int u = 0; u < LB / 4; ++u) {
-        const int blk = t + u * kThreads;
-        if (NB4 % kThreads == 0 || blk < NB4) {
-          const int rg = blk / (BC / 4), cg = blk % (BC / 4);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            *reinterpret_cast<f32x4*>(sB + (4 * cg + i) * LDBT + 4 * rg) =
-                f32x4{rb[4 * u][i], rb[4 * u + 1][i], rb[4 * u + 2][i], rb[4 * u + 3][i]};
-        }
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < LB; ++u) *reinterpret_cast<f32x4*>(sB + 4 * (t + u * kThreads)) = rb[u];
-    }
+    for (int u = 0; u < LB; ++u) *reinterpret_cast<f32x4*>(sB + 4 * (t + u * kThreads)) = rb[u];
   }
 
   __device__ __forceinline__ void compute(const float* st, int wr, int wc) {
@@ -320,38 +342,21 @@ struct NNTile {
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi)
         a[mi] = *reinterpret_cast<const f32x4*>(sA + a_off(wr * 32 * TM + mi * 32 + r, 2 * g + h));
-      if (BT) {
-        f32x4 b4[TN];
+      // all of this group's B fragments are read before its MFMAs (one
+      // LDS wait per group instead of one per 4-MFMA cluster)
+      float b[4][TN];
 #pragma unroll
-        for (int ni = 0; ni < TN; ++ni)
-          b4[ni] = *reinterpret_cast<const f32x4*>(sB + (wc * 32 * TN + ni * 32 + r) * LDBT +
-                                                   8 * g + 4 * h);
+      for (int t4 = 0; t4 < 4; ++t4) {
+        const float* brow = sB + (8 * g + 4 * h + t4) * BC + wc * 32 * TN + r;
 #pragma unroll
-        for (int t4 = 0; t4 < 4; ++t4)
+        for (int ni = 0; ni < TN; ++ni) b[t4][ni] = brow[ni * 32];
+      }
 #pragma unroll
-          for (int mi = 0; mi < TM; ++mi)
+      for (int t4 = 0; t4 < 4; ++t4) {
 #pragma unroll
-            for (int ni = 0; ni < TN; ++ni)
-              acc[mi][ni] = mfma32(a[mi][t4], b4[ni][t4], acc[mi][ni]);
-      } else {
-        // all of this group's B fragments are read before its MFMAs (one
-        // LDS wait per group instead of one per 4-MFMA cluster)
-        float b[4][TN];
+        for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-        for (int t4 = 0; t4 < 4; ++t4) {
-          const float* brow = sB + (8 * g + 4 * h + t4) * BC + wc * 32 * TN + r;
-#pragma unroll
-          for (int ni = 0; ni < TN; ++ni) b[t4][ni] = brow[ni * 32];
-        }
-#pragma unroll
-        for (int t4 = 0; t4 < 4; ++t4) {
-          if (PRIO == 1) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-          for (int mi = 0; mi < TM; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = mfma32(a[mi][t4], b[t4][ni], acc[mi][ni]);
-          if (PRIO == 1) __builtin_amdgcn_s_setprio(0);
-        }
+          for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = mfma32(a[mi][t4], b[t4][ni], acc[mi][ni]);
       }
     }
   }
@@ -372,20 +377,27 @@ struct NNTile {
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[mi][ni][q] = 0.f;
     if (k0 >= k1) return;
-    if (PRIO == 2 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256)
-      __builtin_amdgcn_s_setprio(1);
     load(Apanels, B, ldb, k0);
     store(smem, scale, row_g0 - k0);
     __syncthreads();
-    int cur = 0;
-    for (int64_t j0 = k0; j0 < k1; j0 += BJ) {
-      const bool more = j0 + BJ < k1;
-      if (more) load(Apanels, B, ldb, j0 + BJ);
-      compute(smem + cur * kStage, wr, wc);
-      if (more) store(smem + (cur ^ 1) * kStage, scale, row_g0 - (j0 + BJ));
-      __syncthreads();
-      cur ^= 1;
+    // unrolled by two so both LDS stage bases are compile-time constants
+    // (immediate ds_read / ds_write offsets, no per-step address VALU)
+    for (int64_t j0 = k0; j0 < k1; j0 += 2 * BJ) {
+      step<0>(Apanels, B, ldb, j0, k1, scale, smem, row_g0, wr, wc);
+      if (j0 + BJ < k1) step<1>(Apanels, B, ldb, j0 + BJ, k1, scale, smem, row_g0, wr, wc);
     }
+  }
+
+  template <int CUR>
+  __device__ __forceinline__ void step(const float* __restrict__ Apanels,
+                                       const float* __restrict__ B, int64_t ldb, int64_t j0,
+                                       int64_t k1, float scale, float* smem, int64_t row_g0, int wr,
+                                       int wc) {
+    const bool more = j0 + BJ < k1;
+    if (more) load(Apanels, B, ldb, j0 + BJ);
+    compute(smem + CUR * kStage, wr, wc);
+    if (more) store(smem + (CUR ^ 1) * kStage, scale, row_g0 - (j0 + BJ));
+    __syncthreads();
   }
 
   // EXP: the full row sum of staged row a_map(t, u) (u < RPT) is the sum over

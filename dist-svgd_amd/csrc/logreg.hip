@@ -8,6 +8,7 @@
 // as Z = W Xd^T (NT MFMA engine, sigmoid epilogue -> G in panel layout) and
 // G Xd (NN MFMA engine); 4 n N p flop, MFMA-bound.
 #include <cmath>
+#include <cstdlib>
 
 #include "gemm_tiles.hpp"
 
@@ -73,18 +74,12 @@ __device__ __forceinline__ float sigmoidf_stable(float u) {
 // the other resident blocks' f32 MFMAs (they share the SIMD's issue), so it
 // is kept short: exp2 + rcp (~1 ulp each) and store addresses that are one
 // per-lane base plus compile-time offsets (as the distance epilogue).
-__global__ __launch_bounds__(256) void logreg_z_kernel(const float* __restrict__ W,
-                                                       const float* __restrict__ Xd, int64_t ldb,
-                                                       int pp, const float* __restrict__ tp,
-                                                       int64_t N, int64_t N_pad,
-                                                       float* __restrict__ G) {
-  __shared__ __attribute__((aligned(16))) float smem[ZTile::kSmemFloats];
-  const int64_t i0 = (int64_t)blockIdx.y * ZTile::BM, q0 = (int64_t)blockIdx.x * ZTile::BN;
-  ZTile tile;
-  tile.run(W + i0 * ldb, ldb, Xd + q0 * ldb, ldb, pp, smem);
+__device__ __forceinline__ void z_epilogue(ZTile& tile, int64_t bi, int64_t q0,
+                                           const float* __restrict__ tp, int64_t N_pad,
+                                           float* __restrict__ G) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
   const int h4 = 4 * (lane >> 5);
-  float* const Gt = G + ((int64_t)blockIdx.y * (N_pad >> 4) + (q0 >> 4)) * kPanelElems;
+  float* const Gt = G + (bi * (N_pad >> 4) + (q0 >> 4)) * kPanelElems;
 #pragma unroll
   for (int ni = 0; ni < 2; ++ni) {
     const int cl = wn * 64 + ni * 32 + (lane & 31);
@@ -100,6 +95,19 @@ __global__ __launch_bounds__(256) void logreg_z_kernel(const float* __restrict__
       }
     }
   }
+}
+
+// One (particle tile, data tile) per block.
+__global__ __launch_bounds__(256) void logreg_z_kernel(const float* __restrict__ W,
+                                                       const float* __restrict__ Xd, int64_t ldb,
+                                                       int pp, const float* __restrict__ tp,
+                                                       int64_t N, int64_t N_pad,
+                                                       float* __restrict__ G) {
+  __shared__ __attribute__((aligned(16))) float smem[ZTile::kSmemFloats];
+  const int64_t i0 = (int64_t)blockIdx.y * ZTile::BM, q0 = (int64_t)blockIdx.x * ZTile::BN;
+  ZTile tile;
+  tile.run(W + i0 * ldb, ldb, Xd + q0 * ldb, ldb, pp, smem);
+  z_epilogue(tile, blockIdx.y, q0, tp, N_pad, G);
 }
 
 // one wave per particle row

@@ -20,7 +20,7 @@ namespace dsvgd {
 // in order (deterministic, no atomics).
 // row0: interacting-set index of A's row 0 (EXP: the diagonal j == row0 + i
 // is skipped, see NNTile::store).
-template <int TN, bool EXP, int WM, int TM, bool BT, int BJ, int PRIO>
+template <int TN, bool EXP, int WM, int TM, int BJ>
 __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ A, int64_t a_npad,
                                                       const float* __restrict__ B, int64_t ldb,
                                                       int64_t K, int64_t kchunk,
@@ -28,7 +28,7 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
                                                       float* __restrict__ C, int64_t ldc,
                                                       float* __restrict__ rowsum, int64_t m,
                                                       int64_t row0) {
-  using Tile = NNTile<TN, EXP, WM, TM, BT, BJ, PRIO>;
+  using Tile = NNTile<TN, EXP, WM, TM, BJ>;
   __shared__ __attribute__((aligned(16))) float smem[Tile::kSmemFloats];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
@@ -219,44 +219,24 @@ __global__ __launch_bounds__(256) void phi_row_kernel(float* __restrict__ X, int
   }
 }
 
-// NN block shape (DSVGD_NN_SHAPE overrides, for in-process A/B runs):
-//   "w1"  128 rows, 4 waves x 256 AGPRs        (1 block/CU, 1 wave/SIMD)
-//   "w2"  128 rows, 8 waves x 128 accumulators (1 block/CU, 2 waves/SIMD)
-//   "b64"  64 rows, 4 waves x 128 accumulators (2 blocks/CU)
-//   "w2t"  as w2 with the transposed B image (b128 B-fragment reads)
-//   "w2k"  as w2 with 32-deep K-steps (160 KiB LDS, swizzled A image)
-//   "w1k"  as w1 with 32-deep K-steps
-//   "w2p"  as w2 with s_setprio(1) around each MFMA cluster
-//   "w2s"  as w2 with priority 1 for the younger half of the block
-enum NNShape { kW1, kW2, kB64, kW2T, kW2K, kW1K, kW2P, kW2S };
-static NNShape nn_shape() {
-  const char* e = getenv("DSVGD_NN_SHAPE");
-  if (!e) return kW2;
-  const std::string v(e);
-  if (v == "w1") return kW1;
-  if (v == "b64") return kB64;
-  if (v == "w2t") return kW2T;
-  if (v == "w2k") return kW2K;
-  if (v == "w1k") return kW1K;
-  if (v == "w2p") return kW2P;
-  if (v == "w2s") return kW2S;
-  return kW2;
-}
-
-template <int TN, int WM, int TM, bool BT = false, int BJ = 16, int PRIO = 0>
+// NN block shape: 128 rows x 128*TN columns, 8 waves (2 per SIMD, 128
+// accumulators each); K-steps of 32 columns (two D panels per barrier,
+// 160 KiB LDS, XOR-swizzled A image) when K allows, else 16.
+// DSVGD_NN_SHAPE=w2 forces the 16-deep K-step (A/B switch).
+template <int TN, int BJ>
 int launch_nn_shape(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
                     const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
                     int64_t cols, int64_t row0, hipStream_t s) {
-  constexpr int BM = 32 * TM * WM;
+  constexpr int WM = 2, TM = 2, BM = 32 * TM * WM;
   if (K % BJ != 0) return fail_arg("nn_kernel: K must be a multiple of the K-step");
   const int64_t kchunk = roundup((K + splits - 1) / splits, BJ);
   const dim3 grid(cols / (128 * TN), roundup(m, BM) / BM, splits);
   if (exp_)
-    hipLaunchKernelGGL((nn_kernel<TN, true, WM, TM, BT, BJ, PRIO>), grid, dim3(256 * WM), 0, s, A, K, B,
-                       ldb, K, kchunk, st, C, ldc, rowsum, m, row0);
+    hipLaunchKernelGGL((nn_kernel<TN, true, WM, TM, BJ>), grid, dim3(256 * WM), 0, s, A, K, B, ldb,
+                       K, kchunk, st, C, ldc, rowsum, m, row0);
   else
-    hipLaunchKernelGGL((nn_kernel<TN, false, WM, TM, BT, BJ, PRIO>), grid, dim3(256 * WM), 0, s, A, K, B,
-                       ldb, K, kchunk, st, C, ldc, rowsum, m, row0);
+    hipLaunchKernelGGL((nn_kernel<TN, false, WM, TM, BJ>), grid, dim3(256 * WM), 0, s, A, K, B, ldb,
+                       K, kchunk, st, C, ldc, rowsum, m, row0);
   return check_launch("nn_kernel");
 }
 
@@ -264,37 +244,12 @@ template <int TN>
 int launch_nn(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
               const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
               int64_t cols, int64_t row0, hipStream_t s) {
-  switch (nn_shape()) {
-    case kW1:
-      return launch_nn_shape<TN, 1, 4>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols,
-                                       row0, s);
-    case kB64:
-      return launch_nn_shape<TN, 1, 2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols,
-                                       row0, s);
-    case kW2K:
-      if (K % 32 == 0)
-        return launch_nn_shape<TN, 2, 2, false, 32>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum,
-                                                    m, cols, row0, s);
-      break;
-    case kW1K:
-      if (K % 32 == 0)
-        return launch_nn_shape<TN, 1, 4, false, 32>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum,
-                                                    m, cols, row0, s);
-      break;
-    case kW2P:
-      return launch_nn_shape<TN, 2, 2, false, 16, 1>(exp_, A, B, ldb, K, splits, st, C, ldc,
-                                                     rowsum, m, cols, row0, s);
-    case kW2S:
-      return launch_nn_shape<TN, 2, 2, false, 16, 2>(exp_, A, B, ldb, K, splits, st, C, ldc,
-                                                     rowsum, m, cols, row0, s);
-    case kW2T:
-      return launch_nn_shape<TN, 2, 2, true>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m,
-                                             cols, row0, s);
-    default:
-      break;
-  }
-  return launch_nn_shape<TN, 2, 2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0,
+  const char* e = getenv("DSVGD_NN_SHAPE");
+  const bool bj16 = e && std::string(e) == "w2";
+  if (!bj16 && K % 32 == 0)  // split-K chunks are rounded to the K-step
+    return launch_nn_shape<TN, 32>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0,
                                    s);
+  return launch_nn_shape<TN, 16>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s);
 }
 
 // C[splits x m x cols] = f(A) B with A in panel layout (m_pad x K), B row-major K x cols.

@@ -15,62 +15,6 @@ namespace dsvgd {
 
 using GramTile = NTTile<2, 2, 2, 2>;  // 128 x 128 block, 4 waves of 64 x 64
 
-// Upper-triangle tile pair (bi <= bj) of linear block id b over T x T tiles.
-__device__ __forceinline__ void tri_decode(int64_t b, int T, int& bi, int& bj) {
-  const double A = (double)T + 0.5;
-  int x = (int)(A - sqrt(A * A - 2.0 * (double)b));
-  auto off = [&](int r) { return (int64_t)r * T - (int64_t)r * (r - 1) / 2; };
-  while (x > 0 && off(x) > b) --x;
-  while (x + 1 < T && off(x + 1) <= b) ++x;
-  bi = x;
-  bj = x + (int)(b - off(x));
-}
-
-// XCD-aware, L2-grouped tile order.  Workgroups are dispatched round-robin
-// over the 8 XCDs (block b runs on XCD b % 8), each with its own 4 MiB L2.
-// xcd_linear gives XCD x a contiguous range of logical tiles, and logical
-// tiles run in groups of kGroup x kGroup tiles, so the rows an XCD re-reads
-// (kGroup A + kGroup B blocks of 128 rows x dp, 2 MiB at dp = 256) stay in
-// its L2 instead of re-streaming Y from MALL for every row panel.
-constexpr int kXcds = 8;
-constexpr int kGroup = 8;
-
-__device__ __forceinline__ int64_t xcd_linear(int64_t b, int64_t total) {
-  const int64_t q = total / kXcds, r = total % kXcds, x = b % kXcds;
-  return x * q + min(x, r) + b / kXcds;
-}
-
-// Tile (bi, bj) of block b in a grid of `total` = groups * kGroup^2 blocks
-// over Tm x Tn tiles; SYM: groups over the upper triangle, tiles bi <= bj.
-// Returns false for the padding blocks of diagonal / edge groups.
-__device__ __forceinline__ bool tile_at(int64_t L, int Tm, int Tn, bool sym, int& bi, int& bj);
-__device__ __forceinline__ bool tile_of(int64_t b, int64_t total, int Tm, int Tn, bool sym,
-                                        int& bi, int& bj) {
-  return tile_at(xcd_linear(b, total), Tm, Tn, sym, bi, bj);
-}
-
-// Logical tile L (after the XCD remap) -> (bi, bj); false for padding tiles.
-__device__ __forceinline__ bool tile_at(int64_t L, int Tm, int Tn, bool sym, int& bi, int& bj) {
-  const int64_t g = L / (kGroup * kGroup);
-  const int w = (int)(L % (kGroup * kGroup));
-  int gi, gj;
-  if (sym) {
-    tri_decode(g, (Tn + kGroup - 1) / kGroup, gi, gj);
-  } else {
-    const int ngn = (Tn + kGroup - 1) / kGroup;
-    gi = (int)(g / ngn);
-    gj = (int)(g % ngn);
-  }
-  bi = gi * kGroup + w / kGroup;
-  bj = gj * kGroup + w % kGroup;
-  return bi < Tm && bj < Tn && (!sym || bi <= bj);
-}
-
-__host__ __device__ inline int64_t tile_grid(int64_t Tm, int64_t Tn, bool sym) {
-  const int64_t ngm = (Tm + kGroup - 1) / kGroup, ngn = (Tn + kGroup - 1) / kGroup;
-  return (sym ? ngn * (ngn + 1) / 2 : ngm * ngn) * kGroup * kGroup;
-}
-
 // Epilogue of one 128 x 128 distance tile (bi, bj) from the Gram
 // accumulators: D = max(0, |y_i|^2 + |y_j|^2 - 2 y_i.y_j) (diagonal exactly 0,
 // pads +inf) into the panel layout, the mirror tile for SYM off-diagonal
@@ -292,8 +236,12 @@ __global__ __launch_bounds__(256, 2) void sqdist_persistent_kernel(
     WindowHist wh;
     SlotWriter sw;
     if (smode == kSelBracket) sw.begin(st, sl, slot);
-    sq_epilogue<SYM, smode, true>(tile, bi, bj, row0, m, n, n_pad, D, snorm[par], wh, shist, sw, sl,
-                                  slot, epi);
+    if (epi == 3) {  // timing only: no epilogue at all
+      tile.zero();
+    } else {
+      sq_epilogue<SYM, smode, true>(tile, bi, bj, row0, m, n, n_pad, D, snorm[par], wh, shist, sw,
+                                    sl, slot, epi);
+    }
     if (smode == kSelHist) wh.flush(shist);
     par ^= 1;
     L = Ln;
@@ -402,8 +350,9 @@ int launch_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0,
                        Y, ldy, row0, m, n, n_pad, (int)d, D, st, cand);
     return check_launch("sqdist_direct");
   }
-  // DSVGD_SQ_EPI=1|2: TIMING EXPERIMENTS ONLY (D left incomplete) -- skip the
-  // mirror stores (1) or every D store (2), to price the epilogue.
+  // DSVGD_SQ_EPI=1|2|3: TIMING EXPERIMENTS ONLY (D left incomplete) -- skip
+  // the mirror stores (1), every D store (2), or the whole epilogue (3,
+  // persistent kernel), to price the epilogue.
   const char* ep = getenv("DSVGD_SQ_EPI");
   const int epi = ep ? atoi(ep) : 0;
   // DSVGD_SQ_PERSIST=0: one tile per block (A/B switch against the persistent form)

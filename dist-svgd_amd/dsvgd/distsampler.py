@@ -18,7 +18,9 @@ three exchange modes keep the reference semantics:
 Device model: one process per GPU; the process group (nccl = RCCL) must be
 initialised before make_step when num_shards > 1.  A device `particles`
 tensor is updated in place (the reference mutates the caller's tensor, a7);
-a CPU tensor is copied to the GPU and mirrored back after every make_step.
+a CPU tensor (or a device tensor that is not row-major fp32, e.g. the
+reference's `torch.cat(...).t()` view) is staged through a contiguous device
+copy and mirrored back after every make_step.
 
 Extensions (keyword-only): order="sequential" (reference in-place
 Gauss-Seidel over the owned rows) | "jacobi" (MFMA fast path); device; group.
@@ -72,10 +74,14 @@ class DistSampler(object):
         self._particles_per_shard = int(particles.shape[0] / self._num_shards)
         self._num_particles = self._particles_per_shard * self._num_shards
         self._particles = particles[:self._num_particles]
-        if particles.is_cuda:
+        row_major = (self._particles.dtype == torch.float32 and self._particles.dim() == 2
+                     and self._particles.stride(1) == 1)
+        if particles.is_cuda and row_major:
             self._device = N.require_gpu(particles.device)
-            N.ld(self._particles)                 # row-major fp32 or ValueError
             self._work = self._particles          # updated in place
+        elif particles.is_cuda:                   # e.g. the reference's cat(...).t() view
+            self._device = N.require_gpu(particles.device)
+            self._work = self._particles.to(torch.float32).contiguous()
         else:
             self._device = N.require_gpu(device if device is not None else "cuda")
             self._work = torch.empty(self._particles.shape, dtype=torch.float32,

@@ -4,7 +4,7 @@
     python scripts/ab_kernels.py [--n 65536 --d 256 --rounds 5]
 
 Variants are switched through environment variables the launchers read on
-every call (DSVGD_NN_SHAPE=w1|w2|b64 for the NN MFMA engine).
+every call (DSVGD_NN_SHAPE=w2 forces the 16-deep NN K-step).
 """
 import argparse
 import json
@@ -46,8 +46,7 @@ def main():
     eng.distances(median=True)
     eng.median_bandwidth()
     variants = json.loads(os.environ.get("AB_VARIANTS", "null")) or {
-        "nn=w1": {"DSVGD_NN_SHAPE": "w1"}, "nn=w2": {"DSVGD_NN_SHAPE": "w2"},
-        "nn=b64": {"DSVGD_NN_SHAPE": "b64"}, "nn=w2t": {"DSVGD_NN_SHAPE": "w2t"}}
+        "nn=bj32": {}, "nn=bj16": {"DSVGD_NN_SHAPE": "w2"}}
     res = {k: [] for k in variants}
     ref = None
     keys = {k for env in variants.values() for k in env}
@@ -74,6 +73,12 @@ def main():
             lambda: (eng.distances(median=True), eng.median_bandwidth()))
         for key in v:
             os.environ.pop(key, None)
+    # logistic-regression scores at the bench shape (N = 16384 rows, p = d - 1)
+    xd = torch.randn(16384, d - 1, generator=g) / (d ** 0.5)
+    tl = torch.where(torch.randn(16384, generator=g) > 0, 1.0, -1.0)
+    tgt = dsvgd.targets.LogisticRegression(xd, tl)
+    Sx = torch.empty_like(X)
+    out["logreg_score_ms"] = timed(lambda: tgt.score(X, Sx))
     out["sqdist_bracket_ms"] = timed(lambda: eng.distances(median=True))
     out["sqdist_select_ms"] = timed(lambda: (eng.distances(median=True), eng.median_bandwidth()))
     print(json.dumps(out, indent=1))

@@ -49,6 +49,13 @@ def main():
                 out["%s_d%d_p%s" % (name, d, pv)] = {"ms": ms, "tflops": flops / ms / 1e9,
                                                      "bracket_ms": msb}
             os.environ.pop("DSVGD_SQ_PERSIST", None)
+            for ev in os.environ.get("PROBE_EPI", "").split(","):
+                if not ev:
+                    continue
+                os.environ["DSVGD_SQ_EPI"] = ev
+                ms = timed(lambda: eng.distances(median=False))
+                out["%s_d%d_epi%s" % (name, d, ev)] = {"ms": ms, "tflops": flops / ms / 1e9}
+            os.environ.pop("DSVGD_SQ_EPI", None)
             del eng
             torch.cuda.empty_cache()
     print(json.dumps(out, indent=1))
