@@ -128,7 +128,24 @@ __global__ __launch_bounds__(256) void phi_direct_kernel(
       xi[a][c] = (i < m && col < d) ? Y[(row0 + i) * ldy + col] : 0.f;
       acc[a][c] = 0.f;
     }
+  // the j sum runs in chains of kChain columns added into `tot` (one long
+  // fp32 chain over n ~ 16k terms costs ~5e-6 of max|phi|)
+  constexpr int64_t kChain = 4096;
+  float tot[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) tot[a][c] = 0.f;
   for (int64_t j0 = 0; j0 < n; j0 += 64) {
+    if (j0 % kChain == 0 && j0 > 0) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          tot[a][c] += acc[a][c];
+          acc[a][c] = 0.f;
+        }
+    }
     for (int e = t; e < 64 * 64; e += 256) {
       const int r = e >> 6, q = e & 63;  // kT[q][r]: row i0+r, column j0+q
       const int64_t i = i0 + r, j = j0 + q;
@@ -150,6 +167,10 @@ __global__ __launch_bounds__(256) void phi_direct_kernel(
     }
     __syncthreads();
   }
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[a][c] += tot[a][c];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll

@@ -1,10 +1,13 @@
 // sqdist.hip -- pairwise squared distances D_ij = ||x_i - x_j||^2 in the panel
 // layout, plus the per-entry accounting of the exact median select.
 //
-// d > 64: Gram form on MFMA (v_mfma_f32_32x32x2_f32) over centred particles,
+// d > 2: Gram form on MFMA (v_mfma_f32_32x32x2_f32) over centred particles,
 //   upper-triangle tiles only for a square block (mirror stored).  Roofline per
 //   128x128 tile: 2*128*128*dp flop vs 64 KiB written -> MFMA-bound for dp >= 64.
-// d <= 64: explicit differences on the VALU (torch.dist semantics).
+// d <= 2: explicit differences on the VALU (torch.dist semantics) -- at d = 1
+//   the Gram form's cancellation exceeds the 1e-5 phi tolerance and d = 2 is
+//   within 2x of it (measured, scripts/precision_small_d.py); from d = 3 up
+//   the MFMA path is as or more accurate than the pairwise one.
 #include <cmath>
 #include <cstdlib>
 
@@ -254,12 +257,13 @@ __global__ __launch_bounds__(256, 2) void sqdist_persistent_kernel(
   }
 }
 
-// d <= 64: D_ij = sum_c (y_ic - y_jc)^2 from explicit differences on the VALU
+// d <= 2 (supports up to 64): D_ij = sum_c (y_ic - y_jc)^2 from explicit differences on the VALU
 // (what torch.dist(x, y)**2 computes per pair at experiments/logreg.py:61):
 // no ||x||^2 - 2x.y cancellation, which at small d and a narrow median
 // bandwidth costs more than the 1e-5 phi tolerance.  128 x 128 tile per block,
 // 8 x 8 outputs per thread, both operand tiles transposed in LDS.
-constexpr int kDirectMaxD = 64;
+constexpr int kDirectMaxD = 64;     // the direct kernel's limit
+constexpr int kDirectDefaultD = 2;  // d <= this takes it by default
 
 template <int smode>
 __global__ __launch_bounds__(256) void sqdist_direct_kernel(const float* __restrict__ Y,
@@ -345,7 +349,11 @@ int launch_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0,
                   int64_t n, int64_t d, float* D, dsvgd_select_state* st, float* cand,
                   hipStream_t s) {
   const int64_t dp = roundup(d, 32), m_pad = roundup(m, 128), n_pad = roundup(n, 128);
-  if (d <= kDirectMaxD) {
+  // DSVGD_SQ_DIRECT_MAX_D: the largest d that takes the explicit-difference
+  // kernel (default kDirectDefaultD; precision experiments only)
+  const char* dm = getenv("DSVGD_SQ_DIRECT_MAX_D");
+  const int64_t direct_max = dm ? (int64_t)atoi(dm) : kDirectDefaultD;
+  if (d <= direct_max && d <= kDirectMaxD) {
     hipLaunchKernelGGL((sqdist_direct_kernel<SM>), dim3(n_pad / 128, m_pad / 128), dim3(256), 0, s,
                        Y, ldy, row0, m, n, n_pad, (int)d, D, st, cand);
     return check_launch("sqdist_direct");

@@ -37,14 +37,15 @@ import torch
 
 from . import _native as N
 from . import exchange
-from .engine import PhiEngine, SelectState, sequential_sweep, span
+from .engine import PhiEngine, SelectState, StepGraph, sequential_sweep, span
 from .kernels import resolve_kernel
-from .targets import resolve_target
+from .targets import BuiltinTarget, resolve_target
 from .w2 import W2Term
 
 
 class DistSampler(object):
     timer = None   # optional engine.StageTimer (bench instrumentation)
+    graphs = True  # S = 1, no W2, built-in target: replay each step as a HIP graph
 
     def __init__(self, rank, num_shards, logp, kernel, particles,
                  N_local, N_global,
@@ -100,6 +101,8 @@ class DistSampler(object):
         self._w2 = None
         self._side = None        # score all-reduce stream (Jacobi, S > 1)
         self._sbuf = None
+        self._graph = None
+        self._graph_key = None
 
     # ---------------------------------------------------- reference API --
     @property
@@ -170,23 +173,11 @@ class DistSampler(object):
         eng.timer = self.timer
         return eng
 
-    def make_step(self, step_size, h=1.0):
-        """Performs one step of SVGD (distsampler.py:172-205).
-
-        Params:
-            step_size - step size
-            h - discretization size for the JKO (W2) term
-        """
+    def _compute(self, step_size, h):
+        """Scores, bandwidth, W2 term and the particle update of one step
+        (distsampler.py:190-200), after the exchange."""
         S = self._num_shards
         jacobi = self._order == "jacobi"
-        if S > 1:
-            if self._exchange_particles:
-                with span(self.timer, "allgather_x"):
-                    self._exchange_all_particles()
-            else:
-                with span(self.timer, "ring_shift"):
-                    self._exchange_round_robin()
-
         s, e = self._particle_start_idx, self._particle_end_idx
         X = self._work
         if self._exchange_particles:
@@ -258,6 +249,37 @@ class DistSampler(object):
             sequential_sweep(Xi, Si, range(s - lo, e - lo), state, step_size, target=tgt,
                              score_scale=scale, extra=w2g)
 
+
+    def make_step(self, step_size, h=1.0):
+        """Performs one step of SVGD (distsampler.py:172-205).
+
+        Params:
+            step_size - step size
+            h - discretization size for the JKO (W2) term
+        """
+        S = self._num_shards
+        if S > 1:
+            if self._exchange_particles:
+                with span(self.timer, "allgather_x"):
+                    self._exchange_all_particles()
+            else:
+                with span(self.timer, "ring_shift"):
+                    self._exchange_round_robin()
+
+        # S = 1 without the W2 term is pure kernel launches: one HIP graph
+        # per step size, replayed (dsvgd.engine.StepGraph)
+        if (S == 1 and self.graphs and not self._include_wasserstein and self.timer is None
+                and isinstance(self._target, BuiltinTarget)):
+            key = float(step_size)
+            if self._graph is None or self._graph_key != key:
+                self._graph = StepGraph(lambda: self._compute(step_size, h), self._device)
+                self._graph_key = key
+            self._graph()
+        else:
+            self._compute(step_size, h)
+
+        s, e = self._particle_start_idx, self._particle_end_idx
+        X = self._work
         if self._include_wasserstein:
             src = X if self._exchange_particles else X[s:e]
             self._previous_particles = src.clone()

@@ -247,12 +247,16 @@ class PhiEngine(object):
     def fixed_bandwidth(self, h):
         N.call("dsvgd_set_bandwidth", self.state.ptr, float(h), N.stream(self.device))
 
-    DIRECT_MAX_D = 64
+    # d <= 2: explicit-difference distances and pairwise phi (the Gram /
+    # K.X form cancels past the 1e-5 tolerance at d = 1); d >= 3: MFMA (as
+    # or more accurate there, scripts/precision_small_d.py).  Must match the
+    # library's default (kDirectDefaultD in csrc/sqdist.hip).
+    DIRECT_MAX_D = 2
 
     def direction(self, X_own=None, step=0.0, write_phi=True, inv_n=None, extra=None):
         """phi for the owned rows (+ `extra`, e.g. the h * W2 gradient rows);
         optionally X_own += step * phi (in place).
-        d <= 64: pairwise VALU form (dsvgd_phi_direct); else K.[Xc|S] on MFMA."""
+        d <= DIRECT_MAX_D: pairwise VALU form (dsvgd_phi_direct); else K.[Xc|S] on MFMA."""
         s = N.stream(self.device)
         if X_own is not None:
             assert X_own.shape == (self.m, self.d)
@@ -295,6 +299,38 @@ class PhiEngine(object):
         mp, np_ = self.m_pad, self.n_pad
         Dd = self.D.view(mp // 128, np_ // 16, 128, 16).permute(0, 2, 1, 3).reshape(mp, np_)
         return Dd[:self.m, :self.n]
+
+
+class StepGraph(object):
+    """One SVGD iteration captured as a HIP graph and replayed.
+
+    Every libdsvgd_hip call only enqueues kernels on the current stream (no
+    allocation, no host synchronisation), so a whole iteration -- scores, the
+    median select, and for the reference's Gauss-Seidel order the n row
+    kernels plus n per-particle score refreshes -- is capturable.  The first
+    call runs eagerly (workspaces get allocated), the second captures
+    (torch.cuda.CUDAGraph = hipGraph on ROCm) and every call replays; at
+    small n the eager loop is launch-bound (two host launches per particle),
+    the replay is not.  `fn` must keep its device buffers fixed across calls.
+    """
+
+    def __init__(self, fn, device, enabled=True):
+        self.fn, self.device, self.enabled = fn, device, enabled
+        self.graph = None
+        self.calls = 0
+
+    def __call__(self):
+        self.calls += 1
+        if not self.enabled or self.calls == 1:
+            self.fn()
+            return
+        if self.graph is None:
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.device(self.device), torch.cuda.graph(g):
+                self.fn()
+            self.graph = g
+        self.graph.replay()
 
 
 def sequential_sweep(X, S, rows, h_state, step, target=None, score_scale=1.0, phi_out=None,

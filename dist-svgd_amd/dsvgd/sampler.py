@@ -12,7 +12,9 @@ Extensions (keyword-only, defaults keep the reference behaviour):
                       MFMA fast path (sq-distances, radix-select median, fused
                       exp, K.[X|S]) used for throughput;
   device              HIP device (default: current cuda device);
-  verbose             the reference's per-iteration prints.
+  verbose             the reference's per-iteration prints;
+  graphs              capture one iteration as a HIP graph and replay it
+                      (built-in targets; default on).
 The kernel must be RBF-shaped (see dsvgd.kernels); RBF("median") selects the
 median-heuristic bandwidth h = median(D)/log(n), recomputed every iteration.
 """
@@ -21,9 +23,9 @@ import torch
 from torch.distributions.normal import Normal
 
 from . import _native as N
-from .engine import PhiEngine, SelectState, sequential_sweep
+from .engine import PhiEngine, SelectState, StepGraph, sequential_sweep
 from .kernels import resolve_kernel
-from .targets import resolve_target
+from .targets import BuiltinTarget, resolve_target
 
 
 class Sampler(object):
@@ -41,7 +43,8 @@ class Sampler(object):
         self._target = resolve_target(logp)
         self._rbf = resolve_kernel(kernel, d)
 
-    def sample(self, n, num_iter, step_size, *, order="sequential", device=None, verbose=True):
+    def sample(self, n, num_iter, step_size, *, order="sequential", device=None, verbose=True,
+               graphs=True):
         """Generate samples using SVGD (sampler.py:42-74)."""
         if order not in ("sequential", "jacobi"):
             raise ValueError("order must be 'sequential' or 'jacobi'")
@@ -59,11 +62,10 @@ class Sampler(object):
         state = engine.state if engine is not None else SelectState(dev)
         if not median:
             N.call("dsvgd_set_bandwidth", state.ptr, float(self._rbf.h), N.stream(dev))
-        for l in range(num_iter):
-            if verbose:
-                print('Iteration {}'.format(l))
-            hist[l].copy_(X)
-            self._target.score(X, S)
+        target = self._target
+
+        def iteration():
+            target.score(X, S)
             if order == "jacobi":
                 engine.step(X, S, X_own=X, step=step_size, h=None if median else self._rbf.h,
                             write_phi=False)
@@ -72,7 +74,16 @@ class Sampler(object):
                     engine.pack(X)
                     engine.distances(median=True)
                     engine.median_bandwidth()
-                sequential_sweep(X, S, range(n), state, step_size, target=self._target)
+                sequential_sweep(X, S, range(n), state, step_size, target=target)
+
+        # built-in targets are pure kernel launches: capture the iteration
+        # once and replay it (user callables run eagerly)
+        step = StepGraph(iteration, dev, enabled=graphs and isinstance(target, BuiltinTarget))
+        for l in range(num_iter):
+            if verbose:
+                print('Iteration {}'.format(l))
+            hist[l].copy_(X)
+            step()
             if verbose:
                 print(X.mean(dim=0).cpu())
         hist[num_iter].copy_(X)

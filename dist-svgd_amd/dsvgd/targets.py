@@ -31,7 +31,11 @@ class Target(object):
         return self.logp(x)
 
 
-class Gaussian(Target):
+class BuiltinTarget(Target):
+    """Targets whose score is a libdsvgd_hip kernel sequence (graph-capturable)."""
+
+
+class Gaussian(BuiltinTarget):
     """N(mu, diag(1/lam)): log p = -1/2 sum_c lam_c (x_c - mu_c)^2 (+ const)."""
 
     def __init__(self, mu, lam):
@@ -56,7 +60,7 @@ class Gaussian(Target):
                float(scale), N.ptr(out), N.ld(out), N.stream(X.device))
 
 
-class GaussianMixture1D(Target):
+class GaussianMixture1D(BuiltinTarget):
     """log(1/3 N(x; -2, 1) + 1/3 N(x; 2, 1)) per coordinate (experiments/gmm.py:16-21;
     the code uses equal 1/3 weights although its comment says 1/3, 2/3)."""
 
@@ -71,7 +75,7 @@ class GaussianMixture1D(Target):
                N.ld(out), N.stream(X.device))
 
 
-class LogisticRegression(Target):
+class LogisticRegression(BuiltinTarget):
     """Bayesian logistic regression of experiments/logreg.py:45-58.
 
     x = [log alpha, w] (d = 1 + p); alpha ~ Gamma(1, 1) (no log-Jacobian, as in

@@ -108,8 +108,8 @@ int dsvgd_pack(const float* X, int64_t ldx, const float* S, int64_t lds, float s
 /* ---- pairwise squared distances ---------------------------------------- */
 /* D[i][j] = ||y_i - y_j||^2 for the owned row block i in [row0, row0+m) of Y
  * against all j < n, y = the first d columns of Y (centred particles).
- * d <= 64: explicit differences on the VALU (exact like the reference);
- * d > 64: max(0, |y_i|^2 + |y_j|^2 - 2 y_i.y_j) on v_mfma_f32_32x32x2_f32,
+ * d <= 2: explicit differences on the VALU (exact like the reference);
+ * d > 2: max(0, |y_i|^2 + |y_j|^2 - 2 y_i.y_j) on v_mfma_f32_32x32x2_f32,
  * upper-triangle tiles only when m == n and row0 == 0 (the transpose is
  * stored too).  D[i][i] = 0 exactly, pads = +inf, panel layout (ldd = n_pad).
  * select_mode (DSVGD_SEL_*): HIST accumulates radix digit 1 of the valid
@@ -183,7 +183,7 @@ int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t 
                      int64_t lde, float* phi, int64_t ldphi, float* X, int64_t ldx,
                      void* stream);
 
-/* d <= 64: phi (and the optional X update) straight from the pairwise form
+/* d <= 64 (used for d <= 2): phi (and the optional X update) straight from the pairwise form
  * phi_i = inv_n sum_j k_ij (s_j + (2/h)(x_i - x_j)) on the VALU -- the
  * reference's own per-pair expression (dsvgd/sampler.py:38-40), which avoids
  * the r x - K X cancellation of the GEMM form at small d.  Replaces

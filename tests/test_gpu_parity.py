@@ -190,6 +190,23 @@ def test_phi_matches_oracle(n, d, median):
     assert rel_err(phi, ref) < PHI_TOL
 
 
+@pytest.mark.parametrize("n,d", [(640, 64), (3000, 8)])
+def test_direct_kernels_up_to_d64(n, d, monkeypatch):
+    """The explicit-difference kernels (default for d <= 2) stay exact up to
+    their d = 64 limit (forced here through the engine / library switches)."""
+    monkeypatch.setenv("DSVGD_SQ_DIRECT_MAX_D", "64")
+    rs = np.random.RandomState(n + d)
+    X = rs.randn(n, d).astype(np.float32)
+    S = O.score_gmm(X).astype(np.float32)
+    eng = dsvgd().PhiEngine(n, d, device=DEV)
+    eng.DIRECT_MAX_D = 64
+    eng.step(gpu(X), gpu(S), h=None)
+    h = eng.state.read()[1]
+    D = eng.dense_D().cpu().numpy().astype(np.float64)
+    assert abs_err(D, O.sqdist(X, X)) <= 2e-6 * np.abs(O.sqdist(X, X)).max()
+    assert rel_err(eng.phi.cpu().numpy(), O.phi(X, S, h)) < PHI_TOL
+
+
 @pytest.mark.parametrize("n,d,m,row0", [(4096, 256, 1024, 1024), (16384, 96, 2048, 14336),
                                         (3000, 40, 1000, 1500)])
 def test_phi_row_block_split_k(n, d, m, row0):
