@@ -69,9 +69,18 @@ def run(name, steps):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps
     st = {k: float(np.mean(v)) for k, v in timer.summary().items()}
+    # the same steps as replays of the captured HIP graph (no per-stage events)
+    ds.timer = None
+    e0.record()
+    for _ in range(steps):
+        ds.make_step(1e-4)
+    e1.record()
+    torch.cuda.synchronize()
+    ms_graph = e0.elapsed_time(e1) / steps
     eng = next(iter(ds._engines.values()))
     m = n
     out = {"n": n, "d": d, "ms_per_step": ms, "particle_updates_per_s": n / ms * 1e3,
+           "graph_ms_per_step": ms_graph, "graph_particle_updates_per_s": n / ms_graph * 1e3,
            "stages_ms": st, "bracketed_select": bool(eng.bracketed)}
     rates = {}
     if "phi_mm" in st:
