@@ -198,6 +198,86 @@ static PredictWs predict_ws(int64_t n, int64_t Nt, int64_t p) {
   return w;
 }
 
+
+// Few particles (the reference's Gauss-Seidel order refreshes ONE particle's
+// score after each update): one block per particle, no workspace, one
+// launch.  p <= 32 (the reference's benchmark datasets): a thread per data
+// row computes g_q = t_q sigma(-t_q xd_q.w) and accumulates g_q xd_q into p
+// register partials, reduced over the block in a fixed order.  Larger p: g in
+// LDS (a wave per data row), then the columns.  s_0 = -a + p/2 - a/2 |w|^2.
+constexpr int kSmallMaxN = 8192;   // g in LDS (32 KiB) on the large-p form
+constexpr int64_t kSmallMaxRows = 32;
+constexpr int kSmallRegP = 32;
+
+__global__ __launch_bounds__(256) void logreg_small_kernel(const float* __restrict__ X, int64_t ldx,
+                                                           int64_t p, const float* __restrict__ Xd,
+                                                           int64_t ldxd,
+                                                           const float* __restrict__ t,
+                                                           int64_t N, float scale,
+                                                           float* __restrict__ S, int64_t lds) {
+  __shared__ float g[kSmallMaxN];
+  __shared__ float red[4][kSmallRegP + 1];
+  const int64_t j = blockIdx.x;
+  const float* x = X + j * ldx;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const float a = expf(x[0]);
+  float w2 = 0.f;
+  for (int64_t c = threadIdx.x; c < p; c += 256) w2 = fmaf(x[1 + c], x[1 + c], w2);
+  if (p <= kSmallRegP) {
+    float part[kSmallRegP];
+#pragma unroll
+    for (int c = 0; c < kSmallRegP; ++c) part[c] = 0.f;
+    for (int64_t q = threadIdx.x; q < N; q += 256) {
+      const float* xq = Xd + q * ldxd;
+      float z = 0.f;
+#pragma unroll
+      for (int c = 0; c < kSmallRegP; ++c)
+        if (c < p) z = fmaf(xq[c], x[1 + c], z);
+      const float tq = t[q];
+      const float gq = tq / (1.f + expf(tq * z));   // t sigma(-t z)
+#pragma unroll
+      for (int c = 0; c < kSmallRegP; ++c)
+        if (c < p) part[c] = fmaf(gq, xq[c], part[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < kSmallRegP; ++c) {
+      if (c >= p) break;
+      const float v = warp_sum(part[c]);
+      if (lane == 0) red[wv][c] = v;
+    }
+    w2 = warp_sum(w2);
+    if (lane == 0) red[wv][kSmallRegP] = w2;
+    __syncthreads();
+    for (int64_t c = threadIdx.x; c < p; c += 256)
+      S[j * lds + 1 + c] =
+          scale * (((red[0][c] + red[1][c]) + (red[2][c] + red[3][c])) - a * x[1 + c]);
+  } else {
+    for (int64_t q = wv; q < N; q += 4) {
+      const float* xq = Xd + q * ldxd;
+      float z = 0.f;
+      for (int64_t c = lane; c < p; c += 64) z = fmaf(xq[c], x[1 + c], z);
+      z = warp_sum(z);
+      if (lane == 0) {
+        const float tq = t[q];
+        g[q] = tq / (1.f + expf(tq * z));
+      }
+    }
+    w2 = warp_sum(w2);
+    if (lane == 0) red[wv][kSmallRegP] = w2;
+    __syncthreads();
+    for (int64_t c = threadIdx.x; c < p; c += 256) {
+      float acc = 0.f;
+      for (int64_t q = 0; q < N; ++q) acc = fmaf(g[q], Xd[q * ldxd + c], acc);
+      S[j * lds + 1 + c] = scale * (acc - a * x[1 + c]);
+    }
+  }
+  if (threadIdx.x == 0) {
+    const float ww = (red[0][kSmallRegP] + red[1][kSmallRegP]) +
+                     (red[2][kSmallRegP] + red[3][kSmallRegP]);
+    S[j * lds] = scale * (-a + 0.5f * (float)p - 0.5f * a * ww);
+  }
+}
+
 }  // namespace dsvgd
 
 using namespace dsvgd;
@@ -215,6 +295,11 @@ int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const 
   DSVGD_REQUIRE(n > 0 && d >= 2 && N > 0 && ldx >= d && lds >= d && ldxd >= d - 1, "sizes");
   DSVGD_REQUIRE(((uintptr_t)workspace & 255) == 0, "workspace must be 256-byte aligned");
   const int64_t p = d - 1;
+  if (n <= kSmallMaxRows && (p <= kSmallRegP || N <= kSmallMaxN)) {  // latency path
+    hipLaunchKernelGGL(logreg_small_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream,
+                       X, ldx, p, Xd, ldxd, t, N, scale, S, lds);
+    return check_launch("logreg_small");
+  }
   const LogregWs w = logreg_ws(n, N, p);
   DSVGD_REQUIRE(w.n_pad / 128 <= 65535, "too many row tiles");
   char* base = (char*)workspace;

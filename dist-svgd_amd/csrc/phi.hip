@@ -187,7 +187,12 @@ __global__ __launch_bounds__(256) void phi_direct_kernel(
 }
 
 // Gauss-Seidel row update (reference order, exact differences, no Gram):
-// one block; j in chunks of 256 (one per thread) -> k_j in LDS -> columns.
+// one block; j in chunks of 256 (one per thread) -> k_j in LDS; then the
+// (column, j) sums are split over the block: for a column block of dc <= 256
+// columns, G = 256/dc thread groups each take every G-th j, and the G
+// partials per column are added in group order (deterministic).  At the
+// reference's small d (1-3) that keeps the whole block busy instead of d
+// threads walking every j.
 __global__ __launch_bounds__(256) void phi_row_kernel(float* __restrict__ X, int64_t ldx,
                                                       const float* __restrict__ S, int64_t lds,
                                                       int64_t n, int64_t d, int64_t i,
@@ -199,8 +204,10 @@ __global__ __launch_bounds__(256) void phi_row_kernel(float* __restrict__ X, int
   float* xi = dyn;            // d
   float* acc = dyn + d;       // d
   float* kb = dyn + 2 * d;    // 256
+  float* red = kb + 256;      // 256
   const int t = threadIdx.x;
   const float inv_h = st->inv_h;
+  const float g2 = 2.f * inv_h;
   for (int64_t c = t; c < d; c += 256) {
     xi[c] = X[i * ldx + c];
     acc[c] = 0.f;
@@ -219,17 +226,28 @@ __global__ __launch_bounds__(256) void phi_row_kernel(float* __restrict__ X, int
     }
     kb[t] = k;
     __syncthreads();
-    const int64_t nj = min((int64_t)256, n - j0);
-    for (int64_t c = t; c < d; c += 256) {
-      float a = acc[c];
-      const float x = xi[c];
-      for (int64_t q = 0; q < nj; ++q) {
-        const int64_t jj = j0 + q;
-        a += kb[q] * S[jj * lds + c] + (2.f * inv_h) * kb[q] * (x - X[jj * ldx + c]);
+    const int nj = (int)min((int64_t)256, n - j0);
+    for (int64_t c0 = 0; c0 < d; c0 += 256) {
+      const int dc = (int)min((int64_t)256, d - c0);
+      const int G = 256 / dc;
+      float part = 0.f;
+      if (t < dc * G) {
+        const int64_t c = c0 + t % dc;
+        const float x = xi[c];
+        for (int q = t / dc; q < nj; q += G) {
+          const int64_t jj = j0 + q;
+          part = fmaf(kb[q], fmaf(g2, x - X[jj * ldx + c], S[jj * lds + c]), part);
+        }
       }
-      acc[c] = a;
+      red[t] = part;
+      __syncthreads();
+      if (t < dc) {
+        float a = acc[c0 + t];
+        for (int gi = 0; gi < G; ++gi) a += red[gi * dc + t];
+        acc[c0 + t] = a;
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
   const float inv_n = 1.f / (float)n;
   for (int64_t c = t; c < d; c += 256) {
@@ -372,8 +390,8 @@ int dsvgd_phi_row(float* X, int64_t ldx, const float* S, int64_t lds, int64_t n_
                   float* phi_out, void* stream) {
   DSVGD_REQUIRE(X && S && st, "null pointer");
   DSVGD_REQUIRE(n_int > 0 && d > 0 && i >= 0 && i < n_int && ldx >= d && lds >= d, "sizes");
-  DSVGD_REQUIRE(d <= 8064, "phi_row supports d <= 8064 (64 KiB LDS)");
-  const size_t shm = (size_t)(2 * d + 256) * sizeof(float);
+  DSVGD_REQUIRE(d <= 7936, "phi_row supports d <= 7936 (64 KiB LDS)");
+  const size_t shm = (size_t)(2 * d + 512) * sizeof(float);
   hipLaunchKernelGGL(phi_row_kernel, dim3(1), dim3(256), shm, (hipStream_t)stream, X, ldx, S, lds,
                      n_int, d, i, st, step, extra, phi_out);
   return check_launch("phi_row");

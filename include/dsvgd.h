@@ -239,9 +239,11 @@ int dsvgd_score_gmm(const float* X, int64_t ldx, int64_t n, int64_t d, float sca
                     int64_t lds, void* stream);
 /* Bayesian logistic regression (experiments/logreg.py:45-58), x = [log a, w]:
  *   s_0 = scale*(-a + p/2 - a/2 |w|^2),  s_w = scale*(-a w + Xd^T (t * sigma(-t * Xd w)))
- * as two MFMA GEMMs (Z = W Xd^T with the sigmoid epilogue, G Xd).
+ * as two MFMA GEMMs (Z = W Xd^T with the sigmoid epilogue, G Xd); for
+ * n <= 32 particles and N <= 8192 rows (the Gauss-Seidel order's
+ * one-particle refresh) a single one-block-per-particle launch instead.
  * Xd: N x p data rows (ldxd), t: N labels (+-1).  Workspace:
- * dsvgd_logreg_workspace_bytes(n, N, p). */
+ * dsvgd_logreg_workspace_bytes(n, N, p) (unused on the small path). */
 size_t dsvgd_logreg_workspace_bytes(int64_t n, int64_t N, int64_t p);
 int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const float* Xd,
                        int64_t ldxd, const float* t, int64_t N, float scale, float* S, int64_t lds,

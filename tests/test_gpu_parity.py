@@ -265,6 +265,25 @@ def test_scores_match_oracle():
     assert rel_err(out.cpu().numpy(), 0.5 * O.score_logreg(X, xd, t)) < 1e-5
 
 
+@pytest.mark.parametrize("n,N,p", [(1, 400, 2), (7, 777, 20), (32, 8192, 255), (33, 100, 5)])
+def test_logreg_scores_small_and_gemm_paths(n, N, p):
+    """Both logistic-regression score paths (one block per particle for
+    n <= 32, N <= 8192; the two-GEMM path otherwise) against the oracle,
+    including a single-row view of a bigger particle matrix (the
+    Gauss-Seidel refresh)."""
+    rs = np.random.RandomState(n + N)
+    X = (rs.randn(n + 3, p + 1) * 0.5).astype(np.float32)
+    xd = (rs.randn(N, p) / np.sqrt(p)).astype(np.float32)
+    t = np.where(rs.randn(N) > 0, 1.0, -1.0).astype(np.float32)
+    tgt = dsvgd().targets.LogisticRegression(xd, t)
+    Xg = gpu(X)
+    out = torch.zeros(n + 3, p + 1, device=DEV)
+    tgt.score(Xg[1:n + 1], out[1:n + 1], 3.0)
+    ref = 3.0 * O.score_logreg(X[1:n + 1], xd, t)
+    assert rel_err(out[1:n + 1].cpu().numpy(), ref) < 1e-5
+    assert float(out[0].abs().max()) == 0.0 and float(out[n + 1:].abs().max()) == 0.0
+
+
 def test_callable_target_matches_builtin():
     import dsvgd as m
     rs = np.random.RandomState(9)
