@@ -95,9 +95,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=65536)
-    ap.add_argument("--d", type=int, default=256)
-    ap.add_argument("--N", type=int, default=16384, help="global data rows")
+    # (no option that abbreviates torchrun's own: --n would clash with --nnodes)
+    ap.add_argument("--particles", type=int, default=65536)
+    ap.add_argument("--dim", type=int, default=256)
+    ap.add_argument("--data-rows", type=int, default=16384, help="global data rows")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -120,7 +121,7 @@ def main():
     import dsvgd
     from dsvgd.engine import StageTimer
 
-    n, d, Ng = args.n, args.d, args.N
+    n, d, Ng = args.particles, args.dim, args.data_rows
     p = d - 1
     per_data = Ng // world
     x, t = synthetic_data(Ng, p)

@@ -7,6 +7,7 @@
 // phi_mm: K [Xc | S] on the NN MFMA engine with the exp fused into the A
 // operand; D streams from HBM once (panel layout), [Xc|S] re-reads hit L2/MALL.
 // Roofline: 2 * 128 * BC flop per 8 KiB D panel -> MFMA-bound for d >= 64.
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <string>
@@ -110,7 +111,7 @@ __global__ __launch_bounds__(256) void phi_direct_kernel(
     int64_t row0, int64_t m, int64_t n, int d, int64_t dp,
     const dsvgd_select_state* __restrict__ st, float inv_n, float step,
     const float* __restrict__ extra, int64_t lde, float* __restrict__ phi, int64_t ldphi,
-    float* __restrict__ X, int64_t ldx) {
+    float* __restrict__ X, int64_t ldx, int64_t jchunk, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) float kT[64][64];
   __shared__ __attribute__((aligned(16))) float xs[64][64];
   __shared__ __attribute__((aligned(16))) float ss[64][64];
@@ -136,8 +137,10 @@ __global__ __launch_bounds__(256) void phi_direct_kernel(
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int c = 0; c < 4; ++c) tot[a][c] = 0.f;
-  for (int64_t j0 = 0; j0 < n; j0 += 64) {
-    if (j0 % kChain == 0 && j0 > 0) {
+  // blockIdx.y: split-J slice [jb, je) (part != null: write the raw sums)
+  const int64_t jb = (int64_t)blockIdx.y * jchunk, je = min(n, jb + jchunk);
+  for (int64_t j0 = jb; j0 < je; j0 += 64) {
+    if ((j0 - jb) % kChain == 0 && j0 > jb) {
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -149,13 +152,13 @@ __global__ __launch_bounds__(256) void phi_direct_kernel(
     for (int e = t; e < 64 * 64; e += 256) {
       const int r = e >> 6, q = e & 63;  // kT[q][r]: row i0+r, column j0+q
       const int64_t i = i0 + r, j = j0 + q;
-      kT[q][r] = (i < m && j < n) ? __builtin_amdgcn_exp2f(D[panel_off(i, j, n_pad)] * scale) : 0.f;
+      kT[q][r] = (i < m && j < je) ? __builtin_amdgcn_exp2f(D[panel_off(i, j, n_pad)] * scale) : 0.f;
       const int64_t jr = j0 + r;
-      xs[r][q] = (jr < n && q < d) ? Y[jr * ldy + q] : 0.f;
-      ss[r][q] = (jr < n && q < d) ? Y[jr * ldy + dp + q] : 0.f;
+      xs[r][q] = (jr < je && q < d) ? Y[jr * ldy + q] : 0.f;
+      ss[r][q] = (jr < je && q < d) ? Y[jr * ldy + dp + q] : 0.f;
     }
     __syncthreads();
-    const int jn = (int)min((int64_t)64, n - j0);
+    const int jn = (int)min((int64_t)64, je - j0);
     for (int q = 0; q < jn; ++q) {
       const f32x4 k4 = *reinterpret_cast<const f32x4*>(&kT[q][4 * rq]);
       const f32x4 x4 = *reinterpret_cast<const f32x4*>(&xs[q][4 * cq]);
@@ -178,12 +181,32 @@ __global__ __launch_bounds__(256) void phi_direct_kernel(
       const int64_t i = i0 + 4 * rq + a;
       const int col = 4 * cq + c;
       if (i < m && col < d) {
+        if (part) {
+          part[((int64_t)blockIdx.y * m + i) * d + col] = acc[a][c];
+          continue;
+        }
         float p = inv_n * acc[a][c];
         if (extra) p += extra[i * lde + col];
         if (phi) phi[i * ldphi + col] = p;
         if (X) X[i * ldx + col] += step * p;
       }
     }
+}
+
+// split-J partial sums of phi_direct_kernel, added in slice order
+__global__ __launch_bounds__(256) void phi_direct_finish_kernel(
+    const float* __restrict__ part, int nsplit, int64_t m, int64_t d, float inv_n, float step,
+    const float* __restrict__ extra, int64_t lde, float* __restrict__ phi, int64_t ldphi,
+    float* __restrict__ X, int64_t ldx) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= m * d) return;
+  const int64_t i = e / d, col = e % d;
+  float a = 0.f;
+  for (int z = 0; z < nsplit; ++z) a += part[(int64_t)z * m * d + e];
+  float p = inv_n * a;
+  if (extra) p += extra[i * lde + col];
+  if (phi) phi[i * ldphi + col] = p;
+  if (X) X[i * ldx + col] += step * p;
 }
 
 // Gauss-Seidel row update (reference order, exact differences, no Gram):
@@ -369,7 +392,8 @@ int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t 
 int dsvgd_phi_direct(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t row0,
                      int64_t m, int64_t n, int64_t d, const dsvgd_select_state* st, float inv_n,
                      float step, const float* extra, int64_t lde, float* phi, int64_t ldphi,
-                     float* X, int64_t ldx, void* stream) {
+                     float* X, int64_t ldx, float* partial, int64_t partial_floats,
+                     void* stream) {
   DSVGD_REQUIRE(D && Y && st, "null pointer");
   DSVGD_REQUIRE(!extra || lde >= d, "lde");
   DSVGD_REQUIRE(m > 0 && n > 0 && d > 0 && row0 >= 0, "sizes");
@@ -379,10 +403,28 @@ int dsvgd_phi_direct(const float* D, int64_t ldd, const float* Y, int64_t ldy, i
   DSVGD_REQUIRE(ldy >= 2 * dp, "ldy");
   DSVGD_REQUIRE(!phi || ldphi >= d, "ldphi");
   DSVGD_REQUIRE(!X || ldx >= d, "ldx");
-  hipLaunchKernelGGL(phi_direct_kernel, dim3((m + 63) / 64), dim3(256), 0, (hipStream_t)stream, D,
-                     n_pad, Y, ldy, row0, m, n, (int)d, dp, st, inv_n, step, extra, lde, phi, ldphi, X,
-                     ldx);
-  return check_launch("phi_direct");
+  DSVGD_REQUIRE(!partial || partial_floats >= 0, "partial_floats");
+  // split J over blockIdx.y until ~512 blocks (a few row blocks alone leave
+  // the chip idle at small n), as far as the partial buffer holds
+  const int64_t rb = (m + 63) / 64;
+  int64_t nsplit = 1;
+  if (partial) {
+    nsplit = std::min<int64_t>((512 + rb - 1) / rb, (n + 63) / 64);
+    nsplit = std::min<int64_t>(nsplit, partial_floats / (m * d));
+    nsplit = std::max<int64_t>(nsplit, 1);
+  }
+  const int64_t jchunk = roundup((n + nsplit - 1) / nsplit, 64);
+  nsplit = (n + jchunk - 1) / jchunk;
+  float* part = nsplit > 1 ? partial : nullptr;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(phi_direct_kernel, dim3((unsigned)rb, (unsigned)nsplit), dim3(256), 0, s, D,
+                     n_pad, Y, ldy, row0, m, n, (int)d, dp, st, inv_n, step, extra, lde, phi, ldphi,
+                     X, ldx, jchunk, part);
+  int rc = check_launch("phi_direct");
+  if (rc || !part) return rc;
+  hipLaunchKernelGGL(phi_direct_finish_kernel, dim3((unsigned)((m * d + 255) / 256)), dim3(256), 0,
+                     s, part, (int)nsplit, m, d, inv_n, step, extra, lde, phi, ldphi, X, ldx);
+  return check_launch("phi_direct_finish");
 }
 
 int dsvgd_phi_row(float* X, int64_t ldx, const float* S, int64_t lds, int64_t n_int, int64_t d,

@@ -42,7 +42,7 @@ SIGNATURES = {
     "dsvgd_phi_finish": (_int, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _f,
                                 _f, _p, _i64, _p, _i64, _p, _i64, _p]),
     "dsvgd_phi_direct": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _f, _f, _p,
-                                _i64, _p, _i64, _p, _i64, _p]),
+                                _i64, _p, _i64, _p, _i64, _p, _i64, _p]),
     "dsvgd_phi_row": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _f, _p, _p, _p]),
     "dsvgd_w2_cost": (_int, [_p, _i64, _i64, _p, _i64, _i64, _i64, _p, _i64, _p]),
     "dsvgd_w2_workspace_bytes": (_c.c_size_t, [_i64, _i64]),

@@ -269,9 +269,11 @@ class PhiEngine(object):
         ldx = N.ld(X_own) if X_own is not None else self.d
         if self.d <= self.DIRECT_MAX_D:
             with span(self.timer, "phi_direct"):
+                # KY (the MFMA path's split-K buffer) doubles as the split-J scratch
                 N.call("dsvgd_phi_direct", N.ptr(self.D), self.n_pad, N.ptr(self.Y), self.ldy,
                        self.row0, self.m, self.n, self.d, self.state.ptr, float(inv_n),
-                       float(step), ex, lde, phi, self.d, xo, ldx, s)
+                       float(step), ex, lde, phi, self.d, xo, ldx, N.ptr(self.KY),
+                       self.KY.numel(), s)
             return
         with span(self.timer, "phi_mm"):
             N.call("dsvgd_phi_mm", N.ptr(self.D), self.n_pad, N.ptr(self.Y), self.ldy, self.row0,

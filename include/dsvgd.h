@@ -187,11 +187,15 @@ int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t 
  * phi_i = inv_n sum_j k_ij (s_j + (2/h)(x_i - x_j)) on the VALU -- the
  * reference's own per-pair expression (dsvgd/sampler.py:38-40), which avoids
  * the r x - K X cancellation of the GEMM form at small d.  Replaces
- * dsvgd_phi_mm + dsvgd_phi_finish for small d (extra as in dsvgd_phi_finish). */
+ * dsvgd_phi_mm + dsvgd_phi_finish for small d (extra as in dsvgd_phi_finish).
+ * partial (nullable, partial_floats long): scratch for split-J partial sums
+ * (up to partial_floats / (m d) slices, summed in order by a second kernel),
+ * which keeps the chip busy when m is small. */
 int dsvgd_phi_direct(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t row0,
                      int64_t m, int64_t n, int64_t d, const dsvgd_select_state* st, float inv_n,
                      float step, const float* extra, int64_t lde, float* phi, int64_t ldphi,
-                     float* X, int64_t ldx, void* stream);
+                     float* X, int64_t ldx, float* partial, int64_t partial_floats,
+                     void* stream);
 
 /* Gauss-Seidel single-row update (reference order): for particle i, phi_i
  * from exact differences against the CURRENT X (rows < i already moved),
