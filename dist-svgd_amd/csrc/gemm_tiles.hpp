@@ -98,6 +98,7 @@ __host__ __device__ inline int64_t tile_grid(int64_t Tm, int64_t Tn, bool sym) {
 // behind the MFMAs) instead of one buffer with two barriers per K-step.
 template <int TM, int TN, int WM, int WN, bool DB = false>
 struct NTTile {
+  static constexpr int TM_ = TM, TN_ = TN, WM_ = WM, WN_ = WN;
   static constexpr int kThreads = 64 * WM * WN;
   static constexpr int BM = 32 * TM * WM;
   static constexpr int BN = 32 * TN * WN;

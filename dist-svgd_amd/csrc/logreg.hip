@@ -61,8 +61,6 @@ __global__ __launch_bounds__(256) void pad_copy_kernel(const float* __restrict__
   dst[t] = (r < rows && c < cols) ? src[r * lds + c0 + c] : 0.f;
 }
 
-using ZTile = NTTile<2, 2, 2, 2>;
-
 __device__ __forceinline__ float sigmoidf_stable(float u) {
   if (u >= 0.f) return 1.f / (1.f + expf(-u));
   const float e = expf(u);
@@ -74,20 +72,27 @@ __device__ __forceinline__ float sigmoidf_stable(float u) {
 // the other resident blocks' f32 MFMAs (they share the SIMD's issue), so it
 // is kept short: exp2 + rcp (~1 ulp each) and store addresses that are one
 // per-lane base plus compile-time offsets (as the distance epilogue).
-__device__ __forceinline__ void z_epilogue(ZTile& tile, int64_t bi, int64_t q0,
+// Tile: 128 x 128, 4 waves of 64 x 64 (measured: a 256 x 128 tile with
+// 128 accumulators per wave at 2 waves/SIMD is 6 % slower).
+using ZTile = NTTile<2, 2, 2, 2>;
+
+template <class T>
+__device__ __forceinline__ void z_epilogue(T& tile, int64_t i0, int64_t q0,
                                            const float* __restrict__ tp, int64_t N_pad,
                                            float* __restrict__ G) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
+  constexpr int WR = 32 * T::TM_, WC = 32 * T::TN_;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w / T::WN_, wn = w % T::WN_;
   const int h4 = 4 * (lane >> 5);
-  float* const Gt = G + (bi * (N_pad >> 4) + (q0 >> 4)) * kPanelElems;
 #pragma unroll
-  for (int ni = 0; ni < 2; ++ni) {
-    const int cl = wn * 64 + ni * 32 + (lane & 31);
-    const float tq = tp[q0 + cl];
+  for (int ni = 0; ni < T::TN_; ++ni) {
+    const int64_t q = q0 + wn * WC + ni * 32 + (lane & 31);
+    const float tq = tp[q];
     const float sc = tq * kLog2e;
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-      float* const g0 = Gt + (cl >> 4) * kPanelElems + (cl & 15) + (wm * 64 + mi * 32 + h4) * 16;
+    for (int mi = 0; mi < T::TM_; ++mi) {
+      const int64_t i = i0 + wm * WR + mi * 32 + h4;  // 32-row group: one 128-row panel
+      float* const g0 = G + ((i >> 7) * (N_pad >> 4) + (q >> 4)) * kPanelElems + (q & 15) +
+                        (i & 127) * 16;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float e = __builtin_amdgcn_exp2f(sc * tile.acc[mi][ni][r]);
@@ -107,7 +112,7 @@ __global__ __launch_bounds__(256) void logreg_z_kernel(const float* __restrict__
   const int64_t i0 = (int64_t)blockIdx.y * ZTile::BM, q0 = (int64_t)blockIdx.x * ZTile::BN;
   ZTile tile;
   tile.run(W + i0 * ldb, ldb, Xd + q0 * ldb, ldb, pp, smem);
-  z_epilogue(tile, blockIdx.y, q0, tp, N_pad, G);
+  z_epilogue(tile, i0, q0, tp, N_pad, G);
 }
 
 // one wave per particle row
@@ -130,6 +135,7 @@ __global__ __launch_bounds__(256) void logreg_finish_kernel(const float* __restr
 
 
 // ---- posterior-predictive test accuracy (experiments/logreg_plots.py:42-50) --
+using PTile = ZTile;
 // prob[q] = (1/n) sum_j sigma(xt_q . w_j) over the particles' weights w_j =
 // x_j[1:] (no bias, alpha unused, as the reference's _test_acc); the caller
 // thresholds prob > 0.5 against t_q > 0.  Z tiles on the NT engine; each
@@ -140,10 +146,10 @@ __global__ __launch_bounds__(256) void logreg_predict_kernel(const float* __rest
                                                              int64_t ldb, int pp, int64_t n,
                                                              int64_t Nt_pad,
                                                              float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float smem[ZTile::kSmemFloats];
+  __shared__ __attribute__((aligned(16))) float smem[PTile::kSmemFloats];
   __shared__ float scol[2][128];
-  const int64_t i0 = (int64_t)blockIdx.y * ZTile::BM, q0 = (int64_t)blockIdx.x * ZTile::BN;
-  ZTile tile;
+  const int64_t i0 = (int64_t)blockIdx.y * PTile::BM, q0 = (int64_t)blockIdx.x * PTile::BN;
+  PTile tile;
   tile.run(W + i0 * ldb, ldb, Xt + q0 * ldb, ldb, pp, smem);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
 #pragma unroll
@@ -321,8 +327,8 @@ int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const 
   hipLaunchKernelGGL(pad_copy_kernel, dim3((w.N_pad + 255) / 256), dim3(256), 0, s, t, 1, 0, N, 1,
                      w.N_pad, tp, 1);
   if ((rc = check_launch("pad_copy(t)"))) return rc;
-  hipLaunchKernelGGL(logreg_z_kernel, dim3(w.N_pad / 128, w.n_pad / 128), dim3(256), 0, s, Wp, Xdp,
-                     w.ldb, (int)w.pp, tp, N, w.N_pad, G);
+  hipLaunchKernelGGL(logreg_z_kernel, dim3(w.N_pad / ZTile::BN, w.n_pad / ZTile::BM), dim3(256), 0,
+                     s, Wp, Xdp, w.ldb, (int)w.pp, tp, N, w.N_pad, G);
   if ((rc = check_launch("logreg_z"))) return rc;
   if ((rc = nn_gemm(false, G, w.N_pad, Xdp, w.ldb, w.ldb, 1, nullptr, GW, w.ldb, nullptr, n, 0, s)))
     return rc;

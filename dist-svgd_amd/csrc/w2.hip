@@ -146,10 +146,20 @@ __global__ __launch_bounds__(256) void w2_cmax_kernel(const float* __restrict__ 
   if (bad) atomicExch(&ctl->done, 3);
 }
 
-__global__ void w2_start_kernel(W2Ctl* ctl, int64_t n) {
+// warm_phases > 0: the prices are the previous solve's (a nearby problem:
+// SVGD moves rows and columns by one step), so the auction starts only
+// warm_phases epsilon-scaling phases above eps_final instead of at cmax/theta.
+// Any initial prices give the same eps_final-optimality guarantee.
+__global__ void w2_start_kernel(W2Ctl* ctl, int64_t n, int warm_phases) {
   const double cmax = (double)ctl->cmax;
   ctl->eps_final = fmax(cmax * 0x1p-24 / (double)n, cmax * 1e-13);
-  ctl->eps = fmax(cmax / kTheta, ctl->eps_final);
+  double e0 = cmax / kTheta;
+  if (warm_phases > 0) {
+    double ew = ctl->eps_final;
+    for (int k = 0; k < warm_phases; ++k) ew *= kTheta;
+    e0 = fmin(e0, ew);
+  }
+  ctl->eps = fmax(e0, ctl->eps_final);
   ctl->epoch = 1;
   ctl->unassigned = (unsigned long long)n;
   ctl->rounds = 0;
@@ -379,7 +389,8 @@ int dsvgd_w2_cost(const float* X, int64_t ldx, int64_t m, const float* Y, int64_
 }
 
 int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
-                    int64_t max_rounds, int32_t* assign, int64_t* rounds_out, void* stream) {
+                    int64_t max_rounds, int warm_phases, int32_t* assign, int64_t* rounds_out,
+                    void* stream) {
   DSVGD_REQUIRE(C && ws && assign, "null pointer");
   DSVGD_REQUIRE(m > 0 && n > 0 && ldc >= n, "sizes");
   DSVGD_REQUIRE(n % m == 0, "n must be a multiple of m (n = R m slots)");
@@ -387,15 +398,24 @@ int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
   DSVGD_REQUIRE(m < kMaxRows, "m too large (2^21 rows)");
   DSVGD_REQUIRE(n / m <= kMaxR, "n / m must be <= 32 (slots per row)");
   DSVGD_REQUIRE(max_rounds > 0, "max_rounds");
+  DSVGD_REQUIRE(warm_phases >= 0, "warm_phases");
   hipStream_t s = (hipStream_t)stream;
   W2Ws w(ws, n);
   const int64_t R = n / m;
-  if (hipMemsetAsync(ws, 0, dsvgd_w2_workspace_bytes(m, n), s) != hipSuccess)
+  // warm start keeps the price array (the previous call's duals on this
+  // workspace); everything else restarts
+  const size_t prices = (size_t)n * sizeof(double);
+  const size_t total_b = dsvgd_w2_workspace_bytes(m, n);
+  if ((warm_phases == 0 && hipMemsetAsync(ws, 0, total_b, s) != hipSuccess) ||
+      (warm_phases > 0 &&
+       (hipMemsetAsync(ws, 0, kW2CtlBytes, s) != hipSuccess ||
+        hipMemsetAsync((char*)ws + kW2CtlBytes + prices, 0, total_b - kW2CtlBytes - prices, s) !=
+            hipSuccess)))
     return check_launch("w2 workspace memset");
   const int64_t total = m * n;
   const int cblocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
   hipLaunchKernelGGL(w2_cmax_kernel, dim3(cblocks), dim3(256), 0, s, C, ldc, m, n, w.ctl);
-  hipLaunchKernelGGL(w2_start_kernel, dim3(1), dim3(1), 0, s, w.ctl, n);
+  hipLaunchKernelGGL(w2_start_kernel, dim3(1), dim3(1), 0, s, w.ctl, n, warm_phases);
   int rc = check_launch("w2_start");
   if (rc) return rc;
   const dim3 gb((unsigned)std::min<int64_t>(kBidBlocks, (m + 3) / 4));

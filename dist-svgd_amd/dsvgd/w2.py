@@ -11,6 +11,7 @@ epilogue as `extra`, so the update is x_i += step * (phi_i + G_i) as at
 distsampler.py:196-200.
 """
 import ctypes
+import os
 
 import torch
 
@@ -22,8 +23,11 @@ class W2Term(object):
     slot assignment (n int32) and G (m x d)."""
 
     MAX_ROUNDS = 1 << 18
+    # epsilon phases above the final eps for a warm start from the previous
+    # step's prices (0 disables; the first call on a workspace is always cold)
+    WARM_PHASES = 2
 
-    def __init__(self, m, n, d, device):
+    def __init__(self, m, n, d, device, warm=True):
         if n % m:
             raise ValueError("W2 term needs n to be a multiple of m (n = R m)")
         self.m, self.n, self.d = m, n, d
@@ -34,6 +38,8 @@ class W2Term(object):
         self.assign = torch.empty(n, dtype=torch.int32, device=self.device)
         self.G = torch.empty((m, d), dtype=torch.float32, device=self.device)
         self.rounds = 0
+        self.warm = warm
+        self._solved = False
 
     def grad(self, X, Y, h):
         """G (m, d) = h * W2 gradient of the owned rows X (m, d) against the
@@ -43,9 +49,13 @@ class W2Term(object):
         N.call("dsvgd_w2_cost", N.ptr(X), N.ld(X), self.m, N.ptr(Y), N.ld(Y), self.n, self.d,
                N.ptr(self.C), self.n, s)
         rounds = ctypes.c_int64(0)
+        warm = self.WARM_PHASES if (self.warm and self._solved) else 0
+        if warm and os.environ.get("DSVGD_W2_WARM_PHASES"):     # experiments only
+            warm = max(0, int(os.environ["DSVGD_W2_WARM_PHASES"]))
         N.call("dsvgd_w2_assign", N.ptr(self.C), self.n, self.m, self.n, N.ptr(self.ws),
-               self.MAX_ROUNDS, N.ptr(self.assign), ctypes.addressof(rounds), s)
+               self.MAX_ROUNDS, warm, N.ptr(self.assign), ctypes.addressof(rounds), s)
         self.rounds = int(rounds.value)
+        self._solved = True
         N.call("dsvgd_w2_grad", N.ptr(X), N.ld(X), self.m, N.ptr(Y), N.ld(Y), self.n, self.d,
                N.ptr(self.assign), float(h), N.ptr(self.G), self.d, s)
         return self.G

@@ -224,9 +224,12 @@ size_t dsvgd_w2_workspace_bytes(int64_t m, int64_t n);
  * eps = max C * 2^-24 / n (within one fp32 ulp of max C of the optimum).
  * BLOCKS the calling thread (polls the device between batches of rounds);
  * fails with -3 after max_rounds.  rounds_out (host, nullable) gets the
- * number of bidding rounds. */
+ * number of bidding rounds.  warm_phases > 0: keep the prices left in `ws`
+ * by the previous call on a nearby problem (SVGD's next step) and start
+ * warm_phases epsilon phases above the final eps; 0: cold start. */
 int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
-                    int64_t max_rounds, int32_t* assign, int64_t* rounds_out, void* stream);
+                    int64_t max_rounds, int warm_phases, int32_t* assign, int64_t* rounds_out,
+                    void* stream);
 /* G[i] = h * sum_j P_ij (x_i - y_j) = h/n * sum_{slots s of i} (x_i - y_assign[s])
  * (distsampler.py:128 scaled by the JKO step h of :198); pass G as `extra`
  * to dsvgd_phi_finish / dsvgd_phi_direct / dsvgd_phi_row. */

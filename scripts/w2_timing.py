@@ -30,21 +30,57 @@ def case(m, n, d, kind, seed=0):
         P = torch.randn(n, d, generator=g)
         P[:m] = X - 1e-3 * torch.randn(m, d, generator=g)
     X, P = X.cuda(), P.cuda()
-    w = dsvgd.w2.W2Term(m, n, d, "cuda:0")
+    w = dsvgd.w2.W2Term(m, n, d, "cuda:0", warm=False)
     w.grad(X, P, 1.0)
     torch.cuda.synchronize()
     t = time.perf_counter()
     w.grad(X, P, 1.0)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t) * 1e3
-    return {"m": m, "n": n, "d": d, "kind": kind, "ms": round(ms, 3), "rounds": w.rounds,
-            "us_per_round": round(ms * 1e3 / max(w.rounds, 1), 2)}
+    out = {"m": m, "n": n, "d": d, "kind": kind, "ms": round(ms, 3), "rounds": w.rounds,
+           "us_per_round": round(ms * 1e3 / max(w.rounds, 1), 2)}
+    # the next SVGD step: rows and columns both moved by a small step; warm
+    # start from this solve's prices vs a cold solve of the same problem
+    cold_plan = None
+    g2 = torch.Generator(device="cpu").manual_seed(seed + 7)
+    X2 = X + 1e-3 * torch.randn(m, d, generator=g2).cuda()
+    P2 = P + 1e-3 * torch.randn(n, d, generator=g2).cuda()
+    for warm in (False, True):
+        ww = dsvgd.w2.W2Term(m, n, d, "cuda:0", warm=warm)
+        ww.grad(X, P, 1.0)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        G = ww.grad(X2, P2, 1.0).clone()
+        torch.cuda.synchronize()
+        key = "warm" if warm else "cold"
+        out[key + "_next_ms"] = round((time.perf_counter() - t) * 1e3, 3)
+        out[key + "_next_rounds"] = ww.rounds
+        cost = float(((X2[torch.arange(n, device="cuda") // (n // m)] - P2[ww.assign.long()]) ** 2)
+                     .sum())
+        out[key + "_next_cost"] = cost
+        if cold_plan is None:
+            cold_plan = G
+        else:
+            out["warm_vs_cold_grad_maxdiff"] = float((G - cold_plan).abs().max())
+    return out
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true")
+    ap.add_argument("--warm-sweep", action="store_true",
+                    help="warm-start phases 1..5 on two R > 1 shapes")
     args = ap.parse_args()
+    if args.warm_sweep:
+        for ph in (1, 2, 3, 4, 5):
+            os.environ["DSVGD_W2_WARM_PHASES"] = str(ph)
+            for sh in ((1024, 8192, 16, "svgd"), (2048, 16384, 256, "svgd")):
+                r = case(*sh)
+                print(json.dumps({"warm_phases": ph, "m": sh[0], "n": sh[1],
+                                  "warm_next_ms": r["warm_next_ms"],
+                                  "warm_next_rounds": r["warm_next_rounds"],
+                                  "cold_next_rounds": r["cold_next_rounds"]}), flush=True)
+        return
     shapes = [(256, 256, 16, "random"), (2048, 2048, 64, "random"), (500, 4000, 3, "random"),
               (1024, 8192, 16, "svgd"), (4096, 4096, 256, "svgd"), (2048, 16384, 256, "svgd"),
               (4096, 32768, 64, "svgd")]
