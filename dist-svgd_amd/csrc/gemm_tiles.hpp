@@ -213,7 +213,7 @@ struct NTTile {
 // 2 x (16 KiB A + 64 KiB B) = 160 KiB, so the A image drops its row padding
 // and XOR-swizzles its 16-B chunks instead: chunk' = chunk ^ ((row >> 1) & 7)
 // keeps a ds_read_b128 lane group (16 rows, 2 per 64-bank line) conflict-free.
-template <int TN, bool EXP, int WM = 2, int TM_ = 4 / WM, int BJ_ = 16>
+template <int TN, bool EXP, int WM = 2, int TM_ = 4 / WM, int BJ_ = 16, bool SWZB = true>
 struct NNTile {
   static constexpr int kThreads = 256 * WM;
   static constexpr int TM = TM_;
@@ -241,6 +241,13 @@ struct NNTile {
   // A image offset of (row, 16-B chunk)
   __device__ __forceinline__ static int a_off(int row, int chunk) {
     return row * LDA + 4 * (kSwz ? (chunk ^ ((row >> 1) & 7)) : chunk);
+  }
+  // B image column swizzle: the two half-waves of a fragment read (k rows 4
+  // apart, 4*BC floats = a multiple of 64 banks) would hit the same banks;
+  // flipping column bit 5 on rows with (k >> 2) odd moves the upper half-wave
+  // 32 banks over.  4-aligned column groups stay contiguous (b128 writes).
+  __device__ __forceinline__ static int b_swz(int k, int col) {
+    return SWZB ? (col ^ (((k >> 2) & 1) << 5)) : col;
   }
   // staged A vector u of thread t: panel p (16 columns each), row, chunk in panel
   __device__ __forceinline__ static void a_map(int t, int u, int& p, int& row, int& c4) {
@@ -313,7 +320,10 @@ struct NNTile {
       *reinterpret_cast<f32x4*>(sA + a_off(row, chunk)) = ra[u];
     }
 #pragma unroll
-    for (int u = 0; u < LB; ++u) *reinterpret_cast<f32x4*>(sB + 4 * (t + u * kThreads)) = rb[u];
+    for (int u = 0; u < LB; ++u) {
+      const int f = t + u * kThreads, row = f / (BC / 4), col = 4 * (f % (BC / 4));
+      *reinterpret_cast<f32x4*>(sB + row * BC + b_swz(row, col)) = rb[u];
+    }
   }
 
   __device__ __forceinline__ void compute(const float* st, int wr, int wc) {
@@ -331,9 +341,10 @@ struct NNTile {
       float b[4][TN];
 #pragma unroll
       for (int t4 = 0; t4 < 4; ++t4) {
-        const float* brow = sB + (8 * g + 4 * h + t4) * BC + wc * 32 * TN + r;
+        const int k = 8 * g + 4 * h + t4;
+        const float* brow = sB + k * BC;
 #pragma unroll
-        for (int ni = 0; ni < TN; ++ni) b[t4][ni] = brow[ni * 32];
+        for (int ni = 0; ni < TN; ++ni) b[t4][ni] = brow[b_swz(k, wc * 32 * TN + ni * 32 + r)];
       }
 #pragma unroll
       for (int t4 = 0; t4 < 4; ++t4) {

@@ -21,7 +21,7 @@ namespace dsvgd {
 // in order (deterministic, no atomics).
 // row0: interacting-set index of A's row 0 (EXP: the diagonal j == row0 + i
 // is skipped, see NNTile::store).
-template <int TN, bool EXP, int WM, int TM, int BJ>
+template <int TN, bool EXP, int WM, int TM, int BJ, bool SWZB = true>
 __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ A, int64_t a_npad,
                                                       const float* __restrict__ B, int64_t ldb,
                                                       int64_t K, int64_t kchunk,
@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
                                                       float* __restrict__ C, int64_t ldc,
                                                       float* __restrict__ rowsum, int64_t m,
                                                       int64_t row0) {
-  using Tile = NNTile<TN, EXP, WM, TM, BJ>;
+  using Tile = NNTile<TN, EXP, WM, TM, BJ, SWZB>;
   __shared__ __attribute__((aligned(16))) float smem[Tile::kSmemFloats];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
@@ -293,12 +293,24 @@ int launch_nn_shape(bool exp_, const float* A, const float* B, int64_t ldb, int6
   if (K % BJ != 0) return fail_arg("nn_kernel: K must be a multiple of the K-step");
   const int64_t kchunk = roundup((K + splits - 1) / splits, BJ);
   const dim3 grid(cols / (128 * TN), roundup(m, BM) / BM, splits);
-  if (exp_)
-    hipLaunchKernelGGL((nn_kernel<TN, true, WM, TM, BJ>), grid, dim3(256 * WM), 0, s, A, K, B, ldb,
-                       K, kchunk, st, C, ldc, rowsum, m, row0);
-  else
-    hipLaunchKernelGGL((nn_kernel<TN, false, WM, TM, BJ>), grid, dim3(256 * WM), 0, s, A, K, B, ldb,
-                       K, kchunk, st, C, ldc, rowsum, m, row0);
+  // DSVGD_NN_SWZB=0: unswizzled B image (A/B switch)
+  const char* sw = getenv("DSVGD_NN_SWZB");
+  const bool swz = !(sw && sw[0] == '0');
+#define DSVGD_NN_LAUNCH(E, SW)                                                               \
+  hipLaunchKernelGGL((nn_kernel<TN, E, WM, TM, BJ, SW>), grid, dim3(256 * WM), 0, s, A, K, B, \
+                     ldb, K, kchunk, st, C, ldc, rowsum, m, row0)
+  if (exp_) {
+    if (swz)
+      DSVGD_NN_LAUNCH(true, true);
+    else
+      DSVGD_NN_LAUNCH(true, false);
+  } else {
+    if (swz)
+      DSVGD_NN_LAUNCH(false, true);
+    else
+      DSVGD_NN_LAUNCH(false, false);
+  }
+#undef DSVGD_NN_LAUNCH
   return check_launch("nn_kernel");
 }
 
