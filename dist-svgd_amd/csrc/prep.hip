@@ -108,6 +108,11 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ X, 
   const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (j >= rows_pad) return;
   float* y = Y + j * ldy;
+  if (X == nullptr) {  // scores only: the S half of rows < n
+    if (j < n)
+      for (int64_t c = lane; c < d; c += 64) y[dp + c] = scale * S[j * lds + c];
+    return;
+  }
   float nrm = 0.f;
   if (j < n) {
     for (int64_t c = lane; c < ldy; c += 64) {
@@ -203,8 +208,8 @@ int dsvgd_colmean(const float* X, int64_t ldx, int64_t n, int64_t d, float* part
 int dsvgd_pack(const float* X, int64_t ldx, const float* S, int64_t lds, float score_scale,
                const float* mean, int64_t n, int64_t d, int64_t rows_pad, float* Y, int64_t ldy,
                float* norms, void* stream) {
-  DSVGD_REQUIRE(X && mean && Y && norms, "null pointer");
-  DSVGD_REQUIRE(n > 0 && d > 0 && ldx >= d && rows_pad >= n, "sizes");
+  DSVGD_REQUIRE(Y && (X ? (mean && norms) : (S != nullptr)), "null pointer");
+  DSVGD_REQUIRE(n > 0 && d > 0 && (!X || ldx >= d) && rows_pad >= n, "sizes");
   const int64_t dp = dsvgd_dp(d);
   DSVGD_REQUIRE(ldy >= 2 * dp, "ldy < 2*dp");
   DSVGD_REQUIRE(S == nullptr || lds >= d, "lds");

@@ -230,7 +230,7 @@ class DistSampler(object):
                 eng.fixed_bandwidth(self._rbf.h)
             if side is not main:
                 main.wait_stream(side)
-            eng.pack(Xi, Si)                       # Si already carries the score scale
+            eng.pack_scores(Si)                    # Si already carries the score scale
             eng.direction(X[s:e], step_size, write_phi=False, extra=w2g)
         else:
             if median:

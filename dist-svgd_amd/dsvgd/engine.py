@@ -185,6 +185,14 @@ class PhiEngine(object):
         with span(self.timer, "pack"):
             self._pack(X, S, score_scale, s)
 
+    def pack_scores(self, S, score_scale=1.0):
+        """Write only the S half of Y (the X half from an earlier pack(X))."""
+        assert S.shape == (self.n, self.d)
+        s = N.stream(self.device)
+        with span(self.timer, "pack"):
+            N.call("dsvgd_pack", None, self.d, N.ptr(S), N.ld(S), float(score_scale), None,
+                   self.n, self.d, self.Y.shape[0], N.ptr(self.Y), self.ldy, None, s)
+
     def _pack(self, X, S, score_scale, s):
         N.call("dsvgd_colmean", N.ptr(X), N.ld(X), self.n, self.d, N.ptr(self.mean_ws),
                N.ptr(self.mean), s)

@@ -100,7 +100,8 @@ int dsvgd_colmean(const float* X, int64_t ldx, int64_t n, int64_t d, float* part
 /* Y[j] = [X[j]-mean | score_scale*S[j]] zero padded to (rows_pad x ldy);
  * norms[j] = ||X[j]-mean||^2.  Replaces the per-pair operand gathering of
  * dsvgd/sampler.py:37-39 and dsvgd/distsampler.py:90-99.  S may be NULL
- * (S half left zero). */
+ * (S half left zero); X may be NULL (then only the S half of rows < n is
+ * written: the scores arriving after the distance stage, mean/norms unused). */
 int dsvgd_pack(const float* X, int64_t ldx, const float* S, int64_t lds, float score_scale,
                const float* mean, int64_t n, int64_t d, int64_t rows_pad, float* Y, int64_t ldy,
                float* norms, void* stream);
