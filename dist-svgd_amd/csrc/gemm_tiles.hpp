@@ -125,6 +125,7 @@ struct NTTile {
   // Buffer loads: one per-lane byte offset (row t/8, chunk t%8) and scalar
   // offsets for the u-th 32-row group and the K-step, so the staging needs
   // no per-load 64-bit address registers (the row-block bases are uniform).
+  // Offsets are 32-bit: a block touches BM (BN) rows x K columns only.
   __device__ __forceinline__ void load(const float* __restrict__ A, int64_t lda,
                                        const float* __restrict__ B, int64_t ldb, int k0) {
     const int t = threadIdx.x;

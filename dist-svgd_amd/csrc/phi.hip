@@ -335,6 +335,11 @@ int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, i
   // without the fused exp / row sums, to price the VALU work between MFMAs.
   const char* noexp = getenv("DSVGD_NN_NOEXP");
   if (noexp && noexp[0] == '1') exp_ = false;
+  // buffer-resource loads: 32-bit byte offsets from a block's A row panel
+  // (K columns x 128 rows) and from B's first row (K rows x ldb)
+  if (K * ldb * (int64_t)sizeof(float) >= ((int64_t)1 << 31) ||
+      K * 128 * (int64_t)sizeof(float) >= ((int64_t)1 << 31))
+    return fail_arg("nn_kernel: K x ldb too large for 32-bit buffer offsets (split the columns)");
   if (cols % 512 == 0)
     return launch_nn<4>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s);
   if (cols % 256 == 0)
