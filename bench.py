@@ -14,7 +14,9 @@ One step = exchange + scores + median (exact radix select over n^2 distances)
 Prints ONE JSON line (rank 0).  value = n*K / max-over-ranks wall time of the K
 timed steps (whole job).  roofline: the dominant kernel (phi_mm, the fused
 exp + K.[Xc|S] MFMA GEMM) -- algorithmic 4*m*n*d flop per launch / its mean
-HIP-event duration, against the 157.3 TF fp32 MFMA peak.  cpu_baseline: the
+HIP-event duration, against the ceiling of the engine it runs on: the
+fp32-accurate bf16-split engine (2516 TF bf16 dense / 6 products = 419 TF of
+fp32 products), or the 157.3 TF fp32 MFMA peak with DSVGD_PHI_GEMM=f32.  cpu_baseline: the
 reference algorithm's per-pair autograd loop (oracle/loop_baseline.py, a port)
 timed on this host on a bounded sample, rank 0 at N=1 only.
 """
@@ -34,6 +36,12 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, spec
+# phi_mm runs on v_mfma_f32_32x32x16_bf16 (1024 flop/clk/SIMD x 1024 SIMDs x
+# 2.4 GHz = 2516 TF dense) with six split products per fp32 product
+# (csrc/gemm_x3.hpp): the fp32-equivalent ceiling of that engine
+PEAK_BF16_MFMA_TFLOPS = 2516.6
+X3_PRODUCTS = 6
+PEAK_X3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / X3_PRODUCTS
 PEAK_HBM_GBS = 8000.0
 
 
@@ -163,8 +171,11 @@ def main():
 
     m = n // world
     phi_ms = stages["phi_mm"]
+    x3 = bool(sampler._engines[next(iter(sampler._engines))].x3)
+    peak = PEAK_X3_TFLOPS if x3 else PEAK_FP32_MFMA_TFLOPS
     # the committed PMC summary is an N=1 profile: only quoted for the N=1 run
-    traffic, traffic_src = pmc_traffic("void dsvgd::nn_kernel<4, true") if world == 1 else (None, None)
+    kname = "void dsvgd::nn_x3_kernel<4" if x3 else "void dsvgd::nn_kernel<4, true"
+    traffic, traffic_src = pmc_traffic(kname) if world == 1 else (None, None)
     flops = 4.0 * m * n * d
     achieved = flops / (phi_ms * 1e-3) / 1e12
     out = {
@@ -184,14 +195,21 @@ def main():
         "config": {"workload": "dist-logreg DistSampler all_scores, Jacobi, median bandwidth",
                    "n": n, "d": d, "N_global": Ng, "parallelism": "dp%d" % world,
                    "particles_per_gpu": m},
-        "roofline": {"bound": "mfma", "kernel": "phi_mm (nn_kernel<4,true>)",
-                     "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
+        "roofline": {"bound": "mfma",
+                     "kernel": ("phi_mm (nn_x3_kernel<4>: fp32-accurate 3-way bf16 split, "
+                                "6 bf16 MFMA products per fp32 product)") if x3 else
+                               "phi_mm (nn_kernel<4,true>: f32 MFMA)",
+                     "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                     "peak_basis": ("bf16 dense MFMA %.1f TF / %d split products" %
+                                    (PEAK_BF16_MFMA_TFLOPS, X3_PRODUCTS)) if x3 else
+                                   "f32 MFMA (v_mfma_f32_32x32x2_f32)",
+                     "frac": achieved / peak, "frac_of_f32_mfma_peak": achieved / PEAK_FP32_MFMA_TFLOPS,
+                     "traffic": traffic,
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                      "algorithmic_bytes": 4.0 * m * n + 4.0 * (n + 128) * 512,
                      "flop_per_launch": flops, "avg_launch_ms": phi_ms},
         "stages_ms": stages,
-        "step_6n2d_mfma_frac": (6.0 * m * n * d) / (el / args.steps) / 1e12 / PEAK_FP32_MFMA_TFLOPS,
+        "step_6n2d_f32_mfma_frac": (6.0 * m * n * d) / (el / args.steps) / 1e12 / PEAK_FP32_MFMA_TFLOPS,
         "phi_splits": int(sampler._engines[next(iter(sampler._engines))].splits),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

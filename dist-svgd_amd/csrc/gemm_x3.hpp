@@ -1,0 +1,334 @@
+// gemm_x3.hpp -- the NN engine (C = exp-fused K . Y, gemm_tiles.hpp) on the
+// bf16 MFMA (v_mfma_f32_32x32x16_bf16) with fp32 accuracy: both operands are
+// split three ways into bf16,
+//     v = v0 + v1 + v2 (+ a remainder of about 2^-26 |v|),  v0 = bf16(v),
+//     v1 = bf16(v - v0), v2 = bf16(v - v0 - v1),
+// and the six products with i + j <= 2 are accumulated in fp32 (a_i b_j is
+// exact in fp32: 8 x 8 significant bits).  The dropped terms (a1 b2, a2 b1,
+// a2 b2) are ~2^-26 of |a b| -- below fp32's own rounding of the product sum
+// -- so the result carries fp32 GEMM error, not bf16 error (scripts/
+// precision_x3.py compares it entry by entry with the exact-fp32 engine).
+// Six bf16 MFMAs do the work of eight f32 ones at 1/16 of the cost each:
+// 2.67x the f32 MFMA rate (MI355X_MICROARCH.md: 32x32x16 bf16 = 32 cycles,
+// 32x32x2 f32 = 64 cycles for 1/8 of the k-depth).
+//
+// Operand images (one 16-column K-step; LDS and HBM use the same byte image):
+//   * A (K = exp(-D/h), staged from D by the block): part p, row i: 32 B =
+//     16 bf16 (k = 0..15), the two 16-B halves swapped on rows with bit 3 set
+//     -- a fragment read (lane (r, h) reads row r, half h) then touches every
+//     bank once per 16-lane group (MI355X_MICROARCH.md ds_read_b128 groups).
+//   * B (Y = [Xc | S]): pre-split once per step by dsvgd_ysplit into
+//     Yx[kstep][part][column][16 k] with the same half swizzle on column bit 3,
+//     so a block's 3 x BC x 32 B of one K-step is contiguous per part and
+//     lands in LDS by a lane-linear copy.
+#pragma once
+#include "gemm_tiles.hpp"
+
+namespace dsvgd {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// 32x32x16 bf16 MFMA: lane (r = l&31, h = l>>5) holds A[r][8h + e] and
+// B[8h + e][r] in element e; C/D layout identical to the f32 32x32x2 form.
+__device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// v = s[0] + s[1] + s[2] to ~2^-26 |v| (|v| below bf16's overflow threshold)
+struct Split3 {
+  __bf16 s0, s1, s2;
+};
+__device__ __forceinline__ Split3 split3(float v) {
+  Split3 o;
+  o.s0 = (__bf16)v;
+  float r = v - (float)o.s0;
+  o.s1 = (__bf16)r;
+  r -= (float)o.s1;
+  o.s2 = (__bf16)r;
+  return o;
+}
+
+constexpr int kX3Parts = 3;
+constexpr int kX3Step = 16;  // K-step (columns of D / rows of Y)
+
+// byte offset of (row or column x, 16-B half h) inside a part image
+__device__ __forceinline__ int x3_off(int x, int h) { return x * 32 + ((h ^ ((x >> 3) & 1)) << 4); }
+
+// C[128 x BC] = f(A)[128 x K] . B[K x BC], f = exp2(scale * a) with the
+// diagonal skipped (EXP path of NNTile, same row-sum bookkeeping), 8 waves as
+// 2 (rows) x 4 (columns), each 64 x 32*TN, double-buffered LDS, 16-deep
+// K-steps (48 MFMAs per wave at TN = 4).
+//
+// Pipeline (one register set, cdna_hip_programming.md "Pipelining across
+// barriers"): iteration k computes from LDS stage k&1; halfway through its
+// MFMAs it writes tile k+1 (loaded one iteration earlier) into stage
+// (k+1)&1, then issues the loads of tile k+2, so a load has a whole
+// iteration to land.  The barrier closing an iteration is a raw s_barrier
+// after lgkmcnt(0): __syncthreads() would also wait vmcnt(0) and drain the
+// tile k+2 loads every K-step.
+//
+// DMA: both operands reach LDS by LDS-DMA (the B image is lane-linear; D
+// lands raw in a 2-slot ring and is staged from there), issued at the start
+// of iteration k for B of tile k+1 and D of tile k+2; counted vmcnt waits.
+template <int TN, bool DMA = true>
+struct NNX3Tile {
+  // (DMA needs the same DMA count in every wave: whole 512-chunk rounds)
+  static constexpr int kThreads = 512;
+  static constexpr int TM = 2;
+  static constexpr int BM = 128;
+  static constexpr int BC = 128 * TN;
+  static constexpr int BJ = kX3Step;
+  static constexpr int SA = kX3Parts * BM * 32;  // bytes of one stage's A image
+  static constexpr int SB = kX3Parts * BC * 32;
+  static constexpr int kStage = SA + SB;
+  static constexpr int kSmemBytes = 2 * kStage + (DMA ? 2 * kPanelElems * 4 : 0);
+  static constexpr int kBChunks = SB / 16;
+  static constexpr int LB = (kBChunks + kThreads - 1) / kThreads;
+  static constexpr int kHalf = TN > 1 ? TN / 2 : 1;  // column tiles before the mid-step write
+  static_assert(kSmemBytes <= 160 * 1024, "LDS budget");
+  static_assert(!DMA || kBChunks % kThreads == 0, "DMA: every wave issues LB DMAs");
+
+  f32x16 acc[TM][TN];
+  f32x4 ra;      // the D values being staged
+  u32x4 rb[DMA ? 1 : LB];
+  float rs;
+  bf16x8 a[TM][kX3Parts];
+
+  // A: thread t stages row t >> 2, columns 4 (t & 3) .. +3 of the D panel.
+  // B: 16-B chunk f = t + 512 u of the block's K-step image (part f / (2 BC)).
+  __device__ __forceinline__ void load(const float* __restrict__ Apanels, const __bf16* __restrict__ Yx,
+                                       int64_t ldy, int64_t j0) {
+    const int t = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rA =
+        __builtin_amdgcn_make_buffer_rsrc((void*)Apanels, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB =
+        __builtin_amdgcn_make_buffer_rsrc((void*)Yx, (short)0, 0x7fffffff, 0x00020000);
+    const int soA = (int)((j0 >> 4) * kPanelElems * 4);
+    const int soB = (int)((j0 >> 4) * kX3Parts * ldy * 32);
+    ra = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, t * 16, soA, 0));
+#pragma unroll
+    for (int u = 0; u < LB; ++u) {
+      const int f = t + u * kThreads;
+      if (kBChunks % kThreads == 0 || f < kBChunks) {
+        const int p = f / (2 * BC), rem = f % (2 * BC);
+        rb[u] = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rB, (int)(p * ldy * 32 + rem * 16), soB, 0));
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(char* st, float scale, int64_t dgl) {
+    store_a(st, scale, dgl);
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < LB; ++u) {
+      const int f = t + u * kThreads;
+      if (kBChunks % kThreads == 0 || f < kBChunks)
+        *reinterpret_cast<u32x4*>(st + SA + f * 16) = rb[u];
+    }
+  }
+
+  // exp / diagonal / row sum / 3-way split of this thread's 4 D values (ra)
+  __device__ __forceinline__ void store_a(char* st, float scale, int64_t dgl) {
+    const int t = threadIdx.x, row = t >> 2, c4 = t & 3;
+    if (dgl > -BM && dgl < BJ) {  // the K-step holds diagonal entries (NNTile::store)
+      const int qd = (int)dgl + row - 4 * c4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ra[q] = (qd == q) ? 0.f : __builtin_amdgcn_exp2f(ra[q] * scale);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ra[q] = __builtin_amdgcn_exp2f(ra[q] * scale);
+    }
+    rs += (ra[0] + ra[1]) + (ra[2] + ra[3]);
+    bf16x4 s0, s1, s2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const Split3 v = split3(ra[q]);
+      s0[q] = v.s0;
+      s1[q] = v.s1;
+      s2[q] = v.s2;
+    }
+    const int off = x3_off(row, c4 >> 1) + ((c4 & 1) << 3);
+    *reinterpret_cast<bf16x4*>(st + off) = s0;
+    *reinterpret_cast<bf16x4*>(st + BM * 32 + off) = s1;
+    *reinterpret_cast<bf16x4*>(st + 2 * BM * 32 + off) = s2;
+  }
+
+  // ---- DMA path: both operands by LDS-DMA (buffer_load_dwordx4 ... lds:
+  // wave-uniform LDS base + 16 B per lane, per-lane source offsets).  Only
+  // LDS-DMA in the loop, so every vmcnt wait is counted by hand (a plain
+  // load beside it makes hipcc wait vmcnt(0): cdna_hip_programming.md "three
+  // .s-level traps" (b)).
+  static constexpr int kRaw = 2 * kStage;  // D ring: 2 x 8 KiB raw panels
+
+  __device__ __forceinline__ static void dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff,
+                                               int soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
+                                             voff, soff, 0, 0);
+  }
+
+  // tile j0's B image -> LDS stage st
+  __device__ __forceinline__ void dma_b(char* st, __amdgpu_buffer_rsrc_t rB, int64_t ldy,
+                                        int64_t j0) {
+    const int t = threadIdx.x, wbase = t & ~63;
+    const int soB = (int)((j0 >> 4) * kX3Parts * ldy * 32);
+#pragma unroll
+    for (int u = 0; u < LB; ++u) {
+      const int f = t + u * kThreads, p = f / (2 * BC), rem = f % (2 * BC);
+      dma16(rB, st + SA + (wbase + u * kThreads) * 16, (int)(p * ldy * 32 + rem * 16), soB);
+    }
+  }
+
+  // tile j0's D panel (8 KiB) -> raw slot: thread t's 16 B land at t * 16,
+  // where the same thread reads them (no barrier needed, only its vmcnt)
+  __device__ __forceinline__ void dma_d(char* raw, __amdgpu_buffer_rsrc_t rA, int64_t j0) {
+    const int t = threadIdx.x;
+    dma16(rA, raw + (t & ~63) * 16, t * 16, (int)((j0 >> 4) * kPanelElems * 4));
+  }
+
+  __device__ __forceinline__ void read_a(const char* st, int wr) {
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int p = 0; p < kX3Parts; ++p)
+        a[mi][p] = *reinterpret_cast<const bf16x8*>(st + p * BM * 32 +
+                                                     x3_off(wr * 32 * TM + mi * 32 + r, h));
+  }
+
+  // column tiles [N0, N1) of this wave
+  template <int N0, int N1>
+  __device__ __forceinline__ void compute(const char* st, int wc) {
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int ni = N0; ni < N1; ++ni) {
+      bf16x8 b[kX3Parts];
+#pragma unroll
+      for (int p = 0; p < kX3Parts; ++p)
+        b[p] = *reinterpret_cast<const bf16x8*>(st + SA + p * BC * 32 +
+                                                x3_off(wc * 32 * TN + ni * 32 + r, h));
+      // small terms first; the two row tiles interleaved (independent chains)
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][2], b[0], acc[mi][ni]);
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][1], b[1], acc[mi][ni]);
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][0], b[2], acc[mi][ni]);
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][1], b[0], acc[mi][ni]);
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][0], b[1], acc[mi][ni]);
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][0], b[0], acc[mi][ni]);
+    }
+  }
+
+  // LDS writes of this thread done, then every wave's (no vmcnt wait: the
+  // next tile's loads stay in flight)
+  __device__ __forceinline__ static void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+
+  // Apanels: the block's 128-row panel row (panel layout); Yx: the split Y
+  // image offset to the block's first column; K range [k0, k1) (multiples of 16).
+  __device__ __forceinline__ void run(const float* __restrict__ Apanels, const __bf16* __restrict__ Yx,
+                                      int64_t ldy, int64_t k0, int64_t k1, float scale, char* smem,
+                                      int64_t row_g0) {
+    const int w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
+    rs = 0.f;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[mi][ni][q] = 0.f;
+    if (k0 >= k1) return;
+    if (DMA) {
+      const __amdgpu_buffer_rsrc_t rA =
+          __builtin_amdgcn_make_buffer_rsrc((void*)Apanels, (short)0, 0x7fffffff, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rB =
+          __builtin_amdgcn_make_buffer_rsrc((void*)Yx, (short)0, 0x7fffffff, 0x00020000);
+      char* raw = smem + kRaw;
+      dma_b(smem, rB, ldy, k0);
+      dma_d(raw, rA, k0);
+      if (k0 + BJ < k1) dma_d(raw + kPanelElems * 4, rA, k0 + BJ);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ra = *reinterpret_cast<const f32x4*>(raw + threadIdx.x * 16);
+      store_a(smem, scale, row_g0 - k0);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      for (int64_t j0 = k0; j0 < k1; j0 += 2 * BJ) {
+        step_dma<0>(rA, rB, ldy, j0, k1, scale, smem, row_g0, wr, wc);
+        if (j0 + BJ < k1) step_dma<1>(rA, rB, ldy, j0 + BJ, k1, scale, smem, row_g0, wr, wc);
+      }
+      return;
+    } else {
+      load(Apanels, Yx, ldy, k0);
+      store(smem, scale, row_g0 - k0);
+      if (k0 + BJ < k1) load(Apanels, Yx, ldy, k0 + BJ);
+      lds_barrier();
+    }
+    // unrolled by two so both LDS stage bases are compile-time constants
+    for (int64_t j0 = k0; j0 < k1; j0 += 2 * BJ) {
+      step<0>(Apanels, Yx, ldy, j0, k1, scale, smem, row_g0, wr, wc);
+      if (j0 + BJ < k1) step<1>(Apanels, Yx, ldy, j0 + BJ, k1, scale, smem, row_g0, wr, wc);
+    }
+  }
+
+  template <int CUR>
+  __device__ __forceinline__ void step(const float* __restrict__ Apanels, const __bf16* __restrict__ Yx,
+                                       int64_t ldy, int64_t j0, int64_t k1, float scale, char* smem,
+                                       int64_t row_g0, int wr, int wc) {
+    const char* cur = smem + CUR * kStage;
+    read_a(cur, wr);
+    compute<0, kHalf>(cur, wc);
+    if (j0 + BJ < k1) store(smem + (CUR ^ 1) * kStage, scale, row_g0 - (j0 + BJ));
+    if (j0 + 2 * BJ < k1) load(Apanels, Yx, ldy, j0 + 2 * BJ);
+    compute<kHalf, TN>(cur, wc);
+    lds_barrier();
+  }
+
+  // iteration k (tile j0, LDS stage CUR): DMA tile k+1's B into stage CUR^1
+  // (free since the last barrier) and tile k+2's D into raw slot CUR (its
+  // tile k was consumed last iteration); halfway, stage tile k+1's A from
+  // raw slot CUR^1 (DMA'd last iteration: LB + 1 DMAs younger than it).
+  template <int CUR>
+  __device__ __forceinline__ void step_dma(__amdgpu_buffer_rsrc_t rA, __amdgpu_buffer_rsrc_t rB,
+                                           int64_t ldy, int64_t j0, int64_t k1, float scale,
+                                           char* smem, int64_t row_g0, int wr, int wc) {
+    const char* cur = smem + CUR * kStage;
+    char* raw = smem + kRaw;
+    const bool more = j0 + BJ < k1, more2 = j0 + 2 * BJ < k1;
+    if (more) dma_b(smem + (CUR ^ 1) * kStage, rB, ldy, j0 + BJ);
+    if (more2) dma_d(raw + CUR * kPanelElems * 4, rA, j0 + 2 * BJ);
+    read_a(cur, wr);
+    compute<0, kHalf>(cur, wc);
+    if (more) {
+      if (more2)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB + 1) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB) : "memory");
+      ra = *reinterpret_cast<const f32x4*>(raw + (CUR ^ 1) * kPanelElems * 4 + threadIdx.x * 16);
+      store_a(smem + (CUR ^ 1) * kStage, scale, row_g0 - (j0 + BJ));
+    }
+    compute<kHalf, TN>(cur, wc);
+    // this wave's B DMAs landed (the D DMA may stay in flight), LDS writes
+    // done, then all waves
+    if (more2)
+      asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+
+  // full row sum of row threadIdx.x >> 2 (4 consecutive lanes stage a row)
+  __device__ __forceinline__ float row_sum() const {
+    float v = rs;
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    return v;
+  }
+};
+
+}  // namespace dsvgd

@@ -13,6 +13,7 @@
 #include <string>
 
 #include "gemm_tiles.hpp"
+#include "gemm_x3.hpp"
 
 namespace dsvgd {
 
@@ -66,6 +67,91 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
       if (c4 == 0 && row < m) rowsum[row] = v;
     }
   }
+}
+
+// phi_mm on the bf16 MFMA at fp32 accuracy (gemm_x3.hpp): the same blocks,
+// split-K slices, diagonal skip and row sums as nn_kernel<TN, true>; B is the
+// split image of Y (dsvgd_ysplit).
+template <int TN, bool DMA>
+__global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A, int64_t a_npad,
+                                                    const __bf16* __restrict__ Yx, int64_t ldy,
+                                                    int64_t K, int64_t kchunk,
+                                                    const dsvgd_select_state* __restrict__ st,
+                                                    float* __restrict__ C, int64_t ldc,
+                                                    float* __restrict__ rowsum, int64_t m,
+                                                    int64_t row0) {
+  using Tile = NNX3Tile<TN, DMA>;
+  __shared__ __attribute__((aligned(16))) char smem[Tile::kSmemBytes];
+  const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
+  const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
+  const int64_t k0 = (int64_t)blockIdx.z * kchunk;
+  const int64_t k1 = min(K, k0 + kchunk);
+  C += (int64_t)blockIdx.z * m * ldc;
+  rowsum += (int64_t)blockIdx.z * roundup128(m);
+  const float scale = -st->inv_h * kLog2e;
+  Tile tile;
+  tile.run(A + (i0 >> 7) * (a_npad >> 4) * kPanelElems, Yx + c0 * 16, ldy, k0, k1, scale, smem,
+           row0 + i0);
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
+  const int64_t r0 = i0 + wr * 32 * Tile::TM;
+#pragma unroll
+  for (int mi = 0; mi < Tile::TM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+      const int64_t col = c0 + wc * 32 * TN + ni * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = r0 + mi * 32 + c_row(r, lane);
+        if (row < m) C[row * ldc + col] = tile.acc[mi][ni][r];
+      }
+    }
+  if (blockIdx.x == 0) {
+    const float v = tile.row_sum();
+    const int64_t row = i0 + (threadIdx.x >> 2);
+    if ((threadIdx.x & 3) == 0 && row < m) rowsum[row] = v;
+  }
+}
+
+// Yx[kstep][part][column][16 k] = the three bf16 parts of Y[16 kstep + k][column]
+// (gemm_x3.hpp image: 16-B halves swapped on columns with bit 3 set).
+__global__ __launch_bounds__(256) void ysplit_kernel(const float* __restrict__ Y, int64_t ldy,
+                                                     int64_t ksteps, __bf16* __restrict__ Yx) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= ksteps * ldy) return;
+  const int64_t kb = t / ldy, c = t % ldy;
+  bf16x8 s[kX3Parts][2];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const Split3 v = split3(Y[(kb * 16 + k) * ldy + c]);
+    s[0][k >> 3][k & 7] = v.s0;
+    s[1][k >> 3][k & 7] = v.s1;
+    s[2][k >> 3][k & 7] = v.s2;
+  }
+  const int sw = (int)((c >> 3) & 1);
+#pragma unroll
+  for (int p = 0; p < kX3Parts; ++p) {
+    __bf16* dst = Yx + ((kb * kX3Parts + p) * ldy + c) * 16;
+    *reinterpret_cast<bf16x8*>(dst + 8 * sw) = s[p][0];
+    *reinterpret_cast<bf16x8*>(dst + 8 * (sw ^ 1)) = s[p][1];
+  }
+}
+
+template <int TN>
+int launch_nn_x3(const float* D, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
+                 const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
+                 int64_t row0, hipStream_t s) {
+  const int64_t kchunk = roundup((K + splits - 1) / splits, kX3Step);
+  const dim3 grid(ldy / (128 * TN), roundup(m, 128) / 128, splits);
+  // DSVGD_X3_DMA=0: Yx staged through VGPRs + ds_write (A/B switch)
+  const char* e = getenv("DSVGD_X3_DMA");
+  if ((e && e[0] == '0') || TN == 1)  // TN = 1: 1.5 DMA rounds per K-step
+    hipLaunchKernelGGL((nn_x3_kernel<TN, false>), grid, dim3(512), 0, s, D, K, Yx, ldy, K, kchunk,
+                       st, C, ldc, rowsum, m, row0);
+  else
+    hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1>), grid, dim3(512), 0, s, D, K, Yx, ldy, K, kchunk,
+                       st, C, ldc, rowsum, m, row0);
+  return check_launch("nn_x3_kernel");
 }
 
 // phi[i][c] = inv_n (KS[i][c] + (2/h)(r_i xc[i][c] - KX[i][c])) [+ extra[i][c]];
@@ -387,6 +473,46 @@ int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64
   DSVGD_REQUIRE(row0 >= 0 && row0 + m <= n, "row block outside [0, n)");
   return nn_gemm(true, D, n_pad, Y, ldy, ldy, (int)splits, st, KY, ldk, rowsum, m, row0,
                  (hipStream_t)stream);
+}
+
+int64_t dsvgd_ysplit_bytes(int64_t rows, int64_t ldy) {
+  return roundup(rows, kX3Step) * kX3Parts * ldy * 2;
+}
+
+int dsvgd_ysplit(const float* Y, int64_t ldy, int64_t rows, void* Yx, void* stream) {
+  DSVGD_REQUIRE(Y && Yx, "null pointer");
+  DSVGD_REQUIRE(rows > 0 && rows % kX3Step == 0, "rows must be a positive multiple of 16");
+  DSVGD_REQUIRE(ldy > 0 && ldy % 8 == 0, "ldy must be a multiple of 8");
+  DSVGD_REQUIRE(((uintptr_t)Yx & 15) == 0, "16-byte alignment");
+  const int64_t ksteps = rows / kX3Step, threads = ksteps * ldy;
+  hipLaunchKernelGGL(ysplit_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, Y, ldy, ksteps, (__bf16*)Yx);
+  return check_launch("ysplit");
+}
+
+int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, int64_t row0,
+                    int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
+                    int64_t ldk, float* rowsum, void* stream) {
+  DSVGD_REQUIRE(D && Yx && st && KY && rowsum, "null pointer");
+  DSVGD_REQUIRE(m > 0 && n > 0, "sizes");
+  const int64_t n_pad = roundup(n, 128);
+  DSVGD_REQUIRE(ldd == n_pad, "ldd must equal roundup(n,128) (panel layout)");
+  DSVGD_REQUIRE(ldy % 128 == 0 && ldk >= ldy, "ldy must be a multiple of 128, ldk >= ldy");
+  DSVGD_REQUIRE(((uintptr_t)Yx & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
+  DSVGD_REQUIRE(roundup(m, 128) / 128 <= 65535, "too many row tiles");
+  DSVGD_REQUIRE(splits >= 1 && splits <= 1024, "splits must be in [1, 1024]");
+  DSVGD_REQUIRE(row0 >= 0 && row0 + m <= n, "row block outside [0, n)");
+  // buffer-resource loads: 32-bit byte offsets into the block's D panel row
+  // and into Yx (K rows x 3 parts x ldy x 2 B)
+  DSVGD_REQUIRE(n_pad * ldy * 6 < ((int64_t)1 << 31) && n_pad * 128 * 4 < ((int64_t)1 << 31),
+                "n x ldy too large for 32-bit buffer offsets (use dsvgd_phi_mm)");
+  const __bf16* yx = (const __bf16*)Yx;
+  hipStream_t s = (hipStream_t)stream;
+  if (ldy % 512 == 0)
+    return launch_nn_x3<4>(D, n_pad, yx, ldy, (int)splits, st, KY, ldk, rowsum, m, row0, s);
+  if (ldy % 256 == 0)
+    return launch_nn_x3<2>(D, n_pad, yx, ldy, (int)splits, st, KY, ldk, rowsum, m, row0, s);
+  return launch_nn_x3<1>(D, n_pad, yx, ldy, (int)splits, st, KY, ldk, rowsum, m, row0, s);
 }
 
 int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t splits,

@@ -17,6 +17,7 @@ median global (RCCL all_reduce of 2048 int64 counts per pass).
 """
 import ctypes
 import math
+import os
 
 import torch
 
@@ -157,6 +158,13 @@ class PhiEngine(object):
         self.norms = torch.zeros(rows, **f32)
         self.D = torch.empty(self.m_pad * self.n_pad, **f32)
         self.splits = lib.dsvgd_phi_splits(m, n, self.ldy)
+        # phi_mm engine: "x3" = bf16 MFMA with a 3-way split (fp32-accurate,
+        # csrc/gemm_x3.hpp), "f32" = the f32 MFMA engine (DSVGD_PHI_GEMM=f32)
+        self.x3 = (os.environ.get("DSVGD_PHI_GEMM", "x3") == "x3"
+                   and self.n_pad * self.ldy * 6 < (1 << 31))
+        if self.x3:
+            nb = lib.dsvgd_ysplit_bytes(self.n_pad, self.ldy)
+            self.Yx = torch.empty(nb // 2, dtype=torch.int16, device=dev)
         self.KY = torch.empty(self.splits * m, self.ldy, **f32)
         self.rowsum = torch.empty(self.splits * self.m_pad, **f32)
         self.mean = torch.empty(d, **f32)
@@ -283,10 +291,18 @@ class PhiEngine(object):
                        float(step), ex, lde, phi, self.d, xo, ldx, N.ptr(self.KY),
                        self.KY.numel(), s)
             return
-        with span(self.timer, "phi_mm"):
-            N.call("dsvgd_phi_mm", N.ptr(self.D), self.n_pad, N.ptr(self.Y), self.ldy, self.row0,
-                   self.m, self.n, self.state.ptr, self.splits, N.ptr(self.KY), self.ldy,
-                   N.ptr(self.rowsum), s)
+        if self.x3:
+            with span(self.timer, "ysplit"):
+                N.call("dsvgd_ysplit", N.ptr(self.Y), self.ldy, self.n_pad, N.ptr(self.Yx), s)
+            with span(self.timer, "phi_mm"):
+                N.call("dsvgd_phi_mm_x3", N.ptr(self.D), self.n_pad, N.ptr(self.Yx), self.ldy,
+                       self.row0, self.m, self.n, self.state.ptr, self.splits, N.ptr(self.KY),
+                       self.ldy, N.ptr(self.rowsum), s)
+        else:
+            with span(self.timer, "phi_mm"):
+                N.call("dsvgd_phi_mm", N.ptr(self.D), self.n_pad, N.ptr(self.Y), self.ldy,
+                       self.row0, self.m, self.n, self.state.ptr, self.splits, N.ptr(self.KY),
+                       self.ldy, N.ptr(self.rowsum), s)
         N.call("dsvgd_phi_finish", N.ptr(self.KY), self.ldy, N.ptr(self.rowsum), self.splits,
                N.ptr(self.Y), self.ldy, self.row0, self.m, self.d, self.dp, self.state.ptr,
                float(inv_n), float(step), ex, lde, phi, self.d, xo, ldx, s)

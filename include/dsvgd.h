@@ -172,6 +172,21 @@ int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64
                  int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
                  int64_t ldk, float* rowsum, void* stream);
 
+/* phi_mm on the bf16 MFMA at fp32 accuracy (the default engine): both
+ * operands split three ways into bf16 (v = v0 + v1 + v2 to ~2^-26 |v|) and
+ * the six products a_i b_j with i + j <= 2 accumulated in fp32, so the
+ * result carries fp32 GEMM rounding, not bf16's.  Same arguments, outputs,
+ * split-K slices and diagonal rule as dsvgd_phi_mm; Yx = dsvgd_ysplit(Y)
+ * (rows >= roundup(n, 128)).  Requires roundup(n,128) * ldy * 6 < 2^31.
+ * dsvgd_ysplit: Yx[kstep][part][column][16] (bf16) from the first `rows`
+ * rows of Y (rows a multiple of 16; dsvgd_ysplit_bytes(rows, ldy) bytes,
+ * 16-byte aligned); 16-byte halves swapped on columns with bit 3 set. */
+int64_t dsvgd_ysplit_bytes(int64_t rows, int64_t ldy);
+int dsvgd_ysplit(const float* Y, int64_t ldy, int64_t rows, void* Yx, void* stream);
+int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, int64_t row0,
+                    int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
+                    int64_t ldk, float* rowsum, void* stream);
+
 /* phi[i] = inv_n * (s_i + KS[i] + (2/h) (rowsum[i] xc[i] - KXc[i])) with the
  * split-K partials summed in slice order (s_i: the self term k_ii s_i), plus
  * extra[i] if extra != NULL (the h * W2-gradient row of dsvgd_w2_grad:

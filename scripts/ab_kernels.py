@@ -4,7 +4,8 @@
     python scripts/ab_kernels.py [--n 65536 --d 256 --rounds 5]
 
 Variants are switched through environment variables the launchers read on
-every call (DSVGD_NN_SHAPE=w2 forces the 16-deep NN K-step).
+every call (DSVGD_NN_SHAPE=w2 forces the 16-deep NN K-step of the f32 engine;
+ENGINE_X3 picks the phi_mm engine).
 """
 import argparse
 import json
@@ -45,8 +46,9 @@ def main():
     eng.pack(X, S)
     eng.distances(median=True)
     eng.median_bandwidth()
+    # ENGINE_X3: "1" = the bf16-split phi_mm (default), "0" = the f32 MFMA engine
     variants = json.loads(os.environ.get("AB_VARIANTS", "null")) or {
-        "nn=bj32": {}, "nn=bj16": {"DSVGD_NN_SHAPE": "w2"}}
+        "phi=x3": {"ENGINE_X3": "1"}, "phi=f32": {"ENGINE_X3": "0"}}
     res = {k: [] for k in variants}
     ref = None
     keys = {k for env in variants.values() for k in env}
@@ -55,6 +57,7 @@ def main():
             for k in keys:               # a variant's knobs must not leak into the next
                 os.environ.pop(k, None)
             os.environ.update(env)
+            eng.x3 = env.get("ENGINE_X3", "1") == "1" and hasattr(eng, "Yx")
             res[name].append(timed(lambda: eng.direction(write_phi=True)))
             if ref is None:
                 ref = eng.phi.clone()
