@@ -73,7 +73,8 @@ __device__ __forceinline__ int x3_off(int x, int h) { return x * 32 + ((h ^ ((x 
 // DMA: both operands reach LDS by LDS-DMA (the B image is lane-linear; D
 // lands raw in a 2-slot ring and is staged from there), issued at the start
 // of iteration k for B of tile k+1 and D of tile k+2; counted vmcnt waits.
-template <int TN, bool DMA = true>
+// EXP = false: f = identity (logreg G . Xd): no exp, no diagonal, no row sums.
+template <int TN, bool DMA = true, bool EXP = true>
 struct NNX3Tile {
   // (DMA needs the same DMA count in every wave: whole 512-chunk rounds)
   static constexpr int kThreads = 512;
@@ -134,7 +135,8 @@ struct NNX3Tile {
   // exp / diagonal / row sum / 3-way split of this thread's 4 D values (ra)
   __device__ __forceinline__ void store_a(char* st, float scale, int64_t dgl) {
     const int t = threadIdx.x, row = t >> 2, c4 = t & 3;
-    if (dgl > -BM && dgl < BJ) {  // the K-step holds diagonal entries (NNTile::store)
+    if (!EXP) {
+    } else if (dgl > -BM && dgl < BJ) {  // the K-step holds diagonal entries (NNTile::store)
       const int qd = (int)dgl + row - 4 * c4;
 #pragma unroll
       for (int q = 0; q < 4; ++q) ra[q] = (qd == q) ? 0.f : __builtin_amdgcn_exp2f(ra[q] * scale);
@@ -142,7 +144,7 @@ struct NNX3Tile {
 #pragma unroll
       for (int q = 0; q < 4; ++q) ra[q] = __builtin_amdgcn_exp2f(ra[q] * scale);
     }
-    rs += (ra[0] + ra[1]) + (ra[2] + ra[3]);
+    if (EXP) rs += (ra[0] + ra[1]) + (ra[2] + ra[3]);
     bf16x4 s0, s1, s2;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -328,6 +330,146 @@ struct NNX3Tile {
     v += __shfl_xor(v, 1, 64);
     v += __shfl_xor(v, 2, 64);
     return v;
+  }
+};
+
+// ---- NT engine on the split images: C[BM x BN] = A[BM x K] . B[BN x K]^T
+// (the Gram, logreg Z, predict).  Both operands come as row images
+//     img[kstep][part][row][16 k]  (bf16, 32 B per row, halves swapped on
+//     rows with bit 3 set -- dsvgd_rowsplit)
+// and reach LDS verbatim by LDS-DMA (a block's 128 rows of one part are 4 KiB
+// contiguous), through a 3-stage ring: iteration k issues tile k+2 and waits
+// (counted vmcnt) for tile k+1 before its closing barrier, so a DMA has two
+// iterations to land.  No VGPR staging, no VALU in the loop but the MFMAs.
+template <int TM, int TN, int WM, int WN>
+struct NTX3Tile {
+  static constexpr int TM_ = TM, TN_ = TN, WM_ = WM, WN_ = WN;
+  static constexpr int kThreads = 64 * WM * WN;
+  static constexpr int BM = 32 * TM * WM;
+  static constexpr int BN = 32 * TN * WN;
+  static constexpr int BK = kX3Step;
+  static constexpr int SA = kX3Parts * BM * 32;
+  static constexpr int SB = kX3Parts * BN * 32;
+  static constexpr int kStage = SA + SB;
+  static constexpr int kStages = 3;
+  static constexpr int kSmemBytes = kStages * kStage;
+  static constexpr int LA = SA / 16 / kThreads;  // DMAs per thread per K-step (A)
+  static constexpr int LBn = SB / 16 / kThreads;
+  static constexpr int kDmas = LA + LBn;
+  static_assert(SA % (16 * kThreads) == 0 && SB % (16 * kThreads) == 0, "whole DMA rounds");
+  static_assert(BM * 32 % (16 * kThreads) == 0, "a DMA round stays inside one part");
+  static_assert(kSmemBytes <= 160 * 1024, "LDS budget");
+
+  f32x16 acc[TM][TN];
+
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[mi][ni][q] = 0.f;
+  }
+
+  __device__ __forceinline__ static void dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff,
+                                               int soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
+                                             voff, soff, 0, 0);
+  }
+
+  // K-step kb of A (image rows from rA's base, mA image rows per part) and B
+  // into stage st
+  __device__ __forceinline__ void dma(char* st, __amdgpu_buffer_rsrc_t rA, int64_t mA,
+                                      __amdgpu_buffer_rsrc_t rB, int64_t mB, int64_t kb) {
+    const int t = threadIdx.x, wbase = t & ~63;
+    const int soA = (int)(kb * kX3Parts * mA * 32), soB = (int)(kb * kX3Parts * mB * 32);
+#pragma unroll
+    for (int u = 0; u < LA; ++u) {
+      const int f = t + u * kThreads, pp = f / (BM * 2), in = f % (BM * 2);
+      dma16(rA, st + (wbase + u * kThreads) * 16, (int)(pp * mA * 32 + in * 16), soA);
+    }
+#pragma unroll
+    for (int u = 0; u < LBn; ++u) {
+      const int f = t + u * kThreads, pp = f / (BN * 2), in = f % (BN * 2);
+      dma16(rB, st + SA + (wbase + u * kThreads) * 16, (int)(pp * mB * 32 + in * 16), soB);
+    }
+  }
+
+  __device__ __forceinline__ void compute(const char* st, int wm, int wn) {
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+    bf16x8 a[TM][kX3Parts];
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int p = 0; p < kX3Parts; ++p)
+        a[mi][p] = *reinterpret_cast<const bf16x8*>(st + p * BM * 32 +
+                                                     x3_off(wm * 32 * TM + mi * 32 + r, h));
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+      bf16x8 b[kX3Parts];
+#pragma unroll
+      for (int p = 0; p < kX3Parts; ++p)
+        b[p] = *reinterpret_cast<const bf16x8*>(st + SA + p * BN * 32 +
+                                                x3_off(wn * 32 * TN + ni * 32 + r, h));
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][2], b[0], acc[mi][ni]);
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][1], b[1], acc[mi][ni]);
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][0], b[2], acc[mi][ni]);
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][1], b[0], acc[mi][ni]);
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][0], b[1], acc[mi][ni]);
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][0], b[0], acc[mi][ni]);
+    }
+  }
+
+  // this wave's DMAs but the N youngest landed, its LDS reads done; barrier
+  template <int N>
+  __device__ __forceinline__ static void ring_barrier() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+  }
+
+  // One tile: A rows from imgA (already offset to the block's first row; mA
+  // image rows per part), B likewise; nk K-steps of 16.
+  __device__ __forceinline__ void run(const __bf16* imgA, int64_t mA, const __bf16* imgB,
+                                      int64_t mB, int nk, char* smem) {
+    const int w = threadIdx.x >> 6, wm = w / WN, wn = w % WN;
+    const __amdgpu_buffer_rsrc_t rA =
+        __builtin_amdgcn_make_buffer_rsrc((void*)imgA, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB =
+        __builtin_amdgcn_make_buffer_rsrc((void*)imgB, (short)0, 0x7fffffff, 0x00020000);
+    zero();
+    dma(smem, rA, mA, rB, mB, 0);
+    if (nk > 1) {
+      dma(smem + kStage, rA, mA, rB, mB, 1);
+      ring_barrier<kDmas>();
+    } else {
+      ring_barrier<0>();
+    }
+    // unrolled by three: the ring's stage bases are compile-time constants
+    for (int k = 0; k < nk; k += 3) {
+      step<0>(k, nk, rA, mA, rB, mB, smem, wm, wn);
+      if (k + 1 < nk) step<1>(k + 1, nk, rA, mA, rB, mB, smem, wm, wn);
+      if (k + 2 < nk) step<2>(k + 2, nk, rA, mA, rB, mB, smem, wm, wn);
+    }
+  }
+
+  template <int S>
+  __device__ __forceinline__ void step(int k, int nk, __amdgpu_buffer_rsrc_t rA, int64_t mA,
+                                       __amdgpu_buffer_rsrc_t rB, int64_t mB, char* smem, int wm,
+                                       int wn) {
+    const bool more2 = k + 2 < nk;
+    if (more2) dma(smem + ((S + 2) % 3) * kStage, rA, mA, rB, mB, k + 2);
+    compute(smem + S * kStage, wm, wn);
+    if (k + 1 < nk) {
+      if (more2)
+        ring_barrier<kDmas>();
+      else
+        ring_barrier<0>();
+    }
   }
 };
 

@@ -9,14 +9,19 @@
 // G Xd (NN MFMA engine); 4 n N p flop, MFMA-bound.
 #include <cmath>
 #include <cstdlib>
+#include <string>
 
 #include "gemm_tiles.hpp"
+#include "gemm_x3.hpp"
 
 namespace dsvgd {
 
 int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, int64_t cols,
             int splits, const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum,
             int64_t m, int64_t row0, hipStream_t s);
+int nn_x3_gemm(bool exp_, const float* A, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
+               const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
+               int64_t row0, hipStream_t s);
 
 static int64_t nn_cols(int64_t w) {
   if (w <= 128) return 128;
@@ -26,7 +31,7 @@ static int64_t nn_cols(int64_t w) {
 
 struct LogregWs {
   int64_t n_pad, N_pad, pp, ldb;
-  size_t off_w, off_xd, off_t, off_g, off_gw, total;
+  size_t off_w, off_xd, off_t, off_g, off_gw, off_wx, off_xdx, off_xdy, total;
 };
 
 static LogregWs logreg_ws(int64_t n, int64_t N, int64_t p) {
@@ -46,6 +51,10 @@ static LogregWs logreg_ws(int64_t n, int64_t N, int64_t p) {
   w.off_t = take((size_t)w.N_pad);
   w.off_g = take((size_t)w.n_pad * w.N_pad);
   w.off_gw = take((size_t)w.n_pad * w.ldb);
+  // split images (bf16 x 3 = 6 B per element, counted in floats)
+  w.off_wx = take((size_t)w.n_pad * w.pp * 3 / 2);
+  w.off_xdx = take((size_t)w.N_pad * w.pp * 3 / 2);
+  w.off_xdy = take((size_t)w.N_pad * w.ldb * 3 / 2);
   w.total = o;
   return w;
 }
@@ -100,6 +109,21 @@ __device__ __forceinline__ void z_epilogue(T& tile, int64_t i0, int64_t q0,
       }
     }
   }
+}
+
+// Z on the split engine (fp32-accurate, gemm_x3.hpp): W and Xd as row images.
+using ZX3Tile = NTX3Tile<2, 2, 2, 2>;
+__global__ __launch_bounds__(256) void logreg_z_x3_kernel(const __bf16* __restrict__ Wx,
+                                                          int64_t n_pad,
+                                                          const __bf16* __restrict__ Xdx,
+                                                          int64_t N_pad, int nk,
+                                                          const float* __restrict__ tp,
+                                                          float* __restrict__ G) {
+  __shared__ __attribute__((aligned(16))) char smem[ZX3Tile::kSmemBytes];
+  const int64_t i0 = (int64_t)blockIdx.y * ZX3Tile::BM, q0 = (int64_t)blockIdx.x * ZX3Tile::BN;
+  ZX3Tile tile;
+  tile.run(Wx + i0 * 16, n_pad, Xdx + q0 * 16, N_pad, nk, smem);
+  z_epilogue(tile, i0, q0, tp, N_pad, G);
 }
 
 // One (particle tile, data tile) per block.
@@ -315,11 +339,17 @@ int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const 
   float* G = (float*)(base + w.off_g);
   float* GW = (float*)(base + w.off_gw);
   hipStream_t s = (hipStream_t)stream;
+  // DSVGD_LOGREG_GEMM=f32: the f32 MFMA engines (A/B and precision checks)
+  const char* ge = getenv("DSVGD_LOGREG_GEMM");
+  const bool x3 = !(ge && std::string(ge) == "f32") && w.n_pad * w.pp * 6 < ((int64_t)1 << 31) &&
+                  w.N_pad * w.ldb * 6 < ((int64_t)1 << 31);
   int64_t tot = w.n_pad * w.ldb;
-  hipLaunchKernelGGL(pad_copy_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, X, ldx, 1, n, p,
-                     w.n_pad, Wp, w.ldb);
-  int rc = check_launch("pad_copy(W)");
-  if (rc) return rc;
+  int rc = 0;
+  if (!x3) {
+    hipLaunchKernelGGL(pad_copy_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, X, ldx, 1, n, p,
+                       w.n_pad, Wp, w.ldb);
+    if ((rc = check_launch("pad_copy(W)"))) return rc;
+  }
   tot = w.N_pad * w.ldb;
   hipLaunchKernelGGL(pad_copy_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Xd, ldxd, 0, N, p,
                      w.N_pad, Xdp, w.ldb);
@@ -327,6 +357,23 @@ int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const 
   hipLaunchKernelGGL(pad_copy_kernel, dim3((w.N_pad + 255) / 256), dim3(256), 0, s, t, 1, 0, N, 1,
                      w.N_pad, tp, 1);
   if ((rc = check_launch("pad_copy(t)"))) return rc;
+  if (x3) {
+    void* Wx = base + w.off_wx;
+    void* Xdx = base + w.off_xdx;
+    __bf16* Xdy = (__bf16*)(base + w.off_xdy);
+    if ((rc = dsvgd_rowsplit(X + 1, ldx, n, p, w.n_pad, w.pp, Wx, s))) return rc;
+    if ((rc = dsvgd_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, Xdx, s))) return rc;
+    if ((rc = dsvgd_ysplit(Xdp, w.ldb, w.N_pad, Xdy, s))) return rc;
+    hipLaunchKernelGGL(logreg_z_x3_kernel, dim3(w.N_pad / ZX3Tile::BN, w.n_pad / ZX3Tile::BM),
+                       dim3(256), 0, s, (const __bf16*)Wx, w.n_pad, (const __bf16*)Xdx, w.N_pad,
+                       (int)(w.pp / kX3Step), tp, G);
+    if ((rc = check_launch("logreg_z_x3"))) return rc;
+    if ((rc = nn_x3_gemm(false, G, w.N_pad, Xdy, w.ldb, 1, nullptr, GW, w.ldb, nullptr, n, 0, s)))
+      return rc;
+    hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,
+                       w.ldb, scale, S, lds);
+    return check_launch("logreg_finish");
+  }
   hipLaunchKernelGGL(logreg_z_kernel, dim3(w.N_pad / ZTile::BN, w.n_pad / ZTile::BM), dim3(256), 0,
                      s, Wp, Xdp, w.ldb, (int)w.pp, tp, N, w.N_pad, G);
   if ((rc = check_launch("logreg_z"))) return rc;

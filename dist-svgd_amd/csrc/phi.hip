@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
 // phi_mm on the bf16 MFMA at fp32 accuracy (gemm_x3.hpp): the same blocks,
 // split-K slices, diagonal skip and row sums as nn_kernel<TN, true>; B is the
 // split image of Y (dsvgd_ysplit).
-template <int TN, bool DMA>
+template <int TN, bool DMA, bool EXP>
 __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A, int64_t a_npad,
                                                     const __bf16* __restrict__ Yx, int64_t ldy,
                                                     int64_t K, int64_t kchunk,
@@ -80,15 +80,15 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
                                                     float* __restrict__ C, int64_t ldc,
                                                     float* __restrict__ rowsum, int64_t m,
                                                     int64_t row0) {
-  using Tile = NNX3Tile<TN, DMA>;
+  using Tile = NNX3Tile<TN, DMA, EXP>;
   __shared__ __attribute__((aligned(16))) char smem[Tile::kSmemBytes];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
   const int64_t k0 = (int64_t)blockIdx.z * kchunk;
   const int64_t k1 = min(K, k0 + kchunk);
   C += (int64_t)blockIdx.z * m * ldc;
-  rowsum += (int64_t)blockIdx.z * roundup128(m);
-  const float scale = -st->inv_h * kLog2e;
+  if (EXP) rowsum += (int64_t)blockIdx.z * roundup128(m);
+  const float scale = EXP ? -st->inv_h * kLog2e : 0.f;
   Tile tile;
   tile.run(A + (i0 >> 7) * (a_npad >> 4) * kPanelElems, Yx + c0 * 16, ldy, k0, k1, scale, smem,
            row0 + i0);
@@ -106,10 +106,38 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
         if (row < m) C[row * ldc + col] = tile.acc[mi][ni][r];
       }
     }
-  if (blockIdx.x == 0) {
+  if (EXP && blockIdx.x == 0) {
     const float v = tile.row_sum();
     const int64_t row = i0 + (threadIdx.x >> 2);
     if ((threadIdx.x & 3) == 0 && row < m) rowsum[row] = v;
+  }
+}
+
+// img[kstep][part][row][16 k] (bf16) = the three parts of A[row][16 kstep + k]
+// for row < rows_pad, 16 kstep + k < kpad (zero outside rows x cols); halves
+// swapped on rows with bit 3 set (NTX3Tile's image).
+__global__ __launch_bounds__(256) void rowsplit_kernel(const float* __restrict__ A, int64_t lda,
+                                                       int64_t rows, int64_t cols,
+                                                       int64_t rows_pad, int64_t ksteps,
+                                                       __bf16* __restrict__ img) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= ksteps * rows_pad) return;
+  const int64_t kb = t / rows_pad, i = t % rows_pad;
+  bf16x8 s[kX3Parts][2];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int64_t c = kb * 16 + k;
+    const Split3 v = split3((i < rows && c < cols) ? A[i * lda + c] : 0.f);
+    s[0][k >> 3][k & 7] = v.s0;
+    s[1][k >> 3][k & 7] = v.s1;
+    s[2][k >> 3][k & 7] = v.s2;
+  }
+  const int sw = (int)((i >> 3) & 1);
+#pragma unroll
+  for (int p = 0; p < kX3Parts; ++p) {
+    __bf16* dst = img + ((kb * kX3Parts + p) * rows_pad + i) * 16;
+    *reinterpret_cast<bf16x8*>(dst + 8 * sw) = s[p][0];
+    *reinterpret_cast<bf16x8*>(dst + 8 * (sw ^ 1)) = s[p][1];
   }
 }
 
@@ -137,7 +165,7 @@ __global__ __launch_bounds__(256) void ysplit_kernel(const float* __restrict__ Y
   }
 }
 
-template <int TN>
+template <int TN, bool EXP>
 int launch_nn_x3(const float* D, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
                  const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
                  int64_t row0, hipStream_t s) {
@@ -146,13 +174,31 @@ int launch_nn_x3(const float* D, int64_t K, const __bf16* Yx, int64_t ldy, int s
   // DSVGD_X3_DMA=0: Yx staged through VGPRs + ds_write (A/B switch)
   const char* e = getenv("DSVGD_X3_DMA");
   if ((e && e[0] == '0') || TN == 1)  // TN = 1: 1.5 DMA rounds per K-step
-    hipLaunchKernelGGL((nn_x3_kernel<TN, false>), grid, dim3(512), 0, s, D, K, Yx, ldy, K, kchunk,
-                       st, C, ldc, rowsum, m, row0);
+    hipLaunchKernelGGL((nn_x3_kernel<TN, false, EXP>), grid, dim3(512), 0, s, D, K, Yx, ldy, K,
+                       kchunk, st, C, ldc, rowsum, m, row0);
   else
-    hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1>), grid, dim3(512), 0, s, D, K, Yx, ldy, K, kchunk,
-                       st, C, ldc, rowsum, m, row0);
+    hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP>), grid, dim3(512), 0, s, D, K, Yx, ldy, K,
+                       kchunk, st, C, ldc, rowsum, m, row0);
   return check_launch("nn_x3_kernel");
 }
+
+// C = f(A) B on the split engine; A panel layout (m_pad x K), B = Yx image
+// (K rows, ldy columns, a multiple of 128).  exp_: the phi_mm form.
+int nn_x3_gemm(bool exp_, const float* A, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
+               const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
+               int64_t row0, hipStream_t s) {
+  if (K * ldy * 6 >= ((int64_t)1 << 31) || K * 128 * 4 >= ((int64_t)1 << 31))
+    return fail_arg("nn_x3: K x ldy too large for 32-bit buffer offsets");
+  if (ldy % 128 != 0) return fail_arg("nn_x3: ldy must be a multiple of 128");
+#define DSVGD_X3_TN(TN)                                                                        \
+  return exp_ ? launch_nn_x3<TN, true>(A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0, s)  \
+              : launch_nn_x3<TN, false>(A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0, s)
+  if (ldy % 512 == 0) DSVGD_X3_TN(4);
+  if (ldy % 256 == 0) DSVGD_X3_TN(2);
+  DSVGD_X3_TN(1);
+#undef DSVGD_X3_TN
+}
+
 
 // phi[i][c] = inv_n (KS[i][c] + (2/h)(r_i xc[i][c] - KX[i][c])) [+ extra[i][c]];
 // X[i][c] += step phi.  KY / rowsum hold `splits` split-K partials, summed
@@ -490,6 +536,23 @@ int dsvgd_ysplit(const float* Y, int64_t ldy, int64_t rows, void* Yx, void* stre
   return check_launch("ysplit");
 }
 
+int64_t dsvgd_rowsplit_bytes(int64_t rows_pad, int64_t kpad) {
+  return roundup(kpad, kX3Step) * rows_pad * kX3Parts * 2;
+}
+
+int dsvgd_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                   int64_t kpad, void* img, void* stream) {
+  DSVGD_REQUIRE(A && img, "null pointer");
+  DSVGD_REQUIRE(rows >= 0 && cols >= 0 && rows <= rows_pad && lda >= cols, "sizes");
+  DSVGD_REQUIRE(rows_pad > 0 && rows_pad % 16 == 0 && kpad > 0 && kpad % kX3Step == 0,
+                "rows_pad and kpad must be positive multiples of 16");
+  DSVGD_REQUIRE(((uintptr_t)img & 15) == 0, "16-byte alignment");
+  const int64_t ksteps = kpad / kX3Step, threads = ksteps * rows_pad;
+  hipLaunchKernelGGL(rowsplit_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, A, lda, rows, cols, rows_pad, ksteps, (__bf16*)img);
+  return check_launch("rowsplit");
+}
+
 int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, int64_t row0,
                     int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
                     int64_t ldk, float* rowsum, void* stream) {
@@ -506,13 +569,8 @@ int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, in
   // and into Yx (K rows x 3 parts x ldy x 2 B)
   DSVGD_REQUIRE(n_pad * ldy * 6 < ((int64_t)1 << 31) && n_pad * 128 * 4 < ((int64_t)1 << 31),
                 "n x ldy too large for 32-bit buffer offsets (use dsvgd_phi_mm)");
-  const __bf16* yx = (const __bf16*)Yx;
-  hipStream_t s = (hipStream_t)stream;
-  if (ldy % 512 == 0)
-    return launch_nn_x3<4>(D, n_pad, yx, ldy, (int)splits, st, KY, ldk, rowsum, m, row0, s);
-  if (ldy % 256 == 0)
-    return launch_nn_x3<2>(D, n_pad, yx, ldy, (int)splits, st, KY, ldk, rowsum, m, row0, s);
-  return launch_nn_x3<1>(D, n_pad, yx, ldy, (int)splits, st, KY, ldk, rowsum, m, row0, s);
+  return nn_x3_gemm(true, D, n_pad, (const __bf16*)Yx, ldy, (int)splits, st, KY, ldk, rowsum, m,
+                    row0, (hipStream_t)stream);
 }
 
 int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t splits,

@@ -182,6 +182,14 @@ int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64
  * rows of Y (rows a multiple of 16; dsvgd_ysplit_bytes(rows, ldy) bytes,
  * 16-byte aligned); 16-byte halves swapped on columns with bit 3 set. */
 int64_t dsvgd_ysplit_bytes(int64_t rows, int64_t ldy);
+/* Row image for the split NT engine (Gram, logreg Z): img[kstep][part][row]
+ * [16] (bf16) = the three parts of A[row][16 kstep + k] for row < rows_pad,
+ * column < kpad (zero outside rows x cols); rows_pad, kpad multiples of 16;
+ * dsvgd_rowsplit_bytes(rows_pad, kpad) bytes, 16-byte aligned; 16-byte
+ * halves swapped on rows with bit 3 set. */
+int64_t dsvgd_rowsplit_bytes(int64_t rows_pad, int64_t kpad);
+int dsvgd_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                   int64_t kpad, void* img, void* stream);
 int dsvgd_ysplit(const float* Y, int64_t ldy, int64_t rows, void* Yx, void* stream);
 int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, int64_t row0,
                     int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,

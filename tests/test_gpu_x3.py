@@ -137,3 +137,24 @@ def test_phi_mm_x3_row_block_split_k(monkeypatch):
     e = float(np.abs(phix - ref).max() / np.abs(ref).max())
     record_parity(e)
     assert e < PHI_TOL
+
+
+@pytest.mark.parametrize("n,N,p", [(1000, 3000, 20), (512, 16384, 255), (300, 129, 40)])
+def test_logreg_scores_x3_as_accurate_as_f32(monkeypatch, n, N, p):
+    """The logreg score GEMMs (Z = W Xd^T on the split NT engine, G Xd on
+    the split NN engine without exp) against the fp64 oracle, next to the
+    f32 MFMA engines on the same inputs."""
+    rs = np.random.RandomState(n + N + p)
+    X = (rs.randn(n, p + 1) * 0.5).astype(np.float32)
+    xd = (rs.randn(N, p) / np.sqrt(p)).astype(np.float32)
+    t = np.where(rs.randn(N) > 0, 1.0, -1.0).astype(np.float32)
+    tgt = dsvgd().targets.LogisticRegression(xd, t)
+    ref = O.score_logreg(X, xd, t)
+    err = {}
+    for gemm in ("f32", "x3"):
+        monkeypatch.setenv("DSVGD_LOGREG_GEMM", gemm)
+        out = torch.zeros(n, p + 1, device=DEV)
+        tgt.score(gpu(X), out)
+        err[gemm] = float(np.abs(out.cpu().numpy() - ref).max() / np.abs(ref).max())
+    record_parity(err["x3"])
+    assert err["x3"] <= 2.0 * err["f32"] + 1e-7 and err["x3"] < 1e-5, err
