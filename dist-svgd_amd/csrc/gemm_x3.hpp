@@ -341,7 +341,8 @@ struct NNX3Tile {
 // contiguous), through a 3-stage ring: iteration k issues tile k+2 and waits
 // (counted vmcnt) for tile k+1 before its closing barrier, so a DMA has two
 // iterations to land.  No VGPR staging, no VALU in the loop but the MFMAs.
-template <int TM, int TN, int WM, int WN>
+// NS: ring stages (3: a DMA has two iterations to land; 2: one, at 2/3 of the LDS).
+template <int TM, int TN, int WM, int WN, int NS = 3>
 struct NTX3Tile {
   static constexpr int TM_ = TM, TN_ = TN, WM_ = WM, WN_ = WN;
   static constexpr int kThreads = 64 * WM * WN;
@@ -351,7 +352,8 @@ struct NTX3Tile {
   static constexpr int SA = kX3Parts * BM * 32;
   static constexpr int SB = kX3Parts * BN * 32;
   static constexpr int kStage = SA + SB;
-  static constexpr int kStages = 3;
+  static constexpr int kStages = NS;
+  static_assert(NS == 2 || NS == 3, "2- or 3-stage ring");
   static constexpr int kSmemBytes = kStages * kStage;
   static constexpr int LA = SA / 16 / kThreads;  // DMAs per thread per K-step (A)
   static constexpr int LBn = SB / 16 / kThreads;
@@ -395,15 +397,19 @@ struct NTX3Tile {
     }
   }
 
-  __device__ __forceinline__ void compute(const char* st, int wm, int wn) {
+  // a0: image row of A's row 0, mod 16 (the image swizzles on the absolute
+  // row; a row block may start off a 16-row boundary)
+  __device__ __forceinline__ void compute(const char* st, int wm, int wn, int a0 = 0) {
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
     bf16x8 a[TM][kX3Parts];
 #pragma unroll
-    for (int mi = 0; mi < TM; ++mi)
+    for (int mi = 0; mi < TM; ++mi) {
+      const int lr = wm * 32 * TM + mi * 32 + r;
+      const int off = lr * 32 + ((h ^ (((a0 + lr) >> 3) & 1)) << 4);
 #pragma unroll
       for (int p = 0; p < kX3Parts; ++p)
-        a[mi][p] = *reinterpret_cast<const bf16x8*>(st + p * BM * 32 +
-                                                     x3_off(wm * 32 * TM + mi * 32 + r, h));
+        a[mi][p] = *reinterpret_cast<const bf16x8*>(st + p * BM * 32 + off);
+    }
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
       bf16x8 b[kX3Parts];
@@ -443,11 +449,18 @@ struct NTX3Tile {
         __builtin_amdgcn_make_buffer_rsrc((void*)imgB, (short)0, 0x7fffffff, 0x00020000);
     zero();
     dma(smem, rA, mA, rB, mB, 0);
-    if (nk > 1) {
+    if (NS == 3 && nk > 1) {
       dma(smem + kStage, rA, mA, rB, mB, 1);
       ring_barrier<kDmas>();
     } else {
       ring_barrier<0>();
+    }
+    if (NS == 2) {
+      for (int k = 0; k < nk; k += 2) {
+        step<0>(k, nk, rA, mA, rB, mB, smem, wm, wn);
+        if (k + 1 < nk) step<1>(k + 1, nk, rA, mA, rB, mB, smem, wm, wn);
+      }
+      return;
     }
     // unrolled by three: the ring's stage bases are compile-time constants
     for (int k = 0; k < nk; k += 3) {
@@ -461,6 +474,12 @@ struct NTX3Tile {
   __device__ __forceinline__ void step(int k, int nk, __amdgpu_buffer_rsrc_t rA, int64_t mA,
                                        __amdgpu_buffer_rsrc_t rB, int64_t mB, char* smem, int wm,
                                        int wn) {
+    if (NS == 2) {  // tile k+1 into the other stage, waited for at the end
+      if (k + 1 < nk) dma(smem + ((S + 1) % 2) * kStage, rA, mA, rB, mB, k + 1);
+      compute(smem + S * kStage, wm, wn);
+      if (k + 1 < nk) ring_barrier<0>();
+      return;
+    }
     const bool more2 = k + 2 < nk;
     if (more2) dma(smem + ((S + 2) % 3) * kStage, rA, mA, rB, mB, k + 2);
     compute(smem + S * kStage, wm, wn);

@@ -12,6 +12,7 @@
 #include <cstdlib>
 
 #include "gemm_tiles.hpp"
+#include "gemm_x3.hpp"
 #include "select.hpp"
 
 namespace dsvgd {
@@ -23,8 +24,8 @@ using GramTile = NTTile<2, 2, 2, 2>;  // 128 x 128 block, 4 waves of 64 x 64
 // pads +inf) into the panel layout, the mirror tile for SYM off-diagonal
 // tiles, and the select accounting (weight 2 for mirrored tiles).
 // snorm: [0,128) the tile's row norms, [128,256) its column norms.
-template <bool SYM, int smode, bool ZERO = false>
-__device__ __forceinline__ void sq_epilogue(GramTile& tile, int bi, int bj, int64_t row0,
+template <bool SYM, int smode, bool ZERO = false, class Tile = GramTile>
+__device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t row0,
                                             int64_t m, int64_t n, int64_t n_pad,
                                             float* __restrict__ D, const float* snorm,
                                             WindowHist& wh, uint32_t* shist, SlotWriter& sw,
@@ -257,6 +258,126 @@ __global__ __launch_bounds__(256, 2) void sqdist_persistent_kernel(
   }
 }
 
+// The persistent distance kernel on the split engine (gemm_x3.hpp): the
+// Gram from the row image Yg = dsvgd_rowsplit(Y[:, :dp]) (n_pad image rows),
+// fp32-accurate, K-steps of 16 through a 2-stage LDS-DMA ring that runs
+// across tile boundaries (the next tile's first K-step lands during this
+// tile's last one).  Tile order, epilogue and select accounting as
+// sqdist_persistent_kernel.
+using GramX3Tile = NTX3Tile<2, 2, 2, 2, 2>;
+
+template <bool SYM, int smode>
+__global__ __launch_bounds__(256, 2) void sqdist_x3_kernel(
+    const __bf16* __restrict__ Yg, const float* __restrict__ norms, int64_t row0, int64_t m,
+    int64_t n, int64_t n_pad, int nk, float* __restrict__ D, dsvgd_select_state* __restrict__ st,
+    float* __restrict__ cand, int epi, int64_t total) {
+  __shared__ __attribute__((aligned(16))) char smem[GramX3Tile::kSmemBytes];
+  __shared__ uint32_t shist[DSVGD_RADIX_BINS];
+  __shared__ float snorm[GramX3Tile::BM + GramX3Tile::BN];
+
+  const int Tm = (int)(roundup128(m) / 128), Tn = (int)(n_pad / 128);
+  const int t = threadIdx.x, w = t >> 6, wm = w >> 1, wn = w & 1;
+  const int64_t x = blockIdx.x % kXcds, u = blockIdx.x / kXcds, U = gridDim.x / kXcds;
+  const int64_t q = total / kXcds, rr = total % kXcds;
+  const int64_t lo = x * q + min(x, rr);
+  const int64_t hi = (int64_t)__builtin_amdgcn_readfirstlane((int)(lo + q + (x < rr ? 1 : 0)));
+  SlotLayout sl(cand, total * 4, smode == kSelBracket ? st->cand_cap : 0);
+  if (smode == kSelBracket) sl.publish(st, blockIdx.x);
+  if (smode == kSelHist)
+    for (int b = t; b < DSVGD_RADIX_BINS; b += 256) shist[b] = 0u;
+
+  auto next_valid = [&](int64_t L, int& bi, int& bj) -> int64_t {
+    for (; L < hi; L += U) {
+      if (tile_at(L, Tm, Tn, SYM, bi, bj)) {
+        bi = __builtin_amdgcn_readfirstlane(bi);
+        bj = __builtin_amdgcn_readfirstlane(bj);
+        return L;
+      }
+      if (smode == kSelBracket) slot_clear(sl, L * 4 + w);
+    }
+    return L;
+  };
+  // K-step (tile (bi, bj), ks) -> LDS stage st
+  GramX3Tile tile;
+  auto issue = [&](char* stg, int bi, int bj, int ks) {
+    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Yg + (row0 + (int64_t)bi * 128) * 16), (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Yg + (int64_t)bj * 128 * 16), (short)0, 0x7fffffff, 0x00020000);
+    tile.dma(stg, rA, n_pad, rB, n_pad, ks);
+  };
+
+  int bi = 0, bj = 0;
+  int64_t L = next_valid((int64_t)__builtin_amdgcn_readfirstlane((int)(lo + u)), bi, bj);
+  tile.zero();
+  if (L < hi) issue(smem, bi, bj, 0);
+  GramX3Tile::ring_barrier<0>();
+  int ks = 0, stage = 0;
+  int bin = bi, bjn = bj;  // the tile of the next K-step
+  int64_t Ln = L;
+  while (L < hi) {
+    // position of the next K-step: this tile's ks + 1, or the next tile's 0
+    int ksn = ks + 1;
+    if (ksn == nk) {
+      Ln = next_valid(L + U, bin, bjn);
+      ksn = 0;
+    }
+    const bool more = Ln < hi;
+    if (more) issue(smem + (stage ^ 1) * GramX3Tile::kStage, bin, bjn, ksn);
+    tile.compute(smem + stage * GramX3Tile::kStage, wm, wn, (int)(row0 & 15));
+    GramX3Tile::ring_barrier<0>();
+    if (ks + 1 == nk) {  // tile done: norms, epilogue (re-zeroes the accumulators)
+      snorm[t] = t < 128 ? norms[row0 + (int64_t)bi * 128 + t] : norms[(int64_t)bj * 128 + t - 128];
+      __syncthreads();
+      const int64_t slot = L * 4 + w;
+      WindowHist wh;
+      SlotWriter sw;
+      if (smode == kSelBracket) sw.begin(st, sl, slot);
+      if (epi == 3)
+        tile.zero();
+      else
+        sq_epilogue<SYM, smode, true>(tile, bi, bj, row0, m, n, n_pad, D, snorm, wh, shist, sw, sl,
+                                      slot, epi);
+      if (smode == kSelHist) wh.flush(shist);
+      L = Ln;
+      bi = bin;
+      bj = bjn;
+    }
+    ks = ksn;
+    stage ^= 1;
+  }
+  if (smode == kSelHist) {
+    __syncthreads();
+    flush_block_hist(shist, st);
+  }
+}
+
+template <int SM>
+int launch_sqdist_x3(const __bf16* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
+                     int64_t d, float* D, dsvgd_select_state* st, float* cand, hipStream_t s) {
+  const int64_t dp = roundup(d, 32), m_pad = roundup(m, 128), n_pad = roundup(n, 128);
+  const char* ep = getenv("DSVGD_SQ_EPI");
+  const int epi = ep ? atoi(ep) : 0;
+  const bool sym = m == n && row0 == 0;
+  const int64_t T = n_pad / 128;
+  const int64_t total = sym ? tile_grid(T, T, true) : tile_grid(m_pad / 128, T, false);
+  int blocks = 0;
+  int rc = sym ? persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3_kernel<true, SM>),
+                                   &blocks)
+               : persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3_kernel<false, SM>),
+                                   &blocks);
+  if (rc) return rc;
+  const dim3 grid((unsigned)blocks);
+  const int nk = (int)(dp / kX3Step);
+  if (sym)
+    hipLaunchKernelGGL((sqdist_x3_kernel<true, SM>), grid, dim3(256), 0, s, Yg, norms, row0, m, n,
+                       n_pad, nk, D, st, cand, epi, total);
+  else
+    hipLaunchKernelGGL((sqdist_x3_kernel<false, SM>), grid, dim3(256), 0, s, Yg, norms, row0, m, n,
+                       n_pad, nk, D, st, cand, epi, total);
+  return check_launch("sqdist_x3");
+}
+
 // d <= 2 (supports up to 64): D_ij = sum_c (y_ic - y_jc)^2 from explicit differences on the VALU
 // (what torch.dist(x, y)**2 computes per pair at experiments/logreg.py:61):
 // no ||x||^2 - 2x.y cancellation, which at small d and a narrow median
@@ -420,6 +541,28 @@ int dsvgd_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0, 
     case kSelNone: return launch_sqdist<kSelNone>(Y, ldy, norms, row0, m, n, d, D, st, cand, s);
     case kSelHist: return launch_sqdist<kSelHist>(Y, ldy, norms, row0, m, n, d, D, st, cand, s);
     default: return launch_sqdist<kSelBracket>(Y, ldy, norms, row0, m, n, d, D, st, cand, s);
+  }
+}
+
+int dsvgd_sqdist_x3(const void* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
+                    int64_t d, float* D, int64_t ldd, int select_mode, dsvgd_select_state* st,
+                    float* cand, void* stream) {
+  DSVGD_REQUIRE(Yg && norms && D, "null pointer");
+  DSVGD_REQUIRE(m > 0 && n > 0 && row0 >= 0 && row0 + m <= n && d > 0, "sizes");
+  DSVGD_REQUIRE(select_mode >= 0 && select_mode <= 2, "select_mode must be 0, 1 or 2");
+  DSVGD_REQUIRE(select_mode == 0 || st, "select mode needs a state");
+  DSVGD_REQUIRE(select_mode != 2 || cand, "bracket mode needs a candidate buffer");
+  const int64_t m_pad = roundup(m, 128), n_pad = roundup(n, 128), dp = roundup(d, 32);
+  DSVGD_REQUIRE(ldd == n_pad, "ldd must equal roundup(n,128) (panel layout)");
+  DSVGD_REQUIRE(((uintptr_t)Yg & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
+  DSVGD_REQUIRE(m_pad / 128 <= 65535, "too many row tiles");
+  DSVGD_REQUIRE(dp * n_pad * 6 < ((int64_t)1 << 31), "image too large for 32-bit buffer offsets");
+  const __bf16* yg = (const __bf16*)Yg;
+  hipStream_t s = (hipStream_t)stream;
+  switch (select_mode) {
+    case kSelNone: return launch_sqdist_x3<kSelNone>(yg, norms, row0, m, n, d, D, st, cand, s);
+    case kSelHist: return launch_sqdist_x3<kSelHist>(yg, norms, row0, m, n, d, D, st, cand, s);
+    default: return launch_sqdist_x3<kSelBracket>(yg, norms, row0, m, n, d, D, st, cand, s);
   }
 }
 

@@ -43,6 +43,7 @@ SIGNATURES = {
     "dsvgd_ysplit": (_int, [_p, _i64, _i64, _p, _p]),
     "dsvgd_rowsplit_bytes": (_i64, [_i64, _i64]),
     "dsvgd_rowsplit": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _p, _p]),
+    "dsvgd_sqdist_x3": (_int, [_p, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p]),
     "dsvgd_phi_mm_x3": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p]),
     "dsvgd_phi_finish": (_int, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _f,
                                 _f, _p, _i64, _p, _i64, _p, _i64, _p]),

@@ -165,6 +165,12 @@ class PhiEngine(object):
         if self.x3:
             nb = lib.dsvgd_ysplit_bytes(self.n_pad, self.ldy)
             self.Yx = torch.empty(nb // 2, dtype=torch.int16, device=dev)
+        # distance Gram (d > DIRECT_MAX_D): split engine unless DSVGD_GRAM_GEMM=f32
+        self.x3_gram = (os.environ.get("DSVGD_GRAM_GEMM", "x3") == "x3"
+                        and self.dp * self.n_pad * 6 < (1 << 31))
+        if self.x3_gram:
+            nb = lib.dsvgd_rowsplit_bytes(self.n_pad, self.dp)
+            self.Yg = torch.empty(nb // 2, dtype=torch.int16, device=dev)
         self.KY = torch.empty(self.splits * m, self.ldy, **f32)
         self.rowsum = torch.empty(self.splits * self.m_pad, **f32)
         self.mean = torch.empty(d, **f32)
@@ -224,6 +230,14 @@ class PhiEngine(object):
         elif median:
             N.call("dsvgd_select_init", self.state.ptr, self.n, -1, s)
             st, mode = self.state.ptr, SEL_HIST
+        if self.x3_gram and self.d > self.DIRECT_MAX_D:
+            with span(self.timer, "rowsplit"):
+                N.call("dsvgd_rowsplit", N.ptr(self.Y), self.ldy, self.n_pad, self.dp, self.n_pad,
+                       self.dp, N.ptr(self.Yg), s)
+            with span(self.timer, "sqdist"):
+                N.call("dsvgd_sqdist_x3", N.ptr(self.Yg), N.ptr(self.norms), self.row0, self.m,
+                       self.n, self.d, N.ptr(self.D), self.n_pad, mode, st, cand, s)
+            return
         with span(self.timer, "sqdist"):
             N.call("dsvgd_sqdist", N.ptr(self.Y), self.ldy, N.ptr(self.norms), self.row0, self.m,
                    self.n, self.d, N.ptr(self.D), self.n_pad, mode, st, cand, s)

@@ -157,6 +157,14 @@ int dsvgd_bracket_check(dsvgd_select_state* st, void* stream);
 /* fixed-bandwidth mode: st->h = h, st->inv_h = 1/h */
 int dsvgd_set_bandwidth(dsvgd_select_state* st, float h, void* stream);
 
+/* dsvgd_sqdist's Gram path (d > 2) on the split engine (fp32-accurate, see
+ * dsvgd_phi_mm_x3): Yg = dsvgd_rowsplit(Y, ldy, n_pad, dp, n_pad, dp) with
+ * dp = roundup(d, 32), n_pad = roundup(n, 128); same outputs, layouts and
+ * select modes as dsvgd_sqdist.  Requires dp * n_pad * 6 < 2^31. */
+int dsvgd_sqdist_x3(const void* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
+                    int64_t d, float* D, int64_t ldd, int select_mode, dsvgd_select_state* st,
+                    float* cand, void* stream);
+
 /* ---- phi: K.[Xc | S] on MFMA with the fused RBF exp -------------------- */
 /* KY_z[i][:] = sum_{j in slice z, j != row0+i} exp(-D[i][j]/h) Y[j][:] and
  * rowsum_z[i] = the same sum of exp(-D[i][j]/h), for split-K slices z < splits

@@ -68,6 +68,11 @@ def main():
     out = {k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v)),
                "tflops": flops / (np.median(v) * 1e-3) / 1e12} for k, v in res.items()}
     out["sqdist_ms"] = timed(lambda: eng.distances(median=False))
+    if getattr(eng, "x3_gram", False):
+        eng.x3_gram = False
+        out["sqdist_f32_ms"] = timed(lambda: eng.distances(median=False))
+        out["sqdist_bracket_f32_ms"] = timed(lambda: eng.distances(median=True))
+        eng.x3_gram = True
     for k, v in json.loads(os.environ.get("AB_SQ_VARIANTS", "{}")).items():
         os.environ.update(v)
         out["sqdist_ms[%s]" % k] = timed(lambda: eng.distances(median=False))

@@ -158,3 +158,39 @@ def test_logreg_scores_x3_as_accurate_as_f32(monkeypatch, n, N, p):
         err[gemm] = float(np.abs(out.cpu().numpy() - ref).max() / np.abs(ref).max())
     record_parity(err["x3"])
     assert err["x3"] <= 2.0 * err["f32"] + 1e-7 and err["x3"] < 1e-5, err
+
+
+@pytest.mark.parametrize("n,d,m,row0", [(700, 48, None, 0), (5000, 64, None, 0),
+                                        (3000, 130, 1000, 1500), (513, 3, None, 0)])
+def test_sqdist_x3_as_accurate_as_f32(monkeypatch, n, d, m, row0):
+    """Distances through the split Gram (dsvgd_sqdist_x3) against fp64, next
+    to the f32 Gram on the same particles: symmetric, bracketed (n = 5000:
+    n^2 >= 2^24) and row-block launches; the median select stays bit-exact
+    on the kernel's own D."""
+    rs = np.random.RandomState(n + d)
+    X = (rs.randn(n, d) * 1.5 + 3.0).astype(np.float32)
+    Xc = X.astype(np.float64) - X.astype(np.float64).mean(0)
+    mm = n if m is None else m
+    ref = ((Xc[row0:row0 + mm, None, :] - Xc[None, :, :]) ** 2).sum(-1) if n * mm <= 4e6 else None
+    nrm = (Xc ** 2).sum(1)
+    err, med = {}, {}
+    for gemm in ("f32", "x3"):
+        monkeypatch.setenv("DSVGD_GRAM_GEMM", gemm)
+        eng = dsvgd().PhiEngine(n, d, m=m, row0=row0, device=DEV)
+        assert eng.x3_gram == (gemm == "x3")
+        eng.pack(gpu(X))
+        eng.distances(median=True)
+        eng.median_bandwidth()
+        Dm = eng.dense_D().cpu().numpy().astype(np.float64)
+        k = (n * mm - 1) // 2
+        med[gemm] = eng.state.read()[0]
+        if m is None:
+            assert np.float32(med[gemm]).view(np.uint32) == \
+                np.float32(np.partition(Dm.ravel(), k)[k]).view(np.uint32)
+            assert np.all(np.diag(Dm) == 0.0)
+        if ref is not None:
+            scale = nrm[row0:row0 + mm, None] + nrm[None, :] + 1e-30
+            err[gemm] = float(np.max(np.abs(Dm - ref) / scale))
+    if ref is not None:
+        record_parity(err["x3"])
+        assert err["x3"] <= 2.0 * err["f32"] + 1e-7 and err["x3"] < 2e-6, err
