@@ -188,7 +188,40 @@ struct NNX3Tile {
   // where the same thread reads them (no barrier needed, only its vmcnt)
   __device__ __forceinline__ void dma_d(char* raw, __amdgpu_buffer_rsrc_t rA, int64_t j0) {
     const int t = threadIdx.x;
+    if (transposed(j0)) {
+      // symmetric layout, K-step in a column tile J < I: D[i][j0 + jj] is
+      // stored as tile (J, I); its rows j0..j0+15 of the 8 panels covering
+      // columns I*128.. are 8 contiguous 1-KiB pieces, one per wave:
+      // raw[w][jj][ii] = D[I*128 + 16w + ii][j0 + jj]
+      const float* src = sym_D + (((j0 >> 7) * sym_pcols + sym_I * 8) * kPanelElems +
+                                   (j0 & 127) * 16);
+      const __amdgpu_buffer_rsrc_t rT =
+          __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, 0x7fffffff, 0x00020000);
+      dma16(rT, raw + (t & ~63) * 16, (t >> 6) * kPanelElems * 4 + (t & 63) * 16, 0);
+      return;
+    }
     dma16(rA, raw + (t & ~63) * 16, t * 16, (int)((j0 >> 4) * kPanelElems * 4));
+  }
+
+  // this thread's 4 D values (row t >> 2, columns 4 (t & 3) ..) of K-step j0
+  // from its raw slot
+  __device__ __forceinline__ f32x4 raw_read(const char* raw, int64_t j0) const {
+    const int t = threadIdx.x;
+    if (transposed(j0)) {
+      const int row = t >> 2, c4 = t & 3;
+      const float* r = reinterpret_cast<const float*>(raw) + (row >> 4) * 256 + (row & 15);
+      return f32x4{r[(4 * c4) * 16], r[(4 * c4 + 1) * 16], r[(4 * c4 + 2) * 16],
+                   r[(4 * c4 + 3) * 16]};
+    }
+    return *reinterpret_cast<const f32x4*>(raw + t * 16);
+  }
+
+  // symmetric layout (dsvgd_sqdist_x3 layout 1): only tiles (I, J >= I) exist
+  const float* sym_D = nullptr;  // whole panel-layout D, or null (full layout)
+  int64_t sym_pcols = 0;         // n_pad / 16
+  int64_t sym_I = 0;             // this block's row tile
+  __device__ __forceinline__ bool transposed(int64_t j0) const {
+    return sym_D != nullptr && (j0 >> 7) < sym_I;
   }
 
   __device__ __forceinline__ void read_a(const char* st, int wr) {
@@ -258,7 +291,7 @@ struct NNX3Tile {
       dma_d(raw, rA, k0);
       if (k0 + BJ < k1) dma_d(raw + kPanelElems * 4, rA, k0 + BJ);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      ra = *reinterpret_cast<const f32x4*>(raw + threadIdx.x * 16);
+      ra = raw_read(raw, k0);
       store_a(smem, scale, row_g0 - k0);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       for (int64_t j0 = k0; j0 < k1; j0 += 2 * BJ) {
@@ -312,7 +345,7 @@ struct NNX3Tile {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB + 1) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB) : "memory");
-      ra = *reinterpret_cast<const f32x4*>(raw + (CUR ^ 1) * kPanelElems * 4 + threadIdx.x * 16);
+      ra = raw_read(raw + (CUR ^ 1) * kPanelElems * 4, j0 + BJ);
       store_a(smem + (CUR ^ 1) * kStage, scale, row_g0 - (j0 + BJ));
     }
     compute<kHalf, TN>(cur, wc);

@@ -21,7 +21,7 @@ int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, i
             int64_t m, int64_t row0, hipStream_t s);
 int nn_x3_gemm(bool exp_, const float* A, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
                const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-               int64_t row0, hipStream_t s);
+               int64_t row0, hipStream_t s, int sym = 0);
 
 static int64_t nn_cols(int64_t w) {
   if (w <= 128) return 128;

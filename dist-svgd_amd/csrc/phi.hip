@@ -79,7 +79,7 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
                                                     const dsvgd_select_state* __restrict__ st,
                                                     float* __restrict__ C, int64_t ldc,
                                                     float* __restrict__ rowsum, int64_t m,
-                                                    int64_t row0) {
+                                                    int64_t row0, int sym) {
   using Tile = NNX3Tile<TN, DMA, EXP>;
   __shared__ __attribute__((aligned(16))) char smem[Tile::kSmemBytes];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
@@ -90,6 +90,11 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
   if (EXP) rowsum += (int64_t)blockIdx.z * roundup128(m);
   const float scale = EXP ? -st->inv_h * kLog2e : 0.f;
   Tile tile;
+  if (DMA && sym) {  // symmetric layout: m == n, row0 == 0 (checked by the ABI)
+    tile.sym_D = A;
+    tile.sym_pcols = a_npad >> 4;
+    tile.sym_I = i0 >> 7;
+  }
   tile.run(A + (i0 >> 7) * (a_npad >> 4) * kPanelElems, Yx + c0 * 16, ldy, k0, k1, scale, smem,
            row0 + i0);
 
@@ -168,17 +173,19 @@ __global__ __launch_bounds__(256) void ysplit_kernel(const float* __restrict__ Y
 template <int TN, bool EXP>
 int launch_nn_x3(const float* D, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
                  const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-                 int64_t row0, hipStream_t s) {
+                 int64_t row0, int sym, hipStream_t s) {
+  if (sym && TN == 1) return fail_arg("nn_x3: the symmetric layout needs ldy % 256 == 0");
   const int64_t kchunk = roundup((K + splits - 1) / splits, kX3Step);
   const dim3 grid(ldy / (128 * TN), roundup(m, 128) / 128, splits);
   // DSVGD_X3_DMA=0: Yx staged through VGPRs + ds_write (A/B switch)
   const char* e = getenv("DSVGD_X3_DMA");
+  if (sym && e && e[0] == '0') return fail_arg("nn_x3: the symmetric layout needs the DMA path");
   if ((e && e[0] == '0') || TN == 1)  // TN = 1: 1.5 DMA rounds per K-step
     hipLaunchKernelGGL((nn_x3_kernel<TN, false, EXP>), grid, dim3(512), 0, s, D, K, Yx, ldy, K,
-                       kchunk, st, C, ldc, rowsum, m, row0);
+                       kchunk, st, C, ldc, rowsum, m, row0, 0);
   else
     hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP>), grid, dim3(512), 0, s, D, K, Yx, ldy, K,
-                       kchunk, st, C, ldc, rowsum, m, row0);
+                       kchunk, st, C, ldc, rowsum, m, row0, sym);
   return check_launch("nn_x3_kernel");
 }
 
@@ -186,13 +193,14 @@ int launch_nn_x3(const float* D, int64_t K, const __bf16* Yx, int64_t ldy, int s
 // (K rows, ldy columns, a multiple of 128).  exp_: the phi_mm form.
 int nn_x3_gemm(bool exp_, const float* A, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
                const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-               int64_t row0, hipStream_t s) {
+               int64_t row0, hipStream_t s, int sym) {
   if (K * ldy * 6 >= ((int64_t)1 << 31) || K * 128 * 4 >= ((int64_t)1 << 31))
     return fail_arg("nn_x3: K x ldy too large for 32-bit buffer offsets");
   if (ldy % 128 != 0) return fail_arg("nn_x3: ldy must be a multiple of 128");
 #define DSVGD_X3_TN(TN)                                                                        \
-  return exp_ ? launch_nn_x3<TN, true>(A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0, s)  \
-              : launch_nn_x3<TN, false>(A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0, s)
+  return exp_ ? launch_nn_x3<TN, true>(A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0, sym,  \
+                                       s)                                                      \
+              : launch_nn_x3<TN, false>(A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0, 0, s)
   if (ldy % 512 == 0) DSVGD_X3_TN(4);
   if (ldy % 256 == 0) DSVGD_X3_TN(2);
   DSVGD_X3_TN(1);
@@ -555,7 +563,7 @@ int dsvgd_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int6
 
 int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, int64_t row0,
                     int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
-                    int64_t ldk, float* rowsum, void* stream) {
+                    int64_t ldk, float* rowsum, int sym, void* stream) {
   DSVGD_REQUIRE(D && Yx && st && KY && rowsum, "null pointer");
   DSVGD_REQUIRE(m > 0 && n > 0, "sizes");
   const int64_t n_pad = roundup(n, 128);
@@ -569,8 +577,9 @@ int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, in
   // and into Yx (K rows x 3 parts x ldy x 2 B)
   DSVGD_REQUIRE(n_pad * ldy * 6 < ((int64_t)1 << 31) && n_pad * 128 * 4 < ((int64_t)1 << 31),
                 "n x ldy too large for 32-bit buffer offsets (use dsvgd_phi_mm)");
+  DSVGD_REQUIRE(!sym || (m == n && row0 == 0), "sym: the symmetric layout needs m == n, row0 == 0");
   return nn_x3_gemm(true, D, n_pad, (const __bf16*)Yx, ldy, (int)splits, st, KY, ldk, rowsum, m,
-                    row0, (hipStream_t)stream);
+                    row0, (hipStream_t)stream, sym);
 }
 
 int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t splits,

@@ -10,6 +10,7 @@
 // (~1 % of D).  The choice is made on device (st->fallback).
 #include <cmath>
 
+#include "gemm_tiles.hpp"
 #include "select.hpp"
 
 namespace dsvgd {
@@ -35,9 +36,13 @@ __device__ __forceinline__ void hist_key(uint32_t key, uint32_t want, uint32_t s
 
 // count: entries of D (any order); cand: optional candidate buffer used
 // instead of D when st->fallback == 0 (bracketed mode).
+// sym_npad > 0: D is a symmetric n_pad x n_pad matrix stored as its
+// upper-triangle 128 x 128 tiles only (panel layout; dsvgd_sqdist_x3 with
+// layout 1): a panel of tile (I, J) counts 0x (J < I), 1x (J == I), 2x (J > I).
 __global__ __launch_bounds__(256) void radix_hist_kernel(const float* __restrict__ D, int64_t count,
                                                          const float* __restrict__ cand, int pass,
-                                                         dsvgd_select_state* __restrict__ st) {
+                                                         dsvgd_select_state* __restrict__ st,
+                                                         int64_t sym_npad) {
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
   for (int b = threadIdx.x; b < DSVGD_RADIX_BINS; b += 256) shist[b] = 0u;
   uint32_t shift, mask, hishift;
@@ -60,6 +65,21 @@ __global__ __launch_bounds__(256) void radix_hist_kernel(const float* __restrict
       const int64_t nc = min((int64_t)(c & ~DSVGD_SLOT_WEIGHT2), cap);
       for (int64_t q = lane; q < nc; q += 64)
         hist_key(__float_as_uint(data[sl * cap + q]), want, shift, mask, hishift, shist, w);
+    }
+  } else if (sym_npad > 0) {  // panel by panel (2048 floats = 2 float4 per thread)
+    const int64_t pcols = sym_npad >> 4, npanels = count / kPanelElems;
+    const f32x4* D4 = reinterpret_cast<const f32x4*>(D);
+    for (int64_t pnl = blockIdx.x; pnl < npanels; pnl += gridDim.x) {
+      const int64_t I = pnl / pcols, J = (pnl % pcols) >> 3;
+      if (J < I) continue;  // block-uniform
+      const uint32_t w = J == I ? 1u : 2u;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 v = D4[pnl * (kPanelElems / 4) + h * 256 + threadIdx.x];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          hist_key(__float_as_uint(v[e]), want, shift, mask, hishift, shist, w);
+      }
     }
   } else {
     const int64_t c4 = count >> 2;
@@ -277,15 +297,17 @@ int dsvgd_select_init(dsvgd_select_state* st, int64_t n_total, int64_t k_rank, v
 }
 
 int dsvgd_radix_hist(const float* D, int64_t count, const float* cand, int pass,
-                     dsvgd_select_state* st, void* stream) {
+                     dsvgd_select_state* st, int64_t sym_npad, void* stream) {
   DSVGD_REQUIRE(D && st, "null pointer");
   DSVGD_REQUIRE(pass >= 1 && pass <= 3, "pass must be 1..3");
   DSVGD_REQUIRE(count >= 0 && ((uintptr_t)D & 15) == 0, "count / alignment");
+  DSVGD_REQUIRE(sym_npad == 0 || (sym_npad % 128 == 0 && count == sym_npad * sym_npad),
+                "sym_npad: count must be sym_npad^2 (a square panel-layout matrix)");
   int64_t blocks = (count / 4 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   if (cand && blocks < 1024) blocks = 1024;  // candidate slots: one wave each, grid-stride
   hipLaunchKernelGGL(radix_hist_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, D, count,
-                     cand, pass, st);
+                     cand, pass, st, sym_npad);
   return check_launch("radix_hist");
 }
 

@@ -29,7 +29,8 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
                                             int64_t m, int64_t n, int64_t n_pad,
                                             float* __restrict__ D, const float* snorm,
                                             WindowHist& wh, uint32_t* shist, SlotWriter& sw,
-                                            const SlotLayout& sl, int64_t slot, int epi) {
+                                            const SlotLayout& sl, int64_t slot, int epi,
+                                            bool mirror_store = true) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
   const bool mirror = SYM && bi != bj;
   const int64_t i0 = (int64_t)bi * GramTile::BM;  // within the owned block
@@ -76,7 +77,7 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         if (epi < 2 || v[r] != v[r]) dp0[(r & 3) * 16 + (r >> 2) * 128] = v[r];
-      if (mirror && (epi == 0 || v[0] != v[0])) {  // D[j][i]: 4 consecutive i per register quad -> 16-byte stores
+      if (mirror && mirror_store && (epi == 0 || v[0] != v[0])) {  // D[j][i]: 4 consecutive i per register quad -> 16-byte stores
         float* const mp0 = Dmir + (int64_t)cl * 16 + (wm * 4 + mi * 2) * kPanelElems + h4;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -270,7 +271,7 @@ template <bool SYM, int smode>
 __global__ __launch_bounds__(256, 2) void sqdist_x3_kernel(
     const __bf16* __restrict__ Yg, const float* __restrict__ norms, int64_t row0, int64_t m,
     int64_t n, int64_t n_pad, int nk, float* __restrict__ D, dsvgd_select_state* __restrict__ st,
-    float* __restrict__ cand, int epi, int64_t total) {
+    float* __restrict__ cand, int epi, int64_t total, int layout) {
   __shared__ __attribute__((aligned(16))) char smem[GramX3Tile::kSmemBytes];
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
   __shared__ float snorm[GramX3Tile::BM + GramX3Tile::BN];
@@ -337,7 +338,7 @@ __global__ __launch_bounds__(256, 2) void sqdist_x3_kernel(
         tile.zero();
       else
         sq_epilogue<SYM, smode, true>(tile, bi, bj, row0, m, n, n_pad, D, snorm, wh, shist, sw, sl,
-                                      slot, epi);
+                                      slot, epi, layout == 0);
       if (smode == kSelHist) wh.flush(shist);
       L = Ln;
       bi = bin;
@@ -354,7 +355,8 @@ __global__ __launch_bounds__(256, 2) void sqdist_x3_kernel(
 
 template <int SM>
 int launch_sqdist_x3(const __bf16* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
-                     int64_t d, float* D, dsvgd_select_state* st, float* cand, hipStream_t s) {
+                     int64_t d, float* D, dsvgd_select_state* st, float* cand, int layout,
+                     hipStream_t s) {
   const int64_t dp = roundup(d, 32), m_pad = roundup(m, 128), n_pad = roundup(n, 128);
   const char* ep = getenv("DSVGD_SQ_EPI");
   const int epi = ep ? atoi(ep) : 0;
@@ -371,10 +373,10 @@ int launch_sqdist_x3(const __bf16* Yg, const float* norms, int64_t row0, int64_t
   const int nk = (int)(dp / kX3Step);
   if (sym)
     hipLaunchKernelGGL((sqdist_x3_kernel<true, SM>), grid, dim3(256), 0, s, Yg, norms, row0, m, n,
-                       n_pad, nk, D, st, cand, epi, total);
+                       n_pad, nk, D, st, cand, epi, total, layout);
   else
     hipLaunchKernelGGL((sqdist_x3_kernel<false, SM>), grid, dim3(256), 0, s, Yg, norms, row0, m, n,
-                       n_pad, nk, D, st, cand, epi, total);
+                       n_pad, nk, D, st, cand, epi, total, 0);
   return check_launch("sqdist_x3");
 }
 
@@ -546,7 +548,7 @@ int dsvgd_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0, 
 
 int dsvgd_sqdist_x3(const void* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
                     int64_t d, float* D, int64_t ldd, int select_mode, dsvgd_select_state* st,
-                    float* cand, void* stream) {
+                    float* cand, int layout, void* stream) {
   DSVGD_REQUIRE(Yg && norms && D, "null pointer");
   DSVGD_REQUIRE(m > 0 && n > 0 && row0 >= 0 && row0 + m <= n && d > 0, "sizes");
   DSVGD_REQUIRE(select_mode >= 0 && select_mode <= 2, "select_mode must be 0, 1 or 2");
@@ -557,12 +559,14 @@ int dsvgd_sqdist_x3(const void* Yg, const float* norms, int64_t row0, int64_t m,
   DSVGD_REQUIRE(((uintptr_t)Yg & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
   DSVGD_REQUIRE(m_pad / 128 <= 65535, "too many row tiles");
   DSVGD_REQUIRE(dp * n_pad * 6 < ((int64_t)1 << 31), "image too large for 32-bit buffer offsets");
+  DSVGD_REQUIRE(layout == 0 || (layout == 1 && m == n && row0 == 0),
+                "layout 1 (symmetric) needs the whole matrix: m == n, row0 == 0");
   const __bf16* yg = (const __bf16*)Yg;
   hipStream_t s = (hipStream_t)stream;
   switch (select_mode) {
-    case kSelNone: return launch_sqdist_x3<kSelNone>(yg, norms, row0, m, n, d, D, st, cand, s);
-    case kSelHist: return launch_sqdist_x3<kSelHist>(yg, norms, row0, m, n, d, D, st, cand, s);
-    default: return launch_sqdist_x3<kSelBracket>(yg, norms, row0, m, n, d, D, st, cand, s);
+    case kSelNone: return launch_sqdist_x3<kSelNone>(yg, norms, row0, m, n, d, D, st, cand, layout, s);
+    case kSelHist: return launch_sqdist_x3<kSelHist>(yg, norms, row0, m, n, d, D, st, cand, layout, s);
+    default: return launch_sqdist_x3<kSelBracket>(yg, norms, row0, m, n, d, D, st, cand, layout, s);
   }
 }
 

@@ -30,7 +30,7 @@ SIGNATURES = {
     "dsvgd_pack": (_int, [_p, _i64, _p, _i64, _f, _p, _i64, _i64, _i64, _p, _i64, _p, _p]),
     "dsvgd_sqdist": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p]),
     "dsvgd_select_init": (_int, [_p, _i64, _i64, _p]),
-    "dsvgd_radix_hist": (_int, [_p, _i64, _p, _int, _p, _p]),
+    "dsvgd_radix_hist": (_int, [_p, _i64, _p, _int, _p, _i64, _p]),
     "dsvgd_radix_pick": (_int, [_p, _int, _p]),
     "dsvgd_sample_sqdist": (_int, [_p, _i64, _i64, _i64, _i64, _c.c_uint64, _p, _p]),
     "dsvgd_bracket_init": (_int, [_p, _i64, _p, _p, _i64, _p]),
@@ -43,8 +43,9 @@ SIGNATURES = {
     "dsvgd_ysplit": (_int, [_p, _i64, _i64, _p, _p]),
     "dsvgd_rowsplit_bytes": (_i64, [_i64, _i64]),
     "dsvgd_rowsplit": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _p, _p]),
-    "dsvgd_sqdist_x3": (_int, [_p, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p]),
-    "dsvgd_phi_mm_x3": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p]),
+    "dsvgd_sqdist_x3": (_int, [_p, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _int, _p]),
+    "dsvgd_phi_mm_x3": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _int,
+                                _p]),
     "dsvgd_phi_finish": (_int, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _f,
                                 _f, _p, _i64, _p, _i64, _p, _i64, _p]),
     "dsvgd_phi_direct": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _f, _f, _p,

@@ -236,7 +236,7 @@ class PhiEngine(object):
                        self.dp, N.ptr(self.Yg), s)
             with span(self.timer, "sqdist"):
                 N.call("dsvgd_sqdist_x3", N.ptr(self.Yg), N.ptr(self.norms), self.row0, self.m,
-                       self.n, self.d, N.ptr(self.D), self.n_pad, mode, st, cand, s)
+                       self.n, self.d, N.ptr(self.D), self.n_pad, mode, st, cand, int(self.sym), s)
             return
         with span(self.timer, "sqdist"):
             N.call("dsvgd_sqdist", N.ptr(self.Y), self.ldy, N.ptr(self.norms), self.row0, self.m,
@@ -248,7 +248,7 @@ class PhiEngine(object):
         for sub, k in ((self.st_lo, self.k_lo), (self.st_hi, self.k_hi)):
             N.call("dsvgd_select_init", sub.ptr, self.SAMPLE, k, s)
             for p in (1, 2, 3):
-                N.call("dsvgd_radix_hist", N.ptr(self.sample), self.SAMPLE, None, p, sub.ptr, s)
+                N.call("dsvgd_radix_hist", N.ptr(self.sample), self.SAMPLE, None, p, sub.ptr, 0, s)
                 N.call("dsvgd_radix_pick", sub.ptr, p, s)
         N.call("dsvgd_bracket_init", self.state.ptr, self.n, self.st_lo.ptr, self.st_hi.ptr,
                self.cand_cap, s)
@@ -268,7 +268,8 @@ class PhiEngine(object):
         for p in (1, 2, 3):
             if p > 1 or self.bracketed:
                 with span(self.timer, "radix_hist"):
-                    N.call("dsvgd_radix_hist", N.ptr(self.D), count, cand, p, self.state.ptr, s)
+                    N.call("dsvgd_radix_hist", N.ptr(self.D), count, cand, p, self.state.ptr,
+                           self.n_pad if self.sym else 0, s)
             if allreduce is not None:
                 with span(self.timer, "hist_allreduce"):
                     allreduce(self.state.hist)
@@ -282,6 +283,16 @@ class PhiEngine(object):
     # or more accurate there, scripts/precision_small_d.py).  Must match the
     # library's default (kDirectDefaultD in csrc/sqdist.hip).
     DIRECT_MAX_D = 2
+
+    @property
+    def sym(self):
+        """D is in the symmetric layout (upper-triangle tiles only, written by
+        dsvgd_sqdist_x3 layout 1 and read transposed by dsvgd_phi_mm_x3 and
+        dsvgd_radix_hist): the whole n x n matrix on the split engines, with
+        ldy % 256 == 0.  DSVGD_SYM_LAYOUT=0 keeps the full layout."""
+        return (self.m == self.n and self.row0 == 0 and self.d > self.DIRECT_MAX_D
+                and self.x3 and self.x3_gram and self.ldy % 256 == 0
+                and os.environ.get("DSVGD_SYM_LAYOUT", "1") != "0")
 
     def direction(self, X_own=None, step=0.0, write_phi=True, inv_n=None, extra=None):
         """phi for the owned rows (+ `extra`, e.g. the h * W2 gradient rows);
@@ -311,7 +322,7 @@ class PhiEngine(object):
             with span(self.timer, "phi_mm"):
                 N.call("dsvgd_phi_mm_x3", N.ptr(self.D), self.n_pad, N.ptr(self.Yx), self.ldy,
                        self.row0, self.m, self.n, self.state.ptr, self.splits, N.ptr(self.KY),
-                       self.ldy, N.ptr(self.rowsum), s)
+                       self.ldy, N.ptr(self.rowsum), int(self.sym), s)
         else:
             with span(self.timer, "phi_mm"):
                 N.call("dsvgd_phi_mm", N.ptr(self.D), self.n_pad, N.ptr(self.Y), self.ldy,
@@ -334,11 +345,29 @@ class PhiEngine(object):
             self.fixed_bandwidth(h)
         self.direction(X_own, step, write_phi, extra=extra)
 
-    def dense_D(self):
-        """D as a dense (m, n) tensor (tests/inspection; un-does the panel layout)."""
+    def dense_D(self, padded=False):
+        """D as a dense (m, n) tensor (tests/inspection; un-does the panel
+        layout, and in the symmetric layout fills the unwritten lower tiles
+        from the stored upper ones).  padded: the whole (m_pad, n_pad) buffer."""
         mp, np_ = self.m_pad, self.n_pad
         Dd = self.D.view(mp // 128, np_ // 16, 128, 16).permute(0, 2, 1, 3).reshape(mp, np_)
-        return Dd[:self.m, :self.n]
+        if self.sym:
+            Dd = Dd.clone()
+            for I in range(1, np_ // 128):
+                Dd[I * 128:(I + 1) * 128, :I * 128] = Dd[:I * 128, I * 128:(I + 1) * 128].t()
+        return Dd if padded else Dd[:self.m, :self.n]
+
+    def count_D(self, pred):
+        """Entries of the full n_pad x n_pad D matching pred (a tensor -> bool
+        tensor function), counted without densifying: in the symmetric layout
+        an off-diagonal stored tile stands for its transpose too."""
+        if not self.sym:
+            return int(pred(self.D).sum())
+        T = self.n_pad // 128
+        c = torch.stack([pred(self.D.view(T, T, 128 * 128)[I]).sum(-1) for I in range(T)])
+        w = torch.triu(torch.full((T, T), 2, dtype=c.dtype, device=c.device), 1)
+        w += torch.eye(T, dtype=c.dtype, device=c.device)
+        return int((c * w).sum())
 
 
 class StepGraph(object):

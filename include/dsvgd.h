@@ -133,9 +133,12 @@ int dsvgd_select_init(dsvgd_select_state* st, int64_t n_total, int64_t k_rank, v
 /* histogram of key digit `pass` (1: bits 31..21, 2: 20..10, 3: 9..0) of the
  * finite entries (pads +inf / NaN skipped) whose higher digits equal
  * st->prefix, over D[0:count) -- or, when cand != NULL and the bracket holds
- * (st->fallback == 0), over the local candidate slots instead. */
+ * (st->fallback == 0), over the local candidate slots instead.
+ * sym_npad > 0: D is the symmetric layout dsvgd_sqdist_x3 writes with
+ * layout = 1 (upper-triangle tiles only; count = sym_npad^2): off-diagonal
+ * tiles count twice, lower tiles are skipped. */
 int dsvgd_radix_hist(const float* D, int64_t count, const float* cand, int pass,
-                     dsvgd_select_state* st, void* stream);
+                     dsvgd_select_state* st, int64_t sym_npad, void* stream);
 /* pick the bin holding rank k, fix its digit, clear hist; after pass 3
  * writes median, h = median/log(n_total) (1 if median == 0 or n == 1), inv_h. */
 int dsvgd_radix_pick(dsvgd_select_state* st, int pass, void* stream);
@@ -159,11 +162,14 @@ int dsvgd_set_bandwidth(dsvgd_select_state* st, float h, void* stream);
 
 /* dsvgd_sqdist's Gram path (d > 2) on the split engine (fp32-accurate, see
  * dsvgd_phi_mm_x3): Yg = dsvgd_rowsplit(Y, ldy, n_pad, dp, n_pad, dp) with
- * dp = roundup(d, 32), n_pad = roundup(n, 128); same outputs, layouts and
- * select modes as dsvgd_sqdist.  Requires dp * n_pad * 6 < 2^31. */
+ * dp = roundup(d, 32), n_pad = roundup(n, 128); same outputs and select
+ * modes as dsvgd_sqdist.  layout 0: the full panel-layout D; layout 1 (m ==
+ * n, row0 == 0 only) the SYMMETRIC LAYOUT: tiles (I, J) with J < I are not
+ * written -- consumers read them transposed (dsvgd_phi_mm_x3 with sym = 1,
+ * dsvgd_radix_hist with sym_npad).  Requires dp * n_pad * 6 < 2^31. */
 int dsvgd_sqdist_x3(const void* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
                     int64_t d, float* D, int64_t ldd, int select_mode, dsvgd_select_state* st,
-                    float* cand, void* stream);
+                    float* cand, int layout, void* stream);
 
 /* ---- phi: K.[Xc | S] on MFMA with the fused RBF exp -------------------- */
 /* KY_z[i][:] = sum_{j in slice z, j != row0+i} exp(-D[i][j]/h) Y[j][:] and
@@ -186,6 +192,9 @@ int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64
  * result carries fp32 GEMM rounding, not bf16's.  Same arguments, outputs,
  * split-K slices and diagonal rule as dsvgd_phi_mm; Yx = dsvgd_ysplit(Y)
  * (rows >= roundup(n, 128)).  Requires roundup(n,128) * ldy * 6 < 2^31.
+ * sym = 1: D is dsvgd_sqdist_x3's symmetric layout (m == n, row0 == 0,
+ * ldy % 256 == 0); a K-step in a column tile J < I is read from the stored
+ * tile (J, I), transposed in LDS.
  * dsvgd_ysplit: Yx[kstep][part][column][16] (bf16) from the first `rows`
  * rows of Y (rows a multiple of 16; dsvgd_ysplit_bytes(rows, ldy) bytes,
  * 16-byte aligned); 16-byte halves swapped on columns with bit 3 set. */
@@ -201,7 +210,7 @@ int dsvgd_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int6
 int dsvgd_ysplit(const float* Y, int64_t ldy, int64_t rows, void* Yx, void* stream);
 int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, int64_t row0,
                     int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
-                    int64_t ldk, float* rowsum, void* stream);
+                    int64_t ldk, float* rowsum, int sym, void* stream);
 
 /* phi[i] = inv_n * (s_i + KS[i] + (2/h) (rowsum[i] xc[i] - KXc[i])) with the
  * split-K partials summed in slice order (s_i: the self term k_ii s_i), plus

@@ -58,6 +58,9 @@ def main():
                 os.environ.pop(k, None)
             os.environ.update(env)
             eng.x3 = env.get("ENGINE_X3", "1") == "1" and hasattr(eng, "Yx")
+            if env.get("RECOMPUTE_D") == "1":  # the variant changes D's layout
+                eng.distances(median=True)
+                eng.median_bandwidth()
             res[name].append(timed(lambda: eng.direction(write_phi=True)))
             if ref is None:
                 ref = eng.phi.clone()

@@ -161,7 +161,9 @@ def test_logreg_scores_x3_as_accurate_as_f32(monkeypatch, n, N, p):
 
 
 @pytest.mark.parametrize("n,d,m,row0", [(700, 48, None, 0), (5000, 64, None, 0),
-                                        (3000, 130, 1000, 1500), (513, 3, None, 0)])
+                                        (3000, 130, 1000, 1500), (513, 3, None, 0),
+                                        (1000, 100, None, 0), (1900, 256, None, 0),
+                                        (4500, 128, None, 0)])
 def test_sqdist_x3_as_accurate_as_f32(monkeypatch, n, d, m, row0):
     """Distances through the split Gram (dsvgd_sqdist_x3) against fp64, next
     to the f32 Gram on the same particles: symmetric, bracketed (n = 5000:
@@ -184,6 +186,11 @@ def test_sqdist_x3_as_accurate_as_f32(monkeypatch, n, d, m, row0):
         Dm = eng.dense_D().cpu().numpy().astype(np.float64)
         k = (n * mm - 1) // 2
         med[gemm] = eng.state.read()[0]
+        # symmetric layout exactly when the split engines take the whole matrix at ldy % 256 == 0
+        assert eng.sym == (gemm == "x3" and m is None and d > 2 and eng.ldy % 256 == 0)
+        if eng.sym:  # weighted counting over the stored tiles == counting the dense matrix
+            for v in (med[gemm], 0.5 * med[gemm]):
+                assert eng.count_D(lambda t: t < v) == int((eng.dense_D(padded=True) < v).sum())
         if m is None:
             assert np.float32(med[gemm]).view(np.uint32) == \
                 np.float32(np.partition(Dm.ravel(), k)[k]).view(np.uint32)
