@@ -22,6 +22,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PEAK_TF, PEAK_GBS = 157.3, 8000.0
+PEAK_X3_TF = 2516.6 / 6   # split engine: bf16 dense / six products per fp32 product
 
 
 def logreg_data(N, p, seed=0):
@@ -87,7 +88,9 @@ def run(name, steps):
         rates["sqdist_TFs_on_sym_flops"] = (n * n * eng.dp) / (st["sqdist"] * 1e-3) / 1e12
         rates["sqdist_GBs_written"] = 4.0 * m * n / (st["sqdist"] * 1e-3) / 1e9
         rates["phi_mm_TFs"] = 4.0 * m * n * d / (st["phi_mm"] * 1e-3) / 1e12
-        rates["phi_mm_frac_of_peak"] = rates["phi_mm_TFs"] / PEAK_TF
+        rates["phi_mm_frac_of_f32_peak"] = rates["phi_mm_TFs"] / PEAK_TF
+        if getattr(eng, "x3", False):
+            rates["phi_mm_frac_of_x3_peak"] = rates["phi_mm_TFs"] / PEAK_X3_TF
         rates["phi_mm_GBs_D_read"] = 4.0 * m * n / (st["phi_mm"] * 1e-3) / 1e9
     else:
         # distance pass: 4 B written per entry (the kernel's HBM traffic);
