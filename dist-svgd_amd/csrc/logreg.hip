@@ -21,7 +21,7 @@ int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, i
             int64_t m, int64_t row0, hipStream_t s);
 int nn_x3_gemm(bool exp_, const float* A, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
                const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-               int64_t row0, hipStream_t s, int sym = 0);
+               int64_t row0, hipStream_t s, int sym = 0, int m16 = 0);
 
 static int64_t nn_cols(int64_t w) {
   if (w <= 128) return 128;
@@ -363,7 +363,7 @@ int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const 
     __bf16* Xdy = (__bf16*)(base + w.off_xdy);
     if ((rc = dsvgd_rowsplit(X + 1, ldx, n, p, w.n_pad, w.pp, Wx, s))) return rc;
     if ((rc = dsvgd_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, Xdx, s))) return rc;
-    if ((rc = dsvgd_ysplit(Xdp, w.ldb, w.N_pad, Xdy, s))) return rc;
+    if ((rc = dsvgd_ysplit(Xdp, w.ldb, w.N_pad, Xdy, 1, s))) return rc;
     hipLaunchKernelGGL(logreg_z_x3_kernel, dim3(w.N_pad / ZX3Tile::BN, w.n_pad / ZX3Tile::BM),
                        dim3(256), 0, s, (const __bf16*)Wx, w.n_pad, (const __bf16*)Xdx, w.N_pad,
                        (int)(w.pp / kX3Step), tp, G);

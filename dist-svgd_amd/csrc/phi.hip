@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
 // phi_mm on the bf16 MFMA at fp32 accuracy (gemm_x3.hpp): the same blocks,
 // split-K slices, diagonal skip and row sums as nn_kernel<TN, true>; B is the
 // split image of Y (dsvgd_ysplit).
-template <int TN, bool DMA, bool EXP>
+template <int TN, bool DMA, bool EXP, bool M16>
 __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A, int64_t a_npad,
                                                     const __bf16* __restrict__ Yx, int64_t ldy,
                                                     int64_t K, int64_t kchunk,
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
                                                     float* __restrict__ C, int64_t ldc,
                                                     float* __restrict__ rowsum, int64_t m,
                                                     int64_t row0, int sym) {
-  using Tile = NNX3Tile<TN, DMA, EXP>;
+  using Tile = NNX3Tile<TN, DMA, EXP, M16>;
   __shared__ __attribute__((aligned(16))) char smem[Tile::kSmemBytes];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
@@ -100,17 +100,31 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
   const int64_t r0 = i0 + wr * 32 * Tile::TM;
+  if (M16) {  // 16x16 C layout: column lane & 15, rows 4 (lane >> 4) + reg
 #pragma unroll
-  for (int mi = 0; mi < Tile::TM; ++mi)
+    for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-    for (int ni = 0; ni < TN; ++ni) {
-      const int64_t col = c0 + wc * 32 * TN + ni * 32 + (lane & 31);
+      for (int nt = 0; nt < 2 * TN; ++nt) {
+        const int64_t col = c0 + wc * 32 * TN + nt * 16 + (lane & 15);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = r0 + mi * 32 + c_row(r, lane);
-        if (row < m) C[row * ldc + col] = tile.acc[mi][ni][r];
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = r0 + mt * 16 + 4 * (lane >> 4) + r;
+          if (row < m) C[row * ldc + col] = tile.acc16[mt][nt][r];
+        }
       }
-    }
+  } else {
+#pragma unroll
+    for (int mi = 0; mi < Tile::TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int64_t col = c0 + wc * 32 * TN + ni * 32 + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t row = r0 + mi * 32 + c_row(r, lane);
+          if (row < m) C[row * ldc + col] = tile.acc[mi][ni][r];
+        }
+      }
+  }
   if (EXP && blockIdx.x == 0) {
     const float v = tile.row_sum();
     const int64_t row = i0 + (threadIdx.x >> 2);
@@ -149,7 +163,8 @@ __global__ __launch_bounds__(256) void rowsplit_kernel(const float* __restrict__
 // Yx[kstep][part][column][16 k] = the three bf16 parts of Y[16 kstep + k][column]
 // (gemm_x3.hpp image: 16-B halves swapped on columns with bit 3 set).
 __global__ __launch_bounds__(256) void ysplit_kernel(const float* __restrict__ Y, int64_t ldy,
-                                                     int64_t ksteps, __bf16* __restrict__ Yx) {
+                                                     int64_t ksteps, __bf16* __restrict__ Yx,
+                                                     int swz) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= ksteps * ldy) return;
   const int64_t kb = t / ldy, c = t % ldy;
@@ -161,7 +176,7 @@ __global__ __launch_bounds__(256) void ysplit_kernel(const float* __restrict__ Y
     s[1][k >> 3][k & 7] = v.s1;
     s[2][k >> 3][k & 7] = v.s2;
   }
-  const int sw = (int)((c >> 3) & 1);
+  const int sw = swz ? (int)((c >> 3) & 1) : 0;
 #pragma unroll
   for (int p = 0; p < kX3Parts; ++p) {
     __bf16* dst = Yx + ((kb * kX3Parts + p) * ldy + c) * 16;
@@ -173,19 +188,24 @@ __global__ __launch_bounds__(256) void ysplit_kernel(const float* __restrict__ Y
 template <int TN, bool EXP>
 int launch_nn_x3(const float* D, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
                  const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-                 int64_t row0, int sym, hipStream_t s) {
+                 int64_t row0, int sym, int m16, hipStream_t s) {
   if (sym && TN == 1) return fail_arg("nn_x3: the symmetric layout needs ldy % 256 == 0");
   const int64_t kchunk = roundup((K + splits - 1) / splits, kX3Step);
   const dim3 grid(ldy / (128 * TN), roundup(m, 128) / 128, splits);
   // DSVGD_X3_DMA=0: Yx staged through VGPRs + ds_write (A/B switch)
   const char* e = getenv("DSVGD_X3_DMA");
   if (sym && e && e[0] == '0') return fail_arg("nn_x3: the symmetric layout needs the DMA path");
+  if (m16 && ((e && e[0] == '0') || TN == 1))
+    return fail_arg("nn_x3: the 16x16 form needs the DMA path (ldy % 256 == 0)");
   if ((e && e[0] == '0') || TN == 1)  // TN = 1: 1.5 DMA rounds per K-step
-    hipLaunchKernelGGL((nn_x3_kernel<TN, false, EXP>), grid, dim3(512), 0, s, D, K, Yx, ldy, K,
-                       kchunk, st, C, ldc, rowsum, m, row0, 0);
+    hipLaunchKernelGGL((nn_x3_kernel<TN, false, EXP, false>), grid, dim3(512), 0, s, D, K, Yx, ldy,
+                       K, kchunk, st, C, ldc, rowsum, m, row0, 0);
+  else if (m16)
+    hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, TN != 1>), grid, dim3(512), 0, s, D, K, Yx,
+                       ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym);
   else
-    hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP>), grid, dim3(512), 0, s, D, K, Yx, ldy, K,
-                       kchunk, st, C, ldc, rowsum, m, row0, sym);
+    hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false>), grid, dim3(512), 0, s, D, K, Yx,
+                       ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym);
   return check_launch("nn_x3_kernel");
 }
 
@@ -193,14 +213,15 @@ int launch_nn_x3(const float* D, int64_t K, const __bf16* Yx, int64_t ldy, int s
 // (K rows, ldy columns, a multiple of 128).  exp_: the phi_mm form.
 int nn_x3_gemm(bool exp_, const float* A, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
                const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-               int64_t row0, hipStream_t s, int sym) {
+               int64_t row0, hipStream_t s, int sym, int m16) {
   if (K * ldy * 6 >= ((int64_t)1 << 31) || K * 128 * 4 >= ((int64_t)1 << 31))
     return fail_arg("nn_x3: K x ldy too large for 32-bit buffer offsets");
   if (ldy % 128 != 0) return fail_arg("nn_x3: ldy must be a multiple of 128");
 #define DSVGD_X3_TN(TN)                                                                        \
   return exp_ ? launch_nn_x3<TN, true>(A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0, sym,  \
-                                       s)                                                      \
-              : launch_nn_x3<TN, false>(A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0, 0, s)
+                                       m16, s)                                                 \
+              : launch_nn_x3<TN, false>(A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0, 0,  \
+                                        m16, s)
   if (ldy % 512 == 0) DSVGD_X3_TN(4);
   if (ldy % 256 == 0) DSVGD_X3_TN(2);
   DSVGD_X3_TN(1);
@@ -533,14 +554,14 @@ int64_t dsvgd_ysplit_bytes(int64_t rows, int64_t ldy) {
   return roundup(rows, kX3Step) * kX3Parts * ldy * 2;
 }
 
-int dsvgd_ysplit(const float* Y, int64_t ldy, int64_t rows, void* Yx, void* stream) {
+int dsvgd_ysplit(const float* Y, int64_t ldy, int64_t rows, void* Yx, int swz, void* stream) {
   DSVGD_REQUIRE(Y && Yx, "null pointer");
   DSVGD_REQUIRE(rows > 0 && rows % kX3Step == 0, "rows must be a positive multiple of 16");
   DSVGD_REQUIRE(ldy > 0 && ldy % 8 == 0, "ldy must be a multiple of 8");
   DSVGD_REQUIRE(((uintptr_t)Yx & 15) == 0, "16-byte alignment");
   const int64_t ksteps = rows / kX3Step, threads = ksteps * ldy;
   hipLaunchKernelGGL(ysplit_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, Y, ldy, ksteps, (__bf16*)Yx);
+                     (hipStream_t)stream, Y, ldy, ksteps, (__bf16*)Yx, swz);
   return check_launch("ysplit");
 }
 
@@ -563,7 +584,7 @@ int dsvgd_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int6
 
 int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, int64_t row0,
                     int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
-                    int64_t ldk, float* rowsum, int sym, void* stream) {
+                    int64_t ldk, float* rowsum, int sym, int m16, void* stream) {
   DSVGD_REQUIRE(D && Yx && st && KY && rowsum, "null pointer");
   DSVGD_REQUIRE(m > 0 && n > 0, "sizes");
   const int64_t n_pad = roundup(n, 128);
@@ -579,7 +600,7 @@ int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, in
                 "n x ldy too large for 32-bit buffer offsets (use dsvgd_phi_mm)");
   DSVGD_REQUIRE(!sym || (m == n && row0 == 0), "sym: the symmetric layout needs m == n, row0 == 0");
   return nn_x3_gemm(true, D, n_pad, (const __bf16*)Yx, ldy, (int)splits, st, KY, ldk, rowsum, m,
-                    row0, (hipStream_t)stream, sym);
+                    row0, (hipStream_t)stream, sym, m16);
 }
 
 int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t splits,

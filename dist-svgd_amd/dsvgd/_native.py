@@ -40,12 +40,12 @@ SIGNATURES = {
     "dsvgd_phi_splits": (_i64, [_i64, _i64, _i64]),
     "dsvgd_phi_mm": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p]),
     "dsvgd_ysplit_bytes": (_i64, [_i64, _i64]),
-    "dsvgd_ysplit": (_int, [_p, _i64, _i64, _p, _p]),
+    "dsvgd_ysplit": (_int, [_p, _i64, _i64, _p, _int, _p]),
     "dsvgd_rowsplit_bytes": (_i64, [_i64, _i64]),
     "dsvgd_rowsplit": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _p, _p]),
     "dsvgd_sqdist_x3": (_int, [_p, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _int, _p]),
     "dsvgd_phi_mm_x3": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _int,
-                                _p]),
+                                _int, _p]),
     "dsvgd_phi_finish": (_int, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _f,
                                 _f, _p, _i64, _p, _i64, _p, _i64, _p]),
     "dsvgd_phi_direct": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _f, _f, _p,

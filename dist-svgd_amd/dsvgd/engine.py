@@ -285,6 +285,12 @@ class PhiEngine(object):
     DIRECT_MAX_D = 2
 
     @property
+    def m16(self):
+        """phi_mm's split engine on v_mfma_f32_16x16x32_bf16 (ldy % 256 == 0;
+        DSVGD_X3_MFMA=32 selects the 32x32x16 form)."""
+        return self.ldy % 256 == 0 and os.environ.get("DSVGD_X3_MFMA", "16") != "32"
+
+    @property
     def sym(self):
         """D is in the symmetric layout (upper-triangle tiles only, written by
         dsvgd_sqdist_x3 layout 1 and read transposed by dsvgd_phi_mm_x3 and
@@ -317,12 +323,14 @@ class PhiEngine(object):
                        self.KY.numel(), s)
             return
         if self.x3:
+            m16 = self.m16
             with span(self.timer, "ysplit"):
-                N.call("dsvgd_ysplit", N.ptr(self.Y), self.ldy, self.n_pad, N.ptr(self.Yx), s)
+                N.call("dsvgd_ysplit", N.ptr(self.Y), self.ldy, self.n_pad, N.ptr(self.Yx),
+                       0 if m16 else 1, s)
             with span(self.timer, "phi_mm"):
                 N.call("dsvgd_phi_mm_x3", N.ptr(self.D), self.n_pad, N.ptr(self.Yx), self.ldy,
                        self.row0, self.m, self.n, self.state.ptr, self.splits, N.ptr(self.KY),
-                       self.ldy, N.ptr(self.rowsum), int(self.sym), s)
+                       self.ldy, N.ptr(self.rowsum), int(self.sym), int(m16), s)
         else:
             with span(self.timer, "phi_mm"):
                 N.call("dsvgd_phi_mm", N.ptr(self.D), self.n_pad, N.ptr(self.Y), self.ldy,

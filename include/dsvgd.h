@@ -194,10 +194,13 @@ int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64
  * (rows >= roundup(n, 128)).  Requires roundup(n,128) * ldy * 6 < 2^31.
  * sym = 1: D is dsvgd_sqdist_x3's symmetric layout (m == n, row0 == 0,
  * ldy % 256 == 0); a K-step in a column tile J < I is read from the stored
- * tile (J, I), transposed in LDS.
+ * tile (J, I), transposed in LDS.  m16 = 1: the v_mfma_f32_16x16x32_bf16
+ * form (ldy % 256 == 0), which needs Yx built with swz = 0; m16 = 0 needs
+ * swz = 1.
  * dsvgd_ysplit: Yx[kstep][part][column][16] (bf16) from the first `rows`
  * rows of Y (rows a multiple of 16; dsvgd_ysplit_bytes(rows, ldy) bytes,
- * 16-byte aligned); 16-byte halves swapped on columns with bit 3 set. */
+ * 16-byte aligned); swz = 1: 16-byte halves swapped on columns with bit 3
+ * set (the 32x32x16 engines' image), swz = 0: unswizzled (16x16x32). */
 int64_t dsvgd_ysplit_bytes(int64_t rows, int64_t ldy);
 /* Row image for the split NT engine (Gram, logreg Z): img[kstep][part][row]
  * [16] (bf16) = the three parts of A[row][16 kstep + k] for row < rows_pad,
@@ -207,10 +210,10 @@ int64_t dsvgd_ysplit_bytes(int64_t rows, int64_t ldy);
 int64_t dsvgd_rowsplit_bytes(int64_t rows_pad, int64_t kpad);
 int dsvgd_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
                    int64_t kpad, void* img, void* stream);
-int dsvgd_ysplit(const float* Y, int64_t ldy, int64_t rows, void* Yx, void* stream);
+int dsvgd_ysplit(const float* Y, int64_t ldy, int64_t rows, void* Yx, int swz, void* stream);
 int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, int64_t row0,
                     int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
-                    int64_t ldk, float* rowsum, int sym, void* stream);
+                    int64_t ldk, float* rowsum, int sym, int m16, void* stream);
 
 /* phi[i] = inv_n * (s_i + KS[i] + (2/h) (rowsum[i] xc[i] - KXc[i])) with the
  * split-K partials summed in slice order (s_i: the self term k_ii s_i), plus

@@ -52,7 +52,7 @@ def test_ysplit_reconstructs_fp32(rows, ldy):
     Y[0, :8] = 0.0
     lib = N.load()
     Yx = torch.empty(lib.dsvgd_ysplit_bytes(rows, ldy) // 2, dtype=torch.int16, device=DEV)
-    N.call("dsvgd_ysplit", N.ptr(gpu(Y)), ldy, rows, N.ptr(Yx), N.stream(torch.device(DEV)))
+    N.call("dsvgd_ysplit", N.ptr(gpu(Y)), ldy, rows, N.ptr(Yx), 1, N.stream(torch.device(DEV)))
     torch.cuda.synchronize()
     parts = decode_ysplit(Yx, rows, ldy)
     rec = parts.sum(0)
