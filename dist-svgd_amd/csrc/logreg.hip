@@ -112,7 +112,7 @@ __device__ __forceinline__ void z_epilogue(T& tile, int64_t i0, int64_t q0,
 }
 
 // Z on the split engine (fp32-accurate, gemm_x3.hpp): W and Xd as row images.
-using ZX3Tile = NTX3Tile<2, 2, 2, 2>;
+using ZX3Tile = NTX3Tile<2, 2, 2, 2>;  // 3-stage ring (a 2-stage one at 3 blocks/CU: +8 %)
 __global__ __launch_bounds__(256) void logreg_z_x3_kernel(const __bf16* __restrict__ Wx,
                                                           int64_t n_pad,
                                                           const __bf16* __restrict__ Xdx,
@@ -363,12 +363,14 @@ int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const 
     __bf16* Xdy = (__bf16*)(base + w.off_xdy);
     if ((rc = dsvgd_rowsplit(X + 1, ldx, n, p, w.n_pad, w.pp, Wx, s))) return rc;
     if ((rc = dsvgd_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, Xdx, s))) return rc;
-    if ((rc = dsvgd_ysplit(Xdp, w.ldb, w.N_pad, Xdy, 1, s))) return rc;
+    const int m16 = w.ldb % 256 == 0;  // the 16x16x32 form (unswizzled image) when it applies
+    if ((rc = dsvgd_ysplit(Xdp, w.ldb, w.N_pad, Xdy, m16 ? 0 : 1, s))) return rc;
     hipLaunchKernelGGL(logreg_z_x3_kernel, dim3(w.N_pad / ZX3Tile::BN, w.n_pad / ZX3Tile::BM),
                        dim3(256), 0, s, (const __bf16*)Wx, w.n_pad, (const __bf16*)Xdx, w.N_pad,
                        (int)(w.pp / kX3Step), tp, G);
     if ((rc = check_launch("logreg_z_x3"))) return rc;
-    if ((rc = nn_x3_gemm(false, G, w.N_pad, Xdy, w.ldb, 1, nullptr, GW, w.ldb, nullptr, n, 0, s)))
+    if ((rc = nn_x3_gemm(false, G, w.N_pad, Xdy, w.ldb, 1, nullptr, GW, w.ldb, nullptr, n, 0, s, 0,
+                         m16)))
       return rc;
     hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,
                        w.ldb, scale, S, lds);
