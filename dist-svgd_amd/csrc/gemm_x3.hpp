@@ -217,10 +217,22 @@ struct NNX3Tile {
   __device__ __forceinline__ f32x4 raw_read(const char* raw, int64_t j0) const {
     const int t = threadIdx.x;
     if (transposed(j0)) {
+      // read e fetches column 4 c4 + ((e + c4) & 3): the four c4 lanes of a
+      // row then hit four different 16-bank groups (in column order they
+      // would all hit the same one, 4-way); rotated back in registers
       const int row = t >> 2, c4 = t & 3;
-      const float* r = reinterpret_cast<const float*>(raw) + (row >> 4) * 256 + (row & 15);
-      return f32x4{r[(4 * c4) * 16], r[(4 * c4 + 1) * 16], r[(4 * c4 + 2) * 16],
-                   r[(4 * c4 + 3) * 16]};
+      const float* r = reinterpret_cast<const float*>(raw) + (row >> 4) * 256 + (row & 15) +
+                       (4 * c4) * 16;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = r[((e + c4) & 3) * 16];
+      // v[e] = column (e + c4) & 3  ->  out[q] = v[(q - c4) & 3]
+      float w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[q] = (c4 & 1) ? v[(q + 3) & 3] : v[q];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = (c4 & 2) ? w[(q + 2) & 3] : w[q];
+      return f32x4{v[0], v[1], v[2], v[3]};
     }
     return *reinterpret_cast<const f32x4*>(raw + t * 16);
   }
