@@ -174,11 +174,17 @@ struct NNX3Tile {
   // load beside it makes hipcc wait vmcnt(0): cdna_hip_programming.md "three
   // .s-level traps" (b)).
   static constexpr int kRaw = 2 * kStage;  // D ring: 2 x 8 KiB raw panels
+#ifndef DSVGD_D_AUX
+#define DSVGD_D_AUX 2
+#endif
+  static constexpr int kDAux = DSVGD_D_AUX;  // D panels: nt (read once) so Yx stays in L2
 
+  // aux: cache policy (2 = nt on gfx950: the D stream is read once)
+  template <int AUX = 0>
   __device__ __forceinline__ static void dma16(__amdgpu_buffer_rsrc_t r, char* lds, int voff,
                                                int soff) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
-                                             voff, soff, 0, 0);
+                                             voff, soff, 0, AUX);
   }
 
   // tile j0's B image -> LDS stage st
@@ -206,10 +212,10 @@ struct NNX3Tile {
                                    (j0 & 127) * 16);
       const __amdgpu_buffer_rsrc_t rT =
           __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, 0x7fffffff, 0x00020000);
-      dma16(rT, raw + (t & ~63) * 16, (t >> 6) * kPanelElems * 4 + (t & 63) * 16, 0);
+      dma16<kDAux>(rT, raw + (t & ~63) * 16, (t >> 6) * kPanelElems * 4 + (t & 63) * 16, 0);
       return;
     }
-    dma16(rA, raw + (t & ~63) * 16, t * 16, (int)((j0 >> 4) * kPanelElems * 4));
+    dma16<kDAux>(rA, raw + (t & ~63) * 16, t * 16, (int)((j0 >> 4) * kPanelElems * 4));
   }
 
   // this thread's 4 D values (row t >> 2, columns 4 (t & 3) ..) of K-step j0

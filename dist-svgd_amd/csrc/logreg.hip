@@ -105,7 +105,8 @@ __device__ __forceinline__ void z_epilogue(T& tile, int64_t i0, int64_t q0,
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float e = __builtin_amdgcn_exp2f(sc * tile.acc[mi][ni][r]);
-        g0[(r & 3) * 16 + (r >> 2) * 128] = tq * __builtin_amdgcn_rcpf(1.f + e);
+        __builtin_nontemporal_store(tq * __builtin_amdgcn_rcpf(1.f + e),
+                                    g0 + (r & 3) * 16 + (r >> 2) * 128);  // nt: G streams out
       }
     }
   }

@@ -76,7 +76,8 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        if (epi < 2 || v[r] != v[r]) dp0[(r & 3) * 16 + (r >> 2) * 128] = v[r];
+        if (epi < 2 || v[r] != v[r])  // streamed out: nt, so D does not evict the Gram operands from L2
+          __builtin_nontemporal_store(v[r], dp0 + (r & 3) * 16 + (r >> 2) * 128);
       if (mirror && mirror_store && (epi == 0 || v[0] != v[0])) {  // D[j][i]: 4 consecutive i per register quad -> 16-byte stores
         float* const mp0 = Dmir + (int64_t)cl * 16 + (wm * 4 + mi * 2) * kPanelElems + h4;
 #pragma unroll
