@@ -109,27 +109,30 @@ struct SlotLayout {
 struct SlotWriter {
   float* dst = nullptr;
   uint32_t cnt = 0;    // wave-uniform: entries in [lo, hi] so far (may exceed cap)
-  uint32_t below = 0;  // per lane
+  uint32_t below = 0;  // wave-uniform: entries < lo so far
   uint32_t cap = 0;
-  // keys: fp32 bit patterns, monotone for the values >= 0 (and +inf) this
-  // sees; in-bracket is one unsigned range test, key - klo <= khi - klo
+  // keys: fp32 bit patterns of values >= 0 (and +inf pads): monotone, all
+  // < 2^31.  One subtraction d = key - klo (mod 2^32) serves both tests:
+  // key < klo <=> d >= 2^31 (both < 2^31), in bracket <=> d <= khi - klo;
+  // each is one compare whose lane mask is counted on the scalar unit.
   uint32_t klo = 1u, kspan = 0u;
   __device__ __forceinline__ void begin(const dsvgd_select_state* st, const SlotLayout& L,
                                         int64_t slot) {
     const float lo = st->lo, hi = st->hi;
     // an unordered bracket (NaN sample) counts everything below and nothing
     // in range, so bracket_check falls back to the exact passes over D
+    // (klo = 2^31 - 1 exceeds every key; d = 0 never happens for it)
     const bool ok = hi >= lo && lo >= 0.f;
-    klo = ok ? __float_as_uint(lo) : 0xFFFFFFFFu;
+    klo = ok ? __float_as_uint(lo) : 0x7FFFFFFFu;
     kspan = ok ? __float_as_uint(hi) - klo : 0u;
     dst = L.data + slot * L.cap;
     cap = (uint32_t)L.cap;
   }
   // every lane of the wave must call add() for the same value index
   __device__ __forceinline__ void add(float v) {
-    const uint32_t key = __float_as_uint(v);
-    below += key < klo ? 1u : 0u;
-    const bool in = key - klo <= kspan;
+    const uint32_t d = __float_as_uint(v) - klo;
+    below += (uint32_t)__popcll(__ballot(d >= 0x80000000u));
+    const bool in = d <= kspan;
     const uint64_t bal = __ballot(in);
     if (bal) {
       if (in) {
@@ -142,9 +145,7 @@ struct SlotWriter {
     }
   }
   __device__ __forceinline__ void finish(const SlotLayout& L, int64_t slot, bool weight2) {
-    uint32_t b = below;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o, 64);
+    const uint32_t b = below;
     if ((threadIdx.x & 63) == 0) {
       const uint32_t flag = weight2 ? DSVGD_SLOT_WEIGHT2 : 0u;
       L.cnt[slot] = (cnt < DSVGD_SLOT_WEIGHT2 ? cnt : DSVGD_SLOT_WEIGHT2 - 1u) | flag;

@@ -48,7 +48,8 @@ def main():
     eng.median_bandwidth()
     # ENGINE_X3: "1" = the bf16-split phi_mm (default), "0" = the f32 MFMA engine
     variants = json.loads(os.environ.get("AB_VARIANTS", "null")) or {
-        "phi=x3": {"ENGINE_X3": "1"}, "phi=f32": {"ENGINE_X3": "0"}}
+        "phi=x3": {"ENGINE_X3": "1", "RECOMPUTE_D": "1"},
+        "phi=f32": {"ENGINE_X3": "0", "RECOMPUTE_D": "1"}}  # f32: the full D layout
     res = {k: [] for k in variants}
     ref = None
     keys = {k for env in variants.values() for k in env}
@@ -67,6 +68,9 @@ def main():
             elif not env.get("NOCHECK"):
                 err = float((eng.phi - ref).abs().max() / ref.abs().max())
                 assert err < 1e-5, (name, err)
+    eng.x3 = hasattr(eng, "Yx")  # the default engines (and D layout) for the timings below
+    for k in keys:
+        os.environ.pop(k, None)
     flops = 4.0 * n * n * d
     out = {k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v)),
                "tflops": flops / (np.median(v) * 1e-3) / 1e12} for k, v in res.items()}
