@@ -81,18 +81,25 @@ __device__ __forceinline__ int x3_off(int x, int h) { return x * 32 + ((h ^ ((x 
 // products in three MFMAs of half the cycles, two B and three A fragments.  Its fragment reads (16 rows x
 // 2 halves per 16-lane group) are conflict-free on UNswizzled images
 // (ysplit swz = 0).
-template <int TN, bool DMA = true, bool EXP = true, bool M16 = false>
+// RW: row waves (8 waves = RW x 8/RW, each 64 x 32*TN).  RW = 2: 128-row
+// blocks (phi_mm); RW = 4 (DMA, EXP = false only): 256-row blocks staging two
+// D panels per K-step -- twice the MFMAs per B image (logreg G . Xd, where the
+// B side is only 256 columns wide).
+template <int TN, bool DMA = true, bool EXP = true, bool M16 = false, int RW = 2>
 struct NNX3Tile {
   // (DMA needs the same DMA count in every wave: whole 512-chunk rounds)
   static constexpr int kThreads = 512;
   static constexpr int TM = 2;
-  static constexpr int BM = 128;
-  static constexpr int BC = 128 * TN;
+  static constexpr int kCW = 8 / RW;     // column waves
+  static constexpr int BM = 64 * RW;
+  static constexpr int AR = BM / 128;    // D panels (128-row) per K-step
+  static constexpr int BC = kCW * 32 * TN;
+  static_assert(RW == 2 || (RW == 4 && DMA && !EXP), "256-row blocks: DMA path, no exp");
   static constexpr int BJ = kX3Step;
   static constexpr int SA = kX3Parts * BM * 32;  // bytes of one stage's A image
   static constexpr int SB = kX3Parts * BC * 32;
   static constexpr int kStage = SA + SB;
-  static constexpr int kSmemBytes = 2 * kStage + (DMA ? 2 * kPanelElems * 4 : 0);
+  static constexpr int kSmemBytes = 2 * kStage + (DMA ? 2 * AR * kPanelElems * 4 : 0);
   static constexpr int kBChunks = SB / 16;
   static constexpr int LB = (kBChunks + kThreads - 1) / kThreads;
   static constexpr int kHalf = TN > 1 ? TN / 2 : 1;  // column tiles before the mid-step write
@@ -102,7 +109,8 @@ struct NNX3Tile {
   f32x16 acc[TM][TN];
   f32x4 acc16[4][2 * TN];  // M16: 16 x 16 tiles (4 row tiles x 2 TN column tiles)
   bf16x8 a16[4][3];        // M16: [a0|a1], [a1|a0], [a0|a2] per row tile
-  f32x4 ra;      // the D values being staged
+  f32x4 ra;      // the D values being staged (panel a of the K-step)
+  int64_t prow = 0;  // RW = 4: bytes between the block's two D panel rows
   u32x4 rb[DMA ? 1 : LB];
   float rs;
   bf16x8 a[TM][kX3Parts];
@@ -142,8 +150,9 @@ struct NNX3Tile {
   }
 
   // exp / diagonal / row sum / 3-way split of this thread's 4 D values (ra)
-  __device__ __forceinline__ void store_a(char* st, float scale, int64_t dgl) {
-    const int t = threadIdx.x, row = t >> 2, c4 = t & 3;
+  // of panel a (image rows 128 a + ...)
+  __device__ __forceinline__ void store_a(char* st, float scale, int64_t dgl, int a = 0) {
+    const int t = threadIdx.x, row = (t >> 2) + 128 * a, c4 = t & 3;
     if (!EXP) {
     } else if (dgl > -BM && dgl < BJ) {  // the K-step holds diagonal entries (NNTile::store)
       const int qd = (int)dgl + row - 4 * c4;
@@ -173,7 +182,8 @@ struct NNX3Tile {
   // LDS-DMA in the loop, so every vmcnt wait is counted by hand (a plain
   // load beside it makes hipcc wait vmcnt(0): cdna_hip_programming.md "three
   // .s-level traps" (b)).
-  static constexpr int kRaw = 2 * kStage;  // D ring: 2 x 8 KiB raw panels
+  static constexpr int kRaw = 2 * kStage;  // D ring: 2 slots x AR x 8 KiB raw panels
+  static constexpr int kSlot = AR * kPanelElems * 4;
 #ifndef DSVGD_D_AUX
 #define DSVGD_D_AUX 2
 #endif
@@ -215,14 +225,17 @@ struct NNX3Tile {
       dma16<kDAux>(rT, raw + (t & ~63) * 16, (t >> 6) * kPanelElems * 4 + (t & 63) * 16, 0);
       return;
     }
-    dma16<kDAux>(rA, raw + (t & ~63) * 16, t * 16, (int)((j0 >> 4) * kPanelElems * 4));
+#pragma unroll
+    for (int a = 0; a < AR; ++a)
+      dma16<kDAux>(rA, raw + a * kPanelElems * 4 + (t & ~63) * 16, (int)(a * prow) + t * 16,
+                   (int)((j0 >> 4) * kPanelElems * 4));
   }
 
   // this thread's 4 D values (row t >> 2, columns 4 (t & 3) ..) of K-step j0
   // from its raw slot
-  __device__ __forceinline__ f32x4 raw_read(const char* raw, int64_t j0) const {
+  __device__ __forceinline__ f32x4 raw_read(const char* raw, int64_t j0, int a = 0) const {
     const int t = threadIdx.x;
-    if (transposed(j0)) {
+    if (RW == 2 && transposed(j0)) {
       // read e fetches column 4 c4 + ((e + c4) & 3): the four c4 lanes of a
       // row then hit four different 16-bank groups (in column order they
       // would all hit the same one, 4-way); rotated back in registers
@@ -240,7 +253,7 @@ struct NNX3Tile {
       for (int q = 0; q < 4; ++q) v[q] = (c4 & 2) ? w[(q + 2) & 3] : w[q];
       return f32x4{v[0], v[1], v[2], v[3]};
     }
-    return *reinterpret_cast<const f32x4*>(raw + t * 16);
+    return *reinterpret_cast<const f32x4*>(raw + a * kPanelElems * 4 + t * 16);
   }
 
   // symmetric layout (dsvgd_sqdist_x3 layout 1): only tiles (I, J >= I) exist
@@ -334,7 +347,7 @@ struct NNX3Tile {
   __device__ __forceinline__ void run(const float* __restrict__ Apanels, const __bf16* __restrict__ Yx,
                                       int64_t ldy, int64_t k0, int64_t k1, float scale, char* smem,
                                       int64_t row_g0) {
-    const int w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
+    const int w = threadIdx.x >> 6, wr = w / kCW, wc = w % kCW;
     rs = 0.f;
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi)
@@ -355,10 +368,13 @@ struct NNX3Tile {
       char* raw = smem + kRaw;
       dma_b(smem, rB, ldy, k0);
       dma_d(raw, rA, k0);
-      if (k0 + BJ < k1) dma_d(raw + kPanelElems * 4, rA, k0 + BJ);
+      if (k0 + BJ < k1) dma_d(raw + kSlot, rA, k0 + BJ);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      ra = raw_read(raw, k0);
-      store_a(smem, scale, row_g0 - k0);
+#pragma unroll
+      for (int a = 0; a < AR; ++a) {
+        ra = raw_read(raw, k0, a);
+        store_a(smem, scale, row_g0 - k0, a);
+      }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       for (int64_t j0 = k0; j0 < k1; j0 += 2 * BJ) {
         step_dma<0>(rA, rB, ldy, j0, k1, scale, smem, row_g0, wr, wc);
@@ -403,22 +419,25 @@ struct NNX3Tile {
     char* raw = smem + kRaw;
     const bool more = j0 + BJ < k1, more2 = j0 + 2 * BJ < k1;
     if (more) dma_b(smem + (CUR ^ 1) * kStage, rB, ldy, j0 + BJ);
-    if (more2) dma_d(raw + CUR * kPanelElems * 4, rA, j0 + 2 * BJ);
+    if (more2) dma_d(raw + CUR * kSlot, rA, j0 + 2 * BJ);
     read_a(cur, wr);
     compute<0, kHalf>(cur, wc);
     if (more) {
       if (more2)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB + 1) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB + AR) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB) : "memory");
-      ra = raw_read(raw + (CUR ^ 1) * kPanelElems * 4, j0 + BJ);
-      store_a(smem + (CUR ^ 1) * kStage, scale, row_g0 - (j0 + BJ));
+#pragma unroll
+      for (int a = 0; a < AR; ++a) {
+        ra = raw_read(raw + (CUR ^ 1) * kSlot, j0 + BJ, a);
+        store_a(smem + (CUR ^ 1) * kStage, scale, row_g0 - (j0 + BJ), a);
+      }
     }
     compute<kHalf, TN>(cur, wc);
     // this wave's B DMAs landed (the D DMA may stay in flight), LDS writes
     // done, then all waves
     if (more2)
-      asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(AR) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }

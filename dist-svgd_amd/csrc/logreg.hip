@@ -36,8 +36,8 @@ struct LogregWs {
 
 static LogregWs logreg_ws(int64_t n, int64_t N, int64_t p) {
   LogregWs w;
-  w.n_pad = roundup(n, 128);
-  w.N_pad = roundup(N, 128);
+  w.n_pad = roundup(n, 256);  // whole 256 x 256 Z tiles
+  w.N_pad = roundup(N, 256);
   w.pp = roundup(p < 1 ? 1 : p, 32);
   w.ldb = nn_cols(w.pp);
   size_t o = 0;
@@ -113,8 +113,10 @@ __device__ __forceinline__ void z_epilogue(T& tile, int64_t i0, int64_t q0,
 }
 
 // Z on the split engine (fp32-accurate, gemm_x3.hpp): W and Xd as row images.
-using ZX3Tile = NTX3Tile<2, 2, 2, 2>;  // 3-stage ring (a 2-stage one at 3 blocks/CU: +8 %)
-__global__ __launch_bounds__(256) void logreg_z_x3_kernel(const __bf16* __restrict__ Wx,
+// 256 x 256 tiles, 8 waves of 64 x 128 (half the operand bytes per flop of a
+// 128 x 128 tile), 3-stage ring (144 KiB, one block per CU).
+using ZX3Tile = NTX3Tile<2, 4, 4, 2>;
+__global__ __launch_bounds__(ZX3Tile::kThreads) void logreg_z_x3_kernel(const __bf16* __restrict__ Wx,
                                                           int64_t n_pad,
                                                           const __bf16* __restrict__ Xdx,
                                                           int64_t N_pad, int nk,
@@ -367,7 +369,7 @@ int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const 
     const int m16 = w.ldb % 256 == 0;  // the 16x16x32 form (unswizzled image) when it applies
     if ((rc = dsvgd_ysplit(Xdp, w.ldb, w.N_pad, Xdy, m16 ? 0 : 1, s))) return rc;
     hipLaunchKernelGGL(logreg_z_x3_kernel, dim3(w.N_pad / ZX3Tile::BN, w.n_pad / ZX3Tile::BM),
-                       dim3(256), 0, s, (const __bf16*)Wx, w.n_pad, (const __bf16*)Xdx, w.N_pad,
+                       dim3(ZX3Tile::kThreads), 0, s, (const __bf16*)Wx, w.n_pad, (const __bf16*)Xdx, w.N_pad,
                        (int)(w.pp / kX3Step), tp, G);
     if ((rc = check_launch("logreg_z_x3"))) return rc;
     if ((rc = nn_x3_gemm(false, G, w.N_pad, Xdy, w.ldb, 1, nullptr, GW, w.ldb, nullptr, n, 0, s, 0,

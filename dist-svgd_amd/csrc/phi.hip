@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
 // phi_mm on the bf16 MFMA at fp32 accuracy (gemm_x3.hpp): the same blocks,
 // split-K slices, diagonal skip and row sums as nn_kernel<TN, true>; B is the
 // split image of Y (dsvgd_ysplit).
-template <int TN, bool DMA, bool EXP, bool M16>
+template <int TN, bool DMA, bool EXP, bool M16, int RW = 2>
 __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A, int64_t a_npad,
                                                     const __bf16* __restrict__ Yx, int64_t ldy,
                                                     int64_t K, int64_t kchunk,
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
                                                     float* __restrict__ C, int64_t ldc,
                                                     float* __restrict__ rowsum, int64_t m,
                                                     int64_t row0, int sym) {
-  using Tile = NNX3Tile<TN, DMA, EXP, M16>;
+  using Tile = NNX3Tile<TN, DMA, EXP, M16, RW>;
   __shared__ __attribute__((aligned(16))) char smem[Tile::kSmemBytes];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
@@ -90,6 +90,7 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
   if (EXP) rowsum += (int64_t)blockIdx.z * roundup128(m);
   const float scale = EXP ? -st->inv_h * kLog2e : 0.f;
   Tile tile;
+  tile.prow = (a_npad >> 4) * kPanelElems * 4;
   if (DMA && sym) {  // symmetric layout: m == n, row0 == 0 (checked by the ABI)
     tile.sym_D = A;
     tile.sym_pcols = a_npad >> 4;
@@ -98,7 +99,8 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
   tile.run(A + (i0 >> 7) * (a_npad >> 4) * kPanelElems, Yx + c0 * 16, ldy, k0, k1, scale, smem,
            row0 + i0);
 
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w / Tile::kCW,
+            wc = w % Tile::kCW;
   const int64_t r0 = i0 + wr * 32 * Tile::TM;
   if (M16) {  // 16x16 C layout: column lane & 15, rows 4 (lane >> 4) + reg
 #pragma unroll
@@ -217,6 +219,17 @@ int nn_x3_gemm(bool exp_, const float* A, int64_t K, const __bf16* Yx, int64_t l
   if (K * ldy * 6 >= ((int64_t)1 << 31) || K * 128 * 4 >= ((int64_t)1 << 31))
     return fail_arg("nn_x3: K x ldy too large for 32-bit buffer offsets");
   if (ldy % 128 != 0) return fail_arg("nn_x3: ldy must be a multiple of 128");
+  const char* e = getenv("DSVGD_X3_DMA");
+  const bool dma = !(e && e[0] == '0');
+  if (!exp_ && m16 && dma && ldy % 512 != 0 && ldy % 256 == 0) {
+    // 256-row blocks x 256 columns (G . Xd): the A rows must exist up to a
+    // multiple of 256 (the caller's panel layout; logreg pads n to 256)
+    const int64_t kchunk = roundup((K + splits - 1) / splits, kX3Step);
+    const dim3 grid(ldy / 256, roundup(m, 256) / 256, splits);
+    hipLaunchKernelGGL((nn_x3_kernel<4, true, false, true, 4>), grid, dim3(512), 0, s, A, K, Yx,
+                       ldy, K, kchunk, st, C, ldc, rowsum, m, row0, 0);
+    return check_launch("nn_x3_kernel(256-row)");
+  }
 #define DSVGD_X3_TN(TN)                                                                        \
   return exp_ ? launch_nn_x3<TN, true>(A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0, sym,  \
                                        m16, s)                                                 \
