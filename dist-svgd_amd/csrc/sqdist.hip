@@ -19,19 +19,22 @@ namespace dsvgd {
 
 using GramTile = NTTile<2, 2, 2, 2>;  // 128 x 128 block, 4 waves of 64 x 64
 
-// Epilogue of one 128 x 128 distance tile (bi, bj) from the Gram
-// accumulators: D = max(0, |y_i|^2 + |y_j|^2 - 2 y_i.y_j) (diagonal exactly 0,
-// pads +inf) into the panel layout, the mirror tile for SYM off-diagonal
-// tiles, and the select accounting (weight 2 for mirrored tiles).
-// snorm: [0,128) the tile's row norms, [128,256) its column norms.
-template <bool SYM, int smode, bool ZERO = false, class Tile = GramTile>
+// Epilogue of one wave's part of a 128 x 128 distance tile (bi, bj) from the
+// Gram accumulators: D = max(0, |y_i|^2 + |y_j|^2 - 2 y_i.y_j) (diagonal
+// exactly 0, pads +inf) into the panel layout, the mirror tile for SYM
+// off-diagonal tiles, and the select accounting (weight 2 for mirrored
+// tiles).  The wave holds rows [rbase, rbase + 64) x columns [cbase, cbase +
+// 32 NI) of the tile in acc[mi][ni] (mi < 2, ni < NI); srow / scol: the
+// tile's 128 row / column norms.
+template <bool SYM, int smode, bool ZERO = false, class Tile = GramTile, int NI = 2>
 __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t row0,
                                             int64_t m, int64_t n, int64_t n_pad,
-                                            float* __restrict__ D, const float* snorm,
+                                            float* __restrict__ D, const float* srow,
+                                            const float* scol, int rbase, int cbase,
                                             WindowHist& wh, uint32_t* shist, SlotWriter& sw,
                                             const SlotLayout& sl, int64_t slot, int epi,
                                             bool mirror_store = true) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
+  const int lane = threadIdx.x & 63;
   const bool mirror = SYM && bi != bj;
   const int64_t i0 = (int64_t)bi * GramTile::BM;  // within the owned block
   const int64_t j0 = (int64_t)bj * GramTile::BN;
@@ -49,16 +52,16 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      const int cl = wn * 64 + ni * 32 + (lane & 31);
-      const int rb = wm * 64 + mi * 32 + h4;  // this lane's first row in the sub-tile
-      const float nj = snorm[GramTile::BM + cl];
+    for (int ni = 0; ni < NI; ++ni) {
+      const int cl = cbase + ni * 32 + (lane & 31);
+      const int rb = rbase + mi * 32 + h4;  // this lane's first row in the sub-tile
+      const float nj = scol[cl];
       float* const dp0 = Dtile + (cl >> 4) * kPanelElems + (cl & 15) + rb * 16;
       float v[16];
       if (interior) {
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          v[r] = fmaxf(0.f, (snorm[rb + (r & 3) + 8 * (r >> 2)] + nj) - 2.f * tile.acc[mi][ni][r]);
+          v[r] = fmaxf(0.f, (srow[rb + (r & 3) + 8 * (r >> 2)] + nj) - 2.f * tile.acc[mi][ni][r]);
       } else {
         const bool colok = j0 + cl < n;
 #pragma unroll
@@ -68,7 +71,7 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
           if (colok && i0 + rl < m)
             x = (row0 + i0 + rl == j0 + cl)
                     ? 0.f
-                    : fmaxf(0.f, (snorm[rl] + nj) - 2.f * tile.acc[mi][ni][r]);
+                    : fmaxf(0.f, (srow[rl] + nj) - 2.f * tile.acc[mi][ni][r]);
           else
             x = INFINITY;
           v[r] = x;
@@ -79,7 +82,7 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
         if (epi < 2 || v[r] != v[r])  // streamed out: nt, so D does not evict the Gram operands from L2
           __builtin_nontemporal_store(v[r], dp0 + (r & 3) * 16 + (r >> 2) * 128);
       if (mirror && mirror_store && (epi == 0 || v[0] != v[0])) {  // D[j][i]: 4 consecutive i per register quad -> 16-byte stores
-        float* const mp0 = Dmir + (int64_t)cl * 16 + (wm * 4 + mi * 2) * kPanelElems + h4;
+        float* const mp0 = Dmir + (int64_t)cl * 16 + ((rbase >> 4) + mi * 2) * kPanelElems + h4;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           *reinterpret_cast<f32x4*>(mp0 + (q >> 1) * kPanelElems + 8 * (q & 1)) =
@@ -141,7 +144,11 @@ __global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y
     sl.publish(st, blockIdx.x);
     sw.begin(st, sl, slot);
   }
-  sq_epilogue<SYM, smode>(tile, bi, bj, row0, m, n, n_pad, D, snorm, wh, shist, sw, sl, slot, epi);
+  {
+    const int w = threadIdx.x >> 6;
+    sq_epilogue<SYM, smode>(tile, bi, bj, row0, m, n, n_pad, D, snorm, snorm + 128, (w >> 1) * 64,
+                            (w & 1) * 64, wh, shist, sw, sl, slot, epi);
+  }
   if (smode == kSelHist) {
     wh.flush(shist);
     __syncthreads();
@@ -245,8 +252,9 @@ __global__ __launch_bounds__(256, 2) void sqdist_persistent_kernel(
     if (epi == 3) {  // timing only: no epilogue at all
       tile.zero();
     } else {
-      sq_epilogue<SYM, smode, true>(tile, bi, bj, row0, m, n, n_pad, D, snorm[par], wh, shist, sw,
-                                    sl, slot, epi);
+      sq_epilogue<SYM, smode, true>(tile, bi, bj, row0, m, n, n_pad, D, snorm[par],
+                                    snorm[par] + 128, wm * 64, wn * 64, wh, shist, sw, sl, slot,
+                                    epi);
     }
     if (smode == kSelHist) wh.flush(shist);
     par ^= 1;
@@ -270,9 +278,10 @@ using GramX3Tile = NTX3Tile<2, 2, 2, 2, 2>;
 
 template <bool SYM, int smode>
 __global__ __launch_bounds__(256, 2) void sqdist_x3_kernel(
-    const __bf16* __restrict__ Yg, const float* __restrict__ norms, int64_t row0, int64_t m,
-    int64_t n, int64_t n_pad, int nk, float* __restrict__ D, dsvgd_select_state* __restrict__ st,
-    float* __restrict__ cand, int epi, int64_t total, int layout) {
+    const __bf16* __restrict__ Yg, int64_t img_rows, const float* __restrict__ norms,
+    int64_t row0, int64_t m, int64_t n, int64_t n_pad, int nk, float* __restrict__ D,
+    dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int epi, int64_t total,
+    int layout) {
   __shared__ __attribute__((aligned(16))) char smem[GramX3Tile::kSmemBytes];
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
   __shared__ float snorm[GramX3Tile::BM + GramX3Tile::BN];
@@ -306,7 +315,7 @@ __global__ __launch_bounds__(256, 2) void sqdist_x3_kernel(
         (void*)(Yg + (row0 + (int64_t)bi * 128) * 16), (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(Yg + (int64_t)bj * 128 * 16), (short)0, 0x7fffffff, 0x00020000);
-    tile.dma(stg, rA, n_pad, rB, n_pad, ks);
+    tile.dma(stg, rA, img_rows, rB, img_rows, ks);
   };
 
   int bi = 0, bj = 0;
@@ -338,8 +347,9 @@ __global__ __launch_bounds__(256, 2) void sqdist_x3_kernel(
       if (epi == 3)
         tile.zero();
       else
-        sq_epilogue<SYM, smode, true>(tile, bi, bj, row0, m, n, n_pad, D, snorm, wh, shist, sw, sl,
-                                      slot, epi, layout == 0);
+        sq_epilogue<SYM, smode, true>(tile, bi, bj, row0, m, n, n_pad, D, snorm, snorm + 128,
+                                      wm * 64, wn * 64, wh, shist, sw, sl, slot, epi,
+                                      layout == 0);
       if (smode == kSelHist) wh.flush(shist);
       L = Ln;
       bi = bin;
@@ -354,30 +364,150 @@ __global__ __launch_bounds__(256, 2) void sqdist_x3_kernel(
   }
 }
 
+// The same on 256 x 256 tiles (8 waves of 64 x 128, one block per CU): twice
+// the MFMAs per operand byte of the 128 x 128 form.  Each wave's 64 x 128
+// region lies in one 128 x 128 sub-tile (2 BI + (wr >> 1), 2 BJ + wc); the
+// epilogue runs per sub-tile (sub-tiles below the diagonal of a SYM diagonal
+// tile, and past the padded matrix, are skipped).  Candidate slots: 8 per tile.
+using GramX3WTile = NTX3Tile<2, 4, 4, 2, 2>;
+
+template <bool SYM, int smode>
+__global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
+    const __bf16* __restrict__ Yg, int64_t img_rows, const float* __restrict__ norms,
+    int64_t row0, int64_t m, int64_t n, int64_t n_pad, int nk, float* __restrict__ D,
+    dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int epi, int64_t total,
+    int layout) {
+  __shared__ __attribute__((aligned(16))) char smem[GramX3WTile::kSmemBytes];
+  __shared__ uint32_t shist[DSVGD_RADIX_BINS];
+  __shared__ float snorm[512];  // the tile's 256 row norms, then its 256 column norms
+
+  const int Tm = (int)(roundup128(m) / 128), Tn = (int)(n_pad / 128);  // 128-tiles
+  const int Tm2 = (Tm + 1) / 2, Tn2 = (Tn + 1) / 2;                    // 256-tiles
+  const int t = threadIdx.x, w = t >> 6, wr = w >> 1, wc = w & 1;
+  const int64_t x = blockIdx.x % kXcds, u = blockIdx.x / kXcds, U = gridDim.x / kXcds;
+  const int64_t q = total / kXcds, rr = total % kXcds;
+  const int64_t lo = x * q + min(x, rr);
+  const int64_t hi = (int64_t)__builtin_amdgcn_readfirstlane((int)(lo + q + (x < rr ? 1 : 0)));
+  SlotLayout sl(cand, total * 8, smode == kSelBracket ? st->cand_cap : 0);
+  if (smode == kSelBracket) sl.publish(st, blockIdx.x);
+  if (smode == kSelHist)
+    for (int b = t; b < DSVGD_RADIX_BINS; b += 512) shist[b] = 0u;
+
+  auto next_valid = [&](int64_t L, int& BI, int& BJ) -> int64_t {
+    for (; L < hi; L += U) {
+      if (tile_at(L, Tm2, Tn2, SYM, BI, BJ)) {
+        BI = __builtin_amdgcn_readfirstlane(BI);
+        BJ = __builtin_amdgcn_readfirstlane(BJ);
+        return L;
+      }
+      if (smode == kSelBracket) slot_clear(sl, L * 8 + w);
+    }
+    return L;
+  };
+  GramX3WTile tile;
+  auto issue = [&](char* stg, int BI, int BJ, int ks) {
+    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Yg + (row0 + (int64_t)BI * 256) * 16), (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Yg + (int64_t)BJ * 256 * 16), (short)0, 0x7fffffff, 0x00020000);
+    tile.dma(stg, rA, img_rows, rB, img_rows, ks);
+  };
+
+  int BI = 0, BJ = 0;
+  int64_t L = next_valid((int64_t)__builtin_amdgcn_readfirstlane((int)(lo + u)), BI, BJ);
+  tile.zero();
+  if (L < hi) issue(smem, BI, BJ, 0);
+  GramX3WTile::ring_barrier<0>();
+  int ks = 0, stage = 0;
+  int BIn = BI, BJn = BJ;
+  int64_t Ln = L;
+  while (L < hi) {
+    int ksn = ks + 1;
+    if (ksn == nk) {
+      Ln = next_valid(L + U, BIn, BJn);
+      ksn = 0;
+    }
+    const bool more = Ln < hi;
+    if (more) issue(smem + (stage ^ 1) * GramX3WTile::kStage, BIn, BJn, ksn);
+    tile.compute(smem + stage * GramX3WTile::kStage, wr, wc, (int)(row0 & 15));
+    GramX3WTile::ring_barrier<0>();
+    if (ks + 1 == nk) {  // tile done: norms, per-sub-tile epilogue (re-zeroes the accumulators)
+      {
+        const int64_t gi = t < 256 ? row0 + (int64_t)BI * 256 + t : (int64_t)BJ * 256 + t - 256;
+        snorm[t] = gi < n_pad ? norms[gi] : 0.f;
+      }
+      __syncthreads();
+      const int bi = 2 * BI + (wr >> 1), bj = 2 * BJ + wc;  // this wave's 128-sub-tile
+      const int64_t slot = L * 8 + w;
+      WindowHist wh;
+      SlotWriter sw;
+      if (smode == kSelBracket) sw.begin(st, sl, slot);
+      if (epi == 3 || bi >= Tm || bj >= Tn || (SYM && bi > bj)) {
+        tile.zero();
+        if (smode == kSelBracket) sw.finish(sl, slot, false);
+      } else {
+        sq_epilogue<SYM, smode, true, GramX3WTile, 4>(
+            tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128, snorm + 256 + wc * 128,
+            (wr & 1) * 64, 0, wh, shist, sw, sl, slot, epi, layout == 0);
+      }
+      if (smode == kSelHist) wh.flush(shist);
+      L = Ln;
+      BI = BIn;
+      BJ = BJn;
+    }
+    ks = ksn;
+    stage ^= 1;
+  }
+  if (smode == kSelHist) {
+    __syncthreads();
+    flush_block_hist(shist, st);
+  }
+}
+
+// Yg's image rows per part: the padded matrix plus one 256-row tile of slack
+// (a row block's last 256-row tile may start anywhere below n)
+int64_t gram_img_rows(int64_t n) { return roundup(n, 128) + 256; }
+
 template <int SM>
 int launch_sqdist_x3(const __bf16* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
                      int64_t d, float* D, dsvgd_select_state* st, float* cand, int layout,
                      hipStream_t s) {
   const int64_t dp = roundup(d, 32), m_pad = roundup(m, 128), n_pad = roundup(n, 128);
+  const int64_t img = gram_img_rows(n);
   const char* ep = getenv("DSVGD_SQ_EPI");
   const int epi = ep ? atoi(ep) : 0;
   const bool sym = m == n && row0 == 0;
+  const int nk = (int)(dp / kX3Step);
+  int blocks = 0, rc = 0;
+  // DSVGD_GRAM_TILE=128: the 128 x 128 form (A/B switch)
+  const char* gt = getenv("DSVGD_GRAM_TILE");
+  if (!(gt && atoi(gt) == 128)) {
+    const int64_t T2 = (n_pad / 128 + 1) / 2;
+    const int64_t total = sym ? tile_grid(T2, T2, true) : tile_grid((m_pad / 128 + 1) / 2, T2, false);
+    rc = sym ? persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3w_kernel<true, SM>), &blocks)
+             : persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3w_kernel<false, SM>),
+                                 &blocks);
+    if (rc) return rc;
+    if (sym)
+      hipLaunchKernelGGL((sqdist_x3w_kernel<true, SM>), dim3((unsigned)blocks), dim3(512), 0, s, Yg,
+                         img, norms, row0, m, n, n_pad, nk, D, st, cand, epi, total, layout);
+    else
+      hipLaunchKernelGGL((sqdist_x3w_kernel<false, SM>), dim3((unsigned)blocks), dim3(512), 0, s,
+                         Yg, img, norms, row0, m, n, n_pad, nk, D, st, cand, epi, total, 0);
+    return check_launch("sqdist_x3w");
+  }
   const int64_t T = n_pad / 128;
   const int64_t total = sym ? tile_grid(T, T, true) : tile_grid(m_pad / 128, T, false);
-  int blocks = 0;
-  int rc = sym ? persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3_kernel<true, SM>),
-                                   &blocks)
-               : persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3_kernel<false, SM>),
-                                   &blocks);
+  rc = sym ? persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3_kernel<true, SM>), &blocks)
+           : persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3_kernel<false, SM>), &blocks);
   if (rc) return rc;
   const dim3 grid((unsigned)blocks);
-  const int nk = (int)(dp / kX3Step);
   if (sym)
-    hipLaunchKernelGGL((sqdist_x3_kernel<true, SM>), grid, dim3(256), 0, s, Yg, norms, row0, m, n,
-                       n_pad, nk, D, st, cand, epi, total, layout);
+    hipLaunchKernelGGL((sqdist_x3_kernel<true, SM>), grid, dim3(256), 0, s, Yg, img, norms, row0, m,
+                       n, n_pad, nk, D, st, cand, epi, total, layout);
   else
-    hipLaunchKernelGGL((sqdist_x3_kernel<false, SM>), grid, dim3(256), 0, s, Yg, norms, row0, m, n,
-                       n_pad, nk, D, st, cand, epi, total, 0);
+    hipLaunchKernelGGL((sqdist_x3_kernel<false, SM>), grid, dim3(256), 0, s, Yg, img, norms, row0,
+                       m, n, n_pad, nk, D, st, cand, epi, total, 0);
   return check_launch("sqdist_x3");
 }
 
@@ -559,7 +689,8 @@ int dsvgd_sqdist_x3(const void* Yg, const float* norms, int64_t row0, int64_t m,
   DSVGD_REQUIRE(ldd == n_pad, "ldd must equal roundup(n,128) (panel layout)");
   DSVGD_REQUIRE(((uintptr_t)Yg & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
   DSVGD_REQUIRE(m_pad / 128 <= 65535, "too many row tiles");
-  DSVGD_REQUIRE(dp * n_pad * 6 < ((int64_t)1 << 31), "image too large for 32-bit buffer offsets");
+  DSVGD_REQUIRE(dp * gram_img_rows(n) * 6 < ((int64_t)1 << 31),
+                "image too large for 32-bit buffer offsets");
   DSVGD_REQUIRE(layout == 0 || (layout == 1 && m == n && row0 == 0),
                 "layout 1 (symmetric) needs the whole matrix: m == n, row0 == 0");
   const __bf16* yg = (const __bf16*)Yg;

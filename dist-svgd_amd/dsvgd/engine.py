@@ -166,10 +166,11 @@ class PhiEngine(object):
             nb = lib.dsvgd_ysplit_bytes(self.n_pad, self.ldy)
             self.Yx = torch.empty(nb // 2, dtype=torch.int16, device=dev)
         # distance Gram (d > DIRECT_MAX_D): split engine unless DSVGD_GRAM_GEMM=f32
+        self.gram_rows = self.n_pad + 256   # Yg image rows (include/dsvgd.h, dsvgd_sqdist_x3)
         self.x3_gram = (os.environ.get("DSVGD_GRAM_GEMM", "x3") == "x3"
-                        and self.dp * self.n_pad * 6 < (1 << 31))
+                        and self.dp * self.gram_rows * 6 < (1 << 31))
         if self.x3_gram:
-            nb = lib.dsvgd_rowsplit_bytes(self.n_pad, self.dp)
+            nb = lib.dsvgd_rowsplit_bytes(self.gram_rows, self.dp)
             self.Yg = torch.empty(nb // 2, dtype=torch.int16, device=dev)
         self.KY = torch.empty(self.splits * m, self.ldy, **f32)
         self.rowsum = torch.empty(self.splits * self.m_pad, **f32)
@@ -232,8 +233,8 @@ class PhiEngine(object):
             st, mode = self.state.ptr, SEL_HIST
         if self.x3_gram and self.d > self.DIRECT_MAX_D:
             with span(self.timer, "rowsplit"):
-                N.call("dsvgd_rowsplit", N.ptr(self.Y), self.ldy, self.n_pad, self.dp, self.n_pad,
-                       self.dp, N.ptr(self.Yg), s)
+                N.call("dsvgd_rowsplit", N.ptr(self.Y), self.ldy, self.n_pad, self.dp,
+                       self.gram_rows, self.dp, N.ptr(self.Yg), s)
             with span(self.timer, "sqdist"):
                 N.call("dsvgd_sqdist_x3", N.ptr(self.Yg), N.ptr(self.norms), self.row0, self.m,
                        self.n, self.d, N.ptr(self.D), self.n_pad, mode, st, cand, int(self.sym), s)

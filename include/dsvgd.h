@@ -161,12 +161,13 @@ int dsvgd_bracket_check(dsvgd_select_state* st, void* stream);
 int dsvgd_set_bandwidth(dsvgd_select_state* st, float h, void* stream);
 
 /* dsvgd_sqdist's Gram path (d > 2) on the split engine (fp32-accurate, see
- * dsvgd_phi_mm_x3): Yg = dsvgd_rowsplit(Y, ldy, n_pad, dp, n_pad, dp) with
- * dp = roundup(d, 32), n_pad = roundup(n, 128); same outputs and select
+ * dsvgd_phi_mm_x3): Yg = dsvgd_rowsplit(Y, ldy, n_pad, dp, n_pad + 256, dp)
+ * with dp = roundup(d, 32), n_pad = roundup(n, 128) (256 rows of zero slack
+ * for the 256 x 256 tiles); same outputs and select
  * modes as dsvgd_sqdist.  layout 0: the full panel-layout D; layout 1 (m ==
  * n, row0 == 0 only) the SYMMETRIC LAYOUT: tiles (I, J) with J < I are not
  * written -- consumers read them transposed (dsvgd_phi_mm_x3 with sym = 1,
- * dsvgd_radix_hist with sym_npad).  Requires dp * n_pad * 6 < 2^31. */
+ * dsvgd_radix_hist with sym_npad).  Requires dp * (n_pad + 256) * 6 < 2^31. */
 int dsvgd_sqdist_x3(const void* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
                     int64_t d, float* D, int64_t ldd, int select_mode, dsvgd_select_state* st,
                     float* cand, int layout, void* stream);
