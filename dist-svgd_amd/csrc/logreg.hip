@@ -129,6 +129,66 @@ __global__ __launch_bounds__(ZX3Tile::kThreads) void logreg_z_x3_kernel(const __
   z_epilogue(tile, i0, q0, tp, N_pad, G);
 }
 
+// Persistent form: a grid of one block per CU walks each XCD's L2-grouped
+// range of 256 x 256 tiles (sqdist_x3w_kernel's schedule) through a 2-stage
+// DMA ring that runs across tile boundaries: the next tile's first K-step
+// lands while this one's epilogue (exp2, rcp, G stores) runs.
+using ZX3PTile = NTX3Tile<2, 4, 4, 2, 2>;
+__global__ __launch_bounds__(512, 1) void logreg_z_x3p_kernel(
+    const __bf16* __restrict__ Wx, int64_t n_img, const __bf16* __restrict__ Xdx, int64_t N_img,
+    int nk, const float* __restrict__ tp, int64_t N_pad, float* __restrict__ G, int Tm2, int Tn2,
+    int64_t total) {
+  __shared__ __attribute__((aligned(16))) char smem[ZX3PTile::kSmemBytes];
+  const int w = threadIdx.x >> 6, wr = w / ZX3PTile::WN_, wc = w % ZX3PTile::WN_;
+  const int64_t x = blockIdx.x % kXcds, u = blockIdx.x / kXcds, U = gridDim.x / kXcds;
+  const int64_t q = total / kXcds, rr = total % kXcds;
+  const int64_t lo = x * q + min(x, rr);
+  const int64_t hi = (int64_t)__builtin_amdgcn_readfirstlane((int)(lo + q + (x < rr ? 1 : 0)));
+  auto next_valid = [&](int64_t L, int& BI, int& BJ) -> int64_t {
+    for (; L < hi; L += U)
+      if (tile_at(L, Tm2, Tn2, false, BI, BJ)) {
+        BI = __builtin_amdgcn_readfirstlane(BI);
+        BJ = __builtin_amdgcn_readfirstlane(BJ);
+        return L;
+      }
+    return L;
+  };
+  ZX3PTile tile;
+  auto issue = [&](char* stg, int BI, int BJ, int ks) {
+    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Wx + (int64_t)BI * 256 * 16), (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Xdx + (int64_t)BJ * 256 * 16), (short)0, 0x7fffffff, 0x00020000);
+    tile.dma(stg, rA, n_img, rB, N_img, ks);
+  };
+  int BI = 0, BJ = 0;
+  int64_t L = next_valid((int64_t)__builtin_amdgcn_readfirstlane((int)(lo + u)), BI, BJ);
+  tile.zero();
+  if (L < hi) issue(smem, BI, BJ, 0);
+  ZX3PTile::ring_barrier<0>();
+  int ks = 0, stage = 0, BIn = BI, BJn = BJ;
+  int64_t Ln = L;
+  while (L < hi) {
+    int ksn = ks + 1;
+    if (ksn == nk) {
+      Ln = next_valid(L + U, BIn, BJn);
+      ksn = 0;
+    }
+    if (Ln < hi) issue(smem + (stage ^ 1) * ZX3PTile::kStage, BIn, BJn, ksn);
+    tile.compute(smem + stage * ZX3PTile::kStage, wr, wc);
+    ZX3PTile::ring_barrier<0>();
+    if (ks + 1 == nk) {
+      z_epilogue(tile, (int64_t)BI * 256, (int64_t)BJ * 256, tp, N_pad, G);
+      tile.zero();
+      L = Ln;
+      BI = BIn;
+      BJ = BJn;
+    }
+    ks = ksn;
+    stage ^= 1;
+  }
+}
+
 // One (particle tile, data tile) per block.
 __global__ __launch_bounds__(256) void logreg_z_kernel(const float* __restrict__ W,
                                                        const float* __restrict__ Xd, int64_t ldb,
@@ -368,9 +428,22 @@ int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const 
     if ((rc = dsvgd_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, Xdx, s))) return rc;
     const int m16 = w.ldb % 256 == 0;  // the 16x16x32 form (unswizzled image) when it applies
     if ((rc = dsvgd_ysplit(Xdp, w.ldb, w.N_pad, Xdy, m16 ? 0 : 1, s))) return rc;
-    hipLaunchKernelGGL(logreg_z_x3_kernel, dim3(w.N_pad / ZX3Tile::BN, w.n_pad / ZX3Tile::BM),
-                       dim3(ZX3Tile::kThreads), 0, s, (const __bf16*)Wx, w.n_pad, (const __bf16*)Xdx, w.N_pad,
-                       (int)(w.pp / kX3Step), tp, G);
+    // DSVGD_LOGREG_Z=tile: one tile per block (A/B switch against the persistent form)
+    const char* zf = getenv("DSVGD_LOGREG_Z");
+    if (zf && std::string(zf) == "tile") {
+      hipLaunchKernelGGL(logreg_z_x3_kernel, dim3(w.N_pad / ZX3Tile::BN, w.n_pad / ZX3Tile::BM),
+                         dim3(ZX3Tile::kThreads), 0, s, (const __bf16*)Wx, w.n_pad,
+                         (const __bf16*)Xdx, w.N_pad, (int)(w.pp / kX3Step), tp, G);
+    } else {
+      int blocks = 0;
+      if ((rc = persistent_blocks(reinterpret_cast<const void*>(&logreg_z_x3p_kernel), &blocks)))
+        return rc;
+      const int Tm2 = (int)(w.n_pad / 256), Tn2 = (int)(w.N_pad / 256);
+      hipLaunchKernelGGL(logreg_z_x3p_kernel, dim3((unsigned)blocks), dim3(512), 0, s,
+                         (const __bf16*)Wx, w.n_pad, (const __bf16*)Xdx, w.N_pad,
+                         (int)(w.pp / kX3Step), tp, w.N_pad, G, Tm2, Tn2,
+                         tile_grid(Tm2, Tn2, false));
+    }
     if ((rc = check_launch("logreg_z_x3"))) return rc;
     if ((rc = nn_x3_gemm(false, G, w.N_pad, Xdy, w.ldb, 1, nullptr, GW, w.ldb, nullptr, n, 0, s, 0,
                          m16)))
