@@ -33,9 +33,11 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
                                             const float* scol, int rbase, int cbase,
                                             WindowHist& wh, uint32_t* shist, SlotWriter& sw,
                                             const SlotLayout& sl, int64_t slot, int epi,
-                                            bool mirror_store = true) {
+                                            bool mirror_store = true, int r0t = 0) {
+  // r0t: row0 / 128 when a row block's diagonal square runs SYM (bi is then
+  // block-local, bj global; the mirror of (bi, bj) is (bj - r0t, bi + r0t))
   const int lane = threadIdx.x & 63;
-  const bool mirror = SYM && bi != bj;
+  const bool mirror = SYM && bi + r0t != bj;
   const int64_t i0 = (int64_t)bi * GramTile::BM;  // within the owned block
   const int64_t j0 = (int64_t)bj * GramTile::BN;
   const uint32_t weight = mirror ? 2u : 1u;
@@ -44,7 +46,7 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
   // ((r&3)*16 + (r>>2)*128 floats) is a compile-time immediate.
   const int h4 = 4 * (lane >> 5);
   float* const Dtile = D + ((int64_t)bi * (n_pad >> 4) + (int64_t)bj * 8) * kPanelElems;
-  float* const Dmir = D + ((int64_t)bj * (n_pad >> 4) + (int64_t)bi * 8) * kPanelElems;
+  float* const Dmir = D + ((int64_t)(bj - r0t) * (n_pad >> 4) + (int64_t)(bi + r0t) * 8) * kPanelElems;
   // interior tiles (the bulk): no diagonal entry, every row and column valid
   // -> 3 VALU per value; edge / diagonal tiles take the guarded form
   const bool interior = (row0 + i0 + 128 <= j0 || j0 + 128 <= row0 + i0) && i0 + 128 <= m &&
@@ -376,31 +378,32 @@ __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
     const __bf16* __restrict__ Yg, int64_t img_rows, const float* __restrict__ norms,
     int64_t row0, int64_t m, int64_t n, int64_t n_pad, int nk, float* __restrict__ D,
     dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int epi, int64_t total,
-    int layout) {
+    int layout, int Tm2, int Tc2, int bj_off, int r0t, int64_t slot_base, int64_t ns_total) {
   __shared__ __attribute__((aligned(16))) char smem[GramX3WTile::kSmemBytes];
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
   __shared__ float snorm[512];  // the tile's 256 row norms, then its 256 column norms
 
+  // this launch: Tm2 x Tc2 256-tiles, global column tiles from bj_off
+  // (SYM: the triangle of a Tm2 x Tm2 square; r0t = its row0 / 128)
   const int Tm = (int)(roundup128(m) / 128), Tn = (int)(n_pad / 128);  // 128-tiles
-  const int Tm2 = (Tm + 1) / 2, Tn2 = (Tn + 1) / 2;                    // 256-tiles
   const int t = threadIdx.x, w = t >> 6, wr = w >> 1, wc = w & 1;
   const int64_t x = blockIdx.x % kXcds, u = blockIdx.x / kXcds, U = gridDim.x / kXcds;
   const int64_t q = total / kXcds, rr = total % kXcds;
   const int64_t lo = x * q + min(x, rr);
   const int64_t hi = (int64_t)__builtin_amdgcn_readfirstlane((int)(lo + q + (x < rr ? 1 : 0)));
-  SlotLayout sl(cand, total * 8, smode == kSelBracket ? st->cand_cap : 0);
+  SlotLayout sl(cand, ns_total, smode == kSelBracket ? st->cand_cap : 0);
   if (smode == kSelBracket) sl.publish(st, blockIdx.x);
   if (smode == kSelHist)
     for (int b = t; b < DSVGD_RADIX_BINS; b += 512) shist[b] = 0u;
 
   auto next_valid = [&](int64_t L, int& BI, int& BJ) -> int64_t {
     for (; L < hi; L += U) {
-      if (tile_at(L, Tm2, Tn2, SYM, BI, BJ)) {
+      if (tile_at(L, Tm2, Tc2, SYM, BI, BJ)) {
         BI = __builtin_amdgcn_readfirstlane(BI);
-        BJ = __builtin_amdgcn_readfirstlane(BJ);
+        BJ = __builtin_amdgcn_readfirstlane(BJ + bj_off);
         return L;
       }
-      if (smode == kSelBracket) slot_clear(sl, L * 8 + w);
+      if (smode == kSelBracket) slot_clear(sl, slot_base + L * 8 + w);
     }
     return L;
   };
@@ -438,17 +441,17 @@ __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
       }
       __syncthreads();
       const int bi = 2 * BI + (wr >> 1), bj = 2 * BJ + wc;  // this wave's 128-sub-tile
-      const int64_t slot = L * 8 + w;
+      const int64_t slot = slot_base + L * 8 + w;
       WindowHist wh;
       SlotWriter sw;
       if (smode == kSelBracket) sw.begin(st, sl, slot);
-      if (epi == 3 || bi >= Tm || bj >= Tn || (SYM && bi > bj)) {
+      if (epi == 3 || bi >= Tm || bj >= Tn || (SYM && bi + r0t > bj)) {
         tile.zero();
         if (smode == kSelBracket) sw.finish(sl, slot, false);
       } else {
         sq_epilogue<SYM, smode, true, GramX3WTile, 4>(
             tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128, snorm + 256 + wc * 128,
-            (wr & 1) * 64, 0, wh, shist, sw, sl, slot, epi, layout == 0);
+            (wr & 1) * 64, 0, wh, shist, sw, sl, slot, epi, layout == 0, r0t);
       }
       if (smode == kSelHist) wh.flush(shist);
       L = Ln;
@@ -482,19 +485,49 @@ int launch_sqdist_x3(const __bf16* Yg, const float* norms, int64_t row0, int64_t
   // DSVGD_GRAM_TILE=128: the 128 x 128 form (A/B switch)
   const char* gt = getenv("DSVGD_GRAM_TILE");
   if (!(gt && atoi(gt) == 128)) {
-    const int64_t T2 = (n_pad / 128 + 1) / 2;
-    const int64_t total = sym ? tile_grid(T2, T2, true) : tile_grid((m_pad / 128 + 1) / 2, T2, false);
-    rc = sym ? persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3w_kernel<true, SM>), &blocks)
-             : persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3w_kernel<false, SM>),
-                                 &blocks);
-    if (rc) return rc;
-    if (sym)
-      hipLaunchKernelGGL((sqdist_x3w_kernel<true, SM>), dim3((unsigned)blocks), dim3(512), 0, s, Yg,
-                         img, norms, row0, m, n, n_pad, nk, D, st, cand, epi, total, layout);
-    else
-      hipLaunchKernelGGL((sqdist_x3w_kernel<false, SM>), dim3((unsigned)blocks), dim3(512), 0, s,
-                         Yg, img, norms, row0, m, n, n_pad, nk, D, st, cand, epi, total, 0);
-    return check_launch("sqdist_x3w");
+    int bs = 0, bn = 0;
+    if ((rc = persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3w_kernel<true, SM>), &bs)))
+      return rc;
+    if ((rc = persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3w_kernel<false, SM>), &bn)))
+      return rc;
+    const int Tn2 = (int)((n_pad / 128 + 1) / 2), Tm2 = (int)((m_pad / 128 + 1) / 2);
+    struct Part {
+      bool sym;
+      int tm2, tc2, bj_off, r0t;
+      int64_t total;
+    } parts[3];
+    int np = 0;
+    if (sym) {
+      parts[np++] = {true, Tn2, Tn2, 0, 0, tile_grid(Tn2, Tn2, true)};
+    } else if (row0 % 256 == 0 && m % 256 == 0 && row0 + m <= n) {
+      // a row block holds the diagonal square [row0, row0 + m)^2 of the
+      // symmetric matrix: its upper triangle (+ mirror stores), and the
+      // rectangles left and right of it
+      const int c0 = (int)(row0 / 256), c1 = (int)((row0 + m) / 256), sq = (int)(m / 256);
+      if (c0 > 0) parts[np++] = {false, sq, c0, 0, 0, tile_grid(sq, c0, false)};
+      parts[np++] = {true, sq, sq, c0, (int)(row0 / 128), tile_grid(sq, sq, true)};
+      if (Tn2 > c1) parts[np++] = {false, sq, Tn2 - c1, c1, 0, tile_grid(sq, Tn2 - c1, false)};
+    } else {
+      parts[np++] = {false, Tm2, Tn2, 0, 0, tile_grid(Tm2, Tn2, false)};
+    }
+    int64_t ns_total = 0;
+    for (int i = 0; i < np; ++i) ns_total += parts[i].total * 8;
+    int64_t base = 0;
+    for (int i = 0; i < np; ++i) {
+      const Part& P = parts[i];
+      const int lay = sym ? layout : 0;
+      if (P.sym)
+        hipLaunchKernelGGL((sqdist_x3w_kernel<true, SM>), dim3((unsigned)bs), dim3(512), 0, s, Yg,
+                           img, norms, row0, m, n, n_pad, nk, D, st, cand, epi, P.total, lay, P.tm2,
+                           P.tc2, P.bj_off, P.r0t, base, ns_total);
+      else
+        hipLaunchKernelGGL((sqdist_x3w_kernel<false, SM>), dim3((unsigned)bn), dim3(512), 0, s, Yg,
+                           img, norms, row0, m, n, n_pad, nk, D, st, cand, epi, P.total, 0, P.tm2,
+                           P.tc2, P.bj_off, 0, base, ns_total);
+      if ((rc = check_launch("sqdist_x3w"))) return rc;
+      base += P.total * 8;
+    }
+    return 0;
   }
   const int64_t T = n_pad / 128;
   const int64_t total = sym ? tile_grid(T, T, true) : tile_grid(m_pad / 128, T, false);

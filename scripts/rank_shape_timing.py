@@ -1,0 +1,72 @@
+"""Per-stage time of ONE rank's share of the bench step at S ranks, on one GPU
+(no communication): what the N-GPU bench line should approach per step, minus
+the all-gather / all-reduce time.
+
+    python scripts/rank_shape_timing.py [--shards 1,2,4,8]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dist-svgd_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shards", default="1,2,4,8")
+    ap.add_argument("--steps", type=int, default=5)
+    args = ap.parse_args()
+    import dsvgd
+    from dsvgd.engine import StageTimer
+    from bench import synthetic_data
+    n, d, Ng = 65536, 256, 16384
+    x, t = synthetic_data(Ng, d - 1)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    X = (0.1 * torch.randn(n, d, generator=g)).cuda()
+    for S in [int(v) for v in args.shards.split(",")]:
+        m, r = n // S, S // 2          # a middle rank
+        per = Ng // S
+        tgt = dsvgd.targets.LogisticRegression(x[r * per:(r + 1) * per], t[r * per:(r + 1) * per])
+        eng = dsvgd.PhiEngine(n, d, m=m, row0=r * m, device="cuda:0")
+        Sx = torch.empty_like(X)
+        Xo = X[r * m:(r + 1) * m].clone()
+        timer = StageTimer()
+
+        def step():
+            with torch.cuda.device(0):
+                from dsvgd.engine import span
+                with span(timer, "scores"):
+                    tgt.score(X, Sx)          # all_scores: every particle on the local data
+                eng.pack(X, Sx)
+                eng.distances(median=True)
+                # the other S-1 ranks' counts approximated by this rank's (x S):
+                # keeps the bracket check on its real (candidate) path
+                eng.median_bandwidth((lambda v: v.mul_(S)) if S > 1 else None)
+                eng.direction(Xo, 1e-6, write_phi=False)
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        eng.timer = timer
+        timer.events.clear()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.steps):
+            step()
+        e1.record()
+        torch.cuda.synchronize()
+        st = {k: round(float(np.mean(v)), 3) for k, v in timer.summary().items()}
+        print(json.dumps({"shards": S, "m": m, "row0": r * m, "N_local": per,
+                          "ms_per_step_no_comm": e0.elapsed_time(e1) / args.steps,
+                          "sym_layout": bool(eng.sym), "stages_ms": st}), flush=True)
+        del eng
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -558,16 +558,18 @@ def _dist_median_worker(rank, S, port, X, d, steps, eps, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("d", [16, 80])
-def test_distsampler_median_two_ranks_jacobi(d):
+@pytest.mark.parametrize("n,d", [(6000, 16), (6000, 80), (6144, 80)])
+def test_distsampler_median_two_ranks_jacobi(n, d):
     """Row-sharded D over 2 ranks (bracketed select, all-reduced counts and
-    histograms) vs the oracle's global-median Jacobi step."""
+    histograms) vs the oracle's global-median Jacobi step.  n = 6144: 256-row
+    aligned blocks, whose distance pass computes the diagonal square's upper
+    triangle (+ mirror) and the rectangles beside it in separate launches."""
     import torch.multiprocessing as mp
-    n, S, steps, eps = 6000, 2, 2, 0.05
+    S, steps, eps = 2, 2, 0.05
     X = np.random.RandomState(d).randn(n, d).astype(np.float32)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_dist_median_worker, args=(r, S, 29830 + d, X, d, steps, eps, q))
+    ps = [ctx.Process(target=_dist_median_worker, args=(r, S, 29830 + d + n % 7, X, d, steps, eps, q))
           for r in range(S)]
     for p in ps:
         p.start()

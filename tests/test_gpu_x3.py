@@ -163,7 +163,8 @@ def test_logreg_scores_x3_as_accurate_as_f32(monkeypatch, n, N, p):
 @pytest.mark.parametrize("n,d,m,row0", [(700, 48, None, 0), (5000, 64, None, 0),
                                         (3000, 130, 1000, 1500), (513, 3, None, 0),
                                         (1000, 100, None, 0), (1900, 256, None, 0),
-                                        (4500, 128, None, 0)])
+                                        (4500, 128, None, 0), (3000, 130, 1024, 1024),
+                                        (2300, 96, 1280, 0), (2600, 64, 512, 2048)])
 def test_sqdist_x3_as_accurate_as_f32(monkeypatch, n, d, m, row0):
     """Distances through the split Gram (dsvgd_sqdist_x3) against fp64, next
     to the f32 Gram on the same particles: symmetric, bracketed (n = 5000:
@@ -175,7 +176,7 @@ def test_sqdist_x3_as_accurate_as_f32(monkeypatch, n, d, m, row0):
     mm = n if m is None else m
     ref = ((Xc[row0:row0 + mm, None, :] - Xc[None, :, :]) ** 2).sum(-1) if n * mm <= 4e6 else None
     nrm = (Xc ** 2).sum(1)
-    err, med = {}, {}
+    err, med, Dall = {}, {}, {}
     for gemm in ("f32", "x3"):
         monkeypatch.setenv("DSVGD_GRAM_GEMM", gemm)
         eng = dsvgd().PhiEngine(n, d, m=m, row0=row0, device=DEV)
@@ -198,6 +199,13 @@ def test_sqdist_x3_as_accurate_as_f32(monkeypatch, n, d, m, row0):
         if ref is not None:
             scale = nrm[row0:row0 + mm, None] + nrm[None, :] + 1e-30
             err[gemm] = float(np.max(np.abs(Dm - ref) / scale))
+        Dall[gemm] = Dm
     if ref is not None:
         record_parity(err["x3"])
         assert err["x3"] <= 2.0 * err["f32"] + 1e-7 and err["x3"] < 2e-6, err
+    # every entry of the block, incl. the mirrored / square-split ones of a
+    # 256-aligned row block, against the f32 Gram's
+    scale = nrm[row0:row0 + mm, None] + nrm[None, :] + 1e-30
+    e = float(np.max(np.abs(Dall["x3"] - Dall["f32"]) / scale))
+    record_parity(e)
+    assert e < 4e-6
