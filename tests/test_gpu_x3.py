@@ -102,7 +102,8 @@ def _ky_errors(res):
 
 
 @pytest.mark.parametrize("n,d,h", [(300, 20, 5.0), (1000, 64, None), (2048, 256, None),
-                                   (513, 100, 40.0), (4096, 3, None)])
+                                   (513, 100, 40.0), (4096, 3, None), (1500, 1024, None),
+                                   (777, 500, None)])
 def test_phi_mm_x3_matches_f32_engine_and_oracle(monkeypatch, n, d, h):
     rs = np.random.RandomState(n + d)
     X = rs.randn(n, d).astype(np.float32)
@@ -139,7 +140,8 @@ def test_phi_mm_x3_row_block_split_k(monkeypatch):
     assert e < PHI_TOL
 
 
-@pytest.mark.parametrize("n,N,p", [(1000, 3000, 20), (512, 16384, 255), (300, 129, 40)])
+@pytest.mark.parametrize("n,N,p", [(1000, 3000, 20), (512, 16384, 255), (300, 129, 40),
+                                   (600, 2000, 1023), (257, 700, 511)])
 def test_logreg_scores_x3_as_accurate_as_f32(monkeypatch, n, N, p):
     """The logreg score GEMMs (Z = W Xd^T on the split NT engine, G Xd on
     the split NN engine without exp) against the fp64 oracle, next to the
