@@ -460,9 +460,13 @@ struct NNX3Tile {
 // (counted vmcnt) for tile k+1 before its closing barrier, so a DMA has two
 // iterations to land.  No VGPR staging, no VALU in the loop but the MFMAs.
 // NS: ring stages (3: a DMA has two iterations to land; 2: one, at 2/3 of the LDS).
-template <int TM, int TN, int WM, int WN, int NS = 3>
+// M16: v_mfma_f32_16x16x32_bf16 with concatenated k (NNX3Tile); the results
+// are in acc16[4][2 TN] (16x16 layout) and both images must be unswizzled.
+template <int TM, int TN, int WM, int WN, int NS = 3, bool M16 = false>
 struct NTX3Tile {
   static constexpr int TM_ = TM, TN_ = TN, WM_ = WM, WN_ = WN;
+  static constexpr bool M16_ = M16;
+  static_assert(!M16 || TM == 2, "M16: 64-row waves");
   static constexpr int kThreads = 64 * WM * WN;
   static constexpr int BM = 32 * TM * WM;
   static constexpr int BN = 32 * TN * WN;
@@ -481,8 +485,16 @@ struct NTX3Tile {
   static_assert(kSmemBytes <= 160 * 1024, "LDS budget");
 
   f32x16 acc[TM][TN];
+  f32x4 acc16[M16 ? 4 : 1][M16 ? 2 * TN : 1];
 
   __device__ __forceinline__ void zero() {
+    if (M16) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2 * TN; ++nt) acc16[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      return;
+    }
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
@@ -518,6 +530,33 @@ struct NTX3Tile {
   // a0: image row of A's row 0, mod 16 (the image swizzles on the absolute
   // row; a row block may start off a 16-row boundary)
   __device__ __forceinline__ void compute(const char* st, int wm, int wn, int a0 = 0) {
+    if (M16) {  // lane (rr = l & 15, g = l >> 4): k-slot g >> 1 picks the part, g & 1 the half
+      const int lane = threadIdx.x & 63, rr = lane & 15, g = lane >> 4, hh = g & 1, sl = g >> 1;
+      bf16x8 f[4][3];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const char* aa = st + (wm * 64 + mt * 16 + rr) * 32 + hh * 16;
+        f[mt][0] = *reinterpret_cast<const bf16x8*>(aa + sl * BM * 32);        // [a0|a1]
+        f[mt][1] = *reinterpret_cast<const bf16x8*>(aa + (sl ^ 1) * BM * 32);  // [a1|a0]
+        f[mt][2] = *reinterpret_cast<const bf16x8*>(aa + 2 * sl * BM * 32);    // [a0|a2]
+      }
+#pragma unroll
+      for (int nt = 0; nt < 2 * TN; ++nt) {
+        const char* bb = st + SA + (wn * 32 * TN + nt * 16 + rr) * 32 + hh * 16;
+        const bf16x8 g1 = *reinterpret_cast<const bf16x8*>(bb + sl * BN * 32);            // [b0|b1]
+        const bf16x8 g3 = *reinterpret_cast<const bf16x8*>(bb + (2 - 2 * sl) * BN * 32);  // [b2|b0]
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          acc16[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[mt][2], g3, acc16[mt][nt], 0, 0, 0);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          acc16[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[mt][1], g1, acc16[mt][nt], 0, 0, 0);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          acc16[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[mt][0], g1, acc16[mt][nt], 0, 0, 0);
+      }
+      return;
+    }
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
     bf16x8 a[TM][kX3Parts];
 #pragma unroll

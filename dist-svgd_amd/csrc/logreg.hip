@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #include "gemm_tiles.hpp"
 #include "gemm_x3.hpp"
@@ -85,10 +86,36 @@ __device__ __forceinline__ float sigmoidf_stable(float u) {
 // 128 accumulators per wave at 2 waves/SIMD is 6 % slower).
 using ZTile = NTTile<2, 2, 2, 2>;
 
+template <class T, class = void>
+struct IsM16 : std::false_type {};
+template <class T>
+struct IsM16<T, std::void_t<decltype(T::M16_)>> : std::integral_constant<bool, T::M16_> {};
+
 template <class T>
 __device__ __forceinline__ void z_epilogue(T& tile, int64_t i0, int64_t q0,
                                            const float* __restrict__ tp, int64_t N_pad,
                                            float* __restrict__ G) {
+  if constexpr (IsM16<T>::value) {  // 16x16 tiles: column lane & 15, rows 4 (lane >> 4) + reg
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w / T::WN_, wn = w % T::WN_;
+#pragma unroll
+    for (int nt = 0; nt < 2 * T::TN_; ++nt) {
+      const int64_t q = q0 + wn * 32 * T::TN_ + nt * 16 + (lane & 15);
+      const float tq = tp[q];
+      const float sc = tq * kLog2e;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int64_t i = i0 + wm * 64 + mt * 16 + 4 * (lane >> 4);  // 4 rows in one panel
+        float* const g0 = G + ((i >> 7) * (N_pad >> 4) + (q >> 4)) * kPanelElems + (q & 15) +
+                          (i & 127) * 16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __builtin_amdgcn_exp2f(sc * tile.acc16[mt][nt][r]);
+          __builtin_nontemporal_store(tq * __builtin_amdgcn_rcpf(1.f + e), g0 + r * 16);
+        }
+      }
+    }
+    return;
+  }
   constexpr int WR = 32 * T::TM_, WC = 32 * T::TN_;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w / T::WN_, wn = w % T::WN_;
   const int h4 = 4 * (lane >> 5);
@@ -133,7 +160,7 @@ __global__ __launch_bounds__(ZX3Tile::kThreads) void logreg_z_x3_kernel(const __
 // range of 256 x 256 tiles (sqdist_x3w_kernel's schedule) through a 2-stage
 // DMA ring that runs across tile boundaries: the next tile's first K-step
 // lands while this one's epilogue (exp2, rcp, G stores) runs.
-using ZX3PTile = NTX3Tile<2, 4, 4, 2, 2>;
+using ZX3PTile = NTX3Tile<2, 4, 4, 2, 2, true>;  // 16x16x32 (unswizzled W / Xd images)
 __global__ __launch_bounds__(512, 1) void logreg_z_x3p_kernel(
     const __bf16* __restrict__ Wx, int64_t n_img, const __bf16* __restrict__ Xdx, int64_t N_img,
     int nk, const float* __restrict__ tp, int64_t N_pad, float* __restrict__ G, int Tm2, int Tn2,
@@ -424,13 +451,16 @@ int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const 
     void* Wx = base + w.off_wx;
     void* Xdx = base + w.off_xdx;
     __bf16* Xdy = (__bf16*)(base + w.off_xdy);
-    if ((rc = dsvgd_rowsplit(X + 1, ldx, n, p, w.n_pad, w.pp, Wx, s))) return rc;
-    if ((rc = dsvgd_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, Xdx, s))) return rc;
+    // DSVGD_LOGREG_Z=tile: one 32x32x16 tile per block (A/B switch against
+    // the persistent 16x16x32 form); the images' swizzle follows the form
+    const char* zf = getenv("DSVGD_LOGREG_Z");
+    const bool ztile = zf && std::string(zf) == "tile";
+    if ((rc = dsvgd_rowsplit(X + 1, ldx, n, p, w.n_pad, w.pp, Wx, ztile ? 1 : 0, s))) return rc;
+    if ((rc = dsvgd_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, Xdx, ztile ? 1 : 0, s)))
+      return rc;
     const int m16 = w.ldb % 256 == 0;  // the 16x16x32 form (unswizzled image) when it applies
     if ((rc = dsvgd_ysplit(Xdp, w.ldb, w.N_pad, Xdy, m16 ? 0 : 1, s))) return rc;
-    // DSVGD_LOGREG_Z=tile: one tile per block (A/B switch against the persistent form)
-    const char* zf = getenv("DSVGD_LOGREG_Z");
-    if (zf && std::string(zf) == "tile") {
+    if (ztile) {
       hipLaunchKernelGGL(logreg_z_x3_kernel, dim3(w.N_pad / ZX3Tile::BN, w.n_pad / ZX3Tile::BM),
                          dim3(ZX3Tile::kThreads), 0, s, (const __bf16*)Wx, w.n_pad,
                          (const __bf16*)Xdx, w.N_pad, (int)(w.pp / kX3Step), tp, G);

@@ -140,7 +140,7 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
 __global__ __launch_bounds__(256) void rowsplit_kernel(const float* __restrict__ A, int64_t lda,
                                                        int64_t rows, int64_t cols,
                                                        int64_t rows_pad, int64_t ksteps,
-                                                       __bf16* __restrict__ img) {
+                                                       __bf16* __restrict__ img, int swz) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= ksteps * rows_pad) return;
   const int64_t kb = t / rows_pad, i = t % rows_pad;
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void rowsplit_kernel(const float* __restrict__
     s[1][k >> 3][k & 7] = v.s1;
     s[2][k >> 3][k & 7] = v.s2;
   }
-  const int sw = (int)((i >> 3) & 1);
+  const int sw = swz ? (int)((i >> 3) & 1) : 0;
 #pragma unroll
   for (int p = 0; p < kX3Parts; ++p) {
     __bf16* dst = img + ((kb * kX3Parts + p) * rows_pad + i) * 16;
@@ -583,7 +583,7 @@ int64_t dsvgd_rowsplit_bytes(int64_t rows_pad, int64_t kpad) {
 }
 
 int dsvgd_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
-                   int64_t kpad, void* img, void* stream) {
+                   int64_t kpad, void* img, int swz, void* stream) {
   DSVGD_REQUIRE(A && img, "null pointer");
   DSVGD_REQUIRE(rows >= 0 && cols >= 0 && rows <= rows_pad && lda >= cols, "sizes");
   DSVGD_REQUIRE(rows_pad > 0 && rows_pad % 16 == 0 && kpad > 0 && kpad % kX3Step == 0,
@@ -591,7 +591,7 @@ int dsvgd_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int6
   DSVGD_REQUIRE(((uintptr_t)img & 15) == 0, "16-byte alignment");
   const int64_t ksteps = kpad / kX3Step, threads = ksteps * rows_pad;
   hipLaunchKernelGGL(rowsplit_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, A, lda, rows, cols, rows_pad, ksteps, (__bf16*)img);
+                     (hipStream_t)stream, A, lda, rows, cols, rows_pad, ksteps, (__bf16*)img, swz);
   return check_launch("rowsplit");
 }
 

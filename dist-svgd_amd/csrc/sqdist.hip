@@ -105,6 +105,73 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
   if (smode == kSelBracket) sw.finish(sl, slot, mirror);
 }
 
+// sq_epilogue for 16x16x32 tiles (NTX3Tile M16): the wave holds rows
+// [rbase, rbase + 64) x columns [cbase, cbase + 32 TN) of tile (bi, bj) as
+// acc16[mt][nt], lane (col lane & 15, rows 4 (lane >> 4) + r); a lane's 4
+// values are 4 consecutive rows of one column, i.e. one 16-byte mirror store.
+template <bool SYM, int smode, class Tile>
+__device__ __forceinline__ void sq_epilogue16(Tile& tile, int bi, int bj, int64_t row0,
+                                              int64_t m, int64_t n, int64_t n_pad,
+                                              float* __restrict__ D, const float* srow,
+                                              const float* scol, int rbase, int cbase,
+                                              WindowHist& wh, uint32_t* shist, SlotWriter& sw,
+                                              const SlotLayout& sl, int64_t slot, int epi,
+                                              bool mirror_store, int r0t) {
+  const int lane = threadIdx.x & 63, g4 = 4 * (lane >> 4);
+  const bool mirror = SYM && bi + r0t != bj;
+  const int64_t i0 = (int64_t)bi * 128, j0 = (int64_t)bj * 128;
+  const uint32_t weight = mirror ? 2u : 1u;
+  float* const Dtile = D + ((int64_t)bi * (n_pad >> 4) + (int64_t)bj * 8) * kPanelElems;
+  float* const Dmir =
+      D + ((int64_t)(bj - r0t) * (n_pad >> 4) + (int64_t)(bi + r0t) * 8) * kPanelElems;
+  const bool interior = (row0 + i0 + 128 <= j0 || j0 + 128 <= row0 + i0) && i0 + 128 <= m &&
+                        j0 + 128 <= n;
+#pragma unroll
+  for (int nt = 0; nt < 2 * Tile::TN_; ++nt) {
+    const int cl = cbase + nt * 16 + (lane & 15);
+    const float nj = scol[cl];
+    const bool colok = j0 + cl < n;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int rb = rbase + mt * 16 + g4;  // this lane's first row
+      float* const dp0 = Dtile + (cl >> 4) * kPanelElems + (cl & 15) + rb * 16;
+      float v[4];
+      if (interior) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          v[r] = fmaxf(0.f, (srow[rb + r] + nj) - 2.f * tile.acc16[mt][nt][r]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rl = rb + r;
+          float x;
+          if (colok && i0 + rl < m)
+            x = (row0 + i0 + rl == j0 + cl) ? 0.f
+                                             : fmaxf(0.f, (srow[rl] + nj) - 2.f * tile.acc16[mt][nt][r]);
+          else
+            x = INFINITY;
+          v[r] = x;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (epi < 2 || v[r] != v[r]) __builtin_nontemporal_store(v[r], dp0 + r * 16);
+      if (mirror && mirror_store && (epi == 0 || v[0] != v[0]))  // D[j][i], i = rb .. rb + 3
+        *reinterpret_cast<f32x4*>(Dmir + ((rbase >> 4) + mt) * kPanelElems + (int64_t)cl * 16 +
+                                  g4) = f32x4{v[0], v[1], v[2], v[3]};
+      if (smode == kSelHist) {
+        if (mt == 0 && nt == 0) wh.init(v[0]);
+        hist_account(wh, v, weight, shist);
+      } else if (smode == kSelBracket) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sw.add(v[r]);
+      }
+      tile.acc16[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  if (smode == kSelBracket) sw.finish(sl, slot, mirror);
+}
+
 // One tile per block.  Rows [row0, row0+m) of Y against rows [0,n).  SYM
 // (m == n, row0 == 0): only tiles bi <= bj, the off-diagonal ones stored
 // twice (tile + transpose) and accounted with weight 2.
@@ -371,14 +438,15 @@ __global__ __launch_bounds__(256, 2) void sqdist_x3_kernel(
 // region lies in one 128 x 128 sub-tile (2 BI + (wr >> 1), 2 BJ + wc); the
 // epilogue runs per sub-tile (sub-tiles below the diagonal of a SYM diagonal
 // tile, and past the padded matrix, are skipped).  Candidate slots: 8 per tile.
-using GramX3WTile = NTX3Tile<2, 4, 4, 2, 2>;
-
-template <bool SYM, int smode>
+// M16: 16x16x32 MFMAs on an unswizzled Yg (default), else 32x32x16 on a
+// swizzled one (DSVGD_GRAM_MFMA=32, A/B switch).
+template <bool SYM, int smode, bool M16 = true>
 __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
     const __bf16* __restrict__ Yg, int64_t img_rows, const float* __restrict__ norms,
     int64_t row0, int64_t m, int64_t n, int64_t n_pad, int nk, float* __restrict__ D,
     dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int epi, int64_t total,
     int layout, int Tm2, int Tc2, int bj_off, int r0t, int64_t slot_base, int64_t ns_total) {
+  using GramX3WTile = NTX3Tile<2, 4, 4, 2, 2, M16>;
   __shared__ __attribute__((aligned(16))) char smem[GramX3WTile::kSmemBytes];
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
   __shared__ float snorm[512];  // the tile's 256 row norms, then its 256 column norms
@@ -420,7 +488,7 @@ __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
   int64_t L = next_valid((int64_t)__builtin_amdgcn_readfirstlane((int)(lo + u)), BI, BJ);
   tile.zero();
   if (L < hi) issue(smem, BI, BJ, 0);
-  GramX3WTile::ring_barrier<0>();
+  GramX3WTile::template ring_barrier<0>();
   int ks = 0, stage = 0;
   int BIn = BI, BJn = BJ;
   int64_t Ln = L;
@@ -433,7 +501,7 @@ __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
     const bool more = Ln < hi;
     if (more) issue(smem + (stage ^ 1) * GramX3WTile::kStage, BIn, BJn, ksn);
     tile.compute(smem + stage * GramX3WTile::kStage, wr, wc, (int)(row0 & 15));
-    GramX3WTile::ring_barrier<0>();
+    GramX3WTile::template ring_barrier<0>();
     if (ks + 1 == nk) {  // tile done: norms, per-sub-tile epilogue (re-zeroes the accumulators)
       {
         const int64_t gi = t < 256 ? row0 + (int64_t)BI * 256 + t : (int64_t)BJ * 256 + t - 256;
@@ -449,9 +517,15 @@ __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
         tile.zero();
         if (smode == kSelBracket) sw.finish(sl, slot, false);
       } else {
-        sq_epilogue<SYM, smode, true, GramX3WTile, 4>(
-            tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128, snorm + 256 + wc * 128,
-            (wr & 1) * 64, 0, wh, shist, sw, sl, slot, epi, layout == 0, r0t);
+        if constexpr (M16)
+          sq_epilogue16<SYM, smode>(tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128,
+                                    snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl,
+                                    slot, epi, layout == 0, r0t);
+        else
+          sq_epilogue<SYM, smode, true, GramX3WTile, 4>(
+              tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128,
+              snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl, slot, epi, layout == 0,
+              r0t);
       }
       if (smode == kSelHist) wh.flush(shist);
       L = Ln;
@@ -485,6 +559,8 @@ int launch_sqdist_x3(const __bf16* Yg, const float* norms, int64_t row0, int64_t
   // DSVGD_GRAM_TILE=128: the 128 x 128 form (A/B switch)
   const char* gt = getenv("DSVGD_GRAM_TILE");
   if (!(gt && atoi(gt) == 128)) {
+    const char* gm = getenv("DSVGD_GRAM_MFMA");
+    const bool m16 = !(gm && atoi(gm) == 32);
     int bs = 0, bn = 0;
     if ((rc = persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3w_kernel<true, SM>), &bs)))
       return rc;
@@ -516,14 +592,22 @@ int launch_sqdist_x3(const __bf16* Yg, const float* norms, int64_t row0, int64_t
     for (int i = 0; i < np; ++i) {
       const Part& P = parts[i];
       const int lay = sym ? layout : 0;
-      if (P.sym)
-        hipLaunchKernelGGL((sqdist_x3w_kernel<true, SM>), dim3((unsigned)bs), dim3(512), 0, s, Yg,
-                           img, norms, row0, m, n, n_pad, nk, D, st, cand, epi, P.total, lay, P.tm2,
-                           P.tc2, P.bj_off, P.r0t, base, ns_total);
-      else
-        hipLaunchKernelGGL((sqdist_x3w_kernel<false, SM>), dim3((unsigned)bn), dim3(512), 0, s, Yg,
-                           img, norms, row0, m, n, n_pad, nk, D, st, cand, epi, P.total, 0, P.tm2,
-                           P.tc2, P.bj_off, 0, base, ns_total);
+#define DSVGD_X3W(SY, M, B, LAY, R0T)                                                          \
+  hipLaunchKernelGGL((sqdist_x3w_kernel<SY, SM, M>), dim3((unsigned)B), dim3(512), 0, s, Yg, img,  \
+                     norms, row0, m, n, n_pad, nk, D, st, cand, epi, P.total, LAY, P.tm2, P.tc2, \
+                     P.bj_off, R0T, base, ns_total)
+      if (P.sym) {
+        if (m16)
+          DSVGD_X3W(true, true, bs, lay, P.r0t);
+        else
+          DSVGD_X3W(true, false, bs, lay, P.r0t);
+      } else {
+        if (m16)
+          DSVGD_X3W(false, true, bn, 0, 0);
+        else
+          DSVGD_X3W(false, false, bn, 0, 0);
+      }
+#undef DSVGD_X3W
       if ((rc = check_launch("sqdist_x3w"))) return rc;
       base += P.total * 8;
     }

@@ -42,7 +42,7 @@ SIGNATURES = {
     "dsvgd_ysplit_bytes": (_i64, [_i64, _i64]),
     "dsvgd_ysplit": (_int, [_p, _i64, _i64, _p, _int, _p]),
     "dsvgd_rowsplit_bytes": (_i64, [_i64, _i64]),
-    "dsvgd_rowsplit": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _p, _p]),
+    "dsvgd_rowsplit": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _p, _int, _p]),
     "dsvgd_sqdist_x3": (_int, [_p, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _int, _p]),
     "dsvgd_phi_mm_x3": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _int,
                                 _int, _p]),

@@ -233,8 +233,12 @@ class PhiEngine(object):
             st, mode = self.state.ptr, SEL_HIST
         if self.x3_gram and self.d > self.DIRECT_MAX_D:
             with span(self.timer, "rowsplit"):
+                # image swizzle of the Gram form the library runs: 256 tiles on
+                # 16x16x32 (unswizzled), DSVGD_GRAM_TILE=128 on 32x32x16 (swizzled)
+                swz = 1 if (os.environ.get("DSVGD_GRAM_TILE") == "128"
+                            or os.environ.get("DSVGD_GRAM_MFMA") == "32") else 0
                 N.call("dsvgd_rowsplit", N.ptr(self.Y), self.ldy, self.n_pad, self.dp,
-                       self.gram_rows, self.dp, N.ptr(self.Yg), s)
+                       self.gram_rows, self.dp, N.ptr(self.Yg), swz, s)
             with span(self.timer, "sqdist"):
                 N.call("dsvgd_sqdist_x3", N.ptr(self.Yg), N.ptr(self.norms), self.row0, self.m,
                        self.n, self.d, N.ptr(self.D), self.n_pad, mode, st, cand, int(self.sym), s)

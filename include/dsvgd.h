@@ -161,7 +161,8 @@ int dsvgd_bracket_check(dsvgd_select_state* st, void* stream);
 int dsvgd_set_bandwidth(dsvgd_select_state* st, float h, void* stream);
 
 /* dsvgd_sqdist's Gram path (d > 2) on the split engine (fp32-accurate, see
- * dsvgd_phi_mm_x3): Yg = dsvgd_rowsplit(Y, ldy, n_pad, dp, n_pad + 256, dp)
+ * dsvgd_phi_mm_x3): Yg = dsvgd_rowsplit(Y, ldy, n_pad, dp, n_pad + 256, dp, 0)
+ * (swz 1 under DSVGD_GRAM_TILE=128, the 32x32x16 A/B form)
  * with dp = roundup(d, 32), n_pad = roundup(n, 128) (256 rows of zero slack
  * for the 256 x 256 tiles); same outputs and select
  * modes as dsvgd_sqdist.  layout 0: the full panel-layout D; layout 1 (m ==
@@ -206,11 +207,12 @@ int64_t dsvgd_ysplit_bytes(int64_t rows, int64_t ldy);
 /* Row image for the split NT engine (Gram, logreg Z): img[kstep][part][row]
  * [16] (bf16) = the three parts of A[row][16 kstep + k] for row < rows_pad,
  * column < kpad (zero outside rows x cols); rows_pad, kpad multiples of 16;
- * dsvgd_rowsplit_bytes(rows_pad, kpad) bytes, 16-byte aligned; 16-byte
- * halves swapped on rows with bit 3 set. */
+ * dsvgd_rowsplit_bytes(rows_pad, kpad) bytes, 16-byte aligned; swz = 1:
+ * 16-byte halves swapped on rows with bit 3 set (32x32x16 engines), swz = 0:
+ * unswizzled (16x16x32 engines). */
 int64_t dsvgd_rowsplit_bytes(int64_t rows_pad, int64_t kpad);
 int dsvgd_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
-                   int64_t kpad, void* img, void* stream);
+                   int64_t kpad, void* img, int swz, void* stream);
 int dsvgd_ysplit(const float* Y, int64_t ldy, int64_t rows, void* Yx, int swz, void* stream);
 int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, int64_t row0,
                     int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
