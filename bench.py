@@ -174,7 +174,9 @@ def main():
     x3 = bool(sampler._engines[next(iter(sampler._engines))].x3)
     peak = PEAK_X3_TFLOPS if x3 else PEAK_FP32_MFMA_TFLOPS
     # the committed PMC summary is an N=1 profile: only quoted for the N=1 run
-    kname = "void dsvgd::nn_x3_kernel<4" if x3 else "void dsvgd::nn_kernel<4, true"
+    # phi_mm is the NN tile with the fused exp (x3: <TN, DMA, EXP=true, ...>, f32: <TN, EXP=true, ...>);
+    # the logreg G.Xd launch is the same tile with EXP=false
+    kname = "void dsvgd::nn_x3_kernel<4, true, true," if x3 else "void dsvgd::nn_kernel<4, true,"
     traffic, traffic_src = pmc_traffic(kname) if world == 1 else (None, None)
     flops = 4.0 * m * n * d
     achieved = flops / (phi_ms * 1e-3) / 1e12

@@ -1,0 +1,50 @@
+"""bench.py contract: the roofline traffic comes from the phi_mm launch of the
+committed PMC summary, and the multi-rank path (barrier, max-over-ranks time,
+one JSON line from rank 0) runs under torch.distributed.run."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def test_pmc_traffic_picks_phi_mm():
+    import bench
+    summ = os.path.join(ROOT, "profiles", "latest_summary.json")
+    if not os.path.exists(summ):
+        pytest.skip("no committed PMC summary")
+    with open(summ) as f:
+        ks = json.load(f)["kernels"]
+    phi = [k for k in ks if k.startswith("void dsvgd::nn_x3_kernel<4, true, true,")]
+    gxd = [k for k in ks if k.startswith("void dsvgd::nn_x3_kernel<4, true, false,")]
+    assert len(phi) == 1, phi
+    traffic, src = bench.pmc_traffic("void dsvgd::nn_x3_kernel<4, true, true,")
+    assert traffic == ks[phi[0]]["hbm_bytes_per_launch"]
+    assert src == os.path.join("profiles", "latest_summary.json")
+    if gxd:  # the logreg G.Xd launch (same tile, no exp) must not be the one quoted
+        assert traffic != ks[gxd[0]]["hbm_bytes_per_launch"]
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gloo():
+    """2 ranks sharing cuda:0, gloo exchange: the N>1 timing/reporting path."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29763", "bench.py", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--particles", "4096", "--dim", "64",
+           "--data-rows", "1024", "--backend", "gloo"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 2
+    assert out["config"]["particles_per_gpu"] == 2048
+    assert out["value"] > 0 and out["ms_per_step"] > 0
+    assert abs(out["value"] - 4096 * 2 / (out["ms_per_step"] * 2e-3)) < 1e-6 * out["value"]
+    assert out["roofline"]["traffic"] is None   # N=1 PMC summary is not quoted at N>1
+    assert "cpu_baseline" not in out
