@@ -139,6 +139,8 @@ class DistSampler(object):
     def _exchange_all_particles(self):
         "Gathers all particles to all shards (distsampler.py:152-158)."
         s, e = self._particle_start_idx, self._particle_end_idx
+        if exchange.all_gather_in_place(self._work, s, e, self._group):
+            return
         out = torch.empty_like(self._work)
         exchange.all_gather_blocks(self._work[s:e], out, self._group)
         self._work.copy_(out)

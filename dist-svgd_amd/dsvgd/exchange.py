@@ -25,6 +25,20 @@ def all_gather_blocks(own, out, group=None):
     out.copy_(torch.cat(parts).to(out.device))
 
 
+def all_gather_in_place(full, start, end, group=None):
+    """full[start:end] is this rank's block at rank * (end - start): gather the
+    other blocks around it in place (RCCL in-place all-gather, no staging
+    copy).  Returns False (nothing done) where that layout or backend does not
+    hold; the caller then uses all_gather_blocks."""
+    if not (full.is_cuda and full.is_contiguous()) or _is_gloo(group):
+        return False
+    m = end - start
+    if m <= 0 or start != dist.get_rank(group) * m or full.shape[0] != m * dist.get_world_size(group):
+        return False
+    dist.all_gather_into_tensor(full, full[start:end], group=group)
+    return True
+
+
 def all_reduce_sum(t, group=None):
     """In-place SUM over ranks   [distsampler.py:170]."""
     if t.is_cuda and not _is_gloo(group):

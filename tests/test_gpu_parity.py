@@ -558,18 +558,22 @@ def _dist_median_worker(rank, S, port, X, d, steps, eps, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,d", [(6000, 16), (6000, 80), (6144, 80)])
-def test_distsampler_median_two_ranks_jacobi(n, d):
-    """Row-sharded D over 2 ranks (bracketed select, all-reduced counts and
-    histograms) vs the oracle's global-median Jacobi step.  n = 6144: 256-row
-    aligned blocks, whose distance pass computes the diagonal square's upper
-    triangle (+ mirror) and the rectangles beside it in separate launches."""
+@pytest.mark.parametrize("n,d,S", [(6000, 16, 2), (6000, 80, 2), (6144, 80, 2),
+                                   (8192, 80, 4), (8192, 64, 8)])
+def test_distsampler_median_multi_rank_jacobi(n, d, S):
+    """Row-sharded D over S ranks sharing cuda:0 (all-reduced counts and
+    histograms) vs the oracle's global-median Jacobi step.  Owned blocks of
+    >= 2^24 entries take the bracketed select, smaller ones (S = 8 here) the
+    all-reduced radix passes.  n = 6144 / 8192: 256-row aligned blocks, whose
+    distance pass computes the diagonal square's upper triangle (+ mirror) and
+    the rectangles beside it in separate launches (S = 4 / 8: interior ranks
+    with rectangles on both sides, the bench's S = 8 geometry scaled down)."""
     import torch.multiprocessing as mp
-    S, steps, eps = 2, 2, 0.05
+    steps, eps = 2, 0.05
     X = np.random.RandomState(d).randn(n, d).astype(np.float32)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_dist_median_worker, args=(r, S, 29830 + d + n % 7, X, d, steps, eps, q))
+    ps = [ctx.Process(target=_dist_median_worker, args=(r, S, 29830 + d + n % 7 + 10 * S, X, d, steps, eps, q))
           for r in range(S)]
     for p in ps:
         p.start()
@@ -584,8 +588,10 @@ def test_distsampler_median_two_ranks_jacobi(n, d):
     assert abs_err(got, ref) < TRAJ_TOL
     for _, _, hs in res:
         for bracketed, h, fallback in hs:
-            assert bracketed and fallback == 0
-    assert res[0][2] == res[1][2]            # identical h on both ranks
+            assert bracketed == ((n // S) * n >= (1 << 24))
+            assert not bracketed or fallback == 0
+    for r in res[1:]:
+        assert r[2] == res[0][2]             # identical h on every rank
 
 
 @pytest.mark.parametrize("name", DIST_S2)

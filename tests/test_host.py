@@ -103,6 +103,8 @@ def _gloo_worker(rank, port, q):
     own = torch.full((3, 2), float(rank + 1))
     out = torch.empty(6, 2)
     exchange.all_gather_blocks(own, out)
+    # the in-place form is RCCL-only: a CPU / gloo group declines (caller falls back)
+    assert not exchange.all_gather_in_place(out, 3 * rank, 3 * rank + 3)
     red = torch.arange(4, dtype=torch.int64) * (rank + 1)
     exchange.all_reduce_sum(red)
     recv = torch.empty(3, 2)
