@@ -75,24 +75,48 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __rest
   const int rg = threadIdx.x >> 6;  // 4 row groups
   const int64_t r0 = (int64_t)blockIdx.x * kMeanRows;
   const int64_t r1 = min(r0 + kMeanRows, n);
-  float s = 0.f;
-  if (c < d)
-    for (int64_t r = r0 + rg; r < r1; r += 4) s += X[r * ldx + c];
-  red[rg][threadIdx.x & 63] = s;
+  // four independent chains per lane: four row loads in flight, not one
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (c < d) {
+    int64_t r = r0 + rg;
+    for (; r + 12 < r1; r += 16) {
+      a0 += X[r * ldx + c];
+      a1 += X[(r + 4) * ldx + c];
+      a2 += X[(r + 8) * ldx + c];
+      a3 += X[(r + 12) * ldx + c];
+    }
+    for (; r < r1; r += 4) a0 += X[r * ldx + c];
+  }
+  red[rg][threadIdx.x & 63] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (rg == 0 && c < d)
     partial[(int64_t)blockIdx.x * d + c] =
         ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
 }
 
+// 64 columns per block; the 4 waves split the partial rows, 4 chains each
 __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ partial,
                                                            int64_t nb, int64_t n, int64_t d,
                                                            float* __restrict__ mean) {
-  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (c >= d) return;
-  float s = 0.f;
-  for (int64_t b = 0; b < nb; ++b) s += partial[b * d + c];
-  mean[c] = s / (float)n;
+  __shared__ float red[4][64];
+  const int64_t c = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int w = threadIdx.x >> 6;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (c < d) {
+    int64_t b = w;
+    for (; b + 12 < nb; b += 16) {
+      a0 += partial[b * d + c];
+      a1 += partial[(b + 4) * d + c];
+      a2 += partial[(b + 8) * d + c];
+      a3 += partial[(b + 12) * d + c];
+    }
+    for (; b < nb; b += 4) a0 += partial[b * d + c];
+  }
+  red[w][threadIdx.x & 63] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (w == 0 && c < d)
+    mean[c] = (((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) +
+               red[3][threadIdx.x]) / (float)n;
 }
 
 // ---------------------------------------------------------------- pack ----
@@ -200,7 +224,7 @@ int dsvgd_colmean(const float* X, int64_t ldx, int64_t n, int64_t d, float* part
                      d, partial);
   int rc = check_launch("colsum_partial");
   if (rc) return rc;
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((d + 255) / 256), dim3(256), 0, s, partial, nb, n,
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((d + 63) / 64), dim3(256), 0, s, partial, nb, n,
                      d, mean);
   return check_launch("colsum_final");
 }
