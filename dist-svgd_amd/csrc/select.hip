@@ -8,9 +8,11 @@
 // Sources of a pass: the D panel buffer (HBM stream, 4 B per entry per pass)
 // or, in bracketed mode, the candidate buffer the distance epilogue compacted
 // (~1 % of D).  The choice is made on device (st->fallback).
+#include <algorithm>
 #include <cmath>
 
 #include "gemm_tiles.hpp"
+
 #include "select.hpp"
 
 namespace dsvgd {
@@ -261,10 +263,47 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 
 // out[p] = ||y_i - y_j||^2 (explicit differences) for s hash-chosen pairs
 // (i, j) in [0,n)^2; one wave per pair, deterministic for a given seed.
+// 16 lanes per sampled pair (4 pairs per wave), 16-byte row loads: a
+// 256-wide row pair is one float4 pair per lane per 64 columns, so a wave
+// keeps 4 pairs' gathers in flight instead of walking one pair 64 floats at
+// a time.  Needs ldy % 4 == 0 and a 16-byte aligned Y (checked by the host);
+// columns >= d inside the last float4 are masked out.
 __global__ __launch_bounds__(256) void sample_sqdist_kernel(const float* __restrict__ Y,
                                                             int64_t ldy, int64_t n, int d,
                                                             int64_t s, uint64_t seed,
                                                             float* __restrict__ out) {
+  const int l16 = threadIdx.x & 15;
+  for (int64_t p = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); p < s;
+       p += (int64_t)gridDim.x * 16) {
+    const uint64_t h = mix64(seed ^ (0x9e3779b97f4a7c15ull * (uint64_t)(p + 1)));
+    const int64_t i = (int64_t)((h & 0xffffffffull) % (uint64_t)n);
+    const int64_t j = (int64_t)((h >> 32) % (uint64_t)n);
+    const float* yi = Y + i * ldy;
+    const float* yj = Y + j * ldy;
+    float acc = 0.f;
+    for (int c = l16 * 4; c < d; c += 64) {
+      const float4 a = *reinterpret_cast<const float4*>(yi + c);
+      const float4 b = *reinterpret_cast<const float4*>(yj + c);
+      const float d0 = a.x - b.x;
+      const float d1 = c + 1 < d ? a.y - b.y : 0.f;
+      const float d2 = c + 2 < d ? a.z - b.z : 0.f;
+      const float d3 = c + 3 < d ? a.w - b.w : 0.f;
+      acc = fmaf(d0, d0, acc);
+      acc = fmaf(d1, d1, acc);
+      acc = fmaf(d2, d2, acc);
+      acc = fmaf(d3, d3, acc);
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (l16 == 0) out[p] = acc;
+  }
+}
+
+// generic layout (any ldy / alignment): one wave per pair
+__global__ __launch_bounds__(256) void sample_sqdist_any_kernel(const float* __restrict__ Y,
+                                                                int64_t ldy, int64_t n, int d,
+                                                                int64_t s, uint64_t seed,
+                                                                float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   for (int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < s;
        p += (int64_t)gridDim.x * 4) {
@@ -322,11 +361,16 @@ int dsvgd_sample_sqdist(const float* Y, int64_t ldy, int64_t n, int64_t d, int64
                         uint64_t seed, float* out, void* stream) {
   DSVGD_REQUIRE(Y && out, "null pointer");
   DSVGD_REQUIRE(n > 0 && d > 0 && s > 0 && ldy >= d, "sizes");
-  int64_t blocks = (s + 3) / 4;
-  if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(sample_sqdist_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, Y, ldy,
-                     n, (int)d, s, seed, out);
-  return check_launch("sample_sqdist");
+  if (ldy % 4 == 0 && ((uintptr_t)Y & 15) == 0) {
+    const int64_t blocks = std::min<int64_t>((s + 15) / 16, 8192);
+    hipLaunchKernelGGL(sample_sqdist_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, Y,
+                       ldy, n, (int)d, s, seed, out);
+    return check_launch("sample_sqdist");
+  }
+  const int64_t blocks = std::min<int64_t>((s + 3) / 4, 8192);
+  hipLaunchKernelGGL(sample_sqdist_any_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, Y,
+                     ldy, n, (int)d, s, seed, out);
+  return check_launch("sample_sqdist_any");
 }
 
 int dsvgd_bracket_init(dsvgd_select_state* st, int64_t n_total, const dsvgd_select_state* lo_st,

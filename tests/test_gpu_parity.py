@@ -104,6 +104,41 @@ def test_median_select_bit_exact(n, d):
         assert h == 1.0
 
 
+def _sample_pairs(n, s, seed):
+    """Pair (i, j) of sample p, as csrc/select.hip sample_sqdist_kernel hashes it
+    (test restatement of its 64-bit finalizer)."""
+    M = (1 << 64) - 1
+    out = []
+    for p in range(s):
+        x = (seed ^ ((0x9e3779b97f4a7c15 * (p + 1)) & M)) & M
+        x ^= x >> 33
+        x = (x * 0xff51afd7ed558ccd) & M
+        x ^= x >> 33
+        x = (x * 0xc4ceb9fe1a85ec53) & M
+        x ^= x >> 33
+        out.append(((x & 0xffffffff) % n, (x >> 32) % n))
+    return np.array(out, dtype=np.int64)
+
+
+@pytest.mark.parametrize("d,ldy", [(256, 512), (61, 64), (61, 67), (5, 5)])
+def test_sample_sqdist_pairs(d, ldy):
+    """Sampled-pair distances behind the bracket (16-byte path when ldy % 4 == 0,
+    generic path otherwise; columns >= d are never read into the sum)."""
+    from dsvgd import _native as N
+    n, s, seed = 3000, 4099, 0x5EED5EED
+    rs = np.random.RandomState(d + ldy)
+    Yh = rs.randn(n, ldy).astype(np.float32)
+    Y = gpu(Yh)
+    out = torch.empty(s, dtype=torch.float32, device=DEV)
+    N.call("dsvgd_sample_sqdist", N.ptr(Y), ldy, n, d, s, seed, N.ptr(out), N.stream(DEV))
+    torch.cuda.synchronize()
+    ij = _sample_pairs(n, s, seed)
+    Yd = Yh[:, :d].astype(np.float64)
+    ref = ((Yd[ij[:, 0]] - Yd[ij[:, 1]]) ** 2).sum(1)
+    got = out.cpu().numpy().astype(np.float64)
+    assert np.abs(got - ref).max() <= 1e-5 * ref.max()
+
+
 @pytest.mark.parametrize("n,d,force_miss", [(4200, 100, False), (4200, 8, False),
                                              (4200, 100, True)])
 def test_bracketed_median_bit_exact(n, d, force_miss):
