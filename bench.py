@@ -98,6 +98,52 @@ def pmc_traffic(kernel_prefix):
     return None, None
 
 
+def passes(eng, stages, m, n, d, n_local):
+    """The other passes of the step, each against its own bound (north_star:
+    MFMA rate for the contractions, HBM GB/s for the distance and select
+    passes; the RBF exp is fused into phi_mm's A staging, no pass of its own).
+    The distance pass is credited the D entries its layout writes (upper
+    256-tiles only in the symmetric layout), 2d flop and 4 bytes each (the m*n
+    figure without symmetry credit rides along); the select passes the
+    candidate floats they read (bracketed) or D (radix passes over D)."""
+    out = {}
+    t = stages.get("sqdist")
+    if t:
+        if eng.sym:
+            tiles = -(-eng.n_pad // 256)
+            d_bytes = 4.0 * 256 * 256 * tiles * (tiles + 1) / 2
+        else:
+            d_bytes = 4.0 * m * eng.n_pad
+        # computed work: the tiles the layout writes, 2d flop per entry
+        tf = 2.0 * d * (d_bytes / 4.0) / (t * 1e-3) / 1e12
+        peak = PEAK_X3_TFLOPS if eng.x3_gram else PEAK_FP32_MFMA_TFLOPS
+        out["distances"] = {"ms": t, "bound": "mfma", "tflops": tf, "frac_mfma": tf / peak,
+                            "tflops_no_symmetry_credit": 2.0 * m * n * d / (t * 1e-3) / 1e12,
+                            "d_bytes_written": d_bytes,
+                            "write_gbs": d_bytes / (t * 1e-3) / 1e9,
+                            "frac_hbm": d_bytes / (t * 1e-3) / 1e9 / PEAK_HBM_GBS}
+    t = stages.get("radix_hist")
+    if t:
+        if eng.bracketed:
+            _, _, _, ncand, fb = eng.state.bracket()
+            nbytes = 4.0 * ncand if not fb else 4.0 * m * eng.n_pad
+            # stages average per launch: the bracketed select runs 3 candidate passes
+            out["select"] = {"ms_per_pass": t, "passes": 3, "candidates": int(ncand),
+                             "fallback": int(fb), "bytes_per_pass": nbytes,
+                             "read_gbs": nbytes / (t * 1e-3) / 1e9}
+        else:
+            nbytes = 4.0 * m * eng.n_pad
+            out["select"] = {"ms_per_pass": t, "passes": 2, "bytes_per_pass": nbytes,
+                             "read_gbs": nbytes / (t * 1e-3) / 1e9}
+    t = stages.get("scores")
+    if t:
+        tf = 4.0 * n * n_local * (d - 1) / (t * 1e-3) / 1e12
+        peak = (PEAK_X3_TFLOPS if os.environ.get("DSVGD_LOGREG_GEMM", "x3") == "x3"
+                else PEAK_FP32_MFMA_TFLOPS)
+        out["scores"] = {"ms": t, "bound": "mfma", "tflops": tf, "frac_mfma": tf / peak}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -171,7 +217,8 @@ def main():
 
     m = n // world
     phi_ms = stages["phi_mm"]
-    x3 = bool(sampler._engines[next(iter(sampler._engines))].x3)
+    eng = sampler._engines[next(iter(sampler._engines))]
+    x3 = bool(eng.x3)
     peak = PEAK_X3_TFLOPS if x3 else PEAK_FP32_MFMA_TFLOPS
     # the committed PMC summary is an N=1 profile: only quoted for the N=1 run
     # phi_mm is the NN tile with the fused exp (x3: <TN, DMA, EXP=true, ...>, f32: <TN, EXP=true, ...>);
@@ -211,8 +258,9 @@ def main():
                      "algorithmic_bytes": 4.0 * m * n + 4.0 * (n + 128) * 512,
                      "flop_per_launch": flops, "avg_launch_ms": phi_ms},
         "stages_ms": stages,
+        "passes": passes(eng, stages, m, n, d, per_data),
         "step_6n2d_f32_mfma_frac": (6.0 * m * n * d) / (el / args.steps) / 1e12 / PEAK_FP32_MFMA_TFLOPS,
-        "phi_splits": int(sampler._engines[next(iter(sampler._engines))].splits),
+        "phi_splits": int(eng.splits),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, d, xl, tl, args.cpu_budget)
