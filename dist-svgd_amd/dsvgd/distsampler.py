@@ -30,6 +30,14 @@ exactly as an assignment on the GPU (dsvgd.w2), and h * grad is added to every
 owned row's direction before the update.  previous particles = all n rows
 after the step when particles are exchanged, else the owned block (:202-205).
 
+Replicated data (all_particles with N_local == N_global, i.e. every rank
+holds the whole data set, the only reading under which the reference's
+N_global/N_local factor is 1): every rank's scores of a particle are the same
+numbers, so each rank scores only its owned block and the blocks are
+all-gathered (north_star's "all-gather of particles and scores"; SURVEY.md 5,
+8(e)) instead of every rank scoring all n particles (distsampler.py:94-99).
+`replicated=False` keeps the redundant per-rank scoring.
+
 Deviation: exchange_scores with num_shards == 1 uses the local scores (the
 reference reads an uninitialised buffer there).
 """
@@ -45,12 +53,13 @@ from .w2 import W2Term
 
 class DistSampler(object):
     timer = None   # optional engine.StageTimer (bench instrumentation)
+    keep_phi = False  # Jacobi: also write phi of the owned rows to the engine's `phi` (tests)
     graphs = True  # S = 1, no W2, built-in target: replay each step as a HIP graph
 
     def __init__(self, rank, num_shards, logp, kernel, particles,
                  N_local, N_global,
                  exchange_particles=True, exchange_scores=True, include_wasserstein=True,
-                 *, order="sequential", device=None, group=None):
+                 *, order="sequential", device=None, group=None, replicated=None):
         """Initializes a distributed SVGD sampler (distsampler.py:9-51)."""
         assert not (exchange_scores and not exchange_particles), \
             "must exchange particles to also exchange scores"
@@ -68,6 +77,11 @@ class DistSampler(object):
         self._include_wasserstein = include_wasserstein
         self._order = order
         self._group = group
+        if replicated is None:
+            replicated = N_local == N_global
+        # score all-gather: particles exchanged, scores not all-reduced, S > 1
+        self._replicated = bool(replicated and exchange_particles and not exchange_scores
+                                and num_shards > 1)
         self._target = resolve_target(logp)
         self._rbf = resolve_kernel(kernel, self._d)
 
@@ -153,6 +167,16 @@ class DistSampler(object):
         self._local_scores(self._work, self._scores)
         exchange.all_reduce_sum(self._scores, self._group)
 
+    def _gather_scores(self, Si):
+        """Owned blocks of Si -> every rank (replicated data; like the particle
+        all-gather, in place on RCCL)."""
+        s, e = self._particle_start_idx, self._particle_end_idx
+        if exchange.all_gather_in_place(Si, s, e, self._group):
+            return
+        out = torch.empty_like(Si)
+        exchange.all_gather_blocks(Si[s:e], out, self._group)
+        Si.copy_(out)
+
     def _score_buffer(self, shape):
         if self._sbuf is None or tuple(self._sbuf.shape) != tuple(shape):
             self._sbuf = torch.empty(shape, dtype=torch.float32, device=self._device)
@@ -204,18 +228,24 @@ class DistSampler(object):
         with span(self.timer, "scores"):
             if self._exchange_scores:
                 self._local_scores(X, Si)
+            elif self._replicated:                 # owned block only, gathered below
+                self._local_scores(X[s:e], Si[s:e], scale)
             else:
                 self._local_scores(Xi, Si, scale)
         side = main
-        if self._exchange_scores and S > 1:
+        if (self._exchange_scores or self._replicated) and S > 1:
             if jacobi:
                 if self._side is None:
                     self._side = torch.cuda.Stream(device=self._device)
                 side = self._side
                 side.wait_stream(main)
             with torch.cuda.stream(side):
-                with span(self.timer, "allreduce_scores"):
-                    exchange.all_reduce_sum(Si, self._group)
+                if self._exchange_scores:
+                    with span(self.timer, "allreduce_scores"):
+                        exchange.all_reduce_sum(Si, self._group)
+                else:
+                    with span(self.timer, "allgather_scores"):
+                        self._gather_scores(Si)
 
         w2g = None
         if self._include_wasserstein and self._previous_particles is not None:
@@ -233,7 +263,7 @@ class DistSampler(object):
             if side is not main:
                 main.wait_stream(side)
             eng.pack_scores(Si)                    # Si already carries the score scale
-            eng.direction(X[s:e], step_size, write_phi=False, extra=w2g)
+            eng.direction(X[s:e], step_size, write_phi=self.keep_phi, extra=w2g)
         else:
             if median:
                 eng = self._engine(n_int, e - s, s - lo)

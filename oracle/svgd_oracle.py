@@ -49,6 +49,10 @@ def score_logreg(X, x_train, t_train):
     X = np.asarray(X, np.float64)
     xd = np.asarray(x_train, np.float64)
     t = np.asarray(t_train, np.float64).reshape(-1)
+    rows = max(1, (1 << 27) // max(1, xd.shape[0]))      # bound the (rows, N) Z block
+    if X.shape[0] > rows:
+        return np.concatenate([score_logreg(X[s:s + rows], xd, t)
+                               for s in range(0, X.shape[0], rows)])
     a = np.exp(X[:, 0])
     W = X[:, 1:]
     p = W.shape[1]
@@ -70,15 +74,35 @@ def _sigmoid(u):
 
 
 # ------------------------------------------------------------- bandwidth --
+GRAM_MIN_WORK = 1 << 31
+
+
 def sqdist(Xr, X):
     """||x_i - x_j||^2 from explicit differences (as torch.dist**2 per pair),
-    chunked over rows to bound memory."""
+    chunked over rows to bound memory.  Large problems (rows * n * d >=
+    GRAM_MIN_WORK, e.g. 256 sampled rows of config E: 65536 x 1024) take the
+    fp64 Gram form of sqdist_gram instead, which a CPU test pins to this one."""
     Xr = np.asarray(Xr, np.float64)
     X = np.asarray(X, np.float64)
+    if Xr.shape[0] * X.size >= GRAM_MIN_WORK:
+        return sqdist_gram(Xr, X)
     out = np.empty((Xr.shape[0], X.shape[0]))
     step = max(1, (1 << 24) // max(1, X.size))
     for s in range(0, Xr.shape[0], step):
         out[s:s + step] = ((Xr[s:s + step, None, :] - X[None, :, :]) ** 2).sum(-1)
+    return out
+
+
+def sqdist_gram(Xr, X):
+    """fp64 ||a||^2 + ||b||^2 - 2 a.b about the column mean of X (translation
+    invariant), clamped at 0; fp64 keeps the
+    cancellation error ~1e-16 |x|^2, far below the 1e-5 fp32 tolerances."""
+    X = np.asarray(X, np.float64)
+    mu = X.mean(0)
+    A = np.asarray(Xr, np.float64) - mu
+    B = X - mu
+    out = (A * A).sum(1)[:, None] + (B * B).sum(1)[None, :] - 2.0 * (A @ B.T)
+    np.maximum(out, 0.0, out=out)
     return out
 
 
@@ -205,7 +229,8 @@ class DistOracle:
     """
 
     def __init__(self, particles, score_fns, N_local, N_global, exchange_particles,
-                 exchange_scores, h=1.0, sequential=True, include_wasserstein=False):
+                 exchange_scores, h=1.0, sequential=True, include_wasserstein=False,
+                 replicated=False):
         assert not (exchange_scores and not exchange_particles)
         self.S = len(particles)
         n = np.asarray(particles[0]).shape[0]
@@ -220,6 +245,10 @@ class DistOracle:
         self.start = [r * self.per for r in range(self.S)]
         self.w2 = include_wasserstein
         self.prev = [None] * self.S
+        # replicated data (all_particles, every rank holding the whole data
+        # set): each rank scores its owned block, the blocks are gathered --
+        # the same numbers as every rank scoring all n (identical score_fns)
+        self.replicated = replicated and exchange_particles and not exchange_scores and self.S > 1
 
     def own(self, r):
         return self.X[r][self.start[r]:self.start[r] + self.per]
@@ -235,6 +264,10 @@ class DistOracle:
             if self.xs:
                 tot = sum(self.score_fns[r](full) for r in range(S))
                 return [tot.copy() for _ in range(S)]
+            if self.replicated:
+                scale = self.N_global / self.N_local
+                g = np.concatenate([scale * self.score_fns[r](self.own(r)) for r in range(S)])
+                return [g.copy() for _ in range(S)]
             return None
         blocks = [self.own(r).copy() for r in range(S)]
         for r in range(S):
@@ -259,11 +292,18 @@ class DistOracle:
             if self.sequential:
                 for i in range(s0, s1):
                     Xi = Xr[lo:hi]
-                    Sj = scores[r][lo:hi] if self.xs else scale * self.score_fns[r](Xi)
+                    if self.xs:
+                        Sj = scores[r][lo:hi]
+                    elif self.replicated:        # gathered blocks frozen, owned rows current
+                        Sj = scores[r].copy()
+                        Sj[s0:s1] = scale * self.score_fns[r](Xr[s0:s1])
+                    else:
+                        Sj = scale * self.score_fns[r](Xi)
                     Xr[i] += step_size * (phi(Xi, Sj, self.h, rows=[i - lo])[0] + extra[i - s0])
             else:
                 Xi = Xr[lo:hi].copy()
-                Sj = scores[r][lo:hi] if self.xs else scale * self.score_fns[r](Xi)
+                Sj = scores[r][lo:hi] if (self.xs or self.replicated) else \
+                    scale * self.score_fns[r](Xi)
                 Xr[s0:s1] += step_size * (phi(Xi, Sj, self.h, rows=np.arange(s0 - lo, s1 - lo))
                                           + extra)
             if self.w2:

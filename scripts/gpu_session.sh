@@ -20,12 +20,11 @@ step() {  # name timeout cmd...
 for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step tests 1500 python -m pytest tests -m gpu -q ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} ;;
+    tests) step tests 1500 python -u -m pytest tests -m gpu -v -x --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} ;;
     bench) step bench 900 python bench.py --steps ${BSTEPS:-10} --warmup 3 ${BENCH_ARGS:-} ;;
     prof)  step prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     ab)    step ab 600 python scripts/ab_kernels.py ;;
     w2)    step w2 600 python scripts/w2_timing.py ${W2_ARGS:-} ;;
-    dbg)   step dbg 600 python scripts/debug_dist.py 6000 16 ;;
     diag)  step diag 600 python scripts/diag_precision.py ;;
     pmc)   step pmc 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmcclk) step pmcclk 900 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 --kernel-trace -d "$OUT/pmcclk" -o run --output-format csv -- python3 scripts/ab_kernels.py --rounds 1 ;;

@@ -1,0 +1,149 @@
+"""GPU parity at BASELINE.json's full configuration sizes:
+
+  C  synthetic Gaussian, n = 16384, d = 64, median h, one GPU
+  D  the bench's own DistSampler step: all_scores, Jacobi, median h,
+     logreg p = 255 on N = 16384 rows, n = 65536 (bench.py's inputs)
+  E  BNN-like, n = 65536, d = 1024: one of 8 ranks' share (m = 8192 rows at
+     row0 = 32768), and logreg scores at n = 8192, N = 8192, p = 1023
+
+At these sizes the oracle checks 256 sampled rows of phi in fp64 (north_star:
+1e-5 max-normalised per step), and the median through a size-independent
+property: counting the kernel's own D, below <= k < at_or_below with k =
+(n^2 - 1) // 2, then h == median / log n.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import record_parity
+from oracle import svgd_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+PHI_TOL = 1e-5
+
+
+def dsvgd():
+    import dsvgd as m
+    return m
+
+
+def gpu(a):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float32, device=DEV)
+
+
+def rel_err(got, ref):
+    e = float(np.abs(np.asarray(got, np.float64) - ref).max() / np.abs(ref).max())
+    record_parity(e)
+    return e
+
+
+def check_median_by_counting(eng, n):
+    med, h, _ = eng.state.read()
+    k = (n * n - 1) // 2
+    below = eng.count_D(lambda t: t < med)
+    at_or_below = eng.count_D(lambda t: t <= med)
+    assert below <= k < at_or_below, (below, k, at_or_below)
+    assert h == pytest.approx(med / math.log(n), rel=1e-6)
+    return med, h
+
+
+def check_step(ds, eng, X0, S_ref, eps, rows):
+    """phi of the sampled owned rows vs fp64, and the update X1 = X0 + eps phi."""
+    h = eng.state.read()[1]
+    ref = O.phi(X0, S_ref, h, rows=rows)
+    ridx = torch.as_tensor(rows, device=DEV)
+    phi = eng.phi[ridx].cpu().numpy().astype(np.float64)
+    assert rel_err(phi, ref) < PHI_TOL
+    X1 = ds.particles[ridx].cpu().numpy().astype(np.float64)
+    # X1 is the fp32 rounding of X0 + eps phi (one fma per entry)
+    ulp = np.spacing(np.abs(X1).astype(np.float32)).astype(np.float64)
+    assert np.all(np.abs(X1 - (X0[rows] + eps * phi)) <= 2 * ulp + 1e-30)
+    assert np.abs(X1 - (X0[rows] + eps * ref)).max() <= eps * PHI_TOL * np.abs(ref).max() + 2 * ulp.max()
+
+
+def test_config_C_gaussian_median_step():
+    """Config C through DistSampler (S = 1, Jacobi, RBF("median")): the
+    Gaussian target N(mu, diag(1/lam)), init N(0, I), eps = 1e-2."""
+    n, d, eps = 16384, 64, 1e-2
+    mu = np.random.RandomState(1).randn(d).astype(np.float32)
+    lam = np.random.RandomState(2).uniform(0.5, 2, d).astype(np.float32)
+    X0 = np.random.RandomState(0).randn(n, d).astype(np.float32)
+    ds = dsvgd().DistSampler(0, 1, dsvgd().targets.Gaussian(mu, lam), dsvgd().RBF("median"),
+                             gpu(X0), n, n, exchange_particles=False, exchange_scores=False,
+                             include_wasserstein=False, order="jacobi")
+    ds.keep_phi = True
+    ds.make_step(eps)
+    torch.cuda.synchronize()
+    eng = next(iter(ds._engines.values()))
+    check_median_by_counting(eng, n)
+    rows = np.sort(np.random.RandomState(3).choice(n, 256, replace=False))
+    check_step(ds, eng, X0, O.score_gaussian(X0, mu, lam), eps, rows)
+
+
+def test_config_D_bench_step():
+    """The bench's workload, one step on the bench's own inputs: DistSampler
+    all_scores (at S = 1: the local scores of all n particles), Jacobi,
+    median h, logreg p = 255 over N = 16384 rows, n = 65536, eps = 1e-4.
+    Scores of 256 sampled rows vs fp64; phi vs the fp64 restatement with the
+    fp64 scores of all n particles; the median by counting."""
+    from bench import synthetic_data
+    n, d, Ng, eps = 65536, 256, 16384, 1e-4
+    x, t = synthetic_data(Ng, d - 1)
+    gen = torch.Generator(device="cpu").manual_seed(0)
+    parts = 0.1 * torch.randn(n, d, generator=gen)
+    X0 = parts.numpy().copy()
+    ds = dsvgd().DistSampler(0, 1, dsvgd().targets.LogisticRegression(x, t), dsvgd().RBF("median"),
+                             parts.to(DEV), Ng, Ng, exchange_particles=True, exchange_scores=True,
+                             include_wasserstein=False, order="jacobi")
+    ds.keep_phi = True
+    ds.make_step(eps)
+    torch.cuda.synchronize()
+    eng = next(iter(ds._engines.values()))
+    assert eng.sym and eng.bracketed
+    check_median_by_counting(eng, n)
+    S_ref = O.score_logreg(X0, x, t)
+    rows = np.sort(np.random.RandomState(5).choice(n, 256, replace=False))
+    S_gpu = ds._scores[torch.as_tensor(rows, device=DEV)].cpu().numpy()
+    assert rel_err(S_gpu, S_ref[rows]) < PHI_TOL
+    check_step(ds, eng, X0, S_ref, eps, rows)
+
+
+def test_config_E_rank_share_phi():
+    """Config E, one of 8 ranks' share: rows [32768, 40960) of n = 65536
+    particles at d = 1024 against all n (non-symmetric row block whose
+    diagonal square is split from the rectangles beside it, split-K phi_mm),
+    fixed h near the median heuristic's value for these particles."""
+    n, d, m, row0 = 65536, 1024, 8192, 32768
+    rs = np.random.RandomState(8)
+    X = (0.1 * rs.randn(n, d)).astype(np.float32)
+    S = rs.randn(n, d).astype(np.float32)
+    h = 2.0 * d * 0.01 / math.log(n)
+    eng = dsvgd().PhiEngine(n, d, m=m, row0=row0, device=DEV)
+    assert not eng.sym and eng.splits > 1
+    Xo = gpu(X[row0:row0 + m])
+    eng.step(gpu(X), gpu(S), X_own=Xo, step=0.0, h=h)
+    torch.cuda.synchronize()
+    assert eng.state.read()[1] == pytest.approx(h, rel=1e-7)
+    sample = np.sort(np.random.RandomState(9).choice(m, 256, replace=False))
+    ref = O.phi(X, S, h, rows=row0 + sample)
+    got = eng.phi[torch.as_tensor(sample, device=DEV)].cpu().numpy()
+    assert rel_err(got, ref) < PHI_TOL
+    # the kernel matrix is far from the identity at this h (the test has teeth)
+    K = np.exp(-O.sqdist(X[row0 + sample[:8]], X) / h)
+    assert (K.sum(1) - 1.0).min() > 1e-3
+
+
+def test_config_E_logreg_scores():
+    """Config E's score GEMMs at a rank's share: n = 8192 particles of d = 1024
+    (p = 1023) on N = 8192 replicated data rows, vs the fp64 closed form."""
+    n, N, p = 8192, 8192, 1023
+    rs = np.random.RandomState(10)
+    X = (0.1 * rs.randn(n, p + 1)).astype(np.float32)
+    xd = (rs.randn(N, p) / np.sqrt(p)).astype(np.float32)
+    t = np.where(rs.randn(N) > 0, 1.0, -1.0).astype(np.float32)
+    out = torch.empty(n, p + 1, device=DEV)
+    dsvgd().targets.LogisticRegression(xd, t).score(gpu(X), out)
+    assert rel_err(out.cpu().numpy(), O.score_logreg(X, xd, t)) < PHI_TOL

@@ -118,3 +118,36 @@ def test_scores_match_autograd():
     ref = np.stack([_dlogp(lp, torch.tensor(X[i])).numpy() for i in range(7)])
     got = O.score_logreg(X, x, t)
     assert np.abs(got - ref).max() < 1e-4 * max(1.0, np.abs(ref).max())
+
+
+def test_sqdist_gram_form_matches_explicit_differences():
+    """The fp64 Gram form the oracle takes for large problems (sqdist_gram)
+    agrees with the explicit-difference form on the same inputs, including
+    particles far from the origin (the centring keeps it well conditioned)."""
+    rs = np.random.RandomState(4)
+    for n, d, off in ((300, 64, 0.0), (200, 1024, 0.0), (257, 17, 50.0)):
+        X = rs.randn(n, d) + off
+        rows = rs.choice(n, 40, replace=False)
+        a = O.sqdist_gram(X[rows], X)
+        b = ((X[rows][:, None, :] - X[None, :, :]) ** 2).sum(-1)
+        assert np.abs(a - b).max() <= 1e-11 * b.max()
+
+
+@pytest.mark.parametrize("S,sequential", [(2, True), (2, False), (4, False)])
+def test_replicated_score_gather_equals_redundant_scoring(S, sequential):
+    """Replicated data (all_particles, N_local == N_global): gathering the
+    owners' block scores is the same step as every rank scoring all n
+    particles (distsampler.py:94-99) when every rank holds the same data."""
+    rs = np.random.RandomState(S)
+    n, p = 16 * S, 3
+    x, t = rs.randn(40, p), np.sign(rs.randn(40))
+    init = [rs.randn(n, p + 1) * 0.5 for _ in range(S)]
+    fns = [lambda X: O.score_logreg(X, x, t)] * S
+    a = O.DistOracle(init, fns, 40, 40, True, False, sequential=sequential, replicated=True)
+    b = O.DistOracle(init, fns, 40, 40, True, False, sequential=sequential, replicated=False)
+    assert a.replicated and not b.replicated
+    for _ in range(3):
+        a.step(0.05)
+        b.step(0.05)
+    for r in range(S):
+        assert np.abs(a.X[r] - b.X[r]).max() < 1e-12
