@@ -15,8 +15,9 @@ Prints ONE JSON line (rank 0).  value = n*K / max-over-ranks wall time of the K
 timed steps (whole job).  roofline: the dominant kernel (phi_mm, the fused
 exp + K.[Xc|S] MFMA GEMM) -- algorithmic 4*m*n*d flop per launch / its mean
 HIP-event duration, against the ceiling of the engine it runs on: the
-fp32-accurate bf16-split engine (2516 TF bf16 dense / 6 products = 419 TF of
-fp32 products), or the 157.3 TF fp32 MFMA peak with DSVGD_PHI_GEMM=f32.  cpu_baseline: the
+fp32-accurate fp16-split engine FmtH2 (2516 TF fp16 dense / 3 products = 839
+TF of fp32 products; csrc/gemm_x3.hpp), the bf16-split FmtX3 (/ 6 = 419 TF) or
+the 157.3 TF fp32 MFMA peak (--gemm x3 / f32).  cpu_baseline: the
 reference algorithm's per-pair autograd loop (oracle/loop_baseline.py, a port)
 timed on this host on a bounded sample, rank 0 at N=1 only.
 """
@@ -39,9 +40,19 @@ PEAK_FP32_MFMA_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32,
 # phi_mm runs on v_mfma_f32_32x32x16_bf16 (1024 flop/clk/SIMD x 1024 SIMDs x
 # 2.4 GHz = 2516 TF dense) with six split products per fp32 product
 # (csrc/gemm_x3.hpp): the fp32-equivalent ceiling of that engine
-PEAK_BF16_MFMA_TFLOPS = 2516.6
-X3_PRODUCTS = 6
-PEAK_X3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / X3_PRODUCTS
+PEAK_BF16_MFMA_TFLOPS = 2516.6     # = the fp16 MFMA rate (same cycles)
+SPLIT_PRODUCTS = {"h2": 3, "x3": 6}
+PEAK_X3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / SPLIT_PRODUCTS["x3"]
+
+
+def engine_peak(gemm):
+    """fp32-product ceiling of an engine (TFLOP/s) and its basis."""
+    if gemm == "f32":
+        return PEAK_FP32_MFMA_TFLOPS, "f32 MFMA (v_mfma_f32_32x32x2_f32)"
+    k = SPLIT_PRODUCTS[gemm]
+    return (PEAK_BF16_MFMA_TFLOPS / k,
+            "%s dense MFMA %.1f TF / %d split products" % ("fp16" if gemm == "h2" else "bf16",
+                                                          PEAK_BF16_MFMA_TFLOPS, k))
 PEAK_HBM_GBS = 8000.0
 
 
@@ -98,7 +109,7 @@ def pmc_traffic(kernel_prefix):
     return None, None
 
 
-def passes(eng, stages, m, n, d, n_local):
+def passes(eng, stages, m, n, d, n_local, score_gemm):
     """The other passes of the step, each against its own bound (north_star:
     MFMA rate for the contractions, HBM GB/s for the distance and select
     passes; the RBF exp is fused into phi_mm's A staging, no pass of its own).
@@ -116,7 +127,7 @@ def passes(eng, stages, m, n, d, n_local):
             d_bytes = 4.0 * m * eng.n_pad
         # computed work: the tiles the layout writes, 2d flop per entry
         tf = 2.0 * d * (d_bytes / 4.0) / (t * 1e-3) / 1e12
-        peak = PEAK_X3_TFLOPS if eng.x3_gram else PEAK_FP32_MFMA_TFLOPS
+        peak = engine_peak(eng.gram_gemm)[0]
         out["distances"] = {"ms": t, "bound": "mfma", "tflops": tf, "frac_mfma": tf / peak,
                             "tflops_no_symmetry_credit": 2.0 * m * n * d / (t * 1e-3) / 1e12,
                             "d_bytes_written": d_bytes,
@@ -138,8 +149,7 @@ def passes(eng, stages, m, n, d, n_local):
     t = stages.get("scores")
     if t:
         tf = 4.0 * n * n_local * (d - 1) / (t * 1e-3) / 1e12
-        peak = (PEAK_X3_TFLOPS if os.environ.get("DSVGD_LOGREG_GEMM", "x3") == "x3"
-                else PEAK_FP32_MFMA_TFLOPS)
+        peak = engine_peak(score_gemm)[0]
         out["scores"] = {"ms": t, "bound": "mfma", "tflops": tf, "frac_mfma": tf / peak}
     return out
 
@@ -155,6 +165,8 @@ def main():
     ap.add_argument("--data-rows", type=int, default=16384, help="global data rows")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gemm", default="h2", choices=["h2", "x3", "f32"],
+                    help="MFMA engine of the contractions (h2: fp16 split, the default)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: CPU-staged rehearsal of the multi-rank path (e.g. 2 ranks on 1 GPU)")
     args = ap.parse_args()
@@ -182,7 +194,8 @@ def main():
     xl, tl = x[rank * per_data:(rank + 1) * per_data], t[rank * per_data:(rank + 1) * per_data]
     gen = torch.Generator(device="cpu").manual_seed(0)
     parts = (0.1 * torch.randn(n, d, generator=gen)).to(dev)
-    sampler = dsvgd.DistSampler(rank, world, dsvgd.targets.LogisticRegression(xl, tl),
+    dsvgd.PhiEngine.DEFAULT_GEMM = args.gemm
+    sampler = dsvgd.DistSampler(rank, world, dsvgd.targets.LogisticRegression(xl, tl, gemm=args.gemm),
                                 dsvgd.RBF("median"), parts, per_data, per_data * world,
                                 exchange_particles=True, exchange_scores=True,
                                 include_wasserstein=False, order="jacobi")
@@ -218,12 +231,14 @@ def main():
     m = n // world
     phi_ms = stages["phi_mm"]
     eng = sampler._engines[next(iter(sampler._engines))]
-    x3 = bool(eng.x3)
-    peak = PEAK_X3_TFLOPS if x3 else PEAK_FP32_MFMA_TFLOPS
+    gemm = eng.phi_gemm
+    peak, peak_basis = engine_peak(gemm)
     # the committed PMC summary is an N=1 profile: only quoted for the N=1 run
-    # phi_mm is the NN tile with the fused exp (x3: <TN, DMA, EXP=true, ...>, f32: <TN, EXP=true, ...>);
+    # phi_mm is the NN tile with the fused exp (<TN, DMA, EXP=true, ..., Fmt>);
     # the logreg G.Xd launch is the same tile with EXP=false
-    kname = "void dsvgd::nn_x3_kernel<4, true, true," if x3 else "void dsvgd::nn_kernel<4, true,"
+    kname = {"h2": "void dsvgd::nn_x3_kernel<4, true, true, false, 2, dsvgd::FmtH2>",
+             "x3": "void dsvgd::nn_x3_kernel<4, true, true, true, 2, dsvgd::FmtX3>",
+             "f32": "void dsvgd::nn_kernel<4, true,"}[gemm]
     traffic, traffic_src = pmc_traffic(kname) if world == 1 else (None, None)
     flops = 4.0 * m * n * d
     achieved = flops / (phi_ms * 1e-3) / 1e12
@@ -245,20 +260,21 @@ def main():
                    "n": n, "d": d, "N_global": Ng, "parallelism": "dp%d" % world,
                    "particles_per_gpu": m},
         "roofline": {"bound": "mfma",
-                     "kernel": ("phi_mm (nn_x3_kernel<4>: fp32-accurate 3-way bf16 split, "
-                                "6 bf16 MFMA products per fp32 product)") if x3 else
-                               "phi_mm (nn_kernel<4,true>: f32 MFMA)",
+                     "kernel": {"h2": "phi_mm (nn_x3_kernel<4, FmtH2>: fp32-accurate 2-part fp16 "
+                                      "split, 3 fp16 MFMA products per fp32 product)",
+                                "x3": "phi_mm (nn_x3_kernel<4, FmtX3>: fp32-accurate 3-part bf16 "
+                                      "split, 6 bf16 MFMA products per fp32 product)",
+                                "f32": "phi_mm (nn_kernel<4,true>: f32 MFMA)"}[gemm],
                      "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                     "peak_basis": ("bf16 dense MFMA %.1f TF / %d split products" %
-                                    (PEAK_BF16_MFMA_TFLOPS, X3_PRODUCTS)) if x3 else
-                                   "f32 MFMA (v_mfma_f32_32x32x2_f32)",
+                     "peak_basis": peak_basis,
                      "frac": achieved / peak, "frac_of_f32_mfma_peak": achieved / PEAK_FP32_MFMA_TFLOPS,
                      "traffic": traffic,
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                      "algorithmic_bytes": 4.0 * m * n + 4.0 * (n + 128) * 512,
                      "flop_per_launch": flops, "avg_launch_ms": phi_ms},
         "stages_ms": stages,
-        "passes": passes(eng, stages, m, n, d, per_data),
+        "passes": passes(eng, stages, m, n, d, per_data, args.gemm),
+        "gemm": gemm,
         "step_6n2d_f32_mfma_frac": (6.0 * m * n * d) / (el / args.steps) / 1e12 / PEAK_FP32_MFMA_TFLOPS,
         "phi_splits": int(eng.splits),
     }

@@ -54,6 +54,80 @@ __device__ __forceinline__ Split3 split3(float v) {
 constexpr int kX3Parts = 3;
 constexpr int kX3Step = 16;  // K-step (columns of D / rows of Y)
 
+// ---- split formats: how an fp32 operand becomes MFMA inputs -------------
+// FmtX3: three bf16 parts, six products a_i b_j (i + j <= 2).
+// FmtH2: two fp16 parts of the operand scaled by a power of two,
+//     s v = v0 + v1 (+ r, |r| <= 2^-22 |s v|),  v0 = f16(s v), v1 = f16(s v - v0),
+// and the three products a0 b0 + a0 b1 + a1 b0 (each exact in fp32: 11 x 11
+// significant bits; the dropped a1 b1 is <= 2^-22 |a b|).  The power-of-two
+// scale s puts the operand's largest magnitude in [2^14, 2^15) (fp16's
+// normal range spans 2^-14 .. 65504), so every element within 2^-18 of it
+// keeps 22 significant bits; the caller divides the scale back out of the
+// fp32 result exactly.  Half the MFMAs of FmtX3 at the same fp32-level
+// error (a GEMM's own fp32 accumulation rounding dominates both).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+struct FmtX3 {
+  using E = __bf16;
+  using V8 = bf16x8;
+  using V4 = bf16x4;
+  static constexpr int P = 3;
+  static constexpr float kAScale = 1.f;        // A operand (K, G) staging scale
+  static constexpr float kAScaleLog2 = 0.f;
+};
+struct FmtH2 {
+  using E = _Float16;
+  using V8 = f16x8;
+  using V4 = f16x4;
+  static constexpr int P = 2;
+  static constexpr float kAScale = 32768.f;    // |K| <= 1, |G| <= 1  ->  < 2^15
+  static constexpr float kAScaleLog2 = 15.f;
+};
+
+// 32x32x16 MFMA of the format (C layout of mfma_bf16)
+template <class F>
+__device__ __forceinline__ f32x16 mfma_fmt(typename F::V8 a, typename F::V8 b, f32x16 c) {
+  if constexpr (F::P == 3)
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// the P parts of v (already scaled for FmtH2)
+template <class F>
+__device__ __forceinline__ void split_fmt(float v, typename F::E (&o)[F::P]) {
+  if constexpr (F::P == 3) {
+    const Split3 s = split3(v);
+    o[0] = s.s0;
+    o[1] = s.s1;
+    o[2] = s.s2;
+  } else {
+    o[0] = (_Float16)v;
+    o[1] = (_Float16)(v - (float)o[0]);
+  }
+}
+
+// products of one K-step into acc: small terms first
+template <class F, int TM>
+__device__ __forceinline__ void mfma_products(const typename F::V8 (&a)[TM][F::P],
+                                              const typename F::V8 (&b)[F::P], f32x16* acc) {
+  if constexpr (F::P == 3) {
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) acc[mi] = mfma_fmt<F>(a[mi][2], b[0], acc[mi]);
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) acc[mi] = mfma_fmt<F>(a[mi][1], b[1], acc[mi]);
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) acc[mi] = mfma_fmt<F>(a[mi][0], b[2], acc[mi]);
+  }
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) acc[mi] = mfma_fmt<F>(a[mi][1], b[0], acc[mi]);
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) acc[mi] = mfma_fmt<F>(a[mi][0], b[1], acc[mi]);
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) acc[mi] = mfma_fmt<F>(a[mi][0], b[0], acc[mi]);
+}
+
 // byte offset of (row or column x, 16-B half h) inside a part image
 __device__ __forceinline__ int x3_off(int x, int h) { return x * 32 + ((h ^ ((x >> 3) & 1)) << 4); }
 
@@ -85,8 +159,11 @@ __device__ __forceinline__ int x3_off(int x, int h) { return x * 32 + ((h ^ ((x 
 // blocks (phi_mm); RW = 4 (DMA, EXP = false only): 256-row blocks staging two
 // D panels per K-step -- twice the MFMAs per B image (logreg G . Xd, where the
 // B side is only 256 columns wide).
-template <int TN, bool DMA = true, bool EXP = true, bool M16 = false, int RW = 2>
+template <int TN, bool DMA = true, bool EXP = true, bool M16 = false, int RW = 2, class F = FmtX3>
 struct NNX3Tile {
+  static constexpr int P = F::P;
+  using V8 = typename F::V8;
+  static_assert(!M16 || P == 3, "the 16x16x32 concatenated-k form is the 3-part format's");
   // (DMA needs the same DMA count in every wave: whole 512-chunk rounds)
   static constexpr int kThreads = 512;
   static constexpr int TM = 2;
@@ -96,8 +173,8 @@ struct NNX3Tile {
   static constexpr int BC = kCW * 32 * TN;
   static_assert(RW == 2 || (RW == 4 && DMA && !EXP), "256-row blocks: DMA path, no exp");
   static constexpr int BJ = kX3Step;
-  static constexpr int SA = kX3Parts * BM * 32;  // bytes of one stage's A image
-  static constexpr int SB = kX3Parts * BC * 32;
+  static constexpr int SA = P * BM * 32;  // bytes of one stage's A image
+  static constexpr int SB = P * BC * 32;
   static constexpr int kStage = SA + SB;
   static constexpr int kSmemBytes = 2 * kStage + (DMA ? 2 * AR * kPanelElems * 4 : 0);
   static constexpr int kBChunks = SB / 16;
@@ -113,11 +190,11 @@ struct NNX3Tile {
   int64_t prow = 0;  // RW = 4: bytes between the block's two D panel rows
   u32x4 rb[DMA ? 1 : LB];
   float rs;
-  bf16x8 a[TM][kX3Parts];
+  V8 a[TM][P];
 
   // A: thread t stages row t >> 2, columns 4 (t & 3) .. +3 of the D panel.
   // B: 16-B chunk f = t + 512 u of the block's K-step image (part f / (2 BC)).
-  __device__ __forceinline__ void load(const float* __restrict__ Apanels, const __bf16* __restrict__ Yx,
+  __device__ __forceinline__ void load(const float* __restrict__ Apanels, const typename F::E* __restrict__ Yx,
                                        int64_t ldy, int64_t j0) {
     const int t = threadIdx.x;
     const __amdgpu_buffer_rsrc_t rA =
@@ -125,7 +202,7 @@ struct NNX3Tile {
     const __amdgpu_buffer_rsrc_t rB =
         __builtin_amdgcn_make_buffer_rsrc((void*)Yx, (short)0, 0x7fffffff, 0x00020000);
     const int soA = (int)((j0 >> 4) * kPanelElems * 4);
-    const int soB = (int)((j0 >> 4) * kX3Parts * ldy * 32);
+    const int soB = (int)((j0 >> 4) * P * ldy * 32);
     ra = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rA, t * 16, soA, 0));
 #pragma unroll
     for (int u = 0; u < LB; ++u) {
@@ -153,28 +230,34 @@ struct NNX3Tile {
   // of panel a (image rows 128 a + ...)
   __device__ __forceinline__ void store_a(char* st, float scale, int64_t dgl, int a = 0) {
     const int t = threadIdx.x, row = (t >> 2) + 128 * a, c4 = t & 3;
+    // FmtH2: K scaled by 2^15 inside the exp2 (row sums too: the kernel's
+    // epilogue divides it back out), G by 2^15 (exact)
     if (!EXP) {
+      if constexpr (F::kAScale != 1.f) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ra[q] *= F::kAScale;
+      }
     } else if (dgl > -BM && dgl < BJ) {  // the K-step holds diagonal entries (NNTile::store)
       const int qd = (int)dgl + row - 4 * c4;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) ra[q] = (qd == q) ? 0.f : __builtin_amdgcn_exp2f(ra[q] * scale);
+      for (int q = 0; q < 4; ++q)
+        ra[q] = (qd == q) ? 0.f : __builtin_amdgcn_exp2f(fmaf(ra[q], scale, F::kAScaleLog2));
     } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) ra[q] = __builtin_amdgcn_exp2f(ra[q] * scale);
+      for (int q = 0; q < 4; ++q) ra[q] = __builtin_amdgcn_exp2f(fmaf(ra[q], scale, F::kAScaleLog2));
     }
     if (EXP) rs += (ra[0] + ra[1]) + (ra[2] + ra[3]);
-    bf16x4 s0, s1, s2;
+    typename F::V4 sp[P];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const Split3 v = split3(ra[q]);
-      s0[q] = v.s0;
-      s1[q] = v.s1;
-      s2[q] = v.s2;
+      typename F::E v[P];
+      split_fmt<F>(ra[q], v);
+#pragma unroll
+      for (int p = 0; p < P; ++p) sp[p][q] = v[p];
     }
     const int off = (M16 ? row * 32 + ((c4 >> 1) << 4) : x3_off(row, c4 >> 1)) + ((c4 & 1) << 3);
-    *reinterpret_cast<bf16x4*>(st + off) = s0;
-    *reinterpret_cast<bf16x4*>(st + BM * 32 + off) = s1;
-    *reinterpret_cast<bf16x4*>(st + 2 * BM * 32 + off) = s2;
+#pragma unroll
+    for (int p = 0; p < P; ++p) *reinterpret_cast<typename F::V4*>(st + p * BM * 32 + off) = sp[p];
   }
 
   // ---- DMA path: both operands by LDS-DMA (buffer_load_dwordx4 ... lds:
@@ -201,7 +284,7 @@ struct NNX3Tile {
   __device__ __forceinline__ void dma_b(char* st, __amdgpu_buffer_rsrc_t rB, int64_t ldy,
                                         int64_t j0) {
     const int t = threadIdx.x, wbase = t & ~63;
-    const int soB = (int)((j0 >> 4) * kX3Parts * ldy * 32);
+    const int soB = (int)((j0 >> 4) * P * ldy * 32);
 #pragma unroll
     for (int u = 0; u < LB; ++u) {
       const int f = t + u * kThreads, p = f / (2 * BC), rem = f % (2 * BC);
@@ -281,9 +364,9 @@ struct NNX3Tile {
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-      for (int p = 0; p < kX3Parts; ++p)
-        a[mi][p] = *reinterpret_cast<const bf16x8*>(st + p * BM * 32 +
-                                                     x3_off(wr * 32 * TM + mi * 32 + r, h));
+      for (int p = 0; p < P; ++p)
+        a[mi][p] = *reinterpret_cast<const V8*>(st + p * BM * 32 +
+                                                x3_off(wr * 32 * TM + mi * 32 + r, h));
   }
 
   // column tiles [N0, N1) of this wave
@@ -315,24 +398,18 @@ struct NNX3Tile {
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
 #pragma unroll
     for (int ni = N0; ni < N1; ++ni) {
-      bf16x8 b[kX3Parts];
+      V8 b[P];
 #pragma unroll
-      for (int p = 0; p < kX3Parts; ++p)
-        b[p] = *reinterpret_cast<const bf16x8*>(st + SA + p * BC * 32 +
-                                                x3_off(wc * 32 * TN + ni * 32 + r, h));
+      for (int p = 0; p < P; ++p)
+        b[p] = *reinterpret_cast<const V8*>(st + SA + p * BC * 32 +
+                                            x3_off(wc * 32 * TN + ni * 32 + r, h));
       // small terms first; the two row tiles interleaved (independent chains)
+      f32x16 c[TM];
 #pragma unroll
-      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][2], b[0], acc[mi][ni]);
+      for (int mi = 0; mi < TM; ++mi) c[mi] = acc[mi][ni];
+      mfma_products<F, TM>(a, b, c);
 #pragma unroll
-      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][1], b[1], acc[mi][ni]);
-#pragma unroll
-      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][0], b[2], acc[mi][ni]);
-#pragma unroll
-      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][1], b[0], acc[mi][ni]);
-#pragma unroll
-      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][0], b[1], acc[mi][ni]);
-#pragma unroll
-      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][0], b[0], acc[mi][ni]);
+      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = c[mi];
     }
   }
 
@@ -344,7 +421,7 @@ struct NNX3Tile {
 
   // Apanels: the block's 128-row panel row (panel layout); Yx: the split Y
   // image offset to the block's first column; K range [k0, k1) (multiples of 16).
-  __device__ __forceinline__ void run(const float* __restrict__ Apanels, const __bf16* __restrict__ Yx,
+  __device__ __forceinline__ void run(const float* __restrict__ Apanels, const typename F::E* __restrict__ Yx,
                                       int64_t ldy, int64_t k0, int64_t k1, float scale, char* smem,
                                       int64_t row_g0) {
     const int w = threadIdx.x >> 6, wr = w / kCW, wc = w % kCW;
@@ -395,7 +472,7 @@ struct NNX3Tile {
   }
 
   template <int CUR>
-  __device__ __forceinline__ void step(const float* __restrict__ Apanels, const __bf16* __restrict__ Yx,
+  __device__ __forceinline__ void step(const float* __restrict__ Apanels, const typename F::E* __restrict__ Yx,
                                        int64_t ldy, int64_t j0, int64_t k1, float scale, char* smem,
                                        int64_t row_g0, int wr, int wc) {
     const char* cur = smem + CUR * kStage;
@@ -462,17 +539,20 @@ struct NNX3Tile {
 // NS: ring stages (3: a DMA has two iterations to land; 2: one, at 2/3 of the LDS).
 // M16: v_mfma_f32_16x16x32_bf16 with concatenated k (NNX3Tile); the results
 // are in acc16[4][2 TN] (16x16 layout) and both images must be unswizzled.
-template <int TM, int TN, int WM, int WN, int NS = 3, bool M16 = false>
+template <int TM, int TN, int WM, int WN, int NS = 3, bool M16 = false, class F = FmtX3>
 struct NTX3Tile {
   static constexpr int TM_ = TM, TN_ = TN, WM_ = WM, WN_ = WN;
   static constexpr bool M16_ = M16;
+  static constexpr int P = F::P;
+  using V8 = typename F::V8;
   static_assert(!M16 || TM == 2, "M16: 64-row waves");
+  static_assert(!M16 || P == 3, "the 16x16x32 concatenated-k form is the 3-part format's");
   static constexpr int kThreads = 64 * WM * WN;
   static constexpr int BM = 32 * TM * WM;
   static constexpr int BN = 32 * TN * WN;
   static constexpr int BK = kX3Step;
-  static constexpr int SA = kX3Parts * BM * 32;
-  static constexpr int SB = kX3Parts * BN * 32;
+  static constexpr int SA = P * BM * 32;
+  static constexpr int SB = P * BN * 32;
   static constexpr int kStage = SA + SB;
   static constexpr int kStages = NS;
   static_assert(NS == 2 || NS == 3, "2- or 3-stage ring");
@@ -514,7 +594,7 @@ struct NTX3Tile {
   __device__ __forceinline__ void dma(char* st, __amdgpu_buffer_rsrc_t rA, int64_t mA,
                                       __amdgpu_buffer_rsrc_t rB, int64_t mB, int64_t kb) {
     const int t = threadIdx.x, wbase = t & ~63;
-    const int soA = (int)(kb * kX3Parts * mA * 32), soB = (int)(kb * kX3Parts * mB * 32);
+    const int soA = (int)(kb * P * mA * 32), soB = (int)(kb * P * mB * 32);
 #pragma unroll
     for (int u = 0; u < LA; ++u) {
       const int f = t + u * kThreads, pp = f / (BM * 2), in = f % (BM * 2);
@@ -558,34 +638,27 @@ struct NTX3Tile {
       return;
     }
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-    bf16x8 a[TM][kX3Parts];
+    V8 a[TM][P];
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
       const int lr = wm * 32 * TM + mi * 32 + r;
       const int off = lr * 32 + ((h ^ (((a0 + lr) >> 3) & 1)) << 4);
 #pragma unroll
-      for (int p = 0; p < kX3Parts; ++p)
-        a[mi][p] = *reinterpret_cast<const bf16x8*>(st + p * BM * 32 + off);
+      for (int p = 0; p < P; ++p) a[mi][p] = *reinterpret_cast<const V8*>(st + p * BM * 32 + off);
     }
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
-      bf16x8 b[kX3Parts];
+      V8 b[P];
 #pragma unroll
-      for (int p = 0; p < kX3Parts; ++p)
-        b[p] = *reinterpret_cast<const bf16x8*>(st + SA + p * BN * 32 +
-                                                x3_off(wn * 32 * TN + ni * 32 + r, h));
+      for (int p = 0; p < P; ++p)
+        b[p] = *reinterpret_cast<const V8*>(st + SA + p * BN * 32 +
+                                            x3_off(wn * 32 * TN + ni * 32 + r, h));
+      f32x16 c[TM];
 #pragma unroll
-      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][2], b[0], acc[mi][ni]);
+      for (int mi = 0; mi < TM; ++mi) c[mi] = acc[mi][ni];
+      mfma_products<F, TM>(a, b, c);
 #pragma unroll
-      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][1], b[1], acc[mi][ni]);
-#pragma unroll
-      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][0], b[2], acc[mi][ni]);
-#pragma unroll
-      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][1], b[0], acc[mi][ni]);
-#pragma unroll
-      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][0], b[1], acc[mi][ni]);
-#pragma unroll
-      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = mfma_bf16(a[mi][0], b[0], acc[mi][ni]);
+      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = c[mi];
     }
   }
 

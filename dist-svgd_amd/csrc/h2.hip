@@ -1,0 +1,228 @@
+// h2.hip -- operand preparation of the FmtH2 split engine (gemm_x3.hpp):
+// power-of-two scales and the two-part fp16 images.
+//
+// An operand v is fed to the fp16 MFMA as s v = v0 + v1 (v0 = f16(s v),
+// v1 = f16(s v - v0)), s a power of two that puts the operand's largest
+// magnitude in [2^14, 2^15): per COLUMN for the B operand of the NN engine
+// (phi_mm's Y = [Xc | S], logreg's Xd) -- a column's scale divides out of the
+// same output column -- and per TENSOR for the row images of the NT engine
+// (the Gram's Xc, logreg's W and Xd), whose scales divide out of every entry.
+// HBM passes, O(rows x cols): ~0.1 ms at n = 65536, d = 256.
+#include <cmath>
+
+#include "common.hpp"
+#include "gemm_x3.hpp"
+
+namespace dsvgd {
+
+constexpr int kScaleRows = 512;  // rows per partial-max block
+
+// partial[b][c] = max |A[r][c]| over rows r of block b, as the bit pattern of
+// |v| (unsigned order: finite < inf < NaN, so a NaN or inf is carried through)
+// -- 64-column stripes, 4 row groups of 64 lanes, four loads in flight per lane.
+__device__ __forceinline__ uint32_t abs_bits(float v) {
+  return __float_as_uint(v) & 0x7fffffffu;
+}
+
+__global__ __launch_bounds__(256) void colmax_partial_kernel(const float* __restrict__ A,
+                                                             int64_t lda, int64_t rows,
+                                                             int64_t cols,
+                                                             uint32_t* __restrict__ partial) {
+  __shared__ uint32_t red[4][64];
+  const int64_t c = (int64_t)blockIdx.y * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * kScaleRows, r1 = min(r0 + kScaleRows, rows);
+  uint32_t m0 = 0u, m1 = 0u, m2 = 0u, m3 = 0u;
+  if (c < cols) {
+    int64_t r = r0 + rg;
+    for (; r + 12 < r1; r += 16) {
+      m0 = max(m0, abs_bits(A[r * lda + c]));
+      m1 = max(m1, abs_bits(A[(r + 4) * lda + c]));
+      m2 = max(m2, abs_bits(A[(r + 8) * lda + c]));
+      m3 = max(m3, abs_bits(A[(r + 12) * lda + c]));
+    }
+    for (; r < r1; r += 4) m0 = max(m0, abs_bits(A[r * lda + c]));
+  }
+  red[rg][threadIdx.x & 63] = max(max(m0, m1), max(m2, m3));
+  __syncthreads();
+  if (rg == 0 && c < cols)
+    partial[(int64_t)blockIdx.x * cols + c] =
+        max(max(red[0][threadIdx.x], red[1][threadIdx.x]),
+            max(red[2][threadIdx.x], red[3][threadIdx.x]));
+}
+
+// power-of-two scale of a column whose largest magnitude is m: s m in
+// [2^14, 2^15); 1 for an all-zero or non-finite column (NaN / inf propagate)
+__device__ __forceinline__ float pow2_scale(float m) {
+  if (!(m > 0.f) || !isfinite(m)) return 1.f;
+  int e;
+  frexpf(m, &e);                        // m in [2^(e-1), 2^e)
+  return ldexpf(1.f, min(15 - e, 100));  // s m in [2^14, 2^15)
+}
+
+// one block: out[c] = s_c, out[cols + c] = 1 / s_c; out[2 cols] = t = the
+// smallest s_c over the nonzero finite columns (1 if any column is not
+// finite, or none is nonzero), out[2 cols + 1] = 1 / t
+__global__ __launch_bounds__(256) void colscale_final_kernel(const uint32_t* __restrict__ partial,
+                                                             int64_t nb, int64_t cols,
+                                                             float* __restrict__ out) {
+  __shared__ float red[256];
+  __shared__ int bad[256];
+  float tmin = INFINITY;
+  int nonfinite = 0;
+  for (int64_t c = threadIdx.x; c < cols; c += 256) {
+    uint32_t mb = 0u;
+    for (int64_t b = 0; b < nb; ++b) mb = max(mb, partial[b * cols + c]);
+    const float m = __uint_as_float(mb);
+    const float s = pow2_scale(m);
+    out[c] = s;
+    out[cols + c] = 1.f / s;
+    if (!isfinite(m)) nonfinite = 1;
+    else if (m > 0.f) tmin = fminf(tmin, s);
+  }
+  red[threadIdx.x] = tmin;
+  bad[threadIdx.x] = nonfinite;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      red[threadIdx.x] = fminf(red[threadIdx.x], red[threadIdx.x + o]);
+      bad[threadIdx.x] |= bad[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float t = (bad[0] || !isfinite(red[0])) ? 1.f : red[0];
+    out[2 * cols] = t;
+    out[2 * cols + 1] = 1.f / t;
+  }
+}
+
+// Yh[kstep][part][column][16 k] = the two fp16 parts of s_c Y[16 kstep + k][c]
+// (16-B halves swapped on columns with bit 3 set: the 32x32x16 image)
+__global__ __launch_bounds__(256) void ysplit_h2_kernel(const float* __restrict__ Y, int64_t ldy,
+                                                        int64_t ksteps,
+                                                        const float* __restrict__ colscale,
+                                                        _Float16* __restrict__ Yh) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= ksteps * ldy) return;
+  const int64_t kb = t / ldy, c = t % ldy;
+  const float sc = colscale[c];
+  f16x8 s[2][2];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    _Float16 v[2];
+    split_fmt<FmtH2>(sc * Y[(kb * 16 + k) * ldy + c], v);
+    s[0][k >> 3][k & 7] = v[0];
+    s[1][k >> 3][k & 7] = v[1];
+  }
+  const int sw = (int)((c >> 3) & 1);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    _Float16* dst = Yh + ((kb * 2 + p) * ldy + c) * 16;
+    *reinterpret_cast<f16x8*>(dst + 8 * sw) = s[p][0];
+    *reinterpret_cast<f16x8*>(dst + 8 * (sw ^ 1)) = s[p][1];
+  }
+}
+
+// img[kstep][part][row][16 k] = the two fp16 parts of t A[row][16 kstep + k]
+// (t = *tscale; zero outside rows x cols; halves swapped on rows with bit 3 set)
+__global__ __launch_bounds__(256) void rowsplit_h2_kernel(const float* __restrict__ A,
+                                                          int64_t lda, int64_t rows, int64_t cols,
+                                                          int64_t rows_pad, int64_t ksteps,
+                                                          const float* __restrict__ tscale,
+                                                          _Float16* __restrict__ img) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= ksteps * rows_pad) return;
+  const int64_t kb = t / rows_pad, i = t % rows_pad;
+  const float sc = *tscale;
+  f16x8 s[2][2];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int64_t c = kb * 16 + k;
+    _Float16 v[2];
+    split_fmt<FmtH2>((i < rows && c < cols) ? sc * A[i * lda + c] : 0.f, v);
+    s[0][k >> 3][k & 7] = v[0];
+    s[1][k >> 3][k & 7] = v[1];
+  }
+  const int sw = (int)((i >> 3) & 1);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    _Float16* dst = img + ((kb * 2 + p) * rows_pad + i) * 16;
+    *reinterpret_cast<f16x8*>(dst + 8 * sw) = s[p][0];
+    *reinterpret_cast<f16x8*>(dst + 8 * (sw ^ 1)) = s[p][1];
+  }
+}
+
+size_t h2_colscale_ws_floats(int64_t rows, int64_t cols) {
+  return (size_t)((rows + kScaleRows - 1) / kScaleRows) * (size_t)(cols < 1 ? 1 : cols);
+}
+
+int h2_colscale(const float* A, int64_t lda, int64_t rows, int64_t cols, float* ws, float* out,
+                hipStream_t s) {
+  const int64_t nb = (rows + kScaleRows - 1) / kScaleRows;
+  uint32_t* part = reinterpret_cast<uint32_t*>(ws);
+  hipLaunchKernelGGL(colmax_partial_kernel, dim3((unsigned)nb, (unsigned)((cols + 63) / 64)),
+                     dim3(256), 0, s, A, lda, rows, cols, part);
+  int rc = check_launch("colmax_partial");
+  if (rc) return rc;
+  hipLaunchKernelGGL(colscale_final_kernel, dim3(1), dim3(256), 0, s, part, nb, cols, out);
+  return check_launch("colscale_final");
+}
+
+int h2_ysplit(const float* Y, int64_t ldy, int64_t rows, const float* colscale, void* Yh,
+              hipStream_t s) {
+  const int64_t ksteps = rows / kX3Step, threads = ksteps * ldy;
+  hipLaunchKernelGGL(ysplit_h2_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, Y,
+                     ldy, ksteps, colscale, (_Float16*)Yh);
+  return check_launch("ysplit_h2");
+}
+
+int h2_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                int64_t kpad, const float* tscale, void* img, hipStream_t s) {
+  const int64_t ksteps = kpad / kX3Step, threads = ksteps * rows_pad;
+  hipLaunchKernelGGL(rowsplit_h2_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+                     A, lda, rows, cols, rows_pad, ksteps, tscale, (_Float16*)img);
+  return check_launch("rowsplit_h2");
+}
+
+}  // namespace dsvgd
+
+using namespace dsvgd;
+
+extern "C" {
+
+size_t dsvgd_h2_colscale_workspace_floats(int64_t rows, int64_t cols) {
+  return h2_colscale_ws_floats(rows, cols);
+}
+
+int dsvgd_h2_colscale(const float* A, int64_t lda, int64_t rows, int64_t cols, float* ws,
+                      float* scale, void* stream) {
+  DSVGD_REQUIRE(A && ws && scale, "null pointer");
+  DSVGD_REQUIRE(rows > 0 && cols > 0 && lda >= cols, "sizes");
+  return h2_colscale(A, lda, rows, cols, ws, scale, (hipStream_t)stream);
+}
+
+int64_t dsvgd_h2_image_bytes(int64_t rows, int64_t cols) {
+  return roundup(rows, kX3Step) * roundup(cols, kX3Step) * 2 * 2;
+}
+
+int dsvgd_h2_ysplit(const float* Y, int64_t ldy, int64_t rows, const float* colscale, void* Yh,
+                    void* stream) {
+  DSVGD_REQUIRE(Y && colscale && Yh, "null pointer");
+  DSVGD_REQUIRE(rows > 0 && rows % kX3Step == 0, "rows must be a positive multiple of 16");
+  DSVGD_REQUIRE(ldy > 0 && ldy % 16 == 0, "ldy must be a multiple of 16");
+  DSVGD_REQUIRE(((uintptr_t)Yh & 15) == 0, "16-byte alignment");
+  return h2_ysplit(Y, ldy, rows, colscale, Yh, (hipStream_t)stream);
+}
+
+int dsvgd_h2_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                      int64_t kpad, const float* tscale, void* img, void* stream) {
+  DSVGD_REQUIRE(A && tscale && img, "null pointer");
+  DSVGD_REQUIRE(rows >= 0 && cols >= 0 && rows <= rows_pad && lda >= cols, "sizes");
+  DSVGD_REQUIRE(rows_pad > 0 && rows_pad % 16 == 0 && kpad > 0 && kpad % kX3Step == 0,
+                "rows_pad and kpad must be positive multiples of 16");
+  DSVGD_REQUIRE(((uintptr_t)img & 15) == 0, "16-byte alignment");
+  return h2_rowsplit(A, lda, rows, cols, rows_pad, kpad, tscale, img, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -7,6 +7,7 @@
 //
 // as Z = W Xd^T (NT MFMA engine, sigmoid epilogue -> G in panel layout) and
 // G Xd (NN MFMA engine); 4 n N p flop, MFMA-bound.
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <string>
@@ -23,6 +24,16 @@ int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, i
 int nn_x3_gemm(bool exp_, const float* A, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
                const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
                int64_t row0, hipStream_t s, int sym = 0, int m16 = 0);
+int nn_h2_gemm(bool exp_, const float* A, int64_t K, const _Float16* Yh, int64_t ldy, int splits,
+               const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
+               int64_t row0, hipStream_t s, int sym, const float* colinv);
+int h2_colscale(const float* A, int64_t lda, int64_t rows, int64_t cols, float* ws, float* out,
+                hipStream_t s);
+int h2_ysplit(const float* Y, int64_t ldy, int64_t rows, const float* colscale, void* Yh,
+              hipStream_t s);
+int h2_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                int64_t kpad, const float* tscale, void* img, hipStream_t s);
+size_t h2_colscale_ws_floats(int64_t rows, int64_t cols);
 
 static int64_t nn_cols(int64_t w) {
   if (w <= 128) return 128;
@@ -32,7 +43,8 @@ static int64_t nn_cols(int64_t w) {
 
 struct LogregWs {
   int64_t n_pad, N_pad, pp, ldb;
-  size_t off_w, off_xd, off_t, off_g, off_gw, off_wx, off_xdx, off_xdy, total;
+  size_t off_w, off_xd, off_t, off_g, off_gw, off_wx, off_xdx, off_xdy, off_sw, off_sxd, off_sws,
+      off_zs, total;
 };
 
 static LogregWs logreg_ws(int64_t n, int64_t N, int64_t p) {
@@ -56,6 +68,11 @@ static LogregWs logreg_ws(int64_t n, int64_t N, int64_t p) {
   w.off_wx = take((size_t)w.n_pad * w.pp * 3 / 2);
   w.off_xdx = take((size_t)w.N_pad * w.pp * 3 / 2);
   w.off_xdy = take((size_t)w.N_pad * w.ldb * 3 / 2);
+  // FmtH2 scales (dsvgd_h2_colscale layout) of W = X[:, 1:] and of Xd, + scratch
+  w.off_sw = take((size_t)(2 * w.pp + 2));
+  w.off_sxd = take((size_t)(2 * w.ldb + 2));
+  w.off_sws = take(std::max(h2_colscale_ws_floats(n, w.pp), h2_colscale_ws_floats(w.N_pad, w.ldb)));
+  w.off_zs = take(2);
   w.total = o;
   return w;
 }
@@ -91,10 +108,11 @@ struct IsM16 : std::false_type {};
 template <class T>
 struct IsM16<T, std::void_t<decltype(T::M16_)>> : std::integral_constant<bool, T::M16_> {};
 
+// zs: 1 / (the product of the operands' FmtH2 tensor scales), 1 otherwise
 template <class T>
 __device__ __forceinline__ void z_epilogue(T& tile, int64_t i0, int64_t q0,
                                            const float* __restrict__ tp, int64_t N_pad,
-                                           float* __restrict__ G) {
+                                           float* __restrict__ G, float zs = 1.f) {
   if constexpr (IsM16<T>::value) {  // 16x16 tiles: column lane & 15, rows 4 (lane >> 4) + reg
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w / T::WN_, wn = w % T::WN_;
 #pragma unroll
@@ -123,7 +141,7 @@ __device__ __forceinline__ void z_epilogue(T& tile, int64_t i0, int64_t q0,
   for (int ni = 0; ni < T::TN_; ++ni) {
     const int64_t q = q0 + wn * WC + ni * 32 + (lane & 31);
     const float tq = tp[q];
-    const float sc = tq * kLog2e;
+    const float sc = tq * kLog2e * zs;
 #pragma unroll
     for (int mi = 0; mi < T::TM_; ++mi) {
       const int64_t i = i0 + wm * WR + mi * 32 + h4;  // 32-row group: one 128-row panel
@@ -139,32 +157,19 @@ __device__ __forceinline__ void z_epilogue(T& tile, int64_t i0, int64_t q0,
   }
 }
 
-// Z on the split engine (fp32-accurate, gemm_x3.hpp): W and Xd as row images.
-// 256 x 256 tiles, 8 waves of 64 x 128 (half the operand bytes per flop of a
-// 128 x 128 tile), 3-stage ring (144 KiB, one block per CU).
-using ZX3Tile = NTX3Tile<2, 4, 4, 2>;
-__global__ __launch_bounds__(ZX3Tile::kThreads) void logreg_z_x3_kernel(const __bf16* __restrict__ Wx,
-                                                          int64_t n_pad,
-                                                          const __bf16* __restrict__ Xdx,
-                                                          int64_t N_pad, int nk,
-                                                          const float* __restrict__ tp,
-                                                          float* __restrict__ G) {
-  __shared__ __attribute__((aligned(16))) char smem[ZX3Tile::kSmemBytes];
-  const int64_t i0 = (int64_t)blockIdx.y * ZX3Tile::BM, q0 = (int64_t)blockIdx.x * ZX3Tile::BN;
-  ZX3Tile tile;
-  tile.run(Wx + i0 * 16, n_pad, Xdx + q0 * 16, N_pad, nk, smem);
-  z_epilogue(tile, i0, q0, tp, N_pad, G);
-}
-
 // Persistent form: a grid of one block per CU walks each XCD's L2-grouped
 // range of 256 x 256 tiles (sqdist_x3w_kernel's schedule) through a 2-stage
 // DMA ring that runs across tile boundaries: the next tile's first K-step
 // lands while this one's epilogue (exp2, rcp, G stores) runs.
-using ZX3PTile = NTX3Tile<2, 4, 4, 2, 2, true>;  // 16x16x32 (unswizzled W / Xd images)
+// F = FmtX3: 16x16x32 (unswizzled W / Xd images); FmtH2: 32x32x16 on the
+// swizzled fp16 images of t_w W and t_x Xd (zsc = [1/t_w, 1/t_x]).
+template <class F = FmtX3>
 __global__ __launch_bounds__(512, 1) void logreg_z_x3p_kernel(
-    const __bf16* __restrict__ Wx, int64_t n_img, const __bf16* __restrict__ Xdx, int64_t N_img,
-    int nk, const float* __restrict__ tp, int64_t N_pad, float* __restrict__ G, int Tm2, int Tn2,
-    int64_t total) {
+    const typename F::E* __restrict__ Wx, int64_t n_img, const typename F::E* __restrict__ Xdx,
+    int64_t N_img, int nk, const float* __restrict__ tp, int64_t N_pad, float* __restrict__ G,
+    int Tm2, int Tn2, int64_t total, const float* __restrict__ zsc) {
+  using ZX3PTile = NTX3Tile<2, 4, 4, 2, 2, F::P == 3, F>;
+  const float zs = F::P == 3 ? 1.f : zsc[0] * zsc[1];
   __shared__ __attribute__((aligned(16))) char smem[ZX3PTile::kSmemBytes];
   const int w = threadIdx.x >> 6, wr = w / ZX3PTile::WN_, wc = w % ZX3PTile::WN_;
   const int64_t x = blockIdx.x % kXcds, u = blockIdx.x / kXcds, U = gridDim.x / kXcds;
@@ -192,7 +197,7 @@ __global__ __launch_bounds__(512, 1) void logreg_z_x3p_kernel(
   int64_t L = next_valid((int64_t)__builtin_amdgcn_readfirstlane((int)(lo + u)), BI, BJ);
   tile.zero();
   if (L < hi) issue(smem, BI, BJ, 0);
-  ZX3PTile::ring_barrier<0>();
+  ZX3PTile::template ring_barrier<0>();
   int ks = 0, stage = 0, BIn = BI, BJn = BJ;
   int64_t Ln = L;
   while (L < hi) {
@@ -203,9 +208,9 @@ __global__ __launch_bounds__(512, 1) void logreg_z_x3p_kernel(
     }
     if (Ln < hi) issue(smem + (stage ^ 1) * ZX3PTile::kStage, BIn, BJn, ksn);
     tile.compute(smem + stage * ZX3PTile::kStage, wr, wc);
-    ZX3PTile::ring_barrier<0>();
+    ZX3PTile::template ring_barrier<0>();
     if (ks + 1 == nk) {
-      z_epilogue(tile, (int64_t)BI * 256, (int64_t)BJ * 256, tp, N_pad, G);
+      z_epilogue(tile, (int64_t)BI * 256, (int64_t)BJ * 256, tp, N_pad, G, zs);
       tile.zero();
       L = Ln;
       BI = BIn;
@@ -247,6 +252,12 @@ __global__ __launch_bounds__(256) void logreg_finish_kernel(const float* __restr
   if (lane == 0) S[j * lds] = scale * (-a + 0.5f * (float)p - 0.5f * a * w2);
 }
 
+
+// out[0..1] = the two FmtH2 inverse tensor scales of Z's operands, side by side
+__global__ void zscale_pair_kernel(const float* a, const float* b, float* out) {
+  out[0] = *a;
+  out[1] = *b;
+}
 
 // ---- posterior-predictive test accuracy (experiments/logreg_plots.py:42-50) --
 using PTile = ZTile;
@@ -408,9 +419,10 @@ size_t dsvgd_logreg_workspace_bytes(int64_t n, int64_t N, int64_t p) {
   return logreg_ws(n, N, p).total;
 }
 
-int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const float* Xd,
-                       int64_t ldxd, const float* t, int64_t N, float scale, float* S, int64_t lds,
-                       void* workspace, void* stream) {
+// engine: 0 = FmtH2 split engine (default), 1 = FmtX3, 2 = f32 MFMA (reference)
+static int score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const float* Xd,
+                        int64_t ldxd, const float* t, int64_t N, float scale, float* S, int64_t lds,
+                        void* workspace, void* stream, int engine) {
   DSVGD_REQUIRE(X && Xd && t && S && workspace, "null pointer");
   DSVGD_REQUIRE(n > 0 && d >= 2 && N > 0 && ldx >= d && lds >= d && ldxd >= d - 1, "sizes");
   DSVGD_REQUIRE(((uintptr_t)workspace & 255) == 0, "workspace must be 256-byte aligned");
@@ -429,13 +441,12 @@ int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const 
   float* G = (float*)(base + w.off_g);
   float* GW = (float*)(base + w.off_gw);
   hipStream_t s = (hipStream_t)stream;
-  // DSVGD_LOGREG_GEMM=f32: the f32 MFMA engines (A/B and precision checks)
-  const char* ge = getenv("DSVGD_LOGREG_GEMM");
-  const bool x3 = !(ge && std::string(ge) == "f32") && w.n_pad * w.pp * 6 < ((int64_t)1 << 31) &&
-                  w.N_pad * w.ldb * 6 < ((int64_t)1 << 31);
+  const bool fits = w.n_pad * w.pp * 6 < ((int64_t)1 << 31) && w.N_pad * w.ldb * 6 < ((int64_t)1 << 31);
+  const bool x3 = engine == 1 && fits;
+  const bool h2 = engine == 0 && fits;
   int64_t tot = w.n_pad * w.ldb;
   int rc = 0;
-  if (!x3) {
+  if (!x3 && !h2) {
     hipLaunchKernelGGL(pad_copy_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, X, ldx, 1, n, p,
                        w.n_pad, Wp, w.ldb);
     if ((rc = check_launch("pad_copy(W)"))) return rc;
@@ -447,32 +458,61 @@ int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const 
   hipLaunchKernelGGL(pad_copy_kernel, dim3((w.N_pad + 255) / 256), dim3(256), 0, s, t, 1, 0, N, 1,
                      w.N_pad, tp, 1);
   if ((rc = check_launch("pad_copy(t)"))) return rc;
+  if (h2) {
+    void* Wx = base + w.off_wx;
+    void* Xdx = base + w.off_xdx;
+    _Float16* Xdy = (_Float16*)(base + w.off_xdy);
+    float* sw = (float*)(base + w.off_sw);
+    float* sxd = (float*)(base + w.off_sxd);
+    float* sws = (float*)(base + w.off_sws);
+    float* zs = (float*)(base + w.off_zs);
+    if ((rc = h2_colscale(X + 1, ldx, n, p, sws, sw, s))) return rc;
+    if ((rc = h2_colscale(Xdp, w.ldb, w.N_pad, w.ldb, sws, sxd, s))) return rc;
+    // tensor scales for the Z images, per-column ones for G . Xd's B image
+    if ((rc = h2_rowsplit(X + 1, ldx, n, p, w.n_pad, w.pp, sw + 2 * p, Wx, s))) return rc;
+    if ((rc = h2_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, sxd + 2 * w.ldb, Xdx, s)))
+      return rc;
+    if ((rc = h2_ysplit(Xdp, w.ldb, w.N_pad, sxd, Xdy, s))) return rc;
+    // the Z kernel's scale operand: [1/t_w, 1/t_x] side by side
+    int blocks = 0;
+    if ((rc = persistent_blocks(reinterpret_cast<const void*>(&logreg_z_x3p_kernel<FmtH2>),
+                                &blocks)))
+      return rc;
+    const int Tm2 = (int)(w.n_pad / 256), Tn2 = (int)(w.N_pad / 256);
+    hipLaunchKernelGGL(zscale_pair_kernel, dim3(1), dim3(1), 0, s, sw + 2 * p + 1,
+                       sxd + 2 * w.ldb + 1, zs);
+    if ((rc = check_launch("zscale_pair"))) return rc;
+    hipLaunchKernelGGL(logreg_z_x3p_kernel<FmtH2>, dim3((unsigned)blocks), dim3(512), 0, s,
+                       (const _Float16*)Wx, w.n_pad, (const _Float16*)Xdx, w.N_pad,
+                       (int)(w.pp / kX3Step), tp, w.N_pad, G, Tm2, Tn2,
+                       tile_grid(Tm2, Tn2, false), (const float*)zs);
+    if ((rc = check_launch("logreg_z_h2"))) return rc;
+    if ((rc = nn_h2_gemm(false, G, w.N_pad, Xdy, w.ldb, 1, nullptr, GW, w.ldb, nullptr, n, 0, s, 0,
+                         sxd + w.ldb)))
+      return rc;
+    hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,
+                       w.ldb, scale, S, lds);
+    return check_launch("logreg_finish");
+  }
   if (x3) {
     void* Wx = base + w.off_wx;
     void* Xdx = base + w.off_xdx;
     __bf16* Xdy = (__bf16*)(base + w.off_xdy);
-    // DSVGD_LOGREG_Z=tile: one 32x32x16 tile per block (A/B switch against
-    // the persistent 16x16x32 form); the images' swizzle follows the form
-    const char* zf = getenv("DSVGD_LOGREG_Z");
-    const bool ztile = zf && std::string(zf) == "tile";
-    if ((rc = dsvgd_rowsplit(X + 1, ldx, n, p, w.n_pad, w.pp, Wx, ztile ? 1 : 0, s))) return rc;
-    if ((rc = dsvgd_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, Xdx, ztile ? 1 : 0, s)))
-      return rc;
+    // the persistent 16x16x32 Z form reads unswizzled images
+    if ((rc = dsvgd_rowsplit(X + 1, ldx, n, p, w.n_pad, w.pp, Wx, 0, s))) return rc;
+    if ((rc = dsvgd_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, Xdx, 0, s))) return rc;
     const int m16 = w.ldb % 256 == 0;  // the 16x16x32 form (unswizzled image) when it applies
     if ((rc = dsvgd_ysplit(Xdp, w.ldb, w.N_pad, Xdy, m16 ? 0 : 1, s))) return rc;
-    if (ztile) {
-      hipLaunchKernelGGL(logreg_z_x3_kernel, dim3(w.N_pad / ZX3Tile::BN, w.n_pad / ZX3Tile::BM),
-                         dim3(ZX3Tile::kThreads), 0, s, (const __bf16*)Wx, w.n_pad,
-                         (const __bf16*)Xdx, w.N_pad, (int)(w.pp / kX3Step), tp, G);
-    } else {
+    {
       int blocks = 0;
-      if ((rc = persistent_blocks(reinterpret_cast<const void*>(&logreg_z_x3p_kernel), &blocks)))
+      if ((rc = persistent_blocks(reinterpret_cast<const void*>(&logreg_z_x3p_kernel<FmtX3>),
+                                  &blocks)))
         return rc;
       const int Tm2 = (int)(w.n_pad / 256), Tn2 = (int)(w.N_pad / 256);
-      hipLaunchKernelGGL(logreg_z_x3p_kernel, dim3((unsigned)blocks), dim3(512), 0, s,
+      hipLaunchKernelGGL(logreg_z_x3p_kernel<FmtX3>, dim3((unsigned)blocks), dim3(512), 0, s,
                          (const __bf16*)Wx, w.n_pad, (const __bf16*)Xdx, w.N_pad,
                          (int)(w.pp / kX3Step), tp, w.N_pad, G, Tm2, Tn2,
-                         tile_grid(Tm2, Tn2, false));
+                         tile_grid(Tm2, Tn2, false), nullptr);
     }
     if ((rc = check_launch("logreg_z_x3"))) return rc;
     if ((rc = nn_x3_gemm(false, G, w.N_pad, Xdy, w.ldb, 1, nullptr, GW, w.ldb, nullptr, n, 0, s, 0,
@@ -490,6 +530,19 @@ int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const 
   hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,
                      w.ldb, scale, S, lds);
   return check_launch("logreg_finish");
+}
+
+int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const float* Xd,
+                       int64_t ldxd, const float* t, int64_t N, float scale, float* S, int64_t lds,
+                       void* workspace, void* stream) {
+  return score_logreg(X, ldx, n, d, Xd, ldxd, t, N, scale, S, lds, workspace, stream, 0);
+}
+
+int dsvgd_score_logreg_engine(const float* X, int64_t ldx, int64_t n, int64_t d, const float* Xd,
+                              int64_t ldxd, const float* t, int64_t N, float scale, float* S,
+                              int64_t lds, void* workspace, int engine, void* stream) {
+  DSVGD_REQUIRE(engine >= 0 && engine <= 2, "engine must be 0 (h2), 1 (x3) or 2 (f32)");
+  return score_logreg(X, ldx, n, d, Xd, ldxd, t, N, scale, S, lds, workspace, stream, engine);
 }
 
 size_t dsvgd_logreg_predict_workspace_bytes(int64_t n, int64_t Nt, int64_t p) {

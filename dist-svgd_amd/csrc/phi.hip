@@ -72,15 +72,19 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
 // phi_mm on the bf16 MFMA at fp32 accuracy (gemm_x3.hpp): the same blocks,
 // split-K slices, diagonal skip and row sums as nn_kernel<TN, true>; B is the
 // split image of Y (dsvgd_ysplit).
-template <int TN, bool DMA, bool EXP, bool M16, int RW = 2>
+// F = FmtH2: C and rowsum come out of the MFMAs scaled by 2^15 (the A
+// staging scale) and C's column c by the B image's column scale: the stores
+// multiply by colinv[c] * 2^-15 (exact powers of two).
+template <int TN, bool DMA, bool EXP, bool M16, int RW = 2, class F = FmtX3>
 __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A, int64_t a_npad,
-                                                    const __bf16* __restrict__ Yx, int64_t ldy,
-                                                    int64_t K, int64_t kchunk,
+                                                    const typename F::E* __restrict__ Yx,
+                                                    int64_t ldy, int64_t K, int64_t kchunk,
                                                     const dsvgd_select_state* __restrict__ st,
                                                     float* __restrict__ C, int64_t ldc,
                                                     float* __restrict__ rowsum, int64_t m,
-                                                    int64_t row0, int sym) {
-  using Tile = NNX3Tile<TN, DMA, EXP, M16, RW>;
+                                                    int64_t row0, int sym,
+                                                    const float* __restrict__ colinv) {
+  using Tile = NNX3Tile<TN, DMA, EXP, M16, RW, F>;
   __shared__ __attribute__((aligned(16))) char smem[Tile::kSmemBytes];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
@@ -120,15 +124,16 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
         const int64_t col = c0 + wc * 32 * TN + ni * 32 + (lane & 31);
+        const float cs = F::P == 3 ? 1.f : colinv[col] * (1.f / F::kAScale);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int64_t row = r0 + mi * 32 + c_row(r, lane);
-          if (row < m) C[row * ldc + col] = tile.acc[mi][ni][r];
+          if (row < m) C[row * ldc + col] = F::P == 3 ? tile.acc[mi][ni][r] : tile.acc[mi][ni][r] * cs;
         }
       }
   }
   if (EXP && blockIdx.x == 0) {
-    const float v = tile.row_sum();
+    const float v = tile.row_sum() * (1.f / F::kAScale);
     const int64_t row = i0 + (threadIdx.x >> 2);
     if ((threadIdx.x & 3) == 0 && row < m) rowsum[row] = v;
   }
@@ -187,58 +192,74 @@ __global__ __launch_bounds__(256) void ysplit_kernel(const float* __restrict__ Y
   }
 }
 
-template <int TN, bool EXP>
-int launch_nn_x3(const float* D, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
+template <int TN, bool EXP, class F>
+int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy, int splits,
                  const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-                 int64_t row0, int sym, int m16, hipStream_t s) {
+                 int64_t row0, int sym, int m16, const float* colinv, hipStream_t s) {
   if (sym && TN == 1) return fail_arg("nn_x3: the symmetric layout needs ldy % 256 == 0");
   const int64_t kchunk = roundup((K + splits - 1) / splits, kX3Step);
   const dim3 grid(ldy / (128 * TN), roundup(m, 128) / 128, splits);
-  // DSVGD_X3_DMA=0: Yx staged through VGPRs + ds_write (A/B switch)
-  const char* e = getenv("DSVGD_X3_DMA");
-  if (sym && e && e[0] == '0') return fail_arg("nn_x3: the symmetric layout needs the DMA path");
-  if (m16 && ((e && e[0] == '0') || TN == 1))
+  if (F::P == 3 && m16 && TN == 1)
     return fail_arg("nn_x3: the 16x16 form needs the DMA path (ldy % 256 == 0)");
-  if ((e && e[0] == '0') || TN == 1)  // TN = 1: 1.5 DMA rounds per K-step
-    hipLaunchKernelGGL((nn_x3_kernel<TN, false, EXP, false>), grid, dim3(512), 0, s, D, K, Yx, ldy,
-                       K, kchunk, st, C, ldc, rowsum, m, row0, 0);
-  else if (m16)
-    hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, TN != 1>), grid, dim3(512), 0, s, D, K, Yx,
-                       ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym);
-  else
-    hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false>), grid, dim3(512), 0, s, D, K, Yx,
-                       ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym);
+  if (TN == 1)  // TN = 1: 1.5 DMA rounds per K-step -> the register-staged form
+    hipLaunchKernelGGL((nn_x3_kernel<TN, false, EXP, false, 2, F>), grid, dim3(512), 0, s, D, K, Yx,
+                       ldy, K, kchunk, st, C, ldc, rowsum, m, row0, 0, colinv);
+  else if constexpr (F::P == 3) {
+    if (m16)
+      hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, TN != 1, 2, F>), grid, dim3(512), 0, s, D,
+                         K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv);
+    else
+      hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F>), grid, dim3(512), 0, s, D, K,
+                         Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv);
+  } else {
+    hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F>), grid, dim3(512), 0, s, D, K,
+                       Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv);
+  }
   return check_launch("nn_x3_kernel");
 }
 
 // C = f(A) B on the split engine; A panel layout (m_pad x K), B = Yx image
 // (K rows, ldy columns, a multiple of 128).  exp_: the phi_mm form.
-int nn_x3_gemm(bool exp_, const float* A, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
-               const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-               int64_t row0, hipStream_t s, int sym, int m16) {
+template <class F>
+int nn_split_gemm(bool exp_, const float* A, int64_t K, const typename F::E* Yx, int64_t ldy,
+                  int splits, const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum,
+                  int64_t m, int64_t row0, hipStream_t s, int sym, int m16, const float* colinv) {
+  if (F::P == 2) m16 = 0;  // the fp16 format runs the 32x32x16 form
   if (K * ldy * 6 >= ((int64_t)1 << 31) || K * 128 * 4 >= ((int64_t)1 << 31))
     return fail_arg("nn_x3: K x ldy too large for 32-bit buffer offsets");
   if (ldy % 128 != 0) return fail_arg("nn_x3: ldy must be a multiple of 128");
-  const char* e = getenv("DSVGD_X3_DMA");
-  const bool dma = !(e && e[0] == '0');
-  if (!exp_ && m16 && dma && ldy % 512 != 0 && ldy % 256 == 0) {
+  if (!exp_ && (m16 || F::P == 2) && ldy % 512 != 0 && ldy % 256 == 0) {
     // 256-row blocks x 256 columns (G . Xd): the A rows must exist up to a
     // multiple of 256 (the caller's panel layout; logreg pads n to 256)
     const int64_t kchunk = roundup((K + splits - 1) / splits, kX3Step);
     const dim3 grid(ldy / 256, roundup(m, 256) / 256, splits);
-    hipLaunchKernelGGL((nn_x3_kernel<4, true, false, true, 4>), grid, dim3(512), 0, s, A, K, Yx,
-                       ldy, K, kchunk, st, C, ldc, rowsum, m, row0, 0);
+    hipLaunchKernelGGL((nn_x3_kernel<4, true, false, F::P == 3, 4, F>), grid, dim3(512), 0, s, A, K,
+                       Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, 0, colinv);
     return check_launch("nn_x3_kernel(256-row)");
   }
 #define DSVGD_X3_TN(TN)                                                                        \
-  return exp_ ? launch_nn_x3<TN, true>(A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0, sym,  \
-                                       m16, s)                                                 \
-              : launch_nn_x3<TN, false>(A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0, 0,  \
-                                        m16, s)
+  return exp_ ? launch_nn_x3<TN, true, F>(A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0,    \
+                                          sym, m16, colinv, s)                                 \
+              : launch_nn_x3<TN, false, F>(A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0, 0, \
+                                           m16, colinv, s)
   if (ldy % 512 == 0) DSVGD_X3_TN(4);
   if (ldy % 256 == 0) DSVGD_X3_TN(2);
   DSVGD_X3_TN(1);
 #undef DSVGD_X3_TN
+}
+
+int nn_x3_gemm(bool exp_, const float* A, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
+               const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
+               int64_t row0, hipStream_t s, int sym, int m16) {
+  return nn_split_gemm<FmtX3>(exp_, A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0, s, sym,
+                              m16, nullptr);
+}
+
+int nn_h2_gemm(bool exp_, const float* A, int64_t K, const _Float16* Yh, int64_t ldy, int splits,
+               const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
+               int64_t row0, hipStream_t s, int sym, const float* colinv) {
+  return nn_split_gemm<FmtH2>(exp_, A, K, Yh, ldy, splits, st, C, ldc, rowsum, m, row0, s, sym, 0,
+                              colinv);
 }
 
 
@@ -458,7 +479,6 @@ __global__ __launch_bounds__(256) void phi_row_kernel(float* __restrict__ X, int
 // NN block shape: 128 rows x 128*TN columns, 8 waves (2 per SIMD, 128
 // accumulators each); K-steps of 32 columns (two D panels per barrier,
 // 160 KiB LDS, XOR-swizzled A image) when K allows, else 16.
-// DSVGD_NN_SHAPE=w2 forces the 16-deep K-step (A/B switch).
 template <int TN, int BJ>
 int launch_nn_shape(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
                     const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
@@ -467,24 +487,12 @@ int launch_nn_shape(bool exp_, const float* A, const float* B, int64_t ldb, int6
   if (K % BJ != 0) return fail_arg("nn_kernel: K must be a multiple of the K-step");
   const int64_t kchunk = roundup((K + splits - 1) / splits, BJ);
   const dim3 grid(cols / (128 * TN), roundup(m, BM) / BM, splits);
-  // DSVGD_NN_SWZB=0: unswizzled B image (A/B switch)
-  const char* sw = getenv("DSVGD_NN_SWZB");
-  const bool swz = !(sw && sw[0] == '0');
-#define DSVGD_NN_LAUNCH(E, SW)                                                               \
-  hipLaunchKernelGGL((nn_kernel<TN, E, WM, TM, BJ, SW>), grid, dim3(256 * WM), 0, s, A, K, B, \
-                     ldb, K, kchunk, st, C, ldc, rowsum, m, row0)
-  if (exp_) {
-    if (swz)
-      DSVGD_NN_LAUNCH(true, true);
-    else
-      DSVGD_NN_LAUNCH(true, false);
-  } else {
-    if (swz)
-      DSVGD_NN_LAUNCH(false, true);
-    else
-      DSVGD_NN_LAUNCH(false, false);
-  }
-#undef DSVGD_NN_LAUNCH
+  if (exp_)
+    hipLaunchKernelGGL((nn_kernel<TN, true, WM, TM, BJ>), grid, dim3(256 * WM), 0, s, A, K, B, ldb,
+                       K, kchunk, st, C, ldc, rowsum, m, row0);
+  else
+    hipLaunchKernelGGL((nn_kernel<TN, false, WM, TM, BJ>), grid, dim3(256 * WM), 0, s, A, K, B, ldb,
+                       K, kchunk, st, C, ldc, rowsum, m, row0);
   return check_launch("nn_kernel");
 }
 
@@ -492,9 +500,7 @@ template <int TN>
 int launch_nn(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
               const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
               int64_t cols, int64_t row0, hipStream_t s) {
-  const char* e = getenv("DSVGD_NN_SHAPE");
-  const bool bj16 = e && std::string(e) == "w2";
-  if (!bj16 && K % 32 == 0)  // split-K chunks are rounded to the K-step
+  if (K % 32 == 0)  // split-K chunks are rounded to the K-step
     return launch_nn_shape<TN, 32>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0,
                                    s);
   return launch_nn_shape<TN, 16>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s);
@@ -505,10 +511,6 @@ int launch_nn(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K,
 int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, int64_t cols,
             int splits, const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum,
             int64_t m, int64_t row0, hipStream_t s) {
-  // DSVGD_NN_NOEXP=1: TIMING EXPERIMENTS ONLY (wrong phi) -- the same engine
-  // without the fused exp / row sums, to price the VALU work between MFMAs.
-  const char* noexp = getenv("DSVGD_NN_NOEXP");
-  if (noexp && noexp[0] == '1') exp_ = false;
   // buffer-resource loads: 32-bit byte offsets from a block's A row panel
   // (K columns x 128 rows) and from B's first row (K rows x ldb)
   if (K * ldb * (int64_t)sizeof(float) >= ((int64_t)1 << 31) ||
@@ -614,6 +616,26 @@ int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, in
   DSVGD_REQUIRE(!sym || (m == n && row0 == 0), "sym: the symmetric layout needs m == n, row0 == 0");
   return nn_x3_gemm(true, D, n_pad, (const __bf16*)Yx, ldy, (int)splits, st, KY, ldk, rowsum, m,
                     row0, (hipStream_t)stream, sym, m16);
+}
+
+int dsvgd_phi_mm_h2(const float* D, int64_t ldd, const void* Yh, int64_t ldy, int64_t row0,
+                    int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
+                    int64_t ldk, float* rowsum, int sym, const float* colinv, void* stream) {
+  DSVGD_REQUIRE(D && Yh && st && KY && rowsum && colinv, "null pointer");
+  DSVGD_REQUIRE(m > 0 && n > 0, "sizes");
+  const int64_t n_pad = roundup(n, 128);
+  DSVGD_REQUIRE(ldd == n_pad, "ldd must equal roundup(n,128) (panel layout)");
+  DSVGD_REQUIRE(ldy % 128 == 0 && ldk >= ldy, "ldy must be a multiple of 128, ldk >= ldy");
+  DSVGD_REQUIRE(((uintptr_t)Yh & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
+  DSVGD_REQUIRE(roundup(m, 128) / 128 <= 65535, "too many row tiles");
+  DSVGD_REQUIRE(splits >= 1 && splits <= 1024, "splits must be in [1, 1024]");
+  DSVGD_REQUIRE(row0 >= 0 && row0 + m <= n, "row block outside [0, n)");
+  DSVGD_REQUIRE(n_pad * ldy * 4 < ((int64_t)1 << 31) && n_pad * 128 * 4 < ((int64_t)1 << 31),
+                "n x ldy too large for 32-bit buffer offsets (use dsvgd_phi_mm)");
+  DSVGD_REQUIRE(!sym || (m == n && row0 == 0 && ldy % 256 == 0),
+                "sym: the symmetric layout needs m == n, row0 == 0, ldy % 256 == 0");
+  return nn_h2_gemm(true, D, n_pad, (const _Float16*)Yh, ldy, (int)splits, st, KY, ldk, rowsum, m,
+                    row0, (hipStream_t)stream, sym, colinv);
 }
 
 int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t splits,

@@ -15,7 +15,16 @@
 #include "gemm_x3.hpp"
 #include "select.hpp"
 
+// DSVGD_SQ_EPI (compile time, A/B builds only -- scripts/ab_kernels.py):
+// 1 skips the mirror stores, 2 every D store, 3 the whole epilogue, to price
+// the epilogue; D is then incomplete.  The shipped library is built with 0.
+#ifndef DSVGD_SQ_EPI
+#define DSVGD_SQ_EPI 0
+#endif
+
 namespace dsvgd {
+
+constexpr int kSqEpi = DSVGD_SQ_EPI;
 
 using GramTile = NTTile<2, 2, 2, 2>;  // 128 x 128 block, 4 waves of 64 x 64
 
@@ -33,7 +42,8 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
                                             const float* scol, int rbase, int cbase,
                                             WindowHist& wh, uint32_t* shist, SlotWriter& sw,
                                             const SlotLayout& sl, int64_t slot, int epi,
-                                            bool mirror_store = true, int r0t = 0) {
+                                            bool mirror_store = true, int r0t = 0,
+                                            float c2 = 2.f) {
   // r0t: row0 / 128 when a row block's diagonal square runs SYM (bi is then
   // block-local, bj global; the mirror of (bi, bj) is (bj - r0t, bi + r0t))
   const int lane = threadIdx.x & 63;
@@ -63,7 +73,7 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
       if (interior) {
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          v[r] = fmaxf(0.f, (srow[rb + (r & 3) + 8 * (r >> 2)] + nj) - 2.f * tile.acc[mi][ni][r]);
+          v[r] = fmaxf(0.f, (srow[rb + (r & 3) + 8 * (r >> 2)] + nj) - c2 * tile.acc[mi][ni][r]);
       } else {
         const bool colok = j0 + cl < n;
 #pragma unroll
@@ -73,7 +83,7 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
           if (colok && i0 + rl < m)
             x = (row0 + i0 + rl == j0 + cl)
                     ? 0.f
-                    : fmaxf(0.f, (srow[rl] + nj) - 2.f * tile.acc[mi][ni][r]);
+                    : fmaxf(0.f, (srow[rl] + nj) - c2 * tile.acc[mi][ni][r]);
           else
             x = INFINITY;
           v[r] = x;
@@ -170,59 +180,6 @@ __device__ __forceinline__ void sq_epilogue16(Tile& tile, int bi, int bj, int64_
     }
   }
   if (smode == kSelBracket) sw.finish(sl, slot, mirror);
-}
-
-// One tile per block.  Rows [row0, row0+m) of Y against rows [0,n).  SYM
-// (m == n, row0 == 0): only tiles bi <= bj, the off-diagonal ones stored
-// twice (tile + transpose) and accounted with weight 2.
-template <bool SYM, int smode>
-__global__ __launch_bounds__(256) void sqdist_kernel(const float* __restrict__ Y, int64_t ldy,
-                                                     const float* __restrict__ norms, int64_t row0,
-                                                     int64_t m, int64_t n, int64_t n_pad, int dp,
-                                                     float* __restrict__ D,
-                                                     dsvgd_select_state* __restrict__ st,
-                                                     float* __restrict__ cand, int epi) {
-  __shared__ __attribute__((aligned(16))) float smem[GramTile::kSmemFloats];
-  __shared__ uint32_t shist[DSVGD_RADIX_BINS];
-  __shared__ float snorm[GramTile::BM + GramTile::BN];
-
-  int bi, bj;
-  const int Tm = (int)(roundup128(m) / 128), Tn = (int)(n_pad / 128);
-  const int w = threadIdx.x >> 6;
-  const int64_t slot = (int64_t)blockIdx.x * 4 + w;
-  SlotLayout sl(cand, (int64_t)gridDim.x * 4, smode == kSelBracket ? st->cand_cap : 0);
-  if (!tile_of(blockIdx.x, gridDim.x, Tm, Tn, SYM, bi, bj)) {  // whole block, before any barrier
-    if (smode == kSelBracket) slot_clear(sl, slot);
-    return;
-  }
-  const int64_t i0 = (int64_t)bi * GramTile::BM;
-  const int64_t j0 = (int64_t)bj * GramTile::BN;
-  if (smode == kSelHist)
-    for (int b = threadIdx.x; b < DSVGD_RADIX_BINS; b += 256) shist[b] = 0u;
-
-  GramTile tile;
-  tile.run(Y + (row0 + i0) * ldy, ldy, Y + j0 * ldy, ldy, dp, smem);
-
-  for (int t = threadIdx.x; t < GramTile::BM + GramTile::BN; t += 256)
-    snorm[t] = t < GramTile::BM ? norms[row0 + i0 + t] : norms[j0 + t - GramTile::BM];
-  __syncthreads();
-
-  WindowHist wh;
-  SlotWriter sw;
-  if (smode == kSelBracket) {
-    sl.publish(st, blockIdx.x);
-    sw.begin(st, sl, slot);
-  }
-  {
-    const int w = threadIdx.x >> 6;
-    sq_epilogue<SYM, smode>(tile, bi, bj, row0, m, n, n_pad, D, snorm, snorm + 128, (w >> 1) * 64,
-                            (w & 1) * 64, wh, shist, sw, sl, slot, epi);
-  }
-  if (smode == kSelHist) {
-    wh.flush(shist);
-    __syncthreads();
-    flush_block_hist(shist, st);
-  }
 }
 
 // Persistent form: a grid of (resident blocks per CU) x CUs; block b (on XCD
@@ -337,116 +294,29 @@ __global__ __launch_bounds__(256, 2) void sqdist_persistent_kernel(
   }
 }
 
-// The persistent distance kernel on the split engine (gemm_x3.hpp): the
-// Gram from the row image Yg = dsvgd_rowsplit(Y[:, :dp]) (n_pad image rows),
-// fp32-accurate, K-steps of 16 through a 2-stage LDS-DMA ring that runs
-// across tile boundaries (the next tile's first K-step lands during this
-// tile's last one).  Tile order, epilogue and select accounting as
-// sqdist_persistent_kernel.
-using GramX3Tile = NTX3Tile<2, 2, 2, 2, 2>;
-
-template <bool SYM, int smode>
-__global__ __launch_bounds__(256, 2) void sqdist_x3_kernel(
-    const __bf16* __restrict__ Yg, int64_t img_rows, const float* __restrict__ norms,
-    int64_t row0, int64_t m, int64_t n, int64_t n_pad, int nk, float* __restrict__ D,
-    dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int epi, int64_t total,
-    int layout) {
-  __shared__ __attribute__((aligned(16))) char smem[GramX3Tile::kSmemBytes];
-  __shared__ uint32_t shist[DSVGD_RADIX_BINS];
-  __shared__ float snorm[GramX3Tile::BM + GramX3Tile::BN];
-
-  const int Tm = (int)(roundup128(m) / 128), Tn = (int)(n_pad / 128);
-  const int t = threadIdx.x, w = t >> 6, wm = w >> 1, wn = w & 1;
-  const int64_t x = blockIdx.x % kXcds, u = blockIdx.x / kXcds, U = gridDim.x / kXcds;
-  const int64_t q = total / kXcds, rr = total % kXcds;
-  const int64_t lo = x * q + min(x, rr);
-  const int64_t hi = (int64_t)__builtin_amdgcn_readfirstlane((int)(lo + q + (x < rr ? 1 : 0)));
-  SlotLayout sl(cand, total * 4, smode == kSelBracket ? st->cand_cap : 0);
-  if (smode == kSelBracket) sl.publish(st, blockIdx.x);
-  if (smode == kSelHist)
-    for (int b = t; b < DSVGD_RADIX_BINS; b += 256) shist[b] = 0u;
-
-  auto next_valid = [&](int64_t L, int& bi, int& bj) -> int64_t {
-    for (; L < hi; L += U) {
-      if (tile_at(L, Tm, Tn, SYM, bi, bj)) {
-        bi = __builtin_amdgcn_readfirstlane(bi);
-        bj = __builtin_amdgcn_readfirstlane(bj);
-        return L;
-      }
-      if (smode == kSelBracket) slot_clear(sl, L * 4 + w);
-    }
-    return L;
-  };
-  // K-step (tile (bi, bj), ks) -> LDS stage st
-  GramX3Tile tile;
-  auto issue = [&](char* stg, int bi, int bj, int ks) {
-    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(Yg + (row0 + (int64_t)bi * 128) * 16), (short)0, 0x7fffffff, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(Yg + (int64_t)bj * 128 * 16), (short)0, 0x7fffffff, 0x00020000);
-    tile.dma(stg, rA, img_rows, rB, img_rows, ks);
-  };
-
-  int bi = 0, bj = 0;
-  int64_t L = next_valid((int64_t)__builtin_amdgcn_readfirstlane((int)(lo + u)), bi, bj);
-  tile.zero();
-  if (L < hi) issue(smem, bi, bj, 0);
-  GramX3Tile::ring_barrier<0>();
-  int ks = 0, stage = 0;
-  int bin = bi, bjn = bj;  // the tile of the next K-step
-  int64_t Ln = L;
-  while (L < hi) {
-    // position of the next K-step: this tile's ks + 1, or the next tile's 0
-    int ksn = ks + 1;
-    if (ksn == nk) {
-      Ln = next_valid(L + U, bin, bjn);
-      ksn = 0;
-    }
-    const bool more = Ln < hi;
-    if (more) issue(smem + (stage ^ 1) * GramX3Tile::kStage, bin, bjn, ksn);
-    tile.compute(smem + stage * GramX3Tile::kStage, wm, wn, (int)(row0 & 15));
-    GramX3Tile::ring_barrier<0>();
-    if (ks + 1 == nk) {  // tile done: norms, epilogue (re-zeroes the accumulators)
-      snorm[t] = t < 128 ? norms[row0 + (int64_t)bi * 128 + t] : norms[(int64_t)bj * 128 + t - 128];
-      __syncthreads();
-      const int64_t slot = L * 4 + w;
-      WindowHist wh;
-      SlotWriter sw;
-      if (smode == kSelBracket) sw.begin(st, sl, slot);
-      if (epi == 3)
-        tile.zero();
-      else
-        sq_epilogue<SYM, smode, true>(tile, bi, bj, row0, m, n, n_pad, D, snorm, snorm + 128,
-                                      wm * 64, wn * 64, wh, shist, sw, sl, slot, epi,
-                                      layout == 0);
-      if (smode == kSelHist) wh.flush(shist);
-      L = Ln;
-      bi = bin;
-      bj = bjn;
-    }
-    ks = ksn;
-    stage ^= 1;
-  }
-  if (smode == kSelHist) {
-    __syncthreads();
-    flush_block_hist(shist, st);
-  }
-}
-
-// The same on 256 x 256 tiles (8 waves of 64 x 128, one block per CU): twice
-// the MFMAs per operand byte of the 128 x 128 form.  Each wave's 64 x 128
+// The persistent distance kernel on the split engines (gemm_x3.hpp): the
+// Gram from the row image Yg of Y[:, :dp] (n_pad image rows), fp32-accurate,
+// K-steps of 16 through a 2-stage LDS-DMA ring that runs across tile
+// boundaries (the next tile's first K-step lands during this tile's last
+// one); tile order and select accounting as sqdist_persistent_kernel.
+// 256 x 256 tiles (8 waves of 64 x 128, one block per CU): twice the MFMAs
+// per operand byte of a 128 x 128 form.  Each wave's 64 x 128
 // region lies in one 128 x 128 sub-tile (2 BI + (wr >> 1), 2 BJ + wc); the
 // epilogue runs per sub-tile (sub-tiles below the diagonal of a SYM diagonal
 // tile, and past the padded matrix, are skipped).  Candidate slots: 8 per tile.
-// M16: 16x16x32 MFMAs on an unswizzled Yg (default), else 32x32x16 on a
-// swizzled one (DSVGD_GRAM_MFMA=32, A/B switch).
-template <bool SYM, int smode, bool M16 = true>
+// M16: 16x16x32 MFMAs on an unswizzled Yg (FmtX3), else 32x32x16 on a
+// swizzled one (FmtH2).
+// F = FmtH2: Yg is the fp16 image of t Xc (t = tsc[0]), the Gram comes out
+// scaled by t^2: the epilogue's 2 x.y is c2 acc with c2 = 2 / t^2.
+template <bool SYM, int smode, bool M16 = true, class F = FmtX3>
 __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
-    const __bf16* __restrict__ Yg, int64_t img_rows, const float* __restrict__ norms,
+    const typename F::E* __restrict__ Yg, int64_t img_rows, const float* __restrict__ norms,
     int64_t row0, int64_t m, int64_t n, int64_t n_pad, int nk, float* __restrict__ D,
     dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int epi, int64_t total,
-    int layout, int Tm2, int Tc2, int bj_off, int r0t, int64_t slot_base, int64_t ns_total) {
-  using GramX3WTile = NTX3Tile<2, 4, 4, 2, 2, M16>;
+    int layout, int Tm2, int Tc2, int bj_off, int r0t, int64_t slot_base, int64_t ns_total,
+    const float* __restrict__ tsc) {
+  using GramX3WTile = NTX3Tile<2, 4, 4, 2, 2, M16, F>;
+  const float c2 = F::P == 3 ? 2.f : 2.f * tsc[1] * tsc[1];
   __shared__ __attribute__((aligned(16))) char smem[GramX3WTile::kSmemBytes];
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
   __shared__ float snorm[512];  // the tile's 256 row norms, then its 256 column norms
@@ -525,7 +395,7 @@ __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
           sq_epilogue<SYM, smode, true, GramX3WTile, 4>(
               tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128,
               snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl, slot, epi, layout == 0,
-              r0t);
+              r0t, c2);
       }
       if (smode == kSelHist) wh.flush(shist);
       L = Ln;
@@ -545,26 +415,23 @@ __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
 // (a row block's last 256-row tile may start anywhere below n)
 int64_t gram_img_rows(int64_t n) { return roundup(n, 128) + 256; }
 
-template <int SM>
-int launch_sqdist_x3(const __bf16* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
-                     int64_t d, float* D, dsvgd_select_state* st, float* cand, int layout,
-                     hipStream_t s) {
+template <int SM, class F = FmtX3>
+int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, int64_t m,
+                     int64_t n, int64_t d, float* D, dsvgd_select_state* st, float* cand,
+                     int layout, hipStream_t s, const float* tsc = nullptr) {
   const int64_t dp = roundup(d, 32), m_pad = roundup(m, 128), n_pad = roundup(n, 128);
   const int64_t img = gram_img_rows(n);
-  const char* ep = getenv("DSVGD_SQ_EPI");
-  const int epi = ep ? atoi(ep) : 0;
+  const int epi = kSqEpi;
   const bool sym = m == n && row0 == 0;
   const int nk = (int)(dp / kX3Step);
-  int blocks = 0, rc = 0;
-  // DSVGD_GRAM_TILE=128: the 128 x 128 form (A/B switch)
-  const char* gt = getenv("DSVGD_GRAM_TILE");
-  if (!(gt && atoi(gt) == 128)) {
-    const char* gm = getenv("DSVGD_GRAM_MFMA");
-    const bool m16 = !(gm && atoi(gm) == 32);
+  int rc = 0;
+  {
     int bs = 0, bn = 0;
-    if ((rc = persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3w_kernel<true, SM>), &bs)))
+    if ((rc = persistent_blocks(
+             reinterpret_cast<const void*>(&sqdist_x3w_kernel<true, SM, F::P == 3, F>), &bs)))
       return rc;
-    if ((rc = persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3w_kernel<false, SM>), &bn)))
+    if ((rc = persistent_blocks(
+             reinterpret_cast<const void*>(&sqdist_x3w_kernel<false, SM, F::P == 3, F>), &bn)))
       return rc;
     const int Tn2 = (int)((n_pad / 128 + 1) / 2), Tm2 = (int)((m_pad / 128 + 1) / 2);
     struct Part {
@@ -593,39 +460,19 @@ int launch_sqdist_x3(const __bf16* Yg, const float* norms, int64_t row0, int64_t
       const Part& P = parts[i];
       const int lay = sym ? layout : 0;
 #define DSVGD_X3W(SY, M, B, LAY, R0T)                                                          \
-  hipLaunchKernelGGL((sqdist_x3w_kernel<SY, SM, M>), dim3((unsigned)B), dim3(512), 0, s, Yg, img,  \
-                     norms, row0, m, n, n_pad, nk, D, st, cand, epi, P.total, LAY, P.tm2, P.tc2, \
-                     P.bj_off, R0T, base, ns_total)
-      if (P.sym) {
-        if (m16)
-          DSVGD_X3W(true, true, bs, lay, P.r0t);
-        else
-          DSVGD_X3W(true, false, bs, lay, P.r0t);
-      } else {
-        if (m16)
-          DSVGD_X3W(false, true, bn, 0, 0);
-        else
-          DSVGD_X3W(false, false, bn, 0, 0);
-      }
+  hipLaunchKernelGGL((sqdist_x3w_kernel<SY, SM, M, F>), dim3((unsigned)B), dim3(512), 0, s, Yg,    \
+                     img, norms, row0, m, n, n_pad, nk, D, st, cand, epi, P.total, LAY, P.tm2,   \
+                     P.tc2, P.bj_off, R0T, base, ns_total, tsc)
+      if (P.sym)
+        DSVGD_X3W(true, F::P == 3, bs, lay, P.r0t);
+      else
+        DSVGD_X3W(false, F::P == 3, bn, 0, 0);
 #undef DSVGD_X3W
       if ((rc = check_launch("sqdist_x3w"))) return rc;
       base += P.total * 8;
     }
     return 0;
   }
-  const int64_t T = n_pad / 128;
-  const int64_t total = sym ? tile_grid(T, T, true) : tile_grid(m_pad / 128, T, false);
-  rc = sym ? persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3_kernel<true, SM>), &blocks)
-           : persistent_blocks(reinterpret_cast<const void*>(&sqdist_x3_kernel<false, SM>), &blocks);
-  if (rc) return rc;
-  const dim3 grid((unsigned)blocks);
-  if (sym)
-    hipLaunchKernelGGL((sqdist_x3_kernel<true, SM>), grid, dim3(256), 0, s, Yg, img, norms, row0, m,
-                       n, n_pad, nk, D, st, cand, epi, total, layout);
-  else
-    hipLaunchKernelGGL((sqdist_x3_kernel<false, SM>), grid, dim3(256), 0, s, Yg, img, norms, row0,
-                       m, n, n_pad, nk, D, st, cand, epi, total, 0);
-  return check_launch("sqdist_x3");
 }
 
 // d <= 2 (supports up to 64): D_ij = sum_c (y_ic - y_jc)^2 from explicit differences on the VALU
@@ -633,8 +480,8 @@ int launch_sqdist_x3(const __bf16* Yg, const float* norms, int64_t row0, int64_t
 // no ||x||^2 - 2x.y cancellation, which at small d and a narrow median
 // bandwidth costs more than the 1e-5 phi tolerance.  128 x 128 tile per block,
 // 8 x 8 outputs per thread, both operand tiles transposed in LDS.
-constexpr int kDirectMaxD = 64;     // the direct kernel's limit
-constexpr int kDirectDefaultD = 2;  // d <= this takes it by default
+constexpr int kDirectMaxD = 64;     // the direct kernel's limit (dsvgd_sqdist_direct)
+constexpr int kDirectDefaultD = 2;  // d <= this takes it in dsvgd_sqdist
 
 template <int smode>
 __global__ __launch_bounds__(256) void sqdist_direct_kernel(const float* __restrict__ Y,
@@ -715,32 +562,22 @@ __global__ __launch_bounds__(256) void sqdist_direct_kernel(const float* __restr
   }
 }
 
+// direct: the explicit-difference kernel (d <= kDirectMaxD), else the f32 Gram
 template <int SM>
 int launch_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0, int64_t m,
                   int64_t n, int64_t d, float* D, dsvgd_select_state* st, float* cand,
-                  hipStream_t s) {
+                  hipStream_t s, bool direct) {
   const int64_t dp = roundup(d, 32), m_pad = roundup(m, 128), n_pad = roundup(n, 128);
-  // DSVGD_SQ_DIRECT_MAX_D: the largest d that takes the explicit-difference
-  // kernel (default kDirectDefaultD; precision experiments only)
-  const char* dm = getenv("DSVGD_SQ_DIRECT_MAX_D");
-  const int64_t direct_max = dm ? (int64_t)atoi(dm) : kDirectDefaultD;
-  if (d <= direct_max && d <= kDirectMaxD) {
+  if (direct) {
     hipLaunchKernelGGL((sqdist_direct_kernel<SM>), dim3(n_pad / 128, m_pad / 128), dim3(256), 0, s,
                        Y, ldy, row0, m, n, n_pad, (int)d, D, st, cand);
     return check_launch("sqdist_direct");
   }
-  // DSVGD_SQ_EPI=1|2|3: TIMING EXPERIMENTS ONLY (D left incomplete) -- skip
-  // the mirror stores (1), every D store (2), or the whole epilogue (3,
-  // persistent kernel), to price the epilogue.
-  const char* ep = getenv("DSVGD_SQ_EPI");
-  const int epi = ep ? atoi(ep) : 0;
-  // DSVGD_SQ_PERSIST=0: one tile per block (A/B switch against the persistent form)
-  const char* pe = getenv("DSVGD_SQ_PERSIST");
-  const bool persist = !(pe && pe[0] == '0');
+  const int epi = kSqEpi;
   const bool sym = m == n && row0 == 0;
   const int64_t T = n_pad / 128;
   const int64_t total = sym ? tile_grid(T, T, true) : tile_grid(m_pad / 128, T, false);
-  if (persist) {
+  {
     int blocks = 0;
     int rc = sym ? persistent_blocks(
                        reinterpret_cast<const void*>(&sqdist_persistent_kernel<true, SM>), &blocks)
@@ -756,14 +593,6 @@ int launch_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0,
                          norms, row0, m, n, n_pad, (int)dp, D, st, cand, epi, total);
     return check_launch("sqdist_persistent");
   }
-  const dim3 grid((unsigned)total);
-  if (sym)
-    hipLaunchKernelGGL((sqdist_kernel<true, SM>), grid, dim3(256), 0, s, Y, ldy, norms, row0, m, n,
-                       n_pad, (int)dp, D, st, cand, epi);
-  else
-    hipLaunchKernelGGL((sqdist_kernel<false, SM>), grid, dim3(256), 0, s, Y, ldy, norms, row0, m,
-                       n, n_pad, (int)dp, D, st, cand, epi);
-  return check_launch("sqdist");
 }
 
 }  // namespace dsvgd
@@ -787,10 +616,31 @@ int dsvgd_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0, 
   DSVGD_REQUIRE(((uintptr_t)Y & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
   DSVGD_REQUIRE(m_pad / 128 <= 65535, "too many row tiles");
   hipStream_t s = (hipStream_t)stream;
+  const bool direct = d <= kDirectDefaultD;
   switch (select_mode) {
-    case kSelNone: return launch_sqdist<kSelNone>(Y, ldy, norms, row0, m, n, d, D, st, cand, s);
-    case kSelHist: return launch_sqdist<kSelHist>(Y, ldy, norms, row0, m, n, d, D, st, cand, s);
-    default: return launch_sqdist<kSelBracket>(Y, ldy, norms, row0, m, n, d, D, st, cand, s);
+    case kSelNone: return launch_sqdist<kSelNone>(Y, ldy, norms, row0, m, n, d, D, st, cand, s, direct);
+    case kSelHist: return launch_sqdist<kSelHist>(Y, ldy, norms, row0, m, n, d, D, st, cand, s, direct);
+    default: return launch_sqdist<kSelBracket>(Y, ldy, norms, row0, m, n, d, D, st, cand, s, direct);
+  }
+}
+
+int dsvgd_sqdist_direct(const float* Y, int64_t ldy, const float* norms, int64_t row0, int64_t m,
+                        int64_t n, int64_t d, float* D, int64_t ldd, int select_mode,
+                        dsvgd_select_state* st, float* cand, void* stream) {
+  DSVGD_REQUIRE(Y && D, "null pointer");
+  DSVGD_REQUIRE(m > 0 && n > 0 && row0 >= 0 && d > 0, "sizes");
+  DSVGD_REQUIRE(d <= kDirectMaxD, "the explicit-difference kernel supports d <= 64");
+  DSVGD_REQUIRE(select_mode >= 0 && select_mode <= 2, "select_mode must be 0, 1 or 2");
+  DSVGD_REQUIRE(select_mode == 0 || st, "select mode needs a state");
+  DSVGD_REQUIRE(select_mode != 2 || cand, "bracket mode needs a candidate buffer");
+  DSVGD_REQUIRE(ldy >= roundup(d, 32), "ldy < roundup(d,32)");
+  DSVGD_REQUIRE(ldd == roundup(n, 128), "ldd must equal roundup(n,128) (panel layout)");
+  DSVGD_REQUIRE(roundup(m, 128) / 128 <= 65535, "too many row tiles");
+  hipStream_t s = (hipStream_t)stream;
+  switch (select_mode) {
+    case kSelNone: return launch_sqdist<kSelNone>(Y, ldy, norms, row0, m, n, d, D, st, cand, s, true);
+    case kSelHist: return launch_sqdist<kSelHist>(Y, ldy, norms, row0, m, n, d, D, st, cand, s, true);
+    default: return launch_sqdist<kSelBracket>(Y, ldy, norms, row0, m, n, d, D, st, cand, s, true);
   }
 }
 
@@ -816,6 +666,35 @@ int dsvgd_sqdist_x3(const void* Yg, const float* norms, int64_t row0, int64_t m,
     case kSelNone: return launch_sqdist_x3<kSelNone>(yg, norms, row0, m, n, d, D, st, cand, layout, s);
     case kSelHist: return launch_sqdist_x3<kSelHist>(yg, norms, row0, m, n, d, D, st, cand, layout, s);
     default: return launch_sqdist_x3<kSelBracket>(yg, norms, row0, m, n, d, D, st, cand, layout, s);
+  }
+}
+
+int dsvgd_sqdist_h2(const void* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
+                    int64_t d, float* D, int64_t ldd, int select_mode, dsvgd_select_state* st,
+                    float* cand, int layout, const float* tscale, void* stream) {
+  DSVGD_REQUIRE(Yg && norms && D && tscale, "null pointer");
+  DSVGD_REQUIRE(m > 0 && n > 0 && row0 >= 0 && row0 + m <= n && d > 0, "sizes");
+  DSVGD_REQUIRE(select_mode >= 0 && select_mode <= 2, "select_mode must be 0, 1 or 2");
+  DSVGD_REQUIRE(select_mode == 0 || st, "select mode needs a state");
+  DSVGD_REQUIRE(select_mode != 2 || cand, "bracket mode needs a candidate buffer");
+  const int64_t m_pad = roundup(m, 128), n_pad = roundup(n, 128), dp = roundup(d, 32);
+  DSVGD_REQUIRE(ldd == n_pad, "ldd must equal roundup(n,128) (panel layout)");
+  DSVGD_REQUIRE(((uintptr_t)Yg & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
+  DSVGD_REQUIRE(m_pad / 128 <= 65535, "too many row tiles");
+  DSVGD_REQUIRE(dp * gram_img_rows(n) * 4 < ((int64_t)1 << 31),
+                "image too large for 32-bit buffer offsets");
+  DSVGD_REQUIRE(layout == 0 || (layout == 1 && m == n && row0 == 0),
+                "layout 1 (symmetric) needs the whole matrix: m == n, row0 == 0");
+  const _Float16* yg = (const _Float16*)Yg;
+  hipStream_t s = (hipStream_t)stream;
+  switch (select_mode) {
+    case kSelNone:
+      return launch_sqdist_x3<kSelNone, FmtH2>(yg, norms, row0, m, n, d, D, st, cand, layout, s, tscale);
+    case kSelHist:
+      return launch_sqdist_x3<kSelHist, FmtH2>(yg, norms, row0, m, n, d, D, st, cand, layout, s, tscale);
+    default:
+      return launch_sqdist_x3<kSelBracket, FmtH2>(yg, norms, row0, m, n, d, D, st, cand, layout, s,
+                                                  tscale);
   }
 }
 

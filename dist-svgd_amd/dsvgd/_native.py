@@ -9,6 +9,7 @@ import os
 
 import torch
 
+ABI_VERSION = 2
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libdsvgd_hip.so")
 
 _c = ctypes
@@ -29,6 +30,8 @@ SIGNATURES = {
     "dsvgd_colmean": (_int, [_p, _i64, _i64, _i64, _p, _p, _p]),
     "dsvgd_pack": (_int, [_p, _i64, _p, _i64, _f, _p, _i64, _i64, _i64, _p, _i64, _p, _p]),
     "dsvgd_sqdist": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p]),
+    "dsvgd_sqdist_direct": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p,
+                                   _p]),
     "dsvgd_select_init": (_int, [_p, _i64, _i64, _p]),
     "dsvgd_radix_hist": (_int, [_p, _i64, _p, _int, _p, _i64, _p]),
     "dsvgd_radix_pick": (_int, [_p, _int, _p]),
@@ -46,6 +49,15 @@ SIGNATURES = {
     "dsvgd_sqdist_x3": (_int, [_p, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _int, _p]),
     "dsvgd_phi_mm_x3": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _int,
                                 _int, _p]),
+    "dsvgd_h2_colscale_workspace_floats": (_c.c_size_t, [_i64, _i64]),
+    "dsvgd_h2_colscale": (_int, [_p, _i64, _i64, _i64, _p, _p, _p]),
+    "dsvgd_h2_image_bytes": (_i64, [_i64, _i64]),
+    "dsvgd_h2_ysplit": (_int, [_p, _i64, _i64, _p, _p, _p]),
+    "dsvgd_h2_rowsplit": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _p, _p, _p]),
+    "dsvgd_sqdist_h2": (_int, [_p, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _int, _p,
+                               _p]),
+    "dsvgd_phi_mm_h2": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _int,
+                               _p, _p]),
     "dsvgd_phi_finish": (_int, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _f,
                                 _f, _p, _i64, _p, _i64, _p, _i64, _p]),
     "dsvgd_phi_direct": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _f, _f, _p,
@@ -60,6 +72,8 @@ SIGNATURES = {
     "dsvgd_logreg_workspace_bytes": (_c.c_size_t, [_i64, _i64, _i64]),
     "dsvgd_score_logreg": (_int, [_p, _i64, _i64, _i64, _p, _i64, _p, _i64, _f, _p, _i64, _p,
                                   _p]),
+    "dsvgd_score_logreg_engine": (_int, [_p, _i64, _i64, _i64, _p, _i64, _p, _i64, _f, _p, _i64,
+                                         _p, _int, _p]),
     "dsvgd_logreg_predict_workspace_bytes": (_c.c_size_t, [_i64, _i64, _i64]),
     "dsvgd_logreg_predict": (_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _p, _p]),
 }
@@ -93,7 +107,7 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.dsvgd_abi_version() != 1:
+    if lib.dsvgd_abi_version() != ABI_VERSION:
         raise NativeUnavailable("ABI version mismatch")
     _lib = lib
     return lib

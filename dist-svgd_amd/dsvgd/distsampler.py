@@ -38,6 +38,27 @@ all-gathered (north_star's "all-gather of particles and scores"; SURVEY.md 5,
 8(e)) instead of every rank scoring all n particles (distsampler.py:94-99).
 `replicated=False` keeps the redundant per-rank scoring.
 
+Lagged modes (keyword `lagged`; the reference's notes.md:108-114, which
+describe them and time them at :134-135 but ship no code):
+
+  lagged="local"      ("laggedlocal") every rank keeps a full local copy of
+                      the n particles.  Blocks travel round-robin as in
+                      partitions (the held block goes to rank+1, rank-1's
+                      arrives), but a received block is written to its home
+                      rows, so the copy holds "the most recent copy of x_i
+                      received" and stale rows elsewhere.  The held block
+                      interacts with all n rows of the copy; scores are the
+                      local-data ones scaled by N_global/N_local; a median
+                      bandwidth is the lower median of the held block's own
+                      m x n distances (no collective).
+  lagged="updateall"  ("laggedlocal-updateall") the same exchange, but every
+                      rank moves all n rows of its copy each step (phi of the
+                      whole copy), the received block having overwritten its
+                      rows first.
+
+Both require exchange_particles=False, exchange_scores=False (nothing but
+the travelling block is communicated) and include_wasserstein=False.
+
 Deviation: exchange_scores with num_shards == 1 uses the local scores (the
 reference reads an uninitialised buffer there).
 """
@@ -59,12 +80,20 @@ class DistSampler(object):
     def __init__(self, rank, num_shards, logp, kernel, particles,
                  N_local, N_global,
                  exchange_particles=True, exchange_scores=True, include_wasserstein=True,
-                 *, order="sequential", device=None, group=None, replicated=None):
+                 *, order="sequential", device=None, group=None, replicated=None,
+                 lagged=None):
         """Initializes a distributed SVGD sampler (distsampler.py:9-51)."""
         assert not (exchange_scores and not exchange_particles), \
             "must exchange particles to also exchange scores"
         if order not in ("sequential", "jacobi"):
             raise ValueError("order must be 'sequential' or 'jacobi'")
+        if lagged not in (None, "local", "updateall"):
+            raise ValueError("lagged must be None, 'local' or 'updateall'")
+        if lagged and (exchange_particles or exchange_scores or include_wasserstein):
+            raise ValueError("lagged modes travel blocks round-robin: they need "
+                             "exchange_particles=False, exchange_scores=False, "
+                             "include_wasserstein=False")
+        self._lagged = lagged
         self._rank = rank
         self._num_shards = num_shards
         self._logp = logp
@@ -107,6 +136,7 @@ class DistSampler(object):
             self._scores = torch.empty(self._work.shape, dtype=torch.float32, device=self._device)
 
         (start, end) = self._particle_idx_range(rank)
+        self._held = rank        # lagged modes: index of the block this rank holds
         self._particle_start_idx = start
         self._particle_end_idx = end
         self._previous_particles = None
@@ -146,6 +176,21 @@ class DistSampler(object):
         start, end = self._particle_idx_range(src)
         recv = torch.empty_like(send)
         exchange.ring_shift(send, recv, self._rank, self._num_shards, self._group)
+        self._work[start:end] = recv
+        self._particle_start_idx = start
+        self._particle_end_idx = end
+
+    def _exchange_lagged(self):
+        """laggedlocal exchange (notes.md:110-112): the held block goes to
+        rank+1, rank-1's held block arrives and is written to ITS home rows of
+        the local copy, and is the block held (and moved) from now on."""
+        S = self._num_shards
+        s, e = self._particle_start_idx, self._particle_end_idx
+        send = self._work[s:e].clone()
+        self._held = (self._held - 1 + S) % S
+        start, end = self._particle_idx_range(self._held)
+        recv = torch.empty_like(send)
+        exchange.ring_shift(send, recv, self._rank, S, self._group)
         self._work[start:end] = recv
         self._particle_start_idx = start
         self._particle_end_idx = end
@@ -192,9 +237,11 @@ class DistSampler(object):
 
     # ------------------------------------------------------------ step --
     def _engine(self, n_int, m, row0):
-        key = (n_int, m, row0)
+        local = self._lagged == "local"
+        key = (n_int, m, row0, local)
         if key not in self._engines:
-            self._engines = {key: PhiEngine(n_int, self._d, m=m, row0=row0, device=self._device)}
+            self._engines = {key: PhiEngine(n_int, self._d, m=m, row0=row0, device=self._device,
+                                            local_median=local)}
         eng = self._engines[key]
         eng.timer = self.timer
         return eng
@@ -206,11 +253,13 @@ class DistSampler(object):
         jacobi = self._order == "jacobi"
         s, e = self._particle_start_idx, self._particle_end_idx
         X = self._work
-        if self._exchange_particles:
+        if self._exchange_particles or self._lagged:
             Xi, lo = X, 0
         else:
             Xi, lo = X[s:e], s
         n_int = Xi.shape[0]
+        # the rows this step moves: the owned / held block, or (updateall) all
+        us, ue = (0, n_int) if self._lagged == "updateall" else (s, e)
         scale = 1.0 if self._exchange_scores else self._N_global / self._N_local
         Si = self._scores if self._exchange_scores else self._score_buffer(Xi.shape)
         median = self._rbf.median
@@ -253,7 +302,7 @@ class DistSampler(object):
                 w2g = self._wasserstein_grad(X[s:e], self._previous_particles, h)
 
         if jacobi:
-            eng = self._engine(n_int, e - s, s - lo)
+            eng = self._engine(n_int, ue - us, us - lo)
             eng.pack(Xi)                           # X half only: the scores are in flight
             eng.distances(median=median)
             if median:
@@ -263,10 +312,10 @@ class DistSampler(object):
             if side is not main:
                 main.wait_stream(side)
             eng.pack_scores(Si)                    # Si already carries the score scale
-            eng.direction(X[s:e], step_size, write_phi=self.keep_phi, extra=w2g)
+            eng.direction(X[us:ue], step_size, write_phi=self.keep_phi, extra=w2g)
         else:
             if median:
-                eng = self._engine(n_int, e - s, s - lo)
+                eng = self._engine(n_int, ue - us, us - lo)
                 eng.pack(Xi)
                 eng.distances(median=True)
                 eng.median_bandwidth(hook)
@@ -278,7 +327,7 @@ class DistSampler(object):
                 N.call("dsvgd_set_bandwidth", state.ptr, float(self._rbf.h),
                        N.stream(self._device))
             tgt = None if self._exchange_scores else self._target
-            sequential_sweep(Xi, Si, range(s - lo, e - lo), state, step_size, target=tgt,
+            sequential_sweep(Xi, Si, range(us - lo, ue - lo), state, step_size, target=tgt,
                              score_scale=scale, extra=w2g)
 
 
@@ -294,6 +343,9 @@ class DistSampler(object):
             if self._exchange_particles:
                 with span(self.timer, "allgather_x"):
                     self._exchange_all_particles()
+            elif self._lagged:
+                with span(self.timer, "ring_shift"):
+                    self._exchange_lagged()
             else:
                 with span(self.timer, "ring_shift"):
                     self._exchange_round_robin()

@@ -17,7 +17,6 @@ median global (RCCL all_reduce of 2048 int64 counts per pass).
 """
 import ctypes
 import math
-import os
 
 import torch
 
@@ -142,7 +141,21 @@ class PhiEngine(object):
     SIGMAS = 6.0                # bracket half-width in sample-rank standard deviations
     SEED = 0x5EED5EED
 
-    def __init__(self, n, d, m=None, row0=0, device=None):
+    GEMMS = ("h2", "x3", "f32")
+    DEFAULT_GEMM = "h2"
+
+    def __init__(self, n, d, m=None, row0=0, device=None, local_median=False, gemm=None,
+                 phi_gemm=None, gram_gemm=None, sym_layout=True):
+        """local_median: the median bandwidth is the lower median of the owned
+        block's own m x n entries (k = (m n - 1) // 2, h = median / log n) --
+        a rank-local bandwidth (the lagged DistSampler modes) -- instead of the
+        n x n matrix's (whose rank k needs every row block's counts).
+
+        gemm: the MFMA engine of the two contractions (phi_gemm / gram_gemm
+        override it per contraction; None: DEFAULT_GEMM): "h2" the fp16 two-part split (default,
+        include/dsvgd.h FmtH2), "x3" the bf16 three-part split, "f32" the exact
+        f32 MFMA (precision reference).  sym_layout=False keeps the full D
+        layout where the symmetric one would apply (layout experiments)."""
         dev = N.require_gpu(device if device is not None else "cuda")
         lib = N.load()
         m = n if m is None else m
@@ -158,27 +171,47 @@ class PhiEngine(object):
         self.norms = torch.zeros(rows, **f32)
         self.D = torch.empty(self.m_pad * self.n_pad, **f32)
         self.splits = lib.dsvgd_phi_splits(m, n, self.ldy)
-        # phi_mm engine: "x3" = bf16 MFMA with a 3-way split (fp32-accurate,
-        # csrc/gemm_x3.hpp), "f32" = the f32 MFMA engine (DSVGD_PHI_GEMM=f32)
-        self.x3 = (os.environ.get("DSVGD_PHI_GEMM", "x3") == "x3"
-                   and self.n_pad * self.ldy * 6 < (1 << 31))
-        if self.x3:
+        gemm = gemm or self.DEFAULT_GEMM
+        phi_gemm = phi_gemm or gemm
+        gram_gemm = gram_gemm or gemm
+        if phi_gemm not in self.GEMMS or gram_gemm not in self.GEMMS:
+            raise ValueError("gemm must be one of %s" % (self.GEMMS,))
+        # the split engines address their images with 32-bit offsets: beyond
+        # that, the exact f32 engine (include/dsvgd.h)
+        bpe = {"h2": 4, "x3": 6}
+        if phi_gemm != "f32" and self.n_pad * self.ldy * bpe[phi_gemm] >= (1 << 31):
+            phi_gemm = "f32"
+        self.gram_rows = self.n_pad + 256   # Yg image rows (include/dsvgd.h, dsvgd_sqdist_x3)
+        if gram_gemm != "f32" and self.dp * self.gram_rows * bpe[gram_gemm] >= (1 << 31):
+            gram_gemm = "f32"
+        self.phi_gemm, self.gram_gemm, self.sym_layout = phi_gemm, gram_gemm, sym_layout
+        if phi_gemm == "x3":
             nb = lib.dsvgd_ysplit_bytes(self.n_pad, self.ldy)
             self.Yx = torch.empty(nb // 2, dtype=torch.int16, device=dev)
-        # distance Gram (d > DIRECT_MAX_D): split engine unless DSVGD_GRAM_GEMM=f32
-        self.gram_rows = self.n_pad + 256   # Yg image rows (include/dsvgd.h, dsvgd_sqdist_x3)
-        self.x3_gram = (os.environ.get("DSVGD_GRAM_GEMM", "x3") == "x3"
-                        and self.dp * self.gram_rows * 6 < (1 << 31))
-        if self.x3_gram:
+        elif phi_gemm == "h2":
+            nb = lib.dsvgd_h2_image_bytes(self.n_pad, self.ldy)
+            self.Yx = torch.empty(nb // 2, dtype=torch.int16, device=dev)
+        if gram_gemm == "x3":
             nb = lib.dsvgd_rowsplit_bytes(self.gram_rows, self.dp)
             self.Yg = torch.empty(nb // 2, dtype=torch.int16, device=dev)
+        elif gram_gemm == "h2":
+            nb = lib.dsvgd_h2_image_bytes(self.gram_rows, self.dp)
+            self.Yg = torch.empty(nb // 2, dtype=torch.int16, device=dev)
+        if "h2" in (phi_gemm, gram_gemm):
+            # FmtH2 scales (dsvgd_h2_colscale layout): of Y's X half for the
+            # Gram, of all of Y for phi_mm's B image
+            self.xscale = torch.empty(2 * self.dp + 2, **f32)
+            self.yscale = torch.empty(2 * self.ldy + 2, **f32)
+            self.scale_ws = torch.empty(
+                max(1, lib.dsvgd_h2_colscale_workspace_floats(self.n_pad, self.ldy)), **f32)
         self.KY = torch.empty(self.splits * m, self.ldy, **f32)
         self.rowsum = torch.empty(self.splits * self.m_pad, **f32)
         self.mean = torch.empty(d, **f32)
         self.mean_ws = torch.empty(max(1, lib.dsvgd_colmean_workspace_floats(n, d)), **f32)
         self.phi = torch.empty(m, d, **f32)
         self.state = SelectState(dev)
-        self.bracketed = m * n >= self.BRACKET_MIN_ENTRIES
+        self.k_rank = (m * n - 1) // 2 if (local_median and m < n) else -1
+        self.bracketed = m * n >= self.BRACKET_MIN_ENTRIES and self.k_rank < 0
         if self.bracketed:
             s = self.SAMPLE
             half = 0.5 * s
@@ -229,22 +262,32 @@ class PhiEngine(object):
                 self._bracket(s)
             st, cand, mode = self.state.ptr, N.ptr(self.cand), SEL_BRACKET
         elif median:
-            N.call("dsvgd_select_init", self.state.ptr, self.n, -1, s)
+            N.call("dsvgd_select_init", self.state.ptr, self.n, self.k_rank, s)
             st, mode = self.state.ptr, SEL_HIST
-        if self.x3_gram and self.d > self.DIRECT_MAX_D:
+        if self.gram_gemm == "h2" and self.d > self.DIRECT_MAX_D:
             with span(self.timer, "rowsplit"):
-                # image swizzle of the Gram form the library runs: 256 tiles on
-                # 16x16x32 (unswizzled), DSVGD_GRAM_TILE=128 on 32x32x16 (swizzled)
-                swz = 1 if (os.environ.get("DSVGD_GRAM_TILE") == "128"
-                            or os.environ.get("DSVGD_GRAM_MFMA") == "32") else 0
+                N.call("dsvgd_h2_colscale", N.ptr(self.Y), self.ldy, self.n_pad, self.dp,
+                       N.ptr(self.scale_ws), N.ptr(self.xscale), s)
+                tsc = N.ptr(self.xscale) + 4 * 2 * self.dp        # [t, 1/t]
+                N.call("dsvgd_h2_rowsplit", N.ptr(self.Y), self.ldy, self.n_pad, self.dp,
+                       self.gram_rows, self.dp, tsc, N.ptr(self.Yg), s)
+            with span(self.timer, "sqdist"):
+                N.call("dsvgd_sqdist_h2", N.ptr(self.Yg), N.ptr(self.norms), self.row0, self.m,
+                       self.n, self.d, N.ptr(self.D), self.n_pad, mode, st, cand, int(self.sym),
+                       tsc, s)
+            return
+        if self.gram_gemm == "x3" and self.d > self.DIRECT_MAX_D:
+            with span(self.timer, "rowsplit"):
+                # the 256-tile Gram runs 16x16x32 MFMAs on an unswizzled image
                 N.call("dsvgd_rowsplit", N.ptr(self.Y), self.ldy, self.n_pad, self.dp,
-                       self.gram_rows, self.dp, N.ptr(self.Yg), swz, s)
+                       self.gram_rows, self.dp, N.ptr(self.Yg), 0, s)
             with span(self.timer, "sqdist"):
                 N.call("dsvgd_sqdist_x3", N.ptr(self.Yg), N.ptr(self.norms), self.row0, self.m,
                        self.n, self.d, N.ptr(self.D), self.n_pad, mode, st, cand, int(self.sym), s)
             return
         with span(self.timer, "sqdist"):
-            N.call("dsvgd_sqdist", N.ptr(self.Y), self.ldy, N.ptr(self.norms), self.row0, self.m,
+            fn = "dsvgd_sqdist_direct" if self.d <= self.DIRECT_MAX_D else "dsvgd_sqdist"
+            N.call(fn, N.ptr(self.Y), self.ldy, N.ptr(self.norms), self.row0, self.m,
                    self.n, self.d, N.ptr(self.D), self.n_pad, mode, st, cand, s)
 
     def _bracket(self, s):
@@ -290,20 +333,28 @@ class PhiEngine(object):
     DIRECT_MAX_D = 2
 
     @property
+    def x3(self):
+        """phi_mm runs on a split engine (h2 or x3), not the f32 MFMA."""
+        return self.phi_gemm != "f32"
+
+    @property
+    def x3_gram(self):
+        """the Gram runs on a split engine (h2 or x3), not the f32 MFMA."""
+        return self.gram_gemm != "f32"
+
+    @property
     def m16(self):
-        """phi_mm's split engine on v_mfma_f32_16x16x32_bf16 (ldy % 256 == 0;
-        DSVGD_X3_MFMA=32 selects the 32x32x16 form)."""
-        return self.ldy % 256 == 0 and os.environ.get("DSVGD_X3_MFMA", "16") != "32"
+        """phi_mm's x3 engine on v_mfma_f32_16x16x32_bf16 (ldy % 256 == 0)."""
+        return self.phi_gemm == "x3" and self.ldy % 256 == 0
 
     @property
     def sym(self):
         """D is in the symmetric layout (upper-triangle tiles only, written by
-        dsvgd_sqdist_x3 layout 1 and read transposed by dsvgd_phi_mm_x3 and
-        dsvgd_radix_hist): the whole n x n matrix on the split engines, with
-        ldy % 256 == 0.  DSVGD_SYM_LAYOUT=0 keeps the full layout."""
+        dsvgd_sqdist_{h2,x3} layout 1 and read transposed by dsvgd_phi_mm_{h2,x3}
+        and dsvgd_radix_hist): the whole n x n matrix on the split engines,
+        with ldy % 256 == 0."""
         return (self.m == self.n and self.row0 == 0 and self.d > self.DIRECT_MAX_D
-                and self.x3 and self.x3_gram and self.ldy % 256 == 0
-                and os.environ.get("DSVGD_SYM_LAYOUT", "1") != "0")
+                and self.x3 and self.x3_gram and self.ldy % 256 == 0 and self.sym_layout)
 
     def direction(self, X_own=None, step=0.0, write_phi=True, inv_n=None, extra=None):
         """phi for the owned rows (+ `extra`, e.g. the h * W2 gradient rows);
@@ -327,7 +378,18 @@ class PhiEngine(object):
                        float(step), ex, lde, phi, self.d, xo, ldx, N.ptr(self.KY),
                        self.KY.numel(), s)
             return
-        if self.x3:
+        if self.phi_gemm == "h2":
+            with span(self.timer, "ysplit"):
+                N.call("dsvgd_h2_colscale", N.ptr(self.Y), self.ldy, self.n_pad, self.ldy,
+                       N.ptr(self.scale_ws), N.ptr(self.yscale), s)
+                N.call("dsvgd_h2_ysplit", N.ptr(self.Y), self.ldy, self.n_pad,
+                       N.ptr(self.yscale), N.ptr(self.Yx), s)
+            with span(self.timer, "phi_mm"):
+                N.call("dsvgd_phi_mm_h2", N.ptr(self.D), self.n_pad, N.ptr(self.Yx), self.ldy,
+                       self.row0, self.m, self.n, self.state.ptr, self.splits, N.ptr(self.KY),
+                       self.ldy, N.ptr(self.rowsum), int(self.sym),
+                       N.ptr(self.yscale) + 4 * self.ldy, s)
+        elif self.x3:
             m16 = self.m16
             with span(self.timer, "ysplit"):
                 N.call("dsvgd_ysplit", N.ptr(self.Y), self.ldy, self.n_pad, N.ptr(self.Yx),

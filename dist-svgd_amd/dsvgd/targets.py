@@ -82,10 +82,16 @@ class LogisticRegression(BuiltinTarget):
     the reference), w ~ N(0, I/alpha), labels t in {-1, +1}.
     """
 
-    def __init__(self, x_train, t_train):
+    ENGINES = {"h2": 0, "x3": 1, "f32": 2}   # dsvgd_score_logreg_engine
+    SMALL_ROWS = 32      # one-block-per-particle path (no workspace), csrc/logreg.hip
+
+    def __init__(self, x_train, t_train, gemm="h2"):
         self.x = torch.as_tensor(x_train, dtype=torch.float32)
         self.t = torch.as_tensor(t_train, dtype=torch.float32).reshape(-1)
         assert self.x.shape[0] == self.t.shape[0]
+        if gemm not in self.ENGINES:
+            raise ValueError("gemm must be one of %s" % sorted(self.ENGINES))
+        self.gemm = gemm
         self._dev = {}
         self._ws = {}
 
@@ -115,19 +121,26 @@ class LogisticRegression(BuiltinTarget):
         n, d = X.shape
         assert d == self.x.shape[1] + 1, "logreg target has d = 1 + p = %d" % (self.x.shape[1] + 1)
         xd, t = self._params(X.device)
-        key = (X.device, n)
+        # one workspace per (device, n), kept for the target's lifetime: a
+        # captured HIP graph (engine.StepGraph) holds its address, so it is
+        # never freed behind one (release() frees them explicitly).  The
+        # few-particle path (the Gauss-Seidel refreshes) needs none.
+        small = n <= self.SMALL_ROWS and (d - 1 <= 32 or self.N <= 8192)   # logreg.hip's test
+        key = (X.device, 0 if small else n)
         ws = self._ws.get(key)
         if ws is None:
-            nbytes = N.load().dsvgd_logreg_workspace_bytes(n, self.N, d - 1)
+            nbytes = N.load().dsvgd_logreg_workspace_bytes(n, self.N, d - 1) if key[1] else 256
             ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device=X.device)
-            if len(self._ws) >= 4:         # workspaces can be GiBs: keep a few
-                self._ws.clear()
             self._ws[key] = ws
         base = ws.data_ptr()
         aligned = (base + 255) // 256 * 256
-        N.call("dsvgd_score_logreg", N.ptr(X), N.ld(X), n, d, N.ptr(xd), N.ld(xd),
+        N.call("dsvgd_score_logreg_engine", N.ptr(X), N.ld(X), n, d, N.ptr(xd), N.ld(xd),
                N.ptr(t), self.N, float(scale), N.ptr(out), N.ld(out), aligned,
-               N.stream(X.device))
+               self.ENGINES[self.gemm], N.stream(X.device))
+
+    def release(self):
+        """Free the score workspaces (no graph that captured them may replay after)."""
+        self._ws.clear()
 
 
 class CallableTarget(Target):

@@ -11,7 +11,6 @@ epilogue as `extra`, so the update is x_i += step * (phi_i + G_i) as at
 distsampler.py:196-200.
 """
 import ctypes
-import os
 
 import torch
 
@@ -50,8 +49,6 @@ class W2Term(object):
                N.ptr(self.C), self.n, s)
         rounds = ctypes.c_int64(0)
         warm = self.WARM_PHASES if (self.warm and self._solved) else 0
-        if warm and os.environ.get("DSVGD_W2_WARM_PHASES"):     # experiments only
-            warm = max(0, int(os.environ["DSVGD_W2_WARM_PHASES"]))
         N.call("dsvgd_w2_assign", N.ptr(self.C), self.n, self.m, self.n, N.ptr(self.ws),
                self.MAX_ROUNDS, warm, N.ptr(self.assign), ctypes.addressof(rounds), s)
         self.rounds = int(rounds.value)

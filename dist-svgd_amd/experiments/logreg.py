@@ -47,6 +47,10 @@ RESULTS_DIR = os.environ.get("DSVGD_RESULTS_DIR", os.path.join(os.getcwd(), "res
 DATASETS = ['banana', 'diabetis', 'german', 'image', 'splice', 'titanic', 'waveform']
 
 
+# notes.md:108-114,134-135 (described and timed there, no code in the reference)
+LAGGED = {'laggedlocal': 'local', 'laggedlocal-updateall': 'updateall'}
+
+
 def get_results_dir(dataset_name, fold, nproc, nparticles, stepsize, exchange, wasserstein,
                     results_dir=None):
     """logreg_plots.py:19-22 (same subdirectory name)."""
@@ -104,7 +108,8 @@ def run(rank, num_shards, dataset_name, fold, nparticles, niter, stepsize, excha
                                 samples_per_shard, samples_per_shard * num_shards,
                                 exchange_particles=exchange in ['all_particles', 'all_scores'],
                                 exchange_scores=exchange == 'all_scores',
-                                include_wasserstein=wasserstein, order=order)
+                                include_wasserstein=wasserstein, order=order,
+                                lagged=LAGGED.get(exchange))
     m = sampler.particles.shape[0]
     hist = torch.empty(niter + 1, m, d, dtype=torch.float32, device=dev)
     torch.cuda.synchronize(dev)
@@ -180,7 +185,8 @@ def _init_distributed(rank, nproc, port, args):
 @click.option('--nparticles', type=int, default=10)
 @click.option('--niter', type=int, default=100)
 @click.option('--stepsize', type=float, default=1e-3)
-@click.option('--exchange', type=click.Choice(['partitions', 'all_particles', 'all_scores']),
+@click.option('--exchange', type=click.Choice(['partitions', 'all_particles', 'all_scores']
+                                               + sorted(LAGGED)),
               default='partitions')
 @click.option('--wasserstein/--no-wasserstein', default=False)
 @click.option('--master_addr', default='127.0.0.1', type=str)

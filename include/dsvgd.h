@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DSVGD_ABI_VERSION 1
+#define DSVGD_ABI_VERSION 2
 
 enum {
   DSVGD_OK = 0,
@@ -123,6 +123,11 @@ int dsvgd_pack(const float* X, int64_t ldx, const float* S, int64_t lds, float s
 int dsvgd_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0, int64_t m,
                  int64_t n, int64_t d, float* D, int64_t ldd, int select_mode,
                  dsvgd_select_state* st, float* cand, void* stream);
+/* dsvgd_sqdist's explicit-difference kernel forced for any d <= 64 (the
+ * precision studies of DESIGN.md 3; dsvgd_sqdist takes it for d <= 2). */
+int dsvgd_sqdist_direct(const float* Y, int64_t ldy, const float* norms, int64_t row0, int64_t m,
+                        int64_t n, int64_t d, float* D, int64_t ldd, int select_mode,
+                        dsvgd_select_state* st, float* cand, void* stream);
 
 /* ---- median bandwidth: exact radix select over the n x n distances ----- */
 /* (absent in the reference, whose kernel bandwidth is fixed at h=1; the
@@ -162,7 +167,6 @@ int dsvgd_set_bandwidth(dsvgd_select_state* st, float h, void* stream);
 
 /* dsvgd_sqdist's Gram path (d > 2) on the split engine (fp32-accurate, see
  * dsvgd_phi_mm_x3): Yg = dsvgd_rowsplit(Y, ldy, n_pad, dp, n_pad + 256, dp, 0)
- * (swz 1 under DSVGD_GRAM_TILE=128, the 32x32x16 A/B form)
  * with dp = roundup(d, 32), n_pad = roundup(n, 128) (256 rows of zero slack
  * for the 256 x 256 tiles); same outputs and select
  * modes as dsvgd_sqdist.  layout 0: the full panel-layout D; layout 1 (m ==
@@ -217,6 +221,50 @@ int dsvgd_ysplit(const float* Y, int64_t ldy, int64_t rows, void* Yx, int swz, v
 int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, int64_t row0,
                     int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
                     int64_t ldk, float* rowsum, int sym, int m16, void* stream);
+
+/* ---- FmtH2: the fp16 two-part split engine (the default) ---------------
+ * An operand v enters the fp16 MFMA as s v = v0 + v1, v0 = f16(s v),
+ * v1 = f16(s v - v0), s a power of two putting the operand's largest
+ * magnitude in [2^14, 2^15); the products a0 b0 + a0 b1 + a1 b0 are exact in
+ * fp32 and the dropped a1 b1 and split remainder are <= 2^-22 relative, below
+ * the fp32 accumulation rounding of any of these GEMMs: fp32-level results
+ * from half the MFMAs of the X3 engine (gemm_x3.hpp, h2.hip).  The scale
+ * divides out exactly inside each kernel: outputs are unscaled fp32.
+ *
+ * dsvgd_h2_colscale: per column c of A (rows x cols), scale[c] = s_c and
+ * scale[cols + c] = 1 / s_c; scale[2 cols] = t = min s_c over the nonzero
+ * finite columns (1 if a column holds an inf / NaN, which then propagate),
+ * scale[2 cols + 1] = 1 / t.  scale: 2 cols + 2 floats; ws:
+ * dsvgd_h2_colscale_workspace_floats(rows, cols) floats. */
+size_t dsvgd_h2_colscale_workspace_floats(int64_t rows, int64_t cols);
+int dsvgd_h2_colscale(const float* A, int64_t lda, int64_t rows, int64_t cols, float* ws,
+                      float* scale, void* stream);
+/* fp16 images (dsvgd_h2_image_bytes(rows, cols) bytes, 16-byte aligned):
+ * ysplit: Yh[kstep][part][column][16] of colscale[c] * Y[16 kstep + k][c]
+ * (the NN engine's B operand, rows a multiple of 16); rowsplit:
+ * img[kstep][part][row][16] of tscale[0] * A[row][16 kstep + k] (the NT
+ * engine's operands, zero outside rows x cols).  16-byte halves swapped on
+ * columns / rows with bit 3 set (32x32x16 fragment reads). */
+int64_t dsvgd_h2_image_bytes(int64_t rows, int64_t cols);
+int dsvgd_h2_ysplit(const float* Y, int64_t ldy, int64_t rows, const float* colscale, void* Yh,
+                    void* stream);
+int dsvgd_h2_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                      int64_t kpad, const float* tscale, void* img, void* stream);
+/* dsvgd_sqdist_x3 on the FmtH2 engine: Yg = dsvgd_h2_rowsplit(Y, ldy,
+ * n_pad, dp, n_pad + 256, dp, tscale) with tscale = &scale[2 dp] of a
+ * dsvgd_h2_colscale over Y's first dp columns ([t, 1/t]); same outputs,
+ * select modes and layouts. */
+int dsvgd_sqdist_h2(const void* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
+                    int64_t d, float* D, int64_t ldd, int select_mode, dsvgd_select_state* st,
+                    float* cand, int layout, const float* tscale, void* stream);
+/* dsvgd_phi_mm_x3 on the FmtH2 engine: Yh = dsvgd_h2_ysplit(Y, ldy, n_pad,
+ * scale) and colinv = &scale[ldy] of a dsvgd_h2_colscale over all ldy
+ * columns of Y; same outputs (unscaled), split-K slices, diagonal rule and
+ * symmetric layout (sym needs ldy % 256 == 0).  Requires n_pad * ldy * 4 <
+ * 2^31. */
+int dsvgd_phi_mm_h2(const float* D, int64_t ldd, const void* Yh, int64_t ldy, int64_t row0,
+                    int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
+                    int64_t ldk, float* rowsum, int sym, const float* colinv, void* stream);
 
 /* phi[i] = inv_n * (s_i + KS[i] + (2/h) (rowsum[i] xc[i] - KXc[i])) with the
  * split-K partials summed in slice order (s_i: the self term k_ii s_i), plus
@@ -302,6 +350,11 @@ size_t dsvgd_logreg_workspace_bytes(int64_t n, int64_t N, int64_t p);
 int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const float* Xd,
                        int64_t ldxd, const float* t, int64_t N, float scale, float* S, int64_t lds,
                        void* workspace, void* stream);
+/* the same on a chosen GEMM engine: 0 = FmtH2 (what dsvgd_score_logreg
+ * runs), 1 = FmtX3, 2 = the exact f32 MFMA engines (precision reference) */
+int dsvgd_score_logreg_engine(const float* X, int64_t ldx, int64_t n, int64_t d, const float* Xd,
+                              int64_t ldxd, const float* t, int64_t N, float scale, float* S,
+                              int64_t lds, void* workspace, int engine, void* stream);
 
 /* Posterior-predictive probability of the logistic-regression test set:
  * prob[q] = (1/n) sum_j sigma(xt_q . w_j), w_j = X[j][1:d] (no bias; alpha

@@ -230,7 +230,7 @@ class DistOracle:
 
     def __init__(self, particles, score_fns, N_local, N_global, exchange_particles,
                  exchange_scores, h=1.0, sequential=True, include_wasserstein=False,
-                 replicated=False):
+                 replicated=False, lagged=None):
         assert not (exchange_scores and not exchange_particles)
         self.S = len(particles)
         n = np.asarray(particles[0]).shape[0]
@@ -249,6 +249,15 @@ class DistOracle:
         # set): each rank scores its owned block, the blocks are gathered --
         # the same numbers as every rank scoring all n (identical score_fns)
         self.replicated = replicated and exchange_particles and not exchange_scores and self.S > 1
+        # lagged modes (notes.md:108-114): full local copies, blocks travel
+        # round-robin and land in their home rows; "local" moves the held
+        # block against the whole copy, "updateall" moves the whole copy.
+        # h = "median": the held block's own m x n lower median (updateall:
+        # the copy's n x n), / log n
+        assert lagged in (None, "local", "updateall")
+        assert not (lagged and (exchange_particles or exchange_scores))
+        self.lagged = lagged
+        self.held = list(range(self.S))
 
     def own(self, r):
         return self.X[r][self.start[r]:self.start[r] + self.per]
@@ -269,6 +278,14 @@ class DistOracle:
                 g = np.concatenate([scale * self.score_fns[r](self.own(r)) for r in range(S)])
                 return [g.copy() for _ in range(S)]
             return None
+        if self.lagged:
+            sent = [(self.held[r], self.own(r).copy()) for r in range(S)]
+            for r in range(S):
+                b, rows = sent[(r - 1 + S) % S]
+                self.held[r] = b
+                self.start[r] = b * self.per
+                self.X[r][self.start[r]:self.start[r] + self.per] = rows
+            return None
         blocks = [self.own(r).copy() for r in range(S)]
         for r in range(S):
             src = (r - 1 + S) % S
@@ -284,7 +301,13 @@ class DistOracle:
         for r in range(self.S):
             Xr = self.X[r]
             s0, s1 = self.start[r], self.start[r] + self.per
-            lo, hi = (0, self.n) if self.xp else (s0, s1)
+            lo, hi = (0, self.n) if (self.xp or self.lagged) else (s0, s1)
+            if self.lagged == "updateall":
+                s0, s1 = 0, self.n
+            h = self.h
+            if h == "median":     # all_particles: the global n x n (identical copies)
+                med = lower_median(sqdist(Xr[lo:hi] if self.xp else Xr[s0:s1], Xr[lo:hi]))
+                h = med / math.log(hi - lo) if (hi - lo > 1 and med > 0) else 1.0
             scale = 1.0 if self.xs else self.N_global / self.N_local
             extra = np.zeros((s1 - s0, Xr.shape[1]))
             if self.w2 and self.prev[r] is not None:
@@ -299,12 +322,12 @@ class DistOracle:
                         Sj[s0:s1] = scale * self.score_fns[r](Xr[s0:s1])
                     else:
                         Sj = scale * self.score_fns[r](Xi)
-                    Xr[i] += step_size * (phi(Xi, Sj, self.h, rows=[i - lo])[0] + extra[i - s0])
+                    Xr[i] += step_size * (phi(Xi, Sj, h, rows=[i - lo])[0] + extra[i - s0])
             else:
                 Xi = Xr[lo:hi].copy()
                 Sj = scores[r][lo:hi] if (self.xs or self.replicated) else \
                     scale * self.score_fns[r](Xi)
-                Xr[s0:s1] += step_size * (phi(Xi, Sj, self.h, rows=np.arange(s0 - lo, s1 - lo))
+                Xr[s0:s1] += step_size * (phi(Xi, Sj, h, rows=np.arange(s0 - lo, s1 - lo))
                                           + extra)
             if self.w2:
                 self.prev[r] = (Xr if self.xp else Xr[s0:s1]).copy()

@@ -20,7 +20,7 @@ step() {  # name timeout cmd...
 for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step tests 1500 python -u -m pytest tests -m gpu -v -x --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} ;;
+    tests) step tests 1500 python -u -m pytest ${TESTS:-tests} -m gpu -v -x --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} ;;
     bench) step bench 900 python bench.py --steps ${BSTEPS:-10} --warmup 3 ${BENCH_ARGS:-} ;;
     prof)  step prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     ab)    step ab 600 python scripts/ab_kernels.py ;;

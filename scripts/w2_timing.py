@@ -72,8 +72,9 @@ def main():
                     help="warm-start phases 1..5 on two R > 1 shapes")
     args = ap.parse_args()
     if args.warm_sweep:
+        import dsvgd
         for ph in (1, 2, 3, 4, 5):
-            os.environ["DSVGD_W2_WARM_PHASES"] = str(ph)
+            dsvgd.w2.W2Term.WARM_PHASES = ph
             for sh in ((1024, 8192, 16, "svgd"), (2048, 16384, 256, "svgd")):
                 r = case(*sh)
                 print(json.dumps({"warm_phases": ph, "m": sh[0], "n": sh[1],

@@ -226,10 +226,10 @@ def test_phi_matches_oracle(n, d, median):
 
 
 @pytest.mark.parametrize("n,d", [(640, 64), (3000, 8)])
-def test_direct_kernels_up_to_d64(n, d, monkeypatch):
+def test_direct_kernels_up_to_d64(n, d):
     """The explicit-difference kernels (default for d <= 2) stay exact up to
-    their d = 64 limit (forced here through the engine / library switches)."""
-    monkeypatch.setenv("DSVGD_SQ_DIRECT_MAX_D", "64")
+    their d = 64 limit (forced here through the engine: dsvgd_sqdist_direct,
+    dsvgd_phi_direct)."""
     rs = np.random.RandomState(n + d)
     X = rs.randn(n, d).astype(np.float32)
     S = O.score_gmm(X).astype(np.float32)

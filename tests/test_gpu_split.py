@@ -1,0 +1,297 @@
+"""The split MFMA engines against the exact-fp32 MFMA engine and the fp64
+oracle: FmtH2 (two fp16 parts of a power-of-two-scaled operand, three
+products; the default) and FmtX3 (three bf16 parts, six products), both in
+csrc/gemm_x3.hpp.
+
+Claim under test: a split engine carries fp32 GEMM rounding, not its input
+format's -- so (1) its images reconstruct every fp32 input (FmtX3 to 2^-24,
+FmtH2 to 2^-22 for entries within 2^-18 of their column's largest), (2)
+phi_mm's K.[Xc|S] is as close to the fp64 product of the same D as the f32
+engine's (within 2x + 1e-7; bf16 alone would be ~2^-9 off, fp16 ~2^-12) and
+its row sums match the f32 engine's, (3) the distances and the logreg scores
+likewise, and (4) phi through it meets the north_star tolerance (1e-5
+max-normalised vs fp64) on the cases the f32 path is tested on.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import record_parity
+from oracle import svgd_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+PHI_TOL = 1e-5
+KY_TOL = 5e-6
+SPLIT = ["h2", "x3"]
+
+
+def dsvgd():
+    import dsvgd as m
+    return m
+
+
+def gpu(a):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float32, device=DEV)
+
+
+def decode_ysplit(Yx, rows, ldy):
+    """CPU inverse of dsvgd_ysplit's (FmtX3) image: (3, rows, ldy) float64 parts."""
+    raw = Yx.cpu().numpy().view(np.uint16).astype(np.uint32) << 16
+    v = raw.view(np.float32).astype(np.float64).reshape(rows // 16, 3, ldy, 2, 8)
+    sw = (np.arange(ldy) >> 3) & 1
+    out = np.empty((3, rows, ldy))
+    for c in range(ldy):
+        halves = v[:, :, c, :, :]
+        if sw[c]:
+            halves = halves[:, :, ::-1, :]
+        out[:, :, c] = halves.reshape(rows // 16, 3, 16).transpose(1, 0, 2).reshape(3, rows)
+    return out
+
+
+def decode_h2(img, kdim, xdim):
+    """CPU inverse of an FmtH2 image img[kstep][part][x][16 k] (16-B halves
+    swapped on x with bit 3 set): (2, kdim, xdim) float64 parts."""
+    v = img.cpu().numpy().view(np.float16).astype(np.float64).reshape(kdim // 16, 2, xdim, 2, 8)
+    v = np.where(((np.arange(xdim) >> 3) & 1)[None, None, :, None, None] == 1, v[:, :, :, ::-1, :], v)
+    return v.reshape(kdim // 16, 2, xdim, 16).transpose(1, 0, 3, 2).reshape(2, kdim, xdim)
+
+
+@pytest.mark.parametrize("rows,ldy", [(128, 128), (256, 512), (64, 200)])
+def test_ysplit_reconstructs_fp32(rows, ldy):
+    from dsvgd import _native as N
+    rs = np.random.RandomState(rows + ldy)
+    Y = (rs.randn(rows, ldy) * np.exp(rs.uniform(-20, 20, (rows, ldy)))).astype(np.float32)
+    Y[0, :8] = 0.0
+    lib = N.load()
+    Yx = torch.empty(lib.dsvgd_ysplit_bytes(rows, ldy) // 2, dtype=torch.int16, device=DEV)
+    N.call("dsvgd_ysplit", N.ptr(gpu(Y)), ldy, rows, N.ptr(Yx), 1, N.stream(torch.device(DEV)))
+    torch.cuda.synchronize()
+    parts = decode_ysplit(Yx, rows, ldy)
+    rec = parts.sum(0)
+    Y64 = Y.astype(np.float64)
+    err = np.abs(rec - Y64) / np.maximum(np.abs(Y64), 1e-300)
+    record_parity(float(err.max()))
+    assert err.max() <= 2.0 ** -24
+    # each part is at most half an ulp(bf16) of the remainder before it
+    assert np.all(np.abs(parts[1]) <= np.abs(Y64) * 2.0 ** -8 + 1e-300)
+
+
+@pytest.mark.parametrize("rows,ldy", [(128, 128), (512, 512), (64, 256)])
+def test_h2_images_reconstruct_fp32(rows, ldy):
+    """dsvgd_h2_colscale + dsvgd_h2_ysplit / dsvgd_h2_rowsplit: power-of-two
+    scales putting each column's (tensor's) largest magnitude in [2^14, 2^15),
+    parts that sum back to s v within 2^-22 relative for entries within 2^-18
+    of the scale's reference magnitude, zero / inf / NaN columns handled."""
+    from dsvgd import _native as N
+    lib = N.load()
+    s = N.stream(torch.device(DEV))
+    rs = np.random.RandomState(rows + ldy)
+    colmag = np.exp(rs.uniform(-12, 12, ldy))
+    Y = (rs.randn(rows, ldy) * colmag).astype(np.float32)
+    Y[:, 3] = 0.0                                   # all-zero column: scale 1
+    Yg = gpu(Y)
+    ws = torch.empty(lib.dsvgd_h2_colscale_workspace_floats(rows, ldy), device=DEV)
+    sc = torch.empty(2 * ldy + 2, device=DEV)
+    N.call("dsvgd_h2_colscale", N.ptr(Yg), ldy, rows, ldy, N.ptr(ws), N.ptr(sc), s)
+    img = torch.empty(lib.dsvgd_h2_image_bytes(rows, ldy) // 2, dtype=torch.int16, device=DEV)
+    N.call("dsvgd_h2_ysplit", N.ptr(Yg), ldy, rows, N.ptr(sc), N.ptr(img), s)
+    torch.cuda.synchronize()
+    scale = sc.cpu().numpy().astype(np.float64)
+    s_c = scale[:ldy]
+    mx = np.abs(Y).max(0).astype(np.float64)
+    live = mx > 0
+    assert np.all(np.log2(s_c) == np.round(np.log2(s_c)))           # powers of two
+    assert np.all((s_c * mx)[live] >= 2.0 ** 14) and np.all((s_c * mx)[live] < 2.0 ** 15)
+    assert s_c[3] == 1.0 and np.all(scale[ldy:2 * ldy] * s_c == 1.0)
+    assert scale[2 * ldy] == s_c[live].min() and scale[2 * ldy + 1] * scale[2 * ldy] == 1.0
+    parts = decode_h2(img, rows, ldy)
+    rec = parts.sum(0) / s_c[None, :]
+    Y64 = Y.astype(np.float64)
+    big = np.abs(Y64) >= mx[None, :] * 2.0 ** -18
+    err = np.abs(rec - Y64)[big] / np.abs(Y64)[big]
+    record_parity(float(err.max()))
+    assert err.max() <= 2.0 ** -22
+    assert np.all(np.abs(rec - Y64) <= 2.0 ** -22 * np.abs(Y64) + 2.0 ** -38 * mx[None, :])
+    # the row image of the same tensor with its tensor scale
+    t = sc[2 * ldy:2 * ldy + 1]
+    img2 = torch.empty(lib.dsvgd_h2_image_bytes(rows + 16, ldy) // 2, dtype=torch.int16, device=DEV)
+    N.call("dsvgd_h2_rowsplit", N.ptr(Yg), ldy, rows, ldy, rows + 16, ldy, N.ptr(t),
+           N.ptr(img2), s)
+    torch.cuda.synchronize()
+    rp = decode_h2(img2, ldy, rows + 16)                       # (2, k, row)
+    rec2 = rp.sum(0).T / scale[2 * ldy]
+    assert np.all(rec2[rows:] == 0.0)
+    tb = np.abs(Y64) >= np.abs(Y64).max() * 2.0 ** -18
+    assert np.all(np.abs(rec2[:rows] - Y64)[tb] <= 2.0 ** -22 * np.abs(Y64)[tb])
+    # a non-finite column forces the tensor scale to 1 (inf / NaN propagate)
+    Y[5, 7] = np.inf
+    N.call("dsvgd_h2_colscale", N.ptr(gpu(Y)), ldy, rows, ldy, N.ptr(ws), N.ptr(sc), s)
+    torch.cuda.synchronize()
+    assert float(sc[7]) == 1.0 and float(sc[2 * ldy]) == 1.0
+
+
+def _engines(X, S, h, split, m=None, row0=0):
+    """phi and the raw (KY, rowsum) of one step through the f32 engine and `split`."""
+    out = {}
+    for gemm in ("f32", split):
+        n, d = X.shape
+        # the same (split) Gram under both: phi_mm compared on identical D
+        eng = dsvgd().PhiEngine(n, d, m=m, row0=row0, device=DEV, phi_gemm=gemm, gram_gemm=split)
+        assert eng.phi_gemm == gemm
+        Xo = gpu(X[row0:row0 + eng.m]).clone()
+        eng.pack(gpu(X), gpu(S))
+        eng.distances(median=h is None)
+        if h is None:
+            eng.median_bandwidth()
+        else:
+            eng.fixed_bandwidth(h)
+        eng.direction(Xo, 0.0)
+        torch.cuda.synchronize()
+        KY = eng.KY.view(eng.splits, eng.m, eng.ldy).double().sum(0).cpu().numpy()
+        r = eng.rowsum.view(eng.splits, eng.m_pad)[:, :eng.m].double().sum(0).cpu().numpy()
+        out[gemm] = (eng.phi.cpu().numpy(), KY, r, eng.state.read()[1], eng)
+    # the exact K.[Xc|S] of the split engine's own D (fp64), diagonal left out like phi_mm
+    eng = out[split][4]
+    D = eng.dense_D().double()
+    K = torch.exp(-D / out[split][3])
+    rows = torch.arange(eng.m, device=DEV)
+    K[rows, rows + row0] = 0.0
+    Y = eng.Y[:n].double()
+    out["exact"] = ((K @ Y).cpu().numpy(), K.sum(1).cpu().numpy())
+    return out
+
+
+def _ky_errors(res, split):
+    """max-normalised error of each engine's KY against the fp64 product."""
+    KY64 = res["exact"][0]
+    scale = np.abs(KY64).max()
+    return {g: float(np.abs(res[g][1] - KY64).max() / scale) for g in ("f32", split)}
+
+
+@pytest.mark.parametrize("split", SPLIT)
+@pytest.mark.parametrize("n,d,h", [(300, 20, 5.0), (1000, 64, None), (2048, 256, None),
+                                   (513, 100, 40.0), (4096, 3, None), (1500, 1024, None),
+                                   (777, 500, None)])
+def test_phi_mm_split_matches_f32_engine_and_oracle(split, n, d, h):
+    rs = np.random.RandomState(n + d)
+    X = rs.randn(n, d).astype(np.float32)
+    S = (-X + 0.3 * rs.randn(n, d)).astype(np.float32)
+    res = _engines(X, S, h, split)
+    phix, KYx, rx, hx, _ = res[split]
+    assert res["f32"][3] == hx
+    e = _ky_errors(res, split)
+    record_parity(e[split])
+    assert e[split] <= 2.0 * e["f32"] + 1e-7 and e[split] < KY_TOL, e
+    e_r = float(np.abs(rx - res["exact"][1]).max() / np.abs(res["exact"][1]).max())
+    assert e_r < 1e-6
+    ref = O.phi(X, S, hx)
+    e_phi = float(np.abs(phix - ref).max() / np.abs(ref).max())
+    record_parity(e_phi)
+    assert e_phi < PHI_TOL
+
+
+@pytest.mark.parametrize("split", SPLIT)
+def test_phi_mm_split_row_block_split_k(split):
+    """A DistSampler rank's block (m < n, row0 > 0): diagonal offset, split-K."""
+    n, d, m, row0 = 4096, 128, 1024, 2048
+    rs = np.random.RandomState(11)
+    X = rs.randn(n, d).astype(np.float32)
+    S = rs.randn(n, d).astype(np.float32)
+    res = _engines(X, S, 30.0, split, m=m, row0=row0)
+    phix = res[split][0]
+    e = _ky_errors(res, split)
+    assert e[split] <= 2.0 * e["f32"] + 1e-7 and e[split] < KY_TOL, e
+    ref = O.phi(X, S, 30.0, rows=np.arange(row0, row0 + m))
+    e = float(np.abs(phix - ref).max() / np.abs(ref).max())
+    record_parity(e)
+    assert e < PHI_TOL
+
+
+def test_phi_mm_h2_wide_column_range():
+    """FmtH2's per-column scales: scores 1e4 x larger than the particles (one
+    tensor scale would leave Xc's columns with ~2^-4 of fp16's precision)."""
+    n, d = 2048, 64
+    rs = np.random.RandomState(12)
+    X = (1e-3 * rs.randn(n, d)).astype(np.float32)
+    S = (10.0 * rs.randn(n, d)).astype(np.float32)
+    res = _engines(X, S, None, "h2")
+    e = _ky_errors(res, "h2")
+    assert e["h2"] < KY_TOL, e
+    ref = O.phi(X, S, res["h2"][3])
+    e_phi = float(np.abs(res["h2"][0] - ref).max() / np.abs(ref).max())
+    record_parity(e_phi)
+    assert e_phi < PHI_TOL
+
+
+@pytest.mark.parametrize("split", SPLIT)
+@pytest.mark.parametrize("n,N,p", [(1000, 3000, 20), (512, 16384, 255), (300, 129, 40),
+                                   (600, 2000, 1023), (257, 700, 511)])
+def test_logreg_scores_split_as_accurate_as_f32(split, n, N, p):
+    """The logreg score GEMMs (Z = W Xd^T on the split NT engine, G Xd on the
+    split NN engine without exp) against the fp64 oracle, next to the f32 MFMA
+    engines on the same inputs."""
+    rs = np.random.RandomState(n + N + p)
+    X = (rs.randn(n, p + 1) * 0.5).astype(np.float32)
+    xd = (rs.randn(N, p) / np.sqrt(p)).astype(np.float32)
+    t = np.where(rs.randn(N) > 0, 1.0, -1.0).astype(np.float32)
+    ref = O.score_logreg(X, xd, t)
+    err = {}
+    for gemm in ("f32", split):
+        tgt = dsvgd().targets.LogisticRegression(xd, t, gemm=gemm)
+        out = torch.zeros(n, p + 1, device=DEV)
+        tgt.score(gpu(X), out)
+        err[gemm] = float(np.abs(out.cpu().numpy() - ref).max() / np.abs(ref).max())
+    record_parity(err[split])
+    assert err[split] <= 2.0 * err["f32"] + 1e-7 and err[split] < 1e-5, err
+
+
+@pytest.mark.parametrize("split", SPLIT)
+@pytest.mark.parametrize("n,d,m,row0", [(700, 48, None, 0), (5000, 64, None, 0),
+                                        (3000, 130, 1000, 1500), (513, 3, None, 0),
+                                        (1000, 100, None, 0), (1900, 256, None, 0),
+                                        (4500, 128, None, 0), (3000, 130, 1024, 1024),
+                                        (2300, 96, 1280, 0), (2600, 64, 512, 2048)])
+def test_sqdist_split_as_accurate_as_f32(split, n, d, m, row0):
+    """Distances through the split Gram against fp64, next to the f32 Gram on
+    the same particles: symmetric, bracketed (n = 5000: n^2 >= 2^24) and
+    row-block launches; the median select stays bit-exact on the kernel's
+    own D."""
+    rs = np.random.RandomState(n + d)
+    X = (rs.randn(n, d) * 1.5 + 3.0).astype(np.float32)
+    Xc = X.astype(np.float64) - X.astype(np.float64).mean(0)
+    mm = n if m is None else m
+    ref = ((Xc[row0:row0 + mm, None, :] - Xc[None, :, :]) ** 2).sum(-1) if n * mm <= 4e6 else None
+    nrm = (Xc ** 2).sum(1)
+    err, med, Dall = {}, {}, {}
+    for gemm in ("f32", split):
+        eng = dsvgd().PhiEngine(n, d, m=m, row0=row0, device=DEV, gram_gemm=gemm)
+        assert eng.gram_gemm == gemm
+        eng.pack(gpu(X))
+        eng.distances(median=True)
+        eng.median_bandwidth()
+        Dm = eng.dense_D().cpu().numpy().astype(np.float64)
+        k = (n * mm - 1) // 2
+        med[gemm] = eng.state.read()[0]
+        # symmetric layout exactly when the split engines take the whole matrix at ldy % 256 == 0
+        assert eng.sym == (gemm != "f32" and m is None and d > 2 and eng.ldy % 256 == 0)
+        if eng.sym:  # weighted counting over the stored tiles == counting the dense matrix
+            for v in (med[gemm], 0.5 * med[gemm]):
+                assert eng.count_D(lambda t: t < v) == int((eng.dense_D(padded=True) < v).sum())
+        if m is None:
+            assert np.float32(med[gemm]).view(np.uint32) == \
+                np.float32(np.partition(Dm.ravel(), k)[k]).view(np.uint32)
+            assert np.all(np.diag(Dm) == 0.0)
+        if ref is not None:
+            scale = nrm[row0:row0 + mm, None] + nrm[None, :] + 1e-30
+            err[gemm] = float(np.max(np.abs(Dm - ref) / scale))
+        Dall[gemm] = Dm
+    if ref is not None:
+        record_parity(err[split])
+        assert err[split] <= 2.0 * err["f32"] + 1e-7 and err[split] < 2e-6, err
+    # every entry of the block, incl. the mirrored / square-split ones of a
+    # 256-aligned row block, against the f32 Gram's
+    scale = nrm[row0:row0 + mm, None] + nrm[None, :] + 1e-30
+    e = float(np.max(np.abs(Dall[split] - Dall["f32"]) / scale))
+    record_parity(e)
+    assert e < 4e-6

@@ -151,3 +151,62 @@ def test_replicated_score_gather_equals_redundant_scoring(S, sequential):
         b.step(0.05)
     for r in range(S):
         assert np.abs(a.X[r] - b.X[r]).max() < 1e-12
+
+
+def _lag_setup(S, n=24, p=3, seed=0, same=False):
+    rs = np.random.RandomState(seed)
+    x, t = rs.randn(30, p), np.sign(rs.randn(30))
+    base = rs.randn(n, p + 1) * 0.5
+    init = [base.copy() if same else rs.randn(n, p + 1) * 0.5 for _ in range(S)]
+    fns = [(lambda X, r=r: O.score_logreg(X, x[10 * r % 30:], t[10 * r % 30:])) for r in range(S)]
+    return init, fns
+
+
+@pytest.mark.parametrize("lagged", ["local", "updateall"])
+def test_lagged_modes_reduce_to_all_particles_s1(lagged):
+    """S = 1: nothing travels, the held block is the whole set -> the
+    all_particles / partitions step (both orders, fixed and median h)."""
+    init, fns = _lag_setup(1)
+    for seq in (True, False):
+        for h in (1.0, "median"):
+            a = O.DistOracle(init, fns, 30, 30, False, False, h=h, sequential=seq, lagged=lagged)
+            b = O.DistOracle(init, fns, 30, 30, True, False, h=h, sequential=seq)
+            for _ in range(2):
+                a.step(0.05)
+                b.step(0.05)
+            assert np.abs(a.X[0] - b.X[0]).max() < 1e-12
+
+
+def test_laggedlocal_first_step_is_all_particles_jacobi_step():
+    """With identical local copies nothing is stale at step 1: each rank's
+    received block moves exactly as in all_particles Jacobi (same data)."""
+    S = 4
+    init, _ = _lag_setup(S, same=True)
+    rs = np.random.RandomState(1)
+    x, t = rs.randn(30, 3), np.sign(rs.randn(30))
+    fns = [lambda X: O.score_logreg(X, x, t)] * S
+    a = O.DistOracle(init, fns, 30, 30, False, False, sequential=False, lagged="local")
+    b = O.DistOracle(init, fns, 30, 30, True, False, sequential=False)
+    a.step(0.05)
+    b.step(0.05)
+    for r in range(S):
+        assert a.held[r] == (r - 1) % S
+        assert np.abs(a.own(r) - b.own(a.held[r])).max() < 1e-12
+
+
+def test_laggedlocal_block_travel():
+    """Blocks go round the ring and land in their home rows: after S steps
+    every rank holds its own block again, and a rank's copy of block b is
+    the value b had when it last passed through."""
+    S = 3
+    init, fns = _lag_setup(S)
+    a = O.DistOracle(init, fns, 30, 30, False, False, sequential=False, lagged="local")
+    for step in range(1, 2 * S + 1):
+        a.step(0.05)
+        for r in range(S):
+            assert a.held[r] == (r - step) % S
+    # updateall moves every row of every copy
+    u = O.DistOracle(init, fns, 30, 30, False, False, sequential=False, lagged="updateall")
+    u.step(0.05)
+    for r in range(S):
+        assert np.all(np.abs(u.X[r] - init[r]).max(1) > 0)
