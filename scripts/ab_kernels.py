@@ -1,11 +1,12 @@
-"""Interleaved in-process A/B timing of kernel variants at the headline shape
-(cdna_hip_programming.md rule 24: rounds interleaved in ONE process).
+"""Interleaved in-process A/B timing of the contraction engines at the
+headline shape (cdna_hip_programming.md rule 24: rounds interleaved in ONE
+process): phi_mm, the distance Gram (+ bracket accounting) and the logreg
+scores on FmtH2 / FmtX3 / f32 (PhiEngine(gemm=...), LogisticRegression(gemm=...)).
 
-    python scripts/ab_kernels.py [--n 65536 --d 256 --rounds 5]
+    python scripts/ab_kernels.py [--n 65536 --d 256 --rounds 5 --engines h2,x3]
 
-Variants are switched through environment variables the launchers read on
-every call (DSVGD_NN_SHAPE=w2 forces the 16-deep NN K-step of the f32 engine;
-ENGINE_X3 picks the phi_mm engine).
+Epilogue pricing needs an A/B build of the library (-DDSVGD_SQ_EPI=1|2|3,
+see csrc/sqdist.hip), not a switch of the shipped one.
 """
 import argparse
 import json
@@ -35,67 +36,38 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--d", type=int, default=256)
+    ap.add_argument("--N", type=int, default=16384, help="logreg data rows")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--engines", default="h2,x3")
     args = ap.parse_args()
     import dsvgd
     n, d = args.n, args.d
     g = torch.Generator(device="cpu").manual_seed(0)
-    X = torch.randn(n, d, generator=g).cuda()
+    X = (0.1 * torch.randn(n, d, generator=g)).cuda()
     S = torch.randn(n, d, generator=g).cuda()
-    eng = dsvgd.PhiEngine(n, d, device="cuda:0")
-    eng.pack(X, S)
-    eng.distances(median=True)
-    eng.median_bandwidth()
-    # ENGINE_X3: "1" = the bf16-split phi_mm (default), "0" = the f32 MFMA engine
-    variants = json.loads(os.environ.get("AB_VARIANTS", "null")) or {
-        "phi=x3": {"ENGINE_X3": "1", "RECOMPUTE_D": "1"},
-        "phi=f32": {"ENGINE_X3": "0", "RECOMPUTE_D": "1"}}  # f32: the full D layout
-    res = {k: [] for k in variants}
-    ref = None
-    keys = {k for env in variants.values() for k in env}
+    xd = torch.randn(args.N, d - 1, generator=g) / (d ** 0.5)
+    tl = torch.where(torch.randn(args.N, generator=g) > 0, 1.0, -1.0)
+    engines = args.engines.split(",")
+    res = {e: {"phi_mm": [], "distances": [], "scores": []} for e in engines}
+    phis = {}
     for _ in range(args.rounds):
-        for name, env in variants.items():
-            for k in keys:               # a variant's knobs must not leak into the next
-                os.environ.pop(k, None)
-            os.environ.update(env)
-            eng.x3 = env.get("ENGINE_X3", "1") == "1" and hasattr(eng, "Yx")
-            if env.get("RECOMPUTE_D") == "1":  # the variant changes D's layout
-                eng.distances(median=True)
-                eng.median_bandwidth()
-            res[name].append(timed(lambda: eng.direction(write_phi=True)))
-            if ref is None:
-                ref = eng.phi.clone()
-            elif not env.get("NOCHECK"):
-                err = float((eng.phi - ref).abs().max() / ref.abs().max())
-                assert err < 1e-5, (name, err)
-    eng.x3 = hasattr(eng, "Yx")  # the default engines (and D layout) for the timings below
-    for k in keys:
-        os.environ.pop(k, None)
-    flops = 4.0 * n * n * d
-    out = {k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v)),
-               "tflops": flops / (np.median(v) * 1e-3) / 1e12} for k, v in res.items()}
-    out["sqdist_ms"] = timed(lambda: eng.distances(median=False))
-    if getattr(eng, "x3_gram", False):
-        eng.x3_gram = False
-        out["sqdist_f32_ms"] = timed(lambda: eng.distances(median=False))
-        out["sqdist_bracket_f32_ms"] = timed(lambda: eng.distances(median=True))
-        eng.x3_gram = True
-    for k, v in json.loads(os.environ.get("AB_SQ_VARIANTS", "{}")).items():
-        os.environ.update(v)
-        out["sqdist_ms[%s]" % k] = timed(lambda: eng.distances(median=False))
-        out["sqdist_bracket_ms[%s]" % k] = timed(lambda: eng.distances(median=True))
-        out["sqdist_select_ms[%s]" % k] = timed(
-            lambda: (eng.distances(median=True), eng.median_bandwidth()))
-        for key in v:
-            os.environ.pop(key, None)
-    # logistic-regression scores at the bench shape (N = 16384 rows, p = d - 1)
-    xd = torch.randn(16384, d - 1, generator=g) / (d ** 0.5)
-    tl = torch.where(torch.randn(16384, generator=g) > 0, 1.0, -1.0)
-    tgt = dsvgd.targets.LogisticRegression(xd, tl)
-    Sx = torch.empty_like(X)
-    out["logreg_score_ms"] = timed(lambda: tgt.score(X, Sx))
-    out["sqdist_bracket_ms"] = timed(lambda: eng.distances(median=True))
-    out["sqdist_select_ms"] = timed(lambda: (eng.distances(median=True), eng.median_bandwidth()))
+        for e in engines:
+            eng = dsvgd.PhiEngine(n, d, device="cuda:0", gemm=e)
+            tgt = dsvgd.targets.LogisticRegression(xd, tl, gemm=e)
+            Sx = torch.empty_like(X)
+            res[e]["scores"].append(timed(lambda: tgt.score(X, Sx)))
+            eng.pack(X, S)
+            res[e]["distances"].append(timed(lambda: eng.distances(median=True)))
+            eng.median_bandwidth()
+            res[e]["phi_mm"].append(timed(lambda: eng.direction(write_phi=True)))
+            phis[e] = eng.phi.clone()
+            del eng, tgt
+            torch.cuda.empty_cache()
+    ref = phis[engines[0]]
+    out = {}
+    for e in engines:
+        out[e] = {k: float(np.median(v)) for k, v in res[e].items()}
+        out[e]["phi_vs_%s" % engines[0]] = float((phis[e] - ref).abs().max() / ref.abs().max())
     print(json.dumps(out, indent=1))
 
 

@@ -19,10 +19,6 @@ from oracle import svgd_oracle as O  # noqa: E402
 
 def phi_err(X, S, mfma):
     n, d = X.shape
-    if mfma:
-        os.environ["DSVGD_SQ_DIRECT_MAX_D"] = "0"
-    else:
-        os.environ.pop("DSVGD_SQ_DIRECT_MAX_D", None)
     eng = dsvgd.PhiEngine(n, d, device="cuda:0")
     if mfma:
         eng.DIRECT_MAX_D = 0
@@ -33,7 +29,6 @@ def phi_err(X, S, mfma):
     ref = O.phi(X, S, h, rows=rows)
     got = eng.phi[torch.as_tensor(rows, device="cuda:0")].cpu().numpy()
     e = float(np.abs(got - ref).max() / np.abs(ref).max())
-    os.environ.pop("DSVGD_SQ_DIRECT_MAX_D", None)
     return e, h
 
 

@@ -81,8 +81,9 @@ def test_ysplit_reconstructs_fp32(rows, ldy):
 def test_h2_images_reconstruct_fp32(rows, ldy):
     """dsvgd_h2_colscale + dsvgd_h2_ysplit / dsvgd_h2_rowsplit: power-of-two
     scales putting each column's (tensor's) largest magnitude in [2^14, 2^15),
-    parts that sum back to s v within 2^-22 relative for entries within 2^-18
-    of the scale's reference magnitude, zero / inf / NaN columns handled."""
+    parts that sum back to s v within 2^-22 relative for entries within 2^-16
+    of the scale's reference magnitude (2^-22 relative + 2^-38 of it for all),
+    zero / inf / NaN columns handled."""
     from dsvgd import _native as N
     lib = N.load()
     s = N.stream(torch.device(DEV))
@@ -108,7 +109,9 @@ def test_h2_images_reconstruct_fp32(rows, ldy):
     parts = decode_h2(img, rows, ldy)
     rec = parts.sum(0) / s_c[None, :]
     Y64 = Y.astype(np.float64)
-    big = np.abs(Y64) >= mx[None, :] * 2.0 ** -18
+    # the second part is exact to 2^-11 of itself while normal (|s v| >= 2^-3
+    # keeps 2^-22 |s v| above fp16's subnormal half-spacing 2^-25)
+    big = (np.abs(Y64) >= mx[None, :] * 2.0 ** -16) & (Y64 != 0)
     err = np.abs(rec - Y64)[big] / np.abs(Y64)[big]
     record_parity(float(err.max()))
     assert err.max() <= 2.0 ** -22
@@ -122,8 +125,9 @@ def test_h2_images_reconstruct_fp32(rows, ldy):
     rp = decode_h2(img2, ldy, rows + 16)                       # (2, k, row)
     rec2 = rp.sum(0).T / scale[2 * ldy]
     assert np.all(rec2[rows:] == 0.0)
-    tb = np.abs(Y64) >= np.abs(Y64).max() * 2.0 ** -18
+    tb = (np.abs(Y64) >= np.abs(Y64).max() * 2.0 ** -16) & (Y64 != 0)
     assert np.all(np.abs(rec2[:rows] - Y64)[tb] <= 2.0 ** -22 * np.abs(Y64)[tb])
+    assert np.all(np.abs(rec2[:rows] - Y64) <= 2.0 ** -22 * np.abs(Y64) + 2.0 ** -38 * np.abs(Y64).max())
     # a non-finite column forces the tensor scale to 1 (inf / NaN propagate)
     Y[5, 7] = np.inf
     N.call("dsvgd_h2_colscale", N.ptr(gpu(Y)), ldy, rows, ldy, N.ptr(ws), N.ptr(sc), s)
