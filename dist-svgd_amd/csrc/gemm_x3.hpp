@@ -159,9 +159,14 @@ __device__ __forceinline__ int x3_off(int x, int h) { return x * 32 + ((h ^ ((x 
 // blocks (phi_mm); RW = 4 (DMA, EXP = false only): 256-row blocks staging two
 // D panels per K-step -- twice the MFMAs per B image (logreg G . Xd, where the
 // B side is only 256 columns wide).
-template <int TN, bool DMA = true, bool EXP = true, bool M16 = false, int RW = 2, class F = FmtX3>
+// NB (DMA path): ring stages.  2: iteration k DMAs tile k+1's B image (one
+// iteration to land); 3: tile k+2's B and D (two iterations; the closing
+// barrier then waits for no DMA at all).
+template <int TN, bool DMA = true, bool EXP = true, bool M16 = false, int RW = 2, class F = FmtX3,
+          int NB = 2>
 struct NNX3Tile {
   static constexpr int P = F::P;
+  static_assert(NB == 2 || (NB == 3 && DMA), "3-stage ring: DMA path");
   using V8 = typename F::V8;
   static_assert(!M16 || P == 3, "the 16x16x32 concatenated-k form is the 3-part format's");
   // (DMA needs the same DMA count in every wave: whole 512-chunk rounds)
@@ -176,7 +181,7 @@ struct NNX3Tile {
   static constexpr int SA = P * BM * 32;  // bytes of one stage's A image
   static constexpr int SB = P * BC * 32;
   static constexpr int kStage = SA + SB;
-  static constexpr int kSmemBytes = 2 * kStage + (DMA ? 2 * AR * kPanelElems * 4 : 0);
+  static constexpr int kSmemBytes = NB * kStage + (DMA ? NB * AR * kPanelElems * 4 : 0);
   static constexpr int kBChunks = SB / 16;
   static constexpr int LB = (kBChunks + kThreads - 1) / kThreads;
   static constexpr int kHalf = TN > 1 ? TN / 2 : 1;  // column tiles before the mid-step write
@@ -265,7 +270,7 @@ struct NNX3Tile {
   // LDS-DMA in the loop, so every vmcnt wait is counted by hand (a plain
   // load beside it makes hipcc wait vmcnt(0): cdna_hip_programming.md "three
   // .s-level traps" (b)).
-  static constexpr int kRaw = 2 * kStage;  // D ring: 2 slots x AR x 8 KiB raw panels
+  static constexpr int kRaw = NB * kStage;  // D ring: NB slots x AR x 8 KiB raw panels
   static constexpr int kSlot = AR * kPanelElems * 4;
 #ifndef DSVGD_D_AUX
 #define DSVGD_D_AUX 2
@@ -443,6 +448,30 @@ struct NNX3Tile {
       const __amdgpu_buffer_rsrc_t rB =
           __builtin_amdgcn_make_buffer_rsrc((void*)Yx, (short)0, 0x7fffffff, 0x00020000);
       char* raw = smem + kRaw;
+      if constexpr (NB == 3) {
+        dma_b(smem, rB, ldy, k0);
+        dma_d(raw, rA, k0);
+        if (k0 + BJ < k1) {
+          dma_b(smem + kStage, rB, ldy, k0 + BJ);
+          dma_d(raw + kSlot, rA, k0 + BJ);
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB + AR) : "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+#pragma unroll
+        for (int a = 0; a < AR; ++a) {
+          ra = raw_read(raw, k0, a);
+          store_a(smem, scale, row_g0 - k0, a);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        for (int64_t j0 = k0; j0 < k1; j0 += 3 * BJ) {
+          step_dma3<0>(rA, rB, ldy, j0, k1, scale, smem, row_g0, wr, wc);
+          if (j0 + BJ < k1) step_dma3<1>(rA, rB, ldy, j0 + BJ, k1, scale, smem, row_g0, wr, wc);
+          if (j0 + 2 * BJ < k1)
+            step_dma3<2>(rA, rB, ldy, j0 + 2 * BJ, k1, scale, smem, row_g0, wr, wc);
+        }
+        return;
+      }
       dma_b(smem, rB, ldy, k0);
       dma_d(raw, rA, k0);
       if (k0 + BJ < k1) dma_d(raw + kSlot, rA, k0 + BJ);
@@ -517,6 +546,40 @@ struct NNX3Tile {
       asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(AR) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+
+  // 3-stage ring, iteration k (tile j0, stage CUR = k % 3): DMA tile k+2's B
+  // and D into stage / raw slot (CUR + 2) % 3 (consumed at iteration k-1 and
+  // k-2); halfway, wait for tile k+1's D (issued last iteration, after its B:
+  // both landed) and stage its A into stage (CUR + 1) % 3.  The closing
+  // barrier waits for LDS writes only.
+  template <int CUR>
+  __device__ __forceinline__ void step_dma3(__amdgpu_buffer_rsrc_t rA, __amdgpu_buffer_rsrc_t rB,
+                                            int64_t ldy, int64_t j0, int64_t k1, float scale,
+                                            char* smem, int64_t row_g0, int wr, int wc) {
+    constexpr int NXT = (CUR + 1) % 3, NN = (CUR + 2) % 3;
+    const char* cur = smem + CUR * kStage;
+    char* raw = smem + kRaw;
+    const bool more = j0 + BJ < k1, more2 = j0 + 2 * BJ < k1;
+    if (more2) {
+      dma_b(smem + NN * kStage, rB, ldy, j0 + 2 * BJ);
+      dma_d(raw + NN * kSlot, rA, j0 + 2 * BJ);
+    }
+    read_a(cur, wr);
+    compute<0, kHalf>(cur, wc);
+    if (more) {
+      if (more2)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB + AR) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int a = 0; a < AR; ++a) {
+        ra = raw_read(raw + NXT * kSlot, j0 + BJ, a);
+        store_a(smem + NXT * kStage, scale, row_g0 - (j0 + BJ), a);
+      }
+    }
+    compute<kHalf, TN>(cur, wc);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
 
   // full row sum of row threadIdx.x >> 2 (4 consecutive lanes stage a row)

@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
 // F = FmtH2: C and rowsum come out of the MFMAs scaled by 2^15 (the A
 // staging scale) and C's column c by the B image's column scale: the stores
 // multiply by colinv[c] * 2^-15 (exact powers of two).
-template <int TN, bool DMA, bool EXP, bool M16, int RW = 2, class F = FmtX3>
+template <int TN, bool DMA, bool EXP, bool M16, int RW = 2, class F = FmtX3, int NB = 2>
 __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A, int64_t a_npad,
                                                     const typename F::E* __restrict__ Yx,
                                                     int64_t ldy, int64_t K, int64_t kchunk,
@@ -84,7 +84,7 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
                                                     float* __restrict__ rowsum, int64_t m,
                                                     int64_t row0, int sym,
                                                     const float* __restrict__ colinv) {
-  using Tile = NNX3Tile<TN, DMA, EXP, M16, RW, F>;
+  using Tile = NNX3Tile<TN, DMA, EXP, M16, RW, F, NB>;
   __shared__ __attribute__((aligned(16))) char smem[Tile::kSmemBytes];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
@@ -211,9 +211,10 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
     else
       hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F>), grid, dim3(512), 0, s, D, K,
                          Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv);
-  } else {
-    hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F>), grid, dim3(512), 0, s, D, K,
-                       Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv);
+  } else {  // FmtH2: the smaller stages fit a 3-stage ring
+    hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2>), grid,
+                       dim3(512), 0, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym,
+                       colinv);
   }
   return check_launch("nn_x3_kernel");
 }
@@ -233,8 +234,9 @@ int nn_split_gemm(bool exp_, const float* A, int64_t K, const typename F::E* Yx,
     // multiple of 256 (the caller's panel layout; logreg pads n to 256)
     const int64_t kchunk = roundup((K + splits - 1) / splits, kX3Step);
     const dim3 grid(ldy / 256, roundup(m, 256) / 256, splits);
-    hipLaunchKernelGGL((nn_x3_kernel<4, true, false, F::P == 3, 4, F>), grid, dim3(512), 0, s, A, K,
-                       Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, 0, colinv);
+    hipLaunchKernelGGL((nn_x3_kernel<4, true, false, F::P == 3, 4, F, F::P == 3 ? 2 : 3>), grid,
+                       dim3(512), 0, s, A, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, 0,
+                       colinv);
     return check_launch("nn_x3_kernel(256-row)");
   }
 #define DSVGD_X3_TN(TN)                                                                        \
