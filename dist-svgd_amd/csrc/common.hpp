@@ -24,7 +24,8 @@ constexpr float kLog2e = 1.4426950408889634f;
 void set_error(const char* fmt, ...);
 int fail_arg(const char* what);
 int check_launch(const char* kernel);
-int persistent_blocks(const void* fn, int* blocks);  // resident blocks/CU x CUs, multiple of 8
+// resident blocks/CU x CUs of a kernel launched with `threads` threads, a multiple of 8
+int persistent_blocks(const void* fn, int* blocks, int threads = 256);
 
 inline int64_t roundup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 __host__ __device__ inline int64_t roundup128(int64_t x) { return (x + 127) & ~(int64_t)127; }

@@ -54,6 +54,14 @@ __device__ __forceinline__ Split3 split3(float v) {
 constexpr int kX3Parts = 3;
 constexpr int kX3Step = 16;  // K-step (columns of D / rows of Y)
 
+// mask-bit set ? a : b, per lane, on a compile-time lane mask (v_cndmask_b32
+// with the mask in an SGPR pair)
+__device__ __forceinline__ float lane_select(uint64_t mask, float a, float b) {
+  float d;
+  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(d) : "v"(b), "v"(a), "s"(mask));
+  return d;
+}
+
 // ---- split formats: how an fp32 operand becomes MFMA inputs -------------
 // FmtX3: three bf16 parts, six products a_i b_j (i + j <= 2).
 // FmtH2: two fp16 parts of the operand scaled by a power of two,
@@ -333,12 +341,15 @@ struct NNX3Tile {
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = r[((e + c4) & 3) * 16];
-      // v[e] = column (e + c4) & 3  ->  out[q] = v[(q - c4) & 3]
+      // v[e] = column (e + c4) & 3  ->  out[q] = v[(q - c4) & 3]: two
+      // conditional rotations on the lane masks of c4 = lane & 3 (constant
+      // SGPR masks; the compiler's own selects re-derived the mask per value)
+      constexpr uint64_t kOdd = 0xAAAAAAAAAAAAAAAAull, kHi2 = 0xCCCCCCCCCCCCCCCCull;
       float w[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) w[q] = (c4 & 1) ? v[(q + 3) & 3] : v[q];
+      for (int q = 0; q < 4; ++q) w[q] = lane_select(kOdd, v[(q + 3) & 3], v[q]);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = (c4 & 2) ? w[(q + 2) & 3] : w[q];
+      for (int q = 0; q < 4; ++q) v[q] = lane_select(kHi2, w[(q + 2) & 3], w[q]);
       return f32x4{v[0], v[1], v[2], v[3]};
     }
     return *reinterpret_cast<const f32x4*>(raw + a * kPanelElems * 4 + t * 16);

@@ -476,7 +476,7 @@ static int score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const
     // the Z kernel's scale operand: [1/t_w, 1/t_x] side by side
     int blocks = 0;
     if ((rc = persistent_blocks(reinterpret_cast<const void*>(&logreg_z_x3p_kernel<FmtH2>),
-                                &blocks)))
+                                &blocks, 512)))
       return rc;
     const int Tm2 = (int)(w.n_pad / 256), Tn2 = (int)(w.N_pad / 256);
     hipLaunchKernelGGL(zscale_pair_kernel, dim3(1), dim3(1), 0, s, sw + 2 * p + 1,
@@ -506,7 +506,7 @@ static int score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const
     {
       int blocks = 0;
       if ((rc = persistent_blocks(reinterpret_cast<const void*>(&logreg_z_x3p_kernel<FmtX3>),
-                                  &blocks)))
+                                  &blocks, 512)))
         return rc;
       const int Tm2 = (int)(w.n_pad / 256), Tn2 = (int)(w.N_pad / 256);
       hipLaunchKernelGGL(logreg_z_x3p_kernel<FmtX3>, dim3((unsigned)blocks), dim3(512), 0, s,

@@ -31,9 +31,9 @@ int check_launch(const char* kernel) {
 }
 
 // Grid of a persistent kernel: resident blocks per CU (occupancy of `fn` at
-// 256 threads, no dynamic LDS) x CUs, a multiple of the 8 XCDs.  Cached per
-// (kernel, device).
-int persistent_blocks(const void* fn, int* blocks) {
+// `threads` threads, no dynamic LDS) x CUs, a multiple of the 8 XCDs.
+// Cached per (kernel, device).
+int persistent_blocks(const void* fn, int* blocks, int threads) {
   struct Entry { const void* fn; int dev; int blocks; };
   static thread_local Entry cache[16];
   static thread_local int ncache = 0;
@@ -48,7 +48,7 @@ int persistent_blocks(const void* fn, int* blocks) {
       return DSVGD_OK;
     }
   int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
     set_error("occupancy query failed");
     return DSVGD_E_LAUNCH;

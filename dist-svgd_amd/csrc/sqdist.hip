@@ -25,6 +25,12 @@
 namespace dsvgd {
 
 constexpr int kSqEpi = DSVGD_SQ_EPI;
+// DSVGD_GRAM_H2_FORM (compile time, A/B builds): 0 = 256-tile blocks on a
+// 3-stage ring (shipped), 1 = half-tile blocks, two per CU
+#ifndef DSVGD_GRAM_H2_FORM
+#define DSVGD_GRAM_H2_FORM 0
+#endif
+constexpr int kGramH2Form = DSVGD_GRAM_H2_FORM;
 
 using GramTile = NTTile<2, 2, 2, 2>;  // 128 x 128 block, 4 waves of 64 x 64
 
@@ -308,23 +314,31 @@ __global__ __launch_bounds__(256, 2) void sqdist_persistent_kernel(
 // swizzled one (FmtH2).
 // F = FmtH2: Yg is the fp16 image of t Xc (t = tsc[0]), the Gram comes out
 // scaled by t^2: the epilogue's 2 x.y is c2 acc with c2 = 2 / t^2.
-template <bool SYM, int smode, bool M16 = true, class F = FmtX3>
-__global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
+// WN = 1: a block of 4 waves (one per SIMD) takes HALF a 256-tile (256 rows x
+// 128 columns, unit = 2 L + h) and two such blocks share a CU: they drift
+// apart, so one block's epilogue (D stores, select accounting) runs beside
+// the other's MFMAs instead of every SIMD idling its MFMA pipe through it.
+// NS: LDS ring stages (2: a K-step's DMA has one K-step to land; 3: two).
+template <bool SYM, int smode, bool M16 = true, class F = FmtX3, int WN = 2, int NS = 2>
+__global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
     const typename F::E* __restrict__ Yg, int64_t img_rows, const float* __restrict__ norms,
     int64_t row0, int64_t m, int64_t n, int64_t n_pad, int nk, float* __restrict__ D,
-    dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int epi, int64_t total,
+    dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int epi, int64_t total_tiles,
     int layout, int Tm2, int Tc2, int bj_off, int r0t, int64_t slot_base, int64_t ns_total,
     const float* __restrict__ tsc) {
-  using GramX3WTile = NTX3Tile<2, 4, 4, 2, 2, M16, F>;
+  using GramX3WTile = NTX3Tile<2, 4, 4, WN, NS, M16, F>;
+  constexpr int kT = GramX3WTile::kThreads, kUnits = 2 / WN;  // units per 256-tile
+  constexpr int kBN = GramX3WTile::BN;                         // 256 or 128 columns
   const float c2 = F::P == 3 ? 2.f : 2.f * tsc[1] * tsc[1];
   __shared__ __attribute__((aligned(16))) char smem[GramX3WTile::kSmemBytes];
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
-  __shared__ float snorm[512];  // the tile's 256 row norms, then its 256 column norms
+  __shared__ float snorm[256 + kBN];  // the unit's 256 row norms, then its column norms
 
   // this launch: Tm2 x Tc2 256-tiles, global column tiles from bj_off
   // (SYM: the triangle of a Tm2 x Tm2 square; r0t = its row0 / 128)
   const int Tm = (int)(roundup128(m) / 128), Tn = (int)(n_pad / 128);  // 128-tiles
-  const int t = threadIdx.x, w = t >> 6, wr = w >> 1, wc = w & 1;
+  const int t = threadIdx.x, w = t >> 6, wr = w / WN, wc = w % WN;
+  const int64_t total = total_tiles * kUnits;
   const int64_t x = blockIdx.x % kXcds, u = blockIdx.x / kXcds, U = gridDim.x / kXcds;
   const int64_t q = total / kXcds, rr = total % kXcds;
   const int64_t lo = x * q + min(x, rr);
@@ -332,16 +346,22 @@ __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
   SlotLayout sl(cand, ns_total, smode == kSelBracket ? st->cand_cap : 0);
   if (smode == kSelBracket) sl.publish(st, blockIdx.x);
   if (smode == kSelHist)
-    for (int b = t; b < DSVGD_RADIX_BINS; b += 512) shist[b] = 0u;
+    for (int b = t; b < DSVGD_RADIX_BINS; b += kT) shist[b] = 0u;
 
+  // unit L -> 256-tile (BI, BJ) and (WN = 1) its column half L & 1; BJ is
+  // returned in units of kBN columns (the unit's first column / kBN)
   auto next_valid = [&](int64_t L, int& BI, int& BJ) -> int64_t {
     for (; L < hi; L += U) {
-      if (tile_at(L, Tm2, Tc2, SYM, BI, BJ)) {
-        BI = __builtin_amdgcn_readfirstlane(BI);
-        BJ = __builtin_amdgcn_readfirstlane(BJ + bj_off);
-        return L;
+      if (tile_at(L / kUnits, Tm2, Tc2, SYM, BI, BJ)) {
+        const int bjc = (BJ + bj_off) * kUnits + (int)(L % kUnits);
+        // a half past the padded matrix, or (SYM) wholly below the diagonal
+        if (kUnits == 1 || (bjc < Tn && !(SYM && 2 * BI + r0t > bjc))) {
+          BI = __builtin_amdgcn_readfirstlane(BI);
+          BJ = __builtin_amdgcn_readfirstlane(bjc);
+          return L;
+        }
       }
-      if (smode == kSelBracket) slot_clear(sl, slot_base + L * 8 + w);
+      if (smode == kSelBracket) slot_clear(sl, slot_base + L * (8 / kUnits) + w);
     }
     return L;
   };
@@ -350,60 +370,110 @@ __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
     const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(Yg + (row0 + (int64_t)BI * 256) * 16), (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(Yg + (int64_t)BJ * 256 * 16), (short)0, 0x7fffffff, 0x00020000);
+        (void*)(Yg + (int64_t)BJ * kBN * 16), (short)0, 0x7fffffff, 0x00020000);
     tile.dma(stg, rA, img_rows, rB, img_rows, ks);
+  };
+
+  // tile (L, BI, BJ) done: norms, per-sub-tile epilogue (re-zeroes the accumulators)
+  auto epilogue = [&](int64_t L, int BI, int BJ) {
+    for (int e = t; e < 256 + kBN; e += kT) {
+      const int64_t gi = e < 256 ? row0 + (int64_t)BI * 256 + e : (int64_t)BJ * kBN + e - 256;
+      snorm[e] = gi < n_pad ? norms[gi] : 0.f;
+    }
+    __syncthreads();
+    // this wave's 128-sub-tile
+    const int bi = 2 * BI + (wr >> 1), bj = BJ * (kBN / 128) + wc;
+    const int64_t slot = slot_base + L * (8 / kUnits) + w;
+    WindowHist wh;
+    SlotWriter sw;
+    if (smode == kSelBracket) sw.begin(st, sl, slot);
+    if (epi == 3 || bi >= Tm || bj >= Tn || (SYM && bi + r0t > bj)) {
+      tile.zero();
+      if (smode == kSelBracket) sw.finish(sl, slot, false);
+    } else {
+      if constexpr (M16)
+        sq_epilogue16<SYM, smode>(tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128,
+                                  snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl,
+                                  slot, epi, layout == 0, r0t);
+      else
+        sq_epilogue<SYM, smode, true, GramX3WTile, 4>(
+            tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128,
+            snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl, slot, epi, layout == 0,
+            r0t, c2);
+    }
+    if (smode == kSelHist) wh.flush(shist);
   };
 
   int BI = 0, BJ = 0;
   int64_t L = next_valid((int64_t)__builtin_amdgcn_readfirstlane((int)(lo + u)), BI, BJ);
   tile.zero();
-  if (L < hi) issue(smem, BI, BJ, 0);
-  GramX3WTile::template ring_barrier<0>();
-  int ks = 0, stage = 0;
-  int BIn = BI, BJn = BJ;
-  int64_t Ln = L;
-  while (L < hi) {
-    int ksn = ks + 1;
-    if (ksn == nk) {
-      Ln = next_valid(L + U, BIn, BJn);
-      ksn = 0;
+  if constexpr (NS == 3) {
+    // positions of the next two K-steps (the ring runs two ahead, across tiles)
+    int ks = 0, stage = 0;
+    int64_t L1 = L, L2;
+    int BI1 = BI, BJ1 = BJ, ks1 = 1, BI2, BJ2, ks2;
+    if (ks1 == nk) {
+      L1 = next_valid(L + U, BI1, BJ1);
+      ks1 = 0;
     }
-    const bool more = Ln < hi;
-    if (more) issue(smem + (stage ^ 1) * GramX3WTile::kStage, BIn, BJn, ksn);
-    tile.compute(smem + stage * GramX3WTile::kStage, wr, wc, (int)(row0 & 15));
+    auto advance = [&](int64_t La, int BIa, int BJa, int ka, int64_t& Lb, int& BIb, int& BJb,
+                       int& kb) {
+      Lb = La;
+      BIb = BIa;
+      BJb = BJa;
+      kb = ka + 1;
+      if (kb == nk) {
+        Lb = La < hi ? next_valid(La + U, BIb, BJb) : La;
+        kb = 0;
+      }
+    };
+    advance(L1, BI1, BJ1, ks1, L2, BI2, BJ2, ks2);
+    if (L < hi) issue(smem, BI, BJ, 0);
+    if (L1 < hi) {
+      issue(smem + GramX3WTile::kStage, BI1, BJ1, ks1);
+      GramX3WTile::template ring_barrier<GramX3WTile::kDmas>();
+    } else {
+      GramX3WTile::template ring_barrier<0>();
+    }
+    while (L < hi) {
+      const int s2 = stage >= 1 ? stage - 1 : 2;  // (stage + 2) % 3
+      if (L2 < hi) issue(smem + s2 * GramX3WTile::kStage, BI2, BJ2, ks2);
+      tile.compute(smem + stage * GramX3WTile::kStage, wr, wc, (int)(row0 & 15));
+      if (L2 < hi)
+        GramX3WTile::template ring_barrier<GramX3WTile::kDmas>();
+      else
+        GramX3WTile::template ring_barrier<0>();
+      if (ks + 1 == nk) epilogue(L, BI, BJ);
+      L = L1; BI = BI1; BJ = BJ1; ks = ks1;
+      L1 = L2; BI1 = BI2; BJ1 = BJ2; ks1 = ks2;
+      advance(L1, BI1, BJ1, ks1, L2, BI2, BJ2, ks2);
+      stage = stage == 2 ? 0 : stage + 1;
+    }
+  } else {
+    if (L < hi) issue(smem, BI, BJ, 0);
     GramX3WTile::template ring_barrier<0>();
-    if (ks + 1 == nk) {  // tile done: norms, per-sub-tile epilogue (re-zeroes the accumulators)
-      {
-        const int64_t gi = t < 256 ? row0 + (int64_t)BI * 256 + t : (int64_t)BJ * 256 + t - 256;
-        snorm[t] = gi < n_pad ? norms[gi] : 0.f;
+    int ks = 0, stage = 0;
+    int BIn = BI, BJn = BJ;
+    int64_t Ln = L;
+    while (L < hi) {
+      int ksn = ks + 1;
+      if (ksn == nk) {
+        Ln = next_valid(L + U, BIn, BJn);
+        ksn = 0;
       }
-      __syncthreads();
-      const int bi = 2 * BI + (wr >> 1), bj = 2 * BJ + wc;  // this wave's 128-sub-tile
-      const int64_t slot = slot_base + L * 8 + w;
-      WindowHist wh;
-      SlotWriter sw;
-      if (smode == kSelBracket) sw.begin(st, sl, slot);
-      if (epi == 3 || bi >= Tm || bj >= Tn || (SYM && bi + r0t > bj)) {
-        tile.zero();
-        if (smode == kSelBracket) sw.finish(sl, slot, false);
-      } else {
-        if constexpr (M16)
-          sq_epilogue16<SYM, smode>(tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128,
-                                    snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl,
-                                    slot, epi, layout == 0, r0t);
-        else
-          sq_epilogue<SYM, smode, true, GramX3WTile, 4>(
-              tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128,
-              snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl, slot, epi, layout == 0,
-              r0t, c2);
+      const bool more = Ln < hi;
+      if (more) issue(smem + (stage ^ 1) * GramX3WTile::kStage, BIn, BJn, ksn);
+      tile.compute(smem + stage * GramX3WTile::kStage, wr, wc, (int)(row0 & 15));
+      GramX3WTile::template ring_barrier<0>();
+      if (ks + 1 == nk) {
+        epilogue(L, BI, BJ);
+        L = Ln;
+        BI = BIn;
+        BJ = BJn;
       }
-      if (smode == kSelHist) wh.flush(shist);
-      L = Ln;
-      BI = BIn;
-      BJ = BJn;
+      ks = ksn;
+      stage ^= 1;
     }
-    ks = ksn;
-    stage ^= 1;
   }
   if (smode == kSelHist) {
     __syncthreads();
@@ -427,11 +497,17 @@ int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, 
   int rc = 0;
   {
     int bs = 0, bn = 0;
+    // FmtH2: 3-stage ring (DSVGD_GRAM_H2_FORM 1: half-tile blocks, two per CU);
+    // FmtX3: whole 256-tiles, 2-stage ring
+    constexpr int WN = (F::P == 3 || kGramH2Form != 1) ? 2 : 1;
+    constexpr int NS = (F::P == 2 && WN == 2) ? 3 : 2;
     if ((rc = persistent_blocks(
-             reinterpret_cast<const void*>(&sqdist_x3w_kernel<true, SM, F::P == 3, F>), &bs)))
+             reinterpret_cast<const void*>(&sqdist_x3w_kernel<true, SM, F::P == 3, F, WN, NS>), &bs,
+             256 * WN)))
       return rc;
     if ((rc = persistent_blocks(
-             reinterpret_cast<const void*>(&sqdist_x3w_kernel<false, SM, F::P == 3, F>), &bn)))
+             reinterpret_cast<const void*>(&sqdist_x3w_kernel<false, SM, F::P == 3, F, WN, NS>), &bn,
+             256 * WN)))
       return rc;
     const int Tn2 = (int)((n_pad / 128 + 1) / 2), Tm2 = (int)((m_pad / 128 + 1) / 2);
     struct Part {
@@ -460,7 +536,7 @@ int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, 
       const Part& P = parts[i];
       const int lay = sym ? layout : 0;
 #define DSVGD_X3W(SY, M, B, LAY, R0T)                                                          \
-  hipLaunchKernelGGL((sqdist_x3w_kernel<SY, SM, M, F>), dim3((unsigned)B), dim3(512), 0, s, Yg,    \
+  hipLaunchKernelGGL((sqdist_x3w_kernel<SY, SM, M, F, WN, NS>), dim3((unsigned)B), dim3(256 * WN), 0, s, Yg, \
                      img, norms, row0, m, n, n_pad, nk, D, st, cand, epi, P.total, LAY, P.tm2,   \
                      P.tc2, P.bj_off, R0T, base, ns_total, tsc)
       if (P.sym)

@@ -21,8 +21,11 @@ def main():
     ap.add_argument("--d", type=int, default=256)
     ap.add_argument("--configs", default="h2:sym,h2:full,x3:sym,x3:full")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--lib", default=None, help="an A/B build of the library (make ab)")
     args = ap.parse_args()
     import dsvgd
+    if args.lib:
+        dsvgd._native.LIB_PATH = os.path.abspath(args.lib)
     g = torch.Generator(device="cpu").manual_seed(0)
     X = (0.1 * torch.randn(args.n, args.d, generator=g)).cuda()
     S = torch.randn(args.n, args.d, generator=g).cuda()
