@@ -236,8 +236,8 @@ def main():
     # the committed PMC summary is an N=1 profile: only quoted for the N=1 run
     # phi_mm is the NN tile with the fused exp (<TN, DMA, EXP=true, ..., Fmt>);
     # the logreg G.Xd launch is the same tile with EXP=false
-    kname = {"h2": "void dsvgd::nn_x3_kernel<4, true, true, false, 2, dsvgd::FmtH2>",
-             "x3": "void dsvgd::nn_x3_kernel<4, true, true, true, 2, dsvgd::FmtX3>",
+    kname = {"h2": "void dsvgd::nn_x3_kernel<4, true, true, false, 2, dsvgd::FmtH2,",
+             "x3": "void dsvgd::nn_x3_kernel<4, true, true, true, 2, dsvgd::FmtX3,",
              "f32": "void dsvgd::nn_kernel<4, true,"}[gemm]
     traffic, traffic_src = pmc_traffic(kname) if world == 1 else (None, None)
     flops = 4.0 * m * n * d

@@ -71,8 +71,16 @@ __global__ __launch_bounds__(256) void colscale_final_kernel(const uint32_t* __r
   float tmin = INFINITY;
   int nonfinite = 0;
   for (int64_t c = threadIdx.x; c < cols; c += 256) {
+    // eight independent chains: the loads are in flight together
+    uint32_t mq[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    int64_t b = 0;
+    for (; b + 8 <= nb; b += 8)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) mq[q] = max(mq[q], partial[(b + q) * cols + c]);
+    for (; b < nb; ++b) mq[0] = max(mq[0], partial[b * cols + c]);
     uint32_t mb = 0u;
-    for (int64_t b = 0; b < nb; ++b) mb = max(mb, partial[b * cols + c]);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) mb = max(mb, mq[q]);
     const float m = __uint_as_float(mb);
     const float s = pow2_scale(m);
     out[c] = s;
@@ -126,6 +134,10 @@ __global__ __launch_bounds__(256) void ysplit_h2_kernel(const float* __restrict_
 
 // img[kstep][part][row][16 k] = the two fp16 parts of t A[row][16 kstep + k]
 // (t = *tscale; zero outside rows x cols; halves swapped on rows with bit 3 set)
+// VEC: A 16-byte aligned with lda % 4 == 0 -- a thread's 16 values come in
+// as four 16-byte loads (scalar loads would touch 64 rows' lines per
+// wave-instruction, 16 times over)
+template <bool VEC>
 __global__ __launch_bounds__(256) void rowsplit_h2_kernel(const float* __restrict__ A,
                                                           int64_t lda, int64_t rows, int64_t cols,
                                                           int64_t rows_pad, int64_t ksteps,
@@ -135,12 +147,27 @@ __global__ __launch_bounds__(256) void rowsplit_h2_kernel(const float* __restric
   if (t >= ksteps * rows_pad) return;
   const int64_t kb = t / rows_pad, i = t % rows_pad;
   const float sc = *tscale;
+  float a[16];
+  if (VEC && i < rows && kb * 16 + 16 <= cols) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(A + i * lda + kb * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 v = src[q];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[4 * q + e] = v[e];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int64_t c = kb * 16 + k;
+      a[k] = (i < rows && c < cols) ? A[i * lda + c] : 0.f;
+    }
+  }
   f16x8 s[2][2];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const int64_t c = kb * 16 + k;
     _Float16 v[2];
-    split_fmt<FmtH2>((i < rows && c < cols) ? sc * A[i * lda + c] : 0.f, v);
+    split_fmt<FmtH2>(sc * a[k], v);
     s[0][k >> 3][k & 7] = v[0];
     s[1][k >> 3][k & 7] = v[1];
   }
@@ -180,8 +207,13 @@ int h2_ysplit(const float* Y, int64_t ldy, int64_t rows, const float* colscale, 
 int h2_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
                 int64_t kpad, const float* tscale, void* img, hipStream_t s) {
   const int64_t ksteps = kpad / kX3Step, threads = ksteps * rows_pad;
-  hipLaunchKernelGGL(rowsplit_h2_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
-                     A, lda, rows, cols, rows_pad, ksteps, tscale, (_Float16*)img);
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  if (((uintptr_t)A & 15) == 0 && lda % 4 == 0)
+    hipLaunchKernelGGL(rowsplit_h2_kernel<true>, grid, dim3(256), 0, s, A, lda, rows, cols,
+                       rows_pad, ksteps, tscale, (_Float16*)img);
+  else
+    hipLaunchKernelGGL(rowsplit_h2_kernel<false>, grid, dim3(256), 0, s, A, lda, rows, cols,
+                       rows_pad, ksteps, tscale, (_Float16*)img);
   return check_launch("rowsplit_h2");
 }
 

@@ -466,10 +466,15 @@ static int score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const
     float* sxd = (float*)(base + w.off_sxd);
     float* sws = (float*)(base + w.off_sws);
     float* zs = (float*)(base + w.off_zs);
-    if ((rc = h2_colscale(X + 1, ldx, n, p, sws, sw, s))) return rc;
+    // W = X[:, 1:] is not 16-byte aligned: a padded copy first (the row
+    // image then reads it with 16-byte loads)
+    hipLaunchKernelGGL(pad_copy_kernel, dim3((w.n_pad * w.ldb + 255) / 256), dim3(256), 0, s, X,
+                       ldx, 1, n, p, w.n_pad, Wp, w.ldb);
+    if ((rc = check_launch("pad_copy(W)"))) return rc;
+    if ((rc = h2_colscale(Wp, w.ldb, n, p, sws, sw, s))) return rc;
     if ((rc = h2_colscale(Xdp, w.ldb, w.N_pad, w.ldb, sws, sxd, s))) return rc;
     // tensor scales for the Z images, per-column ones for G . Xd's B image
-    if ((rc = h2_rowsplit(X + 1, ldx, n, p, w.n_pad, w.pp, sw + 2 * p, Wx, s))) return rc;
+    if ((rc = h2_rowsplit(Wp, w.ldb, n, p, w.n_pad, w.pp, sw + 2 * p, Wx, s))) return rc;
     if ((rc = h2_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, sxd + 2 * w.ldb, Xdx, s)))
       return rc;
     if ((rc = h2_ysplit(Xdp, w.ldb, w.N_pad, sxd, Xdy, s))) return rc;

@@ -62,6 +62,8 @@ the travelling block is communicated) and include_wasserstein=False.
 Deviation: exchange_scores with num_shards == 1 uses the local scores (the
 reference reads an uninitialised buffer there).
 """
+import warnings
+
 import torch
 
 from . import _native as N
@@ -76,6 +78,7 @@ class DistSampler(object):
     timer = None   # optional engine.StageTimer (bench instrumentation)
     keep_phi = False  # Jacobi: also write phi of the owned rows to the engine's `phi` (tests)
     graphs = True  # S = 1, no W2, built-in target: replay each step as a HIP graph
+    W2_WARN_ENTRIES = 1 << 24  # R > 1 plans this large warn at construction
 
     def __init__(self, rank, num_shards, logp, kernel, particles,
                  N_local, N_global,
@@ -147,6 +150,22 @@ class DistSampler(object):
         self._sbuf = None
         self._graph = None
         self._graph_key = None
+        self._warn_w2_cost()
+
+    def _warn_w2_cost(self):
+        """The W2 term is the reference default, but with particles exchanged
+        (R = n / m = num_shards > 1) its exact assignment is an auction of
+        10^4-10^5 rounds (DESIGN.md, W2 cost at scale): say so once, at
+        construction, instead of letting make_step stall for seconds."""
+        m = self._particles_per_shard
+        n = self._num_particles if self._exchange_particles else m
+        if self._include_wasserstein and n > m and m * n >= self.W2_WARN_ENTRIES:
+            warnings.warn(
+                "DistSampler: include_wasserstein=True with R = n/m = %d > 1 and an "
+                "%d x %d plan: the exact W2 assignment takes seconds per step at this "
+                "size (m=8192, n=65536: ~46 s cold, ~4-13x less warm); pass "
+                "include_wasserstein=False for throughput" % (n // m, m, n),
+                RuntimeWarning, stacklevel=3)
 
     # ---------------------------------------------------- reference API --
     @property

@@ -166,6 +166,7 @@ class PhiEngine(object):
         self.dp = lib.dsvgd_dp(d)
         self.ldy = lib.dsvgd_ldy(self.dp)
         f32 = dict(dtype=torch.float32, device=dev)
+        self._check_memory(dev)
         rows = self.n_pad + 128
         self.Y = torch.zeros(rows, self.ldy, **f32)
         self.norms = torch.zeros(rows, **f32)
@@ -224,6 +225,24 @@ class PhiEngine(object):
             # 1/16 of the entries leaves ~5x headroom over the ~1.2 % in bracket
             self.cand_cap = max(1 << 22, (m * n) // 16)
             self.cand = torch.empty(self.cand_cap, **f32)
+
+    def _check_memory(self, dev):
+        """D is materialised (m_pad x n_pad fp32, no recompute path), so one
+        engine's footprint grows as m n: refuse up front, with the sizes, what
+        would otherwise be an allocator OOM halfway through the buffers."""
+        d_bytes = 4 * self.m_pad * self.n_pad
+        cand = 4 * max(1 << 22, (self.m * self.n) // 16) if self.m * self.n >= self.BRACKET_MIN_ENTRIES else 0
+        splits = N.load().dsvgd_phi_splits(self.m, self.n, self.ldy)
+        other = 4 * ((self.n_pad + 128) * self.ldy * 3 + splits * self.m * self.ldy)
+        need = d_bytes + cand + other
+        free, _ = torch.cuda.mem_get_info(dev)
+        if need > free:
+            raise MemoryError(
+                "PhiEngine(n=%d, d=%d, m=%d) needs %.1f GiB of device memory (D is %d x %d "
+                "fp32 = %.1f GiB) but %.1f GiB are free; shard the rows over more ranks "
+                "(DistSampler, m = n / num_shards) or reduce n"
+                % (self.n, self.d, self.m, need / 2**30, self.m_pad, self.n_pad,
+                   d_bytes / 2**30, free / 2**30))
 
     # ------------------------------------------------------------ stages --
     def pack(self, X, S=None, score_scale=1.0):
