@@ -134,10 +134,13 @@ __global__ __launch_bounds__(256) void ysplit_h2_kernel(const float* __restrict_
 
 // img[kstep][part][row][16 k] = the two fp16 parts of t A[row][16 kstep + k]
 // (t = *tscale; zero outside rows x cols; halves swapped on rows with bit 3 set)
-// VEC: A 16-byte aligned with lda % 4 == 0 -- a thread's 16 values come in
-// as four 16-byte loads (scalar loads would touch 64 rows' lines per
-// wave-instruction, 16 times over)
-template <bool VEC>
+// OFF >= 0: lda % 4 == 0 and A sits OFF floats past a 16-byte boundary (e.g.
+// logreg's W = X[:, 1:], OFF = 1): a thread's 16 values come in as 16-byte
+// loads of the aligned window around them (four, or five when OFF > 0; each
+// load's 16-byte chunk holds an element of the row, so it stays inside
+// mapped memory) -- scalar loads would touch 64 rows' lines per
+// wave-instruction, 16 times over.  OFF < 0: element loads (any layout).
+template <int OFF>
 __global__ __launch_bounds__(256) void rowsplit_h2_kernel(const float* __restrict__ A,
                                                           int64_t lda, int64_t rows, int64_t cols,
                                                           int64_t rows_pad, int64_t ksteps,
@@ -148,14 +151,19 @@ __global__ __launch_bounds__(256) void rowsplit_h2_kernel(const float* __restric
   const int64_t kb = t / rows_pad, i = t % rows_pad;
   const float sc = *tscale;
   float a[16];
-  if (VEC && i < rows && kb * 16 + 16 <= cols) {
-    const f32x4* src = reinterpret_cast<const f32x4*>(A + i * lda + kb * 16);
+  if (OFF >= 0 && i < rows && kb * 16 + 16 <= cols) {
+    constexpr int kOff = OFF < 0 ? 0 : OFF;
+    constexpr int kLoads = kOff ? 5 : 4;
+    const f32x4* src = reinterpret_cast<const f32x4*>(A + i * lda + kb * 16 - kOff);
+    float win[4 * kLoads];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < kLoads; ++q) {
       const f32x4 v = src[q];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) a[4 * q + e] = v[e];
+      for (int e = 0; e < 4; ++e) win[4 * q + e] = v[e];
     }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a[k] = win[k + kOff];
   } else {
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -208,12 +216,18 @@ int h2_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t
                 int64_t kpad, const float* tscale, void* img, hipStream_t s) {
   const int64_t ksteps = kpad / kX3Step, threads = ksteps * rows_pad;
   const dim3 grid((unsigned)((threads + 255) / 256));
-  if (((uintptr_t)A & 15) == 0 && lda % 4 == 0)
-    hipLaunchKernelGGL(rowsplit_h2_kernel<true>, grid, dim3(256), 0, s, A, lda, rows, cols,
-                       rows_pad, ksteps, tscale, (_Float16*)img);
-  else
-    hipLaunchKernelGGL(rowsplit_h2_kernel<false>, grid, dim3(256), 0, s, A, lda, rows, cols,
-                       rows_pad, ksteps, tscale, (_Float16*)img);
+  const int off = ((uintptr_t)A & 3) == 0 && lda % 4 == 0 ? (int)(((uintptr_t)A >> 2) & 3) : -1;
+#define DSVGD_ROWSPLIT_H2(O)                                                                 \
+  hipLaunchKernelGGL(rowsplit_h2_kernel<O>, grid, dim3(256), 0, s, A, lda, rows, cols, rows_pad, \
+                     ksteps, tscale, (_Float16*)img)
+  switch (off) {
+    case 0: DSVGD_ROWSPLIT_H2(0); break;
+    case 1: DSVGD_ROWSPLIT_H2(1); break;
+    case 2: DSVGD_ROWSPLIT_H2(2); break;
+    case 3: DSVGD_ROWSPLIT_H2(3); break;
+    default: DSVGD_ROWSPLIT_H2(-1); break;
+  }
+#undef DSVGD_ROWSPLIT_H2
   return check_launch("rowsplit_h2");
 }
 

@@ -42,13 +42,14 @@ static int64_t nn_cols(int64_t w) {
 }
 
 struct LogregWs {
-  int64_t n_pad, N_pad, pp, ldb;
+  int64_t N, n_pad, N_pad, pp, ldb;
   size_t off_w, off_xd, off_t, off_g, off_gw, off_wx, off_xdx, off_xdy, off_sw, off_sxd, off_sws,
       off_zs, total;
 };
 
 static LogregWs logreg_ws(int64_t n, int64_t N, int64_t p) {
   LogregWs w;
+  w.N = N;
   w.n_pad = roundup(n, 256);  // whole 256 x 256 Z tiles
   w.N_pad = roundup(N, 256);
   w.pp = roundup(p < 1 ? 1 : p, 32);
@@ -420,64 +421,84 @@ size_t dsvgd_logreg_workspace_bytes(int64_t n, int64_t N, int64_t p) {
 }
 
 // engine: 0 = FmtH2 split engine (default), 1 = FmtX3, 2 = f32 MFMA (reference)
-static int score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const float* Xd,
-                        int64_t ldxd, const float* t, int64_t N, float scale, float* S, int64_t lds,
-                        void* workspace, void* stream, int engine) {
-  DSVGD_REQUIRE(X && Xd && t && S && workspace, "null pointer");
-  DSVGD_REQUIRE(n > 0 && d >= 2 && N > 0 && ldx >= d && lds >= d && ldxd >= d - 1, "sizes");
-  DSVGD_REQUIRE(((uintptr_t)workspace & 255) == 0, "workspace must be 256-byte aligned");
-  const int64_t p = d - 1;
-  if (n <= kSmallMaxRows && (p <= kSmallRegP || N <= kSmallMaxN)) {  // latency path
-    hipLaunchKernelGGL(logreg_small_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream,
-                       X, ldx, p, Xd, ldxd, t, N, scale, S, lds);
-    return check_launch("logreg_small");
+// The data-only half of the workspace (padded Xd / t, Xd's scales and images)
+// depends on (Xd, t) alone: logreg_prepare fills it once per data set and
+// logreg_step reuses it every step (the particles change, the data do not).
+struct LogregPlan {
+  LogregWs w;
+  bool x3, h2;
+  char* base;
+};
+
+static LogregPlan logreg_plan(int64_t n, int64_t N, int64_t p, void* workspace, int engine) {
+  LogregPlan P;
+  P.w = logreg_ws(n, N, p);
+  const LogregWs& w = P.w;
+  const bool fits =
+      w.n_pad * w.pp * 6 < ((int64_t)1 << 31) && w.N_pad * w.ldb * 6 < ((int64_t)1 << 31);
+  P.x3 = engine == 1 && fits;
+  P.h2 = engine == 0 && fits;
+  P.base = (char*)workspace;
+  return P;
+}
+
+static bool logreg_small(int64_t n, int64_t N, int64_t p) {
+  return n <= kSmallMaxRows && (p <= kSmallRegP || N <= kSmallMaxN);
+}
+
+static int logreg_prepare(const float* Xd, int64_t ldxd, const float* t, int64_t N, int64_t p,
+                          const LogregPlan& P, hipStream_t s) {
+  const LogregWs& w = P.w;
+  float* Xdp = (float*)(P.base + w.off_xd);
+  float* tp = (float*)(P.base + w.off_t);
+  const int64_t tot = w.N_pad * w.ldb;
+  hipLaunchKernelGGL(pad_copy_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Xd, ldxd, 0, N, p,
+                     w.N_pad, Xdp, w.ldb);
+  int rc = check_launch("pad_copy(Xd)");
+  if (rc) return rc;
+  hipLaunchKernelGGL(pad_copy_kernel, dim3((w.N_pad + 255) / 256), dim3(256), 0, s, t, 1, 0, N, 1,
+                     w.N_pad, tp, 1);
+  if ((rc = check_launch("pad_copy(t)"))) return rc;
+  if (P.h2) {
+    float* sxd = (float*)(P.base + w.off_sxd);
+    float* sws = (float*)(P.base + w.off_sws);
+    if ((rc = h2_colscale(Xdp, w.ldb, w.N_pad, w.ldb, sws, sxd, s))) return rc;
+    // the tensor scale for Z's Xd image, per-column ones for G . Xd's B image
+    if ((rc = h2_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, sxd + 2 * w.ldb,
+                          P.base + w.off_xdx, s)))
+      return rc;
+    return h2_ysplit(Xdp, w.ldb, w.N_pad, sxd, (_Float16*)(P.base + w.off_xdy), s);
   }
-  const LogregWs w = logreg_ws(n, N, p);
-  DSVGD_REQUIRE(w.n_pad / 128 <= 65535, "too many row tiles");
-  char* base = (char*)workspace;
-  float* Wp = (float*)(base + w.off_w);
+  if (P.x3) {
+    // the persistent 16x16x32 Z form reads unswizzled images
+    if ((rc = dsvgd_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, P.base + w.off_xdx, 0, s)))
+      return rc;
+    const int m16 = w.ldb % 256 == 0;  // the 16x16x32 form (unswizzled image) when it applies
+    return dsvgd_ysplit(Xdp, w.ldb, w.N_pad, P.base + w.off_xdy, m16 ? 0 : 1, s);
+  }
+  return DSVGD_OK;
+}
+
+static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float scale, float* S,
+                       int64_t lds, const LogregPlan& P, hipStream_t s) {
+  const LogregWs& w = P.w;
+  char* base = P.base;
   float* Xdp = (float*)(base + w.off_xd);
   float* tp = (float*)(base + w.off_t);
   float* G = (float*)(base + w.off_g);
   float* GW = (float*)(base + w.off_gw);
-  hipStream_t s = (hipStream_t)stream;
-  const bool fits = w.n_pad * w.pp * 6 < ((int64_t)1 << 31) && w.N_pad * w.ldb * 6 < ((int64_t)1 << 31);
-  const bool x3 = engine == 1 && fits;
-  const bool h2 = engine == 0 && fits;
-  int64_t tot = w.n_pad * w.ldb;
   int rc = 0;
-  if (!x3 && !h2) {
-    hipLaunchKernelGGL(pad_copy_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, X, ldx, 1, n, p,
-                       w.n_pad, Wp, w.ldb);
-    if ((rc = check_launch("pad_copy(W)"))) return rc;
-  }
-  tot = w.N_pad * w.ldb;
-  hipLaunchKernelGGL(pad_copy_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Xd, ldxd, 0, N, p,
-                     w.N_pad, Xdp, w.ldb);
-  if ((rc = check_launch("pad_copy(Xd)"))) return rc;
-  hipLaunchKernelGGL(pad_copy_kernel, dim3((w.N_pad + 255) / 256), dim3(256), 0, s, t, 1, 0, N, 1,
-                     w.N_pad, tp, 1);
-  if ((rc = check_launch("pad_copy(t)"))) return rc;
-  if (h2) {
+  if (P.h2) {
     void* Wx = base + w.off_wx;
-    void* Xdx = base + w.off_xdx;
     _Float16* Xdy = (_Float16*)(base + w.off_xdy);
     float* sw = (float*)(base + w.off_sw);
     float* sxd = (float*)(base + w.off_sxd);
     float* sws = (float*)(base + w.off_sws);
     float* zs = (float*)(base + w.off_zs);
-    // W = X[:, 1:] is not 16-byte aligned: a padded copy first (the row
-    // image then reads it with 16-byte loads)
-    hipLaunchKernelGGL(pad_copy_kernel, dim3((w.n_pad * w.ldb + 255) / 256), dim3(256), 0, s, X,
-                       ldx, 1, n, p, w.n_pad, Wp, w.ldb);
-    if ((rc = check_launch("pad_copy(W)"))) return rc;
-    if ((rc = h2_colscale(Wp, w.ldb, n, p, sws, sw, s))) return rc;
-    if ((rc = h2_colscale(Xdp, w.ldb, w.N_pad, w.ldb, sws, sxd, s))) return rc;
-    // tensor scales for the Z images, per-column ones for G . Xd's B image
-    if ((rc = h2_rowsplit(Wp, w.ldb, n, p, w.n_pad, w.pp, sw + 2 * p, Wx, s))) return rc;
-    if ((rc = h2_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, sxd + 2 * w.ldb, Xdx, s)))
-      return rc;
-    if ((rc = h2_ysplit(Xdp, w.ldb, w.N_pad, sxd, Xdy, s))) return rc;
+    // W = X[:, 1:] in place (the row image reads its unaligned rows through
+    // aligned 16-byte windows)
+    if ((rc = h2_colscale(X + 1, ldx, n, p, sws, sw, s))) return rc;
+    if ((rc = h2_rowsplit(X + 1, ldx, n, p, w.n_pad, w.pp, sw + 2 * p, Wx, s))) return rc;
     // the Z kernel's scale operand: [1/t_w, 1/t_x] side by side
     int blocks = 0;
     if ((rc = persistent_blocks(reinterpret_cast<const void*>(&logreg_z_x3p_kernel<FmtH2>),
@@ -488,53 +509,64 @@ static int score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const
                        sxd + 2 * w.ldb + 1, zs);
     if ((rc = check_launch("zscale_pair"))) return rc;
     hipLaunchKernelGGL(logreg_z_x3p_kernel<FmtH2>, dim3((unsigned)blocks), dim3(512), 0, s,
-                       (const _Float16*)Wx, w.n_pad, (const _Float16*)Xdx, w.N_pad,
+                       (const _Float16*)Wx, w.n_pad, (const _Float16*)(base + w.off_xdx), w.N_pad,
                        (int)(w.pp / kX3Step), tp, w.N_pad, G, Tm2, Tn2,
                        tile_grid(Tm2, Tn2, false), (const float*)zs);
     if ((rc = check_launch("logreg_z_h2"))) return rc;
     if ((rc = nn_h2_gemm(false, G, w.N_pad, Xdy, w.ldb, 1, nullptr, GW, w.ldb, nullptr, n, 0, s, 0,
                          sxd + w.ldb)))
       return rc;
-    hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,
-                       w.ldb, scale, S, lds);
-    return check_launch("logreg_finish");
-  }
-  if (x3) {
+  } else if (P.x3) {
     void* Wx = base + w.off_wx;
-    void* Xdx = base + w.off_xdx;
-    __bf16* Xdy = (__bf16*)(base + w.off_xdy);
-    // the persistent 16x16x32 Z form reads unswizzled images
     if ((rc = dsvgd_rowsplit(X + 1, ldx, n, p, w.n_pad, w.pp, Wx, 0, s))) return rc;
-    if ((rc = dsvgd_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, Xdx, 0, s))) return rc;
-    const int m16 = w.ldb % 256 == 0;  // the 16x16x32 form (unswizzled image) when it applies
-    if ((rc = dsvgd_ysplit(Xdp, w.ldb, w.N_pad, Xdy, m16 ? 0 : 1, s))) return rc;
-    {
-      int blocks = 0;
-      if ((rc = persistent_blocks(reinterpret_cast<const void*>(&logreg_z_x3p_kernel<FmtX3>),
-                                  &blocks, 512)))
-        return rc;
-      const int Tm2 = (int)(w.n_pad / 256), Tn2 = (int)(w.N_pad / 256);
-      hipLaunchKernelGGL(logreg_z_x3p_kernel<FmtX3>, dim3((unsigned)blocks), dim3(512), 0, s,
-                         (const __bf16*)Wx, w.n_pad, (const __bf16*)Xdx, w.N_pad,
-                         (int)(w.pp / kX3Step), tp, w.N_pad, G, Tm2, Tn2,
-                         tile_grid(Tm2, Tn2, false), nullptr);
-    }
-    if ((rc = check_launch("logreg_z_x3"))) return rc;
-    if ((rc = nn_x3_gemm(false, G, w.N_pad, Xdy, w.ldb, 1, nullptr, GW, w.ldb, nullptr, n, 0, s, 0,
-                         m16)))
+    int blocks = 0;
+    if ((rc = persistent_blocks(reinterpret_cast<const void*>(&logreg_z_x3p_kernel<FmtX3>),
+                                &blocks, 512)))
       return rc;
-    hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,
-                       w.ldb, scale, S, lds);
-    return check_launch("logreg_finish");
+    const int Tm2 = (int)(w.n_pad / 256), Tn2 = (int)(w.N_pad / 256);
+    hipLaunchKernelGGL(logreg_z_x3p_kernel<FmtX3>, dim3((unsigned)blocks), dim3(512), 0, s,
+                       (const __bf16*)Wx, w.n_pad, (const __bf16*)(base + w.off_xdx), w.N_pad,
+                       (int)(w.pp / kX3Step), tp, w.N_pad, G, Tm2, Tn2,
+                       tile_grid(Tm2, Tn2, false), nullptr);
+    if ((rc = check_launch("logreg_z_x3"))) return rc;
+    const int m16 = w.ldb % 256 == 0;
+    if ((rc = nn_x3_gemm(false, G, w.N_pad, (const __bf16*)(base + w.off_xdy), w.ldb, 1, nullptr,
+                         GW, w.ldb, nullptr, n, 0, s, 0, m16)))
+      return rc;
+  } else {
+    float* Wp = (float*)(base + w.off_w);
+    hipLaunchKernelGGL(pad_copy_kernel, dim3((w.n_pad * w.ldb + 255) / 256), dim3(256), 0, s, X,
+                       ldx, 1, n, p, w.n_pad, Wp, w.ldb);
+    if ((rc = check_launch("pad_copy(W)"))) return rc;
+    hipLaunchKernelGGL(logreg_z_kernel, dim3(w.N_pad / ZTile::BN, w.n_pad / ZTile::BM), dim3(256),
+                       0, s, Wp, Xdp, w.ldb, (int)w.pp, tp, w.N, w.N_pad, G);
+    if ((rc = check_launch("logreg_z"))) return rc;
+    if ((rc = nn_gemm(false, G, w.N_pad, Xdp, w.ldb, w.ldb, 1, nullptr, GW, w.ldb, nullptr, n, 0,
+                      s)))
+      return rc;
   }
-  hipLaunchKernelGGL(logreg_z_kernel, dim3(w.N_pad / ZTile::BN, w.n_pad / ZTile::BM), dim3(256), 0,
-                     s, Wp, Xdp, w.ldb, (int)w.pp, tp, N, w.N_pad, G);
-  if ((rc = check_launch("logreg_z"))) return rc;
-  if ((rc = nn_gemm(false, G, w.N_pad, Xdp, w.ldb, w.ldb, 1, nullptr, GW, w.ldb, nullptr, n, 0, s)))
-    return rc;
   hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,
                      w.ldb, scale, S, lds);
   return check_launch("logreg_finish");
+}
+
+static int score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const float* Xd,
+                        int64_t ldxd, const float* t, int64_t N, float scale, float* S, int64_t lds,
+                        void* workspace, void* stream, int engine) {
+  DSVGD_REQUIRE(X && Xd && t && S && workspace, "null pointer");
+  DSVGD_REQUIRE(n > 0 && d >= 2 && N > 0 && ldx >= d && lds >= d && ldxd >= d - 1, "sizes");
+  DSVGD_REQUIRE(((uintptr_t)workspace & 255) == 0, "workspace must be 256-byte aligned");
+  const int64_t p = d - 1;
+  if (logreg_small(n, N, p)) {  // latency path
+    hipLaunchKernelGGL(logreg_small_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream,
+                       X, ldx, p, Xd, ldxd, t, N, scale, S, lds);
+    return check_launch("logreg_small");
+  }
+  DSVGD_REQUIRE(roundup(n, 128) / 128 <= 65535, "too many row tiles");
+  const LogregPlan P = logreg_plan(n, N, p, workspace, engine);
+  int rc = logreg_prepare(Xd, ldxd, t, N, p, P, (hipStream_t)stream);
+  if (rc) return rc;
+  return logreg_step(X, ldx, n, p, scale, S, lds, P, (hipStream_t)stream);
 }
 
 int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const float* Xd,
@@ -548,6 +580,32 @@ int dsvgd_score_logreg_engine(const float* X, int64_t ldx, int64_t n, int64_t d,
                               int64_t lds, void* workspace, int engine, void* stream) {
   DSVGD_REQUIRE(engine >= 0 && engine <= 2, "engine must be 0 (h2), 1 (x3) or 2 (f32)");
   return score_logreg(X, ldx, n, d, Xd, ldxd, t, N, scale, S, lds, workspace, stream, engine);
+}
+
+int dsvgd_logreg_prepare(const float* Xd, int64_t ldxd, const float* t, int64_t N, int64_t n,
+                         int64_t d, void* workspace, int engine, void* stream) {
+  DSVGD_REQUIRE(Xd && t && workspace, "null pointer");
+  DSVGD_REQUIRE(n > 0 && d >= 2 && N > 0 && ldxd >= d - 1, "sizes");
+  DSVGD_REQUIRE(((uintptr_t)workspace & 255) == 0, "workspace must be 256-byte aligned");
+  DSVGD_REQUIRE(engine >= 0 && engine <= 2, "engine must be 0 (h2), 1 (x3) or 2 (f32)");
+  DSVGD_REQUIRE(!logreg_small(n, N, d - 1),
+                "n <= 32 takes the one-block path: call dsvgd_score_logreg_engine");
+  DSVGD_REQUIRE(roundup(n, 128) / 128 <= 65535, "too many row tiles");
+  return logreg_prepare(Xd, ldxd, t, N, d - 1, logreg_plan(n, N, d - 1, workspace, engine),
+                        (hipStream_t)stream);
+}
+
+int dsvgd_score_logreg_prepared(const float* X, int64_t ldx, int64_t n, int64_t d, int64_t N,
+                                float scale, float* S, int64_t lds, void* workspace, int engine,
+                                void* stream) {
+  DSVGD_REQUIRE(X && S && workspace, "null pointer");
+  DSVGD_REQUIRE(n > 0 && d >= 2 && N > 0 && ldx >= d && lds >= d, "sizes");
+  DSVGD_REQUIRE(((uintptr_t)workspace & 255) == 0, "workspace must be 256-byte aligned");
+  DSVGD_REQUIRE(engine >= 0 && engine <= 2, "engine must be 0 (h2), 1 (x3) or 2 (f32)");
+  DSVGD_REQUIRE(!logreg_small(n, N, d - 1),
+                "n <= 32 takes the one-block path: call dsvgd_score_logreg_engine");
+  return logreg_step(X, ldx, n, d - 1, scale, S, lds,
+                     logreg_plan(n, N, d - 1, workspace, engine), (hipStream_t)stream);
 }
 
 size_t dsvgd_logreg_predict_workspace_bytes(int64_t n, int64_t Nt, int64_t p) {

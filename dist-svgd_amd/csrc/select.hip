@@ -36,6 +36,27 @@ __device__ __forceinline__ void hist_key(uint32_t key, uint32_t want, uint32_t s
   if (hi == want) atomicAdd(&shist[(key >> shift) & mask], w);
 }
 
+// hist_key for values that pile into few bins (the candidates of a bracket:
+// all within [lo, hi], so digit 1 -- often digit 2 -- is the same for most of
+// a wave): the lanes whose bin equals the first active lane's add with one
+// atomic, the rest one each.
+__device__ __forceinline__ void hist_key_agg(uint32_t key, uint32_t want, uint32_t shift,
+                                             uint32_t mask, uint32_t hishift, uint32_t* shist,
+                                             uint32_t w) {
+  const uint32_t hi = hishift >= 32 ? 0u : (key >> hishift);
+  const bool ok = key < 0x7F800000u && hi == want;
+  const uint32_t bin = (key >> shift) & mask;
+  const uint32_t b0 = __builtin_amdgcn_readfirstlane(bin);
+  const bool agg = ok && bin == b0;
+  const uint64_t m = __ballot(agg);
+  if (agg) {
+    if ((uint32_t)(threadIdx.x & 63) == (uint32_t)(__ffsll((long long)m) - 1))
+      atomicAdd(&shist[b0], w * (uint32_t)__popcll(m));
+  } else if (ok) {
+    atomicAdd(&shist[bin], w);
+  }
+}
+
 // count: entries of D (any order); cand: optional candidate buffer used
 // instead of D when st->fallback == 0 (bracketed mode).
 // sym_npad > 0: D is a symmetric n_pad x n_pad matrix stored as its
@@ -56,6 +77,8 @@ __global__ __launch_bounds__(256) void radix_hist_kernel(const float* __restrict
   const int64_t stride = (int64_t)gridDim.x * 256;
   const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (use_cand) {  // one wave per candidate slot (weight 2: a mirrored tile)
+    // (measured: a block per slot with four loads in flight, or at most 256
+    // workgroups, were both slower -- 0.14 / 0.69 ms vs 0.10 ms per pass)
     const int64_t ns = (int64_t)st->nslots, cap = (int64_t)st->slot_cap;
     const uint32_t* cnt = reinterpret_cast<const uint32_t*>(cand);
     const float* data = cand + 2 * ns;
@@ -99,11 +122,19 @@ __global__ __launch_bounds__(256) void radix_hist_kernel(const float* __restrict
   flush_block_hist(shist, st);
 }
 
-// One block: find the bin that holds rank k, fix its digit, clear the bins.
-__global__ __launch_bounds__(256) void radix_pick_kernel(dsvgd_select_state* __restrict__ st,
-                                                         int pass) {
-  __shared__ unsigned long long part[256];
-  __shared__ unsigned long long excl[256];
+template <bool COHERENT>
+__device__ __forceinline__ unsigned long long load_bin(const uint64_t* p) {
+  if constexpr (COHERENT)  // bins other workgroups of this launch just added to
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    return *p;
+}
+
+// One block of 256: find the bin of `hist` that holds rank st->k, fix its
+// digit in st (prefix, remaining rank; the median and h after pass 3).
+template <bool COHERENT>
+__device__ void pick_digit(const uint64_t* hist, dsvgd_select_state* st, int pass,
+                           unsigned long long* part) {
   const int t = threadIdx.x;
   uint32_t shift, mask, hishift;
   digit_of(pass, shift, mask, hishift);
@@ -113,23 +144,25 @@ __global__ __launch_bounds__(256) void radix_pick_kernel(dsvgd_select_state* __r
   unsigned long long s = 0;
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
-    loc[u] = u < per ? st->hist[t * per + u] : 0ull;
+    loc[u] = u < per ? load_bin<COHERENT>(&hist[t * per + u]) : 0ull;
     s += loc[u];
   }
-  part[t] = s;
-  __syncthreads();
-  if (t == 0) {
-    unsigned long long run = 0;
-    for (int q = 0; q < 256; ++q) {
-      excl[q] = run;
-      run += part[q];
-    }
+  // block-wide exclusive scan of the per-thread sums: wave scans, then the
+  // four wave totals (a serial 256-step loop on one lane was ~5 us per pick)
+  const int lane = t & 63, wv = t >> 6;
+  unsigned long long inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
   }
+  if (lane == 63) part[wv] = inc;
   __syncthreads();
+  unsigned long long lo = inc - s;  // exclusive prefix of this thread's bins
+  for (int q = 0; q < wv; ++q) lo += part[q];
   const unsigned long long k = st->k;
-  const unsigned long long lo = excl[t];
-  __syncthreads();
-  if (k >= lo && k < lo + part[t]) {
+  __syncthreads();                   // all reads of part / st->k before any pick writes
+  if (k >= lo && k < lo + s) {
     unsigned long long run = lo;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -153,8 +186,20 @@ __global__ __launch_bounds__(256) void radix_pick_kernel(dsvgd_select_state* __r
       run += u < per ? loc[u] : 0ull;
     }
   }
+  __syncthreads();  // st and part / excl are reused by the caller
+}
+
+__device__ __forceinline__ void clear_bins(uint64_t* hist) {
 #pragma unroll
-  for (int u = 0; u < 8; ++u) st->hist[t * 8 + u] = 0ull;  // clear all 2048 bins
+  for (int u = 0; u < 8; ++u) hist[threadIdx.x * 8 + u] = 0ull;  // all 2048 bins (256 threads)
+}
+
+// One block: find the bin that holds rank k, fix its digit, clear the bins.
+__global__ __launch_bounds__(256) void radix_pick_kernel(dsvgd_select_state* __restrict__ st,
+                                                         int pass) {
+  __shared__ unsigned long long part[4];
+  pick_digit<false>(st->hist, st, pass, part);
+  clear_bins(st->hist);
 }
 
 __device__ void reset_state(dsvgd_select_state* st, unsigned long long k,
@@ -183,21 +228,26 @@ __global__ void select_init_kernel(dsvgd_select_state* st, int64_t n_total, int6
 }
 
 // bracket [lo, hi] = the medians the two sample selects found
-__global__ void bracket_init_kernel(dsvgd_select_state* st, int64_t n_total,
-                                    const dsvgd_select_state* lo_st,
-                                    const dsvgd_select_state* hi_st, int64_t cap) {
+__device__ __forceinline__ void bracket_reset(dsvgd_select_state* st, int64_t n_total, float lo,
+                                              float hi, int64_t cap) {
   const int t = threadIdx.x;
   for (int b = t; b < DSVGD_RADIX_BINS; b += blockDim.x) st->hist[b] = 0ull;
   if (t == 0) {
     const unsigned long long nn = (unsigned long long)n_total * (unsigned long long)n_total;
     reset_state(st, (nn - 1ull) / 2ull, (unsigned long long)n_total);
     st->fallback = 0u;
-    st->lo = lo_st->median;
-    st->hi = hi_st->median;
+    st->lo = lo;
+    st->hi = hi;
     st->cand_cap = (unsigned long long)cap;
     st->nslots = 0ull;
     st->slot_cap = 0ull;
   }
+}
+
+__global__ void bracket_init_kernel(dsvgd_select_state* st, int64_t n_total,
+                                    const dsvgd_select_state* lo_st,
+                                    const dsvgd_select_state* hi_st, int64_t cap) {
+  bracket_reset(st, n_total, lo_st->median, hi_st->median, cap);
 }
 
 // Sum the local candidate slots into (below_total, ncand_total, overflow),
@@ -322,6 +372,70 @@ __global__ __launch_bounds__(256) void sample_sqdist_any_kernel(const float* __r
   }
 }
 
+// ---- the sample bracket in seven launches -----------------------------------
+// (1 sample + 2 x (init + 3 x (hist + pick)) + bracket_init = 16
+// launches before.)  The two sample selects (ranks k_lo, k_hi of the s
+// sampled distances) share every sweep over the sample: digit 1 has one
+// histogram for both ranks (prefix 0), digits 2 and 3 two histograms under
+// each select's own prefix, filled in the same pass; one single-block launch
+// picks both digits.  The digit-1 pick also re-arms both selects (k, prefix),
+// the digit-3 pick arms the bracketed select of D (bracket_init's work).
+// Few workgroups per sweep (kSampleHistBlocks): every workgroup flushes its
+// bins with global atomics, and the sampled distances fall into a handful of
+// digit-1 bins, so thousands of workgroups would queue on the same addresses.
+constexpr int kSampleHistBlocks = 256;
+
+template <int PASS>
+__global__ __launch_bounds__(256) void sample_hist_kernel(const float* __restrict__ sample,
+                                                          int64_t s,
+                                                          dsvgd_select_state* __restrict__ lo,
+                                                          dsvgd_select_state* __restrict__ hi) {
+  constexpr int kHists = PASS == 1 ? 1 : 2;
+  __shared__ uint32_t shist[kHists][DSVGD_RADIX_BINS];
+  for (int b = threadIdx.x; b < kHists * DSVGD_RADIX_BINS; b += 256) (&shist[0][0])[b] = 0u;
+  uint32_t shift, mask, hishift;
+  digit_of(PASS, shift, mask, hishift);
+  const uint32_t want_lo = PASS == 1 ? 0u : lo->prefix >> hishift;
+  const uint32_t want_hi = PASS == 1 ? 0u : hi->prefix >> hishift;
+  __syncthreads();
+  const f32x4* S4 = reinterpret_cast<const f32x4*>(sample);
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < s / 4;
+       q += (int64_t)gridDim.x * 256) {
+    const f32x4 v = S4[q];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      hist_key_agg(__float_as_uint(v[e]), want_lo, shift, mask, hishift, shist[0], 1u);
+      if constexpr (PASS > 1)
+        hist_key_agg(__float_as_uint(v[e]), want_hi, shift, mask, hishift, shist[1], 1u);
+    }
+  }
+  __syncthreads();
+  flush_block_hist(shist[0], lo);
+  if constexpr (PASS > 1) flush_block_hist(shist[1], hi);
+}
+
+template <int PASS>
+__global__ __launch_bounds__(256) void sample_pick_kernel(dsvgd_select_state* __restrict__ lo,
+                                                          dsvgd_select_state* __restrict__ hi,
+                                                          int64_t s, int64_t k_lo, int64_t k_hi,
+                                                          dsvgd_select_state* __restrict__ st,
+                                                          int64_t n_total, int64_t cand_cap) {
+  __shared__ unsigned long long part[4];
+  if constexpr (PASS == 1) {
+    if (threadIdx.x == 0) {
+      reset_state(lo, (unsigned long long)k_lo, (unsigned long long)s);
+      reset_state(hi, (unsigned long long)k_hi, (unsigned long long)s);
+    }
+    __syncthreads();
+  }
+  // digit 1: both ranks pick from the one shared histogram (lo's bins)
+  pick_digit<false>(lo->hist, lo, PASS, part);
+  pick_digit<false>(PASS == 1 ? lo->hist : hi->hist, hi, PASS, part);
+  clear_bins(lo->hist);
+  clear_bins(hi->hist);
+  if constexpr (PASS == 3) bracket_reset(st, n_total, lo->median, hi->median, cand_cap);
+}
+
 }  // namespace dsvgd
 
 using namespace dsvgd;
@@ -371,6 +485,31 @@ int dsvgd_sample_sqdist(const float* Y, int64_t ldy, int64_t n, int64_t d, int64
   hipLaunchKernelGGL(sample_sqdist_any_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, Y,
                      ldy, n, (int)d, s, seed, out);
   return check_launch("sample_sqdist_any");
+}
+
+int dsvgd_sample_bracket(const float* Y, int64_t ldy, int64_t n, int64_t d, int64_t s,
+                         uint64_t seed, int64_t k_lo, int64_t k_hi, float* sample,
+                         dsvgd_select_state* lo_st, dsvgd_select_state* hi_st,
+                         dsvgd_select_state* st, int64_t n_total, int64_t cand_cap,
+                         void* stream) {
+  DSVGD_REQUIRE(Y && sample && lo_st && hi_st && st, "null pointer");
+  DSVGD_REQUIRE(n > 0 && d > 0 && ldy >= d && n_total > 0 && cand_cap > 0, "sizes");
+  DSVGD_REQUIRE(s > 0 && s % 4 == 0 && ((uintptr_t)sample & 15) == 0,
+                "s must be a positive multiple of 4, sample 16-byte aligned");
+  DSVGD_REQUIRE(0 <= k_lo && k_lo <= k_hi && k_hi < s, "ranks: 0 <= k_lo <= k_hi < s");
+  int rc = dsvgd_sample_sqdist(Y, ldy, n, d, s, seed, sample, stream);
+  if (rc) return rc;
+  hipStream_t strm = (hipStream_t)stream;
+  const dim3 hb((unsigned)std::min<int64_t>((s / 4 + 255) / 256, kSampleHistBlocks));
+#define DSVGD_SAMPLE_PASS(P)                                                                     \
+  hipLaunchKernelGGL(sample_hist_kernel<P>, hb, dim3(256), 0, strm, sample, s, lo_st, hi_st);   \
+  hipLaunchKernelGGL(sample_pick_kernel<P>, dim3(1), dim3(256), 0, strm, lo_st, hi_st, s, k_lo, \
+                     k_hi, st, n_total, cand_cap)
+  DSVGD_SAMPLE_PASS(1);
+  DSVGD_SAMPLE_PASS(2);
+  DSVGD_SAMPLE_PASS(3);
+#undef DSVGD_SAMPLE_PASS
+  return check_launch("sample_bracket");
 }
 
 int dsvgd_bracket_init(dsvgd_select_state* st, int64_t n_total, const dsvgd_select_state* lo_st,

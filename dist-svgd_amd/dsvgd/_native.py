@@ -37,6 +37,8 @@ SIGNATURES = {
     "dsvgd_radix_pick": (_int, [_p, _int, _p]),
     "dsvgd_sample_sqdist": (_int, [_p, _i64, _i64, _i64, _i64, _c.c_uint64, _p, _p]),
     "dsvgd_bracket_init": (_int, [_p, _i64, _p, _p, _i64, _p]),
+    "dsvgd_sample_bracket": (_int, [_p, _i64, _i64, _i64, _i64, _c.c_uint64, _i64, _i64, _p, _p,
+                                    _p, _p, _i64, _i64, _p]),
     "dsvgd_bracket_totals": (_int, [_p, _p, _p]),
     "dsvgd_bracket_check": (_int, [_p, _p]),
     "dsvgd_set_bandwidth": (_int, [_p, _f, _p]),
@@ -74,6 +76,9 @@ SIGNATURES = {
                                   _p]),
     "dsvgd_score_logreg_engine": (_int, [_p, _i64, _i64, _i64, _p, _i64, _p, _i64, _f, _p, _i64,
                                          _p, _int, _p]),
+    "dsvgd_logreg_prepare": (_int, [_p, _i64, _p, _i64, _i64, _i64, _p, _int, _p]),
+    "dsvgd_score_logreg_prepared": (_int, [_p, _i64, _i64, _i64, _i64, _f, _p, _i64, _p, _int,
+                                           _p]),
     "dsvgd_logreg_predict_workspace_bytes": (_c.c_size_t, [_i64, _i64, _i64]),
     "dsvgd_logreg_predict": (_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _p, _p]),
 }

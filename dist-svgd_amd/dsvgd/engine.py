@@ -310,15 +310,9 @@ class PhiEngine(object):
                    self.n, self.d, N.ptr(self.D), self.n_pad, mode, st, cand, s)
 
     def _bracket(self, s):
-        N.call("dsvgd_sample_sqdist", N.ptr(self.Y), self.ldy, self.n, self.d, self.SAMPLE,
-               self.SEED, N.ptr(self.sample), s)
-        for sub, k in ((self.st_lo, self.k_lo), (self.st_hi, self.k_hi)):
-            N.call("dsvgd_select_init", sub.ptr, self.SAMPLE, k, s)
-            for p in (1, 2, 3):
-                N.call("dsvgd_radix_hist", N.ptr(self.sample), self.SAMPLE, None, p, sub.ptr, 0, s)
-                N.call("dsvgd_radix_pick", sub.ptr, p, s)
-        N.call("dsvgd_bracket_init", self.state.ptr, self.n, self.st_lo.ptr, self.st_hi.ptr,
-               self.cand_cap, s)
+        N.call("dsvgd_sample_bracket", N.ptr(self.Y), self.ldy, self.n, self.d, self.SAMPLE,
+               self.SEED, self.k_lo, self.k_hi, N.ptr(self.sample), self.st_lo.ptr,
+               self.st_hi.ptr, self.state.ptr, self.n, self.cand_cap, s)
 
     def median_bandwidth(self, allreduce=None):
         """Exact radix select (after distances(median=True)); `allreduce` sums

@@ -94,6 +94,7 @@ class LogisticRegression(BuiltinTarget):
         self.gemm = gemm
         self._dev = {}
         self._ws = {}
+        self._prepared = {}       # workspace key -> engine whose data image it holds
 
     @property
     def N(self):
@@ -134,13 +135,28 @@ class LogisticRegression(BuiltinTarget):
             self._ws[key] = ws
         base = ws.data_ptr()
         aligned = (base + 255) // 256 * 256
-        N.call("dsvgd_score_logreg_engine", N.ptr(X), N.ld(X), n, d, N.ptr(xd), N.ld(xd),
-               N.ptr(t), self.N, float(scale), N.ptr(out), N.ld(out), aligned,
-               self.ENGINES[self.gemm], N.stream(X.device))
+        eng = self.ENGINES[self.gemm]
+        s = N.stream(X.device)
+        if small:
+            N.call("dsvgd_score_logreg_engine", N.ptr(X), N.ld(X), n, d, N.ptr(xd), N.ld(xd),
+                   N.ptr(t), self.N, float(scale), N.ptr(out), N.ld(out), aligned, eng, s)
+            return
+        if self._prepared.get(key) != eng:
+            # the data-only half of the workspace (padded data, its scales
+            # and split images) once per workspace; every later step reuses it
+            N.call("dsvgd_logreg_prepare", N.ptr(xd), N.ld(xd), N.ptr(t), self.N, n, d, aligned,
+                   eng, s)
+            self._prepared[key] = eng
+            if not torch.cuda.is_current_stream_capturing():
+                # later calls may come on other streams (the DistSampler side stream)
+                torch.cuda.current_stream(X.device).synchronize()
+        N.call("dsvgd_score_logreg_prepared", N.ptr(X), N.ld(X), n, d, self.N, float(scale),
+               N.ptr(out), N.ld(out), aligned, eng, s)
 
     def release(self):
         """Free the score workspaces (no graph that captured them may replay after)."""
         self._ws.clear()
+        self._prepared.clear()
 
 
 class CallableTarget(Target):

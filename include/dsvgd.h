@@ -155,6 +155,17 @@ int dsvgd_sample_sqdist(const float* Y, int64_t ldy, int64_t n, int64_t d, int64
  * `out`) become the bracket [lo, hi] of st (k = (n_total^2-1)/2) ... */
 int dsvgd_bracket_init(dsvgd_select_state* st, int64_t n_total, const dsvgd_select_state* lo_st,
                        const dsvgd_select_state* hi_st, int64_t cand_cap, void* stream);
+/* ... the same three steps (sample_sqdist into `sample`, both sample
+ * selects, bracket_init of st) in seven launches: the two selects share each
+ * sweep over the sample and one launch picks both digits.  lo_st / hi_st:
+ * histograms zero on entry (as dsvgd_select_init or a previous call leave
+ * them); they end as after the three passes.  s % 4 == 0, 16-byte aligned
+ * sample, 0 <= k_lo <= k_hi < s. */
+int dsvgd_sample_bracket(const float* Y, int64_t ldy, int64_t n, int64_t d, int64_t s,
+                         uint64_t seed, int64_t k_lo, int64_t k_hi, float* sample,
+                         dsvgd_select_state* lo_st, dsvgd_select_state* hi_st,
+                         dsvgd_select_state* st, int64_t n_total, int64_t cand_cap,
+                         void* stream);
 /* ... then, after dsvgd_sqdist(BRACKET): bracket_totals sums the slots into
  * below_total / ncand_total / overflow (a distributed caller all-reduces
  * those three int64), and bracket_check decides exactly: below <= k <
@@ -355,6 +366,16 @@ int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const 
 int dsvgd_score_logreg_engine(const float* X, int64_t ldx, int64_t n, int64_t d, const float* Xd,
                               int64_t ldxd, const float* t, int64_t N, float scale, float* S,
                               int64_t lds, void* workspace, int engine, void* stream);
+/* ... as two calls, for a data set scored at many particle sets (every SVGD
+ * step): logreg_prepare writes the data-only part of the workspace (padded
+ * Xd and t, Xd's FmtH2 scales and split images) once; score_logreg_prepared
+ * then reads it every step (same n, N, d, engine and workspace).  Not for
+ * the n <= 32 one-block path (EINVAL there: use dsvgd_score_logreg_engine). */
+int dsvgd_logreg_prepare(const float* Xd, int64_t ldxd, const float* t, int64_t N, int64_t n,
+                         int64_t d, void* workspace, int engine, void* stream);
+int dsvgd_score_logreg_prepared(const float* X, int64_t ldx, int64_t n, int64_t d, int64_t N,
+                                float scale, float* S, int64_t lds, void* workspace, int engine,
+                                void* stream);
 
 /* Posterior-predictive probability of the logistic-regression test set:
  * prob[q] = (1/n) sum_j sigma(xt_q . w_j), w_j = X[j][1:d] (no bias; alpha

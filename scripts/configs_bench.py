@@ -3,7 +3,11 @@ at BASELINE.json's other configurations, with the achieved rate of each
 stage against its roofline (HBM GB/s for the distance / select / exp passes,
 MFMA TF/s for the contractions).
 
-    python scripts/configs_bench.py [--only B,C,E] [--steps 5]
+    python scripts/configs_bench.py [--only B,C,E] [--steps 5] [--order sequential]
+
+--order sequential times the reference's default Gauss-Seidel order (one
+phi_row launch + one score refresh per particle, host-driven) instead of the
+Jacobi fast path; only the whole-step time is reported then.
 
   B  experiments/gmm.py target, n = 1024, d = 1          (direct VALU kernels)
   C  Gaussian N(mu, diag(1/lam)), n = 16384, d = 64       (MFMA, short K)
@@ -49,15 +53,15 @@ def config(name):
     return 65536, 1024, T.LogisticRegression(x, t), 0.1, 8192
 
 
-def run(name, steps):
+def run(name, steps, order="jacobi"):
     import dsvgd
     from dsvgd.engine import StageTimer
     n, d, tgt, scale, N = config(name)
     g = torch.Generator(device="cpu").manual_seed(0)
     X = (scale * torch.randn(n, d, generator=g)).cuda()
     ds = dsvgd.DistSampler(0, 1, tgt, dsvgd.RBF("median"), X, N, N, exchange_particles=False,
-                           exchange_scores=False, include_wasserstein=False, order="jacobi")
-    for _ in range(2):
+                           exchange_scores=False, include_wasserstein=False, order=order)
+    for _ in range(2 if order == "jacobi" else 1):
         ds.make_step(1e-4)
     torch.cuda.synchronize()
     timer = StageTimer()
@@ -70,6 +74,9 @@ def run(name, steps):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps
     st = {k: float(np.mean(v)) for k, v in timer.summary().items()}
+    if order != "jacobi":
+        return {"n": n, "d": d, "order": order, "ms_per_step": ms,
+                "particle_updates_per_s": n / ms * 1e3, "stages_ms": st}
     # the same steps as replays of the captured HIP graph (no per-stage events)
     ds.timer = None
     e0.record()
@@ -110,10 +117,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="B,C,D,E")
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--order", default="jacobi", choices=["jacobi", "sequential"])
     args = ap.parse_args()
     res = {}
     for c in args.only.split(","):
-        res[c] = run(c, args.steps)
+        res[c] = run(c, args.steps, args.order)
         print(json.dumps({c: res[c]}), flush=True)
         torch.cuda.empty_cache()
 

@@ -139,6 +139,36 @@ def test_sample_sqdist_pairs(d, ldy):
     assert np.abs(got - ref).max() <= 1e-5 * ref.max()
 
 
+@pytest.mark.parametrize("d,s,klo,khi", [(256, 1 << 18, 127000, 135143), (61, 4100, 0, 4099),
+                                          (8, 4096, 2047, 2047), (3, 1 << 16, 5, 60000)])
+def test_sample_bracket_fused(d, s, klo, khi):
+    """dsvgd_sample_bracket (7 launches, shared sweeps, both digits per pick)
+    = sample_sqdist + two 3-pass selects + bracket_init: the same sample bits,
+    lo / hi = the exact k_lo-th / k_hi-th order statistics, st armed with them."""
+    from dsvgd import _native as N
+    from dsvgd.engine import SelectState
+    n, ldy, seed = 5000, ((d + 3) // 4) * 4, 0x5EED5EED
+    rs = np.random.RandomState(d + s)
+    Y = gpu(rs.randn(n, ldy).astype(np.float32))
+    ref = torch.empty(s, dtype=torch.float32, device=DEV)
+    out = torch.full((s,), np.nan, dtype=torch.float32, device=DEV)
+    lo, hi, st = SelectState(DEV), SelectState(DEV), SelectState(DEV)
+    strm = N.stream(DEV)
+    N.call("dsvgd_sample_sqdist", N.ptr(Y), ldy, n, d, s, seed, N.ptr(ref), strm)
+    for rep in range(2):                       # the call re-arms itself
+        N.call("dsvgd_sample_bracket", N.ptr(Y), ldy, n, d, s, seed, klo, khi, N.ptr(out),
+               lo.ptr, hi.ptr, st.ptr, 12345, 1 << 20, strm)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+        srt = np.sort(ref.cpu().numpy())
+        for state, k in ((lo, klo), (hi, khi)):
+            med = state.read()[0]
+            assert np.float32(med).view(np.uint32) == srt[k].view(np.uint32), (rep, k)
+            assert int(state.hist.abs().sum()) == 0
+        blo, bhi, below, ncand, fb = st.bracket()
+        assert (blo, bhi, below, ncand, fb) == (float(srt[klo]), float(srt[khi]), 0, 0, 0)
+
+
 @pytest.mark.parametrize("n,d,force_miss", [(4200, 100, False), (4200, 8, False),
                                              (4200, 100, True)])
 def test_bracketed_median_bit_exact(n, d, force_miss):
