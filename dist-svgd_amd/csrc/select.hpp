@@ -144,8 +144,72 @@ struct SlotWriter {
       cnt += (uint32_t)__popcll(bal);
     }
   }
+  __device__ __forceinline__ void flush() {}
   __device__ __forceinline__ void finish(const SlotLayout& L, int64_t slot, bool weight2) {
     const uint32_t b = below;
+    if ((threadIdx.x & 63) == 0) {
+      const uint32_t flag = weight2 ? DSVGD_SLOT_WEIGHT2 : 0u;
+      L.cnt[slot] = (cnt < DSVGD_SLOT_WEIGHT2 ? cnt : DSVGD_SLOT_WEIGHT2 - 1u) | flag;
+      L.below[slot] = b;
+    }
+  }
+};
+
+// LDS-staged form of SlotWriter (the 256-tile Gram's epilogue): no branch
+// and no wave-wide ballot per value.  add() writes every value to the lane's
+// private list in LDS (entry k of lane l at stage[64 k + l]: distinct banks
+// whatever the lanes' positions) and advances the lane's position only for
+// values in [lo, hi]; an out-of-range value is overwritten by the next one.
+// flush() -- after at most kStageDepth add()s -- moves the lists to the slot
+// in lane order (one wave prefix sum of the positions).  Below-counts are
+// per lane, summed at finish().  Per value: a subtract, a shift-add, a
+// compare, an LDS store and a conditional add (the ballot form compiled to
+// ~25 instructions with exec-mask branches per value).
+constexpr int kStageDepth = 16;
+struct SlotWriterLds {
+  float* dst = nullptr;
+  float* stage = nullptr;  // this wave's 64 x kStageDepth floats
+  uint32_t cnt = 0;        // wave-uniform: entries in [lo, hi] flushed so far
+  uint32_t cap = 0;
+  uint32_t below = 0;      // per lane
+  uint32_t pos = 0;        // per lane: staged entries
+  uint32_t klo = 1u, kspan = 0u;
+  __device__ __forceinline__ void begin(const dsvgd_select_state* st, const SlotLayout& L,
+                                        int64_t slot, float* wave_stage) {
+    const float lo = st->lo, hi = st->hi;
+    const bool ok = hi >= lo && lo >= 0.f;  // as SlotWriter::begin
+    klo = ok ? __float_as_uint(lo) : 0x7FFFFFFFu;
+    kspan = ok ? __float_as_uint(hi) - klo : 0u;
+    dst = L.data + slot * L.cap;
+    cap = (uint32_t)L.cap;
+    stage = wave_stage + (threadIdx.x & 63);
+  }
+  __device__ __forceinline__ void add(float v) {
+    const uint32_t d = __float_as_uint(v) - klo;
+    below += d >> 31;
+    stage[pos * 64] = v;
+    pos += d <= kspan ? 1u : 0u;
+  }
+  __device__ __forceinline__ void flush() {
+    if (__ballot(pos != 0u) == 0ull) return;
+    uint32_t total;
+    const uint32_t pre = wave_excl_scan(pos, total);
+    for (uint32_t k = 0;; ++k) {
+      const bool act = k < pos;
+      if (__ballot(act) == 0ull) break;
+      if (act) {
+        const uint32_t p = cnt + pre + k;
+        if (p < cap) dst[p] = stage[k * 64];
+      }
+    }
+    cnt += total;
+    pos = 0u;
+  }
+  __device__ __forceinline__ void finish(const SlotLayout& L, int64_t slot, bool weight2) {
+    flush();
+    uint32_t b = below;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o, 64);
     if ((threadIdx.x & 63) == 0) {
       const uint32_t flag = weight2 ? DSVGD_SLOT_WEIGHT2 : 0u;
       L.cnt[slot] = (cnt < DSVGD_SLOT_WEIGHT2 ? cnt : DSVGD_SLOT_WEIGHT2 - 1u) | flag;

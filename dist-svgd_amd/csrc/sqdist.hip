@@ -10,6 +10,7 @@
 //   the MFMA path is as or more accurate than the pairwise one.
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "gemm_tiles.hpp"
 #include "gemm_x3.hpp"
@@ -31,6 +32,19 @@ constexpr int kSqEpi = DSVGD_SQ_EPI;
 #define DSVGD_GRAM_H2_FORM 0
 #endif
 constexpr int kGramH2Form = DSVGD_GRAM_H2_FORM;
+// DSVGD_GRAM_STAGGER (A/B, half-tile form): shader-clock cycles the second
+// block of each CU waits before its first unit, so the two blocks' epilogues
+// fall between the other's MFMA phases instead of together
+#ifndef DSVGD_GRAM_STAGGER
+#define DSVGD_GRAM_STAGGER 0
+#endif
+constexpr long long kGramStagger = DSVGD_GRAM_STAGGER;
+// DSVGD_GRAM_DMA_PROBE (A/B, timing only, wrong D): every tile DMAs the
+// operands of tile (0, 0), so the ring streams from L2 alone
+#ifndef DSVGD_GRAM_DMA_PROBE
+#define DSVGD_GRAM_DMA_PROBE 0
+#endif
+constexpr int kGramDmaProbe = DSVGD_GRAM_DMA_PROBE;
 
 using GramTile = NTTile<2, 2, 2, 2>;  // 128 x 128 block, 4 waves of 64 x 64
 
@@ -41,12 +55,13 @@ using GramTile = NTTile<2, 2, 2, 2>;  // 128 x 128 block, 4 waves of 64 x 64
 // tiles).  The wave holds rows [rbase, rbase + 64) x columns [cbase, cbase +
 // 32 NI) of the tile in acc[mi][ni] (mi < 2, ni < NI); srow / scol: the
 // tile's 128 row / column norms.
-template <bool SYM, int smode, bool ZERO = false, class Tile = GramTile, int NI = 2>
+template <bool SYM, int smode, bool ZERO = false, class Tile = GramTile, int NI = 2,
+          class SW = SlotWriter>
 __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t row0,
                                             int64_t m, int64_t n, int64_t n_pad,
                                             float* __restrict__ D, const float* srow,
                                             const float* scol, int rbase, int cbase,
-                                            WindowHist& wh, uint32_t* shist, SlotWriter& sw,
+                                            WindowHist& wh, uint32_t* shist, SW& sw,
                                             const SlotLayout& sl, int64_t slot, int epi,
                                             bool mirror_store = true, int r0t = 0,
                                             float c2 = 2.f) {
@@ -97,9 +112,9 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        if (epi < 2 || v[r] != v[r])  // streamed out: nt, so D does not evict the Gram operands from L2
+        if (kSqEpi < 2 || v[r] != v[r])  // streamed out: nt, so D does not evict the Gram operands from L2
           __builtin_nontemporal_store(v[r], dp0 + (r & 3) * 16 + (r >> 2) * 128);
-      if (mirror && mirror_store && (epi == 0 || v[0] != v[0])) {  // D[j][i]: 4 consecutive i per register quad -> 16-byte stores
+      if (mirror && mirror_store && (kSqEpi == 0 || v[0] != v[0])) {  // D[j][i]: 4 consecutive i per register quad -> 16-byte stores
         float* const mp0 = Dmir + (int64_t)cl * 16 + ((rbase >> 4) + mi * 2) * kPanelElems + h4;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -112,6 +127,7 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
       } else if (smode == kSelBracket) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) sw.add(v[r]);
+        sw.flush();  // (LDS-staged writer: at most kStageDepth values between flushes)
       }
       if (ZERO) {
 #pragma unroll
@@ -171,8 +187,8 @@ __device__ __forceinline__ void sq_epilogue16(Tile& tile, int bi, int bj, int64_
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (epi < 2 || v[r] != v[r]) __builtin_nontemporal_store(v[r], dp0 + r * 16);
-      if (mirror && mirror_store && (epi == 0 || v[0] != v[0]))  // D[j][i], i = rb .. rb + 3
+        if (kSqEpi < 2 || v[r] != v[r]) __builtin_nontemporal_store(v[r], dp0 + r * 16);
+      if (mirror && mirror_store && (kSqEpi == 0 || v[0] != v[0]))  // D[j][i], i = rb .. rb + 3
         *reinterpret_cast<f32x4*>(Dmir + ((rbase >> 4) + mt) * kPanelElems + (int64_t)cl * 16 +
                                   g4) = f32x4{v[0], v[1], v[2], v[3]};
       if (smode == kSelHist) {
@@ -281,7 +297,7 @@ __global__ __launch_bounds__(256, 2) void sqdist_persistent_kernel(
     WindowHist wh;
     SlotWriter sw;
     if (smode == kSelBracket) sw.begin(st, sl, slot);
-    if (epi == 3) {  // timing only: no epilogue at all
+    if (kSqEpi == 3) {  // timing only: no epilogue at all
       tile.zero();
     } else {
       sq_epilogue<SYM, smode, true>(tile, bi, bj, row0, m, n, n_pad, D, snorm[par],
@@ -333,6 +349,9 @@ __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
   __shared__ __attribute__((aligned(16))) char smem[GramX3WTile::kSmemBytes];
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
   __shared__ float snorm[256 + kBN];  // the unit's 256 row norms, then its column norms
+  // bracket candidates staged per lane (SlotWriterLds) on the 32x32 form
+  constexpr bool kLdsSlots = smode == kSelBracket && !M16;
+  __shared__ float scand[kLdsSlots ? (kT / 64) * 64 * kStageDepth : 1];
 
   // this launch: Tm2 x Tc2 256-tiles, global column tiles from bj_off
   // (SYM: the triangle of a Tm2 x Tm2 square; r0t = its row0 / 128)
@@ -367,6 +386,7 @@ __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
   };
   GramX3WTile tile;
   auto issue = [&](char* stg, int BI, int BJ, int ks) {
+    if constexpr (kGramDmaProbe != 0) BI = BJ = 0;
     const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(Yg + (row0 + (int64_t)BI * 256) * 16), (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
@@ -385,9 +405,13 @@ __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
     const int bi = 2 * BI + (wr >> 1), bj = BJ * (kBN / 128) + wc;
     const int64_t slot = slot_base + L * (8 / kUnits) + w;
     WindowHist wh;
-    SlotWriter sw;
-    if (smode == kSelBracket) sw.begin(st, sl, slot);
-    if (epi == 3 || bi >= Tm || bj >= Tn || (SYM && bi + r0t > bj)) {
+    using SW = std::conditional_t<kLdsSlots, SlotWriterLds, SlotWriter>;
+    SW sw;
+    if constexpr (kLdsSlots)
+      sw.begin(st, sl, slot, scand + w * 64 * kStageDepth);
+    else if (smode == kSelBracket)
+      sw.begin(st, sl, slot);
+    if (kSqEpi == 3 || bi >= Tm || bj >= Tn || (SYM && bi + r0t > bj)) {
       tile.zero();
       if (smode == kSelBracket) sw.finish(sl, slot, false);
     } else {
@@ -396,7 +420,7 @@ __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
                                   snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl,
                                   slot, epi, layout == 0, r0t);
       else
-        sq_epilogue<SYM, smode, true, GramX3WTile, 4>(
+        sq_epilogue<SYM, smode, true, GramX3WTile, 4, SW>(
             tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128,
             snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl, slot, epi, layout == 0,
             r0t, c2);
@@ -404,6 +428,12 @@ __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
     if (smode == kSelHist) wh.flush(shist);
   };
 
+  if constexpr (WN == 1 && kGramStagger > 0) {
+    if (blockIdx.x >= gridDim.x / 2) {  // the CUs' second blocks (dispatched after one per CU)
+      const long long t0 = __builtin_amdgcn_s_memtime();
+      while (__builtin_amdgcn_s_memtime() - t0 < kGramStagger) __builtin_amdgcn_s_sleep(8);
+    }
+  }
   int BI = 0, BJ = 0;
   int64_t L = next_valid((int64_t)__builtin_amdgcn_readfirstlane((int)(lo + u)), BI, BJ);
   tile.zero();

@@ -65,6 +65,9 @@ SIGNATURES = {
     "dsvgd_phi_direct": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _f, _f, _p,
                                 _i64, _p, _i64, _p, _i64, _p, _i64, _p]),
     "dsvgd_phi_row": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _f, _p, _p, _p]),
+    "dsvgd_phi_row_blocks": (_i64, [_i64, _i64]),
+    "dsvgd_phi_row_split": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _f, _p, _p, _p, _i64,
+                                   _p]),
     "dsvgd_w2_cost": (_int, [_p, _i64, _i64, _p, _i64, _i64, _i64, _p, _i64, _p]),
     "dsvgd_w2_workspace_bytes": (_c.c_size_t, [_i64, _i64]),
     "dsvgd_w2_assign": (_int, [_p, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p]),

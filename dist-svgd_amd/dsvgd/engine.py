@@ -490,6 +490,9 @@ class StepGraph(object):
         self.graph.replay()
 
 
+_ROW_PARTIALS = {}   # (device, blocks, d) -> partial sums of dsvgd_phi_row_split (kept: graphs)
+
+
 def sequential_sweep(X, S, rows, h_state, step, target=None, score_scale=1.0, phi_out=None,
                      extra=None):
     """Gauss-Seidel sweep in the reference order over `rows` of the interacting
@@ -502,9 +505,23 @@ def sequential_sweep(X, S, rows, h_state, step, target=None, score_scale=1.0, ph
     s = N.stream(X.device)
     if extra is not None:
         assert extra.is_contiguous() and extra.shape == (len(rows), d)
+    blocks = int(N.load().dsvgd_phi_row_blocks(n, d))
+    part = None
+    if blocks > 1:
+        # the j range of each row over `blocks` workgroups (csrc/phi.hip)
+        key = (X.device, blocks, d)
+        part = _ROW_PARTIALS.get(key)
+        if part is None:
+            part = _ROW_PARTIALS[key] = torch.empty(blocks * d, dtype=torch.float32,
+                                                    device=X.device)
     for k, i in enumerate(rows):
-        N.call("dsvgd_phi_row", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), n, d, int(i),
-               h_state.ptr, float(step), N.ptr(extra[k]) if extra is not None else None,
-               N.ptr(phi_out[k]) if phi_out is not None else None, s)
+        ex = N.ptr(extra[k]) if extra is not None else None
+        po = N.ptr(phi_out[k]) if phi_out is not None else None
+        if part is None:
+            N.call("dsvgd_phi_row", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), n, d, int(i),
+                   h_state.ptr, float(step), ex, po, s)
+        else:
+            N.call("dsvgd_phi_row_split", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), n, d, int(i),
+                   h_state.ptr, float(step), ex, po, N.ptr(part), blocks, s)
         if target is not None:
             target.score(X[i:i + 1], S[i:i + 1], score_scale)

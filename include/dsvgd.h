@@ -312,6 +312,13 @@ int dsvgd_phi_direct(const float* D, int64_t ldd, const float* Y, int64_t ldy, i
 int dsvgd_phi_row(float* X, int64_t ldx, const float* S, int64_t lds, int64_t n_int, int64_t d,
                   int64_t i, const dsvgd_select_state* st, float step, const float* extra,
                   float* phi_out, void* stream);
+/* The same row update with the j range split over `blocks` workgroups (two
+ * launches; partial: blocks x d floats of scratch), for large n_int.
+ * dsvgd_phi_row_blocks(n, d) = the split to use (1: call dsvgd_phi_row). */
+int64_t dsvgd_phi_row_blocks(int64_t n, int64_t d);
+int dsvgd_phi_row_split(float* X, int64_t ldx, const float* S, int64_t lds, int64_t n, int64_t d,
+                        int64_t i, const dsvgd_select_state* st, float step, const float* extra,
+                        float* phi_out, float* partial, int64_t blocks, void* stream);
 
 /* ---- W2 / JKO term (dsvgd/distsampler.py:103-129, used at :190-198) ---- */
 /* The reference LP  min <P,C>, P >= 0, row sums 1/m, column sums 1/n  over

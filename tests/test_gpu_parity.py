@@ -362,6 +362,42 @@ def test_callable_target_matches_builtin():
     assert torch.allclose(a, b, atol=1e-6)
 
 
+@pytest.mark.parametrize("n,d,ldx", [(6000, 64, 64), (4096, 3, 3), (2048, 70, 72), (9000, 256, 256)])
+def test_phi_row_split_matches_oracle(n, d, ldx):
+    """Gauss-Seidel rows at large n (dsvgd_phi_row_split: the j range over
+    dsvgd_phi_row_blocks workgroups): 24 consecutive row updates against the
+    fp64 sequential restatement, and against the one-workgroup row kernel."""
+    from dsvgd import _native as N
+    from dsvgd.engine import SelectState, sequential_sweep
+    lib = N.load()
+    assert lib.dsvgd_phi_row_blocks(n, d) > 1
+    rs = np.random.RandomState(n + d)
+    X0 = (0.5 * rs.randn(n, d)).astype(np.float32)
+    S = rs.randn(n, d).astype(np.float32)
+    h, step, rows = 0.8 * d, 0.05, list(range(100, 124))
+    st = SelectState(DEV)
+    N.call("dsvgd_set_bandwidth", st.ptr, h, N.stream(DEV))
+    buf = torch.zeros(n, ldx, dtype=torch.float32, device=DEV)
+    Xg = buf[:, :d]
+    Xg.copy_(gpu(X0))
+    Sg = gpu(S)
+    sequential_sweep(Xg, Sg, rows, st, step)
+    got = Xg.cpu().numpy().astype(np.float64)
+    ref = X0.astype(np.float64)
+    for i in rows:
+        ref[i] += step * O.phi(ref, S, h, rows=[i])[0]
+    moved = np.abs(ref[rows] - X0[rows]).max()
+    assert rel_err(got[rows] - X0[rows], ref[rows] - X0[rows]) < PHI_TOL * 10, moved
+    assert np.array_equal(got[:100], X0[:100]) and np.array_equal(got[124:], X0[124:])
+    # the one-workgroup kernel on the same rows
+    X1 = gpu(X0)
+    for i in rows:
+        N.call("dsvgd_phi_row", N.ptr(X1), d, N.ptr(Sg), d, n, d, i, st.ptr, step, None, None,
+               N.stream(DEV))
+    one = X1.cpu().numpy().astype(np.float64)
+    assert np.abs(one[rows] - got[rows]).max() <= 1e-5 * np.abs(got[rows]).max()
+
+
 # --------------------------------------------------------- samplers ----
 @pytest.mark.parametrize("name", ["g2_sample_gauss_n32_d2", "g2_sample_gmm_n50"])
 def test_sampler_sequential_matches_reference(golden, name):
