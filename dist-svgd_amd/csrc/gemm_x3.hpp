@@ -170,11 +170,16 @@ __device__ __forceinline__ int x3_off(int x, int h) { return x * 32 + ((h ^ ((x 
 // NB (DMA path): ring stages.  2: iteration k DMAs tile k+1's B image (one
 // iteration to land); 3: tile k+2's B and D (two iterations; the closing
 // barrier then waits for no DMA at all).
+// DA (NB = 3, RW = 2): how far ahead the D panels are DMA'd.  2: with the B
+// image; 3: one K-step earlier than B, from a 4-slot raw ring -- D streams
+// from HBM once (nt) and lands later than the L2-resident B slices.
 template <int TN, bool DMA = true, bool EXP = true, bool M16 = false, int RW = 2, class F = FmtX3,
-          int NB = 2>
+          int NB = 2, int DA = 2>
 struct NNX3Tile {
   static constexpr int P = F::P;
   static_assert(NB == 2 || (NB == 3 && DMA), "3-stage ring: DMA path");
+  static_assert(DA == 2 || (DA == 3 && NB == 3 && RW == 2), "D three ahead: 3-stage ring, RW 2");
+  static constexpr int ND = DA == 3 ? 4 : NB;  // raw D slots
   using V8 = typename F::V8;
   static_assert(!M16 || P == 3, "the 16x16x32 concatenated-k form is the 3-part format's");
   // (DMA needs the same DMA count in every wave: whole 512-chunk rounds)
@@ -189,7 +194,7 @@ struct NNX3Tile {
   static constexpr int SA = P * BM * 32;  // bytes of one stage's A image
   static constexpr int SB = P * BC * 32;
   static constexpr int kStage = SA + SB;
-  static constexpr int kSmemBytes = NB * kStage + (DMA ? NB * AR * kPanelElems * 4 : 0);
+  static constexpr int kSmemBytes = NB * kStage + (DMA ? ND * AR * kPanelElems * 4 : 0);
   static constexpr int kBChunks = SB / 16;
   static constexpr int LB = (kBChunks + kThreads - 1) / kThreads;
   static constexpr int kHalf = TN > 1 ? TN / 2 : 1;  // column tiles before the mid-step write
@@ -459,7 +464,31 @@ struct NNX3Tile {
       const __amdgpu_buffer_rsrc_t rB =
           __builtin_amdgcn_make_buffer_rsrc((void*)Yx, (short)0, 0x7fffffff, 0x00020000);
       char* raw = smem + kRaw;
-      if constexpr (NB == 3) {
+      if constexpr (DA == 3) {
+        // prologue in steady-state issue order: B(0) D(0) | D(1) | B(1) D(2)
+        // (iteration k issues B(k+2) then D(k+3))
+        const bool m1 = k0 + BJ < k1, m2 = k0 + 2 * BJ < k1;
+        dma_b(smem, rB, ldy, k0);
+        dma_d(raw, rA, k0);
+        if (m1) dma_d(raw + kSlot, rA, k0 + BJ);
+        if (m1) dma_b(smem + kStage, rB, ldy, k0 + BJ);
+        if (m2) dma_d(raw + 2 * kSlot, rA, k0 + 2 * BJ);
+        if (m2)  // D(0) landed: D(1), B(1), D(2) may stay in flight
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB + 2 * AR) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ra = raw_read(raw, k0, 0);
+        store_a(smem, scale, row_g0 - k0, 0);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        int k = 0;
+        for (int64_t j0 = k0; j0 < k1; j0 += 3 * BJ, k += 3) {
+          step_dma3d<0>(rA, rB, ldy, j0, k1, scale, smem, row_g0, wr, wc, k);
+          if (j0 + BJ < k1) step_dma3d<1>(rA, rB, ldy, j0 + BJ, k1, scale, smem, row_g0, wr, wc, k + 1);
+          if (j0 + 2 * BJ < k1)
+            step_dma3d<2>(rA, rB, ldy, j0 + 2 * BJ, k1, scale, smem, row_g0, wr, wc, k + 2);
+        }
+        return;
+      } else if constexpr (NB == 3) {
         dma_b(smem, rB, ldy, k0);
         dma_d(raw, rA, k0);
         if (k0 + BJ < k1) {
@@ -591,6 +620,39 @@ struct NNX3Tile {
     }
     compute<kHalf, TN>(cur, wc);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+
+  // DA = 3, iteration k (tile j0, B stage CUR = k % 3, raw slot k % 4): DMA
+  // tile k+2's B into stage (k+2) % 3 and tile k+3's D into raw slot
+  // (k+3) % 4; halfway, tile k+1's D (issued at k-2: the DMAs of iterations
+  // k-1 and k may stay in flight) becomes its A in stage (k+1) % 3; before
+  // the barrier, tile k+1's B (issued at k-1, before D(k+2)) has landed.
+  // Near the end of the range (fewer DMAs issued) the waits drain fully.
+  template <int CUR>
+  __device__ __forceinline__ void step_dma3d(__amdgpu_buffer_rsrc_t rA, __amdgpu_buffer_rsrc_t rB,
+                                             int64_t ldy, int64_t j0, int64_t k1, float scale,
+                                             char* smem, int64_t row_g0, int wr, int wc, int k) {
+    constexpr int NXT = (CUR + 1) % 3, NN = (CUR + 2) % 3;
+    const char* cur = smem + CUR * kStage;
+    char* raw = smem + kRaw;
+    const bool more = j0 + BJ < k1, more2 = j0 + 2 * BJ < k1, more3 = j0 + 3 * BJ < k1;
+    if (more2) dma_b(smem + NN * kStage, rB, ldy, j0 + 2 * BJ);
+    if (more3) dma_d(raw + ((k + 3) & 3) * kSlot, rA, j0 + 3 * BJ);
+    read_a(cur, wr);
+    compute<0, kHalf>(cur, wc);
+    if (more) {
+      if (more3)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (LB + AR)) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ra = raw_read(raw + ((k + 1) & 3) * kSlot, j0 + BJ, 0);
+      store_a(smem + NXT * kStage, scale, row_g0 - (j0 + BJ), 0);
+    }
+    compute<kHalf, TN>(cur, wc);
+    if (more3)
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(LB + 2 * AR) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
 
   // full row sum of row threadIdx.x >> 2 (4 consecutive lanes stage a row)

@@ -47,6 +47,19 @@ struct LogregWs {
       off_zs, total;
 };
 
+// G . Xd (K = N data rows, 256-row blocks): split K so that a launch has
+// about two blocks per CU (n = 65536 gives only 256 row blocks), each slice
+// at least 1024 rows deep; logreg_finish adds the slices in order.
+#ifndef DSVGD_GXD_SPLITS
+#define DSVGD_GXD_SPLITS 1  // shipped: no split (measured slower at S = 8); A/B builds: 2, 4
+#endif
+constexpr int kGxdMaxSplits = DSVGD_GXD_SPLITS;
+static int gxd_splits(int64_t n_pad, int64_t N_pad) {
+  int sp = 1;
+  while (sp < kGxdMaxSplits && (n_pad / 256) * sp < 512 && N_pad / (2 * sp) >= 1024) sp *= 2;
+  return sp;
+}
+
 static LogregWs logreg_ws(int64_t n, int64_t N, int64_t p) {
   LogregWs w;
   w.N = N;
@@ -64,7 +77,7 @@ static LogregWs logreg_ws(int64_t n, int64_t N, int64_t p) {
   w.off_xd = take((size_t)w.N_pad * w.ldb);
   w.off_t = take((size_t)w.N_pad);
   w.off_g = take((size_t)w.n_pad * w.N_pad);
-  w.off_gw = take((size_t)w.n_pad * w.ldb);
+  w.off_gw = take((size_t)kGxdMaxSplits * w.n_pad * w.ldb);  // split-K slices of G . Xd
   // split images (bf16 x 3 = 6 B per element, counted in floats)
   w.off_wx = take((size_t)w.n_pad * w.pp * 3 / 2);
   w.off_xdx = take((size_t)w.N_pad * w.pp * 3 / 2);
@@ -240,7 +253,8 @@ __global__ __launch_bounds__(256) void logreg_finish_kernel(const float* __restr
                                                             int64_t ldx, int64_t n, int64_t p,
                                                             const float* __restrict__ GW,
                                                             int64_t ldg, float scale,
-                                                            float* __restrict__ S, int64_t lds) {
+                                                            float* __restrict__ S, int64_t lds,
+                                                            int splits = 1) {
   const int lane = threadIdx.x & 63;
   const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (j >= n) return;
@@ -249,7 +263,11 @@ __global__ __launch_bounds__(256) void logreg_finish_kernel(const float* __restr
   float w2 = 0.f;
   for (int64_t c = lane; c < p; c += 64) w2 = fmaf(x[1 + c], x[1 + c], w2);
   w2 = warp_sum(w2);
-  for (int64_t c = lane; c < p; c += 64) S[j * lds + 1 + c] = scale * (GW[j * ldg + c] - a * x[1 + c]);
+  for (int64_t c = lane; c < p; c += 64) {
+    float g = GW[j * ldg + c];
+    for (int z = 1; z < splits; ++z) g += GW[(int64_t)z * n * ldg + j * ldg + c];  // slice order
+    S[j * lds + 1 + c] = scale * (g - a * x[1 + c]);
+  }
   if (lane == 0) S[j * lds] = scale * (-a + 0.5f * (float)p - 0.5f * a * w2);
 }
 
@@ -487,7 +505,7 @@ static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float 
   float* tp = (float*)(base + w.off_t);
   float* G = (float*)(base + w.off_g);
   float* GW = (float*)(base + w.off_gw);
-  int rc = 0;
+  int rc = 0, splits = 1;
   if (P.h2) {
     void* Wx = base + w.off_wx;
     _Float16* Xdy = (_Float16*)(base + w.off_xdy);
@@ -513,8 +531,9 @@ static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float 
                        (int)(w.pp / kX3Step), tp, w.N_pad, G, Tm2, Tn2,
                        tile_grid(Tm2, Tn2, false), (const float*)zs);
     if ((rc = check_launch("logreg_z_h2"))) return rc;
-    if ((rc = nn_h2_gemm(false, G, w.N_pad, Xdy, w.ldb, 1, nullptr, GW, w.ldb, nullptr, n, 0, s, 0,
-                         sxd + w.ldb)))
+    splits = gxd_splits(w.n_pad, w.N_pad);
+    if ((rc = nn_h2_gemm(false, G, w.N_pad, Xdy, w.ldb, splits, nullptr, GW, w.ldb, nullptr, n, 0, s,
+                         0, sxd + w.ldb)))
       return rc;
   } else if (P.x3) {
     void* Wx = base + w.off_wx;
@@ -546,7 +565,7 @@ static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float 
       return rc;
   }
   hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,
-                     w.ldb, scale, S, lds);
+                     w.ldb, scale, S, lds, splits);
   return check_launch("logreg_finish");
 }
 

@@ -15,7 +15,15 @@
 #include "gemm_tiles.hpp"
 #include "gemm_x3.hpp"
 
+// DSVGD_PHI_DA: how many K-steps ahead the FmtH2 NN tile DMAs its D panels
+// (gemm_x3.hpp NNX3Tile DA: 2 = with the B image, 3 = one step earlier)
+#ifndef DSVGD_PHI_DA
+#define DSVGD_PHI_DA 2
+#endif
+
 namespace dsvgd {
+
+constexpr int kPhiDA = DSVGD_PHI_DA;
 
 // blockIdx.z = split-K slice z: K columns [z*kchunk, min(K,(z+1)*kchunk)) into
 // the partial C + z*m*ldc (and rowsum + z*m_pad); phi_finish sums the slices
@@ -75,7 +83,7 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
 // F = FmtH2: C and rowsum come out of the MFMAs scaled by 2^15 (the A
 // staging scale) and C's column c by the B image's column scale: the stores
 // multiply by colinv[c] * 2^-15 (exact powers of two).
-template <int TN, bool DMA, bool EXP, bool M16, int RW = 2, class F = FmtX3, int NB = 2>
+template <int TN, bool DMA, bool EXP, bool M16, int RW = 2, class F = FmtX3, int NB = 2, int DA = 2>
 __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A, int64_t a_npad,
                                                     const typename F::E* __restrict__ Yx,
                                                     int64_t ldy, int64_t K, int64_t kchunk,
@@ -84,7 +92,7 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
                                                     float* __restrict__ rowsum, int64_t m,
                                                     int64_t row0, int sym,
                                                     const float* __restrict__ colinv) {
-  using Tile = NNX3Tile<TN, DMA, EXP, M16, RW, F, NB>;
+  using Tile = NNX3Tile<TN, DMA, EXP, M16, RW, F, NB, DA>;
   __shared__ __attribute__((aligned(16))) char smem[Tile::kSmemBytes];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
@@ -212,7 +220,8 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
       hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F>), grid, dim3(512), 0, s, D, K,
                          Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv);
   } else {  // FmtH2: the smaller stages fit a 3-stage ring
-    hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2>), grid,
+    hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2,
+                                     (TN != 1 && kPhiDA == 3) ? 3 : 2>), grid,
                        dim3(512), 0, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym,
                        colinv);
   }
@@ -406,6 +415,19 @@ __global__ __launch_bounds__(256) void phi_direct_finish_kernel(
   if (X) X[i * ldx + col] += step * p;
 }
 
+// red[g * dc + c] for g < G groups -> red[c] (c < dc): pairwise halving in
+// a fixed order (deterministic; a serial walk over 256 groups on one thread
+// cost ~8 us per chunk at d = 1).  Called by all 256 threads.
+__device__ __forceinline__ void group_reduce(float* red, int dc, int G) {
+  const int t = threadIdx.x;
+  while (G > 1) {
+    const int h = (G + 1) >> 1;
+    if (t < (G - h) * dc) red[t] += red[t + h * dc];
+    __syncthreads();
+    G = h;
+  }
+}
+
 // Gauss-Seidel row update (reference order, exact differences, no Gram):
 // one block; j in chunks of 256 (one per thread) -> k_j in LDS; then the
 // (column, j) sums are split over the block: for a column block of dc <= 256
@@ -461,11 +483,8 @@ __global__ __launch_bounds__(256) void phi_row_kernel(float* __restrict__ X, int
       }
       red[t] = part;
       __syncthreads();
-      if (t < dc) {
-        float a = acc[c0 + t];
-        for (int gi = 0; gi < G; ++gi) a += red[gi * dc + t];
-        acc[c0 + t] = a;
-      }
+      group_reduce(red, dc, G);
+      if (t < dc) acc[c0 + t] += red[t];
       __syncthreads();
     }
   }
@@ -552,11 +571,8 @@ __global__ __launch_bounds__(256) void phi_row_part_kernel(const float* __restri
     }
     red[t] = part;
     __syncthreads();
-    if (t < dc) {
-      float a = 0.f;
-      for (int gi = 0; gi < G; ++gi) a += red[gi * dc + t];
-      partial[(int64_t)blockIdx.x * d + c0 + t] = a;
-    }
+    group_reduce(red, dc, G);
+    if (t < dc) partial[(int64_t)blockIdx.x * d + c0 + t] = red[t];
     __syncthreads();
   }
 }
@@ -567,14 +583,31 @@ __global__ __launch_bounds__(256) void phi_row_finish_kernel(float* __restrict__
                                                              int64_t blocks, float step,
                                                              const float* __restrict__ extra,
                                                              float* __restrict__ phi_out) {
+  // columns in chunks of dc <= 256; G = 256 / dc thread groups take every
+  // G-th block's partial (loads in flight together, not one chained walk
+  // over all blocks), then the group sums are added in group order
+  __shared__ float red[256];
+  const int t = threadIdx.x;
   const float inv_n = 1.f / (float)n;
-  for (int64_t c = threadIdx.x; c < d; c += 256) {
+  for (int64_t c0 = 0; c0 < d; c0 += 256) {
+    const int dc = (int)min((int64_t)256, d - c0);
+    const int G = 256 / dc;
     float a = 0.f;
-    for (int64_t b = 0; b < blocks; ++b) a += partial[b * d + c];
-    float p = inv_n * a;
-    if (extra) p += extra[c];
-    if (phi_out) phi_out[c] = p;
-    X[i * ldx + c] += step * p;
+    if (t < dc * G) {
+      const int64_t c = c0 + t % dc;
+      for (int64_t b = t / dc; b < blocks; b += G) a += partial[b * d + c];
+    }
+    red[t] = a;
+    __syncthreads();
+    group_reduce(red, dc, G);
+    if (t < dc) {
+      const int64_t c = c0 + t;
+      float p = inv_n * red[t];
+      if (extra) p += extra[c];
+      if (phi_out) phi_out[c] = p;
+      X[i * ldx + c] += step * p;
+    }
+    __syncthreads();
   }
 }
 

@@ -15,3 +15,8 @@ for w in $WHAT; do
     bench) timeout -k 10 600 python bench.py > $OUT/bench.log 2>&1 || exit 1; tail -1 $OUT/bench.log | cut -c1-600 ;;
   esac
 done
+for w in $WHAT; do
+  case $w in
+    seq) timeout -k 10 600 python scripts/configs_bench.py --only ${SEQ:-B,C} --steps 1 --order sequential > $OUT/seq.log 2>&1 || exit 1; grep -v amdgpu.ids $OUT/seq.log ;;
+  esac
+done

@@ -21,8 +21,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shards", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--lib", default=None, help="an A/B build of the library (make ab)")
     args = ap.parse_args()
     import dsvgd
+    if args.lib:
+        dsvgd._native.LIB_PATH = os.path.abspath(args.lib)
     from dsvgd.engine import StageTimer
     from bench import synthetic_data
     n, d, Ng = 65536, 256, 16384
