@@ -254,6 +254,11 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
+        # what the contractions run on: fp32 operands split into 16-bit parts
+        # whose products the MFMA accumulates exactly in fp32
+        "mfma_operands": {"h2": "f16 x2 parts (3 products), fp32 accumulate",
+                          "x3": "bf16 x3 parts (6 products), fp32 accumulate",
+                          "f32": "f32"}[args.gemm],
         "data": "synthetic (logreg data N(0,1/p), labels from a random w + logistic noise; "
                 "particles 0.1*N(0,1))",
         "config": {"workload": "dist-logreg DistSampler all_scores, Jacobi, median bandwidth",

@@ -180,6 +180,10 @@ struct NNX3Tile {
   static_assert(NB == 2 || (NB == 3 && DMA), "3-stage ring: DMA path");
   static_assert(DA == 2 || (DA == 3 && NB == 3 && RW == 2), "D three ahead: 3-stage ring, RW 2");
   static constexpr int ND = DA == 3 ? 4 : NB;  // raw D slots
+#ifndef DSVGD_NN_PINGPONG
+#define DSVGD_NN_PINGPONG 0
+#endif
+  static constexpr bool kPingPong = DSVGD_NN_PINGPONG != 0;  // (step_dma3)
   using V8 = typename F::V8;
   static_assert(!M16 || P == 3, "the 16x16x32 concatenated-k form is the 3-part format's");
   // (DMA needs the same DMA count in every wave: whole 512-chunk rounds)
@@ -605,19 +609,27 @@ struct NNX3Tile {
       dma_b(smem + NN * kStage, rB, ldy, j0 + 2 * BJ);
       dma_d(raw + NN * kSlot, rA, j0 + 2 * BJ);
     }
-    read_a(cur, wr);
-    compute<0, kHalf>(cur, wc);
-    if (more) {
-      if (more2)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB + AR) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    auto stage_next = [&]() {
+      if (more) {
+        if (more2)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB + AR) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int a = 0; a < AR; ++a) {
-        ra = raw_read(raw + NXT * kSlot, j0 + BJ, a);
-        store_a(smem + NXT * kStage, scale, row_g0 - (j0 + BJ), a);
+        for (int a = 0; a < AR; ++a) {
+          ra = raw_read(raw + NXT * kSlot, j0 + BJ, a);
+          store_a(smem + NXT * kStage, scale, row_g0 - (j0 + BJ), a);
+        }
       }
-    }
+    };
+    // kPingPong: the second wave of each SIMD (waves 4..7) stages first and
+    // the first wave halfway, so one wave's VALU staging runs beside the
+    // other's MFMAs instead of both SIMD waves leaving the matrix pipe idle
+    const bool early = kPingPong && (threadIdx.x >> 6) >= 4;
+    read_a(cur, wr);
+    if (early) stage_next();
+    compute<0, kHalf>(cur, wc);
+    if (!early) stage_next();
     compute<kHalf, TN>(cur, wc);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
@@ -638,16 +650,21 @@ struct NNX3Tile {
     const bool more = j0 + BJ < k1, more2 = j0 + 2 * BJ < k1, more3 = j0 + 3 * BJ < k1;
     if (more2) dma_b(smem + NN * kStage, rB, ldy, j0 + 2 * BJ);
     if (more3) dma_d(raw + ((k + 3) & 3) * kSlot, rA, j0 + 3 * BJ);
+    auto stage_next = [&]() {
+      if (more) {
+        if (more3)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (LB + AR)) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ra = raw_read(raw + ((k + 1) & 3) * kSlot, j0 + BJ, 0);
+        store_a(smem + NXT * kStage, scale, row_g0 - (j0 + BJ), 0);
+      }
+    };
+    const bool early = kPingPong && (threadIdx.x >> 6) >= 4;  // (step_dma3)
     read_a(cur, wr);
+    if (early) stage_next();
     compute<0, kHalf>(cur, wc);
-    if (more) {
-      if (more3)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (LB + AR)) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      ra = raw_read(raw + ((k + 1) & 3) * kSlot, j0 + BJ, 0);
-      store_a(smem + NXT * kStage, scale, row_g0 - (j0 + BJ), 0);
-    }
+    if (!early) stage_next();
     compute<kHalf, TN>(cur, wc);
     if (more3)
       asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(LB + 2 * AR) : "memory");
@@ -675,7 +692,9 @@ struct NNX3Tile {
 // NS: ring stages (3: a DMA has two iterations to land; 2: one, at 2/3 of the LDS).
 // M16: v_mfma_f32_16x16x32_bf16 with concatenated k (NNX3Tile); the results
 // are in acc16[4][2 TN] (16x16 layout) and both images must be unswizzled.
-template <int TM, int TN, int WM, int WN, int NS = 3, bool M16 = false, class F = FmtX3>
+// KS: 16-deep image K-steps per ring stage (one barrier per stage): 2 halves
+// the barriers per tile at twice the stage size.
+template <int TM, int TN, int WM, int WN, int NS = 3, bool M16 = false, class F = FmtX3, int KS = 1>
 struct NTX3Tile {
   static constexpr int TM_ = TM, TN_ = TN, WM_ = WM, WN_ = WN;
   static constexpr bool M16_ = M16;
@@ -689,13 +708,15 @@ struct NTX3Tile {
   static constexpr int BK = kX3Step;
   static constexpr int SA = P * BM * 32;
   static constexpr int SB = P * BN * 32;
-  static constexpr int kStage = SA + SB;
+  static constexpr int kSub = SA + SB;          // one 16-deep image K-step
+  static constexpr int kStage = KS * kSub;
   static constexpr int kStages = NS;
   static_assert(NS == 2 || NS == 3, "2- or 3-stage ring");
+  static_assert(KS == 1 || (KS == 2 && !M16), "two sub-steps per stage: 32x32 form");
   static constexpr int kSmemBytes = kStages * kStage;
   static constexpr int LA = SA / 16 / kThreads;  // DMAs per thread per K-step (A)
   static constexpr int LBn = SB / 16 / kThreads;
-  static constexpr int kDmas = LA + LBn;
+  static constexpr int kDmas = KS * (LA + LBn);
   static_assert(SA % (16 * kThreads) == 0 && SB % (16 * kThreads) == 0, "whole DMA rounds");
   static_assert(BM * 32 % (16 * kThreads) == 0, "a DMA round stays inside one part");
   static_assert(kSmemBytes <= 160 * 1024, "LDS budget");
@@ -730,16 +751,21 @@ struct NTX3Tile {
   __device__ __forceinline__ void dma(char* st, __amdgpu_buffer_rsrc_t rA, int64_t mA,
                                       __amdgpu_buffer_rsrc_t rB, int64_t mB, int64_t kb) {
     const int t = threadIdx.x, wbase = t & ~63;
-    const int soA = (int)(kb * P * mA * 32), soB = (int)(kb * P * mB * 32);
 #pragma unroll
-    for (int u = 0; u < LA; ++u) {
-      const int f = t + u * kThreads, pp = f / (BM * 2), in = f % (BM * 2);
-      dma16(rA, st + (wbase + u * kThreads) * 16, (int)(pp * mA * 32 + in * 16), soA);
-    }
+    for (int q = 0; q < KS; ++q) {
+      const int64_t ki = kb * KS + q;  // image K-step
+      const int soA = (int)(ki * P * mA * 32), soB = (int)(ki * P * mB * 32);
+      char* sq = st + q * kSub;
 #pragma unroll
-    for (int u = 0; u < LBn; ++u) {
-      const int f = t + u * kThreads, pp = f / (BN * 2), in = f % (BN * 2);
-      dma16(rB, st + SA + (wbase + u * kThreads) * 16, (int)(pp * mB * 32 + in * 16), soB);
+      for (int u = 0; u < LA; ++u) {
+        const int f = t + u * kThreads, pp = f / (BM * 2), in = f % (BM * 2);
+        dma16(rA, sq + (wbase + u * kThreads) * 16, (int)(pp * mA * 32 + in * 16), soA);
+      }
+#pragma unroll
+      for (int u = 0; u < LBn; ++u) {
+        const int f = t + u * kThreads, pp = f / (BN * 2), in = f % (BN * 2);
+        dma16(rB, sq + SA + (wbase + u * kThreads) * 16, (int)(pp * mB * 32 + in * 16), soB);
+      }
     }
   }
 
@@ -774,27 +800,31 @@ struct NTX3Tile {
       return;
     }
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-    V8 a[TM][P];
 #pragma unroll
-    for (int mi = 0; mi < TM; ++mi) {
-      const int lr = wm * 32 * TM + mi * 32 + r;
-      const int off = lr * 32 + ((h ^ (((a0 + lr) >> 3) & 1)) << 4);
+    for (int q = 0; q < KS; ++q) {
+      const char* sq = st + q * kSub;
+      V8 a[TM][P];
 #pragma unroll
-      for (int p = 0; p < P; ++p) a[mi][p] = *reinterpret_cast<const V8*>(st + p * BM * 32 + off);
-    }
+      for (int mi = 0; mi < TM; ++mi) {
+        const int lr = wm * 32 * TM + mi * 32 + r;
+        const int off = lr * 32 + ((h ^ (((a0 + lr) >> 3) & 1)) << 4);
 #pragma unroll
-    for (int ni = 0; ni < TN; ++ni) {
-      V8 b[P];
+        for (int p = 0; p < P; ++p) a[mi][p] = *reinterpret_cast<const V8*>(sq + p * BM * 32 + off);
+      }
 #pragma unroll
-      for (int p = 0; p < P; ++p)
-        b[p] = *reinterpret_cast<const V8*>(st + SA + p * BN * 32 +
-                                            x3_off(wn * 32 * TN + ni * 32 + r, h));
-      f32x16 c[TM];
+      for (int ni = 0; ni < TN; ++ni) {
+        V8 b[P];
 #pragma unroll
-      for (int mi = 0; mi < TM; ++mi) c[mi] = acc[mi][ni];
-      mfma_products<F, TM>(a, b, c);
+        for (int p = 0; p < P; ++p)
+          b[p] = *reinterpret_cast<const V8*>(sq + SA + p * BN * 32 +
+                                              x3_off(wn * 32 * TN + ni * 32 + r, h));
+        f32x16 c[TM];
 #pragma unroll
-      for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = c[mi];
+        for (int mi = 0; mi < TM; ++mi) c[mi] = acc[mi][ni];
+        mfma_products<F, TM>(a, b, c);
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = c[mi];
+      }
     }
   }
 

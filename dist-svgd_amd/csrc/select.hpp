@@ -160,12 +160,12 @@ struct SlotWriter {
 // private list in LDS (entry k of lane l at stage[64 k + l]: distinct banks
 // whatever the lanes' positions) and advances the lane's position only for
 // values in [lo, hi]; an out-of-range value is overwritten by the next one.
-// flush() -- after at most kStageDepth add()s -- moves the lists to the slot
+// flush() -- after at most kStageDepth (8) add()s -- moves the lists to the slot
 // in lane order (one wave prefix sum of the positions).  Below-counts are
 // per lane, summed at finish().  Per value: a subtract, a shift-add, a
 // compare, an LDS store and a conditional add (the ballot form compiled to
 // ~25 instructions with exec-mask branches per value).
-constexpr int kStageDepth = 16;
+constexpr int kStageDepth = 8;
 struct SlotWriterLds {
   float* dst = nullptr;
   float* stage = nullptr;  // this wave's 64 x kStageDepth floats

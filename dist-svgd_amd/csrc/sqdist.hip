@@ -45,6 +45,13 @@ constexpr long long kGramStagger = DSVGD_GRAM_STAGGER;
 #define DSVGD_GRAM_DMA_PROBE 0
 #endif
 constexpr int kGramDmaProbe = DSVGD_GRAM_DMA_PROBE;
+// DSVGD_GRAM_KS (A/B): 16-deep image K-steps per ring stage of the FmtH2 Gram
+// (2, shipped: 32-deep stages, half the barriers, on a 2-stage ring; -5 %
+// vs 1 = 16-deep on a 3-stage ring, profiles/r4z_gram_ks2_ab.log)
+#ifndef DSVGD_GRAM_KS
+#define DSVGD_GRAM_KS 2
+#endif
+constexpr int kGramKS = DSVGD_GRAM_KS;
 
 using GramTile = NTTile<2, 2, 2, 2>;  // 128 x 128 block, 4 waves of 64 x 64
 
@@ -126,8 +133,10 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
         hist_account(wh, v, weight, shist);
       } else if (smode == kSelBracket) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sw.add(v[r]);
-        sw.flush();  // (LDS-staged writer: at most kStageDepth values between flushes)
+        for (int r = 0; r < 16; ++r) {
+          sw.add(v[r]);
+          if ((r + 1) % kStageDepth == 0) sw.flush();  // (LDS-staged writer's list depth)
+        }
       }
       if (ZERO) {
 #pragma unroll
@@ -335,14 +344,14 @@ __global__ __launch_bounds__(256, 2) void sqdist_persistent_kernel(
 // apart, so one block's epilogue (D stores, select accounting) runs beside
 // the other's MFMAs instead of every SIMD idling its MFMA pipe through it.
 // NS: LDS ring stages (2: a K-step's DMA has one K-step to land; 3: two).
-template <bool SYM, int smode, bool M16 = true, class F = FmtX3, int WN = 2, int NS = 2>
+template <bool SYM, int smode, bool M16 = true, class F = FmtX3, int WN = 2, int NS = 2, int KS = 1>
 __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
     const typename F::E* __restrict__ Yg, int64_t img_rows, const float* __restrict__ norms,
     int64_t row0, int64_t m, int64_t n, int64_t n_pad, int nk, float* __restrict__ D,
     dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int epi, int64_t total_tiles,
     int layout, int Tm2, int Tc2, int bj_off, int r0t, int64_t slot_base, int64_t ns_total,
     const float* __restrict__ tsc) {
-  using GramX3WTile = NTX3Tile<2, 4, 4, WN, NS, M16, F>;
+  using GramX3WTile = NTX3Tile<2, 4, 4, WN, NS, M16, F, KS>;
   constexpr int kT = GramX3WTile::kThreads, kUnits = 2 / WN;  // units per 256-tile
   constexpr int kBN = GramX3WTile::BN;                         // 256 or 128 columns
   const float c2 = F::P == 3 ? 2.f : 2.f * tsc[1] * tsc[1];
@@ -523,20 +532,21 @@ int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, 
   const int64_t img = gram_img_rows(n);
   const int epi = kSqEpi;
   const bool sym = m == n && row0 == 0;
-  const int nk = (int)(dp / kX3Step);
+  constexpr int KS = (F::P == 2 && kGramH2Form != 1) ? kGramKS : 1;
+  const int nk = (int)(dp / kX3Step / KS);  // ring stages per tile (dp is a multiple of 32)
   int rc = 0;
   {
     int bs = 0, bn = 0;
     // FmtH2: 3-stage ring (DSVGD_GRAM_H2_FORM 1: half-tile blocks, two per CU);
     // FmtX3: whole 256-tiles, 2-stage ring
     constexpr int WN = (F::P == 3 || kGramH2Form != 1) ? 2 : 1;
-    constexpr int NS = (F::P == 2 && WN == 2) ? 3 : 2;
+    constexpr int NS = (F::P == 2 && WN == 2 && KS == 1) ? 3 : 2;
     if ((rc = persistent_blocks(
-             reinterpret_cast<const void*>(&sqdist_x3w_kernel<true, SM, F::P == 3, F, WN, NS>), &bs,
+             reinterpret_cast<const void*>(&sqdist_x3w_kernel<true, SM, F::P == 3, F, WN, NS, KS>), &bs,
              256 * WN)))
       return rc;
     if ((rc = persistent_blocks(
-             reinterpret_cast<const void*>(&sqdist_x3w_kernel<false, SM, F::P == 3, F, WN, NS>), &bn,
+             reinterpret_cast<const void*>(&sqdist_x3w_kernel<false, SM, F::P == 3, F, WN, NS, KS>), &bn,
              256 * WN)))
       return rc;
     const int Tn2 = (int)((n_pad / 128 + 1) / 2), Tm2 = (int)((m_pad / 128 + 1) / 2);
@@ -566,7 +576,7 @@ int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, 
       const Part& P = parts[i];
       const int lay = sym ? layout : 0;
 #define DSVGD_X3W(SY, M, B, LAY, R0T)                                                          \
-  hipLaunchKernelGGL((sqdist_x3w_kernel<SY, SM, M, F, WN, NS>), dim3((unsigned)B), dim3(256 * WN), 0, s, Yg, \
+  hipLaunchKernelGGL((sqdist_x3w_kernel<SY, SM, M, F, WN, NS, KS>), dim3((unsigned)B), dim3(256 * WN), 0, s, Yg, \
                      img, norms, row0, m, n, n_pad, nk, D, st, cand, epi, P.total, LAY, P.tm2,   \
                      P.tc2, P.bj_off, R0T, base, ns_total, tsc)
       if (P.sym)
