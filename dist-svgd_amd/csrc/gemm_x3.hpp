@@ -184,6 +184,11 @@ struct NNX3Tile {
 #define DSVGD_NN_PINGPONG 0
 #endif
   static constexpr bool kPingPong = DSVGD_NN_PINGPONG != 0;  // (step_dma3)
+#ifndef DSVGD_NN_LATE_DMA
+#define DSVGD_NN_LATE_DMA 0
+#endif
+  static constexpr bool kLateDma = DSVGD_NN_LATE_DMA != 0;  // (step_dma3)
+  static_assert(!(kPingPong && kLateDma), "early staging counts on this iteration's DMAs issued");
   using V8 = typename F::V8;
   static_assert(!M16 || P == 3, "the 16x16x32 concatenated-k form is the 3-part format's");
   // (DMA needs the same DMA count in every wave: whole 512-chunk rounds)
@@ -605,10 +610,16 @@ struct NNX3Tile {
     const char* cur = smem + CUR * kStage;
     char* raw = smem + kRaw;
     const bool more = j0 + BJ < k1, more2 = j0 + 2 * BJ < k1;
-    if (more2) {
-      dma_b(smem + NN * kStage, rB, ldy, j0 + 2 * BJ);
-      dma_d(raw + NN * kSlot, rA, j0 + 2 * BJ);
-    }
+    // kLateDma: issue tile k+2's DMAs after the first half's MFMAs (their
+    // scalar address setup then runs in the MFMAs' shadow, not between the
+    // barrier and the first MFMA); the DMAs still have 1.5 iterations to land
+    auto issue = [&]() {
+      if (more2) {
+        dma_b(smem + NN * kStage, rB, ldy, j0 + 2 * BJ);
+        dma_d(raw + NN * kSlot, rA, j0 + 2 * BJ);
+      }
+    };
+    if (!kLateDma) issue();
     auto stage_next = [&]() {
       if (more) {
         if (more2)
@@ -629,6 +640,7 @@ struct NNX3Tile {
     read_a(cur, wr);
     if (early) stage_next();
     compute<0, kHalf>(cur, wc);
+    if (kLateDma) issue();
     if (!early) stage_next();
     compute<kHalf, TN>(cur, wc);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");

@@ -177,12 +177,21 @@ __device__ __forceinline__ void z_epilogue(T& tile, int64_t i0, int64_t q0,
 // lands while this one's epilogue (exp2, rcp, G stores) runs.
 // F = FmtX3: 16x16x32 (unswizzled W / Xd images); FmtH2: 32x32x16 on the
 // swizzled fp16 images of t_w W and t_x Xd (zsc = [1/t_w, 1/t_x]).
+// DSVGD_Z_KS (A/B): 16-deep image K-steps per ring stage of the FmtH2 Z
+// tiles (2, shipped: 32-deep stages, half the barriers, as the distance Gram;
+// scores -2.6 %, profiles/r5a_z_ks2_rank_ab.log)
+#ifndef DSVGD_Z_KS
+#define DSVGD_Z_KS 2
+#endif
+template <class F>
+constexpr int z_ks() { return F::P == 2 ? DSVGD_Z_KS : 1; }
+
 template <class F = FmtX3>
 __global__ __launch_bounds__(512, 1) void logreg_z_x3p_kernel(
     const typename F::E* __restrict__ Wx, int64_t n_img, const typename F::E* __restrict__ Xdx,
     int64_t N_img, int nk, const float* __restrict__ tp, int64_t N_pad, float* __restrict__ G,
     int Tm2, int Tn2, int64_t total, const float* __restrict__ zsc) {
-  using ZX3PTile = NTX3Tile<2, 4, 4, 2, 2, F::P == 3, F>;
+  using ZX3PTile = NTX3Tile<2, 4, 4, 2, 2, F::P == 3, F, z_ks<F>()>;  // nk: ring stages per tile
   const float zs = F::P == 3 ? 1.f : zsc[0] * zsc[1];
   __shared__ __attribute__((aligned(16))) char smem[ZX3PTile::kSmemBytes];
   const int w = threadIdx.x >> 6, wr = w / ZX3PTile::WN_, wc = w % ZX3PTile::WN_;
@@ -528,7 +537,7 @@ static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float 
     if ((rc = check_launch("zscale_pair"))) return rc;
     hipLaunchKernelGGL(logreg_z_x3p_kernel<FmtH2>, dim3((unsigned)blocks), dim3(512), 0, s,
                        (const _Float16*)Wx, w.n_pad, (const _Float16*)(base + w.off_xdx), w.N_pad,
-                       (int)(w.pp / kX3Step), tp, w.N_pad, G, Tm2, Tn2,
+                       (int)(w.pp / kX3Step / z_ks<FmtH2>()), tp, w.N_pad, G, Tm2, Tn2,
                        tile_grid(Tm2, Tn2, false), (const float*)zs);
     if ((rc = check_launch("logreg_z_h2"))) return rc;
     splits = gxd_splits(w.n_pad, w.N_pad);
