@@ -57,6 +57,11 @@ __device__ __forceinline__ void hist_key_agg(uint32_t key, uint32_t want, uint32
   }
 }
 
+#ifndef DSVGD_CAND_BLOCKS
+#define DSVGD_CAND_BLOCKS 4096  // (A/B builds: fewer workgroups on the candidate passes)
+#endif
+constexpr int kCandBlocks = DSVGD_CAND_BLOCKS;
+
 // count: entries of D (any order); cand: optional candidate buffer used
 // instead of D when st->fallback == 0 (bracketed mode).
 // sym_npad > 0: D is a symmetric n_pad x n_pad matrix stored as its
@@ -83,8 +88,12 @@ __global__ __launch_bounds__(256) void radix_hist_kernel(const float* __restrict
     const uint32_t* cnt = reinterpret_cast<const uint32_t*>(cand);
     const float* data = cand + 2 * ns;
     const int lane = threadIdx.x & 63;
-    const int64_t nw = (int64_t)gridDim.x * 4;
-    for (int64_t sl = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); sl < ns; sl += nw) {
+    // at most kCandBlocks workgroups walk the slots (each flushes its bins
+    // with global atomics onto the few bins the candidates share)
+    const int64_t nb = min((int64_t)gridDim.x, (int64_t)kCandBlocks);
+    const int64_t nw = nb * 4;
+    for (int64_t sl = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); blockIdx.x < nb && sl < ns;
+         sl += nw) {
       const uint32_t c = cnt[sl];
       const uint32_t w = (c & DSVGD_SLOT_WEIGHT2) ? 2u : 1u;
       const int64_t nc = min((int64_t)(c & ~DSVGD_SLOT_WEIGHT2), cap);

@@ -131,7 +131,11 @@ def main():
     ap.add_argument("--only", default="B,C,D,E")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--order", default="jacobi", choices=["jacobi", "sequential"])
+    ap.add_argument("--lib", default=None, help="an A/B build of the library (make ab)")
     args = ap.parse_args()
+    if args.lib:
+        import dsvgd
+        dsvgd._native.LIB_PATH = os.path.abspath(args.lib)
     res = {}
     for c in args.only.split(","):
         res[c] = run(c, args.steps, args.order)

@@ -244,3 +244,94 @@ def test_engine_refuses_oversized_d():
         m.engine.PhiEngine(1 << 20, 64)
     e = m.engine.PhiEngine(1 << 20, 64, m=1024, row0=0)      # 4 GiB row block fits
     assert e.D.numel() == 1024 * (1 << 20)
+
+
+def test_graph_replay_keeps_score_workspace():
+    """A captured step (S = 1, built-in target: DistSampler.graphs) holds the
+    logreg workspace address; scoring the same target at four other particle
+    counts between replays must not free or move it (workspaces
+    are never evicted).  Trajectory == a sampler whose target scored nothing else."""
+    m = dsvgd()
+    x, t, init = _data(n=256)
+    runs = []
+    for extra in (False, True):
+        tgt = m.targets.LogisticRegression(x, t)
+        ds = m.DistSampler(0, 1, tgt, m.RBF("median"), torch.tensor(init, device=DEV),
+                           x.shape[0], x.shape[0], exchange_particles=False,
+                           exchange_scores=False, include_wasserstein=False, order="jacobi")
+        traj = []
+        for step in range(4):
+            ds.make_step(1e-2)
+            traj.append(ds.particles.cpu().numpy())
+            if extra:
+                for n2 in (48, 96, 192, 384):
+                    X2 = torch.tensor(0.1 * np.random.RandomState(n2).randn(n2, init.shape[1]),
+                                      dtype=torch.float32, device=DEV)
+                    S2 = torch.empty_like(X2)
+                    tgt.score(X2, S2)
+        assert ds._graph is not None and ds._graph.graph is not None   # replays ran
+        runs.append(np.stack(traj))
+    np.testing.assert_array_equal(runs[0], runs[1])
+
+
+def _nccl_worker(rank, port, mode, order, q):
+    import os
+    import sys
+    import torch.distributed as dist
+    from conftest import PKG, ROOT
+    for p in (ROOT, PKG):
+        sys.path.insert(0, p)
+    import dsvgd as m
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", rank)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=2, device_id=dev)
+    x, t, init = _data(n=512)
+    per = x.shape[0] // 2
+    tgt = m.targets.LogisticRegression(x[rank * per:(rank + 1) * per], t[rank * per:(rank + 1) * per])
+    ep, es = {"partitions": (False, False), "all_particles": (True, False),
+              "all_scores": (True, True)}[mode]
+    ds = m.DistSampler(rank, 2, tgt, m.RBF(1.0), torch.tensor(init, device=dev), per, x.shape[0],
+                       exchange_particles=ep, exchange_scores=es, include_wasserstein=False,
+                       order=order)
+    traj = []
+    for _ in range(3):
+        ds.make_step(0.05)
+        traj.append(ds.particles.cpu().numpy())
+    q.put((rank, traj))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL path needs two GPUs")
+@pytest.mark.parametrize("mode", ["partitions", "all_particles", "all_scores"])
+@pytest.mark.parametrize("order", ["jacobi", "sequential"])
+def test_rccl_two_gpus_match_oracle(mode, order):
+    """The device collectives (in-place all_gather_into_tensor, batch_isend_irecv
+    ring shift, the all_scores all-reduce on a side stream beside the
+    histogram all-reduces) on two GPUs over RCCL, against DistOracle."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + 2 * ["partitions", "all_particles", "all_scores"].index(mode) + (order == "jacobi")
+    ps = [ctx.Process(target=_nccl_worker, args=(r, port, mode, order, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda r: r[0])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    x, t, init = _data(n=512)
+    per = x.shape[0] // 2
+    fns = [lambda X, r=r: O.score_logreg(X, x[r * per:(r + 1) * per], t[r * per:(r + 1) * per])
+           for r in range(2)]
+    ep, es = {"partitions": (False, False), "all_particles": (True, False),
+              "all_scores": (True, True)}[mode]
+    D = O.DistOracle([init, init], fns, per, x.shape[0], ep, es, sequential=order == "sequential")
+    for step in range(3):
+        D.step(0.05)
+        for rank, traj in res:
+            err = float(np.abs(traj[step] - D.own(rank)).max())
+            record_parity(err)
+            assert err < TRAJ_TOL, (step, rank, err)
