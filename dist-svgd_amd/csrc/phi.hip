@@ -662,9 +662,14 @@ int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, i
 // row block is small (S ranks), (2) at most kMaxChain columns per fp32
 // accumulation chain.  (2) is precision: K.S is a coherent sum (|sum| grows
 // linearly), so one n-long fma chain loses ~sqrt(n) eps |sum| -- 8.7e-6 of
-// max|phi| at n = 65536, d = 256 (scripts/diag_precision.py); slices of 8192
-// summed in slice order by phi_finish cut that ~8x.
-constexpr int64_t kMaxChain = 8192;
+// max|phi| at n = 65536, d = 256 on the round-1 engine (scripts/diag_precision.py);
+// slices summed in slice order by phi_finish cut that.  FmtH2 at n = 65536:
+// 5.2e-7 with 8192-long slices, 7.8e-7 with 16384 (shipped: half the
+// partials to write and re-read, S = 1 step -1.7 %; profiles/r5g_*).
+#ifndef DSVGD_MAX_CHAIN
+#define DSVGD_MAX_CHAIN 16384
+#endif
+constexpr int64_t kMaxChain = DSVGD_MAX_CHAIN;
 
 int64_t phi_splits(int64_t m, int64_t n, int64_t ldy) {
   const int64_t cols = ldy % 512 == 0 ? 512 : (ldy % 256 == 0 ? 256 : 128);

@@ -1,5 +1,7 @@
 """Where does the full-size phi error come from?  n=65536, d=256, sampled rows:
-compare D, r' = sum_{j!=i} k_ij, K'X, K'S and phi against fp64."""
+compare D, r' = sum_{j!=i} k_ij, K'X, K'S and phi against fp64.
+
+    python scripts/diag_precision.py [n] [A/B library]"""
 import os
 import sys
 
@@ -12,6 +14,8 @@ import dsvgd  # noqa: E402
 from oracle import svgd_oracle as O  # noqa: E402
 
 n, d = int(sys.argv[1]) if len(sys.argv) > 1 else 65536, 256
+if len(sys.argv) > 2:
+    dsvgd._native.LIB_PATH = os.path.abspath(sys.argv[2])
 rs = np.random.RandomState(0)
 X = rs.randn(n, d).astype(np.float32)
 mu = rs.randn(d).astype(np.float32)
