@@ -665,7 +665,7 @@ int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, i
 // max|phi| at n = 65536, d = 256 on the round-1 engine (scripts/diag_precision.py);
 // slices summed in slice order by phi_finish cut that.  FmtH2 at n = 65536:
 // 5.2e-7 with 8192-long slices, 7.8e-7 with 16384 (shipped: half the
-// partials to write and re-read, S = 1 step -1.7 %; profiles/r5g_*).
+// partials to write and re-read, S = 1 step -1.7 %; profiles/r5g/).
 #ifndef DSVGD_MAX_CHAIN
 #define DSVGD_MAX_CHAIN 16384
 #endif
