@@ -53,6 +53,14 @@ constexpr size_t kW2CtlBytes = 256;
 constexpr double kTheta = 8.0;
 constexpr int kRoundBatch = 16;
 constexpr int kBidBlocks = 1024;  // grid-stride bid kernel: 4096 waves
+#ifndef DSVGD_W2_CACHE
+#define DSVGD_W2_CACHE 1  // (A/B builds: 0 = every bid scans its whole cost row)
+#endif
+constexpr bool kW2Cache = DSVGD_W2_CACHE != 0;
+#ifndef DSVGD_W2_CTL_LAUNCH
+#define DSVGD_W2_CTL_LAUNCH 0  // (A/B: 1 = control step as a separate launch, no ticket)
+#endif
+constexpr bool kW2CtlLaunch = DSVGD_W2_CTL_LAUNCH != 0;
 
 // holder[j] = epoch tag << 21 | row holding column j (tag = epoch & 0x7ff,
 // never 0: stale entries of earlier phases and the zeroed workspace read as
@@ -62,13 +70,28 @@ constexpr int64_t kMaxRows = (int64_t)1 << kRowBits;
 constexpr int kMaxR = 32;
 __device__ __forceinline__ uint32_t w2_tag(int ep) { return (uint32_t)(ep & 0x7ff) << kRowBits; }
 
+// Price cache (R in [2, kCacheMaxR]): a row's full scan keeps its kCache
+// best columns over ALL columns (col, cost) and the (kCache+1)-th value
+// -C - p as `bound`.  Prices only rise (within and across phases), so every
+// uncached column's current value is <= bound; a later bid that finds its
+// u + 1 best non-held values among the cached columns (current prices) with
+// the (u+1)-th >= bound is exactly the full scan's bid.  The row holds at most
+// R - u columns, so its u + 1 best non-held are among its R + 1 best overall
+// (R + 1 <= kCache).  Otherwise it rescans and refills.  valid[i] = 0 after
+// the workspace memset of every solve (costs change between solves).
+constexpr int kCache = 16;
+constexpr int kCacheMaxR = 8;
+
 struct W2Ws {
   W2Ctl* ctl;
   double* price;
   unsigned long long* bid;
   int32_t *owner, *assigned, *assigned_ep;
   uint32_t* holder;
-  W2Ws(void* ws, int64_t n) {
+  int32_t *ccol, *cvalid;
+  float* ccost;
+  double* cbound;
+  W2Ws(void* ws, int64_t n, int64_t m) {
     char* p = (char*)ws;
     ctl = (W2Ctl*)p;
     price = (double*)(p + kW2CtlBytes);
@@ -77,6 +100,10 @@ struct W2Ws {
     holder = (uint32_t*)(owner + n);
     assigned = (int32_t*)(holder + n);
     assigned_ep = assigned + n;
+    cbound = (double*)(((uintptr_t)(assigned_ep + n) + 7) & ~(uintptr_t)7);
+    ccol = (int32_t*)(cbound + m);
+    ccost = (float*)(ccol + m * kCache);
+    cvalid = (int32_t*)(ccost + m * kCache);
   }
 };
 
@@ -258,6 +285,130 @@ __device__ __forceinline__ void bid_row(const float* __restrict__ row, int64_t n
   atomicMax(&w.bid[kj], key);
 }
 
+// The u + 1 best (value, column) of the wave's lane candidates (cv, cj),
+// in order, into lane k's (kv, kj) (ties -> lower column)
+__device__ __forceinline__ void wave_best(double cv, int cj, int u, int lane, double& kv, int& kj) {
+  kv = -DBL_MAX;
+  kj = INT32_MAX;
+  for (int k = 0; k <= u; ++k) {
+    double bv = cv;
+    int bj = cj;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ov = __shfl_xor(bv, o, 64);
+      const int oj = __shfl_xor(bj, o, 64);
+      if (ov > bv || (ov == bv && oj < bj)) {
+        bv = ov;
+        bj = oj;
+      }
+    }
+    if (lane == k) {
+      kv = bv;
+      kj = bj;
+    }
+    if (cj == bj) cv = -DBL_MAX;  // taken (columns are unique across lanes)
+  }
+}
+
+// bid_row with the price cache (R in [2, kCacheMaxR]); same bids as bid_row
+__device__ __forceinline__ void bid_row_cached(const float* __restrict__ row, int64_t n, int64_t i,
+                                               int64_t R, unsigned long long free, int lane,
+                                               double eps, uint32_t tag, const W2Ws& w) {
+  const int u = __popcll(free);
+  const uint32_t mine = tag | (uint32_t)i;
+  double kv;
+  int kj;
+  bool ok = false;
+  if (w.cvalid[i]) {  // wave-uniform
+    double cv = -DBL_MAX;
+    int cj = INT32_MAX;
+    if (lane < kCache) {
+      const int c = w.ccol[i * kCache + lane];
+      if (c != INT32_MAX && w.holder[c] != mine) {  // held columns never bid
+        cj = c;
+        cv = -(double)w.ccost[i * kCache + lane] - w.price[c];
+      }
+    }
+    wave_best(cv, cj, u, lane, kv, kj);
+    const double vu1 = __shfl(kv, u, 64);
+    ok = vu1 >= w.cbound[i];
+  }
+  if (!ok) {  // full scan over all columns, refill the cache
+    TopK<kCache + 1> t;
+    t.init();
+    for (int64_t j = lane; j < n; j += 64) t.push(-(double)row[j] - w.price[j], (int)j);
+    double ev = -DBL_MAX;
+    int ej = INT32_MAX;
+    for (int k = 0; k <= kCache; ++k) {
+      double bv = t.v[0];
+      int bj = t.j[0];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(bv, o, 64);
+        const int oj = __shfl_xor(bj, o, 64);
+        if (ov > bv || (ov == bv && oj < bj)) {
+          bv = ov;
+          bj = oj;
+        }
+      }
+      if (lane == k) {
+        ev = bv;
+        ej = bj;
+      }
+      if (t.j[0] == bj) t.pop();
+    }
+    if (lane < kCache) {
+      w.ccol[i * kCache + lane] = ej;
+      w.ccost[i * kCache + lane] = ej != INT32_MAX ? row[ej] : 0.f;
+    }
+    if (lane == kCache) w.cbound[i] = ev;
+    if (lane == 0) w.cvalid[i] = 1;
+    // bid from the fresh list (current values), held columns excluded
+    double cv = -DBL_MAX;
+    int cj = INT32_MAX;
+    if (lane < kCache && ej != INT32_MAX && w.holder[ej] != mine) {
+      cj = ej;
+      cv = ev;
+    }
+    wave_best(cv, cj, u, lane, kv, kj);
+  }
+  const double vu1 = __shfl(kv, u, 64), vu = __shfl(kv, u - 1, 64);
+  const double vref = (vu1 > -DBL_MAX) ? vu1 : vu;
+  if (lane >= u || kj == INT32_MAX) return;
+  unsigned long long rest = free;
+  for (int k = 0; k < lane; ++k) rest &= rest - 1;
+  const int64_t s = i * R + (__ffsll((long long)rest) - 1);
+  const double inc = kv - vref + eps;
+  float f = (float)inc;
+  if ((double)f > inc) f = nextafterf(f, 0.f);  // round down: keeps eps-CS
+  if (!(f > 0.f)) f = FLT_MIN;
+  const unsigned long long key =
+      ((unsigned long long)__float_as_uint(f) << 32) | (unsigned long long)(uint32_t)s;
+  atomicMax(&w.bid[kj], key);
+}
+
+__global__ __launch_bounds__(256) void w2_bid_cached_kernel(const float* __restrict__ C,
+                                                            int64_t ldc, int64_t m, int64_t n,
+                                                            int64_t R, W2Ws w) {
+  const W2Ctl* ctl = w.ctl;
+  if (ctl->done) return;
+  const int lane = threadIdx.x & 63;
+  const int ep = ctl->epoch;
+  const double eps = ctl->eps;
+  const uint32_t tag = w2_tag(ep);
+  for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < m;
+       i += (int64_t)gridDim.x * 4) {
+    bool fr = false;
+    if (lane < R) {
+      const int64_t s = i * R + lane;
+      fr = !(w.assigned_ep[s] == ep && w.assigned[s] >= 0);
+    }
+    const unsigned long long free = __ballot(fr);
+    if (free == 0) continue;
+    bid_row_cached(C + i * ldc, n, i, R, free, lane, eps, tag, w);
+  }
+}
+
 // Waves stride over the rows; rows with free slots in this epoch bid.
 template <int K>
 __global__ __launch_bounds__(256) void w2_bid_kernel(const float* __restrict__ C, int64_t ldc,
@@ -328,6 +479,7 @@ __global__ __launch_bounds__(256) void w2_resolve_kernel(int64_t n, int64_t R, W
   for (int o = 32; o > 0; o >>= 1) gained += __shfl_xor(gained, o, 64);
   if ((threadIdx.x & 63) == 0 && gained)
     atomicAdd(&ctl->unassigned, (unsigned long long)(-(long long)gained));
+  if constexpr (kW2CtlLaunch) return;  // w2_control_kernel runs the control step
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -342,6 +494,14 @@ __global__ __launch_bounds__(256) void w2_resolve_kernel(int64_t n, int64_t R, W
       w2_control(ctl, n);
     }
   }
+}
+
+// the control step as its own one-thread launch (kW2CtlLaunch): after the
+// resolve kernel's boundary every block's updates are visible without the
+// per-block release fences of the ticket
+__global__ void w2_control_kernel(W2Ctl* ctl, int64_t n) {
+  if (ctl->done) return;
+  w2_control(ctl, n);
 }
 
 __global__ __launch_bounds__(256) void w2_emit_kernel(int64_t n, W2Ws w, int32_t* assign) {
@@ -374,8 +534,8 @@ using namespace dsvgd;
 extern "C" {
 
 size_t dsvgd_w2_workspace_bytes(int64_t m, int64_t n) {
-  (void)m;
-  return kW2CtlBytes + (size_t)n * (sizeof(double) + sizeof(unsigned long long) + 4 * sizeof(int32_t));
+  return kW2CtlBytes + (size_t)n * (sizeof(double) + sizeof(unsigned long long) + 4 * sizeof(int32_t)) +
+         8 + (size_t)m * (sizeof(double) + kCache * (sizeof(int32_t) + sizeof(float)) + sizeof(int32_t));
 }
 
 int dsvgd_w2_cost(const float* X, int64_t ldx, int64_t m, const float* Y, int64_t ldy, int64_t n,
@@ -400,7 +560,7 @@ int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
   DSVGD_REQUIRE(max_rounds > 0, "max_rounds");
   DSVGD_REQUIRE(warm_phases >= 0, "warm_phases");
   hipStream_t s = (hipStream_t)stream;
-  W2Ws w(ws, n);
+  W2Ws w(ws, n, m);
   const int64_t R = n / m;
   // warm start keeps the price array (the previous call's duals on this
   // workspace); everything else restarts
@@ -420,6 +580,10 @@ int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
   if (rc) return rc;
   const dim3 gb((unsigned)std::min<int64_t>(kBidBlocks, (m + 3) / 4));
   auto bid = [&]() {
+    if (kW2Cache && R >= 2 && R <= kCacheMaxR) {
+      hipLaunchKernelGGL(w2_bid_cached_kernel, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
+      return;
+    }
     if (R <= 1)
       hipLaunchKernelGGL(w2_bid_kernel<2>, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
     else if (R <= 2)
@@ -450,6 +614,7 @@ int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
     for (int b = 0; b < kRoundBatch; ++b) {
       bid();
       hipLaunchKernelGGL(w2_resolve_kernel, gr, dim3(256), 0, s, n, R, w);
+      if (kW2CtlLaunch) hipLaunchKernelGGL(w2_control_kernel, dim3(1), dim3(1), 0, s, w.ctl, n);
     }
     W2Ctl* slot = hbuf + (batch & 1);
     if ((rc = check_launch("w2 auction round")) ||

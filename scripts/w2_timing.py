@@ -1,7 +1,7 @@
 """Time the GPU W2/JKO term (dsvgd.w2.W2Term.grad: cost + auction + gradient)
 on random and SVGD-shaped inputs.
 
-    python scripts/w2_timing.py [--big]
+    python scripts/w2_timing.py [--big] [--lib A/B library]
 
 SVGD shape: the owned block X (m rows) against previous particles of which
 the first m rows are X before a small step (all_particles / all_scores mode
@@ -70,7 +70,11 @@ def main():
     ap.add_argument("--big", action="store_true")
     ap.add_argument("--warm-sweep", action="store_true",
                     help="warm-start phases 1..5 on two R > 1 shapes")
+    ap.add_argument("--lib", default=None, help="an A/B build of the library (make ab)")
     args = ap.parse_args()
+    if args.lib:
+        import dsvgd
+        dsvgd._native.LIB_PATH = os.path.abspath(args.lib)
     if args.warm_sweep:
         import dsvgd
         for ph in (1, 2, 3, 4, 5):
