@@ -163,7 +163,7 @@ class DistSampler(object):
             warnings.warn(
                 "DistSampler: include_wasserstein=True with R = n/m = %d > 1 and an "
                 "%d x %d plan: the exact W2 assignment takes seconds per step at this "
-                "size (m=8192, n=65536: ~46 s cold, ~4-13x less warm); pass "
+                "size (m=8192, n=65536: ~14 s cold, ~2 s warm); pass "
                 "include_wasserstein=False for throughput" % (n // m, m, n),
                 RuntimeWarning, stacklevel=3)
 
