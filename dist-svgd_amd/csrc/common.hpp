@@ -40,6 +40,11 @@ __device__ __forceinline__ int c_row(int reg, int lane) {
   return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
 }
 
+// |v|'s bit pattern: unsigned order is magnitude order, finite < inf < NaN
+__device__ __forceinline__ uint32_t abs_bits(float v) {
+  return __float_as_uint(v) & 0x7fffffffu;
+}
+
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -20,9 +20,6 @@ constexpr int kScaleRows = 512;  // rows per partial-max block
 // partial[b][c] = max |A[r][c]| over rows r of block b, as the bit pattern of
 // |v| (unsigned order: finite < inf < NaN, so a NaN or inf is carried through)
 // -- 64-column stripes, 4 row groups of 64 lanes, four loads in flight per lane.
-__device__ __forceinline__ uint32_t abs_bits(float v) {
-  return __float_as_uint(v) & 0x7fffffffu;
-}
 
 __global__ __launch_bounds__(256) void colmax_partial_kernel(const float* __restrict__ A,
                                                              int64_t lda, int64_t rows,
@@ -102,6 +99,62 @@ __global__ __launch_bounds__(256) void colscale_final_kernel(const uint32_t* __r
     const float t = (bad[0] || !isfinite(red[0])) ? 1.f : red[0];
     out[2 * cols] = t;
     out[2 * cols + 1] = 1.f / t;
+  }
+}
+
+// the scales of dsvgd_h2_colscale's layout from pack_h2's maxima, over the
+// first `cols` columns (cols == dp: the X half, the Gram's row image; cols ==
+// ldy: all of Y, phi_mm's B image).  16 columns x 16 row groups per block;
+// t = pow2_scale(the largest magnitude over those columns) -- the smallest
+// nonzero column scale, since pow2_scale is monotone, and 1 when it is 0 or
+// not finite -- from gmax, by every block's lane group 0 (block 0 writes it).
+constexpr int kScaleCols = 16;
+
+__global__ __launch_bounds__(256) void scales_h2_kernel(const uint32_t* __restrict__ partial,
+                                                        const uint32_t* __restrict__ gmax,
+                                                        int64_t nb, int64_t ldp, int64_t cols,
+                                                        int64_t dp, float* __restrict__ out) {
+  __shared__ uint32_t red[16][kScaleCols];
+  const int cl = threadIdx.x & (kScaleCols - 1), rg = threadIdx.x / kScaleCols;
+  const int64_t c = (int64_t)blockIdx.x * kScaleCols + cl;
+  uint32_t m0 = 0u, m1 = 0u, m2 = 0u, m3 = 0u;
+  if (c < cols) {
+    int64_t b = rg;
+    for (; b + 48 < nb; b += 64) {
+      m0 = max(m0, partial[b * ldp + c]);
+      m1 = max(m1, partial[(b + 16) * ldp + c]);
+      m2 = max(m2, partial[(b + 32) * ldp + c]);
+      m3 = max(m3, partial[(b + 48) * ldp + c]);
+    }
+    for (; b < nb; b += 16) m0 = max(m0, partial[b * ldp + c]);
+  }
+  red[rg][cl] = max(max(m0, m1), max(m2, m3));
+  __syncthreads();
+  if (rg == 0 && c < cols) {
+    uint32_t mb = 0u;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) mb = max(mb, red[q][cl]);
+    const float s = pow2_scale(__uint_as_float(mb));
+    out[c] = s;
+    out[cols + c] = 1.f / s;
+  }
+  if (blockIdx.x == 0) {
+    __syncthreads();
+    // gmax[2b] covers [0, dp), gmax[2b + 1] the rest of the row
+    uint32_t g = 0u;
+    for (int64_t b = threadIdx.x; b < nb; b += 256) {
+      g = max(g, gmax[2 * b]);
+      if (cols > dp) g = max(g, gmax[2 * b + 1]);
+    }
+    for (int o = 32; o > 0; o >>= 1) g = max(g, (uint32_t)__shfl_xor((int)g, o));
+    if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = g;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float t =
+          pow2_scale(__uint_as_float(max(max(red[0][0], red[0][1]), max(red[0][2], red[0][3]))));
+      out[2 * cols] = t;
+      out[2 * cols + 1] = 1.f / t;
+    }
   }
 }
 
@@ -246,6 +299,16 @@ int dsvgd_h2_colscale(const float* A, int64_t lda, int64_t rows, int64_t cols, f
   DSVGD_REQUIRE(A && ws && scale, "null pointer");
   DSVGD_REQUIRE(rows > 0 && cols > 0 && lda >= cols, "sizes");
   return h2_colscale(A, lda, rows, cols, ws, scale, (hipStream_t)stream);
+}
+
+int dsvgd_h2_scales(const uint32_t* partial, const uint32_t* gmax, int64_t nb, int64_t ldy,
+                    int64_t cols, int64_t dp, float* scale, void* stream) {
+  DSVGD_REQUIRE(partial && gmax && scale, "null pointer");
+  DSVGD_REQUIRE(nb > 0 && dp > 0 && (cols == dp || cols == ldy) && ldy >= 2 * dp,
+                "cols must be dp (the X half) or ldy (all of Y)");
+  hipLaunchKernelGGL(scales_h2_kernel, dim3((unsigned)((cols + kScaleCols - 1) / kScaleCols)),
+                     dim3(256), 0, (hipStream_t)stream, partial, gmax, nb, ldy, cols, dp, scale);
+  return check_launch("scales_h2");
 }
 
 int64_t dsvgd_h2_image_bytes(int64_t rows, int64_t cols) {

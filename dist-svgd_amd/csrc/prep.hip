@@ -120,9 +120,115 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
 }
 
 // ---------------------------------------------------------------- pack ----
-// One wave per row: Y[j] = [X[j]-mean (dp cols) | scale*S[j] (dp cols) | 0],
+// Y[j] = [X[j]-mean (dp cols) | scale*S[j] (dp cols) | 0], norms[j] =
+// |X[j]-mean|^2, rows j >= n zero; with partial != nullptr also the FmtH2
+// column maxima of what it writes (h2.hip), so the scales need no second pass
+// over Y: partial[b][c] = max |Y[r][c]| over block b's kPackRows rows, and
+// gmax[2b] / gmax[2b + 1] = the block's largest over the X half [0, dp) /
+// over [dp, ldy).  X == nullptr: the S half of rows < n only (its columns'
+// partials and gmax[2b + 1]).  One wave per row, 16-byte accesses: a lane
+// owns 4 adjacent columns of each 256-column pass (dp % 32 == 0, so a lane's
+// 4 never straddle the X / S boundary).
+constexpr int kPackRows = 64;  // rows per block, 16 per wave
+constexpr int kPackQ = 8;      // 256-column passes per row: ldy <= 2048
+
+template <bool VX, bool VS>  // 16-byte loads of X / S rows (aligned, ld % 4 == 0)
+__global__ __launch_bounds__(256) void pack_kernel(
+    const float* __restrict__ X, int64_t ldx, const float* __restrict__ S, int64_t lds,
+    float scale, const float* __restrict__ mean, int64_t n, int64_t d, int64_t rows_pad,
+    int64_t dp, float* __restrict__ Y, int64_t ldy, float* __restrict__ norms,
+    uint32_t* __restrict__ partial, uint32_t* __restrict__ gmax) {
+  extern __shared__ uint32_t red[];  // [4 waves][ldy]
+  __shared__ uint32_t gred[4][2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * kPackRows;
+  const int64_t r1 = min(r0 + kPackRows, rows_pad);
+  const int64_t c_lo = X ? 0 : dp, c_hi = X ? ldy : 2 * dp;
+  uint32_t mx[kPackQ][4];
+#pragma unroll
+  for (int q = 0; q < kPackQ; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) mx[q][e] = 0u;
+  for (int64_t j = r0 + w; j < r1; j += 4) {
+    float nrm = 0.f;
+    f32x4 v[kPackQ];
+#pragma unroll
+    for (int q = 0; q < kPackQ; ++q) {
+      const int64_t c = 4 * lane + 256 * q;
+      v[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (c >= ldy || j >= n) continue;
+      if (c < dp) {
+        if (!X) continue;
+        if (VX && c + 4 <= d) {
+          v[q] = *reinterpret_cast<const f32x4*>(X + j * ldx + c) -
+                 *reinterpret_cast<const f32x4*>(mean + c);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (c + e < d) v[q][e] = X[j * ldx + c + e] - mean[c + e];
+        }
+      } else if (c < 2 * dp && S != nullptr) {
+        const int64_t cs = c - dp;
+        if (VS && cs + 4 <= d) {
+          v[q] = scale * *reinterpret_cast<const f32x4*>(S + j * lds + cs);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (cs + e < d) v[q][e] = scale * S[j * lds + cs + e];
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kPackQ; ++q) {
+      const int64_t c = 4 * lane + 256 * q;
+      if (c >= ldy || c < c_lo || c >= c_hi) continue;
+      *reinterpret_cast<f32x4*>(Y + j * ldy + c) = v[q];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        mx[q][e] = max(mx[q][e], abs_bits(v[q][e]));
+        if (c < dp) nrm = fmaf(v[q][e], v[q][e], nrm);
+      }
+    }
+    if (X) {
+      nrm = warp_sum(nrm);
+      if (lane == 0) norms[j] = nrm;
+    }
+  }
+  if (partial == nullptr) return;
+  uint32_t gx = 0u, gs = 0u;
+#pragma unroll
+  for (int q = 0; q < kPackQ; ++q) {
+    const int64_t c = 4 * lane + 256 * q;
+    if (c >= ldy) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[w * ldy + c + e] = mx[q][e];
+      if (c < dp) gx = max(gx, mx[q][e]);
+      else gs = max(gs, mx[q][e]);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    gx = max(gx, (uint32_t)__shfl_xor((int)gx, o));
+    gs = max(gs, (uint32_t)__shfl_xor((int)gs, o));
+  }
+  if (lane == 0) {
+    gred[w][0] = gx;
+    gred[w][1] = gs;
+  }
+  __syncthreads();
+  for (int64_t c = threadIdx.x; c < ldy; c += 256)
+    if (c >= c_lo && c < c_hi)
+      partial[(int64_t)blockIdx.x * ldy + c] =
+          max(max(red[c], red[ldy + c]), max(red[2 * ldy + c], red[3 * ldy + c]));
+  if (threadIdx.x < 2 && (X || threadIdx.x == 1))
+    gmax[2 * blockIdx.x + threadIdx.x] =
+        max(max(gred[0][threadIdx.x], gred[1][threadIdx.x]),
+            max(gred[2][threadIdx.x], gred[3][threadIdx.x]));
+}
+
+// ldy > 256 kPackQ (d > 1024): one wave per row, element accesses, no maxima: Y[j] = [X[j]-mean (dp cols) | scale*S[j] (dp cols) | 0],
 // norms[j] = |X[j]-mean|^2.  Rows j >= n are zero.
-__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ X, int64_t ldx,
+__global__ __launch_bounds__(256) void pack_wide_kernel(const float* __restrict__ X, int64_t ldx,
                                                    const float* __restrict__ S, int64_t lds,
                                                    float scale, const float* __restrict__ mean,
                                                    int64_t n, int64_t d, int64_t rows_pad,
@@ -229,17 +335,46 @@ int dsvgd_colmean(const float* X, int64_t ldx, int64_t n, int64_t d, float* part
   return check_launch("colsum_final");
 }
 
+int64_t dsvgd_pack_blocks(int64_t rows_pad) { return (rows_pad + kPackRows - 1) / kPackRows; }
+int64_t dsvgd_pack_max_ldy(void) { return 256 * kPackQ; }
+
+int dsvgd_pack_h2(const float* X, int64_t ldx, const float* S, int64_t lds, float score_scale,
+                  const float* mean, int64_t n, int64_t d, int64_t rows_pad, float* Y, int64_t ldy,
+                  float* norms, uint32_t* partial, uint32_t* gmax, void* stream) {
+  DSVGD_REQUIRE(Y && (X ? (mean && norms) : (S != nullptr)), "null pointer");
+  DSVGD_REQUIRE(!partial == !gmax, "partial and gmax go together");
+  DSVGD_REQUIRE(n > 0 && d > 0 && (!X || ldx >= d) && rows_pad >= n, "sizes");
+  const int64_t dp = dsvgd_dp(d);
+  DSVGD_REQUIRE(ldy >= 2 * dp && ldy % 4 == 0, "ldy");
+  DSVGD_REQUIRE(!partial || ldy <= dsvgd_pack_max_ldy(), "column maxima need ldy <= 2048");
+  DSVGD_REQUIRE(((uintptr_t)Y & 15) == 0, "Y: 16-byte alignment");
+  DSVGD_REQUIRE(S == nullptr || lds >= d, "lds");
+  hipStream_t s = (hipStream_t)stream;
+  if (ldy > dsvgd_pack_max_ldy()) {
+    hipLaunchKernelGGL(pack_wide_kernel, dim3((rows_pad + 3) / 4), dim3(256), 0, s, X, ldx, S,
+                       lds, score_scale, mean, n, d, rows_pad, dp, Y, ldy, norms);
+    return check_launch("pack_wide");
+  }
+  const bool vx = X && ((uintptr_t)X & 15) == 0 && ldx % 4 == 0 && ((uintptr_t)mean & 15) == 0;
+  const bool vs = S && ((uintptr_t)S & 15) == 0 && lds % 4 == 0;
+  const dim3 grid((unsigned)dsvgd_pack_blocks(rows_pad));
+  const size_t lds_bytes = partial ? 4 * sizeof(uint32_t) * (size_t)ldy : 0;
+#define DSVGD_PACK(VX, VS)                                                                    \
+  hipLaunchKernelGGL((pack_kernel<VX, VS>), grid, dim3(256), lds_bytes, s, X, ldx, S, lds,    \
+                     score_scale, mean, n, d, rows_pad, dp, Y, ldy, norms, partial, gmax)
+  if (vx && vs) DSVGD_PACK(true, true);
+  else if (vx) DSVGD_PACK(true, false);
+  else if (vs) DSVGD_PACK(false, true);
+  else DSVGD_PACK(false, false);
+#undef DSVGD_PACK
+  return check_launch("pack");
+}
+
 int dsvgd_pack(const float* X, int64_t ldx, const float* S, int64_t lds, float score_scale,
                const float* mean, int64_t n, int64_t d, int64_t rows_pad, float* Y, int64_t ldy,
                float* norms, void* stream) {
-  DSVGD_REQUIRE(Y && (X ? (mean && norms) : (S != nullptr)), "null pointer");
-  DSVGD_REQUIRE(n > 0 && d > 0 && (!X || ldx >= d) && rows_pad >= n, "sizes");
-  const int64_t dp = dsvgd_dp(d);
-  DSVGD_REQUIRE(ldy >= 2 * dp, "ldy < 2*dp");
-  DSVGD_REQUIRE(S == nullptr || lds >= d, "lds");
-  hipLaunchKernelGGL(pack_kernel, dim3((rows_pad + 3) / 4), dim3(256), 0, (hipStream_t)stream, X,
-                     ldx, S, lds, score_scale, mean, n, d, rows_pad, dp, Y, ldy, norms);
-  return check_launch("pack");
+  return dsvgd_pack_h2(X, ldx, S, lds, score_scale, mean, n, d, rows_pad, Y, ldy, norms, nullptr,
+                       nullptr, stream);
 }
 
 int dsvgd_score_gaussian(const float* X, int64_t ldx, int64_t n, int64_t d, const float* mu,

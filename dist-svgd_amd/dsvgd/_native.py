@@ -29,6 +29,10 @@ SIGNATURES = {
     "dsvgd_colmean_workspace_floats": (_c.c_size_t, [_i64, _i64]),
     "dsvgd_colmean": (_int, [_p, _i64, _i64, _i64, _p, _p, _p]),
     "dsvgd_pack": (_int, [_p, _i64, _p, _i64, _f, _p, _i64, _i64, _i64, _p, _i64, _p, _p]),
+    "dsvgd_pack_blocks": (_i64, [_i64]),
+    "dsvgd_pack_max_ldy": (_i64, []),
+    "dsvgd_pack_h2": (_int, [_p, _i64, _p, _i64, _f, _p, _i64, _i64, _i64, _p, _i64, _p, _p, _p,
+                             _p]),
     "dsvgd_sqdist": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p]),
     "dsvgd_sqdist_direct": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p,
                                    _p]),
@@ -53,6 +57,7 @@ SIGNATURES = {
                                 _int, _p]),
     "dsvgd_h2_colscale_workspace_floats": (_c.c_size_t, [_i64, _i64]),
     "dsvgd_h2_colscale": (_int, [_p, _i64, _i64, _i64, _p, _p, _p]),
+    "dsvgd_h2_scales": (_int, [_p, _p, _i64, _i64, _i64, _i64, _p, _p]),
     "dsvgd_h2_image_bytes": (_i64, [_i64, _i64]),
     "dsvgd_h2_ysplit": (_int, [_p, _i64, _i64, _p, _p, _p]),
     "dsvgd_h2_rowsplit": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _p, _p, _p]),

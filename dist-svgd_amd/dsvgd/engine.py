@@ -203,6 +203,15 @@ class PhiEngine(object):
             # Gram, of all of Y for phi_mm's B image
             self.xscale = torch.empty(2 * self.dp + 2, **f32)
             self.yscale = torch.empty(2 * self.ldy + 2, **f32)
+        # d <= 1024: pack writes the column maxima the scales come from
+        # (dsvgd_pack_h2 / dsvgd_h2_scales); wider, a separate pass over Y
+        self.fused_scales = "h2" in (phi_gemm, gram_gemm) and self.ldy <= lib.dsvgd_pack_max_ldy()
+        if self.fused_scales:
+            self.colmax_nb = lib.dsvgd_pack_blocks(rows)
+            i32 = dict(dtype=torch.int32, device=dev)
+            self.colmax = torch.zeros(self.colmax_nb * self.ldy, **i32)
+            self.gmax = torch.zeros(2 * self.colmax_nb, **i32)
+        elif "h2" in (phi_gemm, gram_gemm):
             self.scale_ws = torch.empty(
                 max(1, lib.dsvgd_h2_colscale_workspace_floats(self.n_pad, self.ldy)), **f32)
         self.KY = torch.empty(self.splits * m, self.ldy, **f32)
@@ -257,8 +266,23 @@ class PhiEngine(object):
         assert S.shape == (self.n, self.d)
         s = N.stream(self.device)
         with span(self.timer, "pack"):
-            N.call("dsvgd_pack", None, self.d, N.ptr(S), N.ld(S), float(score_scale), None,
-                   self.n, self.d, self.Y.shape[0], N.ptr(self.Y), self.ldy, None, s)
+            N.call("dsvgd_pack_h2", None, self.d, N.ptr(S), N.ld(S), float(score_scale), None,
+                   self.n, self.d, self.Y.shape[0], N.ptr(self.Y), self.ldy, None,
+                   *self._maxima(), s)
+
+    def _maxima(self):
+        if self.fused_scales:
+            return N.ptr(self.colmax), N.ptr(self.gmax)
+        return None, None
+
+    def _scales(self, cols, out, s):
+        """FmtH2 column scales of Y's first `cols` columns into `out`."""
+        if self.fused_scales:
+            N.call("dsvgd_h2_scales", N.ptr(self.colmax), N.ptr(self.gmax), self.colmax_nb,
+                   self.ldy, cols, self.dp, N.ptr(out), s)
+        else:
+            N.call("dsvgd_h2_colscale", N.ptr(self.Y), self.ldy, self.n_pad, cols,
+                   N.ptr(self.scale_ws), N.ptr(out), s)
 
     def _pack(self, X, S, score_scale, s):
         N.call("dsvgd_colmean", N.ptr(X), N.ld(X), self.n, self.d, N.ptr(self.mean_ws),
@@ -266,9 +290,9 @@ class PhiEngine(object):
         lds = N.ld(S) if S is not None else self.d
         if S is not None:
             assert S.shape == (self.n, self.d)
-        N.call("dsvgd_pack", N.ptr(X), N.ld(X), N.ptr(S), lds, float(score_scale),
+        N.call("dsvgd_pack_h2", N.ptr(X), N.ld(X), N.ptr(S), lds, float(score_scale),
                N.ptr(self.mean), self.n, self.d, self.Y.shape[0], N.ptr(self.Y), self.ldy,
-               N.ptr(self.norms), s)
+               N.ptr(self.norms), *self._maxima(), s)
 
     def distances(self, median=False):
         """D for the owned rows.  median=True also does the select's first
@@ -285,8 +309,7 @@ class PhiEngine(object):
             st, mode = self.state.ptr, SEL_HIST
         if self.gram_gemm == "h2" and self.d > self.DIRECT_MAX_D:
             with span(self.timer, "rowsplit"):
-                N.call("dsvgd_h2_colscale", N.ptr(self.Y), self.ldy, self.n_pad, self.dp,
-                       N.ptr(self.scale_ws), N.ptr(self.xscale), s)
+                self._scales(self.dp, self.xscale, s)
                 tsc = N.ptr(self.xscale) + 4 * 2 * self.dp        # [t, 1/t]
                 N.call("dsvgd_h2_rowsplit", N.ptr(self.Y), self.ldy, self.n_pad, self.dp,
                        self.gram_rows, self.dp, tsc, N.ptr(self.Yg), s)
@@ -393,8 +416,7 @@ class PhiEngine(object):
             return
         if self.phi_gemm == "h2":
             with span(self.timer, "ysplit"):
-                N.call("dsvgd_h2_colscale", N.ptr(self.Y), self.ldy, self.n_pad, self.ldy,
-                       N.ptr(self.scale_ws), N.ptr(self.yscale), s)
+                self._scales(self.ldy, self.yscale, s)
                 N.call("dsvgd_h2_ysplit", N.ptr(self.Y), self.ldy, self.n_pad,
                        N.ptr(self.yscale), N.ptr(self.Yx), s)
             with span(self.timer, "phi_mm"):

@@ -105,6 +105,17 @@ int dsvgd_colmean(const float* X, int64_t ldx, int64_t n, int64_t d, float* part
 int dsvgd_pack(const float* X, int64_t ldx, const float* S, int64_t lds, float score_scale,
                const float* mean, int64_t n, int64_t d, int64_t rows_pad, float* Y, int64_t ldy,
                float* norms, void* stream);
+/* dsvgd_pack + the FmtH2 column maxima of what it writes (ldy <=
+ * dsvgd_pack_max_ldy() = 2048, i.e. d <= 1024): partial (uint32,
+ * dsvgd_pack_blocks(rows_pad) x ldy) and gmax (2 x that many blocks), the
+ * input of dsvgd_h2_scales -- the scales without a second pass over Y.  With X
+ * NULL only the S half's maxima are (re)written, so pack(X) then pack(NULL, S)
+ * leaves the maxima of the whole Y.  partial = gmax = NULL: dsvgd_pack. */
+int64_t dsvgd_pack_blocks(int64_t rows_pad);
+int64_t dsvgd_pack_max_ldy(void);
+int dsvgd_pack_h2(const float* X, int64_t ldx, const float* S, int64_t lds, float score_scale,
+                  const float* mean, int64_t n, int64_t d, int64_t rows_pad, float* Y, int64_t ldy,
+                  float* norms, uint32_t* partial, uint32_t* gmax, void* stream);
 
 /* ---- pairwise squared distances ---------------------------------------- */
 /* D[i][j] = ||y_i - y_j||^2 for the owned row block i in [row0, row0+m) of Y
@@ -250,6 +261,11 @@ int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, in
 size_t dsvgd_h2_colscale_workspace_floats(int64_t rows, int64_t cols);
 int dsvgd_h2_colscale(const float* A, int64_t lda, int64_t rows, int64_t cols, float* ws,
                       float* scale, void* stream);
+/* dsvgd_h2_colscale's output over Y's first cols columns (cols = dp: the X
+ * half; cols = ldy: all of Y), bit-identical, from dsvgd_pack_h2's maxima
+ * (nb = dsvgd_pack_blocks(rows_pad)). */
+int dsvgd_h2_scales(const uint32_t* partial, const uint32_t* gmax, int64_t nb, int64_t ldy,
+                    int64_t cols, int64_t dp, float* scale, void* stream);
 /* fp16 images (dsvgd_h2_image_bytes(rows, cols) bytes, 16-byte aligned):
  * ysplit: Yh[kstep][part][column][16] of colscale[c] * Y[16 kstep + k][c]
  * (the NN engine's B operand, rows a multiple of 16); rowsplit:

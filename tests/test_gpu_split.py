@@ -135,6 +135,75 @@ def test_h2_images_reconstruct_fp32(rows, ldy):
     assert float(sc[7]) == 1.0 and float(sc[2 * ldy]) == 1.0
 
 
+@pytest.mark.parametrize("n,d,ldx,special", [(1000, 64, 64, None), (777, 100, 101, "zero"),
+                                             (300, 3, 3, "inf"), (2100, 1024, 1024, "nan"),
+                                             (129, 250, 252, None)])
+def test_pack_maxima_match_colscale(n, d, ldx, special):
+    """dsvgd_pack_h2 (pack + the FmtH2 column maxima) then dsvgd_h2_scales:
+    Y / norms as the numpy restatement of dsvgd_pack, scales bit-identical to
+    dsvgd_h2_colscale's over the same Y -- after pack(X, S), and after pack(X)
+    + pack(NULL, S) (the scores arriving after the distance stage); zero and
+    non-finite columns; unaligned row strides (element-load path)."""
+    from dsvgd import _native as N
+    lib = N.load()
+    s = N.stream(torch.device(DEV))
+    rs = np.random.RandomState(n + d)
+    X = (rs.randn(n, ldx) * np.exp(rs.uniform(-6, 6, ldx))).astype(np.float32)
+    S = (rs.randn(n, ldx) * np.exp(rs.uniform(-6, 6, ldx))).astype(np.float32)
+    if special == "zero":
+        X[:, 5] = 1.25                                # centred: an all-zero column
+        S[:, 9] = 0.0
+    elif special == "inf":
+        S[7, 1] = np.inf
+    elif special == "nan":
+        X[3, 600] = np.nan
+    dp, n_pad = lib.dsvgd_dp(d), lib.dsvgd_pad128(n)
+    ldy = lib.dsvgd_ldy(dp)
+    rows = n_pad + 128
+    nb = lib.dsvgd_pack_blocks(rows)
+    Xg, Sg = gpu(X)[:, :d], gpu(S)[:, :d]
+    mean = torch.empty(d, device=DEV)
+    mws = torch.empty(lib.dsvgd_colmean_workspace_floats(n, d), device=DEV)
+    N.call("dsvgd_colmean", N.ptr(Xg), ldx, n, d, N.ptr(mws), N.ptr(mean), s)
+    ws = torch.empty(lib.dsvgd_h2_colscale_workspace_floats(n_pad, ldy), device=DEV)
+    for split_scores in (False, True):
+        Y = torch.full((rows, ldy), 7.0, device=DEV)  # every entry must be written
+        norms = torch.empty(rows, device=DEV)
+        part = torch.full((nb * ldy,), -1, dtype=torch.int32, device=DEV)
+        gmax = torch.full((2 * nb,), -1, dtype=torch.int32, device=DEV)
+        args = (N.ptr(mean), n, d, rows, N.ptr(Y), ldy)
+        if split_scores:
+            N.call("dsvgd_pack_h2", N.ptr(Xg), ldx, None, d, 1.0, *args, N.ptr(norms),
+                   N.ptr(part), N.ptr(gmax), s)
+            N.call("dsvgd_pack_h2", None, d, N.ptr(Sg), ldx, 0.5, *args, None,
+                   N.ptr(part), N.ptr(gmax), s)
+        else:
+            N.call("dsvgd_pack_h2", N.ptr(Xg), ldx, N.ptr(Sg), ldx, 0.5, *args, N.ptr(norms),
+                   N.ptr(part), N.ptr(gmax), s)
+        got = {}
+        for cols in (dp, ldy):
+            ref = torch.empty(2 * cols + 2, device=DEV)
+            out = torch.empty(2 * cols + 2, device=DEV)
+            N.call("dsvgd_h2_colscale", N.ptr(Y), ldy, n_pad, cols, N.ptr(ws), N.ptr(ref), s)
+            N.call("dsvgd_h2_scales", N.ptr(part), N.ptr(gmax), nb, ldy, cols, dp, N.ptr(out), s)
+            got[cols] = (ref, out)
+        torch.cuda.synchronize()
+        Yc = Y.cpu().numpy()
+        mc = mean.cpu().numpy()
+        exp = np.zeros((rows, ldy), np.float32)
+        exp[:n, :d] = X[:, :d] - mc[None, :]
+        exp[:n, dp:dp + d] = np.float32(0.5) * S[:, :d]
+        np.testing.assert_array_equal(Yc, exp)
+        nr = (exp[:, :d].astype(np.float64) ** 2).sum(1)
+        got_n = norms.cpu().numpy()
+        fin = np.isfinite(nr)
+        np.testing.assert_allclose(got_n[fin], nr[fin], rtol=1e-5, atol=1e-30)
+        assert np.all(got_n[rows - 128:] == 0.0)
+        for cols, (ref, out) in got.items():
+            np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32),
+                                          ref.cpu().numpy().view(np.uint32))
+
+
 def _engines(X, S, h, split, m=None, row0=0):
     """phi and the raw (KY, rowsum) of one step through the f32 engine and `split`."""
     out = {}
@@ -176,7 +245,7 @@ def _ky_errors(res, split):
 @pytest.mark.parametrize("split", SPLIT)
 @pytest.mark.parametrize("n,d,h", [(300, 20, 5.0), (1000, 64, None), (2048, 256, None),
                                    (513, 100, 40.0), (4096, 3, None), (1500, 1024, None),
-                                   (777, 500, None)])
+                                   (777, 500, None), (700, 1100, None)])
 def test_phi_mm_split_matches_f32_engine_and_oracle(split, n, d, h):
     rs = np.random.RandomState(n + d)
     X = rs.randn(n, d).astype(np.float32)
