@@ -136,6 +136,21 @@ __device__ __forceinline__ void mfma_products(const typename F::V8 (&a)[TM][F::P
   for (int mi = 0; mi < TM; ++mi) acc[mi] = mfma_fmt<F>(a[mi][0], b[0], acc[mi]);
 }
 
+// the same products with the operands' MFMA roles exchanged: acc[mi] holds
+// the TRANSPOSED 32x32 tile (lane = a's row, registers = b's rows), same
+// products in the same order
+template <class F, int TM>
+__device__ __forceinline__ void mfma_products_tr(const typename F::V8 (&a)[TM][F::P],
+                                                 const typename F::V8 (&b)[F::P], f32x16* acc) {
+  static_assert(F::P == 2, "the transposed form is the FmtH2 Gram's");
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) acc[mi] = mfma_fmt<F>(b[0], a[mi][1], acc[mi]);
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) acc[mi] = mfma_fmt<F>(b[1], a[mi][0], acc[mi]);
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) acc[mi] = mfma_fmt<F>(b[0], a[mi][0], acc[mi]);
+}
+
 // byte offset of (row or column x, 16-B half h) inside a part image
 __device__ __forceinline__ int x3_off(int x, int h) { return x * 32 + ((h ^ ((x >> 3) & 1)) << 4); }
 
@@ -706,7 +721,11 @@ struct NNX3Tile {
 // are in acc16[4][2 TN] (16x16 layout) and both images must be unswizzled.
 // KS: 16-deep image K-steps per ring stage (one barrier per stage): 2 halves
 // the barriers per tile at twice the stage size.
-template <int TM, int TN, int WM, int WN, int NS = 3, bool M16 = false, class F = FmtX3, int KS = 1>
+// TR: accumulate the transposed tile (mfma_products_tr): acc[mi][ni] lane l
+// holds row 32 mi + (l & 31), registers the columns c_row(r, l) of 32 ni --
+// four adjacent columns of one row per register quad.
+template <int TM, int TN, int WM, int WN, int NS = 3, bool M16 = false, class F = FmtX3, int KS = 1,
+          bool TR = false>
 struct NTX3Tile {
   static constexpr int TM_ = TM, TN_ = TN, WM_ = WM, WN_ = WN;
   static constexpr bool M16_ = M16;
@@ -833,7 +852,10 @@ struct NTX3Tile {
         f32x16 c[TM];
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi) c[mi] = acc[mi][ni];
-        mfma_products<F, TM>(a, b, c);
+        if constexpr (TR)
+          mfma_products_tr<F, TM>(a, b, c);
+        else
+          mfma_products<F, TM>(a, b, c);
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = c[mi];
       }

@@ -96,7 +96,9 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
       const int cl = cbase + ni * 32 + (lane & 31);
       const int rb = rbase + mi * 32 + h4;  // this lane's first row in the sub-tile
       const float nj = scol[cl];
-      float* const dp0 = Dtile + (cl >> 4) * kPanelElems + (cl & 15) + rb * 16;
+      // uniform tile base + zero-extended 32-bit lane offset: the SGPR-base
+      // store form, no per-lane 64-bit address arithmetic
+      float* const dp0 = Dtile + (uint32_t)((cl >> 4) * kPanelElems + (cl & 15) + rb * 16);
       float v[16];
       if (interior) {
 #pragma unroll
@@ -122,7 +124,7 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
         if (kSqEpi < 2 || v[r] != v[r])  // streamed out: nt, so D does not evict the Gram operands from L2
           __builtin_nontemporal_store(v[r], dp0 + (r & 3) * 16 + (r >> 2) * 128);
       if (mirror && mirror_store && (kSqEpi == 0 || v[0] != v[0])) {  // D[j][i]: 4 consecutive i per register quad -> 16-byte stores
-        float* const mp0 = Dmir + (int64_t)cl * 16 + ((rbase >> 4) + mi * 2) * kPanelElems + h4;
+        float* const mp0 = Dmir + (uint32_t)(cl * 16 + ((rbase >> 4) + mi * 2) * kPanelElems + h4);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           *reinterpret_cast<f32x4*>(mp0 + (q >> 1) * kPanelElems + 8 * (q & 1)) =
@@ -143,6 +145,101 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
         for (int r = 0; r < 16; ++r) tile.acc[mi][ni][r] = 0.f;
       }
     }
+  if (smode == kSelBracket) sw.finish(sl, slot, mirror);
+}
+
+// D stores of the transposed epilogue: 16 bytes per lane through a buffer
+// descriptor on the tile, cache policy kDStorePolicy (DSVGD_D_STORE_POLICY,
+// A/B: 0 plain, 2 nt, 16 sc1 = written through and dropped from L2).
+// Measured (profiles/r5n_gram_tr_ab.log, S = 1 / S = 8 rank share): the
+// shipped form 4.80 / 1.17 ms; transposed + nt 5.53 / 1.45, + plain 5.80 /
+// 1.42, + sc1 8.93 / 2.08 -- the transposed bracket kernels spill (180
+// scratch ops) and sc1 stores pay a fabric write each; kept as an A/B only.
+#ifndef DSVGD_D_STORE_POLICY
+#define DSVGD_D_STORE_POLICY 2
+#endif
+constexpr int kDStorePolicy = DSVGD_D_STORE_POLICY;
+// DSVGD_GRAM_TR (A/B): 1 = the FmtH2 Gram on transposed accumulators
+// (sq_epilogue_tr) where no mirror tile is stored, 0 = sq_epilogue
+// everywhere (shipped: see above)
+#ifndef DSVGD_GRAM_TR
+#define DSVGD_GRAM_TR 0
+#endif
+
+// sq_epilogue on transposed accumulators (NTX3Tile TR): lane l holds row
+// rbase + 32 mi + (l & 31) of the tile and, per register quad q, the four
+// adjacent columns cbase + 32 ni + 8 q + 4 (l >> 5) + 0..3 -- one 16-byte
+// store into the panel layout (a panel row is 16 adjacent columns).  Same
+// values (the norm sum is commutative, the MFMA products the same), same
+// select accounting; no mirror stores (launches that need them run sq_epilogue).
+template <bool SYM, int smode, class Tile, int NI, class SW>
+__device__ __forceinline__ void sq_epilogue_tr(Tile& tile, int bi, int bj, int64_t row0,
+                                               int64_t m, int64_t n, int64_t n_pad,
+                                               float* __restrict__ D, const float* srow,
+                                               const float* scol, int rbase, int cbase,
+                                               WindowHist& wh, uint32_t* shist, SW& sw,
+                                               const SlotLayout& sl, int64_t slot, int r0t,
+                                               float c2) {
+  const int lane = threadIdx.x & 63, il = lane & 31, h4 = 4 * (lane >> 5);
+  const bool mirror = SYM && bi + r0t != bj;
+  const int64_t i0 = (int64_t)bi * 128, j0 = (int64_t)bj * 128;
+  const uint32_t weight = mirror ? 2u : 1u;
+  const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(D + ((int64_t)bi * (n_pad >> 4) + (int64_t)bj * 8) * kPanelElems), (short)0,
+      0x7fffffff, 0x00020000);
+  const bool interior = (row0 + i0 + 128 <= j0 || j0 + 128 <= row0 + i0) && i0 + 128 <= m &&
+                        j0 + 128 <= n;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+    const int rl = rbase + mi * 32 + il;  // this lane's row in the tile
+    const float ni_ = srow[rl];
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int cb = cbase + ni * 32;  // the sub-tile's first column
+      f32x4 nc[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) nc[q] = *reinterpret_cast<const f32x4*>(scol + cb + 8 * q + h4);
+      float v[16];
+      if (interior) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          v[r] = fmaxf(0.f, (ni_ + nc[r >> 2][r & 3]) - c2 * tile.acc[mi][ni][r]);
+      } else {
+        const bool rowok = i0 + rl < m;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int cl = cb + 8 * (r >> 2) + h4 + (r & 3);
+          float x;
+          if (rowok && j0 + cl < n)
+            x = (row0 + i0 + rl == j0 + cl)
+                    ? 0.f
+                    : fmaxf(0.f, (ni_ + nc[r >> 2][r & 3]) - c2 * tile.acc[mi][ni][r]);
+          else
+            x = INFINITY;
+          v[r] = x;
+        }
+      }
+      // panel (cb >> 4) + (q >> 1), row rl, columns 8 (q & 1) + h4 .. + 3
+      const int off = 4 * ((cb >> 4) * kPanelElems + rl * 16 + h4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4, (f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]})),
+            rD, off + 4 * ((q >> 1) * kPanelElems + 8 * (q & 1)), 0, kDStorePolicy);
+      if (smode == kSelHist) {
+        if (mi == 0 && ni == 0) wh.init(v[0]);
+        hist_account(wh, v, weight, shist);
+      } else if (smode == kSelBracket) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          sw.add(v[r]);
+          if ((r + 1) % kStageDepth == 0) sw.flush();
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tile.acc[mi][ni][r] = 0.f;
+    }
+  }
   if (smode == kSelBracket) sw.finish(sl, slot, mirror);
 }
 
@@ -344,14 +441,15 @@ __global__ __launch_bounds__(256, 2) void sqdist_persistent_kernel(
 // apart, so one block's epilogue (D stores, select accounting) runs beside
 // the other's MFMAs instead of every SIMD idling its MFMA pipe through it.
 // NS: LDS ring stages (2: a K-step's DMA has one K-step to land; 3: two).
-template <bool SYM, int smode, bool M16 = true, class F = FmtX3, int WN = 2, int NS = 2, int KS = 1>
+template <bool SYM, int smode, bool M16 = true, class F = FmtX3, int WN = 2, int NS = 2, int KS = 1,
+          bool TR = false>
 __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
     const typename F::E* __restrict__ Yg, int64_t img_rows, const float* __restrict__ norms,
     int64_t row0, int64_t m, int64_t n, int64_t n_pad, int nk, float* __restrict__ D,
     dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int epi, int64_t total_tiles,
     int layout, int Tm2, int Tc2, int bj_off, int r0t, int64_t slot_base, int64_t ns_total,
     const float* __restrict__ tsc) {
-  using GramX3WTile = NTX3Tile<2, 4, 4, WN, NS, M16, F, KS>;
+  using GramX3WTile = NTX3Tile<2, 4, 4, WN, NS, M16, F, KS, TR>;
   constexpr int kT = GramX3WTile::kThreads, kUnits = 2 / WN;  // units per 256-tile
   constexpr int kBN = GramX3WTile::BN;                         // 256 or 128 columns
   const float c2 = F::P == 3 ? 2.f : 2.f * tsc[1] * tsc[1];
@@ -365,7 +463,10 @@ __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
   // this launch: Tm2 x Tc2 256-tiles, global column tiles from bj_off
   // (SYM: the triangle of a Tm2 x Tm2 square; r0t = its row0 / 128)
   const int Tm = (int)(roundup128(m) / 128), Tn = (int)(n_pad / 128);  // 128-tiles
-  const int t = threadIdx.x, w = t >> 6, wr = w / WN, wc = w % WN;
+  // the wave index made provably uniform: tile, slot and D-tile bases derived
+  // from it stay in SGPRs (stores take the SGPR-base + 32-bit offset form)
+  const int t = threadIdx.x, w = __builtin_amdgcn_readfirstlane(t >> 6), wr = w / WN,
+            wc = w % WN;
   const int64_t total = total_tiles * kUnits;
   const int64_t x = blockIdx.x % kXcds, u = blockIdx.x / kXcds, U = gridDim.x / kXcds;
   const int64_t q = total / kXcds, rr = total % kXcds;
@@ -424,7 +525,11 @@ __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
       tile.zero();
       if (smode == kSelBracket) sw.finish(sl, slot, false);
     } else {
-      if constexpr (M16)
+      if constexpr (TR)
+        sq_epilogue_tr<SYM, smode, GramX3WTile, 4, SW>(
+            tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128, snorm + 256 + wc * 128,
+            (wr & 1) * 64, 0, wh, shist, sw, sl, slot, r0t, c2);
+      else if constexpr (M16)
         sq_epilogue16<SYM, smode>(tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128,
                                   snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl,
                                   slot, epi, layout == 0, r0t);
@@ -541,13 +646,16 @@ int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, 
     // FmtX3: whole 256-tiles, 2-stage ring
     constexpr int WN = (F::P == 3 || kGramH2Form != 1) ? 2 : 1;
     constexpr int NS = (F::P == 2 && WN == 2 && KS == 1) ? 3 : 2;
+    // FmtH2: transposed accumulators (16-byte D stores, sqdist_x3w TR) except
+    // on launches that store mirror tiles (the full layout's triangle)
+    constexpr bool TRF = F::P == 2 && DSVGD_GRAM_TR;
     if ((rc = persistent_blocks(
              reinterpret_cast<const void*>(&sqdist_x3w_kernel<true, SM, F::P == 3, F, WN, NS, KS>), &bs,
              256 * WN)))
       return rc;
     if ((rc = persistent_blocks(
-             reinterpret_cast<const void*>(&sqdist_x3w_kernel<false, SM, F::P == 3, F, WN, NS, KS>), &bn,
-             256 * WN)))
+             reinterpret_cast<const void*>(&sqdist_x3w_kernel<false, SM, F::P == 3, F, WN, NS, KS, TRF>),
+             &bn, 256 * WN)))
       return rc;
     const int Tn2 = (int)((n_pad / 128 + 1) / 2), Tm2 = (int)((m_pad / 128 + 1) / 2);
     struct Part {
@@ -575,14 +683,16 @@ int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, 
     for (int i = 0; i < np; ++i) {
       const Part& P = parts[i];
       const int lay = sym ? layout : 0;
-#define DSVGD_X3W(SY, M, B, LAY, R0T)                                                          \
-  hipLaunchKernelGGL((sqdist_x3w_kernel<SY, SM, M, F, WN, NS, KS>), dim3((unsigned)B), dim3(256 * WN), 0, s, Yg, \
-                     img, norms, row0, m, n, n_pad, nk, D, st, cand, epi, P.total, LAY, P.tm2,   \
-                     P.tc2, P.bj_off, R0T, base, ns_total, tsc)
-      if (P.sym)
-        DSVGD_X3W(true, F::P == 3, bs, lay, P.r0t);
+#define DSVGD_X3W(SY, M, B, LAY, R0T, TR)                                                      \
+  hipLaunchKernelGGL((sqdist_x3w_kernel<SY, SM, M, F, WN, NS, KS, TR>), dim3((unsigned)B),       \
+                     dim3(256 * WN), 0, s, Yg, img, norms, row0, m, n, n_pad, nk, D, st, cand, epi, \
+                     P.total, LAY, P.tm2, P.tc2, P.bj_off, R0T, base, ns_total, tsc)
+      if (P.sym && lay == 0)  // mirror stores
+        DSVGD_X3W(true, F::P == 3, bs, lay, P.r0t, false);
+      else if (P.sym)
+        DSVGD_X3W(true, F::P == 3, bs, lay, P.r0t, TRF);
       else
-        DSVGD_X3W(false, F::P == 3, bn, 0, 0);
+        DSVGD_X3W(false, F::P == 3, bn, 0, 0, TRF);
 #undef DSVGD_X3W
       if ((rc = check_launch("sqdist_x3w"))) return rc;
       base += P.total * 8;
