@@ -724,8 +724,12 @@ struct NNX3Tile {
 // TR: accumulate the transposed tile (mfma_products_tr): acc[mi][ni] lane l
 // holds row 32 mi + (l & 31), registers the columns c_row(r, l) of 32 ni --
 // four adjacent columns of one row per register quad.
+// WC: wave-contiguous DMA chunks -- wave w fills the 1 KiB chunks [w C,
+// (w + 1) C) of a stage (C = kChunksPerWave), so once every wave is past the
+// barrier that retires a stage, each wave's own C KiB of it stay untouched
+// until that wave issues its next DMA into it: private scratch in between.
 template <int TM, int TN, int WM, int WN, int NS = 3, bool M16 = false, class F = FmtX3, int KS = 1,
-          bool TR = false>
+          bool TR = false, bool WC = false>
 struct NTX3Tile {
   static constexpr int TM_ = TM, TN_ = TN, WM_ = WM, WN_ = WN;
   static constexpr bool M16_ = M16;
@@ -779,8 +783,30 @@ struct NTX3Tile {
 
   // K-step kb of A (image rows from rA's base, mA image rows per part) and B
   // into stage st
+  static constexpr int kChunks = kStage / 1024, kChunksPerWave = kChunks / (kThreads / 64);
+  static_assert(!WC || (SA % 1024 == 0 && SB % 1024 == 0 && kChunks % (kThreads / 64) == 0),
+                "wave-contiguous chunks: whole 1 KiB chunks per wave");
+
   __device__ __forceinline__ void dma(char* st, __amdgpu_buffer_rsrc_t rA, int64_t mA,
                                       __amdgpu_buffer_rsrc_t rB, int64_t mB, int64_t kb) {
+    if constexpr (WC) {
+      // chunk c = w C + u: sub-step c / (kSub / 1K), then A or B, then 64
+      // consecutive 16-byte units of that image slice (as below)
+      const int lane = threadIdx.x & 63;
+      const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+#pragma unroll
+      for (int u = 0; u < kChunksPerWave; ++u) {
+        const int c = w * kChunksPerWave + u;
+        const int q = c / (kSub / 1024), r = c % (kSub / 1024);
+        const int64_t ki = kb * KS + q;
+        const bool isA = r < SA / 1024;
+        const int rr = isA ? r : r - SA / 1024, BX = isA ? BM : BN;
+        const int64_t mX = isA ? mA : mB;
+        const int f = rr * 64 + lane, pp = f / (BX * 2), in = f % (BX * 2);
+        dma16(isA ? rA : rB, st + c * 1024, (int)(pp * mX * 32 + in * 16), (int)(ki * P * mX * 32));
+      }
+      return;
+    }
     const int t = threadIdx.x, wbase = t & ~63;
 #pragma unroll
     for (int q = 0; q < KS; ++q) {
@@ -801,7 +827,10 @@ struct NTX3Tile {
   }
 
   // a0: image row of A's row 0, mod 16 (the image swizzles on the absolute
-  // row; a row block may start off a 16-row boundary)
+  // row; a row block may start off a 16-row boundary).  FIRST (32x32 form):
+  // the tile's first stage -- its first MFMAs take C = 0 instead of the
+  // accumulators, so no pass re-zeroes them between tiles.
+  template <bool FIRST = false>
   __device__ __forceinline__ void compute(const char* st, int wm, int wn, int a0 = 0) {
     if (M16) {  // lane (rr = l & 15, g = l >> 4): k-slot g >> 1 picks the part, g & 1 the half
       const int lane = threadIdx.x & 63, rr = lane & 15, g = lane >> 4, hh = g & 1, sl = g >> 1;
@@ -851,7 +880,7 @@ struct NTX3Tile {
                                               x3_off(wn * 32 * TN + ni * 32 + r, h));
         f32x16 c[TM];
 #pragma unroll
-        for (int mi = 0; mi < TM; ++mi) c[mi] = acc[mi][ni];
+        for (int mi = 0; mi < TM; ++mi) c[mi] = (FIRST && q == 0) ? f32x16{} : acc[mi][ni];
         if constexpr (TR)
           mfma_products_tr<F, TM>(a, b, c);
         else

@@ -144,6 +144,7 @@ struct SlotWriter {
       cnt += (uint32_t)__popcll(bal);
     }
   }
+  static constexpr int kDepth = 1 << 30;  // flush() is a no-op
   __device__ __forceinline__ void flush() {}
   __device__ __forceinline__ void finish(const SlotLayout& L, int64_t slot, bool weight2) {
     const uint32_t b = below;
@@ -160,15 +161,19 @@ struct SlotWriter {
 // private list in LDS (entry k of lane l at stage[64 k + l]: distinct banks
 // whatever the lanes' positions) and advances the lane's position only for
 // values in [lo, hi]; an out-of-range value is overwritten by the next one.
-// flush() -- after at most kStageDepth (8) add()s -- moves the lists to the slot
-// in lane order (one wave prefix sum of the positions).  Below-counts are
-// per lane, summed at finish().  Per value: a subtract, a shift-add, a
-// compare, an LDS store and a conditional add (the ballot form compiled to
-// ~25 instructions with exec-mask branches per value).
+// flush() -- after at most DEPTH add()s -- moves the lists to the slot in
+// lane order (one wave prefix sum of the positions).  Below-counts are per
+// lane, summed at finish().  Per value: a subtract, a shift-add, a compare,
+// an LDS store and a conditional add (the ballot form compiled to ~25
+// instructions with exec-mask branches per value).  DEPTH 8 on a list area
+// of its own; 32 on the retired ring stage of the 256-tile Gram (a wave's own
+// chunks, NTX3Tile WC): a quarter of the flushes.
 constexpr int kStageDepth = 8;
-struct SlotWriterLds {
+template <int DEPTH = kStageDepth>
+struct SlotWriterLdsT {
+  static constexpr int kDepth = DEPTH;
   float* dst = nullptr;
-  float* stage = nullptr;  // this wave's 64 x kStageDepth floats
+  float* stage = nullptr;  // this wave's 64 x DEPTH floats
   uint32_t cnt = 0;        // wave-uniform: entries in [lo, hi] flushed so far
   uint32_t cap = 0;
   uint32_t below = 0;      // per lane
@@ -217,6 +222,8 @@ struct SlotWriterLds {
     }
   }
 };
+
+using SlotWriterLds = SlotWriterLdsT<>;
 
 // slots of a wave that has no values (padding blocks): empty counts
 __device__ __forceinline__ void slot_clear(const SlotLayout& L, int64_t slot) {

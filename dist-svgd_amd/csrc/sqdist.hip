@@ -52,6 +52,28 @@ constexpr int kGramDmaProbe = DSVGD_GRAM_DMA_PROBE;
 #define DSVGD_GRAM_KS 2
 #endif
 constexpr int kGramKS = DSVGD_GRAM_KS;
+// DSVGD_GRAM_WC (A/B): 1 = the bracket candidates of the 256-tile FmtH2 Gram
+// staged 32 deep in the wave's own chunks of the just-retired ring stage
+// (NTX3Tile WC, SlotWriterLdsT<32>), 0 = 8 deep in an LDS area of their own.
+// Shipped 1: S = 1 4.83 -> 4.49 ms, S = 8 1.21 -> 1.14 (profiles/r5o_gram_ab.log)
+#ifndef DSVGD_GRAM_WC
+#define DSVGD_GRAM_WC 1
+#endif
+constexpr bool kGramWC = DSVGD_GRAM_WC;
+// DSVGD_GRAM_ZEROC (A/B): 1 = a tile's first MFMAs take C = 0 (no re-zeroing
+// pass over the 128 accumulators per lane), 0 = the epilogue re-zeroes them
+// (shipped 0: the compiler materialises the zero operands, 300-600 spills)
+#ifndef DSVGD_GRAM_ZEROC
+#define DSVGD_GRAM_ZEROC 0
+#endif
+constexpr bool kGramZeroC = DSVGD_GRAM_ZEROC;
+// DSVGD_GRAM_NPF (A/B): 1 = a tile's 512 norms loaded into registers at its
+// first stage (latency under the MFMAs), 0 = loaded at its epilogue (shipped
+// 0: 4.41 vs 4.49 ms with the prefetch, r5o)
+#ifndef DSVGD_GRAM_NPF
+#define DSVGD_GRAM_NPF 0
+#endif
+constexpr bool kGramNpf = DSVGD_GRAM_NPF;
 
 using GramTile = NTTile<2, 2, 2, 2>;  // 128 x 128 block, 4 waves of 64 x 64
 
@@ -137,7 +159,7 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           sw.add(v[r]);
-          if ((r + 1) % kStageDepth == 0) sw.flush();  // (LDS-staged writer's list depth)
+          if (((mi * NI + ni) * 16 + r + 1) % SW::kDepth == 0) sw.flush();  // list depth
         }
       }
       if (ZERO) {
@@ -233,11 +255,13 @@ __device__ __forceinline__ void sq_epilogue_tr(Tile& tile, int bi, int bj, int64
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           sw.add(v[r]);
-          if ((r + 1) % kStageDepth == 0) sw.flush();
+          if (((mi * NI + ni) * 16 + r + 1) % SW::kDepth == 0) sw.flush();
         }
       }
+      if (!kGramZeroC) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) tile.acc[mi][ni][r] = 0.f;
+        for (int r = 0; r < 16; ++r) tile.acc[mi][ni][r] = 0.f;
+      }
     }
   }
   if (smode == kSelBracket) sw.finish(sl, slot, mirror);
@@ -449,7 +473,13 @@ __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
     dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int epi, int64_t total_tiles,
     int layout, int Tm2, int Tc2, int bj_off, int r0t, int64_t slot_base, int64_t ns_total,
     const float* __restrict__ tsc) {
-  using GramX3WTile = NTX3Tile<2, 4, 4, WN, NS, M16, F, KS, TR>;
+  // candidates staged in the retired ring stage (bracket mode, 32x32 form,
+  // 2-stage ring of 32-deep stages)
+  constexpr bool kWC = kGramWC && smode == kSelBracket && !M16 && NS == 2 && KS == 2 && WN == 2;
+  constexpr bool kZeroC = kGramZeroC && !M16;
+  using GramX3WTile = NTX3Tile<2, 4, 4, WN, NS, M16, F, KS, TR, kWC>;
+  static_assert(!kWC || GramX3WTile::kChunksPerWave * 1024 >= 64 * 32 * 4,
+                "32-deep candidate lists fit the wave's chunks");
   constexpr int kT = GramX3WTile::kThreads, kUnits = 2 / WN;  // units per 256-tile
   constexpr int kBN = GramX3WTile::BN;                         // 256 or 128 columns
   const float c2 = F::P == 3 ? 2.f : 2.f * tsc[1] * tsc[1];
@@ -458,7 +488,18 @@ __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
   __shared__ float snorm[256 + kBN];  // the unit's 256 row norms, then its column norms
   // bracket candidates staged per lane (SlotWriterLds) on the 32x32 form
   constexpr bool kLdsSlots = smode == kSelBracket && !M16;
-  __shared__ float scand[kLdsSlots ? (kT / 64) * 64 * kStageDepth : 1];
+  __shared__ float scand[kLdsSlots && !kWC ? (kT / 64) * 64 * kStageDepth : 1];
+  constexpr int kNR = (256 + kBN + kT - 1) / kT;  // norms per thread
+  float nreg[kNR];
+  // the norms of unit (BI, BJ): rows 256 BI.., then columns kBN BJ..
+  auto load_norms = [&](int BI, int BJ) {
+#pragma unroll
+    for (int i = 0; i < kNR; ++i) {
+      const int e = (int)threadIdx.x + i * kT;
+      const int64_t gi = e < 256 ? row0 + (int64_t)BI * 256 + e : (int64_t)BJ * kBN + e - 256;
+      nreg[i] = (e < 256 + kBN && gi < n_pad) ? norms[gi] : 0.f;
+    }
+  };
 
   // this launch: Tm2 x Tc2 256-tiles, global column tiles from bj_off
   // (SYM: the triangle of a Tm2 x Tm2 square; r0t = its row0 / 128)
@@ -504,20 +545,26 @@ __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
     tile.dma(stg, rA, img_rows, rB, img_rows, ks);
   };
 
-  // tile (L, BI, BJ) done: norms, per-sub-tile epilogue (re-zeroes the accumulators)
-  auto epilogue = [&](int64_t L, int BI, int BJ) {
-    for (int e = t; e < 256 + kBN; e += kT) {
-      const int64_t gi = e < 256 ? row0 + (int64_t)BI * 256 + e : (int64_t)BJ * kBN + e - 256;
-      snorm[e] = gi < n_pad ? norms[gi] : 0.f;
-    }
+  // tile (L, BI, BJ) done (its last stage retired from ring stage stg):
+  // norms, per-sub-tile epilogue
+  auto epilogue = [&](int64_t L, int BI, int BJ, int stg) {
+    if (!kGramNpf) load_norms(BI, BJ);
+#pragma unroll
+    for (int i = 0; i < kNR; ++i)
+      if (t + i * kT < 256 + kBN) snorm[t + i * kT] = nreg[i];
     __syncthreads();
     // this wave's 128-sub-tile
     const int bi = 2 * BI + (wr >> 1), bj = BJ * (kBN / 128) + wc;
     const int64_t slot = slot_base + L * (8 / kUnits) + w;
     WindowHist wh;
-    using SW = std::conditional_t<kLdsSlots, SlotWriterLds, SlotWriter>;
+    using SW = std::conditional_t<kWC, SlotWriterLdsT<32>,
+                                  std::conditional_t<kLdsSlots, SlotWriterLds, SlotWriter>>;
     SW sw;
-    if constexpr (kLdsSlots)
+    if constexpr (kWC)
+      sw.begin(st, sl, slot,
+               reinterpret_cast<float*>(smem + stg * GramX3WTile::kStage +
+                                        w * GramX3WTile::kChunksPerWave * 1024));
+    else if constexpr (kLdsSlots)
       sw.begin(st, sl, slot, scand + w * 64 * kStageDepth);
     else if (smode == kSelBracket)
       sw.begin(st, sl, slot);
@@ -534,7 +581,7 @@ __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
                                   snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl,
                                   slot, epi, layout == 0, r0t);
       else
-        sq_epilogue<SYM, smode, true, GramX3WTile, 4, SW>(
+        sq_epilogue<SYM, smode, !kZeroC, GramX3WTile, 4, SW>(
             tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128,
             snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl, slot, epi, layout == 0,
             r0t, c2);
@@ -581,13 +628,17 @@ __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
     }
     while (L < hi) {
       const int s2 = stage >= 1 ? stage - 1 : 2;  // (stage + 2) % 3
+      if (kGramNpf && ks == 0) load_norms(BI, BJ);
       if (L2 < hi) issue(smem + s2 * GramX3WTile::kStage, BI2, BJ2, ks2);
-      tile.compute(smem + stage * GramX3WTile::kStage, wr, wc, (int)(row0 & 15));
+      if (kZeroC && ks == 0)
+        tile.template compute<true>(smem + stage * GramX3WTile::kStage, wr, wc, (int)(row0 & 15));
+      else
+        tile.compute(smem + stage * GramX3WTile::kStage, wr, wc, (int)(row0 & 15));
       if (L2 < hi)
         GramX3WTile::template ring_barrier<GramX3WTile::kDmas>();
       else
         GramX3WTile::template ring_barrier<0>();
-      if (ks + 1 == nk) epilogue(L, BI, BJ);
+      if (ks + 1 == nk) epilogue(L, BI, BJ, stage);
       L = L1; BI = BI1; BJ = BJ1; ks = ks1;
       L1 = L2; BI1 = BI2; BJ1 = BJ2; ks1 = ks2;
       advance(L1, BI1, BJ1, ks1, L2, BI2, BJ2, ks2);
@@ -606,11 +657,15 @@ __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
         ksn = 0;
       }
       const bool more = Ln < hi;
+      if (kGramNpf && ks == 0) load_norms(BI, BJ);
       if (more) issue(smem + (stage ^ 1) * GramX3WTile::kStage, BIn, BJn, ksn);
-      tile.compute(smem + stage * GramX3WTile::kStage, wr, wc, (int)(row0 & 15));
+      if (kZeroC && ks == 0)
+        tile.template compute<true>(smem + stage * GramX3WTile::kStage, wr, wc, (int)(row0 & 15));
+      else
+        tile.compute(smem + stage * GramX3WTile::kStage, wr, wc, (int)(row0 & 15));
       GramX3WTile::template ring_barrier<0>();
       if (ks + 1 == nk) {
-        epilogue(L, BI, BJ);
+        epilogue(L, BI, BJ, stage);
         L = Ln;
         BI = BIn;
         BJ = BJn;
