@@ -325,7 +325,7 @@ struct NNX3Tile {
   // tile j0's B image -> LDS stage st
   __device__ __forceinline__ void dma_b(char* st, __amdgpu_buffer_rsrc_t rB, int64_t ldy,
                                         int64_t j0) {
-    const int t = threadIdx.x, wbase = t & ~63;
+    const int t = threadIdx.x, wbase = __builtin_amdgcn_readfirstlane(t >> 6) * 64;
     const int soB = (int)((j0 >> 4) * P * ldy * 32);
 #pragma unroll
     for (int u = 0; u < LB; ++u) {
@@ -347,12 +347,12 @@ struct NNX3Tile {
                                    (j0 & 127) * 16);
       const __amdgpu_buffer_rsrc_t rT =
           __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, 0x7fffffff, 0x00020000);
-      dma16<kDAux>(rT, raw + (t & ~63) * 16, (t >> 6) * kPanelElems * 4 + (t & 63) * 16, 0);
+      dma16<kDAux>(rT, raw + __builtin_amdgcn_readfirstlane(t >> 6) * 1024, (t >> 6) * kPanelElems * 4 + (t & 63) * 16, 0);
       return;
     }
 #pragma unroll
     for (int a = 0; a < AR; ++a)
-      dma16<kDAux>(rA, raw + a * kPanelElems * 4 + (t & ~63) * 16, (int)(a * prow) + t * 16,
+      dma16<kDAux>(rA, raw + a * kPanelElems * 4 + __builtin_amdgcn_readfirstlane(t >> 6) * 1024, (int)(a * prow) + t * 16,
                    (int)((j0 >> 4) * kPanelElems * 4));
   }
 
@@ -469,7 +469,7 @@ struct NNX3Tile {
   __device__ __forceinline__ void run(const float* __restrict__ Apanels, const typename F::E* __restrict__ Yx,
                                       int64_t ldy, int64_t k0, int64_t k1, float scale, char* smem,
                                       int64_t row_g0) {
-    const int w = threadIdx.x >> 6, wr = w / kCW, wc = w % kCW;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), wr = w / kCW, wc = w % kCW;
     rs = 0.f;
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi)
@@ -784,8 +784,9 @@ struct NTX3Tile {
   // K-step kb of A (image rows from rA's base, mA image rows per part) and B
   // into stage st
   static constexpr int kChunks = kStage / 1024, kChunksPerWave = kChunks / (kThreads / 64);
-  static_assert(!WC || (SA % 1024 == 0 && SB % 1024 == 0 && kChunks % (kThreads / 64) == 0),
-                "wave-contiguous chunks: whole 1 KiB chunks per wave");
+  static_assert(!WC || (SA % 1024 == 0 && SB % 1024 == 0 && kChunks % (kThreads / 64) == 0 &&
+                        BM % 32 == 0 && BN % 32 == 0),
+                "wave-contiguous chunks: whole 1 KiB chunks per wave and per part");
 
   __device__ __forceinline__ void dma(char* st, __amdgpu_buffer_rsrc_t rA, int64_t mA,
                                       __amdgpu_buffer_rsrc_t rB, int64_t mB, int64_t kb) {
@@ -798,16 +799,18 @@ struct NTX3Tile {
       for (int u = 0; u < kChunksPerWave; ++u) {
         const int c = w * kChunksPerWave + u;
         const int q = c / (kSub / 1024), r = c % (kSub / 1024);
-        const int64_t ki = kb * KS + q;
+        const int ki = (int)kb * KS + q;
         const bool isA = r < SA / 1024;
         const int rr = isA ? r : r - SA / 1024, BX = isA ? BM : BN;
-        const int64_t mX = isA ? mA : mB;
-        const int f = rr * 64 + lane, pp = f / (BX * 2), in = f % (BX * 2);
-        dma16(isA ? rA : rB, st + c * 1024, (int)(pp * mX * 32 + in * 16), (int)(ki * P * mX * 32));
+        const int mX = (int)(isA ? mA : mB);  // image offsets are 32-bit (< 2^31 bytes)
+        // a part is BX / 32 chunks: chunk rr = part rr / (BX / 32), 16-byte
+        // units (rr % (BX / 32)) 64 + lane -- all but lane * 16 wave-uniform
+        const int pp = rr / (BX / 32), in0 = (rr % (BX / 32)) * 64;
+        dma16(isA ? rA : rB, st + c * 1024, lane * 16, (ki * P + pp) * mX * 32 + in0 * 16);
       }
       return;
     }
-    const int t = threadIdx.x, wbase = t & ~63;
+    const int t = threadIdx.x, wbase = __builtin_amdgcn_readfirstlane(t >> 6) * 64;
 #pragma unroll
     for (int q = 0; q < KS; ++q) {
       const int64_t ki = kb * KS + q;  // image K-step
@@ -901,7 +904,7 @@ struct NTX3Tile {
   // image rows per part), B likewise; nk K-steps of 16.
   __device__ __forceinline__ void run(const __bf16* imgA, int64_t mA, const __bf16* imgB,
                                       int64_t mB, int nk, char* smem) {
-    const int w = threadIdx.x >> 6, wm = w / WN, wn = w % WN;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), wm = w / WN, wn = w % WN;
     const __amdgpu_buffer_rsrc_t rA =
         __builtin_amdgcn_make_buffer_rsrc((void*)imgA, (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t rB =
