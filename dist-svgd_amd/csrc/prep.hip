@@ -123,14 +123,20 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
 // Y[j] = [X[j]-mean (dp cols) | scale*S[j] (dp cols) | 0], norms[j] =
 // |X[j]-mean|^2, rows j >= n zero; with partial != nullptr also the FmtH2
 // column maxima of what it writes (h2.hip), so the scales need no second pass
-// over Y: partial[b][c] = max |Y[r][c]| over block b's kPackRows rows, and
+// over Y: partial[b][c] = max |Y[r][c]| over block b's rows (pack_rows_per_block), and
 // gmax[2b] / gmax[2b + 1] = the block's largest over the X half [0, dp) /
 // over [dp, ldy).  X == nullptr: the S half of rows < n only (its columns'
 // partials and gmax[2b + 1]).  One wave per row, 16-byte accesses: a lane
 // owns 4 adjacent columns of each 256-column pass (dp % 32 == 0, so a lane's
 // 4 never straddle the X / S boundary).
-constexpr int kPackRows = 64;  // rows per block, 16 per wave
-constexpr int kPackQ = 8;      // 256-column passes per row: ldy <= 2048
+constexpr int kPackQ = 8;  // 256-column passes per row: ldy <= 2048
+// rows per block: 64 (16 per wave) from ~64K rows, down to 4 (one per wave)
+// below ~4K -- a small pack is latency-bound, its waves must not loop
+__host__ __device__ inline int64_t pack_rows_per_block(int64_t rows_pad) {
+  int64_t r = 4;
+  while (r < 64 && rows_pad / (2 * r) >= 1024) r *= 2;
+  return r;
+}
 
 template <bool VX, bool VS>  // 16-byte loads of X / S rows (aligned, ld % 4 == 0)
 __global__ __launch_bounds__(256) void pack_kernel(
@@ -141,8 +147,9 @@ __global__ __launch_bounds__(256) void pack_kernel(
   extern __shared__ uint32_t red[];  // [4 waves][ldy]
   __shared__ uint32_t gred[4][2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t r0 = (int64_t)blockIdx.x * kPackRows;
-  const int64_t r1 = min(r0 + kPackRows, rows_pad);
+  const int64_t rpb = pack_rows_per_block(rows_pad);
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = min(r0 + rpb, rows_pad);
   const int64_t c_lo = X ? 0 : dp, c_hi = X ? ldy : 2 * dp;
   uint32_t mx[kPackQ][4];
 #pragma unroll
@@ -335,7 +342,10 @@ int dsvgd_colmean(const float* X, int64_t ldx, int64_t n, int64_t d, float* part
   return check_launch("colsum_final");
 }
 
-int64_t dsvgd_pack_blocks(int64_t rows_pad) { return (rows_pad + kPackRows - 1) / kPackRows; }
+int64_t dsvgd_pack_blocks(int64_t rows_pad) {
+  const int64_t r = pack_rows_per_block(rows_pad);
+  return (rows_pad + r - 1) / r;
+}
 int64_t dsvgd_pack_max_ldy(void) { return 256 * kPackQ; }
 
 int dsvgd_pack_h2(const float* X, int64_t ldx, const float* S, int64_t lds, float score_scale,

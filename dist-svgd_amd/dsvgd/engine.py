@@ -205,7 +205,8 @@ class PhiEngine(object):
             self.yscale = torch.empty(2 * self.ldy + 2, **f32)
         # d <= 1024: pack writes the column maxima the scales come from
         # (dsvgd_pack_h2 / dsvgd_h2_scales); wider, a separate pass over Y
-        self.fused_scales = "h2" in (phi_gemm, gram_gemm) and self.ldy <= lib.dsvgd_pack_max_ldy()
+        self.fused_scales = ("h2" in (phi_gemm, gram_gemm) and self.ldy <= lib.dsvgd_pack_max_ldy()
+                             and d > self.DIRECT_MAX_D)
         if self.fused_scales:
             self.colmax_nb = lib.dsvgd_pack_blocks(rows)
             i32 = dict(dtype=torch.int32, device=dev)
