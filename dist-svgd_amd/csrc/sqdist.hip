@@ -84,8 +84,10 @@ using GramTile = NTTile<2, 2, 2, 2>;  // 128 x 128 block, 4 waves of 64 x 64
 // tiles).  The wave holds rows [rbase, rbase + 64) x columns [cbase, cbase +
 // 32 NI) of the tile in acc[mi][ni] (mi < 2, ni < NI); srow / scol: the
 // tile's 128 row / column norms.
+// MIR = false: the launch never stores mirror tiles (compile-time: no
+// register shuffles for them)
 template <bool SYM, int smode, bool ZERO = false, class Tile = GramTile, int NI = 2,
-          class SW = SlotWriter>
+          class SW = SlotWriter, bool MIR = true>
 __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t row0,
                                             int64_t m, int64_t n, int64_t n_pad,
                                             float* __restrict__ D, const float* srow,
@@ -145,7 +147,7 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
       for (int r = 0; r < 16; ++r)
         if (kSqEpi < 2 || v[r] != v[r])  // streamed out: nt, so D does not evict the Gram operands from L2
           __builtin_nontemporal_store(v[r], dp0 + (r & 3) * 16 + (r >> 2) * 128);
-      if (mirror && mirror_store && (kSqEpi == 0 || v[0] != v[0])) {  // D[j][i]: 4 consecutive i per register quad -> 16-byte stores
+      if (MIR && mirror && mirror_store && (kSqEpi == 0 || v[0] != v[0])) {  // D[j][i]: 4 consecutive i per register quad -> 16-byte stores
         float* const mp0 = Dmir + (uint32_t)(cl * 16 + ((rbase >> 4) + mi * 2) * kPanelElems + h4);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -466,7 +468,7 @@ __global__ __launch_bounds__(256, 2) void sqdist_persistent_kernel(
 // the other's MFMAs instead of every SIMD idling its MFMA pipe through it.
 // NS: LDS ring stages (2: a K-step's DMA has one K-step to land; 3: two).
 template <bool SYM, int smode, bool M16 = true, class F = FmtX3, int WN = 2, int NS = 2, int KS = 1,
-          bool TR = false>
+          bool TR = false, bool MIR = true>
 __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
     const typename F::E* __restrict__ Yg, int64_t img_rows, const float* __restrict__ norms,
     int64_t row0, int64_t m, int64_t n, int64_t n_pad, int nk, float* __restrict__ D,
@@ -581,7 +583,7 @@ __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
                                   snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl,
                                   slot, epi, layout == 0, r0t);
       else
-        sq_epilogue<SYM, smode, !kZeroC, GramX3WTile, 4, SW>(
+        sq_epilogue<SYM, smode, !kZeroC, GramX3WTile, 4, SW, MIR>(
             tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128,
             snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl, slot, epi, layout == 0,
             r0t, c2);
@@ -709,7 +711,7 @@ int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, 
              256 * WN)))
       return rc;
     if ((rc = persistent_blocks(
-             reinterpret_cast<const void*>(&sqdist_x3w_kernel<false, SM, F::P == 3, F, WN, NS, KS, TRF>),
+             reinterpret_cast<const void*>(&sqdist_x3w_kernel<false, SM, F::P == 3, F, WN, NS, KS, TRF, false>),
              &bn, 256 * WN)))
       return rc;
     const int Tn2 = (int)((n_pad / 128 + 1) / 2), Tm2 = (int)((m_pad / 128 + 1) / 2);
@@ -738,16 +740,16 @@ int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, 
     for (int i = 0; i < np; ++i) {
       const Part& P = parts[i];
       const int lay = sym ? layout : 0;
-#define DSVGD_X3W(SY, M, B, LAY, R0T, TR)                                                      \
-  hipLaunchKernelGGL((sqdist_x3w_kernel<SY, SM, M, F, WN, NS, KS, TR>), dim3((unsigned)B),       \
+#define DSVGD_X3W(SY, M, B, LAY, R0T, TR, MIR)                                                 \
+  hipLaunchKernelGGL((sqdist_x3w_kernel<SY, SM, M, F, WN, NS, KS, TR, MIR>), dim3((unsigned)B),  \
                      dim3(256 * WN), 0, s, Yg, img, norms, row0, m, n, n_pad, nk, D, st, cand, epi, \
                      P.total, LAY, P.tm2, P.tc2, P.bj_off, R0T, base, ns_total, tsc)
       if (P.sym && lay == 0)  // mirror stores
-        DSVGD_X3W(true, F::P == 3, bs, lay, P.r0t, false);
+        DSVGD_X3W(true, F::P == 3, bs, lay, P.r0t, false, true);
       else if (P.sym)
-        DSVGD_X3W(true, F::P == 3, bs, lay, P.r0t, TRF);
+        DSVGD_X3W(true, F::P == 3, bs, lay, P.r0t, TRF, false);
       else
-        DSVGD_X3W(false, F::P == 3, bn, 0, 0, TRF);
+        DSVGD_X3W(false, F::P == 3, bn, 0, 0, TRF, false);
 #undef DSVGD_X3W
       if ((rc = check_launch("sqdist_x3w"))) return rc;
       base += P.total * 8;
