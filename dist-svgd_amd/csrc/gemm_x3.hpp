@@ -204,6 +204,16 @@ struct NNX3Tile {
 #endif
   static constexpr bool kLateDma = DSVGD_NN_LATE_DMA != 0;  // (step_dma3)
   static_assert(!(kPingPong && kLateDma), "early staging counts on this iteration's DMAs issued");
+#ifndef DSVGD_NN_SGB
+#define DSVGD_NN_SGB 0
+#endif
+  // kSgb (A/B): the next K-step's A staging (exp2 + split: VALU) made
+  // branch-free and spread between the K-step's MFMAs, kSgb VALU per MFMA,
+  // by sched_group_barrier (cdna_hip_programming.md T19); left to itself the
+  // compiler issues the staging after the MFMAs.  Measured (r5t, phi_mm
+  // S = 1): 0 (shipped) 12.46 ms, 1: 12.78, 2: 12.62, 4: 12.47 -- the
+  // staging's placement is not what holds the matrix pipe back
+  static constexpr int kSgb = DSVGD_NN_SGB;
   using V8 = typename F::V8;
   static_assert(!M16 || P == 3, "the 16x16x32 concatenated-k form is the 3-part format's");
   // (DMA needs the same DMA count in every wave: whole 512-chunk rounds)
@@ -528,6 +538,15 @@ struct NNX3Tile {
           store_a(smem, scale, row_g0 - k0, a);
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if constexpr (kSgb != 0 && EXP && RW == 2 && !M16 && !kPingPong && !kLateDma) {
+          for (int64_t j0 = k0; j0 < k1; j0 += 3 * BJ) {
+            step_dma3_sgb<0>(rA, rB, ldy, j0, k1, scale, smem, row_g0, wr, wc);
+            if (j0 + BJ < k1) step_dma3_sgb<1>(rA, rB, ldy, j0 + BJ, k1, scale, smem, row_g0, wr, wc);
+            if (j0 + 2 * BJ < k1)
+              step_dma3_sgb<2>(rA, rB, ldy, j0 + 2 * BJ, k1, scale, smem, row_g0, wr, wc);
+          }
+          return;
+        }
         for (int64_t j0 = k0; j0 < k1; j0 += 3 * BJ) {
           step_dma3<0>(rA, rB, ldy, j0, k1, scale, smem, row_g0, wr, wc);
           if (j0 + BJ < k1) step_dma3<1>(rA, rB, ldy, j0 + BJ, k1, scale, smem, row_g0, wr, wc);
@@ -658,6 +677,94 @@ struct NNX3Tile {
     if (kLateDma) issue();
     if (!early) stage_next();
     compute<kHalf, TN>(cur, wc);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+
+  // ---- kSgb (EXP, RW = 2): the staging without branches, so that it and
+  // the K-step's MFMAs form one basic block -- one scheduling region in
+  // which sched_group_barrier can spread the staging VALU between MFMAs.
+  // The transposed read (symmetric layout) and the plain one are the same
+  // four ds_read_b32 with lane-selected addresses; the rotation takes a zero
+  // mask when not transposed; the diagonal test runs on every K-step; a
+  // K-step past the range stages stale values that nothing reads, and its
+  // row-sum share is selected away.
+  // bit select (m ? a : b per bit): one v_bfi_b32, never a branch
+  __device__ __forceinline__ static uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) {
+    return (a & m) | (b & ~m);
+  }
+  __device__ __forceinline__ static float fsel(uint32_t m, float a, float b) {
+    return __uint_as_float(bsel(m, __float_as_uint(a), __float_as_uint(b)));
+  }
+
+  __device__ __forceinline__ f32x4 raw_read_bf(const char* raw, int64_t j0) const {
+    const int t = threadIdx.x, row = t >> 2, c4 = t & 3;
+    const uint32_t m = transposed(j0) ? ~0u : 0u;  // wave-uniform
+    const float* rf = reinterpret_cast<const float*>(raw);
+    const int tb = (row >> 4) * 256 + (row & 15) + (4 * c4) * 16;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      v[e] = rf[(int)bsel(m, (uint32_t)(tb + ((e + c4) & 3) * 16), (uint32_t)(4 * t + e))];
+    // rotate back (transposed only): lanes with c4 odd, then with c4 >= 2
+    const uint32_t so = m & (0u - (uint32_t)(c4 & 1)), sh = m & (0u - (uint32_t)(c4 >> 1));
+    float w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w[q] = fsel(so, v[(q + 3) & 3], v[q]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = fsel(sh, w[(q + 2) & 3], w[q]);
+    return f32x4{v[0], v[1], v[2], v[3]};
+  }
+
+  __device__ __forceinline__ void store_a_bf(char* st, float scale, int64_t dgl, bool live) {
+    const int t = threadIdx.x, row = t >> 2, c4 = t & 3;
+    const int qd = (int)max(min(dgl, (int64_t)BJ), (int64_t)-BM - 4) + row - 4 * c4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float e = __builtin_amdgcn_exp2f(fmaf(ra[q], scale, F::kAScaleLog2));
+      ra[q] = (qd == q) ? 0.f : e;
+    }
+    rs += fsel(live ? ~0u : 0u, (ra[0] + ra[1]) + (ra[2] + ra[3]), 0.f);
+    typename F::V4 sp[P];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      typename F::E v[P];
+      split_fmt<F>(ra[q], v);
+#pragma unroll
+      for (int p = 0; p < P; ++p) sp[p][q] = v[p];
+    }
+    const int off = x3_off(row, c4 >> 1) + ((c4 & 1) << 3);
+#pragma unroll
+    for (int p = 0; p < P; ++p) *reinterpret_cast<typename F::V4*>(st + p * BM * 32 + off) = sp[p];
+  }
+
+  template <int CUR>
+  __device__ __forceinline__ void step_dma3_sgb(__amdgpu_buffer_rsrc_t rA,
+                                                __amdgpu_buffer_rsrc_t rB, int64_t ldy,
+                                                int64_t j0, int64_t k1, float scale, char* smem,
+                                                int64_t row_g0, int wr, int wc) {
+    static_assert(EXP && RW == 2 && !M16, "the interleaved step is phi_mm's");
+    constexpr int NXT = (CUR + 1) % 3, NN = (CUR + 2) % 3;
+    const char* cur = smem + CUR * kStage;
+    char* raw = smem + kRaw;
+    const bool more = j0 + BJ < k1, more2 = j0 + 2 * BJ < k1;
+    if (more2) {
+      dma_b(smem + NN * kStage, rB, ldy, j0 + 2 * BJ);
+      dma_d(raw + NN * kSlot, rA, j0 + 2 * BJ);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB + AR) : "memory");  // tile k+1's D landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    read_a(cur, wr);
+    compute<0, kHalf>(cur, wc);
+    ra = raw_read_bf(raw + NXT * kSlot, j0 + BJ);
+    store_a_bf(smem + NXT * kStage, scale, row_g0 - (j0 + BJ), more);
+    compute<kHalf, TN>(cur, wc);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * P * TM / 2 + P * kHalf + 4, 0);  // DS reads
+#pragma unroll
+    for (int i = 0; i < 3 * TM * TN; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, kSgb, 0);  // VALU
+    }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
 
