@@ -304,6 +304,90 @@ def _nccl_worker(rank, port, mode, order, q):
     dist.destroy_process_group()
 
 
+def _nccl_world1_worker(port, q):
+    """Every device-collective branch of dsvgd.exchange on RCCL with one rank:
+    the calls, aliasing, stream use and dtypes are the S > 1 ones; with one
+    rank each collective's result is known exactly."""
+    import os
+    import sys
+    import torch.distributed as dist
+    from conftest import PKG, ROOT
+    for p in (ROOT, PKG):
+        sys.path.insert(0, p)
+    import dsvgd as m
+    from dsvgd import exchange
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    assert not exchange._is_gloo()
+    out = {}
+    g = torch.Generator(device="cpu").manual_seed(5)
+    X = torch.randn(1024, 48, generator=g).to(dev)
+    X0 = X.clone()
+    # in-place all-gather: the rank's block aliases its slot of the output
+    out["inplace_taken"] = exchange.all_gather_in_place(X, 0, X.shape[0])
+    out["inplace_equal"] = bool(torch.equal(X, X0))
+    # out-of-place all-gather into a separate buffer
+    o = torch.full_like(X, float("nan"))
+    exchange.all_gather_blocks(X[:256], o[:256])
+    out["gather_equal"] = bool(torch.equal(o[:256], X0[:256]))
+    # ring shift through batch_isend_irecv (rank 0 sends to and receives from itself)
+    r = torch.full((256, 48), float("nan"), device=dev)
+    exchange.ring_shift(X[256:512].contiguous(), r, 0, 1)
+    out["ring_equal"] = bool(torch.equal(r, X0[256:512]))
+    # the all_scores all-reduce on a side stream, joined back like DistSampler._compute
+    side = torch.cuda.Stream(device=dev)
+    S = X * 3.0
+    S0 = S.clone()
+    main = torch.cuda.current_stream(dev)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        exchange.all_reduce_sum(S)
+    main.wait_stream(side)
+    out["allreduce_equal"] = bool(torch.equal(S, S0))
+    # the median's histogram all-reduce hook (int64 bins, bracket counts) on a
+    # row-block engine: the same bandwidth as without the hook
+    # (radix passes over D; the bracketed select, m * n >= 2^24)
+    out["median_h"] = []
+    for n, mb, row0 in ((4096, 1024, 2048), (8192, 2048, 4096)):
+        Xm = (0.3 * torch.randn(n, 32, generator=g)).to(dev)
+        hs = []
+        for hook in (None, lambda t: exchange.all_reduce_sum(t)):
+            eng = m.PhiEngine(n, 32, m=mb, row0=row0, device=dev)
+            eng.pack(Xm)
+            eng.distances(median=True)
+            eng.median_bandwidth(hook)
+            torch.cuda.synchronize()
+            hs.append(eng.state.read()[1])
+        out["median_h"].append(hs)
+    torch.cuda.synchronize()
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put(out)
+
+
+def test_rccl_world1_exchange_primitives():
+    """One GPU: the RCCL branches of dsvgd.exchange (in-place
+    all_gather_into_tensor, batch_isend_irecv ring shift, the side-stream
+    all-reduce, the median hook's int64 all-reduces) run on hardware -- the
+    S > 1 call sites (reference distsampler.py:136,143,156,170) with results
+    known exactly at one rank."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_world1_worker, args=(29650, q))
+    p.start()
+    out = q.get(timeout=240)
+    p.join(60)
+    assert p.exitcode == 0
+    for k in ("inplace_taken", "inplace_equal", "gather_equal", "ring_equal", "allreduce_equal"):
+        assert out[k], k
+    for a, b in out["median_h"]:
+        assert a == b, out["median_h"]
+
+
 @pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL path needs two GPUs")
 @pytest.mark.parametrize("mode", ["partitions", "all_particles", "all_scores"])
 @pytest.mark.parametrize("order", ["jacobi", "sequential"])
