@@ -14,6 +14,7 @@
 
 #include "gemm_tiles.hpp"
 #include "gemm_x3.hpp"
+#include "phi_w1.hpp"
 
 // DSVGD_PHI_DA: how many K-steps ahead the FmtH2 NN tile DMAs its D panels
 // (gemm_x3.hpp NNX3Tile DA: 2 = with the B image, 3 = one step earlier)
@@ -24,6 +25,12 @@
 namespace dsvgd {
 
 constexpr int kPhiDA = DSVGD_PHI_DA;
+// DSVGD_PHI_W1 (A/B): phi_mm on the full D layout by phi_w1_kernel (one wave
+// per SIMD, B fragments straight from the image; phi_w1.hpp)
+#ifndef DSVGD_PHI_W1
+#define DSVGD_PHI_W1 0
+#endif
+constexpr bool kPhiW1 = DSVGD_PHI_W1 != 0;
 
 // blockIdx.z = split-K slice z: K columns [z*kchunk, min(K,(z+1)*kchunk)) into
 // the partial C + z*m*ldc (and rowsum + z*m_pad); phi_finish sums the slices
@@ -220,6 +227,11 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
       hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F>), grid, dim3(512), 0, s, D, K,
                          Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv);
   } else {  // FmtH2: the smaller stages fit a 3-stage ring
+    if (kPhiW1 && TN == 4 && EXP && !sym) {
+      hipLaunchKernelGGL(phi_w1_kernel, grid, dim3(PhiW1::kThreads), 0, s, D, K, Yx, ldy, K, kchunk,
+                         st, C, ldc, rowsum, m, row0, colinv);
+      return check_launch("phi_w1_kernel");
+    }
     hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2,
                                      (TN != 1 && kPhiDA == 3) ? 3 : 2>), grid,
                        dim3(512), 0, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym,

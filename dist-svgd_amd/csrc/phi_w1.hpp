@@ -1,0 +1,218 @@
+// phi_w1.hpp -- phi_mm (C = exp-fused K . Y on the FmtH2 split engine) with
+// ONE wave per SIMD: 4 waves of 128 x 128 (256 accumulator registers each, in
+// AGPRs), block 128 rows x 512 columns, 16-deep K-steps.
+//
+// What differs from NNX3Tile (gemm_x3.hpp, 8 waves of 64 x 128):
+//   * B (the Yx image) never goes through LDS: a wave's 128 columns are its
+//     own, so each lane loads its MFMA B fragments straight from the image
+//     (buffer_load_dwordx4, one K-step ahead, double-buffered in VGPRs);
+//   * the D panel is loaded by the thread that stages it (two dwordx4, two
+//     K-steps ahead) -- no LDS-DMA anywhere, so every wait is the compiler's
+//     own counted vmcnt;
+//   * LDS holds only the staged A image (2 stages x 8 KiB); each wave reads
+//     all 128 rows of it (64 KiB of fragment reads per K-step per block
+//     instead of 96 KiB);
+//   * each K-step is one basic block (branch-free staging: clamped loads past
+//     the range, masked row sums, the diagonal by compare/select), so the
+//     scheduler can interleave the staging VALU with the 48 MFMAs.
+// Full D layout only (no transposed tiles).
+#pragma once
+#include "gemm_x3.hpp"
+
+namespace dsvgd {
+
+struct PhiW1 {
+  static constexpr int kThreads = 256;
+  static constexpr int BM = 128, BC = 512, BJ = 16, P = 2;
+  static constexpr int SA = P * BM * 32;  // one stage's A image (8 KiB)
+  static constexpr int kSmemBytes = 2 * SA;
+};
+
+// aux bit 31 (volatile, compiler-only): the loads stay where they are issued --
+// otherwise the register allocator rematerialises these read-only loads next
+// to their uses, which turns every prefetch into an exposed L2/HBM wait
+#ifndef DSVGD_W1_SGB
+#define DSVGD_W1_SGB 4
+#endif
+#ifndef DSVGD_W1_KEEP
+#define DSVGD_W1_KEEP 0
+#endif
+constexpr int kW1Keep = DSVGD_W1_KEEP ? (int)(1u << 31) : 0;
+__device__ __forceinline__ f32x4 w1_load(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kW1Keep));
+}
+__device__ __forceinline__ f32x4 w1_load_nt(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(f32x4,
+                            __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kW1Keep | 2));
+}
+
+// A: panel row of the block (panel layout, 128 x 16 fp32 panels); Yx: FmtH2
+// image [kstep][part][column][16 k]; K range [kchunk z, +kchunk) of K.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void phi_w1_kernel(
+    const float* A, int64_t a_npad, const _Float16* Yx, int64_t ldy,
+    int64_t K, int64_t kchunk, const dsvgd_select_state* __restrict__ st, float* __restrict__ C,
+    int64_t ldc, float* __restrict__ rowsum, int64_t m, int64_t row0,
+    const float* __restrict__ colinv) {
+  using F = FmtH2;
+  using V8 = F::V8;
+  constexpr int P = PhiW1::P;
+  __shared__ __attribute__((aligned(16))) char smem[PhiW1::kSmemBytes];
+  const int t = threadIdx.x, lane = t & 63, r = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int64_t i0 = (int64_t)blockIdx.y * PhiW1::BM;
+  const int64_t c0 = (int64_t)blockIdx.x * PhiW1::BC + w * 128;
+  const int64_t kb0 = (int64_t)blockIdx.z * kchunk;
+  const int64_t kend = min(K, kb0 + kchunk);
+  const int nsteps = kend > kb0 ? (int)((kend - kb0) / PhiW1::BJ) : 0;
+  C += (int64_t)blockIdx.z * m * ldc;
+  rowsum += (int64_t)blockIdx.z * roundup128(m);
+  const float scale = -st->inv_h * kLog2e;
+
+  // D: the block's panel row; thread t stages row t >> 1, columns 8 (t & 1) .. +7
+  const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(A + (i0 >> 7) * (a_npad >> 4) * kPanelElems), (short)0, 0x7fffffff, 0x00020000);
+  // B: the wave's first column; lane (r, h) reads column r, half h of each 32-column tile
+  const __amdgpu_buffer_rsrc_t rB =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Yx + c0 * 16), (short)0, 0x7fffffff, 0x00020000);
+  const int pstride = (int)(ldy * 32);        // bytes of one part image of one K-step
+  const int vB = x3_off(r, h);                // column base is a multiple of 32
+  const int vD = t * 32;
+  const int srow = t >> 1, shalf = t & 1;
+  const int aoff = x3_off(srow, shalf);       // this thread's 16 B of a part image row
+  // diagonal: global row - the thread's first column at K-step 0, clamped to
+  // int range (only |.| < 16 matters)
+  const int64_t dg = row0 + i0 + srow - kb0 - 8 * shalf;
+  const int qd0 = (int)max(min(dg, (int64_t)(1 << 30)), (int64_t)-(1 << 30));
+
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[mi][ni][q] = 0.f;
+  float rs = 0.f;
+
+  if (nsteps > 0) {
+    V8 b[4][P];       // B fragments of the current K-step; column tile ni is
+                      // reloaded for the next K-step right after its last MFMA
+    f32x4 dr[2][2];   // D values: K-step k in dr[k & 1]
+    const int last = nsteps - 1;
+    auto loadB = [&](int ni, int k) {
+      const int soff = (int)((kb0 >> 4) + min(k, last)) * P * pstride;
+#pragma unroll
+      for (int p = 0; p < P; ++p)
+        b[ni][p] = __builtin_bit_cast(V8, w1_load(rB, vB + ni * 1024, soff + p * pstride));
+    };
+    auto loadD = [&](f32x4 (&d)[2], int k) {
+      const int soff = (int)((kb0 >> 4) + min(k, last)) * kPanelElems * 4;
+      d[0] = w1_load_nt(rD, vD, soff);
+      d[1] = w1_load_nt(rD, vD + 16, soff);
+    };
+    // exp2 / diagonal / row sum / 2-part split of K-step k's 8 values -> stage
+    auto stage = [&](char* st_, const f32x4 (&d)[2], int k) {
+      const int qd = max(min(qd0 - k * PhiW1::BJ, 8), -1);  // diagonal column, or -1 / 8
+      float e[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float v = q < 4 ? d[0][q] : d[1][q - 4];
+        const float x = __builtin_amdgcn_exp2f(fmaf(v, scale, F::kAScaleLog2));
+        e[q] = qd == q ? 0.f : x;
+      }
+      const float s = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
+      rs += k <= last ? s : 0.f;
+      V8 p0, p1;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const _Float16 a0 = (_Float16)e[q];
+        p0[q] = a0;
+        p1[q] = (_Float16)(e[q] - (float)a0);
+      }
+      *reinterpret_cast<V8*>(st_ + aoff) = p0;
+      *reinterpret_cast<V8*>(st_ + PhiW1::BM * 32 + aoff) = p1;
+    };
+    auto barrier = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    // K-step k from stage cur: A(k+1) -> stage nxt from ds_; D(k+2) -> dl;
+    // MFMAs column tile by column tile, each tile's B reloaded for k+1
+    auto step = [&](int k, const char* cur, char* nxt, const f32x4 (&ds_)[2], f32x4 (&dl)[2]) {
+      V8 a[4][P];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+          a[mi][p] = *reinterpret_cast<const V8*>(cur + p * PhiW1::BM * 32 + x3_off(mi * 32 + r, h));
+      stage(nxt, ds_, k + 1);
+      loadD(dl, k + 2);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        // small terms first, as mfma_products
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) acc[mi][ni] = mfma_fmt<F>(a[mi][1], b[ni][0], acc[mi][ni]);
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) acc[mi][ni] = mfma_fmt<F>(a[mi][0], b[ni][1], acc[mi][ni]);
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) acc[mi][ni] = mfma_fmt<F>(a[mi][0], b[ni][0], acc[mi][ni]);
+        loadB(ni, k + 1);
+      }
+#if DSVGD_W1_SGB
+      // one wave per SIMD: nothing else hides the staging VALU, so spread it
+      // between the MFMAs (cdna_hip_programming.md T19): the A fragment reads,
+      // then 16 MFMAs each followed by up to 4 VALU (the staging of A(k+1)),
+      // its two LDS stores, then the other 32 MFMAs with the 10 prefetch loads
+      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, DSVGD_W1_SGB, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (i % 3 == 2) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+#endif
+    };
+
+    // prologue: B(0), D(0), D(1); A(0) -> stage 0
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) loadB(ni, 0);
+    loadD(dr[0], 0);
+    loadD(dr[1], 1);
+    stage(smem, dr[0], 0);
+    barrier();
+    // unrolled by 4: the compiler's wait counts are exact inside the body and
+    // conservative (vmcnt(0)) where the back edge meets the prologue
+    for (int k = 0; k < nsteps; k += 4) {
+      step(k, smem, smem + PhiW1::SA, dr[1], dr[0]);
+      barrier();
+      if (k + 1 >= nsteps) break;
+      step(k + 1, smem + PhiW1::SA, smem, dr[0], dr[1]);
+      barrier();
+      if (k + 2 >= nsteps) break;
+      step(k + 2, smem, smem + PhiW1::SA, dr[1], dr[0]);
+      barrier();
+      if (k + 3 >= nsteps) break;
+      step(k + 3, smem + PhiW1::SA, smem, dr[0], dr[1]);
+      barrier();
+    }
+  }
+
+  // epilogue (nn_x3_kernel's): C = acc * colinv * 2^-15; row sums by column block 0
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int64_t col = c0 + ni * 32 + r;
+      const float cs = colinv[col] * (1.f / F::kAScale);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t row = i0 + mi * 32 + c_row(q, lane);
+        if (row < m) C[row * ldc + col] = acc[mi][ni][q] * cs;
+      }
+    }
+  const float v = rs + __shfl_xor(rs, 1, 64);
+  if (blockIdx.x == 0 && shalf == 0 && i0 + srow < m) rowsum[i0 + srow] = v * (1.f / F::kAScale);
+}
+
+}  // namespace dsvgd

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--configs", default="h2:sym,h2:full,x3:sym,x3:full")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--lib", default=None, help="an A/B build of the library (make ab)")
+    ap.add_argument("--dump", default=None,
+                    help="save every 256th row of phi per configuration to DUMP_<cfg>.npy")
     args = ap.parse_args()
     import dsvgd
     if args.lib:
@@ -51,6 +53,10 @@ def main():
             eng.direction(write_phi=True)
         e1.record()
         torch.cuda.synchronize()
+        if args.dump:
+            import numpy as np
+            np.save("%s_%s.npy" % (args.dump, cfg.replace(":", "_")),
+                    eng.phi[::256].float().cpu().numpy())
         out[cfg] = {"sym": bool(eng.sym), "phi_ms": e0.elapsed_time(e1) / args.reps,
                     "distances_ms": dist_ms}
         print(json.dumps({cfg: out[cfg]}), flush=True)

@@ -349,13 +349,14 @@ def _nccl_world1_worker(port, q):
     out["allreduce_equal"] = bool(torch.equal(S, S0))
     # the median's histogram all-reduce hook (int64 bins, bracket counts) on a
     # row-block engine: the same bandwidth as without the hook
-    # (radix passes over D; the bracketed select, m * n >= 2^24)
+    # (radix passes over D; the bracketed select, n * n >= 2^24; one rank
+    # holds the whole matrix, so its order statistic exists without peers)
     out["median_h"] = []
-    for n, mb, row0 in ((4096, 1024, 2048), (8192, 2048, 4096)):
+    for n in (2048, 4096):
         Xm = (0.3 * torch.randn(n, 32, generator=g)).to(dev)
         hs = []
         for hook in (None, lambda t: exchange.all_reduce_sum(t)):
-            eng = m.PhiEngine(n, 32, m=mb, row0=row0, device=dev)
+            eng = m.PhiEngine(n, 32, device=dev)
             eng.pack(Xm)
             eng.distances(median=True)
             eng.median_bandwidth(hook)
@@ -385,7 +386,7 @@ def test_rccl_world1_exchange_primitives():
     for k in ("inplace_taken", "inplace_equal", "gather_equal", "ring_equal", "allreduce_equal"):
         assert out[k], k
     for a, b in out["median_h"]:
-        assert a == b, out["median_h"]
+        assert a == b and np.isfinite(a) and a > 0, out["median_h"]
 
 
 @pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL path needs two GPUs")
