@@ -25,12 +25,14 @@
 namespace dsvgd {
 
 constexpr int kPhiDA = DSVGD_PHI_DA;
-// DSVGD_PHI_W1 (A/B): phi_mm on the full D layout by phi_w1_kernel (one wave
-// per SIMD, B fragments straight from the image; phi_w1.hpp)
+// DSVGD_PHI_W1: phi_mm on the FmtH2 engine by phi_w1_kernel (one wave per
+// SIMD, B fragments straight from the image; phi_w1.hpp) -- 1 (default): the
+// full D layout (row blocks, S > 1), 2: also the symmetric layout (A/B: its
+// transposed K-steps still cost more than NNX3Tile's), 0: never
 #ifndef DSVGD_PHI_W1
-#define DSVGD_PHI_W1 0
+#define DSVGD_PHI_W1 1
 #endif
-constexpr bool kPhiW1 = DSVGD_PHI_W1 != 0;
+constexpr int kPhiW1 = DSVGD_PHI_W1;
 
 // blockIdx.z = split-K slice z: K columns [z*kchunk, min(K,(z+1)*kchunk)) into
 // the partial C + z*m*ldc (and rowsum + z*m_pad); phi_finish sums the slices
@@ -227,9 +229,9 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
       hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F>), grid, dim3(512), 0, s, D, K,
                          Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv);
   } else {  // FmtH2: the smaller stages fit a 3-stage ring
-    if (kPhiW1 && TN == 4 && EXP && !sym) {
+    if (TN == 4 && EXP && (kPhiW1 == 2 || (kPhiW1 == 1 && !sym))) {
       hipLaunchKernelGGL(phi_w1_kernel, grid, dim3(PhiW1::kThreads), 0, s, D, K, Yx, ldy, K, kchunk,
-                         st, C, ldc, rowsum, m, row0, colinv);
+                         st, C, ldc, rowsum, m, row0, sym, colinv);
       return check_launch("phi_w1_kernel");
     }
     hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2,

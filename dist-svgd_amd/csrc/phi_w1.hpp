@@ -15,7 +15,8 @@
 //   * each K-step is one basic block (branch-free staging: clamped loads past
 //     the range, masked row sums, the diagonal by compare/select), so the
 //     scheduler can interleave the staging VALU with the 48 MFMAs.
-// Full D layout only (no transposed tiles).
+// Both D layouts: the symmetric one's transposed K-steps are read as 8
+// dword loads per thread (column srow of the stored tile's 16 rows).
 #pragma once
 #include "gemm_x3.hpp"
 
@@ -51,7 +52,7 @@ __device__ __forceinline__ f32x4 w1_load_nt(__amdgpu_buffer_rsrc_t r, int voff, 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void phi_w1_kernel(
     const float* A, int64_t a_npad, const _Float16* Yx, int64_t ldy,
     int64_t K, int64_t kchunk, const dsvgd_select_state* __restrict__ st, float* __restrict__ C,
-    int64_t ldc, float* __restrict__ rowsum, int64_t m, int64_t row0,
+    int64_t ldc, float* __restrict__ rowsum, int64_t m, int64_t row0, int sym,
     const float* __restrict__ colinv) {
   using F = FmtH2;
   using V8 = F::V8;
@@ -93,10 +94,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int q = 0; q < 16; ++q) acc[mi][ni][q] = 0.f;
   float rs = 0.f;
 
+  // symmetric layout (m == n, row0 == 0): K-steps left of the block's
+  // diagonal tile read the stored tile (J, I) transposed
+  const int symI = sym ? (int)(i0 >> 7) : -1;
+  const int64_t pcols = a_npad >> 4;
+  // transposed: row srow's value q of a K-step sits in the panel of column
+  // block I*8 + (srow >> 4), row (j0 & 127) + 8 shalf + q, column srow & 15
+  const int vT = ((srow >> 4) * kPanelElems + 8 * shalf * 16 + (srow & 15)) * 4;
+
   if (nsteps > 0) {
     V8 b[4][P];       // B fragments of the current K-step; column tile ni is
                       // reloaded for the next K-step right after its last MFMA
-    f32x4 dr[2][2];   // D values: K-step k in dr[k & 1]
+    f32x4 dr[4][2];   // D values: K-step k in dr[k & 3], loaded 3 K-steps ahead
     const int last = nsteps - 1;
     auto loadB = [&](int ni, int k) {
       const int soff = (int)((kb0 >> 4) + min(k, last)) * P * pstride;
@@ -105,9 +114,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         b[ni][p] = __builtin_bit_cast(V8, w1_load(rB, vB + ni * 1024, soff + p * pstride));
     };
     auto loadD = [&](f32x4 (&d)[2], int k) {
-      const int soff = (int)((kb0 >> 4) + min(k, last)) * kPanelElems * 4;
-      d[0] = w1_load_nt(rD, vD, soff);
-      d[1] = w1_load_nt(rD, vD + 16, soff);
+      const int kc = min(k, last);
+      const int64_t j0 = kb0 + (int64_t)kc * PhiW1::BJ;
+      if ((int)(j0 >> 7) < symI) {  // wave-uniform
+        const float* src = A + (((j0 >> 7) * pcols + symI * 8) * kPanelElems + (j0 & 127) * 16);
+        const __amdgpu_buffer_rsrc_t rT =
+            __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          d[q >> 2][q & 3] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(rT, vT + q * 64, 0, kW1Keep | 2));
+      } else {
+        const int soff = (int)((kb0 >> 4) + kc) * kPanelElems * 4;
+        d[0] = w1_load_nt(rD, vD, soff);
+        d[1] = w1_load_nt(rD, vD + 16, soff);
+      }
     };
     // exp2 / diagonal / row sum / 2-part split of K-step k's 8 values -> stage
     auto stage = [&](char* st_, const f32x4 (&d)[2], int k) {
@@ -132,8 +153,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       *reinterpret_cast<V8*>(st_ + PhiW1::BM * 32 + aoff) = p1;
     };
     auto barrier = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-    // K-step k from stage cur: A(k+1) -> stage nxt from ds_; D(k+2) -> dl;
-    // MFMAs column tile by column tile, each tile's B reloaded for k+1
+    // K-step k (slot KS = k & 3) from stage cur: A(k+1) -> stage nxt; MFMAs
+    // column tile by column tile, each tile's B reloaded for k+1; then D(k+3)
     auto step = [&](int k, const char* cur, char* nxt, const f32x4 (&ds_)[2], f32x4 (&dl)[2]) {
       V8 a[4][P];
 #pragma unroll
@@ -142,7 +163,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int p = 0; p < P; ++p)
           a[mi][p] = *reinterpret_cast<const V8*>(cur + p * PhiW1::BM * 32 + x3_off(mi * 32 + r, h));
       stage(nxt, ds_, k + 1);
-      loadD(dl, k + 2);
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
         // small terms first, as mfma_products
@@ -157,8 +177,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #if DSVGD_W1_SGB
       // one wave per SIMD: nothing else hides the staging VALU, so spread it
       // between the MFMAs (cdna_hip_programming.md T19): the A fragment reads,
-      // then 16 MFMAs each followed by up to 4 VALU (the staging of A(k+1)),
-      // its two LDS stores, then the other 32 MFMAs with the 10 prefetch loads
+      // then 16 MFMAs each followed by up to DSVGD_W1_SGB VALU (the staging of
+      // A(k+1)), its two LDS stores, then the other 32 MFMAs with the 8 B loads
       __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -169,31 +189,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int i = 0; i < 32; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if (i % 3 == 2) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        if (i % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
       }
 #endif
+      loadD(dl, k + 3);
     };
 
-    // prologue: B(0), D(0), D(1); A(0) -> stage 0
+    // prologue: B(0), D(0..2); A(0) -> stage 0
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) loadB(ni, 0);
     loadD(dr[0], 0);
     loadD(dr[1], 1);
+    loadD(dr[2], 2);
     stage(smem, dr[0], 0);
     barrier();
-    // unrolled by 4: the compiler's wait counts are exact inside the body and
-    // conservative (vmcnt(0)) where the back edge meets the prologue
+    // unrolled by 4 (the D ring's slots are compile-time); the compiler's
+    // wait counts are exact inside the body, conservative at the loop head
     for (int k = 0; k < nsteps; k += 4) {
-      step(k, smem, smem + PhiW1::SA, dr[1], dr[0]);
+      step(k, smem, smem + PhiW1::SA, dr[1], dr[3]);
       barrier();
       if (k + 1 >= nsteps) break;
-      step(k + 1, smem + PhiW1::SA, smem, dr[0], dr[1]);
+      step(k + 1, smem + PhiW1::SA, smem, dr[2], dr[0]);
       barrier();
       if (k + 2 >= nsteps) break;
-      step(k + 2, smem, smem + PhiW1::SA, dr[1], dr[0]);
+      step(k + 2, smem, smem + PhiW1::SA, dr[3], dr[1]);
       barrier();
       if (k + 3 >= nsteps) break;
-      step(k + 3, smem + PhiW1::SA, smem, dr[0], dr[1]);
+      step(k + 3, smem + PhiW1::SA, smem, dr[0], dr[2]);
       barrier();
     }
   }
