@@ -205,7 +205,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     barrier();
     // unrolled by 4 (the D ring's slots are compile-time); the compiler's
     // wait counts are exact inside the body, conservative at the loop head
-    for (int k = 0; k < nsteps; k += 4) {
+#ifndef DSVGD_W1_UNROLL8
+#define DSVGD_W1_UNROLL8 1
+#endif
+    for (int k = 0; k < nsteps; k += 4 * (1 + DSVGD_W1_UNROLL8)) {
       step(k, smem, smem + PhiW1::SA, dr[1], dr[3]);
       barrier();
       if (k + 1 >= nsteps) break;
@@ -217,6 +220,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if (k + 3 >= nsteps) break;
       step(k + 3, smem + PhiW1::SA, smem, dr[0], dr[2]);
       barrier();
+#if DSVGD_W1_UNROLL8
+      // a second copy: the loop head's conservative waits every 8 K-steps
+      // (h2:full phi_mm 11.25 -> 11.05 ms, profiles/r6g)
+      if (k + 4 >= nsteps) break;
+      step(k + 4, smem, smem + PhiW1::SA, dr[1], dr[3]);
+      barrier();
+      if (k + 5 >= nsteps) break;
+      step(k + 5, smem + PhiW1::SA, smem, dr[2], dr[0]);
+      barrier();
+      if (k + 6 >= nsteps) break;
+      step(k + 6, smem, smem + PhiW1::SA, dr[3], dr[1]);
+      barrier();
+      if (k + 7 >= nsteps) break;
+      step(k + 7, smem + PhiW1::SA, smem, dr[0], dr[2]);
+      barrier();
+#endif
     }
   }
 
