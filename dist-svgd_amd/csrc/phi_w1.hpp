@@ -113,6 +113,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int p = 0; p < P; ++p)
         b[ni][p] = __builtin_bit_cast(V8, w1_load(rB, vB + ni * 1024, soff + p * pstride));
     };
+#if DSVGD_PHI_W1 == 2
+    // (A/B) one load shape for both K-step kinds, no branch (so no PHI copies
+    // that wait for the loads): 8 dword loads at the thread's 8 values,
+    // base / lane offset / stride selected per K-step (uniform)
+    auto loadD = [&](f32x4 (&d)[2], int k) {
+      const int kc = min(k, last);
+      const int64_t j0 = kb0 + (int64_t)kc * PhiW1::BJ;
+      const bool tr = (int)(j0 >> 7) < symI;  // wave-uniform
+      const float* src = tr ? A + (((j0 >> 7) * pcols + symI * 8) * kPanelElems + (j0 & 127) * 16)
+                            : A + (i0 >> 7) * pcols * kPanelElems + (j0 >> 4) * kPanelElems;
+      const __amdgpu_buffer_rsrc_t rS =
+          __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, 0x7fffffff, 0x00020000);
+      const int vo = tr ? vT : vD;
+      const int stp = tr ? 64 : 4;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        d[q >> 2][q & 3] =
+            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rS, vo, q * stp, 2));
+    };
+#else
     auto loadD = [&](f32x4 (&d)[2], int k) {
       const int kc = min(k, last);
       const int64_t j0 = kb0 + (int64_t)kc * PhiW1::BJ;
@@ -130,6 +150,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         d[1] = w1_load_nt(rD, vD + 16, soff);
       }
     };
+#endif
     // exp2 / diagonal / row sum / 2-part split of K-step k's 8 values -> stage
     auto stage = [&](char* st_, const f32x4 (&d)[2], int k) {
       const int qd = max(min(qd0 - k * PhiW1::BJ, 8), -1);  // diagonal column, or -1 / 8

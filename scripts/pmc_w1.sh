@@ -1,0 +1,10 @@
+# PMC passes over phi_mm on the full D layout (phi_w1) and the symmetric one
+# (NNX3Tile): one rocprofv3 --pmc run per counter group, each under its own limit.
+set -o pipefail
+OUT=gpurun_out/${TAG:-pmcw1}; mkdir -p $OUT
+export TMPDIR=/tmp
+P="python3 scripts/phi_probe.py --configs h2:full,h2:sym --reps 2"
+timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM --kernel-trace -d $OUT/mfma -o run --output-format csv -- $P > $OUT/mfma.log 2>&1 || exit 1
+timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES --kernel-trace -d $OUT/stall -o run --output-format csv -- $P > $OUT/stall.log 2>&1 || exit 1
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/fetch -o run --output-format csv -- $P > $OUT/fetch.log 2>&1 || exit 1
+echo PMC DONE
