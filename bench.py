@@ -265,8 +265,11 @@ def main():
                    "n": n, "d": d, "N_global": Ng, "parallelism": "dp%d" % world,
                    "particles_per_gpu": m},
         "roofline": {"bound": "mfma",
-                     "kernel": {"h2": "phi_mm (nn_x3_kernel<4, FmtH2>: fp32-accurate 2-part fp16 "
-                                      "split, 3 fp16 MFMA products per fp32 product)",
+                     "kernel": {"h2": ("phi_mm (nn_x3_kernel<4, FmtH2>" if eng.sym else
+                                       "phi_mm (phi_w1_kernel: one wave per SIMD, FmtH2") +
+                                      ": fp32-accurate 2-part fp16 split, 3 fp16 MFMA products "
+                                      "per fp32 product; D layout %s)" % ("symmetric" if eng.sym
+                                                                          else "full"),
                                 "x3": "phi_mm (nn_x3_kernel<4, FmtX3>: fp32-accurate 3-part bf16 "
                                       "split, 6 bf16 MFMA products per fp32 product)",
                                 "f32": "phi_mm (nn_kernel<4,true>: f32 MFMA)"}[gemm],
