@@ -33,6 +33,13 @@ constexpr int kPhiDA = DSVGD_PHI_DA;
 #define DSVGD_PHI_W1 1
 #endif
 constexpr int kPhiW1 = DSVGD_PHI_W1;
+// DSVGD_PHI_HYBRID: on the symmetric layout, NNX3Tile for each row block's
+// transposed K-steps and phi_w1 for the rest (two launches, half the split-K
+// slices each)
+#ifndef DSVGD_PHI_HYBRID
+#define DSVGD_PHI_HYBRID 0
+#endif
+constexpr bool kPhiHybrid = DSVGD_PHI_HYBRID != 0;
 
 // blockIdx.z = split-K slice z: K columns [z*kchunk, min(K,(z+1)*kchunk)) into
 // the partial C + z*m*ldc (and rowsum + z*m_pad); phi_finish sums the slices
@@ -100,15 +107,24 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
                                                     float* __restrict__ C, int64_t ldc,
                                                     float* __restrict__ rowsum, int64_t m,
                                                     int64_t row0, int sym,
-                                                    const float* __restrict__ colinv) {
+                                                    const float* __restrict__ colinv,
+                                                    int dsplit, int slice0) {
   using Tile = NNX3Tile<TN, DMA, EXP, M16, RW, F, NB, DA>;
   __shared__ __attribute__((aligned(16))) char smem[Tile::kSmemBytes];
-  const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
+  // dsplit (symmetric layout, 128-row blocks): 1 = only the K-steps left of
+  // the block's diagonal tile (the transposed ones), longest rows first; the
+  // z slices split that range and land in slices slice0 + z
+  const int64_t i0 =
+      (int64_t)(dsplit == 1 ? gridDim.y - 1 - blockIdx.y : blockIdx.y) * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
-  const int64_t k0 = (int64_t)blockIdx.z * kchunk;
-  const int64_t k1 = min(K, k0 + kchunk);
-  C += (int64_t)blockIdx.z * m * ldc;
-  if (EXP) rowsum += (int64_t)blockIdx.z * roundup128(m);
+  int64_t k0 = (int64_t)blockIdx.z * kchunk, k1 = min(K, k0 + kchunk);
+  if (dsplit == 1) {
+    const int64_t len = (i0 / gridDim.z + kX3Step - 1) / kX3Step * kX3Step;
+    k0 = blockIdx.z * len;
+    k1 = min(i0, k0 + len);
+  }
+  C += (int64_t)(slice0 + blockIdx.z) * m * ldc;
+  if (EXP) rowsum += (int64_t)(slice0 + blockIdx.z) * roundup128(m);
   const float scale = EXP ? -st->inv_h * kLog2e : 0.f;
   Tile tile;
   tile.prow = (a_npad >> 4) * kPanelElems * 4;
@@ -220,24 +236,40 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
     return fail_arg("nn_x3: the 16x16 form needs the DMA path (ldy % 256 == 0)");
   if (TN == 1)  // TN = 1: 1.5 DMA rounds per K-step -> the register-staged form
     hipLaunchKernelGGL((nn_x3_kernel<TN, false, EXP, false, 2, F>), grid, dim3(512), 0, s, D, K, Yx,
-                       ldy, K, kchunk, st, C, ldc, rowsum, m, row0, 0, colinv);
+                       ldy, K, kchunk, st, C, ldc, rowsum, m, row0, 0, colinv, 0, 0);
   else if constexpr (F::P == 3) {
     if (m16)
       hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, TN != 1, 2, F>), grid, dim3(512), 0, s, D,
-                         K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv);
+                         K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0, 0);
     else
       hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F>), grid, dim3(512), 0, s, D, K,
-                         Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv);
+                         Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0, 0);
   } else {  // FmtH2: the smaller stages fit a 3-stage ring
+    if (TN == 4 && EXP && sym && kPhiHybrid && splits >= 2 && kPhiW1 == 1) {
+      // symmetric layout split at each row block's diagonal tile: the
+      // transposed K-steps on NNX3Tile (its LDS-rotated reads), the plain
+      // ones on phi_w1; half the split-K slices each
+      const int sl = splits / 2;
+      const dim3 g1(grid.x, grid.y, sl), g2(grid.x, grid.y, splits - sl);
+      hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2,
+                                       (TN != 1 && kPhiDA == 3) ? 3 : 2>), g1,
+                         dim3(512), 0, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0,
+                         sym, colinv, 1, 0);
+      const int rc = check_launch("nn_x3_kernel(lower)");
+      if (rc) return rc;
+      hipLaunchKernelGGL(phi_w1_kernel, g2, dim3(PhiW1::kThreads), 0, s, D, K, Yx, ldy, K, kchunk,
+                         st, C, ldc, rowsum, m, row0, sym, colinv, 2, sl);
+      return check_launch("phi_w1_kernel(upper)");
+    }
     if (TN == 4 && EXP && (kPhiW1 == 2 || (kPhiW1 == 1 && !sym))) {
       hipLaunchKernelGGL(phi_w1_kernel, grid, dim3(PhiW1::kThreads), 0, s, D, K, Yx, ldy, K, kchunk,
-                         st, C, ldc, rowsum, m, row0, sym, colinv);
+                         st, C, ldc, rowsum, m, row0, sym, colinv, 0, 0);
       return check_launch("phi_w1_kernel");
     }
     hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2,
                                      (TN != 1 && kPhiDA == 3) ? 3 : 2>), grid,
                        dim3(512), 0, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym,
-                       colinv);
+                       colinv, 0, 0);
   }
   return check_launch("nn_x3_kernel");
 }
@@ -259,7 +291,7 @@ int nn_split_gemm(bool exp_, const float* A, int64_t K, const typename F::E* Yx,
     const dim3 grid(ldy / 256, roundup(m, 256) / 256, splits);
     hipLaunchKernelGGL((nn_x3_kernel<4, true, false, F::P == 3, 4, F, F::P == 3 ? 2 : 3>), grid,
                        dim3(512), 0, s, A, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, 0,
-                       colinv);
+                       colinv, 0, 0);
     return check_launch("nn_x3_kernel(256-row)");
   }
 #define DSVGD_X3_TN(TN)                                                                        \

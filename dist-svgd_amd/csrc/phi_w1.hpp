@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const float* A, int64_t a_npad, const _Float16* Yx, int64_t ldy,
     int64_t K, int64_t kchunk, const dsvgd_select_state* __restrict__ st, float* __restrict__ C,
     int64_t ldc, float* __restrict__ rowsum, int64_t m, int64_t row0, int sym,
-    const float* __restrict__ colinv) {
+    const float* __restrict__ colinv, int dsplit, int slice0) {
   using F = FmtH2;
   using V8 = F::V8;
   constexpr int P = PhiW1::P;
@@ -62,11 +62,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int64_t i0 = (int64_t)blockIdx.y * PhiW1::BM;
   const int64_t c0 = (int64_t)blockIdx.x * PhiW1::BC + w * 128;
-  const int64_t kb0 = (int64_t)blockIdx.z * kchunk;
-  const int64_t kend = min(K, kb0 + kchunk);
+  // dsplit == 2 (symmetric layout): only the K-steps from the block's
+  // diagonal tile on (the plain ones; NNX3Tile takes the transposed ones),
+  // split over the z slices, which land in slices slice0 + z
+  int64_t kb0 = (int64_t)blockIdx.z * kchunk, kend = min(K, kb0 + kchunk);
+  if (dsplit == 2) {
+    const int64_t len = ((K - i0) / gridDim.z + PhiW1::BJ - 1) / PhiW1::BJ * PhiW1::BJ;
+    kb0 = i0 + blockIdx.z * len;
+    kend = min(K, kb0 + len);
+  }
   const int nsteps = kend > kb0 ? (int)((kend - kb0) / PhiW1::BJ) : 0;
-  C += (int64_t)blockIdx.z * m * ldc;
-  rowsum += (int64_t)blockIdx.z * roundup128(m);
+  C += (int64_t)(slice0 + blockIdx.z) * m * ldc;
+  rowsum += (int64_t)(slice0 + blockIdx.z) * roundup128(m);
   const float scale = -st->inv_h * kLog2e;
 
   // D: the block's panel row; thread t stages row t >> 1, columns 8 (t & 1) .. +7
