@@ -93,20 +93,26 @@ def cpu_baseline(n, d, x_local, t_local, budget_s):
     return out
 
 
-def pmc_traffic(kernel_prefix):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    --pmc summary (FETCH_SIZE x2 [gfx950 half-count] + WRITE_SIZE, separate
-    passes; scripts/pmc_summary.py) -- None if no summary is present."""
+def pmc_traffic(kernel_prefixes):
+    """HBM bytes per phi_mm from the committed rocprofv3 --pmc summary
+    (FETCH_SIZE x2 [gfx950 half-count] + WRITE_SIZE, separate passes;
+    scripts/pmc_summary.py): the sum over the launches phi_mm makes (one
+    kernel, or on the symmetric layout NNX3Tile's transposed part + phi_w1's
+    plain part) -- None unless every one of them is in the summary."""
     path = os.path.join(ROOT, "profiles", "latest_summary.json")
     try:
         with open(path) as f:
             ks = json.load(f)["kernels"]
     except (OSError, ValueError, KeyError):
         return None, None
-    for name, v in ks.items():
-        if name.startswith(kernel_prefix) and "hbm_bytes_per_launch" in v:
-            return v["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
-    return None, None
+    total = 0.0
+    for prefix in kernel_prefixes:
+        hit = [v["hbm_bytes_per_launch"] for name, v in ks.items()
+               if name.startswith(prefix) and "hbm_bytes_per_launch" in v]
+        if not hit:
+            return None, None
+        total += hit[0]
+    return total, os.path.relpath(path, ROOT)
 
 
 def passes(eng, stages, m, n, d, n_local, score_gemm):
@@ -236,10 +242,11 @@ def main():
     # the committed PMC summary is an N=1 profile: only quoted for the N=1 run
     # phi_mm is the NN tile with the fused exp (<TN, DMA, EXP=true, ..., Fmt>);
     # the logreg G.Xd launch is the same tile with EXP=false
-    kname = {"h2": "void dsvgd::nn_x3_kernel<4, true, true, false, 2, dsvgd::FmtH2,",
-             "x3": "void dsvgd::nn_x3_kernel<4, true, true, true, 2, dsvgd::FmtX3,",
-             "f32": "void dsvgd::nn_kernel<4, true,"}[gemm]
-    traffic, traffic_src = pmc_traffic(kname) if world == 1 else (None, None)
+    knames = {"h2": ["void dsvgd::nn_x3_kernel<4, true, true, false, 2, dsvgd::FmtH2,",
+                     "_ZN5dsvgd13phi_w1_kernel"],
+              "x3": ["void dsvgd::nn_x3_kernel<4, true, true, true, 2, dsvgd::FmtX3,"],
+              "f32": ["void dsvgd::nn_kernel<4, true,"]}[gemm]
+    traffic, traffic_src = pmc_traffic(knames) if world == 1 else (None, None)
     flops = 4.0 * m * n * d
     achieved = flops / (phi_ms * 1e-3) / 1e12
     out = {
@@ -265,8 +272,9 @@ def main():
                    "n": n, "d": d, "N_global": Ng, "parallelism": "dp%d" % world,
                    "particles_per_gpu": m},
         "roofline": {"bound": "mfma",
-                     "kernel": {"h2": ("phi_mm (nn_x3_kernel<4, FmtH2>" if eng.sym else
-                                       "phi_mm (phi_w1_kernel: one wave per SIMD, FmtH2") +
+                     "kernel": {"h2": ("phi_mm (NNX3Tile nn_x3_kernel<4, FmtH2> on the "
+                                       "transposed K-steps + phi_w1_kernel on the rest" if eng.sym
+                                       else "phi_mm (phi_w1_kernel: one wave per SIMD, FmtH2") +
                                       ": fp32-accurate 2-part fp16 split, 3 fp16 MFMA products "
                                       "per fp32 product; D layout %s)" % ("symmetric" if eng.sym
                                                                           else "full"),

@@ -37,7 +37,7 @@ constexpr int kPhiW1 = DSVGD_PHI_W1;
 // transposed K-steps and phi_w1 for the rest (two launches, half the split-K
 // slices each)
 #ifndef DSVGD_PHI_HYBRID
-#define DSVGD_PHI_HYBRID 0
+#define DSVGD_PHI_HYBRID 1
 #endif
 constexpr bool kPhiHybrid = DSVGD_PHI_HYBRID != 0;
 
@@ -114,17 +114,23 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
   // dsplit (symmetric layout, 128-row blocks): 1 = only the K-steps left of
   // the block's diagonal tile (the transposed ones), longest rows first; the
   // z slices split that range and land in slices slice0 + z
-  const int64_t i0 =
-      (int64_t)(dsplit == 1 ? gridDim.y - 1 - blockIdx.y : blockIdx.y) * Tile::BM;
+  // (dispatch order: a row block's slices back to back, longest first)
+  int64_t by = blockIdx.y, bz = blockIdx.z;
+  if (dsplit == 1) {
+    const int64_t lin = (int64_t)blockIdx.z * gridDim.y + blockIdx.y;
+    by = gridDim.y - 1 - lin / gridDim.z;
+    bz = lin % gridDim.z;
+  }
+  const int64_t i0 = by * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
-  int64_t k0 = (int64_t)blockIdx.z * kchunk, k1 = min(K, k0 + kchunk);
+  int64_t k0 = bz * kchunk, k1 = min(K, k0 + kchunk);
   if (dsplit == 1) {
     const int64_t len = (i0 / gridDim.z + kX3Step - 1) / kX3Step * kX3Step;
-    k0 = blockIdx.z * len;
+    k0 = bz * len;
     k1 = min(i0, k0 + len);
   }
-  C += (int64_t)(slice0 + blockIdx.z) * m * ldc;
-  if (EXP) rowsum += (int64_t)(slice0 + blockIdx.z) * roundup128(m);
+  C += (int64_t)(slice0 + bz) * m * ldc;
+  if (EXP) rowsum += (int64_t)(slice0 + bz) * roundup128(m);
   const float scale = EXP ? -st->inv_h * kLog2e : 0.f;
   Tile tile;
   tile.prow = (a_npad >> 4) * kPanelElems * 4;

@@ -60,20 +60,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __shared__ __attribute__((aligned(16))) char smem[PhiW1::kSmemBytes];
   const int t = threadIdx.x, lane = t & 63, r = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int64_t i0 = (int64_t)blockIdx.y * PhiW1::BM;
+  // dsplit == 2: a row block's slices dispatched back to back, longest first
+  const int64_t lin = (int64_t)blockIdx.z * gridDim.y + blockIdx.y;
+  const int64_t by = dsplit == 2 ? lin / gridDim.z : blockIdx.y;
+  const int64_t bz = dsplit == 2 ? lin % gridDim.z : blockIdx.z;
+  const int64_t i0 = by * PhiW1::BM;
   const int64_t c0 = (int64_t)blockIdx.x * PhiW1::BC + w * 128;
   // dsplit == 2 (symmetric layout): only the K-steps from the block's
   // diagonal tile on (the plain ones; NNX3Tile takes the transposed ones),
   // split over the z slices, which land in slices slice0 + z
-  int64_t kb0 = (int64_t)blockIdx.z * kchunk, kend = min(K, kb0 + kchunk);
+  int64_t kb0 = bz * kchunk, kend = min(K, kb0 + kchunk);
   if (dsplit == 2) {
     const int64_t len = ((K - i0) / gridDim.z + PhiW1::BJ - 1) / PhiW1::BJ * PhiW1::BJ;
-    kb0 = i0 + blockIdx.z * len;
+    kb0 = i0 + bz * len;
     kend = min(K, kb0 + len);
   }
   const int nsteps = kend > kb0 ? (int)((kend - kb0) / PhiW1::BJ) : 0;
-  C += (int64_t)(slice0 + blockIdx.z) * m * ldc;
-  rowsum += (int64_t)(slice0 + blockIdx.z) * roundup128(m);
+  C += (int64_t)(slice0 + bz) * m * ldc;
+  rowsum += (int64_t)(slice0 + bz) * roundup128(m);
   const float scale = -st->inv_h * kLog2e;
 
   // D: the block's panel row; thread t stages row t >> 1, columns 8 (t & 1) .. +7
