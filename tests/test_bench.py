@@ -1,4 +1,4 @@
-"""bench.py contract: the roofline traffic comes from the phi_mm launch of the
+"""bench.py contract: the roofline traffic comes from the phi_mm launches of the
 committed PMC summary, and the multi-rank path (barrier, max-over-ranks time,
 one JSON line from rank 0) runs under torch.distributed.run."""
 import json
@@ -13,20 +13,31 @@ sys.path.insert(0, ROOT)
 
 
 def test_pmc_traffic_picks_phi_mm():
+    """The quoted traffic is phi_mm's: the EXP=true NN tile (and, on the
+    symmetric layout, phi_w1's launch of the same step summed with it) --
+    never the logreg G.Xd launch of the same tile."""
     import bench
     summ = os.path.join(ROOT, "profiles", "latest_summary.json")
     if not os.path.exists(summ):
         pytest.skip("no committed PMC summary")
     with open(summ) as f:
         ks = json.load(f)["kernels"]
-    phi = [k for k in ks if k.startswith("void dsvgd::nn_x3_kernel<4, true, true,")]
+    nn = "void dsvgd::nn_x3_kernel<4, true, true,"
+    w1 = "_ZN5dsvgd13phi_w1_kernel"
+    phi = [k for k in ks if k.startswith(nn)]
     gxd = [k for k in ks if k.startswith("void dsvgd::nn_x3_kernel<4, true, false,")]
     assert len(phi) == 1, phi
-    traffic, src = bench.pmc_traffic("void dsvgd::nn_x3_kernel<4, true, true,")
+    traffic, src = bench.pmc_traffic([nn])
     assert traffic == ks[phi[0]]["hbm_bytes_per_launch"]
     assert src == os.path.join("profiles", "latest_summary.json")
     if gxd:  # the logreg G.Xd launch (same tile, no exp) must not be the one quoted
         assert traffic != ks[gxd[0]]["hbm_bytes_per_launch"]
+    both, _ = bench.pmc_traffic([nn, w1])
+    w = [k for k in ks if k.startswith(w1) and "hbm_bytes_per_launch" in ks[k]]
+    if w:
+        assert both == traffic + ks[w[0]]["hbm_bytes_per_launch"]
+    else:
+        assert both is None   # a launch of the pair missing: nothing quoted
 
 
 @pytest.mark.gpu
