@@ -263,13 +263,13 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
                          sym, colinv, 1, 0);
       const int rc = check_launch("nn_x3_kernel(lower)");
       if (rc) return rc;
-      hipLaunchKernelGGL(phi_w1_kernel, g2, dim3(PhiW1::kThreads), 0, s, D, K, Yx, ldy, K, kchunk,
-                         st, C, ldc, rowsum, m, row0, sym, colinv, 2, sl);
+      hipLaunchKernelGGL(phi_w1_kernel<2>, g2, dim3(PhiW1::kThreads), 0, s, D, K, Yx, ldy, K,
+                         kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, sl);
       return check_launch("phi_w1_kernel(upper)");
     }
     if (TN == 4 && EXP && (kPhiW1 == 2 || (kPhiW1 == 1 && !sym))) {
-      hipLaunchKernelGGL(phi_w1_kernel, grid, dim3(PhiW1::kThreads), 0, s, D, K, Yx, ldy, K, kchunk,
-                         st, C, ldc, rowsum, m, row0, sym, colinv, 0, 0);
+      hipLaunchKernelGGL(phi_w1_kernel<0>, grid, dim3(PhiW1::kThreads), 0, s, D, K, Yx, ldy, K,
+                         kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0);
       return check_launch("phi_w1_kernel");
     }
     hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2,

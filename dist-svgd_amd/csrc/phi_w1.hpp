@@ -49,11 +49,15 @@ __device__ __forceinline__ f32x4 w1_load_nt(__amdgpu_buffer_rsrc_t r, int voff, 
 
 // A: panel row of the block (panel layout, 128 x 16 fp32 panels); Yx: FmtH2
 // image [kstep][part][column][16 k]; K range [kchunk z, +kchunk) of K.
+// DS (compile-time dsplit): 0 = the K range [kchunk z, +kchunk); 2 = the
+// plain K-steps of a symmetric-layout row block (the hybrid's upper part)
+template <int DS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void phi_w1_kernel(
     const float* A, int64_t a_npad, const _Float16* Yx, int64_t ldy,
     int64_t K, int64_t kchunk, const dsvgd_select_state* __restrict__ st, float* __restrict__ C,
     int64_t ldc, float* __restrict__ rowsum, int64_t m, int64_t row0, int sym,
-    const float* __restrict__ colinv, int dsplit, int slice0) {
+    const float* __restrict__ colinv, int slice0) {
+  constexpr int dsplit = DS;
   using F = FmtH2;
   using V8 = F::V8;
   constexpr int P = PhiW1::P;
@@ -69,13 +73,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // dsplit == 2 (symmetric layout): only the K-steps from the block's
   // diagonal tile on (the plain ones; NNX3Tile takes the transposed ones),
   // split over the z slices, which land in slices slice0 + z
-  int64_t kb0 = bz * kchunk, kend = min(K, kb0 + kchunk);
-  if (dsplit == 2) {
-    const int64_t len = ((K - i0) / gridDim.z + PhiW1::BJ - 1) / PhiW1::BJ * PhiW1::BJ;
-    kb0 = i0 + bz * len;
-    kend = min(K, kb0 + len);
+  // K-step k of this block is global K-step ks0 + kdir * k.  dsplit == 2
+  // walks its range top-down, slice z taking every Z-th K-step: the blocks
+  // running together then read the same Yx K-steps at the same time (L2
+  // reuse), whatever row they start from
+  const int64_t kb0 = bz * kchunk, kend = min(K, kb0 + kchunk);
+  int ks0 = (int)(kb0 / PhiW1::BJ);
+  int nsteps = kend > kb0 ? (int)((kend - kb0) / PhiW1::BJ) : 0;
+  const int Z = (int)gridDim.z;
+  const int kdir = DS == 2 ? -Z : 1;
+  if (DS == 2) {
+    const int T = (int)((K - i0) / PhiW1::BJ);
+    ks0 = (int)(K / PhiW1::BJ) - 1 - (int)bz;
+    nsteps = T > bz ? (T - (int)bz + Z - 1) / Z : 0;
   }
-  const int nsteps = kend > kb0 ? (int)((kend - kb0) / PhiW1::BJ) : 0;
   C += (int64_t)(slice0 + bz) * m * ldc;
   rowsum += (int64_t)(slice0 + bz) * roundup128(m);
   const float scale = -st->inv_h * kLog2e;
@@ -93,7 +104,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int aoff = x3_off(srow, shalf);       // this thread's 16 B of a part image row
   // diagonal: global row - the thread's first column at K-step 0, clamped to
   // int range (only |.| < 16 matters)
-  const int64_t dg = row0 + i0 + srow - kb0 - 8 * shalf;
+  const int64_t dg = row0 + i0 + srow - 8 * shalf - (int64_t)ks0 * PhiW1::BJ;
   const int qd0 = (int)max(min(dg, (int64_t)(1 << 30)), (int64_t)-(1 << 30));
 
   f32x16 acc[4][4];
@@ -119,7 +130,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     f32x4 dr[4][2];   // D values: K-step k in dr[k & 3], loaded 3 K-steps ahead
     const int last = nsteps - 1;
     auto loadB = [&](int ni, int k) {
-      const int soff = (int)((kb0 >> 4) + min(k, last)) * P * pstride;
+      const int soff = (ks0 + kdir * min(k, last)) * P * pstride;
 #pragma unroll
       for (int p = 0; p < P; ++p)
         b[ni][p] = __builtin_bit_cast(V8, w1_load(rB, vB + ni * 1024, soff + p * pstride));
@@ -130,7 +141,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // base / lane offset / stride selected per K-step (uniform)
     auto loadD = [&](f32x4 (&d)[2], int k) {
       const int kc = min(k, last);
-      const int64_t j0 = kb0 + (int64_t)kc * PhiW1::BJ;
+      const int64_t j0 = (int64_t)(ks0 + kdir * kc) * PhiW1::BJ;
       const bool tr = (int)(j0 >> 7) < symI;  // wave-uniform
       const float* src = tr ? A + (((j0 >> 7) * pcols + symI * 8) * kPanelElems + (j0 & 127) * 16)
                             : A + (i0 >> 7) * pcols * kPanelElems + (j0 >> 4) * kPanelElems;
@@ -146,7 +157,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #else
     auto loadD = [&](f32x4 (&d)[2], int k) {
       const int kc = min(k, last);
-      const int64_t j0 = kb0 + (int64_t)kc * PhiW1::BJ;
+      const int64_t j0 = (int64_t)(ks0 + kdir * kc) * PhiW1::BJ;
       if ((int)(j0 >> 7) < symI) {  // wave-uniform
         const float* src = A + (((j0 >> 7) * pcols + symI * 8) * kPanelElems + (j0 & 127) * 16);
         const __amdgpu_buffer_rsrc_t rT =
@@ -156,7 +167,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           d[q >> 2][q & 3] = __builtin_bit_cast(
               float, __builtin_amdgcn_raw_buffer_load_b32(rT, vT + q * 64, 0, kW1Keep | 2));
       } else {
-        const int soff = (int)((kb0 >> 4) + kc) * kPanelElems * 4;
+        const int soff = (int)(j0 >> 4) * kPanelElems * 4;
         d[0] = w1_load_nt(rD, vD, soff);
         d[1] = w1_load_nt(rD, vD + 16, soff);
       }
@@ -164,7 +175,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #endif
     // exp2 / diagonal / row sum / 2-part split of K-step k's 8 values -> stage
     auto stage = [&](char* st_, const f32x4 (&d)[2], int k) {
-      const int qd = max(min(qd0 - k * PhiW1::BJ, 8), -1);  // diagonal column, or -1 / 8
+      // diagonal column among the thread's 8, or -1 / 8
+      const int qd = max(min(qd0 - kdir * k * PhiW1::BJ, 8), -1);
       float e[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
