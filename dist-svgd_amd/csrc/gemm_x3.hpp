@@ -394,6 +394,9 @@ struct NNX3Tile {
     return *reinterpret_cast<const f32x4*>(raw + a * kPanelElems * 4 + t * 16);
   }
 
+  // K-step stride of the 3-stage DMA path (run/step_dma3): BJ, or Z * BJ when
+  // Z split-K slices interleave their K-steps (slice z: z, z + Z, ...)
+  int64_t kst = BJ;
   // symmetric layout (dsvgd_sqdist_x3 layout 1): only tiles (I, J >= I) exist
   const float* sym_D = nullptr;  // whole panel-layout D, or null (full layout)
   int64_t sym_pcols = 0;         // n_pad / 16
@@ -525,9 +528,9 @@ struct NNX3Tile {
       } else if constexpr (NB == 3) {
         dma_b(smem, rB, ldy, k0);
         dma_d(raw, rA, k0);
-        if (k0 + BJ < k1) {
-          dma_b(smem + kStage, rB, ldy, k0 + BJ);
-          dma_d(raw + kSlot, rA, k0 + BJ);
+        if (k0 + kst < k1) {
+          dma_b(smem + kStage, rB, ldy, k0 + kst);
+          dma_d(raw + kSlot, rA, k0 + kst);
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB + AR) : "memory");
         } else {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -547,11 +550,11 @@ struct NNX3Tile {
           }
           return;
         }
-        for (int64_t j0 = k0; j0 < k1; j0 += 3 * BJ) {
+        for (int64_t j0 = k0; j0 < k1; j0 += 3 * kst) {
           step_dma3<0>(rA, rB, ldy, j0, k1, scale, smem, row_g0, wr, wc);
-          if (j0 + BJ < k1) step_dma3<1>(rA, rB, ldy, j0 + BJ, k1, scale, smem, row_g0, wr, wc);
-          if (j0 + 2 * BJ < k1)
-            step_dma3<2>(rA, rB, ldy, j0 + 2 * BJ, k1, scale, smem, row_g0, wr, wc);
+          if (j0 + kst < k1) step_dma3<1>(rA, rB, ldy, j0 + kst, k1, scale, smem, row_g0, wr, wc);
+          if (j0 + 2 * kst < k1)
+            step_dma3<2>(rA, rB, ldy, j0 + 2 * kst, k1, scale, smem, row_g0, wr, wc);
         }
         return;
       }
@@ -643,14 +646,14 @@ struct NNX3Tile {
     constexpr int NXT = (CUR + 1) % 3, NN = (CUR + 2) % 3;
     const char* cur = smem + CUR * kStage;
     char* raw = smem + kRaw;
-    const bool more = j0 + BJ < k1, more2 = j0 + 2 * BJ < k1;
+    const bool more = j0 + kst < k1, more2 = j0 + 2 * kst < k1;
     // kLateDma: issue tile k+2's DMAs after the first half's MFMAs (their
     // scalar address setup then runs in the MFMAs' shadow, not between the
     // barrier and the first MFMA); the DMAs still have 1.5 iterations to land
     auto issue = [&]() {
       if (more2) {
-        dma_b(smem + NN * kStage, rB, ldy, j0 + 2 * BJ);
-        dma_d(raw + NN * kSlot, rA, j0 + 2 * BJ);
+        dma_b(smem + NN * kStage, rB, ldy, j0 + 2 * kst);
+        dma_d(raw + NN * kSlot, rA, j0 + 2 * kst);
       }
     };
     if (!kLateDma) issue();
@@ -662,8 +665,8 @@ struct NNX3Tile {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
         for (int a = 0; a < AR; ++a) {
-          ra = raw_read(raw + NXT * kSlot, j0 + BJ, a);
-          store_a(smem + NXT * kStage, scale, row_g0 - (j0 + BJ), a);
+          ra = raw_read(raw + NXT * kSlot, j0 + kst, a);
+          store_a(smem + NXT * kStage, scale, row_g0 - (j0 + kst), a);
         }
       }
     };

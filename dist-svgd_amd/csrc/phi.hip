@@ -124,15 +124,17 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
   const int64_t i0 = by * Tile::BM;
   const int64_t c0 = (int64_t)blockIdx.x * Tile::BC;
   int64_t k0 = bz * kchunk, k1 = min(K, k0 + kchunk);
+  Tile tile;
   if (dsplit == 1) {
-    const int64_t len = (i0 / gridDim.z + kX3Step - 1) / kX3Step * kX3Step;
-    k0 = bz * len;
-    k1 = min(i0, k0 + len);
+    // slice z: K-steps z, z + Z, ... left of the diagonal tile, so the blocks
+    // running together read the same Yx K-steps (L2 reuse)
+    k0 = bz * kX3Step;
+    k1 = i0;
+    tile.kst = (int64_t)gridDim.z * kX3Step;
   }
   C += (int64_t)(slice0 + bz) * m * ldc;
   if (EXP) rowsum += (int64_t)(slice0 + bz) * roundup128(m);
   const float scale = EXP ? -st->inv_h * kLog2e : 0.f;
-  Tile tile;
   tile.prow = (a_npad >> 4) * kPanelElems * 4;
   if (DMA && sym) {  // symmetric layout: m == n, row0 == 0 (checked by the ABI)
     tile.sym_D = A;
