@@ -732,6 +732,13 @@ int64_t phi_splits(int64_t m, int64_t n, int64_t ldy) {
   int64_t s = 1;
   while (blocks * s < 512 && n_pad / (2 * s) >= 1024) s *= 2;
   while (n_pad / s > kMaxChain && s < 64) s *= 2;
+#ifndef DSVGD_SYM_SPLIT2X
+#define DSVGD_SYM_SPLIT2X 0
+#endif
+  // (A/B) the whole matrix (the symmetric layout's hybrid phi_mm gives each
+  // of its two launches half the slices): twice the slices, so a slice's
+  // chain stays within kMaxChain there too
+  if (DSVGD_SYM_SPLIT2X && m == n && s > 1 && s < 64) s *= 2;
   return s;
 }
 
