@@ -257,7 +257,11 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
       // symmetric layout split at each row block's diagonal tile: the
       // transposed K-steps on NNX3Tile (its LDS-rotated reads), the plain
       // ones on phi_w1; half the split-K slices each
-      const int sl = splits / 2;
+#ifndef DSVGD_HYB_SL
+#define DSVGD_HYB_SL 0
+#endif
+      // (A/B DSVGD_HYB_SL: NNX3Tile's slice count; 0 = half)
+      const int sl = DSVGD_HYB_SL > 0 && DSVGD_HYB_SL < splits ? DSVGD_HYB_SL : splits / 2;
       const dim3 g1(grid.x, grid.y, sl), g2(grid.x, grid.y, splits - sl);
       hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2,
                                        (TN != 1 && kPhiDA == 3) ? 3 : 2>), g1,
