@@ -313,6 +313,30 @@ def test_phi_full_size_sampled_rows():
     assert rel_err(got, ref) < PHI_TOL
 
 
+@pytest.mark.parametrize("n,d", [(4096, 1024), (8192, 256)])
+def test_phi_symmetric_hybrid_sampled_rows(n, d):
+    """The symmetric layout's phi_mm at split-K >= 2 is the hybrid (NNX3Tile on
+    each row block's transposed K-steps, phi_w1 on the rest, interleaved
+    slices): rows from every region of the triangle -- first and last row
+    blocks, block edges, the diagonal tiles -- vs fp64; d = 1024 runs four
+    column blocks per row block."""
+    rs = np.random.RandomState(n + d)
+    X = (0.2 * rs.randn(n, d)).astype(np.float32)
+    mu = rs.randn(d).astype(np.float32)
+    lam = rs.uniform(0.5, 2, d).astype(np.float32)
+    S = O.score_gaussian(X, mu, lam).astype(np.float32)
+    eng = dsvgd().PhiEngine(n, d, device=DEV)
+    assert eng.sym and eng.splits >= 2
+    eng.step(gpu(X), gpu(S), h=None)
+    h = eng.state.read()[1]
+    rows = np.unique(np.concatenate([np.arange(0, 130), np.arange(n - 130, n),
+                                     np.arange(127, n, 1024), np.arange(128, n, 1024),
+                                     rs.choice(n, 64, replace=False)]))
+    ref = O.phi(X, S, h, rows=rows)
+    got = eng.phi[torch.as_tensor(rows, device=DEV)].cpu().numpy()
+    assert rel_err(got, ref) < PHI_TOL
+
+
 # --------------------------------------------------------------- scores --
 def test_scores_match_oracle():
     T = dsvgd().targets
