@@ -11,6 +11,12 @@ One step = exchange + scores + median (exact radix select over n^2 distances)
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU, RCCL)
 
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment
+launches its N ranks itself (a torch.distributed.run child on 127.0.0.1,
+started before this process touches the GPU; like the reference harness's
+one-Process-per-rank launch, experiments/logreg.py:126-140) and relays rank
+0's line.  Every rank checks that the process group has exactly --gpus ranks.
+
 Prints ONE JSON line (rank 0).  value = n*K / max-over-ranks wall time of the K
 timed steps (whole job).  roofline: the dominant kernel (phi_mm, the fused
 exp + K.[Xc|S] MFMA GEMM) -- algorithmic 4*m*n*d flop per launch / its mean
@@ -160,7 +166,49 @@ def passes(eng, stages, m, n, d, n_local, score_gemm):
     return out
 
 
-def main():
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv):
+    """--gpus N > 1 without a launcher: run N ranks as a torch.distributed.run
+    child (one process per GPU, rendezvous on 127.0.0.1) and pass its output
+    through.  This process never initialises the GPU (device_count() does not
+    on this image), so the ranks own their devices; exits with the child's code."""
+    import subprocess
+    if args.backend == "nccl":
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print("bench.py: --gpus %d but only %d GPU(s) visible" % (args.gpus, have),
+                  file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    for line in proc.stdout:           # streamed: rank 0's JSON line and progress
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return proc.wait()
+
+
+def gather_max(d, world, backend, dev):
+    """{name: value} -> {name: max over ranks} (stage times at N > 1)."""
+    if world == 1:
+        return d
+    objs = [None] * world
+    dist.all_gather_object(objs, d)
+    keys = sorted(set().union(*[o.keys() for o in objs]))
+    return {k: max(o.get(k, 0.0) for o in objs) for k in keys}
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -175,11 +223,29 @@ def main():
                     help="MFMA engine of the contractions (h2: fp16 split, the default)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: CPU-staged rehearsal of the multi-rank path (e.g. 2 ranks on 1 GPU)")
-    args = ap.parse_args()
+    ap.add_argument("--launch-check", action="store_true",
+                    help="launcher self-test: ranks form the (gloo) group and report, no GPU work")
+    args = ap.parse_args(argv)
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args, argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        if world > 1:
+            dist.init_process_group("gloo")
+        seen = dist.get_world_size() if world > 1 else 1
+        ranks = [None] * seen
+        if world > 1:
+            dist.all_gather_object(ranks, rank)
+        if rank == 0:
+            print(json.dumps({"n_gpus": seen, "ranks": ranks if world > 1 else [0],
+                              "gpus_requested": args.gpus}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return 0 if seen == args.gpus else 3
     if args.backend == "gloo":
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
@@ -189,6 +255,13 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+        if dist.get_world_size() != args.gpus:
+            print("bench.py: process group has %d ranks but --gpus %d"
+                  % (dist.get_world_size(), args.gpus), file=sys.stderr)
+            return 3
+    elif args.gpus != 1:
+        print("bench.py: --gpus %d but WORLD_SIZE=1" % args.gpus, file=sys.stderr)
+        return 3
 
     import dsvgd
     from dsvgd.engine import StageTimer
@@ -232,6 +305,9 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     stages = {k: float(np.mean(v)) for k, v in timer.summary().items()}
+    # N > 1: each stage's mean HIP-event time, max over ranks (the exchange
+    # stages allgather_x / allreduce_scores / hist_allreduce included)
+    stages = gather_max(stages, world, args.backend, dev)
     assert bool(torch.isfinite(sampler._work).all()), "non-finite particles"
 
     m = n // world
@@ -293,6 +369,9 @@ def main():
         "gemm": gemm,
         "step_6n2d_f32_mfma_frac": (6.0 * m * n * d) / (el / args.steps) / 1e12 / PEAK_FP32_MFMA_TFLOPS,
         "phi_splits": int(eng.splits),
+        "process_group": {"backend": args.backend if world > 1 else None,
+                          "world_size_seen": dist.get_world_size() if world > 1 else 1,
+                          "stages": "mean per step, max over ranks" if world > 1 else "mean per step"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, d, xl, tl, args.cpu_budget)
@@ -300,7 +379,8 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -136,21 +136,6 @@ __device__ __forceinline__ void mfma_products(const typename F::V8 (&a)[TM][F::P
   for (int mi = 0; mi < TM; ++mi) acc[mi] = mfma_fmt<F>(a[mi][0], b[0], acc[mi]);
 }
 
-// the same products with the operands' MFMA roles exchanged: acc[mi] holds
-// the TRANSPOSED 32x32 tile (lane = a's row, registers = b's rows), same
-// products in the same order
-template <class F, int TM>
-__device__ __forceinline__ void mfma_products_tr(const typename F::V8 (&a)[TM][F::P],
-                                                 const typename F::V8 (&b)[F::P], f32x16* acc) {
-  static_assert(F::P == 2, "the transposed form is the FmtH2 Gram's");
-#pragma unroll
-  for (int mi = 0; mi < TM; ++mi) acc[mi] = mfma_fmt<F>(b[0], a[mi][1], acc[mi]);
-#pragma unroll
-  for (int mi = 0; mi < TM; ++mi) acc[mi] = mfma_fmt<F>(b[1], a[mi][0], acc[mi]);
-#pragma unroll
-  for (int mi = 0; mi < TM; ++mi) acc[mi] = mfma_fmt<F>(b[0], a[mi][0], acc[mi]);
-}
-
 // byte offset of (row or column x, 16-B half h) inside a part image
 __device__ __forceinline__ int x3_off(int x, int h) { return x * 32 + ((h ^ ((x >> 3) & 1)) << 4); }
 
@@ -185,35 +170,15 @@ __device__ __forceinline__ int x3_off(int x, int h) { return x * 32 + ((h ^ ((x 
 // NB (DMA path): ring stages.  2: iteration k DMAs tile k+1's B image (one
 // iteration to land); 3: tile k+2's B and D (two iterations; the closing
 // barrier then waits for no DMA at all).
-// DA (NB = 3, RW = 2): how far ahead the D panels are DMA'd.  2: with the B
-// image; 3: one K-step earlier than B, from a 4-slot raw ring -- D streams
-// from HBM once (nt) and lands later than the L2-resident B slices.
+// (Measured and dropped, DESIGN.md 3: D panels DMA'd three K-steps ahead, a
+// ping-pong staging order, DMA issue after the first MFMA half, branch-free
+// staging interleaved by sched_group_barrier.)
 template <int TN, bool DMA = true, bool EXP = true, bool M16 = false, int RW = 2, class F = FmtX3,
-          int NB = 2, int DA = 2>
+          int NB = 2>
 struct NNX3Tile {
   static constexpr int P = F::P;
   static_assert(NB == 2 || (NB == 3 && DMA), "3-stage ring: DMA path");
-  static_assert(DA == 2 || (DA == 3 && NB == 3 && RW == 2), "D three ahead: 3-stage ring, RW 2");
-  static constexpr int ND = DA == 3 ? 4 : NB;  // raw D slots
-#ifndef DSVGD_NN_PINGPONG
-#define DSVGD_NN_PINGPONG 0
-#endif
-  static constexpr bool kPingPong = DSVGD_NN_PINGPONG != 0;  // (step_dma3)
-#ifndef DSVGD_NN_LATE_DMA
-#define DSVGD_NN_LATE_DMA 0
-#endif
-  static constexpr bool kLateDma = DSVGD_NN_LATE_DMA != 0;  // (step_dma3)
-  static_assert(!(kPingPong && kLateDma), "early staging counts on this iteration's DMAs issued");
-#ifndef DSVGD_NN_SGB
-#define DSVGD_NN_SGB 0
-#endif
-  // kSgb (A/B): the next K-step's A staging (exp2 + split: VALU) made
-  // branch-free and spread between the K-step's MFMAs, kSgb VALU per MFMA,
-  // by sched_group_barrier (cdna_hip_programming.md T19); left to itself the
-  // compiler issues the staging after the MFMAs.  Measured (r5t, phi_mm
-  // S = 1): 0 (shipped) 12.46 ms, 1: 12.78, 2: 12.62, 4: 12.47 -- the
-  // staging's placement is not what holds the matrix pipe back
-  static constexpr int kSgb = DSVGD_NN_SGB;
+  static constexpr int ND = NB;  // raw D slots
   using V8 = typename F::V8;
   static_assert(!M16 || P == 3, "the 16x16x32 concatenated-k form is the 3-part format's");
   // (DMA needs the same DMA count in every wave: whole 512-chunk rounds)
@@ -319,10 +284,7 @@ struct NNX3Tile {
   // .s-level traps" (b)).
   static constexpr int kRaw = NB * kStage;  // D ring: NB slots x AR x 8 KiB raw panels
   static constexpr int kSlot = AR * kPanelElems * 4;
-#ifndef DSVGD_D_AUX
-#define DSVGD_D_AUX 2
-#endif
-  static constexpr int kDAux = DSVGD_D_AUX;  // D panels: nt (read once) so Yx stays in L2
+  static constexpr int kDAux = 2;  // D panels: nt (read once) so Yx stays in L2
 
   // aux: cache policy (2 = nt on gfx950: the D stream is read once)
   template <int AUX = 0>
@@ -501,31 +463,7 @@ struct NNX3Tile {
       const __amdgpu_buffer_rsrc_t rB =
           __builtin_amdgcn_make_buffer_rsrc((void*)Yx, (short)0, 0x7fffffff, 0x00020000);
       char* raw = smem + kRaw;
-      if constexpr (DA == 3) {
-        // prologue in steady-state issue order: B(0) D(0) | D(1) | B(1) D(2)
-        // (iteration k issues B(k+2) then D(k+3))
-        const bool m1 = k0 + BJ < k1, m2 = k0 + 2 * BJ < k1;
-        dma_b(smem, rB, ldy, k0);
-        dma_d(raw, rA, k0);
-        if (m1) dma_d(raw + kSlot, rA, k0 + BJ);
-        if (m1) dma_b(smem + kStage, rB, ldy, k0 + BJ);
-        if (m2) dma_d(raw + 2 * kSlot, rA, k0 + 2 * BJ);
-        if (m2)  // D(0) landed: D(1), B(1), D(2) may stay in flight
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB + 2 * AR) : "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        ra = raw_read(raw, k0, 0);
-        store_a(smem, scale, row_g0 - k0, 0);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        int k = 0;
-        for (int64_t j0 = k0; j0 < k1; j0 += 3 * BJ, k += 3) {
-          step_dma3d<0>(rA, rB, ldy, j0, k1, scale, smem, row_g0, wr, wc, k);
-          if (j0 + BJ < k1) step_dma3d<1>(rA, rB, ldy, j0 + BJ, k1, scale, smem, row_g0, wr, wc, k + 1);
-          if (j0 + 2 * BJ < k1)
-            step_dma3d<2>(rA, rB, ldy, j0 + 2 * BJ, k1, scale, smem, row_g0, wr, wc, k + 2);
-        }
-        return;
-      } else if constexpr (NB == 3) {
+      if constexpr (NB == 3) {
         dma_b(smem, rB, ldy, k0);
         dma_d(raw, rA, k0);
         if (k0 + kst < k1) {
@@ -541,15 +479,6 @@ struct NNX3Tile {
           store_a(smem, scale, row_g0 - k0, a);
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if constexpr (kSgb != 0 && EXP && RW == 2 && !M16 && !kPingPong && !kLateDma) {
-          for (int64_t j0 = k0; j0 < k1; j0 += 3 * BJ) {
-            step_dma3_sgb<0>(rA, rB, ldy, j0, k1, scale, smem, row_g0, wr, wc);
-            if (j0 + BJ < k1) step_dma3_sgb<1>(rA, rB, ldy, j0 + BJ, k1, scale, smem, row_g0, wr, wc);
-            if (j0 + 2 * BJ < k1)
-              step_dma3_sgb<2>(rA, rB, ldy, j0 + 2 * BJ, k1, scale, smem, row_g0, wr, wc);
-          }
-          return;
-        }
         for (int64_t j0 = k0; j0 < k1; j0 += 3 * kst) {
           step_dma3<0>(rA, rB, ldy, j0, k1, scale, smem, row_g0, wr, wc);
           if (j0 + kst < k1) step_dma3<1>(rA, rB, ldy, j0 + kst, k1, scale, smem, row_g0, wr, wc);
@@ -647,166 +576,25 @@ struct NNX3Tile {
     const char* cur = smem + CUR * kStage;
     char* raw = smem + kRaw;
     const bool more = j0 + kst < k1, more2 = j0 + 2 * kst < k1;
-    // kLateDma: issue tile k+2's DMAs after the first half's MFMAs (their
-    // scalar address setup then runs in the MFMAs' shadow, not between the
-    // barrier and the first MFMA); the DMAs still have 1.5 iterations to land
-    auto issue = [&]() {
-      if (more2) {
-        dma_b(smem + NN * kStage, rB, ldy, j0 + 2 * kst);
-        dma_d(raw + NN * kSlot, rA, j0 + 2 * kst);
-      }
-    };
-    if (!kLateDma) issue();
-    auto stage_next = [&]() {
-      if (more) {
-        if (more2)
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB + AR) : "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int a = 0; a < AR; ++a) {
-          ra = raw_read(raw + NXT * kSlot, j0 + kst, a);
-          store_a(smem + NXT * kStage, scale, row_g0 - (j0 + kst), a);
-        }
-      }
-    };
-    // kPingPong: the second wave of each SIMD (waves 4..7) stages first and
-    // the first wave halfway, so one wave's VALU staging runs beside the
-    // other's MFMAs instead of both SIMD waves leaving the matrix pipe idle
-    const bool early = kPingPong && (threadIdx.x >> 6) >= 4;
-    read_a(cur, wr);
-    if (early) stage_next();
-    compute<0, kHalf>(cur, wc);
-    if (kLateDma) issue();
-    if (!early) stage_next();
-    compute<kHalf, TN>(cur, wc);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  }
-
-  // ---- kSgb (EXP, RW = 2): the staging without branches, so that it and
-  // the K-step's MFMAs form one basic block -- one scheduling region in
-  // which sched_group_barrier can spread the staging VALU between MFMAs.
-  // The transposed read (symmetric layout) and the plain one are the same
-  // four ds_read_b32 with lane-selected addresses; the rotation takes a zero
-  // mask when not transposed; the diagonal test runs on every K-step; a
-  // K-step past the range stages stale values that nothing reads, and its
-  // row-sum share is selected away.
-  // bit select (m ? a : b per bit): one v_bfi_b32, never a branch
-  __device__ __forceinline__ static uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) {
-    return (a & m) | (b & ~m);
-  }
-  __device__ __forceinline__ static float fsel(uint32_t m, float a, float b) {
-    return __uint_as_float(bsel(m, __float_as_uint(a), __float_as_uint(b)));
-  }
-
-  __device__ __forceinline__ f32x4 raw_read_bf(const char* raw, int64_t j0) const {
-    const int t = threadIdx.x, row = t >> 2, c4 = t & 3;
-    const uint32_t m = transposed(j0) ? ~0u : 0u;  // wave-uniform
-    const float* rf = reinterpret_cast<const float*>(raw);
-    const int tb = (row >> 4) * 256 + (row & 15) + (4 * c4) * 16;
-    float v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      v[e] = rf[(int)bsel(m, (uint32_t)(tb + ((e + c4) & 3) * 16), (uint32_t)(4 * t + e))];
-    // rotate back (transposed only): lanes with c4 odd, then with c4 >= 2
-    const uint32_t so = m & (0u - (uint32_t)(c4 & 1)), sh = m & (0u - (uint32_t)(c4 >> 1));
-    float w[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) w[q] = fsel(so, v[(q + 3) & 3], v[q]);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = fsel(sh, w[(q + 2) & 3], w[q]);
-    return f32x4{v[0], v[1], v[2], v[3]};
-  }
-
-  __device__ __forceinline__ void store_a_bf(char* st, float scale, int64_t dgl, bool live) {
-    const int t = threadIdx.x, row = t >> 2, c4 = t & 3;
-    const int qd = (int)max(min(dgl, (int64_t)BJ), (int64_t)-BM - 4) + row - 4 * c4;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float e = __builtin_amdgcn_exp2f(fmaf(ra[q], scale, F::kAScaleLog2));
-      ra[q] = (qd == q) ? 0.f : e;
-    }
-    rs += fsel(live ? ~0u : 0u, (ra[0] + ra[1]) + (ra[2] + ra[3]), 0.f);
-    typename F::V4 sp[P];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      typename F::E v[P];
-      split_fmt<F>(ra[q], v);
-#pragma unroll
-      for (int p = 0; p < P; ++p) sp[p][q] = v[p];
-    }
-    const int off = x3_off(row, c4 >> 1) + ((c4 & 1) << 3);
-#pragma unroll
-    for (int p = 0; p < P; ++p) *reinterpret_cast<typename F::V4*>(st + p * BM * 32 + off) = sp[p];
-  }
-
-  template <int CUR>
-  __device__ __forceinline__ void step_dma3_sgb(__amdgpu_buffer_rsrc_t rA,
-                                                __amdgpu_buffer_rsrc_t rB, int64_t ldy,
-                                                int64_t j0, int64_t k1, float scale, char* smem,
-                                                int64_t row_g0, int wr, int wc) {
-    static_assert(EXP && RW == 2 && !M16, "the interleaved step is phi_mm's");
-    constexpr int NXT = (CUR + 1) % 3, NN = (CUR + 2) % 3;
-    const char* cur = smem + CUR * kStage;
-    char* raw = smem + kRaw;
-    const bool more = j0 + BJ < k1, more2 = j0 + 2 * BJ < k1;
     if (more2) {
-      dma_b(smem + NN * kStage, rB, ldy, j0 + 2 * BJ);
-      dma_d(raw + NN * kSlot, rA, j0 + 2 * BJ);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB + AR) : "memory");  // tile k+1's D landed
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      dma_b(smem + NN * kStage, rB, ldy, j0 + 2 * kst);
+      dma_d(raw + NN * kSlot, rA, j0 + 2 * kst);
     }
     read_a(cur, wr);
     compute<0, kHalf>(cur, wc);
-    ra = raw_read_bf(raw + NXT * kSlot, j0 + BJ);
-    store_a_bf(smem + NXT * kStage, scale, row_g0 - (j0 + BJ), more);
-    compute<kHalf, TN>(cur, wc);
-    __builtin_amdgcn_sched_group_barrier(0x100, 2 * P * TM / 2 + P * kHalf + 4, 0);  // DS reads
+    if (more) {
+      if (more2)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LB + AR) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int i = 0; i < 3 * TM * TN; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, kSgb, 0);  // VALU
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  }
-
-  // DA = 3, iteration k (tile j0, B stage CUR = k % 3, raw slot k % 4): DMA
-  // tile k+2's B into stage (k+2) % 3 and tile k+3's D into raw slot
-  // (k+3) % 4; halfway, tile k+1's D (issued at k-2: the DMAs of iterations
-  // k-1 and k may stay in flight) becomes its A in stage (k+1) % 3; before
-  // the barrier, tile k+1's B (issued at k-1, before D(k+2)) has landed.
-  // Near the end of the range (fewer DMAs issued) the waits drain fully.
-  template <int CUR>
-  __device__ __forceinline__ void step_dma3d(__amdgpu_buffer_rsrc_t rA, __amdgpu_buffer_rsrc_t rB,
-                                             int64_t ldy, int64_t j0, int64_t k1, float scale,
-                                             char* smem, int64_t row_g0, int wr, int wc, int k) {
-    constexpr int NXT = (CUR + 1) % 3, NN = (CUR + 2) % 3;
-    const char* cur = smem + CUR * kStage;
-    char* raw = smem + kRaw;
-    const bool more = j0 + BJ < k1, more2 = j0 + 2 * BJ < k1, more3 = j0 + 3 * BJ < k1;
-    if (more2) dma_b(smem + NN * kStage, rB, ldy, j0 + 2 * BJ);
-    if (more3) dma_d(raw + ((k + 3) & 3) * kSlot, rA, j0 + 3 * BJ);
-    auto stage_next = [&]() {
-      if (more) {
-        if (more3)
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (LB + AR)) : "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        ra = raw_read(raw + ((k + 1) & 3) * kSlot, j0 + BJ, 0);
-        store_a(smem + NXT * kStage, scale, row_g0 - (j0 + BJ), 0);
+      for (int a = 0; a < AR; ++a) {
+        ra = raw_read(raw + NXT * kSlot, j0 + kst, a);
+        store_a(smem + NXT * kStage, scale, row_g0 - (j0 + kst), a);
       }
-    };
-    const bool early = kPingPong && (threadIdx.x >> 6) >= 4;  // (step_dma3)
-    read_a(cur, wr);
-    if (early) stage_next();
-    compute<0, kHalf>(cur, wc);
-    if (!early) stage_next();
+    }
     compute<kHalf, TN>(cur, wc);
-    if (more3)
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(LB + 2 * AR) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
 
   // full row sum of row threadIdx.x >> 2 (4 consecutive lanes stage a row)
@@ -831,15 +619,12 @@ struct NNX3Tile {
 // are in acc16[4][2 TN] (16x16 layout) and both images must be unswizzled.
 // KS: 16-deep image K-steps per ring stage (one barrier per stage): 2 halves
 // the barriers per tile at twice the stage size.
-// TR: accumulate the transposed tile (mfma_products_tr): acc[mi][ni] lane l
-// holds row 32 mi + (l & 31), registers the columns c_row(r, l) of 32 ni --
-// four adjacent columns of one row per register quad.
 // WC: wave-contiguous DMA chunks -- wave w fills the 1 KiB chunks [w C,
 // (w + 1) C) of a stage (C = kChunksPerWave), so once every wave is past the
 // barrier that retires a stage, each wave's own C KiB of it stay untouched
 // until that wave issues its next DMA into it: private scratch in between.
 template <int TM, int TN, int WM, int WN, int NS = 3, bool M16 = false, class F = FmtX3, int KS = 1,
-          bool TR = false, bool WC = false>
+          bool WC = false>
 struct NTX3Tile {
   static constexpr int TM_ = TM, TN_ = TN, WM_ = WM, WN_ = WN;
   static constexpr bool M16_ = M16;
@@ -940,10 +725,7 @@ struct NTX3Tile {
   }
 
   // a0: image row of A's row 0, mod 16 (the image swizzles on the absolute
-  // row; a row block may start off a 16-row boundary).  FIRST (32x32 form):
-  // the tile's first stage -- its first MFMAs take C = 0 instead of the
-  // accumulators, so no pass re-zeroes them between tiles.
-  template <bool FIRST = false>
+  // row; a row block may start off a 16-row boundary).
   __device__ __forceinline__ void compute(const char* st, int wm, int wn, int a0 = 0) {
     if (M16) {  // lane (rr = l & 15, g = l >> 4): k-slot g >> 1 picks the part, g & 1 the half
       const int lane = threadIdx.x & 63, rr = lane & 15, g = lane >> 4, hh = g & 1, sl = g >> 1;
@@ -993,11 +775,8 @@ struct NTX3Tile {
                                               x3_off(wn * 32 * TN + ni * 32 + r, h));
         f32x16 c[TM];
 #pragma unroll
-        for (int mi = 0; mi < TM; ++mi) c[mi] = (FIRST && q == 0) ? f32x16{} : acc[mi][ni];
-        if constexpr (TR)
-          mfma_products_tr<F, TM>(a, b, c);
-        else
-          mfma_products<F, TM>(a, b, c);
+        for (int mi = 0; mi < TM; ++mi) c[mi] = acc[mi][ni];
+        mfma_products<F, TM>(a, b, c);
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi) acc[mi][ni] = c[mi];
       }

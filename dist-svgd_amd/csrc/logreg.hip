@@ -50,10 +50,7 @@ struct LogregWs {
 // G . Xd (K = N data rows, 256-row blocks): split K so that a launch has
 // about two blocks per CU (n = 65536 gives only 256 row blocks), each slice
 // at least 1024 rows deep; logreg_finish adds the slices in order.
-#ifndef DSVGD_GXD_SPLITS
-#define DSVGD_GXD_SPLITS 1  // shipped: no split (measured slower at S = 8); A/B builds: 2, 4
-#endif
-constexpr int kGxdMaxSplits = DSVGD_GXD_SPLITS;
+constexpr int kGxdMaxSplits = 1;  // 2, 4 measured slower at S = 8
 static int gxd_splits(int64_t n_pad, int64_t N_pad) {
   int sp = 1;
   while (sp < kGxdMaxSplits && (n_pad / 256) * sp < 512 && N_pad / (2 * sp) >= 1024) sp *= 2;
@@ -177,14 +174,11 @@ __device__ __forceinline__ void z_epilogue(T& tile, int64_t i0, int64_t q0,
 // lands while this one's epilogue (exp2, rcp, G stores) runs.
 // F = FmtX3: 16x16x32 (unswizzled W / Xd images); FmtH2: 32x32x16 on the
 // swizzled fp16 images of t_w W and t_x Xd (zsc = [1/t_w, 1/t_x]).
-// DSVGD_Z_KS (A/B): 16-deep image K-steps per ring stage of the FmtH2 Z
-// tiles (2, shipped: 32-deep stages, half the barriers, as the distance Gram;
-// scores -2.6 %, profiles/r5a_z_ks2_rank_ab.log)
-#ifndef DSVGD_Z_KS
-#define DSVGD_Z_KS 2
-#endif
+// FmtH2 Z tiles: two 16-deep image K-steps per ring stage (32-deep stages,
+// half the barriers, as the distance Gram; scores -2.6 % vs one,
+// profiles/r5a_z_ks2_rank_ab.log)
 template <class F>
-constexpr int z_ks() { return F::P == 2 ? DSVGD_Z_KS : 1; }
+constexpr int z_ks() { return F::P == 2 ? 2 : 1; }
 
 template <class F = FmtX3>
 __global__ __launch_bounds__(512, 1) void logreg_z_x3p_kernel(

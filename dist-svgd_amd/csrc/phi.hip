@@ -16,30 +16,14 @@
 #include "gemm_x3.hpp"
 #include "phi_w1.hpp"
 
-// DSVGD_PHI_DA: how many K-steps ahead the FmtH2 NN tile DMAs its D panels
-// (gemm_x3.hpp NNX3Tile DA: 2 = with the B image, 3 = one step earlier)
-#ifndef DSVGD_PHI_DA
-#define DSVGD_PHI_DA 2
-#endif
-
 namespace dsvgd {
 
-constexpr int kPhiDA = DSVGD_PHI_DA;
-// DSVGD_PHI_W1: phi_mm on the FmtH2 engine by phi_w1_kernel (one wave per
-// SIMD, B fragments straight from the image; phi_w1.hpp) -- 1 (default): the
-// full D layout (row blocks, S > 1), 2: also the symmetric layout (A/B: its
-// transposed K-steps still cost more than NNX3Tile's), 0: never
-#ifndef DSVGD_PHI_W1
-#define DSVGD_PHI_W1 1
-#endif
-constexpr int kPhiW1 = DSVGD_PHI_W1;
-// DSVGD_PHI_HYBRID: on the symmetric layout, NNX3Tile for each row block's
-// transposed K-steps and phi_w1 for the rest (two launches, half the split-K
-// slices each)
-#ifndef DSVGD_PHI_HYBRID
-#define DSVGD_PHI_HYBRID 1
-#endif
-constexpr bool kPhiHybrid = DSVGD_PHI_HYBRID != 0;
+// phi_mm on the FmtH2 engine (TN = 4): phi_w1_kernel (one wave per SIMD, B
+// fragments straight from the image; phi_w1.hpp) on the full D layout (row
+// blocks, S > 1); on the symmetric layout the hybrid -- NNX3Tile for each row
+// block's transposed K-steps, phi_w1 for the rest, two launches with half the
+// split-K slices each (phi_w1 alone, or a 3:1 / 1:3 slice split,
+// measured slower there).
 
 // blockIdx.z = split-K slice z: K columns [z*kchunk, min(K,(z+1)*kchunk)) into
 // the partial C + z*m*ldc (and rowsum + z*m_pad); phi_finish sums the slices
@@ -99,7 +83,7 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
 // F = FmtH2: C and rowsum come out of the MFMAs scaled by 2^15 (the A
 // staging scale) and C's column c by the B image's column scale: the stores
 // multiply by colinv[c] * 2^-15 (exact powers of two).
-template <int TN, bool DMA, bool EXP, bool M16, int RW = 2, class F = FmtX3, int NB = 2, int DA = 2>
+template <int TN, bool DMA, bool EXP, bool M16, int RW = 2, class F = FmtX3, int NB = 2>
 __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A, int64_t a_npad,
                                                     const typename F::E* __restrict__ Yx,
                                                     int64_t ldy, int64_t K, int64_t kchunk,
@@ -109,7 +93,7 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
                                                     int64_t row0, int sym,
                                                     const float* __restrict__ colinv,
                                                     int dsplit, int slice0) {
-  using Tile = NNX3Tile<TN, DMA, EXP, M16, RW, F, NB, DA>;
+  using Tile = NNX3Tile<TN, DMA, EXP, M16, RW, F, NB>;
   __shared__ __attribute__((aligned(16))) char smem[Tile::kSmemBytes];
   // dsplit (symmetric layout, 128-row blocks): 1 = only the K-steps left of
   // the block's diagonal tile (the transposed ones), longest rows first; the
@@ -253,18 +237,13 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
       hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F>), grid, dim3(512), 0, s, D, K,
                          Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0, 0);
   } else {  // FmtH2: the smaller stages fit a 3-stage ring
-    if (TN == 4 && EXP && sym && kPhiHybrid && splits >= 2 && kPhiW1 == 1) {
+    if (TN == 4 && EXP && sym && splits >= 2) {
       // symmetric layout split at each row block's diagonal tile: the
       // transposed K-steps on NNX3Tile (its LDS-rotated reads), the plain
       // ones on phi_w1; half the split-K slices each
-#ifndef DSVGD_HYB_SL
-#define DSVGD_HYB_SL 0
-#endif
-      // (A/B DSVGD_HYB_SL: NNX3Tile's slice count; 0 = half)
-      const int sl = DSVGD_HYB_SL > 0 && DSVGD_HYB_SL < splits ? DSVGD_HYB_SL : splits / 2;
+      const int sl = splits / 2;
       const dim3 g1(grid.x, grid.y, sl), g2(grid.x, grid.y, splits - sl);
-      hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2,
-                                       (TN != 1 && kPhiDA == 3) ? 3 : 2>), g1,
+      hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2>), g1,
                          dim3(512), 0, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0,
                          sym, colinv, 1, 0);
       const int rc = check_launch("nn_x3_kernel(lower)");
@@ -273,13 +252,12 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
                          kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, sl);
       return check_launch("phi_w1_kernel(upper)");
     }
-    if (TN == 4 && EXP && (kPhiW1 == 2 || (kPhiW1 == 1 && !sym))) {
+    if (TN == 4 && EXP && !sym) {
       hipLaunchKernelGGL(phi_w1_kernel<0>, grid, dim3(PhiW1::kThreads), 0, s, D, K, Yx, ldy, K,
                          kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0);
       return check_launch("phi_w1_kernel");
     }
-    hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2,
-                                     (TN != 1 && kPhiDA == 3) ? 3 : 2>), grid,
+    hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2>), grid,
                        dim3(512), 0, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym,
                        colinv, 0, 0);
   }
@@ -293,7 +271,9 @@ int nn_split_gemm(bool exp_, const float* A, int64_t K, const typename F::E* Yx,
                   int splits, const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum,
                   int64_t m, int64_t row0, hipStream_t s, int sym, int m16, const float* colinv) {
   if (F::P == 2) m16 = 0;  // the fp16 format runs the 32x32x16 form
-  if (K * ldy * 6 >= ((int64_t)1 << 31) || K * 128 * 4 >= ((int64_t)1 << 31))
+  // buffer offsets are 32-bit: K rows x ldy columns x P parts x 2 bytes of
+  // the image (as dsvgd_phi_mm_{h2,x3} check), K x 128 x 4 bytes of D
+  if (K * ldy * 2 * F::P >= ((int64_t)1 << 31) || K * 128 * 4 >= ((int64_t)1 << 31))
     return fail_arg("nn_x3: K x ldy too large for 32-bit buffer offsets");
   if (ldy % 128 != 0) return fail_arg("nn_x3: ldy must be a multiple of 128");
   if (!exp_ && (m16 || F::P == 2) && ldy % 512 != 0 && ldy % 256 == 0) {
@@ -724,10 +704,7 @@ int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, i
 // slices summed in slice order by phi_finish cut that.  FmtH2 at n = 65536:
 // 5.2e-7 with 8192-long slices, 7.8e-7 with 16384 (shipped: half the
 // partials to write and re-read, S = 1 step -1.7 %; profiles/r5g/).
-#ifndef DSVGD_MAX_CHAIN
-#define DSVGD_MAX_CHAIN 16384
-#endif
-constexpr int64_t kMaxChain = DSVGD_MAX_CHAIN;
+constexpr int64_t kMaxChain = 16384;
 
 int64_t phi_splits(int64_t m, int64_t n, int64_t ldy) {
   const int64_t cols = ldy % 512 == 0 ? 512 : (ldy % 256 == 0 ? 256 : 128);
@@ -736,13 +713,9 @@ int64_t phi_splits(int64_t m, int64_t n, int64_t ldy) {
   int64_t s = 1;
   while (blocks * s < 512 && n_pad / (2 * s) >= 1024) s *= 2;
   while (n_pad / s > kMaxChain && s < 64) s *= 2;
-#ifndef DSVGD_SYM_SPLIT2X
-#define DSVGD_SYM_SPLIT2X 0
-#endif
-  // (A/B) the whole matrix (the symmetric layout's hybrid phi_mm gives each
-  // of its two launches half the slices): twice the slices, so a slice's
-  // chain stays within kMaxChain there too
-  if (DSVGD_SYM_SPLIT2X && m == n && s > 1 && s < 64) s *= 2;
+  // (the symmetric layout's hybrid gives each of its two launches half the
+  // slices, so a chain reaches 2 kMaxChain there: 1.2e-6 phi error at n =
+  // 65536; twice the slices cost 1.4 % of phi_mm, profiles/r6y)
   return s;
 }
 

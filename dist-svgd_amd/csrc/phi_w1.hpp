@@ -29,22 +29,14 @@ struct PhiW1 {
   static constexpr int kSmemBytes = 2 * SA;
 };
 
-// aux bit 31 (volatile, compiler-only): the loads stay where they are issued --
-// otherwise the register allocator rematerialises these read-only loads next
-// to their uses, which turns every prefetch into an exposed L2/HBM wait
-#ifndef DSVGD_W1_SGB
-#define DSVGD_W1_SGB 4
-#endif
-#ifndef DSVGD_W1_KEEP
-#define DSVGD_W1_KEEP 0
-#endif
-constexpr int kW1Keep = DSVGD_W1_KEEP ? (int)(1u << 31) : 0;
+// VALU instructions placed after each of a K-step's first 16 MFMAs (the
+// staging of the next A image); 2 / 6 / 0 measured slower (profiles/r6g)
+constexpr int kW1Sgb = 4;
 __device__ __forceinline__ f32x4 w1_load(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kW1Keep));
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 __device__ __forceinline__ f32x4 w1_load_nt(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  return __builtin_bit_cast(f32x4,
-                            __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kW1Keep | 2));
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 2));
 }
 
 // A: panel row of the block (panel layout, 128 x 16 fp32 panels); Yx: FmtH2
@@ -135,26 +127,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int p = 0; p < P; ++p)
         b[ni][p] = __builtin_bit_cast(V8, w1_load(rB, vB + ni * 1024, soff + p * pstride));
     };
-#if DSVGD_PHI_W1 == 2
-    // (A/B) one load shape for both K-step kinds, no branch (so no PHI copies
-    // that wait for the loads): 8 dword loads at the thread's 8 values,
-    // base / lane offset / stride selected per K-step (uniform)
-    auto loadD = [&](f32x4 (&d)[2], int k) {
-      const int kc = min(k, last);
-      const int64_t j0 = (int64_t)(ks0 + kdir * kc) * PhiW1::BJ;
-      const bool tr = (int)(j0 >> 7) < symI;  // wave-uniform
-      const float* src = tr ? A + (((j0 >> 7) * pcols + symI * 8) * kPanelElems + (j0 & 127) * 16)
-                            : A + (i0 >> 7) * pcols * kPanelElems + (j0 >> 4) * kPanelElems;
-      const __amdgpu_buffer_rsrc_t rS =
-          __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, 0x7fffffff, 0x00020000);
-      const int vo = tr ? vT : vD;
-      const int stp = tr ? 64 : 4;
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        d[q >> 2][q & 3] =
-            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rS, vo, q * stp, 2));
-    };
-#else
     auto loadD = [&](f32x4 (&d)[2], int k) {
       const int kc = min(k, last);
       const int64_t j0 = (int64_t)(ks0 + kdir * kc) * PhiW1::BJ;
@@ -165,14 +137,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
         for (int q = 0; q < 8; ++q)
           d[q >> 2][q & 3] = __builtin_bit_cast(
-              float, __builtin_amdgcn_raw_buffer_load_b32(rT, vT + q * 64, 0, kW1Keep | 2));
+              float, __builtin_amdgcn_raw_buffer_load_b32(rT, vT + q * 64, 0, 2));
       } else {
         const int soff = (int)(j0 >> 4) * kPanelElems * 4;
         d[0] = w1_load_nt(rD, vD, soff);
         d[1] = w1_load_nt(rD, vD + 16, soff);
       }
     };
-#endif
     // exp2 / diagonal / row sum / 2-part split of K-step k's 8 values -> stage
     auto stage = [&](char* st_, const f32x4 (&d)[2], int k) {
       // diagonal column among the thread's 8, or -1 / 8
@@ -218,16 +189,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int mi = 0; mi < 4; ++mi) acc[mi][ni] = mfma_fmt<F>(a[mi][0], b[ni][0], acc[mi][ni]);
         loadB(ni, k + 1);
       }
-#if DSVGD_W1_SGB
       // one wave per SIMD: nothing else hides the staging VALU, so spread it
       // between the MFMAs (cdna_hip_programming.md T19): the A fragment reads,
-      // then 16 MFMAs each followed by up to DSVGD_W1_SGB VALU (the staging of
+      // then 16 MFMAs each followed by up to kW1Sgb VALU (the staging of
       // A(k+1)), its two LDS stores, then the other 32 MFMAs with the 8 B loads
       __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, DSVGD_W1_SGB, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, kW1Sgb, 0);
       }
       __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
 #pragma unroll
@@ -235,7 +205,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         if (i % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
       }
-#endif
       loadD(dl, k + 3);
     };
 
@@ -247,12 +216,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     loadD(dr[2], 2);
     stage(smem, dr[0], 0);
     barrier();
-    // unrolled by 4 (the D ring's slots are compile-time); the compiler's
+    // unrolled by 8 (the D ring's slots are compile-time); the compiler's
     // wait counts are exact inside the body, conservative at the loop head
-#ifndef DSVGD_W1_UNROLL8
-#define DSVGD_W1_UNROLL8 1
-#endif
-    for (int k = 0; k < nsteps; k += 4 * (1 + DSVGD_W1_UNROLL8)) {
+    // (unroll 4 -> 8: h2:full phi_mm 11.25 -> 11.05 ms, profiles/r6g)
+    for (int k = 0; k < nsteps; k += 8) {
       step(k, smem, smem + PhiW1::SA, dr[1], dr[3]);
       barrier();
       if (k + 1 >= nsteps) break;
@@ -264,9 +231,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if (k + 3 >= nsteps) break;
       step(k + 3, smem + PhiW1::SA, smem, dr[0], dr[2]);
       barrier();
-#if DSVGD_W1_UNROLL8
-      // a second copy: the loop head's conservative waits every 8 K-steps
-      // (h2:full phi_mm 11.25 -> 11.05 ms, profiles/r6g)
       if (k + 4 >= nsteps) break;
       step(k + 4, smem, smem + PhiW1::SA, dr[1], dr[3]);
       barrier();
@@ -279,7 +243,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if (k + 7 >= nsteps) break;
       step(k + 7, smem + PhiW1::SA, smem, dr[0], dr[2]);
       barrier();
-#endif
     }
   }
 

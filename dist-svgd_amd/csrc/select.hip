@@ -57,10 +57,9 @@ __device__ __forceinline__ void hist_key_agg(uint32_t key, uint32_t want, uint32
   }
 }
 
-#ifndef DSVGD_CAND_BLOCKS
-#define DSVGD_CAND_BLOCKS 1024  // shipped (4096: S=8 pass 0.058 -> 0.037 ms, config C -8.6 %; 512 slower at S=1)
-#endif
-constexpr int kCandBlocks = DSVGD_CAND_BLOCKS;
+// workgroups walking the candidate slots (4096 -> 1024: S = 8 pass 0.058 ->
+// 0.037 ms, config C -8.6 %; 512 slower at S = 1)
+constexpr int kCandBlocks = 1024;
 
 // count: entries of D (any order); cand: optional candidate buffer used
 // instead of D when st->fallback == 0 (bracketed mode).

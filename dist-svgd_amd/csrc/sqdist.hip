@@ -16,64 +16,17 @@
 #include "gemm_x3.hpp"
 #include "select.hpp"
 
-// DSVGD_SQ_EPI (compile time, A/B builds only -- scripts/ab_kernels.py):
-// 1 skips the mirror stores, 2 every D store, 3 the whole epilogue, to price
-// the epilogue; D is then incomplete.  The shipped library is built with 0.
-#ifndef DSVGD_SQ_EPI
-#define DSVGD_SQ_EPI 0
-#endif
-
 namespace dsvgd {
 
-constexpr int kSqEpi = DSVGD_SQ_EPI;
-// DSVGD_GRAM_H2_FORM (compile time, A/B builds): 0 = 256-tile blocks on a
-// 3-stage ring (shipped), 1 = half-tile blocks, two per CU
-#ifndef DSVGD_GRAM_H2_FORM
-#define DSVGD_GRAM_H2_FORM 0
-#endif
-constexpr int kGramH2Form = DSVGD_GRAM_H2_FORM;
-// DSVGD_GRAM_STAGGER (A/B, half-tile form): shader-clock cycles the second
-// block of each CU waits before its first unit, so the two blocks' epilogues
-// fall between the other's MFMA phases instead of together
-#ifndef DSVGD_GRAM_STAGGER
-#define DSVGD_GRAM_STAGGER 0
-#endif
-constexpr long long kGramStagger = DSVGD_GRAM_STAGGER;
-// DSVGD_GRAM_DMA_PROBE (A/B, timing only, wrong D): every tile DMAs the
-// operands of tile (0, 0), so the ring streams from L2 alone
-#ifndef DSVGD_GRAM_DMA_PROBE
-#define DSVGD_GRAM_DMA_PROBE 0
-#endif
-constexpr int kGramDmaProbe = DSVGD_GRAM_DMA_PROBE;
-// DSVGD_GRAM_KS (A/B): 16-deep image K-steps per ring stage of the FmtH2 Gram
-// (2, shipped: 32-deep stages, half the barriers, on a 2-stage ring; -5 %
-// vs 1 = 16-deep on a 3-stage ring, profiles/r4z_gram_ks2_ab.log)
-#ifndef DSVGD_GRAM_KS
-#define DSVGD_GRAM_KS 2
-#endif
-constexpr int kGramKS = DSVGD_GRAM_KS;
-// DSVGD_GRAM_WC (A/B): 1 = the bracket candidates of the 256-tile FmtH2 Gram
-// staged 32 deep in the wave's own chunks of the just-retired ring stage
-// (NTX3Tile WC, SlotWriterLdsT<32>), 0 = 8 deep in an LDS area of their own.
-// Shipped 1: S = 1 4.83 -> 4.49 ms, S = 8 1.21 -> 1.14 (profiles/r5o_gram_ab.log)
-#ifndef DSVGD_GRAM_WC
-#define DSVGD_GRAM_WC 1
-#endif
-constexpr bool kGramWC = DSVGD_GRAM_WC;
-// DSVGD_GRAM_ZEROC (A/B): 1 = a tile's first MFMAs take C = 0 (no re-zeroing
-// pass over the 128 accumulators per lane), 0 = the epilogue re-zeroes them
-// (shipped 0: the compiler materialises the zero operands, 300-600 spills)
-#ifndef DSVGD_GRAM_ZEROC
-#define DSVGD_GRAM_ZEROC 0
-#endif
-constexpr bool kGramZeroC = DSVGD_GRAM_ZEROC;
-// DSVGD_GRAM_NPF (A/B): 1 = a tile's 512 norms loaded into registers at its
-// first stage (latency under the MFMAs), 0 = loaded at its epilogue (shipped
-// 0: 4.41 vs 4.49 ms with the prefetch, r5o)
-#ifndef DSVGD_GRAM_NPF
-#define DSVGD_GRAM_NPF 0
-#endif
-constexpr bool kGramNpf = DSVGD_GRAM_NPF;
+// The FmtH2 Gram (sqdist_x3w_kernel) runs 256-tile blocks, one per CU, on a
+// 2-stage ring of 32-deep stages (two 16-deep image K-steps per barrier: -5 %
+// vs 16-deep stages on a 3-stage ring), the bracket candidates staged 32 deep
+// in the wave's own chunks of the just-retired ring stage (S = 1 4.83 -> 4.49
+// ms).  Measured and dropped: half-tile blocks two per CU, with
+// or without a staggered start; C = 0 first MFMAs; norms prefetched at a
+// tile's first stage; transposed accumulators with 16-byte D stores.
+constexpr int kGramKS = 2;
+constexpr bool kGramWC = true;
 
 using GramTile = NTTile<2, 2, 2, 2>;  // 128 x 128 block, 4 waves of 64 x 64
 
@@ -93,7 +46,7 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
                                             float* __restrict__ D, const float* srow,
                                             const float* scol, int rbase, int cbase,
                                             WindowHist& wh, uint32_t* shist, SW& sw,
-                                            const SlotLayout& sl, int64_t slot, int epi,
+                                            const SlotLayout& sl, int64_t slot,
                                             bool mirror_store = true, int r0t = 0,
                                             float c2 = 2.f) {
   // r0t: row0 / 128 when a row block's diagonal square runs SYM (bi is then
@@ -145,9 +98,9 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        if (kSqEpi < 2 || v[r] != v[r])  // streamed out: nt, so D does not evict the Gram operands from L2
-          __builtin_nontemporal_store(v[r], dp0 + (r & 3) * 16 + (r >> 2) * 128);
-      if (MIR && mirror && mirror_store && (kSqEpi == 0 || v[0] != v[0])) {  // D[j][i]: 4 consecutive i per register quad -> 16-byte stores
+        // streamed out: nt, so D does not evict the Gram operands from L2
+        __builtin_nontemporal_store(v[r], dp0 + (r & 3) * 16 + (r >> 2) * 128);
+      if (MIR && mirror && mirror_store) {  // D[j][i]: 4 consecutive i per register quad -> 16-byte stores
         float* const mp0 = Dmir + (uint32_t)(cl * 16 + ((rbase >> 4) + mi * 2) * kPanelElems + h4);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -172,103 +125,6 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
   if (smode == kSelBracket) sw.finish(sl, slot, mirror);
 }
 
-// D stores of the transposed epilogue: 16 bytes per lane through a buffer
-// descriptor on the tile, cache policy kDStorePolicy (DSVGD_D_STORE_POLICY,
-// A/B: 0 plain, 2 nt, 16 sc1 = written through and dropped from L2).
-// Measured (profiles/r5n_gram_tr_ab.log, S = 1 / S = 8 rank share): the
-// shipped form 4.80 / 1.17 ms; transposed + nt 5.53 / 1.45, + plain 5.80 /
-// 1.42, + sc1 8.93 / 2.08 -- the transposed bracket kernels spill (180
-// scratch ops) and sc1 stores pay a fabric write each; kept as an A/B only.
-#ifndef DSVGD_D_STORE_POLICY
-#define DSVGD_D_STORE_POLICY 2
-#endif
-constexpr int kDStorePolicy = DSVGD_D_STORE_POLICY;
-// DSVGD_GRAM_TR (A/B): 1 = the FmtH2 Gram on transposed accumulators
-// (sq_epilogue_tr) where no mirror tile is stored, 0 = sq_epilogue
-// everywhere (shipped: see above)
-#ifndef DSVGD_GRAM_TR
-#define DSVGD_GRAM_TR 0
-#endif
-
-// sq_epilogue on transposed accumulators (NTX3Tile TR): lane l holds row
-// rbase + 32 mi + (l & 31) of the tile and, per register quad q, the four
-// adjacent columns cbase + 32 ni + 8 q + 4 (l >> 5) + 0..3 -- one 16-byte
-// store into the panel layout (a panel row is 16 adjacent columns).  Same
-// values (the norm sum is commutative, the MFMA products the same), same
-// select accounting; no mirror stores (launches that need them run sq_epilogue).
-template <bool SYM, int smode, class Tile, int NI, class SW>
-__device__ __forceinline__ void sq_epilogue_tr(Tile& tile, int bi, int bj, int64_t row0,
-                                               int64_t m, int64_t n, int64_t n_pad,
-                                               float* __restrict__ D, const float* srow,
-                                               const float* scol, int rbase, int cbase,
-                                               WindowHist& wh, uint32_t* shist, SW& sw,
-                                               const SlotLayout& sl, int64_t slot, int r0t,
-                                               float c2) {
-  const int lane = threadIdx.x & 63, il = lane & 31, h4 = 4 * (lane >> 5);
-  const bool mirror = SYM && bi + r0t != bj;
-  const int64_t i0 = (int64_t)bi * 128, j0 = (int64_t)bj * 128;
-  const uint32_t weight = mirror ? 2u : 1u;
-  const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(D + ((int64_t)bi * (n_pad >> 4) + (int64_t)bj * 8) * kPanelElems), (short)0,
-      0x7fffffff, 0x00020000);
-  const bool interior = (row0 + i0 + 128 <= j0 || j0 + 128 <= row0 + i0) && i0 + 128 <= m &&
-                        j0 + 128 <= n;
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi) {
-    const int rl = rbase + mi * 32 + il;  // this lane's row in the tile
-    const float ni_ = srow[rl];
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      const int cb = cbase + ni * 32;  // the sub-tile's first column
-      f32x4 nc[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) nc[q] = *reinterpret_cast<const f32x4*>(scol + cb + 8 * q + h4);
-      float v[16];
-      if (interior) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          v[r] = fmaxf(0.f, (ni_ + nc[r >> 2][r & 3]) - c2 * tile.acc[mi][ni][r]);
-      } else {
-        const bool rowok = i0 + rl < m;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int cl = cb + 8 * (r >> 2) + h4 + (r & 3);
-          float x;
-          if (rowok && j0 + cl < n)
-            x = (row0 + i0 + rl == j0 + cl)
-                    ? 0.f
-                    : fmaxf(0.f, (ni_ + nc[r >> 2][r & 3]) - c2 * tile.acc[mi][ni][r]);
-          else
-            x = INFINITY;
-          v[r] = x;
-        }
-      }
-      // panel (cb >> 4) + (q >> 1), row rl, columns 8 (q & 1) + h4 .. + 3
-      const int off = 4 * ((cb >> 4) * kPanelElems + rl * 16 + h4);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(u32x4, (f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]})),
-            rD, off + 4 * ((q >> 1) * kPanelElems + 8 * (q & 1)), 0, kDStorePolicy);
-      if (smode == kSelHist) {
-        if (mi == 0 && ni == 0) wh.init(v[0]);
-        hist_account(wh, v, weight, shist);
-      } else if (smode == kSelBracket) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          sw.add(v[r]);
-          if (((mi * NI + ni) * 16 + r + 1) % SW::kDepth == 0) sw.flush();
-        }
-      }
-      if (!kGramZeroC) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) tile.acc[mi][ni][r] = 0.f;
-      }
-    }
-  }
-  if (smode == kSelBracket) sw.finish(sl, slot, mirror);
-}
-
 // sq_epilogue for 16x16x32 tiles (NTX3Tile M16): the wave holds rows
 // [rbase, rbase + 64) x columns [cbase, cbase + 32 TN) of tile (bi, bj) as
 // acc16[mt][nt], lane (col lane & 15, rows 4 (lane >> 4) + r); a lane's 4
@@ -279,7 +135,7 @@ __device__ __forceinline__ void sq_epilogue16(Tile& tile, int bi, int bj, int64_
                                               float* __restrict__ D, const float* srow,
                                               const float* scol, int rbase, int cbase,
                                               WindowHist& wh, uint32_t* shist, SlotWriter& sw,
-                                              const SlotLayout& sl, int64_t slot, int epi,
+                                              const SlotLayout& sl, int64_t slot,
                                               bool mirror_store, int r0t) {
   const int lane = threadIdx.x & 63, g4 = 4 * (lane >> 4);
   const bool mirror = SYM && bi + r0t != bj;
@@ -319,8 +175,8 @@ __device__ __forceinline__ void sq_epilogue16(Tile& tile, int bi, int bj, int64_
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (kSqEpi < 2 || v[r] != v[r]) __builtin_nontemporal_store(v[r], dp0 + r * 16);
-      if (mirror && mirror_store && (kSqEpi == 0 || v[0] != v[0]))  // D[j][i], i = rb .. rb + 3
+        __builtin_nontemporal_store(v[r], dp0 + r * 16);
+      if (mirror && mirror_store)  // D[j][i], i = rb .. rb + 3
         *reinterpret_cast<f32x4*>(Dmir + ((rbase >> 4) + mt) * kPanelElems + (int64_t)cl * 16 +
                                   g4) = f32x4{v[0], v[1], v[2], v[3]};
       if (smode == kSelHist) {
@@ -349,7 +205,7 @@ template <bool SYM, int smode>
 __global__ __launch_bounds__(256, 2) void sqdist_persistent_kernel(
     const float* __restrict__ Y, int64_t ldy, const float* __restrict__ norms, int64_t row0,
     int64_t m, int64_t n, int64_t n_pad, int dp, float* __restrict__ D,
-    dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int epi, int64_t total) {
+    dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int64_t total) {
   __shared__ __attribute__((aligned(16))) float smem[GramTile::kSmemFloats];
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
   __shared__ float snorm[2][GramTile::BM + GramTile::BN];  // current / next tile
@@ -429,13 +285,8 @@ __global__ __launch_bounds__(256, 2) void sqdist_persistent_kernel(
     WindowHist wh;
     SlotWriter sw;
     if (smode == kSelBracket) sw.begin(st, sl, slot);
-    if (kSqEpi == 3) {  // timing only: no epilogue at all
-      tile.zero();
-    } else {
-      sq_epilogue<SYM, smode, true>(tile, bi, bj, row0, m, n, n_pad, D, snorm[par],
-                                    snorm[par] + 128, wm * 64, wn * 64, wh, shist, sw, sl, slot,
-                                    epi);
-    }
+    sq_epilogue<SYM, smode, true>(tile, bi, bj, row0, m, n, n_pad, D, snorm[par],
+                                  snorm[par] + 128, wm * 64, wn * 64, wh, shist, sw, sl, slot);
     if (smode == kSelHist) wh.flush(shist);
     par ^= 1;
     L = Ln;
@@ -450,9 +301,9 @@ __global__ __launch_bounds__(256, 2) void sqdist_persistent_kernel(
 
 // The persistent distance kernel on the split engines (gemm_x3.hpp): the
 // Gram from the row image Yg of Y[:, :dp] (n_pad image rows), fp32-accurate,
-// K-steps of 16 through a 2-stage LDS-DMA ring that runs across tile
-// boundaries (the next tile's first K-step lands during this tile's last
-// one); tile order and select accounting as sqdist_persistent_kernel.
+// through a 2-stage LDS-DMA ring that runs across tile boundaries (the next
+// tile's first K-step lands during this tile's last one); tile order and
+// select accounting as sqdist_persistent_kernel.
 // 256 x 256 tiles (8 waves of 64 x 128, one block per CU): twice the MFMAs
 // per operand byte of a 128 x 128 form.  Each wave's 64 x 128
 // region lies in one 128 x 128 sub-tile (2 BI + (wr >> 1), 2 BJ + wc); the
@@ -462,57 +313,37 @@ __global__ __launch_bounds__(256, 2) void sqdist_persistent_kernel(
 // swizzled one (FmtH2).
 // F = FmtH2: Yg is the fp16 image of t Xc (t = tsc[0]), the Gram comes out
 // scaled by t^2: the epilogue's 2 x.y is c2 acc with c2 = 2 / t^2.
-// WN = 1: a block of 4 waves (one per SIMD) takes HALF a 256-tile (256 rows x
-// 128 columns, unit = 2 L + h) and two such blocks share a CU: they drift
-// apart, so one block's epilogue (D stores, select accounting) runs beside
-// the other's MFMAs instead of every SIMD idling its MFMA pipe through it.
-// NS: LDS ring stages (2: a K-step's DMA has one K-step to land; 3: two).
-template <bool SYM, int smode, bool M16 = true, class F = FmtX3, int WN = 2, int NS = 2, int KS = 1,
-          bool TR = false, bool MIR = true>
-__global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
+// KS: 16-deep image K-steps per ring stage.
+template <bool SYM, int smode, bool M16 = true, class F = FmtX3, int KS = 1, bool MIR = true>
+__global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
     const typename F::E* __restrict__ Yg, int64_t img_rows, const float* __restrict__ norms,
     int64_t row0, int64_t m, int64_t n, int64_t n_pad, int nk, float* __restrict__ D,
-    dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int epi, int64_t total_tiles,
+    dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int64_t total_tiles,
     int layout, int Tm2, int Tc2, int bj_off, int r0t, int64_t slot_base, int64_t ns_total,
     const float* __restrict__ tsc) {
   // candidates staged in the retired ring stage (bracket mode, 32x32 form,
-  // 2-stage ring of 32-deep stages)
-  constexpr bool kWC = kGramWC && smode == kSelBracket && !M16 && NS == 2 && KS == 2 && WN == 2;
-  constexpr bool kZeroC = kGramZeroC && !M16;
-  using GramX3WTile = NTX3Tile<2, 4, 4, WN, NS, M16, F, KS, TR, kWC>;
+  // 32-deep stages)
+  constexpr bool kWC = kGramWC && smode == kSelBracket && !M16 && KS == 2;
+  using GramX3WTile = NTX3Tile<2, 4, 4, 2, 2, M16, F, KS, kWC>;
   static_assert(!kWC || GramX3WTile::kChunksPerWave * 1024 >= 64 * 32 * 4,
                 "32-deep candidate lists fit the wave's chunks");
-  constexpr int kT = GramX3WTile::kThreads, kUnits = 2 / WN;  // units per 256-tile
-  constexpr int kBN = GramX3WTile::BN;                         // 256 or 128 columns
+  constexpr int kT = GramX3WTile::kThreads;
   const float c2 = F::P == 3 ? 2.f : 2.f * tsc[1] * tsc[1];
   __shared__ __attribute__((aligned(16))) char smem[GramX3WTile::kSmemBytes];
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
-  __shared__ float snorm[256 + kBN];  // the unit's 256 row norms, then its column norms
+  __shared__ float snorm[512];  // the tile's 256 row norms, then its 256 column norms
   // bracket candidates staged per lane (SlotWriterLds) on the 32x32 form
   constexpr bool kLdsSlots = smode == kSelBracket && !M16;
   __shared__ float scand[kLdsSlots && !kWC ? (kT / 64) * 64 * kStageDepth : 1];
-  constexpr int kNR = (256 + kBN + kT - 1) / kT;  // norms per thread
-  float nreg[kNR];
-  // the norms of unit (BI, BJ): rows 256 BI.., then columns kBN BJ..
-  auto load_norms = [&](int BI, int BJ) {
-#pragma unroll
-    for (int i = 0; i < kNR; ++i) {
-      const int e = (int)threadIdx.x + i * kT;
-      const int64_t gi = e < 256 ? row0 + (int64_t)BI * 256 + e : (int64_t)BJ * kBN + e - 256;
-      nreg[i] = (e < 256 + kBN && gi < n_pad) ? norms[gi] : 0.f;
-    }
-  };
 
   // this launch: Tm2 x Tc2 256-tiles, global column tiles from bj_off
   // (SYM: the triangle of a Tm2 x Tm2 square; r0t = its row0 / 128)
   const int Tm = (int)(roundup128(m) / 128), Tn = (int)(n_pad / 128);  // 128-tiles
   // the wave index made provably uniform: tile, slot and D-tile bases derived
   // from it stay in SGPRs (stores take the SGPR-base + 32-bit offset form)
-  const int t = threadIdx.x, w = __builtin_amdgcn_readfirstlane(t >> 6), wr = w / WN,
-            wc = w % WN;
-  const int64_t total = total_tiles * kUnits;
+  const int t = threadIdx.x, w = __builtin_amdgcn_readfirstlane(t >> 6), wr = w / 2, wc = w % 2;
   const int64_t x = blockIdx.x % kXcds, u = blockIdx.x / kXcds, U = gridDim.x / kXcds;
-  const int64_t q = total / kXcds, rr = total % kXcds;
+  const int64_t q = total_tiles / kXcds, rr = total_tiles % kXcds;
   const int64_t lo = x * q + min(x, rr);
   const int64_t hi = (int64_t)__builtin_amdgcn_readfirstlane((int)(lo + q + (x < rr ? 1 : 0)));
   SlotLayout sl(cand, ns_total, smode == kSelBracket ? st->cand_cap : 0);
@@ -520,44 +351,38 @@ __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
   if (smode == kSelHist)
     for (int b = t; b < DSVGD_RADIX_BINS; b += kT) shist[b] = 0u;
 
-  // unit L -> 256-tile (BI, BJ) and (WN = 1) its column half L & 1; BJ is
-  // returned in units of kBN columns (the unit's first column / kBN)
+  // tile L -> 256-tile (BI, BJ); BJ returned as the global 256-column tile
   auto next_valid = [&](int64_t L, int& BI, int& BJ) -> int64_t {
     for (; L < hi; L += U) {
-      if (tile_at(L / kUnits, Tm2, Tc2, SYM, BI, BJ)) {
-        const int bjc = (BJ + bj_off) * kUnits + (int)(L % kUnits);
-        // a half past the padded matrix, or (SYM) wholly below the diagonal
-        if (kUnits == 1 || (bjc < Tn && !(SYM && 2 * BI + r0t > bjc))) {
-          BI = __builtin_amdgcn_readfirstlane(BI);
-          BJ = __builtin_amdgcn_readfirstlane(bjc);
-          return L;
-        }
+      if (tile_at(L, Tm2, Tc2, SYM, BI, BJ)) {
+        BI = __builtin_amdgcn_readfirstlane(BI);
+        BJ = __builtin_amdgcn_readfirstlane(BJ + bj_off);
+        return L;
       }
-      if (smode == kSelBracket) slot_clear(sl, slot_base + L * (8 / kUnits) + w);
+      if (smode == kSelBracket) slot_clear(sl, slot_base + L * 8 + w);
     }
     return L;
   };
   GramX3WTile tile;
   auto issue = [&](char* stg, int BI, int BJ, int ks) {
-    if constexpr (kGramDmaProbe != 0) BI = BJ = 0;
     const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(Yg + (row0 + (int64_t)BI * 256) * 16), (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(Yg + (int64_t)BJ * kBN * 16), (short)0, 0x7fffffff, 0x00020000);
+        (void*)(Yg + (int64_t)BJ * 256 * 16), (short)0, 0x7fffffff, 0x00020000);
     tile.dma(stg, rA, img_rows, rB, img_rows, ks);
   };
 
   // tile (L, BI, BJ) done (its last stage retired from ring stage stg):
   // norms, per-sub-tile epilogue
   auto epilogue = [&](int64_t L, int BI, int BJ, int stg) {
-    if (!kGramNpf) load_norms(BI, BJ);
-#pragma unroll
-    for (int i = 0; i < kNR; ++i)
-      if (t + i * kT < 256 + kBN) snorm[t + i * kT] = nreg[i];
+    {
+      const int64_t gi = t < 256 ? row0 + (int64_t)BI * 256 + t : (int64_t)BJ * 256 + t - 256;
+      snorm[t] = gi < n_pad ? norms[gi] : 0.f;
+    }
     __syncthreads();
     // this wave's 128-sub-tile
-    const int bi = 2 * BI + (wr >> 1), bj = BJ * (kBN / 128) + wc;
-    const int64_t slot = slot_base + L * (8 / kUnits) + w;
+    const int bi = 2 * BI + (wr >> 1), bj = 2 * BJ + wc;
+    const int64_t slot = slot_base + L * 8 + w;
     WindowHist wh;
     using SW = std::conditional_t<kWC, SlotWriterLdsT<32>,
                                   std::conditional_t<kLdsSlots, SlotWriterLds, SlotWriter>>;
@@ -570,111 +395,49 @@ __global__ __launch_bounds__(256 * WN, 2 / WN) void sqdist_x3w_kernel(
       sw.begin(st, sl, slot, scand + w * 64 * kStageDepth);
     else if (smode == kSelBracket)
       sw.begin(st, sl, slot);
-    if (kSqEpi == 3 || bi >= Tm || bj >= Tn || (SYM && bi + r0t > bj)) {
+    if (bi >= Tm || bj >= Tn || (SYM && bi + r0t > bj)) {
       tile.zero();
       if (smode == kSelBracket) sw.finish(sl, slot, false);
     } else {
-      if constexpr (TR)
-        sq_epilogue_tr<SYM, smode, GramX3WTile, 4, SW>(
-            tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128, snorm + 256 + wc * 128,
-            (wr & 1) * 64, 0, wh, shist, sw, sl, slot, r0t, c2);
-      else if constexpr (M16)
+      if constexpr (M16)
         sq_epilogue16<SYM, smode>(tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128,
                                   snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl,
-                                  slot, epi, layout == 0, r0t);
+                                  slot, layout == 0, r0t);
       else
-        sq_epilogue<SYM, smode, !kZeroC, GramX3WTile, 4, SW, MIR>(
+        sq_epilogue<SYM, smode, true, GramX3WTile, 4, SW, MIR>(
             tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128,
-            snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl, slot, epi, layout == 0,
+            snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl, slot, layout == 0,
             r0t, c2);
     }
     if (smode == kSelHist) wh.flush(shist);
   };
 
-  if constexpr (WN == 1 && kGramStagger > 0) {
-    if (blockIdx.x >= gridDim.x / 2) {  // the CUs' second blocks (dispatched after one per CU)
-      const long long t0 = __builtin_amdgcn_s_memtime();
-      while (__builtin_amdgcn_s_memtime() - t0 < kGramStagger) __builtin_amdgcn_s_sleep(8);
-    }
-  }
   int BI = 0, BJ = 0;
   int64_t L = next_valid((int64_t)__builtin_amdgcn_readfirstlane((int)(lo + u)), BI, BJ);
   tile.zero();
-  if constexpr (NS == 3) {
-    // positions of the next two K-steps (the ring runs two ahead, across tiles)
-    int ks = 0, stage = 0;
-    int64_t L1 = L, L2;
-    int BI1 = BI, BJ1 = BJ, ks1 = 1, BI2, BJ2, ks2;
-    if (ks1 == nk) {
-      L1 = next_valid(L + U, BI1, BJ1);
-      ks1 = 0;
+  if (L < hi) issue(smem, BI, BJ, 0);
+  GramX3WTile::template ring_barrier<0>();
+  int ks = 0, stage = 0;
+  int BIn = BI, BJn = BJ;
+  int64_t Ln = L;
+  while (L < hi) {
+    int ksn = ks + 1;
+    if (ksn == nk) {
+      Ln = next_valid(L + U, BIn, BJn);
+      ksn = 0;
     }
-    auto advance = [&](int64_t La, int BIa, int BJa, int ka, int64_t& Lb, int& BIb, int& BJb,
-                       int& kb) {
-      Lb = La;
-      BIb = BIa;
-      BJb = BJa;
-      kb = ka + 1;
-      if (kb == nk) {
-        Lb = La < hi ? next_valid(La + U, BIb, BJb) : La;
-        kb = 0;
-      }
-    };
-    advance(L1, BI1, BJ1, ks1, L2, BI2, BJ2, ks2);
-    if (L < hi) issue(smem, BI, BJ, 0);
-    if (L1 < hi) {
-      issue(smem + GramX3WTile::kStage, BI1, BJ1, ks1);
-      GramX3WTile::template ring_barrier<GramX3WTile::kDmas>();
-    } else {
-      GramX3WTile::template ring_barrier<0>();
-    }
-    while (L < hi) {
-      const int s2 = stage >= 1 ? stage - 1 : 2;  // (stage + 2) % 3
-      if (kGramNpf && ks == 0) load_norms(BI, BJ);
-      if (L2 < hi) issue(smem + s2 * GramX3WTile::kStage, BI2, BJ2, ks2);
-      if (kZeroC && ks == 0)
-        tile.template compute<true>(smem + stage * GramX3WTile::kStage, wr, wc, (int)(row0 & 15));
-      else
-        tile.compute(smem + stage * GramX3WTile::kStage, wr, wc, (int)(row0 & 15));
-      if (L2 < hi)
-        GramX3WTile::template ring_barrier<GramX3WTile::kDmas>();
-      else
-        GramX3WTile::template ring_barrier<0>();
-      if (ks + 1 == nk) epilogue(L, BI, BJ, stage);
-      L = L1; BI = BI1; BJ = BJ1; ks = ks1;
-      L1 = L2; BI1 = BI2; BJ1 = BJ2; ks1 = ks2;
-      advance(L1, BI1, BJ1, ks1, L2, BI2, BJ2, ks2);
-      stage = stage == 2 ? 0 : stage + 1;
-    }
-  } else {
-    if (L < hi) issue(smem, BI, BJ, 0);
+    const bool more = Ln < hi;
+    if (more) issue(smem + (stage ^ 1) * GramX3WTile::kStage, BIn, BJn, ksn);
+    tile.compute(smem + stage * GramX3WTile::kStage, wr, wc, (int)(row0 & 15));
     GramX3WTile::template ring_barrier<0>();
-    int ks = 0, stage = 0;
-    int BIn = BI, BJn = BJ;
-    int64_t Ln = L;
-    while (L < hi) {
-      int ksn = ks + 1;
-      if (ksn == nk) {
-        Ln = next_valid(L + U, BIn, BJn);
-        ksn = 0;
-      }
-      const bool more = Ln < hi;
-      if (kGramNpf && ks == 0) load_norms(BI, BJ);
-      if (more) issue(smem + (stage ^ 1) * GramX3WTile::kStage, BIn, BJn, ksn);
-      if (kZeroC && ks == 0)
-        tile.template compute<true>(smem + stage * GramX3WTile::kStage, wr, wc, (int)(row0 & 15));
-      else
-        tile.compute(smem + stage * GramX3WTile::kStage, wr, wc, (int)(row0 & 15));
-      GramX3WTile::template ring_barrier<0>();
-      if (ks + 1 == nk) {
-        epilogue(L, BI, BJ, stage);
-        L = Ln;
-        BI = BIn;
-        BJ = BJn;
-      }
-      ks = ksn;
-      stage ^= 1;
+    if (ks + 1 == nk) {
+      epilogue(L, BI, BJ, stage);
+      L = Ln;
+      BI = BIn;
+      BJ = BJn;
     }
+    ks = ksn;
+    stage ^= 1;
   }
   if (smode == kSelHist) {
     __syncthreads();
@@ -692,70 +455,59 @@ int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, 
                      int layout, hipStream_t s, const float* tsc = nullptr) {
   const int64_t dp = roundup(d, 32), m_pad = roundup(m, 128), n_pad = roundup(n, 128);
   const int64_t img = gram_img_rows(n);
-  const int epi = kSqEpi;
   const bool sym = m == n && row0 == 0;
-  constexpr int KS = (F::P == 2 && kGramH2Form != 1) ? kGramKS : 1;
+  constexpr int KS = F::P == 2 ? kGramKS : 1;
   const int nk = (int)(dp / kX3Step / KS);  // ring stages per tile (dp is a multiple of 32)
   int rc = 0;
-  {
-    int bs = 0, bn = 0;
-    // FmtH2: 3-stage ring (DSVGD_GRAM_H2_FORM 1: half-tile blocks, two per CU);
-    // FmtX3: whole 256-tiles, 2-stage ring
-    constexpr int WN = (F::P == 3 || kGramH2Form != 1) ? 2 : 1;
-    constexpr int NS = (F::P == 2 && WN == 2 && KS == 1) ? 3 : 2;
-    // FmtH2: transposed accumulators (16-byte D stores, sqdist_x3w TR) except
-    // on launches that store mirror tiles (the full layout's triangle)
-    constexpr bool TRF = F::P == 2 && DSVGD_GRAM_TR;
-    if ((rc = persistent_blocks(
-             reinterpret_cast<const void*>(&sqdist_x3w_kernel<true, SM, F::P == 3, F, WN, NS, KS>), &bs,
-             256 * WN)))
-      return rc;
-    if ((rc = persistent_blocks(
-             reinterpret_cast<const void*>(&sqdist_x3w_kernel<false, SM, F::P == 3, F, WN, NS, KS, TRF, false>),
-             &bn, 256 * WN)))
-      return rc;
-    const int Tn2 = (int)((n_pad / 128 + 1) / 2), Tm2 = (int)((m_pad / 128 + 1) / 2);
-    struct Part {
-      bool sym;
-      int tm2, tc2, bj_off, r0t;
-      int64_t total;
-    } parts[3];
-    int np = 0;
-    if (sym) {
-      parts[np++] = {true, Tn2, Tn2, 0, 0, tile_grid(Tn2, Tn2, true)};
-    } else if (row0 % 256 == 0 && m % 256 == 0 && row0 + m <= n) {
-      // a row block holds the diagonal square [row0, row0 + m)^2 of the
-      // symmetric matrix: its upper triangle (+ mirror stores), and the
-      // rectangles left and right of it
-      const int c0 = (int)(row0 / 256), c1 = (int)((row0 + m) / 256), sq = (int)(m / 256);
-      if (c0 > 0) parts[np++] = {false, sq, c0, 0, 0, tile_grid(sq, c0, false)};
-      parts[np++] = {true, sq, sq, c0, (int)(row0 / 128), tile_grid(sq, sq, true)};
-      if (Tn2 > c1) parts[np++] = {false, sq, Tn2 - c1, c1, 0, tile_grid(sq, Tn2 - c1, false)};
-    } else {
-      parts[np++] = {false, Tm2, Tn2, 0, 0, tile_grid(Tm2, Tn2, false)};
-    }
-    int64_t ns_total = 0;
-    for (int i = 0; i < np; ++i) ns_total += parts[i].total * 8;
-    int64_t base = 0;
-    for (int i = 0; i < np; ++i) {
-      const Part& P = parts[i];
-      const int lay = sym ? layout : 0;
-#define DSVGD_X3W(SY, M, B, LAY, R0T, TR, MIR)                                                 \
-  hipLaunchKernelGGL((sqdist_x3w_kernel<SY, SM, M, F, WN, NS, KS, TR, MIR>), dim3((unsigned)B),  \
-                     dim3(256 * WN), 0, s, Yg, img, norms, row0, m, n, n_pad, nk, D, st, cand, epi, \
-                     P.total, LAY, P.tm2, P.tc2, P.bj_off, R0T, base, ns_total, tsc)
-      if (P.sym && lay == 0)  // mirror stores
-        DSVGD_X3W(true, F::P == 3, bs, lay, P.r0t, false, true);
-      else if (P.sym)
-        DSVGD_X3W(true, F::P == 3, bs, lay, P.r0t, TRF, false);
-      else
-        DSVGD_X3W(false, F::P == 3, bn, 0, 0, TRF, false);
-#undef DSVGD_X3W
-      if ((rc = check_launch("sqdist_x3w"))) return rc;
-      base += P.total * 8;
-    }
-    return 0;
+  int bs = 0, bn = 0;
+  if ((rc = persistent_blocks(
+           reinterpret_cast<const void*>(&sqdist_x3w_kernel<true, SM, F::P == 3, F, KS>), &bs, 512)))
+    return rc;
+  if ((rc = persistent_blocks(
+           reinterpret_cast<const void*>(&sqdist_x3w_kernel<false, SM, F::P == 3, F, KS, false>), &bn,
+           512)))
+    return rc;
+  const int Tn2 = (int)((n_pad / 128 + 1) / 2), Tm2 = (int)((m_pad / 128 + 1) / 2);
+  struct Part {
+    bool sym;
+    int tm2, tc2, bj_off, r0t;
+    int64_t total;
+  } parts[3];
+  int np = 0;
+  if (sym) {
+    parts[np++] = {true, Tn2, Tn2, 0, 0, tile_grid(Tn2, Tn2, true)};
+  } else if (row0 % 256 == 0 && m % 256 == 0 && row0 + m <= n) {
+    // a row block holds the diagonal square [row0, row0 + m)^2 of the
+    // symmetric matrix: its upper triangle (+ mirror stores), and the
+    // rectangles left and right of it
+    const int c0 = (int)(row0 / 256), c1 = (int)((row0 + m) / 256), sq = (int)(m / 256);
+    if (c0 > 0) parts[np++] = {false, sq, c0, 0, 0, tile_grid(sq, c0, false)};
+    parts[np++] = {true, sq, sq, c0, (int)(row0 / 128), tile_grid(sq, sq, true)};
+    if (Tn2 > c1) parts[np++] = {false, sq, Tn2 - c1, c1, 0, tile_grid(sq, Tn2 - c1, false)};
+  } else {
+    parts[np++] = {false, Tm2, Tn2, 0, 0, tile_grid(Tm2, Tn2, false)};
   }
+  int64_t ns_total = 0;
+  for (int i = 0; i < np; ++i) ns_total += parts[i].total * 8;
+  int64_t base = 0;
+  for (int i = 0; i < np; ++i) {
+    const Part& P = parts[i];
+    const int lay = sym ? layout : 0;
+#define DSVGD_X3W(SY, B, LAY, R0T, MIR)                                                          \
+  hipLaunchKernelGGL((sqdist_x3w_kernel<SY, SM, F::P == 3, F, KS, MIR>), dim3((unsigned)B),       \
+                     dim3(512), 0, s, Yg, img, norms, row0, m, n, n_pad, nk, D, st, cand, P.total, \
+                     LAY, P.tm2, P.tc2, P.bj_off, R0T, base, ns_total, tsc)
+    if (P.sym && lay == 0)  // mirror stores
+      DSVGD_X3W(true, bs, lay, P.r0t, true);
+    else if (P.sym)
+      DSVGD_X3W(true, bs, lay, P.r0t, false);
+    else
+      DSVGD_X3W(false, bn, 0, 0, false);
+#undef DSVGD_X3W
+    if ((rc = check_launch("sqdist_x3w"))) return rc;
+    base += P.total * 8;
+  }
+  return 0;
 }
 
 // d <= 2 (supports up to 64): D_ij = sum_c (y_ic - y_jc)^2 from explicit differences on the VALU
@@ -856,7 +608,6 @@ int launch_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0,
                        Y, ldy, row0, m, n, n_pad, (int)d, D, st, cand);
     return check_launch("sqdist_direct");
   }
-  const int epi = kSqEpi;
   const bool sym = m == n && row0 == 0;
   const int64_t T = n_pad / 128;
   const int64_t total = sym ? tile_grid(T, T, true) : tile_grid(m_pad / 128, T, false);
@@ -870,10 +621,10 @@ int launch_sqdist(const float* Y, int64_t ldy, const float* norms, int64_t row0,
     const dim3 grid((unsigned)blocks);
     if (sym)
       hipLaunchKernelGGL((sqdist_persistent_kernel<true, SM>), grid, dim3(256), 0, s, Y, ldy, norms,
-                         row0, m, n, n_pad, (int)dp, D, st, cand, epi, total);
+                         row0, m, n, n_pad, (int)dp, D, st, cand, total);
     else
       hipLaunchKernelGGL((sqdist_persistent_kernel<false, SM>), grid, dim3(256), 0, s, Y, ldy,
-                         norms, row0, m, n, n_pad, (int)dp, D, st, cand, epi, total);
+                         norms, row0, m, n, n_pad, (int)dp, D, st, cand, total);
     return check_launch("sqdist_persistent");
   }
 }

@@ -53,14 +53,9 @@ constexpr size_t kW2CtlBytes = 256;
 constexpr double kTheta = 8.0;
 constexpr int kRoundBatch = 16;
 constexpr int kBidBlocks = 1024;  // grid-stride bid kernel: 4096 waves
-#ifndef DSVGD_W2_CACHE
-#define DSVGD_W2_CACHE 1  // (A/B builds: 0 = every bid scans its whole cost row)
-#endif
-constexpr bool kW2Cache = DSVGD_W2_CACHE != 0;
-#ifndef DSVGD_W2_CTL_LAUNCH
-#define DSVGD_W2_CTL_LAUNCH 0  // (A/B: 1 = control step as a separate launch, no ticket)
-#endif
-constexpr bool kW2CtlLaunch = DSVGD_W2_CTL_LAUNCH != 0;
+// R = 2 .. kCacheMaxR bids go through the per-row price cache (measured
+// against full scans: same plans, 3-20x fewer cost-row reads)
+constexpr bool kW2Cache = true;
 
 // holder[j] = epoch tag << 21 | row holding column j (tag = epoch & 0x7ff,
 // never 0: stale entries of earlier phases and the zeroed workspace read as
@@ -479,7 +474,6 @@ __global__ __launch_bounds__(256) void w2_resolve_kernel(int64_t n, int64_t R, W
   for (int o = 32; o > 0; o >>= 1) gained += __shfl_xor(gained, o, 64);
   if ((threadIdx.x & 63) == 0 && gained)
     atomicAdd(&ctl->unassigned, (unsigned long long)(-(long long)gained));
-  if constexpr (kW2CtlLaunch) return;  // w2_control_kernel runs the control step
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -494,14 +488,6 @@ __global__ __launch_bounds__(256) void w2_resolve_kernel(int64_t n, int64_t R, W
       w2_control(ctl, n);
     }
   }
-}
-
-// the control step as its own one-thread launch (kW2CtlLaunch): after the
-// resolve kernel's boundary every block's updates are visible without the
-// per-block release fences of the ticket
-__global__ void w2_control_kernel(W2Ctl* ctl, int64_t n) {
-  if (ctl->done) return;
-  w2_control(ctl, n);
 }
 
 __global__ __launch_bounds__(256) void w2_emit_kernel(int64_t n, W2Ws w, int32_t* assign) {
@@ -614,7 +600,6 @@ int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
     for (int b = 0; b < kRoundBatch; ++b) {
       bid();
       hipLaunchKernelGGL(w2_resolve_kernel, gr, dim3(256), 0, s, n, R, w);
-      if (kW2CtlLaunch) hipLaunchKernelGGL(w2_control_kernel, dim3(1), dim3(1), 0, s, w.ctl, n);
     }
     W2Ctl* slot = hbuf + (batch & 1);
     if ((rc = check_launch("w2 auction round")) ||

@@ -274,7 +274,7 @@ def test_graph_replay_keeps_score_workspace():
     np.testing.assert_array_equal(runs[0], runs[1])
 
 
-def _nccl_worker(rank, port, mode, order, q):
+def _nccl_worker(rank, S, port, mode, order, q):
     import os
     import sys
     import torch.distributed as dist
@@ -286,13 +286,13 @@ def _nccl_worker(rank, port, mode, order, q):
     os.environ["MASTER_PORT"] = str(port)
     dev = torch.device("cuda", rank)
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=rank, world_size=2, device_id=dev)
+    dist.init_process_group("nccl", rank=rank, world_size=S, device_id=dev)
     x, t, init = _data(n=512)
-    per = x.shape[0] // 2
+    per = x.shape[0] // S
     tgt = m.targets.LogisticRegression(x[rank * per:(rank + 1) * per], t[rank * per:(rank + 1) * per])
     ep, es = {"partitions": (False, False), "all_particles": (True, False),
               "all_scores": (True, True)}[mode]
-    ds = m.DistSampler(rank, 2, tgt, m.RBF(1.0), torch.tensor(init, device=dev), per, x.shape[0],
+    ds = m.DistSampler(rank, S, tgt, m.RBF(1.0), torch.tensor(init, device=dev), per, x.shape[0],
                        exchange_particles=ep, exchange_scores=es, include_wasserstein=False,
                        order=order)
     traj = []
@@ -389,31 +389,35 @@ def test_rccl_world1_exchange_primitives():
         assert a == b and np.isfinite(a) and a > 0, out["median_h"]
 
 
-@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL path needs two GPUs")
+@pytest.mark.parametrize("S", [2, 4, 8])
 @pytest.mark.parametrize("mode", ["partitions", "all_particles", "all_scores"])
 @pytest.mark.parametrize("order", ["jacobi", "sequential"])
-def test_rccl_two_gpus_match_oracle(mode, order):
+def test_rccl_ranks_match_oracle(S, mode, order):
     """The device collectives (in-place all_gather_into_tensor, batch_isend_irecv
     ring shift, the all_scores all-reduce on a side stream beside the
-    histogram all-reduces) on two GPUs over RCCL, against DistOracle."""
+    histogram all-reduces) on S GPUs over RCCL, one process per GPU, against
+    DistOracle -- every S the box has GPUs for."""
+    if torch.cuda.device_count() < S:
+        pytest.skip("RCCL at S=%d needs %d GPUs" % (S, S))
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29600 + 2 * ["partitions", "all_particles", "all_scores"].index(mode) + (order == "jacobi")
-    ps = [ctx.Process(target=_nccl_worker, args=(r, port, mode, order, q)) for r in range(2)]
+    port = (29600 + 8 * [2, 4, 8].index(S) + 2 * ["partitions", "all_particles", "all_scores"].index(mode)
+            + (order == "jacobi"))
+    ps = [ctx.Process(target=_nccl_worker, args=(r, S, port, mode, order, q)) for r in range(S)]
     for p in ps:
         p.start()
-    res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda r: r[0])
+    res = sorted([q.get(timeout=300) for _ in range(S)], key=lambda r: r[0])
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
     x, t, init = _data(n=512)
-    per = x.shape[0] // 2
+    per = x.shape[0] // S
     fns = [lambda X, r=r: O.score_logreg(X, x[r * per:(r + 1) * per], t[r * per:(r + 1) * per])
-           for r in range(2)]
+           for r in range(S)]
     ep, es = {"partitions": (False, False), "all_particles": (True, False),
               "all_scores": (True, True)}[mode]
-    D = O.DistOracle([init, init], fns, per, x.shape[0], ep, es, sequential=order == "sequential")
+    D = O.DistOracle([init] * S, fns, per, x.shape[0], ep, es, sequential=order == "sequential")
     for step in range(3):
         D.step(0.05)
         for rank, traj in res:
