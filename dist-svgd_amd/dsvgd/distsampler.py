@@ -30,13 +30,16 @@ exactly as an assignment on the GPU (dsvgd.w2), and h * grad is added to every
 owned row's direction before the update.  previous particles = all n rows
 after the step when particles are exchanged, else the owned block (:202-205).
 
-Replicated data (all_particles with N_local == N_global, i.e. every rank
-holds the whole data set, the only reading under which the reference's
-N_global/N_local factor is 1): every rank's scores of a particle are the same
-numbers, so each rank scores only its owned block and the blocks are
-all-gathered (north_star's "all-gather of particles and scores"; SURVEY.md 5,
-8(e)) instead of every rank scoring all n particles (distsampler.py:94-99).
-`replicated=False` keeps the redundant per-rank scoring.
+Replicated data (all_particles, every rank holding the same data set): every
+rank's scores of a particle are the same numbers, so each rank scores only
+its owned block and the blocks are all-gathered (north_star's "all-gather of
+particles and scores") instead of every rank scoring all
+n particles (distsampler.py:94-99).  `replicated=None` (default) turns this
+on only where it is provably the reference's result: N_local == N_global and
+built-in targets whose data digests (`fingerprint()`) agree on every rank,
+checked once at the first step; a plain `logp` callable (which may close over
+rank-specific data, as logreg.py:68's `logp(rank, x)` can) keeps the
+redundant per-rank scoring.  `replicated=True` forces it, False disables it.
 
 Lagged modes (keyword `lagged`; the reference's notes.md:108-114, which
 describe them and time them at :134-135 but ship no code):
@@ -109,12 +112,16 @@ class DistSampler(object):
         self._include_wasserstein = include_wasserstein
         self._order = order
         self._group = group
-        if replicated is None:
-            replicated = N_local == N_global
-        # score all-gather: particles exchanged, scores not all-reduced, S > 1
-        self._replicated = bool(replicated and exchange_particles and not exchange_scores
-                                and num_shards > 1)
         self._target = resolve_target(logp)
+        # score all-gather: particles exchanged, scores not all-reduced, S > 1
+        eligible = exchange_particles and not exchange_scores and num_shards > 1
+        if not eligible or replicated is False:
+            self._replicated = False
+        elif replicated:
+            self._replicated = True
+        else:   # decided at the first step (needs the process group)
+            self._replicated = None if (N_local == N_global and
+                                        hasattr(self._target, "fingerprint")) else False
         self._rbf = resolve_kernel(kernel, self._d)
 
         # NOTE: drops particles if not divisible by num_shards (as the reference)
@@ -254,14 +261,26 @@ class DistSampler(object):
             self._w2 = W2Term(*key, device=self._device)
         return self._w2.grad(particles, previous_particles, h)
 
+    def _resolve_replicated(self):
+        """replicated=None: on iff every rank's target has the same data
+        digest (one all_gather_object of a short string, first step only)."""
+        import torch.distributed as dist
+        fps = [None] * self._num_shards
+        dist.all_gather_object(fps, self._target.fingerprint(), group=self._group)
+        self._replicated = all(f == fps[0] for f in fps)
+
     # ------------------------------------------------------------ step --
     def _engine(self, n_int, m, row0):
+        """One engine per (interacting set, owned rows, median kind); the
+        owned rows' offset row0 is set per step (lagged modes rotate it)."""
         local = self._lagged == "local"
-        key = (n_int, m, row0, local)
+        key = (n_int, m, local)
         if key not in self._engines:
-            self._engines = {key: PhiEngine(n_int, self._d, m=m, row0=row0, device=self._device,
-                                            local_median=local)}
+            self._engines.clear()      # the old D is freed before the new one is allocated
+            self._engines[key] = PhiEngine(n_int, self._d, m=m, row0=row0, device=self._device,
+                                           local_median=local)
         eng = self._engines[key]
+        eng.set_row0(row0)
         eng.timer = self.timer
         return eng
 
@@ -358,6 +377,8 @@ class DistSampler(object):
             h - discretization size for the JKO (W2) term
         """
         S = self._num_shards
+        if self._replicated is None:
+            self._resolve_replicated()
         if S > 1:
             if self._exchange_particles:
                 with span(self.timer, "allgather_x"):

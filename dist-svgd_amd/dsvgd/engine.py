@@ -236,6 +236,15 @@ class PhiEngine(object):
             self.cand_cap = max(1 << 22, (m * n) // 16)
             self.cand = torch.empty(self.cand_cap, **f32)
 
+    def set_row0(self, row0):
+        """Move the owned block to rows [row0, row0 + m) of the same
+        interacting set (no buffer depends on it; the symmetric layout is
+        only used for row0 == 0 == n - m)."""
+        assert 0 <= row0 and row0 + self.m <= self.n
+        if row0 != self.row0:
+            assert self.m < self.n, "the whole matrix has no other row block"
+            self.row0 = row0
+
     def _check_memory(self, dev):
         """D is materialised (m_pad x n_pad fp32, no recompute path), so one
         engine's footprint grows as m n: refuse up front, with the sizes, what
@@ -246,6 +255,8 @@ class PhiEngine(object):
         other = 4 * ((self.n_pad + 128) * self.ldy * 3 + splits * self.m * self.ldy)
         need = d_bytes + cand + other
         free, _ = torch.cuda.mem_get_info(dev)
+        # the caching allocator's reserved-but-unused blocks are free to torch too
+        free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
         if need > free:
             raise MemoryError(
                 "PhiEngine(n=%d, d=%d, m=%d) needs %.1f GiB of device memory (D is %d x %d "

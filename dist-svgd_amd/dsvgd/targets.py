@@ -52,6 +52,10 @@ class Gaussian(BuiltinTarget):
             self._dev[dev] = (self.mu.to(dev).contiguous(), self.lam.to(dev).contiguous())
         return self._dev[dev]
 
+    def fingerprint(self):
+        import hashlib
+        return hashlib.sha1(b"gauss" + self.mu.numpy().tobytes() + self.lam.numpy().tobytes()).hexdigest()
+
     def score(self, X, out, scale=1.0):
         n, d = X.shape
         assert d == self.mu.numel(), "Gaussian target has d=%d" % self.mu.numel()
@@ -68,6 +72,9 @@ class GaussianMixture1D(BuiltinTarget):
         a = -0.5 * (x + 2.0) ** 2
         b = -0.5 * (x - 2.0) ** 2
         return (torch.logaddexp(a, b) + math.log(1.0 / 3.0) - 0.5 * math.log(2 * math.pi)).sum()
+
+    def fingerprint(self):
+        return "gmm1d"
 
     def score(self, X, out, scale=1.0):
         n, d = X.shape
@@ -93,8 +100,9 @@ class LogisticRegression(BuiltinTarget):
             raise ValueError("gemm must be one of %s" % sorted(self.ENGINES))
         self.gemm = gemm
         self._dev = {}
-        self._ws = {}
+        self._ws = {}             # workspace key -> buffer, least recently used first
         self._prepared = {}       # workspace key -> engine whose data image it holds
+        self._pinned = set()      # keys a captured HIP graph holds (never evicted)
 
     @property
     def N(self):
@@ -118,21 +126,43 @@ class LogisticRegression(BuiltinTarget):
             self._dev[dev] = (self.x.to(dev).contiguous(), self.t.to(dev).contiguous())
         return self._dev[dev]
 
+    def fingerprint(self):
+        """Digest of the data (DistSampler: ranks whose targets agree on it
+        hold the same data, so their scores of a particle are the same)."""
+        import hashlib
+        h = hashlib.sha1(b"logreg")
+        h.update(self.x.contiguous().numpy().tobytes())
+        h.update(self.t.contiguous().numpy().tobytes())
+        return h.hexdigest()
+
+    MAX_WORKSPACES = 4   # unpinned score workspaces kept (least recently used evicted)
+
+    def _workspace(self, key, n, d, dev):
+        ws = self._ws.pop(key, None)
+        if ws is None:
+            nbytes = N.load().dsvgd_logreg_workspace_bytes(n, self.N, d - 1) if key[1] else 256
+            ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device=dev)
+        self._ws[key] = ws                     # most recently used last
+        if torch.cuda.is_current_stream_capturing():
+            self._pinned.add(key)              # a graph now holds its address
+        free = [k for k in self._ws if k not in self._pinned and k != key]
+        for k in free[:max(0, len(free) + 1 - self.MAX_WORKSPACES)]:
+            del self._ws[k]
+            self._prepared.pop(k, None)
+        return ws
+
     def score(self, X, out, scale=1.0):
         n, d = X.shape
         assert d == self.x.shape[1] + 1, "logreg target has d = 1 + p = %d" % (self.x.shape[1] + 1)
         xd, t = self._params(X.device)
-        # one workspace per (device, n), kept for the target's lifetime: a
-        # captured HIP graph (engine.StepGraph) holds its address, so it is
-        # never freed behind one (release() frees them explicitly).  The
-        # few-particle path (the Gauss-Seidel refreshes) needs none.
+        # one workspace per (device, n): the ones a captured HIP graph
+        # (engine.StepGraph) holds are pinned and never freed behind it
+        # (release() frees them explicitly); of the others the
+        # MAX_WORKSPACES most recently used stay.  The few-particle path
+        # (the Gauss-Seidel refreshes) needs none.
         small = n <= self.SMALL_ROWS and (d - 1 <= 32 or self.N <= 8192)   # logreg.hip's test
         key = (X.device, 0 if small else n)
-        ws = self._ws.get(key)
-        if ws is None:
-            nbytes = N.load().dsvgd_logreg_workspace_bytes(n, self.N, d - 1) if key[1] else 256
-            ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device=X.device)
-            self._ws[key] = ws
+        ws = self._workspace(key, n, d, X.device)
         base = ws.data_ptr()
         aligned = (base + 255) // 256 * 256
         eng = self.ENGINES[self.gemm]
@@ -157,6 +187,7 @@ class LogisticRegression(BuiltinTarget):
         """Free the score workspaces (no graph that captured them may replay after)."""
         self._ws.clear()
         self._prepared.clear()
+        self._pinned.clear()
 
 
 class CallableTarget(Target):

@@ -7,9 +7,16 @@
      row0 = 32768), and logreg scores at n = 8192, N = 8192, p = 1023
 
 At these sizes the oracle checks 256 sampled rows of phi in fp64 (north_star:
-1e-5 max-normalised per step), and the median through a size-independent
-property: counting the kernel's own D, below <= k < at_or_below with k =
-(n^2 - 1) // 2 (SURVEY.md a18), then h == median / log n.
+1e-5 max-normalised per step), and the median two ways: counting the
+kernel's own D, below <= k < at_or_below with k = (n^2 - 1) // 2 (SURVEY.md
+a18), then h == median / log n; and independently of every product kernel,
+against fp64 distances of all n^2 pairs (torch float64 on the device, row
+chunks): fewer than k + 1 of them lie below median (1 - 1e-5), more than k
+at or below median (1 + 1e-5).
+
+D sharded: the bench's step at S = 2 (two gloo ranks sharing cuda:0, each
+owning n / 2 rows, N / 2 data rows, all_scores all-reduce, row-sharded
+median through the histogram all-reduce), 256 sampled rows per rank.
 """
 import math
 
@@ -48,6 +55,28 @@ def check_median_by_counting(eng, n):
     assert below <= k < at_or_below, (below, k, at_or_below)
     assert h == pytest.approx(med / math.log(n), rel=1e-6)
     return med, h
+
+
+def check_median_fp64(X, med, rel=1e-5, chunk=4096):
+    """k = (n^2 - 1) // 2 lies in [#(D64 < med (1 - rel)), #(D64 <= med (1 + rel)))
+    over the fp64 distances of all n^2 pairs (diagonal included)."""
+    n = X.shape[0]
+    k = (n * n - 1) // 2
+    Xd = torch.as_tensor(np.asarray(X, np.float64), device=DEV)
+    Xd = Xd - Xd.mean(0)
+    nr = (Xd * Xd).sum(1)
+    lo_t, hi_t = med * (1.0 - rel), med * (1.0 + rel)
+    below = at_or_below = 0
+    for i in range(0, n, chunk):
+        D = (nr[i:i + chunk, None] + nr[None, :]) - 2.0 * (Xd[i:i + chunk] @ Xd.t())
+        D.clamp_(min=0.0)
+        idx = torch.arange(i, min(n, i + chunk), device=DEV)
+        D[idx - i, idx] = 0.0
+        below += int((D < lo_t).sum())
+        at_or_below += int((D <= hi_t).sum())
+        del D
+    assert below <= k < at_or_below, (below, k, at_or_below)
+    return below, at_or_below
 
 
 def check_step(ds, eng, X0, S_ref, eps, rows):
@@ -103,12 +132,92 @@ def test_config_D_bench_step():
     torch.cuda.synchronize()
     eng = next(iter(ds._engines.values()))
     assert eng.sym and eng.bracketed
-    check_median_by_counting(eng, n)
+    med, _ = check_median_by_counting(eng, n)
+    check_median_fp64(X0, med)
     S_ref = O.score_logreg(X0, x, t)
     rows = np.sort(np.random.RandomState(5).choice(n, 256, replace=False))
     S_gpu = ds._scores[torch.as_tensor(rows, device=DEV)].cpu().numpy()
     assert rel_err(S_gpu, S_ref[rows]) < PHI_TOL
     check_step(ds, eng, X0, S_ref, eps, rows)
+
+
+def _shard_worker(rank, S, port, q):
+    import os
+    import sys
+    import torch.distributed as dist
+    from conftest import PKG, ROOT
+    for p in (ROOT, PKG):
+        sys.path.insert(0, p)
+    import dsvgd as m
+    from bench import synthetic_data
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=S)
+    n, d, Ng, eps = 65536, 256, 16384, 1e-4
+    per = Ng // S
+    x, t = synthetic_data(Ng, d - 1)
+    gen = torch.Generator(device="cpu").manual_seed(0)
+    parts = (0.1 * torch.randn(n, d, generator=gen)).to(DEV)
+    tgt = m.targets.LogisticRegression(x[rank * per:(rank + 1) * per], t[rank * per:(rank + 1) * per])
+    ds = m.DistSampler(rank, S, tgt, m.RBF("median"), parts, per, per * S, exchange_particles=True,
+                       exchange_scores=True, include_wasserstein=False, order="jacobi")
+    ds.keep_phi = True
+    ds.make_step(eps)
+    torch.cuda.synchronize()
+    eng = next(iter(ds._engines.values()))
+    rows = np.sort(np.random.RandomState(20 + rank).choice(n // S, 256, replace=False))
+    ridx = torch.as_tensor(rows, device=DEV)
+    s0 = ds._particle_start_idx
+    out = {"rows": s0 + rows, "own_rows": rows, "h": eng.state.read()[1],
+           "median": eng.state.read()[0], "bracketed": eng.bracketed, "sym": eng.sym,
+           "scores": ds._scores[torch.as_tensor(s0 + rows, device=DEV)].cpu().numpy(),
+           "phi": eng.phi[ridx].cpu().numpy(), "X1": ds.particles[ridx].cpu().numpy()}
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_config_D_sharded_two_ranks():
+    """config 4 (dist-logreg) sharded at full size, S = 2
+    ranks sharing cuda:0 over gloo: each owns 32768 of n = 65536 particles
+    (full-layout row block, phi_w1, split-K) and N / 2 data rows; the scores
+    are the all-reduced sum of both ranks' local-data scores (prior counted
+    twice, distsampler.py:160-170); the bandwidth is the median of the whole
+    n x n matrix through the histogram all-reduce.  Per rank 256 sampled rows
+    of scores, phi and the update vs fp64; the median vs fp64 distances."""
+    from bench import synthetic_data
+    import torch.multiprocessing as mp
+    S, n, d, Ng, eps = 2, 65536, 256, 16384, 1e-4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_shard_worker, args=(r, S, 29980, q)) for r in range(S)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in range(S)], key=lambda r: r[0])
+    for p in ps:
+        p.join(120)
+        assert p.exitcode == 0
+    x, t = synthetic_data(Ng, d - 1)
+    gen = torch.Generator(device="cpu").manual_seed(0)
+    X0 = (0.1 * torch.randn(n, d, generator=gen)).numpy().astype(np.float64)
+    per = Ng // S
+    S_ref = sum(O.score_logreg(X0, x[r * per:(r + 1) * per], t[r * per:(r + 1) * per])
+                for r in range(S))
+    h = res[0][1]["h"]
+    assert all(o["h"] == h and o["median"] == res[0][1]["median"] for _, o in res)
+    assert all(o["bracketed"] and not o["sym"] for _, o in res)
+    med = res[0][1]["median"]
+    check_median_fp64(X0, med)
+    assert h == pytest.approx(med / math.log(n), rel=1e-6)
+    for rank, o in res:
+        rows = o["rows"]
+        assert rows.min() >= rank * (n // S) and rows.max() < (rank + 1) * (n // S)
+        assert rel_err(o["scores"], S_ref[rows]) < PHI_TOL
+        ref = O.phi(X0, S_ref, h, rows=rows)
+        assert rel_err(o["phi"], ref) < PHI_TOL
+        X1 = o["X1"].astype(np.float64)
+        assert np.abs(X1 - (X0[rows] + eps * ref)).max() <= \
+            eps * PHI_TOL * np.abs(ref).max() + 2 * np.spacing(np.abs(X1).astype(np.float32)).max()
 
 
 def test_config_E_rank_share_phi():

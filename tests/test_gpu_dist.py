@@ -100,6 +100,98 @@ def test_replicated_scores_allgather(S, order):
             assert err < TRAJ_TOL, err
 
 
+def _auto_worker(rank, S, port, q):
+    import os
+    import sys
+    import torch.distributed as dist
+    from conftest import PKG, ROOT
+    for p in (ROOT, PKG):
+        sys.path.insert(0, p)
+    import dsvgd as m
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=S)
+    x, t, init = _data(n=256)
+    xr, tr, _ = _data(seed=40 + rank, n=256)          # rank-specific data, same N
+    out = {}
+    for case, tgt in (("same", m.targets.LogisticRegression(x, t)),
+                      ("differ", m.targets.LogisticRegression(xr, tr))):
+        ds = m.DistSampler(rank, S, tgt, m.RBF(1.0), torch.tensor(init, device=DEV), x.shape[0],
+                           x.shape[0], exchange_particles=True, exchange_scores=False,
+                           include_wasserstein=False, order="jacobi")
+        assert ds._replicated is None            # decided at the first step
+        traj = []
+        for _ in range(2):
+            ds.make_step(0.05)
+            traj.append(ds.particles.cpu().numpy())
+        out[case] = (ds._replicated, traj)
+    lp = m.targets.LogisticRegression(xr, tr).logp   # a plain callable: never assumed replicated
+    ds = m.DistSampler(rank, S, lp, m.RBF(1.0), torch.tensor(init, device=DEV), x.shape[0],
+                       x.shape[0], exchange_particles=True, exchange_scores=False,
+                       include_wasserstein=False, order="jacobi")
+    out["callable"] = ds._replicated
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_replicated_default_needs_identical_data():
+    """replicated=None (default) all-gathers owned-block scores
+    only when every rank's built-in target digests the same data; ranks with
+    rank-specific data of the same size (N_local == N_global) keep scoring
+    every particle with their own logp, as the reference does -- both
+    against the oracle; a plain callable is never assumed replicated."""
+    S = 2
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_auto_worker, args=(r, S, 29940, q)) for r in range(S)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(S)], key=lambda r: r[0])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    x, t, init = _data(n=256)
+    same = lambda X: O.score_logreg(X, x, t)  # noqa: E731
+    own = [(lambda X, r=r: O.score_logreg(X, *_data(seed=40 + r, n=256)[:2])) for r in range(S)]
+    for case, fns, rep in (("same", [same] * S, True), ("differ", own, False)):
+        D = O.DistOracle([init] * S, fns, x.shape[0], x.shape[0], True, False, sequential=False,
+                         replicated=rep)
+        for step in range(2):
+            D.step(0.05)
+            for rank, out in res:
+                flag, traj = out[case]
+                assert flag is rep, (case, flag)
+                err = float(np.abs(traj[step] - D.own(rank)).max())
+                record_parity(err)
+                assert err < TRAJ_TOL, (case, step, rank, err)
+    for rank, out in res:
+        assert out["callable"] is False
+
+
+def test_logreg_workspaces_bounded():
+    """scoring many particle counts keeps at most MAX_WORKSPACES
+    unpinned workspaces (least recently used evicted) and the scores stay
+    right after an eviction."""
+    m = dsvgd()
+    x, t, _ = _data()
+    tgt = m.targets.LogisticRegression(x, t)
+    ref = {}
+    for n2 in (40, 48, 64, 96, 128, 192, 40):
+        X2 = torch.tensor(0.1 * np.random.RandomState(n2).randn(n2, x.shape[1] + 1),
+                          dtype=torch.float32, device=DEV)
+        S2 = torch.empty_like(X2)
+        tgt.score(X2, S2)
+        assert len(tgt._ws) <= tgt.MAX_WORKSPACES
+        got = S2.cpu().numpy()
+        want = O.score_logreg(X2.cpu().numpy().astype(np.float64), x, t)
+        assert np.abs(got - want).max() <= 1e-5 * np.abs(want).max()
+        if n2 in ref:
+            np.testing.assert_array_equal(got, ref[n2])
+        ref[n2] = got
+
+
 @pytest.mark.parametrize("where", ["cuda", "cpu"])
 def test_particles_setter(where):
     """distsampler.py:58-62: the setter asserts the shape and writes the owned
