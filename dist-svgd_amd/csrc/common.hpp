@@ -45,6 +45,20 @@ __device__ __forceinline__ uint32_t abs_bits(float v) {
   return __float_as_uint(v) & 0x7fffffffu;
 }
 
+// FmtH2 power-of-two scale of an operand whose largest magnitude is m: s m
+// in [2^14, 2^15); 1 for an all-zero or non-finite operand (NaN / inf
+// propagate).  s is in [2^-113, 2^100], so pow2_inv is exact.
+__device__ __forceinline__ float pow2_scale(float m) {
+  if (!(m > 0.f) || !isfinite(m)) return 1.f;
+  int e;
+  frexpf(m, &e);                        // m in [2^(e-1), 2^e)
+  return ldexpf(1.f, min(15 - e, 100));  // s m in [2^14, 2^15)
+}
+// 1 / s for a normal power of two s (exact; no rcp rounding)
+__device__ __forceinline__ float pow2_inv(float s) {
+  return __uint_as_float(0x7F000000u - __float_as_uint(s));
+}
+
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -48,15 +48,6 @@ __global__ __launch_bounds__(256) void colmax_partial_kernel(const float* __rest
             max(red[2][threadIdx.x], red[3][threadIdx.x]));
 }
 
-// power-of-two scale of a column whose largest magnitude is m: s m in
-// [2^14, 2^15); 1 for an all-zero or non-finite column (NaN / inf propagate)
-__device__ __forceinline__ float pow2_scale(float m) {
-  if (!(m > 0.f) || !isfinite(m)) return 1.f;
-  int e;
-  frexpf(m, &e);                        // m in [2^(e-1), 2^e)
-  return ldexpf(1.f, min(15 - e, 100));  // s m in [2^14, 2^15)
-}
-
 // one block: out[c] = s_c, out[cols + c] = 1 / s_c; out[2 cols] = t = the
 // smallest s_c over the nonzero finite columns (1 if any column is not
 // finite, or none is nonzero), out[2 cols + 1] = 1 / t
@@ -99,22 +90,29 @@ __global__ __launch_bounds__(256) void colscale_final_kernel(const uint32_t* __r
     const float t = (bad[0] || !isfinite(red[0])) ? 1.f : red[0];
     out[2 * cols] = t;
     out[2 * cols + 1] = 1.f / t;
+    out[2 * cols + 2] = 0.f;  // no range guard on this path (no row maxima)
   }
 }
 
 // the scales of dsvgd_h2_colscale's layout from pack_h2's maxima, over the
-// first `cols` columns (cols == dp: the X half, the Gram's row image; cols ==
-// ldy: all of Y, phi_mm's B image).  16 columns x 16 row groups per block;
-// t = pow2_scale(the largest magnitude over those columns) -- the smallest
+// first `cols` columns (cols == dp: the X half; cols == ldy: all of Y,
+// phi_mm's B image).  16 columns x 16 row groups per block; t =
+// pow2_scale(the largest magnitude over those columns) -- the smallest
 // nonzero column scale, since pow2_scale is monotone, and 1 when it is 0 or
-// not finite -- from gmax, by every block's lane group 0 (block 0 writes it).
+// not finite -- from gmax, by every block's lane group 0 (block 0 writes it),
+// and the RANGE GUARD out[2 cols + 2]: 1 when a half of Y in those columns
+// has its largest magnitude more than kH2Range times its smallest nonzero
+// row max (some particle's row then sits below FmtH2's 2^-16 window of its
+// column's scale), else 0.
 constexpr int kScaleCols = 16;
+constexpr float kH2Range = 65536.f;  // 2^16
 
 __global__ __launch_bounds__(256) void scales_h2_kernel(const uint32_t* __restrict__ partial,
                                                         const uint32_t* __restrict__ gmax,
                                                         int64_t nb, int64_t ldp, int64_t cols,
                                                         int64_t dp, float* __restrict__ out) {
   __shared__ uint32_t red[16][kScaleCols];
+  __shared__ uint32_t gred[4][4];
   const int cl = threadIdx.x & (kScaleCols - 1), rg = threadIdx.x / kScaleCols;
   const int64_t c = (int64_t)blockIdx.x * kScaleCols + cl;
   uint32_t m0 = 0u, m1 = 0u, m2 = 0u, m3 = 0u;
@@ -139,22 +137,64 @@ __global__ __launch_bounds__(256) void scales_h2_kernel(const uint32_t* __restri
     out[cols + c] = 1.f / s;
   }
   if (blockIdx.x == 0) {
-    __syncthreads();
-    // gmax[2b] covers [0, dp), gmax[2b + 1] the rest of the row
-    uint32_t g = 0u;
+    // gmax[4b + h]: largest |entry| of half h; gmax[4b + 2 + h]: smallest
+    // nonzero row max of half h (h = 0: [0, dp), h = 1: the rest of the row)
+    uint32_t gx = 0u, gs = 0u, rx = 0x7F800000u, rs = 0x7F800000u;
     for (int64_t b = threadIdx.x; b < nb; b += 256) {
-      g = max(g, gmax[2 * b]);
-      if (cols > dp) g = max(g, gmax[2 * b + 1]);
+      gx = max(gx, gmax[4 * b]);
+      gs = max(gs, gmax[4 * b + 1]);
+      rx = min(rx, gmax[4 * b + 2]);
+      rs = min(rs, gmax[4 * b + 3]);
     }
-    for (int o = 32; o > 0; o >>= 1) g = max(g, (uint32_t)__shfl_xor((int)g, o));
-    if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = g;
+    for (int o = 32; o > 0; o >>= 1) {
+      gx = max(gx, (uint32_t)__shfl_xor((int)gx, o));
+      gs = max(gs, (uint32_t)__shfl_xor((int)gs, o));
+      rx = min(rx, (uint32_t)__shfl_xor((int)rx, o));
+      rs = min(rs, (uint32_t)__shfl_xor((int)rs, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+      gred[threadIdx.x >> 6][0] = gx;
+      gred[threadIdx.x >> 6][1] = gs;
+      gred[threadIdx.x >> 6][2] = rx;
+      gred[threadIdx.x >> 6][3] = rs;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-      const float t =
-          pow2_scale(__uint_as_float(max(max(red[0][0], red[0][1]), max(red[0][2], red[0][3]))));
+      uint32_t g[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h)
+        g[h] = h < 2 ? max(max(gred[0][h], gred[1][h]), max(gred[2][h], gred[3][h]))
+                     : min(min(gred[0][h], gred[1][h]), min(gred[2][h], gred[3][h]));
+      const bool both = cols > dp;
+      const float t = pow2_scale(__uint_as_float(both ? max(g[0], g[1]) : g[0]));
       out[2 * cols] = t;
       out[2 * cols + 1] = 1.f / t;
+      const bool gx_wide = __uint_as_float(g[0]) > kH2Range * __uint_as_float(g[2]);
+      const bool gs_wide = __uint_as_float(g[1]) > kH2Range * __uint_as_float(g[3]);
+      out[2 * cols + 2] = (gx_wide || (both && gs_wide)) ? 1.f : 0.f;
     }
+  }
+}
+
+// rscale[i] = pow2_scale(max_c |A[i][c]|) and rinv[i] = 1 / rscale[i] for
+// rows i < rows (1 for a zero / non-finite row; rows_pad > rows: 1): the
+// per-row scales of an NT row image (the Gram's, logreg's W) -- one wave per row.
+__global__ __launch_bounds__(256) void rowscale_h2_kernel(const float* __restrict__ A,
+                                                          int64_t lda, int64_t rows, int64_t cols,
+                                                          int64_t rows_pad,
+                                                          float* __restrict__ rscale,
+                                                          float* __restrict__ rinv) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= rows_pad) return;
+  uint32_t m = 0u;
+  if (i < rows)
+    for (int64_t c = lane; c < cols; c += 64) m = max(m, abs_bits(A[i * lda + c]));
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+  if (lane == 0) {
+    const float s = pow2_scale(__uint_as_float(m));
+    rscale[i] = s;
+    if (rinv) rinv[i] = pow2_inv(s);
   }
 }
 
@@ -193,7 +233,8 @@ __global__ __launch_bounds__(256) void ysplit_h2_kernel(const float* __restrict_
 // load's 16-byte chunk holds an element of the row, so it stays inside
 // mapped memory) -- scalar loads would touch 64 rows' lines per
 // wave-instruction, 16 times over.  OFF < 0: element loads (any layout).
-template <int OFF>
+// RS: tscale is per ROW (tscale[i], rows < rows_pad), else one tensor scale.
+template <int OFF, bool RS = false>
 __global__ __launch_bounds__(256) void rowsplit_h2_kernel(const float* __restrict__ A,
                                                           int64_t lda, int64_t rows, int64_t cols,
                                                           int64_t rows_pad, int64_t ksteps,
@@ -202,7 +243,7 @@ __global__ __launch_bounds__(256) void rowsplit_h2_kernel(const float* __restric
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= ksteps * rows_pad) return;
   const int64_t kb = t / rows_pad, i = t % rows_pad;
-  const float sc = *tscale;
+  const float sc = RS ? (i < rows ? tscale[i] : 1.f) : *tscale;
   float a[16];
   if (OFF >= 0 && i < rows && kb * 16 + 16 <= cols) {
     constexpr int kOff = OFF < 0 ? 0 : OFF;
@@ -265,14 +306,15 @@ int h2_ysplit(const float* Y, int64_t ldy, int64_t rows, const float* colscale, 
   return check_launch("ysplit_h2");
 }
 
-int h2_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
-                int64_t kpad, const float* tscale, void* img, hipStream_t s) {
+template <bool RS>
+static int h2_rowsplit_t(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                         int64_t kpad, const float* tscale, void* img, hipStream_t s) {
   const int64_t ksteps = kpad / kX3Step, threads = ksteps * rows_pad;
   const dim3 grid((unsigned)((threads + 255) / 256));
   const int off = ((uintptr_t)A & 3) == 0 && lda % 4 == 0 ? (int)(((uintptr_t)A >> 2) & 3) : -1;
-#define DSVGD_ROWSPLIT_H2(O)                                                                 \
-  hipLaunchKernelGGL(rowsplit_h2_kernel<O>, grid, dim3(256), 0, s, A, lda, rows, cols, rows_pad, \
-                     ksteps, tscale, (_Float16*)img)
+#define DSVGD_ROWSPLIT_H2(O)                                                                  \
+  hipLaunchKernelGGL((rowsplit_h2_kernel<O, RS>), grid, dim3(256), 0, s, A, lda, rows, cols,   \
+                     rows_pad, ksteps, tscale, (_Float16*)img)
   switch (off) {
     case 0: DSVGD_ROWSPLIT_H2(0); break;
     case 1: DSVGD_ROWSPLIT_H2(1); break;
@@ -282,6 +324,23 @@ int h2_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t
   }
 #undef DSVGD_ROWSPLIT_H2
   return check_launch("rowsplit_h2");
+}
+
+int h2_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                int64_t kpad, const float* tscale, void* img, hipStream_t s) {
+  return h2_rowsplit_t<false>(A, lda, rows, cols, rows_pad, kpad, tscale, img, s);
+}
+
+int h2_rowsplit_rows(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                     int64_t kpad, const float* rscale, void* img, hipStream_t s) {
+  return h2_rowsplit_t<true>(A, lda, rows, cols, rows_pad, kpad, rscale, img, s);
+}
+
+int h2_rowscale(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                float* rscale, float* rinv, hipStream_t s) {
+  hipLaunchKernelGGL(rowscale_h2_kernel, dim3((unsigned)((rows_pad + 3) / 4)), dim3(256), 0, s, A,
+                     lda, rows, cols, rows_pad, rscale, rinv);
+  return check_launch("rowscale_h2");
 }
 
 }  // namespace dsvgd
@@ -332,6 +391,24 @@ int dsvgd_h2_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, i
                 "rows_pad and kpad must be positive multiples of 16");
   DSVGD_REQUIRE(((uintptr_t)img & 15) == 0, "16-byte alignment");
   return h2_rowsplit(A, lda, rows, cols, rows_pad, kpad, tscale, img, (hipStream_t)stream);
+}
+
+int dsvgd_h2_rowsplit_rows(const float* A, int64_t lda, int64_t rows, int64_t cols,
+                           int64_t rows_pad, int64_t kpad, const float* rscale, void* img,
+                           void* stream) {
+  DSVGD_REQUIRE(A && rscale && img, "null pointer");
+  DSVGD_REQUIRE(rows >= 0 && cols >= 0 && rows <= rows_pad && lda >= cols, "sizes");
+  DSVGD_REQUIRE(rows_pad > 0 && rows_pad % 16 == 0 && kpad > 0 && kpad % kX3Step == 0,
+                "rows_pad and kpad must be positive multiples of 16");
+  DSVGD_REQUIRE(((uintptr_t)img & 15) == 0, "16-byte alignment");
+  return h2_rowsplit_rows(A, lda, rows, cols, rows_pad, kpad, rscale, img, (hipStream_t)stream);
+}
+
+int dsvgd_h2_rowscale(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                      float* rscale, float* rinv, void* stream) {
+  DSVGD_REQUIRE(A && rscale, "null pointer");
+  DSVGD_REQUIRE(rows >= 0 && cols > 0 && rows <= rows_pad && lda >= cols, "sizes");
+  return h2_rowscale(A, lda, rows, cols, rows_pad, rscale, rinv, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -23,16 +23,20 @@ int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, i
             int64_t m, int64_t row0, hipStream_t s);
 int nn_x3_gemm(bool exp_, const float* A, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
                const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-               int64_t row0, hipStream_t s, int sym = 0, int m16 = 0);
+               int64_t row0, hipStream_t s, int sym, int m16, const float* gate);
 int nn_h2_gemm(bool exp_, const float* A, int64_t K, const _Float16* Yh, int64_t ldy, int splits,
                const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-               int64_t row0, hipStream_t s, int sym, const float* colinv);
+               int64_t row0, hipStream_t s, int sym, const float* colinv, const float* gate);
 int h2_colscale(const float* A, int64_t lda, int64_t rows, int64_t cols, float* ws, float* out,
                 hipStream_t s);
 int h2_ysplit(const float* Y, int64_t ldy, int64_t rows, const float* colscale, void* Yh,
               hipStream_t s);
 int h2_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
                 int64_t kpad, const float* tscale, void* img, hipStream_t s);
+int h2_rowsplit_rows(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                     int64_t kpad, const float* rscale, void* img, hipStream_t s);
+int h2_rowscale(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                float* rscale, float* rinv, hipStream_t s);
 size_t h2_colscale_ws_floats(int64_t rows, int64_t cols);
 
 static int64_t nn_cols(int64_t w) {
@@ -43,8 +47,8 @@ static int64_t nn_cols(int64_t w) {
 
 struct LogregWs {
   int64_t N, n_pad, N_pad, pp, ldb;
-  size_t off_w, off_xd, off_t, off_g, off_gw, off_wx, off_xdx, off_xdy, off_sw, off_sxd, off_sws,
-      off_zs, total;
+  size_t off_w, off_xd, off_t, off_g, off_gw, off_wx, off_xdx, off_xdy, off_rsw, off_riw, off_sxd,
+      off_sws, total;
 };
 
 // G . Xd (K = N data rows, 256-row blocks): split K so that a launch has
@@ -79,11 +83,12 @@ static LogregWs logreg_ws(int64_t n, int64_t N, int64_t p) {
   w.off_wx = take((size_t)w.n_pad * w.pp * 3 / 2);
   w.off_xdx = take((size_t)w.N_pad * w.pp * 3 / 2);
   w.off_xdy = take((size_t)w.N_pad * w.ldb * 3 / 2);
-  // FmtH2 scales (dsvgd_h2_colscale layout) of W = X[:, 1:] and of Xd, + scratch
-  w.off_sw = take((size_t)(2 * w.pp + 2));
-  w.off_sxd = take((size_t)(2 * w.ldb + 2));
-  w.off_sws = take(std::max(h2_colscale_ws_floats(n, w.pp), h2_colscale_ws_floats(w.N_pad, w.ldb)));
-  w.off_zs = take(2);
+  // FmtH2 scales: per-row of W = X[:, 1:] (scale, inverse), of Xd
+  // (dsvgd_h2_colscale layout), + scratch
+  w.off_rsw = take((size_t)w.n_pad);
+  w.off_riw = take((size_t)w.n_pad);
+  w.off_sxd = take((size_t)(2 * w.ldb + 3));
+  w.off_sws = take(h2_colscale_ws_floats(w.N_pad, w.ldb));
   w.total = o;
   return w;
 }
@@ -119,11 +124,13 @@ struct IsM16 : std::false_type {};
 template <class T>
 struct IsM16<T, std::void_t<decltype(T::M16_)>> : std::integral_constant<bool, T::M16_> {};
 
-// zs: 1 / (the product of the operands' FmtH2 tensor scales), 1 otherwise
+// zs: 1 / (Xd's FmtH2 tensor scale), 1 otherwise; rinv (FmtH2): 1 / (W row
+// i's scale) per row i -- z_iq = rinv_i zs acc_iq, both exact powers of two
 template <class T>
 __device__ __forceinline__ void z_epilogue(T& tile, int64_t i0, int64_t q0,
                                            const float* __restrict__ tp, int64_t N_pad,
-                                           float* __restrict__ G, float zs = 1.f) {
+                                           float* __restrict__ G, float zs = 1.f,
+                                           const float* __restrict__ rinv = nullptr) {
   if constexpr (IsM16<T>::value) {  // 16x16 tiles: column lane & 15, rows 4 (lane >> 4) + reg
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w / T::WN_, wn = w % T::WN_;
 #pragma unroll
@@ -148,6 +155,14 @@ __device__ __forceinline__ void z_epilogue(T& tile, int64_t i0, int64_t q0,
   constexpr int WR = 32 * T::TM_, WC = 32 * T::TN_;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w / T::WN_, wn = w % T::WN_;
   const int h4 = 4 * (lane >> 5);
+  // the 16 rows of each mi this lane holds: i + (r & 3) + 8 (r >> 2)
+  f32x4 ri[T::TM_][4];
+#pragma unroll
+  for (int mi = 0; mi < T::TM_; ++mi)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      ri[mi][g] = rinv ? *reinterpret_cast<const f32x4*>(rinv + i0 + wm * WR + mi * 32 + h4 + 8 * g)
+                       : f32x4{1.f, 1.f, 1.f, 1.f};
 #pragma unroll
   for (int ni = 0; ni < T::TN_; ++ni) {
     const int64_t q = q0 + wn * WC + ni * 32 + (lane & 31);
@@ -160,7 +175,8 @@ __device__ __forceinline__ void z_epilogue(T& tile, int64_t i0, int64_t q0,
                         (i & 127) * 16;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float e = __builtin_amdgcn_exp2f(sc * tile.acc[mi][ni][r]);
+        const float a = rinv ? ri[mi][r >> 2][r & 3] * tile.acc[mi][ni][r] : tile.acc[mi][ni][r];
+        const float e = __builtin_amdgcn_exp2f(sc * a);
         __builtin_nontemporal_store(tq * __builtin_amdgcn_rcpf(1.f + e),
                                     g0 + (r & 3) * 16 + (r >> 2) * 128);  // nt: G streams out
       }
@@ -173,7 +189,9 @@ __device__ __forceinline__ void z_epilogue(T& tile, int64_t i0, int64_t q0,
 // DMA ring that runs across tile boundaries: the next tile's first K-step
 // lands while this one's epilogue (exp2, rcp, G stores) runs.
 // F = FmtX3: 16x16x32 (unswizzled W / Xd images); FmtH2: 32x32x16 on the
-// swizzled fp16 images of t_w W and t_x Xd (zsc = [1/t_w, 1/t_x]).
+// swizzled fp16 images of s_i w_i (a power-of-two scale per particle row:
+// no particle's weights fall below another's fp16 window) and t_x Xd
+// (xinv = 1/t_x, rinv[i] = 1/s_i).
 // FmtH2 Z tiles: two 16-deep image K-steps per ring stage (32-deep stages,
 // half the barriers, as the distance Gram; scores -2.6 % vs one,
 // profiles/r5a_z_ks2_rank_ab.log)
@@ -184,9 +202,10 @@ template <class F = FmtX3>
 __global__ __launch_bounds__(512, 1) void logreg_z_x3p_kernel(
     const typename F::E* __restrict__ Wx, int64_t n_img, const typename F::E* __restrict__ Xdx,
     int64_t N_img, int nk, const float* __restrict__ tp, int64_t N_pad, float* __restrict__ G,
-    int Tm2, int Tn2, int64_t total, const float* __restrict__ zsc) {
+    int Tm2, int Tn2, int64_t total, const float* __restrict__ xinv,
+    const float* __restrict__ rinv) {
   using ZX3PTile = NTX3Tile<2, 4, 4, 2, 2, F::P == 3, F, z_ks<F>()>;  // nk: ring stages per tile
-  const float zs = F::P == 3 ? 1.f : zsc[0] * zsc[1];
+  const float zs = F::P == 3 ? 1.f : *xinv;
   __shared__ __attribute__((aligned(16))) char smem[ZX3PTile::kSmemBytes];
   const int w = threadIdx.x >> 6, wr = w / ZX3PTile::WN_, wc = w % ZX3PTile::WN_;
   const int64_t x = blockIdx.x % kXcds, u = blockIdx.x / kXcds, U = gridDim.x / kXcds;
@@ -227,7 +246,8 @@ __global__ __launch_bounds__(512, 1) void logreg_z_x3p_kernel(
     tile.compute(smem + stage * ZX3PTile::kStage, wr, wc);
     ZX3PTile::template ring_barrier<0>();
     if (ks + 1 == nk) {
-      z_epilogue(tile, (int64_t)BI * 256, (int64_t)BJ * 256, tp, N_pad, G, zs);
+      z_epilogue(tile, (int64_t)BI * 256, (int64_t)BJ * 256, tp, N_pad, G, zs,
+                 F::P == 3 ? nullptr : rinv);
       tile.zero();
       L = Ln;
       BI = BIn;
@@ -274,12 +294,6 @@ __global__ __launch_bounds__(256) void logreg_finish_kernel(const float* __restr
   if (lane == 0) S[j * lds] = scale * (-a + 0.5f * (float)p - 0.5f * a * w2);
 }
 
-
-// out[0..1] = the two FmtH2 inverse tensor scales of Z's operands, side by side
-__global__ void zscale_pair_kernel(const float* a, const float* b, float* out) {
-  out[0] = *a;
-  out[1] = *b;
-}
 
 // ---- posterior-predictive test accuracy (experiments/logreg_plots.py:42-50) --
 using PTile = ZTile;
@@ -495,7 +509,7 @@ static int logreg_prepare(const float* Xd, int64_t ldxd, const float* t, int64_t
     if ((rc = dsvgd_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, P.base + w.off_xdx, 0, s)))
       return rc;
     const int m16 = w.ldb % 256 == 0;  // the 16x16x32 form (unswizzled image) when it applies
-    return dsvgd_ysplit(Xdp, w.ldb, w.N_pad, P.base + w.off_xdy, m16 ? 0 : 1, s);
+    return dsvgd_ysplit(Xdp, w.ldb, w.N_pad, P.base + w.off_xdy, m16 ? 0 : 1, nullptr, s);
   }
   return DSVGD_OK;
 }
@@ -512,31 +526,27 @@ static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float 
   if (P.h2) {
     void* Wx = base + w.off_wx;
     _Float16* Xdy = (_Float16*)(base + w.off_xdy);
-    float* sw = (float*)(base + w.off_sw);
+    float* rsw = (float*)(base + w.off_rsw);
+    float* riw = (float*)(base + w.off_riw);
     float* sxd = (float*)(base + w.off_sxd);
-    float* sws = (float*)(base + w.off_sws);
-    float* zs = (float*)(base + w.off_zs);
     // W = X[:, 1:] in place (the row image reads its unaligned rows through
-    // aligned 16-byte windows)
-    if ((rc = h2_colscale(X + 1, ldx, n, p, sws, sw, s))) return rc;
-    if ((rc = h2_rowsplit(X + 1, ldx, n, p, w.n_pad, w.pp, sw + 2 * p, Wx, s))) return rc;
-    // the Z kernel's scale operand: [1/t_w, 1/t_x] side by side
+    // aligned 16-byte windows), one power-of-two scale per particle row
+    if ((rc = h2_rowscale(X + 1, ldx, n, p, w.n_pad, rsw, riw, s))) return rc;
+    if ((rc = h2_rowsplit_rows(X + 1, ldx, n, p, w.n_pad, w.pp, rsw, Wx, s))) return rc;
     int blocks = 0;
     if ((rc = persistent_blocks(reinterpret_cast<const void*>(&logreg_z_x3p_kernel<FmtH2>),
                                 &blocks, 512)))
       return rc;
     const int Tm2 = (int)(w.n_pad / 256), Tn2 = (int)(w.N_pad / 256);
-    hipLaunchKernelGGL(zscale_pair_kernel, dim3(1), dim3(1), 0, s, sw + 2 * p + 1,
-                       sxd + 2 * w.ldb + 1, zs);
-    if ((rc = check_launch("zscale_pair"))) return rc;
     hipLaunchKernelGGL(logreg_z_x3p_kernel<FmtH2>, dim3((unsigned)blocks), dim3(512), 0, s,
                        (const _Float16*)Wx, w.n_pad, (const _Float16*)(base + w.off_xdx), w.N_pad,
                        (int)(w.pp / kX3Step / z_ks<FmtH2>()), tp, w.N_pad, G, Tm2, Tn2,
-                       tile_grid(Tm2, Tn2, false), (const float*)zs);
+                       tile_grid(Tm2, Tn2, false), (const float*)(sxd + 2 * w.ldb + 1),
+                       (const float*)riw);
     if ((rc = check_launch("logreg_z_h2"))) return rc;
     splits = gxd_splits(w.n_pad, w.N_pad);
     if ((rc = nn_h2_gemm(false, G, w.N_pad, Xdy, w.ldb, splits, nullptr, GW, w.ldb, nullptr, n, 0, s,
-                         0, sxd + w.ldb)))
+                         0, sxd + w.ldb, nullptr)))
       return rc;
   } else if (P.x3) {
     void* Wx = base + w.off_wx;
@@ -549,11 +559,11 @@ static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float 
     hipLaunchKernelGGL(logreg_z_x3p_kernel<FmtX3>, dim3((unsigned)blocks), dim3(512), 0, s,
                        (const __bf16*)Wx, w.n_pad, (const __bf16*)(base + w.off_xdx), w.N_pad,
                        (int)(w.pp / kX3Step), tp, w.N_pad, G, Tm2, Tn2,
-                       tile_grid(Tm2, Tn2, false), nullptr);
+                       tile_grid(Tm2, Tn2, false), nullptr, nullptr);
     if ((rc = check_launch("logreg_z_x3"))) return rc;
     const int m16 = w.ldb % 256 == 0;
     if ((rc = nn_x3_gemm(false, G, w.N_pad, (const __bf16*)(base + w.off_xdy), w.ldb, 1, nullptr,
-                         GW, w.ldb, nullptr, n, 0, s, 0, m16)))
+                         GW, w.ldb, nullptr, n, 0, s, 0, m16, nullptr)))
       return rc;
   } else {
     float* Wp = (float*)(base + w.off_w);

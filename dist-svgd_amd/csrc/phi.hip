@@ -92,7 +92,10 @@ __global__ __launch_bounds__(512) void nn_x3_kernel(const float* __restrict__ A,
                                                     float* __restrict__ rowsum, int64_t m,
                                                     int64_t row0, int sym,
                                                     const float* __restrict__ colinv,
-                                                    int dsplit, int slice0) {
+                                                    int dsplit, int slice0,
+                                                    const float* __restrict__ gate, int gate_on) {
+  // gate (the FmtH2 range guard, dsvgd_h2_scales): run iff *gate != 0 equals gate_on
+  if (gate && ((*gate != 0.f) != (gate_on != 0))) return;
   using Tile = NNX3Tile<TN, DMA, EXP, M16, RW, F, NB>;
   __shared__ __attribute__((aligned(16))) char smem[Tile::kSmemBytes];
   // dsplit (symmetric layout, 128-row blocks): 1 = only the K-steps left of
@@ -196,7 +199,8 @@ __global__ __launch_bounds__(256) void rowsplit_kernel(const float* __restrict__
 // (gemm_x3.hpp image: 16-B halves swapped on columns with bit 3 set).
 __global__ __launch_bounds__(256) void ysplit_kernel(const float* __restrict__ Y, int64_t ldy,
                                                      int64_t ksteps, __bf16* __restrict__ Yx,
-                                                     int swz) {
+                                                     int swz, const float* __restrict__ gate) {
+  if (gate && *gate == 0.f) return;  // the FmtH2 range guard's fallback image only
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= ksteps * ldy) return;
   const int64_t kb = t / ldy, c = t % ldy;
@@ -220,7 +224,8 @@ __global__ __launch_bounds__(256) void ysplit_kernel(const float* __restrict__ Y
 template <int TN, bool EXP, class F>
 int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy, int splits,
                  const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-                 int64_t row0, int sym, int m16, const float* colinv, hipStream_t s) {
+                 int64_t row0, int sym, int m16, const float* colinv, hipStream_t s,
+                 const float* gate, int gate_on) {
   if (sym && TN == 1) return fail_arg("nn_x3: the symmetric layout needs ldy % 256 == 0");
   const int64_t kchunk = roundup((K + splits - 1) / splits, kX3Step);
   const dim3 grid(ldy / (128 * TN), roundup(m, 128) / 128, splits);
@@ -228,14 +233,14 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
     return fail_arg("nn_x3: the 16x16 form needs the DMA path (ldy % 256 == 0)");
   if (TN == 1)  // TN = 1: 1.5 DMA rounds per K-step -> the register-staged form
     hipLaunchKernelGGL((nn_x3_kernel<TN, false, EXP, false, 2, F>), grid, dim3(512), 0, s, D, K, Yx,
-                       ldy, K, kchunk, st, C, ldc, rowsum, m, row0, 0, colinv, 0, 0);
+                       ldy, K, kchunk, st, C, ldc, rowsum, m, row0, 0, colinv, 0, 0, gate, gate_on);
   else if constexpr (F::P == 3) {
     if (m16)
       hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, TN != 1, 2, F>), grid, dim3(512), 0, s, D,
-                         K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0, 0);
+                         K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0, 0, gate, gate_on);
     else
       hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F>), grid, dim3(512), 0, s, D, K,
-                         Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0, 0);
+                         Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0, 0, gate, gate_on);
   } else {  // FmtH2: the smaller stages fit a 3-stage ring
     if (TN == 4 && EXP && sym && splits >= 2) {
       // symmetric layout split at each row block's diagonal tile: the
@@ -245,21 +250,21 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
       const dim3 g1(grid.x, grid.y, sl), g2(grid.x, grid.y, splits - sl);
       hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2>), g1,
                          dim3(512), 0, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0,
-                         sym, colinv, 1, 0);
+                         sym, colinv, 1, 0, gate, gate_on);
       const int rc = check_launch("nn_x3_kernel(lower)");
       if (rc) return rc;
       hipLaunchKernelGGL(phi_w1_kernel<2>, g2, dim3(PhiW1::kThreads), 0, s, D, K, Yx, ldy, K,
-                         kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, sl);
+                         kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, sl, gate, gate_on);
       return check_launch("phi_w1_kernel(upper)");
     }
     if (TN == 4 && EXP && !sym) {
       hipLaunchKernelGGL(phi_w1_kernel<0>, grid, dim3(PhiW1::kThreads), 0, s, D, K, Yx, ldy, K,
-                         kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0);
+                         kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0, gate, gate_on);
       return check_launch("phi_w1_kernel");
     }
     hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2>), grid,
                        dim3(512), 0, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym,
-                       colinv, 0, 0);
+                       colinv, 0, 0, gate, gate_on);
   }
   return check_launch("nn_x3_kernel");
 }
@@ -269,7 +274,8 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
 template <class F>
 int nn_split_gemm(bool exp_, const float* A, int64_t K, const typename F::E* Yx, int64_t ldy,
                   int splits, const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum,
-                  int64_t m, int64_t row0, hipStream_t s, int sym, int m16, const float* colinv) {
+                  int64_t m, int64_t row0, hipStream_t s, int sym, int m16, const float* colinv,
+                  const float* gate = nullptr, int gate_on = 0) {
   if (F::P == 2) m16 = 0;  // the fp16 format runs the 32x32x16 form
   // buffer offsets are 32-bit: K rows x ldy columns x P parts x 2 bytes of
   // the image (as dsvgd_phi_mm_{h2,x3} check), K x 128 x 4 bytes of D
@@ -283,14 +289,14 @@ int nn_split_gemm(bool exp_, const float* A, int64_t K, const typename F::E* Yx,
     const dim3 grid(ldy / 256, roundup(m, 256) / 256, splits);
     hipLaunchKernelGGL((nn_x3_kernel<4, true, false, F::P == 3, 4, F, F::P == 3 ? 2 : 3>), grid,
                        dim3(512), 0, s, A, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, 0,
-                       colinv, 0, 0);
+                       colinv, 0, 0, gate, gate_on);
     return check_launch("nn_x3_kernel(256-row)");
   }
 #define DSVGD_X3_TN(TN)                                                                        \
   return exp_ ? launch_nn_x3<TN, true, F>(A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0,    \
-                                          sym, m16, colinv, s)                                 \
+                                          sym, m16, colinv, s, gate, gate_on)                  \
               : launch_nn_x3<TN, false, F>(A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0, 0, \
-                                           m16, colinv, s)
+                                           m16, colinv, s, gate, gate_on)
   if (ldy % 512 == 0) DSVGD_X3_TN(4);
   if (ldy % 256 == 0) DSVGD_X3_TN(2);
   DSVGD_X3_TN(1);
@@ -299,16 +305,16 @@ int nn_split_gemm(bool exp_, const float* A, int64_t K, const typename F::E* Yx,
 
 int nn_x3_gemm(bool exp_, const float* A, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
                const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-               int64_t row0, hipStream_t s, int sym, int m16) {
+               int64_t row0, hipStream_t s, int sym, int m16, const float* gate) {
   return nn_split_gemm<FmtX3>(exp_, A, K, Yx, ldy, splits, st, C, ldc, rowsum, m, row0, s, sym,
-                              m16, nullptr);
+                              m16, nullptr, gate, 1);
 }
 
 int nn_h2_gemm(bool exp_, const float* A, int64_t K, const _Float16* Yh, int64_t ldy, int splits,
                const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-               int64_t row0, hipStream_t s, int sym, const float* colinv) {
+               int64_t row0, hipStream_t s, int sym, const float* colinv, const float* gate) {
   return nn_split_gemm<FmtH2>(exp_, A, K, Yh, ldy, splits, st, C, ldc, rowsum, m, row0, s, sym, 0,
-                              colinv);
+                              colinv, gate, 0);
 }
 
 
@@ -747,14 +753,15 @@ int64_t dsvgd_ysplit_bytes(int64_t rows, int64_t ldy) {
   return roundup(rows, kX3Step) * kX3Parts * ldy * 2;
 }
 
-int dsvgd_ysplit(const float* Y, int64_t ldy, int64_t rows, void* Yx, int swz, void* stream) {
+int dsvgd_ysplit(const float* Y, int64_t ldy, int64_t rows, void* Yx, int swz, const float* gate,
+                 void* stream) {
   DSVGD_REQUIRE(Y && Yx, "null pointer");
   DSVGD_REQUIRE(rows > 0 && rows % kX3Step == 0, "rows must be a positive multiple of 16");
   DSVGD_REQUIRE(ldy > 0 && ldy % 8 == 0, "ldy must be a multiple of 8");
   DSVGD_REQUIRE(((uintptr_t)Yx & 15) == 0, "16-byte alignment");
   const int64_t ksteps = rows / kX3Step, threads = ksteps * ldy;
   hipLaunchKernelGGL(ysplit_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, Y, ldy, ksteps, (__bf16*)Yx, swz);
+                     (hipStream_t)stream, Y, ldy, ksteps, (__bf16*)Yx, swz, gate);
   return check_launch("ysplit");
 }
 
@@ -777,7 +784,8 @@ int dsvgd_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int6
 
 int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, int64_t row0,
                     int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
-                    int64_t ldk, float* rowsum, int sym, int m16, void* stream) {
+                    int64_t ldk, float* rowsum, int sym, int m16, const float* gate,
+                    void* stream) {
   DSVGD_REQUIRE(D && Yx && st && KY && rowsum, "null pointer");
   DSVGD_REQUIRE(m > 0 && n > 0, "sizes");
   const int64_t n_pad = roundup(n, 128);
@@ -793,12 +801,13 @@ int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, in
                 "n x ldy too large for 32-bit buffer offsets (use dsvgd_phi_mm)");
   DSVGD_REQUIRE(!sym || (m == n && row0 == 0), "sym: the symmetric layout needs m == n, row0 == 0");
   return nn_x3_gemm(true, D, n_pad, (const __bf16*)Yx, ldy, (int)splits, st, KY, ldk, rowsum, m,
-                    row0, (hipStream_t)stream, sym, m16);
+                    row0, (hipStream_t)stream, sym, m16, gate);
 }
 
 int dsvgd_phi_mm_h2(const float* D, int64_t ldd, const void* Yh, int64_t ldy, int64_t row0,
                     int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
-                    int64_t ldk, float* rowsum, int sym, const float* colinv, void* stream) {
+                    int64_t ldk, float* rowsum, int sym, const float* colinv, const float* gate,
+                    void* stream) {
   DSVGD_REQUIRE(D && Yh && st && KY && rowsum && colinv, "null pointer");
   DSVGD_REQUIRE(m > 0 && n > 0, "sizes");
   const int64_t n_pad = roundup(n, 128);
@@ -813,7 +822,7 @@ int dsvgd_phi_mm_h2(const float* D, int64_t ldd, const void* Yh, int64_t ldy, in
   DSVGD_REQUIRE(!sym || (m == n && row0 == 0 && ldy % 256 == 0),
                 "sym: the symmetric layout needs m == n, row0 == 0, ldy % 256 == 0");
   return nn_h2_gemm(true, D, n_pad, (const _Float16*)Yh, ldy, (int)splits, st, KY, ldk, rowsum, m,
-                    row0, (hipStream_t)stream, sym, colinv);
+                    row0, (hipStream_t)stream, sym, colinv, gate);
 }
 
 int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t splits,

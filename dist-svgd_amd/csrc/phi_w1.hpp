@@ -48,7 +48,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const float* A, int64_t a_npad, const _Float16* Yx, int64_t ldy,
     int64_t K, int64_t kchunk, const dsvgd_select_state* __restrict__ st, float* __restrict__ C,
     int64_t ldc, float* __restrict__ rowsum, int64_t m, int64_t row0, int sym,
-    const float* __restrict__ colinv, int slice0) {
+    const float* __restrict__ colinv, int slice0, const float* __restrict__ gate, int gate_on) {
+  if (gate && ((*gate != 0.f) != (gate_on != 0))) return;  // the FmtH2 range guard (nn_x3_kernel)
   constexpr int dsplit = DS;
   using F = FmtH2;
   using V8 = F::V8;

@@ -119,17 +119,59 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
                red[3][threadIdx.x]) / (float)n;
 }
 
+// --------------------------------------------------------------- center ----
+// center[c] = the lower median of column c over m = min(n, kCenterRows) evenly
+// spaced rows (row (k n) / m, k < m): a robust centre for the Gram form.
+// Centering is exact algebra for phi (translation invariant) and D; what it
+// changes is the conditioning of |x|^2 + |y|^2 - 2 x.y and of r x - K X,
+// whose fp32 cancellation grows with the particles' distance from the centre.
+// The mean moves by (outlier) / n when one particle diverges, and every
+// other particle then sits that far from it (a particle 2^16 spreads away
+// costs the mean-centred Gram ~3e-4 of phi in fp32); the median of a sample
+// stays inside the bulk.  One block per column: the sample is bitonic-sorted
+// in LDS (deterministic, no data-dependent control flow).
+constexpr int kCenterRows = 1024;
+
+__global__ __launch_bounds__(256) void colcenter_kernel(const float* __restrict__ X, int64_t ldx,
+                                                        int64_t n, float* __restrict__ center) {
+  __shared__ float v[kCenterRows];
+  const int64_t c = blockIdx.x;
+  const int m = (int)min(n, (int64_t)kCenterRows);
+  for (int k = threadIdx.x; k < kCenterRows; k += 256)
+    v[k] = k < m ? X[((int64_t)k * n / m) * ldx + c] : INFINITY;
+  __syncthreads();
+  for (int size = 2; size <= kCenterRows; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < kCenterRows / 2; t += 256) {
+        const int i = 2 * t - (t & (stride - 1)), j = i + stride;
+        const float a = v[i], b = v[j];
+        if ((a > b) == ((i & size) == 0)) {
+          v[i] = b;
+          v[j] = a;
+        }
+      }
+      __syncthreads();
+    }
+  if (threadIdx.x == 0) center[c] = v[(m - 1) / 2];
+}
+
 // ---------------------------------------------------------------- pack ----
 // Y[j] = [X[j]-mean (dp cols) | scale*S[j] (dp cols) | 0], norms[j] =
 // |X[j]-mean|^2, rows j >= n zero; with partial != nullptr also the FmtH2
-// column maxima of what it writes (h2.hip), so the scales need no second pass
-// over Y: partial[b][c] = max |Y[r][c]| over block b's rows (pack_rows_per_block), and
-// gmax[2b] / gmax[2b + 1] = the block's largest over the X half [0, dp) /
-// over [dp, ldy).  X == nullptr: the S half of rows < n only (its columns'
-// partials and gmax[2b + 1]).  One wave per row, 16-byte accesses: a lane
-// owns 4 adjacent columns of each 256-column pass (dp % 32 == 0, so a lane's
-// 4 never straddle the X / S boundary).
+// statistics of what it writes (h2.hip), so the scales need no second pass
+// over Y: partial[b][c] = max |Y[r][c]| over block b's rows
+// (pack_rows_per_block), and per block four words (kPackStats) gmax[4b + h]
+// = the largest |entry| of half h (0: the X half [0, dp), 1: the S half),
+// gmax[4b + 2 + h] = the smallest NONZERO row max of half h over the block's
+// rows < n (+inf if none) -- the FmtH2 range guard's input.  rsc != nullptr
+// (with X): rsc[j] = the power-of-two FmtH2 scale of row j's X half (its
+// largest magnitude -> [2^14, 2^15), 1 for a zero row or a row >= n), the
+// per-row scales of the Gram's row image.  X == nullptr: the S half of rows
+// < n only (its columns' partials and the S words of gmax).  One wave per
+// row, 16-byte accesses: a lane owns 4 adjacent columns of each 256-column
+// pass (dp % 32 == 0, so a lane's 4 never straddle the X / S boundary).
 constexpr int kPackQ = 8;  // 256-column passes per row: ldy <= 2048
+constexpr int kPackStats = 4;
 // rows per block: 64 (16 per wave) from ~64K rows, down to 4 (one per wave)
 // below ~4K -- a small pack is latency-bound, its waves must not loop
 __host__ __device__ inline int64_t pack_rows_per_block(int64_t rows_pad) {
@@ -138,14 +180,19 @@ __host__ __device__ inline int64_t pack_rows_per_block(int64_t rows_pad) {
   return r;
 }
 
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  return v;
+}
+
 template <bool VX, bool VS>  // 16-byte loads of X / S rows (aligned, ld % 4 == 0)
 __global__ __launch_bounds__(256) void pack_kernel(
     const float* __restrict__ X, int64_t ldx, const float* __restrict__ S, int64_t lds,
     float scale, const float* __restrict__ mean, int64_t n, int64_t d, int64_t rows_pad,
     int64_t dp, float* __restrict__ Y, int64_t ldy, float* __restrict__ norms,
-    uint32_t* __restrict__ partial, uint32_t* __restrict__ gmax) {
+    uint32_t* __restrict__ partial, uint32_t* __restrict__ gmax, float* __restrict__ rsc) {
   extern __shared__ uint32_t red[];  // [4 waves][ldy]
-  __shared__ uint32_t gred[4][2];
+  __shared__ uint32_t gred[4][kPackStats];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t rpb = pack_rows_per_block(rows_pad);
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
@@ -156,8 +203,10 @@ __global__ __launch_bounds__(256) void pack_kernel(
   for (int q = 0; q < kPackQ; ++q)
 #pragma unroll
     for (int e = 0; e < 4; ++e) mx[q][e] = 0u;
+  uint32_t rminx = 0x7F800000u, rmins = 0x7F800000u;  // +inf
   for (int64_t j = r0 + w; j < r1; j += 4) {
     float nrm = 0.f;
+    uint32_t rx = 0u, rs = 0u;  // this row's largest |entry| per half
     f32x4 v[kPackQ];
 #pragma unroll
     for (int q = 0; q < kPackQ; ++q) {
@@ -192,13 +241,28 @@ __global__ __launch_bounds__(256) void pack_kernel(
       *reinterpret_cast<f32x4*>(Y + j * ldy + c) = v[q];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        mx[q][e] = max(mx[q][e], abs_bits(v[q][e]));
-        if (c < dp) nrm = fmaf(v[q][e], v[q][e], nrm);
+        const uint32_t a = abs_bits(v[q][e]);
+        mx[q][e] = max(mx[q][e], a);
+        if (c < dp) {
+          nrm = fmaf(v[q][e], v[q][e], nrm);
+          rx = max(rx, a);
+        } else {
+          rs = max(rs, a);
+        }
       }
     }
     if (X) {
       nrm = warp_sum(nrm);
       if (lane == 0) norms[j] = nrm;
+    }
+    if (partial != nullptr || rsc != nullptr) {
+      rx = wave_max_u32(rx);
+      rs = wave_max_u32(rs);
+      if (j < n) {
+        if (rx != 0u) rminx = min(rminx, rx);
+        if (rs != 0u) rmins = min(rmins, rs);
+      }
+      if (X && rsc && lane == 0) rsc[j] = pow2_scale(j < n ? __uint_as_float(rx) : 0.f);
     }
   }
   if (partial == nullptr) return;
@@ -214,23 +278,26 @@ __global__ __launch_bounds__(256) void pack_kernel(
       else gs = max(gs, mx[q][e]);
     }
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    gx = max(gx, (uint32_t)__shfl_xor((int)gx, o));
-    gs = max(gs, (uint32_t)__shfl_xor((int)gs, o));
-  }
+  gx = wave_max_u32(gx);
+  gs = wave_max_u32(gs);
   if (lane == 0) {
     gred[w][0] = gx;
     gred[w][1] = gs;
+    gred[w][2] = rminx;
+    gred[w][3] = rmins;
   }
   __syncthreads();
   for (int64_t c = threadIdx.x; c < ldy; c += 256)
     if (c >= c_lo && c < c_hi)
       partial[(int64_t)blockIdx.x * ldy + c] =
           max(max(red[c], red[ldy + c]), max(red[2 * ldy + c], red[3 * ldy + c]));
-  if (threadIdx.x < 2 && (X || threadIdx.x == 1))
-    gmax[2 * blockIdx.x + threadIdx.x] =
-        max(max(gred[0][threadIdx.x], gred[1][threadIdx.x]),
-            max(gred[2][threadIdx.x], gred[3][threadIdx.x]));
+  // X half: words 0, 2; S half: words 1, 3 (pack(NULL, S) leaves the X words)
+  if (threadIdx.x < kPackStats && (X || (threadIdx.x & 1))) {
+    const int h = threadIdx.x;
+    const uint32_t v = h < 2 ? max(max(gred[0][h], gred[1][h]), max(gred[2][h], gred[3][h]))
+                             : min(min(gred[0][h], gred[1][h]), min(gred[2][h], gred[3][h]));
+    gmax[kPackStats * blockIdx.x + h] = v;
+  }
 }
 
 // ldy > 256 kPackQ (d > 1024): one wave per row, element accesses, no maxima: Y[j] = [X[j]-mean (dp cols) | scale*S[j] (dp cols) | 0],
@@ -342,6 +409,16 @@ int dsvgd_colmean(const float* X, int64_t ldx, int64_t n, int64_t d, float* part
   return check_launch("colsum_final");
 }
 
+int dsvgd_colcenter(const float* X, int64_t ldx, int64_t n, int64_t d, float* center,
+                    void* stream) {
+  DSVGD_REQUIRE(X && center, "null pointer");
+  DSVGD_REQUIRE(n > 0 && d > 0 && ldx >= d, "sizes");
+  DSVGD_REQUIRE(d <= 0x7fffffff, "d too large for the grid");
+  hipLaunchKernelGGL(colcenter_kernel, dim3((unsigned)d), dim3(256), 0, (hipStream_t)stream, X, ldx,
+                     n, center);
+  return check_launch("colcenter");
+}
+
 int64_t dsvgd_pack_blocks(int64_t rows_pad) {
   const int64_t r = pack_rows_per_block(rows_pad);
   return (rows_pad + r - 1) / r;
@@ -350,9 +427,11 @@ int64_t dsvgd_pack_max_ldy(void) { return 256 * kPackQ; }
 
 int dsvgd_pack_h2(const float* X, int64_t ldx, const float* S, int64_t lds, float score_scale,
                   const float* mean, int64_t n, int64_t d, int64_t rows_pad, float* Y, int64_t ldy,
-                  float* norms, uint32_t* partial, uint32_t* gmax, void* stream) {
+                  float* norms, uint32_t* partial, uint32_t* gmax, float* rowscale,
+                  void* stream) {
   DSVGD_REQUIRE(Y && (X ? (mean && norms) : (S != nullptr)), "null pointer");
   DSVGD_REQUIRE(!partial == !gmax, "partial and gmax go together");
+  DSVGD_REQUIRE(!rowscale || ldy <= dsvgd_pack_max_ldy(), "row scales need ldy <= 2048");
   DSVGD_REQUIRE(n > 0 && d > 0 && (!X || ldx >= d) && rows_pad >= n, "sizes");
   const int64_t dp = dsvgd_dp(d);
   DSVGD_REQUIRE(ldy >= 2 * dp && ldy % 4 == 0, "ldy");
@@ -371,7 +450,8 @@ int dsvgd_pack_h2(const float* X, int64_t ldx, const float* S, int64_t lds, floa
   const size_t lds_bytes = partial ? 4 * sizeof(uint32_t) * (size_t)ldy : 0;
 #define DSVGD_PACK(VX, VS)                                                                    \
   hipLaunchKernelGGL((pack_kernel<VX, VS>), grid, dim3(256), lds_bytes, s, X, ldx, S, lds,    \
-                     score_scale, mean, n, d, rows_pad, dp, Y, ldy, norms, partial, gmax)
+                     score_scale, mean, n, d, rows_pad, dp, Y, ldy, norms, partial, gmax,      \
+                     rowscale)
   if (vx && vs) DSVGD_PACK(true, true);
   else if (vx) DSVGD_PACK(true, false);
   else if (vs) DSVGD_PACK(false, true);
@@ -384,7 +464,7 @@ int dsvgd_pack(const float* X, int64_t ldx, const float* S, int64_t lds, float s
                const float* mean, int64_t n, int64_t d, int64_t rows_pad, float* Y, int64_t ldy,
                float* norms, void* stream) {
   return dsvgd_pack_h2(X, ldx, S, lds, score_scale, mean, n, d, rows_pad, Y, ldy, norms, nullptr,
-                       nullptr, stream);
+                       nullptr, nullptr, stream);
 }
 
 int dsvgd_score_gaussian(const float* X, int64_t ldx, int64_t n, int64_t d, const float* mu,

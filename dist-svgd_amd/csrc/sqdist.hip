@@ -39,8 +39,11 @@ using GramTile = NTTile<2, 2, 2, 2>;  // 128 x 128 block, 4 waves of 64 x 64
 // tile's 128 row / column norms.
 // MIR = false: the launch never stores mirror tiles (compile-time: no
 // register shuffles for them)
+// RS (FmtH2 row images): the Gram comes out scaled by s_i s_j (per-row
+// power-of-two scales); sirow holds 2 / s_i per row, sicol 1 / s_j per column,
+// and 2 x.y = sirow_i (sicol_j acc) (exact power-of-two factors).
 template <bool SYM, int smode, bool ZERO = false, class Tile = GramTile, int NI = 2,
-          class SW = SlotWriter, bool MIR = true>
+          class SW = SlotWriter, bool MIR = true, bool RS = false>
 __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t row0,
                                             int64_t m, int64_t n, int64_t n_pad,
                                             float* __restrict__ D, const float* srow,
@@ -48,7 +51,8 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
                                             WindowHist& wh, uint32_t* shist, SW& sw,
                                             const SlotLayout& sl, int64_t slot,
                                             bool mirror_store = true, int r0t = 0,
-                                            float c2 = 2.f) {
+                                            float c2 = 2.f, const float* sirow = nullptr,
+                                            const float* sicol = nullptr) {
   // r0t: row0 / 128 when a row block's diagonal square runs SYM (bi is then
   // block-local, bj global; the mirror of (bi, bj) is (bj - r0t, bi + r0t))
   const int lane = threadIdx.x & 63;
@@ -73,14 +77,21 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
       const int cl = cbase + ni * 32 + (lane & 31);
       const int rb = rbase + mi * 32 + h4;  // this lane's first row in the sub-tile
       const float nj = scol[cl];
+      const float ij = RS ? sicol[cl] : 1.f;
       // uniform tile base + zero-extended 32-bit lane offset: the SGPR-base
       // store form, no per-lane 64-bit address arithmetic
       float* const dp0 = Dtile + (uint32_t)((cl >> 4) * kPanelElems + (cl & 15) + rb * 16);
+      // 2 y_i.y_j of register r (row rl)
+      auto gram2 = [&](int r, int rl) {
+        return RS ? sirow[rl] * (ij * tile.acc[mi][ni][r]) : c2 * tile.acc[mi][ni][r];
+      };
       float v[16];
       if (interior) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          v[r] = fmaxf(0.f, (srow[rb + (r & 3) + 8 * (r >> 2)] + nj) - c2 * tile.acc[mi][ni][r]);
+        for (int r = 0; r < 16; ++r) {
+          const int rl = rb + (r & 3) + 8 * (r >> 2);
+          v[r] = fmaxf(0.f, (srow[rl] + nj) - gram2(r, rl));
+        }
       } else {
         const bool colok = j0 + cl < n;
 #pragma unroll
@@ -88,9 +99,7 @@ __device__ __forceinline__ void sq_epilogue(Tile& tile, int bi, int bj, int64_t 
           const int rl = rb + (r & 3) + 8 * (r >> 2);
           float x;
           if (colok && i0 + rl < m)
-            x = (row0 + i0 + rl == j0 + cl)
-                    ? 0.f
-                    : fmaxf(0.f, (srow[rl] + nj) - c2 * tile.acc[mi][ni][r]);
+            x = (row0 + i0 + rl == j0 + cl) ? 0.f : fmaxf(0.f, (srow[rl] + nj) - gram2(r, rl));
           else
             x = INFINITY;
           v[r] = x;
@@ -311,8 +320,10 @@ __global__ __launch_bounds__(256, 2) void sqdist_persistent_kernel(
 // tile, and past the padded matrix, are skipped).  Candidate slots: 8 per tile.
 // M16: 16x16x32 MFMAs on an unswizzled Yg (FmtX3), else 32x32x16 on a
 // swizzled one (FmtH2).
-// F = FmtH2: Yg is the fp16 image of t Xc (t = tsc[0]), the Gram comes out
-// scaled by t^2: the epilogue's 2 x.y is c2 acc with c2 = 2 / t^2.
+// F = FmtH2: Yg is the fp16 image of s_i Xc[i] with a power-of-two scale per
+// ROW (rsc[i], dsvgd_pack_h2's / dsvgd_h2_rowscale's), so no particle's
+// coordinates sit below another's fp16 window; the Gram comes out scaled by
+// s_i s_j and the epilogue divides both back out (sq_epilogue RS).
 // KS: 16-deep image K-steps per ring stage.
 template <bool SYM, int smode, bool M16 = true, class F = FmtX3, int KS = 1, bool MIR = true>
 __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
@@ -320,7 +331,7 @@ __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
     int64_t row0, int64_t m, int64_t n, int64_t n_pad, int nk, float* __restrict__ D,
     dsvgd_select_state* __restrict__ st, float* __restrict__ cand, int64_t total_tiles,
     int layout, int Tm2, int Tc2, int bj_off, int r0t, int64_t slot_base, int64_t ns_total,
-    const float* __restrict__ tsc) {
+    const float* __restrict__ rsc) {
   // candidates staged in the retired ring stage (bracket mode, 32x32 form,
   // 32-deep stages)
   constexpr bool kWC = kGramWC && smode == kSelBracket && !M16 && KS == 2;
@@ -328,10 +339,11 @@ __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
   static_assert(!kWC || GramX3WTile::kChunksPerWave * 1024 >= 64 * 32 * 4,
                 "32-deep candidate lists fit the wave's chunks");
   constexpr int kT = GramX3WTile::kThreads;
-  const float c2 = F::P == 3 ? 2.f : 2.f * tsc[1] * tsc[1];
+  constexpr bool RS = F::P == 2;  // per-row scales
   __shared__ __attribute__((aligned(16))) char smem[GramX3WTile::kSmemBytes];
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
   __shared__ float snorm[512];  // the tile's 256 row norms, then its 256 column norms
+  __shared__ float sinv[RS ? 512 : 1];  // RS: 2 / s_i of its rows, then 1 / s_j of its columns
   // bracket candidates staged per lane (SlotWriterLds) on the 32x32 form
   constexpr bool kLdsSlots = smode == kSelBracket && !M16;
   __shared__ float scand[kLdsSlots && !kWC ? (kT / 64) * 64 * kStageDepth : 1];
@@ -378,6 +390,7 @@ __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
     {
       const int64_t gi = t < 256 ? row0 + (int64_t)BI * 256 + t : (int64_t)BJ * 256 + t - 256;
       snorm[t] = gi < n_pad ? norms[gi] : 0.f;
+      if constexpr (RS) sinv[t] = (t < 256 ? 2.f : 1.f) * pow2_inv(gi < n_pad ? rsc[gi] : 1.f);
     }
     __syncthreads();
     // this wave's 128-sub-tile
@@ -404,10 +417,10 @@ __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
                                   snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl,
                                   slot, layout == 0, r0t);
       else
-        sq_epilogue<SYM, smode, true, GramX3WTile, 4, SW, MIR>(
+        sq_epilogue<SYM, smode, true, GramX3WTile, 4, SW, MIR, RS>(
             tile, bi, bj, row0, m, n, n_pad, D, snorm + (wr >> 1) * 128,
             snorm + 256 + wc * 128, (wr & 1) * 64, 0, wh, shist, sw, sl, slot, layout == 0,
-            r0t, c2);
+            r0t, 2.f, sinv + (wr >> 1) * 128, sinv + 256 + wc * 128);
     }
     if (smode == kSelHist) wh.flush(shist);
   };
@@ -452,7 +465,7 @@ int64_t gram_img_rows(int64_t n) { return roundup(n, 128) + 256; }
 template <int SM, class F = FmtX3>
 int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, int64_t m,
                      int64_t n, int64_t d, float* D, dsvgd_select_state* st, float* cand,
-                     int layout, hipStream_t s, const float* tsc = nullptr) {
+                     int layout, hipStream_t s, const float* rsc = nullptr) {
   const int64_t dp = roundup(d, 32), m_pad = roundup(m, 128), n_pad = roundup(n, 128);
   const int64_t img = gram_img_rows(n);
   const bool sym = m == n && row0 == 0;
@@ -496,7 +509,7 @@ int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, 
 #define DSVGD_X3W(SY, B, LAY, R0T, MIR)                                                          \
   hipLaunchKernelGGL((sqdist_x3w_kernel<SY, SM, F::P == 3, F, KS, MIR>), dim3((unsigned)B),       \
                      dim3(512), 0, s, Yg, img, norms, row0, m, n, n_pad, nk, D, st, cand, P.total, \
-                     LAY, P.tm2, P.tc2, P.bj_off, R0T, base, ns_total, tsc)
+                     LAY, P.tm2, P.tc2, P.bj_off, R0T, base, ns_total, rsc)
     if (P.sym && lay == 0)  // mirror stores
       DSVGD_X3W(true, bs, lay, P.r0t, true);
     else if (P.sym)
@@ -705,8 +718,8 @@ int dsvgd_sqdist_x3(const void* Yg, const float* norms, int64_t row0, int64_t m,
 
 int dsvgd_sqdist_h2(const void* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
                     int64_t d, float* D, int64_t ldd, int select_mode, dsvgd_select_state* st,
-                    float* cand, int layout, const float* tscale, void* stream) {
-  DSVGD_REQUIRE(Yg && norms && D && tscale, "null pointer");
+                    float* cand, int layout, const float* rowscale, void* stream) {
+  DSVGD_REQUIRE(Yg && norms && D && rowscale, "null pointer");
   DSVGD_REQUIRE(m > 0 && n > 0 && row0 >= 0 && row0 + m <= n && d > 0, "sizes");
   DSVGD_REQUIRE(select_mode >= 0 && select_mode <= 2, "select_mode must be 0, 1 or 2");
   DSVGD_REQUIRE(select_mode == 0 || st, "select mode needs a state");
@@ -723,12 +736,14 @@ int dsvgd_sqdist_h2(const void* Yg, const float* norms, int64_t row0, int64_t m,
   hipStream_t s = (hipStream_t)stream;
   switch (select_mode) {
     case kSelNone:
-      return launch_sqdist_x3<kSelNone, FmtH2>(yg, norms, row0, m, n, d, D, st, cand, layout, s, tscale);
+      return launch_sqdist_x3<kSelNone, FmtH2>(yg, norms, row0, m, n, d, D, st, cand, layout, s,
+                                               rowscale);
     case kSelHist:
-      return launch_sqdist_x3<kSelHist, FmtH2>(yg, norms, row0, m, n, d, D, st, cand, layout, s, tscale);
+      return launch_sqdist_x3<kSelHist, FmtH2>(yg, norms, row0, m, n, d, D, st, cand, layout, s,
+                                               rowscale);
     default:
       return launch_sqdist_x3<kSelBracket, FmtH2>(yg, norms, row0, m, n, d, D, st, cand, layout, s,
-                                                  tscale);
+                                                  rowscale);
   }
 }
 

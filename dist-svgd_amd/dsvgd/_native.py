@@ -9,7 +9,7 @@ import os
 
 import torch
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libdsvgd_hip.so")
 
 _c = ctypes
@@ -28,11 +28,12 @@ SIGNATURES = {
     "dsvgd_ldy": (_i64, [_i64]),
     "dsvgd_colmean_workspace_floats": (_c.c_size_t, [_i64, _i64]),
     "dsvgd_colmean": (_int, [_p, _i64, _i64, _i64, _p, _p, _p]),
+    "dsvgd_colcenter": (_int, [_p, _i64, _i64, _i64, _p, _p]),
     "dsvgd_pack": (_int, [_p, _i64, _p, _i64, _f, _p, _i64, _i64, _i64, _p, _i64, _p, _p]),
     "dsvgd_pack_blocks": (_i64, [_i64]),
     "dsvgd_pack_max_ldy": (_i64, []),
     "dsvgd_pack_h2": (_int, [_p, _i64, _p, _i64, _f, _p, _i64, _i64, _i64, _p, _i64, _p, _p, _p,
-                             _p]),
+                             _p, _p]),
     "dsvgd_sqdist": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p]),
     "dsvgd_sqdist_direct": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p,
                                    _p]),
@@ -49,22 +50,24 @@ SIGNATURES = {
     "dsvgd_phi_splits": (_i64, [_i64, _i64, _i64]),
     "dsvgd_phi_mm": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p]),
     "dsvgd_ysplit_bytes": (_i64, [_i64, _i64]),
-    "dsvgd_ysplit": (_int, [_p, _i64, _i64, _p, _int, _p]),
+    "dsvgd_ysplit": (_int, [_p, _i64, _i64, _p, _int, _p, _p]),
     "dsvgd_rowsplit_bytes": (_i64, [_i64, _i64]),
     "dsvgd_rowsplit": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _p, _int, _p]),
     "dsvgd_sqdist_x3": (_int, [_p, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _int, _p]),
     "dsvgd_phi_mm_x3": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _int,
-                                _int, _p]),
+                                _int, _p, _p]),
     "dsvgd_h2_colscale_workspace_floats": (_c.c_size_t, [_i64, _i64]),
     "dsvgd_h2_colscale": (_int, [_p, _i64, _i64, _i64, _p, _p, _p]),
     "dsvgd_h2_scales": (_int, [_p, _p, _i64, _i64, _i64, _i64, _p, _p]),
     "dsvgd_h2_image_bytes": (_i64, [_i64, _i64]),
     "dsvgd_h2_ysplit": (_int, [_p, _i64, _i64, _p, _p, _p]),
     "dsvgd_h2_rowsplit": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _p, _p, _p]),
+    "dsvgd_h2_rowsplit_rows": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _p, _p, _p]),
+    "dsvgd_h2_rowscale": (_int, [_p, _i64, _i64, _i64, _i64, _p, _p, _p]),
     "dsvgd_sqdist_h2": (_int, [_p, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _int, _p,
                                _p]),
     "dsvgd_phi_mm_h2": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _int,
-                               _p, _p]),
+                               _p, _p, _p]),
     "dsvgd_phi_finish": (_int, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _f,
                                 _f, _p, _i64, _p, _i64, _p, _i64, _p]),
     "dsvgd_phi_direct": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _f, _f, _p,

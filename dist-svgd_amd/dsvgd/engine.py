@@ -4,7 +4,7 @@ One engine serves an owned row block [row0, row0+m) of an interacting set of n
 particles (the whole set for Sampler; the DistSampler rank's block otherwise).
 Per Jacobi step, all stream-ordered on the current HIP stream, no host sync:
 
-  colmean -> pack          Y = [X - mean | scale*S] (n_pad+128, ldy), norms
+  colcenter -> pack        Y = [X - c | scale*S] (n_pad+128, ldy), norms (c: robust centre)
   select_init -> sqdist    D = ||y_i||^2+||y_j||^2-2 y_i.y_j on MFMA (panel layout)
                            + radix histogram of key digit 1 (bits 31..21)
   [allreduce hist] pick1 -> hist2 -> [allreduce] pick2 -> hist3 -> [allreduce] pick3
@@ -198,11 +198,21 @@ class PhiEngine(object):
         elif gram_gemm == "h2":
             nb = lib.dsvgd_h2_image_bytes(self.gram_rows, self.dp)
             self.Yg = torch.empty(nb // 2, dtype=torch.int16, device=dev)
-        if "h2" in (phi_gemm, gram_gemm):
-            # FmtH2 scales (dsvgd_h2_colscale layout): of Y's X half for the
-            # Gram, of all of Y for phi_mm's B image
-            self.xscale = torch.empty(2 * self.dp + 2, **f32)
-            self.yscale = torch.empty(2 * self.ldy + 2, **f32)
+        if gram_gemm == "h2":
+            # per-row FmtH2 scales of Y's X half: the Gram's row image
+            self.rsc = torch.ones(rows, **f32)
+        if phi_gemm == "h2":
+            # FmtH2 column scales of all of Y for phi_mm's B image
+            # (dsvgd_h2_colscale layout: [s_c | 1/s_c | t | 1/t | range guard])
+            self.yscale = torch.empty(2 * self.ldy + 3, **f32)
+            # the range guard's fallback: phi_mm on the FmtX3 image (when its
+            # 32-bit offsets allow; include/dsvgd.h FmtH2)
+            self.m16_fb = self.ldy % 256 == 0
+            if self.n_pad * self.ldy * 6 < (1 << 31):
+                nb = lib.dsvgd_ysplit_bytes(self.n_pad, self.ldy)
+                self.Yx3 = torch.empty(nb // 2, dtype=torch.int16, device=dev)
+            else:
+                self.Yx3 = None
         # d <= 1024: pack writes the column maxima the scales come from
         # (dsvgd_pack_h2 / dsvgd_h2_scales); wider, a separate pass over Y
         self.fused_scales = ("h2" in (phi_gemm, gram_gemm) and self.ldy <= lib.dsvgd_pack_max_ldy()
@@ -211,14 +221,13 @@ class PhiEngine(object):
             self.colmax_nb = lib.dsvgd_pack_blocks(rows)
             i32 = dict(dtype=torch.int32, device=dev)
             self.colmax = torch.zeros(self.colmax_nb * self.ldy, **i32)
-            self.gmax = torch.zeros(2 * self.colmax_nb, **i32)
+            self.gmax = torch.zeros(4 * self.colmax_nb, **i32)
         elif "h2" in (phi_gemm, gram_gemm):
             self.scale_ws = torch.empty(
                 max(1, lib.dsvgd_h2_colscale_workspace_floats(self.n_pad, self.ldy)), **f32)
         self.KY = torch.empty(self.splits * m, self.ldy, **f32)
         self.rowsum = torch.empty(self.splits * self.m_pad, **f32)
-        self.mean = torch.empty(d, **f32)
-        self.mean_ws = torch.empty(max(1, lib.dsvgd_colmean_workspace_floats(n, d)), **f32)
+        self.mean = torch.empty(d, **f32)    # the packing centre (dsvgd_colcenter)
         self.phi = torch.empty(m, d, **f32)
         self.state = SelectState(dev)
         self.k_rank = (m * n - 1) // 2 if (local_median and m < n) else -1
@@ -252,7 +261,9 @@ class PhiEngine(object):
         d_bytes = 4 * self.m_pad * self.n_pad
         cand = 4 * max(1 << 22, (self.m * self.n) // 16) if self.m * self.n >= self.BRACKET_MIN_ENTRIES else 0
         splits = N.load().dsvgd_phi_splits(self.m, self.n, self.ldy)
-        other = 4 * ((self.n_pad + 128) * self.ldy * 3 + splits * self.m * self.ldy)
+        # Y, its FmtH2 image, the FmtX3 fallback image (1.5 Y) and the Gram's
+        # row image, rounded up; the split-K partials
+        other = 4 * ((self.n_pad + 128) * self.ldy * 4 + splits * self.m * self.ldy)
         need = d_bytes + cand + other
         free, _ = torch.cuda.mem_get_info(dev)
         # the caching allocator's reserved-but-unused blocks are free to torch too
@@ -280,7 +291,7 @@ class PhiEngine(object):
         with span(self.timer, "pack"):
             N.call("dsvgd_pack_h2", None, self.d, N.ptr(S), N.ld(S), float(score_scale), None,
                    self.n, self.d, self.Y.shape[0], N.ptr(self.Y), self.ldy, None,
-                   *self._maxima(), s)
+                   *self._maxima(), None, s)
 
     def _maxima(self):
         if self.fused_scales:
@@ -297,14 +308,14 @@ class PhiEngine(object):
                    N.ptr(self.scale_ws), N.ptr(out), s)
 
     def _pack(self, X, S, score_scale, s):
-        N.call("dsvgd_colmean", N.ptr(X), N.ld(X), self.n, self.d, N.ptr(self.mean_ws),
-               N.ptr(self.mean), s)
+        N.call("dsvgd_colcenter", N.ptr(X), N.ld(X), self.n, self.d, N.ptr(self.mean), s)
         lds = N.ld(S) if S is not None else self.d
         if S is not None:
             assert S.shape == (self.n, self.d)
+        rsc = self.rsc if (self.gram_gemm == "h2" and self.fused_scales) else None
         N.call("dsvgd_pack_h2", N.ptr(X), N.ld(X), N.ptr(S), lds, float(score_scale),
                N.ptr(self.mean), self.n, self.d, self.Y.shape[0], N.ptr(self.Y), self.ldy,
-               N.ptr(self.norms), *self._maxima(), s)
+               N.ptr(self.norms), *self._maxima(), N.ptr(rsc), s)
 
     def distances(self, median=False):
         """D for the owned rows.  median=True also does the select's first
@@ -321,14 +332,15 @@ class PhiEngine(object):
             st, mode = self.state.ptr, SEL_HIST
         if self.gram_gemm == "h2" and self.d > self.DIRECT_MAX_D:
             with span(self.timer, "rowsplit"):
-                self._scales(self.dp, self.xscale, s)
-                tsc = N.ptr(self.xscale) + 4 * 2 * self.dp        # [t, 1/t]
-                N.call("dsvgd_h2_rowsplit", N.ptr(self.Y), self.ldy, self.n_pad, self.dp,
-                       self.gram_rows, self.dp, tsc, N.ptr(self.Yg), s)
+                if not self.fused_scales:   # (pack wrote them otherwise)
+                    N.call("dsvgd_h2_rowscale", N.ptr(self.Y), self.ldy, self.n_pad, self.dp,
+                           self.rsc.numel(), N.ptr(self.rsc), None, s)
+                N.call("dsvgd_h2_rowsplit_rows", N.ptr(self.Y), self.ldy, self.n_pad, self.dp,
+                       self.gram_rows, self.dp, N.ptr(self.rsc), N.ptr(self.Yg), s)
             with span(self.timer, "sqdist"):
                 N.call("dsvgd_sqdist_h2", N.ptr(self.Yg), N.ptr(self.norms), self.row0, self.m,
                        self.n, self.d, N.ptr(self.D), self.n_pad, mode, st, cand, int(self.sym),
-                       tsc, s)
+                       N.ptr(self.rsc), s)
             return
         if self.gram_gemm == "x3" and self.d > self.DIRECT_MAX_D:
             with span(self.timer, "rowsplit"):
@@ -427,6 +439,10 @@ class PhiEngine(object):
                        self.KY.numel(), s)
             return
         if self.phi_gemm == "h2":
+            # the range guard word of the scales: phi_mm_h2 runs while it
+            # reads 0; otherwise the FmtX3 image and phi_mm_x3 behind it do
+            # (both stay on the stream -- no host round trip)
+            guard = (N.ptr(self.yscale) + 4 * (2 * self.ldy + 2)) if self.Yx3 is not None else None
             with span(self.timer, "ysplit"):
                 self._scales(self.ldy, self.yscale, s)
                 N.call("dsvgd_h2_ysplit", N.ptr(self.Y), self.ldy, self.n_pad,
@@ -435,16 +451,24 @@ class PhiEngine(object):
                 N.call("dsvgd_phi_mm_h2", N.ptr(self.D), self.n_pad, N.ptr(self.Yx), self.ldy,
                        self.row0, self.m, self.n, self.state.ptr, self.splits, N.ptr(self.KY),
                        self.ldy, N.ptr(self.rowsum), int(self.sym),
-                       N.ptr(self.yscale) + 4 * self.ldy, s)
+                       N.ptr(self.yscale) + 4 * self.ldy, guard, s)
+            if guard is not None:
+                with span(self.timer, "phi_guard"):
+                    N.call("dsvgd_ysplit", N.ptr(self.Y), self.ldy, self.n_pad, N.ptr(self.Yx3),
+                           0 if self.m16_fb else 1, guard, s)
+                    N.call("dsvgd_phi_mm_x3", N.ptr(self.D), self.n_pad, N.ptr(self.Yx3),
+                           self.ldy, self.row0, self.m, self.n, self.state.ptr, self.splits,
+                           N.ptr(self.KY), self.ldy, N.ptr(self.rowsum), int(self.sym),
+                           int(self.m16_fb), guard, s)
         elif self.x3:
             m16 = self.m16
             with span(self.timer, "ysplit"):
                 N.call("dsvgd_ysplit", N.ptr(self.Y), self.ldy, self.n_pad, N.ptr(self.Yx),
-                       0 if m16 else 1, s)
+                       0 if m16 else 1, None, s)
             with span(self.timer, "phi_mm"):
                 N.call("dsvgd_phi_mm_x3", N.ptr(self.D), self.n_pad, N.ptr(self.Yx), self.ldy,
                        self.row0, self.m, self.n, self.state.ptr, self.splits, N.ptr(self.KY),
-                       self.ldy, N.ptr(self.rowsum), int(self.sym), int(m16), s)
+                       self.ldy, N.ptr(self.rowsum), int(self.sym), int(m16), None, s)
         else:
             with span(self.timer, "phi_mm"):
                 N.call("dsvgd_phi_mm", N.ptr(self.D), self.n_pad, N.ptr(self.Y), self.ldy,
@@ -453,6 +477,13 @@ class PhiEngine(object):
         N.call("dsvgd_phi_finish", N.ptr(self.KY), self.ldy, N.ptr(self.rowsum), self.splits,
                N.ptr(self.Y), self.ldy, self.row0, self.m, self.d, self.dp, self.state.ptr,
                float(inv_n), float(step), ex, lde, phi, self.d, xo, ldx, s)
+
+    def range_guard(self):
+        """The last phi_mm's FmtH2 range guard (True: it ran on the FmtX3
+        fallback; None: not the h2 engine) -- synchronises."""
+        if self.phi_gemm != "h2" or self.d <= self.DIRECT_MAX_D:
+            return None
+        return bool(float(self.yscale[2 * self.ldy + 2]) != 0.0)
 
     # ------------------------------------------------------------ helpers --
     def step(self, X, S, X_own=None, step=0.0, h=None, score_scale=1.0, allreduce=None,

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DSVGD_ABI_VERSION 2
+#define DSVGD_ABI_VERSION 3
 
 enum {
   DSVGD_OK = 0,
@@ -96,6 +96,12 @@ int64_t dsvgd_ldy(int64_t dp); /* row stride of Y = [Xc | S] (phi col tile) */
 size_t dsvgd_colmean_workspace_floats(int64_t n, int64_t d);
 int dsvgd_colmean(const float* X, int64_t ldx, int64_t n, int64_t d, float* partial, float* mean,
                   void* stream);
+/* center[c] = the lower median of X[:, c] over min(n, 1024) evenly spaced rows
+ * (row k n / m): the centre the engine packs against.  Robust where the mean
+ * is not: one diverging particle moves the mean by its distance / n and every
+ * other particle's |x|^2 + |y|^2 - 2 x.y (and r x - K X) cancellation with it. */
+int dsvgd_colcenter(const float* X, int64_t ldx, int64_t n, int64_t d, float* center,
+                    void* stream);
 
 /* Y[j] = [X[j]-mean | score_scale*S[j]] zero padded to (rows_pad x ldy);
  * norms[j] = ||X[j]-mean||^2.  Replaces the per-pair operand gathering of
@@ -105,17 +111,24 @@ int dsvgd_colmean(const float* X, int64_t ldx, int64_t n, int64_t d, float* part
 int dsvgd_pack(const float* X, int64_t ldx, const float* S, int64_t lds, float score_scale,
                const float* mean, int64_t n, int64_t d, int64_t rows_pad, float* Y, int64_t ldy,
                float* norms, void* stream);
-/* dsvgd_pack + the FmtH2 column maxima of what it writes (ldy <=
+/* dsvgd_pack + the FmtH2 statistics of what it writes (ldy <=
  * dsvgd_pack_max_ldy() = 2048, i.e. d <= 1024): partial (uint32,
- * dsvgd_pack_blocks(rows_pad) x ldy) and gmax (2 x that many blocks), the
- * input of dsvgd_h2_scales -- the scales without a second pass over Y.  With X
- * NULL only the S half's maxima are (re)written, so pack(X) then pack(NULL, S)
- * leaves the maxima of the whole Y.  partial = gmax = NULL: dsvgd_pack. */
+ * dsvgd_pack_blocks(rows_pad) x ldy column maxima) and gmax (4 words per
+ * block: [4b] / [4b+1] the largest |entry| of the X half [0, dp) / of the
+ * rest; [4b+2] / [4b+3] the smallest nonzero row max of each half over the
+ * block's rows < n, +inf if none -- fp32 bit patterns), the input of
+ * dsvgd_h2_scales -- the scales and the range guard without a second pass
+ * over Y.  With X NULL only the S half's statistics are (re)written, so
+ * pack(X) then pack(NULL, S) leaves those of the whole Y.  partial = gmax =
+ * NULL: dsvgd_pack.  rowscale (nullable, rows_pad floats, with X): the FmtH2
+ * power-of-two scale of each row's X half (largest magnitude -> [2^14,
+ * 2^15); 1 for a zero row or a row >= n) -- the Gram's per-row image scales. */
 int64_t dsvgd_pack_blocks(int64_t rows_pad);
 int64_t dsvgd_pack_max_ldy(void);
 int dsvgd_pack_h2(const float* X, int64_t ldx, const float* S, int64_t lds, float score_scale,
                   const float* mean, int64_t n, int64_t d, int64_t rows_pad, float* Y, int64_t ldy,
-                  float* norms, uint32_t* partial, uint32_t* gmax, void* stream);
+                  float* norms, uint32_t* partial, uint32_t* gmax, float* rowscale,
+                  void* stream);
 
 /* ---- pairwise squared distances ---------------------------------------- */
 /* D[i][j] = ||y_i - y_j||^2 for the owned row block i in [row0, row0+m) of Y
@@ -239,10 +252,16 @@ int64_t dsvgd_ysplit_bytes(int64_t rows, int64_t ldy);
 int64_t dsvgd_rowsplit_bytes(int64_t rows_pad, int64_t kpad);
 int dsvgd_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
                    int64_t kpad, void* img, int swz, void* stream);
-int dsvgd_ysplit(const float* Y, int64_t ldy, int64_t rows, void* Yx, int swz, void* stream);
+/* gate (nullable): the FmtH2 range-guard word of a dsvgd_h2_scales output
+ * over all ldy columns (&scale[2 ldy + 2]): dsvgd_ysplit and dsvgd_phi_mm_x3
+ * do nothing while it reads 0 -- the FmtX3 fallback of dsvgd_phi_mm_h2,
+ * launched behind it on the same stream, so exactly one of the two writes KY
+ * and rowsum without a host round trip (graph-capturable). */
+int dsvgd_ysplit(const float* Y, int64_t ldy, int64_t rows, void* Yx, int swz, const float* gate,
+                 void* stream);
 int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, int64_t row0,
                     int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
-                    int64_t ldk, float* rowsum, int sym, int m16, void* stream);
+                    int64_t ldk, float* rowsum, int sym, int m16, const float* gate, void* stream);
 
 /* ---- FmtH2: the fp16 two-part split engine (the default) ---------------
  * An operand v enters the fp16 MFMA as s v = v0 + v1, v0 = f16(s v),
@@ -253,17 +272,29 @@ int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, in
  * from half the MFMAs of the X3 engine (gemm_x3.hpp, h2.hip).  The scale
  * divides out exactly inside each kernel: outputs are unscaled fp32.
  *
+ * The window: an entry keeps 22 significant bits only within 2^-16 of the
+ * largest magnitude sharing its scale; below it, only 2^-38 of that largest
+ * (absolute).  So the NT row images (the Gram's Xc, logreg's W) take one
+ * scale per ROW (dsvgd_h2_rowscale / dsvgd_pack_h2's rowscale: no particle
+ * sits in another's window), and the NN B operand (phi_mm's [Xc | S], one
+ * scale per column) is guarded: dsvgd_h2_scales flags a step whose particles'
+ * rows span more than 2^16 in a half of Y, and that step's phi_mm runs on the
+ * FmtX3 engine instead (dsvgd_phi_mm_h2 / _x3 `gate`).
+ *
  * dsvgd_h2_colscale: per column c of A (rows x cols), scale[c] = s_c and
  * scale[cols + c] = 1 / s_c; scale[2 cols] = t = min s_c over the nonzero
  * finite columns (1 if a column holds an inf / NaN, which then propagate),
- * scale[2 cols + 1] = 1 / t.  scale: 2 cols + 2 floats; ws:
+ * scale[2 cols + 1] = 1 / t, scale[2 cols + 2] = 0 (no range guard on this
+ * path).  scale: 2 cols + 3 floats; ws:
  * dsvgd_h2_colscale_workspace_floats(rows, cols) floats. */
 size_t dsvgd_h2_colscale_workspace_floats(int64_t rows, int64_t cols);
 int dsvgd_h2_colscale(const float* A, int64_t lda, int64_t rows, int64_t cols, float* ws,
                       float* scale, void* stream);
 /* dsvgd_h2_colscale's output over Y's first cols columns (cols = dp: the X
  * half; cols = ldy: all of Y), bit-identical, from dsvgd_pack_h2's maxima
- * (nb = dsvgd_pack_blocks(rows_pad)). */
+ * (nb = dsvgd_pack_blocks(rows_pad)); scale[2 cols + 2] = the RANGE GUARD:
+ * 1.0 when the X half (or, cols = ldy, the S half) has its largest magnitude
+ * more than 2^16 times its smallest nonzero row max, else 0.0. */
 int dsvgd_h2_scales(const uint32_t* partial, const uint32_t* gmax, int64_t nb, int64_t ldy,
                     int64_t cols, int64_t dp, float* scale, void* stream);
 /* fp16 images (dsvgd_h2_image_bytes(rows, cols) bytes, 16-byte aligned):
@@ -277,21 +308,31 @@ int dsvgd_h2_ysplit(const float* Y, int64_t ldy, int64_t rows, const float* cols
                     void* stream);
 int dsvgd_h2_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
                       int64_t kpad, const float* tscale, void* img, void* stream);
-/* dsvgd_sqdist_x3 on the FmtH2 engine: Yg = dsvgd_h2_rowsplit(Y, ldy,
- * n_pad, dp, n_pad + 256, dp, tscale) with tscale = &scale[2 dp] of a
- * dsvgd_h2_colscale over Y's first dp columns ([t, 1/t]); same outputs,
- * select modes and layouts. */
+/* the same image with one scale per row: rowscale[i] * A[row i] (rows < rows) */
+int dsvgd_h2_rowsplit_rows(const float* A, int64_t lda, int64_t rows, int64_t cols,
+                           int64_t rows_pad, int64_t kpad, const float* rowscale, void* img,
+                           void* stream);
+/* rowscale[i] = the FmtH2 power-of-two scale of row i of A (rows x cols) and
+ * rowinv[i] = 1 / rowscale[i] (nullable), for i < rows_pad (1 past rows) */
+int dsvgd_h2_rowscale(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                      float* rowscale, float* rowinv, void* stream);
+/* dsvgd_sqdist_x3 on the FmtH2 engine: Yg = dsvgd_h2_rowsplit_rows(Y, ldy,
+ * n_pad, dp, n_pad + 256, dp, rowscale) with the per-row scales of Y's X half
+ * (dsvgd_pack_h2's rowscale, or dsvgd_h2_rowscale; >= n_pad floats); same
+ * outputs, select modes and layouts. */
 int dsvgd_sqdist_h2(const void* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
                     int64_t d, float* D, int64_t ldd, int select_mode, dsvgd_select_state* st,
-                    float* cand, int layout, const float* tscale, void* stream);
+                    float* cand, int layout, const float* rowscale, void* stream);
 /* dsvgd_phi_mm_x3 on the FmtH2 engine: Yh = dsvgd_h2_ysplit(Y, ldy, n_pad,
  * scale) and colinv = &scale[ldy] of a dsvgd_h2_colscale over all ldy
  * columns of Y; same outputs (unscaled), split-K slices, diagonal rule and
  * symmetric layout (sym needs ldy % 256 == 0).  Requires n_pad * ldy * 4 <
- * 2^31. */
+ * 2^31.  gate (nullable, &scale[2 ldy + 2]): does nothing while it reads
+ * nonzero (the range guard hands the step to dsvgd_phi_mm_x3). */
 int dsvgd_phi_mm_h2(const float* D, int64_t ldd, const void* Yh, int64_t ldy, int64_t row0,
                     int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
-                    int64_t ldk, float* rowsum, int sym, const float* colinv, void* stream);
+                    int64_t ldk, float* rowsum, int sym, const float* colinv, const float* gate,
+                    void* stream);
 
 /* phi[i] = inv_n * (s_i + KS[i] + (2/h) (rowsum[i] xc[i] - KXc[i])) with the
  * split-K partials summed in slice order (s_i: the self term k_ii s_i), plus

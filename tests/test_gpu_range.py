@@ -48,42 +48,78 @@ def _outlier_case(n, d, kind, k, seed=0):
     X = (0.3 * rs.randn(n, d)).astype(np.float32)
     S = (-X / 0.09 + rs.randn(n, d)).astype(np.float32)
     j = 17
+    far = np.float32(2.0 ** k * 0.3)
     if kind in ("far", "far_score"):
-        X[j] = X[j] + np.float32(2.0 ** k * 0.3)          # no kernel weight to anyone
-    if kind in ("score", "far_score"):
+        X[j, 0] += far                                   # no kernel weight to anyone
+    if kind == "far_pair":                               # two of them, opposite sides
+        X[j, 0] += far
+        X[j + 1, 0] -= far
+    if kind in ("score", "far_score", "far_pair"):
         S[j] = S[j] * np.float32(2.0 ** k)
     return X, S
 
 
-def _phi(X, S, gemm):
+def _phi(X, S, **kw):
     n, d = X.shape
-    eng = dsvgd().PhiEngine(n, d, device=DEV, gemm=gemm)
+    eng = dsvgd().PhiEngine(n, d, device=DEV, **kw)
     Xo = gpu(X).clone()
     eng.step(gpu(X), gpu(S), X_own=Xo, step=0.0, h=None)
     torch.cuda.synchronize()
     return eng.phi.cpu().numpy(), eng.state.read()[1], eng
 
 
-CASES = [(kind, k) for kind in ("score", "far", "far_score") for k in (16, 20, 24, 30)]
+KINDS = ("score", "far", "far_score", "far_pair")
+CASES = [(kind, k) for kind in KINDS for k in (16, 20, 24, 30)]
 
 
 @pytest.mark.parametrize("n,d", [(2048, 64), (4096, 256)])
 @pytest.mark.parametrize("kind,k", CASES)
 def test_phi_row_normalised_with_outlier(n, d, kind, k):
+    """One particle (two for far_pair) 2^k away from the rest and / or with
+    scores 2^k larger: every row of phi within 1e-5 of fp64, row-normalised,
+    on the default engine (the f32 engine beside it for reference).  Far
+    particles exercise the robust centre (dsvgd_colcenter) and the per-row
+    scales of the Gram's row image; scores 2^k larger the phi_mm range guard."""
     X, S = _outlier_case(n, d, kind, k)
-    phi_h2, h, eng = _phi(X, S, "h2")
-    phi_f32, h32, _ = _phi(X, S, "f32")
+    phi_h2, h, eng = _phi(X, S)
+    phi_f32, h32, _ = _phi(X, S, gemm="f32")
     ref = O.phi(X, S, h)
     e_h2, e_f32 = row_err(phi_h2, ref), row_err(phi_f32, O.phi(X, S, h32))
-    record_parity(float(e_h2.max()), f32=float(e_f32.max()), kind=kind, k=k,
-                  guard=getattr(eng, "range_guard", lambda: None)())
+    guard = eng.range_guard()
+    record_parity(float(e_h2.max()), f32=float(e_f32.max()), kind=kind, k=k, guard=guard)
     assert e_h2.max() <= ROW_TOL, (e_h2.max(), int(e_h2.argmax()), e_f32.max())
+    assert e_f32.max() <= ROW_TOL, e_f32.max()
+    if k >= 20:      # rows spanning > 2^16 in a half of [Xc | S]: the step ran on FmtX3
+        assert guard is True
+    if kind == "far_pair":
+        assert h == pytest.approx(h32, rel=1e-5)
+
+
+@pytest.mark.parametrize("n,d", [(2048, 64), (4096, 256)])
+def test_guard_off_for_ordinary_particles(n, d):
+    """The guard stays off on the distributions the other tests use."""
+    rs = np.random.RandomState(n)
+    X = rs.randn(n, d).astype(np.float32)
+    S = (-X + 0.3 * rs.randn(n, d)).astype(np.float32)
+    _, _, eng = _phi(X, S)
+    assert eng.range_guard() is False
+
+
+def test_guard_path_is_the_x3_phi_mm():
+    """With the guard on, KY and the row sums are bit for bit those of the
+    FmtX3 phi_mm on the same D (gram_gemm h2 under both)."""
+    X, S = _outlier_case(4096, 256, "far_pair", 20)
+    _, _, eng = _phi(X, S)
+    _, _, eng3 = _phi(X, S, phi_gemm="x3", gram_gemm="h2")
+    assert eng.range_guard() is True and eng3.phi_gemm == "x3"
+    torch.testing.assert_close(eng.dense_D(), eng3.dense_D(), rtol=0, atol=0)
+    assert torch.equal(eng.KY, eng3.KY) and torch.equal(eng.rowsum, eng3.rowsum)
 
 
 @pytest.mark.parametrize("k", [18, 24, 30])
 def test_logreg_scores_row_normalised_with_outlier(k):
-    """One particle's w 2^k times the others' (logreg's W image shares one
-    tensor scale): every particle's score row vs fp64, row-normalised."""
+    """One particle's w 2^k times the others' (logreg's W image: one FmtH2
+    scale per particle row): every particle's score row vs fp64, row-normalised."""
     n, N, p = 1024, 4096, 255
     rs = np.random.RandomState(k)
     X = (0.1 * rs.randn(n, p + 1)).astype(np.float32)

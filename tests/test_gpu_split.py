@@ -65,7 +65,7 @@ def test_ysplit_reconstructs_fp32(rows, ldy):
     Y[0, :8] = 0.0
     lib = N.load()
     Yx = torch.empty(lib.dsvgd_ysplit_bytes(rows, ldy) // 2, dtype=torch.int16, device=DEV)
-    N.call("dsvgd_ysplit", N.ptr(gpu(Y)), ldy, rows, N.ptr(Yx), 1, N.stream(torch.device(DEV)))
+    N.call("dsvgd_ysplit", N.ptr(gpu(Y)), ldy, rows, N.ptr(Yx), 1, None, N.stream(torch.device(DEV)))
     torch.cuda.synchronize()
     parts = decode_ysplit(Yx, rows, ldy)
     rec = parts.sum(0)
@@ -93,7 +93,7 @@ def test_h2_images_reconstruct_fp32(rows, ldy):
     Y[:, 3] = 0.0                                   # all-zero column: scale 1
     Yg = gpu(Y)
     ws = torch.empty(lib.dsvgd_h2_colscale_workspace_floats(rows, ldy), device=DEV)
-    sc = torch.empty(2 * ldy + 2, device=DEV)
+    sc = torch.empty(2 * ldy + 3, device=DEV)
     N.call("dsvgd_h2_colscale", N.ptr(Yg), ldy, rows, ldy, N.ptr(ws), N.ptr(sc), s)
     img = torch.empty(lib.dsvgd_h2_image_bytes(rows, ldy) // 2, dtype=torch.int16, device=DEV)
     N.call("dsvgd_h2_ysplit", N.ptr(Yg), ldy, rows, N.ptr(sc), N.ptr(img), s)
@@ -106,6 +106,7 @@ def test_h2_images_reconstruct_fp32(rows, ldy):
     assert np.all((s_c * mx)[live] >= 2.0 ** 14) and np.all((s_c * mx)[live] < 2.0 ** 15)
     assert s_c[3] == 1.0 and np.all(scale[ldy:2 * ldy] * s_c == 1.0)
     assert scale[2 * ldy] == s_c[live].min() and scale[2 * ldy + 1] * scale[2 * ldy] == 1.0
+    assert scale[2 * ldy + 2] == 0.0      # no range guard on the colscale path
     parts = decode_h2(img, rows, ldy)
     rec = parts.sum(0) / s_c[None, :]
     Y64 = Y.astype(np.float64)
@@ -135,15 +136,27 @@ def test_h2_images_reconstruct_fp32(rows, ldy):
     assert float(sc[7]) == 1.0 and float(sc[2 * ldy]) == 1.0
 
 
+def _pow2_scale(m):
+    """numpy restatement of pow2_scale (csrc/common.hpp)."""
+    m = np.asarray(m, np.float64)
+    out = np.ones_like(m)
+    ok = (m > 0) & np.isfinite(m)
+    e = np.frexp(m[ok])[1]
+    out[ok] = np.ldexp(1.0, np.minimum(15 - e, 100))
+    return out
+
+
 @pytest.mark.parametrize("n,d,ldx,special", [(1000, 64, 64, None), (777, 100, 101, "zero"),
                                              (300, 3, 3, "inf"), (2100, 1024, 1024, "nan"),
-                                             (129, 250, 252, None)])
+                                             (129, 250, 252, None), (1000, 64, 64, "range")])
 def test_pack_maxima_match_colscale(n, d, ldx, special):
-    """dsvgd_pack_h2 (pack + the FmtH2 column maxima) then dsvgd_h2_scales:
+    """dsvgd_pack_h2 (pack + the FmtH2 statistics) then dsvgd_h2_scales:
     Y / norms as the numpy restatement of dsvgd_pack, scales bit-identical to
     dsvgd_h2_colscale's over the same Y -- after pack(X, S), and after pack(X)
     + pack(NULL, S) (the scores arriving after the distance stage); zero and
-    non-finite columns; unaligned row strides (element-load path)."""
+    non-finite columns; unaligned row strides (element-load path); the per-row
+    scales of the X half; the range guard word against its numpy restatement
+    (largest |entry| of a half > 2^16 x its smallest nonzero row max)."""
     from dsvgd import _native as N
     lib = N.load()
     s = N.stream(torch.device(DEV))
@@ -153,6 +166,10 @@ def test_pack_maxima_match_colscale(n, d, ldx, special):
     if special == "zero":
         X[:, 5] = 1.25                                # centred: an all-zero column
         S[:, 9] = 0.0
+    elif special == "range":                          # one particle's scores 2^20 x
+        X = (rs.randn(n, ldx)).astype(np.float32)
+        S = (rs.randn(n, ldx)).astype(np.float32)
+        S[11] *= np.float32(2.0 ** 20)
     elif special == "inf":
         S[7, 1] = np.inf
     elif special == "nan":
@@ -163,27 +180,27 @@ def test_pack_maxima_match_colscale(n, d, ldx, special):
     nb = lib.dsvgd_pack_blocks(rows)
     Xg, Sg = gpu(X)[:, :d], gpu(S)[:, :d]
     mean = torch.empty(d, device=DEV)
-    mws = torch.empty(lib.dsvgd_colmean_workspace_floats(n, d), device=DEV)
-    N.call("dsvgd_colmean", N.ptr(Xg), ldx, n, d, N.ptr(mws), N.ptr(mean), s)
+    N.call("dsvgd_colcenter", N.ptr(Xg), ldx, n, d, N.ptr(mean), s)
     ws = torch.empty(lib.dsvgd_h2_colscale_workspace_floats(n_pad, ldy), device=DEV)
     for split_scores in (False, True):
         Y = torch.full((rows, ldy), 7.0, device=DEV)  # every entry must be written
         norms = torch.empty(rows, device=DEV)
         part = torch.full((nb * ldy,), -1, dtype=torch.int32, device=DEV)
-        gmax = torch.full((2 * nb,), -1, dtype=torch.int32, device=DEV)
+        gmax = torch.full((4 * nb,), -1, dtype=torch.int32, device=DEV)
+        rsc = torch.full((rows,), -1.0, device=DEV)
         args = (N.ptr(mean), n, d, rows, N.ptr(Y), ldy)
         if split_scores:
             N.call("dsvgd_pack_h2", N.ptr(Xg), ldx, None, d, 1.0, *args, N.ptr(norms),
-                   N.ptr(part), N.ptr(gmax), s)
+                   N.ptr(part), N.ptr(gmax), N.ptr(rsc), s)
             N.call("dsvgd_pack_h2", None, d, N.ptr(Sg), ldx, 0.5, *args, None,
-                   N.ptr(part), N.ptr(gmax), s)
+                   N.ptr(part), N.ptr(gmax), None, s)
         else:
             N.call("dsvgd_pack_h2", N.ptr(Xg), ldx, N.ptr(Sg), ldx, 0.5, *args, N.ptr(norms),
-                   N.ptr(part), N.ptr(gmax), s)
+                   N.ptr(part), N.ptr(gmax), N.ptr(rsc), s)
         got = {}
         for cols in (dp, ldy):
-            ref = torch.empty(2 * cols + 2, device=DEV)
-            out = torch.empty(2 * cols + 2, device=DEV)
+            ref = torch.empty(2 * cols + 3, device=DEV)
+            out = torch.empty(2 * cols + 3, device=DEV)
             N.call("dsvgd_h2_colscale", N.ptr(Y), ldy, n_pad, cols, N.ptr(ws), N.ptr(ref), s)
             N.call("dsvgd_h2_scales", N.ptr(part), N.ptr(gmax), nb, ldy, cols, dp, N.ptr(out), s)
             got[cols] = (ref, out)
@@ -199,9 +216,26 @@ def test_pack_maxima_match_colscale(n, d, ldx, special):
         fin = np.isfinite(nr)
         np.testing.assert_allclose(got_n[fin], nr[fin], rtol=1e-5, atol=1e-30)
         assert np.all(got_n[rows - 128:] == 0.0)
+        Y64 = np.abs(Yc[:n].astype(np.float64))
+        with np.errstate(invalid="ignore"):
+            rx, rs_ = Y64[:, :dp].max(1), Y64[:, dp:].max(1)
+        np.testing.assert_array_equal(rsc.cpu().numpy()[:n], _pow2_scale(rx).astype(np.float32))
+        assert np.all(rsc.cpu().numpy()[n:] == 1.0)
+
+        def wide(r):
+            r = r[np.isfinite(r) | np.isnan(r)]
+            nz = r[r > 0]
+            return bool(nz.size and np.nanmax(r) > 2.0 ** 16 * nz.min())
         for cols, (ref, out) in got.items():
-            np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32),
-                                          ref.cpu().numpy().view(np.uint32))
+            o = out.cpu().numpy()
+            np.testing.assert_array_equal(o[:2 * cols + 2].view(np.uint32),
+                                          ref.cpu().numpy()[:2 * cols + 2].view(np.uint32))
+            if special in ("inf", "nan"):
+                continue
+            expect = wide(rx) or (cols > dp and wide(rs_))
+            assert o[2 * cols + 2] == (1.0 if expect else 0.0), (cols, o[2 * cols + 2])
+            if special == "range":
+                assert o[2 * cols + 2] == (1.0 if cols > dp else 0.0)
 
 
 def _engines(X, S, h, split, m=None, row0=0):

@@ -35,7 +35,7 @@ def test_meta_calls_without_gpu():
     from dsvgd import _native
     from dsvgd.engine import _SelectState
     lib = _native.load()
-    assert lib.dsvgd_abi_version() == 2
+    assert lib.dsvgd_abi_version() == 3
     assert lib.dsvgd_select_state_bytes() == ctypes.sizeof(_SelectState)
     assert lib.dsvgd_pad128(1) == 128 and lib.dsvgd_pad128(129) == 256
     assert lib.dsvgd_dp(1) == 32 and lib.dsvgd_dp(256) == 256 and lib.dsvgd_dp(255) == 256
