@@ -19,11 +19,10 @@
 namespace dsvgd {
 
 // phi_mm on the FmtH2 engine (TN = 4): phi_w1_kernel (one wave per SIMD, B
-// fragments straight from the image; phi_w1.hpp) on the full D layout (row
-// blocks, S > 1); on the symmetric layout the hybrid -- NNX3Tile for each row
-// block's transposed K-steps, phi_w1 for the rest, two launches with half the
-// split-K slices each (phi_w1 alone, or a 3:1 / 1:3 slice split,
-// measured slower there).
+// fragments straight from the image; phi_w1.hpp) -- on the full D layout (row
+// blocks, S > 1) one launch; on the symmetric layout two, each row block
+// split at its diagonal tile into the transposed K-steps (DS 1) and the plain
+// ones (DS 2), with half the split-K slices each.
 
 // blockIdx.z = split-K slice z: K columns [z*kchunk, min(K,(z+1)*kchunk)) into
 // the partial C + z*m*ldc (and rowsum + z*m_pad); phi_finish sums the slices
@@ -244,14 +243,14 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
   } else {  // FmtH2: the smaller stages fit a 3-stage ring
     if (TN == 4 && EXP && sym && splits >= 2) {
       // symmetric layout split at each row block's diagonal tile: the
-      // transposed K-steps on NNX3Tile (its LDS-rotated reads), the plain
-      // ones on phi_w1; half the split-K slices each
+      // transposed K-steps (phi_w1 DS 1: the stored tiles transposed through
+      // a per-wave LDS scratch) and the plain ones (DS 2); half the split-K
+      // slices each
       const int sl = splits / 2;
       const dim3 g1(grid.x, grid.y, sl), g2(grid.x, grid.y, splits - sl);
-      hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2>), g1,
-                         dim3(512), 0, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0,
-                         sym, colinv, 1, 0, gate, gate_on);
-      const int rc = check_launch("nn_x3_kernel(lower)");
+      hipLaunchKernelGGL(phi_w1_kernel<1>, g1, dim3(PhiW1::kThreads), 0, s, D, K, Yx, ldy, K,
+                         kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0, gate, gate_on);
+      const int rc = check_launch("phi_w1_kernel(lower)");
       if (rc) return rc;
       hipLaunchKernelGGL(phi_w1_kernel<2>, g2, dim3(PhiW1::kThreads), 0, s, D, K, Yx, ldy, K,
                          kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, sl, gate, gate_on);

@@ -6,7 +6,7 @@
 //   * B (the Yx image) never goes through LDS: a wave's 128 columns are its
 //     own, so each lane loads its MFMA B fragments straight from the image
 //     (buffer_load_dwordx4, one K-step ahead, double-buffered in VGPRs);
-//   * the D panel is loaded by the thread that stages it (two dwordx4, two
+//   * the D panel is loaded by the thread that stages it (two dwordx4, three
 //     K-steps ahead) -- no LDS-DMA anywhere, so every wait is the compiler's
 //     own counted vmcnt;
 //   * LDS holds only the staged A image (2 stages x 8 KiB); each wave reads
@@ -15,8 +15,13 @@
 //   * each K-step is one basic block (branch-free staging: clamped loads past
 //     the range, masked row sums, the diagonal by compare/select), so the
 //     scheduler can interleave the staging VALU with the 48 MFMAs.
-// Both D layouts: the symmetric one's transposed K-steps are read as 8
-// dword loads per thread (column srow of the stored tile's 16 rows).
+// Symmetric D layout: the K-steps left of a row block's diagonal tile exist
+// only as the stored tiles (J, I), J < I -- transposed.  DS = 1 walks those:
+// each lane loads 32 contiguous bytes of the stored tile (8 consecutive rows
+// i of one column j: the same two dwordx4 as a plain K-step), the wave
+// transposes its 32 x 16 share through a private 2.75 KiB LDS scratch (two
+// ds_write_b128 and eight ds_read_b32 per lane, conflict-free layout) one
+// K-step before staging it, and stages exactly as a plain K-step.
 #pragma once
 #include "gemm_x3.hpp"
 
@@ -27,6 +32,11 @@ struct PhiW1 {
   static constexpr int BM = 128, BC = 512, BJ = 16, P = 2;
   static constexpr int SA = P * BM * 32;  // one stage's A image (8 KiB)
   static constexpr int kSmemBytes = 2 * SA;
+  // DS = 1: per-wave transpose scratch, [16 j][kScrLd floats] for the wave's
+  // 32 rows; kScrLd = 44: the 16-byte writes of 8 lanes and the dword reads
+  // of 64 lanes each hit 64 distinct banks
+  static constexpr int kScrLd = 44;
+  static constexpr int kScrBytes = 16 * kScrLd * 4;
 };
 
 // VALU instructions placed after each of a K-step's first 16 MFMAs (the
@@ -41,8 +51,10 @@ __device__ __forceinline__ f32x4 w1_load_nt(__amdgpu_buffer_rsrc_t r, int voff, 
 
 // A: panel row of the block (panel layout, 128 x 16 fp32 panels); Yx: FmtH2
 // image [kstep][part][column][16 k]; K range [kchunk z, +kchunk) of K.
-// DS (compile-time dsplit): 0 = the K range [kchunk z, +kchunk); 2 = the
-// plain K-steps of a symmetric-layout row block (the hybrid's upper part)
+// DS (compile-time dsplit): 0 = the K range [kchunk z, +kchunk) (full D
+// layout); on the symmetric layout (m == n, row0 == 0) 1 = the transposed
+// K-steps left of a row block's diagonal tile, 2 = the plain ones from it on
+// (the hybrid's two launches; slices land in slice0 + z)
 template <int DS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void phi_w1_kernel(
     const float* A, int64_t a_npad, const _Float16* Yx, int64_t ldy,
@@ -50,34 +62,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     int64_t ldc, float* __restrict__ rowsum, int64_t m, int64_t row0, int sym,
     const float* __restrict__ colinv, int slice0, const float* __restrict__ gate, int gate_on) {
   if (gate && ((*gate != 0.f) != (gate_on != 0))) return;  // the FmtH2 range guard (nn_x3_kernel)
-  constexpr int dsplit = DS;
   using F = FmtH2;
   using V8 = F::V8;
   constexpr int P = PhiW1::P;
-  __shared__ __attribute__((aligned(16))) char smem[PhiW1::kSmemBytes];
+  constexpr bool TR = DS == 1;
+  __shared__ __attribute__((aligned(16))) char smem[PhiW1::kSmemBytes + (TR ? 4 * PhiW1::kScrBytes : 0)];
   const int t = threadIdx.x, lane = t & 63, r = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  // dsplit == 2: a row block's slices dispatched back to back, longest first
+  // DS 1 / 2: a row block's slices dispatched back to back, longest first
+  // (the transposed part grows with the row, the plain part shrinks)
   const int64_t lin = (int64_t)blockIdx.z * gridDim.y + blockIdx.y;
-  const int64_t by = dsplit == 2 ? lin / gridDim.z : blockIdx.y;
-  const int64_t bz = dsplit == 2 ? lin % gridDim.z : blockIdx.z;
+  const int64_t by = DS == 2 ? lin / gridDim.z
+                   : DS == 1 ? (int64_t)gridDim.y - 1 - lin / gridDim.z : blockIdx.y;
+  const int64_t bz = DS != 0 ? lin % gridDim.z : blockIdx.z;
   const int64_t i0 = by * PhiW1::BM;
   const int64_t c0 = (int64_t)blockIdx.x * PhiW1::BC + w * 128;
-  // dsplit == 2 (symmetric layout): only the K-steps from the block's
-  // diagonal tile on (the plain ones; NNX3Tile takes the transposed ones),
-  // split over the z slices, which land in slices slice0 + z
-  // K-step k of this block is global K-step ks0 + kdir * k.  dsplit == 2
-  // walks its range top-down, slice z taking every Z-th K-step: the blocks
-  // running together then read the same Yx K-steps at the same time (L2
-  // reuse), whatever row they start from
+  // K-step k of this block is global K-step ks0 + kdir * k.  The symmetric
+  // forms interleave the slices, slice z taking every Z-th K-step of its
+  // range (DS 2 top-down from K, DS 1 up from 0): the blocks running together
+  // then read the same Yx K-steps at the same time (L2 reuse), whatever row
+  // they start from
   const int64_t kb0 = bz * kchunk, kend = min(K, kb0 + kchunk);
   int ks0 = (int)(kb0 / PhiW1::BJ);
   int nsteps = kend > kb0 ? (int)((kend - kb0) / PhiW1::BJ) : 0;
   const int Z = (int)gridDim.z;
-  const int kdir = DS == 2 ? -Z : 1;
+  const int kdir = DS == 2 ? -Z : DS == 1 ? Z : 1;
   if (DS == 2) {
     const int T = (int)((K - i0) / PhiW1::BJ);
     ks0 = (int)(K / PhiW1::BJ) - 1 - (int)bz;
+    nsteps = T > bz ? (T - (int)bz + Z - 1) / Z : 0;
+  } else if (DS == 1) {
+    const int T = (int)(i0 / PhiW1::BJ);
+    ks0 = (int)bz;
     nsteps = T > bz ? (T - (int)bz + Z - 1) / Z : 0;
   }
   C += (int64_t)(slice0 + bz) * m * ldc;
@@ -96,7 +112,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int srow = t >> 1, shalf = t & 1;
   const int aoff = x3_off(srow, shalf);       // this thread's 16 B of a part image row
   // diagonal: global row - the thread's first column at K-step 0, clamped to
-  // int range (only |.| < 16 matters)
+  // int range (only |.| < 16 matters; DS 1 never meets it)
   const int64_t dg = row0 + i0 + srow - 8 * shalf - (int64_t)ks0 * PhiW1::BJ;
   const int qd0 = (int)max(min(dg, (int64_t)(1 << 30)), (int64_t)-(1 << 30));
 
@@ -110,17 +126,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   float rs = 0.f;
 
   // symmetric layout (m == n, row0 == 0): K-steps left of the block's
-  // diagonal tile read the stored tile (J, I) transposed
+  // diagonal tile (DS 1) read the stored tile (J, I) transposed
   const int symI = sym ? (int)(i0 >> 7) : -1;
   const int64_t pcols = a_npad >> 4;
-  // transposed: row srow's value q of a K-step sits in the panel of column
-  // block I*8 + (srow >> 4), row (j0 & 127) + 8 shalf + q, column srow & 15
-  const int vT = ((srow >> 4) * kPanelElems + 8 * shalf * 16 + (srow & 15)) * 4;
+  // DS 1: lane (piece p = t >> 5, s = t & 31) loads rows i0 + 16 p + 8 (s & 1)
+  // .. +7 of column j0 + (s >> 1): 32 contiguous bytes of panel I*8 + p
+  const int vP = (t >> 5) * kPanelElems * 4 + (t & 31) * 32;
+  // DS 1 scratch of this wave: element (i' = row - 32 w, j) at j * kScrLd + i'
+  float* const scr = reinterpret_cast<float*>(smem + PhiW1::kSmemBytes + w * PhiW1::kScrBytes);
+  const int sw_off = ((lane & 31) >> 1) * PhiW1::kScrLd + 16 * (lane >> 5) + 8 * (lane & 1);
+  const int sr_off = 8 * shalf * PhiW1::kScrLd + (lane >> 1);
 
   if (nsteps > 0) {
     V8 b[4][P];       // B fragments of the current K-step; column tile ni is
                       // reloaded for the next K-step right after its last MFMA
     f32x4 dr[4][2];   // D values: K-step k in dr[k & 3], loaded 3 K-steps ahead
+    f32x4 tr[2];      // DS 1: K-step k+1's values, transposed during K-step k - 1
     const int last = nsteps - 1;
     auto loadB = [&](int ni, int k) {
       const int soff = (ks0 + kdir * min(k, last)) * P * pstride;
@@ -131,19 +152,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     auto loadD = [&](f32x4 (&d)[2], int k) {
       const int kc = min(k, last);
       const int64_t j0 = (int64_t)(ks0 + kdir * kc) * PhiW1::BJ;
-      if ((int)(j0 >> 7) < symI) {  // wave-uniform
+      if constexpr (TR) {
         const float* src = A + (((j0 >> 7) * pcols + symI * 8) * kPanelElems + (j0 & 127) * 16);
         const __amdgpu_buffer_rsrc_t rT =
             __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, 0x7fffffff, 0x00020000);
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-          d[q >> 2][q & 3] = __builtin_bit_cast(
-              float, __builtin_amdgcn_raw_buffer_load_b32(rT, vT + q * 64, 0, 2));
-      } else {
+        d[0] = w1_load_nt(rT, vP, 0);
+        d[1] = w1_load_nt(rT, vP + 16, 0);
+      } else {  // DS 0 (full layout) and DS 2 (from the diagonal tile on): plain
         const int soff = (int)(j0 >> 4) * kPanelElems * 4;
         d[0] = w1_load_nt(rD, vD, soff);
         d[1] = w1_load_nt(rD, vD + 16, soff);
       }
+    };
+    // DS 1: the wave's 32 rows x 16 columns of one K-step, from the load
+    // layout (lane: 8 rows of one column) to the staging one (lane: 8
+    // columns of one row), through the wave's scratch (in-order LDS: no
+    // barrier, and the next transpose's writes follow this one's reads)
+    auto transpose = [&](const f32x4 (&d)[2], f32x4 (&o)[2]) {
+      *reinterpret_cast<f32x4*>(scr + sw_off) = d[0];
+      *reinterpret_cast<f32x4*>(scr + sw_off + 4) = d[1];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q >> 2][q & 3] = scr[sr_off + q * PhiW1::kScrLd];
     };
     // exp2 / diagonal / row sum / 2-part split of K-step k's 8 values -> stage
     auto stage = [&](char* st_, const f32x4 (&d)[2], int k) {
@@ -154,7 +183,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int q = 0; q < 8; ++q) {
         const float v = q < 4 ? d[0][q] : d[1][q - 4];
         const float x = __builtin_amdgcn_exp2f(fmaf(v, scale, F::kAScaleLog2));
-        e[q] = qd == q ? 0.f : x;
+        e[q] = (!TR && qd == q) ? 0.f : x;
       }
       const float s = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
       rs += k <= last ? s : 0.f;
@@ -171,14 +200,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     auto barrier = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
     // K-step k (slot KS = k & 3) from stage cur: A(k+1) -> stage nxt; MFMAs
     // column tile by column tile, each tile's B reloaded for k+1; then D(k+3)
-    auto step = [&](int k, const char* cur, char* nxt, const f32x4 (&ds_)[2], f32x4 (&dl)[2]) {
+    // (DS 1: stages tr = K-step k+1, and transposes dt = D(k+2) into tr)
+    auto step = [&](int k, const char* cur, char* nxt, const f32x4 (&ds_)[2], f32x4 (&dl)[2],
+                    const f32x4 (&dt)[2]) {
       V8 a[4][P];
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int p = 0; p < P; ++p)
           a[mi][p] = *reinterpret_cast<const V8*>(cur + p * PhiW1::BM * 32 + x3_off(mi * 32 + r, h));
-      stage(nxt, ds_, k + 1);
+      if constexpr (TR)
+        stage(nxt, tr, k + 1);
+      else
+        stage(nxt, ds_, k + 1);
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
         // small terms first, as mfma_products
@@ -190,10 +224,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int mi = 0; mi < 4; ++mi) acc[mi][ni] = mfma_fmt<F>(a[mi][0], b[ni][0], acc[mi][ni]);
         loadB(ni, k + 1);
       }
+      if constexpr (TR) transpose(dt, tr);
       // one wave per SIMD: nothing else hides the staging VALU, so spread it
       // between the MFMAs (cdna_hip_programming.md T19): the A fragment reads,
       // then 16 MFMAs each followed by up to kW1Sgb VALU (the staging of
       // A(k+1)), its two LDS stores, then the other 32 MFMAs with the 8 B loads
+      // (DS 1: and the transpose of K-step k+2 -- two stores, eight reads --
+      // early among them, so its reads land before the closing barrier)
       __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -204,45 +241,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int i = 0; i < 32; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (TR && i == 1) __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
+        if (TR && i >= 2 && i < 10) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         if (i % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
       }
       loadD(dl, k + 3);
     };
 
-    // prologue: B(0), D(0..2); A(0) -> stage 0
+    // prologue: B(0), D(0..2); A(0) -> stage 0 (DS 1: D(0), D(1) transposed)
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) loadB(ni, 0);
     loadD(dr[0], 0);
     loadD(dr[1], 1);
     loadD(dr[2], 2);
-    stage(smem, dr[0], 0);
+    if constexpr (TR) {
+      transpose(dr[0], tr);
+      stage(smem, tr, 0);
+      transpose(dr[1], tr);
+    } else {
+      stage(smem, dr[0], 0);
+    }
     barrier();
     // unrolled by 8 (the D ring's slots are compile-time); the compiler's
     // wait counts are exact inside the body, conservative at the loop head
     // (unroll 4 -> 8: h2:full phi_mm 11.25 -> 11.05 ms, profiles/r6g)
     for (int k = 0; k < nsteps; k += 8) {
-      step(k, smem, smem + PhiW1::SA, dr[1], dr[3]);
+      step(k, smem, smem + PhiW1::SA, dr[1], dr[3], dr[2]);
       barrier();
       if (k + 1 >= nsteps) break;
-      step(k + 1, smem + PhiW1::SA, smem, dr[2], dr[0]);
+      step(k + 1, smem + PhiW1::SA, smem, dr[2], dr[0], dr[3]);
       barrier();
       if (k + 2 >= nsteps) break;
-      step(k + 2, smem, smem + PhiW1::SA, dr[3], dr[1]);
+      step(k + 2, smem, smem + PhiW1::SA, dr[3], dr[1], dr[0]);
       barrier();
       if (k + 3 >= nsteps) break;
-      step(k + 3, smem + PhiW1::SA, smem, dr[0], dr[2]);
+      step(k + 3, smem + PhiW1::SA, smem, dr[0], dr[2], dr[1]);
       barrier();
       if (k + 4 >= nsteps) break;
-      step(k + 4, smem, smem + PhiW1::SA, dr[1], dr[3]);
+      step(k + 4, smem, smem + PhiW1::SA, dr[1], dr[3], dr[2]);
       barrier();
       if (k + 5 >= nsteps) break;
-      step(k + 5, smem + PhiW1::SA, smem, dr[2], dr[0]);
+      step(k + 5, smem + PhiW1::SA, smem, dr[2], dr[0], dr[3]);
       barrier();
       if (k + 6 >= nsteps) break;
-      step(k + 6, smem, smem + PhiW1::SA, dr[3], dr[1]);
+      step(k + 6, smem, smem + PhiW1::SA, dr[3], dr[1], dr[0]);
       barrier();
       if (k + 7 >= nsteps) break;
-      step(k + 7, smem + PhiW1::SA, smem, dr[0], dr[2]);
+      step(k + 7, smem + PhiW1::SA, smem, dr[0], dr[2], dr[1]);
       barrier();
     }
   }

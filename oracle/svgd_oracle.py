@@ -77,15 +77,20 @@ def _sigmoid(u):
 GRAM_MIN_WORK = 1 << 31
 
 
-def sqdist(Xr, X):
+def sqdist(Xr, X, self_cols=None):
     """||x_i - x_j||^2 from explicit differences (as torch.dist**2 per pair),
     chunked over rows to bound memory.  Large problems (rows * n * d >=
     GRAM_MIN_WORK, e.g. 256 sampled rows of config E: 65536 x 1024) take the
-    fp64 Gram form of sqdist_gram instead, which a CPU test pins to this one."""
+    fp64 Gram form of sqdist_gram instead, which a CPU test pins to this one.
+    self_cols[k]: the column of X that row k of Xr is (its distance is exactly
+    0; the Gram form would leave fp64 rounding of |x|^2 there)."""
     Xr = np.asarray(Xr, np.float64)
     X = np.asarray(X, np.float64)
     if Xr.shape[0] * X.size >= GRAM_MIN_WORK:
-        return sqdist_gram(Xr, X)
+        out = sqdist_gram(Xr, X)
+        if self_cols is not None:
+            out[np.arange(Xr.shape[0]), np.asarray(self_cols)] = 0.0
+        return out
     out = np.empty((Xr.shape[0], X.shape[0]))
     step = max(1, (1 << 24) // max(1, X.size))
     for s in range(0, Xr.shape[0], step):
@@ -94,11 +99,12 @@ def sqdist(Xr, X):
 
 
 def sqdist_gram(Xr, X):
-    """fp64 ||a||^2 + ||b||^2 - 2 a.b about the column mean of X (translation
-    invariant), clamped at 0; fp64 keeps the
-    cancellation error ~1e-16 |x|^2, far below the 1e-5 fp32 tolerances."""
+    """fp64 ||a||^2 + ||b||^2 - 2 a.b about the coordinate-wise median of X
+    (translation invariant; unlike the mean it stays inside the bulk when
+    one particle is far away), clamped at 0; fp64 keeps the cancellation
+    error ~1e-16 |x|^2, far below the 1e-5 fp32 tolerances."""
     X = np.asarray(X, np.float64)
-    mu = X.mean(0)
+    mu = np.median(X, 0)
     A = np.asarray(Xr, np.float64) - mu
     B = X - mu
     out = (A * A).sum(1)[:, None] + (B * B).sum(1)[None, :] - 2.0 * (A @ B.T)
@@ -118,7 +124,7 @@ def median_bandwidth(X):
     h = 1 when n <= 1 or the median is 0 (all particles coincide)."""
     X = np.asarray(X, np.float64)
     n = X.shape[0]
-    med = float(lower_median(sqdist(X, X)))
+    med = float(lower_median(sqdist(X, X, self_cols=np.arange(n))))
     if n <= 1 or med <= 0.0:
         return 1.0, med
     return med / math.log(n), med
@@ -130,7 +136,8 @@ def phi(X, S, h, rows=None):
     X = np.asarray(X, np.float64)
     S = np.asarray(S, np.float64)
     Xr = X if rows is None else X[rows]
-    K = np.exp(-sqdist(Xr, X) / h)             # K[i, j] = k(x_j, x_i)
+    self_cols = np.arange(X.shape[0]) if rows is None else np.asarray(rows).reshape(-1)
+    K = np.exp(-sqdist(Xr, X, self_cols) / h)  # K[i, j] = k(x_j, x_i)
     n = X.shape[0]
     rep = (2.0 / h) * (K.sum(1)[:, None] * Xr - K @ X)
     return (K @ S + rep) / n
