@@ -76,6 +76,11 @@ SIGNATURES = {
     "dsvgd_phi_row_blocks": (_i64, [_i64, _i64]),
     "dsvgd_phi_row_split": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _f, _p, _p, _p, _i64,
                                    _p]),
+    "dsvgd_gs_block_rows": (_i64, []),
+    "dsvgd_gs_splits": (_i64, [_i64]),
+    "dsvgd_gs_block_part": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _p, _i64, _p]),
+    "dsvgd_gs_block_sweep": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _f, _p, _i64,
+                                    _p, _i64, _p, _i64, _int, _p, _p, _f, _p]),
     "dsvgd_w2_cost": (_int, [_p, _i64, _i64, _p, _i64, _i64, _i64, _p, _i64, _p]),
     "dsvgd_w2_workspace_bytes": (_c.c_size_t, [_i64, _i64]),
     "dsvgd_w2_assign": (_int, [_p, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p]),

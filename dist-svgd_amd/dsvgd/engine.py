@@ -558,18 +558,47 @@ class StepGraph(object):
 _ROW_PARTIALS = {}   # (device, blocks, d) -> partial sums of dsvgd_phi_row_split (kept: graphs)
 
 
+_GS_PARTIALS = {}    # (device, nsplit, d) -> split-J partials of dsvgd_gs_block_part (kept: graphs)
+GS_BLOCK_MIN_ROWS = 128   # shorter sweeps keep the per-row kernels
+
+
+def _gs_score_kind(target):
+    """The blocked sweep refreshes the scores of elementwise targets itself:
+    dsvgd_gs_block_sweep's score_kind, or None (per-row path)."""
+    from .targets import Gaussian, GaussianMixture1D
+    if target is None:
+        return 0
+    if isinstance(target, Gaussian):
+        return 1
+    if isinstance(target, GaussianMixture1D):
+        return 2
+    return None
+
+
 def sequential_sweep(X, S, rows, h_state, step, target=None, score_scale=1.0, phi_out=None,
-                     extra=None):
+                     extra=None, blocked=True):
     """Gauss-Seidel sweep in the reference order over `rows` of the interacting
     set X (n, d): for each i, phi_i from the CURRENT X (earlier rows already
     moved), X[i] += step * (phi_i + extra[k]), then (if `target`) S[i] is
     recomputed for the moved particle, which is what re-running _dlogp per
     pair amounts to (dsvgd/sampler.py:64-68, dsvgd/distsampler.py:194-200).
-    extra: optional (len(rows), d) contiguous rows (the h * W2 gradient)."""
+    extra: optional (len(rows), d) contiguous rows (the h * W2 gradient).
+
+    Blocked form (d <= 64, contiguous rows, frozen scores or an elementwise
+    target): 64 rows at a time, one wide pass for the block against all n
+    rows and one workgroup for the in-block order (csrc/gs.hip) -- the same
+    sweep; otherwise one row kernel (+ one score refresh) per row."""
     n, d = X.shape
     s = N.stream(X.device)
     if extra is not None:
         assert extra.is_contiguous() and extra.shape == (len(rows), d)
+    kind = _gs_score_kind(target)
+    rows = range(rows.start, rows.stop) if isinstance(rows, range) else rows
+    contiguous = isinstance(rows, range) and rows.step == 1
+    if (blocked and kind is not None and d <= 64 and contiguous and len(rows) >= GS_BLOCK_MIN_ROWS
+            and X.is_contiguous() and S.is_contiguous()):
+        _blocked_sweep(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s)
+        return
     blocks = int(N.load().dsvgd_phi_row_blocks(n, d))
     part = None
     if blocks > 1:
@@ -590,3 +619,29 @@ def sequential_sweep(X, S, rows, h_state, step, target=None, score_scale=1.0, ph
                    h_state.ptr, float(step), ex, po, N.ptr(part), blocks, s)
         if target is not None:
             target.score(X[i:i + 1], S[i:i + 1], score_scale)
+
+
+def _blocked_sweep(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s):
+    n, d = X.shape
+    lib = N.load()
+    B = int(lib.dsvgd_gs_block_rows())
+    nsplit = int(lib.dsvgd_gs_splits(n))
+    key = (X.device, nsplit, d)
+    part = _GS_PARTIALS.get(key)
+    if part is None:
+        part = _GS_PARTIALS[key] = torch.empty(nsplit * B * d, dtype=torch.float32,
+                                               device=X.device)
+    sk, mu, lam = kind, None, None
+    if sk == 1:   # the Gaussian target's parameters on this device
+        mu, lam = target._params(X.device)
+    for b0 in range(rows.start, rows.stop, B):
+        nb = min(B, rows.stop - b0)
+        k0 = b0 - rows.start
+        N.call("dsvgd_gs_block_part", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), n, d, b0, nb,
+               h_state.ptr, N.ptr(part), nsplit, s)
+        ex = N.ptr(extra[k0:k0 + nb]) if extra is not None else None
+        po = N.ptr(phi_out[k0:k0 + nb]) if phi_out is not None else None
+        N.call("dsvgd_gs_block_sweep", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), n, d, b0, nb,
+               h_state.ptr, float(step), N.ptr(part), nsplit, ex, d, po,
+               N.ld(phi_out) if phi_out is not None else d, sk, N.ptr(mu), N.ptr(lam),
+               float(score_scale), s)

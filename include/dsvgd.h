@@ -377,6 +377,29 @@ int dsvgd_phi_row_split(float* X, int64_t ldx, const float* S, int64_t lds, int6
                         int64_t i, const dsvgd_select_state* st, float step, const float* extra,
                         float* phi_out, float* partial, int64_t blocks, void* stream);
 
+/* Blocked Gauss-Seidel sweep (the same reference order, d <= 64): rows
+ * [r0, r0 + B), B <= dsvgd_gs_block_rows() = 64, of the interacting set X
+ * (n x d).  gs_block_part: partial[z][i][c] = raw sums over the j slice z
+ * (nsplit = dsvgd_gs_splits(n) slices; nsplit x B x d floats) of
+ * k(x_i, x_j) (s_j + (2/h)(x_i - x_j)) against ALL n rows as the block
+ * starts; gs_block_sweep then walks the block in order in one workgroup:
+ * phi_i = (sum of the partials + the corrections for the block rows already
+ * moved) / n [+ extra row i], X[r0+i] += step phi_i, and the moved
+ * particle's score refreshed in S (score_kind 1: scale * (-lam (x - mu)),
+ * 2: the experiments/gmm.py mixture per coordinate; 0: S left as is --
+ * exchanged scores are frozen for the step, distsampler.py:194-200).  Two
+ * launches per 64 rows instead of two per row (dsvgd_phi_row_split). */
+int64_t dsvgd_gs_block_rows(void);
+int64_t dsvgd_gs_splits(int64_t n);
+int dsvgd_gs_block_part(const float* X, int64_t ldx, const float* S, int64_t lds, int64_t n,
+                        int64_t d, int64_t r0, int64_t B, const dsvgd_select_state* st,
+                        float* partial, int64_t nsplit, void* stream);
+int dsvgd_gs_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, int64_t n, int64_t d,
+                         int64_t r0, int64_t B, const dsvgd_select_state* st, float step,
+                         const float* partial, int64_t nsplit, const float* extra, int64_t lde,
+                         float* phi_out, int64_t ldphi, int score_kind, const float* mu,
+                         const float* lam, float score_scale, void* stream);
+
 /* ---- W2 / JKO term (dsvgd/distsampler.py:103-129, used at :190-198) ---- */
 /* The reference LP  min <P,C>, P >= 0, row sums 1/m, column sums 1/n  over
  * C_ij = ||x_i - y_j||^2 (x: m owned particles, y: n previous particles) has

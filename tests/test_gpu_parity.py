@@ -422,6 +422,71 @@ def test_phi_row_split_matches_oracle(n, d, ldx):
     assert np.abs(one[rows] - got[rows]).max() <= 1e-5 * np.abs(got[rows]).max()
 
 
+@pytest.mark.parametrize("n,d,lo,hi,kind", [(300, 3, 0, 300, "gauss"), (2000, 64, 37, 300, "none"),
+                                             (1000, 1, 100, 331, "gmm"), (700, 33, 0, 700, "gauss")])
+def test_blocked_sweep_matches_oracle(n, d, lo, hi, kind):
+    """The blocked Gauss-Seidel sweep (csrc/gs.hip: 64-row blocks, a wide pass
+    against all n rows + one workgroup for the in-block order) against the
+    fp64 sequential restatement -- blocks cut anywhere in the range, scores
+    frozen or refreshed after every move (Gaussian, GMM), W2-style extra rows
+    and phi_out -- and against the per-row path."""
+    from dsvgd import _native as N
+    from dsvgd.engine import SelectState, sequential_sweep
+    m = dsvgd()
+    rs = np.random.RandomState(n + d)
+    X0 = (0.7 * rs.randn(n, d)).astype(np.float32)
+    mu = rs.randn(d).astype(np.float32)
+    lam = rs.uniform(0.5, 2.0, d).astype(np.float32)
+    tgt = {"gauss": m.targets.Gaussian(mu, lam), "gmm": m.targets.GaussianMixture1D(),
+           "none": None}[kind]
+    fn = {"gauss": lambda X: O.score_gaussian(X, mu, lam), "gmm": O.score_gmm,
+          "none": None}[kind]
+    S0 = (fn(X0) if fn else rs.randn(n, d)).astype(np.float32)
+    h, step = 0.9 * d + 0.5, 0.05
+    rows = range(lo, hi)
+    extra = (0.01 * rs.randn(hi - lo, d)).astype(np.float32)
+    st = SelectState(DEV)
+    N.call("dsvgd_set_bandwidth", st.ptr, h, N.stream(DEV))
+    out = {}
+    for blocked in (True, False):
+        Xg, Sg = gpu(X0), gpu(S0)
+        phi = torch.zeros(hi - lo, d, device=DEV)
+        sequential_sweep(Xg, Sg, rows, st, step, target=tgt, phi_out=phi, extra=gpu(extra),
+                         blocked=blocked)
+        out[blocked] = (Xg.cpu().numpy().astype(np.float64), Sg.cpu().numpy(), phi.cpu().numpy())
+    ref = X0.astype(np.float64)
+    S = S0.astype(np.float64)
+    ref_phi = np.zeros((hi - lo, d))
+    for k, i in enumerate(rows):
+        ref_phi[k] = O.phi(ref, S, h, rows=[i])[0] + extra[k]
+        ref[i] += step * ref_phi[k]
+        if fn:
+            S[i] = fn(ref[i:i + 1])[0]
+    got, gs, gphi = out[True]
+    assert np.array_equal(got[:lo], X0[:lo]) and np.array_equal(got[hi:], X0[hi:])
+    e = rel_err(gphi, ref_phi)
+    assert e < PHI_TOL, e
+    assert abs_err(got, ref) < TRAJ_TOL
+    if fn:
+        assert np.abs(gs[rows.start:rows.stop] - S[rows.start:rows.stop]).max() <= \
+            1e-5 * np.abs(S).max()
+    # the per-row kernels on the same sweep (different summation order only)
+    assert np.abs(out[False][0] - got).max() <= 1e-5 * max(1.0, np.abs(got).max())
+
+
+def test_sampler_blocked_sweep_matches_reference(golden, monkeypatch):
+    """The reference's own Sampler trajectories (GMM n = 50, Gauss-Seidel) run
+    through the blocked sweep (its row threshold lowered to 1)."""
+    import dsvgd.engine as E
+    monkeypatch.setattr(E, "GS_BLOCK_MIN_ROWS", 1)
+    g = golden("g2_sample_gmm_n50")
+    torch.manual_seed(int(g["seed"]))
+    s = dsvgd().Sampler(1, dsvgd().targets.GaussianMixture1D(), dsvgd().RBF(float(g["h"])))
+    df = s.sample(int(g["n"]), int(g["T"]), float(g["eps"]), verbose=False)
+    vals = np.stack(df["value"].to_list()).reshape(g["values"].shape)
+    assert abs_err(vals, g["values"]) < TRAJ_TOL
+
+
 # --------------------------------------------------------- samplers ----
 @pytest.mark.parametrize("name", ["g2_sample_gauss_n32_d2", "g2_sample_gmm_n50"])
 def test_sampler_sequential_matches_reference(golden, name):
