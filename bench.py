@@ -103,7 +103,7 @@ def pmc_traffic(kernel_prefixes):
     """HBM bytes per phi_mm from the committed rocprofv3 --pmc summary
     (FETCH_SIZE x2 [gfx950 half-count] + WRITE_SIZE, separate passes;
     scripts/pmc_summary.py): the sum over the launches phi_mm makes (one
-    kernel, or on the symmetric layout NNX3Tile's transposed part + phi_w1's
+    kernel, or on the symmetric layout phi_w1<1>'s transposed part + phi_w1<2>'s
     plain part) -- None unless every one of them is in the summary."""
     path = os.path.join(ROOT, "profiles", "latest_summary.json")
     try:
@@ -318,8 +318,8 @@ def main(argv=None):
     # the committed PMC summary is an N=1 profile: only quoted for the N=1 run
     # phi_mm is the NN tile with the fused exp (<TN, DMA, EXP=true, ..., Fmt>);
     # the logreg G.Xd launch is the same tile with EXP=false
-    knames = {"h2": ["void dsvgd::nn_x3_kernel<4, true, true, false, 2, dsvgd::FmtH2,",
-                     "_ZN5dsvgd13phi_w1_kernel"],
+    knames = {"h2": (["_ZN5dsvgd13phi_w1_kernelILi1E", "_ZN5dsvgd13phi_w1_kernelILi2E"]
+                     if eng.sym else ["_ZN5dsvgd13phi_w1_kernelILi0E"]),
               "x3": ["void dsvgd::nn_x3_kernel<4, true, true, true, 2, dsvgd::FmtX3,"],
               "f32": ["void dsvgd::nn_kernel<4, true,"]}[gemm]
     traffic, traffic_src = pmc_traffic(knames) if world == 1 else (None, None)
@@ -348,9 +348,10 @@ def main(argv=None):
                    "n": n, "d": d, "N_global": Ng, "parallelism": "dp%d" % world,
                    "particles_per_gpu": m},
         "roofline": {"bound": "mfma",
-                     "kernel": {"h2": ("phi_mm (NNX3Tile nn_x3_kernel<4, FmtH2> on the "
-                                       "transposed K-steps + phi_w1_kernel on the rest" if eng.sym
-                                       else "phi_mm (phi_w1_kernel: one wave per SIMD, FmtH2") +
+                     "kernel": {"h2": ("phi_mm (phi_w1_kernel<1> on each row block's "
+                                       "transposed K-steps + phi_w1_kernel<2> on the rest: one wave "
+                                       "per SIMD, FmtH2" if eng.sym
+                                       else "phi_mm (phi_w1_kernel<0>: one wave per SIMD, FmtH2") +
                                       ": fp32-accurate 2-part fp16 split, 3 fp16 MFMA products "
                                       "per fp32 product; D layout %s)" % ("symmetric" if eng.sym
                                                                           else "full"),

@@ -71,6 +71,7 @@ __global__ __launch_bounds__(256) void radix_hist_kernel(const float* __restrict
                                                          dsvgd_select_state* __restrict__ st,
                                                          int64_t sym_npad) {
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
+  if (st->passes_done >= (uint32_t)pass) return;  // digit fixed by bracket_check
   for (int b = threadIdx.x; b < DSVGD_RADIX_BINS; b += 256) shist[b] = 0u;
   uint32_t shift, mask, hishift;
   digit_of(pass, shift, mask, hishift);
@@ -206,6 +207,7 @@ __device__ __forceinline__ void clear_bins(uint64_t* hist) {
 __global__ __launch_bounds__(256) void radix_pick_kernel(dsvgd_select_state* __restrict__ st,
                                                          int pass) {
   __shared__ unsigned long long part[4];
+  if (st->passes_done >= (uint32_t)pass) return;  // digit fixed, bins untouched (zero)
   pick_digit<false>(st->hist, st, pass, part);
   clear_bins(st->hist);
 }
@@ -305,6 +307,15 @@ __global__ void bracket_check_kernel(dsvgd_select_state* st) {
   if (st->overflow == 0ull && below <= k && k < below + nc) {
     st->k = k - below;
     st->fallback = 0u;
+    // every candidate key lies in [bits(lo), bits(hi)]: when those share
+    // digit 1 (the bracket spans ~1 % of the value, the usual case) the
+    // digit-1 pass would put them all in that one bin -- fix it here and let
+    // the pass-1 hist / pick launches return at once (one candidate read less)
+    const uint32_t a = __float_as_uint(st->lo), b = __float_as_uint(st->hi);
+    if ((a >> 21) == (b >> 21)) {
+      st->prefix = a & 0xFFE00000u;
+      st->passes_done = 1u;
+    }
   } else {
     st->fallback = 1u;
   }

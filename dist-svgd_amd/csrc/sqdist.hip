@@ -14,6 +14,7 @@
 
 #include "gemm_tiles.hpp"
 #include "gemm_x3.hpp"
+#include "gram_w1.hpp"
 #include "select.hpp"
 
 namespace dsvgd {
@@ -500,12 +501,40 @@ int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, 
   } else {
     parts[np++] = {false, Tm2, Tn2, 0, 0, tile_grid(Tm2, Tn2, false)};
   }
+  // FmtH2: the one-wave-per-SIMD Gram (gram_w1.hpp) for every part it
+  // supports -- no mirror stores, the none / bracket select modes, K-steps
+  // in sixteens, 16-row-aligned images; 128 x 256 units, 4 slots each
+  const bool w1ok = F::P == 2 && SM != kSelHist && nk * KS % 16 == 0 && row0 % 16 == 0;
+  auto w1part = [&](const Part& P) { return w1ok && !(P.sym && (sym ? layout : 0) == 0); };
+  // every part spans the owned block's strips; its column pairs from bj_off
+  auto w1walk = [&](const Part& P) { return GramUnitWalk((int)(m_pad / 128), P.tc2, P.sym); };
   int64_t ns_total = 0;
-  for (int i = 0; i < np; ++i) ns_total += parts[i].total * 8;
+  for (int i = 0; i < np; ++i)
+    ns_total += w1part(parts[i]) ? w1walk(parts[i]).total() * GramW1::kSlots : parts[i].total * 8;
+  int bw = 0;
+  if (w1ok && (rc = persistent_blocks(reinterpret_cast<const void*>(&gram_w1_kernel<SM, true>), &bw,
+                                      GramW1::kThreads)))
+    return rc;
   int64_t base = 0;
   for (int i = 0; i < np; ++i) {
     const Part& P = parts[i];
     const int lay = sym ? layout : 0;
+    if (w1part(P)) {
+      const GramUnitWalk wk = w1walk(P);
+      const int64_t tot = wk.total();
+#define DSVGD_GW1(SY)                                                                             \
+  hipLaunchKernelGGL((gram_w1_kernel<SM, SY>), dim3((unsigned)bw), dim3(GramW1::kThreads), 0, s,  \
+                     (const _Float16*)Yg, img, norms, rsc, row0, m, n, n_pad, nk * KS, D, st,     \
+                     cand, tot, wk.Tm, wk.Tc, P.bj_off, base, ns_total)
+      if (P.sym)
+        DSVGD_GW1(true);
+      else
+        DSVGD_GW1(false);
+#undef DSVGD_GW1
+      if ((rc = check_launch("gram_w1"))) return rc;
+      base += tot * GramW1::kSlots;
+      continue;
+    }
 #define DSVGD_X3W(SY, B, LAY, R0T, MIR)                                                          \
   hipLaunchKernelGGL((sqdist_x3w_kernel<SY, SM, F::P == 3, F, KS, MIR>), dim3((unsigned)B),       \
                      dim3(512), 0, s, Yg, img, norms, row0, m, n, n_pad, nk, D, st, cand, P.total, \

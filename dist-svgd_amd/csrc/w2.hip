@@ -33,6 +33,7 @@
 #include <float.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "common.hpp"
 
@@ -517,7 +518,21 @@ __global__ __launch_bounds__(256) void w2_grad_kernel(const float* __restrict__ 
 
 using namespace dsvgd;
 
+// the last dsvgd_w2_assign's progress on this host thread: (rounds, phase,
+// unassigned slots) at every control readback (kRoundBatch rounds apart)
+static std::vector<long long>& w2_trace() {
+  static thread_local std::vector<long long> t;
+  return t;
+}
+
 extern "C" {
+
+int64_t dsvgd_w2_trace(int64_t* out, int64_t cap) {
+  const std::vector<long long>& t = w2_trace();
+  const int64_t k = (int64_t)t.size() / 3;
+  for (int64_t e = 0; out && e < std::min(k, cap) * 3; ++e) out[e] = t[e];
+  return k;
+}
 
 size_t dsvgd_w2_workspace_bytes(int64_t m, int64_t n) {
   return kW2CtlBytes + (size_t)n * (sizeof(double) + sizeof(unsigned long long) + 4 * sizeof(int32_t)) +
@@ -596,6 +611,7 @@ int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
     return check_launch("w2 events");
   W2Ctl h{};
   rc = 0;
+  w2_trace().clear();
   for (int64_t batch = 0;; ++batch) {
     for (int b = 0; b < kRoundBatch; ++b) {
       bid();
@@ -614,6 +630,7 @@ int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
       break;
     }
     h = hbuf[(batch - 1) & 1];
+    w2_trace().insert(w2_trace().end(), {h.rounds, h.phases, (long long)h.unassigned});
     if (h.done) break;
     if ((batch - 1) * kRoundBatch >= max_rounds) {
       set_error("dsvgd_w2_assign: no convergence after %lld rounds (%lld phases, %llu unassigned)",

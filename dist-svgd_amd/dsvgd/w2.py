@@ -57,6 +57,13 @@ class W2Term(object):
                N.ptr(self.assign), float(h), N.ptr(self.G), self.d, s)
         return self.G
 
+    def trace(self):
+        """The last solve's progress: (rounds, phase, unassigned) every 16 rounds."""
+        k = int(N.load().dsvgd_w2_trace(None, 0))
+        buf = (ctypes.c_int64 * (3 * k))()
+        N.load().dsvgd_w2_trace(buf, k)
+        return [tuple(buf[3 * e:3 * e + 3]) for e in range(k)]
+
     def plan(self):
         """The last slot -> column assignment as a host int64 array."""
         return self.assign.cpu().numpy().astype("int64")

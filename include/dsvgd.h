@@ -423,6 +423,10 @@ size_t dsvgd_w2_workspace_bytes(int64_t m, int64_t n);
 int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
                     int64_t max_rounds, int warm_phases, int32_t* assign, int64_t* rounds_out,
                     void* stream);
+/* Progress of this host thread's last dsvgd_w2_assign: out[3k..3k+2] =
+ * (rounds, epsilon phase, unassigned slots) at the k-th control readback
+ * (every 16 rounds); copies min(count, cap) triples, returns count. */
+int64_t dsvgd_w2_trace(int64_t* out, int64_t cap);
 /* G[i] = h * sum_j P_ij (x_i - y_j) = h/n * sum_{slots s of i} (x_i - y_assign[s])
  * (distsampler.py:128 scaled by the JKO step h of :198); pass G as `extra`
  * to dsvgd_phi_finish / dsvgd_phi_direct / dsvgd_phi_row. */

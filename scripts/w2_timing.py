@@ -62,7 +62,25 @@ def case(m, n, d, kind, seed=0):
             cold_plan = G
         else:
             out["warm_vs_cold_grad_maxdiff"] = float((G - cold_plan).abs().max())
+        if TRACE:
+            out[key + "_next_profile"] = profile(ww.trace())
     return out
+
+
+def profile(tr):
+    """Rounds per epsilon phase, split by how many slots were unassigned when
+    they ran (from the 16-round control readbacks)."""
+    buckets = (16, 256, 4096, 1 << 62)
+    prof, prev = {}, 0
+    for rounds, phase, un in tr:
+        b = next(k for k in buckets if un < k)
+        ph = prof.setdefault(str(phase), {str(k): 0 for k in buckets})
+        ph[str(b)] += rounds - prev
+        prev = rounds
+    return prof
+
+
+TRACE = False
 
 
 def main():
@@ -71,7 +89,26 @@ def main():
     ap.add_argument("--warm-sweep", action="store_true",
                     help="warm-start phases 1..5 on two R > 1 shapes")
     ap.add_argument("--lib", default=None, help="an A/B build of the library (make ab)")
+    ap.add_argument("--shapes", default=None,
+                    help="m x n x d list, e.g. 8192x65536x256,2048x16384x256 (svgd shape)")
+    ap.add_argument("--trace", action="store_true",
+                    help="rounds per phase by unassigned-slot count")
+    ap.add_argument("--warm-phases", default=None,
+                    help="comma list of warm phase counts to sweep on --shapes")
     args = ap.parse_args()
+    global TRACE
+    TRACE = args.trace
+    if args.shapes:
+        import dsvgd
+        shapes = [tuple(int(v) for v in sh.split("x")) + ("svgd",) for sh in args.shapes.split(",")]
+        for ph in ([int(v) for v in args.warm_phases.split(",")] if args.warm_phases
+                   else [dsvgd.w2.W2Term.WARM_PHASES]):
+            dsvgd.w2.W2Term.WARM_PHASES = ph
+            for sh in shapes:
+                r = case(*sh)
+                r["warm_phases"] = ph
+                print(json.dumps(r), flush=True)
+        return
     if args.lib:
         import dsvgd
         dsvgd._native.LIB_PATH = os.path.abspath(args.lib)

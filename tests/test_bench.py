@@ -13,31 +13,34 @@ sys.path.insert(0, ROOT)
 
 
 def test_pmc_traffic_picks_phi_mm():
-    """The quoted traffic is phi_mm's: the EXP=true NN tile (and, on the
-    symmetric layout, phi_w1's launch of the same step summed with it) --
-    never the logreg G.Xd launch of the same tile."""
+    """The quoted traffic is phi_mm's: on the symmetric layout the sum of
+    phi_w1<1> (transposed K-steps) and phi_w1<2> (the rest) of the same step --
+    never a logreg launch -- and nothing when a launch of the pair is missing."""
     import bench
     summ = os.path.join(ROOT, "profiles", "latest_summary.json")
     if not os.path.exists(summ):
         pytest.skip("no committed PMC summary")
     with open(summ) as f:
         ks = json.load(f)["kernels"]
-    nn = "void dsvgd::nn_x3_kernel<4, true, true,"
-    w1 = "_ZN5dsvgd13phi_w1_kernel"
-    phi = [k for k in ks if k.startswith(nn)]
-    gxd = [k for k in ks if k.startswith("void dsvgd::nn_x3_kernel<4, true, false,")]
-    assert len(phi) == 1, phi
-    traffic, src = bench.pmc_traffic([nn])
-    assert traffic == ks[phi[0]]["hbm_bytes_per_launch"]
-    assert src == os.path.join("profiles", "latest_summary.json")
-    if gxd:  # the logreg G.Xd launch (same tile, no exp) must not be the one quoted
-        assert traffic != ks[gxd[0]]["hbm_bytes_per_launch"]
-    both, _ = bench.pmc_traffic([nn, w1])
-    w = [k for k in ks if k.startswith(w1) and "hbm_bytes_per_launch" in ks[k]]
-    if w:
-        assert both == traffic + ks[w[0]]["hbm_bytes_per_launch"]
-    else:
+    w1 = "_ZN5dsvgd13phi_w1_kernelILi1E"
+    w2 = "_ZN5dsvgd13phi_w1_kernelILi2E"
+
+    def per_launch(prefix):
+        hit = [v["hbm_bytes_per_launch"] for k, v in ks.items()
+               if k.startswith(prefix) and "hbm_bytes_per_launch" in v]
+        return hit[0] if hit else None
+
+    a, b = per_launch(w1), per_launch(w2)
+    both, src = bench.pmc_traffic([w1, w2])
+    if a is None or b is None:
         assert both is None   # a launch of the pair missing: nothing quoted
+    else:
+        assert both == a + b
+        assert src == os.path.join("profiles", "latest_summary.json")
+    assert bench.pmc_traffic(["no-such-kernel"]) == (None, None)
+    lr = [k for k in ks if "logreg" in k and "hbm_bytes_per_launch" in ks[k]]
+    if lr and a is not None:
+        assert all(not k.startswith(w1) for k in lr)
 
 
 def _env():
