@@ -283,6 +283,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     const int vo = (32 * bi + (lane & 15)) * 64 + 16 * h + 32 * ((lane >> 4) & 1);
     const int so = (2 * bj + (SL & 1)) * kPanelElems * 4;
+    // nt (aux 2): measured against default, sc1 and nt sc1 -- equal or
+    // faster (profiles/r8i)
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[0]), rD, vo, so, 2);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[1]), rD, vo + 1024, so, 2);
   };
@@ -352,8 +354,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     *reinterpret_cast<f32x4*>(dst + ldsA) = ra[sa][0];
     *reinterpret_cast<f32x4*>(dst + ldsA + GramW1::BM * 32) = ra[sa][1];
   };
-  // the K-step boundary: LDS writes landed, every wave past its reads; and a
-  // scheduling fence, so no instruction migrates between K-steps
+  // the strip's fragments of one K-step from its LDS stage
+  V8 af[2][4][2];
+  auto read_frags = [&](V8 (&a)[4][2], const char* st_) {
+#pragma unroll
+    for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        a[bi][p] = *reinterpret_cast<const V8*>(st_ + p * GramW1::BM * 32 + x3_off(32 * bi + r, h));
+  };
+  // LDS writes landed, every wave past its LDS reads; and a scheduling
+  // fence, so no instruction migrates across it
   auto barrier = []() {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -371,14 +382,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     constexpr bool FIRST = decltype(FIRST_)::value;
     constexpr int E = S ^ 1;                           // the set being written out
     constexpr int ebi = (SL < 0 ? 0 : SL) >> 2, ebj = ((SL < 0 ? 0 : SL) >> 1) & 1;
-    const char* cur_st = smem + (KS & 1) * GramW1::SA;
     char* nxt_st = smem + ((KS + 1) & 1) * GramW1::SA;
-    V8 a[4][2];
-#pragma unroll
-    for (int bi = 0; bi < 4; ++bi)
-#pragma unroll
-      for (int p = 0; p < 2; ++p)
-        a[bi][p] = *reinterpret_cast<const V8*>(cur_st + p * GramW1::BM * 32 + x3_off(32 * bi + r, h));
+    V8 (&a)[4][2] = af[KS & 1];  // this K-step's strip fragments (read last K-step)
     stage(nxt_st, (KS + 1) & 1);
     // epilogue operands of this slice (see slice())
     int tgv = 0;
@@ -430,25 +435,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
       }
       if (grp == 1) load_A(KS & 1, k + 2);
-      if (grp == 3) load_B((KS + 2) & 3, k + 2);
+      if (grp == 2) load_B((KS + 2) & 3, k + 2);
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
+      if (grp == 3) {
+        // mid-step: every wave's staging of K-step k + 1 has landed (and
+        // every wave's reads of the buffer it replaced were done a K-step
+        // ago); the next K-step's fragments are read now, behind the
+        // remaining 12 MFMAs, so no K-step starts waiting on LDS
+        barrier();
+        read_frags(af[(KS + 1) & 1], nxt_st);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     if constexpr (SL >= 0) store_slice(v, std::integral_constant<int, SL>{});
-    barrier();
   };
 
-  // prologue: A(0), A(1), B(0), B(1) loaded, A(0) staged
+  // prologue: A(0), A(1), B(0), B(1) loaded, A(0) staged and read
   load_A(0, 0);
   load_A(1, 1);
   load_B(0, 0);
   load_B(1, 1);
   stage(smem, 0);
   barrier();
+  read_frags(af[0], smem);
 
   auto tile = [&](auto S_) {
 #define DSVGD_GW1_STEP(KK)                                                                      \

@@ -22,9 +22,11 @@ class W2Term(object):
     slot assignment (n int32) and G (m x d)."""
 
     MAX_ROUNDS = 1 << 18
-    # epsilon phases above the final eps for a warm start from the previous
-    # step's prices (0 disables; the first call on a workspace is always cold)
-    WARM_PHASES = 2
+    # warm start from the previous step's prices and plan: None = adaptive
+    # (the first epsilon from the old plan's slackness violation under the
+    # new costs, dsvgd_w2_assign_warm); k > 0 = k fixed phases above the
+    # final eps; 0 = cold every step.  The first call on a workspace is cold.
+    WARM_PHASES = None
 
     def __init__(self, m, n, d, device, warm=True):
         if n % m:
@@ -48,9 +50,15 @@ class W2Term(object):
         N.call("dsvgd_w2_cost", N.ptr(X), N.ld(X), self.m, N.ptr(Y), N.ld(Y), self.n, self.d,
                N.ptr(self.C), self.n, s)
         rounds = ctypes.c_int64(0)
-        warm = self.WARM_PHASES if (self.warm and self._solved) else 0
-        N.call("dsvgd_w2_assign", N.ptr(self.C), self.n, self.m, self.n, N.ptr(self.ws),
-               self.MAX_ROUNDS, warm, N.ptr(self.assign), ctypes.addressof(rounds), s)
+        if self.warm and self._solved and self.WARM_PHASES is None:
+            # prev and out may alias: the plan is only written after the solve
+            N.call("dsvgd_w2_assign_warm", N.ptr(self.C), self.n, self.m, self.n,
+                   N.ptr(self.ws), self.MAX_ROUNDS, N.ptr(self.assign), N.ptr(self.assign),
+                   ctypes.addressof(rounds), s)
+        else:
+            warm = (self.WARM_PHASES or 0) if (self.warm and self._solved) else 0
+            N.call("dsvgd_w2_assign", N.ptr(self.C), self.n, self.m, self.n, N.ptr(self.ws),
+                   self.MAX_ROUNDS, warm, N.ptr(self.assign), ctypes.addressof(rounds), s)
         self.rounds = int(rounds.value)
         self._solved = True
         N.call("dsvgd_w2_grad", N.ptr(X), N.ld(X), self.m, N.ptr(Y), N.ld(Y), self.n, self.d,

@@ -423,6 +423,14 @@ size_t dsvgd_w2_workspace_bytes(int64_t m, int64_t n);
 int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
                     int64_t max_rounds, int warm_phases, int32_t* assign, int64_t* rounds_out,
                     void* stream);
+/* dsvgd_w2_assign warm-started from the previous call on this workspace
+ * (its prices) and that call's plan prev_assign (n slots): the first epsilon
+ * is the previous plan's complementary-slackness violation under the new
+ * costs / 64 (so a small SVGD step starts near eps_final, a large one high),
+ * then the usual phases down to eps_final -- same optimality guarantee. */
+int dsvgd_w2_assign_warm(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
+                         int64_t max_rounds, const int32_t* prev_assign, int32_t* assign,
+                         int64_t* rounds_out, void* stream);
 /* Progress of this host thread's last dsvgd_w2_assign: out[3k..3k+2] =
  * (rounds, epsilon phase, unassigned slots) at the k-th control readback
  * (every 16 rounds); copies min(count, cap) triples, returns count. */

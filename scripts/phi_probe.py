@@ -45,6 +45,13 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         dist_ms = e0.elapsed_time(e1) / args.reps
+        e0.record()
+        for _ in range(args.reps):
+            eng.distances(median=False)
+        e1.record()
+        torch.cuda.synchronize()
+        dist_plain_ms = e0.elapsed_time(e1) / args.reps
+        eng.distances(median=True)
         eng.median_bandwidth()
         eng.direction(write_phi=True)
         torch.cuda.synchronize()
@@ -58,7 +65,7 @@ def main():
             np.save("%s_%s.npy" % (args.dump, cfg.replace(":", "_")),
                     eng.phi[::256].float().cpu().numpy())
         out[cfg] = {"sym": bool(eng.sym), "phi_ms": e0.elapsed_time(e1) / args.reps,
-                    "distances_ms": dist_ms}
+                    "distances_ms": dist_ms, "distances_no_select_ms": dist_plain_ms}
         print(json.dumps({cfg: out[cfg]}), flush=True)
         del eng
         torch.cuda.empty_cache()

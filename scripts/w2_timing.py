@@ -94,15 +94,15 @@ def main():
     ap.add_argument("--trace", action="store_true",
                     help="rounds per phase by unassigned-slot count")
     ap.add_argument("--warm-phases", default=None,
-                    help="comma list of warm phase counts to sweep on --shapes")
+                    help="comma list of warm phase counts to sweep on --shapes (a = adaptive)")
     args = ap.parse_args()
     global TRACE
     TRACE = args.trace
     if args.shapes:
         import dsvgd
         shapes = [tuple(int(v) for v in sh.split("x")) + ("svgd",) for sh in args.shapes.split(",")]
-        for ph in ([int(v) for v in args.warm_phases.split(",")] if args.warm_phases
-                   else [dsvgd.w2.W2Term.WARM_PHASES]):
+        for ph in ([None if v == "a" else int(v) for v in args.warm_phases.split(",")]
+                   if args.warm_phases else [dsvgd.w2.W2Term.WARM_PHASES]):
             dsvgd.w2.W2Term.WARM_PHASES = ph
             for sh in shapes:
                 r = case(*sh)

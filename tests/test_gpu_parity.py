@@ -626,6 +626,37 @@ def test_w2_assignment_optimal(m, n, d, near):
     assert err < PHI_TOL, err
 
 
+@pytest.mark.parametrize("m,n,d,step", [(512, 4096, 16, 1e-3), (512, 4096, 16, 0.3),
+                                        (1024, 1024, 32, 1e-2), (256, 2048, 8, 1e-4)])
+def test_w2_warm_start_same_plan(m, n, d, step):
+    """The next SVGD step's solve warm-started from this one's prices and
+    plan (dsvgd_w2_assign_warm: first epsilon from the old plan's slackness
+    violation) == scipy's exact plan of the new problem, for small and large
+    steps; fixed-phase warm starts and a cold solve agree with it."""
+    rs = np.random.RandomState(m + n + d)
+    X = rs.randn(m, d).astype(np.float32)
+    P = rs.randn(n, d).astype(np.float32)
+    P[:m] = X - 1e-3 * rs.randn(m, d).astype(np.float32)
+    X2 = (X + step * rs.randn(m, d)).astype(np.float32)
+    P2 = (P + step * rs.randn(n, d)).astype(np.float32)
+    ref = O.w2_plan(O.w2_cost(X2, P2))
+    W2 = dsvgd().w2.W2Term
+    plans = {}
+    for mode in (None, 2, 0):
+        w = W2(m, n, d, DEV, warm=True)
+        old = W2.WARM_PHASES
+        W2.WARM_PHASES = mode
+        try:
+            w.grad(gpu(X), gpu(P), 1.0)
+            w.grad(gpu(X2), gpu(P2), 1.0)
+        finally:
+            W2.WARM_PHASES = old
+        plans[mode] = (w.plan(), w.rounds)
+    for mode, (plan, rounds) in plans.items():
+        np.testing.assert_array_equal(_row_sets(plan, m), _row_sets(ref, m), err_msg=str(mode))
+    record_parity(0.0, rounds_adaptive=plans[None][1], rounds_cold=plans[0][1])
+
+
 def test_w2_degenerate_and_identity():
     """All-equal particles (every cost 0) -> zero gradient; previous ==
     current (S = 1 consecutive steps) -> identity plan, zero gradient."""
