@@ -161,17 +161,18 @@ class DistSampler(object):
 
     def _warn_w2_cost(self):
         """The W2 term is the reference default, but with particles exchanged
-        (R = n / m = num_shards > 1) its exact assignment is an auction of
-        10^4-10^5 rounds (DESIGN.md, W2 cost at scale): say so once, at
-        construction, instead of letting make_step stall for seconds."""
+        (R = n / m = num_shards > 1) the first step's exact assignment is a
+        cold auction of ~10^5 rounds (DESIGN.md, W2 cost at scale; later steps
+        start warm from the previous plan): say so once, at construction,
+        instead of letting the first make_step stall for seconds."""
         m = self._particles_per_shard
         n = self._num_particles if self._exchange_particles else m
         if self._include_wasserstein and n > m and m * n >= self.W2_WARN_ENTRIES:
             warnings.warn(
                 "DistSampler: include_wasserstein=True with R = n/m = %d > 1 and an "
-                "%d x %d plan: the exact W2 assignment takes seconds per step at this "
-                "size (m=8192, n=65536: ~14 s cold, ~2 s warm); pass "
-                "include_wasserstein=False for throughput" % (n // m, m, n),
+                "%d x %d plan: the exact W2 assignment of the first step takes seconds "
+                "at this size (m=8192, n=65536: ~14 s cold, then ~0.26 s per step warm); "
+                "pass include_wasserstein=False for throughput" % (n // m, m, n),
                 RuntimeWarning, stacklevel=3)
 
     # ---------------------------------------------------- reference API --
