@@ -5,18 +5,21 @@
 // rows before i already moved, rows from i on not yet.  For a block of rows
 // [r0, r0 + B):
 //
-//   P_i  = sum_{all j} t(x_i, x_j, s_j)        (the particles as the block starts)
-//   phi_i = (P_i + sum_{r0 <= j < i} [t(x_i, x_j', s_j') - t(x_i, x_j, s_j)]) / n
+//   Q_i  = sum_{j outside [r0, r0 + i)} t(x_i, x_j, s_j)   (as the block starts)
+//   phi_i = (Q_i + sum_{r0 <= j < r0 + i} t(x_i, x_j', s_j')) / n
 //
 // t(x, y, s) = k(x, y) (s + (2/h)(x - y)), k = exp(-|x - y|^2 / h), x_j' / s_j'
-// the moved particle and its refreshed score.  P for the whole block is one
+// the moved particle and its refreshed score.  Q for the whole block is one
 // wide pass over all n rows (gs_part_kernel: every CU busy, exact
-// differences, split-J partials); only the in-block corrections are
-// sequential (gs_sweep_kernel: one workgroup walks the B rows, the block's
-// old and new rows in LDS, one barrier-separated row at a time).  The score
-// refresh of a moved particle (the reference re-evaluates logp per pair, so
-// later rows see it) is fused for the elementwise targets.  Same terms as the
-// per-row path (dsvgd_phi_row_split), in a different summation order.
+// differences, split-J partials, the block's own earlier rows masked out)
+// plus a slice reduction (gs_reduce_kernel, fixed order); only the sums over
+// the rows moved in this block are sequential (gs_sweep_kernel: ONE wave walks
+// the B rows -- lane j for the distances to the moved rows, lane c for the
+// columns -- with no barrier between rows: one wave's LDS accesses execute in
+// order).  The score refresh of a moved particle (the reference re-evaluates
+// logp per pair, so later rows see it) is fused for the elementwise targets.
+// Same terms as the per-row path (dsvgd_phi_row_split), in a different
+// summation order.
 #include <algorithm>
 #include <cmath>
 
@@ -28,8 +31,8 @@ constexpr int kGsB = 64;      // rows per block
 constexpr int kGsMaxD = 64;   // features (one thread column group of 4 per 4 features)
 constexpr int64_t kGsChain = 4096;
 
-// part[z][i][c] = sum_{j in [z J, (z+1) J)} t(x_{r0+i}, x_j, s_j)[c] (raw
-// sums, not / n), i < B, c < d.  Block z: the B x d outputs as 64 x 64,
+// part[z][i][c] = sum_{j in [z J, (z+1) J), j outside [r0, r0 + i)}
+// t(x_{r0+i}, x_j, s_j)[c] (raw sums, not / n), i < B, c < d.  Block z: the B x d outputs as 64 x 64,
 // thread (rq, cq) rows 4 rq .. +3 x columns 4 cq .. +3; j in chunks of 64
 // staged in LDS -- transposed copies for the distances (conflict-free f32x4
 // reads along j / i), row copies for the accumulation.
@@ -99,12 +102,18 @@ __global__ __launch_bounds__(256) void gs_part_kernel(const float* __restrict__ 
           dd[a][b] = fmaf(df, df, dd[a][b]);
         }
     }
+    // pairs with the block's own earlier rows (r0 <= j < r0 + i) are left to
+    // the sweep, which uses the moved rows there
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b)
-        kT[4 * cq + b][4 * rq + a] =
-            (4 * rq + a < B && 4 * cq + b < jn) ? __builtin_amdgcn_exp2f(dd[a][b] * scale) : 0.f;
+      for (int b = 0; b < 4; ++b) {
+        const int64_t jr = j0 + 4 * cq + b - r0;
+        const bool moved = jr >= 0 && jr < 4 * rq + a;
+        kT[4 * cq + b][4 * rq + a] = (4 * rq + a < B && 4 * cq + b < jn && !moved)
+                                         ? __builtin_amdgcn_exp2f(dd[a][b] * scale)
+                                         : 0.f;
+      }
     __syncthreads();
     for (int q = 0; q < jn; ++q) {
       const f32x4 k4 = *reinterpret_cast<const f32x4*>(&kT[q][4 * rq]);
@@ -126,13 +135,41 @@ __global__ __launch_bounds__(256) void gs_part_kernel(const float* __restrict__ 
     }
 }
 
-// The block's rows in order, one workgroup.  LDS: the block's old rows and
-// scores, the moved rows and refreshed scores, k(x_i, x_j) of the old pairs
-// (all at the start), P (the partials summed in slice order).
+// Q = the slices of gs_part summed in slice order (z = w, w + 4, ... per
+// wave, then the four wave sums in a fixed tree), written over slice 0.
+// Element e = 64 blockIdx.x + lane; each element is read and written by one
+// workgroup only, so the in-place write after the barrier is safe.
+__global__ __launch_bounds__(256) void gs_reduce_kernel(float* __restrict__ part, int64_t elems,
+                                                        int nsplit) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (e < elems) {
+    int z = w;
+    for (; z + 28 < nsplit; z += 32) {  // 8 loads in flight
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(z + 4 * u) * elems + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; z < nsplit; z += 4) s += part[(int64_t)z * elems + e];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && e < elems) part[e] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+// The block's rows in order, by ONE wave (the other three only help load).
+// LDS: the block's old rows, the moved rows and their scores, Q.  Per row i:
+// lane j < i: k(x_i, x_j') (exact differences, 16-byte reads along the
+// features); lane c: sum_{j < i} k_j (s_j' + g (x_i - x_j')) with k_j read
+// from lane j (v_readlane), then phi_i, the move and the score refresh.
 // score_kind: 0 scores frozen (exchanged scores, or the caller refreshes),
 // 1 Gaussian s = scale * (-lam (x - mu)), 2 the 1-D two-component mixture of
 // experiments/gmm.py per coordinate (csrc/prep.hip score_gmm_kernel).
-constexpr int kGsLd = kGsMaxD + 1;  // row pitch: lanes reading one column of many rows spread over banks
+constexpr int kGsLd = kGsMaxD + 4;  // row pitch (floats): 16-byte rows, 4 banks apart
 
 __device__ __forceinline__ float gs_score(int kind, float x, float mu, float lam, float sc) {
   if (kind == 1) return sc * (-lam * (x - mu));
@@ -145,82 +182,68 @@ __device__ __forceinline__ float gs_score(int kind, float x, float mu, float lam
 __global__ __launch_bounds__(256) void gs_sweep_kernel(
     float* __restrict__ X, int64_t ldx, float* __restrict__ S, int64_t lds, int64_t n, int d,
     int64_t r0, int B, const dsvgd_select_state* __restrict__ st, float step,
-    const float* __restrict__ part, int nsplit, const float* __restrict__ extra, int64_t lde,
+    const float* __restrict__ Q, const float* __restrict__ extra, int64_t lde,
     float* __restrict__ phi_out, int64_t ldphi, int score_kind, const float* __restrict__ mu,
     const float* __restrict__ lam, float score_scale) {
-  __shared__ float xo[kGsB][kGsLd], so[kGsB][kGsLd], xn[kGsB][kGsLd], sn[kGsB][kGsLd];
-  __shared__ float P[kGsB][kGsMaxD];
-  __shared__ float ko[kGsB][kGsB + 1];  // k(x_i, x_j), both as the block starts
-  __shared__ float kn[kGsB];            // k(x_i, x_j') of the row in progress
-  __shared__ float red[4][kGsMaxD];
+  // xo: old rows (zero past d, so the 16-byte distance reads need no mask)
+  __shared__ __attribute__((aligned(16))) float xo[kGsB][kGsLd];
+  __shared__ __attribute__((aligned(16))) float xn[kGsB][kGsLd];
+  __shared__ float sn[kGsB][kGsLd];
+  __shared__ float q[kGsB][kGsMaxD];
   const int t = threadIdx.x;
   const float inv_h = st->inv_h, g = 2.f * inv_h, scale = -inv_h * kLog2e;
   const float inv_n = 1.f / (float)n;
-  for (int e = t; e < B * d; e += 256) {
-    const int i = e / d, c = e % d;
-    xo[i][c] = X[(r0 + i) * ldx + c];
-    so[i][c] = S[(r0 + i) * lds + c];
-    float p = 0.f;
-    for (int z = 0; z < nsplit; ++z) p += part[((int64_t)z * B + i) * d + c];  // slice order
-    P[i][c] = p;
+  for (int e = t; e < kGsB * kGsLd; e += 256) {
+    const int i = e / kGsLd, c = e % kGsLd;
+    const bool ok = i < B && c < d;
+    xo[i][c] = ok ? X[(r0 + i) * ldx + c] : 0.f;
+    xn[i][c] = 0.f;
+    if (i < B && c < d) q[i][c] = Q[(int64_t)i * d + c];
   }
   __syncthreads();
-  // k of the old pairs (j < i), exact differences
-  for (int e = t; e < B * B; e += 256) {
-    const int i = e / B, j = e % B;
-    if (j >= i) continue;
-    float s2 = 0.f;
-    for (int c = 0; c < d; ++c) {
-      const float df = xo[i][c] - xo[j][c];
-      s2 = fmaf(df, df, s2);
-    }
-    ko[i][j] = __builtin_amdgcn_exp2f(s2 * scale);
-  }
-  __syncthreads();
-  // distances: lane quad (j = t >> 2, quarter q4 = t & 3 of the columns);
-  // accumulation: column cg = t % 64 of group gg = t / 64, over j = gg, gg + 4, ...
-  const int jq = t >> 2, q4 = t & 3;
-  const int dq = (d + 3) / 4;
-  const int G = 256 / kGsMaxD;  // 4 groups of (up to) 64 columns
-  const int cg = t % kGsMaxD, gg = t / kGsMaxD;
+  if (t >= 64) return;
+  const int lane = t;
+  const int d4 = (d + 3) >> 2;
+  const float mu_c = (score_kind == 1 && lane < d) ? mu[lane] : 0.f;
+  const float lam_c = (score_kind == 1 && lane < d) ? lam[lane] : 0.f;
   for (int i = 0; i < B; ++i) {
-    // k(x_i, x_j') for the rows already moved in this block
-    if (jq < i) {
-      float s2 = 0.f;
-      for (int c = q4 * dq; c < min(d, (q4 + 1) * dq); ++c) {
-        const float df = xo[i][c] - xn[jq][c];
+    // k(x_i, x_j') of the rows already moved: lane j
+    float s2 = 0.f;
+    for (int c4 = 0; c4 < d4; ++c4) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(&xo[i][4 * c4]);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(&xn[lane][4 * c4]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float df = a[u] - b[u];
         s2 = fmaf(df, df, s2);
       }
-      s2 += __shfl_xor(s2, 1, 64);
-      s2 += __shfl_xor(s2, 2, 64);
-      if (q4 == 0) kn[jq] = __builtin_amdgcn_exp2f(s2 * scale);
     }
-    __syncthreads();
-    // sum over j < i of t(x_i, x_j', s_j') - t(x_i, x_j, s_j), group gg: j = gg, gg + G, ...
-    float a = 0.f;
-    if (cg < d) {
-      const float xi = xo[i][cg];
-      for (int j = gg; j < i; j += G)
-        a += kn[j] * fmaf(g, xi - xn[j][cg], sn[j][cg]) - ko[i][j] * fmaf(g, xi - xo[j][cg], so[j][cg]);
+    const float kj = lane < i ? __builtin_amdgcn_exp2f(s2 * scale) : 0.f;
+    // lane c: the moved rows' terms
+    const int c = lane < d ? lane : 0;
+    const float xi = xo[i][c];
+    float acc = 0.f;
+    for (int j = 0; j < i; ++j) {
+      const float k = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kj), j));
+      acc = fmaf(k, fmaf(g, xi - xn[j][c], sn[j][c]), acc);
     }
-    red[gg][cg] = a;
-    __syncthreads();
-    if (t < d) {
-      const float corr = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
-      float p = inv_n * (P[i][t] + corr);
-      if (extra) p += extra[(int64_t)i * lde + t];
-      if (phi_out) phi_out[(int64_t)i * ldphi + t] = p;
-      const float x = xo[i][t] + step * p;
-      xn[i][t] = x;
-      X[(r0 + i) * ldx + t] = x;
-      float s = so[i][t];
+    if (lane < d) {
+      float p = inv_n * (q[i][c] + acc);
+      if (extra) p += extra[(int64_t)i * lde + c];
+      if (phi_out) phi_out[(int64_t)i * ldphi + c] = p;
+      const float x = xi + step * p;
+      X[(r0 + i) * ldx + c] = x;
+      float s = S[(r0 + i) * lds + c];
       if (score_kind != 0) {
-        s = gs_score(score_kind, x, mu ? mu[t] : 0.f, lam ? lam[t] : 0.f, score_scale);
-        S[(r0 + i) * lds + t] = s;
+        s = gs_score(score_kind, x, mu_c, lam_c, score_scale);
+        S[(r0 + i) * lds + c] = s;
       }
-      sn[i][t] = s;
+      xn[i][c] = x;
+      sn[i][c] = s;
     }
-    __syncthreads();
+    // the next row reads row i's LDS writes: one wave's LDS accesses run in
+    // order; keep the compiler from moving them
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
 }
 
@@ -248,7 +271,12 @@ int dsvgd_gs_block_part(const float* X, int64_t ldx, const float* S, int64_t lds
   const int64_t jchunk = roundup((n + nsplit - 1) / nsplit, 64);
   hipLaunchKernelGGL(gs_part_kernel, dim3((unsigned)nsplit), dim3(256), 0, (hipStream_t)stream, X,
                      ldx, S, lds, n, (int)d, r0, (int)B, st, jchunk, partial);
-  return check_launch("gs_part");
+  const int rc = check_launch("gs_part");
+  if (rc || nsplit == 1) return rc;
+  const int64_t elems = B * d;
+  hipLaunchKernelGGL(gs_reduce_kernel, dim3((unsigned)((elems + 63) / 64)), dim3(256), 0,
+                     (hipStream_t)stream, partial, elems, (int)nsplit);
+  return check_launch("gs_reduce");
 }
 
 int dsvgd_gs_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, int64_t n, int64_t d,
@@ -265,7 +293,7 @@ int dsvgd_gs_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, int64_t n
   DSVGD_REQUIRE(!extra || lde >= d, "lde");
   DSVGD_REQUIRE(!phi_out || ldphi >= d, "ldphi");
   hipLaunchKernelGGL(gs_sweep_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, X, ldx, S, lds,
-                     n, (int)d, r0, (int)B, st, step, partial, (int)nsplit, extra, lde, phi_out,
+                     n, (int)d, r0, (int)B, st, step, partial, extra, lde, phi_out,
                      ldphi, score_kind, mu, lam, score_scale);
   return check_launch("gs_sweep");
 }

@@ -379,16 +379,18 @@ int dsvgd_phi_row_split(float* X, int64_t ldx, const float* S, int64_t lds, int6
 
 /* Blocked Gauss-Seidel sweep (the same reference order, d <= 64): rows
  * [r0, r0 + B), B <= dsvgd_gs_block_rows() = 64, of the interacting set X
- * (n x d).  gs_block_part: partial[z][i][c] = raw sums over the j slice z
- * (nsplit = dsvgd_gs_splits(n) slices; nsplit x B x d floats) of
- * k(x_i, x_j) (s_j + (2/h)(x_i - x_j)) against ALL n rows as the block
- * starts; gs_block_sweep then walks the block in order in one workgroup:
- * phi_i = (sum of the partials + the corrections for the block rows already
- * moved) / n [+ extra row i], X[r0+i] += step phi_i, and the moved
- * particle's score refreshed in S (score_kind 1: scale * (-lam (x - mu)),
- * 2: the experiments/gmm.py mixture per coordinate; 0: S left as is --
- * exchanged scores are frozen for the step, distsampler.py:194-200).  Two
- * launches per 64 rows instead of two per row (dsvgd_phi_row_split). */
+ * (n x d).  gs_block_part: Q[i][c] = the raw sum over every j outside
+ * [r0, r0 + i) of k(x_i, x_j) (s_j + (2/h)(x_i - x_j)) as the block starts,
+ * computed as nsplit = dsvgd_gs_splits(n) j slices (partial: nsplit x B x d
+ * floats of scratch) and summed in slice order into partial[0 .. B d);
+ * gs_block_sweep then walks the block in order in one wave: phi_i = (Q_i +
+ * the terms of the block rows already moved, at their new positions) / n
+ * [+ extra row i], X[r0+i] += step phi_i, and the moved particle's score
+ * refreshed in S (score_kind 1: scale * (-lam (x - mu)), 2: the
+ * experiments/gmm.py mixture per coordinate; 0: S left as is -- exchanged
+ * scores are frozen for the step, distsampler.py:194-200).  Three launches
+ * per 64 rows instead of two per row (dsvgd_phi_row_split).  nsplit of the
+ * sweep: the gs_block_part call's (>= 1; only partial[0 .. B d) is read). */
 int64_t dsvgd_gs_block_rows(void);
 int64_t dsvgd_gs_splits(int64_t n);
 int dsvgd_gs_block_part(const float* X, int64_t ldx, const float* S, int64_t lds, int64_t n,
