@@ -29,6 +29,7 @@ timed on this host on a bounded sample, rank 0 at N=1 only.
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -218,6 +219,9 @@ def main(argv=None):
     ap.add_argument("--dim", type=int, default=256)
     ap.add_argument("--data-rows", type=int, default=16384, help="global data rows")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--soak", type=float, default=6.0,
+                    help="seconds of untimed steps after the timed ones (the GPU stays busy "
+                         "long enough for an outside utilisation sampler to see it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gemm", default="h2", choices=["h2", "x3", "f32"],
                     help="MFMA engine of the contractions (h2: fp16 split, the default)")
@@ -309,6 +313,12 @@ def main(argv=None):
     # stages allgather_x / allreduce_scores / hist_allreduce included)
     stages = gather_max(stages, world, args.backend, dev)
     assert bool(torch.isfinite(sampler._work).all()), "non-finite particles"
+    # untimed soak: the same number of steps on every rank (el is the max)
+    n_soak = int(math.ceil(args.soak / (el / args.steps))) if args.soak > 0 else 0
+    for _ in range(n_soak):
+        sampler.make_step(eps)
+    torch.cuda.synchronize()
+    barrier()
 
     m = n // world
     phi_ms = stages["phi_mm"]
@@ -370,6 +380,7 @@ def main(argv=None):
         "gemm": gemm,
         "step_6n2d_f32_mfma_frac": (6.0 * m * n * d) / (el / args.steps) / 1e12 / PEAK_FP32_MFMA_TFLOPS,
         "phi_splits": int(eng.splits),
+        "soak_steps_after_timing": n_soak,
         "process_group": {"backend": args.backend if world > 1 else None,
                           "world_size_seen": dist.get_world_size() if world > 1 else 1,
                           "stages": "mean per step, max over ranks" if world > 1 else "mean per step"},
