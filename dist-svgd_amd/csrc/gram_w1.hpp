@@ -22,10 +22,9 @@
 //   * the strip's image rows (shared by the 4 waves) are staged through LDS
 //     (2 x 8 KiB, loaded two K-steps ahead into VGPRs); each wave loads its
 //     own column fragments straight from the image, two K-steps ahead;
-//   * unit order: groups of 16 strips walk their column pairs together, so
-//     the 32 blocks an XCD runs at once share 2048 image rows (2 MiB, L2
-//     resident) while the column pairs stream -- the image is fetched about
-//     once per group instead of once per 256-row panel.
+//   * unit order: groups of 8 strips walk their column pairs together, so
+//     the 32 blocks an XCD runs at once work on 8 strips x 4 column pairs
+//     (1 MiB + 1 MiB of image, L2 resident) while the column pairs stream.
 // The wave tile's D region is addressed through a buffer resource whose
 // size is 0 for tiles that are not stored (below the diagonal of the
 // symmetric layout, past the padded matrix): those stores are dropped by the
@@ -48,7 +47,7 @@ struct GramW1 {
   static constexpr int BN = 256;   // unit columns: two 128-column tiles, 64 per wave
   static constexpr int P = 2;
   static constexpr int SA = P * BM * 32;   // one K-step of the strip's image (8 KiB)
-  static constexpr int kGroup = 16;        // strips per unit group
+  static constexpr int kGroup = 8;         // strips per unit group (4, 16, 32: slower, profiles/r9e)
   // SlotWriterLdsT list depth: a tile's 128 values per lane, flushed once at
   // the tile's end (no loop inside the K-steps)
   static constexpr int kCandDepth = 128;
@@ -58,9 +57,9 @@ struct GramW1 {
   static constexpr int kSlots = 4;         // candidate slots per unit (one per wave)
 };
 
-// Unit L -> (strip I, column pair J2).  Group g = strips [16 g, 16 g + 16)
-// over column pairs [j0(g), Tc) (symmetric: j0(g) = 8 g, the pair holding
-// the group's first diagonal tile), strip-fastest.
+// Unit L -> (strip I, column pair J2).  Group g = strips [G g, G g + G)
+// (G = kGroup) over column pairs [j0(g), Tc) (symmetric: j0(g) = G g / 2,
+// the pair holding the group's first diagonal tile), strip-fastest.
 struct GramUnitWalk {
   int Tm, Tc, ng;
   bool sym;

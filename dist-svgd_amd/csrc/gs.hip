@@ -28,6 +28,12 @@
 namespace dsvgd {
 
 constexpr int kGsB = 64;      // rows per block
+// few slices (small n, small d): the sweep sums them itself (one launch less
+// per block); otherwise gs_reduce_kernel does, over many workgroups
+constexpr int64_t kGsFoldMax = 16384;  // B d nsplit values summed in the sweep
+__host__ __device__ inline bool gs_fold(int64_t B, int64_t d, int64_t nsplit) {
+  return B * d * nsplit <= kGsFoldMax;
+}
 constexpr int kGsMaxD = 64;   // features (one thread column group of 4 per 4 features)
 constexpr int64_t kGsChain = 4096;
 
@@ -182,7 +188,7 @@ __device__ __forceinline__ float gs_score(int kind, float x, float mu, float lam
 __global__ __launch_bounds__(256) void gs_sweep_kernel(
     float* __restrict__ X, int64_t ldx, float* __restrict__ S, int64_t lds, int64_t n, int d,
     int64_t r0, int B, const dsvgd_select_state* __restrict__ st, float step,
-    const float* __restrict__ Q, const float* __restrict__ extra, int64_t lde,
+    const float* __restrict__ Q, int nsum, const float* __restrict__ extra, int64_t lde,
     float* __restrict__ phi_out, int64_t ldphi, int score_kind, const float* __restrict__ mu,
     const float* __restrict__ lam, float score_scale) {
   // xo: old rows (zero past d, so the 16-byte distance reads need no mask)
@@ -198,7 +204,11 @@ __global__ __launch_bounds__(256) void gs_sweep_kernel(
     const bool ok = i < B && c < d;
     xo[i][c] = ok ? X[(r0 + i) * ldx + c] : 0.f;
     xn[i][c] = 0.f;
-    if (i < B && c < d) q[i][c] = Q[(int64_t)i * d + c];
+    if (i < B && c < d) {
+      float v = 0.f;
+      for (int z = 0; z < nsum; ++z) v += Q[((int64_t)z * B + i) * d + c];  // slice order
+      q[i][c] = v;
+    }
   }
   __syncthreads();
   if (t >= 64) return;
@@ -208,25 +218,42 @@ __global__ __launch_bounds__(256) void gs_sweep_kernel(
   const float lam_c = (score_kind == 1 && lane < d) ? lam[lane] : 0.f;
   for (int i = 0; i < B; ++i) {
     // k(x_i, x_j') of the rows already moved: lane j
-    float s2 = 0.f;
+    // (both loops are LDS-latency chains: unrolled so the reads of several
+    // iterations are in flight together, two partial sums each)
+    float s2a = 0.f, s2b = 0.f;
+#pragma unroll 4
     for (int c4 = 0; c4 < d4; ++c4) {
       const f32x4 a = *reinterpret_cast<const f32x4*>(&xo[i][4 * c4]);
       const f32x4 b = *reinterpret_cast<const f32x4*>(&xn[lane][4 * c4]);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float df = a[u] - b[u];
-        s2 = fmaf(df, df, s2);
-      }
+      const float d0 = a[0] - b[0], d1 = a[1] - b[1], d2 = a[2] - b[2], d3 = a[3] - b[3];
+      s2a = fmaf(d0, d0, fmaf(d2, d2, s2a));
+      s2b = fmaf(d1, d1, fmaf(d3, d3, s2b));
     }
-    const float kj = lane < i ? __builtin_amdgcn_exp2f(s2 * scale) : 0.f;
+    const float kj = lane < i ? __builtin_amdgcn_exp2f((s2a + s2b) * scale) : 0.f;
     // lane c: the moved rows' terms
     const int c = lane < d ? lane : 0;
     const float xi = xo[i][c];
-    float acc = 0.f;
-    for (int j = 0; j < i; ++j) {
-      const float k = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kj), j));
-      acc = fmaf(k, fmaf(g, xi - xn[j][c], sn[j][c]), acc);
+    float acc0 = 0.f, acc1 = 0.f;
+    int j = 0;
+    for (; j + 8 <= i; j += 8) {
+      float xv[8], sv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        xv[u] = xn[j + u][c];
+        sv[u] = sn[j + u][c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float k = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kj), j + u));
+        const float tv = k * fmaf(g, xi - xv[u], sv[u]);
+        if (u & 1) acc1 += tv; else acc0 += tv;
+      }
     }
+    for (; j < i; ++j) {
+      const float k = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kj), j));
+      acc0 = fmaf(k, fmaf(g, xi - xn[j][c], sn[j][c]), acc0);
+    }
+    const float acc = acc0 + acc1;
     if (lane < d) {
       float p = inv_n * (q[i][c] + acc);
       if (extra) p += extra[(int64_t)i * lde + c];
@@ -272,7 +299,7 @@ int dsvgd_gs_block_part(const float* X, int64_t ldx, const float* S, int64_t lds
   hipLaunchKernelGGL(gs_part_kernel, dim3((unsigned)nsplit), dim3(256), 0, (hipStream_t)stream, X,
                      ldx, S, lds, n, (int)d, r0, (int)B, st, jchunk, partial);
   const int rc = check_launch("gs_part");
-  if (rc || nsplit == 1) return rc;
+  if (rc || nsplit == 1 || gs_fold(B, d, nsplit)) return rc;
   const int64_t elems = B * d;
   hipLaunchKernelGGL(gs_reduce_kernel, dim3((unsigned)((elems + 63) / 64)), dim3(256), 0,
                      (hipStream_t)stream, partial, elems, (int)nsplit);
@@ -293,7 +320,8 @@ int dsvgd_gs_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, int64_t n
   DSVGD_REQUIRE(!extra || lde >= d, "lde");
   DSVGD_REQUIRE(!phi_out || ldphi >= d, "ldphi");
   hipLaunchKernelGGL(gs_sweep_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, X, ldx, S, lds,
-                     n, (int)d, r0, (int)B, st, step, partial, extra, lde, phi_out,
+                     n, (int)d, r0, (int)B, st, step, partial, gs_fold(B, d, nsplit) ? (int)nsplit : 1,
+                     extra, lde, phi_out,
                      ldphi, score_kind, mu, lam, score_scale);
   return check_launch("gs_sweep");
 }

@@ -382,15 +382,16 @@ int dsvgd_phi_row_split(float* X, int64_t ldx, const float* S, int64_t lds, int6
  * (n x d).  gs_block_part: Q[i][c] = the raw sum over every j outside
  * [r0, r0 + i) of k(x_i, x_j) (s_j + (2/h)(x_i - x_j)) as the block starts,
  * computed as nsplit = dsvgd_gs_splits(n) j slices (partial: nsplit x B x d
- * floats of scratch) and summed in slice order into partial[0 .. B d);
+ * floats of scratch) and summed in slice order (into partial[0 .. B d) when
+ * B d nsplit > 16384, else by the sweep);
  * gs_block_sweep then walks the block in order in one wave: phi_i = (Q_i +
  * the terms of the block rows already moved, at their new positions) / n
  * [+ extra row i], X[r0+i] += step phi_i, and the moved particle's score
  * refreshed in S (score_kind 1: scale * (-lam (x - mu)), 2: the
  * experiments/gmm.py mixture per coordinate; 0: S left as is -- exchanged
- * scores are frozen for the step, distsampler.py:194-200).  Three launches
- * per 64 rows instead of two per row (dsvgd_phi_row_split).  nsplit of the
- * sweep: the gs_block_part call's (>= 1; only partial[0 .. B d) is read). */
+ * scores are frozen for the step, distsampler.py:194-200).  Two or three launches
+ * per 64 rows instead of two per row (dsvgd_phi_row_split).  nsplit, B, d of
+ * the sweep: those of the gs_block_part call. */
 int64_t dsvgd_gs_block_rows(void);
 int64_t dsvgd_gs_splits(int64_t n);
 int dsvgd_gs_block_part(const float* X, int64_t ldx, const float* S, int64_t lds, int64_t n,
