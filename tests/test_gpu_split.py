@@ -333,7 +333,7 @@ def test_phi_mm_h2_wide_column_range():
 
 @pytest.mark.parametrize("split", SPLIT)
 @pytest.mark.parametrize("n,N,p", [(1000, 3000, 20), (512, 16384, 255), (300, 129, 40),
-                                   (600, 2000, 1023), (257, 700, 511)])
+                                   (600, 2000, 1023), (257, 700, 511), (1000, 1000, 255)])
 def test_logreg_scores_split_as_accurate_as_f32(split, n, N, p):
     """The logreg score GEMMs (Z = W Xd^T on the split NT engine, G Xd on the
     split NN engine without exp) against the fp64 oracle, next to the f32 MFMA
@@ -402,3 +402,25 @@ def test_sqdist_split_as_accurate_as_f32(split, n, d, m, row0):
     e = float(np.max(np.abs(Dall[split] - Dall["f32"]) / scale))
     record_parity(e)
     assert e < 4e-6
+
+
+@pytest.mark.parametrize("n,N", [(1000, 1000), (200, 33), (4096, 8192)])
+def test_logreg_fused_tile_general_labels(n, N):
+    """The fused score tile (p = 255: Z -> sigma -> G.Xd without G in HBM,
+    csrc/logreg.hip logreg_fused_kernel) with labels that are not +-1 (t folded
+    into the data image: t sigma(-t z) xd = sigma(-z') xd', z' = t z), particle
+    and data counts off the 128 / 32 tiles, against fp64 and next to the f32
+    engine."""
+    p = 255
+    rs = np.random.RandomState(n + 7 * N)
+    X = (rs.randn(n, p + 1) * 0.3).astype(np.float32)
+    xd = (rs.randn(N, p) / np.sqrt(p)).astype(np.float32)
+    t = rs.uniform(-3.0, 3.0, N).astype(np.float32)
+    ref = O.score_logreg(X, xd, t)
+    err = {}
+    for gemm in ("f32", "h2"):
+        out = torch.zeros(n, p + 1, device=DEV)
+        dsvgd().targets.LogisticRegression(xd, t, gemm=gemm).score(gpu(X), out)
+        err[gemm] = float(np.abs(out.cpu().numpy() - ref).max() / np.abs(ref).max())
+    record_parity(err["h2"], f32=err["f32"])
+    assert err["h2"] <= 2.0 * err["f32"] + 1e-7 and err["h2"] < 1e-5, err
