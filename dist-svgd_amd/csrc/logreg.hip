@@ -45,17 +45,10 @@ static int64_t nn_cols(int64_t w) {
   return roundup(w, 512);
 }
 
-// the fused score tile (logreg_fused_kernel, below)
-constexpr int kFzQ = 32;                     // data rows per chunk
-constexpr int kFzHalf = 32 * 1024;           // A_Z or A_G of one chunk
-constexpr int kFzChunkBytes = 2 * kFzHalf;   // chunk image: [A_Z | A_G]
-// it serves p = 255 (pp = ldb = 256): the bench's and config D's shape
-static bool fused_ok(int64_t pp, int64_t ldb) { return pp == 256 && ldb == 256; }
-
 struct LogregWs {
   int64_t N, n_pad, N_pad, pp, ldb;
   size_t off_w, off_xd, off_t, off_g, off_gw, off_wx, off_xdx, off_xdy, off_rsw, off_riw, off_sxd,
-      off_sws, off_xdt, off_fimg, off_sfz, total;
+      off_sws, total;
 };
 
 // G . Xd (K = N data rows, 256-row blocks): split K so that a launch has
@@ -96,10 +89,6 @@ static LogregWs logreg_ws(int64_t n, int64_t N, int64_t p) {
   w.off_riw = take((size_t)w.n_pad);
   w.off_sxd = take((size_t)(2 * w.ldb + 3));
   w.off_sws = take(h2_colscale_ws_floats(w.N_pad, w.ldb));
-  // the fused tile (logreg_fused_kernel): t (.) Xd, its chunk images, scales
-  w.off_xdt = take((size_t)w.N_pad * w.ldb);
-  w.off_fimg = take((size_t)(w.N_pad / kFzQ) * kFzChunkBytes / 4);
-  w.off_sfz = take((size_t)(2 * w.ldb + 3));
   w.total = o;
   return w;
 }
@@ -115,14 +104,30 @@ __global__ __launch_bounds__(256) void pad_copy_kernel(const float* __restrict__
   dst[t] = (r < rows && c < cols) ? src[r * lds + c0 + c] : 0.f;
 }
 
+// Xd[q][:] *= t[q] (then set_ones_kernel makes t = 1: rows past N had t = 0,
+// so they stay zero rows); the Z epilogue's t_q sigma(-t_q z) is then
+// sigma(-z') on the folded data.
+__global__ __launch_bounds__(256) void fold_labels_kernel(float* __restrict__ Xd,
+                                                          const float* __restrict__ t,
+                                                          int64_t rows, int64_t ld) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e < rows * ld) Xd[e] *= t[e / ld];
+}
+
+__global__ __launch_bounds__(256) void set_ones_kernel(float* __restrict__ v, int64_t n) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e < n) v[e] = 1.f;
+}
+
 __device__ __forceinline__ float sigmoidf_stable(float u) {
   if (u >= 0.f) return 1.f / (1.f + expf(-u));
   const float e = expf(u);
   return e / (1.f + e);
 }
 
-// G[j][q] = t_q sigma(-t_q (w_j . xd_q)) = t_q / (1 + exp(t_q z)), zero for
-// padded q (t_q = 0 there); panel layout.  The epilogue is VALU work beside
+// G[j][q] = t_q sigma(-t_q (w_j . xd_q)) = t_q / (1 + exp(t_q z)); after
+// logreg_prepare's fold (xd' = t xd, t = 1) this is sigma(-z') in (0, 1), and
+// padded q hold sigma(0) against a zero data row; panel layout.  The epilogue is VALU work beside
 // the other resident blocks' f32 MFMAs (they share the SIMD's issue), so it
 // is kept short: exp2 + rcp (~1 ulp each) and store addresses that are one
 // per-lane base plus compile-time offsets (as the distance epilogue).
@@ -280,206 +285,6 @@ __global__ __launch_bounds__(256) void logreg_z_kernel(const float* __restrict__
   ZTile tile;
   tile.run(W + i0 * ldb, ldb, Xd + q0 * ldb, ldb, pp, smem);
   z_epilogue(tile, i0, q0, tp, N_pad, G);
-}
-
-// ---- the fused score tile: Z -> sigma -> G.Xd without G in HBM -----------
-// With xd'_q = t_q xd_q and z' = w . xd' = t z, the score's data term is
-//   sum_q t_q sigma(-t_q z_q) xd_q = sum_q sigma(-z'_q) xd'_q,
-// so one block of 128 particles streams the data in chunks of kFzQ = 32 rows:
-//   Z-phase  zT[q][i] = Xd'_chunk . W^T          (K = p = 256, 48 MFMAs per wave)
-//   G'[q][i] = 2^15 sigma(-z'[q][i]), split into two fp16 parts in registers
-//   G-phase  accT[c][i] += Xd'^T_chunk . G'      (K = 32, 8 column blocks, 48 MFMAs)
-// One wave per SIMD; wave w owns particles 32 w .. +31 of the block, its
-// 32 x 256 W rows held as FmtH2 B fragments in 128 VGPRs for the whole
-// launch, the G-phase accumulators (256 columns x its 32 particles) in 128
-// AGPRs.  G' never leaves the registers: the Z-phase's C layout (lane: one
-// particle, 16 data rows q = 8 (e >> 2) + 4 h + (e & 3)) IS the G-phase's B
-// operand once the k order of the G-phase is permuted to match -- the chunk
-// image's A_G part is written in that q order (logreg_fused_image_kernel).
-// The data images stream through two 2-slot LDS-DMA rings (A_Z of chunk
-// c + 1 beside A_G of chunk c: the Z-phase of the next chunk runs with the
-// sigmoid of this one spread between its MFMAs, then this chunk's G-phase).
-// Replaces logreg_z_x3p_kernel + the G.Xd launch at p = 255 (pp = ldb = 256):
-// no 4 n N bytes of G written and read back.
-
-// Xd'[q][c] = t_q Xd[q][c] (padded rows: t = 0)
-__global__ __launch_bounds__(256) void scale_rows_kernel(const float* __restrict__ A,
-                                                         const float* __restrict__ tq,
-                                                         int64_t rows, int64_t ld,
-                                                         float* __restrict__ out) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e < rows * ld) out[e] = tq[e / ld] * A[e];
-}
-
-// chunk image of Xd' (N_pad x 256, ld 256), 16-byte items:
-//   A_Z[part][ks][q][16 k] = parts of tz Xd'[32 ch + q][16 ks + k]   (item: ks, q, half)
-//   A_G[part][kg][c][16 k] = parts of s_c Xd'[32 ch + q(kg, k)][c],
-//     q(kg, 8 h + j) = 16 kg + 8 (j >> 2) + 4 h + (j & 3)          (item: kg, c, half)
-// halves swapped on rows / columns with bit 3 set (x3_off); sfz: h2_colscale
-// layout of Xd' ([s_c | 1/s_c | tz | 1/tz]).
-__global__ __launch_bounds__(256) void logreg_fused_image_kernel(const float* __restrict__ Xt,
-                                                                 const float* __restrict__ sfz,
-                                                                 int64_t nchunks,
-                                                                 char* __restrict__ img) {
-  const int64_t item = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (item >= nchunks * 2048) return;
-  const int64_t ch = item / 2048;
-  const int it = (int)(item % 2048);
-  char* base = img + ch * kFzChunkBytes;
-  float v[8];
-  int off;
-  if (it < 1024) {  // A_Z
-    const int ks = it >> 6, q = (it >> 1) & 31, hh = it & 1;
-    const float tz = sfz[2 * 256];
-    const float* src = Xt + (ch * kFzQ + q) * 256 + 16 * ks + 8 * hh;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = tz * src[j];
-    off = ks * 1024 + x3_off(q, hh);
-  } else {  // A_G
-    const int i2 = it - 1024;
-    const int kg = i2 >> 9, c = (i2 >> 1) & 255, hh = i2 & 1;
-    const float sc = sfz[c];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int q = 16 * kg + 8 * (j >> 2) + 4 * hh + (j & 3);
-      v[j] = sc * Xt[(ch * kFzQ + q) * 256 + c];
-    }
-    base += kFzHalf;
-    off = kg * 8192 + x3_off(c, hh);
-  }
-  FmtH2::V8 p0, p1;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const _Float16 a = (_Float16)v[j];
-    p0[j] = a;
-    p1[j] = (_Float16)(v[j] - (float)a);
-  }
-  // part 1 sits half an image (16 KiB) after part 0 in both halves
-  *reinterpret_cast<FmtH2::V8*>(base + off) = p0;
-  *reinterpret_cast<FmtH2::V8*>(base + kFzHalf / 2 + off) = p1;
-}
-
-// Wx: logreg's FmtH2 W row image ([ks][part][row][16 k], n_img rows, per-row
-// scales: riw[i] = 1 / s_i); img: the chunk images; sfz: Xd''s scales.
-// GW[i][c] (ld 256) = sum_q sigma(-z'_iq) Xd'[q][c] for i < n.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void logreg_fused_kernel(
-    const _Float16* __restrict__ Wx, int64_t n_img, const float* __restrict__ riw,
-    const char* __restrict__ img, int nchunks, const float* __restrict__ sfz, int64_t n,
-    float* __restrict__ GW) {
-  using V8 = FmtH2::V8;
-  __shared__ __attribute__((aligned(16))) char smem[4 * kFzHalf];  // A_Z ring, A_G ring
-  char* const zring = smem;
-  char* const gring = smem + 2 * kFzHalf;
-  const int t = threadIdx.x, lane = t & 63, r = lane & 31, h = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int64_t i = (int64_t)blockIdx.x * 128 + 32 * w + r;  // this lane's particle
-  // the wave's W fragments (B operand of the Z-phase): [K-step][part]
-  V8 wb[16][2];
-  {
-    const __amdgpu_buffer_rsrc_t rW =
-        __builtin_amdgcn_make_buffer_rsrc((void*)Wx, (short)0, 0x7fffffff, 0x00020000);
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks)
-#pragma unroll
-      for (int p = 0; p < 2; ++p)
-        wb[ks][p] = __builtin_bit_cast(
-            V8, __builtin_amdgcn_raw_buffer_load_b128(
-                    rW, (int)(((int64_t)(2 * ks + p) * n_img) * 32 + x3_off((int)i, h)), 0, 0));
-  }
-  // z' = acc riw_i / tz; G' = 2^15 / (1 + exp(z'))
-  const float zc = kLog2e * riw[i] * sfz[2 * 256 + 1];
-  f32x16 acc[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) acc[c] = f32x16{};
-  const __amdgpu_buffer_rsrc_t rI =
-      __builtin_amdgcn_make_buffer_rsrc((void*)img, (short)0, 0x7fffffff, 0x00020000);
-  // one half (A_Z or A_G) of chunk ch -> LDS: 8 x 1 KiB per wave
-  auto dma = [&](int ch, int half, char* dst) {
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int off = (w * 8 + u) * 1024;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rI, (__attribute__((address_space(3))) void*)(dst + off), 16, off + lane * 16,
-          ch * kFzChunkBytes + half * kFzHalf, 0, 0);
-    }
-  };
-  // G' of one z value: its two fp16 parts
-  auto sig = [&](float zv, V8 (&g)[2][2], int e) {
-    const float ex = __builtin_amdgcn_exp2f(zv * zc);
-    const float gv = FmtH2::kAScale * __builtin_amdgcn_rcpf(1.f + ex);
-    const _Float16 g0 = (_Float16)gv;
-    g[e >> 3][0][e & 7] = g0;
-    g[e >> 3][1][e & 7] = (_Float16)(gv - (float)g0);
-  };
-  // Z-phase of the chunk whose A_Z sits at az (zT[q][i], K = 256) with the
-  // previous chunk's z (zp) turned into G' between its MFMAs, one value per
-  // K-step -- the G-phase's B fragments g[K-step][part] (lane's value e is
-  // data row 8 (e >> 2) + 4 h + (e & 3): K-step e >> 3, element e & 7)
-  auto zphase = [&](const char* az, f32x16& z, const f32x16& zp, V8 (&g)[2][2]) {
-    z = f32x16{};
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) {
-      const V8 a0 = *reinterpret_cast<const V8*>(az + ks * 1024 + x3_off(r, h));
-      const V8 a1 = *reinterpret_cast<const V8*>(az + kFzHalf / 2 + ks * 1024 + x3_off(r, h));
-      z = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, wb[ks][0], z, 0, 0, 0);
-      sig(zp[ks], g, ks);
-      z = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, wb[ks][1], z, 0, 0, 0);
-      z = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, wb[ks][0], z, 0, 0, 0);
-    }
-  };
-  auto gphase = [&](const char* ag, const V8 (&g)[2][2]) {
-#pragma unroll
-    for (int kg = 0; kg < 2; ++kg)
-#pragma unroll
-      for (int cb = 0; cb < 8; ++cb) {
-        const V8 a0 = *reinterpret_cast<const V8*>(ag + kg * 8192 + x3_off(32 * cb + r, h));
-        const V8 a1 = *reinterpret_cast<const V8*>(ag + kFzHalf / 2 + kg * 8192 + x3_off(32 * cb + r, h));
-        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, g[kg][0], acc[cb], 0, 0, 0);
-        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, g[kg][1], acc[cb], 0, 0, 0);
-        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, g[kg][0], acc[cb], 0, 0, 0);
-      }
-  };
-
-  // prologue: A_Z(0) -> z = z(0); A_Z(1), A_G(0) DMA'd
-  f32x16 z, zp;
-  V8 g[2][2];
-  dma(0, 0, zring);
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  if (nchunks > 1) dma(1, 0, zring + kFzHalf);
-  dma(0, 1, gring);
-  zphase(zring, z, z, g);  // (its G' values are discarded)
-  // chunk c: A_Z(c+1) in zring[(c+1)&1], A_G(c) in gring[c&1], z = z(c).
-  // One barrier per chunk: after it every wave's DMAs of the last iteration
-  // have landed AND every wave is past the last iteration's LDS reads, so
-  // the slots those reads used are refilled (for chunk c + 2's A_Z and
-  // chunk c + 1's A_G) right after it, a whole iteration ahead of their use
-  for (int c = 0; c < nchunks; ++c) {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (c + 2 < nchunks) dma(c + 2, 0, zring + (c & 1) * kFzHalf);
-    if (c + 1 < nchunks) dma(c + 1, 1, gring + ((c + 1) & 1) * kFzHalf);
-    zp = z;
-    if (c + 1 < nchunks) {
-      zphase(zring + ((c + 1) & 1) * kFzHalf, z, zp, g);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) sig(zp[e], g, e);
-    }
-    gphase(gring + (c & 1) * kFzHalf, g);
-  }
-  // GW[i][c] = acc * (1 / s_c) * 2^-15: lane's column i, rows c = 32 cb + 8 g + 4 h + e
-  if (i < n) {
-#pragma unroll
-    for (int cb = 0; cb < 8; ++cb)
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const int c0 = 32 * cb + 8 * gq + 4 * h;
-        const f32x4 ci = *reinterpret_cast<const f32x4*>(sfz + 256 + c0);
-        f32x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = acc[cb][4 * gq + e] * ci[e] * (1.f / FmtH2::kAScale);
-        *reinterpret_cast<f32x4*>(GW + i * 256 + c0) = o;
-      }
-  }
 }
 
 // one wave per particle row
@@ -705,25 +510,19 @@ static int logreg_prepare(const float* Xd, int64_t ldxd, const float* t, int64_t
   hipLaunchKernelGGL(pad_copy_kernel, dim3((w.N_pad + 255) / 256), dim3(256), 0, s, t, 1, 0, N, 1,
                      w.N_pad, tp, 1);
   if ((rc = check_launch("pad_copy(t)"))) return rc;
+  // t folded into the data: t_q sigma(-t_q z_q) xd_q = sigma(-z'_q) xd'_q with
+  // xd' = t xd, z' = w . xd' -- so G = sigma(-z') lies in (0, 1) whatever the
+  // labels (the FmtH2 A image of G holds 2^15 G: |t| > 2 would overflow fp16)
+  hipLaunchKernelGGL(fold_labels_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Xdp, tp, w.N_pad,
+                     w.ldb);
+  if ((rc = check_launch("fold_labels"))) return rc;
+  hipLaunchKernelGGL(set_ones_kernel, dim3((w.N_pad + 255) / 256), dim3(256), 0, s, tp, w.N_pad);
+  if ((rc = check_launch("set_ones(t)"))) return rc;
   if (P.h2) {
     float* sxd = (float*)(P.base + w.off_sxd);
     float* sws = (float*)(P.base + w.off_sws);
     if ((rc = h2_colscale(Xdp, w.ldb, w.N_pad, w.ldb, sws, sxd, s))) return rc;
     // the tensor scale for Z's Xd image, per-column ones for G . Xd's B image
-    if (fused_ok(w.pp, w.ldb)) {
-      // the fused tile's chunk images of Xd' = t (.) Xd and their scales
-      float* xdt = (float*)(P.base + w.off_xdt);
-      float* sfz = (float*)(P.base + w.off_sfz);
-      const int64_t tot2 = w.N_pad * w.ldb;
-      hipLaunchKernelGGL(scale_rows_kernel, dim3((tot2 + 255) / 256), dim3(256), 0, s, Xdp, tp,
-                         w.N_pad, w.ldb, xdt);
-      if ((rc = check_launch("scale_rows"))) return rc;
-      if ((rc = h2_colscale(xdt, w.ldb, w.N_pad, w.ldb, sws, sfz, s))) return rc;
-      const int64_t nch = w.N_pad / kFzQ;
-      hipLaunchKernelGGL(logreg_fused_image_kernel, dim3((unsigned)((nch * 2048 + 255) / 256)),
-                         dim3(256), 0, s, xdt, sfz, nch, P.base + w.off_fimg);
-      return check_launch("logreg_fused_image");
-    }
     if ((rc = h2_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, sxd + 2 * w.ldb,
                           P.base + w.off_xdx, s)))
       return rc;
@@ -758,16 +557,6 @@ static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float 
     // aligned 16-byte windows), one power-of-two scale per particle row
     if ((rc = h2_rowscale(X + 1, ldx, n, p, w.n_pad, rsw, riw, s))) return rc;
     if ((rc = h2_rowsplit_rows(X + 1, ldx, n, p, w.n_pad, w.pp, rsw, Wx, s))) return rc;
-    if (fused_ok(w.pp, w.ldb)) {
-      hipLaunchKernelGGL(logreg_fused_kernel, dim3((unsigned)(w.n_pad / 128)), dim3(256), 0, s,
-                         (const _Float16*)Wx, w.n_pad, (const float*)riw,
-                         (const char*)(base + w.off_fimg), (int)(w.N_pad / kFzQ),
-                         (const float*)(base + w.off_sfz), n, GW);
-      if ((rc = check_launch("logreg_fused"))) return rc;
-      hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,
-                         w.ldb, scale, S, lds, 1);
-      return check_launch("logreg_finish");
-    }
     int blocks = 0;
     if ((rc = persistent_blocks(reinterpret_cast<const void*>(&logreg_z_x3p_kernel<FmtH2>),
                                 &blocks, 512)))

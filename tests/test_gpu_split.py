@@ -405,12 +405,12 @@ def test_sqdist_split_as_accurate_as_f32(split, n, d, m, row0):
 
 
 @pytest.mark.parametrize("n,N", [(1000, 1000), (200, 33), (4096, 8192)])
-def test_logreg_fused_tile_general_labels(n, N):
-    """The fused score tile (p = 255: Z -> sigma -> G.Xd without G in HBM,
-    csrc/logreg.hip logreg_fused_kernel) with labels that are not +-1 (t folded
-    into the data image: t sigma(-t z) xd = sigma(-z') xd', z' = t z), particle
-    and data counts off the 128 / 32 tiles, against fp64 and next to the f32
-    engine."""
+def test_logreg_scores_general_labels(n, N):
+    """Labels that are not +-1 (logreg_prepare folds t into the data:
+    t sigma(-t z) xd = sigma(-z') xd' with z' = t z, so the FmtH2 image of G
+    holds 2^15 sigma in (0, 2^15) whatever |t| -- unfolded, |t| > 2 overflowed
+    fp16), particle and data counts off the tiles, at p = 255, against fp64
+    and next to the f32 engine."""
     p = 255
     rs = np.random.RandomState(n + 7 * N)
     X = (rs.randn(n, p + 1) * 0.3).astype(np.float32)
