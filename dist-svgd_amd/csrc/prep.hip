@@ -185,7 +185,9 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return v;
 }
 
-template <bool VX, bool VS>  // 16-byte loads of X / S rows (aligned, ld % 4 == 0)
+// VX / VS: 16-byte loads of X / S rows (aligned, ld % 4 == 0); NQ: the
+// 256-column passes ldy needs (<= kPackQ: registers for those only)
+template <bool VX, bool VS, int NQ>
 __global__ __launch_bounds__(256) void pack_kernel(
     const float* __restrict__ X, int64_t ldx, const float* __restrict__ S, int64_t lds,
     float scale, const float* __restrict__ mean, int64_t n, int64_t d, int64_t rows_pad,
@@ -198,18 +200,16 @@ __global__ __launch_bounds__(256) void pack_kernel(
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
   const int64_t r1 = min(r0 + rpb, rows_pad);
   const int64_t c_lo = X ? 0 : dp, c_hi = X ? ldy : 2 * dp;
-  uint32_t mx[kPackQ][4];
+  uint32_t mx[NQ][4];
 #pragma unroll
-  for (int q = 0; q < kPackQ; ++q)
+  for (int q = 0; q < NQ; ++q)
 #pragma unroll
     for (int e = 0; e < 4; ++e) mx[q][e] = 0u;
   uint32_t rminx = 0x7F800000u, rmins = 0x7F800000u;  // +inf
-  for (int64_t j = r0 + w; j < r1; j += 4) {
-    float nrm = 0.f;
-    uint32_t rx = 0u, rs = 0u;  // this row's largest |entry| per half
-    f32x4 v[kPackQ];
+  // row j's 16-byte pieces (zero past n / outside the halves read)
+  auto load_row = [&](int64_t j, f32x4 (&v)[NQ]) {
 #pragma unroll
-    for (int q = 0; q < kPackQ; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       const int64_t c = 4 * lane + 256 * q;
       v[q] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (c >= ldy || j >= n) continue;
@@ -234,8 +234,12 @@ __global__ __launch_bounds__(256) void pack_kernel(
         }
       }
     }
+  };
+  auto store_row = [&](int64_t j, const f32x4 (&v)[NQ]) {
+    float nrm = 0.f;
+    uint32_t rx = 0u, rs = 0u;  // this row's largest |entry| per half
 #pragma unroll
-    for (int q = 0; q < kPackQ; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       const int64_t c = 4 * lane + 256 * q;
       if (c >= ldy || c < c_lo || c >= c_hi) continue;
       *reinterpret_cast<f32x4*>(Y + j * ldy + c) = v[q];
@@ -264,11 +268,25 @@ __global__ __launch_bounds__(256) void pack_kernel(
       }
       if (X && rsc && lane == 0) rsc[j] = pow2_scale(j < n ? __uint_as_float(rx) : 0.f);
     }
+  };
+  // two rows in flight per wave: the next row's loads are issued before this
+  // row's reductions (one row at a time left each wave waiting out a full
+  // HBM latency per row: ~2 TB/s)
+  f32x4 va[NQ], vb[NQ];
+  int64_t j = r0 + w;
+  if (j < r1) load_row(j, va);
+  for (; j < r1; j += 8) {
+    const int64_t j2 = j + 4;
+    if (j2 < r1) load_row(j2, vb);
+    store_row(j, va);
+    if (j2 >= r1) break;
+    if (j2 + 4 < r1) load_row(j2 + 4, va);
+    store_row(j2, vb);
   }
   if (partial == nullptr) return;
   uint32_t gx = 0u, gs = 0u;
 #pragma unroll
-  for (int q = 0; q < kPackQ; ++q) {
+  for (int q = 0; q < NQ; ++q) {
     const int64_t c = 4 * lane + 256 * q;
     if (c >= ldy) continue;
 #pragma unroll
@@ -448,15 +466,21 @@ int dsvgd_pack_h2(const float* X, int64_t ldx, const float* S, int64_t lds, floa
   const bool vs = S && ((uintptr_t)S & 15) == 0 && lds % 4 == 0;
   const dim3 grid((unsigned)dsvgd_pack_blocks(rows_pad));
   const size_t lds_bytes = partial ? 4 * sizeof(uint32_t) * (size_t)ldy : 0;
-#define DSVGD_PACK(VX, VS)                                                                    \
-  hipLaunchKernelGGL((pack_kernel<VX, VS>), grid, dim3(256), lds_bytes, s, X, ldx, S, lds,    \
+#define DSVGD_PACK_Q(VX, VS, NQ)                                                              \
+  hipLaunchKernelGGL((pack_kernel<VX, VS, NQ>), grid, dim3(256), lds_bytes, s, X, ldx, S, lds, \
                      score_scale, mean, n, d, rows_pad, dp, Y, ldy, norms, partial, gmax,      \
                      rowscale)
-  if (vx && vs) DSVGD_PACK(true, true);
-  else if (vx) DSVGD_PACK(true, false);
-  else if (vs) DSVGD_PACK(false, true);
-  else DSVGD_PACK(false, false);
+#define DSVGD_PACK(VX, VS)                                                                    \
+  if (ldy <= 256) DSVGD_PACK_Q(VX, VS, 1);                                                    \
+  else if (ldy <= 512) DSVGD_PACK_Q(VX, VS, 2);                                               \
+  else if (ldy <= 1024) DSVGD_PACK_Q(VX, VS, 4);                                              \
+  else DSVGD_PACK_Q(VX, VS, 8);
+  if (vx && vs) { DSVGD_PACK(true, true) }
+  else if (vx) { DSVGD_PACK(true, false) }
+  else if (vs) { DSVGD_PACK(false, true) }
+  else { DSVGD_PACK(false, false) }
 #undef DSVGD_PACK
+#undef DSVGD_PACK_Q
   return check_launch("pack");
 }
 
