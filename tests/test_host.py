@@ -31,6 +31,19 @@ def test_library_exports_every_declared_symbol():
     assert sorted(_native.SIGNATURES) == names
 
 
+def test_integration_stub_matches_bindings():
+    """INTEGRATION.md's ctypes stub (what a maintainer would paste) declares
+    the same argument counts as dsvgd/_native.py for every symbol it binds."""
+    from dsvgd import _native
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    stub = re.findall(r"lib\.(dsvgd_\w+)\.argtypes = \[([^\]]*)\]", doc)
+    assert len(stub) >= 15
+    for name, args in stub:
+        n_doc = len([a for a in args.replace("\n", " ").split(",") if a.strip()])
+        assert name in _native.SIGNATURES, name
+        assert n_doc == len(_native.SIGNATURES[name][1]), (name, n_doc)
+
+
 def test_meta_calls_without_gpu():
     from dsvgd import _native
     from dsvgd.engine import _SelectState
