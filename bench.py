@@ -61,6 +61,10 @@ def engine_peak(gemm):
             "%s dense MFMA %.1f TF / %d split products" % ("fp16" if gemm == "h2" else "bf16",
                                                           PEAK_BF16_MFMA_TFLOPS, k))
 PEAK_HBM_GBS = 8000.0
+# what the chip sustains on bare back-to-back v_mfma_f32_32x32x16_f16 with
+# random operands, one wave per SIMD on every CU (the clock it holds under
+# that load): scripts/mfma_shape_probe.hip, profiles/r9b/mfma_probe.log
+SUSTAINED_F16_MFMA_TFLOPS = 1724.0
 
 
 def synthetic_data(N, p, seed=0):
@@ -371,6 +375,10 @@ def main(argv=None):
                      "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "peak_basis": peak_basis,
                      "frac": achieved / peak, "frac_of_f32_mfma_peak": achieved / PEAK_FP32_MFMA_TFLOPS,
+                     "frac_of_sustained_mfma": (achieved / (SUSTAINED_F16_MFMA_TFLOPS / SPLIT_PRODUCTS[gemm])
+                                                if gemm in SPLIT_PRODUCTS else None),
+                     "sustained_basis": "bare fp16 32x32x16 MFMA loop under DVFS, 1724 TF "
+                                        "(profiles/r9b/mfma_probe.log) / split products",
                      "traffic": traffic,
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                      "algorithmic_bytes": 4.0 * m * n + 4.0 * (n + 128) * 512,
