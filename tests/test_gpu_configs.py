@@ -141,7 +141,7 @@ def test_config_D_bench_step():
     check_step(ds, eng, X0, S_ref, eps, rows)
 
 
-def _shard_worker(rank, S, port, q):
+def _shard_worker(rank, S, port, q, nrows=256):
     import os
     import sys
     import torch.distributed as dist
@@ -165,7 +165,7 @@ def _shard_worker(rank, S, port, q):
     ds.make_step(eps)
     torch.cuda.synchronize()
     eng = next(iter(ds._engines.values()))
-    rows = np.sort(np.random.RandomState(20 + rank).choice(n // S, 256, replace=False))
+    rows = np.sort(np.random.RandomState(20 + rank).choice(n // S, nrows, replace=False))
     ridx = torch.as_tensor(rows, device=DEV)
     s0 = ds._particle_start_idx
     out = {"rows": s0 + rows, "own_rows": rows, "h": eng.state.read()[1],
@@ -177,20 +177,23 @@ def _shard_worker(rank, S, port, q):
     dist.destroy_process_group()
 
 
-def test_config_D_sharded_two_ranks():
-    """config 4 (dist-logreg) sharded at full size, S = 2
-    ranks sharing cuda:0 over gloo: each owns 32768 of n = 65536 particles
-    (full-layout row block, phi_w1, split-K) and N / 2 data rows; the scores
-    are the all-reduced sum of both ranks' local-data scores (prior counted
-    twice, distsampler.py:160-170); the bandwidth is the median of the whole
-    n x n matrix through the histogram all-reduce.  Per rank 256 sampled rows
-    of scores, phi and the update vs fp64; the median vs fp64 distances."""
+@pytest.mark.parametrize("S", [2, 4, 8])
+def test_config_D_sharded(S):
+    """config 4 (dist-logreg) sharded at full size, S
+    ranks sharing cuda:0 over gloo: each owns n / S of n = 65536 particles
+    (full-layout row block: its diagonal square and the rectangles beside it,
+    phi_w1, split-K) and N / S data rows; the scores are the all-reduced sum
+    of every rank's local-data scores (prior counted S times,
+    distsampler.py:160-170); the bandwidth is the median of the whole n x n
+    matrix through the histogram all-reduce.  Per rank 512 / S sampled rows of
+    scores, phi and the update vs fp64; the median vs fp64 distances."""
     from bench import synthetic_data
     import torch.multiprocessing as mp
-    S, n, d, Ng, eps = 2, 65536, 256, 16384, 1e-4
+    n, d, Ng, eps = 65536, 256, 16384, 1e-4
+    nrows = 512 // S
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_shard_worker, args=(r, S, 29980, q)) for r in range(S)]
+    ps = [ctx.Process(target=_shard_worker, args=(r, S, 29970 + S, q, nrows)) for r in range(S)]
     for p in ps:
         p.start()
     res = sorted([q.get(timeout=600) for _ in range(S)], key=lambda r: r[0])
