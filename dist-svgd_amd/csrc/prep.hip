@@ -199,7 +199,9 @@ __global__ __launch_bounds__(256) void pack_kernel(
   const int64_t rpb = pack_rows_per_block(rows_pad);
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
   const int64_t r1 = min(r0 + rpb, rows_pad);
-  const int64_t c_lo = X ? 0 : dp, c_hi = X ? ldy : 2 * dp;
+  // X alone: the X half only (the S half is written by the pack of the
+  // scores that follows, or not read); both: the whole row, pad columns zero
+  const int64_t c_lo = X ? 0 : dp, c_hi = X ? (S ? ldy : dp) : 2 * dp;
   uint32_t mx[NQ][4];
 #pragma unroll
   for (int q = 0; q < NQ; ++q)

@@ -278,7 +278,9 @@ class PhiEngine(object):
 
     # ------------------------------------------------------------ stages --
     def pack(self, X, S=None, score_scale=1.0):
-        """X, S: (n, d) device tensors (row stride may exceed d)."""
+        """X, S: (n, d) device tensors (row stride may exceed d).  S=None packs
+        the X half only and leaves Y's S half as it was (pack_scores fills it
+        before direction(); the distances read only the X half)."""
         assert X.shape == (self.n, self.d)
         s = N.stream(self.device)
         with span(self.timer, "pack"):
