@@ -112,6 +112,35 @@ def test_config_C_gaussian_median_step():
     check_step(ds, eng, X0, O.score_gaussian(X0, mu, lam), eps, rows)
 
 
+def test_config_C_sequential_full_size():
+    """Config C in the reference's default Gauss-Seidel order at full size
+    (n = 16384, d = 64, Gaussian target refreshed after every move, median h
+    of the step's starting particles): one DistSampler step through the
+    blocked sweep (csrc/gs.hip) against the fp64 sequential restatement of
+    row updates (sampler.py:64-68), every one of the 16384 rows compared."""
+    n, d, eps = 16384, 64, 1e-2
+    mu = np.random.RandomState(1).randn(d).astype(np.float32)
+    lam = np.random.RandomState(2).uniform(0.5, 2, d).astype(np.float32)
+    X0 = np.random.RandomState(0).randn(n, d).astype(np.float32)
+    ds = dsvgd().DistSampler(0, 1, dsvgd().targets.Gaussian(mu, lam), dsvgd().RBF("median"),
+                             gpu(X0), n, n, exchange_particles=False, exchange_scores=False,
+                             include_wasserstein=False, order="sequential")
+    ds.make_step(eps)
+    torch.cuda.synchronize()
+    eng = next(iter(ds._engines.values()))
+    med, h = check_median_by_counting(eng, n)
+    got = ds.particles.cpu().numpy().astype(np.float64)
+    X = X0.astype(np.float64)
+    S = O.score_gaussian(X, mu, lam)
+    rows = n
+    for i in range(rows):
+        X[i] += eps * O.phi(X, S, h, rows=[i])[0]
+        S[i] = O.score_gaussian(X[i:i + 1], mu, lam)[0]
+    e = float(np.abs(got[:rows] - X[:rows]).max())
+    record_parity(e)
+    assert e < 1e-4, e
+
+
 def test_config_D_bench_step():
     """The bench's workload, one step on the bench's own inputs: DistSampler
     all_scores (at S = 1: the local scores of all n particles), Jacobi,
