@@ -223,6 +223,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc((void*)D, (short)0, 0, 0x00020000);
   int64_t eslot = -1;
   bool ew2 = false;
+  bool ediag = false;  // the wave's tile region holds diagonal entries (i == j)
   float* const colbase = reinterpret_cast<float*>(smem + GramW1::kColOff) + w * 128;
   GramSlotWriter<GramW1::kCandDepth> sw;
   float* const cstage = reinterpret_cast<float*>(smem + GramW1::kCandOff) + w * 64 * GramW1::kCandDepth;
@@ -263,6 +264,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                                            0x00020000);
     eslot = slot_base + un.L * GramW1::kSlots + w;
     ew2 = SYM && Jt != un.I;
+    ediag = valid && gj0 + 64 > gi0 && gj0 < gi0 + 128;
   };
 
   // runs g (columns 4 h + 0..3) and g + 1 (8 + 4 h + 0..3) of panel
@@ -273,6 +275,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   auto store_slice = [&](f32x4 (&v)[2], auto SL_) {
     constexpr int SL = decltype(SL_)::value;
     constexpr int bi = SL >> 2, bj = (SL >> 1) & 1;
+    // no select accounting: the diagonal (i == j) set to exactly 0 here, on
+    // the tiles that hold it only (a wave-uniform branch) instead of a
+    // compare + select per value between the MFMAs: the Gram without the
+    // median select 3.92 -> 3.61 ms (profiles/r9u).  With the accounting the
+    // per-value form stays (measured: no gain there)
+    if (!kBr && ediag) {
+      const int tgv = tg[bi];
+#pragma unroll
+      for (int gg = 0; gg < 2; ++gg) {
+        const int g = 2 * (SL & 1) + gg;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (tgv == e + 8 * g + 32 * bj) v[gg][e] = 0.f;
+      }
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const auto sv = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[0][e]),
@@ -293,7 +310,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   auto slice = [&](auto S_, auto SL_) {
     constexpr int S = decltype(S_)::value, SL = decltype(SL_)::value;
     constexpr int bi = SL >> 2, bj = (SL >> 1) & 1;
-    // per-slice copies (keeps the compiler from hoisting 16 compare masks
+    // per-slice copies (keeps the compiler from hoisting the row values
     // and products of them over the whole tile into SGPRs; not volatile: a
     // side-effecting asm would cut the K-step's scheduling region in two)
     int tgv = tg[bi];
@@ -312,7 +329,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         float a;
         asm("v_accvgpr_read_b32 %0, %1" : "=v"(a) : "a"(acc[S][bi][bj][4 * g + e]));
         const float x = fmaxf(0.f, (nrv + cn[e]) - siv * (cs[e] * a));
-        v[gg][e] = tgv == e + 8 * g + 32 * bj ? 0.f : x;
+        v[gg][e] = (kBr && tgv == e + 8 * g + 32 * bj) ? 0.f : x;
       }
       if constexpr (kBr) {
 #pragma unroll
@@ -425,7 +442,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         float av;
         asm("v_accvgpr_read_b32 %0, %1" : "=v"(av) : "a"(acc[E][ebi][ebj][4 * g + e]));
         const float x = fmaxf(0.f, (nrv + cn[gg][e]) - siv * (cs[gg][e] * av));
-        v[gg][e] = tgv == e + 8 * g + 32 * ebj ? 0.f : x;
+        v[gg][e] = (kBr && tgv == e + 8 * g + 32 * ebj) ? 0.f : x;
         if constexpr (kBr) {
           sw.add(v[gg][e]);
           // settle the per-lane counts here: left alone, the compiler defers
