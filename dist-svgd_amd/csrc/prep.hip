@@ -199,9 +199,13 @@ __global__ __launch_bounds__(256) void pack_kernel(
   const int64_t rpb = pack_rows_per_block(rows_pad);
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
   const int64_t r1 = min(r0 + rpb, rows_pad);
-  // X alone: the X half only (the S half is written by the pack of the
-  // scores that follows, or not read); both: the whole row, pad columns zero
-  const int64_t c_lo = X ? 0 : dp, c_hi = X ? (S ? ldy : dp) : 2 * dp;
+  // the columns this launch owns -- both: the whole row, pad columns zero;
+  // X alone: all but the S half (written by the pack of the scores that
+  // follows, or not read); S alone: the S half only
+  auto owns = [&](int64_t c) {
+    const bool sh = c >= dp && c < 2 * dp;
+    return X ? (S != nullptr || !sh) : sh;
+  };
   uint32_t mx[NQ][4];
 #pragma unroll
   for (int q = 0; q < NQ; ++q)
@@ -243,7 +247,7 @@ __global__ __launch_bounds__(256) void pack_kernel(
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int64_t c = 4 * lane + 256 * q;
-      if (c >= ldy || c < c_lo || c >= c_hi) continue;
+      if (c >= ldy || !owns(c)) continue;
       *reinterpret_cast<f32x4*>(Y + j * ldy + c) = v[q];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -308,7 +312,7 @@ __global__ __launch_bounds__(256) void pack_kernel(
   }
   __syncthreads();
   for (int64_t c = threadIdx.x; c < ldy; c += 256)
-    if (c >= c_lo && c < c_hi)
+    if (owns(c))
       partial[(int64_t)blockIdx.x * ldy + c] =
           max(max(red[c], red[ldy + c]), max(red[2 * ldy + c], red[3 * ldy + c]));
   // X half: words 0, 2; S half: words 1, 3 (pack(NULL, S) leaves the X words)
