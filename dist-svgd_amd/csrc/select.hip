@@ -92,29 +92,35 @@ __global__ __launch_bounds__(256) void radix_hist_kernel(const float* __restrict
     // with global atomics onto the few bins the candidates share)
     const int64_t nb = min((int64_t)gridDim.x, (int64_t)kCandBlocks);
     const int64_t nw = nb * 4;
-    // a slot holds a few hundred candidates: the first 4 x 64 of a slot are
-    // loaded together (padding lanes read as +inf, which hist_key skips) and
-    // the next slot's count one slot ahead, so a wave is not one dependent
+    // a slot holds a few hundred candidates: a wave takes two slots at a
+    // time and loads the first 4 x 64 values of both together (padding lanes
+    // read as +inf, which hist_key skips), so it is not one dependent
     // count -> data -> atomics round trip per 64 values
     constexpr uint32_t kInf = 0x7F800000u;
     int64_t sl = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    uint32_t c = (blockIdx.x < nb && sl < ns) ? cnt[sl] : 0u;
-    for (; blockIdx.x < nb && sl < ns; sl += nw) {
-      const uint32_t cn = sl + nw < ns ? cnt[sl + nw] : 0u;
-      const uint32_t w = (c & DSVGD_SLOT_WEIGHT2) ? 2u : 1u;
-      const int64_t nc = min((int64_t)(c & ~DSVGD_SLOT_WEIGHT2), cap);
-      const float* sd = data + sl * cap;
-      uint32_t k4[4];
+    for (; blockIdx.x < nb && sl < ns; sl += 2 * nw) {
+      const int64_t s2 = sl + nw;
+      const uint32_t ca = cnt[sl], cb = s2 < ns ? cnt[s2] : 0u;
+      const uint32_t wa = (ca & DSVGD_SLOT_WEIGHT2) ? 2u : 1u, wb = (cb & DSVGD_SLOT_WEIGHT2) ? 2u : 1u;
+      const int64_t na = min((int64_t)(ca & ~DSVGD_SLOT_WEIGHT2), cap);
+      const int64_t nb2 = min((int64_t)(cb & ~DSVGD_SLOT_WEIGHT2), cap);
+      const float* sa = data + sl * cap;
+      const float* sb = data + s2 * cap;
+      uint32_t ka[4], kb[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t q = lane + 64 * u;
-        k4[u] = q < nc ? __float_as_uint(sd[q]) : kInf;
+        ka[u] = q < na ? __float_as_uint(sa[q]) : kInf;
+        kb[u] = q < nb2 ? __float_as_uint(sb[q]) : kInf;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) hist_key(k4[u], want, shift, mask, hishift, shist, w);
-      for (int64_t q = lane + 256; q < nc; q += 64)
-        hist_key(__float_as_uint(sd[q]), want, shift, mask, hishift, shist, w);
-      c = cn;
+      for (int u = 0; u < 4; ++u) hist_key(ka[u], want, shift, mask, hishift, shist, wa);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) hist_key(kb[u], want, shift, mask, hishift, shist, wb);
+      for (int64_t q = lane + 256; q < na; q += 64)
+        hist_key(__float_as_uint(sa[q]), want, shift, mask, hishift, shist, wa);
+      for (int64_t q = lane + 256; q < nb2; q += 64)
+        hist_key(__float_as_uint(sb[q]), want, shift, mask, hishift, shist, wb);
     }
   } else if (sym_npad > 0) {  // panel by panel (2048 floats = 2 float4 per thread)
     const int64_t pcols = sym_npad >> 4, npanels = count / kPanelElems;
