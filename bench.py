@@ -29,7 +29,6 @@ timed on this host on a bounded sample, rank 0 at N=1 only.
 """
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -178,15 +177,38 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def kfd_gpu_count():
+    """GPUs the KFD topology lists (nodes with a nonzero gpu_id), read from
+    sysfs: no HIP runtime call, so the launching parent never initialises the
+    GPU stack before it starts the ranks.  None when the topology is unreadable."""
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        nodes = os.listdir(base)
+    except OSError:
+        return None
+    count = 0
+    for nd in nodes:
+        try:
+            with open(os.path.join(base, nd, "gpu_id")) as f:
+                count += int(f.read().strip() or 0) != 0
+        except (OSError, ValueError):
+            continue
+    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+    if vis is not None:
+        count = min(count, len([v for v in vis.split(",") if v.strip() != ""]))
+    return count
+
+
 def launch_ranks(args, argv):
     """--gpus N > 1 without a launcher: run N ranks as a torch.distributed.run
     child (one process per GPU, rendezvous on 127.0.0.1) and pass its output
-    through.  This process never initialises the GPU (device_count() does not
-    on this image), so the ranks own their devices; exits with the child's code."""
+    through.  This process never touches the HIP runtime (GPUs are counted from
+    the KFD sysfs topology), so the ranks own their devices; exits with the
+    child's code."""
     import subprocess
     if args.backend == "nccl":
-        have = torch.cuda.device_count()
-        if have < args.gpus:
+        have = kfd_gpu_count()
+        if have is not None and have < args.gpus:
             print("bench.py: --gpus %d but only %d GPU(s) visible" % (args.gpus, have),
                   file=sys.stderr)
             return 2
@@ -223,9 +245,6 @@ def main(argv=None):
     ap.add_argument("--dim", type=int, default=256)
     ap.add_argument("--data-rows", type=int, default=16384, help="global data rows")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
-    ap.add_argument("--soak", type=float, default=6.0,
-                    help="seconds of untimed steps after the timed ones (the GPU stays busy "
-                         "long enough for an outside utilisation sampler to see it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gemm", default="h2", choices=["h2", "x3", "f32"],
                     help="MFMA engine of the contractions (h2: fp16 split, the default)")
@@ -317,12 +336,6 @@ def main(argv=None):
     # stages allgather_x / allreduce_scores / hist_allreduce included)
     stages = gather_max(stages, world, args.backend, dev)
     assert bool(torch.isfinite(sampler._work).all()), "non-finite particles"
-    # untimed soak: the same number of steps on every rank (el is the max)
-    n_soak = int(math.ceil(args.soak / (el / args.steps))) if args.soak > 0 else 0
-    for _ in range(n_soak):
-        sampler.make_step(eps)
-    torch.cuda.synchronize()
-    barrier()
 
     m = n // world
     phi_ms = stages["phi_mm"]
@@ -388,7 +401,6 @@ def main(argv=None):
         "gemm": gemm,
         "step_6n2d_f32_mfma_frac": (6.0 * m * n * d) / (el / args.steps) / 1e12 / PEAK_FP32_MFMA_TFLOPS,
         "phi_splits": int(eng.splits),
-        "soak_steps_after_timing": n_soak,
         "process_group": {"backend": args.backend if world > 1 else None,
                           "world_size_seen": dist.get_world_size() if world > 1 else 1,
                           "stages": "mean per step, max over ranks" if world > 1 else "mean per step"},

@@ -253,12 +253,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       const int64_t il = (int64_t)un.I * 128 + 32 * bi + r;  // row within the owned block
       const bool ok = valid && il < m;
       nr[bi] = ok ? norms[row0 + il] : INFINITY;
-      si2[bi] = 2.f * pow2_inv(rsc[row0 + il]);
+      si2[bi] = 2.f * pow2_inv(ok ? rsc[row0 + il] : 1.f);
       tg[bi] = ok ? (int)(gi0 + 32 * bi + r - gj0) - 4 * h : (1 << 20);
     }
     const int64_t j = gj0 + lane;
     colbase[lane] = j < n ? norms[j] : INFINITY;
-    colbase[64 + lane] = pow2_inv(rsc[j]);
+    colbase[64 + lane] = pow2_inv(j < n ? rsc[j] : 1.f);  // rsc holds >= n floats
     float* dt = D + ((int64_t)un.I * (n_pad >> 4) + (int64_t)Jt * 8 + 4 * (w & 1)) * kPanelElems;
     rD = __builtin_amdgcn_make_buffer_rsrc((void*)dt, (short)0, valid ? 4 * kPanelElems * 4 : 0,
                                            0x00020000);

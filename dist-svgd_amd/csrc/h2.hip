@@ -16,6 +16,7 @@
 namespace dsvgd {
 
 constexpr int kScaleRows = 512;  // rows per partial-max block
+constexpr float kH2Range = 65536.f;  // 2^16: FmtH2's window
 
 // partial[b][c] = max |A[r][c]| over rows r of block b, as the bit pattern of
 // |v| (unsigned order: finite < inf < NaN, so a NaN or inf is carried through)
@@ -48,12 +49,47 @@ __global__ __launch_bounds__(256) void colmax_partial_kernel(const float* __rest
             max(red[2][threadIdx.x], red[3][threadIdx.x]));
 }
 
+// the range statistics of the unfused path (d > 1024, no pack maxima):
+// rng[0 | 1] = largest |entry| of the half [0, dp) | [dp, cols), rng[2 | 3] =
+// the smallest nonzero row max of that half (bit patterns; one wave per row,
+// one atomic per wave and statistic -- vector-memory atomics on 4 words)
+__global__ void rowrange_init_kernel(uint32_t* __restrict__ rng) {
+  if (threadIdx.x < 4) rng[threadIdx.x] = threadIdx.x < 2 ? 0u : 0x7F800000u;
+}
+
+__global__ __launch_bounds__(256) void rowrange_kernel(const float* __restrict__ A, int64_t lda,
+                                                       int64_t rows, int64_t cols, int64_t dp,
+                                                       uint32_t* __restrict__ rng) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= rows) return;
+  uint32_t mx = 0u, ms = 0u;
+  for (int64_t c = lane; c < cols; c += 64) {
+    const uint32_t v = abs_bits(A[i * lda + c]);
+    if (c < dp) mx = max(mx, v);
+    else ms = max(ms, v);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    ms = max(ms, (uint32_t)__shfl_xor((int)ms, o));
+  }
+  if (lane == 0) {
+    atomicMax(&rng[0], mx);
+    atomicMax(&rng[1], ms);
+    if (mx) atomicMin(&rng[2], mx);
+    if (ms) atomicMin(&rng[3], ms);
+  }
+}
+
 // one block: out[c] = s_c, out[cols + c] = 1 / s_c; out[2 cols] = t = the
 // smallest s_c over the nonzero finite columns (1 if any column is not
-// finite, or none is nonzero), out[2 cols + 1] = 1 / t
+// finite, or none is nonzero), out[2 cols + 1] = 1 / t; out[2 cols + 2] =
+// the range guard from rng (as scales_h2_kernel's; 0 without rng)
 __global__ __launch_bounds__(256) void colscale_final_kernel(const uint32_t* __restrict__ partial,
                                                              int64_t nb, int64_t cols,
-                                                             float* __restrict__ out) {
+                                                             float* __restrict__ out,
+                                                             const uint32_t* __restrict__ rng,
+                                                             int both) {
   __shared__ float red[256];
   __shared__ int bad[256];
   float tmin = INFINITY;
@@ -90,7 +126,13 @@ __global__ __launch_bounds__(256) void colscale_final_kernel(const uint32_t* __r
     const float t = (bad[0] || !isfinite(red[0])) ? 1.f : red[0];
     out[2 * cols] = t;
     out[2 * cols + 1] = 1.f / t;
-    out[2 * cols + 2] = 0.f;  // no range guard on this path (no row maxima)
+    float guard = 0.f;
+    if (rng) {
+      const bool gx_wide = __uint_as_float(rng[0]) > kH2Range * __uint_as_float(rng[2]);
+      const bool gs_wide = __uint_as_float(rng[1]) > kH2Range * __uint_as_float(rng[3]);
+      guard = (gx_wide || (both && gs_wide)) ? 1.f : 0.f;
+    }
+    out[2 * cols + 2] = guard;
   }
 }
 
@@ -105,7 +147,6 @@ __global__ __launch_bounds__(256) void colscale_final_kernel(const uint32_t* __r
 // row max (some particle's row then sits below FmtH2's 2^-16 window of its
 // column's scale), else 0.
 constexpr int kScaleCols = 16;
-constexpr float kH2Range = 65536.f;  // 2^16
 
 __global__ __launch_bounds__(256) void scales_h2_kernel(const uint32_t* __restrict__ partial,
                                                         const uint32_t* __restrict__ gmax,
@@ -282,19 +323,30 @@ __global__ __launch_bounds__(256) void rowsplit_h2_kernel(const float* __restric
   }
 }
 
+// the partial maxima, then 4 words of range statistics (dsvgd_h2_colscale_guarded)
 size_t h2_colscale_ws_floats(int64_t rows, int64_t cols) {
-  return (size_t)((rows + kScaleRows - 1) / kScaleRows) * (size_t)(cols < 1 ? 1 : cols);
+  return (size_t)((rows + kScaleRows - 1) / kScaleRows) * (size_t)(cols < 1 ? 1 : cols) + 4;
 }
 
-int h2_colscale(const float* A, int64_t lda, int64_t rows, int64_t cols, float* ws, float* out,
-                hipStream_t s) {
+// dp > 0: also the range guard of the halves [0, dp) and [dp, cols) (a
+// second pass over A's rows: the unfused path only)
+int h2_colscale(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t dp, float* ws,
+                float* out, hipStream_t s) {
   const int64_t nb = (rows + kScaleRows - 1) / kScaleRows;
   uint32_t* part = reinterpret_cast<uint32_t*>(ws);
+  uint32_t* rng = dp > 0 ? part + nb * cols : nullptr;
   hipLaunchKernelGGL(colmax_partial_kernel, dim3((unsigned)nb, (unsigned)((cols + 63) / 64)),
                      dim3(256), 0, s, A, lda, rows, cols, part);
   int rc = check_launch("colmax_partial");
   if (rc) return rc;
-  hipLaunchKernelGGL(colscale_final_kernel, dim3(1), dim3(256), 0, s, part, nb, cols, out);
+  if (rng) {
+    hipLaunchKernelGGL(rowrange_init_kernel, dim3(1), dim3(64), 0, s, rng);
+    hipLaunchKernelGGL(rowrange_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, A, lda,
+                       rows, cols, dp, rng);
+    if ((rc = check_launch("rowrange"))) return rc;
+  }
+  hipLaunchKernelGGL(colscale_final_kernel, dim3(1), dim3(256), 0, s, part, nb, cols, out, rng,
+                     (int)(cols > dp));
   return check_launch("colscale_final");
 }
 
@@ -357,7 +409,14 @@ int dsvgd_h2_colscale(const float* A, int64_t lda, int64_t rows, int64_t cols, f
                       float* scale, void* stream) {
   DSVGD_REQUIRE(A && ws && scale, "null pointer");
   DSVGD_REQUIRE(rows > 0 && cols > 0 && lda >= cols, "sizes");
-  return h2_colscale(A, lda, rows, cols, ws, scale, (hipStream_t)stream);
+  return h2_colscale(A, lda, rows, cols, 0, ws, scale, (hipStream_t)stream);
+}
+
+int dsvgd_h2_colscale_guarded(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t dp,
+                              float* ws, float* scale, void* stream) {
+  DSVGD_REQUIRE(A && ws && scale, "null pointer");
+  DSVGD_REQUIRE(rows > 0 && cols > 0 && lda >= cols && dp > 0 && dp <= cols, "sizes");
+  return h2_colscale(A, lda, rows, cols, dp, ws, scale, (hipStream_t)stream);
 }
 
 int dsvgd_h2_scales(const uint32_t* partial, const uint32_t* gmax, int64_t nb, int64_t ldy,

@@ -20,14 +20,14 @@ namespace dsvgd {
 
 int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, int64_t cols,
             int splits, const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum,
-            int64_t m, int64_t row0, hipStream_t s);
+            int64_t m, int64_t row0, hipStream_t s, const float* gate);
 int nn_x3_gemm(bool exp_, const float* A, int64_t K, const __bf16* Yx, int64_t ldy, int splits,
                const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
                int64_t row0, hipStream_t s, int sym, int m16, const float* gate);
 int nn_h2_gemm(bool exp_, const float* A, int64_t K, const _Float16* Yh, int64_t ldy, int splits,
                const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
                int64_t row0, hipStream_t s, int sym, const float* colinv, const float* gate);
-int h2_colscale(const float* A, int64_t lda, int64_t rows, int64_t cols, float* ws, float* out,
+int h2_colscale(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t dp, float* ws, float* out,
                 hipStream_t s);
 int h2_ysplit(const float* Y, int64_t ldy, int64_t rows, const float* colscale, void* Yh,
               hipStream_t s);
@@ -521,7 +521,7 @@ static int logreg_prepare(const float* Xd, int64_t ldxd, const float* t, int64_t
   if (P.h2) {
     float* sxd = (float*)(P.base + w.off_sxd);
     float* sws = (float*)(P.base + w.off_sws);
-    if ((rc = h2_colscale(Xdp, w.ldb, w.N_pad, w.ldb, sws, sxd, s))) return rc;
+    if ((rc = h2_colscale(Xdp, w.ldb, w.N_pad, w.ldb, 0, sws, sxd, s))) return rc;
     // the tensor scale for Z's Xd image, per-column ones for G . Xd's B image
     if ((rc = h2_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, sxd + 2 * w.ldb,
                           P.base + w.off_xdx, s)))
@@ -598,7 +598,7 @@ static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float 
                        0, s, Wp, Xdp, w.ldb, (int)w.pp, tp, w.N, w.N_pad, G);
     if ((rc = check_launch("logreg_z"))) return rc;
     if ((rc = nn_gemm(false, G, w.N_pad, Xdp, w.ldb, w.ldb, 1, nullptr, GW, w.ldb, nullptr, n, 0,
-                      s)))
+                      s, nullptr)))
       return rc;
   }
   hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,

@@ -36,7 +36,10 @@ __global__ __launch_bounds__(256 * WM) void nn_kernel(const float* __restrict__ 
                                                       const dsvgd_select_state* __restrict__ st,
                                                       float* __restrict__ C, int64_t ldc,
                                                       float* __restrict__ rowsum, int64_t m,
-                                                      int64_t row0) {
+                                                      int64_t row0,
+                                                      const float* __restrict__ gate) {
+  // gate: run iff *gate != 0 (the FmtH2 range guard when no FmtX3 image fits)
+  if (gate && *gate == 0.f) return;
   using Tile = NNTile<TN, EXP, WM, TM, BJ, SWZB>;
   __shared__ __attribute__((aligned(16))) float smem[Tile::kSmemFloats];
   const int64_t i0 = (int64_t)blockIdx.y * Tile::BM;
@@ -660,45 +663,46 @@ __global__ __launch_bounds__(256) void phi_row_finish_kernel(float* __restrict__
 template <int TN, int BJ>
 int launch_nn_shape(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
                     const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-                    int64_t cols, int64_t row0, hipStream_t s) {
+                    int64_t cols, int64_t row0, hipStream_t s, const float* gate) {
   constexpr int WM = 2, TM = 2, BM = 32 * TM * WM;
   if (K % BJ != 0) return fail_arg("nn_kernel: K must be a multiple of the K-step");
   const int64_t kchunk = roundup((K + splits - 1) / splits, BJ);
   const dim3 grid(cols / (128 * TN), roundup(m, BM) / BM, splits);
   if (exp_)
     hipLaunchKernelGGL((nn_kernel<TN, true, WM, TM, BJ>), grid, dim3(256 * WM), 0, s, A, K, B, ldb,
-                       K, kchunk, st, C, ldc, rowsum, m, row0);
+                       K, kchunk, st, C, ldc, rowsum, m, row0, gate);
   else
     hipLaunchKernelGGL((nn_kernel<TN, false, WM, TM, BJ>), grid, dim3(256 * WM), 0, s, A, K, B, ldb,
-                       K, kchunk, st, C, ldc, rowsum, m, row0);
+                       K, kchunk, st, C, ldc, rowsum, m, row0, gate);
   return check_launch("nn_kernel");
 }
 
 template <int TN>
 int launch_nn(bool exp_, const float* A, const float* B, int64_t ldb, int64_t K, int splits,
               const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
-              int64_t cols, int64_t row0, hipStream_t s) {
+              int64_t cols, int64_t row0, hipStream_t s, const float* gate) {
   if (K % 32 == 0)  // split-K chunks are rounded to the K-step
     return launch_nn_shape<TN, 32>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0,
-                                   s);
-  return launch_nn_shape<TN, 16>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s);
+                                   s, gate);
+  return launch_nn_shape<TN, 16>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s,
+                                 gate);
 }
 
 // C[splits x m x cols] = f(A) B with A in panel layout (m_pad x K), B row-major K x cols.
 // exp_: f = exp2(-inv_h log2e a) with the diagonal (column row0 + i) skipped.
 int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, int64_t cols,
             int splits, const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum,
-            int64_t m, int64_t row0, hipStream_t s) {
+            int64_t m, int64_t row0, hipStream_t s, const float* gate) {
   // buffer-resource loads: 32-bit byte offsets from a block's A row panel
   // (K columns x 128 rows) and from B's first row (K rows x ldb)
   if (K * ldb * (int64_t)sizeof(float) >= ((int64_t)1 << 31) ||
       K * 128 * (int64_t)sizeof(float) >= ((int64_t)1 << 31))
     return fail_arg("nn_kernel: K x ldb too large for 32-bit buffer offsets (split the columns)");
   if (cols % 512 == 0)
-    return launch_nn<4>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s);
+    return launch_nn<4>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s, gate);
   if (cols % 256 == 0)
-    return launch_nn<2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s);
-  return launch_nn<1>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s);
+    return launch_nn<2>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s, gate);
+  return launch_nn<1>(exp_, A, B, ldb, K, splits, st, C, ldc, rowsum, m, cols, row0, s, gate);
 }
 
 // split-K slices: (1) enough for >= 2 blocks per CU (256 CUs) when the owned
@@ -745,7 +749,23 @@ int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64
   DSVGD_REQUIRE(splits >= 1 && splits <= 1024, "splits must be in [1, 1024]");
   DSVGD_REQUIRE(row0 >= 0 && row0 + m <= n, "row block outside [0, n)");
   return nn_gemm(true, D, n_pad, Y, ldy, ldy, (int)splits, st, KY, ldk, rowsum, m, row0,
-                 (hipStream_t)stream);
+                 (hipStream_t)stream, nullptr);
+}
+
+int dsvgd_phi_mm_gated(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t row0,
+                       int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits,
+                       float* KY, int64_t ldk, float* rowsum, const float* gate, void* stream) {
+  DSVGD_REQUIRE(D && Y && st && KY && rowsum && gate, "null pointer");
+  DSVGD_REQUIRE(m > 0 && n > 0, "sizes");
+  const int64_t n_pad = roundup(n, 128);
+  DSVGD_REQUIRE(ldd == n_pad, "ldd must equal roundup(n,128) (panel layout)");
+  DSVGD_REQUIRE(ldy % 128 == 0 && ldk >= ldy, "ldy must be a multiple of 128, ldk >= ldy");
+  DSVGD_REQUIRE(((uintptr_t)Y & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
+  DSVGD_REQUIRE(roundup(m, 128) / 128 <= 65535, "too many row tiles");
+  DSVGD_REQUIRE(splits >= 1 && splits <= 1024, "splits must be in [1, 1024]");
+  DSVGD_REQUIRE(row0 >= 0 && row0 + m <= n, "row block outside [0, n)");
+  return nn_gemm(true, D, n_pad, Y, ldy, ldy, (int)splits, st, KY, ldk, rowsum, m, row0,
+                 (hipStream_t)stream, gate);
 }
 
 int64_t dsvgd_ysplit_bytes(int64_t rows, int64_t ldy) {

@@ -9,7 +9,7 @@ import os
 
 import torch
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libdsvgd_hip.so")
 
 _c = ctypes
@@ -49,6 +49,8 @@ SIGNATURES = {
     "dsvgd_set_bandwidth": (_int, [_p, _f, _p]),
     "dsvgd_phi_splits": (_i64, [_i64, _i64, _i64]),
     "dsvgd_phi_mm": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p]),
+    "dsvgd_phi_mm_gated": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p,
+                                  _p]),
     "dsvgd_ysplit_bytes": (_i64, [_i64, _i64]),
     "dsvgd_ysplit": (_int, [_p, _i64, _i64, _p, _int, _p, _p]),
     "dsvgd_rowsplit_bytes": (_i64, [_i64, _i64]),
@@ -58,6 +60,7 @@ SIGNATURES = {
                                 _int, _p, _p]),
     "dsvgd_h2_colscale_workspace_floats": (_c.c_size_t, [_i64, _i64]),
     "dsvgd_h2_colscale": (_int, [_p, _i64, _i64, _i64, _p, _p, _p]),
+    "dsvgd_h2_colscale_guarded": (_int, [_p, _i64, _i64, _i64, _i64, _p, _p, _p]),
     "dsvgd_h2_scales": (_int, [_p, _p, _i64, _i64, _i64, _i64, _p, _p]),
     "dsvgd_h2_image_bytes": (_i64, [_i64, _i64]),
     "dsvgd_h2_ysplit": (_int, [_p, _i64, _i64, _p, _p, _p]),

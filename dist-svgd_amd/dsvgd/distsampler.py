@@ -157,6 +157,7 @@ class DistSampler(object):
         self._sbuf = None
         self._graph = None
         self._graph_key = None
+        self._group_checked = False
         self._warn_w2_cost()
 
     def _warn_w2_cost(self):
@@ -261,6 +262,17 @@ class DistSampler(object):
         if self._w2 is None or (self._w2.m, self._w2.n, self._w2.d) != key:
             self._w2 = W2Term(*key, device=self._device)
         return self._w2.grad(particles, previous_particles, h)
+
+    def _check_group(self):
+        """The shard rank / count are ranks of `group` (all_gather order and
+        the ring's peers): refuse a mismatch before any collective."""
+        import torch.distributed as dist
+        size, rank = dist.get_world_size(self._group), dist.get_rank(self._group)
+        if size != self._num_shards or rank != self._rank:
+            raise ValueError("DistSampler(rank=%d, num_shards=%d) but this process is rank %d "
+                             "of a %d-rank group: pass the group rank and size"
+                             % (self._rank, self._num_shards, rank, size))
+        self._group_checked = True
 
     def _resolve_replicated(self):
         """replicated=None: on iff every rank's target has the same data
@@ -378,6 +390,8 @@ class DistSampler(object):
             h - discretization size for the JKO (W2) term
         """
         S = self._num_shards
+        if S > 1 and not self._group_checked:
+            self._check_group()
         if self._replicated is None:
             self._resolve_replicated()
         if S > 1:

@@ -212,7 +212,11 @@ class PhiEngine(object):
                 nb = lib.dsvgd_ysplit_bytes(self.n_pad, self.ldy)
                 self.Yx3 = torch.empty(nb // 2, dtype=torch.int16, device=dev)
             else:
+                # no FmtX3 image fits its 32-bit offsets: the guard's fallback
+                # is the exact f32 phi_mm (dsvgd_phi_mm_gated), which reads the
+                # full D layout only
                 self.Yx3 = None
+                self.sym_layout = False
         # d <= 1024: pack writes the column maxima the scales come from
         # (dsvgd_pack_h2 / dsvgd_h2_scales); wider, a separate pass over Y
         self.fused_scales = ("h2" in (phi_gemm, gram_gemm) and self.ldy <= lib.dsvgd_pack_max_ldy()
@@ -305,9 +309,9 @@ class PhiEngine(object):
         if self.fused_scales:
             N.call("dsvgd_h2_scales", N.ptr(self.colmax), N.ptr(self.gmax), self.colmax_nb,
                    self.ldy, cols, self.dp, N.ptr(out), s)
-        else:
-            N.call("dsvgd_h2_colscale", N.ptr(self.Y), self.ldy, self.n_pad, cols,
-                   N.ptr(self.scale_ws), N.ptr(out), s)
+        else:   # d > 1024: a pass over Y, with the range guard of its halves
+            N.call("dsvgd_h2_colscale_guarded", N.ptr(self.Y), self.ldy, self.n_pad, cols,
+                   min(self.dp, cols), N.ptr(self.scale_ws), N.ptr(out), s)
 
     def _pack(self, X, S, score_scale, s):
         N.call("dsvgd_colcenter", N.ptr(X), N.ld(X), self.n, self.d, N.ptr(self.mean), s)
@@ -442,9 +446,10 @@ class PhiEngine(object):
             return
         if self.phi_gemm == "h2":
             # the range guard word of the scales: phi_mm_h2 runs while it
-            # reads 0; otherwise the FmtX3 image and phi_mm_x3 behind it do
-            # (both stay on the stream -- no host round trip)
-            guard = (N.ptr(self.yscale) + 4 * (2 * self.ldy + 2)) if self.Yx3 is not None else None
+            # reads 0; otherwise the FmtX3 image and phi_mm_x3 behind it do,
+            # or (no FmtX3 image fits) the exact f32 phi_mm (all stay on the
+            # stream -- no host round trip)
+            guard = N.ptr(self.yscale) + 4 * (2 * self.ldy + 2)
             with span(self.timer, "ysplit"):
                 self._scales(self.ldy, self.yscale, s)
                 N.call("dsvgd_h2_ysplit", N.ptr(self.Y), self.ldy, self.n_pad,
@@ -454,7 +459,12 @@ class PhiEngine(object):
                        self.row0, self.m, self.n, self.state.ptr, self.splits, N.ptr(self.KY),
                        self.ldy, N.ptr(self.rowsum), int(self.sym),
                        N.ptr(self.yscale) + 4 * self.ldy, guard, s)
-            if guard is not None:
+            if self.Yx3 is None:
+                with span(self.timer, "phi_guard"):
+                    N.call("dsvgd_phi_mm_gated", N.ptr(self.D), self.n_pad, N.ptr(self.Y),
+                           self.ldy, self.row0, self.m, self.n, self.state.ptr, self.splits,
+                           N.ptr(self.KY), self.ldy, N.ptr(self.rowsum), guard, s)
+            else:
                 with span(self.timer, "phi_guard"):
                     N.call("dsvgd_ysplit", N.ptr(self.Y), self.ldy, self.n_pad, N.ptr(self.Yx3),
                            0 if self.m16_fb else 1, guard, s)
@@ -481,8 +491,9 @@ class PhiEngine(object):
                float(inv_n), float(step), ex, lde, phi, self.d, xo, ldx, s)
 
     def range_guard(self):
-        """The last phi_mm's FmtH2 range guard (True: it ran on the FmtX3
-        fallback; None: not the h2 engine) -- synchronises."""
+        """The last phi_mm's FmtH2 range guard (True: it ran on the fallback
+        -- the FmtX3 engine, or the exact f32 one where no FmtX3 image fits;
+        None: not the h2 engine) -- synchronises."""
         if self.phi_gemm != "h2" or self.d <= self.DIRECT_MAX_D:
             return None
         return bool(float(self.yscale[2 * self.ldy + 2]) != 0.0)

@@ -50,18 +50,39 @@ def all_reduce_sum(t, group=None):
 
 
 def ring_shift(send, recv, rank, size, group=None):
-    """send -> rank+1, recv <- rank-1   [distsampler.py:131-150]."""
+    """send -> rank+1, recv <- rank-1   [distsampler.py:131-150].
+
+    `rank` and `size` are the caller's shard rank and count inside `group`
+    (group-local ranks, the order all_gather uses); the peers are addressed
+    as group ranks (`group_peer`), so a subgroup of a larger world sends to
+    the right processes."""
     dst, src = (rank + 1) % size, (rank - 1 + size) % size
-    if send.is_cuda and not _is_gloo(group):
-        ops = [dist.P2POp(dist.isend, send.contiguous(), dst, group=group),
-               dist.P2POp(dist.irecv, recv, src, group=group)]
+    exchange_p2p([(send, dst)], [(recv, src)], group)
+
+
+def exchange_p2p(sends, recvs, group=None):
+    """Point-to-point transfers in one batch: sends = [(tensor, group_rank)],
+    recvs = [(tensor, group_rank)], peers as ranks of `group`.  On RCCL the
+    ops are posted together (batch_isend_irecv: one fused group call, each
+    pair of peers on its own xGMI link) and joined before returning; on gloo
+    the tensors are staged through host copies."""
+    if not sends and not recvs:
+        return
+    dev = any(t.is_cuda for t, _ in list(sends) + list(recvs))
+    if dev and not _is_gloo(group):
+        ops = [dist.P2POp(dist.isend, t.contiguous(), group=group, group_peer=p) for t, p in sends]
+        ops += [dist.P2POp(dist.irecv, t, group=group, group_peer=p) for t, p in recvs]
         for r in dist.batch_isend_irecv(ops):
             r.wait()
         return
-    hs = send.detach().cpu().contiguous()
-    hr = torch.empty(recv.shape, dtype=recv.dtype)
-    r1 = dist.isend(hs, dst, group=group)
-    r2 = dist.irecv(hr, src, group=group)
-    r1.wait()
-    r2.wait()
-    recv.copy_(hr.to(recv.device))
+    work, host = [], []
+    for t, p in sends:
+        work.append(dist.isend(t.detach().cpu().contiguous(), group=group, group_dst=p))
+    for t, p in recvs:
+        h = torch.empty(t.shape, dtype=t.dtype)
+        host.append((t, h))
+        work.append(dist.irecv(h, group=group, group_src=p))
+    for w in work:
+        w.wait()
+    for t, h in host:
+        t.copy_(h.to(t.device))

@@ -22,6 +22,12 @@ import torch
 from . import _native as N
 
 
+def _host_bytes(t):
+    """The bytes of a tensor's values wherever it lives (a target built from
+    device tensors digests the same as one built from host tensors)."""
+    return t.detach().cpu().contiguous().numpy().tobytes()
+
+
 class Target(object):
     def score(self, X, out, scale=1.0):
         """out[:] = scale * grad log p(X) for X (n, d) on the device."""
@@ -54,7 +60,7 @@ class Gaussian(BuiltinTarget):
 
     def fingerprint(self):
         import hashlib
-        return hashlib.sha1(b"gauss" + self.mu.numpy().tobytes() + self.lam.numpy().tobytes()).hexdigest()
+        return hashlib.sha1(b"gauss" + _host_bytes(self.mu) + _host_bytes(self.lam)).hexdigest()
 
     def score(self, X, out, scale=1.0):
         n, d = X.shape
@@ -131,8 +137,8 @@ class LogisticRegression(BuiltinTarget):
         hold the same data, so their scores of a particle are the same)."""
         import hashlib
         h = hashlib.sha1(b"logreg")
-        h.update(self.x.contiguous().numpy().tobytes())
-        h.update(self.t.contiguous().numpy().tobytes())
+        h.update(_host_bytes(self.x))
+        h.update(_host_bytes(self.t))
         return h.hexdigest()
 
     MAX_WORKSPACES = 4   # unpinned score workspaces kept (least recently used evicted)

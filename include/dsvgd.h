@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DSVGD_ABI_VERSION 3
+#define DSVGD_ABI_VERSION 4
 
 enum {
   DSVGD_OK = 0,
@@ -226,6 +226,13 @@ int64_t dsvgd_phi_splits(int64_t m, int64_t n, int64_t ldy);
 int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t row0,
                  int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
                  int64_t ldk, float* rowsum, void* stream);
+/* dsvgd_phi_mm gated on a device word: does nothing while *gate reads 0 --
+ * the exact f32 fallback of dsvgd_phi_mm_h2 where the FmtX3 image does not
+ * fit its 32-bit offsets (roundup(n,128) * ldy * 6 >= 2^31); full D layout
+ * only (ABI 4). */
+int dsvgd_phi_mm_gated(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t row0,
+                       int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits,
+                       float* KY, int64_t ldk, float* rowsum, const float* gate, void* stream);
 
 /* phi_mm on the bf16 MFMA at fp32 accuracy (the default engine): both
  * operands split three ways into bf16 (v = v0 + v1 + v2 to ~2^-26 |v|) and
@@ -284,12 +291,16 @@ int dsvgd_phi_mm_x3(const float* D, int64_t ldd, const void* Yx, int64_t ldy, in
  * dsvgd_h2_colscale: per column c of A (rows x cols), scale[c] = s_c and
  * scale[cols + c] = 1 / s_c; scale[2 cols] = t = min s_c over the nonzero
  * finite columns (1 if a column holds an inf / NaN, which then propagate),
- * scale[2 cols + 1] = 1 / t, scale[2 cols + 2] = 0 (no range guard on this
- * path).  scale: 2 cols + 3 floats; ws:
- * dsvgd_h2_colscale_workspace_floats(rows, cols) floats. */
+ * scale[2 cols + 1] = 1 / t, scale[2 cols + 2] = 0 (no range guard).
+ * scale: 2 cols + 3 floats; ws: dsvgd_h2_colscale_workspace_floats(rows,
+ * cols) floats.  dsvgd_h2_colscale_guarded (ABI 4; the unfused d > 1024
+ * path) also writes the RANGE GUARD of dsvgd_h2_scales for the halves
+ * [0, dp) and [dp, cols) (a second pass over A's rows). */
 size_t dsvgd_h2_colscale_workspace_floats(int64_t rows, int64_t cols);
 int dsvgd_h2_colscale(const float* A, int64_t lda, int64_t rows, int64_t cols, float* ws,
                       float* scale, void* stream);
+int dsvgd_h2_colscale_guarded(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t dp,
+                              float* ws, float* scale, void* stream);
 /* dsvgd_h2_colscale's output over Y's first cols columns (cols = dp: the X
  * half; cols = ldy: all of Y), bit-identical, from dsvgd_pack_h2's maxima
  * (nb = dsvgd_pack_blocks(rows_pad)); scale[2 cols + 2] = the RANGE GUARD:
@@ -328,7 +339,8 @@ int dsvgd_sqdist_h2(const void* Yg, const float* norms, int64_t row0, int64_t m,
  * columns of Y; same outputs (unscaled), split-K slices, diagonal rule and
  * symmetric layout (sym needs ldy % 256 == 0).  Requires n_pad * ldy * 4 <
  * 2^31.  gate (nullable, &scale[2 ldy + 2]): does nothing while it reads
- * nonzero (the range guard hands the step to dsvgd_phi_mm_x3). */
+ * nonzero (the range guard hands the step to dsvgd_phi_mm_x3, or to
+ * dsvgd_phi_mm_gated where no FmtX3 image fits). */
 int dsvgd_phi_mm_h2(const float* D, int64_t ldd, const void* Yh, int64_t ldy, int64_t row0,
                     int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
                     int64_t ldk, float* rowsum, int sym, const float* colinv, const float* gate,

@@ -22,19 +22,19 @@ for s in ${STEPS:-smoke tests bench prof}; do
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step tests 1500 python -u -m pytest ${TESTS:-tests} -m gpu -v -x --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} ;;
     bench) step bench 900 python bench.py --steps ${BSTEPS:-10} --warmup 3 ${BENCH_ARGS:-} ;;
-    prof)  step prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --soak 0 ;;
+    prof)  step prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     ab)    step ab 600 python scripts/ab_kernels.py ;;
     w2)    step w2 600 python scripts/w2_timing.py ${W2_ARGS:-} ;;
     diag)  step diag 600 python scripts/diag_precision.py ;;
-    pmc)   step pmc 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --soak 0 ;;
+    pmc)   step pmc 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmcclk) step pmcclk 900 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 --kernel-trace -d "$OUT/pmcclk" -o run --output-format csv -- python3 scripts/ab_kernels.py --rounds 1 ;;
     pmcstall) step pmcstall 900 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES --kernel-trace -d "$OUT/pmcstall" -o run --output-format csv -- python3 scripts/ab_kernels.py --rounds 1 ;;
-    pmcstallb) step pmcstallb 900 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES --kernel-trace -d "$OUT/pmcstallb" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --soak 0 ;;
-    pmcmfma) step pmcmfma 900 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM --kernel-trace -d "$OUT/pmcmfma" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --soak 0 ;;
+    pmcstallb) step pmcstallb 900 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES --kernel-trace -d "$OUT/pmcstallb" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pmcmfma) step pmcmfma 900 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM --kernel-trace -d "$OUT/pmcmfma" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     pmcmfmaab) step pmcmfmaab 900 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES --kernel-trace -d "$OUT/pmcmfmaab" -o run --output-format csv -- python3 scripts/ab_kernels.py --rounds 1 ;;
     configs) step configs 600 python scripts/configs_bench.py ;;
     notes) step notes 600 python scripts/notes_timing.py ;;
-    pmcw)  step pmcw 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --soak 0 ;;
+    pmcw)  step pmcw 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
   esac
 done
 echo ALL DONE

