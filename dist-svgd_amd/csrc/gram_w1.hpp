@@ -141,7 +141,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const _Float16* __restrict__ Yg, int64_t img_rows, const float* __restrict__ norms,
     const float* __restrict__ rsc, int64_t row0, int64_t m, int64_t n, int64_t n_pad, int nk,
     float* __restrict__ D, dsvgd_select_state* __restrict__ st, float* __restrict__ cand,
-    int64_t total_units, int Tm, int Tc, int jp_off, int64_t slot_base, int64_t ns_total) {
+    int64_t total_units, int Tm, int Tc, int jp_off, int64_t slot_base, int64_t ns_total,
+    int w2all = 0, const float* __restrict__ gate = nullptr) {
+  // gate: a fallback-only part of the pair-split layout (dsvgd_sqdist_h2_parts)
+  // runs iff the FmtH2 range guard word is set
+  if (gate && *gate == 0.f) return;
   using V8 = FmtH2::V8;
   constexpr bool kBr = smode == kSelBracket;
   __builtin_assume(nk >= 16 && nk % 16 == 0);  // checked by the host
@@ -263,7 +267,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     rD = __builtin_amdgcn_make_buffer_rsrc((void*)dt, (short)0, valid ? 4 * kPanelElems * 4 : 0,
                                            0x00020000);
     eslot = slot_base + un.L * GramW1::kSlots + w;
-    ew2 = SYM && Jt != un.I;
+    ew2 = (SYM && Jt != un.I) || w2all != 0;  // w2all: a pair-split forward block
     ediag = valid && gj0 + 64 > gi0 && gj0 < gi0 + 128;
   };
 

@@ -350,6 +350,81 @@ __global__ __launch_bounds__(256) void phi_finish_kernel(
   if (X) X[i * ldx + c] += step * p;
 }
 
+// ---- the pair-split layout's partials (dsvgd_phi_h2_transposed)
+// out[i][c] = sum_z P[z][i][c], out_rs[i] = sum_z rs[z][i] (slice order);
+// four columns per thread
+__global__ __launch_bounds__(256) void partial_reduce_kernel(
+    const float* __restrict__ P, int64_t ldp, const float* __restrict__ rs, int splits,
+    int64_t rows, int64_t cols, float* __restrict__ out, int64_t ldo, float* __restrict__ out_rs) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t c4 = cols >> 2;
+  const int64_t rp = roundup128(rows);
+  if (t < rows * c4) {
+    const int64_t i = t / c4, c = (t % c4) * 4;
+    f32x4 a = *reinterpret_cast<const f32x4*>(P + i * ldp + c);
+    for (int z = 1; z < splits; ++z)
+      a += *reinterpret_cast<const f32x4*>(P + ((int64_t)z * rows + i) * ldp + c);
+    *reinterpret_cast<f32x4*>(out + i * ldo + c) = a;
+  }
+  if (t < rows) {
+    float r = rs[t];
+    for (int z = 1; z < splits; ++z) r += rs[(int64_t)z * rp + t];
+    out_rs[t] = r;
+  }
+}
+
+// phi_finish over the own slices plus the partials of the pair-split layout
+// (list order after the own slices: deterministic); gate != 0: the range
+// guard's whole-row fallback wrote splits_fb own slices, the parts are skipped
+constexpr int kMaxPhiParts = 16;
+struct PhiPartsArg {
+  int n;
+  const float* ky[kMaxPhiParts];
+  const float* rs[kMaxPhiParts];
+  int64_t ldk[kMaxPhiParts], row_off[kMaxPhiParts], rows[kMaxPhiParts];
+  int splits[kMaxPhiParts];
+};
+
+__global__ __launch_bounds__(256) void phi_finish_parts_kernel(
+    const float* __restrict__ KY, int64_t ldk, const float* __restrict__ rowsum, int splits,
+    const float* __restrict__ Y, int64_t ldy, int64_t row0, int64_t m, int64_t d, int64_t dp,
+    const dsvgd_select_state* __restrict__ st, float inv_n, float step,
+    const float* __restrict__ extra, int64_t lde, float* __restrict__ phi, int64_t ldphi,
+    float* __restrict__ X, int64_t ldx, PhiPartsArg parts, const float* __restrict__ gate,
+    int splits_fb) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= m * d) return;
+  const int64_t i = t / d, c = t % d;
+  const bool fb = gate && *gate != 0.f;
+  const int ns = fb ? splits_fb : splits;
+  const float two_inv_h = 2.f * st->inv_h;
+  const int64_t mp = roundup128(m);
+  float kx = 0.f, ks = 0.f, r = 0.f;
+  for (int z = 0; z < ns; ++z) {
+    const float* ky = KY + (int64_t)z * m * ldk + i * ldk;
+    kx += ky[c];
+    ks += ky[dp + c];
+    r += rowsum[(int64_t)z * mp + i];
+  }
+  const int np = fb ? 0 : parts.n;
+  for (int p = 0; p < np; ++p) {
+    const int64_t li = i - parts.row_off[p];
+    if (li < 0 || li >= parts.rows[p]) continue;
+    const int64_t rows = parts.rows[p], lk = parts.ldk[p];
+    for (int z = 0; z < parts.splits[p]; ++z) {
+      const float* ky = parts.ky[p] + ((int64_t)z * rows + li) * lk;
+      kx += ky[c];
+      ks += ky[dp + c];
+      r += parts.rs[p][(int64_t)z * roundup128(rows) + li];
+    }
+  }
+  const float* yi = Y + (row0 + i) * ldy;
+  float p = inv_n * ((yi[dp + c] + ks) + two_inv_h * (r * yi[c] - kx));
+  if (extra) p += extra[i * lde + c];
+  if (phi) phi[i * ldphi + c] = p;
+  if (X) X[i * ldx + c] += step * p;
+}
+
 // d <= 64: phi from explicit differences, the reference's own pairwise form
 //   phi_i = inv_n sum_j k_ij (s_j + (2/h)(x_i - x_j))
 // (no r_i x_i - (K X)_i cancellation, which at small d and a narrow bandwidth
@@ -842,6 +917,110 @@ int dsvgd_phi_mm_h2(const float* D, int64_t ldd, const void* Yh, int64_t ldy, in
                 "sym: the symmetric layout needs m == n, row0 == 0, ldy % 256 == 0");
   return nn_h2_gemm(true, D, n_pad, (const _Float16*)Yh, ldy, (int)splits, st, KY, ldk, rowsum, m,
                     row0, (hipStream_t)stream, sym, colinv, gate);
+}
+
+int dsvgd_phi_h2_window(const float* D, int64_t ldd, const void* Yh, int64_t ldy, int64_t row0,
+                        int64_t m, int64_t n, int64_t col0, int64_t wlen,
+                        const dsvgd_select_state* st, int64_t splits, float* KY, int64_t ldk,
+                        float* rowsum, const float* colinv, const float* gate, int gate_on,
+                        void* stream) {
+  DSVGD_REQUIRE(D && Yh && st && KY && rowsum && colinv, "null pointer");
+  const int64_t n_pad = roundup(n, 128);
+  DSVGD_REQUIRE(ldd == n_pad, "ldd must equal roundup(n,128) (panel layout)");
+  DSVGD_REQUIRE(m > 0 && row0 >= 0 && row0 + m <= n, "rows outside [0, n)");
+  DSVGD_REQUIRE(ldy % 512 == 0 && ldk >= ldy, "ldy must be a multiple of 512, ldk >= ldy");
+  DSVGD_REQUIRE(col0 >= 0 && col0 < n_pad && col0 % 16 == 0 && wlen > 0 && wlen <= n_pad &&
+                    wlen % 16 == 0,
+                "window: col0 in [0, n_pad), wlen in (0, n_pad], multiples of 16");
+  DSVGD_REQUIRE(splits >= 1 && splits <= 1024, "splits must be in [1, 1024]");
+  DSVGD_REQUIRE(n_pad * ldy * 4 < ((int64_t)1 << 31), "n x ldy too large for 32-bit offsets");
+  DSVGD_REQUIRE(((uintptr_t)Yh & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
+  const int64_t kchunk = roundup((wlen + splits - 1) / splits, (int64_t)PhiW1::BJ);
+  const dim3 grid((unsigned)(ldy / PhiW1::BC), (unsigned)(roundup(m, 128) / 128), (unsigned)splits);
+  hipLaunchKernelGGL(phi_w1_kernel<0>, grid, dim3(PhiW1::kThreads), 0, (hipStream_t)stream, D,
+                     n_pad, (const _Float16*)Yh, ldy, wlen, kchunk, st, KY, ldk, rowsum, m, row0,
+                     0, colinv, 0, gate, gate_on, (int)(col0 / PhiW1::BJ),
+                     (int)(n_pad / PhiW1::BJ), 0);
+  return check_launch("phi_w1_kernel(window)");
+}
+
+int dsvgd_phi_h2_transposed(const float* D, int64_t ldd, const void* Yh, int64_t ldy,
+                            int64_t yrow0, int64_t krows, int64_t col0, int64_t mo, int64_t n,
+                            const dsvgd_select_state* st, int64_t splits, float* P, int64_t ldp,
+                            float* rs, const float* colinv, const float* gate, int gate_on,
+                            void* stream) {
+  DSVGD_REQUIRE(D && Yh && st && P && rs && colinv, "null pointer");
+  const int64_t n_pad = roundup(n, 128);
+  DSVGD_REQUIRE(ldd == n_pad, "ldd must equal roundup(n,128) (panel layout)");
+  DSVGD_REQUIRE(ldy % 512 == 0 && ldp >= ldy, "ldy must be a multiple of 512, ldp >= ldy");
+  DSVGD_REQUIRE(krows > 0 && krows % 16 == 0 && yrow0 >= 0 && yrow0 % 16 == 0 &&
+                    yrow0 + krows <= n_pad,
+                "the rectangle's rows: a multiple of 16 inside [0, n_pad)");
+  DSVGD_REQUIRE(mo > 0 && col0 >= 0 && col0 % 128 == 0 && col0 + roundup(mo, 128) <= n_pad,
+                "the rectangle's columns: 128-aligned inside [0, n_pad)");
+  DSVGD_REQUIRE(splits >= 1 && splits <= 1024, "splits must be in [1, 1024]");
+  DSVGD_REQUIRE(n_pad * ldy * 4 < ((int64_t)1 << 31), "n x ldy too large for 32-bit offsets");
+  DSVGD_REQUIRE(((uintptr_t)Yh & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
+  const int64_t kchunk = roundup((krows + splits - 1) / splits, (int64_t)PhiW1::BJ);
+  const dim3 grid((unsigned)(ldy / PhiW1::BC), (unsigned)(roundup(mo, 128) / 128),
+                  (unsigned)splits);
+  hipLaunchKernelGGL(phi_w1_kernel<3>, grid, dim3(PhiW1::kThreads), 0, (hipStream_t)stream, D,
+                     n_pad, (const _Float16*)Yh, ldy, krows, kchunk, st, P, ldp, rs, mo,
+                     (int64_t)0, 0, colinv, 0, gate, gate_on, (int)(yrow0 / PhiW1::BJ), 0,
+                     (int)(col0 / 128));
+  return check_launch("phi_w1_kernel(transposed)");
+}
+
+int dsvgd_phi_partial_reduce(const float* P, int64_t ldp, const float* rs, int64_t splits,
+                             int64_t rows, int64_t cols, float* out, int64_t ldo, float* out_rs,
+                             void* stream) {
+  DSVGD_REQUIRE(P && rs && out && out_rs, "null pointer");
+  DSVGD_REQUIRE(rows > 0 && cols > 0 && cols % 4 == 0 && ldp >= cols && ldo >= cols &&
+                    ldp % 4 == 0 && ldo % 4 == 0,
+                "sizes (cols, ldp, ldo multiples of 4)");
+  DSVGD_REQUIRE(splits >= 1 && splits <= 1024, "splits must be in [1, 1024]");
+  DSVGD_REQUIRE(((uintptr_t)P & 15) == 0 && ((uintptr_t)out & 15) == 0, "16-byte alignment");
+  const int64_t threads = std::max(rows * (cols / 4), rows);
+  hipLaunchKernelGGL(partial_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, P, ldp, rs, (int)splits, rows, cols, out, ldo, out_rs);
+  return check_launch("partial_reduce");
+}
+
+int dsvgd_phi_finish_parts(const float* KY, int64_t ldk, const float* rowsum, int64_t splits,
+                           const float* Y, int64_t ldy, int64_t row0, int64_t m, int64_t d,
+                           int64_t dp, const dsvgd_select_state* st, float inv_n, float step,
+                           const float* extra, int64_t lde, float* phi, int64_t ldphi, float* X,
+                           int64_t ldx, const dsvgd_phi_part* parts, int nparts,
+                           const float* gate, int64_t splits_fb, void* stream) {
+  DSVGD_REQUIRE(KY && rowsum && Y && st, "null pointer");
+  DSVGD_REQUIRE(!extra || lde >= d, "lde");
+  DSVGD_REQUIRE(splits >= 1 && splits <= 1024 && splits_fb >= 0 && splits_fb <= 1024,
+                "splits must be in [1, 1024]");
+  DSVGD_REQUIRE(m > 0 && d > 0 && dp >= d && ldk >= 2 * dp && ldy >= 2 * dp, "sizes");
+  DSVGD_REQUIRE(!phi || ldphi >= d, "ldphi");
+  DSVGD_REQUIRE(!X || ldx >= d, "ldx");
+  DSVGD_REQUIRE(nparts >= 0 && nparts <= kMaxPhiParts && (nparts == 0 || parts),
+                "at most 16 parts");
+  PhiPartsArg pa{};
+  pa.n = nparts;
+  for (int p = 0; p < nparts; ++p) {
+    const dsvgd_phi_part& q = parts[p];
+    DSVGD_REQUIRE(q.ky && q.rs, "null part");
+    DSVGD_REQUIRE(q.row_off >= 0 && q.rows > 0 && q.row_off + q.rows <= m && q.ldk >= 2 * dp &&
+                      q.splits >= 1 && q.splits <= 1024,
+                  "part rows inside the block, ldk >= 2 dp, splits in [1, 1024]");
+    pa.ky[p] = q.ky;
+    pa.rs[p] = q.rs;
+    pa.ldk[p] = q.ldk;
+    pa.row_off[p] = q.row_off;
+    pa.rows[p] = q.rows;
+    pa.splits[p] = (int)q.splits;
+  }
+  hipLaunchKernelGGL(phi_finish_parts_kernel, dim3((unsigned)((m * d + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, KY, ldk, rowsum, (int)splits, Y, ldy, row0, m, d, dp,
+                     st, inv_n, step, extra, lde, phi, ldphi, X, ldx, pa, gate,
+                     (int)(splits_fb ? splits_fb : splits));
+  return check_launch("phi_finish_parts");
 }
 
 int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t splits,

@@ -54,18 +54,27 @@ __device__ __forceinline__ f32x4 w1_load_nt(__amdgpu_buffer_rsrc_t r, int voff, 
 // DS (compile-time dsplit): 0 = the K range [kchunk z, +kchunk) (full D
 // layout); on the symmetric layout (m == n, row0 == 0) 1 = the transposed
 // K-steps left of a row block's diagonal tile, 2 = the plain ones from it on
-// (the hybrid's two launches; slices land in slice0 + z)
+// (the hybrid's two launches; slices land in slice0 + z).
+// The pair-split layout of a DistSampler rank:
+//   DS 0 with ks_wrap > 0: a cyclic window of K-steps -- window column k is
+//     global K-step (ks_begin + k) mod ks_wrap (of both D and the image);
+//   DS 3: a TRANSPOSED rectangle -- output row block `by` is D's column tile
+//     tcol0 + by, the K-steps run down D's rows from A (A: the first of them,
+//     a panel-row boundary), and the image K-step of D row j is ks_begin + j/16
+//     (the owned rows' place in the interacting set): C = K(rows, cols)^T Y_rows,
+//     the partial a rank sends to the owner of those columns.
 template <int DS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void phi_w1_kernel(
     const float* A, int64_t a_npad, const _Float16* Yx, int64_t ldy,
     int64_t K, int64_t kchunk, const dsvgd_select_state* __restrict__ st, float* __restrict__ C,
     int64_t ldc, float* __restrict__ rowsum, int64_t m, int64_t row0, int sym,
-    const float* __restrict__ colinv, int slice0, const float* __restrict__ gate, int gate_on) {
+    const float* __restrict__ colinv, int slice0, const float* __restrict__ gate, int gate_on,
+    int ks_begin = 0, int ks_wrap = 0, int tcol0 = 0) {
   if (gate && ((*gate != 0.f) != (gate_on != 0))) return;  // the FmtH2 range guard (nn_x3_kernel)
   using F = FmtH2;
   using V8 = F::V8;
   constexpr int P = PhiW1::P;
-  constexpr bool TR = DS == 1;
+  constexpr bool TR = DS == 1 || DS == 3;
   __shared__ __attribute__((aligned(16))) char smem[PhiW1::kSmemBytes + (TR ? 4 * PhiW1::kScrBytes : 0)];
   const int t = threadIdx.x, lane = t & 63, r = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -74,7 +83,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int64_t lin = (int64_t)blockIdx.z * gridDim.y + blockIdx.y;
   const int64_t by = DS == 2 ? lin / gridDim.z
                    : DS == 1 ? (int64_t)gridDim.y - 1 - lin / gridDim.z : blockIdx.y;
-  const int64_t bz = DS != 0 ? lin % gridDim.z : blockIdx.z;
+  const int64_t bz = (DS == 1 || DS == 2) ? lin % gridDim.z : blockIdx.z;
   const int64_t i0 = by * PhiW1::BM;
   const int64_t c0 = (int64_t)blockIdx.x * PhiW1::BC + w * 128;
   // K-step k of this block is global K-step ks0 + kdir * k.  The symmetric
@@ -83,10 +92,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // then read the same Yx K-steps at the same time (L2 reuse), whatever row
   // they start from
   const int64_t kb0 = bz * kchunk, kend = min(K, kb0 + kchunk);
-  int ks0 = (int)(kb0 / PhiW1::BJ);
+  int ks0 = (int)(kb0 / PhiW1::BJ) + (DS == 0 ? ks_begin : 0);
   int nsteps = kend > kb0 ? (int)((kend - kb0) / PhiW1::BJ) : 0;
   const int Z = (int)gridDim.z;
   const int kdir = DS == 2 ? -Z : DS == 1 ? Z : 1;
+  // K-step index of window step ks (DS 0 cyclic window; ks_wrap == 0: none)
+  auto wrapk = [&](int ks) { return (DS == 0 && ks_wrap > 0 && ks >= ks_wrap) ? ks - ks_wrap : ks; };
+  // the image K-step of D-row K-step ks (DS 3: the owned rows' offset)
+  const int kyoff = DS == 3 ? ks_begin : 0;
   if (DS == 2) {
     const int T = (int)((K - i0) / PhiW1::BJ);
     ks0 = (int)(K / PhiW1::BJ) - 1 - (int)bz;
@@ -127,7 +140,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   // symmetric layout (m == n, row0 == 0): K-steps left of the block's
   // diagonal tile (DS 1) read the stored tile (J, I) transposed
-  const int symI = sym ? (int)(i0 >> 7) : -1;
+  const int symI = DS == 3 ? tcol0 + (int)by : sym ? (int)(i0 >> 7) : -1;
   const int64_t pcols = a_npad >> 4;
   // DS 1: lane (piece p = t >> 5, s = t & 31) loads rows i0 + 16 p + 8 (s & 1)
   // .. +7 of column j0 + (s >> 1): 32 contiguous bytes of panel I*8 + p
@@ -144,14 +157,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     f32x4 tr[2];      // DS 1: K-step k+1's values, transposed during K-step k - 1
     const int last = nsteps - 1;
     auto loadB = [&](int ni, int k) {
-      const int soff = (ks0 + kdir * min(k, last)) * P * pstride;
+      const int soff = (wrapk(ks0 + kdir * min(k, last)) + kyoff) * P * pstride;
 #pragma unroll
       for (int p = 0; p < P; ++p)
         b[ni][p] = __builtin_bit_cast(V8, w1_load(rB, vB + ni * 1024, soff + p * pstride));
     };
     auto loadD = [&](f32x4 (&d)[2], int k) {
       const int kc = min(k, last);
-      const int64_t j0 = (int64_t)(ks0 + kdir * kc) * PhiW1::BJ;
+      const int64_t j0 = (int64_t)wrapk(ks0 + kdir * kc) * PhiW1::BJ;
       if constexpr (TR) {
         const float* src = A + (((j0 >> 7) * pcols + symI * 8) * kPanelElems + (j0 & 127) * 16);
         const __amdgpu_buffer_rsrc_t rT =

@@ -69,7 +69,8 @@ constexpr int kCandBlocks = 1024;
 __global__ __launch_bounds__(256) void radix_hist_kernel(const float* __restrict__ D, int64_t count,
                                                          const float* __restrict__ cand, int pass,
                                                          dsvgd_select_state* __restrict__ st,
-                                                         int64_t sym_npad) {
+                                                         int64_t sym_npad,
+                                                         const uint8_t* __restrict__ wmap = nullptr) {
   __shared__ uint32_t shist[DSVGD_RADIX_BINS];
   if (st->passes_done >= (uint32_t)pass) return;  // digit fixed by bracket_check
   for (int b = threadIdx.x; b < DSVGD_RADIX_BINS; b += 256) shist[b] = 0u;
@@ -127,8 +128,9 @@ __global__ __launch_bounds__(256) void radix_hist_kernel(const float* __restrict
     const f32x4* D4 = reinterpret_cast<const f32x4*>(D);
     for (int64_t pnl = blockIdx.x; pnl < npanels; pnl += gridDim.x) {
       const int64_t I = pnl / pcols, J = (pnl % pcols) >> 3;
-      if (J < I) continue;  // block-uniform
-      const uint32_t w = J == I ? 1u : 2u;
+      // wmap: the pair-split layout's tile weights; else the symmetric rule
+      const uint32_t w = wmap ? (uint32_t)wmap[I * (pcols >> 3) + J] : (J < I ? 0u : J == I ? 1u : 2u);
+      if (w == 0u) continue;  // block-uniform
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const f32x4 v = D4[pnl * (kPanelElems / 4) + h * 256 + threadIdx.x];
@@ -503,6 +505,20 @@ int dsvgd_radix_hist(const float* D, int64_t count, const float* cand, int pass,
   hipLaunchKernelGGL(radix_hist_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, D, count,
                      cand, pass, st, sym_npad);
   return check_launch("radix_hist");
+}
+
+int dsvgd_radix_hist_wmap(const float* D, int64_t m_pad, int64_t n_pad, const float* cand,
+                          int pass, dsvgd_select_state* st, const uint8_t* wmap, void* stream) {
+  DSVGD_REQUIRE(D && st && wmap, "null pointer");
+  DSVGD_REQUIRE(pass >= 1 && pass <= 3, "pass must be 1, 2 or 3");
+  DSVGD_REQUIRE(m_pad > 0 && n_pad > 0 && m_pad % 128 == 0 && n_pad % 128 == 0,
+                "m_pad, n_pad must be positive multiples of 128");
+  const int64_t count = m_pad * n_pad;
+  int64_t blocks = min((int64_t)4096, max((int64_t)1, count / kPanelElems));
+  if (cand && blocks < 1024) blocks = 1024;  // candidate slots: one wave each, grid-stride
+  hipLaunchKernelGGL(radix_hist_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     D, count, cand, pass, st, n_pad, wmap);
+  return check_launch("radix_hist_wmap");
 }
 
 int dsvgd_radix_pick(dsvgd_select_state* st, int pass, void* stream) {

@@ -552,6 +552,78 @@ int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, 
   return 0;
 }
 
+// The pair-split layout of a DistSampler rank (dsvgd_sqdist_h2_parts):
+// the owned row block's D as a list of parts -- its diagonal square (the
+// 8-wave symmetric launch with mirror stores), rectangles on the
+// one-wave-per-SIMD Gram (weight 2 when the rank holds the block pair
+// {(r, c), (c, r)} for both owners), and rectangles computed only when the
+// FmtH2 range guard trips (the fallback phi_mm then reads the whole row
+// block; no select accounting).  One candidate-slot numbering over the
+// accounted parts.
+template <int SM>
+int launch_sqdist_h2_parts(const _Float16* Yg, const float* norms, int64_t row0, int64_t m,
+                           int64_t n, int64_t d, float* D, dsvgd_select_state* st, float* cand,
+                           const dsvgd_gram_part* parts, int np, const float* gate,
+                           hipStream_t s, const float* rsc) {
+  using F = FmtH2;
+  const int64_t dp = roundup(d, 32), n_pad = roundup(n, 128);
+  const int64_t img = gram_img_rows(n);
+  constexpr int KS = kGramKS;
+  const int nk = (int)(dp / kX3Step / KS);
+  int rc = 0, bs = 0, bw = 0, bg = 0;
+  if ((rc = persistent_blocks(
+           reinterpret_cast<const void*>(&sqdist_x3w_kernel<true, SM, false, F, KS>), &bs, 512)))
+    return rc;
+  if ((rc = persistent_blocks(reinterpret_cast<const void*>(&gram_w1_kernel<SM, false>), &bw,
+                              GramW1::kThreads)))
+    return rc;
+  if ((rc = persistent_blocks(reinterpret_cast<const void*>(&gram_w1_kernel<kSelNone, false>),
+                              &bg, GramW1::kThreads)))
+    return rc;
+  auto walk = [&](const dsvgd_gram_part& P) {
+    return GramUnitWalk((int)(P.rows / 128), (int)(P.cols / 256), false);
+  };
+  int64_t ns_total = 0;
+  for (int i = 0; i < np; ++i) {
+    const dsvgd_gram_part& P = parts[i];
+    if (P.kind == 1)
+      ns_total += tile_grid(P.rows / 256, P.rows / 256, true) * 8;
+    else if (P.kind == 0)
+      ns_total += walk(P).total() * GramW1::kSlots;
+  }
+  int64_t base = 0;
+  for (int i = 0; i < np; ++i) {
+    const dsvgd_gram_part& P = parts[i];
+    if (P.kind == 1) {  // the diagonal square, upper tiles + mirror stores
+      const int sq = (int)(P.rows / 256);
+      const int64_t tot = tile_grid(sq, sq, true);
+      hipLaunchKernelGGL((sqdist_x3w_kernel<true, SM, false, F, KS, true>), dim3((unsigned)bs),
+                         dim3(512), 0, s, Yg, img, norms, row0, m, n, n_pad, nk, D, st, cand, tot,
+                         0, sq, sq, (int)(P.col0 / 256), (int)(row0 / 128), base, ns_total, rsc);
+      if ((rc = check_launch("sqdist_x3w(diag)"))) return rc;
+      base += tot * 8;
+      continue;
+    }
+    const GramUnitWalk wk = walk(P);
+    const int64_t tot = wk.total();
+    float* Dp = D + P.row_off * n_pad;  // panel rows of the part's strips
+    if (P.kind == 0) {
+      hipLaunchKernelGGL((gram_w1_kernel<SM, false>), dim3((unsigned)bw), dim3(GramW1::kThreads), 0,
+                         s, Yg, img, norms, rsc, row0 + P.row_off, P.rows, n, n_pad, nk * KS, Dp,
+                         st, cand, tot, wk.Tm, wk.Tc, (int)(P.col0 / 256), base, ns_total,
+                         (int)P.weight2, (const float*)nullptr);
+      base += tot * GramW1::kSlots;
+    } else {
+      hipLaunchKernelGGL((gram_w1_kernel<kSelNone, false>), dim3((unsigned)bg),
+                         dim3(GramW1::kThreads), 0, s, Yg, img, norms, rsc, row0 + P.row_off,
+                         P.rows, n, n_pad, nk * KS, Dp, st, (float*)nullptr, tot, wk.Tm, wk.Tc,
+                         (int)(P.col0 / 256), (int64_t)0, (int64_t)0, 0, gate);
+    }
+    if ((rc = check_launch("gram_w1(part)"))) return rc;
+  }
+  return 0;
+}
+
 // d <= 2 (supports up to 64): D_ij = sum_c (y_ic - y_jc)^2 from explicit differences on the VALU
 // (what torch.dist(x, y)**2 computes per pair at experiments/logreg.py:61):
 // no ||x||^2 - 2x.y cancellation, which at small d and a narrow median
@@ -774,6 +846,44 @@ int dsvgd_sqdist_h2(const void* Yg, const float* norms, int64_t row0, int64_t m,
       return launch_sqdist_x3<kSelBracket, FmtH2>(yg, norms, row0, m, n, d, D, st, cand, layout, s,
                                                   rowscale);
   }
+}
+
+int dsvgd_sqdist_h2_parts(const void* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
+                          int64_t d, float* D, int64_t ldd, int select_mode,
+                          dsvgd_select_state* st, float* cand, const dsvgd_gram_part* parts,
+                          int nparts, const float* gate, const float* rowscale, void* stream) {
+  DSVGD_REQUIRE(Yg && norms && D && rowscale && parts, "null pointer");
+  DSVGD_REQUIRE(m > 0 && n > 0 && row0 >= 0 && row0 + m <= n && d > 0, "sizes");
+  DSVGD_REQUIRE(select_mode == 0 || select_mode == 2, "select_mode must be 0 or 2 (bracket)");
+  DSVGD_REQUIRE(select_mode == 0 || (st && cand), "bracket mode needs a state and candidates");
+  const int64_t n_pad = roundup(n, 128), dp = roundup(d, 32);
+  DSVGD_REQUIRE(ldd == n_pad, "ldd must equal roundup(n,128) (panel layout)");
+  DSVGD_REQUIRE(dp % 256 == 0, "parts need roundup(d, 32) % 256 == 0 (the one-wave Gram)");
+  DSVGD_REQUIRE(row0 % 256 == 0 && m % 256 == 0, "row0 and m must be multiples of 256");
+  DSVGD_REQUIRE(((uintptr_t)Yg & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
+  DSVGD_REQUIRE(dp * gram_img_rows(n) * 4 < ((int64_t)1 << 31),
+                "image too large for 32-bit buffer offsets");
+  DSVGD_REQUIRE(nparts > 0 && nparts <= 64, "1 .. 64 parts");
+  for (int i = 0; i < nparts; ++i) {
+    const dsvgd_gram_part& P = parts[i];
+    DSVGD_REQUIRE(P.kind >= 0 && P.kind <= 2, "part kind must be 0, 1 or 2");
+    DSVGD_REQUIRE(P.row_off >= 0 && P.rows > 0 && P.row_off + P.rows <= m &&
+                      P.row_off % 128 == 0 && P.rows % 128 == 0,
+                  "part rows must be a 128-aligned range of the owned block");
+    DSVGD_REQUIRE(P.col0 >= 0 && P.cols > 0 && P.col0 + P.cols <= n_pad && P.col0 % 256 == 0 &&
+                      P.cols % 256 == 0,
+                  "part columns must be a 256-aligned range of [0, n_pad)");
+    DSVGD_REQUIRE(P.kind != 1 || (P.row_off == 0 && P.rows == m && P.cols == m && P.col0 == row0),
+                  "the diagonal part is the owned block's square");
+    DSVGD_REQUIRE(P.kind != 2 || gate, "a fallback part needs the range-guard word");
+  }
+  const _Float16* yg = (const _Float16*)Yg;
+  hipStream_t s = (hipStream_t)stream;
+  if (select_mode == 0)
+    return launch_sqdist_h2_parts<kSelNone>(yg, norms, row0, m, n, d, D, st, cand, parts, nparts,
+                                            gate, s, rowscale);
+  return launch_sqdist_h2_parts<kSelBracket>(yg, norms, row0, m, n, d, D, st, cand, parts, nparts,
+                                             gate, s, rowscale);
 }
 
 }  // extern "C"

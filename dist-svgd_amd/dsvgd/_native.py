@@ -18,6 +18,20 @@ _i64 = _c.c_int64
 _f = _c.c_float
 _int = _c.c_int
 
+
+
+class GramPart(ctypes.Structure):
+    """Mirror of dsvgd_gram_part (include/dsvgd.h)."""
+    _fields_ = [("row_off", _i64), ("rows", _i64), ("col0", _i64), ("cols", _i64),
+                ("kind", ctypes.c_int32), ("weight2", ctypes.c_int32)]
+
+
+class PhiPart(ctypes.Structure):
+    """Mirror of dsvgd_phi_part (include/dsvgd.h)."""
+    _fields_ = [("ky", _p), ("rs", _p), ("ldk", _i64), ("row_off", _i64), ("rows", _i64),
+                ("splits", _i64)]
+
+
 # name -> (restype, argtypes); must mirror include/dsvgd.h exactly
 SIGNATURES = {
     "dsvgd_abi_version": (_int, []),
@@ -102,6 +116,17 @@ SIGNATURES = {
                                            _p]),
     "dsvgd_logreg_predict_workspace_bytes": (_c.c_size_t, [_i64, _i64, _i64]),
     "dsvgd_logreg_predict": (_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _p, _p]),
+    # the pair-split layout (ABI 4)
+    "dsvgd_sqdist_h2_parts": (_int, [_p, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p,
+                                     _int, _p, _p, _p]),
+    "dsvgd_radix_hist_wmap": (_int, [_p, _i64, _i64, _p, _int, _p, _p, _p]),
+    "dsvgd_phi_h2_window": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p,
+                                   _i64, _p, _p, _p, _int, _p]),
+    "dsvgd_phi_h2_transposed": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _i64,
+                                       _p, _i64, _p, _p, _p, _int, _p]),
+    "dsvgd_phi_partial_reduce": (_int, [_p, _i64, _p, _i64, _i64, _i64, _p, _i64, _p, _p]),
+    "dsvgd_phi_finish_parts": (_int, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _f,
+                                      _f, _p, _i64, _p, _i64, _p, _i64, _p, _int, _p, _i64, _p]),
 }
 
 

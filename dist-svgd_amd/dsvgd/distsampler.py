@@ -283,15 +283,29 @@ class DistSampler(object):
         self._replicated = all(f == fps[0] for f in fps)
 
     # ------------------------------------------------------------ step --
+    pair_split = True   # Jacobi with identical scores on every rank: the block-pair layout
+
+    def _use_pair_split(self, n_int, m):
+        """The pair-split layout (dsvgd.pairsplit) applies when
+        every rank moves its own block with the same scores of all n
+        particles (all_scores, or replicated data) in the Jacobi order."""
+        S = self._num_shards
+        return (self.pair_split and S > 1 and self._order == "jacobi" and self._exchange_particles
+                and (self._exchange_scores or self._replicated) and not self._lagged
+                and n_int == S * m and PhiEngine.pair_split_ok(n_int, self._d, S,
+                                                               median=self._rbf.median))
+
     def _engine(self, n_int, m, row0):
-        """One engine per (interacting set, owned rows, median kind); the
-        owned rows' offset row0 is set per step (lagged modes rotate it)."""
+        """One engine per (interacting set, owned rows, median kind, layout);
+        the owned rows' offset row0 is set per step (lagged modes rotate it)."""
         local = self._lagged == "local"
-        key = (n_int, m, local)
+        ps = self._use_pair_split(n_int, m)
+        key = (n_int, m, local, ps)
         if key not in self._engines:
             self._engines.clear()      # the old D is freed before the new one is allocated
-            self._engines[key] = PhiEngine(n_int, self._d, m=m, row0=row0, device=self._device,
-                                           local_median=local)
+            self._engines[key] = PhiEngine(
+                n_int, self._d, m=m, row0=row0, device=self._device, local_median=local,
+                pair_split=(self._rank, self._num_shards) if ps else None)
         eng = self._engines[key]
         eng.set_row0(row0)
         eng.timer = self.timer
@@ -363,7 +377,10 @@ class DistSampler(object):
             if side is not main:
                 main.wait_stream(side)
             eng.pack_scores(Si)                    # Si already carries the score scale
-            eng.direction(X[us:ue], step_size, write_phi=self.keep_phi, extra=w2g)
+            p2p = None
+            if eng.plan is not None:
+                p2p = lambda sends, recvs: exchange.exchange_p2p_async(sends, recvs, self._group)
+            eng.direction(X[us:ue], step_size, write_phi=self.keep_phi, extra=w2g, p2p=p2p)
         else:
             if median:
                 eng = self._engine(n_int, ue - us, us - lo)

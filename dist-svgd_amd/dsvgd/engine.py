@@ -145,7 +145,7 @@ class PhiEngine(object):
     DEFAULT_GEMM = "h2"
 
     def __init__(self, n, d, m=None, row0=0, device=None, local_median=False, gemm=None,
-                 phi_gemm=None, gram_gemm=None, sym_layout=True):
+                 phi_gemm=None, gram_gemm=None, sym_layout=True, pair_split=None):
         """local_median: the median bandwidth is the lower median of the owned
         block's own m x n entries (k = (m n - 1) // 2, h = median / log n) --
         a rank-local bandwidth (the lagged DistSampler modes) -- instead of the
@@ -155,7 +155,15 @@ class PhiEngine(object):
         override it per contraction; None: DEFAULT_GEMM): "h2" the fp16 two-part split (default,
         include/dsvgd.h FmtH2), "x3" the bf16 three-part split, "f32" the exact
         f32 MFMA (precision reference).  sym_layout=False keeps the full D
-        layout where the symmetric one would apply (layout experiments)."""
+        layout where the symmetric one would apply (layout experiments).
+
+        pair_split=(rank, S): the owned block is rank's row block of S and
+        the S ranks split the symmetric matrix by block pairs
+        (dsvgd.pairsplit): distances() computes this rank's
+        parts only, direction(p2p=...) exchanges the transposed partials.
+        Needs the same scores on every rank, the FmtH2 engines, m = n / S a
+        multiple of 256, roundup(d, 32) a multiple of 256 and a bracketed
+        (or fixed) bandwidth -- PhiEngine.pair_split_ok says whether it applies."""
         dev = N.require_gpu(device if device is not None else "cuda")
         lib = N.load()
         m = n if m is None else m
@@ -234,6 +242,9 @@ class PhiEngine(object):
         self.mean = torch.empty(d, **f32)    # the packing centre (dsvgd_colcenter)
         self.phi = torch.empty(m, d, **f32)
         self.state = SelectState(dev)
+        self.plan = None
+        if pair_split is not None:
+            self._init_pair_split(*pair_split)
         self.k_rank = (m * n - 1) // 2 if (local_median and m < n) else -1
         self.bracketed = m * n >= self.BRACKET_MIN_ENTRIES and self.k_rank < 0
         if self.bracketed:
@@ -336,6 +347,13 @@ class PhiEngine(object):
         elif median:
             N.call("dsvgd_select_init", self.state.ptr, self.n, self.k_rank, s)
             st, mode = self.state.ptr, SEL_HIST
+        if self.plan is not None:
+            with span(self.timer, "rowsplit"):
+                N.call("dsvgd_h2_rowsplit_rows", N.ptr(self.Y), self.ldy, self.n_pad, self.dp,
+                       self.gram_rows, self.dp, N.ptr(self.rsc), N.ptr(self.Yg), s)
+            with span(self.timer, "sqdist"):
+                self._gram_parts(self._gparts, mode, st, cand, s)
+            return
         if self.gram_gemm == "h2" and self.d > self.DIRECT_MAX_D:
             with span(self.timer, "rowsplit"):
                 if not self.fused_scales:   # (pack wrote them otherwise)
@@ -382,8 +400,12 @@ class PhiEngine(object):
         for p in (1, 2, 3):
             if p > 1 or self.bracketed:
                 with span(self.timer, "radix_hist"):
-                    N.call("dsvgd_radix_hist", N.ptr(self.D), count, cand, p, self.state.ptr,
-                           self.n_pad if self.sym else 0, s)
+                    if self.plan is not None:   # the fallback over D weighs the rank's tiles
+                        N.call("dsvgd_radix_hist_wmap", N.ptr(self.D), self.m_pad, self.n_pad,
+                               cand, p, self.state.ptr, N.ptr(self.wmap), s)
+                    else:
+                        N.call("dsvgd_radix_hist", N.ptr(self.D), count, cand, p,
+                               self.state.ptr, self.n_pad if self.sym else 0, s)
             if allreduce is not None:
                 with span(self.timer, "hist_allreduce"):
                     allreduce(self.state.hist)
@@ -422,11 +444,16 @@ class PhiEngine(object):
         return (self.m == self.n and self.row0 == 0 and self.d > self.DIRECT_MAX_D
                 and self.x3 and self.x3_gram and self.ldy % 256 == 0 and self.sym_layout)
 
-    def direction(self, X_own=None, step=0.0, write_phi=True, inv_n=None, extra=None):
+    def direction(self, X_own=None, step=0.0, write_phi=True, inv_n=None, extra=None, p2p=None):
         """phi for the owned rows (+ `extra`, e.g. the h * W2 gradient rows);
         optionally X_own += step * phi (in place).
-        d <= DIRECT_MAX_D: pairwise VALU form (dsvgd_phi_direct); else K.[Xc|S] on MFMA."""
+        d <= DIRECT_MAX_D: pairwise VALU form (dsvgd_phi_direct); else K.[Xc|S] on MFMA.
+        Pair split: p2p(sends, recvs) posts the partials' exchange
+        ([(tensor, rank)] each) and returns a callable that joins it."""
         s = N.stream(self.device)
+        if self.plan is not None:
+            self._direction_pair_split(X_own, step, write_phi, inv_n, extra, p2p, s)
+            return
         if X_own is not None:
             assert X_own.shape == (self.m, self.d)
         if extra is not None:
@@ -489,6 +516,161 @@ class PhiEngine(object):
         N.call("dsvgd_phi_finish", N.ptr(self.KY), self.ldy, N.ptr(self.rowsum), self.splits,
                N.ptr(self.Y), self.ldy, self.row0, self.m, self.d, self.dp, self.state.ptr,
                float(inv_n), float(step), ex, lde, phi, self.d, xo, ldx, s)
+
+    # ---------------------------------------------------- pair split --
+    @classmethod
+    def pair_split_ok(cls, n, d, S, gemm=None, median=True):
+        """Whether PhiEngine(n, d, m=n/S, pair_split=(r, S)) applies."""
+        lib = N.load()
+        m = n // S
+        dp = lib.dsvgd_dp(d)
+        ldy = lib.dsvgd_ldy(dp)
+        n_pad = lib.dsvgd_pad128(n)
+        return (S >= 2 and m * S == n and m % 256 == 0 and dp % 256 == 0 and ldy % 512 == 0
+                and (gemm or cls.DEFAULT_GEMM) == "h2" and d > cls.DIRECT_MAX_D
+                and n_pad * ldy * 6 < (1 << 31) and dp * (n_pad + 256) * 4 < (1 << 31)
+                and (not median or m * n >= cls.BRACKET_MIN_ENTRIES)
+                and ldy <= lib.dsvgd_pack_max_ldy())
+
+    def _init_pair_split(self, rank, S):
+        from .pairsplit import PairSplitPlan
+        lib = N.load()
+        if not (self.m * S == self.n and self.row0 == rank * self.m and self.phi_gemm == "h2"
+                and self.gram_gemm == "h2" and self.fused_scales and self.Yx3 is not None
+                and self.ldy % 512 == 0 and self.dp % 256 == 0):
+            raise ValueError("pair_split needs m = n / S = the rank's block, the FmtH2 engines, "
+                             "m % 256 == 0 and roundup(d, 32) % 256 == 0")
+        P = self.plan = PairSplitPlan(rank, S, self.m)
+        dev, f32 = self.device, dict(dtype=torch.float32, device=self.device)
+
+        def gparts(lst):
+            arr = (N.GramPart * len(lst))()
+            for a, q in zip(arr, lst):
+                a.row_off, a.rows, a.col0, a.cols = q["row_off"], q["rows"], q["col0"], q["cols"]
+                a.kind, a.weight2 = q["kind"], q["weight2"]
+            return arr
+        self._gparts = gparts(P.gram_parts)
+        self._fbparts = gparts(P.fallback_parts)
+        self.wmap = torch.tensor(P.tile_weights(), dtype=torch.uint8, device=dev).reshape(-1)
+        ldy = self.ldy
+        # own direct product over the window: split-K slices into KY (the
+        # fallback's whole-row phi_mm uses self.splits slices of the same KY)
+        wlen = P.window[1]
+        self.w_splits = int(lib.dsvgd_phi_splits(self.m, wlen, ldy))
+        need = max(self.w_splits, self.splits)
+        if self.KY.shape[0] < need * self.m:
+            self.KY = torch.empty(need * self.m, ldy, **f32)
+            self.rowsum = torch.empty(need * self.m_pad, **f32)
+        # the high rank's row half: its own slices
+        if P.row_half:
+            ro, nr, c0, nc = P.row_half
+            self.h_splits = int(lib.dsvgd_phi_splits(nr, nc, ldy))
+            self.KYh = torch.empty(self.h_splits * nr, ldy, **f32)
+            self.rsh = torch.empty(self.h_splits * lib.dsvgd_pad128(nr), **f32)
+
+        # partials: one message per peer = [mo x ldy | roundup128(mo)] floats
+        def msg(rows):
+            return torch.empty(rows * ldy + lib.dsvgd_pad128(rows), **f32)
+        self.t_splits = []
+        smax = 0
+        for q in P.sends:
+            blocks = (ldy // 512) * (q["mo"] // 128)
+            z = 1
+            while blocks * z < 256 and q["krows"] // (2 * z) >= 1024:
+                z *= 2
+            self.t_splits.append(z)
+            smax = max(smax, z * q["mo"]) if z > 1 else smax
+        self.sendbuf = [msg(q["mo"]) for q in P.sends]
+        self.recvbuf = [msg(q["rows"]) for q in P.recvs]
+        mo_max = max([q["mo"] for q in P.sends] + [128])
+        self.tP = torch.empty(max(smax, 1), ldy, **f32)
+        self.tRS = torch.empty(max(t for t in self.t_splits) * lib.dsvgd_pad128(mo_max), **f32)
+        parts = []
+        if P.row_half:
+            ro, nr, _, _ = P.row_half
+            parts.append((N.ptr(self.KYh), N.ptr(self.rsh), ldy, ro, nr, self.h_splits))
+        for q, buf in zip(P.recvs, self.recvbuf):
+            parts.append((N.ptr(buf), N.ptr(buf) + 4 * q["rows"] * ldy, ldy, q["row_off"],
+                          q["rows"], 1))
+        arr = (N.PhiPart * len(parts))()
+        for a, q in zip(arr, parts):
+            a.ky, a.rs, a.ldk, a.row_off, a.rows, a.splits = q
+        self._phiparts = arr
+
+    def _gram_parts(self, arr, mode, st, cand, s, gate=None):
+        N.call("dsvgd_sqdist_h2_parts", N.ptr(self.Yg), N.ptr(self.norms), self.row0, self.m,
+               self.n, self.d, N.ptr(self.D), self.n_pad, mode, st, cand, ctypes.addressof(arr),
+               len(arr), gate, N.ptr(self.rsc), s)
+
+    def _direction_pair_split(self, X_own, step, write_phi, inv_n, extra, p2p, s):
+        """phi of the owned rows in the pair-split layout: the transposed
+        partials of the blocks this rank holds for others (sent as soon as
+        they are reduced), the own window (and row half) while they travel,
+        then phi_finish over the own slices + the partials received.  The
+        FmtH2 range guard (device word) instead runs the FmtX3 phi_mm over
+        the whole row block, after the Gram of the parts this rank does not
+        hold (gated launches: no host round trip)."""
+        P, ldy, lib = self.plan, self.ldy, N.load()
+        guard = N.ptr(self.yscale) + 4 * (2 * ldy + 2)
+        colinv = N.ptr(self.yscale) + 4 * ldy
+        with span(self.timer, "ysplit"):
+            self._scales(ldy, self.yscale, s)
+            N.call("dsvgd_h2_ysplit", N.ptr(self.Y), ldy, self.n_pad, N.ptr(self.yscale),
+                   N.ptr(self.Yx), s)
+        with span(self.timer, "phi_partials"):
+            for q, z, buf in zip(P.sends, self.t_splits, self.sendbuf):
+                Dq = N.ptr(self.D) + 4 * q["row_off"] * self.n_pad
+                mo = q["mo"]
+                rs_out = N.ptr(buf) + 4 * mo * ldy
+                if z == 1:
+                    N.call("dsvgd_phi_h2_transposed", Dq, self.n_pad, N.ptr(self.Yx), ldy,
+                           self.row0 + q["row_off"], q["krows"], q["col0"], mo, self.n,
+                           self.state.ptr, 1, N.ptr(buf), ldy, rs_out, colinv, guard, 0, s)
+                else:
+                    N.call("dsvgd_phi_h2_transposed", Dq, self.n_pad, N.ptr(self.Yx), ldy,
+                           self.row0 + q["row_off"], q["krows"], q["col0"], mo, self.n,
+                           self.state.ptr, z, N.ptr(self.tP), ldy, N.ptr(self.tRS), colinv,
+                           guard, 0, s)
+                    N.call("dsvgd_phi_partial_reduce", N.ptr(self.tP), ldy, N.ptr(self.tRS), z,
+                           mo, ldy, N.ptr(buf), ldy, rs_out, s)
+        join = None
+        if p2p is not None:
+            with span(self.timer, "partials_post"):
+                join = p2p([(b, q["dest"]) for q, b in zip(P.sends, self.sendbuf)],
+                           [(b, q["src"]) for q, b in zip(P.recvs, self.recvbuf)])
+        with span(self.timer, "phi_mm"):
+            w0, wl = P.window
+            N.call("dsvgd_phi_h2_window", N.ptr(self.D), self.n_pad, N.ptr(self.Yx), ldy,
+                   self.row0, self.m, self.n, w0, wl, self.state.ptr, self.w_splits,
+                   N.ptr(self.KY), ldy, N.ptr(self.rowsum), colinv, guard, 0, s)
+            if P.row_half:
+                ro, nr, c0, nc = P.row_half
+                N.call("dsvgd_phi_h2_window", N.ptr(self.D) + 4 * ro * self.n_pad, self.n_pad,
+                       N.ptr(self.Yx), ldy, self.row0 + ro, nr, self.n, c0, nc, self.state.ptr,
+                       self.h_splits, N.ptr(self.KYh), ldy, N.ptr(self.rsh), colinv, guard, 0, s)
+        with span(self.timer, "phi_guard"):
+            # the range guard's fallback: the rest of the row block's D, then
+            # the FmtX3 phi_mm over all of it (gated: nothing while the guard is 0)
+            self._gram_parts(self._fbparts, SEL_NONE, None, None, s, gate=guard)
+            N.call("dsvgd_ysplit", N.ptr(self.Y), ldy, self.n_pad, N.ptr(self.Yx3),
+                   0 if self.m16_fb else 1, guard, s)
+            N.call("dsvgd_phi_mm_x3", N.ptr(self.D), self.n_pad, N.ptr(self.Yx3), ldy, self.row0,
+                   self.m, self.n, self.state.ptr, self.splits, N.ptr(self.KY), ldy,
+                   N.ptr(self.rowsum), 0, int(self.m16_fb), guard, s)
+        if join is not None:
+            with span(self.timer, "partials_wait"):
+                join()
+        if extra is not None:
+            assert extra.shape == (self.m, self.d) and extra.dtype == torch.float32
+        ex, lde = (N.ptr(extra), N.ld(extra)) if extra is not None else (None, self.d)
+        inv_n = 1.0 / self.n if inv_n is None else inv_n
+        phi = N.ptr(self.phi) if write_phi else None
+        xo = N.ptr(X_own)
+        ldx = N.ld(X_own) if X_own is not None else self.d
+        N.call("dsvgd_phi_finish_parts", N.ptr(self.KY), ldy, N.ptr(self.rowsum), self.w_splits,
+               N.ptr(self.Y), ldy, self.row0, self.m, self.d, self.dp, self.state.ptr,
+               float(inv_n), float(step), ex, lde, phi, self.d, xo, ldx,
+               ctypes.addressof(self._phiparts), len(self._phiparts), guard, self.splits, s)
 
     def range_guard(self):
         """The last phi_mm's FmtH2 range guard (True: it ran on the fallback

@@ -60,6 +60,26 @@ def ring_shift(send, recv, rank, size, group=None):
     exchange_p2p([(send, dst)], [(recv, src)], group)
 
 
+def exchange_p2p_async(sends, recvs, group=None):
+    """exchange_p2p without the join: returns a callable that joins the
+    transfers.  On RCCL the ops are posted on the process group's stream
+    (after the work already queued on the current stream) and the join makes
+    the current stream wait for them, so kernels enqueued in between overlap
+    the transfers; gloo completes them here (host staging) and returns a no-op."""
+    dev = any(t.is_cuda for t, _ in list(sends) + list(recvs))
+    if not (dev and not _is_gloo(group)) or (not sends and not recvs):
+        exchange_p2p(sends, recvs, group)
+        return lambda: None
+    ops = [dist.P2POp(dist.isend, t, group=group, group_peer=p) for t, p in sends]
+    ops += [dist.P2POp(dist.irecv, t, group=group, group_peer=p) for t, p in recvs]
+    works = dist.batch_isend_irecv(ops)
+
+    def join():
+        for w in works:
+            w.wait()
+    return join
+
+
 def exchange_p2p(sends, recvs, group=None):
     """Point-to-point transfers in one batch: sends = [(tensor, group_rank)],
     recvs = [(tensor, group_rank)], peers as ranks of `group`.  On RCCL the

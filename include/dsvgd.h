@@ -334,6 +334,83 @@ int dsvgd_h2_rowscale(const float* A, int64_t lda, int64_t rows, int64_t cols, i
 int dsvgd_sqdist_h2(const void* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
                     int64_t d, float* D, int64_t ldd, int select_mode, dsvgd_select_state* st,
                     float* cand, int layout, const float* rowscale, void* stream);
+/* ---- the pair-split layout of a DistSampler rank (ABI 4) ---
+ * With the scores identical on every rank (all_scores, or replicated data),
+ * the S ranks split the symmetric n x n matrix by BLOCK PAIRS: rank r
+ * computes its diagonal square, the forward blocks (r, r+1) .. (r, r+S/2-1)
+ * (mod S) and half of the antipodal pair {(r, r+S/2), (r+S/2, r)}; for each
+ * block (r, c) it holds it sends the owner of c the partial K(r,c)^T Y_r
+ * (dsvgd_phi_h2_transposed), and sums the partials it receives into its own
+ * phi (dsvgd_phi_finish_parts).  Replaces the interaction loop of
+ * dsvgd/distsampler.py:84-101 over the all-gathered particles (:152-170).
+ *
+ * dsvgd_sqdist_h2_parts: dsvgd_sqdist_h2 over a list of parts of the owned
+ * row block [row0, row0 + m) (host array).  kind 0: a rectangle (rows
+ * [row_off, +rows) of the block x global columns [col0, +cols)) whose
+ * entries count twice in the median select when weight2 (the rank holds the
+ * pair for both owners); kind 1: the block's diagonal square (row_off = 0,
+ * rows = cols = m, col0 = row0; upper tiles + mirror stores); kind 2: a
+ * rectangle computed only while *gate != 0 (the FmtH2 range guard: the
+ * fallback phi_mm reads the whole row block), without select accounting.
+ * select_mode 0 or 2 (bracket); dp % 256 == 0; row0, m multiples of 256;
+ * col0, cols multiples of 256, row_off, rows of 128. */
+typedef struct dsvgd_gram_part {
+  int64_t row_off, rows, col0, cols;
+  int32_t kind, weight2;
+} dsvgd_gram_part;
+int dsvgd_sqdist_h2_parts(const void* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
+                          int64_t d, float* D, int64_t ldd, int select_mode,
+                          dsvgd_select_state* st, float* cand, const dsvgd_gram_part* parts,
+                          int nparts, const float* gate, const float* rowscale, void* stream);
+/* dsvgd_radix_hist with a tile weight map instead of the symmetric rule:
+ * the panel of D tile (I, J) (128 x 128, panel layout, m_pad x n_pad) counts
+ * wmap[I * (n_pad / 128) + J] times (0: not an entry of this rank's share). */
+int dsvgd_radix_hist_wmap(const float* D, int64_t m_pad, int64_t n_pad, const float* cand,
+                          int pass, dsvgd_select_state* st, const uint8_t* wmap, void* stream);
+/* phi_mm (FmtH2) of rows [row0, row0 + m) of the interacting set (D: their
+ * panel rows) over a CYCLIC window of columns [col0, col0 + wlen) mod
+ * n_pad, into `splits` split-K slices (KY + z m ldk, rowsum + z
+ * roundup(m,128)); the diagonal j == row0 + i skipped as in dsvgd_phi_mm.
+ * col0, wlen multiples of 16.  gate / gate_on as dsvgd_phi_mm_h2 (run iff
+ * (*gate != 0) == gate_on). */
+int dsvgd_phi_h2_window(const float* D, int64_t ldd, const void* Yh, int64_t ldy, int64_t row0,
+                        int64_t m, int64_t n, int64_t col0, int64_t wlen,
+                        const dsvgd_select_state* st, int64_t splits, float* KY, int64_t ldk,
+                        float* rowsum, const float* colinv, const float* gate, int gate_on,
+                        void* stream);
+/* The transposed partial of a rectangle of D: D points at the rectangle's
+ * first row (a 128-row panel row; its rows are interacting-set rows yrow0 ..
+ * yrow0 + krows - 1), its columns [col0, col0 + mo) (col0 a multiple of
+ * 128).  P_z[i][:] = sum_{j in slice z} exp(-D[j][col0 + i]/h) Y[yrow0 + j][:]
+ * and rs_z[i] the same sum of the weights, for i < mo (KY layout: P + z mo
+ * ldp, rs + z roundup(mo,128)).  krows a multiple of 16. */
+int dsvgd_phi_h2_transposed(const float* D, int64_t ldd, const void* Yh, int64_t ldy,
+                            int64_t yrow0, int64_t krows, int64_t col0, int64_t mo, int64_t n,
+                            const dsvgd_select_state* st, int64_t splits, float* P, int64_t ldp,
+                            float* rs, const float* colinv, const float* gate, int gate_on,
+                            void* stream);
+/* out[i][c] = sum_z P[z][i][c] (c < cols) and out_rs[i] = sum_z rs[z][i], in
+ * slice order (the P / rs layout of dsvgd_phi_h2_transposed). */
+int dsvgd_phi_partial_reduce(const float* P, int64_t ldp, const float* rs, int64_t splits,
+                             int64_t rows, int64_t cols, float* out, int64_t ldo, float* out_rs,
+                             void* stream);
+/* dsvgd_phi_finish over the own split-K slices plus `nparts` partials, each
+ * adding ky[z][i - row_off][:] and rs[z][i - row_off] (z < splits) to rows
+ * row_off <= i < row_off + rows, summed in list order after the own slices.
+ * gate (nullable): while *gate != 0 the parts are skipped and the own slices
+ * are `splits_fb` (the range guard's whole-row-block fallback). */
+typedef struct dsvgd_phi_part {
+  const float* ky;
+  const float* rs;
+  int64_t ldk, row_off, rows, splits;
+} dsvgd_phi_part;
+int dsvgd_phi_finish_parts(const float* KY, int64_t ldk, const float* rowsum, int64_t splits,
+                           const float* Y, int64_t ldy, int64_t row0, int64_t m, int64_t d,
+                           int64_t dp, const dsvgd_select_state* st, float inv_n, float step,
+                           const float* extra, int64_t lde, float* phi, int64_t ldphi, float* X,
+                           int64_t ldx, const dsvgd_phi_part* parts, int nparts,
+                           const float* gate, int64_t splits_fb, void* stream);
+
 /* dsvgd_phi_mm_x3 on the FmtH2 engine: Yh = dsvgd_h2_ysplit(Y, ldy, n_pad,
  * scale) and colinv = &scale[ldy] of a dsvgd_h2_colscale over all ldy
  * columns of Y; same outputs (unscaled), split-K slices, diagonal rule and

@@ -211,3 +211,62 @@ def test_dist_oracle_jacobi_equals_sequential_at_tiny_step(golden):
     a.step(1e-7)
     b.step(1e-7)
     assert np.abs(a.X[0] - b.X[0]).max() < 1e-9
+
+
+@pytest.mark.parametrize("S", [2, 3, 4, 5, 6, 8])
+def test_pair_split_plan_covers_the_matrix(S):
+    """The pair-split layout (dsvgd/pairsplit.py) simulated on
+    index sets: (1) every phi_i receives K_ij Y_j exactly once for every j --
+    from its own window / row half, or transposed from the partial of the
+    rank that holds (j, i); (2) every partial sent is a rectangle its sender
+    computed, received by the destination with the same rows; (3) the Gram
+    parts compute each unordered pair with total select weight 2 (the
+    diagonal once), i.e. n^2 weighted entries; (4) the fallback parts
+    complete each rank's row block."""
+    from dsvgd.pairsplit import PairSplitPlan
+    m = 256
+    n = S * m
+    cov = np.zeros((n, n), np.int32)
+    wsum = np.zeros((n, n), np.int32)
+    plans = [PairSplitPlan(r, S, m) for r in range(S)]
+    for r, P in enumerate(plans):
+        rows = slice(r * m, (r + 1) * m)
+        computed = np.zeros((m, n), bool)
+        for p in P.gram_parts:
+            blk = (slice(p["row_off"], p["row_off"] + p["rows"]), slice(p["col0"], p["col0"] + p["cols"]))
+            assert not computed[blk].any()
+            computed[blk] = True
+            g = (slice(r * m + p["row_off"], r * m + p["row_off"] + p["rows"]), blk[1])
+            wsum[g] += 1 if p["kind"] == P.GRAM_DIAG else (2 if p["weight2"] else 1)
+        tw = np.kron(np.array(P.tile_weights()), np.ones((128, 128), np.int32))
+        assert np.array_equal(tw > 0, computed)
+        full = computed.copy()
+        for p in P.fallback_parts:
+            blk = (slice(p["row_off"], p["row_off"] + p["rows"]), slice(p["col0"], p["col0"] + p["cols"]))
+            assert not full[blk].any()
+            full[blk] = True
+        assert full.all()
+        for c0, ln in P.window_parts():
+            assert computed[:, c0:c0 + ln].all()
+            cov[rows, c0:c0 + ln] += 1
+        if P.row_half:
+            ro, nr, c0, nc = P.row_half
+            assert computed[ro:ro + nr, c0:c0 + nc].all()
+            cov[r * m + ro:r * m + ro + nr, c0:c0 + nc] += 1
+        for s in P.sends:
+            blk = computed[s["row_off"]:s["row_off"] + s["krows"], s["col0"]:s["col0"] + s["mo"]]
+            assert blk.all()
+            d = s["dest"]
+            rv = [q for q in plans[d].recvs if q["src"] == r]
+            assert len(rv) == 1 and rv[0]["rows"] == s["mo"] and rv[0]["row_off"] == s["dst_row_off"]
+            # transposed: column j of the rectangle is row j of the destination's phi
+            assert d * m + s["dst_row_off"] == s["col0"]
+            cov[s["col0"]:s["col0"] + s["mo"],
+                r * m + s["row_off"]:r * m + s["row_off"] + s["krows"]] += 1
+        assert sorted(q["src"] for q in P.recvs) == sorted(
+            q for q in range(S) if any(s["dest"] == r for s in plans[q].sends))
+    assert (cov == 1).all()
+    sym = wsum + wsum.T
+    assert (np.diag(wsum) == 1).all()
+    off = ~np.eye(n, dtype=bool)
+    assert (sym[off] == 2).all() and int(wsum.sum()) == n * n
