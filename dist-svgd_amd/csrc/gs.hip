@@ -24,6 +24,7 @@
 #include <cmath>
 
 #include "common.hpp"
+#include "gemm_tiles.hpp"
 
 namespace dsvgd {
 
@@ -274,6 +275,140 @@ __global__ __launch_bounds__(256) void gs_sweep_kernel(
   }
 }
 
+// ---- d > 64: the wide blocked sweep (engine.sequential_sweep) -----------
+// The block's wide pass runs on the exact f32 MFMA engines of the Jacobi
+// step (dsvgd_sqdist over the centred rows Y = [X - c | S], then
+// dsvgd_phi_mm over all n columns with the block's own earlier rows masked
+// to +inf here, then dsvgd_phi_partial_reduce): Q = [K Xc | K S] and r = K 1
+// of the rows [r0, r0 + B) against every row not moved before them in the
+// block.  The walk (gsw_sweep_kernel) then moves the B rows in order with one
+// workgroup: per row the distances to the rows already moved (all 256
+// threads, a quarter of the features each), their kernel values, and per
+// column the moved rows' terms k_j w_j, w_j = s_j' - (2/h)(x_j' - c).  LDS
+// holds the moved rows (centred x' and w) and the old row being moved, so B
+// d <= kGswLds.
+constexpr int kGswLds = 16384;   // floats per LDS array (64 KiB): B = min(64, kGswLds / dp)
+constexpr int kGswMaxD = 1024;
+
+__host__ __device__ inline int gsw_rows(int64_t dp) {
+  const int64_t b = kGswLds / dp;
+  return (int)(b >= kGsB ? kGsB : b);
+}
+
+// D[i][r0 + j] = +inf for j < i < B (panel layout, row i of the block's D):
+// the pairs the walk takes with the moved rows
+__global__ void gs_mask_kernel(float* __restrict__ D, int64_t ldd, int64_t r0, int B) {
+  const int i = blockIdx.x, j = threadIdx.x;
+  if (j >= i || i >= B) return;
+  const int64_t col = r0 + j;
+  D[((int64_t)(i >> 7) * (ldd >> 4) + (col >> 4)) * kPanelElems + (i & 127) * 16 + (col & 15)] =
+      INFINITY;
+}
+
+// One workgroup of 256 threads walks rows [r0, r0 + B).  Q: [K Xc | K S] of
+// the wide pass (ldq >= 2 dp), Qr its row sums; Y: [X - c | S] (updated for
+// each moved row, with norms[]), centre c = the Y packing centre.
+__global__ __launch_bounds__(256) void gsw_sweep_kernel(
+    float* __restrict__ X, int64_t ldx, float* __restrict__ S, int64_t lds, float* __restrict__ Y,
+    int64_t ldy, float* __restrict__ norms, const float* __restrict__ center, int64_t n, int d,
+    int dp, int64_t r0, int B, const dsvgd_select_state* __restrict__ st, float step,
+    const float* __restrict__ Q, int64_t ldq, const float* __restrict__ Qr,
+    const float* __restrict__ extra, int64_t lde, float* __restrict__ phi_out, int64_t ldphi,
+    int score_kind, const float* __restrict__ mu, const float* __restrict__ lam,
+    float score_scale) {
+  extern __shared__ __attribute__((aligned(16))) float gsw_smem[];
+  const int pitch = dp + 4;                       // 16-byte rows, 4 banks apart
+  float* xn = gsw_smem;                           // [B][pitch]: moved rows, centred
+  float* wn = xn + (int64_t)B * pitch;            // [B][dp]: s' - g (x' - c)
+  float* xo = wn + (int64_t)B * dp;               // [dp]: the row being moved (old, centred)
+  float* part = xo + dp;                          // [4][64] partial distances
+  float* kj = part + 256;                         // [64]
+  float* red = kj + 64;                           // [4] wave sums of kj
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const float inv_h = st->inv_h, g = 2.f * inv_h, scale = -inv_h * kLog2e;
+  const float inv_n = 1.f / (float)n;
+  const int q4 = dp >> 2;                         // features per quarter (dp % 32 == 0)
+  for (int e = t; e < B * pitch; e += 256) xn[e] = 0.f;
+  for (int e = t; e < dp; e += 256) xo[e] = Y[r0 * ldy + e];
+  __syncthreads();
+  for (int i = 0; i < B; ++i) {
+    // (a) distances of the old row i to the moved rows j < i: thread (j =
+    // lane, quarter w) over features [w q4, (w + 1) q4)
+    {
+      float sa = 0.f, sb = 0.f;
+      if (lane < i) {
+        const float* a = xo + w * q4;
+        const float* b = xn + lane * pitch + w * q4;
+        for (int c = 0; c < q4; c += 4) {
+          const f32x4 va = *reinterpret_cast<const f32x4*>(a + c);
+          const f32x4 vb = *reinterpret_cast<const f32x4*>(b + c);
+          const float d0 = va[0] - vb[0], d1 = va[1] - vb[1], d2 = va[2] - vb[2], d3 = va[3] - vb[3];
+          sa = fmaf(d0, d0, fmaf(d2, d2, sa));
+          sb = fmaf(d1, d1, fmaf(d3, d3, sb));
+        }
+      }
+      part[w * 64 + lane] = sa + sb;
+    }
+    __syncthreads();
+    if (w == 0) {
+      const float dd = (part[lane] + part[64 + lane]) + (part[128 + lane] + part[192 + lane]);
+      const float k = lane < i ? __builtin_amdgcn_exp2f(dd * scale) : 0.f;
+      kj[lane] = k;
+      float r = k;
+      for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
+      if (lane == 0) red[0] = r;
+    }
+    __syncthreads();
+    // (b) per column: the wide pass + the moved rows' terms + the self term
+    const float rm = red[0];
+    const int64_t gi = r0 + i;
+    const float rtot = Qr[i] + rm;
+    for (int c = t; c < d; c += 256) {
+      float acc0 = 0.f, acc1 = 0.f;
+      int j = 0;
+      for (; j + 2 <= i; j += 2) {
+        acc0 = fmaf(kj[j], wn[j * dp + c], acc0);
+        acc1 = fmaf(kj[j + 1], wn[(j + 1) * dp + c], acc1);
+      }
+      if (j < i) acc0 = fmaf(kj[j], wn[j * dp + c], acc0);
+      const float xc = xo[c];                       // x_i - c (old)
+      const float s_old = Y[gi * ldy + dp + c];     // s_i (the self term k_ii s_i)
+      float p = inv_n * (((Q[i * ldq + dp + c] + s_old) - g * Q[i * ldq + c]) + (acc0 + acc1) +
+                         g * rtot * xc);
+      if (extra) p += extra[(int64_t)i * lde + c];
+      if (phi_out) phi_out[(int64_t)i * ldphi + c] = p;
+      const float x = X[gi * ldx + c] + step * p;
+      X[gi * ldx + c] = x;
+      float s = s_old;
+      if (score_kind != 0) {
+        s = gs_score(score_kind, x, score_kind == 1 ? mu[c] : 0.f,
+                     score_kind == 1 ? lam[c] : 0.f, score_scale);
+        S[gi * lds + c] = s;
+      }
+      const float xcn = x - center[c];
+      xn[i * pitch + c] = xcn;
+      wn[i * dp + c] = s - g * xcn;
+      Y[gi * ldy + c] = xcn;
+      Y[gi * ldy + dp + c] = s;
+    }
+    __syncthreads();
+    // the next row's old values (after this row's reads of xo)
+    if (i + 1 < B)
+      for (int e = t; e < dp; e += 256) xo[e] = Y[(gi + 1) * ldy + e];
+    __syncthreads();
+  }
+  // the moved rows' norms |x' - c|^2 (the later blocks' distances)
+  for (int i = w; i < B; i += 4) {
+    float s2 = 0.f;
+    for (int c = lane; c < d; c += 64) {
+      const float v = xn[i * pitch + c];
+      s2 = fmaf(v, v, s2);
+    }
+    for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+    if (lane == 0) norms[r0 + i] = s2;
+  }
+}
+
 }  // namespace dsvgd
 
 using namespace dsvgd;
@@ -324,6 +459,45 @@ int dsvgd_gs_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, int64_t n
                      extra, lde, phi_out,
                      ldphi, score_kind, mu, lam, score_scale);
   return check_launch("gs_sweep");
+}
+
+int64_t dsvgd_gsw_block_rows(int64_t d) {
+  if (d <= kGsMaxD) return kGsB;
+  return gsw_rows(roundup(d, 32));
+}
+
+int dsvgd_gs_mask(float* D, int64_t ldd, int64_t r0, int64_t B, void* stream) {
+  DSVGD_REQUIRE(D, "null pointer");
+  DSVGD_REQUIRE(B > 0 && B <= 128 && r0 >= 0 && r0 + B <= ldd && ldd % 128 == 0, "sizes");
+  hipLaunchKernelGGL(gs_mask_kernel, dim3((unsigned)B), dim3(128), 0, (hipStream_t)stream, D, ldd,
+                     r0, (int)B);
+  return check_launch("gs_mask");
+}
+
+int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y, int64_t ldy,
+                          float* norms, const float* center, int64_t n, int64_t d, int64_t r0,
+                          int64_t B, const dsvgd_select_state* st, float step, const float* Q,
+                          int64_t ldq, const float* Qr, const float* extra, int64_t lde,
+                          float* phi_out, int64_t ldphi, int score_kind, const float* mu,
+                          const float* lam, float score_scale, void* stream) {
+  DSVGD_REQUIRE(X && S && Y && norms && center && st && Q && Qr, "null pointer");
+  const int64_t dp = roundup(d, 32);
+  DSVGD_REQUIRE(n > 0 && d > 0 && d <= kGswMaxD && ldx >= d && lds >= d && ldy >= 2 * dp &&
+                    ldq >= 2 * dp,
+                "sizes (d <= 1024, ldy and ldq >= 2 roundup(d, 32))");
+  DSVGD_REQUIRE(B > 0 && B <= gsw_rows(dp) && r0 >= 0 && r0 + B <= n, "block rows");
+  DSVGD_REQUIRE(score_kind >= 0 && score_kind <= 2, "score_kind must be 0, 1 or 2");
+  DSVGD_REQUIRE(score_kind != 1 || (mu && lam), "Gaussian scores need mu and lam");
+  DSVGD_REQUIRE(!extra || lde >= d, "lde");
+  DSVGD_REQUIRE(!phi_out || ldphi >= d, "ldphi");
+  const size_t smem = sizeof(float) * ((size_t)B * (dp + 4) + (size_t)B * dp + dp + 256 + 64 + 4);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gsw_sweep_kernel),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
+    return fail_arg("gsw_sweep: cannot reserve the walk's LDS");
+  hipLaunchKernelGGL(gsw_sweep_kernel, dim3(1), dim3(256), smem, (hipStream_t)stream, X, ldx, S,
+                     lds, Y, ldy, norms, center, n, (int)d, (int)dp, r0, (int)B, st, step, Q, ldq,
+                     Qr, extra, lde, phi_out, ldphi, score_kind, mu, lam, score_scale);
+  return check_launch("gsw_sweep");
 }
 
 }  // extern "C"

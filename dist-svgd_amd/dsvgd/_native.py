@@ -116,6 +116,12 @@ SIGNATURES = {
                                            _p]),
     "dsvgd_logreg_predict_workspace_bytes": (_c.c_size_t, [_i64, _i64, _i64]),
     "dsvgd_logreg_predict": (_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _p, _p]),
+    # the wide blocked Gauss-Seidel sweep (ABI 4)
+    "dsvgd_gsw_block_rows": (_i64, [_i64]),
+    "dsvgd_gs_mask": (_int, [_p, _i64, _i64, _i64, _p]),
+    "dsvgd_gsw_block_sweep": (_int, [_p, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64,
+                                     _p, _f, _p, _i64, _p, _p, _i64, _p, _i64, _int, _p, _p, _f,
+                                     _p]),
     # the pair-split layout (ABI 4)
     "dsvgd_sqdist_h2_parts": (_int, [_p, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p,
                                      _int, _p, _p, _p]),

@@ -790,10 +790,15 @@ def sequential_sweep(X, S, rows, h_state, step, target=None, score_scale=1.0, ph
     kind = _gs_score_kind(target)
     rows = range(rows.start, rows.stop) if isinstance(rows, range) else rows
     contiguous = isinstance(rows, range) and rows.step == 1
-    if (blocked and kind is not None and d <= 64 and contiguous and len(rows) >= GS_BLOCK_MIN_ROWS
+    if (blocked and kind is not None and contiguous and len(rows) >= GS_BLOCK_MIN_ROWS
             and X.is_contiguous() and S.is_contiguous()):
-        _blocked_sweep(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s)
-        return
+        if d <= 64:
+            _blocked_sweep(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s)
+            return
+        if d <= GSW_MAX_D:
+            _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, phi_out,
+                                extra, s)
+            return
     blocks = int(N.load().dsvgd_phi_row_blocks(n, d))
     part = None
     if blocks > 1:
@@ -814,6 +819,80 @@ def sequential_sweep(X, S, rows, h_state, step, target=None, score_scale=1.0, ph
                    h_state.ptr, float(step), ex, po, N.ptr(part), blocks, s)
         if target is not None:
             target.score(X[i:i + 1], S[i:i + 1], score_scale)
+
+
+GSW_MAX_D = 1024       # the wide blocked sweep (csrc/gs.hip gsw_sweep_kernel)
+
+
+class _WideSweep(object):
+    """Buffers of the wide blocked sweep for (device, n, d): Y = [X - c | S]
+    and norms (kept current as rows move), the block's D panel row, the
+    split-K partials of its wide pass and their sums."""
+
+    def __init__(self, dev, n, d):
+        lib = N.load()
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.n, self.d = n, d
+        self.n_pad = lib.dsvgd_pad128(n)
+        self.dp = lib.dsvgd_dp(d)
+        self.ldy = lib.dsvgd_ldy(self.dp)
+        self.B = int(lib.dsvgd_gsw_block_rows(d))
+        self.Y = torch.zeros(self.n_pad + 128, self.ldy, **f32)
+        self.norms = torch.zeros(self.n_pad + 128, **f32)
+        self.mean = torch.empty(d, **f32)
+        self.D = torch.empty(128 * self.n_pad, **f32)
+        # split-K slices of the B-row wide pass: the f32 NN engine runs
+        # ldy / 512 column blocks per slice, so ~256 slices fill the CUs
+        cb = max(1, self.ldy // 512)
+        z = max(1, 256 // cb)
+        while z > 1 and self.n_pad // z < 128:
+            z //= 2
+        self.splits = z
+        self.KY = torch.empty(z * self.B, self.ldy, **f32)
+        self.rowsum = torch.empty(z * 128, **f32)
+        self.Q = torch.empty(self.B, self.ldy, **f32)
+        self.Qr = torch.empty(128, **f32)
+
+
+_WIDE = {}
+
+
+def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s):
+    """The reference's Gauss-Seidel sweep for 64 < d <= 1024, B rows at a
+    time: the block's interactions with every row not moved before it in
+    the block on the f32 MFMA engines (dsvgd_sqdist, dsvgd_gs_mask,
+    dsvgd_phi_mm over split-K slices, dsvgd_phi_partial_reduce), then one
+    workgroup walks the B rows in order (dsvgd_gsw_block_sweep) -- the same
+    terms as the per-row path, in blocked order."""
+    n, d = X.shape
+    key = (X.device, n, d)
+    W = _WIDE.get(key)
+    if W is None:
+        _WIDE.clear()
+        W = _WIDE[key] = _WideSweep(X.device, n, d)
+    sk, mu, lam = kind, None, None
+    if sk == 1:
+        mu, lam = target._params(X.device)
+    N.call("dsvgd_colcenter", N.ptr(X), N.ld(X), n, d, N.ptr(W.mean), s)
+    N.call("dsvgd_pack", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), 1.0, N.ptr(W.mean), n, d,
+           W.Y.shape[0], N.ptr(W.Y), W.ldy, N.ptr(W.norms), s)
+    B = W.B
+    for b0 in range(rows.start, rows.stop, B):
+        nb = min(B, rows.stop - b0)
+        k0 = b0 - rows.start
+        N.call("dsvgd_sqdist", N.ptr(W.Y), W.ldy, N.ptr(W.norms), b0, nb, n, d, N.ptr(W.D),
+               W.n_pad, 0, None, None, s)
+        N.call("dsvgd_gs_mask", N.ptr(W.D), W.n_pad, b0, nb, s)
+        N.call("dsvgd_phi_mm", N.ptr(W.D), W.n_pad, N.ptr(W.Y), W.ldy, b0, nb, n, h_state.ptr,
+               W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), s)
+        N.call("dsvgd_phi_partial_reduce", N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), W.splits, nb,
+               2 * W.dp, N.ptr(W.Q), W.ldy, N.ptr(W.Qr), s)
+        ex = N.ptr(extra[k0:k0 + nb]) if extra is not None else None
+        po = N.ptr(phi_out[k0:k0 + nb]) if phi_out is not None else None
+        N.call("dsvgd_gsw_block_sweep", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), N.ptr(W.Y), W.ldy,
+               N.ptr(W.norms), N.ptr(W.mean), n, d, b0, nb, h_state.ptr, float(step), N.ptr(W.Q),
+               W.ldy, N.ptr(W.Qr), ex, d, po, N.ld(phi_out) if phi_out is not None else d, sk,
+               N.ptr(mu), N.ptr(lam), float(score_scale), s)
 
 
 def _blocked_sweep(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s):

@@ -334,6 +334,27 @@ int dsvgd_h2_rowscale(const float* A, int64_t lda, int64_t rows, int64_t cols, i
 int dsvgd_sqdist_h2(const void* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,
                     int64_t d, float* D, int64_t ldd, int select_mode, dsvgd_select_state* st,
                     float* cand, int layout, const float* rowscale, void* stream);
+/* ---- the reference's Gauss-Seidel order for 64 < d <= 1024 (ABI 4) -----
+ * dsvgd/sampler.py:64-68 / distsampler.py:194-200 move row i with phi_i of the
+ * CURRENT particles.  The wide blocked sweep takes B = dsvgd_gsw_block_rows(d)
+ * rows at a time: their interactions with every row not moved before them in
+ * the block on the f32 engines (dsvgd_sqdist of the centred Y = [X - c | S]
+ * rows [r0, r0 + B); dsvgd_gs_mask: D[i][r0 + j] = +inf for j < i, the pairs
+ * the walk takes; dsvgd_phi_mm into split-K slices; dsvgd_phi_partial_reduce
+ * -> Q = [K Xc | K S], Qr = K 1), then dsvgd_gsw_block_sweep walks the B rows
+ * in order in one workgroup: phi_i = (Q_i + s_i + sum_{j<i} k(x_i, x_j')
+ * (s_j' + (2/h)(x_i - x_j'))) / n (+ extra), X[i] += step phi_i, the score
+ * refreshed (score_kind as dsvgd_gs_block_sweep), Y's row and norms[] kept
+ * current (centre c = center, the packing centre of Y). */
+int64_t dsvgd_gsw_block_rows(int64_t d);
+int dsvgd_gs_mask(float* D, int64_t ldd, int64_t r0, int64_t B, void* stream);
+int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y, int64_t ldy,
+                          float* norms, const float* center, int64_t n, int64_t d, int64_t r0,
+                          int64_t B, const dsvgd_select_state* st, float step, const float* Q,
+                          int64_t ldq, const float* Qr, const float* extra, int64_t lde,
+                          float* phi_out, int64_t ldphi, int score_kind, const float* mu,
+                          const float* lam, float score_scale, void* stream);
+
 /* ---- the pair-split layout of a DistSampler rank (ABI 4) ---
  * With the scores identical on every rank (all_scores, or replicated data),
  * the S ranks split the symmetric n x n matrix by BLOCK PAIRS: rank r

@@ -171,6 +171,51 @@ def sampler_sequential(X0, score_fn, h, num_iter, step_size, dtype=np.float64):
     return np.stack(hist)
 
 
+def sequential_sweep(X, S, h, rows, step, score_fn=None, extra=None, block=64):
+    """One Gauss-Seidel sweep over `rows` (sampler.py:64-68: row i moves with
+    phi_i of the CURRENT particles, its score refreshed after the move when
+    score_fn is given), in place on fp64 copies; returns (X, S, phi rows).
+
+    The same arithmetic as looping O.phi(X, S, h, rows=[i]) row by row (a CPU
+    test pins the two), organised in blocks so full-size sweeps finish: a
+    block's interactions with every row outside the rows moved before it are
+    one matrix product, the in-block terms a short loop."""
+    X = np.array(X, np.float64)
+    S = np.array(S, np.float64)
+    rows = list(rows)
+    n = X.shape[0]
+    out = np.zeros((len(rows), X.shape[1]))
+    for b in range(0, len(rows), block):
+        idx = np.array(rows[b:b + block])
+        # the block's rows against all n as the block starts (large: the fp64
+        # centred Gram, pinned to the explicit differences by a CPU test)
+        if len(idx) * X.size >= (1 << 26):
+            D = sqdist_gram(X[idx], X)
+            D[np.arange(len(idx)), idx] = 0.0
+        else:
+            D = sqdist(X[idx], X, self_cols=idx)
+        K = np.exp(-D / h)
+        # terms with block rows moved before i are recomputed below
+        for a, i in enumerate(idx):
+            K[a, idx[:a]] = 0.0
+        xi = X[idx].copy()
+        Q = K @ S + (2.0 / h) * (K.sum(1)[:, None] * xi - K @ X)
+        for a, i in enumerate(idx):
+            moved = idx[:a]
+            p = Q[a].copy()
+            if len(moved):
+                km = np.exp(-((xi[a][None, :] - X[moved]) ** 2).sum(1) / h)
+                p += km @ S[moved] + (2.0 / h) * (km.sum() * xi[a] - km @ X[moved])
+            p /= n
+            if extra is not None:
+                p = p + extra[b + a]
+            out[b + a] = p
+            X[i] = xi[a] + step * p
+            if score_fn is not None:
+                S[i] = score_fn(X[i:i + 1])[0]
+    return X, S, out
+
+
 def sampler_jacobi(X0, score_fn, h, num_iter, step_size, median=False):
     X = np.array(X0, np.float64)
     hist = [X.copy()]

@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--shards", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--lib", default=None, help="an A/B build of the library (make ab)")
+    ap.add_argument("--layout", default="both", choices=["rows", "pairs", "both"],
+                    help="rows: the row-block layout; pairs: the pair-split layout (DESIGN.md 6; "
+                         "the partials' exchange left out, their buffers zero)")
     args = ap.parse_args()
     import dsvgd
     if args.lib:
@@ -32,11 +35,20 @@ def main():
     x, t = synthetic_data(Ng, d - 1)
     g = torch.Generator(device="cpu").manual_seed(0)
     X = (0.1 * torch.randn(n, d, generator=g)).cuda()
+    runs = []
     for S in [int(v) for v in args.shards.split(",")]:
-        m, r = n // S, S // 2          # a middle rank
+        for lay in (("rows", "pairs") if args.layout == "both" else (args.layout,)):
+            if lay == "rows" or (S > 1 and dsvgd.PhiEngine.pair_split_ok(n, d, S)):
+                runs.append((S, lay))
+    for S, lay in runs:
+        m, r = n // S, S // 2          # a middle rank (a high one of the pair split)
         per = Ng // S
         tgt = dsvgd.targets.LogisticRegression(x[r * per:(r + 1) * per], t[r * per:(r + 1) * per])
-        eng = dsvgd.PhiEngine(n, d, m=m, row0=r * m, device="cuda:0")
+        eng = dsvgd.PhiEngine(n, d, m=m, row0=r * m, device="cuda:0",
+                              pair_split=(r, S) if lay == "pairs" else None)
+        if eng.plan is not None:
+            for b in eng.recvbuf:
+                b.zero_()
         Sx = torch.empty_like(X)
         Xo = X[r * m:(r + 1) * m].clone()
         timer = StageTimer()
@@ -64,7 +76,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         st = {k: round(float(np.mean(v)), 3) for k, v in timer.summary().items()}
-        print(json.dumps({"shards": S, "m": m, "row0": r * m, "N_local": per,
+        print(json.dumps({"shards": S, "layout": lay, "m": m, "row0": r * m, "N_local": per,
                           "ms_per_step_no_comm": e0.elapsed_time(e1) / args.steps,
                           "sym_layout": bool(eng.sym), "stages_ms": st}), flush=True)
         del eng

@@ -423,7 +423,12 @@ def test_phi_row_split_matches_oracle(n, d, ldx):
 
 
 @pytest.mark.parametrize("n,d,lo,hi,kind", [(300, 3, 0, 300, "gauss"), (2000, 64, 37, 300, "none"),
-                                             (1000, 1, 100, 331, "gmm"), (700, 33, 0, 700, "gauss")])
+                                             (1000, 1, 100, 331, "gmm"), (700, 33, 0, 700, "gauss"),
+                                             # the wide sweep (64 < d <= 1024, f32 MFMA wide pass)
+                                             (1500, 128, 10, 700, "gauss"),
+                                             (1200, 256, 0, 1200, "none"),
+                                             (800, 700, 50, 400, "gauss"),
+                                             (600, 1024, 0, 300, "gmm")])
 def test_blocked_sweep_matches_oracle(n, d, lo, hi, kind):
     """The blocked Gauss-Seidel sweep (csrc/gs.hip: 64-row blocks, a wide pass
     against all n rows + one workgroup for the in-block order) against the

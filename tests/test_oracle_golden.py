@@ -210,3 +210,29 @@ def test_laggedlocal_block_travel():
     u.step(0.05)
     for r in range(S):
         assert np.all(np.abs(u.X[r] - init[r]).max(1) > 0)
+
+
+@pytest.mark.parametrize("n,d,lo,hi,fn", [(200, 5, 0, 200, "gauss"), (150, 3, 17, 140, None),
+                                          (90, 7, 5, 90, "gmm")])
+def test_blocked_sequential_restatement_equals_row_loop(n, d, lo, hi, fn):
+    """O.sequential_sweep (blocked, for full-size checks) against the plain
+    row-by-row restatement of sampler.py:64-68 (O.phi per row, score refreshed
+    after each move): the same sweep to fp64 rounding."""
+    rs = np.random.RandomState(n)
+    X0 = 0.8 * rs.randn(n, d)
+    mu, lam = rs.randn(d), rs.uniform(0.5, 2.0, d)
+    score = {"gauss": lambda X: O.score_gaussian(X, mu, lam), "gmm": O.score_gmm, None: None}[fn]
+    S0 = score(X0) if score else rs.randn(n, d)
+    h, step = 0.8 * d + 0.3, 0.07
+    extra = 0.01 * rs.randn(hi - lo, d)
+    X, S = X0.copy(), S0.copy()
+    ref_phi = np.zeros((hi - lo, d))
+    for k, i in enumerate(range(lo, hi)):
+        ref_phi[k] = O.phi(X, S, h, rows=[i])[0] + extra[k]
+        X[i] += step * ref_phi[k]
+        if score:
+            S[i] = score(X[i:i + 1])[0]
+    Xb, Sb, pb = O.sequential_sweep(X0, S0, h, range(lo, hi), step, score_fn=score, extra=extra,
+                                    block=16)
+    assert np.abs(Xb - X).max() < 1e-12 and np.abs(pb - ref_phi).max() < 1e-12
+    assert np.abs(Sb - S).max() < 1e-10
