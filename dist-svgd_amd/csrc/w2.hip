@@ -268,25 +268,21 @@ struct TopK {
   }
 };
 
-// Row i's bid: its u free slots (bit r of `free` = slot iR + r) bid on the
-// u best columns the row does not hold, each at v_k - v_{u+1} + eps.
+// ---- block-cooperative scans (one workgroup per bidding row) -------------
+// A full scan of a cost row reads n costs, n fp64 prices (and n holders):
+// ~1 MB at n = 65536.  One wave walking it with a load -> top-K dependency per
+// column was latency-bound (~150 us: the ~180 us rounds of the cold solve,
+// profiles/r8j); here the workgroup's 256 threads take columns t, t + 256,
+// ... with four columns' loads in flight each, then the four waves' top-K
+// lists are merged.  Same values and the same tie rule (lower column first).
+constexpr int kScanUnroll = 4;
+
+// Wave w's K best of its lanes' lists (lane k < K: the k-th) into sv / sj
+// [w K + k]; every lane's list is sorted descending, columns unique.
 template <int K>
-__device__ __forceinline__ void bid_row(const float* __restrict__ row, int64_t n, int64_t i,
-                                        int64_t R, unsigned long long free, int lane, double eps,
-                                        uint32_t tag, const W2Ws& w) {
-  const int u = __popcll(free);
-  TopK<K> t;
-  t.init();
-  const uint32_t mine = tag | (uint32_t)i;
-  for (int64_t j = lane; j < n; j += 64) {
-    if (w.holder[j] == mine) continue;
-    t.push(-(double)row[j] - w.price[j], (int)j);
-  }
-  // wave merge: extract the u + 1 best in order (ties -> lower column); the
-  // k-th lands in lane k's (kv, kj)
-  double kv = -DBL_MAX;
-  int kj = INT32_MAX;
-  for (int k = 0; k <= u; ++k) {
+__device__ __forceinline__ void wave_topk_to_lds(TopK<K>& t, int lane, int wv, double* sv,
+                                                 int* sj) {
+  for (int k = 0; k < K; ++k) {
     double bv = t.v[0];
     int bj = t.j[0];
 #pragma unroll
@@ -298,17 +294,77 @@ __device__ __forceinline__ void bid_row(const float* __restrict__ row, int64_t n
         bj = oj;
       }
     }
-    if (lane == k) {
-      kv = bv;
-      kj = bj;
+    if (lane == 0) {
+      sv[wv * K + k] = bv;
+      sj[wv * K + k] = bj;
     }
     if (t.j[0] == bj) t.pop();
   }
-  // v_{u+1}; if the row has no (u+1)-th alternative, price against the u-th
+}
+
+// The workgroup's K best (value, column) of -C_ij - p_j over the columns j
+// the row does not hold (skip_held) or over all columns, sorted descending,
+// into out_v / out_j [K] (LDS, visible to the whole block on return).
+template <int K>
+__device__ void block_topk(const float* __restrict__ row, int64_t n, const W2Ws& w,
+                           uint32_t mine, bool skip_held, double* sv, int* sj, double* out_v,
+                           int* out_j) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  TopK<K> tk;
+  tk.init();
+  int64_t j = t;
+  for (; j + (kScanUnroll - 1) * 256 < n; j += kScanUnroll * 256) {
+    float c[kScanUnroll];
+    double p[kScanUnroll];
+    uint32_t h[kScanUnroll];
+#pragma unroll
+    for (int u = 0; u < kScanUnroll; ++u) {
+      c[u] = row[j + u * 256];
+      p[u] = w.price[j + u * 256];
+      h[u] = skip_held ? w.holder[j + u * 256] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kScanUnroll; ++u)
+      if (!skip_held || h[u] != mine) tk.push(-(double)c[u] - p[u], (int)(j + u * 256));
+  }
+  for (; j < n; j += 256)
+    if (!skip_held || w.holder[j] != mine) tk.push(-(double)row[j] - w.price[j], (int)j);
+  wave_topk_to_lds<K>(tk, lane, wv, sv, sj);
+  __syncthreads();
+  if (t == 0) {  // merge the four sorted lists
+    int pos[4] = {0, 0, 0, 0};
+    for (int k = 0; k < K; ++k) {
+      int bq = -1;
+      double bv = -DBL_MAX;
+      int bj = INT32_MAX;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (pos[q] >= K) continue;
+        const double v = sv[q * K + pos[q]];
+        const int jj = sj[q * K + pos[q]];
+        if (bq < 0 || v > bv || (v == bv && jj < bj)) {
+          bq = q;
+          bv = v;
+          bj = jj;
+        }
+      }
+      out_v[k] = bv;
+      out_j[k] = bj;
+      ++pos[bq];
+    }
+  }
+  __syncthreads();
+}
+
+// The bid of row i's u free slots from the u + 1 best non-held columns
+// (kv, kj in lane k < u + 1; lanes >= u + 1 hold -DBL_MAX / INT32_MAX) --
+// the tail of a row's bid
+__device__ __forceinline__ void bid_from_best(double kv, int kj, int u, int64_t i, int64_t R,
+                                              unsigned long long free, int lane, double eps,
+                                              const W2Ws& w) {
   const double vu1 = __shfl(kv, u, 64), vu = __shfl(kv, u - 1, 64);
   const double vref = (vu1 > -DBL_MAX) ? vu1 : vu;
   if (lane >= u || kj == INT32_MAX) return;
-  // lane k bids for the k-th free slot of the row
   unsigned long long rest = free;
   for (int k = 0; k < lane; ++k) rest &= rest - 1;
   const int64_t s = i * R + (__ffsll((long long)rest) - 1);
@@ -346,125 +402,133 @@ __device__ __forceinline__ void wave_best(double cv, int cj, int u, int lane, do
   }
 }
 
-// bid_row with the price cache (R in [2, kCacheMaxR]); same bids as bid_row
-__device__ __forceinline__ void bid_row_cached(const float* __restrict__ row, int64_t n, int64_t i,
-                                               int64_t R, unsigned long long free, int lane,
-                                               double eps, uint32_t tag, const W2Ws& w) {
-  const int u = __popcll(free);
-  const uint32_t mine = tag | (uint32_t)i;
-  double kv;
-  int kj;
-  bool ok = false;
-  if (w.cvalid[i]) {  // wave-uniform
-    double cv = -DBL_MAX;
-    int cj = INT32_MAX;
-    if (lane < kCache) {
-      const int c = w.ccol[i * kCache + lane];
-      if (c != INT32_MAX && w.holder[c] != mine) {  // held columns never bid
-        cj = c;
-        cv = -(double)w.ccost[i * kCache + lane] - w.price[c];
-      }
-    }
-    wave_best(cv, cj, u, lane, kv, kj);
-    const double vu1 = __shfl(kv, u, 64);
-    ok = vu1 >= w.cbound[i];
-  }
-  if (!ok) {  // full scan over all columns, refill the cache
-    TopK<kCache + 1> t;
-    t.init();
-    for (int64_t j = lane; j < n; j += 64) t.push(-(double)row[j] - w.price[j], (int)j);
-    double ev = -DBL_MAX;
-    int ej = INT32_MAX;
-    for (int k = 0; k <= kCache; ++k) {
-      double bv = t.v[0];
-      int bj = t.j[0];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const double ov = __shfl_xor(bv, o, 64);
-        const int oj = __shfl_xor(bj, o, 64);
-        if (ov > bv || (ov == bv && oj < bj)) {
-          bv = ov;
-          bj = oj;
-        }
-      }
-      if (lane == k) {
-        ev = bv;
-        ej = bj;
-      }
-      if (t.j[0] == bj) t.pop();
-    }
-    if (lane < kCache) {
-      w.ccol[i * kCache + lane] = ej;
-      w.ccost[i * kCache + lane] = ej != INT32_MAX ? row[ej] : 0.f;
-    }
-    if (lane == kCache) w.cbound[i] = ev;
-    if (lane == 0) w.cvalid[i] = 1;
-    // bid from the fresh list (current values), held columns excluded
-    double cv = -DBL_MAX;
-    int cj = INT32_MAX;
-    if (lane < kCache && ej != INT32_MAX && w.holder[ej] != mine) {
-      cj = ej;
-      cv = ev;
-    }
-    wave_best(cv, cj, u, lane, kv, kj);
-  }
-  const double vu1 = __shfl(kv, u, 64), vu = __shfl(kv, u - 1, 64);
-  const double vref = (vu1 > -DBL_MAX) ? vu1 : vu;
-  if (lane >= u || kj == INT32_MAX) return;
-  unsigned long long rest = free;
-  for (int k = 0; k < lane; ++k) rest &= rest - 1;
-  const int64_t s = i * R + (__ffsll((long long)rest) - 1);
-  const double inc = kv - vref + eps;
-  float f = (float)inc;
-  if ((double)f > inc) f = nextafterf(f, 0.f);  // round down: keeps eps-CS
-  if (!(f > 0.f)) f = FLT_MIN;
-  const unsigned long long key =
-      ((unsigned long long)__float_as_uint(f) << 32) | (unsigned long long)(uint32_t)s;
-  atomicMax(&w.bid[kj], key);
-}
-
+// Rows in groups of four per workgroup-iteration (wave q: row base + q):
+// each wave finds its row's free slots and, with the price cache, tries the
+// cached bid; the rows left (no cache hit) are scanned one after the other by
+// the whole workgroup (block_topk), which refills the cache and bids.
 __global__ __launch_bounds__(256) void w2_bid_cached_kernel(const float* __restrict__ C,
                                                             int64_t ldc, int64_t m, int64_t n,
                                                             int64_t R, W2Ws w) {
+  constexpr int K = kCache + 1;
+  __shared__ double sv[4 * K], outv[K];
+  __shared__ int sj[4 * K], outj[K];
+  __shared__ unsigned long long need[4];
   const W2Ctl* ctl = w.ctl;
   if (ctl->done) return;
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int ep = ctl->epoch;
   const double eps = ctl->eps;
   const uint32_t tag = w2_tag(ep);
-  for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < m;
-       i += (int64_t)gridDim.x * 4) {
-    bool fr = false;
-    if (lane < R) {
-      const int64_t s = i * R + lane;
-      fr = !(w.assigned_ep[s] == ep && w.assigned[s] >= 0);
+  for (int64_t base = (int64_t)blockIdx.x * 4; base < m; base += (int64_t)gridDim.x * 4) {
+    const int64_t i = base + wv;
+    unsigned long long free = 0;
+    if (i < m) {
+      bool fr = false;
+      if (lane < R) {
+        const int64_t s = i * R + lane;
+        fr = !(w.assigned_ep[s] == ep && w.assigned[s] >= 0);
+      }
+      free = __ballot(fr);
     }
-    const unsigned long long free = __ballot(fr);
-    if (free == 0) continue;
-    bid_row_cached(C + i * ldc, n, i, R, free, lane, eps, tag, w);
+    bool scan = false;
+    if (free && w.cvalid[i]) {  // wave-uniform: the cached bid
+      const int u = __popcll(free);
+      const uint32_t mine = tag | (uint32_t)i;
+      double cv = -DBL_MAX;
+      int cj = INT32_MAX;
+      if (lane < kCache) {
+        const int c = w.ccol[i * kCache + lane];
+        if (c != INT32_MAX && w.holder[c] != mine) {  // held columns never bid
+          cj = c;
+          cv = -(double)w.ccost[i * kCache + lane] - w.price[c];
+        }
+      }
+      double kv;
+      int kj;
+      wave_best(cv, cj, u, lane, kv, kj);
+      if (__shfl(kv, u, 64) >= w.cbound[i])
+        bid_from_best(kv, kj, u, i, R, free, lane, eps, w);
+      else
+        scan = true;
+    } else if (free) {
+      scan = true;
+    }
+    if (lane == 0) need[wv] = scan ? free : 0ull;
+    __syncthreads();
+    for (int q = 0; q < 4; ++q) {
+      const unsigned long long fq = need[q];  // block-uniform
+      if (fq == 0ull) continue;
+      const int64_t iq = base + q;
+      const uint32_t mine = tag | (uint32_t)iq;
+      const float* row = C + iq * ldc;
+      block_topk<K>(row, n, w, mine, false, sv, sj, outv, outj);
+      if (wv == 0) {
+        const double ev = lane < K ? outv[lane] : -DBL_MAX;
+        const int ej = lane < K ? outj[lane] : INT32_MAX;
+        if (lane < kCache) {
+          w.ccol[iq * kCache + lane] = ej;
+          w.ccost[iq * kCache + lane] = ej != INT32_MAX ? row[ej] : 0.f;
+        }
+        if (lane == kCache) w.cbound[iq] = ev;
+        if (lane == 0) w.cvalid[iq] = 1;
+        // bid from the fresh list (current values), held columns excluded
+        double cv = -DBL_MAX;
+        int cj = INT32_MAX;
+        if (lane < kCache && ej != INT32_MAX && w.holder[ej] != mine) {
+          cj = ej;
+          cv = ev;
+        }
+        const int u = __popcll(fq);
+        double kv;
+        int kj;
+        wave_best(cv, cj, u, lane, kv, kj);
+        bid_from_best(kv, kj, u, iq, R, fq, lane, eps, w);
+      }
+      __syncthreads();  // sv / outv reused by the next row
+    }
   }
 }
 
-// Waves stride over the rows; rows with free slots in this epoch bid.
+// Without the cache (R = 1, R > kCacheMaxR): every bidding row is a full
+// scan over the columns it does not hold, by the whole workgroup.
 template <int K>
 __global__ __launch_bounds__(256) void w2_bid_kernel(const float* __restrict__ C, int64_t ldc,
                                                      int64_t m, int64_t n, int64_t R, W2Ws w) {
+  __shared__ double sv[4 * K], outv[K];
+  __shared__ int sj[4 * K], outj[K];
+  __shared__ unsigned long long need[4];
   const W2Ctl* ctl = w.ctl;
   if (ctl->done) return;
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int ep = ctl->epoch;
   const double eps = ctl->eps;
   const uint32_t tag = w2_tag(ep);
-  for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < m;
-       i += (int64_t)gridDim.x * 4) {
-    bool fr = false;
-    if (lane < R) {
-      const int64_t s = i * R + lane;
-      fr = !(w.assigned_ep[s] == ep && w.assigned[s] >= 0);
+  for (int64_t base = (int64_t)blockIdx.x * 4; base < m; base += (int64_t)gridDim.x * 4) {
+    const int64_t i = base + wv;
+    unsigned long long free = 0;
+    if (i < m) {
+      bool fr = false;
+      if (lane < R) {
+        const int64_t s = i * R + lane;
+        fr = !(w.assigned_ep[s] == ep && w.assigned[s] >= 0);
+      }
+      free = __ballot(fr);
     }
-    const unsigned long long free = __ballot(fr);
-    if (free == 0) continue;
-    bid_row<K>(C + i * ldc, n, i, R, free, lane, eps, tag, w);
+    if (lane == 0) need[wv] = free;
+    __syncthreads();
+    for (int q = 0; q < 4; ++q) {
+      const unsigned long long fq = need[q];  // block-uniform
+      if (fq == 0ull) continue;
+      const int64_t iq = base + q;
+      block_topk<K>(C + iq * ldc, n, w, tag | (uint32_t)iq, true, sv, sj, outv, outj);
+      if (wv == 0) {
+        const int u = __popcll(fq);
+        const double kv = lane <= u && lane < K ? outv[lane] : -DBL_MAX;
+        const int kj = lane <= u && lane < K ? outj[lane] : INT32_MAX;
+        bid_from_best(kv, kj, u, iq, R, fq, lane, eps, w);
+      }
+      __syncthreads();
+    }
   }
 }
 

@@ -1,0 +1,75 @@
+"""The reference's default Gauss-Seidel order (sampler.py:64-68,
+distsampler.py:194-200) at the BASELINE shapes: one DistSampler step of
+config D (n = 65536, d = 256, logreg, all_scores: the scores frozen for the
+sweep) and of config E's shape (d = 1024) through the wide blocked sweep,
+next to the per-row path (one phi_row_split launch per particle) timed on a
+bounded sample of rows and extrapolated to the whole sweep.
+
+    python scripts/seq_timing.py [--only D,E] [--rows-sample 2048]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dist-svgd_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="D,E")
+    ap.add_argument("--rows-sample", type=int, default=2048)
+    args = ap.parse_args()
+    import dsvgd
+    from dsvgd.engine import sequential_sweep
+    from bench import synthetic_data
+    shapes = {"D": (65536, 256, 16384), "E": (65536, 1024, 8192)}
+    for name in args.only.split(","):
+        n, d, Ng = shapes[name]
+        x, t = synthetic_data(Ng, d - 1)
+        g = torch.Generator(device="cpu").manual_seed(0)
+        X = (0.1 * torch.randn(n, d, generator=g)).cuda()
+        ds = dsvgd.DistSampler(0, 1, dsvgd.targets.LogisticRegression(x, t), dsvgd.RBF("median"),
+                               X, Ng, Ng, exchange_particles=True, exchange_scores=True,
+                               include_wasserstein=False, order="sequential")
+        ds.graphs = False
+        ds.make_step(1e-4)                      # warm-up (workspaces, median engine)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ds.make_step(1e-4)
+        torch.cuda.synchronize()
+        blocked_ms = 1e3 * (time.perf_counter() - t0)
+        # the per-row kernels over a sample of rows, same scores and bandwidth
+        eng = next(iter(ds._engines.values()))
+        k = min(args.rows_sample, n)
+        Xc, Sc = X.clone(), ds._scores.clone()
+        sequential_sweep(Xc, Sc, range(0, 64), eng.state, 1e-4, blocked=False)   # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sequential_sweep(Xc, Sc, range(64, 64 + k), eng.state, 1e-4, blocked=False)
+        torch.cuda.synchronize()
+        per_row_ms = 1e3 * (time.perf_counter() - t0) * n / k
+        # the blocked sweep alone (no median / scores), for the stage split
+        Xb, Sb = X.clone(), ds._scores.clone()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sequential_sweep(Xb, Sb, range(n), eng.state, 1e-4)
+        torch.cuda.synchronize()
+        sweep_ms = 1e3 * (time.perf_counter() - t0)
+        print(json.dumps({"config": name, "n": n, "d": d, "order": "sequential",
+                          "step_ms_blocked": blocked_ms, "sweep_only_ms_blocked": sweep_ms,
+                          "particle_updates_per_s": n / blocked_ms * 1e3,
+                          "per_row_ms_extrapolated": per_row_ms, "per_row_sample_rows": k,
+                          "speedup_vs_per_row": per_row_ms / sweep_ms}), flush=True)
+        del ds, eng
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
