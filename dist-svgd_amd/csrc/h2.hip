@@ -280,10 +280,14 @@ __global__ __launch_bounds__(256) void rowsplit_h2_kernel(const float* __restric
                                                           int64_t lda, int64_t rows, int64_t cols,
                                                           int64_t rows_pad, int64_t ksteps,
                                                           const float* __restrict__ tscale,
-                                                          _Float16* __restrict__ img) {
+                                                          _Float16* __restrict__ img,
+                                                          int64_t row_begin = 0,
+                                                          int64_t nrows = -1) {
+  // rows [row_begin, row_begin + nrows) of the image (default: all rows_pad)
+  const int64_t nr = nrows < 0 ? rows_pad : nrows;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= ksteps * rows_pad) return;
-  const int64_t kb = t / rows_pad, i = t % rows_pad;
+  if (t >= ksteps * nr) return;
+  const int64_t kb = t / nr, i = row_begin + t % nr;
   const float sc = RS ? (i < rows ? tscale[i] : 1.f) : *tscale;
   float a[16];
   if (OFF >= 0 && i < rows && kb * 16 + 16 <= cols) {
@@ -388,6 +392,18 @@ int h2_rowsplit_rows(const float* A, int64_t lda, int64_t rows, int64_t cols, in
   return h2_rowsplit_t<true>(A, lda, rows, cols, rows_pad, kpad, rscale, img, s);
 }
 
+// rows [row_begin, row_begin + nrows) of the per-row-scaled image only (the
+// wide Gauss-Seidel sweep re-splits the rows a block moved); element loads
+int h2_rowsplit_rows_range(const float* A, int64_t lda, int64_t rows, int64_t cols,
+                           int64_t rows_pad, int64_t kpad, const float* rscale, void* img,
+                           int64_t row_begin, int64_t nrows, hipStream_t s) {
+  const int64_t ksteps = kpad / kX3Step, threads = ksteps * nrows;
+  hipLaunchKernelGGL((rowsplit_h2_kernel<-1, true>), dim3((unsigned)((threads + 255) / 256)),
+                     dim3(256), 0, s, A, lda, rows, cols, rows_pad, ksteps, rscale,
+                     (_Float16*)img, row_begin, nrows);
+  return check_launch("rowsplit_h2(range)");
+}
+
 int h2_rowscale(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
                 float* rscale, float* rinv, hipStream_t s) {
   hipLaunchKernelGGL(rowscale_h2_kernel, dim3((unsigned)((rows_pad + 3) / 4)), dim3(256), 0, s, A,
@@ -461,6 +477,19 @@ int dsvgd_h2_rowsplit_rows(const float* A, int64_t lda, int64_t rows, int64_t co
                 "rows_pad and kpad must be positive multiples of 16");
   DSVGD_REQUIRE(((uintptr_t)img & 15) == 0, "16-byte alignment");
   return h2_rowsplit_rows(A, lda, rows, cols, rows_pad, kpad, rscale, img, (hipStream_t)stream);
+}
+
+int dsvgd_h2_rowsplit_rows_range(const float* A, int64_t lda, int64_t rows, int64_t cols,
+                                 int64_t rows_pad, int64_t kpad, const float* rscale, void* img,
+                                 int64_t row_begin, int64_t nrows, void* stream) {
+  DSVGD_REQUIRE(A && rscale && img, "null pointer");
+  DSVGD_REQUIRE(rows >= 0 && cols >= 0 && rows <= rows_pad && lda >= cols, "sizes");
+  DSVGD_REQUIRE(rows_pad > 0 && rows_pad % 16 == 0 && kpad > 0 && kpad % kX3Step == 0,
+                "rows_pad and kpad must be positive multiples of 16");
+  DSVGD_REQUIRE(row_begin >= 0 && nrows > 0 && row_begin + nrows <= rows_pad, "row range");
+  DSVGD_REQUIRE(((uintptr_t)img & 15) == 0, "16-byte alignment");
+  return h2_rowsplit_rows_range(A, lda, rows, cols, rows_pad, kpad, rscale, img, row_begin, nrows,
+                                (hipStream_t)stream);
 }
 
 int dsvgd_h2_rowscale(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,

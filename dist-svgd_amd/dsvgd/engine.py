@@ -822,14 +822,17 @@ def sequential_sweep(X, S, rows, h_state, step, target=None, score_scale=1.0, ph
 
 
 GSW_MAX_D = 1024       # the wide blocked sweep (csrc/gs.hip gsw_sweep_kernel)
+GSW_GEMM = "split"     # its wide pass: "split" (FmtH2 Gram + FmtX3 phi_mm) or "f32"
 
 
 class _WideSweep(object):
     """Buffers of the wide blocked sweep for (device, n, d): Y = [X - c | S]
-    and norms (kept current as rows move), the block's D panel row, the
-    split-K partials of its wide pass and their sums."""
+    and norms (kept current as rows move), the split engines' images of Y
+    (the Gram's per-row-scaled FmtH2 row image, phi_mm's FmtX3 image; the
+    rows a block moves are re-split after its walk), the block's D panel
+    row, the split-K partials of its wide pass and their sums."""
 
-    def __init__(self, dev, n, d):
+    def __init__(self, dev, n, d, gemm):
         lib = N.load()
         f32 = dict(dtype=torch.float32, device=dev)
         self.n, self.d = n, d
@@ -841,8 +844,24 @@ class _WideSweep(object):
         self.norms = torch.zeros(self.n_pad + 128, **f32)
         self.mean = torch.empty(d, **f32)
         self.D = torch.empty(128 * self.n_pad, **f32)
-        # split-K slices of the B-row wide pass: the f32 NN engine runs
-        # ldy / 512 column blocks per slice, so ~256 slices fill the CUs
+        split = gemm == "split"
+        # phi_mm on FmtX3 (no scales: moved rows cannot leave a scale's window)
+        self.phi_x3 = split and self.n_pad * self.ldy * 6 < (1 << 31)
+        if self.phi_x3:
+            self.m16 = self.ldy % 256 == 0
+            self.Yx3 = torch.empty(lib.dsvgd_ysplit_bytes(self.n_pad, self.ldy) // 2,
+                                   dtype=torch.int16, device=dev)
+        # the Gram on FmtH2 row images with per-row scales (the one-wave Gram
+        # needs roundup(d, 32) % 256 == 0; otherwise the exact f32 engine)
+        self.gram_rows = self.n_pad + 256
+        self.gram_h2 = (split and self.dp % 256 == 0
+                        and self.dp * self.gram_rows * 4 < (1 << 31))
+        if self.gram_h2:
+            self.rsc = torch.ones(self.n_pad + 128, **f32)
+            self.Yg = torch.empty(lib.dsvgd_h2_image_bytes(self.gram_rows, self.dp) // 2,
+                                  dtype=torch.int16, device=dev)
+        # split-K slices of the B-row wide pass: ldy / 512 column blocks per
+        # slice, so ~256 slices fill the CUs
         cb = max(1, self.ldy // 512)
         z = max(1, 256 // cb)
         while z > 1 and self.n_pad // z < 128:
@@ -853,38 +872,68 @@ class _WideSweep(object):
         self.Q = torch.empty(self.B, self.ldy, **f32)
         self.Qr = torch.empty(128, **f32)
 
+    def images(self, r0, nr, s):
+        """(Re)split rows [r0, r0 + nr) of Y into the engines' images (the
+        whole image, padding rows zeroed, when nr = n_pad)."""
+        if self.gram_h2:
+            rb = 4 * r0
+            N.call("dsvgd_h2_rowscale", N.ptr(self.Y) + rb * self.ldy, self.ldy, nr, self.dp, nr,
+                   N.ptr(self.rsc) + rb, None, s)
+            if nr == self.n_pad:
+                N.call("dsvgd_h2_rowsplit_rows", N.ptr(self.Y), self.ldy, self.n_pad, self.dp,
+                       self.gram_rows, self.dp, N.ptr(self.rsc), N.ptr(self.Yg), s)
+            else:
+                N.call("dsvgd_h2_rowsplit_rows_range", N.ptr(self.Y), self.ldy, self.n_pad,
+                       self.dp, self.gram_rows, self.dp, N.ptr(self.rsc), N.ptr(self.Yg), r0, nr,
+                       s)
+        if self.phi_x3:
+            k0, k1 = r0 // 16, -(-(r0 + nr) // 16)    # whole 16-row K-steps
+            N.call("dsvgd_ysplit", N.ptr(self.Y) + 4 * 16 * k0 * self.ldy, self.ldy,
+                   16 * (k1 - k0), N.ptr(self.Yx3) + 2 * 3 * 16 * k0 * self.ldy,
+                   0 if self.m16 else 1, None, s)
+
 
 _WIDE = {}
 
 
 def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s):
     """The reference's Gauss-Seidel sweep for 64 < d <= 1024, B rows at a
-    time: the block's interactions with every row not moved before it in
-    the block on the f32 MFMA engines (dsvgd_sqdist, dsvgd_gs_mask,
-    dsvgd_phi_mm over split-K slices, dsvgd_phi_partial_reduce), then one
-    workgroup walks the B rows in order (dsvgd_gsw_block_sweep) -- the same
-    terms as the per-row path, in blocked order."""
+    time: the block's interactions with every row not moved before it in the
+    block on the MFMA engines (the Gram, dsvgd_gs_mask, phi_mm over split-K
+    slices, dsvgd_phi_partial_reduce), then one workgroup walks the B rows in
+    order (dsvgd_gsw_block_sweep) and the moved rows are re-split into the
+    engines' images -- the same terms as the per-row path, in blocked order."""
     n, d = X.shape
-    key = (X.device, n, d)
+    key = (X.device, n, d, GSW_GEMM)
     W = _WIDE.get(key)
     if W is None:
         _WIDE.clear()
-        W = _WIDE[key] = _WideSweep(X.device, n, d)
+        W = _WIDE[key] = _WideSweep(X.device, n, d, GSW_GEMM)
     sk, mu, lam = kind, None, None
     if sk == 1:
         mu, lam = target._params(X.device)
     N.call("dsvgd_colcenter", N.ptr(X), N.ld(X), n, d, N.ptr(W.mean), s)
     N.call("dsvgd_pack", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), 1.0, N.ptr(W.mean), n, d,
            W.Y.shape[0], N.ptr(W.Y), W.ldy, N.ptr(W.norms), s)
+    W.images(0, W.n_pad, s)
     B = W.B
     for b0 in range(rows.start, rows.stop, B):
         nb = min(B, rows.stop - b0)
         k0 = b0 - rows.start
-        N.call("dsvgd_sqdist", N.ptr(W.Y), W.ldy, N.ptr(W.norms), b0, nb, n, d, N.ptr(W.D),
-               W.n_pad, 0, None, None, s)
+        if W.gram_h2:
+            N.call("dsvgd_sqdist_h2", N.ptr(W.Yg), N.ptr(W.norms), b0, nb, n, d, N.ptr(W.D),
+                   W.n_pad, 0, None, None, 0, N.ptr(W.rsc), s)
+        else:
+            N.call("dsvgd_sqdist", N.ptr(W.Y), W.ldy, N.ptr(W.norms), b0, nb, n, d, N.ptr(W.D),
+                   W.n_pad, 0, None, None, s)
         N.call("dsvgd_gs_mask", N.ptr(W.D), W.n_pad, b0, nb, s)
-        N.call("dsvgd_phi_mm", N.ptr(W.D), W.n_pad, N.ptr(W.Y), W.ldy, b0, nb, n, h_state.ptr,
-               W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), s)
+        if W.phi_x3:
+            N.call("dsvgd_phi_mm_x3", N.ptr(W.D), W.n_pad, N.ptr(W.Yx3), W.ldy, b0, nb, n,
+                   h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), 0, int(W.m16),
+                   None, s)
+        else:
+            N.call("dsvgd_phi_mm", N.ptr(W.D), W.n_pad, N.ptr(W.Y), W.ldy, b0, nb, n,
+                   h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), s)
         N.call("dsvgd_phi_partial_reduce", N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), W.splits, nb,
                2 * W.dp, N.ptr(W.Q), W.ldy, N.ptr(W.Qr), s)
         ex = N.ptr(extra[k0:k0 + nb]) if extra is not None else None
@@ -893,6 +942,7 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
                N.ptr(W.norms), N.ptr(W.mean), n, d, b0, nb, h_state.ptr, float(step), N.ptr(W.Q),
                W.ldy, N.ptr(W.Qr), ex, d, po, N.ld(phi_out) if phi_out is not None else d, sk,
                N.ptr(mu), N.ptr(lam), float(score_scale), s)
+        W.images(b0, nb, s)
 
 
 def _blocked_sweep(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s):

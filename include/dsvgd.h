@@ -323,6 +323,12 @@ int dsvgd_h2_rowsplit(const float* A, int64_t lda, int64_t rows, int64_t cols, i
 int dsvgd_h2_rowsplit_rows(const float* A, int64_t lda, int64_t rows, int64_t cols,
                            int64_t rows_pad, int64_t kpad, const float* rowscale, void* img,
                            void* stream);
+/* rows [row_begin, row_begin + nrows) of dsvgd_h2_rowsplit_rows's image only
+ * (the same arguments; ABI 4: the wide Gauss-Seidel sweep re-splits the rows a
+ * block moved). */
+int dsvgd_h2_rowsplit_rows_range(const float* A, int64_t lda, int64_t rows, int64_t cols,
+                                 int64_t rows_pad, int64_t kpad, const float* rscale, void* img,
+                                 int64_t row_begin, int64_t nrows, void* stream);
 /* rowscale[i] = the FmtH2 power-of-two scale of row i of A (rows x cols) and
  * rowinv[i] = 1 / rowscale[i] (nullable), for i < rows_pad (1 past rows) */
 int dsvgd_h2_rowscale(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
