@@ -364,9 +364,11 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 __global__ __launch_bounds__(256) void sample_sqdist_kernel(const float* __restrict__ Y,
                                                             int64_t ldy, int64_t n, int d,
                                                             int64_t s, uint64_t seed,
-                                                            float* __restrict__ out) {
+                                                            float* __restrict__ out,
+                                                            int64_t p0 = 0) {
+  // pairs [p0, s) (a rank's share of the sample: dsvgd_sample_sqdist_range)
   const int l16 = threadIdx.x & 15;
-  for (int64_t p = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); p < s;
+  for (int64_t p = p0 + (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); p < s;
        p += (int64_t)gridDim.x * 16) {
     const uint64_t h = mix64(seed ^ (0x9e3779b97f4a7c15ull * (uint64_t)(p + 1)));
     const int64_t i = (int64_t)((h & 0xffffffffull) % (uint64_t)n);
@@ -396,9 +398,10 @@ __global__ __launch_bounds__(256) void sample_sqdist_kernel(const float* __restr
 __global__ __launch_bounds__(256) void sample_sqdist_any_kernel(const float* __restrict__ Y,
                                                                 int64_t ldy, int64_t n, int d,
                                                                 int64_t s, uint64_t seed,
-                                                                float* __restrict__ out) {
+                                                                float* __restrict__ out,
+                                                                int64_t p0 = 0) {
   const int lane = threadIdx.x & 63;
-  for (int64_t p = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < s;
+  for (int64_t p = p0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < s;
        p += (int64_t)gridDim.x * 4) {
     const uint64_t h = mix64(seed ^ (0x9e3779b97f4a7c15ull * (uint64_t)(p + 1)));
     const int64_t i = (int64_t)((h & 0xffffffffull) % (uint64_t)n);
@@ -542,6 +545,45 @@ int dsvgd_sample_sqdist(const float* Y, int64_t ldy, int64_t n, int64_t d, int64
   hipLaunchKernelGGL(sample_sqdist_any_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, Y,
                      ldy, n, (int)d, s, seed, out);
   return check_launch("sample_sqdist_any");
+}
+
+int dsvgd_sample_sqdist_range(const float* Y, int64_t ldy, int64_t n, int64_t d, int64_t s,
+                              uint64_t seed, int64_t p0, int64_t p1, float* out, void* stream) {
+  DSVGD_REQUIRE(Y && out, "null pointer");
+  DSVGD_REQUIRE(n > 0 && d > 0 && s > 0 && ldy >= d && 0 <= p0 && p0 < p1 && p1 <= s, "sizes");
+  const int64_t np = p1 - p0;
+  if (ldy % 4 == 0 && ((uintptr_t)Y & 15) == 0) {
+    const int64_t blocks = std::min<int64_t>((np + 15) / 16, 8192);
+    hipLaunchKernelGGL(sample_sqdist_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, Y,
+                       ldy, n, (int)d, p1, seed, out, p0);
+    return check_launch("sample_sqdist");
+  }
+  const int64_t blocks = std::min<int64_t>((np + 3) / 4, 8192);
+  hipLaunchKernelGGL(sample_sqdist_any_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, Y,
+                     ldy, n, (int)d, p1, seed, out, p0);
+  return check_launch("sample_sqdist_any");
+}
+
+int dsvgd_sample_bracket_select(const float* sample, int64_t s, int64_t k_lo, int64_t k_hi,
+                                dsvgd_select_state* lo_st, dsvgd_select_state* hi_st,
+                                dsvgd_select_state* st, int64_t n_total, int64_t cand_cap,
+                                void* stream) {
+  DSVGD_REQUIRE(sample && lo_st && hi_st && st, "null pointer");
+  DSVGD_REQUIRE(n_total > 0 && cand_cap > 0, "sizes");
+  DSVGD_REQUIRE(s > 0 && s % 4 == 0 && ((uintptr_t)sample & 15) == 0,
+                "s must be a positive multiple of 4, sample 16-byte aligned");
+  DSVGD_REQUIRE(0 <= k_lo && k_lo <= k_hi && k_hi < s, "ranks: 0 <= k_lo <= k_hi < s");
+  hipStream_t strm = (hipStream_t)stream;
+  const dim3 hb((unsigned)std::min<int64_t>((s / 4 + 255) / 256, kSampleHistBlocks));
+#define DSVGD_SAMPLE_PASS(P)                                                                     \
+  hipLaunchKernelGGL(sample_hist_kernel<P>, hb, dim3(256), 0, strm, sample, s, lo_st, hi_st);   \
+  hipLaunchKernelGGL(sample_pick_kernel<P>, dim3(1), dim3(256), 0, strm, lo_st, hi_st, s, k_lo, \
+                     k_hi, st, n_total, cand_cap)
+  DSVGD_SAMPLE_PASS(1);
+  DSVGD_SAMPLE_PASS(2);
+  DSVGD_SAMPLE_PASS(3);
+#undef DSVGD_SAMPLE_PASS
+  return check_launch("sample_bracket_select");
 }
 
 int dsvgd_sample_bracket(const float* Y, int64_t ldy, int64_t n, int64_t d, int64_t s,

@@ -58,6 +58,9 @@ SIGNATURES = {
     "dsvgd_bracket_init": (_int, [_p, _i64, _p, _p, _i64, _p]),
     "dsvgd_sample_bracket": (_int, [_p, _i64, _i64, _i64, _i64, _c.c_uint64, _i64, _i64, _p, _p,
                                     _p, _p, _i64, _i64, _p]),
+    "dsvgd_sample_sqdist_range": (_int, [_p, _i64, _i64, _i64, _i64, _c.c_uint64, _i64, _i64, _p,
+                                         _p]),
+    "dsvgd_sample_bracket_select": (_int, [_p, _i64, _i64, _i64, _p, _p, _p, _i64, _i64, _p]),
     "dsvgd_bracket_totals": (_int, [_p, _p, _p]),
     "dsvgd_bracket_check": (_int, [_p, _p]),
     "dsvgd_set_bandwidth": (_int, [_p, _f, _p]),

@@ -309,7 +309,17 @@ class DistSampler(object):
         eng = self._engines[key]
         eng.set_row0(row0)
         eng.timer = self.timer
+        if self._exchange_particles and self._num_shards > 1 and not self._lagged:
+            # every rank packs the same particles: 1/S of the bracket sample each
+            eng.sample_share = (self._rank, self._num_shards, self._gather_sample)
         return eng
+
+    def _gather_sample(self, sample, start, end):
+        if exchange.all_gather_in_place(sample, start, end, self._group):
+            return
+        out = torch.empty_like(sample)
+        exchange.all_gather_blocks(sample[start:end], out, self._group)
+        sample.copy_(out)
 
     def _compute(self, step_size, h):
         """Scores, bandwidth, W2 term and the particle update of one step

@@ -380,7 +380,22 @@ class PhiEngine(object):
             N.call(fn, N.ptr(self.Y), self.ldy, N.ptr(self.norms), self.row0, self.m,
                    self.n, self.d, N.ptr(self.D), self.n_pad, mode, st, cand, s)
 
+    # (rank, S, gather): the S ranks that share this interacting set (same Y)
+    # each compute 1/S of the bracket sample and gather(sample, start, end)
+    # all-gathers the shares in place (DistSampler, particles exchanged)
+    sample_share = None
+
     def _bracket(self, s):
+        if self.sample_share is not None and self.SAMPLE % self.sample_share[1] == 0:
+            rank, S, gather = self.sample_share
+            per = self.SAMPLE // S
+            N.call("dsvgd_sample_sqdist_range", N.ptr(self.Y), self.ldy, self.n, self.d,
+                   self.SAMPLE, self.SEED, rank * per, (rank + 1) * per, N.ptr(self.sample), s)
+            gather(self.sample, rank * per, (rank + 1) * per)
+            N.call("dsvgd_sample_bracket_select", N.ptr(self.sample), self.SAMPLE, self.k_lo,
+                   self.k_hi, self.st_lo.ptr, self.st_hi.ptr, self.state.ptr, self.n,
+                   self.cand_cap, s)
+            return
         N.call("dsvgd_sample_bracket", N.ptr(self.Y), self.ldy, self.n, self.d, self.SAMPLE,
                self.SEED, self.k_lo, self.k_hi, N.ptr(self.sample), self.st_lo.ptr,
                self.st_hi.ptr, self.state.ptr, self.n, self.cand_cap, s)

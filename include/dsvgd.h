@@ -190,6 +190,16 @@ int dsvgd_sample_bracket(const float* Y, int64_t ldy, int64_t n, int64_t d, int6
                          dsvgd_select_state* lo_st, dsvgd_select_state* hi_st,
                          dsvgd_select_state* st, int64_t n_total, int64_t cand_cap,
                          void* stream);
+/* dsvgd_sample_bracket in two parts (ABI 4): a rank's share of the sample --
+ * dsvgd_sample_sqdist's pairs [p0, p1) of s, the same pairs and values --
+ * and, once the shares are all-gathered into the whole sample, the selects
+ * and the bracket (the last six launches of dsvgd_sample_bracket). */
+int dsvgd_sample_sqdist_range(const float* Y, int64_t ldy, int64_t n, int64_t d, int64_t s,
+                              uint64_t seed, int64_t p0, int64_t p1, float* out, void* stream);
+int dsvgd_sample_bracket_select(const float* sample, int64_t s, int64_t k_lo, int64_t k_hi,
+                                dsvgd_select_state* lo_st, dsvgd_select_state* hi_st,
+                                dsvgd_select_state* st, int64_t n_total, int64_t cand_cap,
+                                void* stream);
 /* ... then, after dsvgd_sqdist(BRACKET): bracket_totals sums the slots into
  * below_total / ncand_total / overflow (a distributed caller all-reduces
  * those three int64), and bracket_check decides exactly: below <= k <

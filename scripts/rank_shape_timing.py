@@ -49,6 +49,8 @@ def main():
         if eng.plan is not None:
             for b in eng.recvbuf:
                 b.zero_()
+        if S > 1:   # the rank's 1/S of the bracket sample (the all-gather left out)
+            eng.sample_share = (r, S, lambda *a: None)
         Sx = torch.empty_like(X)
         Xo = X[r * m:(r + 1) * m].clone()
         timer = StageTimer()
