@@ -308,6 +308,14 @@ __global__ void gs_mask_kernel(float* __restrict__ D, int64_t ldd, int64_t r0, i
 // One workgroup of 256 threads walks rows [r0, r0 + B).  Q: [K Xc | K S] of
 // the wide pass (ldq >= 2 dp), Qr its row sums; Y: [X - c | S] (updated for
 // each moved row, with norms[]), centre c = the Y packing centre.
+// Per row two barriers: (1) after the distance partials, (2) after the moved
+// row's LDS writes.  Every wave forms the row's kernel values itself (lane j:
+// k(x_i, x_j'), its moved-row sum by a wave reduction) and the column loop
+// broadcasts them with v_readlane; the next row's global operands (Q, Qr,
+// its old x and s, X) are loaded one row ahead into registers, so no row
+// waits on memory.
+constexpr int kGswCols = kGswMaxD / 256;  // columns per thread
+
 __global__ __launch_bounds__(256) void gsw_sweep_kernel(
     float* __restrict__ X, int64_t ldx, float* __restrict__ S, int64_t lds, float* __restrict__ Y,
     int64_t ldy, float* __restrict__ norms, const float* __restrict__ center, int64_t n, int d,
@@ -320,28 +328,67 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
   const int pitch = dp + 4;                       // 16-byte rows, 4 banks apart
   float* xn = gsw_smem;                           // [B][pitch]: moved rows, centred
   float* wn = xn + (int64_t)B * pitch;            // [B][dp]: s' - g (x' - c)
-  float* xo = wn + (int64_t)B * dp;               // [dp]: the row being moved (old, centred)
-  float* part = xo + dp;                          // [4][64] partial distances
-  float* kj = part + 256;                         // [64]
-  float* red = kj + 64;                           // [4] wave sums of kj
+  float* xo = wn + (int64_t)B * dp;               // [2][dp]: the row being moved (old, centred)
+  float* part = xo + 2 * dp;                      // [4][64] partial distances
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const float inv_h = st->inv_h, g = 2.f * inv_h, scale = -inv_h * kLog2e;
   const float inv_n = 1.f / (float)n;
   const int q4 = dp >> 2;                         // features per quarter (dp % 32 == 0)
   for (int e = t; e < B * pitch; e += 256) xn[e] = 0.f;
-  for (int e = t; e < dp; e += 256) xo[e] = Y[r0 * ldy + e];
+  // per-thread columns c = t + 256 u, u < kGswCols, and the next row's operands
+  float cen[kGswCols], mu_c[kGswCols], lam_c[kGswCols];
+  float nq_x[kGswCols], nq_s[kGswCols], n_xo[kGswCols], n_so[kGswCols], n_x[kGswCols];
+  float nqr = 0.f;
+  auto prefetch = [&](int i) {  // row i's operands (i < B)
+    const int64_t gi = r0 + i;
+#pragma unroll
+    for (int u = 0; u < kGswCols; ++u) {
+      const int c = t + 256 * u;
+      const bool ok = c < d;
+      nq_x[u] = ok ? Q[i * ldq + c] : 0.f;
+      nq_s[u] = ok ? Q[i * ldq + dp + c] : 0.f;
+      n_xo[u] = c < dp ? Y[gi * ldy + c] : 0.f;
+      n_so[u] = ok ? Y[gi * ldy + dp + c] : 0.f;
+      n_x[u] = ok ? X[gi * ldx + c] : 0.f;
+    }
+    nqr = Qr[i];
+  };
+#pragma unroll
+  for (int u = 0; u < kGswCols; ++u) {
+    const int c = t + 256 * u;
+    cen[u] = c < d ? center[c] : 0.f;
+    mu_c[u] = (score_kind == 1 && c < d) ? mu[c] : 0.f;
+    lam_c[u] = (score_kind == 1 && c < d) ? lam[c] : 0.f;
+  }
+  prefetch(0);
+#pragma unroll
+  for (int u = 0; u < kGswCols; ++u)
+    if (t + 256 * u < dp) xo[t + 256 * u] = n_xo[u];
   __syncthreads();
   for (int i = 0; i < B; ++i) {
+    const int64_t gi = r0 + i;
+    float q_x[kGswCols], q_s[kGswCols], xc_o[kGswCols], s_o[kGswCols], x_o[kGswCols];
+#pragma unroll
+    for (int u = 0; u < kGswCols; ++u) {
+      q_x[u] = nq_x[u];
+      q_s[u] = nq_s[u];
+      xc_o[u] = n_xo[u];
+      s_o[u] = n_so[u];
+      x_o[u] = n_x[u];
+    }
+    const float qr = nqr;
+    if (i + 1 < B) prefetch(i + 1);
+    const float* xoi = xo + (i & 1) * dp;
     // (a) distances of the old row i to the moved rows j < i: thread (j =
     // lane, quarter w) over features [w q4, (w + 1) q4)
     {
       float sa = 0.f, sb = 0.f;
       if (lane < i) {
-        const float* a = xo + w * q4;
-        const float* b = xn + lane * pitch + w * q4;
+        const float* pa = xoi + w * q4;
+        const float* pb = xn + lane * pitch + w * q4;
         for (int c = 0; c < q4; c += 4) {
-          const f32x4 va = *reinterpret_cast<const f32x4*>(a + c);
-          const f32x4 vb = *reinterpret_cast<const f32x4*>(b + c);
+          const f32x4 va = *reinterpret_cast<const f32x4*>(pa + c);
+          const f32x4 vb = *reinterpret_cast<const f32x4*>(pb + c);
           const float d0 = va[0] - vb[0], d1 = va[1] - vb[1], d2 = va[2] - vb[2], d3 = va[3] - vb[3];
           sa = fmaf(d0, d0, fmaf(d2, d2, sa));
           sb = fmaf(d1, d1, fmaf(d3, d3, sb));
@@ -349,53 +396,54 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
       }
       part[w * 64 + lane] = sa + sb;
     }
-    __syncthreads();
-    if (w == 0) {
-      const float dd = (part[lane] + part[64 + lane]) + (part[128 + lane] + part[192 + lane]);
-      const float k = lane < i ? __builtin_amdgcn_exp2f(dd * scale) : 0.f;
-      kj[lane] = k;
-      float r = k;
-      for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
-      if (lane == 0) red[0] = r;
-    }
-    __syncthreads();
+    __syncthreads();                                                        // (1)
+    // every wave: lane j's k(x_i, x_j') and the moved rows' kernel sum
+    const float dd = (part[lane] + part[64 + lane]) + (part[128 + lane] + part[192 + lane]);
+    const float kj = lane < i ? __builtin_amdgcn_exp2f(dd * scale) : 0.f;
+    float rm = kj;
+    for (int o = 32; o > 0; o >>= 1) rm += __shfl_xor(rm, o, 64);
+    const float rtot = qr + rm;
     // (b) per column: the wide pass + the moved rows' terms + the self term
-    const float rm = red[0];
-    const int64_t gi = r0 + i;
-    const float rtot = Qr[i] + rm;
-    for (int c = t; c < d; c += 256) {
+#pragma unroll
+    for (int u = 0; u < kGswCols; ++u) {
+      const int c = t + 256 * u;
+      if (c >= d) continue;
       float acc0 = 0.f, acc1 = 0.f;
       int j = 0;
       for (; j + 2 <= i; j += 2) {
-        acc0 = fmaf(kj[j], wn[j * dp + c], acc0);
-        acc1 = fmaf(kj[j + 1], wn[(j + 1) * dp + c], acc1);
+        const float k0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kj), j));
+        const float k1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kj), j + 1));
+        acc0 = fmaf(k0, wn[j * dp + c], acc0);
+        acc1 = fmaf(k1, wn[(j + 1) * dp + c], acc1);
       }
-      if (j < i) acc0 = fmaf(kj[j], wn[j * dp + c], acc0);
-      const float xc = xo[c];                       // x_i - c (old)
-      const float s_old = Y[gi * ldy + dp + c];     // s_i (the self term k_ii s_i)
-      float p = inv_n * (((Q[i * ldq + dp + c] + s_old) - g * Q[i * ldq + c]) + (acc0 + acc1) +
-                         g * rtot * xc);
+      if (j < i) {
+        const float k0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kj), j));
+        acc0 = fmaf(k0, wn[j * dp + c], acc0);
+      }
+      // + the self term k_ii s_i (the wide pass skipped the diagonal)
+      float p = inv_n * (((q_s[u] + s_o[u]) - g * q_x[u]) + (acc0 + acc1) + g * rtot * xc_o[u]);
       if (extra) p += extra[(int64_t)i * lde + c];
       if (phi_out) phi_out[(int64_t)i * ldphi + c] = p;
-      const float x = X[gi * ldx + c] + step * p;
+      const float x = x_o[u] + step * p;
       X[gi * ldx + c] = x;
-      float s = s_old;
+      float sv = s_o[u];
       if (score_kind != 0) {
-        s = gs_score(score_kind, x, score_kind == 1 ? mu[c] : 0.f,
-                     score_kind == 1 ? lam[c] : 0.f, score_scale);
-        S[gi * lds + c] = s;
+        sv = gs_score(score_kind, x, mu_c[u], lam_c[u], score_scale);
+        S[gi * lds + c] = sv;
       }
-      const float xcn = x - center[c];
+      const float xcn = x - cen[u];
       xn[i * pitch + c] = xcn;
-      wn[i * dp + c] = s - g * xcn;
+      wn[i * dp + c] = sv - g * xcn;
       Y[gi * ldy + c] = xcn;
-      Y[gi * ldy + dp + c] = s;
+      Y[gi * ldy + dp + c] = sv;
     }
-    __syncthreads();
-    // the next row's old values (after this row's reads of xo)
-    if (i + 1 < B)
-      for (int e = t; e < dp; e += 256) xo[e] = Y[(gi + 1) * ldy + e];
-    __syncthreads();
+    // the next row's old values into the other xo buffer
+    if (i + 1 < B) {
+#pragma unroll
+      for (int u = 0; u < kGswCols; ++u)
+        if (t + 256 * u < dp) xo[((i + 1) & 1) * dp + t + 256 * u] = n_xo[u];
+    }
+    __syncthreads();                                                        // (2)
   }
   // the moved rows' norms |x' - c|^2 (the later blocks' distances)
   for (int i = w; i < B; i += 4) {
@@ -490,7 +538,7 @@ int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y
   DSVGD_REQUIRE(score_kind != 1 || (mu && lam), "Gaussian scores need mu and lam");
   DSVGD_REQUIRE(!extra || lde >= d, "lde");
   DSVGD_REQUIRE(!phi_out || ldphi >= d, "ldphi");
-  const size_t smem = sizeof(float) * ((size_t)B * (dp + 4) + (size_t)B * dp + dp + 256 + 64 + 4);
+  const size_t smem = sizeof(float) * ((size_t)B * (dp + 4) + (size_t)B * dp + 2 * dp + 256);
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gsw_sweep_kernel),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
     return fail_arg("gsw_sweep: cannot reserve the walk's LDS");
