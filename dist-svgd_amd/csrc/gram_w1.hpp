@@ -143,9 +143,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     float* __restrict__ D, dsvgd_select_state* __restrict__ st, float* __restrict__ cand,
     int64_t total_units, int Tm, int Tc, int jp_off, int64_t slot_base, int64_t ns_total,
     int w2all = 0, const float* __restrict__ gate = nullptr) {
-  // gate: a fallback-only part of the pair-split layout (dsvgd_sqdist_h2_parts)
-  // runs iff the FmtH2 range guard word is set
-  if (gate && *gate == 0.f) return;
   using V8 = FmtH2::V8;
   constexpr bool kBr = smode == kSelBracket;
   __builtin_assume(nk >= 16 && nk % 16 == 0);  // checked by the host
@@ -156,7 +153,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   // this XCD's contiguous range of units, strided by its blocks
   const int64_t x = blockIdx.x % kXcds, u = blockIdx.x / kXcds, U = gridDim.x / kXcds;
-  const int64_t q = total_units / kXcds, rr = total_units % kXcds;
+  // gate: a fallback-only part of the pair-split layout (dsvgd_sqdist_h2_parts)
+  // has units iff the FmtH2 range guard word is set (folded into the unit
+  // count: an early return here cost the kernel 73 VGPRs and 160 B of spills)
+  int64_t units = total_units;
+  if constexpr (smode == kSelNone)  // (fallback parts never do select accounting)
+    units = (gate && *gate == 0.f) ? 0 : total_units;
+  const int64_t q = units / kXcds, rr = units % kXcds;
   const int64_t lo = x * q + min(x, rr);
   const int64_t hi = (int64_t)__builtin_amdgcn_readfirstlane((int)(lo + q + (x < rr ? 1 : 0)));
   SlotLayout sl(cand, ns_total, kBr ? st->cand_cap : 0);

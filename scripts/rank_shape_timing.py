@@ -49,8 +49,19 @@ def main():
         if eng.plan is not None:
             for b in eng.recvbuf:
                 b.zero_()
-        if S > 1:   # the rank's 1/S of the bracket sample (the all-gather left out)
-            eng.sample_share = (r, S, lambda *a: None)
+        if S > 1:
+            # the rank's 1/S of the bracket sample; the other ranks' shares
+            # (the all-gather) stand in as a device copy of the whole sample
+            full = torch.empty(eng.SAMPLE, device="cuda:0")
+            from dsvgd import _native as NN
+            eng.pack(X, None)
+            NN.call("dsvgd_sample_sqdist", NN.ptr(eng.Y), eng.ldy, n, d, eng.SAMPLE, eng.SEED,
+                    NN.ptr(full), NN.stream(0))
+
+            def gather(sample, a, b, full=full):
+                sample[:a].copy_(full[:a])
+                sample[b:].copy_(full[b:])
+            eng.sample_share = (r, S, gather)
         Sx = torch.empty_like(X)
         Xo = X[r * m:(r + 1) * m].clone()
         timer = StageTimer()

@@ -24,7 +24,8 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="D,E")
-    ap.add_argument("--rows-sample", type=int, default=2048)
+    ap.add_argument("--rows-sample", type=int, default=2048,
+                    help="rows of the per-row path to time (0: skip it)")
     args = ap.parse_args()
     import dsvgd
     from dsvgd.engine import sequential_sweep
@@ -48,13 +49,15 @@ def main():
         # the per-row kernels over a sample of rows, same scores and bandwidth
         eng = next(iter(ds._engines.values()))
         k = min(args.rows_sample, n)
-        Xc, Sc = X.clone(), ds._scores.clone()
-        sequential_sweep(Xc, Sc, range(0, 64), eng.state, 1e-4, blocked=False)   # warm-up
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        sequential_sweep(Xc, Sc, range(64, 64 + k), eng.state, 1e-4, blocked=False)
-        torch.cuda.synchronize()
-        per_row_ms = 1e3 * (time.perf_counter() - t0) * n / k
+        per_row_ms = None
+        if k > 0:
+            Xc, Sc = X.clone(), ds._scores.clone()
+            sequential_sweep(Xc, Sc, range(0, 64), eng.state, 1e-4, blocked=False)   # warm-up
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            sequential_sweep(Xc, Sc, range(64, 64 + k), eng.state, 1e-4, blocked=False)
+            torch.cuda.synchronize()
+            per_row_ms = 1e3 * (time.perf_counter() - t0) * n / k
         # the blocked sweep alone (no median / scores), for the stage split
         Xb, Sb = X.clone(), ds._scores.clone()
         torch.cuda.synchronize()
@@ -66,7 +69,8 @@ def main():
                           "step_ms_blocked": blocked_ms, "sweep_only_ms_blocked": sweep_ms,
                           "particle_updates_per_s": n / blocked_ms * 1e3,
                           "per_row_ms_extrapolated": per_row_ms, "per_row_sample_rows": k,
-                          "speedup_vs_per_row": per_row_ms / sweep_ms}), flush=True)
+                          "speedup_vs_per_row": per_row_ms / sweep_ms if per_row_ms else None}),
+              flush=True)
         del ds, eng
         torch.cuda.empty_cache()
 
