@@ -60,17 +60,23 @@ struct GramW1 {
 // Unit L -> (strip I, column pair J2).  Group g = strips [G g, G g + G)
 // (G = kGroup) over column pairs [j0(g), Tc) (symmetric: j0(g) = G g / 2,
 // the pair holding the group's first diagonal tile), strip-fastest.
+// A row block of fewer than kGroup strips (the wide Gauss-Seidel pass: one
+// strip) groups them all: phantom strips in the walk would leave 7 of 8
+// blocks idle (96 us for a 64-row block on r11d, one unit per live block).
+// The symmetric walk keeps kGroup (a compile-time group: no spills).
 struct GramUnitWalk {
-  int Tm, Tc, ng;
+  int Tm, Tc, G, ng;
   bool sym;
   int g = 0;
   int64_t goff = 0;
   __host__ __device__ GramUnitWalk(int Tm_, int Tc_, bool sym_)
-      : Tm(Tm_), Tc(Tc_), ng((Tm_ + GramW1::kGroup - 1) / GramW1::kGroup), sym(sym_) {}
-  __host__ __device__ int j0(int gg) const { return sym ? gg * (GramW1::kGroup / 2) : 0; }
+      : Tm(Tm_), Tc(Tc_),
+        G(sym_ || Tm_ >= GramW1::kGroup ? GramW1::kGroup : (Tm_ > 0 ? Tm_ : 1)),
+        ng((Tm_ + G - 1) / G), sym(sym_) {}
+  __host__ __device__ int j0(int gg) const { return sym ? gg * (G / 2) : 0; }
   __host__ __device__ int64_t count(int gg) const {
     const int c = Tc - j0(gg);
-    return c > 0 ? (int64_t)c * GramW1::kGroup : 0;
+    return c > 0 ? (int64_t)c * G : 0;
   }
   __host__ __device__ int64_t total() const {
     int64_t s = 0;
@@ -85,8 +91,8 @@ struct GramUnitWalk {
     }
     if (g >= ng) return false;
     const int64_t rem = L - goff;
-    J2 = j0(g) + (int)(rem / GramW1::kGroup);
-    I = g * GramW1::kGroup + (int)(rem % GramW1::kGroup);
+    J2 = j0(g) + (int)(rem / G);
+    I = g * G + (int)(rem % G);
     return I < Tm && J2 < Tc && (!sym || I <= 2 * J2 + 1);
   }
 };

@@ -316,6 +316,16 @@ __global__ void gs_mask_kernel(float* __restrict__ D, int64_t ldd, int64_t r0, i
 // waits on memory.
 constexpr int kGswCols = kGswMaxD / 256;  // columns per thread
 
+// LDS hand-offs only: wait for this wave's LDS operations, then s_barrier.
+// (__syncthreads() also drains every global load and store -- the next
+// row's prefetch included -- which cost ~2.7 us per row, r11d.)  No global
+// location the walk writes is read inside it by another thread.
+__device__ __forceinline__ void gsw_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 __global__ __launch_bounds__(256) void gsw_sweep_kernel(
     float* __restrict__ X, int64_t ldx, float* __restrict__ S, int64_t lds, float* __restrict__ Y,
     int64_t ldy, float* __restrict__ norms, const float* __restrict__ center, int64_t n, int d,
@@ -396,7 +406,7 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
       }
       part[w * 64 + lane] = sa + sb;
     }
-    __syncthreads();                                                        // (1)
+    gsw_barrier();                                                          // (1)
     // every wave: lane j's k(x_i, x_j') and the moved rows' kernel sum
     const float dd = (part[lane] + part[64 + lane]) + (part[128 + lane] + part[192 + lane]);
     const float kj = lane < i ? __builtin_amdgcn_exp2f(dd * scale) : 0.f;
@@ -443,7 +453,7 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
       for (int u = 0; u < kGswCols; ++u)
         if (t + 256 * u < dp) xo[((i + 1) & 1) * dp + t + 256 * u] = n_xo[u];
     }
-    __syncthreads();                                                        // (2)
+    gsw_barrier();                                                          // (2)
   }
   // the moved rows' norms |x' - c|^2 (the later blocks' distances)
   for (int i = w; i < B; i += 4) {

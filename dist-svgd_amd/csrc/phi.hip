@@ -350,26 +350,47 @@ __global__ __launch_bounds__(256) void phi_finish_kernel(
   if (X) X[i * ldx + c] += step * p;
 }
 
-// ---- the pair-split layout's partials (dsvgd_phi_h2_transposed)
-// out[i][c] = sum_z P[z][i][c], out_rs[i] = sum_z rs[z][i] (slice order);
-// four columns per thread
+// ---- split-K partials summed (dsvgd_phi_h2_transposed, the wide sweep) ---
+// out[i][c] = sum_z P[z][i][c], out_rs[i] = sum_z rs[z][i] in a fixed order:
+// a workgroup takes 16 float4 positions; its 16 thread groups sum the slices
+// z = g, g + 16, ... (16 independent loads in flight per thread), then the
+// 16 group sums are added in g order.  (One thread per position walking all
+// the slices was latency-bound: 122 us for 256 slices of 64 x 512, r11d.)
 __global__ __launch_bounds__(256) void partial_reduce_kernel(
     const float* __restrict__ P, int64_t ldp, const float* __restrict__ rs, int splits,
     int64_t rows, int64_t cols, float* __restrict__ out, int64_t ldo, float* __restrict__ out_rs) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t c4 = cols >> 2;
-  const int64_t rp = roundup128(rows);
-  if (t < rows * c4) {
-    const int64_t i = t / c4, c = (t % c4) * 4;
-    f32x4 a = *reinterpret_cast<const f32x4*>(P + i * ldp + c);
-    for (int z = 1; z < splits; ++z)
+  __shared__ f32x4 red[16][16];
+  const int q = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int64_t c4 = cols >> 2, rp = roundup128(rows);
+  const int64_t npos = rows * c4, nrs = (rows + 3) >> 2;
+  const int64_t p = (int64_t)blockIdx.x * 16 + q;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f};
+  if (p < npos) {
+    const int64_t i = p / c4, c = (p % c4) * 4;
+    for (int z = g; z < splits; z += 16)
       a += *reinterpret_cast<const f32x4*>(P + ((int64_t)z * rows + i) * ldp + c);
-    *reinterpret_cast<f32x4*>(out + i * ldo + c) = a;
+  } else if (p < npos + nrs) {
+    const int64_t i0 = (p - npos) * 4;
+    for (int z = g; z < splits; z += 16)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (i0 + e < rows) a[e] += rs[(int64_t)z * rp + i0 + e];
   }
-  if (t < rows) {
-    float r = rs[t];
-    for (int z = 1; z < splits; ++z) r += rs[(int64_t)z * rp + t];
-    out_rs[t] = r;
+  red[g][q] = a;
+  __syncthreads();
+  if (g == 0) {
+    f32x4 sum = red[0][q];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) sum += red[k][q];
+    if (p < npos) {
+      const int64_t i = p / c4, c = (p % c4) * 4;
+      *reinterpret_cast<f32x4*>(out + i * ldo + c) = sum;
+    } else if (p < npos + nrs) {
+      const int64_t i0 = (p - npos) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (i0 + e < rows) out_rs[i0 + e] = sum[e];
+    }
   }
 }
 
@@ -980,8 +1001,8 @@ int dsvgd_phi_partial_reduce(const float* P, int64_t ldp, const float* rs, int64
                 "sizes (cols, ldp, ldo multiples of 4)");
   DSVGD_REQUIRE(splits >= 1 && splits <= 1024, "splits must be in [1, 1024]");
   DSVGD_REQUIRE(((uintptr_t)P & 15) == 0 && ((uintptr_t)out & 15) == 0, "16-byte alignment");
-  const int64_t threads = std::max(rows * (cols / 4), rows);
-  hipLaunchKernelGGL(partial_reduce_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+  const int64_t positions = rows * (cols / 4) + (rows + 3) / 4;
+  hipLaunchKernelGGL(partial_reduce_kernel, dim3((unsigned)((positions + 15) / 16)), dim3(256), 0,
                      (hipStream_t)stream, P, ldp, rs, (int)splits, rows, cols, out, ldo, out_rs);
   return check_launch("partial_reduce");
 }

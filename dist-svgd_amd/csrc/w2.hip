@@ -402,6 +402,152 @@ __device__ __forceinline__ void wave_best(double cv, int cj, int u, int lane, do
   }
 }
 
+// ---- the phase tail, Gauss-Seidel (one workgroup) -----------------------
+// A phase ends with long runs of rounds in which a handful of slots bid
+// (profiles/r8j: 17k of the 19k rounds of a warm m = 8192, n = 65536 solve
+// had <= 16 unassigned slots), each round two launches.  Once the unassigned
+// count is <= kTailMax, block 0 of the bid launch runs the rest of the phase
+// itself: the unassigned slots (found by a scan, sorted: deterministic) bid
+// one at a time -- the u = 1 bid of the parallel rounds, from the row's price
+// cache or a workgroup scan -- and each bid is resolved on the spot (a
+// displaced slot goes back on the stack).  The same eps-complementary-
+// slackness invariant as the Jacobi rounds, so the phase ends eps-optimal;
+// the resolve launch behind it then runs the control step.  At most
+// kTailBids bids per launch (the next round's launch continues).
+constexpr int kTailMax = 64;
+constexpr int kTailBids = 4096;
+
+template <int K>
+__device__ void w2_tail(const float* __restrict__ C, int64_t ldc, int64_t n, int64_t R, W2Ws w,
+                        int ep, double eps, uint32_t tag, bool cached, double* sv, int* sj,
+                        double* outv, int* outj) {
+  __shared__ int stack[kTailMax], sorted[kTailMax];
+  __shared__ int sp, cnt;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t == 0) cnt = 0;
+  __syncthreads();
+  for (int64_t s0 = t; s0 < n; s0 += 256)
+    if (!(w.assigned_ep[s0] == ep && w.assigned[s0] >= 0)) {
+      const int pos = atomicAdd(&cnt, 1);
+      if (pos < kTailMax) stack[pos] = (int)s0;
+    }
+  __syncthreads();
+  const int c0 = min(cnt, kTailMax);
+  if (t < c0) {  // sort (descending: the lowest slot bids first, from the top)
+    const int v = stack[t];
+    int r = 0;
+    for (int q = 0; q < c0; ++q) r += stack[q] > v;
+    sorted[r] = v;
+  }
+  __syncthreads();
+  if (t < c0) stack[t] = sorted[t];
+  if (t == 0) sp = c0;
+  __syncthreads();
+  for (int b = 0; b < kTailBids; ++b) {
+    const int top = sp;  // block-uniform (read after the barrier)
+    if (top == 0) break;
+    const int s = stack[top - 1];
+    const int64_t i = s / R;
+    const uint32_t mine = tag | (uint32_t)i;
+    const float* row = C + i * ldc;
+    double v1 = -DBL_MAX, v2 = -DBL_MAX;
+    int j1 = INT32_MAX;
+    bool have = false;
+    if (cached && w.cvalid[i]) {  // block-uniform: wave 0 tries the cache
+      if (wv == 0) {
+        double cv = -DBL_MAX;
+        int cj = INT32_MAX;
+        if (lane < kCache) {
+          const int c = w.ccol[i * kCache + lane];
+          if (c != INT32_MAX && w.holder[c] != mine) {
+            cj = c;
+            cv = -(double)w.ccost[i * kCache + lane] - w.price[c];
+          }
+        }
+        double kv;
+        int kj;
+        wave_best(cv, cj, 1, lane, kv, kj);
+        const double b1 = __shfl(kv, 0, 64), b2 = __shfl(kv, 1, 64);
+        const int bj = __shfl(kj, 0, 64);
+        if (lane == 0) {
+          outv[0] = b1;
+          outv[1] = b2;
+          outj[0] = bj;
+          sp = (b2 >= w.cbound[i]) ? -top : top;  // the sign carries the hit
+        }
+      }
+      __syncthreads();
+      have = sp < 0;
+      __syncthreads();
+      if (t == 0 && have) sp = top;
+      __syncthreads();
+    }
+    if (!have) {
+      if (cached) {  // full scan over all columns, refill the cache
+        block_topk<kCache + 1>(row, n, w, mine, false, sv, sj, outv, outj);
+        if (wv == 0) {
+          const double ev = lane < kCache + 1 ? outv[lane] : -DBL_MAX;
+          const int ej = lane < kCache + 1 ? outj[lane] : INT32_MAX;
+          if (lane < kCache) {
+            w.ccol[i * kCache + lane] = ej;
+            w.ccost[i * kCache + lane] = ej != INT32_MAX ? row[ej] : 0.f;
+          }
+          if (lane == kCache) w.cbound[i] = ev;
+          if (lane == 0) w.cvalid[i] = 1;
+          double cv = -DBL_MAX;
+          int cj = INT32_MAX;
+          if (lane < kCache && ej != INT32_MAX && w.holder[ej] != mine) {
+            cj = ej;
+            cv = ev;
+          }
+          double kv;
+          int kj;
+          wave_best(cv, cj, 1, lane, kv, kj);
+          const double b1 = __shfl(kv, 0, 64), b2 = __shfl(kv, 1, 64);
+          const int bj = __shfl(kj, 0, 64);
+          if (lane == 0) {  // (one wave: its LDS reads of outv are in order before)
+            outv[0] = b1;
+            outv[1] = b2;
+            outj[0] = bj;
+          }
+        }
+      } else {
+        block_topk<K>(row, n, w, mine, true, sv, sj, outv, outj);
+      }
+      __syncthreads();
+    }
+    v1 = outv[0];
+    v2 = outv[1];
+    j1 = outj[0];
+    if (t == 0) {
+      int next = top - 1;
+      if (j1 != INT32_MAX) {
+        const double vref = (v2 > -DBL_MAX) ? v2 : v1;
+        const double inc = v1 - vref + eps;
+        float f = (float)inc;
+        if ((double)f > inc) f = nextafterf(f, 0.f);  // round down: keeps eps-CS
+        if (!(f > 0.f)) f = FLT_MIN;
+        w.price[j1] += (double)f;
+        const uint32_t h = w.holder[j1];
+        const int old = ((h & ~(uint32_t)(kMaxRows - 1)) == tag) ? w.owner[j1] : -1;
+        if (old >= 0) {
+          w.assigned[old] = -1;  // displaced: bids next
+          stack[next++] = old;
+        } else {
+          atomicAdd(&w.ctl->unassigned, (unsigned long long)(-1ll));
+        }
+        w.owner[j1] = s;
+        w.holder[j1] = tag | (uint32_t)i;
+        w.assigned[s] = j1;
+        w.assigned_ep[s] = ep;
+      }
+      sp = next;
+      __threadfence_block();
+    }
+    __syncthreads();
+  }
+}
+
 // Rows in groups of four per workgroup-iteration (wave q: row base + q):
 // each wave finds its row's free slots and, with the price cache, tries the
 // cached bid; the rows left (no cache hit) are scanned one after the other by
@@ -419,6 +565,10 @@ __global__ __launch_bounds__(256) void w2_bid_cached_kernel(const float* __restr
   const int ep = ctl->epoch;
   const double eps = ctl->eps;
   const uint32_t tag = w2_tag(ep);
+  if (ctl->unassigned <= (unsigned long long)kTailMax) {  // the phase tail (uniform)
+    if (blockIdx.x == 0) w2_tail<2>(C, ldc, n, R, w, ep, eps, tag, true, sv, sj, outv, outj);
+    return;
+  }
   for (int64_t base = (int64_t)blockIdx.x * 4; base < m; base += (int64_t)gridDim.x * 4) {
     const int64_t i = base + wv;
     unsigned long long free = 0;
@@ -503,6 +653,10 @@ __global__ __launch_bounds__(256) void w2_bid_kernel(const float* __restrict__ C
   const int ep = ctl->epoch;
   const double eps = ctl->eps;
   const uint32_t tag = w2_tag(ep);
+  if (ctl->unassigned <= (unsigned long long)kTailMax) {  // the phase tail (uniform)
+    if (blockIdx.x == 0) w2_tail<K>(C, ldc, n, R, w, ep, eps, tag, false, sv, sj, outv, outj);
+    return;
+  }
   for (int64_t base = (int64_t)blockIdx.x * 4; base < m; base += (int64_t)gridDim.x * 4) {
     const int64_t i = base + wv;
     unsigned long long free = 0;
