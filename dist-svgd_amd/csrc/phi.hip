@@ -352,36 +352,38 @@ __global__ __launch_bounds__(256) void phi_finish_kernel(
 
 // ---- split-K partials summed (dsvgd_phi_h2_transposed, the wide sweep) ---
 // out[i][c] = sum_z P[z][i][c], out_rs[i] = sum_z rs[z][i] in a fixed order:
-// a workgroup takes 16 float4 positions; its 16 thread groups sum the slices
-// z = g, g + 16, ... (16 independent loads in flight per thread), then the
-// 16 group sums are added in g order.  (One thread per position walking all
-// the slices was latency-bound: 122 us for 256 slices of 64 x 512, r11d.)
+// a workgroup takes 256 / G float4 positions; its G thread groups (G = the
+// slice count rounded up to a power of two, at most 16) sum the slices z =
+// g, g + G, ... (independent loads in flight), then the G group sums are
+// added in g order.  (One thread per position walking all the slices was
+// latency-bound: 122 us for 256 slices of 64 x 512, r11d.)
 __global__ __launch_bounds__(256) void partial_reduce_kernel(
     const float* __restrict__ P, int64_t ldp, const float* __restrict__ rs, int splits,
-    int64_t rows, int64_t cols, float* __restrict__ out, int64_t ldo, float* __restrict__ out_rs) {
-  __shared__ f32x4 red[16][16];
-  const int q = threadIdx.x & 15, g = threadIdx.x >> 4;
+    int64_t rows, int64_t cols, float* __restrict__ out, int64_t ldo, float* __restrict__ out_rs,
+    int G) {
+  __shared__ f32x4 red[256];
+  const int per = 256 / G;
+  const int q = threadIdx.x % per, g = threadIdx.x / per;
   const int64_t c4 = cols >> 2, rp = roundup128(rows);
   const int64_t npos = rows * c4, nrs = (rows + 3) >> 2;
-  const int64_t p = (int64_t)blockIdx.x * 16 + q;
+  const int64_t p = (int64_t)blockIdx.x * per + q;
   f32x4 a = {0.f, 0.f, 0.f, 0.f};
   if (p < npos) {
     const int64_t i = p / c4, c = (p % c4) * 4;
-    for (int z = g; z < splits; z += 16)
+    for (int z = g; z < splits; z += G)
       a += *reinterpret_cast<const f32x4*>(P + ((int64_t)z * rows + i) * ldp + c);
   } else if (p < npos + nrs) {
     const int64_t i0 = (p - npos) * 4;
-    for (int z = g; z < splits; z += 16)
+    for (int z = g; z < splits; z += G)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         if (i0 + e < rows) a[e] += rs[(int64_t)z * rp + i0 + e];
   }
-  red[g][q] = a;
+  red[g * per + q] = a;
   __syncthreads();
   if (g == 0) {
-    f32x4 sum = red[0][q];
-#pragma unroll
-    for (int k = 1; k < 16; ++k) sum += red[k][q];
+    f32x4 sum = red[q];
+    for (int k = 1; k < G; ++k) sum += red[k * per + q];
     if (p < npos) {
       const int64_t i = p / c4, c = (p % c4) * 4;
       *reinterpret_cast<f32x4*>(out + i * ldo + c) = sum;
@@ -1002,8 +1004,12 @@ int dsvgd_phi_partial_reduce(const float* P, int64_t ldp, const float* rs, int64
   DSVGD_REQUIRE(splits >= 1 && splits <= 1024, "splits must be in [1, 1024]");
   DSVGD_REQUIRE(((uintptr_t)P & 15) == 0 && ((uintptr_t)out & 15) == 0, "16-byte alignment");
   const int64_t positions = rows * (cols / 4) + (rows + 3) / 4;
-  hipLaunchKernelGGL(partial_reduce_kernel, dim3((unsigned)((positions + 15) / 16)), dim3(256), 0,
-                     (hipStream_t)stream, P, ldp, rs, (int)splits, rows, cols, out, ldo, out_rs);
+  int G = 1;
+  while (G < splits && G < 16) G *= 2;
+  const int64_t per = 256 / G;
+  hipLaunchKernelGGL(partial_reduce_kernel, dim3((unsigned)((positions + per - 1) / per)), dim3(256),
+                     0, (hipStream_t)stream, P, ldp, rs, (int)splits, rows, cols, out, ldo, out_rs,
+                     G);
   return check_launch("partial_reduce");
 }
 
