@@ -994,6 +994,31 @@ int dsvgd_phi_h2_transposed(const float* D, int64_t ldd, const void* Yh, int64_t
   return check_launch("phi_w1_kernel(transposed)");
 }
 
+int dsvgd_phi_h2_transposed_blocks(const float* D, int64_t ldd, const void* Yh, int64_t ldy,
+                                   int64_t yrow0, int64_t m, int64_t first, int64_t nblocks,
+                                   int64_t count, int64_t n, const dsvgd_select_state* st,
+                                   float* P, int64_t ldp, int64_t pstride, const float* colinv,
+                                   const float* gate, int gate_on, void* stream) {
+  DSVGD_REQUIRE(D && Yh && st && P && colinv, "null pointer");
+  const int64_t n_pad = roundup(n, 128);
+  DSVGD_REQUIRE(ldd == n_pad, "ldd must equal roundup(n,128) (panel layout)");
+  DSVGD_REQUIRE(ldy % 512 == 0 && ldp >= ldy, "ldy must be a multiple of 512, ldp >= ldy");
+  DSVGD_REQUIRE(m > 0 && m % 128 == 0 && nblocks * m <= n_pad && count >= 1 &&
+                    count <= nblocks && first >= 0 && first < nblocks,
+                "blocks: m a multiple of 128, count <= nblocks, nblocks m <= n_pad");
+  DSVGD_REQUIRE(yrow0 >= 0 && yrow0 % 16 == 0 && yrow0 + m <= n_pad, "the rectangle's rows");
+  DSVGD_REQUIRE(pstride >= m * ldp + roundup(m, 128), "pstride: room for P and its row sums");
+  DSVGD_REQUIRE(n_pad * ldy * 4 < ((int64_t)1 << 31), "n x ldy too large for 32-bit offsets");
+  DSVGD_REQUIRE(((uintptr_t)Yh & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
+  const int64_t per = m / 128;
+  const dim3 grid((unsigned)(ldy / PhiW1::BC), (unsigned)(per * count), 1u);
+  hipLaunchKernelGGL(phi_w1_kernel<3>, grid, dim3(PhiW1::kThreads), 0, (hipStream_t)stream, D,
+                     n_pad, (const _Float16*)Yh, ldy, m, m, st, P, ldp, P + m * ldp, m, (int64_t)0,
+                     0, colinv, 0, gate, gate_on, (int)(yrow0 / PhiW1::BJ), 0, 0, (int)per,
+                     (int)first, (int)nblocks, pstride);
+  return check_launch("phi_w1_kernel(transposed blocks)");
+}
+
 int dsvgd_phi_partial_reduce(const float* P, int64_t ldp, const float* rs, int64_t splits,
                              int64_t rows, int64_t cols, float* out, int64_t ldo, float* out_rs,
                              void* stream) {

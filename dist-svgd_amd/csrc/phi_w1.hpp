@@ -69,7 +69,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     int64_t K, int64_t kchunk, const dsvgd_select_state* __restrict__ st, float* __restrict__ C,
     int64_t ldc, float* __restrict__ rowsum, int64_t m, int64_t row0, int sym,
     const float* __restrict__ colinv, int slice0, const float* __restrict__ gate, int gate_on,
-    int ks_begin = 0, int ks_wrap = 0, int tcol0 = 0) {
+    int ks_begin = 0, int ks_wrap = 0, int tcol0 = 0, int t_per = 0, int t_first = 0,
+    int t_nblk = 1, int64_t t_ostride = 0) {
   if (gate && ((*gate != 0.f) != (gate_on != 0))) return;  // the FmtH2 range guard (nn_x3_kernel)
   using F = FmtH2;
   using V8 = F::V8;
@@ -84,7 +85,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int64_t by = DS == 2 ? lin / gridDim.z
                    : DS == 1 ? (int64_t)gridDim.y - 1 - lin / gridDim.z : blockIdx.y;
   const int64_t bz = (DS == 1 || DS == 2) ? lin % gridDim.z : blockIdx.z;
-  const int64_t i0 = by * PhiW1::BM;
+  // DS 3 batched over several column blocks of D (t_per > 0: t_per row
+  // blocks of output per part; part q is D's column block (t_first + q) mod
+  // t_nblk, its output t_ostride floats after part q - 1's)
+  const bool tb = DS == 3 && t_per > 0;
+  const int64_t tpart = tb ? by / t_per : 0;
+  const int64_t byl = tb ? by % t_per : by;
+  const int64_t i0 = byl * PhiW1::BM;
   const int64_t c0 = (int64_t)blockIdx.x * PhiW1::BC + w * 128;
   // K-step k of this block is global K-step ks0 + kdir * k.  The symmetric
   // forms interleave the slices, slice z taking every Z-th K-step of its
@@ -109,8 +116,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     ks0 = (int)bz;
     nsteps = T > bz ? (T - (int)bz + Z - 1) / Z : 0;
   }
-  C += (int64_t)(slice0 + bz) * m * ldc;
-  rowsum += (int64_t)(slice0 + bz) * roundup128(m);
+  C += (int64_t)(slice0 + bz) * m * ldc + tpart * t_ostride;
+  rowsum += (int64_t)(slice0 + bz) * roundup128(m) + tpart * t_ostride;
   const float scale = -st->inv_h * kLog2e;
 
   // D: the block's panel row; thread t stages row t >> 1, columns 8 (t & 1) .. +7
@@ -140,7 +147,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   // symmetric layout (m == n, row0 == 0): K-steps left of the block's
   // diagonal tile (DS 1) read the stored tile (J, I) transposed
-  const int symI = DS == 3 ? tcol0 + (int)by : sym ? (int)(i0 >> 7) : -1;
+  const int symI = tb ? (int)(((t_first + tpart) % t_nblk) * t_per + byl)
+                   : DS == 3 ? tcol0 + (int)by : sym ? (int)(i0 >> 7) : -1;
   const int64_t pcols = a_npad >> 4;
   // DS 1: lane (piece p = t >> 5, s = t & 31) loads rows i0 + 16 p + 8 (s & 1)
   // .. +7 of column j0 + (s >> 1): 32 contiguous bytes of panel I*8 + p

@@ -586,6 +586,13 @@ class PhiEngine(object):
         # partials: one message per peer = [mo x ldy | roundup128(mo)] floats
         def msg(rows):
             return torch.empty(rows * ldy + lib.dsvgd_pad128(rows), **f32)
+        # the forward blocks' partials in ONE launch without split-K when
+        # they fill most of the CUs (S >= 8: 3 x 64 workgroups of 512
+        # K-steps), written straight into one contiguous message buffer
+        nf = len(P.forward)
+        self.fwd_msg = self.m * ldy + lib.dsvgd_pad128(self.m)
+        self.fwd_batched = nf > 0 and nf * (self.m // 128) * (ldy // 512) >= 192
+        self.send_fwd = torch.empty(max(1, nf) * self.fwd_msg, **f32) if self.fwd_batched else None
         self.t_splits = []
         smax = 0
         for q in P.sends:
@@ -596,6 +603,9 @@ class PhiEngine(object):
             self.t_splits.append(z)
             smax = max(smax, z * q["mo"]) if z > 1 else smax
         self.sendbuf = [msg(q["mo"]) for q in P.sends]
+        if self.fwd_batched:   # the forward messages as views of the one buffer
+            for k in range(nf):
+                self.sendbuf[k] = self.send_fwd[k * self.fwd_msg:(k + 1) * self.fwd_msg]
         self.recvbuf = [msg(q["rows"]) for q in P.recvs]
         mo_max = max([q["mo"] for q in P.sends] + [128])
         self.tP = torch.empty(max(smax, 1), ldy, **f32)
@@ -633,7 +643,13 @@ class PhiEngine(object):
             N.call("dsvgd_h2_ysplit", N.ptr(self.Y), ldy, self.n_pad, N.ptr(self.yscale),
                    N.ptr(self.Yx), s)
         with span(self.timer, "phi_partials"):
-            for q, z, buf in zip(P.sends, self.t_splits, self.sendbuf):
+            nf = len(P.forward) if self.fwd_batched else 0
+            if nf:
+                N.call("dsvgd_phi_h2_transposed_blocks", N.ptr(self.D), self.n_pad,
+                       N.ptr(self.Yx), ldy, self.row0, self.m, (P.rank + 1) % P.S, P.S, nf,
+                       self.n, self.state.ptr, N.ptr(self.send_fwd), ldy, self.fwd_msg, colinv,
+                       guard, 0, s)
+            for q, z, buf in list(zip(P.sends, self.t_splits, self.sendbuf))[nf:]:
                 Dq = N.ptr(self.D) + 4 * q["row_off"] * self.n_pad
                 mo = q["mo"]
                 rs_out = N.ptr(buf) + 4 * mo * ldy

@@ -426,6 +426,15 @@ int dsvgd_phi_h2_transposed(const float* D, int64_t ldd, const void* Yh, int64_t
                             const dsvgd_select_state* st, int64_t splits, float* P, int64_t ldp,
                             float* rs, const float* colinv, const float* gate, int gate_on,
                             void* stream);
+/* dsvgd_phi_h2_transposed for `count` whole m x m blocks of the owned rows'
+ * D in one launch, no split-K: block q (< count) is D's column block (first +
+ * q) mod nblocks (the forward blocks of a rank), its partial [m x ldp | m row
+ * sums] written at P + q pstride. */
+int dsvgd_phi_h2_transposed_blocks(const float* D, int64_t ldd, const void* Yh, int64_t ldy,
+                                   int64_t yrow0, int64_t m, int64_t first, int64_t nblocks,
+                                   int64_t count, int64_t n, const dsvgd_select_state* st,
+                                   float* P, int64_t ldp, int64_t pstride, const float* colinv,
+                                   const float* gate, int gate_on, void* stream);
 /* out[i][c] = sum_z P[z][i][c] (c < cols) and out_rs[i] = sum_z rs[z][i], in
  * slice order (the P / rs layout of dsvgd_phi_h2_transposed). */
 int dsvgd_phi_partial_reduce(const float* P, int64_t ldp, const float* rs, int64_t splits,
