@@ -306,25 +306,131 @@ __global__ void gs_mask_kernel(float* __restrict__ D, int64_t ldd, int64_t r0, i
 }
 
 // One workgroup of 256 threads walks rows [r0, r0 + B).  Q: [K Xc | K S] of
-// the wide pass (ldq >= 2 dp), Qr its row sums; Y: [X - c | S] (updated for
-// each moved row, with norms[]), centre c = the Y packing centre.
+// the wide pass (ldq >= 2 dp), Qr its row sums; Y: [X - c | S] (rewritten for
+// the moved rows, with norms[], at the block's end), centre c = the Y
+// packing centre.
 // Per row two barriers: (1) after the distance partials, (2) after the moved
 // row's LDS writes.  Every wave forms the row's kernel values itself (lane j:
 // k(x_i, x_j'), its moved-row sum by a wave reduction) and the column loop
-// broadcasts them with v_readlane; the next row's global operands (Q, Qr,
-// its old x and s, X) are loaded one row ahead into registers, so no row
-// waits on memory.
+// broadcasts them with v_readlane.  The next row's global operands (Q, Qr,
+// its old x and s, the extra row) are loaded one row ahead into registers,
+// and NO global store is issued inside the row loop (X, S, Y and the norms
+// of the moved rows go out from LDS after it): vmcnt counts loads and stores
+// in order, so a store of row i made the loop-head wait for row i + 1's
+// operands also wait for it (~2.7 us per row, r11e).  phi_out (tests only) is
+// the one in-loop store.
 constexpr int kGswCols = kGswMaxD / 256;  // columns per thread
-
 // LDS hand-offs only: wait for this wave's LDS operations, then s_barrier.
-// (__syncthreads() also drains every global load and store -- the next
-// row's prefetch included -- which cost ~2.7 us per row, r11d.)  No global
-// location the walk writes is read inside it by another thread.
+// No global location the walk writes is read inside it by another thread.
 __device__ __forceinline__ void gsw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
+
+constexpr int kGswCoef = 4096;            // logreg refresh: the waves' partials [4][dp]
+
+// The logistic regression score of the moved row x' (logreg_small_kernel's
+// terms: s_0 = -a + p/2 - a/2 |w|^2, s_w = sum_q t_q sigma(-t_q xd_q . w) xd_q
+// - a w, times scale) in ONE pass over the rank's nd data rows: every wave
+// holds w in the dwordx4 lane layout (lane: w[256 v + 4 lane .. + 3]), takes
+// R = 16 / NV rows per batch (one dwordx4 load per row and 256 features,
+// the next batch in flight while this one is reduced: 32 loads per wave),
+// forms z_q by an interleaved wave reduction, and adds t_q sigma(-t_q z_q)
+// xd_q into register partials from the SAME loaded values; the four waves'
+// partials meet in LDS.  A single workgroup streams the data at the rate
+// its loads in flight allow (~128 KiB), so rows are 16-byte aligned
+// (ldxd % 4 == 0, the caller's padded copy).
+template <int NV>
+__device__ __forceinline__ void gsw_logreg_refresh(
+    const float* xr, float cla, const float (&cw)[kGswMaxD / 64], const float* __restrict__ xd,
+    int64_t ldxd, const float* __restrict__ td, int nd, float* red, int dp, float scale, int d,
+    float* snrow, const float (&cen)[kGswCols]) {
+  constexpr int R = 16 / NV;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int p = d - 1;
+  const float a = expf(xr[0] + cla);
+  float wv[NV][4], g[NV][4];
+  float w2 = 0.f;
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = 256 * v + 4 * lane + k;
+      wv[v][k] = c < p ? xr[1 + c] + cw[4 * v + k] : 0.f;
+      w2 = fmaf(wv[v][k], wv[v][k], w2);
+      g[v][k] = 0.f;
+    }
+  for (int o = 32; o > 0; o >>= 1) w2 += __shfl_xor(w2, o, 64);
+  // wave w's batches: rows [4 R it + R w, + R), it = 0, 1, ...
+  const int nb = (nd + 4 * R - 1) / (4 * R);
+  f32x4 buf[2][R][NV];
+  float tb[2][R];
+  auto load = [&](f32x4 (&bb)[R][NV], float (&tt)[R], int it) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int q = min(4 * R * it + R * w + r, nd - 1);
+      const float* xq = xd + (int64_t)q * ldxd + 4 * lane;
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+        bb[r][v] = (256 * v + 4 * lane < p) ? *reinterpret_cast<const f32x4*>(xq + 256 * v)
+                                            : f32x4{0.f, 0.f, 0.f, 0.f};
+      tt[r] = td[q];
+    }
+  };
+  auto use = [&](const f32x4 (&bb)[R][NV], const float (&tt)[R], int it) {
+    float z[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        s0 = fmaf(bb[r][v][0], wv[v][0], fmaf(bb[r][v][2], wv[v][2], s0));
+        s1 = fmaf(bb[r][v][1], wv[v][1], fmaf(bb[r][v][3], wv[v][3], s1));
+      }
+      z[r] = s0 + s1;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int r = 0; r < R; ++r) z[r] += __shfl_xor(z[r], o, 64);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool ok = 4 * R * it + R * w + r < nd;
+      const float cf = ok ? tt[r] / (1.f + expf(tt[r] * z[r])) : 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g[v][k] = fmaf(cf, bb[r][v][k], g[v][k]);
+    }
+  };
+  if (nb > 0) load(buf[0], tb[0], 0);
+  for (int it = 0; it < nb; it += 2) {
+    if (it + 1 < nb) load(buf[1], tb[1], it + 1);
+    use(buf[0], tb[0], it);
+    if (it + 1 >= nb) break;
+    if (it + 2 < nb) load(buf[0], tb[0], it + 2);
+    use(buf[1], tb[1], it + 1);
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+    if (256 * v + 4 * lane < p)
+      *reinterpret_cast<f32x4*>(red + w * dp + 256 * v + 4 * lane) =
+          f32x4{g[v][0], g[v][1], g[v][2], g[v][3]};
+  gsw_barrier();
+#pragma unroll
+  for (int u = 0; u < kGswCols; ++u) {
+    const int c = t + 256 * u;
+    if (c >= d) continue;
+    if (c == 0) {
+      snrow[0] = scale * (-a + 0.5f * (float)p - 0.5f * a * w2);
+    } else {
+      const float gs = (red[c - 1] + red[dp + c - 1]) + (red[2 * dp + c - 1] + red[3 * dp + c - 1]);
+      snrow[c] = scale * (gs - a * (xr[c] + cen[u]));
+    }
+  }
+}
+
 
 __global__ __launch_bounds__(256) void gsw_sweep_kernel(
     float* __restrict__ X, int64_t ldx, float* __restrict__ S, int64_t lds, float* __restrict__ Y,
@@ -333,13 +439,15 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
     const float* __restrict__ Q, int64_t ldq, const float* __restrict__ Qr,
     const float* __restrict__ extra, int64_t lde, float* __restrict__ phi_out, int64_t ldphi,
     int score_kind, const float* __restrict__ mu, const float* __restrict__ lam,
-    float score_scale) {
+    float score_scale, const float* __restrict__ xd, int64_t ldxd, const float* __restrict__ td,
+    int nd) {
   extern __shared__ __attribute__((aligned(16))) float gsw_smem[];
   const int pitch = dp + 4;                       // 16-byte rows, 4 banks apart
   float* xn = gsw_smem;                           // [B][pitch]: moved rows, centred
-  float* wn = xn + (int64_t)B * pitch;            // [B][dp]: s' - g (x' - c)
-  float* xo = wn + (int64_t)B * dp;               // [2][dp]: the row being moved (old, centred)
+  float* sn = xn + (int64_t)B * pitch;            // [B][dp]: their scores
+  float* xo = sn + (int64_t)B * dp;               // [2][dp]: the row being moved (old, centred)
   float* part = xo + 2 * dp;                      // [4][64] partial distances
+  float* coef = part + 256;                       // [kGswCoef] logreg: t_q sigma(-t_q z_q)
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const float inv_h = st->inv_h, g = 2.f * inv_h, scale = -inv_h * kLog2e;
   const float inv_n = 1.f / (float)n;
@@ -347,7 +455,7 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
   for (int e = t; e < B * pitch; e += 256) xn[e] = 0.f;
   // per-thread columns c = t + 256 u, u < kGswCols, and the next row's operands
   float cen[kGswCols], mu_c[kGswCols], lam_c[kGswCols];
-  float nq_x[kGswCols], nq_s[kGswCols], n_xo[kGswCols], n_so[kGswCols], n_x[kGswCols];
+  float nq_x[kGswCols], nq_s[kGswCols], n_xo[kGswCols], n_so[kGswCols], n_ex[kGswCols];
   float nqr = 0.f;
   auto prefetch = [&](int i) {  // row i's operands (i < B)
     const int64_t gi = r0 + i;
@@ -359,7 +467,7 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
       nq_s[u] = ok ? Q[i * ldq + dp + c] : 0.f;
       n_xo[u] = c < dp ? Y[gi * ldy + c] : 0.f;
       n_so[u] = ok ? Y[gi * ldy + dp + c] : 0.f;
-      n_x[u] = ok ? X[gi * ldx + c] : 0.f;
+      n_ex[u] = (ok && extra) ? extra[(int64_t)i * lde + c] : 0.f;
     }
     nqr = Qr[i];
   };
@@ -370,21 +478,31 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
     mu_c[u] = (score_kind == 1 && c < d) ? mu[c] : 0.f;
     lam_c[u] = (score_kind == 1 && c < d) ? lam[c] : 0.f;
   }
+  // logreg (score_kind 3): the centre of log alpha and of this lane's
+  // weights w[c], c = lane + 64 v
+  const float cla = score_kind == 3 ? center[0] : 0.f;
+  float cw[kGswMaxD / 64];   // w[256 v + 4 lane + k] at cw[4 v + k]
+#pragma unroll
+  for (int v = 0; v < kGswMaxD / 256; ++v)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = 256 * v + 4 * lane + k;
+      cw[4 * v + k] = (score_kind == 3 && c + 1 < d) ? center[1 + c] : 0.f;
+    }
   prefetch(0);
 #pragma unroll
   for (int u = 0; u < kGswCols; ++u)
     if (t + 256 * u < dp) xo[t + 256 * u] = n_xo[u];
   __syncthreads();
   for (int i = 0; i < B; ++i) {
-    const int64_t gi = r0 + i;
-    float q_x[kGswCols], q_s[kGswCols], xc_o[kGswCols], s_o[kGswCols], x_o[kGswCols];
+    float q_x[kGswCols], q_s[kGswCols], xc_o[kGswCols], s_o[kGswCols], ex[kGswCols];
 #pragma unroll
     for (int u = 0; u < kGswCols; ++u) {
       q_x[u] = nq_x[u];
       q_s[u] = nq_s[u];
       xc_o[u] = n_xo[u];
       s_o[u] = n_so[u];
-      x_o[u] = n_x[u];
+      ex[u] = n_ex[u];
     }
     const float qr = nqr;
     if (i + 1 < B) prefetch(i + 1);
@@ -412,40 +530,39 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
     const float kj = lane < i ? __builtin_amdgcn_exp2f(dd * scale) : 0.f;
     float rm = kj;
     for (int o = 32; o > 0; o >>= 1) rm += __shfl_xor(rm, o, 64);
-    const float rtot = qr + rm;
     // (b) per column: the wide pass + the moved rows' terms + the self term
 #pragma unroll
     for (int u = 0; u < kGswCols; ++u) {
       const int c = t + 256 * u;
       if (c >= d) continue;
-      float acc0 = 0.f, acc1 = 0.f;
+      float as0 = 0.f, as1 = 0.f, ax0 = 0.f, ax1 = 0.f;
       int j = 0;
       for (; j + 2 <= i; j += 2) {
         const float k0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kj), j));
         const float k1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kj), j + 1));
-        acc0 = fmaf(k0, wn[j * dp + c], acc0);
-        acc1 = fmaf(k1, wn[(j + 1) * dp + c], acc1);
+        as0 = fmaf(k0, sn[j * dp + c], as0);
+        ax0 = fmaf(k0, xn[j * pitch + c], ax0);
+        as1 = fmaf(k1, sn[(j + 1) * dp + c], as1);
+        ax1 = fmaf(k1, xn[(j + 1) * pitch + c], ax1);
       }
       if (j < i) {
         const float k0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kj), j));
-        acc0 = fmaf(k0, wn[j * dp + c], acc0);
+        as0 = fmaf(k0, sn[j * dp + c], as0);
+        ax0 = fmaf(k0, xn[j * pitch + c], ax0);
       }
-      // + the self term k_ii s_i (the wide pass skipped the diagonal)
-      float p = inv_n * (((q_s[u] + s_o[u]) - g * q_x[u]) + (acc0 + acc1) + g * rtot * xc_o[u]);
-      if (extra) p += extra[(int64_t)i * lde + c];
+      // sum_{j<i} k_j (s_j' + g (x_i - x_j')), centred; + the self term s_i
+      // (the wide pass skipped the diagonal) + the wide pass's terms
+      const float rtot = qr + rm;
+      float p = inv_n * (((q_s[u] + s_o[u]) - g * q_x[u]) + (as0 + as1) +
+                         g * (rtot * xc_o[u] - (ax0 + ax1)));
+      p += ex[u];
       if (phi_out) phi_out[(int64_t)i * ldphi + c] = p;
-      const float x = x_o[u] + step * p;
-      X[gi * ldx + c] = x;
+      const float x = (xc_o[u] + cen[u]) + step * p;
       float sv = s_o[u];
-      if (score_kind != 0) {
+      if (score_kind == 1 || score_kind == 2)
         sv = gs_score(score_kind, x, mu_c[u], lam_c[u], score_scale);
-        S[gi * lds + c] = sv;
-      }
-      const float xcn = x - cen[u];
-      xn[i * pitch + c] = xcn;
-      wn[i * dp + c] = sv - g * xcn;
-      Y[gi * ldy + c] = xcn;
-      Y[gi * ldy + dp + c] = sv;
+      xn[i * pitch + c] = x - cen[u];
+      if (score_kind != 3) sn[i * dp + c] = sv;
     }
     // the next row's old values into the other xo buffer
     if (i + 1 < B) {
@@ -454,8 +571,37 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
         if (t + 256 * u < dp) xo[((i + 1) & 1) * dp + t + 256 * u] = n_xo[u];
     }
     gsw_barrier();                                                          // (2)
+    if (score_kind == 3) {
+      // the moved row's logreg score on the rank's data, in one pass over it
+      const float* xr = xn + i * pitch;
+      const int nv4 = (d - 1 + 255) >> 8;   // 256-feature groups (1 .. 4)
+      if (nv4 == 1)
+        gsw_logreg_refresh<1>(xr, cla, cw, xd, ldxd, td, nd, coef, dp, score_scale, d,
+                              sn + i * dp, cen);
+      else if (nv4 == 2)
+        gsw_logreg_refresh<2>(xr, cla, cw, xd, ldxd, td, nd, coef, dp, score_scale, d,
+                              sn + i * dp, cen);
+      else if (nv4 == 3)
+        gsw_logreg_refresh<3>(xr, cla, cw, xd, ldxd, td, nd, coef, dp, score_scale, d,
+                              sn + i * dp, cen);
+      else
+        gsw_logreg_refresh<4>(xr, cla, cw, xd, ldxd, td, nd, coef, dp, score_scale, d,
+                              sn + i * dp, cen);
+      // sn[i] is read after the next row's barrier (1); the partials' LDS is
+      // rewritten only after it
+    }
   }
-  // the moved rows' norms |x' - c|^2 (the later blocks' distances)
+  // the moved rows out: X (= the centred row + c), the refreshed scores, Y's
+  // row [x' - c | s'] and its norm |x' - c|^2 (the later blocks' distances)
+  for (int e = t; e < B * d; e += 256) {
+    const int i = e / d, c = e % d;
+    const int64_t gi = r0 + i;
+    const float xc = xn[i * pitch + c], sv = sn[i * dp + c];
+    X[gi * ldx + c] = xc + center[c];
+    if (score_kind != 0) S[gi * lds + c] = sv;
+    Y[gi * ldy + c] = xc;
+    Y[gi * ldy + dp + c] = sv;
+  }
   for (int i = w; i < B; i += 4) {
     float s2 = 0.f;
     for (int c = lane; c < d; c += 64) {
@@ -537,24 +683,32 @@ int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y
                           int64_t B, const dsvgd_select_state* st, float step, const float* Q,
                           int64_t ldq, const float* Qr, const float* extra, int64_t lde,
                           float* phi_out, int64_t ldphi, int score_kind, const float* mu,
-                          const float* lam, float score_scale, void* stream) {
+                          const float* lam, float score_scale, const float* xd, int64_t ldxd,
+                          const float* td, int64_t nd, void* stream) {
   DSVGD_REQUIRE(X && S && Y && norms && center && st && Q && Qr, "null pointer");
   const int64_t dp = roundup(d, 32);
   DSVGD_REQUIRE(n > 0 && d > 0 && d <= kGswMaxD && ldx >= d && lds >= d && ldy >= 2 * dp &&
                     ldq >= 2 * dp,
                 "sizes (d <= 1024, ldy and ldq >= 2 roundup(d, 32))");
   DSVGD_REQUIRE(B > 0 && B <= gsw_rows(dp) && r0 >= 0 && r0 + B <= n, "block rows");
-  DSVGD_REQUIRE(score_kind >= 0 && score_kind <= 2, "score_kind must be 0, 1 or 2");
+  DSVGD_REQUIRE(score_kind >= 0 && score_kind <= 3, "score_kind must be 0, 1, 2 or 3");
   DSVGD_REQUIRE(score_kind != 1 || (mu && lam), "Gaussian scores need mu and lam");
+  DSVGD_REQUIRE(score_kind != 3 || (xd && td && d >= 2 && ldxd >= d - 1 && nd > 0 &&
+                                    nd < ((int64_t)1 << 31)),
+                "logreg scores need the data (nd rows of d - 1 features) and the labels");
+  DSVGD_REQUIRE(score_kind != 3 || (ldxd % 4 == 0 && ((uintptr_t)xd & 15) == 0),
+                "logreg data rows must be 16-byte aligned (ldxd % 4 == 0)");
   DSVGD_REQUIRE(!extra || lde >= d, "lde");
   DSVGD_REQUIRE(!phi_out || ldphi >= d, "ldphi");
-  const size_t smem = sizeof(float) * ((size_t)B * (dp + 4) + (size_t)B * dp + 2 * dp + 256);
+  const size_t smem = sizeof(float) * ((size_t)B * (dp + 4) + (size_t)B * dp + 2 * dp + 256 +
+                                       (score_kind == 3 ? kGswCoef : 0));
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gsw_sweep_kernel),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
     return fail_arg("gsw_sweep: cannot reserve the walk's LDS");
   hipLaunchKernelGGL(gsw_sweep_kernel, dim3(1), dim3(256), smem, (hipStream_t)stream, X, ldx, S,
                      lds, Y, ldy, norms, center, n, (int)d, (int)dp, r0, (int)B, st, step, Q, ldq,
-                     Qr, extra, lde, phi_out, ldphi, score_kind, mu, lam, score_scale);
+                     Qr, extra, lde, phi_out, ldphi, score_kind, mu, lam, score_scale, xd, ldxd,
+                     td, (int)(score_kind == 3 ? nd : 0));
   return check_launch("gsw_sweep");
 }
 

@@ -406,24 +406,68 @@ __device__ __forceinline__ void wave_best(double cv, int cj, int u, int lane, do
 // A phase ends with long runs of rounds in which a handful of slots bid
 // (profiles/r8j: 17k of the 19k rounds of a warm m = 8192, n = 65536 solve
 // had <= 16 unassigned slots), each round two launches.  Once the unassigned
-// count is <= kTailMax, block 0 of the bid launch runs the rest of the phase
-// itself: the unassigned slots (found by a scan, sorted: deterministic) bid
-// one at a time -- the u = 1 bid of the parallel rounds, from the row's price
-// cache or a workgroup scan -- and each bid is resolved on the spot (a
+// count is <= kTailMax, the one-workgroup tail launch (queued every round,
+// a no-op otherwise; the bid launch is then the no-op) runs the rest of the
+// phase itself: the unassigned slots (found by a scan, sorted: deterministic)
+// bid one at a time -- the u = 1 bid of the parallel rounds, from the row's
+// price cache or a workgroup scan -- and each bid is resolved on the spot (a
 // displaced slot goes back on the stack).  The same eps-complementary-
 // slackness invariant as the Jacobi rounds, so the phase ends eps-optimal;
 // the resolve launch behind it then runs the control step.  At most
 // kTailBids bids per launch (the next round's launch continues).
+//
+// A tail bid is a chain of dependent reads (the row's cache, its columns'
+// prices and holders, the won column's holder and owner): ~5 L2 round trips
+// when they go to global memory.  The tail is the only writer while it runs,
+// so it keeps direct-mapped LDS tables of the columns and rows it touches,
+// written through to global memory on every update (the scans and the next
+// launch read global memory, which is therefore always current): a price war
+// over a few columns then runs out of LDS.
 constexpr int kTailMax = 64;
-constexpr int kTailBids = 4096;
+constexpr int kTailBids = 16384;
+constexpr int kTabCols = 4096;  // column entries: price, holder, owner, tag
+constexpr int kTabRows = 256;   // row entries: the price cache of a row
+constexpr size_t kTailLds =
+    (size_t)kTabCols * (8 + 4 + 4 + 4) + (size_t)kTabRows * (8 + 4 + 4 + kCache * 8);
 
-template <int K>
-__device__ void w2_tail(const float* __restrict__ C, int64_t ldc, int64_t n, int64_t R, W2Ws w,
-                        int ep, double eps, uint32_t tag, bool cached, double* sv, int* sj,
-                        double* outv, int* outj) {
+struct TailTab {
+  double* cp;
+  int32_t *ct, *co;
+  uint32_t* ch;
+  double* rb;
+  int32_t *rt, *rv, *rc;
+  float* rx;
+  __device__ explicit TailTab(char* base) {
+    cp = (double*)base;
+    rb = cp + kTabCols;
+    ct = (int32_t*)(rb + kTabRows);
+    co = ct + kTabCols;
+    ch = (uint32_t*)(co + kTabCols);
+    rt = (int32_t*)(ch + kTabCols);
+    rv = rt + kTabRows;
+    rc = rv + kTabRows;
+    rx = (float*)(rc + kTabRows * kCache);
+  }
+};
+
+template <int K, bool CACHED>
+__global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ C, int64_t ldc,
+                                                      int64_t n, int64_t R, W2Ws w) {
+  extern __shared__ __attribute__((aligned(16))) char w2_tail_lds[];
+  constexpr int KS = CACHED ? kCache + 1 : K;  // the scans' list length
+  __shared__ double sv[4 * KS], outv[KS];
+  __shared__ int sj[4 * KS], outj[KS];
   __shared__ int stack[kTailMax], sorted[kTailMax];
-  __shared__ int sp, cnt;
+  __shared__ int sp, cnt, hit;
+  const W2Ctl* ctl = w.ctl;
+  if (ctl->done || ctl->unassigned > (unsigned long long)kTailMax) return;  // uniform
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int ep = ctl->epoch;
+  const double eps = ctl->eps;
+  const uint32_t tag = w2_tag(ep);
+  TailTab T(w2_tail_lds);
+  for (int e = t; e < kTabCols; e += 256) T.ct[e] = -1;
+  for (int e = t; e < kTabRows; e += 256) T.rt[e] = -1;
   if (t == 0) cnt = 0;
   __syncthreads();
   for (int64_t s0 = t; s0 < n; s0 += 256)
@@ -450,50 +494,91 @@ __device__ void w2_tail(const float* __restrict__ C, int64_t ldc, int64_t n, int
     const int64_t i = s / R;
     const uint32_t mine = tag | (uint32_t)i;
     const float* row = C + i * ldc;
-    double v1 = -DBL_MAX, v2 = -DBL_MAX;
-    int j1 = INT32_MAX;
-    bool have = false;
-    if (cached && w.cvalid[i]) {  // block-uniform: wave 0 tries the cache
-      if (wv == 0) {
-        double cv = -DBL_MAX;
-        int cj = INT32_MAX;
-        if (lane < kCache) {
-          const int c = w.ccol[i * kCache + lane];
-          if (c != INT32_MAX && w.holder[c] != mine) {
-            cj = c;
-            cv = -(double)w.ccost[i * kCache + lane] - w.price[c];
+    if (CACHED) {
+      if (wv == 0) {  // the row's cache (table, else global + install), its bid
+        const int re = (int)(i & (kTabRows - 1));
+        int valid, c = INT32_MAX;
+        float cc = 0.f;
+        double bound;
+        if (T.rt[re] == (int)i) {
+          valid = T.rv[re];
+          bound = T.rb[re];
+          if (lane < kCache) {
+            c = T.rc[re * kCache + lane];
+            cc = T.rx[re * kCache + lane];
+          }
+        } else {
+          valid = w.cvalid[i];
+          bound = w.cbound[i];
+          if (lane < kCache) {
+            c = w.ccol[i * kCache + lane];
+            cc = w.ccost[i * kCache + lane];
+            T.rc[re * kCache + lane] = c;
+            T.rx[re * kCache + lane] = cc;
+          }
+          if (lane == 0) {
+            T.rt[re] = (int)i;
+            T.rv[re] = valid;
+            T.rb[re] = bound;
           }
         }
-        double kv;
-        int kj;
-        wave_best(cv, cj, 1, lane, kv, kj);
-        const double b1 = __shfl(kv, 0, 64), b2 = __shfl(kv, 1, 64);
-        const int bj = __shfl(kj, 0, 64);
-        if (lane == 0) {
-          outv[0] = b1;
-          outv[1] = b2;
-          outj[0] = bj;
-          sp = (b2 >= w.cbound[i]) ? -top : top;  // the sign carries the hit
+        bool h1 = false;
+        if (valid) {
+          double cv = -DBL_MAX;
+          int cj = INT32_MAX;
+          if (lane < kCache && c != INT32_MAX) {
+            const int e = c & (kTabCols - 1);
+            double p;
+            uint32_t hd;
+            if (T.ct[e] == c) {
+              p = T.cp[e];
+              hd = T.ch[e];
+            } else {
+              p = w.price[c];
+              hd = w.holder[c];
+            }
+            if (hd != mine) {  // held columns never bid
+              cj = c;
+              cv = -(double)cc - p;
+            }
+          }
+          double kv;
+          int kj;
+          wave_best(cv, cj, 1, lane, kv, kj);
+          const double b1 = __shfl(kv, 0, 64), b2 = __shfl(kv, 1, 64);
+          const int bj = __shfl(kj, 0, 64);
+          h1 = b2 >= bound;
+          if (lane == 0) {
+            outv[0] = b1;
+            outv[1] = b2;
+            outj[0] = bj;
+          }
         }
+        if (lane == 0) hit = h1;
       }
       __syncthreads();
-      have = sp < 0;
-      __syncthreads();
-      if (t == 0 && have) sp = top;
-      __syncthreads();
-    }
-    if (!have) {
-      if (cached) {  // full scan over all columns, refill the cache
+      if (!hit) {  // full scan over all columns, refill the cache (global + table)
         block_topk<kCache + 1>(row, n, w, mine, false, sv, sj, outv, outj);
         if (wv == 0) {
+          const int re = (int)(i & (kTabRows - 1));
           const double ev = lane < kCache + 1 ? outv[lane] : -DBL_MAX;
           const int ej = lane < kCache + 1 ? outj[lane] : INT32_MAX;
           if (lane < kCache) {
+            const float cc = ej != INT32_MAX ? row[ej] : 0.f;
             w.ccol[i * kCache + lane] = ej;
-            w.ccost[i * kCache + lane] = ej != INT32_MAX ? row[ej] : 0.f;
+            w.ccost[i * kCache + lane] = cc;
+            T.rc[re * kCache + lane] = ej;
+            T.rx[re * kCache + lane] = cc;
           }
-          if (lane == kCache) w.cbound[i] = ev;
-          if (lane == 0) w.cvalid[i] = 1;
+          if (lane == kCache) {
+            w.cbound[i] = ev;
+            T.rb[re] = ev;
+          }
+          if (lane == 0) {
+            w.cvalid[i] = 1;
+            T.rv[re] = 1;
+            T.rt[re] = (int)i;
+          }
           double cv = -DBL_MAX;
           int cj = INT32_MAX;
           if (lane < kCache && ej != INT32_MAX && w.holder[ej] != mine) {
@@ -511,14 +596,13 @@ __device__ void w2_tail(const float* __restrict__ C, int64_t ldc, int64_t n, int
             outj[0] = bj;
           }
         }
-      } else {
-        block_topk<K>(row, n, w, mine, true, sv, sj, outv, outj);
+        __syncthreads();
       }
-      __syncthreads();
+    } else {
+      block_topk<K>(row, n, w, mine, true, sv, sj, outv, outj);
     }
-    v1 = outv[0];
-    v2 = outv[1];
-    j1 = outj[0];
+    const double v1 = outv[0], v2 = outv[1];
+    const int j1 = outj[0];
     if (t == 0) {
       int next = top - 1;
       if (j1 != INT32_MAX) {
@@ -527,17 +611,34 @@ __device__ void w2_tail(const float* __restrict__ C, int64_t ldc, int64_t n, int
         float f = (float)inc;
         if ((double)f > inc) f = nextafterf(f, 0.f);  // round down: keeps eps-CS
         if (!(f > 0.f)) f = FLT_MIN;
-        w.price[j1] += (double)f;
-        const uint32_t h = w.holder[j1];
-        const int old = ((h & ~(uint32_t)(kMaxRows - 1)) == tag) ? w.owner[j1] : -1;
+        const int e = j1 & (kTabCols - 1);
+        double p;
+        uint32_t h;
+        int own;
+        if (T.ct[e] == j1) {
+          p = T.cp[e];
+          h = T.ch[e];
+          own = T.co[e];
+        } else {
+          p = w.price[j1];
+          h = w.holder[j1];
+          own = w.owner[j1];
+        }
+        p += (double)f;
+        const int old = ((h & ~(uint32_t)(kMaxRows - 1)) == tag) ? own : -1;
         if (old >= 0) {
           w.assigned[old] = -1;  // displaced: bids next
           stack[next++] = old;
         } else {
           atomicAdd(&w.ctl->unassigned, (unsigned long long)(-1ll));
         }
+        T.ct[e] = j1;
+        T.cp[e] = p;
+        T.ch[e] = mine;
+        T.co[e] = s;
+        w.price[j1] = p;
         w.owner[j1] = s;
-        w.holder[j1] = tag | (uint32_t)i;
+        w.holder[j1] = mine;
         w.assigned[s] = j1;
         w.assigned_ep[s] = ep;
       }
@@ -565,10 +666,7 @@ __global__ __launch_bounds__(256) void w2_bid_cached_kernel(const float* __restr
   const int ep = ctl->epoch;
   const double eps = ctl->eps;
   const uint32_t tag = w2_tag(ep);
-  if (ctl->unassigned <= (unsigned long long)kTailMax) {  // the phase tail (uniform)
-    if (blockIdx.x == 0) w2_tail<2>(C, ldc, n, R, w, ep, eps, tag, true, sv, sj, outv, outj);
-    return;
-  }
+  if (ctl->unassigned <= (unsigned long long)kTailMax) return;  // the tail launch's (uniform)
   for (int64_t base = (int64_t)blockIdx.x * 4; base < m; base += (int64_t)gridDim.x * 4) {
     const int64_t i = base + wv;
     unsigned long long free = 0;
@@ -653,10 +751,7 @@ __global__ __launch_bounds__(256) void w2_bid_kernel(const float* __restrict__ C
   const int ep = ctl->epoch;
   const double eps = ctl->eps;
   const uint32_t tag = w2_tag(ep);
-  if (ctl->unassigned <= (unsigned long long)kTailMax) {  // the phase tail (uniform)
-    if (blockIdx.x == 0) w2_tail<K>(C, ldc, n, R, w, ep, eps, tag, false, sv, sj, outv, outj);
-    return;
-  }
+  if (ctl->unassigned <= (unsigned long long)kTailMax) return;  // the tail launch's (uniform)
   for (int64_t base = (int64_t)blockIdx.x * 4; base < m; base += (int64_t)gridDim.x * 4) {
     const int64_t i = base + wv;
     unsigned long long free = 0;
@@ -858,23 +953,44 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
   int rc = check_launch("w2_start");
   if (rc) return rc;
   const dim3 gb((unsigned)std::min<int64_t>(kBidBlocks, (m + 3) / 4));
+  // the phase tail: one workgroup, its LDS tables as dynamic LDS
+  const bool cached = kW2Cache && R >= 2 && R <= kCacheMaxR;
+  const void* tail_fn = cached ? reinterpret_cast<const void*>(&w2_tail_kernel<2, true>)
+                      : R <= 1 ? reinterpret_cast<const void*>(&w2_tail_kernel<2, false>)
+                      : R <= 2 ? reinterpret_cast<const void*>(&w2_tail_kernel<3, false>)
+                      : R <= 4 ? reinterpret_cast<const void*>(&w2_tail_kernel<5, false>)
+                      : R <= 8 ? reinterpret_cast<const void*>(&w2_tail_kernel<9, false>)
+                      : R <= 16 ? reinterpret_cast<const void*>(&w2_tail_kernel<17, false>)
+                                : reinterpret_cast<const void*>(&w2_tail_kernel<33, false>);
+  if (hipFuncSetAttribute(tail_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTailLds) !=
+      hipSuccess)
+    return fail_arg("w2 tail: cannot reserve its LDS tables");
   auto bid = [&]() {
-    if (kW2Cache && R >= 2 && R <= kCacheMaxR) {
+    if (cached) {
       hipLaunchKernelGGL(w2_bid_cached_kernel, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
+      hipLaunchKernelGGL((w2_tail_kernel<2, true>), dim3(1), dim3(256), kTailLds, s, C, ldc, n, R,
+                         w);
       return;
     }
+#define DSVGD_W2_BID(KK)                                                                       \
+  do {                                                                                         \
+    hipLaunchKernelGGL(w2_bid_kernel<KK>, gb, dim3(256), 0, s, C, ldc, m, n, R, w);            \
+    hipLaunchKernelGGL((w2_tail_kernel<KK, false>), dim3(1), dim3(256), kTailLds, s, C, ldc, n, \
+                       R, w);                                                                  \
+  } while (0)
     if (R <= 1)
-      hipLaunchKernelGGL(w2_bid_kernel<2>, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
+      DSVGD_W2_BID(2);
     else if (R <= 2)
-      hipLaunchKernelGGL(w2_bid_kernel<3>, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
+      DSVGD_W2_BID(3);
     else if (R <= 4)
-      hipLaunchKernelGGL(w2_bid_kernel<5>, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
+      DSVGD_W2_BID(5);
     else if (R <= 8)
-      hipLaunchKernelGGL(w2_bid_kernel<9>, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
+      DSVGD_W2_BID(9);
     else if (R <= 16)
-      hipLaunchKernelGGL(w2_bid_kernel<17>, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
+      DSVGD_W2_BID(17);
     else
-      hipLaunchKernelGGL(w2_bid_kernel<33>, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
+      DSVGD_W2_BID(33);
+#undef DSVGD_W2_BID
   };
   const dim3 gr((unsigned)((n + 255) / 256));
   // pinned, double-buffered control readback (one pair per host thread)

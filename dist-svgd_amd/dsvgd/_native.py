@@ -126,7 +126,7 @@ SIGNATURES = {
     "dsvgd_gs_mask": (_int, [_p, _i64, _i64, _i64, _p]),
     "dsvgd_gsw_block_sweep": (_int, [_p, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64,
                                      _p, _f, _p, _i64, _p, _p, _i64, _p, _i64, _int, _p, _p, _f,
-                                     _p]),
+                                     _p, _i64, _p, _i64, _p]),
     # the pair-split layout (ABI 4)
     "dsvgd_sqdist_h2_parts": (_int, [_p, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p,
                                      _int, _p, _p, _p]),

@@ -610,6 +610,7 @@ class PhiEngine(object):
         mo_max = max([q["mo"] for q in P.sends] + [128])
         self.tP = torch.empty(max(smax, 1), ldy, **f32)
         self.tRS = torch.empty(max(t for t in self.t_splits) * lib.dsvgd_pad128(mo_max), **f32)
+        self.side = torch.cuda.Stream(device=dev)   # the own window (_direction_pair_split)
         parts = []
         if P.row_half:
             ro, nr, _, _ = P.row_half
@@ -642,6 +643,13 @@ class PhiEngine(object):
             self._scales(ldy, self.yscale, s)
             N.call("dsvgd_h2_ysplit", N.ptr(self.Y), ldy, self.n_pad, N.ptr(self.yscale),
                    N.ptr(self.Yx), s)
+        # the own window runs on a side stream next to the partials: the
+        # batched forward launch holds 192 workgroups (one per CU) for most
+        # of the phase, the window's slices fill the other CUs.  Both wait
+        # only for ysplit; the partials are queued first (this stream), the
+        # exchange is posted behind them.
+        main = torch.cuda.current_stream(self.device)
+        fork = main.record_event()
         with span(self.timer, "phi_partials"):
             nf = len(P.forward) if self.fwd_batched else 0
             if nf:
@@ -664,21 +672,27 @@ class PhiEngine(object):
                            guard, 0, s)
                     N.call("dsvgd_phi_partial_reduce", N.ptr(self.tP), ldy, N.ptr(self.tRS), z,
                            mo, ldy, N.ptr(buf), ldy, rs_out, s)
+        self.side.wait_event(fork)
+        with torch.cuda.stream(self.side):
+            s2 = N.stream(self.device)
+            with span(self.timer, "phi_mm"):
+                w0, wl = P.window
+                N.call("dsvgd_phi_h2_window", N.ptr(self.D), self.n_pad, N.ptr(self.Yx), ldy,
+                       self.row0, self.m, self.n, w0, wl, self.state.ptr, self.w_splits,
+                       N.ptr(self.KY), ldy, N.ptr(self.rowsum), colinv, guard, 0, s2)
+                if P.row_half:
+                    ro, nr, c0, nc = P.row_half
+                    N.call("dsvgd_phi_h2_window", N.ptr(self.D) + 4 * ro * self.n_pad,
+                           self.n_pad, N.ptr(self.Yx), ldy, self.row0 + ro, nr, self.n, c0, nc,
+                           self.state.ptr, self.h_splits, N.ptr(self.KYh), ldy, N.ptr(self.rsh),
+                           colinv, guard, 0, s2)
         join = None
         if p2p is not None:
             with span(self.timer, "partials_post"):
                 join = p2p([(b, q["dest"]) for q, b in zip(P.sends, self.sendbuf)],
                            [(b, q["src"]) for q, b in zip(P.recvs, self.recvbuf)])
-        with span(self.timer, "phi_mm"):
-            w0, wl = P.window
-            N.call("dsvgd_phi_h2_window", N.ptr(self.D), self.n_pad, N.ptr(self.Yx), ldy,
-                   self.row0, self.m, self.n, w0, wl, self.state.ptr, self.w_splits,
-                   N.ptr(self.KY), ldy, N.ptr(self.rowsum), colinv, guard, 0, s)
-            if P.row_half:
-                ro, nr, c0, nc = P.row_half
-                N.call("dsvgd_phi_h2_window", N.ptr(self.D) + 4 * ro * self.n_pad, self.n_pad,
-                       N.ptr(self.Yx), ldy, self.row0 + ro, nr, self.n, c0, nc, self.state.ptr,
-                       self.h_splits, N.ptr(self.KYh), ldy, N.ptr(self.rsh), colinv, guard, 0, s)
+        # the window's KY / rowsum, and D free for the next step's Gram
+        main.wait_stream(self.side)
         with span(self.timer, "phi_guard"):
             # the range guard's fallback: the rest of the row block's D, then
             # the FmtX3 phi_mm over all of it (gated: nothing while the guard is 0)
@@ -789,15 +803,18 @@ GS_BLOCK_MIN_ROWS = 128   # shorter sweeps keep the per-row kernels
 
 
 def _gs_score_kind(target):
-    """The blocked sweep refreshes the scores of elementwise targets itself:
-    dsvgd_gs_block_sweep's score_kind, or None (per-row path)."""
-    from .targets import Gaussian, GaussianMixture1D
+    """The blocked sweeps refresh the built-in targets' scores themselves:
+    dsvgd_gs_block_sweep's / dsvgd_gsw_block_sweep's score_kind (3, the
+    logistic regression: the wide sweep only), or None (per-row path)."""
+    from .targets import Gaussian, GaussianMixture1D, LogisticRegression
     if target is None:
         return 0
     if isinstance(target, Gaussian):
         return 1
     if isinstance(target, GaussianMixture1D):
         return 2
+    if isinstance(target, LogisticRegression):
+        return 3
     return None
 
 
@@ -810,10 +827,13 @@ def sequential_sweep(X, S, rows, h_state, step, target=None, score_scale=1.0, ph
     pair amounts to (dsvgd/sampler.py:64-68, dsvgd/distsampler.py:194-200).
     extra: optional (len(rows), d) contiguous rows (the h * W2 gradient).
 
-    Blocked form (d <= 64, contiguous rows, frozen scores or an elementwise
-    target): 64 rows at a time, one wide pass for the block against all n
-    rows and one workgroup for the in-block order (csrc/gs.hip) -- the same
-    sweep; otherwise one row kernel (+ one score refresh) per row."""
+    Blocked form (contiguous rows, frozen scores or a built-in target): a
+    block of rows at a time, one wide pass for the block against all n rows
+    and one workgroup for the in-block order (csrc/gs.hip) -- the same sweep;
+    d <= 64 with an elementwise target on the VALU form, 64 < d <= 1024 (and
+    the logistic regression at any d <= 1024, its score refreshed in the
+    walk) on the wide one; otherwise one row kernel (+ one score refresh) per
+    row."""
     n, d = X.shape
     s = N.stream(X.device)
     if extra is not None:
@@ -823,7 +843,7 @@ def sequential_sweep(X, S, rows, h_state, step, target=None, score_scale=1.0, ph
     contiguous = isinstance(rows, range) and rows.step == 1
     if (blocked and kind is not None and contiguous and len(rows) >= GS_BLOCK_MIN_ROWS
             and X.is_contiguous() and S.is_contiguous()):
-        if d <= 64:
+        if d <= 64 and kind != 3:
             _blocked_sweep(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s)
             return
         if d <= GSW_MAX_D:
@@ -940,9 +960,11 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
     if W is None:
         _WIDE.clear()
         W = _WIDE[key] = _WideSweep(X.device, n, d, GSW_GEMM)
-    sk, mu, lam = kind, None, None
+    sk, mu, lam, xd, td = kind, None, None, None, None
     if sk == 1:
         mu, lam = target._params(X.device)
+    elif sk == 3:    # the rank's data (16-byte rows) and labels
+        xd, td = target._params_aligned(X.device)
     N.call("dsvgd_colcenter", N.ptr(X), N.ld(X), n, d, N.ptr(W.mean), s)
     N.call("dsvgd_pack", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), 1.0, N.ptr(W.mean), n, d,
            W.Y.shape[0], N.ptr(W.Y), W.ldy, N.ptr(W.norms), s)
@@ -972,7 +994,9 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
         N.call("dsvgd_gsw_block_sweep", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), N.ptr(W.Y), W.ldy,
                N.ptr(W.norms), N.ptr(W.mean), n, d, b0, nb, h_state.ptr, float(step), N.ptr(W.Q),
                W.ldy, N.ptr(W.Qr), ex, d, po, N.ld(phi_out) if phi_out is not None else d, sk,
-               N.ptr(mu), N.ptr(lam), float(score_scale), s)
+               N.ptr(mu), N.ptr(lam), float(score_scale), N.ptr(xd),
+               N.ld(xd) if xd is not None else d, N.ptr(td), td.numel() if td is not None else 0,
+               s)
         W.images(b0, nb, s)
 
 

@@ -132,6 +132,20 @@ class LogisticRegression(BuiltinTarget):
             self._dev[dev] = (self.x.to(dev).contiguous(), self.t.to(dev).contiguous())
         return self._dev[dev]
 
+    def _params_aligned(self, dev):
+        """(data with 16-byte rows -- ld = roundup(p, 4), zero pad -- labels)
+        on dev: the Gauss-Seidel walk's one-pass score refresh
+        (dsvgd_gsw_block_sweep, score_kind 3) reads the rows as dwordx4."""
+        key = ("aligned", dev)
+        if key not in self._dev:
+            xd, t = self._params(dev)
+            p = xd.shape[1]
+            pa = -(-p // 4) * 4
+            buf = torch.zeros(xd.shape[0], pa, dtype=torch.float32, device=dev)
+            buf[:, :p] = xd
+            self._dev[key] = (buf, t)
+        return self._dev[key]
+
     def fingerprint(self):
         """Digest of the data (DistSampler: ranks whose targets agree on it
         hold the same data, so their scores of a particle are the same)."""

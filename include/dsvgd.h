@@ -360,8 +360,11 @@ int dsvgd_sqdist_h2(const void* Yg, const float* norms, int64_t row0, int64_t m,
  * -> Q = [K Xc | K S], Qr = K 1), then dsvgd_gsw_block_sweep walks the B rows
  * in order in one workgroup: phi_i = (Q_i + s_i + sum_{j<i} k(x_i, x_j')
  * (s_j' + (2/h)(x_i - x_j'))) / n (+ extra), X[i] += step phi_i, the score
- * refreshed (score_kind as dsvgd_gs_block_sweep), Y's row and norms[] kept
- * current (centre c = center, the packing centre of Y). */
+ * refreshed (score_kind as dsvgd_gs_block_sweep, or 3: the logistic
+ * regression score of logreg_small_kernel on nd data rows xd (ld ldxd, d - 1
+ * features) with labels td, times score_scale -- experiments/logreg.py:45-58
+ * re-run per pair by distsampler.py:97-99), Y's row and norms[] kept current
+ * (centre c = center, the packing centre of Y).  Any d <= 1024 for kind 3. */
 int64_t dsvgd_gsw_block_rows(int64_t d);
 int dsvgd_gs_mask(float* D, int64_t ldd, int64_t r0, int64_t B, void* stream);
 int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y, int64_t ldy,
@@ -369,7 +372,8 @@ int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y
                           int64_t B, const dsvgd_select_state* st, float step, const float* Q,
                           int64_t ldq, const float* Qr, const float* extra, int64_t lde,
                           float* phi_out, int64_t ldphi, int score_kind, const float* mu,
-                          const float* lam, float score_scale, void* stream);
+                          const float* lam, float score_scale, const float* xd, int64_t ldxd,
+                          const float* td, int64_t nd, void* stream);
 
 /* ---- the pair-split layout of a DistSampler rank (ABI 4) ---
  * With the scores identical on every rank (all_scores, or replicated data),

@@ -30,15 +30,22 @@ def main():
     import dsvgd
     from dsvgd.engine import sequential_sweep
     from bench import synthetic_data
-    shapes = {"D": (65536, 256, 16384), "E": (65536, 1024, 8192)}
+    # R: a logreg target whose scores are refreshed after every move (the
+    # partition mode's exchange_scores=False; 2048 data rows = config D's
+    # N_local at S = 8), scores scaled by N_global / N_local = 8
+    shapes = {"D": (65536, 256, 16384), "E": (65536, 1024, 8192), "R": (16384, 256, 2048)}
     for name in args.only.split(","):
         n, d, Ng = shapes[name]
+        refresh = name == "R"
         x, t = synthetic_data(Ng, d - 1)
         g = torch.Generator(device="cpu").manual_seed(0)
         X = (0.1 * torch.randn(n, d, generator=g)).cuda()
         ds = dsvgd.DistSampler(0, 1, dsvgd.targets.LogisticRegression(x, t), dsvgd.RBF("median"),
-                               X, Ng, Ng, exchange_particles=True, exchange_scores=True,
-                               include_wasserstein=False, order="sequential")
+                               X, 8 * Ng if refresh else Ng, Ng, exchange_particles=True,
+                               exchange_scores=not refresh, include_wasserstein=False,
+                               order="sequential")
+        tgt = ds._target if refresh else None
+        scale = 8.0 if refresh else 1.0
         ds.graphs = False
         ds.make_step(1e-4)                      # warm-up (workspaces, median engine)
         torch.cuda.synchronize()
@@ -52,20 +59,24 @@ def main():
         per_row_ms = None
         if k > 0:
             Xc, Sc = X.clone(), ds._scores.clone()
-            sequential_sweep(Xc, Sc, range(0, 64), eng.state, 1e-4, blocked=False)   # warm-up
+            sequential_sweep(Xc, Sc, range(0, 64), eng.state, 1e-4, target=tgt, score_scale=scale,
+                             blocked=False)   # warm-up
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            sequential_sweep(Xc, Sc, range(64, 64 + k), eng.state, 1e-4, blocked=False)
+            sequential_sweep(Xc, Sc, range(64, 64 + k), eng.state, 1e-4, target=tgt,
+                             score_scale=scale, blocked=False)
             torch.cuda.synchronize()
             per_row_ms = 1e3 * (time.perf_counter() - t0) * n / k
         # the blocked sweep alone (no median / scores), for the stage split
         Xb, Sb = X.clone(), ds._scores.clone()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        sequential_sweep(Xb, Sb, range(n), eng.state, 1e-4)
+        sequential_sweep(Xb, Sb, range(n), eng.state, 1e-4, target=tgt, score_scale=scale)
         torch.cuda.synchronize()
         sweep_ms = 1e3 * (time.perf_counter() - t0)
-        print(json.dumps({"config": name, "n": n, "d": d, "order": "sequential",
+        print(json.dumps({"config": name, "n": n, "d": d, "N_local": Ng,
+                          "scores": "refreshed (logreg)" if refresh else "frozen (all_scores)",
+                          "order": "sequential",
                           "step_ms_blocked": blocked_ms, "sweep_only_ms_blocked": sweep_ms,
                           "particle_updates_per_s": n / blocked_ms * 1e3,
                           "per_row_ms_extrapolated": per_row_ms, "per_row_sample_rows": k,

@@ -428,13 +428,20 @@ def test_phi_row_split_matches_oracle(n, d, ldx):
                                              (1500, 128, 10, 700, "gauss"),
                                              (1200, 256, 0, 1200, "none"),
                                              (800, 700, 50, 400, "gauss"),
-                                             (600, 1024, 0, 300, "gmm")])
+                                             (600, 1024, 0, 300, "gmm"),
+                                             # the logistic regression's score
+                                             # refreshed in the walk (any d)
+                                             (4096, 128, 0, 4096, "logreg"),
+                                             (1000, 55, 13, 900, "logreg"),
+                                             (700, 96, 0, 300, "logreg_big")])
 def test_blocked_sweep_matches_oracle(n, d, lo, hi, kind):
     """The blocked Gauss-Seidel sweep (csrc/gs.hip: 64-row blocks, a wide pass
     against all n rows + one workgroup for the in-block order) against the
     fp64 sequential restatement -- blocks cut anywhere in the range, scores
-    frozen or refreshed after every move (Gaussian, GMM), W2-style extra rows
-    and phi_out -- and against the per-row path."""
+    frozen or refreshed after every move (Gaussian, GMM, the logistic
+    regression on N = 1024 data rows or 5000 of them (two LDS chunks) with
+    the partition mode's N_global / N_local scale), W2-style extra rows and
+    phi_out -- and against the per-row path."""
     from dsvgd import _native as N
     from dsvgd.engine import SelectState, sequential_sweep
     m = dsvgd()
@@ -442,12 +449,21 @@ def test_blocked_sweep_matches_oracle(n, d, lo, hi, kind):
     X0 = (0.7 * rs.randn(n, d)).astype(np.float32)
     mu = rs.randn(d).astype(np.float32)
     lam = rs.uniform(0.5, 2.0, d).astype(np.float32)
-    tgt = {"gauss": m.targets.Gaussian(mu, lam), "gmm": m.targets.GaussianMixture1D(),
-           "none": None}[kind]
+    scale, step = 1.0, 0.05
+    if kind.startswith("logreg"):
+        nd = 5000 if kind == "logreg_big" else 1024
+        xd = (0.3 * rs.randn(nd, d - 1) / np.sqrt(d)).astype(np.float32)
+        td = np.where(rs.rand(nd) < 0.5, -1.0, 1.0).astype(np.float32)
+        X0[:, 0] = (0.3 * rs.randn(n)).astype(np.float32)      # log alpha
+        scale, step = 2.0, 0.01
+    tgt = {"gauss": lambda: m.targets.Gaussian(mu, lam), "gmm": m.targets.GaussianMixture1D,
+           "none": lambda: None, "logreg": lambda: m.targets.LogisticRegression(xd, td),
+           "logreg_big": lambda: m.targets.LogisticRegression(xd, td)}[kind]()
     fn = {"gauss": lambda X: O.score_gaussian(X, mu, lam), "gmm": O.score_gmm,
-          "none": None}[kind]
+          "none": None, "logreg": lambda X: scale * O.score_logreg(X, xd, td),
+          "logreg_big": lambda X: scale * O.score_logreg(X, xd, td)}[kind]
     S0 = (fn(X0) if fn else rs.randn(n, d)).astype(np.float32)
-    h, step = 0.9 * d + 0.5, 0.05
+    h = 0.9 * d + 0.5
     rows = range(lo, hi)
     extra = (0.01 * rs.randn(hi - lo, d)).astype(np.float32)
     st = SelectState(DEV)
@@ -456,8 +472,8 @@ def test_blocked_sweep_matches_oracle(n, d, lo, hi, kind):
     for blocked in (True, False):
         Xg, Sg = gpu(X0), gpu(S0)
         phi = torch.zeros(hi - lo, d, device=DEV)
-        sequential_sweep(Xg, Sg, rows, st, step, target=tgt, phi_out=phi, extra=gpu(extra),
-                         blocked=blocked)
+        sequential_sweep(Xg, Sg, rows, st, step, target=tgt, score_scale=scale, phi_out=phi,
+                         extra=gpu(extra), blocked=blocked)
         out[blocked] = (Xg.cpu().numpy().astype(np.float64), Sg.cpu().numpy(), phi.cpu().numpy())
     ref = X0.astype(np.float64)
     S = S0.astype(np.float64)
