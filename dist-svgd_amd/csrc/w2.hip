@@ -44,16 +44,19 @@ struct W2Ctl {
   float cmax;
   int32_t epoch;
   int32_t done;  // 0 running, 1 converged, 2 degenerate (all costs 0), 3 bad input
-  int32_t pad_;
+  int32_t fresh;  // this round starts a phase with the last one's plan: keep-checks first
   unsigned long long unassigned;
   long long rounds, phases;
   unsigned int ticket;  // resolve-kernel arrival counter (last arriver resets it)
   unsigned long long viol;  // warm start: the previous plan's CS violation (fp64 bits, >= 0)
+  int32_t tail;   // this round is the one-workgroup tail's (unassigned <= kTailMax)
+  int32_t pad_;
 };
 
 constexpr size_t kW2CtlBytes = 256;
 constexpr double kTheta = 8.0;
 constexpr int kRoundBatch = 16;
+constexpr int kTailMax = 64;  // the phase tail's unassigned slots (w2_tail_kernel)
 constexpr int kBidBlocks = 1024;  // grid-stride bid kernel: 4096 waves
 // R = 2 .. kCacheMaxR bids go through the per-row price cache (measured
 // against full scans: same plans, 3-20x fewer cost-row reads)
@@ -211,7 +214,7 @@ __global__ __launch_bounds__(256) void w2_violation_kernel(const float* __restri
 // VERDICT r2 item 9).  Any initial prices give the same eps_final-optimality
 // guarantee.
 constexpr double kWarmDiv = 64.0;
-__global__ void w2_start_kernel(W2Ctl* ctl, int64_t n, int warm_phases) {
+__global__ void w2_start_kernel(W2Ctl* ctl, int64_t n, int warm_phases, int keep) {
   const double cmax = (double)ctl->cmax;
   ctl->eps_final = fmax(cmax * 0x1p-24 / (double)n, cmax * 1e-13);
   double e0 = cmax / kTheta;
@@ -227,7 +230,20 @@ __global__ void w2_start_kernel(W2Ctl* ctl, int64_t n, int warm_phases) {
   ctl->unassigned = (unsigned long long)n;
   ctl->rounds = 0;
   ctl->phases = 1;
+  ctl->fresh = keep;
+  ctl->tail = n <= kTailMax;
   if (ctl->done == 0 && !(cmax > 0.0)) ctl->done = 2;
+}
+
+// Warm start: the previous plan as epoch 0's assignment, so that the first
+// phase keeps every slot whose column still meets eps-CS (w2_keep).
+__global__ __launch_bounds__(256) void w2_load_prev_kernel(int64_t n, const int32_t* __restrict__ prev,
+                                                           W2Ws w) {
+  const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (s >= n) return;
+  const int32_t j = prev[s];
+  w.assigned[s] = (j >= 0 && j < n) ? j : -1;
+  w.assigned_ep[s] = 0;
 }
 
 // A lane's K best (value, column) pairs, sorted descending; ties keep the
@@ -402,6 +418,50 @@ __device__ __forceinline__ void wave_best(double cv, int cj, int u, int lane, do
   }
 }
 
+// ---- keeping the last phase's plan -----------------------------------------
+// A new eps phase (and a warm start, whose "last phase" is the previous
+// solve's plan) starts with every slot unassigned in the new epoch.  The
+// slots whose column still meets eps-complementary slackness for the new eps
+//   -C_ij - p_j >= max_k (-C_ik - p_k) - eps       (max over ALL columns)
+// keep it instead (Bertsekas' auction keeps such pairs across phases): the
+// invariant the auction maintains holds for them, so the phase still ends
+// eps-optimal, and only the slots that violate it bid again.  Called by the
+// wave that owns row i in the first round of a phase (ctl->fresh), with the
+// row's best value over all columns; returns the kept slots' mask.
+__device__ __forceinline__ unsigned long long w2_keep(const float* __restrict__ row, int64_t i,
+                                                      int64_t R, int lane, int ep, uint32_t mine,
+                                                      double best, double eps, const W2Ws& w) {
+  bool k = false;
+  if (lane < R) {
+    const int64_t s = i * R + lane;
+    const int j = w.assigned[s];
+    if (w.assigned_ep[s] == ep - 1 && j >= 0) {
+      const double v = -(double)row[j] - w.price[j];
+      if (v >= best - eps) {
+        k = true;
+        w.assigned_ep[s] = ep;
+        w.holder[j] = mine;
+        w.owner[j] = (int)s;
+      }
+    }
+  }
+  const unsigned long long km = __ballot(k);
+  if (lane == 0 && km)
+    atomicAdd(&w.ctl->unassigned, (unsigned long long)(-(long long)__popcll(km)));
+  __threadfence_block();  // the new holders before this wave's held-column tests
+  return km;
+}
+
+// Whether lane's slot of row i holds a column of the previous epoch (wave-uniform result)
+__device__ __forceinline__ bool w2_has_prev(int64_t i, int64_t R, int lane, int ep, const W2Ws& w) {
+  bool hp = false;
+  if (lane < R) {
+    const int64_t s = i * R + lane;
+    hp = w.assigned_ep[s] == ep - 1 && w.assigned[s] >= 0;
+  }
+  return __ballot(hp) != 0ull;
+}
+
 // ---- the phase tail, Gauss-Seidel (one workgroup) -----------------------
 // A phase ends with long runs of rounds in which a handful of slots bid
 // (profiles/r8j: 17k of the 19k rounds of a warm m = 8192, n = 65536 solve
@@ -423,7 +483,6 @@ __device__ __forceinline__ void wave_best(double cv, int cj, int u, int lane, do
 // written through to global memory on every update (the scans and the next
 // launch read global memory, which is therefore always current): a price war
 // over a few columns then runs out of LDS.
-constexpr int kTailMax = 64;
 constexpr int kTailBids = 16384;
 constexpr int kTabCols = 4096;  // column entries: price, holder, owner, tag
 constexpr int kTabRows = 256;   // row entries: the price cache of a row
@@ -460,7 +519,7 @@ __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ 
   __shared__ int stack[kTailMax], sorted[kTailMax];
   __shared__ int sp, cnt, hit;
   const W2Ctl* ctl = w.ctl;
-  if (ctl->done || ctl->unassigned > (unsigned long long)kTailMax) return;  // uniform
+  if (ctl->done || !ctl->tail) return;  // uniform
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int ep = ctl->epoch;
   const double eps = ctl->eps;
@@ -652,7 +711,10 @@ __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ 
 // Rows in groups of four per workgroup-iteration (wave q: row base + q):
 // each wave finds its row's free slots and, with the price cache, tries the
 // cached bid; the rows left (no cache hit) are scanned one after the other by
-// the whole workgroup (block_topk), which refills the cache and bids.
+// the whole workgroup (block_topk), which refills the cache and bids.  In the
+// first round of a phase (fresh) the row's previous columns are kept where
+// eps-CS allows (w2_keep) before its bid: with the cache's best value when
+// the cache proves it the maximum over all columns, else after the scan.
 __global__ __launch_bounds__(256) void w2_bid_cached_kernel(const float* __restrict__ C,
                                                             int64_t ldc, int64_t m, int64_t n,
                                                             int64_t R, W2Ws w) {
@@ -660,13 +722,14 @@ __global__ __launch_bounds__(256) void w2_bid_cached_kernel(const float* __restr
   __shared__ double sv[4 * K], outv[K];
   __shared__ int sj[4 * K], outj[K];
   __shared__ unsigned long long need[4];
+  __shared__ int needkeep[4];
   const W2Ctl* ctl = w.ctl;
-  if (ctl->done) return;
+  if (ctl->done || ctl->tail) return;  // (uniform) the tail launch's round
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int ep = ctl->epoch;
   const double eps = ctl->eps;
+  const bool fresh = ctl->fresh != 0;
   const uint32_t tag = w2_tag(ep);
-  if (ctl->unassigned <= (unsigned long long)kTailMax) return;  // the tail launch's (uniform)
   for (int64_t base = (int64_t)blockIdx.x * 4; base < m; base += (int64_t)gridDim.x * 4) {
     const int64_t i = base + wv;
     unsigned long long free = 0;
@@ -678,30 +741,51 @@ __global__ __launch_bounds__(256) void w2_bid_cached_kernel(const float* __restr
       }
       free = __ballot(fr);
     }
+    bool keep = free && fresh && w2_has_prev(i, R, lane, ep, w);
     bool scan = false;
     if (free && w.cvalid[i]) {  // wave-uniform: the cached bid
-      const int u = __popcll(free);
       const uint32_t mine = tag | (uint32_t)i;
-      double cv = -DBL_MAX;
-      int cj = INT32_MAX;
+      int c = INT32_MAX;
+      double cval = -DBL_MAX;
       if (lane < kCache) {
-        const int c = w.ccol[i * kCache + lane];
-        if (c != INT32_MAX && w.holder[c] != mine) {  // held columns never bid
-          cj = c;
-          cv = -(double)w.ccost[i * kCache + lane] - w.price[c];
+        c = w.ccol[i * kCache + lane];
+        if (c != INT32_MAX) cval = -(double)w.ccost[i * kCache + lane] - w.price[c];
+      }
+      const double bound = w.cbound[i];
+      if (keep) {  // the row's best over all columns, if the cache proves it
+        double b1 = cval;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) b1 = fmax(b1, __shfl_xor(b1, o, 64));
+        if (b1 >= bound) {
+          free &= ~w2_keep(C + i * ldc, i, R, lane, ep, mine, b1, eps, w);
+          keep = false;
+        } else {
+          scan = true;
         }
       }
-      double kv;
-      int kj;
-      wave_best(cv, cj, u, lane, kv, kj);
-      if (__shfl(kv, u, 64) >= w.cbound[i])
-        bid_from_best(kv, kj, u, i, R, free, lane, eps, w);
-      else
-        scan = true;
+      if (!scan && free) {
+        const int u = __popcll(free);
+        double cv = -DBL_MAX;
+        int cj = INT32_MAX;
+        if (c != INT32_MAX && w.holder[c] != mine) {  // held columns never bid
+          cj = c;
+          cv = cval;
+        }
+        double kv;
+        int kj;
+        wave_best(cv, cj, u, lane, kv, kj);
+        if (__shfl(kv, u, 64) >= bound)
+          bid_from_best(kv, kj, u, i, R, free, lane, eps, w);
+        else
+          scan = true;
+      }
     } else if (free) {
       scan = true;
     }
-    if (lane == 0) need[wv] = scan ? free : 0ull;
+    if (lane == 0) {
+      need[wv] = scan ? free : 0ull;
+      needkeep[wv] = scan && keep;
+    }
     __syncthreads();
     for (int q = 0; q < 4; ++q) {
       const unsigned long long fq = need[q];  // block-uniform
@@ -719,18 +803,22 @@ __global__ __launch_bounds__(256) void w2_bid_cached_kernel(const float* __restr
         }
         if (lane == kCache) w.cbound[iq] = ev;
         if (lane == 0) w.cvalid[iq] = 1;
-        // bid from the fresh list (current values), held columns excluded
-        double cv = -DBL_MAX;
-        int cj = INT32_MAX;
-        if (lane < kCache && ej != INT32_MAX && w.holder[ej] != mine) {
-          cj = ej;
-          cv = ev;
+        unsigned long long f2 = fq;
+        if (needkeep[q]) f2 &= ~w2_keep(row, iq, R, lane, ep, mine, __shfl(ev, 0, 64), eps, w);
+        if (f2) {
+          // bid from the fresh list (current values), held columns excluded
+          double cv = -DBL_MAX;
+          int cj = INT32_MAX;
+          if (lane < kCache && ej != INT32_MAX && w.holder[ej] != mine) {
+            cj = ej;
+            cv = ev;
+          }
+          const int u = __popcll(f2);
+          double kv;
+          int kj;
+          wave_best(cv, cj, u, lane, kv, kj);
+          bid_from_best(kv, kj, u, iq, R, f2, lane, eps, w);
         }
-        const int u = __popcll(fq);
-        double kv;
-        int kj;
-        wave_best(cv, cj, u, lane, kv, kj);
-        bid_from_best(kv, kj, u, iq, R, fq, lane, eps, w);
       }
       __syncthreads();  // sv / outv reused by the next row
     }
@@ -738,20 +826,23 @@ __global__ __launch_bounds__(256) void w2_bid_cached_kernel(const float* __restr
 }
 
 // Without the cache (R = 1, R > kCacheMaxR): every bidding row is a full
-// scan over the columns it does not hold, by the whole workgroup.
+// scan over the columns it does not hold, by the whole workgroup (in a fresh
+// round nothing is held yet: the scan's best is over all columns, the keep
+// test's reference, and the kept columns are then dropped from the list).
 template <int K>
 __global__ __launch_bounds__(256) void w2_bid_kernel(const float* __restrict__ C, int64_t ldc,
                                                      int64_t m, int64_t n, int64_t R, W2Ws w) {
   __shared__ double sv[4 * K], outv[K];
   __shared__ int sj[4 * K], outj[K];
   __shared__ unsigned long long need[4];
+  __shared__ int needkeep[4];
   const W2Ctl* ctl = w.ctl;
-  if (ctl->done) return;
+  if (ctl->done || ctl->tail) return;  // (uniform) the tail launch's round
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int ep = ctl->epoch;
   const double eps = ctl->eps;
+  const bool fresh = ctl->fresh != 0;
   const uint32_t tag = w2_tag(ep);
-  if (ctl->unassigned <= (unsigned long long)kTailMax) return;  // the tail launch's (uniform)
   for (int64_t base = (int64_t)blockIdx.x * 4; base < m; base += (int64_t)gridDim.x * 4) {
     const int64_t i = base + wv;
     unsigned long long free = 0;
@@ -763,18 +854,40 @@ __global__ __launch_bounds__(256) void w2_bid_kernel(const float* __restrict__ C
       }
       free = __ballot(fr);
     }
-    if (lane == 0) need[wv] = free;
+    const bool keep = free && fresh && w2_has_prev(i, R, lane, ep, w);
+    if (lane == 0) {
+      need[wv] = free;
+      needkeep[wv] = keep;
+    }
     __syncthreads();
     for (int q = 0; q < 4; ++q) {
       const unsigned long long fq = need[q];  // block-uniform
       if (fq == 0ull) continue;
       const int64_t iq = base + q;
-      block_topk<K>(C + iq * ldc, n, w, tag | (uint32_t)iq, true, sv, sj, outv, outj);
+      const uint32_t mine = tag | (uint32_t)iq;
+      const float* row = C + iq * ldc;
+      block_topk<K>(row, n, w, mine, true, sv, sj, outv, outj);
       if (wv == 0) {
-        const int u = __popcll(fq);
-        const double kv = lane <= u && lane < K ? outv[lane] : -DBL_MAX;
-        const int kj = lane <= u && lane < K ? outj[lane] : INT32_MAX;
-        bid_from_best(kv, kj, u, iq, R, fq, lane, eps, w);
+        unsigned long long f2 = fq;
+        double kv = -DBL_MAX;
+        int kj = INT32_MAX;
+        if (needkeep[q]) {
+          f2 &= ~w2_keep(row, iq, R, lane, ep, mine, outv[0], eps, w);
+          if (f2) {
+            double cv = -DBL_MAX;
+            int cj = INT32_MAX;
+            if (lane < K && outj[lane] != INT32_MAX && w.holder[outj[lane]] != mine) {
+              cj = outj[lane];
+              cv = outv[lane];
+            }
+            wave_best(cv, cj, __popcll(f2), lane, kv, kj);
+          }
+        } else {
+          const int u = __popcll(fq);
+          kv = lane <= u && lane < K ? outv[lane] : -DBL_MAX;
+          kj = lane <= u && lane < K ? outj[lane] : INT32_MAX;
+        }
+        if (f2) bid_from_best(kv, kj, __popcll(f2), iq, R, f2, lane, eps, w);
       }
       __syncthreads();
     }
@@ -783,7 +896,13 @@ __global__ __launch_bounds__(256) void w2_bid_kernel(const float* __restrict__ C
 
 __device__ void w2_control(W2Ctl* ctl, int64_t n) {
   ctl->rounds += 1;
-  if (__hip_atomic_load(&ctl->unassigned, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  ctl->fresh = 0;
+  const unsigned long long un =
+      __hip_atomic_load(&ctl->unassigned, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (un != 0) {
+    ctl->tail = un <= (unsigned long long)kTailMax;
+    return;
+  }
   if (ctl->eps <= ctl->eps_final) {
     ctl->done = 1;
     return;
@@ -792,6 +911,8 @@ __device__ void w2_control(W2Ctl* ctl, int64_t n) {
   ctl->epoch += 1;
   ctl->phases += 1;
   ctl->unassigned = (unsigned long long)n;
+  ctl->fresh = 1;  // the next round keeps what still meets eps-CS
+  ctl->tail = n <= kTailMax;
 }
 
 // One thread per column: award the column to its highest bidder; the last
@@ -949,7 +1070,11 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
   if (prev)
     hipLaunchKernelGGL(w2_violation_kernel, dim3((unsigned)std::min<int64_t>(1024, (m + 3) / 4)),
                        dim3(256), 0, s, C, ldc, m, n, n / m, prev, w);
-  hipLaunchKernelGGL(w2_start_kernel, dim3(1), dim3(1), 0, s, w.ctl, n, warm_phases);
+  if (prev)
+    hipLaunchKernelGGL(w2_load_prev_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n,
+                       prev, w);
+  hipLaunchKernelGGL(w2_start_kernel, dim3(1), dim3(1), 0, s, w.ctl, n, warm_phases,
+                     prev ? 1 : 0);
   int rc = check_launch("w2_start");
   if (rc) return rc;
   const dim3 gb((unsigned)std::min<int64_t>(kBidBlocks, (m + 3) / 4));
