@@ -49,8 +49,8 @@ struct W2Ctl {
   long long rounds, phases;
   unsigned int ticket;  // resolve-kernel arrival counter (last arriver resets it)
   unsigned long long viol;  // warm start: the previous plan's CS violation (fp64 bits, >= 0)
-  int32_t tail;   // this round is the one-workgroup tail's (unassigned <= kTailMax)
-  int32_t pad_;
+  int32_t tail;     // this round is the one-workgroup tail's (unassigned <= kTailMax)
+  int32_t keep_on;  // phases keep the last plan's eps-CS slots (dsvgd_w2_set_keep)
 };
 
 constexpr size_t kW2CtlBytes = 256;
@@ -230,7 +230,8 @@ __global__ void w2_start_kernel(W2Ctl* ctl, int64_t n, int warm_phases, int keep
   ctl->unassigned = (unsigned long long)n;
   ctl->rounds = 0;
   ctl->phases = 1;
-  ctl->fresh = keep;
+  ctl->keep_on = keep & 1;
+  ctl->fresh = keep >> 1;
   ctl->tail = n <= kTailMax;
   if (ctl->done == 0 && !(cmax > 0.0)) ctl->done = 2;
 }
@@ -911,7 +912,7 @@ __device__ void w2_control(W2Ctl* ctl, int64_t n) {
   ctl->epoch += 1;
   ctl->phases += 1;
   ctl->unassigned = (unsigned long long)n;
-  ctl->fresh = 1;  // the next round keeps what still meets eps-CS
+  ctl->fresh = ctl->keep_on;  // the next round keeps what still meets eps-CS
   ctl->tail = n <= kTailMax;
 }
 
@@ -992,6 +993,13 @@ __global__ __launch_bounds__(256) void w2_grad_kernel(const float* __restrict__ 
 
 using namespace dsvgd;
 
+// phases keep the last plan's eps-CS slots (default on; off = every phase
+// and warm start re-assigns all slots -- the round-3 auction, kept for A/B)
+static bool& w2_keep_flag() {
+  static bool k = true;
+  return k;
+}
+
 // the last dsvgd_w2_assign's progress on this host thread: (rounds, phase,
 // unassigned slots) at every control readback (kRoundBatch rounds apart)
 static std::vector<long long>& w2_trace() {
@@ -1006,6 +1014,12 @@ int64_t dsvgd_w2_trace(int64_t* out, int64_t cap) {
   const int64_t k = (int64_t)t.size() / 3;
   for (int64_t e = 0; out && e < std::min(k, cap) * 3; ++e) out[e] = t[e];
   return k;
+}
+
+int dsvgd_w2_set_keep(int keep) {
+  const int old = w2_keep_flag() ? 1 : 0;
+  w2_keep_flag() = keep != 0;
+  return old;
 }
 
 size_t dsvgd_w2_workspace_bytes(int64_t m, int64_t n) {
@@ -1070,11 +1084,13 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
   if (prev)
     hipLaunchKernelGGL(w2_violation_kernel, dim3((unsigned)std::min<int64_t>(1024, (m + 3) / 4)),
                        dim3(256), 0, s, C, ldc, m, n, n / m, prev, w);
-  if (prev)
+  const bool keep = w2_keep_flag();
+  if (prev && keep)
     hipLaunchKernelGGL(w2_load_prev_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n,
                        prev, w);
+  // keep bit 0: phases keep eps-CS slots; bit 1: the first round keeps prev's
   hipLaunchKernelGGL(w2_start_kernel, dim3(1), dim3(1), 0, s, w.ctl, n, warm_phases,
-                     prev ? 1 : 0);
+                     (keep ? 1 : 0) | ((prev && keep) ? 2 : 0));
   int rc = check_launch("w2_start");
   if (rc) return rc;
   const dim3 gb((unsigned)std::min<int64_t>(kBidBlocks, (m + 3) / 4));

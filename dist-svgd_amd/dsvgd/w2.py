@@ -27,6 +27,9 @@ class W2Term(object):
     # new costs, dsvgd_w2_assign_warm); k > 0 = k fixed phases above the
     # final eps; 0 = cold every step.  The first call on a workspace is cold.
     WARM_PHASES = None
+    # a new epsilon phase (and the warm start's first) keeps the slots whose
+    # column still meets eps-CS (dsvgd_w2_set_keep); False: all re-bid
+    KEEP = True
 
     def __init__(self, m, n, d, device, warm=True):
         if n % m:
@@ -50,6 +53,7 @@ class W2Term(object):
         N.call("dsvgd_w2_cost", N.ptr(X), N.ld(X), self.m, N.ptr(Y), N.ld(Y), self.n, self.d,
                N.ptr(self.C), self.n, s)
         rounds = ctypes.c_int64(0)
+        N.load().dsvgd_w2_set_keep(int(bool(self.KEEP)))    # returns the old setting
         if self.warm and self._solved and self.WARM_PHASES is None:
             # prev and out may alias: the plan is only written after the solve
             N.call("dsvgd_w2_assign_warm", N.ptr(self.C), self.n, self.m, self.n,

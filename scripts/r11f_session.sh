@@ -14,5 +14,5 @@ timeout -k 10 300 python -u scripts/rank_shape_timing.py --shards 4,8 --steps 5 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/seqprof -o run --output-format csv -- \
   python3 scripts/seq_timing.py --only D --rows-sample 0 > $OUT/seqprof.log 2>&1 || exit $?
 timeout -k 10 300 python -u scripts/seq_timing.py --only D,E,R --rows-sample 1024 > $OUT/seq.log 2>&1 || exit $?
-timeout -k 10 300 python -u scripts/w2_timing.py --shapes 2048x16384x256,8192x65536x256 > $OUT/w2.log 2>&1 || exit $?
+timeout -k 10 300 python -u scripts/w2_timing.py --shapes 2048x16384x256,8192x65536x256 --keep 1,0 > $OUT/w2.log 2>&1 || exit $?
 echo ALL DONE

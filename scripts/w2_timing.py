@@ -93,6 +93,8 @@ def main():
                     help="m x n x d list, e.g. 8192x65536x256,2048x16384x256 (svgd shape)")
     ap.add_argument("--trace", action="store_true",
                     help="rounds per phase by unassigned-slot count")
+    ap.add_argument("--keep", default="1",
+                    help="comma list of W2Term.KEEP settings to sweep on --shapes (1, 0)")
     ap.add_argument("--warm-phases", default=None,
                     help="comma list of warm phase counts to sweep on --shapes (a = adaptive)")
     args = ap.parse_args()
@@ -101,13 +103,16 @@ def main():
     if args.shapes:
         import dsvgd
         shapes = [tuple(int(v) for v in sh.split("x")) + ("svgd",) for sh in args.shapes.split(",")]
-        for ph in ([None if v == "a" else int(v) for v in args.warm_phases.split(",")]
-                   if args.warm_phases else [dsvgd.w2.W2Term.WARM_PHASES]):
-            dsvgd.w2.W2Term.WARM_PHASES = ph
-            for sh in shapes:
-                r = case(*sh)
-                r["warm_phases"] = ph
-                print(json.dumps(r), flush=True)
+        for keep in [bool(int(v)) for v in args.keep.split(",")]:
+            dsvgd.w2.W2Term.KEEP = keep
+            for ph in ([None if v == "a" else int(v) for v in args.warm_phases.split(",")]
+                       if args.warm_phases else [dsvgd.w2.W2Term.WARM_PHASES]):
+                dsvgd.w2.W2Term.WARM_PHASES = ph
+                for sh in shapes:
+                    r = case(*sh)
+                    r["warm_phases"] = ph
+                    r["keep"] = keep
+                    print(json.dumps(r), flush=True)
         return
     if args.lib:
         import dsvgd
