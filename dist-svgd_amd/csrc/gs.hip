@@ -288,10 +288,11 @@ __global__ __launch_bounds__(256) void gs_sweep_kernel(
 // holds the moved rows (centred x' and w) and the old row being moved, so B
 // d <= kGswLds.
 constexpr int kGswLds = 16384;   // floats per LDS array (64 KiB): B = min(64, kGswLds / dp)
+constexpr int kGswLdsR = 10240;  // refreshed scores: three arrays (x', w, s') of 40 KiB
 constexpr int kGswMaxD = 1024;
 
-__host__ __device__ inline int gsw_rows(int64_t dp) {
-  const int64_t b = kGswLds / dp;
+__host__ __device__ inline int gsw_rows(int64_t dp, bool refreshed) {
+  const int64_t b = (refreshed ? kGswLdsR : kGswLds) / dp;
   return (int)(b >= kGsB ? kGsB : b);
 }
 
@@ -345,7 +346,7 @@ template <int NV>
 __device__ __forceinline__ void gsw_logreg_refresh(
     const float* xr, float cla, const float (&cw)[kGswMaxD / 64], const float* __restrict__ xd,
     int64_t ldxd, const float* __restrict__ td, int nd, float* red, int dp, float scale, int d,
-    float* snrow, const float (&cen)[kGswCols]) {
+    float* snrow, float* wnrow, float g2, const float (&cen)[kGswCols]) {
   constexpr int R = 16 / NV;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int p = d - 1;
@@ -422,16 +423,20 @@ __device__ __forceinline__ void gsw_logreg_refresh(
   for (int u = 0; u < kGswCols; ++u) {
     const int c = t + 256 * u;
     if (c >= d) continue;
+    float sv;
     if (c == 0) {
-      snrow[0] = scale * (-a + 0.5f * (float)p - 0.5f * a * w2);
+      sv = scale * (-a + 0.5f * (float)p - 0.5f * a * w2);
     } else {
       const float gs = (red[c - 1] + red[dp + c - 1]) + (red[2 * dp + c - 1] + red[3 * dp + c - 1]);
-      snrow[c] = scale * (gs - a * (xr[c] + cen[u]));
+      sv = scale * (gs - a * (xr[c] + cen[u]));
     }
+    snrow[c] = sv;
+    wnrow[c] = sv - g2 * xr[c];
   }
 }
 
 
+template <bool LOGREG>  // score_kind 3 (its refresh's registers stay out of the others' walk)
 __global__ __launch_bounds__(256) void gsw_sweep_kernel(
     float* __restrict__ X, int64_t ldx, float* __restrict__ S, int64_t lds, float* __restrict__ Y,
     int64_t ldy, float* __restrict__ norms, const float* __restrict__ center, int64_t n, int d,
@@ -442,12 +447,14 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
     float score_scale, const float* __restrict__ xd, int64_t ldxd, const float* __restrict__ td,
     int nd) {
   extern __shared__ __attribute__((aligned(16))) float gsw_smem[];
+  const bool refreshed = score_kind != 0;
   const int pitch = dp + 4;                       // 16-byte rows, 4 banks apart
   float* xn = gsw_smem;                           // [B][pitch]: moved rows, centred
-  float* sn = xn + (int64_t)B * pitch;            // [B][dp]: their scores
-  float* xo = sn + (int64_t)B * dp;               // [2][dp]: the row being moved (old, centred)
+  float* wn = xn + (int64_t)B * pitch;            // [B][dp]: w_j = s_j' - g (x_j' - c)
+  float* sn = wn + (int64_t)B * dp;               // [B][dp]: their scores (refreshed only)
+  float* xo = sn + (refreshed ? (int64_t)B * dp : 0);  // [2][dp]: the row being moved (old, centred)
   float* part = xo + 2 * dp;                      // [4][64] partial distances
-  float* coef = part + 256;                       // [kGswCoef] logreg: t_q sigma(-t_q z_q)
+  float* coef = part + 256;                       // [kGswCoef] logreg: the waves' partials
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const float inv_h = st->inv_h, g = 2.f * inv_h, scale = -inv_h * kLog2e;
   const float inv_n = 1.f / (float)n;
@@ -479,15 +486,15 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
     lam_c[u] = (score_kind == 1 && c < d) ? lam[c] : 0.f;
   }
   // logreg (score_kind 3): the centre of log alpha and of this lane's
-  // weights w[c], c = lane + 64 v
-  const float cla = score_kind == 3 ? center[0] : 0.f;
+  // weights w[c], c = 256 v + 4 lane + k
+  const float cla = LOGREG ? center[0] : 0.f;
   float cw[kGswMaxD / 64];   // w[256 v + 4 lane + k] at cw[4 v + k]
 #pragma unroll
   for (int v = 0; v < kGswMaxD / 256; ++v)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int c = 256 * v + 4 * lane + k;
-      cw[4 * v + k] = (score_kind == 3 && c + 1 < d) ? center[1 + c] : 0.f;
+      cw[4 * v + k] = (LOGREG && c + 1 < d) ? center[1 + c] : 0.f;
     }
   prefetch(0);
 #pragma unroll
@@ -514,55 +521,89 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
       if (lane < i) {
         const float* pa = xoi + w * q4;
         const float* pb = xn + lane * pitch + w * q4;
-        for (int c = 0; c < q4; c += 4) {
-          const f32x4 va = *reinterpret_cast<const f32x4*>(pa + c);
-          const f32x4 vb = *reinterpret_cast<const f32x4*>(pb + c);
+        auto acc4 = [&](const f32x4& va, const f32x4& vb) {
           const float d0 = va[0] - vb[0], d1 = va[1] - vb[1], d2 = va[2] - vb[2], d3 = va[3] - vb[3];
           sa = fmaf(d0, d0, fmaf(d2, d2, sa));
           sb = fmaf(d1, d1, fmaf(d3, d3, sb));
+        };
+        int c = 0;
+        for (; c + 16 <= q4; c += 16) {  // eight 16-byte LDS reads in flight
+          f32x4 va[4], vb[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            va[r] = *reinterpret_cast<const f32x4*>(pa + c + 4 * r);
+            vb[r] = *reinterpret_cast<const f32x4*>(pb + c + 4 * r);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc4(va[r], vb[r]);
         }
+        for (; c < q4; c += 4)
+          acc4(*reinterpret_cast<const f32x4*>(pa + c), *reinterpret_cast<const f32x4*>(pb + c));
       }
       part[w * 64 + lane] = sa + sb;
     }
     gsw_barrier();                                                          // (1)
     // every wave: lane j's k(x_i, x_j') and the moved rows' kernel sum
     const float dd = (part[lane] + part[64 + lane]) + (part[128 + lane] + part[192 + lane]);
-    const float kj = lane < i ? __builtin_amdgcn_exp2f(dd * scale) : 0.f;
-    float rm = kj;
+    const int kb = __builtin_bit_cast(int, lane < i ? __builtin_amdgcn_exp2f(dd * scale) : 0.f);
+    float rm = __builtin_bit_cast(float, kb);
     for (int o = 32; o > 0; o >>= 1) rm += __shfl_xor(rm, o, 64);
-    // (b) per column: the wide pass + the moved rows' terms + the self term
+    // (b) per column: sum_{j<i} k_j w_j (k_j broadcast by v_readlane), eight
+    // moved rows' LDS reads in flight at a time
+    float acc[kGswCols][2];
+#pragma unroll
+    for (int u = 0; u < kGswCols; ++u) acc[u][0] = acc[u][1] = 0.f;
+    int j = 0;
+    for (; j + 8 <= i; j += 8) {
+      float kk[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        kk[r] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(kb, j + r));
+#pragma unroll
+      for (int u = 0; u < kGswCols; ++u) {
+        const int c = t + 256 * u;
+        if (256 * u >= d) break;   // (uniform) no column of this u anywhere
+        if (c >= d) continue;
+        float wv8[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) wv8[r] = wn[(j + r) * dp + c];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) acc[u][r & 1] = fmaf(kk[r], wv8[r], acc[u][r & 1]);
+      }
+    }
+    for (; j < i; ++j) {
+      const float k0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(kb, j));
+#pragma unroll
+      for (int u = 0; u < kGswCols; ++u) {
+        const int c = t + 256 * u;
+        if (256 * u >= d) break;
+        if (c >= d) continue;
+        acc[u][0] = fmaf(k0, wn[j * dp + c], acc[u][0]);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < kGswCols; ++u) {
       const int c = t + 256 * u;
       if (c >= d) continue;
-      float as0 = 0.f, as1 = 0.f, ax0 = 0.f, ax1 = 0.f;
-      int j = 0;
-      for (; j + 2 <= i; j += 2) {
-        const float k0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kj), j));
-        const float k1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kj), j + 1));
-        as0 = fmaf(k0, sn[j * dp + c], as0);
-        ax0 = fmaf(k0, xn[j * pitch + c], ax0);
-        as1 = fmaf(k1, sn[(j + 1) * dp + c], as1);
-        ax1 = fmaf(k1, xn[(j + 1) * pitch + c], ax1);
-      }
-      if (j < i) {
-        const float k0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kj), j));
-        as0 = fmaf(k0, sn[j * dp + c], as0);
-        ax0 = fmaf(k0, xn[j * pitch + c], ax0);
-      }
-      // sum_{j<i} k_j (s_j' + g (x_i - x_j')), centred; + the self term s_i
-      // (the wide pass skipped the diagonal) + the wide pass's terms
+      // sum_{j<i} k_j (s_j' + g (x_i - x_j')) = sum k_j w_j + g x_i sum k_j
+      // (centred); + the self term s_i (the wide pass skipped the diagonal)
+      // + the wide pass's terms
       const float rtot = qr + rm;
-      float p = inv_n * (((q_s[u] + s_o[u]) - g * q_x[u]) + (as0 + as1) +
-                         g * (rtot * xc_o[u] - (ax0 + ax1)));
+      float p = inv_n * (((q_s[u] + s_o[u]) - g * q_x[u]) + (acc[u][0] + acc[u][1]) +
+                         g * (rtot * xc_o[u]));
       p += ex[u];
       if (phi_out) phi_out[(int64_t)i * ldphi + c] = p;
       const float x = (xc_o[u] + cen[u]) + step * p;
-      float sv = s_o[u];
-      if (score_kind == 1 || score_kind == 2)
-        sv = gs_score(score_kind, x, mu_c[u], lam_c[u], score_scale);
-      xn[i * pitch + c] = x - cen[u];
-      if (score_kind != 3) sn[i * dp + c] = sv;
+      const float xc = x - cen[u];
+      xn[i * pitch + c] = xc;
+      if (!LOGREG) {
+        float sv = s_o[u];
+        if (score_kind == 1 || score_kind == 2) {
+          sv = gs_score(score_kind, x, mu_c[u], lam_c[u], score_scale);
+          sn[i * dp + c] = sv;
+        }
+        wn[i * dp + c] = sv - g * xc;
+      }
     }
     // the next row's old values into the other xo buffer
     if (i + 1 < B) {
@@ -571,36 +612,40 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
         if (t + 256 * u < dp) xo[((i + 1) & 1) * dp + t + 256 * u] = n_xo[u];
     }
     gsw_barrier();                                                          // (2)
-    if (score_kind == 3) {
+    if (LOGREG) {
       // the moved row's logreg score on the rank's data, in one pass over it
       const float* xr = xn + i * pitch;
       const int nv4 = (d - 1 + 255) >> 8;   // 256-feature groups (1 .. 4)
       if (nv4 == 1)
         gsw_logreg_refresh<1>(xr, cla, cw, xd, ldxd, td, nd, coef, dp, score_scale, d,
-                              sn + i * dp, cen);
+                              sn + i * dp, wn + i * dp, g, cen);
       else if (nv4 == 2)
         gsw_logreg_refresh<2>(xr, cla, cw, xd, ldxd, td, nd, coef, dp, score_scale, d,
-                              sn + i * dp, cen);
+                              sn + i * dp, wn + i * dp, g, cen);
       else if (nv4 == 3)
         gsw_logreg_refresh<3>(xr, cla, cw, xd, ldxd, td, nd, coef, dp, score_scale, d,
-                              sn + i * dp, cen);
+                              sn + i * dp, wn + i * dp, g, cen);
       else
         gsw_logreg_refresh<4>(xr, cla, cw, xd, ldxd, td, nd, coef, dp, score_scale, d,
-                              sn + i * dp, cen);
-      // sn[i] is read after the next row's barrier (1); the partials' LDS is
-      // rewritten only after it
+                              sn + i * dp, wn + i * dp, g, cen);
+      // sn[i] / wn[i] are read after the next row's barrier (1); the
+      // partials' LDS is rewritten only after it
     }
   }
-  // the moved rows out: X (= the centred row + c), the refreshed scores, Y's
-  // row [x' - c | s'] and its norm |x' - c|^2 (the later blocks' distances)
+  // the moved rows out: X (= the centred row + c), Y's row x' - c and its
+  // norm |x' - c|^2 (the later blocks' distances), and with refreshed scores
+  // S and Y's score half (frozen scores: both unchanged)
   for (int e = t; e < B * d; e += 256) {
     const int i = e / d, c = e % d;
     const int64_t gi = r0 + i;
-    const float xc = xn[i * pitch + c], sv = sn[i * dp + c];
+    const float xc = xn[i * pitch + c];
     X[gi * ldx + c] = xc + center[c];
-    if (score_kind != 0) S[gi * lds + c] = sv;
     Y[gi * ldy + c] = xc;
-    Y[gi * ldy + dp + c] = sv;
+    if (refreshed) {
+      const float sv = sn[i * dp + c];
+      S[gi * lds + c] = sv;
+      Y[gi * ldy + dp + c] = sv;
+    }
   }
   for (int i = w; i < B; i += 4) {
     float s2 = 0.f;
@@ -665,9 +710,9 @@ int dsvgd_gs_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, int64_t n
   return check_launch("gs_sweep");
 }
 
-int64_t dsvgd_gsw_block_rows(int64_t d) {
-  if (d <= kGsMaxD) return kGsB;
-  return gsw_rows(roundup(d, 32));
+int64_t dsvgd_gsw_block_rows(int64_t d, int score_kind) {
+  if (d <= 0 || d > kGswMaxD) return 0;
+  return gsw_rows(roundup(d, 32), score_kind != 0);
 }
 
 int dsvgd_gs_mask(float* D, int64_t ldd, int64_t r0, int64_t B, void* stream) {
@@ -690,7 +735,8 @@ int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y
   DSVGD_REQUIRE(n > 0 && d > 0 && d <= kGswMaxD && ldx >= d && lds >= d && ldy >= 2 * dp &&
                     ldq >= 2 * dp,
                 "sizes (d <= 1024, ldy and ldq >= 2 roundup(d, 32))");
-  DSVGD_REQUIRE(B > 0 && B <= gsw_rows(dp) && r0 >= 0 && r0 + B <= n, "block rows");
+  DSVGD_REQUIRE(B > 0 && B <= gsw_rows(dp, score_kind != 0) && r0 >= 0 && r0 + B <= n,
+                "block rows (dsvgd_gsw_block_rows(d, score_kind))");
   DSVGD_REQUIRE(score_kind >= 0 && score_kind <= 3, "score_kind must be 0, 1, 2 or 3");
   DSVGD_REQUIRE(score_kind != 1 || (mu && lam), "Gaussian scores need mu and lam");
   DSVGD_REQUIRE(score_kind != 3 || (xd && td && d >= 2 && ldxd >= d - 1 && nd > 0 &&
@@ -700,12 +746,21 @@ int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y
                 "logreg data rows must be 16-byte aligned (ldxd % 4 == 0)");
   DSVGD_REQUIRE(!extra || lde >= d, "lde");
   DSVGD_REQUIRE(!phi_out || ldphi >= d, "ldphi");
-  const size_t smem = sizeof(float) * ((size_t)B * (dp + 4) + (size_t)B * dp + 2 * dp + 256 +
-                                       (score_kind == 3 ? kGswCoef : 0));
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gsw_sweep_kernel),
+  const size_t smem =
+      sizeof(float) * ((size_t)B * (dp + 4) + (size_t)B * dp * (score_kind != 0 ? 2 : 1) +
+                       2 * dp + 256 + (score_kind == 3 ? kGswCoef : 0));
+  const void* fn = score_kind == 3 ? reinterpret_cast<const void*>(&gsw_sweep_kernel<true>)
+                                    : reinterpret_cast<const void*>(&gsw_sweep_kernel<false>);
+  if (hipFuncSetAttribute(fn,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
     return fail_arg("gsw_sweep: cannot reserve the walk's LDS");
-  hipLaunchKernelGGL(gsw_sweep_kernel, dim3(1), dim3(256), smem, (hipStream_t)stream, X, ldx, S,
+  if (score_kind == 3)
+    hipLaunchKernelGGL(gsw_sweep_kernel<true>, dim3(1), dim3(256), smem, (hipStream_t)stream, X, ldx, S,
+                     lds, Y, ldy, norms, center, n, (int)d, (int)dp, r0, (int)B, st, step, Q, ldq,
+                     Qr, extra, lde, phi_out, ldphi, score_kind, mu, lam, score_scale, xd, ldxd,
+                     td, (int)(score_kind == 3 ? nd : 0));
+  else
+    hipLaunchKernelGGL(gsw_sweep_kernel<false>, dim3(1), dim3(256), smem, (hipStream_t)stream, X, ldx, S,
                      lds, Y, ldy, norms, center, n, (int)d, (int)dp, r0, (int)B, st, step, Q, ldq,
                      Qr, extra, lde, phi_out, ldphi, score_kind, mu, lam, score_scale, xd, ldxd,
                      td, (int)(score_kind == 3 ? nd : 0));

@@ -610,7 +610,6 @@ class PhiEngine(object):
         mo_max = max([q["mo"] for q in P.sends] + [128])
         self.tP = torch.empty(max(smax, 1), ldy, **f32)
         self.tRS = torch.empty(max(t for t in self.t_splits) * lib.dsvgd_pad128(mo_max), **f32)
-        self.side = torch.cuda.Stream(device=dev)   # the own window (_direction_pair_split)
         parts = []
         if P.row_half:
             ro, nr, _, _ = P.row_half
@@ -643,13 +642,6 @@ class PhiEngine(object):
             self._scales(ldy, self.yscale, s)
             N.call("dsvgd_h2_ysplit", N.ptr(self.Y), ldy, self.n_pad, N.ptr(self.yscale),
                    N.ptr(self.Yx), s)
-        # the own window runs on a side stream next to the partials: the
-        # batched forward launch holds 192 workgroups (one per CU) for most
-        # of the phase, the window's slices fill the other CUs.  Both wait
-        # only for ysplit; the partials are queued first (this stream), the
-        # exchange is posted behind them.
-        main = torch.cuda.current_stream(self.device)
-        fork = main.record_event()
         with span(self.timer, "phi_partials"):
             nf = len(P.forward) if self.fwd_batched else 0
             if nf:
@@ -672,27 +664,24 @@ class PhiEngine(object):
                            guard, 0, s)
                     N.call("dsvgd_phi_partial_reduce", N.ptr(self.tP), ldy, N.ptr(self.tRS), z,
                            mo, ldy, N.ptr(buf), ldy, rs_out, s)
-        self.side.wait_event(fork)
-        with torch.cuda.stream(self.side):
-            s2 = N.stream(self.device)
-            with span(self.timer, "phi_mm"):
-                w0, wl = P.window
-                N.call("dsvgd_phi_h2_window", N.ptr(self.D), self.n_pad, N.ptr(self.Yx), ldy,
-                       self.row0, self.m, self.n, w0, wl, self.state.ptr, self.w_splits,
-                       N.ptr(self.KY), ldy, N.ptr(self.rowsum), colinv, guard, 0, s2)
-                if P.row_half:
-                    ro, nr, c0, nc = P.row_half
-                    N.call("dsvgd_phi_h2_window", N.ptr(self.D) + 4 * ro * self.n_pad,
-                           self.n_pad, N.ptr(self.Yx), ldy, self.row0 + ro, nr, self.n, c0, nc,
-                           self.state.ptr, self.h_splits, N.ptr(self.KYh), ldy, N.ptr(self.rsh),
-                           colinv, guard, 0, s2)
         join = None
         if p2p is not None:
             with span(self.timer, "partials_post"):
                 join = p2p([(b, q["dest"]) for q, b in zip(P.sends, self.sendbuf)],
                            [(b, q["src"]) for q, b in zip(P.recvs, self.recvbuf)])
-        # the window's KY / rowsum, and D free for the next step's Gram
-        main.wait_stream(self.side)
+        # the own window after the partials on the same stream: run beside
+        # them on a second stream (the batched forward launch holds only 192
+        # CUs) it measured slower, 3.30 vs 3.18 ms at S = 8 (profiles/r11f)
+        with span(self.timer, "phi_mm"):
+            w0, wl = P.window
+            N.call("dsvgd_phi_h2_window", N.ptr(self.D), self.n_pad, N.ptr(self.Yx), ldy,
+                   self.row0, self.m, self.n, w0, wl, self.state.ptr, self.w_splits,
+                   N.ptr(self.KY), ldy, N.ptr(self.rowsum), colinv, guard, 0, s)
+            if P.row_half:
+                ro, nr, c0, nc = P.row_half
+                N.call("dsvgd_phi_h2_window", N.ptr(self.D) + 4 * ro * self.n_pad, self.n_pad,
+                       N.ptr(self.Yx), ldy, self.row0 + ro, nr, self.n, c0, nc, self.state.ptr,
+                       self.h_splits, N.ptr(self.KYh), ldy, N.ptr(self.rsh), colinv, guard, 0, s)
         with span(self.timer, "phi_guard"):
             # the range guard's fallback: the rest of the row block's D, then
             # the FmtX3 phi_mm over all of it (gated: nothing while the guard is 0)
@@ -883,14 +872,15 @@ class _WideSweep(object):
     rows a block moves are re-split after its walk), the block's D panel
     row, the split-K partials of its wide pass and their sums."""
 
-    def __init__(self, dev, n, d, gemm):
+    def __init__(self, dev, n, d, gemm, kind):
         lib = N.load()
         f32 = dict(dtype=torch.float32, device=dev)
         self.n, self.d = n, d
         self.n_pad = lib.dsvgd_pad128(n)
         self.dp = lib.dsvgd_dp(d)
         self.ldy = lib.dsvgd_ldy(self.dp)
-        self.B = int(lib.dsvgd_gsw_block_rows(d))
+        # rows per block: the walk keeps x' and w (and, refreshed, s') in LDS
+        self.B = int(lib.dsvgd_gsw_block_rows(d, kind))
         self.Y = torch.zeros(self.n_pad + 128, self.ldy, **f32)
         self.norms = torch.zeros(self.n_pad + 128, **f32)
         self.mean = torch.empty(d, **f32)
@@ -955,11 +945,11 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
     order (dsvgd_gsw_block_sweep) and the moved rows are re-split into the
     engines' images -- the same terms as the per-row path, in blocked order."""
     n, d = X.shape
-    key = (X.device, n, d, GSW_GEMM)
+    key = (X.device, n, d, GSW_GEMM, kind != 0)
     W = _WIDE.get(key)
     if W is None:
         _WIDE.clear()
-        W = _WIDE[key] = _WideSweep(X.device, n, d, GSW_GEMM)
+        W = _WIDE[key] = _WideSweep(X.device, n, d, GSW_GEMM, kind)
     sk, mu, lam, xd, td = kind, None, None, None, None
     if sk == 1:
         mu, lam = target._params(X.device)

@@ -352,7 +352,7 @@ int dsvgd_sqdist_h2(const void* Yg, const float* norms, int64_t row0, int64_t m,
                     float* cand, int layout, const float* rowscale, void* stream);
 /* ---- the reference's Gauss-Seidel order for 64 < d <= 1024 (ABI 4) -----
  * dsvgd/sampler.py:64-68 / distsampler.py:194-200 move row i with phi_i of the
- * CURRENT particles.  The wide blocked sweep takes B = dsvgd_gsw_block_rows(d)
+ * CURRENT particles.  The wide blocked sweep takes B = dsvgd_gsw_block_rows(d, kind)
  * rows at a time: their interactions with every row not moved before them in
  * the block on the f32 engines (dsvgd_sqdist of the centred Y = [X - c | S]
  * rows [r0, r0 + B); dsvgd_gs_mask: D[i][r0 + j] = +inf for j < i, the pairs
@@ -365,7 +365,7 @@ int dsvgd_sqdist_h2(const void* Yg, const float* norms, int64_t row0, int64_t m,
  * features) with labels td, times score_scale -- experiments/logreg.py:45-58
  * re-run per pair by distsampler.py:97-99), Y's row and norms[] kept current
  * (centre c = center, the packing centre of Y).  Any d <= 1024 for kind 3. */
-int64_t dsvgd_gsw_block_rows(int64_t d);
+int64_t dsvgd_gsw_block_rows(int64_t d, int score_kind);  /* 0 if d > 1024 */
 int dsvgd_gs_mask(float* D, int64_t ldd, int64_t r0, int64_t B, void* stream);
 int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y, int64_t ldy,
                           float* norms, const float* center, int64_t n, int64_t d, int64_t r0,

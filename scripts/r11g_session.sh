@@ -1,10 +1,18 @@
 #!/bin/bash
-# the W2 auction's kernel split at m = 8192, n = 65536 (cold and warm), and
-# the guard trip rate on converging runs
+# the walk's w-only column loop and unrolled distance reads, the W2 phase
+# keep and LDS tail: parity, then the default order at D / E / R, the W2
+# solve (keep on / off) and its kernel split, the guard trip rate
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/r11g
 mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -v -x \
+  --timeout 300 --timeout-method thread -k "blocked_sweep or sequential or w2 or wasserstein" \
+  > $OUT/tests.log 2>&1; rc=$?; tail -3 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u scripts/seq_timing.py --only D,E,R --rows-sample 1024 > $OUT/seq.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/seqprof -o run --output-format csv -- \
+  python3 scripts/seq_timing.py --only D,R --rows-sample 0 > $OUT/seqprof.log 2>&1 || exit $?
+timeout -k 10 400 python -u scripts/w2_timing.py --shapes 2048x16384x256,8192x65536x256 --keep 1,0 > $OUT/w2.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/w2prof -o run --output-format csv -- \
   python3 scripts/w2_timing.py --shapes 8192x65536x256 --trace > $OUT/w2prof.log 2>&1 || exit $?
 timeout -k 10 400 python -u scripts/guard_trip_rate.py --steps 300 > $OUT/guard.log 2>&1 || exit $?

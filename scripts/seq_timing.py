@@ -55,10 +55,15 @@ def main():
         blocked_ms = 1e3 * (time.perf_counter() - t0)
         # the per-row kernels over a sample of rows, same scores and bandwidth
         eng = next(iter(ds._engines.values()))
+        if refresh:     # the sweep's starting scores (the sampler keeps them internal)
+            S0 = torch.empty_like(X)
+            tgt.score(X, S0, scale)
+        else:
+            S0 = ds._scores
         k = min(args.rows_sample, n)
         per_row_ms = None
         if k > 0:
-            Xc, Sc = X.clone(), ds._scores.clone()
+            Xc, Sc = X.clone(), S0.clone()
             sequential_sweep(Xc, Sc, range(0, 64), eng.state, 1e-4, target=tgt, score_scale=scale,
                              blocked=False)   # warm-up
             torch.cuda.synchronize()
@@ -68,7 +73,7 @@ def main():
             torch.cuda.synchronize()
             per_row_ms = 1e3 * (time.perf_counter() - t0) * n / k
         # the blocked sweep alone (no median / scores), for the stage split
-        Xb, Sb = X.clone(), ds._scores.clone()
+        Xb, Sb = X.clone(), S0.clone()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         sequential_sweep(Xb, Sb, range(n), eng.state, 1e-4, target=tgt, score_scale=scale)
