@@ -449,20 +449,26 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
   extern __shared__ __attribute__((aligned(16))) float gsw_smem[];
   const bool refreshed = score_kind != 0;
   const int pitch = dp + 4;                       // 16-byte rows, 4 banks apart
-  float* xn = gsw_smem;                           // [B][pitch]: moved rows, centred
+  // xn row j: the old row (centred) until row j moves, then the moved one
+  float* xn = gsw_smem;                           // [B][pitch]
   float* wn = xn + (int64_t)B * pitch;            // [B][dp]: w_j = s_j' - g (x_j' - c)
   float* sn = wn + (int64_t)B * dp;               // [B][dp]: their scores (refreshed only)
-  float* xo = sn + (refreshed ? (int64_t)B * dp : 0);  // [2][dp]: the row being moved (old, centred)
-  float* part = xo + 2 * dp;                      // [4][64] partial distances
+  float* part = sn + (refreshed ? (int64_t)B * dp : 0);  // [4][64] partial distances
   float* coef = part + 256;                       // [kGswCoef] logreg: the waves' partials
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const float inv_h = st->inv_h, g = 2.f * inv_h, scale = -inv_h * kLog2e;
   const float inv_n = 1.f / (float)n;
   const int q4 = dp >> 2;                         // features per quarter (dp % 32 == 0)
-  for (int e = t; e < B * pitch; e += 256) xn[e] = 0.f;
+  // the block's old rows (Y's centred half, zero past d) into xn: the walk's
+  // only global loads are then the next row's operands, one row ahead
+  for (int e = t; e < B * (dp >> 2); e += 256) {
+    const int i = e / (dp >> 2), c4 = (e % (dp >> 2)) << 2;
+    *reinterpret_cast<f32x4*>(xn + i * pitch + c4) =
+        *reinterpret_cast<const f32x4*>(Y + (r0 + i) * ldy + c4);
+  }
   // per-thread columns c = t + 256 u, u < kGswCols, and the next row's operands
   float cen[kGswCols], mu_c[kGswCols], lam_c[kGswCols];
-  float nq_x[kGswCols], nq_s[kGswCols], n_xo[kGswCols], n_so[kGswCols], n_ex[kGswCols];
+  float nq_x[kGswCols], nq_s[kGswCols], n_so[kGswCols], n_ex[kGswCols];
   float nqr = 0.f;
   auto prefetch = [&](int i) {  // row i's operands (i < B)
     const int64_t gi = r0 + i;
@@ -472,7 +478,6 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
       const bool ok = c < d;
       nq_x[u] = ok ? Q[i * ldq + c] : 0.f;
       nq_s[u] = ok ? Q[i * ldq + dp + c] : 0.f;
-      n_xo[u] = c < dp ? Y[gi * ldy + c] : 0.f;
       n_so[u] = ok ? Y[gi * ldy + dp + c] : 0.f;
       n_ex[u] = (ok && extra) ? extra[(int64_t)i * lde + c] : 0.f;
     }
@@ -497,23 +502,19 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
       cw[4 * v + k] = (LOGREG && c + 1 < d) ? center[1 + c] : 0.f;
     }
   prefetch(0);
-#pragma unroll
-  for (int u = 0; u < kGswCols; ++u)
-    if (t + 256 * u < dp) xo[t + 256 * u] = n_xo[u];
   __syncthreads();
   for (int i = 0; i < B; ++i) {
-    float q_x[kGswCols], q_s[kGswCols], xc_o[kGswCols], s_o[kGswCols], ex[kGswCols];
+    float q_x[kGswCols], q_s[kGswCols], s_o[kGswCols], ex[kGswCols];
 #pragma unroll
     for (int u = 0; u < kGswCols; ++u) {
       q_x[u] = nq_x[u];
       q_s[u] = nq_s[u];
-      xc_o[u] = n_xo[u];
       s_o[u] = n_so[u];
       ex[u] = n_ex[u];
     }
     const float qr = nqr;
     if (i + 1 < B) prefetch(i + 1);
-    const float* xoi = xo + (i & 1) * dp;
+    const float* xoi = xn + i * pitch;   // row i, still the old one
     // (a) distances of the old row i to the moved rows j < i: thread (j =
     // lane, quarter w) over features [w q4, (w + 1) q4)
     {
@@ -581,6 +582,12 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
         acc[u][0] = fmaf(k0, wn[j * dp + c], acc[u][0]);
       }
     }
+    float xc_o[kGswCols];   // row i's old values (this thread's columns)
+#pragma unroll
+    for (int u = 0; u < kGswCols; ++u) {
+      const int c = t + 256 * u;
+      xc_o[u] = c < d ? xoi[c] : 0.f;
+    }
 #pragma unroll
     for (int u = 0; u < kGswCols; ++u) {
       const int c = t + 256 * u;
@@ -604,12 +611,6 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
         }
         wn[i * dp + c] = sv - g * xc;
       }
-    }
-    // the next row's old values into the other xo buffer
-    if (i + 1 < B) {
-#pragma unroll
-      for (int u = 0; u < kGswCols; ++u)
-        if (t + 256 * u < dp) xo[((i + 1) & 1) * dp + t + 256 * u] = n_xo[u];
     }
     gsw_barrier();                                                          // (2)
     if (LOGREG) {
@@ -747,8 +748,8 @@ int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y
   DSVGD_REQUIRE(!extra || lde >= d, "lde");
   DSVGD_REQUIRE(!phi_out || ldphi >= d, "ldphi");
   const size_t smem =
-      sizeof(float) * ((size_t)B * (dp + 4) + (size_t)B * dp * (score_kind != 0 ? 2 : 1) +
-                       2 * dp + 256 + (score_kind == 3 ? kGswCoef : 0));
+      sizeof(float) * ((size_t)B * (dp + 4) + (size_t)B * dp * (score_kind != 0 ? 2 : 1) + 256 +
+                       (score_kind == 3 ? kGswCoef : 0));
   const void* fn = score_kind == 3 ? reinterpret_cast<const void*>(&gsw_sweep_kernel<true>)
                                     : reinterpret_cast<const void*>(&gsw_sweep_kernel<false>);
   if (hipFuncSetAttribute(fn,

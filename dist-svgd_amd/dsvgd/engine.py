@@ -141,6 +141,10 @@ class PhiEngine(object):
     SIGMAS = 6.0                # bracket half-width in sample-rank standard deviations
     SEED = 0x5EED5EED
 
+    # pair split: run the own window on a second stream beside the transposed
+    # partials (the batched forward launch holds 192 of the 256 CUs)
+    WINDOW_SIDE_STREAM = False
+
     GEMMS = ("h2", "x3", "f32")
     DEFAULT_GEMM = "h2"
 
@@ -556,6 +560,7 @@ class PhiEngine(object):
             raise ValueError("pair_split needs m = n / S = the rank's block, the FmtH2 engines, "
                              "m % 256 == 0 and roundup(d, 32) % 256 == 0")
         P = self.plan = PairSplitPlan(rank, S, self.m)
+        self._side = None   # WINDOW_SIDE_STREAM's stream
         dev, f32 = self.device, dict(dtype=torch.float32, device=self.device)
 
         def gparts(lst):
@@ -642,6 +647,8 @@ class PhiEngine(object):
             self._scales(ldy, self.yscale, s)
             N.call("dsvgd_h2_ysplit", N.ptr(self.Y), ldy, self.n_pad, N.ptr(self.yscale),
                    N.ptr(self.Yx), s)
+        fork = torch.cuda.current_stream(self.device).record_event() \
+            if self.WINDOW_SIDE_STREAM else None
         with span(self.timer, "phi_partials"):
             nf = len(P.forward) if self.fwd_batched else 0
             if nf:
@@ -669,19 +676,29 @@ class PhiEngine(object):
             with span(self.timer, "partials_post"):
                 join = p2p([(b, q["dest"]) for q, b in zip(P.sends, self.sendbuf)],
                            [(b, q["src"]) for q, b in zip(P.recvs, self.recvbuf)])
-        # the own window after the partials on the same stream: run beside
-        # them on a second stream (the batched forward launch holds only 192
-        # CUs) it measured slower, 3.30 vs 3.18 ms at S = 8 (profiles/r11f)
-        with span(self.timer, "phi_mm"):
-            w0, wl = P.window
-            N.call("dsvgd_phi_h2_window", N.ptr(self.D), self.n_pad, N.ptr(self.Yx), ldy,
-                   self.row0, self.m, self.n, w0, wl, self.state.ptr, self.w_splits,
-                   N.ptr(self.KY), ldy, N.ptr(self.rowsum), colinv, guard, 0, s)
-            if P.row_half:
-                ro, nr, c0, nc = P.row_half
-                N.call("dsvgd_phi_h2_window", N.ptr(self.D) + 4 * ro * self.n_pad, self.n_pad,
-                       N.ptr(self.Yx), ldy, self.row0 + ro, nr, self.n, c0, nc, self.state.ptr,
-                       self.h_splits, N.ptr(self.KYh), ldy, N.ptr(self.rsh), colinv, guard, 0, s)
+        # the own window: after the partials on this stream, or (the A/B
+        # option) on a second stream that waited only for ysplit
+        main = torch.cuda.current_stream(self.device)
+        side = self.WINDOW_SIDE_STREAM
+        if side:
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=self.device)
+            self._side.wait_event(fork)
+        with torch.cuda.stream(self._side if side else main):
+            sw = N.stream(self.device)
+            with span(self.timer, "phi_mm"):
+                w0, wl = P.window
+                N.call("dsvgd_phi_h2_window", N.ptr(self.D), self.n_pad, N.ptr(self.Yx), ldy,
+                       self.row0, self.m, self.n, w0, wl, self.state.ptr, self.w_splits,
+                       N.ptr(self.KY), ldy, N.ptr(self.rowsum), colinv, guard, 0, sw)
+                if P.row_half:
+                    ro, nr, c0, nc = P.row_half
+                    N.call("dsvgd_phi_h2_window", N.ptr(self.D) + 4 * ro * self.n_pad,
+                           self.n_pad, N.ptr(self.Yx), ldy, self.row0 + ro, nr, self.n, c0, nc,
+                           self.state.ptr, self.h_splits, N.ptr(self.KYh), ldy, N.ptr(self.rsh),
+                           colinv, guard, 0, sw)
+        if side:
+            main.wait_stream(self._side)   # KY / rowsum, and D free for the next Gram
         with span(self.timer, "phi_guard"):
             # the range guard's fallback: the rest of the row block's D, then
             # the FmtX3 phi_mm over all of it (gated: nothing while the guard is 0)

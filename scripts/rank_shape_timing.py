@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--shards", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--lib", default=None, help="an A/B build of the library (make ab)")
+    ap.add_argument("--side", default="0",
+                    help="pairs: comma list of PhiEngine.WINDOW_SIDE_STREAM settings (0, 1)")
     ap.add_argument("--layout", default="both", choices=["rows", "pairs", "both"],
                     help="rows: the row-block layout; pairs: the pair-split layout (DESIGN.md 6; "
                          "the partials' exchange left out, their buffers zero)")
@@ -38,9 +40,13 @@ def main():
     runs = []
     for S in [int(v) for v in args.shards.split(",")]:
         for lay in (("rows", "pairs") if args.layout == "both" else (args.layout,)):
-            if lay == "rows" or (S > 1 and dsvgd.PhiEngine.pair_split_ok(n, d, S)):
-                runs.append((S, lay))
-    for S, lay in runs:
+            if lay == "rows":
+                runs.append((S, lay, False))
+            elif S > 1 and dsvgd.PhiEngine.pair_split_ok(n, d, S):
+                for side in args.side.split(","):
+                    runs.append((S, lay, bool(int(side))))
+    for S, lay, side in runs:
+        dsvgd.PhiEngine.WINDOW_SIDE_STREAM = side
         m, r = n // S, S // 2          # a middle rank (a high one of the pair split)
         per = Ng // S
         tgt = dsvgd.targets.LogisticRegression(x[r * per:(r + 1) * per], t[r * per:(r + 1) * per])
@@ -89,7 +95,8 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         st = {k: round(float(np.mean(v)), 3) for k, v in timer.summary().items()}
-        print(json.dumps({"shards": S, "layout": lay, "m": m, "row0": r * m, "N_local": per,
+        print(json.dumps({"shards": S, "layout": lay + ("+side" if side else ""), "m": m,
+                          "row0": r * m, "N_local": per,
                           "ms_per_step_no_comm": e0.elapsed_time(e1) / args.steps,
                           "sym_layout": bool(eng.sym), "stages_ms": st}), flush=True)
         del eng
