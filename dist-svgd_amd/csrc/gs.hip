@@ -547,8 +547,7 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
     // every wave: lane j's k(x_i, x_j') and the moved rows' kernel sum
     const float dd = (part[lane] + part[64 + lane]) + (part[128 + lane] + part[192 + lane]);
     const int kb = __builtin_bit_cast(int, lane < i ? __builtin_amdgcn_exp2f(dd * scale) : 0.f);
-    float rm = __builtin_bit_cast(float, kb);
-    for (int o = 32; o > 0; o >>= 1) rm += __shfl_xor(rm, o, 64);
+    float rm = 0.f;   // sum_{j<i} k_j, summed along the column loop's broadcasts
     // (b) per column: sum_{j<i} k_j w_j (k_j broadcast by v_readlane), eight
     // moved rows' LDS reads in flight at a time
     float acc[kGswCols][2];
@@ -560,6 +559,7 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
 #pragma unroll
       for (int r = 0; r < 8; ++r)
         kk[r] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(kb, j + r));
+      rm += ((kk[0] + kk[1]) + (kk[2] + kk[3])) + ((kk[4] + kk[5]) + (kk[6] + kk[7]));
 #pragma unroll
       for (int u = 0; u < kGswCols; ++u) {
         const int c = t + 256 * u;
@@ -574,6 +574,7 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
     }
     for (; j < i; ++j) {
       const float k0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(kb, j));
+      rm += k0;
 #pragma unroll
       for (int u = 0; u < kGswCols; ++u) {
         const int c = t + 256 * u;
@@ -636,26 +637,37 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
   // the moved rows out: X (= the centred row + c), Y's row x' - c and its
   // norm |x' - c|^2 (the later blocks' distances), and with refreshed scores
   // S and Y's score half (frozen scores: both unchanged)
-  for (int e = t; e < B * d; e += 256) {
-    const int i = e / d, c = e % d;
+  for (int i = 0; i < B; ++i) {
     const int64_t gi = r0 + i;
-    const float xc = xn[i * pitch + c];
-    X[gi * ldx + c] = xc + center[c];
-    Y[gi * ldy + c] = xc;
-    if (refreshed) {
-      const float sv = sn[i * dp + c];
-      S[gi * lds + c] = sv;
-      Y[gi * ldy + dp + c] = sv;
+#pragma unroll
+    for (int u = 0; u < kGswCols; ++u) {
+      const int c = t + 256 * u;
+      if (c >= d) continue;
+      const float xc = xn[i * pitch + c];
+      X[gi * ldx + c] = xc + cen[u];
+      Y[gi * ldy + c] = xc;
+      if (refreshed) {
+        const float sv = sn[i * dp + c];
+        S[gi * lds + c] = sv;
+        Y[gi * ldy + dp + c] = sv;
+      }
     }
   }
-  for (int i = w; i < B; i += 4) {
-    float s2 = 0.f;
-    for (int c = lane; c < d; c += 64) {
-      const float v = xn[i * pitch + c];
-      s2 = fmaf(v, v, s2);
+  {  // norms: four threads per row, a quarter of the features each (zero past d)
+    const int i = t >> 2, qq = t & 3;
+    float s2a = 0.f, s2b = 0.f;
+    if (i < B) {
+      const float* pr = xn + i * pitch + qq * q4;
+      for (int c = 0; c < q4; c += 4) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(pr + c);
+        s2a = fmaf(v[0], v[0], fmaf(v[2], v[2], s2a));
+        s2b = fmaf(v[1], v[1], fmaf(v[3], v[3], s2b));
+      }
     }
-    for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
-    if (lane == 0) norms[r0 + i] = s2;
+    float s2 = s2a + s2b;
+    s2 += __shfl_xor(s2, 1, 64);
+    s2 += __shfl_xor(s2, 2, 64);
+    if (i < B && qq == 0) norms[r0 + i] = s2;
   }
 }
 

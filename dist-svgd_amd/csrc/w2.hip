@@ -510,6 +510,12 @@ struct TailTab {
   }
 };
 
+// One wave runs the bids: a bid answered by the row's price cache (most of
+// them in a price war) touches no barrier at all -- wave 0 alone pops the
+// slot, bids, resolves and pushes the displaced slot.  The other three waves
+// only join the full scans: they spin on an LDS sequence number (s_sleep
+// between polls), read the row wave 0 posted and run block_topk with it, all
+// four reaching its barriers together.
 template <int K, bool CACHED>
 __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ C, int64_t ldc,
                                                       int64_t n, int64_t R, W2Ws w) {
@@ -518,7 +524,8 @@ __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ 
   __shared__ double sv[4 * KS], outv[KS];
   __shared__ int sj[4 * KS], outj[KS];
   __shared__ int stack[kTailMax], sorted[kTailMax];
-  __shared__ int sp, cnt, hit;
+  __shared__ int cnt, seq;
+  __shared__ long long req;  // the row to scan, or -1: the tail is over
   const W2Ctl* ctl = w.ctl;
   if (ctl->done || !ctl->tail) return;  // uniform
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -528,7 +535,10 @@ __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ 
   TailTab T(w2_tail_lds);
   for (int e = t; e < kTabCols; e += 256) T.ct[e] = -1;
   for (int e = t; e < kTabRows; e += 256) T.rt[e] = -1;
-  if (t == 0) cnt = 0;
+  if (t == 0) {
+    cnt = 0;
+    seq = 0;
+  }
   __syncthreads();
   for (int64_t s0 = t; s0 < n; s0 += 256)
     if (!(w.assigned_ep[s0] == ep && w.assigned[s0] >= 0)) {
@@ -545,167 +555,185 @@ __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ 
   }
   __syncthreads();
   if (t < c0) stack[t] = sorted[t];
-  if (t == 0) sp = c0;
   __syncthreads();
-  for (int b = 0; b < kTailBids; ++b) {
-    const int top = sp;  // block-uniform (read after the barrier)
-    if (top == 0) break;
-    const int s = stack[top - 1];
+  if (wv != 0) {  // the scan helpers
+    int last = 0;
+    for (;;) {
+      int sq;
+      while ((sq = __hip_atomic_load(&seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == last)
+        __builtin_amdgcn_s_sleep(1);
+      last = sq;
+      const long long rq = req;
+      if (rq < 0) return;
+      block_topk<KS>(C + rq * ldc, n, w, tag | (uint32_t)rq, !CACHED, sv, sj, outv, outj);
+    }
+  }
+  // wave 0: the bids
+  int nseq = 0;
+  auto scan = [&](int64_t i, uint32_t mine) {  // post row i, scan it with the helpers
+    if (lane == 0) {
+      req = i;
+      __hip_atomic_store(&seq, ++nseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      ++nseq;
+    }
+    block_topk<KS>(C + i * ldc, n, w, mine, !CACHED, sv, sj, outv, outj);
+  };
+  int sp = c0;
+  for (int b = 0; b < kTailBids && sp > 0; ++b) {
+    const int s = stack[sp - 1];
     const int64_t i = s / R;
     const uint32_t mine = tag | (uint32_t)i;
     const float* row = C + i * ldc;
-    if (CACHED) {
-      if (wv == 0) {  // the row's cache (table, else global + install), its bid
-        const int re = (int)(i & (kTabRows - 1));
-        int valid, c = INT32_MAX;
-        float cc = 0.f;
-        double bound;
-        if (T.rt[re] == (int)i) {
-          valid = T.rv[re];
-          bound = T.rb[re];
-          if (lane < kCache) {
-            c = T.rc[re * kCache + lane];
-            cc = T.rx[re * kCache + lane];
-          }
-        } else {
-          valid = w.cvalid[i];
-          bound = w.cbound[i];
-          if (lane < kCache) {
-            c = w.ccol[i * kCache + lane];
-            cc = w.ccost[i * kCache + lane];
-            T.rc[re * kCache + lane] = c;
-            T.rx[re * kCache + lane] = cc;
-          }
-          if (lane == 0) {
-            T.rt[re] = (int)i;
-            T.rv[re] = valid;
-            T.rb[re] = bound;
-          }
+    double b1 = -DBL_MAX, b2 = -DBL_MAX;
+    int bj = INT32_MAX;
+    bool hit = false;
+    if (CACHED) {  // the row's cache (table, else global + install), its bid
+      const int re = (int)(i & (kTabRows - 1));
+      int valid, c = INT32_MAX;
+      float cc = 0.f;
+      double bound;
+      if (T.rt[re] == (int)i) {
+        valid = T.rv[re];
+        bound = T.rb[re];
+        if (lane < kCache) {
+          c = T.rc[re * kCache + lane];
+          cc = T.rx[re * kCache + lane];
         }
-        bool h1 = false;
-        if (valid) {
-          double cv = -DBL_MAX;
-          int cj = INT32_MAX;
-          if (lane < kCache && c != INT32_MAX) {
-            const int e = c & (kTabCols - 1);
-            double p;
-            uint32_t hd;
-            if (T.ct[e] == c) {
-              p = T.cp[e];
-              hd = T.ch[e];
-            } else {
-              p = w.price[c];
-              hd = w.holder[c];
-            }
-            if (hd != mine) {  // held columns never bid
-              cj = c;
-              cv = -(double)cc - p;
-            }
-          }
-          double kv;
-          int kj;
-          wave_best(cv, cj, 1, lane, kv, kj);
-          const double b1 = __shfl(kv, 0, 64), b2 = __shfl(kv, 1, 64);
-          const int bj = __shfl(kj, 0, 64);
-          h1 = b2 >= bound;
-          if (lane == 0) {
-            outv[0] = b1;
-            outv[1] = b2;
-            outj[0] = bj;
-          }
+      } else {
+        valid = w.cvalid[i];
+        bound = w.cbound[i];
+        if (lane < kCache) {
+          c = w.ccol[i * kCache + lane];
+          cc = w.ccost[i * kCache + lane];
+          T.rc[re * kCache + lane] = c;
+          T.rx[re * kCache + lane] = cc;
         }
-        if (lane == 0) hit = h1;
+        if (lane == 0) {
+          T.rt[re] = (int)i;
+          T.rv[re] = valid;
+          T.rb[re] = bound;
+        }
       }
-      __syncthreads();
-      if (!hit) {  // full scan over all columns, refill the cache (global + table)
-        block_topk<kCache + 1>(row, n, w, mine, false, sv, sj, outv, outj);
-        if (wv == 0) {
-          const int re = (int)(i & (kTabRows - 1));
-          const double ev = lane < kCache + 1 ? outv[lane] : -DBL_MAX;
-          const int ej = lane < kCache + 1 ? outj[lane] : INT32_MAX;
-          if (lane < kCache) {
-            const float cc = ej != INT32_MAX ? row[ej] : 0.f;
-            w.ccol[i * kCache + lane] = ej;
-            w.ccost[i * kCache + lane] = cc;
-            T.rc[re * kCache + lane] = ej;
-            T.rx[re * kCache + lane] = cc;
+      if (valid) {
+        double cv = -DBL_MAX;
+        int cj = INT32_MAX;
+        if (lane < kCache && c != INT32_MAX) {
+          const int e = c & (kTabCols - 1);
+          double p;
+          uint32_t hd;
+          if (T.ct[e] == c) {
+            p = T.cp[e];
+            hd = T.ch[e];
+          } else {
+            p = w.price[c];
+            hd = w.holder[c];
           }
-          if (lane == kCache) {
-            w.cbound[i] = ev;
-            T.rb[re] = ev;
-          }
-          if (lane == 0) {
-            w.cvalid[i] = 1;
-            T.rv[re] = 1;
-            T.rt[re] = (int)i;
-          }
-          double cv = -DBL_MAX;
-          int cj = INT32_MAX;
-          if (lane < kCache && ej != INT32_MAX && w.holder[ej] != mine) {
-            cj = ej;
-            cv = ev;
-          }
-          double kv;
-          int kj;
-          wave_best(cv, cj, 1, lane, kv, kj);
-          const double b1 = __shfl(kv, 0, 64), b2 = __shfl(kv, 1, 64);
-          const int bj = __shfl(kj, 0, 64);
-          if (lane == 0) {  // (one wave: its LDS reads of outv are in order before)
-            outv[0] = b1;
-            outv[1] = b2;
-            outj[0] = bj;
+          if (hd != mine) {  // held columns never bid
+            cj = c;
+            cv = -(double)cc - p;
           }
         }
-        __syncthreads();
+        double kv;
+        int kj;
+        wave_best(cv, cj, 1, lane, kv, kj);
+        b1 = __shfl(kv, 0, 64);
+        b2 = __shfl(kv, 1, 64);
+        bj = __shfl(kj, 0, 64);
+        hit = b2 >= bound;
+      }
+      if (!hit) {  // full scan over all columns, refill the cache (global + table)
+        scan(i, mine);
+        const double ev = lane < kCache + 1 ? outv[lane] : -DBL_MAX;
+        const int ej = lane < kCache + 1 ? outj[lane] : INT32_MAX;
+        if (lane < kCache) {
+          const float c2 = ej != INT32_MAX ? row[ej] : 0.f;
+          w.ccol[i * kCache + lane] = ej;
+          w.ccost[i * kCache + lane] = c2;
+          T.rc[re * kCache + lane] = ej;
+          T.rx[re * kCache + lane] = c2;
+        }
+        if (lane == kCache) {
+          w.cbound[i] = ev;
+          T.rb[re] = ev;
+        }
+        if (lane == 0) {
+          w.cvalid[i] = 1;
+          T.rv[re] = 1;
+          T.rt[re] = (int)i;
+        }
+        double cv = -DBL_MAX;
+        int cj = INT32_MAX;
+        if (lane < kCache && ej != INT32_MAX && w.holder[ej] != mine) {
+          cj = ej;
+          cv = ev;
+        }
+        double kv;
+        int kj;
+        wave_best(cv, cj, 1, lane, kv, kj);
+        b1 = __shfl(kv, 0, 64);
+        b2 = __shfl(kv, 1, 64);
+        bj = __shfl(kj, 0, 64);
       }
     } else {
-      block_topk<K>(row, n, w, mine, true, sv, sj, outv, outj);
+      scan(i, mine);
+      b1 = outv[0];
+      b2 = outv[1];
+      bj = outj[0];
     }
-    const double v1 = outv[0], v2 = outv[1];
-    const int j1 = outj[0];
-    if (t == 0) {
-      int next = top - 1;
-      if (j1 != INT32_MAX) {
-        const double vref = (v2 > -DBL_MAX) ? v2 : v1;
-        const double inc = v1 - vref + eps;
-        float f = (float)inc;
-        if ((double)f > inc) f = nextafterf(f, 0.f);  // round down: keeps eps-CS
-        if (!(f > 0.f)) f = FLT_MIN;
-        const int e = j1 & (kTabCols - 1);
-        double p;
-        uint32_t h;
-        int own;
-        if (T.ct[e] == j1) {
-          p = T.cp[e];
-          h = T.ch[e];
-          own = T.co[e];
-        } else {
-          p = w.price[j1];
-          h = w.holder[j1];
-          own = w.owner[j1];
-        }
-        p += (double)f;
-        const int old = ((h & ~(uint32_t)(kMaxRows - 1)) == tag) ? own : -1;
-        if (old >= 0) {
-          w.assigned[old] = -1;  // displaced: bids next
-          stack[next++] = old;
-        } else {
-          atomicAdd(&w.ctl->unassigned, (unsigned long long)(-1ll));
-        }
-        T.ct[e] = j1;
-        T.cp[e] = p;
-        T.ch[e] = mine;
-        T.co[e] = s;
-        w.price[j1] = p;
-        w.owner[j1] = s;
-        w.holder[j1] = mine;
-        w.assigned[s] = j1;
-        w.assigned_ep[s] = ep;
+    // resolve on the spot (lane 0), the stack kept by the whole wave
+    int old = -1;
+    if (bj != INT32_MAX && lane == 0) {
+      const double vref = (b2 > -DBL_MAX) ? b2 : b1;
+      const double inc = b1 - vref + eps;
+      float f = (float)inc;
+      if ((double)f > inc) f = nextafterf(f, 0.f);  // round down: keeps eps-CS
+      if (!(f > 0.f)) f = FLT_MIN;
+      const int e = bj & (kTabCols - 1);
+      double p;
+      uint32_t h;
+      int own;
+      if (T.ct[e] == bj) {
+        p = T.cp[e];
+        h = T.ch[e];
+        own = T.co[e];
+      } else {
+        p = w.price[bj];
+        h = w.holder[bj];
+        own = w.owner[bj];
       }
-      sp = next;
-      __threadfence_block();
+      p += (double)f;
+      old = ((h & ~(uint32_t)(kMaxRows - 1)) == tag) ? own : -1;
+      if (old >= 0)
+        w.assigned[old] = -1;  // displaced: bids next
+      else
+        atomicAdd(&w.ctl->unassigned, (unsigned long long)(-1ll));
+      T.ct[e] = bj;
+      T.cp[e] = p;
+      T.ch[e] = mine;
+      T.co[e] = s;
+      w.price[bj] = p;
+      w.owner[bj] = s;
+      w.holder[bj] = mine;
+      w.assigned[s] = bj;
+      w.assigned_ep[s] = ep;
     }
-    __syncthreads();
+    old = __shfl(old, 0, 64);
+    if (bj != INT32_MAX) {
+      --sp;
+      if (old >= 0) {
+        if (lane == 0) stack[sp] = old;
+        ++sp;
+      }
+    } else {
+      --sp;  // no column to bid on (cannot happen with n slots = n columns)
+    }
+    __threadfence_block();  // the global writes before the next bid's (or a scan's) reads
+  }
+  // release the helpers
+  if (lane == 0) {
+    req = -1;
+    __hip_atomic_store(&seq, nseq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 }
 
@@ -993,10 +1021,10 @@ __global__ __launch_bounds__(256) void w2_grad_kernel(const float* __restrict__ 
 
 using namespace dsvgd;
 
-// phases keep the last plan's eps-CS slots (default on; off = every phase
-// and warm start re-assigns all slots -- the round-3 auction, kept for A/B)
+// phases keep the last plan's eps-CS slots (default off: every phase and
+// warm start re-assigns all slots; on measured slower warm, profiles/r11g)
 static bool& w2_keep_flag() {
-  static bool k = true;
+  static bool k = false;
   return k;
 }
 

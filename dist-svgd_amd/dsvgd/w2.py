@@ -28,8 +28,10 @@ class W2Term(object):
     # final eps; 0 = cold every step.  The first call on a workspace is cold.
     WARM_PHASES = None
     # a new epsilon phase (and the warm start's first) keeps the slots whose
-    # column still meets eps-CS (dsvgd_w2_set_keep); False: all re-bid
-    KEEP = True
+    # column still meets eps-CS (dsvgd_w2_set_keep); False: all re-bid.  Off:
+    # at m = 8192, n = 65536 the warm solve took 1.81 s with it against 79 ms
+    # without, the cold one 3.95 vs 4.04 s (profiles/r11g/w2.log)
+    KEEP = False
 
     def __init__(self, m, n, d, device, warm=True):
         if n % m:

@@ -573,7 +573,7 @@ int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
 int dsvgd_w2_assign_warm(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
                          int64_t max_rounds, const int32_t* prev_assign, int32_t* assign,
                          int64_t* rounds_out, void* stream);
-/* Process-wide switch of the auction's phase keep (default 1): a new
+/* Process-wide switch of the auction's phase keep (default 0): a new
  * epsilon phase, and dsvgd_w2_assign_warm's first phase with the previous
  * plan, keep every slot whose column still meets epsilon-complementary
  * slackness; 0 re-assigns every slot each phase.  Same optimality guarantee
