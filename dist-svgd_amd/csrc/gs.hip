@@ -445,7 +445,7 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
     const float* __restrict__ extra, int64_t lde, float* __restrict__ phi_out, int64_t ldphi,
     int score_kind, const float* __restrict__ mu, const float* __restrict__ lam,
     float score_scale, const float* __restrict__ xd, int64_t ldxd, const float* __restrict__ td,
-    int nd) {
+    int nd, int dbg) {
   extern __shared__ __attribute__((aligned(16))) float gsw_smem[];
   const bool refreshed = score_kind != 0;
   const int pitch = dp + 4;                       // 16-byte rows, 4 banks apart
@@ -513,13 +513,13 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
       ex[u] = n_ex[u];
     }
     const float qr = nqr;
-    if (i + 1 < B) prefetch(i + 1);
+    if (i + 1 < B && !(dbg & 1)) prefetch(i + 1);
     const float* xoi = xn + i * pitch;   // row i, still the old one
     // (a) distances of the old row i to the moved rows j < i: thread (j =
     // lane, quarter w) over features [w q4, (w + 1) q4)
     {
       float sa = 0.f, sb = 0.f;
-      if (lane < i) {
+      if (lane < i && !(dbg & 2)) {
         const float* pa = xoi + w * q4;
         const float* pb = xn + lane * pitch + w * q4;
         auto acc4 = [&](const f32x4& va, const f32x4& vb) {
@@ -553,8 +553,9 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
     float acc[kGswCols][2];
 #pragma unroll
     for (int u = 0; u < kGswCols; ++u) acc[u][0] = acc[u][1] = 0.f;
+    const int iw = (dbg & 4) ? 0 : i;   // (timing probe: no column loop)
     int j = 0;
-    for (; j + 8 <= i; j += 8) {
+    for (; j + 8 <= iw; j += 8) {
       float kk[8];
 #pragma unroll
       for (int r = 0; r < 8; ++r)
@@ -572,7 +573,7 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
         for (int r = 0; r < 8; ++r) acc[u][r & 1] = fmaf(kk[r], wv8[r], acc[u][r & 1]);
       }
     }
-    for (; j < i; ++j) {
+    for (; j < iw; ++j) {
       const float k0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(kb, j));
       rm += k0;
 #pragma unroll
@@ -723,6 +724,17 @@ int dsvgd_gs_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, int64_t n
   return check_launch("gs_sweep");
 }
 
+static int& gsw_debug_mask() {
+  static int m = 0;
+  return m;
+}
+
+int dsvgd_gsw_debug(int mask) {
+  const int old = gsw_debug_mask();
+  gsw_debug_mask() = mask;
+  return old;
+}
+
 int64_t dsvgd_gsw_block_rows(int64_t d, int score_kind) {
   if (d <= 0 || d > kGswMaxD) return 0;
   return gsw_rows(roundup(d, 32), score_kind != 0);
@@ -771,12 +783,12 @@ int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y
     hipLaunchKernelGGL(gsw_sweep_kernel<true>, dim3(1), dim3(256), smem, (hipStream_t)stream, X, ldx, S,
                      lds, Y, ldy, norms, center, n, (int)d, (int)dp, r0, (int)B, st, step, Q, ldq,
                      Qr, extra, lde, phi_out, ldphi, score_kind, mu, lam, score_scale, xd, ldxd,
-                     td, (int)(score_kind == 3 ? nd : 0));
+                     td, (int)(score_kind == 3 ? nd : 0), gsw_debug_mask());
   else
     hipLaunchKernelGGL(gsw_sweep_kernel<false>, dim3(1), dim3(256), smem, (hipStream_t)stream, X, ldx, S,
                      lds, Y, ldy, norms, center, n, (int)d, (int)dp, r0, (int)B, st, step, Q, ldq,
                      Qr, extra, lde, phi_out, ldphi, score_kind, mu, lam, score_scale, xd, ldxd,
-                     td, (int)(score_kind == 3 ? nd : 0));
+                     td, (int)(score_kind == 3 ? nd : 0), gsw_debug_mask());
   return check_launch("gsw_sweep");
 }
 

@@ -122,6 +122,7 @@ SIGNATURES = {
     "dsvgd_logreg_predict": (_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _p, _p]),
     # the wide blocked Gauss-Seidel sweep (ABI 4)
     "dsvgd_gsw_block_rows": (_i64, [_i64, _int]),
+    "dsvgd_gsw_debug": (_int, [_int]),
     "dsvgd_h2_rowsplit_rows_range": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _p, _p, _i64, _i64,
                                             _p]),
     "dsvgd_gs_mask": (_int, [_p, _i64, _i64, _i64, _p]),

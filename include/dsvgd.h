@@ -366,6 +366,10 @@ int dsvgd_sqdist_h2(const void* Yg, const float* norms, int64_t row0, int64_t m,
  * re-run per pair by distsampler.py:97-99), Y's row and norms[] kept current
  * (centre c = center, the packing centre of Y).  Any d <= 1024 for kind 3. */
 int64_t dsvgd_gsw_block_rows(int64_t d, int score_kind);  /* 0 if d > 1024 */
+/* Timing probe of the walk (scripts/walk_probe.py; results are garbage while
+ * set): bit 0 skips the next row's operand loads, bit 1 the distances, bit 2
+ * the column loop.  Process-wide; returns the previous mask.  0 = normal. */
+int dsvgd_gsw_debug(int mask);
 int dsvgd_gs_mask(float* D, int64_t ldd, int64_t r0, int64_t B, void* stream);
 int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y, int64_t ldy,
                           float* norms, const float* center, int64_t n, int64_t d, int64_t r0,

@@ -14,4 +14,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/w2prof -o run --outpu
 timeout -k 10 300 python -u scripts/seq_timing.py --only D,E --rows-sample 0 > $OUT/seq.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/seqprof -o run --output-format csv -- \
   python3 scripts/seq_timing.py --only D --rows-sample 0 > $OUT/seqprof.log 2>&1 || exit $?
+timeout -k 10 200 python -u scripts/walk_probe.py > $OUT/walk_probe.log 2>&1 || exit $?
 echo ALL DONE
