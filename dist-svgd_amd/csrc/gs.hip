@@ -454,7 +454,15 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
   float* wn = xn + (int64_t)B * pitch;            // [B][dp]: w_j = s_j' - g (x_j' - c)
   float* sn = wn + (int64_t)B * dp;               // [B][dp]: their scores (refreshed only)
   float* part = sn + (refreshed ? (int64_t)B * dp : 0);  // [4][64] partial distances
-  float* coef = part + 256;                       // [kGswCoef] logreg: the waves' partials
+  float* red = part + 256;                        // [js][dp] the column loop's j-group sums
+  float* redr = red + 1024;                       // [js] their kernel sums
+  float* coef = redr + 16;                        // [kGswCoef] logreg: the waves' partials
+  // dp % 256 == 0: the column loop over f32x4 column quads, the moved rows
+  // split over js = 1024 / dp wave groups (wave-uniform j: v_readlane)
+  const int nq = dp >> 2;
+  const bool quad = (dp & 255) == 0;
+  const int js = quad ? 1024 / dp : 1;
+  const int qd = (int)threadIdx.x % nq, jq = (int)threadIdx.x / nq;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const float inv_h = st->inv_h, g = 2.f * inv_h, scale = -inv_h * kLog2e;
   const float inv_n = 1.f / (float)n;
@@ -554,6 +562,47 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
 #pragma unroll
     for (int u = 0; u < kGswCols; ++u) acc[u][0] = acc[u][1] = 0.f;
     const int iw = (dbg & 4) ? 0 : i;   // (timing probe: no column loop)
+    if (quad) {
+      // thread (quad qd, group jq): sum_{j = jq mod js, j < i} k_j w_j[4 qd .. +3]
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+      float rp = 0.f;
+      if (jq < js) {
+        const float* wq = wn + 4 * qd;
+        int j = jq;
+        for (; j + 7 * js < iw; j += 8 * js) {
+          float kk[8];
+          f32x4 wv8[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            kk[r] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(kb, j + r * js));
+            wv8[r] = *reinterpret_cast<const f32x4*>(wq + (j + r * js) * dp);
+          }
+          rp += ((kk[0] + kk[1]) + (kk[2] + kk[3])) + ((kk[4] + kk[5]) + (kk[6] + kk[7]));
+#pragma unroll
+          for (int r = 0; r < 8; r += 2) {
+            a0 += kk[r] * wv8[r];
+            a1 += kk[r + 1] * wv8[r + 1];
+          }
+        }
+        for (; j < iw; j += js) {
+          const float k0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(kb, j));
+          rp += k0;
+          a0 += k0 * *reinterpret_cast<const f32x4*>(wq + j * dp);
+        }
+        *reinterpret_cast<f32x4*>(red + jq * dp + 4 * qd) = a0 + a1;
+        if (qd == 0) redr[jq] = rp;
+      }
+      gsw_barrier();                                                        // (1b)
+#pragma unroll
+      for (int u = 0; u < kGswCols; ++u) {
+        const int c = t + 256 * u;
+        if (c >= d) continue;
+        float sacc = 0.f;
+        for (int q = 0; q < js; ++q) sacc += red[q * dp + c];
+        acc[u][0] = sacc;
+      }
+      for (int q = 0; q < js; ++q) rm += redr[q];
+    } else {
     int j = 0;
     for (; j + 8 <= iw; j += 8) {
       float kk[8];
@@ -583,6 +632,7 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
         if (c >= d) continue;
         acc[u][0] = fmaf(k0, wn[j * dp + c], acc[u][0]);
       }
+    }
     }
     float xc_o[kGswCols];   // row i's old values (this thread's columns)
 #pragma unroll
@@ -773,7 +823,7 @@ int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y
   DSVGD_REQUIRE(!phi_out || ldphi >= d, "ldphi");
   const size_t smem =
       sizeof(float) * ((size_t)B * (dp + 4) + (size_t)B * dp * (score_kind != 0 ? 2 : 1) + 256 +
-                       (score_kind == 3 ? kGswCoef : 0));
+                       1024 + 16 + (score_kind == 3 ? kGswCoef : 0));
   const void* fn = score_kind == 3 ? reinterpret_cast<const void*>(&gsw_sweep_kernel<true>)
                                     : reinterpret_cast<const void*>(&gsw_sweep_kernel<false>);
   if (hipFuncSetAttribute(fn,
