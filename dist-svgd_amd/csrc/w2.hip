@@ -51,9 +51,11 @@ struct W2Ctl {
   unsigned long long viol;  // warm start: the previous plan's CS violation (fp64 bits, >= 0)
   int32_t tail;     // this round is the one-workgroup tail's (unassigned <= kTailMax)
   int32_t keep_on;  // phases keep the last plan's eps-CS slots (dsvgd_w2_set_keep)
+  double theta;     // eps divisor between phases (dsvgd_w2_set_theta; kTheta)
 };
 
 constexpr size_t kW2CtlBytes = 256;
+static_assert(sizeof(W2Ctl) <= kW2CtlBytes, "control block outgrew its slot");
 constexpr double kTheta = 8.0;
 constexpr int kRoundBatch = 16;
 constexpr int kTailMax = 64;  // the phase tail's unassigned slots (w2_tail_kernel)
@@ -214,13 +216,14 @@ __global__ __launch_bounds__(256) void w2_violation_kernel(const float* __restri
 // VERDICT r2 item 9).  Any initial prices give the same eps_final-optimality
 // guarantee.
 constexpr double kWarmDiv = 64.0;
-__global__ void w2_start_kernel(W2Ctl* ctl, int64_t n, int warm_phases, int keep) {
+__global__ void w2_start_kernel(W2Ctl* ctl, int64_t n, int warm_phases, int keep, double theta) {
+  ctl->theta = theta;
   const double cmax = (double)ctl->cmax;
   ctl->eps_final = fmax(cmax * 0x1p-24 / (double)n, cmax * 1e-13);
-  double e0 = cmax / kTheta;
+  double e0 = cmax / theta;
   if (warm_phases > 0) {
     double ew = ctl->eps_final;
-    for (int k = 0; k < warm_phases; ++k) ew *= kTheta;
+    for (int k = 0; k < warm_phases; ++k) ew *= theta;
     e0 = fmin(e0, ew);
   } else if (warm_phases < 0) {
     e0 = fmin(e0, __longlong_as_double((long long)ctl->viol) / kWarmDiv);
@@ -936,7 +939,7 @@ __device__ void w2_control(W2Ctl* ctl, int64_t n) {
     ctl->done = 1;
     return;
   }
-  ctl->eps = fmax(ctl->eps / kTheta, ctl->eps_final);
+  ctl->eps = fmax(ctl->eps / ctl->theta, ctl->eps_final);
   ctl->epoch += 1;
   ctl->phases += 1;
   ctl->unassigned = (unsigned long long)n;
@@ -1028,6 +1031,12 @@ static bool& w2_keep_flag() {
   return k;
 }
 
+// eps divisor between phases (default kTheta; A/B: dsvgd_w2_set_theta)
+static double& w2_theta() {
+  static double th = kTheta;
+  return th;
+}
+
 // the last dsvgd_w2_assign's progress on this host thread: (rounds, phase,
 // unassigned slots) at every control readback (kRoundBatch rounds apart)
 static std::vector<long long>& w2_trace() {
@@ -1047,6 +1056,12 @@ int64_t dsvgd_w2_trace(int64_t* out, int64_t cap) {
 int dsvgd_w2_set_keep(int keep) {
   const int old = w2_keep_flag() ? 1 : 0;
   w2_keep_flag() = keep != 0;
+  return old;
+}
+
+double dsvgd_w2_set_theta(double theta) {
+  const double old = w2_theta();
+  if (theta >= 2.0 && theta <= 1024.0) w2_theta() = theta;
   return old;
 }
 
@@ -1118,7 +1133,7 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
                        prev, w);
   // keep bit 0: phases keep eps-CS slots; bit 1: the first round keeps prev's
   hipLaunchKernelGGL(w2_start_kernel, dim3(1), dim3(1), 0, s, w.ctl, n, warm_phases,
-                     (keep ? 1 : 0) | ((prev && keep) ? 2 : 0));
+                     (keep ? 1 : 0) | ((prev && keep) ? 2 : 0), w2_theta());
   int rc = check_launch("w2_start");
   if (rc) return rc;
   const dim3 gb((unsigned)std::min<int64_t>(kBidBlocks, (m + 3) / 4));

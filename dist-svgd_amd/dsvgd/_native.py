@@ -16,6 +16,7 @@ _c = ctypes
 _p = _c.c_void_p
 _i64 = _c.c_int64
 _f = _c.c_float
+_f64 = _c.c_double
 _int = _c.c_int
 
 
@@ -107,6 +108,7 @@ SIGNATURES = {
     "dsvgd_w2_assign_warm": (_int, [_p, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p]),
     "dsvgd_w2_trace": (_i64, [_p, _i64]),
     "dsvgd_w2_set_keep": (_int, [_int]),
+    "dsvgd_w2_set_theta": (_f64, [_f64]),
     "dsvgd_w2_grad": (_int, [_p, _i64, _i64, _p, _i64, _i64, _i64, _p, _f, _p, _i64, _p]),
     "dsvgd_score_gaussian": (_int, [_p, _i64, _i64, _i64, _p, _p, _f, _p, _i64, _p]),
     "dsvgd_score_gmm": (_int, [_p, _i64, _i64, _i64, _f, _p, _i64, _p]),

@@ -32,6 +32,7 @@ class W2Term(object):
     # at m = 8192, n = 65536 the warm solve took 1.81 s with it against 79 ms
     # without, the cold one 3.95 vs 4.04 s (profiles/r11g/w2.log)
     KEEP = False
+    THETA = 8.0   # eps divisor between phases (dsvgd_w2_set_theta)
 
     def __init__(self, m, n, d, device, warm=True):
         if n % m:
@@ -56,6 +57,7 @@ class W2Term(object):
                N.ptr(self.C), self.n, s)
         rounds = ctypes.c_int64(0)
         N.load().dsvgd_w2_set_keep(int(bool(self.KEEP)))    # returns the old setting
+        N.load().dsvgd_w2_set_theta(float(self.THETA))
         if self.warm and self._solved and self.WARM_PHASES is None:
             # prev and out may alias: the plan is only written after the solve
             N.call("dsvgd_w2_assign_warm", N.ptr(self.C), self.n, self.m, self.n,

@@ -583,6 +583,9 @@ int dsvgd_w2_assign_warm(const float* C, int64_t ldc, int64_t m, int64_t n, void
  * slackness; 0 re-assigns every slot each phase.  Same optimality guarantee
  * either way.  Returns the previous setting. */
 int dsvgd_w2_set_keep(int keep);
+/* Process-wide epsilon divisor between the auction's phases (default 8;
+ * accepted in [2, 1024], otherwise ignored).  Returns the previous value. */
+double dsvgd_w2_set_theta(double theta);
 /* Progress of this host thread's last dsvgd_w2_assign: out[3k..3k+2] =
  * (rounds, epsilon phase, unassigned slots) at the k-th control readback
  * (every 16 rounds); copies min(count, cap) triples, returns count. */

@@ -93,7 +93,9 @@ def main():
                     help="m x n x d list, e.g. 8192x65536x256,2048x16384x256 (svgd shape)")
     ap.add_argument("--trace", action="store_true",
                     help="rounds per phase by unassigned-slot count")
-    ap.add_argument("--keep", default="1",
+    ap.add_argument("--theta", default="8",
+                    help="comma list of W2Term.THETA settings to sweep on --shapes")
+    ap.add_argument("--keep", default="0",
                     help="comma list of W2Term.KEEP settings to sweep on --shapes (1, 0)")
     ap.add_argument("--warm-phases", default=None,
                     help="comma list of warm phase counts to sweep on --shapes (a = adaptive)")
@@ -103,8 +105,10 @@ def main():
     if args.shapes:
         import dsvgd
         shapes = [tuple(int(v) for v in sh.split("x")) + ("svgd",) for sh in args.shapes.split(",")]
-        for keep in [bool(int(v)) for v in args.keep.split(",")]:
+        for keep, theta in [(bool(int(k)), float(th)) for k in args.keep.split(",")
+                            for th in args.theta.split(",")]:
             dsvgd.w2.W2Term.KEEP = keep
+            dsvgd.w2.W2Term.THETA = theta
             for ph in ([None if v == "a" else int(v) for v in args.warm_phases.split(",")]
                        if args.warm_phases else [dsvgd.w2.W2Term.WARM_PHASES]):
                 dsvgd.w2.W2Term.WARM_PHASES = ph
@@ -112,6 +116,7 @@ def main():
                     r = case(*sh)
                     r["warm_phases"] = ph
                     r["keep"] = keep
+                    r["theta"] = theta
                     print(json.dumps(r), flush=True)
         return
     if args.lib:
