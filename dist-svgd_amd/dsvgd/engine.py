@@ -144,6 +144,10 @@ class PhiEngine(object):
     # pair split: run the own window on a second stream beside the transposed
     # partials (the batched forward launch holds 192 of the 256 CUs)
     WINDOW_SIDE_STREAM = False
+    # pair split: the transposed partials left beside the batched forward
+    # launch (the antipodal half) run on a second stream next to it without
+    # split-K when both fit the 256 CUs together (S = 8: 192 + 32 or 64)
+    REST_BESIDE = True
 
     GEMMS = ("h2", "x3", "f32")
     DEFAULT_GEMM = "h2"
@@ -607,6 +611,14 @@ class PhiEngine(object):
                 z *= 2
             self.t_splits.append(z)
             smax = max(smax, z * q["mo"]) if z > 1 else smax
+        fwd_wg = nf * (self.m // 128) * (ldy // 512) if self.fwd_batched else 0
+        rest_wg = [(ldy // 512) * (q["mo"] // 128) for q in P.sends[nf:]]
+        self.rest_beside = bool(self.REST_BESIDE and self.fwd_batched and rest_wg
+                                and fwd_wg + sum(rest_wg) <= 256)
+        if self.rest_beside:
+            for k in range(nf, len(P.sends)):
+                self.t_splits[k] = 1
+        self._tside = None
         self.sendbuf = [msg(q["mo"]) for q in P.sends]
         if self.fwd_batched:   # the forward messages as views of the one buffer
             for k in range(nf):
@@ -656,21 +668,31 @@ class PhiEngine(object):
                        N.ptr(self.Yx), ldy, self.row0, self.m, (P.rank + 1) % P.S, P.S, nf,
                        self.n, self.state.ptr, N.ptr(self.send_fwd), ldy, self.fwd_msg, colinv,
                        guard, 0, s)
-            for q, z, buf in list(zip(P.sends, self.t_splits, self.sendbuf))[nf:]:
-                Dq = N.ptr(self.D) + 4 * q["row_off"] * self.n_pad
-                mo = q["mo"]
-                rs_out = N.ptr(buf) + 4 * mo * ldy
-                if z == 1:
-                    N.call("dsvgd_phi_h2_transposed", Dq, self.n_pad, N.ptr(self.Yx), ldy,
-                           self.row0 + q["row_off"], q["krows"], q["col0"], mo, self.n,
-                           self.state.ptr, 1, N.ptr(buf), ldy, rs_out, colinv, guard, 0, s)
-                else:
-                    N.call("dsvgd_phi_h2_transposed", Dq, self.n_pad, N.ptr(self.Yx), ldy,
-                           self.row0 + q["row_off"], q["krows"], q["col0"], mo, self.n,
-                           self.state.ptr, z, N.ptr(self.tP), ldy, N.ptr(self.tRS), colinv,
-                           guard, 0, s)
-                    N.call("dsvgd_phi_partial_reduce", N.ptr(self.tP), ldy, N.ptr(self.tRS), z,
-                           mo, ldy, N.ptr(buf), ldy, rs_out, s)
+            beside = bool(nf) and self.rest_beside
+            main = torch.cuda.current_stream(self.device)
+            if beside:
+                if self._tside is None:
+                    self._tside = torch.cuda.Stream(device=self.device)
+                self._tside.wait_stream(main)     # behind ysplit only
+            with torch.cuda.stream(self._tside if beside else main):
+                sr = N.stream(self.device)
+                for q, z, buf in list(zip(P.sends, self.t_splits, self.sendbuf))[nf:]:
+                    Dq = N.ptr(self.D) + 4 * q["row_off"] * self.n_pad
+                    mo = q["mo"]
+                    rs_out = N.ptr(buf) + 4 * mo * ldy
+                    if z == 1:
+                        N.call("dsvgd_phi_h2_transposed", Dq, self.n_pad, N.ptr(self.Yx), ldy,
+                               self.row0 + q["row_off"], q["krows"], q["col0"], mo, self.n,
+                               self.state.ptr, 1, N.ptr(buf), ldy, rs_out, colinv, guard, 0, sr)
+                    else:
+                        N.call("dsvgd_phi_h2_transposed", Dq, self.n_pad, N.ptr(self.Yx), ldy,
+                               self.row0 + q["row_off"], q["krows"], q["col0"], mo, self.n,
+                               self.state.ptr, z, N.ptr(self.tP), ldy, N.ptr(self.tRS), colinv,
+                               guard, 0, sr)
+                        N.call("dsvgd_phi_partial_reduce", N.ptr(self.tP), ldy, N.ptr(self.tRS),
+                               z, mo, ldy, N.ptr(buf), ldy, rs_out, sr)
+            if beside:
+                main.wait_stream(self._tside)     # every partial before the exchange
         join = None
         if p2p is not None:
             with span(self.timer, "partials_post"):

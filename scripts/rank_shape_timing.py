@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--shards", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--lib", default=None, help="an A/B build of the library (make ab)")
+    ap.add_argument("--rest", default="1",
+                    help="pairs: comma list of PhiEngine.REST_BESIDE settings (1, 0)")
     ap.add_argument("--side", default="0",
                     help="pairs: comma list of PhiEngine.WINDOW_SIDE_STREAM settings (0, 1)")
     ap.add_argument("--layout", default="both", choices=["rows", "pairs", "both"],
@@ -41,12 +43,14 @@ def main():
     for S in [int(v) for v in args.shards.split(",")]:
         for lay in (("rows", "pairs") if args.layout == "both" else (args.layout,)):
             if lay == "rows":
-                runs.append((S, lay, False))
+                runs.append((S, lay, False, True))
             elif S > 1 and dsvgd.PhiEngine.pair_split_ok(n, d, S):
                 for side in args.side.split(","):
-                    runs.append((S, lay, bool(int(side))))
-    for S, lay, side in runs:
+                    for rest in args.rest.split(","):
+                        runs.append((S, lay, bool(int(side)), bool(int(rest))))
+    for S, lay, side, *rest in runs:
         dsvgd.PhiEngine.WINDOW_SIDE_STREAM = side
+        dsvgd.PhiEngine.REST_BESIDE = rest[0] if rest else True
         m, r = n // S, S // 2          # a middle rank (a high one of the pair split)
         per = Ng // S
         tgt = dsvgd.targets.LogisticRegression(x[r * per:(r + 1) * per], t[r * per:(r + 1) * per])
@@ -95,7 +99,9 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         st = {k: round(float(np.mean(v)), 3) for k, v in timer.summary().items()}
-        print(json.dumps({"shards": S, "layout": lay + ("+side" if side else ""), "m": m,
+        print(json.dumps({"shards": S, "layout": lay + ("+side" if side else "")
+                          + ("+rest" if lay == "pairs" and eng.plan is not None
+                             and eng.rest_beside else ""), "m": m,
                           "row0": r * m, "N_local": per,
                           "ms_per_step_no_comm": e0.elapsed_time(e1) / args.steps,
                           "sym_layout": bool(eng.sym), "stages_ms": st}), flush=True)
