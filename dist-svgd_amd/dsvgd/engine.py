@@ -145,9 +145,11 @@ class PhiEngine(object):
     # partials (the batched forward launch holds 192 of the 256 CUs)
     WINDOW_SIDE_STREAM = False
     # pair split: the transposed partials left beside the batched forward
-    # launch (the antipodal half) run on a second stream next to it without
-    # split-K when both fit the 256 CUs together (S = 8: 192 + 32 or 64)
-    REST_BESIDE = True
+    # launch (the antipodal half) on a second stream next to it without
+    # split-K when both fit the 256 CUs together (S = 8: 192 + 32 or 64).
+    # Off: measured slower, partials 0.98-1.00 vs 0.78 ms at S = 8 in one
+    # process (profiles/r11m/rank_rest.log)
+    REST_BESIDE = False
 
     GEMMS = ("h2", "x3", "f32")
     DEFAULT_GEMM = "h2"
