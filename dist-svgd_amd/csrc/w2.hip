@@ -81,7 +81,11 @@ __device__ __forceinline__ uint32_t w2_tag(int ep) { return (uint32_t)(ep & 0x7f
 // R - u columns, so its u + 1 best non-held are among its R + 1 best overall
 // (R + 1 <= kCache).  Otherwise it rescans and refills.  valid[i] = 0 after
 // the workspace memset of every solve (costs change between solves).
-constexpr int kCache = 16;
+// 32 (round 4; was 16): a tail bid that misses the cache rescans a whole
+// cost row (~1 MB, one workgroup); in a price war the cached second best
+// falls below the bound after far fewer bids with 16 columns (profiles/r11i:
+// the tail's launches averaged ~160 ms, ~9 us per bid)
+constexpr int kCache = 32;
 constexpr int kCacheMaxR = 8;
 
 struct W2Ws {
