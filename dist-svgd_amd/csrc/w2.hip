@@ -81,11 +81,9 @@ __device__ __forceinline__ uint32_t w2_tag(int ep) { return (uint32_t)(ep & 0x7f
 // R - u columns, so its u + 1 best non-held are among its R + 1 best overall
 // (R + 1 <= kCache).  Otherwise it rescans and refills.  valid[i] = 0 after
 // the workspace memset of every solve (costs change between solves).
-// 32 (round 4; was 16): a tail bid that misses the cache rescans a whole
-// cost row (~1 MB, one workgroup); in a price war the cached second best
-// falls below the bound after far fewer bids with 16 columns (profiles/r11i:
-// the tail's launches averaged ~160 ms, ~9 us per bid)
-constexpr int kCache = 32;
+// 16 columns (32 measured the same: the tail's cost is not its rescans,
+// profiles/r11n)
+constexpr int kCache = 16;
 constexpr int kCacheMaxR = 8;
 
 struct W2Ws {
@@ -493,7 +491,7 @@ __device__ __forceinline__ bool w2_has_prev(int64_t i, int64_t R, int lane, int 
 // over a few columns then runs out of LDS.
 constexpr int kTailBids = 16384;
 constexpr int kTabCols = 4096;  // column entries: price, holder, owner, tag
-constexpr int kTabRows = 256;   // row entries: the price cache of a row
+constexpr int kTabRows = 512;   // row entries: the price cache of a row
 constexpr size_t kTailLds =
     (size_t)kTabCols * (8 + 4 + 4 + 4) + (size_t)kTabRows * (8 + 4 + 4 + kCache * 8);
 
@@ -578,6 +576,7 @@ __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ 
   // wave 0: the bids
   int nseq = 0;
   auto scan = [&](int64_t i, uint32_t mine) {  // post row i, scan it with the helpers
+    __threadfence_block();  // this wave's price / holder writes before the helpers read
     if (lane == 0) {
       req = i;
       __hip_atomic_store(&seq, ++nseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -735,7 +734,8 @@ __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ 
     } else {
       --sp;  // no column to bid on (cannot happen with n slots = n columns)
     }
-    __threadfence_block();  // the global writes before the next bid's (or a scan's) reads
+    // (no fence per bid: this wave's own later reads of these words are in
+    // order after its writes; the helpers get one in scan())
   }
   // release the helpers
   if (lane == 0) {

@@ -1,9 +1,9 @@
 #!/bin/bash
-# the W2 price cache at 32 columns: parity (plans vs scipy / golden LP),
+# the W2 tail without a fence per bid, 512 cached rows: parity (plans vs scipy / golden LP),
 # timing, and the per-solve kernel trace
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r11n
+OUT=gpurun_out/r11o
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dist.py -m gpu -v -x \
   --timeout 300 --timeout-method thread -k "w2 or wasserstein" \
