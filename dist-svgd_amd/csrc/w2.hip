@@ -52,6 +52,7 @@ struct W2Ctl {
   int32_t tail;     // this round is the one-workgroup tail's (unassigned <= kTailMax)
   int32_t keep_on;  // phases keep the last plan's eps-CS slots (dsvgd_w2_set_keep)
   double theta;     // eps divisor between phases (dsvgd_w2_set_theta; kTheta)
+  unsigned long long tail_bids, tail_scans;  // the tails' work (dsvgd_w2_tail_stats)
 };
 
 constexpr size_t kW2CtlBytes = 256;
@@ -586,7 +587,9 @@ __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ 
     block_topk<KS>(C + i * ldc, n, w, mine, !CACHED, sv, sj, outv, outj);
   };
   int sp = c0;
+  int nbids = 0;
   for (int b = 0; b < kTailBids && sp > 0; ++b) {
+    ++nbids;
     const int s = stack[sp - 1];
     const int64_t i = s / R;
     const uint32_t mine = tag | (uint32_t)i;
@@ -594,6 +597,10 @@ __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ 
     double b1 = -DBL_MAX, b2 = -DBL_MAX;
     int bj = INT32_MAX;
     bool hit = false;
+    double pj = 0.0;   // the bid column's price / holder / owner, when read already
+    uint32_t hj = 0;
+    int oj = -1;
+    bool have_j = false;
     if (CACHED) {  // the row's cache (table, else global + install), its bid
       const int re = (int)(i & (kTabRows - 1));
       int valid, c = INT32_MAX;
@@ -624,16 +631,21 @@ __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ 
       if (valid) {
         double cv = -DBL_MAX;
         int cj = INT32_MAX;
+        double p = 0.0;
+        uint32_t hd = 0;
+        int own = -1;
         if (lane < kCache && c != INT32_MAX) {
+          // price, holder and owner together: the resolve below needs no
+          // read of its own when the bid is the cache's (one round trip less)
           const int e = c & (kTabCols - 1);
-          double p;
-          uint32_t hd;
           if (T.ct[e] == c) {
             p = T.cp[e];
             hd = T.ch[e];
+            own = T.co[e];
           } else {
             p = w.price[c];
             hd = w.holder[c];
+            own = w.owner[c];
           }
           if (hd != mine) {  // held columns never bid
             cj = c;
@@ -647,6 +659,14 @@ __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ 
         b2 = __shfl(kv, 1, 64);
         bj = __shfl(kj, 0, 64);
         hit = b2 >= bound;
+        if (hit && bj != INT32_MAX) {
+          const unsigned long long at = __ballot(c == bj && lane < kCache);
+          const int L = __ffsll((long long)at) - 1;
+          pj = __shfl(p, L, 64);
+          hj = (uint32_t)__shfl((int)hd, L, 64);
+          oj = __shfl(own, L, 64);
+          have_j = true;
+        }
       }
       if (!hit) {  // full scan over all columns, refill the cache (global + table)
         scan(i, mine);
@@ -699,7 +719,11 @@ __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ 
       double p;
       uint32_t h;
       int own;
-      if (T.ct[e] == bj) {
+      if (have_j) {
+        p = pj;
+        h = hj;
+        own = oj;
+      } else if (T.ct[e] == bj) {
         p = T.cp[e];
         h = T.ch[e];
         own = T.co[e];
@@ -737,8 +761,10 @@ __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ 
     // (no fence per bid: this wave's own later reads of these words are in
     // order after its writes; the helpers get one in scan())
   }
-  // release the helpers
+  // the launch's work, then release the helpers
   if (lane == 0) {
+    atomicAdd(&w.ctl->tail_bids, (unsigned long long)nbids);
+    atomicAdd(&w.ctl->tail_scans, (unsigned long long)nseq);
     req = -1;
     __hip_atomic_store(&seq, nseq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
@@ -1035,6 +1061,12 @@ static bool& w2_keep_flag() {
   return k;
 }
 
+// the last dsvgd_w2_assign's tail work on this host thread: (bids, scans)
+static long long* w2_tail_stats() {
+  static thread_local long long st[2] = {0, 0};
+  return st;
+}
+
 // eps divisor between phases (default kTheta; A/B: dsvgd_w2_set_theta)
 static double& w2_theta() {
   static double th = kTheta;
@@ -1061,6 +1093,14 @@ int dsvgd_w2_set_keep(int keep) {
   const int old = w2_keep_flag() ? 1 : 0;
   w2_keep_flag() = keep != 0;
   return old;
+}
+
+int64_t dsvgd_w2_tail_stats(int64_t* out) {
+  if (out) {
+    out[0] = w2_tail_stats()[0];
+    out[1] = w2_tail_stats()[1];
+  }
+  return 2;
 }
 
 double dsvgd_w2_set_theta(double theta) {
@@ -1213,6 +1253,8 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
     }
     h = hbuf[(batch - 1) & 1];
     w2_trace().insert(w2_trace().end(), {h.rounds, h.phases, (long long)h.unassigned});
+    w2_tail_stats()[0] = (long long)h.tail_bids;
+    w2_tail_stats()[1] = (long long)h.tail_scans;
     if (h.done) break;
     if ((batch - 1) * kRoundBatch >= max_rounds) {
       set_error("dsvgd_w2_assign: no convergence after %lld rounds (%lld phases, %llu unassigned)",

@@ -73,6 +73,12 @@ class W2Term(object):
                N.ptr(self.assign), float(h), N.ptr(self.G), self.d, s)
         return self.G
 
+    def tail_stats(self):
+        """The last solve's phase tails: (bids, full row scans)."""
+        buf = (ctypes.c_int64 * 2)()
+        N.load().dsvgd_w2_tail_stats(buf)
+        return int(buf[0]), int(buf[1])
+
     def trace(self):
         """The last solve's progress: (rounds, phase, unassigned) every 16 rounds."""
         k = int(N.load().dsvgd_w2_trace(None, 0))

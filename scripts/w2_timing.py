@@ -55,6 +55,7 @@ def case(m, n, d, kind, seed=0):
         key = "warm" if warm else "cold"
         out[key + "_next_ms"] = round((time.perf_counter() - t) * 1e3, 3)
         out[key + "_next_rounds"] = ww.rounds
+        out[key + "_next_tail_bids_scans"] = ww.tail_stats()
         cost = float(((X2[torch.arange(n, device="cuda") // (n // m)] - P2[ww.assign.long()]) ** 2)
                      .sum())
         out[key + "_next_cost"] = cost
