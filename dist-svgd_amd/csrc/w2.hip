@@ -298,7 +298,7 @@ struct TopK {
 // profiles/r8j); here the workgroup's 256 threads take columns t, t + 256,
 // ... with four columns' loads in flight each, then the four waves' top-K
 // lists are merged.  Same values and the same tie rule (lower column first).
-constexpr int kScanUnroll = 4;
+constexpr int kScanUnroll = 8;
 
 // Wave w's K best of its lanes' lists (lane k < K: the k-th) into sv / sj
 // [w K + k]; every lane's list is sorted descending, columns unique.
@@ -335,20 +335,46 @@ __device__ void block_topk(const float* __restrict__ row, int64_t n, const W2Ws&
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   TopK<K> tk;
   tk.init();
+  // batches of U columns per thread, double-buffered: the next batch's loads
+  // are in flight while this one is pushed (2 U loads of each array per
+  // thread outstanding; a lone workgroup -- the phase tail -- reading other
+  // XCDs' writes was latency-bound at 4: ~130 us per scan, profiles/r11p)
+  constexpr int U = kScanUnroll;
+  const int64_t step = (int64_t)U * 256;
   int64_t j = t;
-  for (; j + (kScanUnroll - 1) * 256 < n; j += kScanUnroll * 256) {
-    float c[kScanUnroll];
-    double p[kScanUnroll];
-    uint32_t h[kScanUnroll];
+  if (j + (U - 1) * 256 < n) {
+    float c0[U], c1[U];
+    double p0[U], p1[U];
+    uint32_t h0[U], h1[U];
+    auto load = [&](float (&c)[U], double (&p)[U], uint32_t (&h)[U], int64_t jj) {
 #pragma unroll
-    for (int u = 0; u < kScanUnroll; ++u) {
-      c[u] = row[j + u * 256];
-      p[u] = w.price[j + u * 256];
-      h[u] = skip_held ? w.holder[j + u * 256] : 0u;
+      for (int u = 0; u < U; ++u) {
+        c[u] = row[jj + u * 256];
+        p[u] = w.price[jj + u * 256];
+        h[u] = skip_held ? w.holder[jj + u * 256] : 0u;
+      }
+    };
+    auto push = [&](const float (&c)[U], const double (&p)[U], const uint32_t (&h)[U],
+                    int64_t jj) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (!skip_held || h[u] != mine) tk.push(-(double)c[u] - p[u], (int)(jj + u * 256));
+    };
+    load(c0, p0, h0, j);
+    for (;;) {
+      const int64_t j1 = j + step;
+      const bool more1 = j1 + (U - 1) * 256 < n;
+      if (more1) load(c1, p1, h1, j1);
+      push(c0, p0, h0, j);
+      j = j1;
+      if (!more1) break;
+      const int64_t j2 = j + step;
+      const bool more2 = j2 + (U - 1) * 256 < n;
+      if (more2) load(c0, p0, h0, j2);
+      push(c1, p1, h1, j);
+      j = j2;
+      if (!more2) break;
     }
-#pragma unroll
-    for (int u = 0; u < kScanUnroll; ++u)
-      if (!skip_held || h[u] != mine) tk.push(-(double)c[u] - p[u], (int)(j + u * 256));
   }
   for (; j < n; j += 256)
     if (!skip_held || w.holder[j] != mine) tk.push(-(double)row[j] - w.price[j], (int)j);

@@ -1,8 +1,8 @@
 #!/bin/bash
-# W2 tail work counters (bids, scans) and the cached resolve without a read
+# W2 scans double-buffered, eight columns per thread per batch
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r11p
+OUT=gpurun_out/r11q
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dist.py -m gpu -v -x \
   --timeout 300 --timeout-method thread -k "w2 or wasserstein" \
