@@ -328,10 +328,11 @@ __device__ __forceinline__ void wave_topk_to_lds(TopK<K>& t, int lane, int wv, d
 // The workgroup's K best (value, column) of -C_ij - p_j over the columns j
 // the row does not hold (skip_held) or over all columns, sorted descending,
 // into out_v / out_j [K] (LDS, visible to the whole block on return).
-template <int K>
-__device__ void block_topk(const float* __restrict__ row, int64_t n, const W2Ws& w,
+template <int K, int NW = 4>
+__device__ __forceinline__ void block_topk(const float* __restrict__ row, int64_t n, const W2Ws& w,
                            uint32_t mine, bool skip_held, double* sv, int* sj, double* out_v,
                            int* out_j) {
+  constexpr int NT = NW * 64;   // the workgroup's threads
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   TopK<K> tk;
   tk.init();
@@ -340,54 +341,56 @@ __device__ void block_topk(const float* __restrict__ row, int64_t n, const W2Ws&
   // thread outstanding; a lone workgroup -- the phase tail -- reading other
   // XCDs' writes was latency-bound at 4: ~130 us per scan, profiles/r11p)
   constexpr int U = kScanUnroll;
-  const int64_t step = (int64_t)U * 256;
+  const int64_t step = (int64_t)U * NT;
   int64_t j = t;
-  if (j + (U - 1) * 256 < n) {
+  if (j + (U - 1) * NT < n) {
     float c0[U], c1[U];
     double p0[U], p1[U];
     uint32_t h0[U], h1[U];
     auto load = [&](float (&c)[U], double (&p)[U], uint32_t (&h)[U], int64_t jj) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        c[u] = row[jj + u * 256];
-        p[u] = w.price[jj + u * 256];
-        h[u] = skip_held ? w.holder[jj + u * 256] : 0u;
+        c[u] = row[jj + u * NT];
+        p[u] = w.price[jj + u * NT];
+        h[u] = skip_held ? w.holder[jj + u * NT] : 0u;
       }
     };
     auto push = [&](const float (&c)[U], const double (&p)[U], const uint32_t (&h)[U],
                     int64_t jj) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (!skip_held || h[u] != mine) tk.push(-(double)c[u] - p[u], (int)(jj + u * 256));
+        if (!skip_held || h[u] != mine) tk.push(-(double)c[u] - p[u], (int)(jj + u * NT));
     };
     load(c0, p0, h0, j);
     for (;;) {
       const int64_t j1 = j + step;
-      const bool more1 = j1 + (U - 1) * 256 < n;
+      const bool more1 = j1 + (U - 1) * NT < n;
       if (more1) load(c1, p1, h1, j1);
       push(c0, p0, h0, j);
       j = j1;
       if (!more1) break;
       const int64_t j2 = j + step;
-      const bool more2 = j2 + (U - 1) * 256 < n;
+      const bool more2 = j2 + (U - 1) * NT < n;
       if (more2) load(c0, p0, h0, j2);
       push(c1, p1, h1, j);
       j = j2;
       if (!more2) break;
     }
   }
-  for (; j < n; j += 256)
+  for (; j < n; j += NT)
     if (!skip_held || w.holder[j] != mine) tk.push(-(double)row[j] - w.price[j], (int)j);
   wave_topk_to_lds<K>(tk, lane, wv, sv, sj);
   __syncthreads();
-  if (t == 0) {  // merge the four sorted lists
-    int pos[4] = {0, 0, 0, 0};
+  if (t == 0) {  // merge the NW sorted lists
+    int pos[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) pos[q] = 0;
     for (int k = 0; k < K; ++k) {
       int bq = -1;
       double bv = -DBL_MAX;
       int bj = INT32_MAX;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < NW; ++q) {
         if (pos[q] >= K) continue;
         const double v = sv[q * K + pos[q]];
         const int jj = sj[q * K + pos[q]];
@@ -399,7 +402,8 @@ __device__ void block_topk(const float* __restrict__ row, int64_t n, const W2Ws&
       }
       out_v[k] = bv;
       out_j[k] = bj;
-      ++pos[bq];
+#pragma unroll
+      for (int q = 0; q < NW; ++q) pos[q] += q == bq;   // (registers: no dynamic index)
     }
   }
   __syncthreads();
@@ -517,6 +521,10 @@ __device__ __forceinline__ bool w2_has_prev(int64_t i, int64_t R, int lane, int 
 // launch read global memory, which is therefore always current): a price war
 // over a few columns then runs out of LDS.
 constexpr int kTailBids = 16384;
+// eight waves: the scans are one workgroup's reads of other XCDs' writes,
+// latency-bound -- twice the waves, twice the loads in flight
+constexpr int kTailWaves = 8;
+constexpr int kTailThreads = kTailWaves * 64;
 constexpr int kTabCols = 4096;  // column entries: price, holder, owner, tag
 constexpr int kTabRows = 512;   // row entries: the price cache of a row
 constexpr size_t kTailLds =
@@ -549,12 +557,12 @@ struct TailTab {
 // between polls), read the row wave 0 posted and run block_topk with it, all
 // four reaching its barriers together.
 template <int K, bool CACHED>
-__global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ C, int64_t ldc,
+__global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __restrict__ C, int64_t ldc,
                                                       int64_t n, int64_t R, W2Ws w) {
   extern __shared__ __attribute__((aligned(16))) char w2_tail_lds[];
   constexpr int KS = CACHED ? kCache + 1 : K;  // the scans' list length
-  __shared__ double sv[4 * KS], outv[KS];
-  __shared__ int sj[4 * KS], outj[KS];
+  __shared__ double sv[kTailWaves * KS], outv[KS];
+  __shared__ int sj[kTailWaves * KS], outj[KS];
   __shared__ int stack[kTailMax], sorted[kTailMax];
   __shared__ int cnt, seq;
   __shared__ long long req;  // the row to scan, or -1: the tail is over
@@ -565,14 +573,14 @@ __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ 
   const double eps = ctl->eps;
   const uint32_t tag = w2_tag(ep);
   TailTab T(w2_tail_lds);
-  for (int e = t; e < kTabCols; e += 256) T.ct[e] = -1;
-  for (int e = t; e < kTabRows; e += 256) T.rt[e] = -1;
+  for (int e = t; e < kTabCols; e += kTailThreads) T.ct[e] = -1;
+  for (int e = t; e < kTabRows; e += kTailThreads) T.rt[e] = -1;
   if (t == 0) {
     cnt = 0;
     seq = 0;
   }
   __syncthreads();
-  for (int64_t s0 = t; s0 < n; s0 += 256)
+  for (int64_t s0 = t; s0 < n; s0 += kTailThreads)
     if (!(w.assigned_ep[s0] == ep && w.assigned[s0] >= 0)) {
       const int pos = atomicAdd(&cnt, 1);
       if (pos < kTailMax) stack[pos] = (int)s0;
@@ -597,7 +605,7 @@ __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ 
       last = sq;
       const long long rq = req;
       if (rq < 0) return;
-      block_topk<KS>(C + rq * ldc, n, w, tag | (uint32_t)rq, !CACHED, sv, sj, outv, outj);
+      block_topk<KS, kTailWaves>(C + rq * ldc, n, w, tag | (uint32_t)rq, !CACHED, sv, sj, outv, outj);
     }
   }
   // wave 0: the bids
@@ -610,7 +618,7 @@ __global__ __launch_bounds__(256) void w2_tail_kernel(const float* __restrict__ 
     } else {
       ++nseq;
     }
-    block_topk<KS>(C + i * ldc, n, w, mine, !CACHED, sv, sj, outv, outj);
+    block_topk<KS, kTailWaves>(C + i * ldc, n, w, mine, !CACHED, sv, sj, outv, outj);
   };
   int sp = c0;
   int nbids = 0;
@@ -1222,14 +1230,15 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
   auto bid = [&]() {
     if (cached) {
       hipLaunchKernelGGL(w2_bid_cached_kernel, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
-      hipLaunchKernelGGL((w2_tail_kernel<2, true>), dim3(1), dim3(256), kTailLds, s, C, ldc, n, R,
+      hipLaunchKernelGGL((w2_tail_kernel<2, true>), dim3(1), dim3(kTailThreads), kTailLds, s, C,
+                         ldc, n, R,
                          w);
       return;
     }
 #define DSVGD_W2_BID(KK)                                                                       \
   do {                                                                                         \
     hipLaunchKernelGGL(w2_bid_kernel<KK>, gb, dim3(256), 0, s, C, ldc, m, n, R, w);            \
-    hipLaunchKernelGGL((w2_tail_kernel<KK, false>), dim3(1), dim3(256), kTailLds, s, C, ldc, n, \
+    hipLaunchKernelGGL((w2_tail_kernel<KK, false>), dim3(1), dim3(kTailThreads), kTailLds, s, C, ldc, n, \
                        R, w);                                                                  \
   } while (0)
     if (R <= 1)

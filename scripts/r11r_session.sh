@@ -1,8 +1,8 @@
 #!/bin/bash
-# W2 scans double-buffered, eight columns per thread per batch
+# W2 tail with eight waves (scans twice the loads in flight), W2Ws kept out of scratch
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r11q
+OUT=gpurun_out/r11r
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dist.py -m gpu -v -x \
   --timeout 300 --timeout-method thread -k "w2 or wasserstein" \
