@@ -328,7 +328,7 @@ __device__ __forceinline__ void wave_topk_to_lds(TopK<K>& t, int lane, int wv, d
 // The workgroup's K best (value, column) of -C_ij - p_j over the columns j
 // the row does not hold (skip_held) or over all columns, sorted descending,
 // into out_v / out_j [K] (LDS, visible to the whole block on return).
-template <int K, int NW = 4>
+template <int K, int NW = 4, int U = kScanUnroll>
 __device__ __forceinline__ void block_topk(const float* __restrict__ row, int64_t n, const W2Ws& w,
                            uint32_t mine, bool skip_held, double* sv, int* sj, double* out_v,
                            int* out_j) {
@@ -340,7 +340,6 @@ __device__ __forceinline__ void block_topk(const float* __restrict__ row, int64_
   // are in flight while this one is pushed (2 U loads of each array per
   // thread outstanding; a lone workgroup -- the phase tail -- reading other
   // XCDs' writes was latency-bound at 4: ~130 us per scan, profiles/r11p)
-  constexpr int U = kScanUnroll;
   const int64_t step = (int64_t)U * NT;
   int64_t j = t;
   if (j + (U - 1) * NT < n) {
@@ -525,6 +524,9 @@ constexpr int kTailBids = 16384;
 // latency-bound -- twice the waves, twice the loads in flight
 constexpr int kTailWaves = 8;
 constexpr int kTailThreads = kTailWaves * 64;
+// the cached tail's scans' batch (x2 in flight, double-buffered); the
+// uncached tails (R = 1, R > 8) read the holders too and keep kScanUnroll
+constexpr int kTailUnroll = 16;
 constexpr int kTabCols = 4096;  // column entries: price, holder, owner, tag
 constexpr int kTabRows = 512;   // row entries: the price cache of a row
 constexpr size_t kTailLds =
@@ -605,7 +607,7 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
       last = sq;
       const long long rq = req;
       if (rq < 0) return;
-      block_topk<KS, kTailWaves>(C + rq * ldc, n, w, tag | (uint32_t)rq, !CACHED, sv, sj, outv, outj);
+      block_topk<KS, kTailWaves, CACHED ? kTailUnroll : kScanUnroll>(C + rq * ldc, n, w, tag | (uint32_t)rq, !CACHED, sv, sj, outv, outj);
     }
   }
   // wave 0: the bids
@@ -618,7 +620,7 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
     } else {
       ++nseq;
     }
-    block_topk<KS, kTailWaves>(C + i * ldc, n, w, mine, !CACHED, sv, sj, outv, outj);
+    block_topk<KS, kTailWaves, CACHED ? kTailUnroll : kScanUnroll>(C + i * ldc, n, w, mine, !CACHED, sv, sj, outv, outj);
   };
   int sp = c0;
   int nbids = 0;

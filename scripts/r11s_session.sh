@@ -1,8 +1,8 @@
 #!/bin/bash
-# W2 tail with eight waves (scans twice the loads in flight), W2Ws kept out of scratch
+# W2 cached tail scans in batches of 16 columns per thread
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r11r
+OUT=gpurun_out/r11s
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dist.py -m gpu -v -x \
   --timeout 300 --timeout-method thread -k "w2 or wasserstein" \
