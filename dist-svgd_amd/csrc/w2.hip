@@ -331,7 +331,7 @@ __device__ __forceinline__ void wave_topk_to_lds(TopK<K>& t, int lane, int wv, d
 template <int K, int NW = 4, int U = kScanUnroll>
 __device__ __forceinline__ void block_topk(const float* __restrict__ row, int64_t n, const W2Ws& w,
                            uint32_t mine, bool skip_held, double* sv, int* sj, double* out_v,
-                           int* out_j) {
+                           int* out_j, double floor = -DBL_MAX) {
   constexpr int NT = NW * 64;   // the workgroup's threads
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   TopK<K> tk;
@@ -358,7 +358,14 @@ __device__ __forceinline__ void block_topk(const float* __restrict__ row, int64_
                     int64_t jj) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (!skip_held || h[u] != mine) tk.push(-(double)c[u] - p[u], (int)(jj + u * NT));
+        if (!skip_held || h[u] != mine) {
+          // floor: a value at or below the K-th best overall (the caller
+          // knows K such values); below it nothing can enter the list, so
+          // most lanes skip the insertion (a wave pays for one whenever any
+          // of its lanes inserts)
+          const double x = -(double)c[u] - p[u];
+          if (x >= floor) tk.push(x, (int)(jj + u * NT));
+        }
     };
     load(c0, p0, h0, j);
     for (;;) {
@@ -377,7 +384,10 @@ __device__ __forceinline__ void block_topk(const float* __restrict__ row, int64_
     }
   }
   for (; j < n; j += NT)
-    if (!skip_held || w.holder[j] != mine) tk.push(-(double)row[j] - w.price[j], (int)j);
+    if (!skip_held || w.holder[j] != mine) {
+      const double x = -(double)row[j] - w.price[j];
+      if (x >= floor) tk.push(x, (int)j);
+    }
   wave_topk_to_lds<K>(tk, lane, wv, sv, sj);
   __syncthreads();
   if (t == 0) {  // merge the NW sorted lists
@@ -454,6 +464,30 @@ __device__ __forceinline__ void wave_best(double cv, int cj, int u, int lane, do
   }
 }
 
+// wave_best with u = 1 over the price cache's lanes 0 .. kCache-1 (16):
+// one four-step butterfly carrying (best, its column, second best) instead
+// of two six-step passes -- the tail's bids are a dependent chain, and the
+// shuffles were most of a cached bid.  Ties: the lower column first.
+__device__ __forceinline__ void top2_16(double cv, int cj, double& b1, int& j1, double& b2) {
+  static_assert(kCache == 16, "top2_16 reduces over 16 lanes");
+  double a1 = cv, a2 = -DBL_MAX;
+  int i1 = cj;
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) {
+    const double p1 = __shfl_xor(a1, o, 64), p2 = __shfl_xor(a2, o, 64);
+    const int q1 = __shfl_xor(i1, o, 64);
+    const bool first = a1 > p1 || (a1 == p1 && i1 < q1);
+    a2 = fmax(first ? p1 : a1, fmax(a2, p2));
+    if (!first) {
+      a1 = p1;
+      i1 = q1;
+    }
+  }
+  b1 = __shfl(a1, 0, 64);
+  b2 = __shfl(a2, 0, 64);
+  j1 = __shfl(i1, 0, 64);
+}
+
 // ---- keeping the last phase's plan -----------------------------------------
 // A new eps phase (and a warm start, whose "last phase" is the previous
 // solve's plan) starts with every slot unassigned in the new epoch.  The
@@ -524,9 +558,9 @@ constexpr int kTailBids = 16384;
 // latency-bound -- twice the waves, twice the loads in flight
 constexpr int kTailWaves = 8;
 constexpr int kTailThreads = kTailWaves * 64;
-// the cached tail's scans' batch (x2 in flight, double-buffered); the
-// uncached tails (R = 1, R > 8) read the holders too and keep kScanUnroll
-constexpr int kTailUnroll = 16;
+// the cached tail's scans' batch (x2 in flight, double-buffered; 16
+// measured the same, r11s)
+constexpr int kTailUnroll = 8;
 constexpr int kTabCols = 4096;  // column entries: price, holder, owner, tag
 constexpr int kTabRows = 512;   // row entries: the price cache of a row
 constexpr size_t kTailLds =
@@ -568,6 +602,8 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
   __shared__ int stack[kTailMax], sorted[kTailMax];
   __shared__ int cnt, seq;
   __shared__ long long req;  // the row to scan, or -1: the tail is over
+  __shared__ double req_floor;  // its scan's floor (block_topk)
+  __shared__ int tcols[kCache];  // wave 0: the bidding row's cached columns
   const W2Ctl* ctl = w.ctl;
   if (ctl->done || !ctl->tail) return;  // uniform
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -607,20 +643,24 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
       last = sq;
       const long long rq = req;
       if (rq < 0) return;
-      block_topk<KS, kTailWaves, CACHED ? kTailUnroll : kScanUnroll>(C + rq * ldc, n, w, tag | (uint32_t)rq, !CACHED, sv, sj, outv, outj);
+      block_topk<KS, kTailWaves, CACHED ? kTailUnroll : kScanUnroll>(
+          C + rq * ldc, n, w, tag | (uint32_t)rq, !CACHED, sv, sj, outv, outj, req_floor);
     }
   }
   // wave 0: the bids
   int nseq = 0;
-  auto scan = [&](int64_t i, uint32_t mine) {  // post row i, scan it with the helpers
+  auto scan = [&](int64_t i, uint32_t mine, double floor) {  // post row i, scan it with the helpers
     __threadfence_block();  // this wave's price / holder writes before the helpers read
     if (lane == 0) {
       req = i;
+      req_floor = floor;
       __hip_atomic_store(&seq, ++nseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else {
       ++nseq;
     }
-    block_topk<KS, kTailWaves, CACHED ? kTailUnroll : kScanUnroll>(C + i * ldc, n, w, mine, !CACHED, sv, sj, outv, outj);
+    block_topk<KS, kTailWaves, CACHED ? kTailUnroll : kScanUnroll>(C + i * ldc, n, w, mine,
+                                                                   !CACHED, sv, sj, outv, outj,
+                                                                   floor);
   };
   int sp = c0;
   int nbids = 0;
@@ -637,6 +677,7 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
     uint32_t hj = 0;
     int oj = -1;
     bool have_j = false;
+    double floor = -DBL_MAX;   // the rescan's (block_topk)
     if (CACHED) {  // the row's cache (table, else global + install), its bid
       const int re = (int)(i & (kTabRows - 1));
       int valid, c = INT32_MAX;
@@ -688,13 +729,22 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
             cv = -(double)cc - p;
           }
         }
-        double kv;
-        int kj;
-        wave_best(cv, cj, 1, lane, kv, kj);
-        b1 = __shfl(kv, 0, 64);
-        b2 = __shfl(kv, 1, 64);
-        bj = __shfl(kj, 0, 64);
+        top2_16(cv, cj, b1, bj, b2);
         hit = b2 >= bound;
+        if (!hit && n > kCache) {
+          // the rescan's floor: the 16 cached columns' values now (held or
+          // not) and one column outside the cache are 17 known values, so
+          // the 17th best overall is at least their minimum
+          if (lane < kCache) tcols[lane] = c;
+          double fv = lane < kCache ? (c != INT32_MAX ? -(double)cc - p : -DBL_MAX) : DBL_MAX;
+#pragma unroll
+          for (int o = 8; o > 0; o >>= 1) fv = fmin(fv, __shfl_xor(fv, o, 64));
+          bool outside = lane <= kCache;
+          for (int k = 0; k < kCache; ++k) outside = outside && tcols[k] != lane;
+          const int jx = __ffsll((long long)__ballot(outside)) - 1;
+          const double vx = -(double)row[jx] - w.price[jx];
+          floor = fmin(__shfl(fv, 0, 64), vx);
+        }
         if (hit && bj != INT32_MAX) {
           const unsigned long long at = __ballot(c == bj && lane < kCache);
           const int L = __ffsll((long long)at) - 1;
@@ -705,7 +755,7 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
         }
       }
       if (!hit) {  // full scan over all columns, refill the cache (global + table)
-        scan(i, mine);
+        scan(i, mine, floor);
         const double ev = lane < kCache + 1 ? outv[lane] : -DBL_MAX;
         const int ej = lane < kCache + 1 ? outj[lane] : INT32_MAX;
         if (lane < kCache) {
@@ -730,15 +780,10 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
           cj = ej;
           cv = ev;
         }
-        double kv;
-        int kj;
-        wave_best(cv, cj, 1, lane, kv, kj);
-        b1 = __shfl(kv, 0, 64);
-        b2 = __shfl(kv, 1, 64);
-        bj = __shfl(kj, 0, 64);
+        top2_16(cv, cj, b1, bj, b2);
       }
     } else {
-      scan(i, mine);
+      scan(i, mine, -DBL_MAX);
       b1 = outv[0];
       b2 = outv[1];
       bj = outj[0];
