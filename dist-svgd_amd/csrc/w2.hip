@@ -317,6 +317,13 @@ __device__ __forceinline__ void wave_topk_to_lds(TopK<K>& t, int lane, int wv, d
         bj = oj;
       }
     }
+    if (bj == INT32_MAX) {  // (uniform) the wave's lists are spent: pad, stop
+      for (int r = k + lane; r < K; r += 64) {
+        sv[wv * K + r] = -DBL_MAX;
+        sj[wv * K + r] = INT32_MAX;
+      }
+      break;
+    }
     if (lane == 0) {
       sv[wv * K + k] = bv;
       sj[wv * K + k] = bj;

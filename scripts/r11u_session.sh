@@ -1,8 +1,8 @@
 #!/bin/bash
-# W2 tail: single-pass top-2 of cached bids, rescans floored by the known cached values
+# W2 scans: a wave stops extracting once its lists are spent
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r11t
+OUT=gpurun_out/r11u
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dist.py -m gpu -v -x \
   --timeout 300 --timeout-method thread -k "w2 or wasserstein" \
