@@ -55,6 +55,18 @@ def test_meta_calls_without_gpu():
     assert lib.dsvgd_ldy(32) == 128 and lib.dsvgd_ldy(128) == 256 and lib.dsvgd_ldy(256) == 512
     assert lib.dsvgd_ldy(1024) == 2048
     assert lib.dsvgd_logreg_workspace_bytes(100, 400, 2) % 256 == 0
+    # the wide Gauss-Seidel sweep's rows per block: x', w (and s' when
+    # refreshed) in the walk's LDS
+    assert lib.dsvgd_gsw_block_rows(256, 0) == 64 and lib.dsvgd_gsw_block_rows(256, 3) == 40
+    assert lib.dsvgd_gsw_block_rows(1024, 0) == 16 and lib.dsvgd_gsw_block_rows(1024, 1) == 10
+    assert lib.dsvgd_gsw_block_rows(55, 3) == 64 and lib.dsvgd_gsw_block_rows(2048, 0) == 0
+    # the W2 A/B switches are process-wide settings (no GPU needed)
+    assert lib.dsvgd_w2_set_theta(16.0) == 8.0 and lib.dsvgd_w2_set_theta(1.0) == 16.0
+    assert lib.dsvgd_w2_set_theta(8.0) == 16.0          # 1.0 was out of range: ignored
+    assert lib.dsvgd_w2_set_keep(1) == 0 and lib.dsvgd_w2_set_keep(0) == 1
+    assert lib.dsvgd_gsw_debug(0) == 0
+    stats = (ctypes.c_int64 * 2)()
+    assert lib.dsvgd_w2_tail_stats(stats) == 2
     # argument validation returns an error code (no GPU work is enqueued)
     rc = lib.dsvgd_sqdist(None, 0, None, 0, 0, 0, 32, None, 128, 0, None, None, None)
     assert rc == -1 and b"null" in lib.dsvgd_last_error()
