@@ -53,6 +53,7 @@ struct W2Ctl {
   int32_t keep_on;  // phases keep the last plan's eps-CS slots (dsvgd_w2_set_keep)
   double theta;     // eps divisor between phases (dsvgd_w2_set_theta; kTheta)
   unsigned long long tail_bids, tail_scans;  // the tails' work (dsvgd_w2_tail_stats)
+  unsigned long long tail_t[3];  // their time in the cached bids, the scans, the resolves (10 ns)
 };
 
 constexpr size_t kW2CtlBytes = 256;
@@ -671,8 +672,11 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
   };
   int sp = c0;
   int nbids = 0;
+  unsigned long long tl = 0, tsc = 0, trs = 0;   // wall clock (100 MHz): lookups, scans, resolves
   for (int b = 0; b < kTailBids && sp > 0; ++b) {
     ++nbids;
+    const unsigned long long t0 = wall_clock64();
+    unsigned long long tsc0 = 0;
     const int s = stack[sp - 1];
     const int64_t i = s / R;
     const uint32_t mine = tag | (uint32_t)i;
@@ -762,6 +766,7 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
         }
       }
       if (!hit) {  // full scan over all columns, refill the cache (global + table)
+        tsc0 = wall_clock64();
         scan(i, mine, floor);
         const double ev = lane < kCache + 1 ? outv[lane] : -DBL_MAX;
         const int ej = lane < kCache + 1 ? outj[lane] : INT32_MAX;
@@ -794,6 +799,13 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
       b1 = outv[0];
       b2 = outv[1];
       bj = outj[0];
+    }
+    const unsigned long long t1 = wall_clock64();
+    if (tsc0) {
+      tl += tsc0 - t0;
+      tsc += t1 - tsc0;
+    } else {
+      tl += t1 - t0;
     }
     // resolve on the spot (lane 0), the stack kept by the whole wave
     int old = -1;
@@ -848,11 +860,15 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
     }
     // (no fence per bid: this wave's own later reads of these words are in
     // order after its writes; the helpers get one in scan())
+    trs += wall_clock64() - t1;
   }
   // the launch's work, then release the helpers
   if (lane == 0) {
     atomicAdd(&w.ctl->tail_bids, (unsigned long long)nbids);
     atomicAdd(&w.ctl->tail_scans, (unsigned long long)nseq);
+    atomicAdd(&w.ctl->tail_t[0], tl);
+    atomicAdd(&w.ctl->tail_t[1], tsc);
+    atomicAdd(&w.ctl->tail_t[2], trs);
     req = -1;
     __hip_atomic_store(&seq, nseq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
@@ -1151,7 +1167,7 @@ static bool& w2_keep_flag() {
 
 // the last dsvgd_w2_assign's tail work on this host thread: (bids, scans)
 static long long* w2_tail_stats() {
-  static thread_local long long st[2] = {0, 0};
+  static thread_local long long st[5] = {0, 0, 0, 0, 0};
   return st;
 }
 
@@ -1185,10 +1201,9 @@ int dsvgd_w2_set_keep(int keep) {
 
 int64_t dsvgd_w2_tail_stats(int64_t* out) {
   if (out) {
-    out[0] = w2_tail_stats()[0];
-    out[1] = w2_tail_stats()[1];
+    for (int k = 0; k < 5; ++k) out[k] = w2_tail_stats()[k];
   }
-  return 2;
+  return 5;
 }
 
 double dsvgd_w2_set_theta(double theta) {
@@ -1344,6 +1359,7 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
     w2_trace().insert(w2_trace().end(), {h.rounds, h.phases, (long long)h.unassigned});
     w2_tail_stats()[0] = (long long)h.tail_bids;
     w2_tail_stats()[1] = (long long)h.tail_scans;
+    for (int k = 0; k < 3; ++k) w2_tail_stats()[2 + k] = (long long)(h.tail_t[k] / 100);  // us
     if (h.done) break;
     if ((batch - 1) * kRoundBatch >= max_rounds) {
       set_error("dsvgd_w2_assign: no convergence after %lld rounds (%lld phases, %llu unassigned)",

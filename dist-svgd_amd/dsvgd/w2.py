@@ -74,10 +74,11 @@ class W2Term(object):
         return self.G
 
     def tail_stats(self):
-        """The last solve's phase tails: (bids, full row scans)."""
-        buf = (ctypes.c_int64 * 2)()
+        """The last solve's phase tails: (bids, full row scans, us in the
+        cached bids, us in the scans, us in the resolves)."""
+        buf = (ctypes.c_int64 * 5)()
         N.load().dsvgd_w2_tail_stats(buf)
-        return int(buf[0]), int(buf[1])
+        return tuple(int(v) for v in buf)
 
     def trace(self):
         """The last solve's progress: (rounds, phase, unassigned) every 16 rounds."""

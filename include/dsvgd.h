@@ -587,8 +587,9 @@ int dsvgd_w2_set_keep(int keep);
  * accepted in [2, 1024], otherwise ignored).  Returns the previous value. */
 double dsvgd_w2_set_theta(double theta);
 /* The last dsvgd_w2_assign's phase tails on this host thread: out[0] bids,
- * out[1] full row scans among them (as of the last control readback).
- * Returns 2. */
+ * out[1] full row scans among them, out[2..4] microseconds spent in the
+ * cached bids, the scans (with their cache refill) and the resolves (as of
+ * the last control readback).  Returns 5 (the length of out). */
 int64_t dsvgd_w2_tail_stats(int64_t* out);
 /* Progress of this host thread's last dsvgd_w2_assign: out[3k..3k+2] =
  * (rounds, epsilon phase, unassigned slots) at the k-th control readback

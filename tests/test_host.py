@@ -65,8 +65,8 @@ def test_meta_calls_without_gpu():
     assert lib.dsvgd_w2_set_theta(8.0) == 16.0          # 1.0 was out of range: ignored
     assert lib.dsvgd_w2_set_keep(1) == 0 and lib.dsvgd_w2_set_keep(0) == 1
     assert lib.dsvgd_gsw_debug(0) == 0
-    stats = (ctypes.c_int64 * 2)()
-    assert lib.dsvgd_w2_tail_stats(stats) == 2
+    stats = (ctypes.c_int64 * 5)()
+    assert lib.dsvgd_w2_tail_stats(stats) == 5
     # argument validation returns an error code (no GPU work is enqueued)
     rc = lib.dsvgd_sqdist(None, 0, None, 0, 0, 0, 32, None, 128, 0, None, None, None)
     assert rc == -1 and b"null" in lib.dsvgd_last_error()
