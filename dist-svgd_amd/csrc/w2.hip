@@ -43,7 +43,7 @@ struct W2Ctl {
   double eps, eps_final;
   float cmax;
   int32_t epoch;
-  int32_t done;  // 0 running, 1 converged, 2 degenerate (all costs 0), 3 bad input
+  int32_t done;  // 0 running, 1 converged, 2 degenerate (all costs 0), 3 bad input, 4 tail stall
   int32_t fresh;  // this round starts a phase with the last one's plan: keep-checks first
   unsigned long long unassigned;
   long long rounds, phases;
@@ -54,6 +54,12 @@ struct W2Ctl {
   double theta;     // eps divisor between phases (dsvgd_w2_set_theta; kTheta)
   unsigned long long tail_bids, tail_scans;  // the tails' work (dsvgd_w2_tail_stats)
   unsigned long long tail_t[3];  // their time in the cached bids, the scans, the resolves (10 ns)
+  // the tail's scan mailbox (w2_tail_kernel: workgroup 0 posts, the helper
+  // workgroups scan a column share each and count themselves done)
+  unsigned long long mb_seq;  // (round << 20) | k
+  unsigned int mb_done, mb_pad;
+  long long mb_row;
+  double mb_floor;
 };
 
 constexpr size_t kW2CtlBytes = 256;
@@ -88,6 +94,10 @@ __device__ __forceinline__ uint32_t w2_tag(int ep) { return (uint32_t)(ep & 0x7f
 constexpr int kCache = 16;
 constexpr int kCacheMaxR = 8;
 
+// the phase tail's scan helpers (w2_tail_kernel): workgroups, list length
+constexpr int kTailHelpers = 32;
+constexpr int kTailListMax = 33;
+
 struct W2Ws {
   W2Ctl* ctl;
   double* price;
@@ -97,6 +107,8 @@ struct W2Ws {
   int32_t *ccol, *cvalid;
   float* ccost;
   double* cbound;
+  double* tv;   // the tail helpers' lists: kTailHelpers x kTailListMax
+  int32_t* tj;
   W2Ws(void* ws, int64_t n, int64_t m) {
     char* p = (char*)ws;
     ctl = (W2Ctl*)p;
@@ -110,6 +122,8 @@ struct W2Ws {
     ccol = (int32_t*)(cbound + m);
     ccost = (float*)(ccol + m * kCache);
     cvalid = (int32_t*)(ccost + m * kCache);
+    tv = (double*)(((uintptr_t)(cvalid + m) + 7) & ~(uintptr_t)7);
+    tj = (int32_t*)(tv + kTailHelpers * kTailListMax);
   }
 };
 
@@ -339,7 +353,7 @@ __device__ __forceinline__ void wave_topk_to_lds(TopK<K>& t, int lane, int wv, d
 template <int K, int NW = 4, int U = kScanUnroll>
 __device__ __forceinline__ void block_topk(const float* __restrict__ row, int64_t n, const W2Ws& w,
                            uint32_t mine, bool skip_held, double* sv, int* sj, double* out_v,
-                           int* out_j, double floor = -DBL_MAX) {
+                           int* out_j, double floor = -DBL_MAX, int64_t col0 = 0) {
   constexpr int NT = NW * 64;   // the workgroup's threads
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   TopK<K> tk;
@@ -358,8 +372,8 @@ __device__ __forceinline__ void block_topk(const float* __restrict__ row, int64_
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         c[u] = row[jj + u * NT];
-        p[u] = w.price[jj + u * NT];
-        h[u] = skip_held ? w.holder[jj + u * NT] : 0u;
+        p[u] = w.price[col0 + jj + u * NT];
+        h[u] = skip_held ? w.holder[col0 + jj + u * NT] : 0u;
       }
     };
     auto push = [&](const float (&c)[U], const double (&p)[U], const uint32_t (&h)[U],
@@ -372,7 +386,7 @@ __device__ __forceinline__ void block_topk(const float* __restrict__ row, int64_
           // most lanes skip the insertion (a wave pays for one whenever any
           // of its lanes inserts)
           const double x = -(double)c[u] - p[u];
-          if (x >= floor) tk.push(x, (int)(jj + u * NT));
+          if (x >= floor) tk.push(x, (int)(col0 + jj + u * NT));
         }
     };
     load(c0, p0, h0, j);
@@ -392,9 +406,9 @@ __device__ __forceinline__ void block_topk(const float* __restrict__ row, int64_
     }
   }
   for (; j < n; j += NT)
-    if (!skip_held || w.holder[j] != mine) {
-      const double x = -(double)row[j] - w.price[j];
-      if (x >= floor) tk.push(x, (int)j);
+    if (!skip_held || w.holder[col0 + j] != mine) {
+      const double x = -(double)row[j] - w.price[col0 + j];
+      if (x >= floor) tk.push(x, (int)(col0 + j));
     }
   wave_topk_to_lds<K>(tk, lane, wv, sv, sj);
   __syncthreads();
@@ -608,22 +622,70 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
   __shared__ double sv[kTailWaves * KS], outv[KS];
   __shared__ int sj[kTailWaves * KS], outj[KS];
   __shared__ int stack[kTailMax], sorted[kTailMax];
-  __shared__ int cnt, seq;
-  __shared__ long long req;  // the row to scan, or -1: the tail is over
+  __shared__ int cnt;
+  __shared__ long long req;     // helper workgroups: the row to scan, or -1: the tail is over
   __shared__ double req_floor;  // its scan's floor (block_topk)
   __shared__ int tcols[kCache];  // wave 0: the bidding row's cached columns
   const W2Ctl* ctl = w.ctl;
-  if (ctl->done || !ctl->tail) return;  // uniform
+  if (ctl->done || !ctl->tail) return;  // uniform over the grid
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int ep = ctl->epoch;
   const double eps = ctl->eps;
   const uint32_t tag = w2_tag(ep);
+  // mailbox sequence numbers carry this round (stale posts of earlier tail
+  // launches never match): (round << 20) | k, k = 1, 2, ... ; kQuit ends it
+  constexpr unsigned long long kQuit = 0xFFFFFull;
+  const unsigned long long rtag = (unsigned long long)ctl->rounds << 20;
+  W2Ctl* mb = w.ctl;
+  // every spin is bounded: a helper that never sees a post (or workgroup 0
+  // that never sees its helpers) gives up and flags the solve (done = 4)
+  constexpr long long kSpinMax = 1ll << 20;   // ~1-2 s of polls
+  if (blockIdx.x > 0) {  // a scan helper: columns [c0, c1)
+    const int64_t share = ((n + kTailHelpers - 1) / kTailHelpers + 63) & ~(int64_t)63;
+    const int64_t hc0 = min(n, (int64_t)(blockIdx.x - 1) * share), hc1 = min(n, hc0 + share);
+    unsigned long long expect = 1;
+    for (;;) {
+      if (t == 0) {
+        long long spins = 0;
+        unsigned long long sq;
+        for (;;) {
+          sq = __hip_atomic_load(&mb->mb_seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+          if ((sq & ~kQuit) == rtag && ((sq & kQuit) == expect || (sq & kQuit) == kQuit)) break;
+          if (++spins > kSpinMax) {
+            sq = rtag | kQuit;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        req = ((sq & kQuit) == kQuit) ? -1 : mb->mb_row;
+        req_floor = mb->mb_floor;
+      }
+      __syncthreads();
+      const long long rq = req;
+      if (rq < 0) return;
+      if (hc1 > hc0)
+        block_topk<KS, kTailWaves, CACHED ? kTailUnroll : kScanUnroll>(
+            C + rq * ldc + hc0, hc1 - hc0, w, tag | (uint32_t)rq, !CACHED, sv, sj, outv, outj,
+            req_floor, hc0);
+      const int h = blockIdx.x - 1;
+      if (t < KS) {
+        w.tv[h * kTailListMax + t] = hc1 > hc0 ? outv[t] : -DBL_MAX;
+        w.tj[h * kTailListMax + t] = hc1 > hc0 ? outj[t] : INT32_MAX;
+      }
+      __syncthreads();
+      if (t == 0) {
+        __threadfence();  // the list before the count (agent scope)
+        __hip_atomic_fetch_add(&mb->mb_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      ++expect;
+    }
+  }
   TailTab T(w2_tail_lds);
   for (int e = t; e < kTabCols; e += kTailThreads) T.ct[e] = -1;
   for (int e = t; e < kTabRows; e += kTailThreads) T.rt[e] = -1;
   if (t == 0) {
     cnt = 0;
-    seq = 0;
+    __hip_atomic_store(&mb->mb_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   for (int64_t s0 = t; s0 < n; s0 += kTailThreads)
@@ -642,38 +704,46 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
   __syncthreads();
   if (t < c0) stack[t] = sorted[t];
   __syncthreads();
-  if (wv != 0) {  // the scan helpers
-    int last = 0;
-    for (;;) {
-      int sq;
-      while ((sq = __hip_atomic_load(&seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == last)
-        __builtin_amdgcn_s_sleep(1);
-      last = sq;
-      const long long rq = req;
-      if (rq < 0) return;
-      block_topk<KS, kTailWaves, CACHED ? kTailUnroll : kScanUnroll>(
-          C + rq * ldc, n, w, tag | (uint32_t)rq, !CACHED, sv, sj, outv, outj, req_floor);
-    }
-  }
+  if (wv != 0) return;  // wave 0 bids; the scans are the helper workgroups'
   // wave 0: the bids
-  int nseq = 0;
-  auto scan = [&](int64_t i, uint32_t mine, double floor) {  // post row i, scan it with the helpers
-    __threadfence_block();  // this wave's price / holder writes before the helpers read
+  unsigned nseq = 0;
+  bool stalled = false;
+  auto scan = [&](int64_t i, uint32_t mine, double floor) {  // post row i, merge the helpers' lists
+    __threadfence();  // this wave's price / holder writes before the helpers read (agent)
+    ++nseq;
     if (lane == 0) {
-      req = i;
-      req_floor = floor;
-      __hip_atomic_store(&seq, ++nseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    } else {
-      ++nseq;
+      mb->mb_row = i;
+      mb->mb_floor = floor;
+      __hip_atomic_store(&mb->mb_seq, rtag | (unsigned long long)nseq, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      long long spins = 0;
+      while (__hip_atomic_load(&mb->mb_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) <
+             nseq * (unsigned)kTailHelpers) {
+        if (++spins > kSpinMax) {
+          stalled = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
     }
-    block_topk<KS, kTailWaves, CACHED ? kTailUnroll : kScanUnroll>(C + i * ldc, n, w, mine,
-                                                                   !CACHED, sv, sj, outv, outj,
-                                                                   floor);
+    stalled = __shfl(stalled, 0, 64);
+    __threadfence();
+    // the helpers' sorted lists, one per lane, merged by the wave
+    TopK<KS> tk;
+    tk.init();
+    if (lane < kTailHelpers && !stalled)
+      for (int k = KS - 1; k >= 0; --k)
+        tk.push(w.tv[lane * kTailListMax + k], w.tj[lane * kTailListMax + k]);
+    wave_topk_to_lds<KS>(tk, lane, 0, sv, sj);
+    if (lane < KS) {
+      outv[lane] = sv[lane];
+      outj[lane] = sj[lane];
+    }
   };
   int sp = c0;
   int nbids = 0;
   unsigned long long tl = 0, tsc = 0, trs = 0;   // wall clock (100 MHz): lookups, scans, resolves
-  for (int b = 0; b < kTailBids && sp > 0; ++b) {
+  for (int b = 0; b < kTailBids && sp > 0 && !stalled; ++b) {
     ++nbids;
     const unsigned long long t0 = wall_clock64();
     unsigned long long tsc0 = 0;
@@ -869,8 +939,8 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
     atomicAdd(&w.ctl->tail_t[0], tl);
     atomicAdd(&w.ctl->tail_t[1], tsc);
     atomicAdd(&w.ctl->tail_t[2], trs);
-    req = -1;
-    __hip_atomic_store(&seq, nseq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (stalled) atomicExch(&mb->done, 4);
+    __hip_atomic_store(&mb->mb_seq, rtag | kQuit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1214,7 +1284,8 @@ double dsvgd_w2_set_theta(double theta) {
 
 size_t dsvgd_w2_workspace_bytes(int64_t m, int64_t n) {
   return kW2CtlBytes + (size_t)n * (sizeof(double) + sizeof(unsigned long long) + 4 * sizeof(int32_t)) +
-         8 + (size_t)m * (sizeof(double) + kCache * (sizeof(int32_t) + sizeof(float)) + sizeof(int32_t));
+         8 + (size_t)m * (sizeof(double) + kCache * (sizeof(int32_t) + sizeof(float)) + sizeof(int32_t)) +
+         8 + (size_t)kTailHelpers * kTailListMax * (sizeof(double) + sizeof(int32_t));
 }
 
 int dsvgd_w2_cost(const float* X, int64_t ldx, int64_t m, const float* Y, int64_t ldy, int64_t n,
@@ -1299,15 +1370,16 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
   auto bid = [&]() {
     if (cached) {
       hipLaunchKernelGGL(w2_bid_cached_kernel, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
-      hipLaunchKernelGGL((w2_tail_kernel<2, true>), dim3(1), dim3(kTailThreads), kTailLds, s, C,
-                         ldc, n, R,
+      hipLaunchKernelGGL((w2_tail_kernel<2, true>), dim3(1 + kTailHelpers), dim3(kTailThreads),
+                         kTailLds, s, C, ldc, n, R,
                          w);
       return;
     }
 #define DSVGD_W2_BID(KK)                                                                       \
   do {                                                                                         \
     hipLaunchKernelGGL(w2_bid_kernel<KK>, gb, dim3(256), 0, s, C, ldc, m, n, R, w);            \
-    hipLaunchKernelGGL((w2_tail_kernel<KK, false>), dim3(1), dim3(kTailThreads), kTailLds, s, C, ldc, n, \
+    hipLaunchKernelGGL((w2_tail_kernel<KK, false>), dim3(1 + kTailHelpers), dim3(kTailThreads),    \
+                       kTailLds, s, C, ldc, n,                                                  \
                        R, w);                                                                  \
   } while (0)
     if (R <= 1)
@@ -1377,6 +1449,10 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
   if (h.done == 3) {
     set_error("dsvgd_w2_assign: non-finite or negative cost");
     return -2;
+  }
+  if (h.done == 4) {
+    set_error("dsvgd_w2_assign: the phase tail's scan helpers did not answer");
+    return -4;
   }
   if (rounds_out) *rounds_out = h.rounds;
   hipLaunchKernelGGL(w2_emit_kernel, gr, dim3(256), 0, s, n, w, assign);
