@@ -655,7 +655,7 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
             sq = rtag | kQuit;
             break;
           }
-          __builtin_amdgcn_s_sleep(2);
+          __builtin_amdgcn_s_sleep(1);
         }
         req = ((sq & kQuit) == kQuit) ? -1 : mb->mb_row;
         req_floor = mb->mb_floor;
@@ -719,11 +719,10 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
       long long spins = 0;
       while (__hip_atomic_load(&mb->mb_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) <
              nseq * (unsigned)kTailHelpers) {
-        if (++spins > kSpinMax) {
+        if (++spins > kSpinMax) {   // (a tight poll: the helpers answer in microseconds)
           stalled = true;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
       }
     }
     stalled = __shfl(stalled, 0, 64);
