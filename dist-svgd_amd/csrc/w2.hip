@@ -109,6 +109,7 @@ struct W2Ws {
   double* cbound;
   double* tv;   // the tail helpers' lists: kTailHelpers x kTailListMax
   int32_t* tj;
+  int32_t* cbcol;  // the column of each row's bound (its scan's 17th best)
   W2Ws(void* ws, int64_t n, int64_t m) {
     char* p = (char*)ws;
     ctl = (W2Ctl*)p;
@@ -124,6 +125,7 @@ struct W2Ws {
     cvalid = (int32_t*)(ccost + m * kCache);
     tv = (double*)(((uintptr_t)(cvalid + m) + 7) & ~(uintptr_t)7);
     tj = (int32_t*)(tv + kTailHelpers * kTailListMax);
+    cbcol = tj + kTailHelpers * kTailListMax;
   }
 };
 
@@ -625,7 +627,6 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
   __shared__ int cnt;
   __shared__ long long req;     // helper workgroups: the row to scan, or -1: the tail is over
   __shared__ double req_floor;  // its scan's floor (block_topk)
-  __shared__ int tcols[kCache];  // wave 0: the bidding row's cached columns
   const W2Ctl* ctl = w.ctl;
   if (ctl->done || !ctl->tail) return;  // uniform over the grid
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -811,19 +812,16 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
         }
         top2_16(cv, cj, b1, bj, b2);
         hit = b2 >= bound;
-        if (!hit && n > kCache) {
-          // the rescan's floor: the 16 cached columns' values now (held or
-          // not) and one column outside the cache are 17 known values, so
-          // the 17th best overall is at least their minimum
-          if (lane < kCache) tcols[lane] = c;
+        if (!hit) {
+          // the rescan's floor: the 16 cached columns and the last scan's
+          // 17th (the bound's column) are 17 known values now, so the 17th
+          // best overall is at least their minimum
           double fv = lane < kCache ? (c != INT32_MAX ? -(double)cc - p : -DBL_MAX) : DBL_MAX;
 #pragma unroll
           for (int o = 8; o > 0; o >>= 1) fv = fmin(fv, __shfl_xor(fv, o, 64));
-          bool outside = lane <= kCache;
-          for (int k = 0; k < kCache; ++k) outside = outside && tcols[k] != lane;
-          const int jx = __ffsll((long long)__ballot(outside)) - 1;
-          const double vx = -(double)row[jx] - w.price[jx];
-          floor = fmin(__shfl(fv, 0, 64), vx);
+          const int jb = w.cbcol[i];
+          const double vb = (jb >= 0 && jb < n) ? -(double)row[jb] - w.price[jb] : -DBL_MAX;
+          floor = fmin(__shfl(fv, 0, 64), vb);
         }
         if (hit && bj != INT32_MAX) {
           const unsigned long long at = __ballot(c == bj && lane < kCache);
@@ -848,6 +846,7 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
         }
         if (lane == kCache) {
           w.cbound[i] = ev;
+          w.cbcol[i] = ej;
           T.rb[re] = ev;
         }
         if (lane == 0) {
@@ -1036,7 +1035,10 @@ __global__ __launch_bounds__(256) void w2_bid_cached_kernel(const float* __restr
           w.ccol[iq * kCache + lane] = ej;
           w.ccost[iq * kCache + lane] = ej != INT32_MAX ? row[ej] : 0.f;
         }
-        if (lane == kCache) w.cbound[iq] = ev;
+        if (lane == kCache) {
+          w.cbound[iq] = ev;
+          w.cbcol[iq] = ej;
+        }
         if (lane == 0) w.cvalid[iq] = 1;
         unsigned long long f2 = fq;
         if (needkeep[q]) f2 &= ~w2_keep(row, iq, R, lane, ep, mine, __shfl(ev, 0, 64), eps, w);
@@ -1284,7 +1286,8 @@ double dsvgd_w2_set_theta(double theta) {
 size_t dsvgd_w2_workspace_bytes(int64_t m, int64_t n) {
   return kW2CtlBytes + (size_t)n * (sizeof(double) + sizeof(unsigned long long) + 4 * sizeof(int32_t)) +
          8 + (size_t)m * (sizeof(double) + kCache * (sizeof(int32_t) + sizeof(float)) + sizeof(int32_t)) +
-         8 + (size_t)kTailHelpers * kTailListMax * (sizeof(double) + sizeof(int32_t));
+         8 + (size_t)kTailHelpers * kTailListMax * (sizeof(double) + sizeof(int32_t)) +
+         (size_t)m * sizeof(int32_t);
 }
 
 int dsvgd_w2_cost(const float* X, int64_t ldx, int64_t m, const float* Y, int64_t ldy, int64_t n,
