@@ -610,12 +610,15 @@ struct TailTab {
   }
 };
 
-// One wave runs the bids: a bid answered by the row's price cache (most of
-// them in a price war) touches no barrier at all -- wave 0 alone pops the
-// slot, bids, resolves and pushes the displaced slot.  The other three waves
-// only join the full scans: they spin on an LDS sequence number (s_sleep
-// between polls), read the row wave 0 posted and run block_topk with it, all
-// four reaching its barriers together.
+// Workgroup 0's wave 0 runs the bids: a bid answered by the row's price
+// cache (most of them in a price war) touches no barrier at all -- it pops
+// the slot, bids, resolves and pushes the displaced slot.  A rescan goes to
+// the kTailHelpers other workgroups of the launch: wave 0 posts the row and
+// its floor in the control block's mailbox (sequence number tagged with the
+// round, agent-scope release), each helper scans its column share with
+// block_topk and publishes its sorted list, wave 0 merges the lists.  Every
+// poll is bounded (kSpinMax): a stall flags the solve (done = 4) and ends
+// the launch instead of hanging it.
 template <int K, bool CACHED>
 __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __restrict__ C, int64_t ldc,
                                                       int64_t n, int64_t R, W2Ws w) {
