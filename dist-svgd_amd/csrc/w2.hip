@@ -130,48 +130,85 @@ struct W2Ws {
 };
 
 // C[i][j] = ||x_i - y_j||^2 from explicit fp32 differences (the reference's
-// diffs / norm, distsampler.py:107-114).  64 x 64 tile per block, each thread
-// 4 x 4; 32-dim chunks of both operands transposed into LDS ([k][row]) so a
-// thread's 4 rows / 4 columns are one ds_read_b128 each.
+// diffs / norm, distsampler.py:107-114).  128 x 128 tile per block, each
+// thread 8 x 8 (rows 4rq..+3 and 64+4rq..+3, columns likewise); 32-dim chunks
+// of both operands transposed into LDS ([k][row]) so a thread's rows / columns
+// are two ds_read_b128 each: 64 outputs per four LDS reads keeps the packed
+// f32 VALU (v_pk_add / v_pk_fma) the bound -- the 64 x 64 / 4 x 4 tiling it
+// replaces issued one LDS read per eight outputs and ran at half that rate.
+// Every C_ij is the same k-ordered fma chain as before (bitwise).
+constexpr int kCostTile = 128;
 __global__ __launch_bounds__(256) void w2_cost_kernel(const float* __restrict__ X, int64_t ldx,
                                                       int64_t m, const float* __restrict__ Y,
                                                       int64_t ldy, int64_t n, int64_t d,
                                                       float* __restrict__ C, int64_t ldc) {
-  __shared__ __attribute__((aligned(16))) float xs[32][68];
-  __shared__ __attribute__((aligned(16))) float ys[32][68];
+  __shared__ __attribute__((aligned(16))) float xs[32][kCostTile + 4];
+  __shared__ __attribute__((aligned(16))) float ys[32][kCostTile + 4];
   const int t = threadIdx.x, rq = t >> 4, cq = t & 15;
-  const int64_t i0 = (int64_t)blockIdx.y * 64, j0 = (int64_t)blockIdx.x * 64;
-  float acc[4][4] = {};
-  for (int64_t k0 = 0; k0 < d; k0 += 32) {
-    for (int e = t; e < 64 * 32; e += 256) {
-      const int r = e >> 5, k = e & 31;
+  const int64_t i0 = (int64_t)blockIdx.y * kCostTile, j0 = (int64_t)blockIdx.x * kCostTile;
+  float acc[8][8] = {};
+  // the next 32-dim chunk is loaded into registers while this one computes:
+  // every load is unconditional (clamped address, zeroed after), so all 32
+  // are in flight together instead of one load-wait-store at a time
+  constexpr int kQ = kCostTile * 32 / 256;
+  float xr[kQ], yr[kQ];
+  auto load = [&](int64_t k0) {
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const int e = t + 256 * q, r = e >> 5, k = e & 31;
       const int64_t i = i0 + r, j = j0 + r, kk = k0 + k;
-      xs[k][r] = (i < m && kk < d) ? X[i * ldx + kk] : 0.f;
-      ys[k][r] = (j < n && kk < d) ? Y[j * ldy + kk] : 0.f;
+      const int64_t kc = kk < d ? kk : d - 1;
+      xr[q] = X[(i < m ? i : m - 1) * ldx + kc];
+      yr[q] = Y[(j < n ? j : n - 1) * ldy + kc];
+      if (!(i < m && kk < d)) xr[q] = 0.f;
+      if (!(j < n && kk < d)) yr[q] = 0.f;
+    }
+  };
+  load(0);
+  for (int64_t k0 = 0; k0 < d; k0 += 32) {
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const int e = t + 256 * q, r = e >> 5, k = e & 31;
+      xs[k][r] = xr[q];
+      ys[k][r] = yr[q];
     }
     __syncthreads();
-#pragma unroll 8
+    if (k0 + 32 < d) load(k0 + 32);
+#pragma unroll 4
     for (int k = 0; k < 32; ++k) {
-      const f32x4 x4 = *reinterpret_cast<const f32x4*>(&xs[k][4 * rq]);
-      const f32x4 y4 = *reinterpret_cast<const f32x4*>(&ys[k][4 * cq]);
+      const f32x4 xa = *reinterpret_cast<const f32x4*>(&xs[k][4 * rq]);
+      const f32x4 xb = *reinterpret_cast<const f32x4*>(&xs[k][64 + 4 * rq]);
+      const f32x4 ya = *reinterpret_cast<const f32x4*>(&ys[k][4 * cq]);
+      const f32x4 yb = *reinterpret_cast<const f32x4*>(&ys[k][64 + 4 * cq]);
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < 8; ++a) {
+        const float xv = a < 4 ? xa[a] : xb[a - 4];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const float df = x4[a] - y4[b];
+        for (int b = 0; b < 8; ++b) {
+          const float df = xv - (b < 4 ? ya[b] : yb[b - 4]);
           acc[a][b] = fmaf(df, df, acc[a][b]);
         }
+      }
     }
     __syncthreads();
   }
+  const bool vec = (ldc & 3) == 0 && ((uintptr_t)C & 15) == 0;
 #pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    const int64_t i = i0 + 4 * rq + a;
+  for (int a = 0; a < 8; ++a) {
+    const int64_t i = i0 + (a < 4 ? 4 * rq + a : 64 + 4 * rq + a - 4);
     if (i >= m) continue;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int64_t j = j0 + 4 * cq + b;
-      if (j < n) C[i * ldc + j] = acc[a][b];
+    for (int h = 0; h < 2; ++h) {
+      const int64_t j = j0 + 64 * h + 4 * cq;
+      float* dst = C + i * ldc + j;
+      if (vec && j + 3 < n) {
+        *reinterpret_cast<f32x4*>(dst) = f32x4{acc[a][4 * h], acc[a][4 * h + 1],
+                                               acc[a][4 * h + 2], acc[a][4 * h + 3]};
+      } else {
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if (j + b < n) dst[b] = acc[a][4 * h + b];
+      }
     }
   }
 }
@@ -182,12 +219,21 @@ __global__ __launch_bounds__(256) void w2_cmax_kernel(const float* __restrict__ 
                                                       int64_t m, int64_t n, W2Ctl* ctl) {
   uint32_t mx = 0;
   bool bad = false;
-  const int64_t total = m * n;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * 256) {
-    const float v = C[(e / n) * ldc + e % n];
-    bad |= !(v >= 0.f && v <= FLT_MAX);
-    mx = max(mx, __float_as_uint(v));
+  // row segments of 2048 columns: one 64-bit division per segment, not per
+  // element; eight independent loads in flight per thread
+  const int64_t nseg = (n + 2047) / 2048, total = m * nseg;
+  for (int64_t sg = blockIdx.x; sg < total; sg += gridDim.x) {
+    const int64_t i = sg / nseg, jb = (sg - i * nseg) * 2048;
+    const float* row = C + i * ldc;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t j = jb + 256 * u + threadIdx.x;
+      if (j < n) {
+        const float v = row[j];
+        bad |= !(v >= 0.f && v <= FLT_MAX);
+        mx = max(mx, __float_as_uint(v));
+      }
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
@@ -210,7 +256,15 @@ __global__ __launch_bounds__(256) void w2_violation_kernel(const float* __restri
        i += (int64_t)gridDim.x * 4) {
     const float* row = C + i * ldc;
     double best = -DBL_MAX;
-    for (int64_t j = lane; j < n; j += 64) best = fmax(best, -(double)row[j] - w.price[j]);
+    int64_t j = lane;
+    for (; j + 192 < n; j += 256) {   // four independent loads in flight per lane
+      const float c0 = row[j], c1 = row[j + 64], c2 = row[j + 128], c3 = row[j + 192];
+      const double p0 = w.price[j], p1 = w.price[j + 64], p2 = w.price[j + 128],
+                   p3 = w.price[j + 192];
+      best = fmax(fmax(fmax(best, -(double)c0 - p0), fmax(-(double)c1 - p1, -(double)c2 - p2)),
+                  -(double)c3 - p3);
+    }
+    for (; j < n; j += 64) best = fmax(best, -(double)row[j] - w.price[j]);
     double worst = DBL_MAX;
     if (lane < R) {
       const int64_t a = prev[i * R + lane];
@@ -1297,8 +1351,12 @@ int dsvgd_w2_cost(const float* X, int64_t ldx, int64_t m, const float* Y, int64_
                   int64_t d, float* C, int64_t ldc, void* stream) {
   DSVGD_REQUIRE(X && Y && C, "null pointer");
   DSVGD_REQUIRE(m > 0 && n > 0 && d > 0 && ldx >= d && ldy >= d && ldc >= n, "sizes");
-  DSVGD_REQUIRE((n + 63) / 64 <= INT32_MAX && (m + 63) / 64 <= 65535, "grid too large");
-  hipLaunchKernelGGL(w2_cost_kernel, dim3((n + 63) / 64, (m + 63) / 64), dim3(256), 0,
+  DSVGD_REQUIRE((n + kCostTile - 1) / kCostTile <= INT32_MAX &&
+                    (m + kCostTile - 1) / kCostTile <= 65535,
+                "grid too large");
+  hipLaunchKernelGGL(w2_cost_kernel,
+                     dim3((n + kCostTile - 1) / kCostTile, (m + kCostTile - 1) / kCostTile),
+                     dim3(256), 0,
                      (hipStream_t)stream, X, ldx, m, Y, ldy, n, d, C, ldc);
   return check_launch("w2_cost");
 }
@@ -1344,8 +1402,7 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
         hipMemsetAsync((char*)ws + kW2CtlBytes + prices, 0, total_b - kW2CtlBytes - prices, s) !=
             hipSuccess)))
     return check_launch("w2 workspace memset");
-  const int64_t total = m * n;
-  const int cblocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
+  const int cblocks = (int)std::min<int64_t>(4096, m * ((n + 2047) / 2048));
   hipLaunchKernelGGL(w2_cmax_kernel, dim3(cblocks), dim3(256), 0, s, C, ldc, m, n, w.ctl);
   if (prev)
     hipLaunchKernelGGL(w2_violation_kernel, dim3((unsigned)std::min<int64_t>(1024, (m + 3) / 4)),

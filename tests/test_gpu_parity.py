@@ -678,6 +678,30 @@ def test_w2_warm_start_same_plan(m, n, d, step):
     record_parity(0.0, rounds_adaptive=plans[None][1], rounds_cold=plans[0][1])
 
 
+@pytest.mark.parametrize("m,n,d,pad", [(1, 1, 1, 0), (129, 127, 37, 3), (130, 300, 64, 0),
+                                       (256, 1024, 256, 1), (77, 515, 5, 2)])
+def test_w2_cost_tiles(m, n, d, pad):
+    """dsvgd_w2_cost (128 x 128 tiles): C_ij = ||x_i - y_j||^2 from explicit
+    fp32 differences, ragged tile edges, row-strided X / Y, ldc > n and a C
+    that is not 16-byte aligned (pad) -- vs fp64 within fp32 rounding; the
+    padding columns stay untouched."""
+    N = dsvgd()._native
+    rs = np.random.RandomState(m * 7 + n + d)
+    X = rs.randn(m, d + 3).astype(np.float32)
+    Y = rs.randn(n, d + 1).astype(np.float32)
+    ldc = n + 5
+    Xg, Yg = gpu(X), gpu(Y)
+    buf = torch.full((m * ldc + pad,), -1.0, device=DEV)
+    C = buf[pad:]
+    N.call("dsvgd_w2_cost", N.ptr(Xg), d + 3, m, N.ptr(Yg), d + 1, n, d, N.ptr(C), ldc,
+           N.stream(torch.device(DEV)))
+    got = C.view(m, ldc).cpu().numpy()
+    ref = ((X[:, None, :d].astype(np.float64) - Y[None, :, :d]) ** 2).sum(-1)
+    np.testing.assert_allclose(got[:, :n], ref, rtol=2e-6 * d, atol=1e-6)
+    assert np.all(got[:, n:] == -1.0)
+    assert np.all(buf[:pad].cpu().numpy() == -1.0)
+
+
 def test_w2_degenerate_and_identity():
     """All-equal particles (every cost 0) -> zero gradient; previous ==
     current (S = 1 consecutive steps) -> identity plan, zero gradient."""
