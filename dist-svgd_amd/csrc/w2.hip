@@ -43,7 +43,7 @@ struct W2Ctl {
   double eps, eps_final;
   float cmax;
   int32_t epoch;
-  int32_t done;  // 0 running, 1 converged, 2 degenerate (all costs 0), 3 bad input, 4 tail stall
+  int32_t done;  // 0 running, 1 converged, 2 degenerate (all costs 0), 3 bad input
   int32_t fresh;  // this round starts a phase with the last one's plan: keep-checks first
   unsigned long long unassigned;
   long long rounds, phases;
@@ -57,7 +57,11 @@ struct W2Ctl {
   // the tail's scan mailbox (w2_tail_kernel: workgroup 0 posts, the helper
   // workgroups scan a column share each and count themselves done)
   unsigned long long mb_seq;  // (round << 20) | k
-  unsigned int mb_done, mb_pad;
+  unsigned int mb_done;
+  unsigned int tail_off;  // no phase tails this solve: its helpers could not be
+                          // co-resident (occupancy) or one stalled (the bid rounds finish)
+  unsigned int tail_stalls;  // tails that gave up on their helpers (dsvgd_w2_tail_stats)
+  unsigned int debug_nohelp;  // tests: the helpers exit at once (dsvgd_w2_set_tail_debug)
   long long mb_row;
   double mb_floor;
 };
@@ -290,8 +294,12 @@ __global__ __launch_bounds__(256) void w2_violation_kernel(const float* __restri
 // VERDICT r2 item 9).  Any initial prices give the same eps_final-optimality
 // guarantee.
 constexpr double kWarmDiv = 64.0;
-__global__ void w2_start_kernel(W2Ctl* ctl, int64_t n, int warm_phases, int keep, double theta) {
+__global__ void w2_start_kernel(W2Ctl* ctl, int64_t n, int warm_phases, int keep, double theta,
+                                int tail_off, int debug_nohelp) {
   ctl->theta = theta;
+  ctl->tail_off = tail_off ? 1u : 0u;
+  ctl->tail_stalls = 0;
+  ctl->debug_nohelp = debug_nohelp ? 1u : 0u;
   const double cmax = (double)ctl->cmax;
   ctl->eps_final = fmax(cmax * 0x1p-24 / (double)n, cmax * 1e-13);
   double e0 = cmax / theta;
@@ -309,7 +317,7 @@ __global__ void w2_start_kernel(W2Ctl* ctl, int64_t n, int warm_phases, int keep
   ctl->phases = 1;
   ctl->keep_on = keep & 1;
   ctl->fresh = keep >> 1;
-  ctl->tail = n <= kTailMax;
+  ctl->tail = !tail_off && n <= kTailMax;
   if (ctl->done == 0 && !(cmax > 0.0)) ctl->done = 2;
 }
 
@@ -671,8 +679,11 @@ struct TailTab {
 // its floor in the control block's mailbox (sequence number tagged with the
 // round, agent-scope release), each helper scans its column share with
 // block_topk and publishes its sorted list, wave 0 merges the lists.  Every
-// poll is bounded (kSpinMax): a stall flags the solve (done = 4) and ends
-// the launch instead of hanging it.
+// poll is bounded (kSpinMax): the helpers share the CUs with whatever else
+// runs on the device (another stream's kernels, RCCL's), so one that is not
+// dispatched in time ends the launch instead of hanging it -- the tail then
+// turns itself off for the rest of the solve (tail_off) and the ordinary bid
+// rounds finish the phase: a slower solve, never a failed one.
 template <int K, bool CACHED>
 __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __restrict__ C, int64_t ldc,
                                                       int64_t n, int64_t R, W2Ws w) {
@@ -696,9 +707,10 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
   const unsigned long long rtag = (unsigned long long)ctl->rounds << 20;
   W2Ctl* mb = w.ctl;
   // every spin is bounded: a helper that never sees a post (or workgroup 0
-  // that never sees its helpers) gives up and flags the solve (done = 4)
+  // that never sees its helpers) gives up; workgroup 0 then sets tail_off
   constexpr long long kSpinMax = 1ll << 20;   // ~1-2 s of polls
   if (blockIdx.x > 0) {  // a scan helper: columns [c0, c1)
+    if (ctl->debug_nohelp) return;  // (tests: a helper that never answers)
     const int64_t share = ((n + kTailHelpers - 1) / kTailHelpers + 63) & ~(int64_t)63;
     const int64_t hc0 = min(n, (int64_t)(blockIdx.x - 1) * share), hc1 = min(n, hc0 + share);
     unsigned long long expect = 1;
@@ -994,7 +1006,10 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
     atomicAdd(&w.ctl->tail_t[0], tl);
     atomicAdd(&w.ctl->tail_t[1], tsc);
     atomicAdd(&w.ctl->tail_t[2], trs);
-    if (stalled) atomicExch(&mb->done, 4);
+    if (stalled) {   // no more tails this solve: the bid rounds finish the phase
+      atomicExch(&mb->tail_off, 1u);
+      atomicAdd(&mb->tail_stalls, 1u);
+    }
     __hip_atomic_store(&mb->mb_seq, rtag | kQuit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -1194,7 +1209,7 @@ __device__ void w2_control(W2Ctl* ctl, int64_t n) {
   const unsigned long long un =
       __hip_atomic_load(&ctl->unassigned, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (un != 0) {
-    ctl->tail = un <= (unsigned long long)kTailMax;
+    ctl->tail = !ctl->tail_off && un <= (unsigned long long)kTailMax;
     return;
   }
   if (ctl->eps <= ctl->eps_final) {
@@ -1206,7 +1221,7 @@ __device__ void w2_control(W2Ctl* ctl, int64_t n) {
   ctl->phases += 1;
   ctl->unassigned = (unsigned long long)n;
   ctl->fresh = ctl->keep_on;  // the next round keeps what still meets eps-CS
-  ctl->tail = n <= kTailMax;
+  ctl->tail = !ctl->tail_off && n <= kTailMax;
 }
 
 // One thread per column: award the column to its highest bidder; the last
@@ -1293,10 +1308,17 @@ static bool& w2_keep_flag() {
   return k;
 }
 
-// the last dsvgd_w2_assign's tail work on this host thread: (bids, scans)
+// the last dsvgd_w2_assign's tail work on this host thread: (bids, scans,
+// three times, stalls)
 static long long* w2_tail_stats() {
-  static thread_local long long st[5] = {0, 0, 0, 0, 0};
+  static thread_local long long st[6] = {0, 0, 0, 0, 0, 0};
   return st;
+}
+
+// tests: the tails' helpers exit at once (a stall on every tail launch)
+static bool& w2_nohelp_flag() {
+  static bool k = false;
+  return k;
 }
 
 // eps divisor between phases (default kTheta; A/B: dsvgd_w2_set_theta)
@@ -1329,9 +1351,15 @@ int dsvgd_w2_set_keep(int keep) {
 
 int64_t dsvgd_w2_tail_stats(int64_t* out) {
   if (out) {
-    for (int k = 0; k < 5; ++k) out[k] = w2_tail_stats()[k];
+    for (int k = 0; k < 6; ++k) out[k] = w2_tail_stats()[k];
   }
-  return 5;
+  return 6;
+}
+
+int dsvgd_w2_set_tail_debug(int nohelp) {
+  const int old = w2_nohelp_flag() ? 1 : 0;
+  w2_nohelp_flag() = nohelp != 0;
+  return old;
 }
 
 double dsvgd_w2_set_theta(double theta) {
@@ -1411,11 +1439,6 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
   if (prev && keep)
     hipLaunchKernelGGL(w2_load_prev_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n,
                        prev, w);
-  // keep bit 0: phases keep eps-CS slots; bit 1: the first round keeps prev's
-  hipLaunchKernelGGL(w2_start_kernel, dim3(1), dim3(1), 0, s, w.ctl, n, warm_phases,
-                     (keep ? 1 : 0) | ((prev && keep) ? 2 : 0), w2_theta());
-  int rc = check_launch("w2_start");
-  if (rc) return rc;
   const dim3 gb((unsigned)std::min<int64_t>(kBidBlocks, (m + 3) / 4));
   // the phase tail: one workgroup, its LDS tables as dynamic LDS
   const bool cached = kW2Cache && R >= 2 && R <= kCacheMaxR;
@@ -1429,6 +1452,22 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
   if (hipFuncSetAttribute(tail_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTailLds) !=
       hipSuccess)
     return fail_arg("w2 tail: cannot reserve its LDS tables");
+  // the tail's helpers poll a mailbox beside workgroup 0: if the device
+  // cannot hold all 1 + kTailHelpers workgroups at once even when idle, the
+  // solve runs without tails (bid rounds only)
+  int occ = 0, cus = 0, dev = 0;
+  const bool resident =
+      hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, tail_fn, kTailThreads, kTailLds) ==
+          hipSuccess &&
+      (int64_t)occ * cus >= 1 + kTailHelpers;
+  // keep bit 0: phases keep eps-CS slots; bit 1: the first round keeps prev's
+  hipLaunchKernelGGL(w2_start_kernel, dim3(1), dim3(1), 0, s, w.ctl, n, warm_phases,
+                     (keep ? 1 : 0) | ((prev && keep) ? 2 : 0), w2_theta(), resident ? 0 : 1,
+                     w2_nohelp_flag() ? 1 : 0);
+  int rc = check_launch("w2_start");
+  if (rc) return rc;
   auto bid = [&]() {
     if (cached) {
       hipLaunchKernelGGL(w2_bid_cached_kernel, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
@@ -1494,6 +1533,7 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
     w2_tail_stats()[0] = (long long)h.tail_bids;
     w2_tail_stats()[1] = (long long)h.tail_scans;
     for (int k = 0; k < 3; ++k) w2_tail_stats()[2 + k] = (long long)(h.tail_t[k] / 100);  // us
+    w2_tail_stats()[5] = (long long)h.tail_stalls;
     if (h.done) break;
     if ((batch - 1) * kRoundBatch >= max_rounds) {
       set_error("dsvgd_w2_assign: no convergence after %lld rounds (%lld phases, %llu unassigned)",
@@ -1511,10 +1551,6 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
   if (h.done == 3) {
     set_error("dsvgd_w2_assign: non-finite or negative cost");
     return -2;
-  }
-  if (h.done == 4) {
-    set_error("dsvgd_w2_assign: the phase tail's scan helpers did not answer");
-    return -4;
   }
   if (rounds_out) *rounds_out = h.rounds;
   hipLaunchKernelGGL(w2_emit_kernel, gr, dim3(256), 0, s, n, w, assign);

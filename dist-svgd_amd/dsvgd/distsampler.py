@@ -163,8 +163,8 @@ class DistSampler(object):
     def _warn_w2_cost(self):
         """The W2 term is the reference default, but with particles exchanged
         (R = n / m = num_shards > 1) the first step's exact assignment is a
-        cold auction of ~10^5 rounds (DESIGN.md, W2 cost at scale; later steps
-        start warm from the previous plan): say so once, at construction,
+        cold auction (1.75 s at 8192 x 65536; later steps
+        start warm from the previous plan, 55 ms): say so once, at construction,
         instead of letting the first make_step stall for seconds."""
         m = self._particles_per_shard
         n = self._num_particles if self._exchange_particles else m
@@ -172,7 +172,8 @@ class DistSampler(object):
             warnings.warn(
                 "DistSampler: include_wasserstein=True with R = n/m = %d > 1 and an "
                 "%d x %d plan: the exact W2 assignment of the first step takes seconds "
-                "at this size (m=8192, n=65536: ~14 s cold, then ~0.26 s per step warm); "
+                "at this size (m=8192, n=65536 on one MI355X: ~1.8 s cold, then ~55 ms per "
+                "step warm-started from the previous plan); "
                 "pass include_wasserstein=False for throughput" % (n // m, m, n),
                 RuntimeWarning, stacklevel=3)
 
@@ -295,11 +296,32 @@ class DistSampler(object):
                 and n_int == S * m and PhiEngine.pair_split_ok(n_int, self._d, S,
                                                                median=self._rbf.median))
 
+    _routes_ok = None    # the pair split's point-to-point routes, checked once
+
+    def _pair_split_routes(self, m):
+        """The pair split exchanges transposed partials point to point; before
+        its first step, every rank checks the plan's routes on the live
+        backend with a tagged probe through the same post / join path
+        (exchange.probe_p2p, ADVICE r4: that path had never run on a
+        multi-rank RCCL group).  A failed probe keeps the row-block layout on
+        every rank (the verdict is shared), with a warning."""
+        if self._routes_ok is None:
+            from .pairsplit import PairSplitPlan
+            P = PairSplitPlan(self._rank, self._num_shards, m)
+            self._routes_ok = exchange.probe_p2p([q["dest"] for q in P.sends],
+                                                 [q["src"] for q in P.recvs], self._rank,
+                                                 self._device, self._group)
+            if not self._routes_ok:
+                warnings.warn("DistSampler: the pair-split layout's point-to-point probe "
+                              "failed on this process group; using the row-block layout",
+                              RuntimeWarning, stacklevel=4)
+        return self._routes_ok
+
     def _engine(self, n_int, m, row0):
         """One engine per (interacting set, owned rows, median kind, layout);
         the owned rows' offset row0 is set per step (lagged modes rotate it)."""
         local = self._lagged == "local"
-        ps = self._use_pair_split(n_int, m)
+        ps = self._use_pair_split(n_int, m) and self._pair_split_routes(m)
         key = (n_int, m, local, ps)
         if key not in self._engines:
             self._engines.clear()      # the old D is freed before the new one is allocated

@@ -172,7 +172,7 @@ class PhiEngine(object):
         (dsvgd.pairsplit): distances() computes this rank's
         parts only, direction(p2p=...) exchanges the transposed partials.
         Needs the same scores on every rank, the FmtH2 engines, m = n / S a
-        multiple of 256, roundup(d, 32) a multiple of 256 and a bracketed
+        multiple of 256 (of 512 for even S), roundup(d, 32) a multiple of 256 and a bracketed
         (or fixed) bandwidth -- PhiEngine.pair_split_ok says whether it applies."""
         dev = N.require_gpu(device if device is not None else "cuda")
         lib = N.load()
@@ -551,7 +551,9 @@ class PhiEngine(object):
         dp = lib.dsvgd_dp(d)
         ldy = lib.dsvgd_ldy(dp)
         n_pad = lib.dsvgd_pad128(n)
-        return (S >= 2 and m * S == n and m % 256 == 0 and dp % 256 == 0 and ldy % 512 == 0
+        from .pairsplit import PairSplitPlan
+        return (S >= 2 and m * S == n and PairSplitPlan.aligned(S, m) and dp % 256 == 0
+                and ldy % 512 == 0
                 and (gemm or cls.DEFAULT_GEMM) == "h2" and d > cls.DIRECT_MAX_D
                 and n_pad * ldy * 6 < (1 << 31) and dp * (n_pad + 256) * 4 < (1 << 31)
                 and (not median or m * n >= cls.BRACKET_MIN_ENTRIES)
@@ -562,9 +564,11 @@ class PhiEngine(object):
         lib = N.load()
         if not (self.m * S == self.n and self.row0 == rank * self.m and self.phi_gemm == "h2"
                 and self.gram_gemm == "h2" and self.fused_scales and self.Yx3 is not None
-                and self.ldy % 512 == 0 and self.dp % 256 == 0):
+                and self.ldy % 512 == 0 and self.dp % 256 == 0
+                and PairSplitPlan.aligned(S, self.m)):
             raise ValueError("pair_split needs m = n / S = the rank's block, the FmtH2 engines, "
-                             "m % 256 == 0 and roundup(d, 32) % 256 == 0")
+                             "m % 256 == 0 (m % 512 == 0 for even S) and "
+                             "roundup(d, 32) % 256 == 0")
         P = self.plan = PairSplitPlan(rank, S, self.m)
         self._side = None   # WINDOW_SIDE_STREAM's stream
         dev, f32 = self.device, dict(dtype=torch.float32, device=self.device)

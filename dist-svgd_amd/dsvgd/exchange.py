@@ -80,6 +80,41 @@ def exchange_p2p_async(sends, recvs, group=None):
     return join
 
 
+def probe_p2p(send_peers, recv_peers, rank, device, group=None, _corrupt=False):
+    """Route check of a point-to-point plan on the live backend, through the
+    same path the step uses (exchange_p2p_async: post, kernels on the
+    current stream, join, read on the current stream): every rank sends each
+    planned peer a small tensor tagged (sender, receiver), produced by a
+    kernel right before the post, and checks what arrives from each planned
+    source.  The verdicts are combined over the group (MIN), so every rank
+    gets the same answer -- DistSampler falls back to the row-block layout on
+    all ranks together when any rank saw a wrong or missing message.
+    `_corrupt` (tests only) spoils this rank's first received buffer."""
+    L = 259
+    ramp = torch.arange(L, dtype=torch.float32, device=device)
+
+    def tag(src, dst):
+        return float(src * 8192 + dst + 1)
+    sb = [torch.empty(L, device=device) for _ in send_peers]
+    rb = [torch.full((L,), float("nan"), device=device) for _ in recv_peers]
+    for t, p in zip(sb, send_peers):
+        torch.add(ramp, tag(rank, p), out=t)
+    join = exchange_p2p_async(list(zip(sb, send_peers)), list(zip(rb, recv_peers)), group)
+    busy = torch.ones(256, 256, device=device)
+    for _ in range(3):                     # work queued between the post and the join
+        busy = torch.mm(busy, busy) * (1.0 / 256)
+    join()
+    ok = True
+    for t, p in zip(rb, recv_peers):
+        ok = ok and bool(torch.equal(t, ramp + tag(p, rank)))
+    if _corrupt:
+        ok = False
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int64,
+                        device=device if not _is_gloo(group) else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    return bool(flag.item() == 1)
+
+
 def exchange_p2p(sends, recvs, group=None):
     """Point-to-point transfers in one batch: sends = [(tensor, group_rank)],
     recvs = [(tensor, group_rank)], peers as ranks of `group`.  On RCCL the

@@ -43,8 +43,17 @@ def _cyclic(c0, length, n):
 class PairSplitPlan(object):
     GRAM_RECT, GRAM_DIAG, GRAM_FALLBACK = 0, 1, 2
 
+    @staticmethod
+    def aligned(S, m):
+        """Whether every part of the plan meets the kernels' alignment: the
+        Gram parts' columns are 256-aligned (dsvgd_sqdist_h2_parts), and for
+        even S the antipodal half-block m/2 starts or ends a Gram part, so
+        m/2 must be a multiple of 256 as well (m = 256 (mod 512)
+        would otherwise be rejected by the kernel mid-step)."""
+        return S >= 2 and m > 0 and m % 256 == 0 and (S % 2 == 1 or m % 512 == 0)
+
     def __init__(self, rank, S, m):
-        assert S >= 2 and 0 <= rank < S and m > 0 and m % 256 == 0
+        assert 0 <= rank < S and self.aligned(S, m), (rank, S, m)
         self.rank, self.S, self.m = rank, S, m
         n = self.n = S * m
         even = S % 2 == 0

@@ -75,8 +75,9 @@ class W2Term(object):
 
     def tail_stats(self):
         """The last solve's phase tails: (bids, full row scans, us in the
-        cached bids, us in the scans, us in the resolves)."""
-        buf = (ctypes.c_int64 * 5)()
+        cached bids, us in the scans, us in the resolves, tails that stalled
+        on their helpers and handed the phase back to the bid rounds)."""
+        buf = (ctypes.c_int64 * 6)()
         N.load().dsvgd_w2_tail_stats(buf)
         return tuple(int(v) for v in buf)
 

@@ -588,9 +588,15 @@ int dsvgd_w2_set_keep(int keep);
 double dsvgd_w2_set_theta(double theta);
 /* The last dsvgd_w2_assign's phase tails on this host thread: out[0] bids,
  * out[1] full row scans among them, out[2..4] microseconds spent in the
- * cached bids, the scans (with their cache refill) and the resolves (as of
- * the last control readback).  Returns 5 (the length of out). */
+ * cached bids, the scans (with their cache refill) and the resolves, out[5]
+ * tails whose scan helpers did not answer in time (the solve then finishes
+ * on the bid rounds, same plan) -- as of the last control readback.
+ * Returns 6 (the length of out). */
 int64_t dsvgd_w2_tail_stats(int64_t* out);
+/* Process-wide test switch (default 0): the phase tail's scan helpers exit
+ * at once, so every tail stalls and hands its phase back to the bid rounds.
+ * Returns the previous setting. */
+int dsvgd_w2_set_tail_debug(int nohelp);
 /* Progress of this host thread's last dsvgd_w2_assign: out[3k..3k+2] =
  * (rounds, epsilon phase, unassigned slots) at the k-th control readback
  * (every 16 rounds); copies min(count, cap) triples, returns count. */

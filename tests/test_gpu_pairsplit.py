@@ -107,7 +107,9 @@ def _check(S, cfg, res):
     else:
         S_ref = O.score_logreg(X0, x, t)
     h, med = res[0][1]["h"], res[0][1]["median"]
-    assert all(o["plan"] for _, o in res), "the pair-split layout did not engage"
+    want = cfg.get("expect_plan", True)
+    assert all(o["plan"] == want for _, o in res), "pair-split layout engaged: %s, expected %s" % (
+        [o["plan"] for _, o in res], want)
     assert all(o["h"] == h for _, o in res)
     if cfg["h"] == "median":
         assert all(o["median"] == med for _, o in res)
@@ -167,3 +169,13 @@ def test_pair_split_range_guard_fallback():
     cfg = dict(n=S * m, d=256, N=2048, eps=1e-3, seed=7, h="median", mode="all_scores",
                nrows=48, far=5000)
     _check(S, cfg, _run(S, 29830, cfg))
+
+
+def test_pair_split_declined_for_unaligned_half_block():
+    """even S with m = 256 (mod 512) -- the antipodal
+    half-block m/2 is not a 256-aligned Gram part -- must keep the row-block
+    layout (the plan is declined up front) and still match the oracle."""
+    S, m = 2, 2304
+    cfg = dict(n=S * m, d=256, N=1024, eps=1e-3, seed=21, h=2.0 * 256 * 0.01 / 8.0,
+               mode="all_scores", nrows=48, expect_plan=False)
+    _check(S, cfg, _run(S, 29835, cfg))

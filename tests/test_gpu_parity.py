@@ -647,6 +647,31 @@ def test_w2_assignment_optimal(m, n, d, near):
     assert err < PHI_TOL, err
 
 
+@pytest.mark.parametrize("m,n,d", [(512, 4096, 16), (1024, 1024, 32)])
+def test_w2_tail_stall_finishes_on_bid_rounds(m, n, d):
+    """the phase tail's scan helpers share the device with other
+    work; if they do not answer in time the tail turns itself off for the
+    solve and the bid rounds finish it.  Forced here (dsvgd_w2_set_tail_debug:
+    the helpers exit at once): at least one stall is recorded and the plan is
+    still scipy's exact assignment (R = 8 with the price cache, R = 1)."""
+    from dsvgd import _native
+    lib = _native.load()
+    rs = np.random.RandomState(m + n + d + 1)
+    X = rs.randn(m, d).astype(np.float32)
+    P = rs.randn(n, d).astype(np.float32)
+    lib.dsvgd_w2_set_tail_debug(1)
+    try:
+        G, plan, w = _w2_gpu(X, P, h=2.5)
+        stats = w.tail_stats()
+    finally:
+        lib.dsvgd_w2_set_tail_debug(0)
+    assert stats[5] >= 1, stats
+    ref_plan = O.w2_plan(O.w2_cost(X, P))
+    assert (_row_sets(plan, m) == _row_sets(ref_plan, m)).all()
+    ref = 2.5 * O.w2_grad(X, P, ref_plan)[0]
+    assert abs_err(G, ref) / np.abs(ref).max() < PHI_TOL
+
+
 @pytest.mark.parametrize("m,n,d,step", [(512, 4096, 16, 1e-3), (512, 4096, 16, 0.3),
                                         (1024, 1024, 32, 1e-2), (256, 2048, 8, 1e-4)])
 def test_w2_warm_start_same_plan(m, n, d, step):

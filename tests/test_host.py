@@ -65,8 +65,9 @@ def test_meta_calls_without_gpu():
     assert lib.dsvgd_w2_set_theta(8.0) == 16.0          # 1.0 was out of range: ignored
     assert lib.dsvgd_w2_set_keep(1) == 0 and lib.dsvgd_w2_set_keep(0) == 1
     assert lib.dsvgd_gsw_debug(0) == 0
-    stats = (ctypes.c_int64 * 5)()
-    assert lib.dsvgd_w2_tail_stats(stats) == 5
+    stats = (ctypes.c_int64 * 6)()
+    assert lib.dsvgd_w2_tail_stats(stats) == 6
+    assert lib.dsvgd_w2_set_tail_debug(1) == 0 and lib.dsvgd_w2_set_tail_debug(0) == 1
     # argument validation returns an error code (no GPU work is enqueued)
     rc = lib.dsvgd_sqdist(None, 0, None, 0, 0, 0, 32, None, 128, 0, None, None, None)
     assert rc == -1 and b"null" in lib.dsvgd_last_error()
@@ -236,7 +237,7 @@ def test_pair_split_plan_covers_the_matrix(S):
     diagonal once), i.e. n^2 weighted entries; (4) the fallback parts
     complete each rank's row block."""
     from dsvgd.pairsplit import PairSplitPlan
-    m = 256
+    m = 512   # even S: m / 2 is a Gram part boundary (PairSplitPlan.aligned)
     n = S * m
     cov = np.zeros((n, n), np.int32)
     wsum = np.zeros((n, n), np.int32)
@@ -282,3 +283,76 @@ def test_pair_split_plan_covers_the_matrix(S):
     assert (np.diag(wsum) == 1).all()
     off = ~np.eye(n, dtype=bool)
     assert (sym[off] == 2).all() and int(wsum.sum()) == n * n
+
+
+@pytest.mark.parametrize("S", [2, 3, 4, 5, 6, 8])
+@pytest.mark.parametrize("m", [256, 512, 768, 1024, 2304, 3328, 8192])
+def test_pair_split_parts_meet_kernel_alignment(S, m):
+    """every part of an accepted plan satisfies the
+    launchers' alignment rules -- Gram parts (dsvgd_sqdist_h2_parts: rows a
+    128-aligned range, columns a 256-aligned range), the phi window
+    (dsvgd_phi_h2_window: 16-aligned), the row half and the transposed
+    partials (dsvgd_phi_h2_transposed: K rows 16-aligned, output columns
+    128-aligned) -- and a plan whose antipodal half-block would break them
+    (even S with m = 256 mod 512) is refused up front, so DistSampler keeps
+    the row-block layout for it instead of failing mid-step."""
+    from dsvgd.engine import PhiEngine
+    from dsvgd.pairsplit import PairSplitPlan
+    ok = PairSplitPlan.aligned(S, m)
+    assert ok == (m % 256 == 0 and (S % 2 == 1 or m % 512 == 0))
+    # the engine's gate agrees (fixed bandwidth: only the layout rules apply)
+    assert PhiEngine.pair_split_ok(S * m, 256, S, median=False) == ok
+    if not ok:
+        with pytest.raises(AssertionError):
+            PairSplitPlan(0, S, m)
+        return
+    n = S * m
+    for r in range(S):
+        P = PairSplitPlan(r, S, m)
+        for p in P.gram_parts + P.fallback_parts:
+            assert p["row_off"] % 128 == 0 and p["rows"] % 128 == 0 and p["rows"] > 0
+            assert p["row_off"] + p["rows"] <= m
+            assert p["col0"] % 256 == 0 and p["cols"] % 256 == 0 and p["cols"] > 0
+            assert p["col0"] + p["cols"] <= n
+        assert P.window[0] % 16 == 0 and P.window[1] % 16 == 0 and 0 < P.window[1] <= n
+        if P.row_half:
+            ro, nr, c0, nc = P.row_half
+            assert ro % 128 == 0 and nr % 128 == 0 and c0 % 16 == 0 and nc % 16 == 0
+        for s in P.sends:
+            assert s["krows"] % 16 == 0 and s["row_off"] % 16 == 0
+            assert s["col0"] % 128 == 0 and s["mo"] % 128 == 0
+
+
+def _probe_worker(rank, S, port, corrupt_rank, q):
+    import torch.distributed as dist
+    from dsvgd import exchange
+    from dsvgd.pairsplit import PairSplitPlan
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=S)
+    P = PairSplitPlan(rank, S, 512)
+    ok = exchange.probe_p2p([s["dest"] for s in P.sends], [r["src"] for r in P.recvs], rank,
+                            "cpu", _corrupt=rank == corrupt_rank)
+    q.put((rank, ok))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("S,corrupt", [(2, -1), (3, -1), (4, -1), (4, 2)])
+def test_pair_split_route_probe_gloo(S, corrupt):
+    """The route probe DistSampler runs before its first pair-split step
+    (exchange.probe_p2p): the plan's sends and receives, tagged by (sender,
+    receiver), arrive where the plan says on a gloo group of S ranks; one rank
+    seeing a bad message makes every rank decline (MIN over the group)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29770 + S + (corrupt >= 0) * 10
+    ps = [ctx.Process(target=_probe_worker, args=(r, S, port, corrupt, q)) for r in range(S)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(S)]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    assert all(ok == (corrupt < 0) for _, ok in res), res
