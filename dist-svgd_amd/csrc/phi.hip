@@ -18,6 +18,22 @@
 
 namespace dsvgd {
 
+// phi_w1_kernel's A-fragment prefetch (PF template argument; process-wide
+// switch dsvgd_phi_set_prefetch, for in-process A/B)
+static int& phi_w1_pf() {
+  static int pf = 0;
+  return pf;
+}
+
+// every phi_w1_kernel launch: the PF form the switch selects
+template <int DS, class... Args>
+static void launch_w1(dim3 grid, hipStream_t s, Args... args) {
+  if (phi_w1_pf())
+    hipLaunchKernelGGL((phi_w1_kernel<DS, 1>), grid, dim3(PhiW1::kThreads), 0, s, args...);
+  else
+    hipLaunchKernelGGL((phi_w1_kernel<DS, 0>), grid, dim3(PhiW1::kThreads), 0, s, args...);
+}
+
 // phi_mm on the FmtH2 engine (TN = 4): phi_w1_kernel (one wave per SIMD, B
 // fragments straight from the image; phi_w1.hpp) -- on the full D layout (row
 // blocks, S > 1) one launch; on the symmetric layout two, each row block
@@ -251,17 +267,17 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
       // slices each
       const int sl = splits / 2;
       const dim3 g1(grid.x, grid.y, sl), g2(grid.x, grid.y, splits - sl);
-      hipLaunchKernelGGL(phi_w1_kernel<1>, g1, dim3(PhiW1::kThreads), 0, s, D, K, Yx, ldy, K,
-                         kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0, gate, gate_on);
+      launch_w1<1>(g1, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0,
+                   gate, gate_on);
       const int rc = check_launch("phi_w1_kernel(lower)");
       if (rc) return rc;
-      hipLaunchKernelGGL(phi_w1_kernel<2>, g2, dim3(PhiW1::kThreads), 0, s, D, K, Yx, ldy, K,
-                         kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, sl, gate, gate_on);
+      launch_w1<2>(g2, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, sl,
+                   gate, gate_on);
       return check_launch("phi_w1_kernel(upper)");
     }
     if (TN == 4 && EXP && !sym) {
-      hipLaunchKernelGGL(phi_w1_kernel<0>, grid, dim3(PhiW1::kThreads), 0, s, D, K, Yx, ldy, K,
-                         kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0, gate, gate_on);
+      launch_w1<0>(grid, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0,
+                   gate, gate_on);
       return check_launch("phi_w1_kernel");
     }
     hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2>), grid,
@@ -942,6 +958,12 @@ int dsvgd_phi_mm_h2(const float* D, int64_t ldd, const void* Yh, int64_t ldy, in
                     row0, (hipStream_t)stream, sym, colinv, gate);
 }
 
+int dsvgd_phi_set_prefetch(int on) {
+  const int old = phi_w1_pf();
+  phi_w1_pf() = on ? 1 : 0;
+  return old;
+}
+
 int dsvgd_phi_h2_window(const float* D, int64_t ldd, const void* Yh, int64_t ldy, int64_t row0,
                         int64_t m, int64_t n, int64_t col0, int64_t wlen,
                         const dsvgd_select_state* st, int64_t splits, float* KY, int64_t ldk,
@@ -960,10 +982,9 @@ int dsvgd_phi_h2_window(const float* D, int64_t ldd, const void* Yh, int64_t ldy
   DSVGD_REQUIRE(((uintptr_t)Yh & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
   const int64_t kchunk = roundup((wlen + splits - 1) / splits, (int64_t)PhiW1::BJ);
   const dim3 grid((unsigned)(ldy / PhiW1::BC), (unsigned)(roundup(m, 128) / 128), (unsigned)splits);
-  hipLaunchKernelGGL(phi_w1_kernel<0>, grid, dim3(PhiW1::kThreads), 0, (hipStream_t)stream, D,
-                     n_pad, (const _Float16*)Yh, ldy, wlen, kchunk, st, KY, ldk, rowsum, m, row0,
-                     0, colinv, 0, gate, gate_on, (int)(col0 / PhiW1::BJ),
-                     (int)(n_pad / PhiW1::BJ), 0);
+  launch_w1<0>(grid, (hipStream_t)stream, D, n_pad, (const _Float16*)Yh, ldy, wlen, kchunk, st, KY,
+               ldk, rowsum, m, row0, 0, colinv, 0, gate, gate_on, (int)(col0 / PhiW1::BJ),
+               (int)(n_pad / PhiW1::BJ), 0);
   return check_launch("phi_w1_kernel(window)");
 }
 
@@ -987,10 +1008,9 @@ int dsvgd_phi_h2_transposed(const float* D, int64_t ldd, const void* Yh, int64_t
   const int64_t kchunk = roundup((krows + splits - 1) / splits, (int64_t)PhiW1::BJ);
   const dim3 grid((unsigned)(ldy / PhiW1::BC), (unsigned)(roundup(mo, 128) / 128),
                   (unsigned)splits);
-  hipLaunchKernelGGL(phi_w1_kernel<3>, grid, dim3(PhiW1::kThreads), 0, (hipStream_t)stream, D,
-                     n_pad, (const _Float16*)Yh, ldy, krows, kchunk, st, P, ldp, rs, mo,
-                     (int64_t)0, 0, colinv, 0, gate, gate_on, (int)(yrow0 / PhiW1::BJ), 0,
-                     (int)(col0 / 128));
+  launch_w1<3>(grid, (hipStream_t)stream, D, n_pad, (const _Float16*)Yh, ldy, krows, kchunk, st, P,
+               ldp, rs, mo, (int64_t)0, 0, colinv, 0, gate, gate_on, (int)(yrow0 / PhiW1::BJ), 0,
+               (int)(col0 / 128));
   return check_launch("phi_w1_kernel(transposed)");
 }
 
@@ -1012,10 +1032,9 @@ int dsvgd_phi_h2_transposed_blocks(const float* D, int64_t ldd, const void* Yh, 
   DSVGD_REQUIRE(((uintptr_t)Yh & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
   const int64_t per = m / 128;
   const dim3 grid((unsigned)(ldy / PhiW1::BC), (unsigned)(per * count), 1u);
-  hipLaunchKernelGGL(phi_w1_kernel<3>, grid, dim3(PhiW1::kThreads), 0, (hipStream_t)stream, D,
-                     n_pad, (const _Float16*)Yh, ldy, m, m, st, P, ldp, P + m * ldp, m, (int64_t)0,
-                     0, colinv, 0, gate, gate_on, (int)(yrow0 / PhiW1::BJ), 0, 0, (int)per,
-                     (int)first, (int)nblocks, pstride);
+  launch_w1<3>(grid, (hipStream_t)stream, D, n_pad, (const _Float16*)Yh, ldy, m, m, st, P, ldp,
+               P + m * ldp, m, (int64_t)0, 0, colinv, 0, gate, gate_on, (int)(yrow0 / PhiW1::BJ), 0,
+               0, (int)per, (int)first, (int)nblocks, pstride);
   return check_launch("phi_w1_kernel(transposed blocks)");
 }
 
