@@ -373,27 +373,33 @@ __global__ __launch_bounds__(256) void phi_finish_kernel(
 // g, g + G, ... (independent loads in flight), then the G group sums are
 // added in g order.  (One thread per position walking all the slices was
 // latency-bound: 122 us for 256 slices of 64 x 512, r11d.)
+// Slice z at P + z zs, its row sums at rs + z zrs; blockIdx.y = part: the
+// inputs ps_in, the outputs ps_out floats after the previous part's.
 __global__ __launch_bounds__(256) void partial_reduce_kernel(
     const float* __restrict__ P, int64_t ldp, const float* __restrict__ rs, int splits,
     int64_t rows, int64_t cols, float* __restrict__ out, int64_t ldo, float* __restrict__ out_rs,
-    int G) {
+    int G, int64_t zs, int64_t zrs, int64_t ps_in, int64_t ps_out) {
   __shared__ f32x4 red[256];
   const int per = 256 / G;
   const int q = threadIdx.x % per, g = threadIdx.x / per;
-  const int64_t c4 = cols >> 2, rp = roundup128(rows);
+  const int64_t c4 = cols >> 2;
+  P += blockIdx.y * ps_in;
+  rs += blockIdx.y * ps_in;
+  out += blockIdx.y * ps_out;
+  out_rs += blockIdx.y * ps_out;
   const int64_t npos = rows * c4, nrs = (rows + 3) >> 2;
   const int64_t p = (int64_t)blockIdx.x * per + q;
   f32x4 a = {0.f, 0.f, 0.f, 0.f};
   if (p < npos) {
     const int64_t i = p / c4, c = (p % c4) * 4;
     for (int z = g; z < splits; z += G)
-      a += *reinterpret_cast<const f32x4*>(P + ((int64_t)z * rows + i) * ldp + c);
+      a += *reinterpret_cast<const f32x4*>(P + (int64_t)z * zs + i * ldp + c);
   } else if (p < npos + nrs) {
     const int64_t i0 = (p - npos) * 4;
     for (int z = g; z < splits; z += G)
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        if (i0 + e < rows) a[e] += rs[(int64_t)z * rp + i0 + e];
+        if (i0 + e < rows) a[e] += rs[(int64_t)z * zrs + i0 + e];
   }
   red[g * per + q] = a;
   __syncthreads();
@@ -1019,6 +1025,17 @@ int dsvgd_phi_h2_transposed_blocks(const float* D, int64_t ldd, const void* Yh, 
                                    int64_t count, int64_t n, const dsvgd_select_state* st,
                                    float* P, int64_t ldp, int64_t pstride, const float* colinv,
                                    const float* gate, int gate_on, void* stream) {
+  return dsvgd_phi_h2_transposed_blocks_split(D, ldd, Yh, ldy, yrow0, m, first, nblocks, count, 1,
+                                              n, st, P, ldp, pstride, colinv, gate, gate_on,
+                                              stream);
+}
+
+int dsvgd_phi_h2_transposed_blocks_split(const float* D, int64_t ldd, const void* Yh, int64_t ldy,
+                                         int64_t yrow0, int64_t m, int64_t first, int64_t nblocks,
+                                         int64_t count, int64_t zsplit, int64_t n,
+                                         const dsvgd_select_state* st, float* P, int64_t ldp,
+                                         int64_t pstride, const float* colinv, const float* gate,
+                                         int gate_on, void* stream) {
   DSVGD_REQUIRE(D && Yh && st && P && colinv, "null pointer");
   const int64_t n_pad = roundup(n, 128);
   DSVGD_REQUIRE(ldd == n_pad, "ldd must equal roundup(n,128) (panel layout)");
@@ -1028,14 +1045,39 @@ int dsvgd_phi_h2_transposed_blocks(const float* D, int64_t ldd, const void* Yh, 
                 "blocks: m a multiple of 128, count <= nblocks, nblocks m <= n_pad");
   DSVGD_REQUIRE(yrow0 >= 0 && yrow0 % 16 == 0 && yrow0 + m <= n_pad, "the rectangle's rows");
   DSVGD_REQUIRE(pstride >= m * ldp + roundup(m, 128), "pstride: room for P and its row sums");
+  DSVGD_REQUIRE(zsplit >= 1 && zsplit <= 64 && m % (16 * zsplit) == 0,
+                "zsplit in [1, 64], m a multiple of 16 zsplit");
   DSVGD_REQUIRE(n_pad * ldy * 4 < ((int64_t)1 << 31), "n x ldy too large for 32-bit offsets");
   DSVGD_REQUIRE(((uintptr_t)Yh & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
   const int64_t per = m / 128;
-  const dim3 grid((unsigned)(ldy / PhiW1::BC), (unsigned)(per * count), 1u);
-  launch_w1<3>(grid, (hipStream_t)stream, D, n_pad, (const _Float16*)Yh, ldy, m, m, st, P, ldp,
+  const dim3 grid((unsigned)(ldy / PhiW1::BC), (unsigned)(per * count), (unsigned)zsplit);
+  launch_w1<3>(grid, (hipStream_t)stream, D, n_pad, (const _Float16*)Yh, ldy, m, m / zsplit, st, P, ldp,
                P + m * ldp, m, (int64_t)0, 0, colinv, 0, gate, gate_on, (int)(yrow0 / PhiW1::BJ), 0,
                0, (int)per, (int)first, (int)nblocks, pstride);
   return check_launch("phi_w1_kernel(transposed blocks)");
+}
+
+int dsvgd_phi_partial_reduce_blocks(const float* P, int64_t ldp, int64_t pstride, int64_t zsplit,
+                                    int64_t count, int64_t rows, int64_t cols, float* out,
+                                    int64_t ldo, int64_t ostride, void* stream) {
+  DSVGD_REQUIRE(P && out, "null pointer");
+  DSVGD_REQUIRE(rows > 0 && cols > 0 && cols % 4 == 0 && ldp >= cols && ldo >= cols &&
+                    ldp % 4 == 0 && ldo % 4 == 0,
+                "sizes (cols, ldp, ldo multiples of 4)");
+  DSVGD_REQUIRE(zsplit >= 1 && zsplit <= 1024 && count >= 1 && count <= 65535, "zsplit, count");
+  DSVGD_REQUIRE(pstride >= rows * ldp + roundup(rows, 128) && ostride >= rows * ldo + rows &&
+                    pstride % 4 == 0 && ostride % 4 == 0,
+                "strides: room for a partial and its row sums");
+  DSVGD_REQUIRE(((uintptr_t)P & 15) == 0 && ((uintptr_t)out & 15) == 0, "16-byte alignment");
+  const int64_t positions = rows * (cols / 4) + (rows + 3) / 4;
+  int G = 1;
+  while (G < zsplit && G < 16) G *= 2;
+  const int64_t per = 256 / G;
+  hipLaunchKernelGGL(partial_reduce_kernel,
+                     dim3((unsigned)((positions + per - 1) / per), (unsigned)count), dim3(256), 0,
+                     (hipStream_t)stream, P, ldp, P + rows * ldp, (int)zsplit, rows, cols, out, ldo,
+                     out + rows * ldo, G, count * pstride, count * pstride, pstride, ostride);
+  return check_launch("partial_reduce(blocks)");
 }
 
 int dsvgd_phi_partial_reduce(const float* P, int64_t ldp, const float* rs, int64_t splits,
@@ -1053,7 +1095,7 @@ int dsvgd_phi_partial_reduce(const float* P, int64_t ldp, const float* rs, int64
   const int64_t per = 256 / G;
   hipLaunchKernelGGL(partial_reduce_kernel, dim3((unsigned)((positions + per - 1) / per)), dim3(256),
                      0, (hipStream_t)stream, P, ldp, rs, (int)splits, rows, cols, out, ldo, out_rs,
-                     G);
+                     G, rows * ldp, roundup(rows, (int64_t)128), (int64_t)0, (int64_t)0);
   return check_launch("partial_reduce");
 }
 

@@ -94,7 +94,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int64_t bz = (DS == 1 || DS == 2) ? lin % gridDim.z : blockIdx.z;
   // DS 3 batched over several column blocks of D (t_per > 0: t_per row
   // blocks of output per part; part q is D's column block (t_first + q) mod
-  // t_nblk, its output t_ostride floats after part q - 1's)
+  // t_nblk, its output t_ostride floats after part q - 1's; split-K slice z
+  // of all parts after slice z - 1's)
   const bool tb = DS == 3 && t_per > 0;
   const int64_t tpart = tb ? by / t_per : 0;
   const int64_t byl = tb ? by % t_per : by;
@@ -123,8 +124,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     ks0 = (int)bz;
     nsteps = T > bz ? (T - (int)bz + Z - 1) / Z : 0;
   }
-  C += (int64_t)(slice0 + bz) * m * ldc + tpart * t_ostride;
-  rowsum += (int64_t)(slice0 + bz) * roundup128(m) + tpart * t_ostride;
+  if (tb) {   // batched DS 3: slice z of part q at (z * parts + q) t_ostride
+    const int64_t at = ((int64_t)bz * (gridDim.y / t_per) + tpart) * t_ostride;
+    C += at;
+    rowsum += at;
+  } else {
+    C += (int64_t)(slice0 + bz) * m * ldc;
+    rowsum += (int64_t)(slice0 + bz) * roundup128(m);
+  }
   const float scale = -st->inv_h * kLog2e;
 
   // D: the block's panel row; thread t stages row t >> 1, columns 8 (t & 1) .. +7

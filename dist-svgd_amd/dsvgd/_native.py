@@ -144,6 +144,11 @@ SIGNATURES = {
                                        _p, _i64, _p, _p, _p, _int, _p]),
     "dsvgd_phi_h2_transposed_blocks": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _i64,
                                               _i64, _p, _p, _i64, _i64, _p, _p, _int, _p]),
+    "dsvgd_phi_h2_transposed_blocks_split": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _i64,
+                                                    _i64, _i64, _i64, _p, _p, _i64, _i64, _p, _p,
+                                                    _int, _p]),
+    "dsvgd_phi_partial_reduce_blocks": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _i64,
+                                               _i64, _p]),
     "dsvgd_phi_partial_reduce": (_int, [_p, _i64, _p, _i64, _i64, _i64, _p, _i64, _p, _p]),
     "dsvgd_phi_finish_parts": (_int, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _p, _f,
                                       _f, _p, _i64, _p, _i64, _p, _i64, _p, _int, _p, _i64, _p]),

@@ -150,6 +150,12 @@ class PhiEngine(object):
     # Off: measured slower, partials 0.98-1.00 vs 0.78 ms at S = 8 in one
     # process (profiles/r11m/rank_rest.log)
     REST_BESIDE = False
+    # pair split: the batched forward launch's K range (each block's m rows
+    # of D) split into this many slices so that its workgroups fill whole
+    # waves of the 256 CUs (None: chosen -- S = 8 at the headline: 3 x 64
+    # workgroups x 4 = three full waves instead of 192 of 256), the slices
+    # summed in order into the messages (dsvgd_phi_partial_reduce_blocks)
+    FWD_ZSPLIT = None
 
     GEMMS = ("h2", "x3", "f32")
     DEFAULT_GEMM = "h2"
@@ -608,6 +614,12 @@ class PhiEngine(object):
         self.fwd_msg = self.m * ldy + lib.dsvgd_pad128(self.m)
         self.fwd_batched = nf > 0 and nf * (self.m // 128) * (ldy // 512) >= 192
         self.send_fwd = torch.empty(max(1, nf) * self.fwd_msg, **f32) if self.fwd_batched else None
+        self.fwd_z = 1
+        if self.fwd_batched:
+            wg = nf * (self.m // 128) * (ldy // 512)
+            self.fwd_z = self.FWD_ZSPLIT or self.fill_split(wg, self.m)
+        self.fwd_tmp = (torch.empty(self.fwd_z * nf * self.fwd_msg, **f32)
+                        if self.fwd_z > 1 else None)
         self.t_splits = []
         smax = 0
         for q in P.sends:
@@ -645,6 +657,21 @@ class PhiEngine(object):
             a.ky, a.rs, a.ldk, a.row_off, a.rows, a.splits = q
         self._phiparts = arr
 
+    @staticmethod
+    def fill_split(wg, rows, cus=256, min_rows=1024):
+        """The split-K factor z (a power of two, rows / z >= min_rows) whose
+        wg * z workgroups -- one per CU at a time -- fill whole waves of the
+        CUs best (ties: the smallest z)."""
+        best, best_eff = 1, 0.0
+        z = 1
+        while z <= 16 and rows // z >= min_rows and rows % (16 * z) == 0:
+            w = wg * z
+            eff = w / (cus * -(-w // cus))
+            if eff > best_eff + 1e-9:
+                best, best_eff = z, eff
+            z *= 2
+        return best
+
     def _gram_parts(self, arr, mode, st, cand, s, gate=None):
         N.call("dsvgd_sqdist_h2_parts", N.ptr(self.Yg), N.ptr(self.norms), self.row0, self.m,
                self.n, self.d, N.ptr(self.D), self.n_pad, mode, st, cand, ctypes.addressof(arr),
@@ -669,7 +696,14 @@ class PhiEngine(object):
             if self.WINDOW_SIDE_STREAM else None
         with span(self.timer, "phi_partials"):
             nf = len(P.forward) if self.fwd_batched else 0
-            if nf:
+            if nf and self.fwd_z > 1:
+                N.call("dsvgd_phi_h2_transposed_blocks_split", N.ptr(self.D), self.n_pad,
+                       N.ptr(self.Yx), ldy, self.row0, self.m, (P.rank + 1) % P.S, P.S, nf,
+                       self.fwd_z, self.n, self.state.ptr, N.ptr(self.fwd_tmp), ldy,
+                       self.fwd_msg, colinv, guard, 0, s)
+                N.call("dsvgd_phi_partial_reduce_blocks", N.ptr(self.fwd_tmp), ldy, self.fwd_msg,
+                       self.fwd_z, nf, self.m, ldy, N.ptr(self.send_fwd), ldy, self.fwd_msg, s)
+            elif nf:
                 N.call("dsvgd_phi_h2_transposed_blocks", N.ptr(self.D), self.n_pad,
                        N.ptr(self.Yx), ldy, self.row0, self.m, (P.rank + 1) % P.S, P.S, nf,
                        self.n, self.state.ptr, N.ptr(self.send_fwd), ldy, self.fwd_msg, colinv,

@@ -448,6 +448,22 @@ int dsvgd_phi_h2_transposed_blocks(const float* D, int64_t ldd, const void* Yh, 
                                    int64_t count, int64_t n, const dsvgd_select_state* st,
                                    float* P, int64_t ldp, int64_t pstride, const float* colinv,
                                    const float* gate, int gate_on, void* stream);
+/* dsvgd_phi_h2_transposed_blocks with each block's K range (its m rows of D)
+ * split into zsplit slices (m a multiple of 16 zsplit), so that count x
+ * m/128 x zsplit workgroups fill the CUs: slice z of block q written at
+ * P + (z count + q) pstride (dsvgd_phi_partial_reduce_blocks sums them). */
+int dsvgd_phi_h2_transposed_blocks_split(const float* D, int64_t ldd, const void* Yh, int64_t ldy,
+                                         int64_t yrow0, int64_t m, int64_t first, int64_t nblocks,
+                                         int64_t count, int64_t zsplit, int64_t n,
+                                         const dsvgd_select_state* st, float* P, int64_t ldp,
+                                         int64_t pstride, const float* colinv, const float* gate,
+                                         int gate_on, void* stream);
+/* For q < count: out + q ostride = sum over z < zsplit (in slice order) of
+ * the [rows x ldp | row sums] partial at P + (z count + q) pstride (row sums
+ * at + rows ldp in, + rows ldo out) -- the split forward blocks' messages. */
+int dsvgd_phi_partial_reduce_blocks(const float* P, int64_t ldp, int64_t pstride, int64_t zsplit,
+                                    int64_t count, int64_t rows, int64_t cols, float* out,
+                                    int64_t ldo, int64_t ostride, void* stream);
 /* out[i][c] = sum_z P[z][i][c] (c < cols) and out_rs[i] = sum_z rs[z][i], in
  * slice order (the P / rs layout of dsvgd_phi_h2_transposed). */
 int dsvgd_phi_partial_reduce(const float* P, int64_t ldp, const float* rs, int64_t splits,

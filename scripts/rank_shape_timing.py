@@ -26,6 +26,10 @@ def main():
                     help="pairs: comma list of PhiEngine.REST_BESIDE settings (1, 0)")
     ap.add_argument("--side", default="0",
                     help="pairs: comma list of PhiEngine.WINDOW_SIDE_STREAM settings (0, 1)")
+    ap.add_argument("--fwdz", default="0",
+                    help="pairs: comma list of PhiEngine.FWD_ZSPLIT settings (0 = chosen, 1 = none)")
+    ap.add_argument("--pf", default=None,
+                    help="comma list of phi_w1 prefetch settings (dsvgd_phi_set_prefetch)")
     ap.add_argument("--layout", default="both", choices=["rows", "pairs", "both"],
                     help="rows: the row-block layout; pairs: the pair-split layout (DESIGN.md 6; "
                          "the partials' exchange left out, their buffers zero)")
@@ -40,17 +44,24 @@ def main():
     g = torch.Generator(device="cpu").manual_seed(0)
     X = (0.1 * torch.randn(n, d, generator=g)).cuda()
     runs = []
+    pfs = [None] if args.pf is None else [int(v) for v in args.pf.split(",")]
     for S in [int(v) for v in args.shards.split(",")]:
-        for lay in (("rows", "pairs") if args.layout == "both" else (args.layout,)):
-            if lay == "rows":
-                runs.append((S, lay, False, True))
-            elif S > 1 and dsvgd.PhiEngine.pair_split_ok(n, d, S):
-                for side in args.side.split(","):
-                    for rest in args.rest.split(","):
-                        runs.append((S, lay, bool(int(side)), bool(int(rest))))
-    for S, lay, side, *rest in runs:
+        for pf in pfs:
+            for lay in (("rows", "pairs") if args.layout == "both" else (args.layout,)):
+                if lay == "rows":
+                    runs.append((S, lay, False, True, 0, pf))
+                elif S > 1 and dsvgd.PhiEngine.pair_split_ok(n, d, S):
+                    for side in args.side.split(","):
+                        for rest in args.rest.split(","):
+                            for fz in args.fwdz.split(","):
+                                runs.append((S, lay, bool(int(side)), bool(int(rest)), int(fz), pf))
+    lib = dsvgd._native.load()
+    for S, lay, side, rest, fz, pf in runs:
         dsvgd.PhiEngine.WINDOW_SIDE_STREAM = side
-        dsvgd.PhiEngine.REST_BESIDE = rest[0] if rest else True
+        dsvgd.PhiEngine.REST_BESIDE = rest
+        dsvgd.PhiEngine.FWD_ZSPLIT = fz or None
+        if pf is not None:
+            lib.dsvgd_phi_set_prefetch(pf)
         m, r = n // S, S // 2          # a middle rank (a high one of the pair split)
         per = Ng // S
         tgt = dsvgd.targets.LogisticRegression(x[r * per:(r + 1) * per], t[r * per:(r + 1) * per])
@@ -101,7 +112,8 @@ def main():
         st = {k: round(float(np.mean(v)), 3) for k, v in timer.summary().items()}
         print(json.dumps({"shards": S, "layout": lay + ("+side" if side else "")
                           + ("+rest" if lay == "pairs" and eng.plan is not None
-                             and eng.rest_beside else ""), "m": m,
+                             and eng.rest_beside else ""), "m": m, "pf": pf,
+                          "fwd_z": getattr(eng, "fwd_z", None),
                           "row0": r * m, "N_local": per,
                           "ms_per_step_no_comm": e0.elapsed_time(e1) / args.steps,
                           "sym_layout": bool(eng.sym), "stages_ms": st}), flush=True)
