@@ -26,9 +26,20 @@ static int& phi_w1_pf() {
 }
 
 // every phi_w1_kernel launch: the PF form the switch selects
+// (settings 11 .. 15: phi_w1_kernel's timing probes on DS 2, wrong results)
 template <int DS, class... Args>
 static void launch_w1(dim3 grid, hipStream_t s, Args... args) {
-  if (phi_w1_pf())
+  const int v = phi_w1_pf();
+  if constexpr (DS == 2) {
+#define DSVGD_W1_PROBE(P)                                                                           \
+  if (v == 10 + (P)) {                                                                              \
+    hipLaunchKernelGGL((phi_w1_kernel<DS, 0, P>), grid, dim3(PhiW1::kThreads), 0, s, args...);      \
+    return;                                                                                         \
+  }
+    DSVGD_W1_PROBE(1) DSVGD_W1_PROBE(2) DSVGD_W1_PROBE(3) DSVGD_W1_PROBE(4) DSVGD_W1_PROBE(5)
+#undef DSVGD_W1_PROBE
+  }
+  if (v == 1)
     hipLaunchKernelGGL((phi_w1_kernel<DS, 1>), grid, dim3(PhiW1::kThreads), 0, s, args...);
   else
     hipLaunchKernelGGL((phi_w1_kernel<DS, 0>), grid, dim3(PhiW1::kThreads), 0, s, args...);
@@ -966,7 +977,7 @@ int dsvgd_phi_mm_h2(const float* D, int64_t ldd, const void* Yh, int64_t ldy, in
 
 int dsvgd_phi_set_prefetch(int on) {
   const int old = phi_w1_pf();
-  phi_w1_pf() = on ? 1 : 0;
+  phi_w1_pf() = (on >= 11 && on <= 15) ? on : (on ? 1 : 0);
   return old;
 }
 

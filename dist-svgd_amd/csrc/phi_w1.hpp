@@ -69,7 +69,10 @@ __device__ __forceinline__ f32x4 w1_load_nt(__amdgpu_buffer_rsrc_t r, int voff, 
 // and reads A(k+1)'s MFMA fragments into a second register set among its
 // MFMAs, so no wave waits on LDS after the K-step's barrier (PF = 0: the
 // fragments of A(k) are read right after it, ahead of the first MFMA)
-template <int DS, int PF = 0>
+// PROBE (timing probes only, results wrong; dsvgd_phi_set_prefetch 11..15
+// on DS 2): 1 D loads from K-step 0 (L2-resident), 2 B loads from K-step 0,
+// 3 no barrier, 4 staging without the exp / split VALU, 5 = 1 + 2
+template <int DS, int PF = 0, int PROBE = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void phi_w1_kernel(
     const float* A, int64_t a_npad, const _Float16* Yx, int64_t ldy,
     int64_t K, int64_t kchunk, const dsvgd_select_state* __restrict__ st, float* __restrict__ C,
@@ -179,13 +182,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     f32x4 tr[2];      // DS 1: K-step k+1's values, transposed during K-step k - 1
     const int last = nsteps - 1;
     auto loadB = [&](int ni, int k) {
-      const int soff = (wrapk(ks0 + kdir * min(k, last)) + kyoff) * P * pstride;
+      const int soff = (PROBE == 2 || PROBE == 5) ? 0 : (wrapk(ks0 + kdir * min(k, last)) + kyoff) * P * pstride;
 #pragma unroll
       for (int p = 0; p < P; ++p)
         b[ni][p] = __builtin_bit_cast(V8, w1_load(rB, vB + ni * 1024, soff + p * pstride));
     };
     auto loadD = [&](f32x4 (&d)[2], int k) {
-      const int kc = min(k, last);
+      const int kc = (PROBE == 1 || PROBE == 5) ? 0 : min(k, last);
       const int64_t j0 = (int64_t)wrapk(ks0 + kdir * kc) * PhiW1::BJ;
       if constexpr (TR) {
         const float* src = A + (((j0 >> 7) * pcols + symI * 8) * kPanelElems + (j0 & 127) * 16);
@@ -217,7 +220,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const float v = q < 4 ? d[0][q] : d[1][q - 4];
-        const float x = __builtin_amdgcn_exp2f(fmaf(v, scale, F::kAScaleLog2));
+        const float x = PROBE == 4 ? v : __builtin_amdgcn_exp2f(fmaf(v, scale, F::kAScaleLog2));
         e[q] = (!TR && qd == q) ? 0.f : x;
       }
       const float s = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
@@ -227,12 +230,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int q = 0; q < 8; ++q) {
         const _Float16 a0 = (_Float16)e[q];
         p0[q] = a0;
-        p1[q] = (_Float16)(e[q] - (float)a0);
+        p1[q] = PROBE == 4 ? a0 : (_Float16)(e[q] - (float)a0);
       }
       *reinterpret_cast<V8*>(st_ + aoff) = p0;
       *reinterpret_cast<V8*>(st_ + PhiW1::BM * 32 + aoff) = p1;
     };
-    auto barrier = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    auto barrier = []() {
+      if constexpr (PROBE == 3)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
     // K-step k (slot KS = k & 3) from stage cur: A(k+1) -> stage nxt; MFMAs
     // column tile by column tile, each tile's B reloaded for k+1; then D(k+3)
     // (DS 1: stages tr = K-step k+1, and transposes dt = D(k+2) into tr)

@@ -904,6 +904,7 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
       if (!hit) {  // full scan over all columns, refill the cache (global + table)
         tsc0 = wall_clock64();
         scan(i, mine, floor);
+        if (stalled) break;   // no lists: leave the row's cache and the slot as they are
         const double ev = lane < kCache + 1 ? outv[lane] : -DBL_MAX;
         const int ej = lane < kCache + 1 ? outj[lane] : INT32_MAX;
         if (lane < kCache) {
@@ -933,6 +934,7 @@ __global__ __launch_bounds__(kTailThreads) void w2_tail_kernel(const float* __re
       }
     } else {
       scan(i, mine, -DBL_MAX);
+      if (stalled) break;
       b1 = outv[0];
       b2 = outv[1];
       bj = outj[0];
