@@ -18,31 +18,10 @@
 
 namespace dsvgd {
 
-// phi_w1_kernel's A-fragment prefetch (PF template argument; process-wide
-// switch dsvgd_phi_set_prefetch, for in-process A/B)
-static int& phi_w1_pf() {
-  static int pf = 0;
-  return pf;
-}
-
-// every phi_w1_kernel launch: the PF form the switch selects
-// (settings 11 .. 15: phi_w1_kernel's timing probes on DS 2, wrong results)
+// every phi_w1_kernel launch
 template <int DS, class... Args>
 static void launch_w1(dim3 grid, hipStream_t s, Args... args) {
-  const int v = phi_w1_pf();
-  if constexpr (DS == 2) {
-#define DSVGD_W1_PROBE(P)                                                                           \
-  if (v == 10 + (P)) {                                                                              \
-    hipLaunchKernelGGL((phi_w1_kernel<DS, 0, P>), grid, dim3(PhiW1::kThreads), 0, s, args...);      \
-    return;                                                                                         \
-  }
-    DSVGD_W1_PROBE(1) DSVGD_W1_PROBE(2) DSVGD_W1_PROBE(3) DSVGD_W1_PROBE(4) DSVGD_W1_PROBE(5)
-#undef DSVGD_W1_PROBE
-  }
-  if (v == 1)
-    hipLaunchKernelGGL((phi_w1_kernel<DS, 1>), grid, dim3(PhiW1::kThreads), 0, s, args...);
-  else
-    hipLaunchKernelGGL((phi_w1_kernel<DS, 0>), grid, dim3(PhiW1::kThreads), 0, s, args...);
+  hipLaunchKernelGGL((phi_w1_kernel<DS>), grid, dim3(PhiW1::kThreads), 0, s, args...);
 }
 
 // phi_mm on the FmtH2 engine (TN = 4): phi_w1_kernel (one wave per SIMD, B
@@ -973,12 +952,6 @@ int dsvgd_phi_mm_h2(const float* D, int64_t ldd, const void* Yh, int64_t ldy, in
                 "sym: the symmetric layout needs m == n, row0 == 0, ldy % 256 == 0");
   return nn_h2_gemm(true, D, n_pad, (const _Float16*)Yh, ldy, (int)splits, st, KY, ldk, rowsum, m,
                     row0, (hipStream_t)stream, sym, colinv, gate);
-}
-
-int dsvgd_phi_set_prefetch(int on) {
-  const int old = phi_w1_pf();
-  phi_w1_pf() = (on >= 11 && on <= 15) ? on : (on ? 1 : 0);
-  return old;
 }
 
 int dsvgd_phi_h2_window(const float* D, int64_t ldd, const void* Yh, int64_t ldy, int64_t row0,

@@ -31,8 +31,6 @@ struct PhiW1 {
   static constexpr int kThreads = 256;
   static constexpr int BM = 128, BC = 512, BJ = 16, P = 2;
   static constexpr int SA = P * BM * 32;  // one stage's A image (8 KiB)
-  // stages of the A image: 2, or 3 with the fragment prefetch (PF = 1)
-  static constexpr int smem_bytes(int pf) { return (pf ? 3 : 2) * SA; }
   static constexpr int kSmemBytes = 2 * SA;
   // DS = 1: per-wave transpose scratch, [16 j][kScrLd floats] for the wave's
   // 32 rows; kScrLd = 44: the 16-byte writes of 8 lanes and the dword reads
@@ -65,14 +63,7 @@ __device__ __forceinline__ f32x4 w1_load_nt(__amdgpu_buffer_rsrc_t r, int voff, 
 //     a panel-row boundary), and the image K-step of D row j is ks_begin + j/16
 //     (the owned rows' place in the interacting set): C = K(rows, cols)^T Y_rows,
 //     the partial a rank sends to the owner of those columns.
-// PF = 1 (the fragment prefetch): three A stages; K-step k stages A(k+2)
-// and reads A(k+1)'s MFMA fragments into a second register set among its
-// MFMAs, so no wave waits on LDS after the K-step's barrier (PF = 0: the
-// fragments of A(k) are read right after it, ahead of the first MFMA)
-// PROBE (timing probes only, results wrong; dsvgd_phi_set_prefetch 11..15
-// on DS 2): 1 D loads from K-step 0 (L2-resident), 2 B loads from K-step 0,
-// 3 no barrier, 4 staging without the exp / split VALU, 5 = 1 + 2
-template <int DS, int PF = 0, int PROBE = 0>
+template <int DS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void phi_w1_kernel(
     const float* A, int64_t a_npad, const _Float16* Yx, int64_t ldy,
     int64_t K, int64_t kchunk, const dsvgd_select_state* __restrict__ st, float* __restrict__ C,
@@ -85,8 +76,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   using V8 = F::V8;
   constexpr int P = PhiW1::P;
   constexpr bool TR = DS == 1 || DS == 3;
-  constexpr int kSm = PhiW1::smem_bytes(PF);
-  __shared__ __attribute__((aligned(16))) char smem[kSm + (TR ? 4 * PhiW1::kScrBytes : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[PhiW1::kSmemBytes + (TR ? 4 * PhiW1::kScrBytes : 0)];
   const int t = threadIdx.x, lane = t & 63, r = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   // DS 1 / 2: a row block's slices dispatched back to back, longest first
@@ -171,7 +161,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // .. +7 of column j0 + (s >> 1): 32 contiguous bytes of panel I*8 + p
   const int vP = (t >> 5) * kPanelElems * 4 + (t & 31) * 32;
   // DS 1 scratch of this wave: element (i' = row - 32 w, j) at j * kScrLd + i'
-  float* const scr = reinterpret_cast<float*>(smem + kSm + w * PhiW1::kScrBytes);
+  float* const scr = reinterpret_cast<float*>(smem + PhiW1::kSmemBytes + w * PhiW1::kScrBytes);
   const int sw_off = ((lane & 31) >> 1) * PhiW1::kScrLd + 16 * (lane >> 5) + 8 * (lane & 1);
   const int sr_off = 8 * shalf * PhiW1::kScrLd + (lane >> 1);
 
@@ -182,13 +172,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     f32x4 tr[2];      // DS 1: K-step k+1's values, transposed during K-step k - 1
     const int last = nsteps - 1;
     auto loadB = [&](int ni, int k) {
-      const int soff = (PROBE == 2 || PROBE == 5) ? 0 : (wrapk(ks0 + kdir * min(k, last)) + kyoff) * P * pstride;
+      const int soff = (wrapk(ks0 + kdir * min(k, last)) + kyoff) * P * pstride;
 #pragma unroll
       for (int p = 0; p < P; ++p)
         b[ni][p] = __builtin_bit_cast(V8, w1_load(rB, vB + ni * 1024, soff + p * pstride));
     };
     auto loadD = [&](f32x4 (&d)[2], int k) {
-      const int kc = (PROBE == 1 || PROBE == 5) ? 0 : min(k, last);
+      const int kc = min(k, last);
       const int64_t j0 = (int64_t)wrapk(ks0 + kdir * kc) * PhiW1::BJ;
       if constexpr (TR) {
         const float* src = A + (((j0 >> 7) * pcols + symI * 8) * kPanelElems + (j0 & 127) * 16);
@@ -220,7 +210,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const float v = q < 4 ? d[0][q] : d[1][q - 4];
-        const float x = PROBE == 4 ? v : __builtin_amdgcn_exp2f(fmaf(v, scale, F::kAScaleLog2));
+        const float x = __builtin_amdgcn_exp2f(fmaf(v, scale, F::kAScaleLog2));
         e[q] = (!TR && qd == q) ? 0.f : x;
       }
       const float s = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
@@ -230,17 +220,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int q = 0; q < 8; ++q) {
         const _Float16 a0 = (_Float16)e[q];
         p0[q] = a0;
-        p1[q] = PROBE == 4 ? a0 : (_Float16)(e[q] - (float)a0);
+        p1[q] = (_Float16)(e[q] - (float)a0);
       }
       *reinterpret_cast<V8*>(st_ + aoff) = p0;
       *reinterpret_cast<V8*>(st_ + PhiW1::BM * 32 + aoff) = p1;
     };
-    auto barrier = []() {
-      if constexpr (PROBE == 3)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      else
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    };
+    auto barrier = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
     // K-step k (slot KS = k & 3) from stage cur: A(k+1) -> stage nxt; MFMAs
     // column tile by column tile, each tile's B reloaded for k+1; then D(k+3)
     // (DS 1: stages tr = K-step k+1, and transposes dt = D(k+2) into tr)
@@ -291,109 +276,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       loadD(dl, k + 3);
     };
 
-    if constexpr (PF) {
-      // ---- the fragment prefetch: stages S(j) = smem + (j % 3) SA hold
-      // A(j); D(j) in ring slot j % 3 (dp[3]: two K-steps of load distance,
-      // as below).  K-step k: stage A(k+2) (from D(k+2); DS 1/3: from tr, the
-      // transposed D(k+2)), MFMAs on ac = A(k)'s fragments, read A(k+1)'s
-      // fragments (staged during k - 1, visible since its barrier) into an,
-      // then (DS 1/3) transpose D(k+3) into tr, load D(k+4) (DS 1/3: D(k+5))
-      // into the freed slot; one barrier.  Stage S(k+2) last held A(k-1),
-      // whose fragments were read during k - 2: two barriers ago.
-      f32x4 dp[3][2];
-      V8 fa[4][P], fb[4][P];
-      auto readA = [&](V8 (&a)[4][P], const char* src) {
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-          for (int p = 0; p < P; ++p)
-            a[mi][p] = *reinterpret_cast<const V8*>(src + p * PhiW1::BM * 32 + x3_off(mi * 32 + r, h));
-      };
-      auto stepP = [&](int k, const V8 (&ac)[4][P], V8 (&an)[4][P], char* stg, const char* rd,
-                       const f32x4 (&ds_)[2], f32x4 (&dl)[2], const f32x4 (&dt)[2]) {
-        if constexpr (TR)
-          stage(stg, tr, k + 2);
-        else
-          stage(stg, ds_, k + 2);
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi) acc[mi][ni] = mfma_fmt<F>(ac[mi][1], b[ni][0], acc[mi][ni]);
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi) acc[mi][ni] = mfma_fmt<F>(ac[mi][0], b[ni][1], acc[mi][ni]);
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi) acc[mi][ni] = mfma_fmt<F>(ac[mi][0], b[ni][0], acc[mi][ni]);
-          loadB(ni, k + 1);
-        }
-        readA(an, rd);
-        if constexpr (TR) transpose(dt, tr);
-        // 16 MFMAs each followed by the staging VALU, its two LDS stores,
-        // then the other 32 MFMAs with (DS 1/3) the transpose's LDS traffic,
-        // A(k+1)'s eight fragment reads and the eight B loads among them
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, kW1Sgb, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
-#pragma unroll
-        for (int i = 0; i < 32; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          if (TR && i == 1) __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
-          if (TR && i >= 2 && i < 10) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          if (i >= (TR ? 10 : 2) && i < (TR ? 18 : 10)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          if (i % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-        }
-        loadD(dl, k + (TR ? 5 : 4));
-      };
-      char* const S0 = smem;
-      char* const S1 = smem + PhiW1::SA;
-      char* const S2 = smem + 2 * PhiW1::SA;
-      // prologue: B(0), D(0..2); A(0) -> S0, A(1) -> S1 (DS 1/3 through tr),
-      // D(3) (DS 1/3: and D(4)) behind them; A(0)'s fragments
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) loadB(ni, 0);
-      loadD(dp[0], 0);
-      loadD(dp[1], 1);
-      loadD(dp[2], 2);
-      if constexpr (TR) {
-        transpose(dp[0], tr);
-        stage(S0, tr, 0);
-        transpose(dp[1], tr);
-        stage(S1, tr, 1);
-        loadD(dp[0], 3);
-        transpose(dp[2], tr);
-        loadD(dp[1], 4);
-      } else {
-        stage(S0, dp[0], 0);
-        loadD(dp[0], 3);
-        stage(S1, dp[1], 1);
-      }
-      barrier();
-      readA(fa, S0);
-      // unrolled by 6: the stage (3), ring slot (3) and fragment set (2)
-      // indices are compile-time.  Non-TR: stage from slot (k+2)%3, load
-      // into (k+1)%3; TR: transpose slot k%3, load into (k+2)%3
-      for (int k = 0; k < nsteps; k += 6) {
-        stepP(k, fa, fb, S2, S1, dp[2], TR ? dp[2] : dp[1], dp[0]);
-        barrier();
-        if (k + 1 >= nsteps) break;
-        stepP(k + 1, fb, fa, S0, S2, dp[0], TR ? dp[0] : dp[2], dp[1]);
-        barrier();
-        if (k + 2 >= nsteps) break;
-        stepP(k + 2, fa, fb, S1, S0, dp[1], TR ? dp[1] : dp[0], dp[2]);
-        barrier();
-        if (k + 3 >= nsteps) break;
-        stepP(k + 3, fb, fa, S2, S1, dp[2], TR ? dp[2] : dp[1], dp[0]);
-        barrier();
-        if (k + 4 >= nsteps) break;
-        stepP(k + 4, fa, fb, S0, S2, dp[0], TR ? dp[0] : dp[2], dp[1]);
-        barrier();
-        if (k + 5 >= nsteps) break;
-        stepP(k + 5, fb, fa, S1, S0, dp[1], TR ? dp[1] : dp[0], dp[2]);
-        barrier();
-      }
-    } else {
     // prologue: B(0), D(0..2); A(0) -> stage 0 (DS 1: D(0), D(1) transposed)
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) loadB(ni, 0);
@@ -435,7 +317,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if (k + 7 >= nsteps) break;
       step(k + 7, smem + PhiW1::SA, smem, dr[0], dr[2], dr[1]);
       barrier();
-    }
     }
   }
 

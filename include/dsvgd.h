@@ -412,11 +412,6 @@ int dsvgd_sqdist_h2_parts(const void* Yg, const float* norms, int64_t row0, int6
  * wmap[I * (n_pad / 128) + J] times (0: not an entry of this rank's share). */
 int dsvgd_radix_hist_wmap(const float* D, int64_t m_pad, int64_t n_pad, const float* cand,
                           int pass, dsvgd_select_state* st, const uint8_t* wmap, void* stream);
-/* Process-wide switch of phi_w1_kernel's A-fragment prefetch (three A
- * stages; each K-step reads the next one's MFMA fragments among its MFMAs):
- * 1 on, 0 off (two stages, fragments read after the barrier).  Same results
- * bit for bit either way (same MFMA order).  Returns the previous setting. */
-int dsvgd_phi_set_prefetch(int on);
 /* phi_mm (FmtH2) of rows [row0, row0 + m) of the interacting set (D: their
  * panel rows) over a CYCLIC window of columns [col0, col0 + wlen) mod
  * n_pad, into `splits` split-K slices (KY + z m ldk, rowsum + z

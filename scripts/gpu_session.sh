@@ -24,7 +24,6 @@ for s in ${STEPS:-smoke tests bench prof}; do
     bench) step bench 900 python bench.py --steps ${BSTEPS:-10} --warmup 3 ${BENCH_ARGS:-} ;;
     prof)  step prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     ab)    step ab 600 python scripts/ab_kernels.py ;;
-    pfab)  step pfab 600 python scripts/phi_pf_ab.py ${PFAB_ARGS:-} ;;
     w2)    step w2 600 python scripts/w2_timing.py ${W2_ARGS:-} ;;
     diag)  step diag 600 python scripts/diag_precision.py ;;
     pmc)   step pmc 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;

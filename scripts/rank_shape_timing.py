@@ -28,8 +28,6 @@ def main():
                     help="pairs: comma list of PhiEngine.WINDOW_SIDE_STREAM settings (0, 1)")
     ap.add_argument("--fwdz", default="0",
                     help="pairs: comma list of PhiEngine.FWD_ZSPLIT settings (0 = chosen, 1 = none)")
-    ap.add_argument("--pf", default=None,
-                    help="comma list of phi_w1 prefetch settings (dsvgd_phi_set_prefetch)")
     ap.add_argument("--layout", default="both", choices=["rows", "pairs", "both"],
                     help="rows: the row-block layout; pairs: the pair-split layout (DESIGN.md 6; "
                          "the partials' exchange left out, their buffers zero)")
@@ -44,7 +42,7 @@ def main():
     g = torch.Generator(device="cpu").manual_seed(0)
     X = (0.1 * torch.randn(n, d, generator=g)).cuda()
     runs = []
-    pfs = [None] if args.pf is None else [int(v) for v in args.pf.split(",")]
+    pfs = [None]
     for S in [int(v) for v in args.shards.split(",")]:
         for pf in pfs:
             for lay in (("rows", "pairs") if args.layout == "both" else (args.layout,)):
@@ -60,8 +58,6 @@ def main():
         dsvgd.PhiEngine.WINDOW_SIDE_STREAM = side
         dsvgd.PhiEngine.REST_BESIDE = rest
         dsvgd.PhiEngine.FWD_ZSPLIT = fz or None
-        if pf is not None:
-            lib.dsvgd_phi_set_prefetch(pf)
         m, r = n // S, S // 2          # a middle rank (a high one of the pair split)
         per = Ng // S
         tgt = dsvgd.targets.LogisticRegression(x[r * per:(r + 1) * per], t[r * per:(r + 1) * per])
