@@ -991,6 +991,11 @@ class _WideSweep(object):
         self.rowsum = torch.empty(z * 128, **f32)
         self.Q = torch.empty(self.B, self.ldy, **f32)
         self.Qr = torch.empty(128, **f32)
+        # the pipelined sweep: block b + 1's sums beside block b's, and the
+        # stream its wide pass runs on
+        self.Q2 = torch.empty(self.B, self.ldy, **f32)
+        self.Qr2 = torch.empty(128, **f32)
+        self.side = None
 
     def images(self, r0, nr, s):
         """(Re)split rows [r0, r0 + nr) of Y into the engines' images (the
@@ -1014,6 +1019,33 @@ class _WideSweep(object):
 
 
 _WIDE = {}
+# the wide pass of block b + 1 on a second stream while block b walks (block
+# b's columns left out, then added at their moved positions by
+# dsvgd_gsw_prev_corr); False: one stream, block after block
+GSW_PIPELINE = True
+
+
+def _wide_pass(W, b0, nb, n, d, h_state, Q, Qr, s, exclude=None):
+    """Q = [K Xc | K S], Qr = K 1 of rows [b0, b0 + nb) against every row
+    except the block's own earlier ones (and the `exclude` = (p0, pB) block)."""
+    if W.gram_h2:
+        N.call("dsvgd_sqdist_h2", N.ptr(W.Yg), N.ptr(W.norms), b0, nb, n, d, N.ptr(W.D),
+               W.n_pad, 0, None, None, 0, N.ptr(W.rsc), s)
+    else:
+        N.call("dsvgd_sqdist", N.ptr(W.Y), W.ldy, N.ptr(W.norms), b0, nb, n, d, N.ptr(W.D),
+               W.n_pad, 0, None, None, s)
+    N.call("dsvgd_gs_mask", N.ptr(W.D), W.n_pad, b0, nb, s)
+    if exclude is not None:
+        N.call("dsvgd_gs_mask_cols", N.ptr(W.D), W.n_pad, nb, exclude[0], exclude[1], s)
+    if W.phi_x3:
+        N.call("dsvgd_phi_mm_x3", N.ptr(W.D), W.n_pad, N.ptr(W.Yx3), W.ldy, b0, nb, n,
+               h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), 0, int(W.m16),
+               None, s)
+    else:
+        N.call("dsvgd_phi_mm", N.ptr(W.D), W.n_pad, N.ptr(W.Y), W.ldy, b0, nb, n,
+               h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), s)
+    N.call("dsvgd_phi_partial_reduce", N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), W.splits, nb,
+           2 * W.dp, N.ptr(Q), W.ldy, N.ptr(Qr), s)
 
 
 def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s):
@@ -1039,34 +1071,62 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
            W.Y.shape[0], N.ptr(W.Y), W.ldy, N.ptr(W.norms), s)
     W.images(0, W.n_pad, s)
     B = W.B
-    for b0 in range(rows.start, rows.stop, B):
-        nb = min(B, rows.stop - b0)
+    blocks = [(b0, min(B, rows.stop - b0)) for b0 in range(rows.start, rows.stop, B)]
+
+    def walk(b0, nb, Q, Qr):
         k0 = b0 - rows.start
-        if W.gram_h2:
-            N.call("dsvgd_sqdist_h2", N.ptr(W.Yg), N.ptr(W.norms), b0, nb, n, d, N.ptr(W.D),
-                   W.n_pad, 0, None, None, 0, N.ptr(W.rsc), s)
-        else:
-            N.call("dsvgd_sqdist", N.ptr(W.Y), W.ldy, N.ptr(W.norms), b0, nb, n, d, N.ptr(W.D),
-                   W.n_pad, 0, None, None, s)
-        N.call("dsvgd_gs_mask", N.ptr(W.D), W.n_pad, b0, nb, s)
-        if W.phi_x3:
-            N.call("dsvgd_phi_mm_x3", N.ptr(W.D), W.n_pad, N.ptr(W.Yx3), W.ldy, b0, nb, n,
-                   h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), 0, int(W.m16),
-                   None, s)
-        else:
-            N.call("dsvgd_phi_mm", N.ptr(W.D), W.n_pad, N.ptr(W.Y), W.ldy, b0, nb, n,
-                   h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), s)
-        N.call("dsvgd_phi_partial_reduce", N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), W.splits, nb,
-               2 * W.dp, N.ptr(W.Q), W.ldy, N.ptr(W.Qr), s)
         ex = N.ptr(extra[k0:k0 + nb]) if extra is not None else None
         po = N.ptr(phi_out[k0:k0 + nb]) if phi_out is not None else None
         N.call("dsvgd_gsw_block_sweep", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), N.ptr(W.Y), W.ldy,
-               N.ptr(W.norms), N.ptr(W.mean), n, d, b0, nb, h_state.ptr, float(step), N.ptr(W.Q),
-               W.ldy, N.ptr(W.Qr), ex, d, po, N.ld(phi_out) if phi_out is not None else d, sk,
+               N.ptr(W.norms), N.ptr(W.mean), n, d, b0, nb, h_state.ptr, float(step), N.ptr(Q),
+               W.ldy, N.ptr(Qr), ex, d, po, N.ld(phi_out) if phi_out is not None else d, sk,
                N.ptr(mu), N.ptr(lam), float(score_scale), N.ptr(xd),
                N.ld(xd) if xd is not None else d, N.ptr(td), td.numel() if td is not None else 0,
                s)
+
+    if not GSW_PIPELINE or len(blocks) < 2:
+        for b0, nb in blocks:
+            _wide_pass(W, b0, nb, n, d, h_state, W.Q, W.Qr, s)
+            walk(b0, nb, W.Q, W.Qr)
+            W.images(b0, nb, s)
+        return
+    # pipelined: the wide pass of block k (side stream) leaves block k - 1
+    # out and may run while block k - 1 walks; it waits for block k - 2's
+    # images, and block k - 1's images wait for it (it reads their old rows).
+    # Block k then adds block k - 1's moved rows (dsvgd_gsw_prev_corr) and
+    # walks.  Sums double-buffered: block k's in Qs[k % 2].
+    dev = X.device
+    main = torch.cuda.current_stream(dev)
+    if W.side is None:
+        W.side = torch.cuda.Stream(device=dev)
+    side = W.side
+    Qs = ((W.Q, W.Qr), (W.Q2, W.Qr2))
+    done = {}
+
+    def issue_wide(k, after):
+        side.wait_event(after)
+        b0, nb = blocks[k]
+        with torch.cuda.stream(side):
+            _wide_pass(W, b0, nb, n, d, h_state, *Qs[k % 2], side.cuda_stream,
+                       exclude=blocks[k - 1] if k > 0 else None)
+            done[k] = side.record_event()
+
+    start = main.record_event()          # Y, its images and the centre are ready
+    issue_wide(0, start)
+    issue_wide(1, start)
+    for k, (b0, nb) in enumerate(blocks):
+        main.wait_event(done.pop(k))
+        Q, Qr = Qs[k % 2]
+        if k > 0:
+            p0, pb = blocks[k - 1]
+            N.call("dsvgd_gsw_prev_corr", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), N.ptr(W.mean), n,
+                   d, b0, nb, p0, pb, h_state.ptr, N.ptr(Q), W.ldy, N.ptr(Qr), s)
+        walk(b0, nb, Q, Qr)
+        if k + 1 < len(blocks):
+            main.wait_event(done[k + 1])  # block k + 1's wide pass read these rows' old images
         W.images(b0, nb, s)
+        if k + 2 < len(blocks):
+            issue_wide(k + 2, main.record_event())
 
 
 def _blocked_sweep(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s):
