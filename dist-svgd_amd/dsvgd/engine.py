@@ -1023,6 +1023,7 @@ _WIDE = {}
 # b's columns left out, then added at their moved positions by
 # dsvgd_gsw_prev_corr); False: one stream, block after block
 GSW_PIPELINE = True
+_GSW_DEBUG = 0   # 1: keep the events alive; 2: serialise the two streams (math only)
 
 
 def _wide_pass(W, b0, nb, n, d, h_state, Q, Qr, s, exclude=None):
@@ -1103,13 +1104,21 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
     Qs = ((W.Q, W.Qr), (W.Q2, W.Qr2))
     done = {}
 
+    keep = []
+
     def issue_wide(k, after):
         side.wait_event(after)
+        if _GSW_DEBUG == 2:
+            side.wait_stream(main)
         b0, nb = blocks[k]
         with torch.cuda.stream(side):
             _wide_pass(W, b0, nb, n, d, h_state, *Qs[k % 2], side.cuda_stream,
                        exclude=blocks[k - 1] if k > 0 else None)
             done[k] = side.record_event()
+        if _GSW_DEBUG:
+            keep.extend([after, done[k]])
+        if _GSW_DEBUG == 2:
+            main.wait_stream(side)
 
     start = main.record_event()          # Y, its images and the centre are ready
     issue_wide(0, start)
@@ -1127,6 +1136,8 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
         W.images(b0, nb, s)
         if k + 2 < len(blocks):
             issue_wide(k + 2, main.record_event())
+    if _GSW_DEBUG:
+        torch.cuda.synchronize()
 
 
 def _blocked_sweep(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s):

@@ -24,10 +24,11 @@ def main():
     N.call("dsvgd_set_bandwidth", st.ptr, h, N.stream("cuda:0"))
     real_call = N.call
     out = {}
-    for name, pipe, skip in (("serial", False, None), ("pipe", True, None),
-                             ("pipe_nocorr", True, "dsvgd_gsw_prev_corr"),
-                             ("pipe_nomask", True, "dsvgd_gs_mask_cols")):
+    for name, pipe, skip, dbg in (("serial", False, None, 0), ("pipe", True, None, 0),
+                                  ("pipe_keep", True, None, 1), ("pipe_serialised", True, None, 2),
+                                  ("pipe2", True, None, 0), ("pipe_keep2", True, None, 1)):
         E.GSW_PIPELINE = pipe
+        E._GSW_DEBUG = dbg
 
         def call(fn, *a, skip=skip):
             if fn == skip:
