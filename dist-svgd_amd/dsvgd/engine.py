@@ -1108,7 +1108,7 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
 
     def issue_wide(k, after):
         side.wait_event(after)
-        if _GSW_DEBUG == 2:
+        if _GSW_DEBUG in (2, 4):
             side.wait_stream(main)
         b0, nb = blocks[k]
         with torch.cuda.stream(side):
@@ -1117,7 +1117,7 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
             done[k] = side.record_event()
         if _GSW_DEBUG:
             keep.extend([after, done[k]])
-        if _GSW_DEBUG == 2:
+        if _GSW_DEBUG in (2, 3):
             main.wait_stream(side)
 
     start = main.record_event()          # Y, its images and the centre are ready
