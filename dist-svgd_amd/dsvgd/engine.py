@@ -1124,9 +1124,15 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
     issue_wide(0, start)
     issue_wide(1, start)
     for k, (b0, nb) in enumerate(blocks):
-        main.wait_event(done.pop(k))
         Q, Qr = Qs[k % 2]
-        if k > 0:
+        if k > 0 and _GSW_DEBUG == 5:     # the correction on the side stream
+            side.wait_event(main.record_event())
+            p0, pb = blocks[k - 1]
+            N.call("dsvgd_gsw_prev_corr", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), N.ptr(W.mean), n,
+                   d, b0, nb, p0, pb, h_state.ptr, N.ptr(Q), W.ldy, N.ptr(Qr), side.cuda_stream)
+            done[k] = side.record_event()
+        main.wait_event(done.pop(k))
+        if k > 0 and _GSW_DEBUG != 5:
             p0, pb = blocks[k - 1]
             N.call("dsvgd_gsw_prev_corr", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), N.ptr(W.mean), n,
                    d, b0, nb, p0, pb, h_state.ptr, N.ptr(Q), W.ldy, N.ptr(Qr), s)

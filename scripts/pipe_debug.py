@@ -25,10 +25,8 @@ def main():
     real_call = N.call
     out = {}
     for name, pipe, skip, dbg in (("serial", False, None, 0), ("pipe", True, None, 0),
-                                  ("pipe_serialised", True, None, 2),
-                                  ("pipe_main_waits_wide", True, None, 3),
-                                  ("pipe_wide_waits_main", True, None, 4),
-                                  ("pipe_nocorr", True, "dsvgd_gsw_prev_corr", 0)):
+                                  ("pipe_corr_on_side", True, None, 5),
+                                  ("pipe_again", True, None, 0)):
         E.GSW_PIPELINE = pipe
         E._GSW_DEBUG = dbg
 
