@@ -1134,8 +1134,14 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
         main.wait_event(done.pop(k))
         if k > 0 and _GSW_DEBUG != 5:
             p0, pb = blocks[k - 1]
+            if _GSW_DEBUG == 6:       # the correction into a scratch copy (Q untouched)
+                if getattr(W, "Qd", None) is None:
+                    W.Qd, W.Qrd = torch.zeros_like(W.Q), torch.zeros_like(W.Qr)
+                Q_, Qr_ = W.Qd, W.Qrd
+            else:
+                Q_, Qr_ = Q, Qr
             N.call("dsvgd_gsw_prev_corr", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), N.ptr(W.mean), n,
-                   d, b0, nb, p0, pb, h_state.ptr, N.ptr(Q), W.ldy, N.ptr(Qr), s)
+                   d, b0, nb, p0, pb, h_state.ptr, N.ptr(Q_), W.ldy, N.ptr(Qr_), s)
         walk(b0, nb, Q, Qr)
         if k + 1 < len(blocks):
             main.wait_event(done[k + 1])  # block k + 1's wide pass read these rows' old images
