@@ -1074,7 +1074,7 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
     B = W.B
     blocks = [(b0, min(B, rows.stop - b0)) for b0 in range(rows.start, rows.stop, B)]
 
-    def walk(b0, nb, Q, Qr):
+    def walk(b0, nb, Q, Qr, s=s):
         k0 = b0 - rows.start
         ex = N.ptr(extra[k0:k0 + nb]) if extra is not None else None
         po = N.ptr(phi_out[k0:k0 + nb]) if phi_out is not None else None
@@ -1101,6 +1101,14 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
     if W.side is None:
         W.side = torch.cuda.Stream(device=dev)
     side = W.side
+    caller = None
+    if _GSW_DEBUG == 7:         # both streams non-default
+        if getattr(W, "main2", None) is None:
+            W.main2 = torch.cuda.Stream(device=dev)
+        caller = main
+        main = W.main2
+        main.wait_stream(caller)
+        s = main.cuda_stream
     Qs = ((W.Q, W.Qr), (W.Q2, W.Qr2))
     done = {}
 
@@ -1142,12 +1150,14 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
                 Q_, Qr_ = Q, Qr
             N.call("dsvgd_gsw_prev_corr", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), N.ptr(W.mean), n,
                    d, b0, nb, p0, pb, h_state.ptr, N.ptr(Q_), W.ldy, N.ptr(Qr_), s)
-        walk(b0, nb, Q, Qr)
+        walk(b0, nb, Q, Qr, s)
         if k + 1 < len(blocks):
             main.wait_event(done[k + 1])  # block k + 1's wide pass read these rows' old images
         W.images(b0, nb, s)
         if k + 2 < len(blocks):
             issue_wide(k + 2, main.record_event())
+    if caller is not None:
+        caller.wait_stream(main)
     if _GSW_DEBUG:
         torch.cuda.synchronize()
 

@@ -25,10 +25,8 @@ def main():
     real_call = N.call
     out = {}
     for name, pipe, skip, dbg in (("serial", False, None, 0), ("pipe", True, None, 0),
-                                  ("pipe_corr_to_scratch", True, None, 6),
-                                  ("pipe_nocorr", True, "dsvgd_gsw_prev_corr", 0),
-                                  ("pipe_walk4", True, None, 0),
-                                  ("serial_walk4", False, None, 0)):
+                                  ("pipe_own_streams", True, None, 7),
+                                  ("pipe_own_streams2", True, None, 7)):
         E.GSW_PIPELINE = pipe
         E._GSW_DEBUG = dbg
         N.load().dsvgd_gsw_debug(8 if name.endswith("walk4") else 0)
