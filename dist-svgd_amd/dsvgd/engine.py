@@ -1128,6 +1128,7 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
         if _GSW_DEBUG in (2, 3):
             main.wait_stream(side)
 
+    W.dbg = []
     start = main.record_event()          # Y, its images and the centre are ready
     issue_wide(0, start)
     issue_wide(1, start)
@@ -1150,6 +1151,8 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
                 Q_, Qr_ = Q, Qr
             N.call("dsvgd_gsw_prev_corr", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), N.ptr(W.mean), n,
                    d, b0, nb, p0, pb, h_state.ptr, N.ptr(Q_), W.ldy, N.ptr(Qr_), s)
+        if _GSW_DEBUG == 8:      # the sums each walk reads
+            W.dbg.append((k, Q[:nb].clone(), Qr[:nb].clone()))
         walk(b0, nb, Q, Qr, s)
         if k + 1 < len(blocks):
             main.wait_event(done[k + 1])  # block k + 1's wide pass read these rows' old images

@@ -25,8 +25,7 @@ def main():
     real_call = N.call
     out = {}
     for name, pipe, skip, dbg in (("serial", False, None, 0), ("pipe", True, None, 0),
-                                  ("pipe_own_streams", True, None, 7),
-                                  ("pipe_own_streams2", True, None, 7)):
+                                  ("pipe_dbgQ", True, None, 8), ("serial_dbgQ", False, None, 8)):
         E.GSW_PIPELINE = pipe
         E._GSW_DEBUG = dbg
         N.load().dsvgd_gsw_debug(8 if name.endswith("walk4") else 0)
@@ -48,6 +47,24 @@ def main():
         if name != "serial":
             dif = np.abs(p - out["serial"]).max(1)
             rec["block_maxdiff"] = [float(np.nanmax(dif[b:b + 64])) for b in range(0, n, 64)][:16]
+        if dbg == 8:
+            W = list(E._WIDE.values())[0]
+            qs = {k: (q.cpu().numpy(), r.cpu().numpy()) for k, q, r in W.dbg}
+            out["q_" + name] = qs
+            badq = [(k, np.where(~np.isfinite(q).all(1))[0][:6].tolist(),
+                     np.where(~np.isfinite(r))[0][:6].tolist()) for k, (q, r) in qs.items()
+                    if not (np.isfinite(q).all() and np.isfinite(r).all())]
+            rec["q_nonfinite"] = badq[:4]
+            if name.startswith("serial") and "q_pipe_dbgQ" in out:
+                other = out["q_pipe_dbgQ"]
+                dif = []
+                for k in sorted(qs):
+                    if k in other:
+                        a, b = qs[k][0], other[k][0]
+                        dq = np.abs(a - b)
+                        dif.append((k, float(np.nanmax(dq)) if np.isfinite(b).any() else None,
+                                    int(np.argmax(np.nanmax(np.where(np.isfinite(dq), dq, 0), 1)))))
+                rec["q_vs_pipe"] = dif[:8]
         print(json.dumps({name: rec}), flush=True)
 
 
