@@ -991,11 +991,6 @@ class _WideSweep(object):
         self.rowsum = torch.empty(z * 128, **f32)
         self.Q = torch.empty(self.B, self.ldy, **f32)
         self.Qr = torch.empty(128, **f32)
-        # the pipelined sweep: block b + 1's sums beside block b's, and the
-        # stream its wide pass runs on
-        self.Q2 = torch.empty(self.B, self.ldy, **f32)
-        self.Qr2 = torch.empty(128, **f32)
-        self.side = None
 
     def images(self, r0, nr, s):
         """(Re)split rows [r0, r0 + nr) of Y into the engines' images (the
@@ -1019,16 +1014,9 @@ class _WideSweep(object):
 
 
 _WIDE = {}
-# the wide pass of block b + 1 on a second stream while block b walks (block
-# b's columns left out, then added at their moved positions by
-# dsvgd_gsw_prev_corr); False: one stream, block after block
-GSW_PIPELINE = True
-_GSW_DEBUG = 0   # 1: keep the events alive; 2: serialise the two streams (math only)
-
-
-def _wide_pass(W, b0, nb, n, d, h_state, Q, Qr, s, exclude=None):
+def _wide_pass(W, b0, nb, n, d, h_state, Q, Qr, s):
     """Q = [K Xc | K S], Qr = K 1 of rows [b0, b0 + nb) against every row
-    except the block's own earlier ones (and the `exclude` = (p0, pB) block)."""
+    except the block's own earlier ones."""
     if W.gram_h2:
         N.call("dsvgd_sqdist_h2", N.ptr(W.Yg), N.ptr(W.norms), b0, nb, n, d, N.ptr(W.D),
                W.n_pad, 0, None, None, 0, N.ptr(W.rsc), s)
@@ -1036,8 +1024,6 @@ def _wide_pass(W, b0, nb, n, d, h_state, Q, Qr, s, exclude=None):
         N.call("dsvgd_sqdist", N.ptr(W.Y), W.ldy, N.ptr(W.norms), b0, nb, n, d, N.ptr(W.D),
                W.n_pad, 0, None, None, s)
     N.call("dsvgd_gs_mask", N.ptr(W.D), W.n_pad, b0, nb, s)
-    if exclude is not None:
-        N.call("dsvgd_gs_mask_cols", N.ptr(W.D), W.n_pad, nb, exclude[0], exclude[1], s)
     if W.phi_x3:
         N.call("dsvgd_phi_mm_x3", N.ptr(W.D), W.n_pad, N.ptr(W.Yx3), W.ldy, b0, nb, n,
                h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), 0, int(W.m16),
@@ -1074,7 +1060,7 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
     B = W.B
     blocks = [(b0, min(B, rows.stop - b0)) for b0 in range(rows.start, rows.stop, B)]
 
-    def walk(b0, nb, Q, Qr, s=s):
+    def walk(b0, nb, Q, Qr):
         k0 = b0 - rows.start
         ex = N.ptr(extra[k0:k0 + nb]) if extra is not None else None
         po = N.ptr(phi_out[k0:k0 + nb]) if phi_out is not None else None
@@ -1085,84 +1071,10 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
                N.ld(xd) if xd is not None else d, N.ptr(td), td.numel() if td is not None else 0,
                s)
 
-    if not GSW_PIPELINE or len(blocks) < 2:
-        for b0, nb in blocks:
-            _wide_pass(W, b0, nb, n, d, h_state, W.Q, W.Qr, s)
-            walk(b0, nb, W.Q, W.Qr)
-            W.images(b0, nb, s)
-        return
-    # pipelined: the wide pass of block k (side stream) leaves block k - 1
-    # out and may run while block k - 1 walks; it waits for block k - 2's
-    # images, and block k - 1's images wait for it (it reads their old rows).
-    # Block k then adds block k - 1's moved rows (dsvgd_gsw_prev_corr) and
-    # walks.  Sums double-buffered: block k's in Qs[k % 2].
-    dev = X.device
-    main = torch.cuda.current_stream(dev)
-    if W.side is None:
-        W.side = torch.cuda.Stream(device=dev)
-    side = W.side
-    caller = None
-    if _GSW_DEBUG == 7:         # both streams non-default
-        if getattr(W, "main2", None) is None:
-            W.main2 = torch.cuda.Stream(device=dev)
-        caller = main
-        main = W.main2
-        main.wait_stream(caller)
-        s = main.cuda_stream
-    Qs = ((W.Q, W.Qr), (W.Q2, W.Qr2))
-    done = {}
-
-    keep = []
-
-    def issue_wide(k, after):
-        side.wait_event(after)
-        if _GSW_DEBUG in (2, 4):
-            side.wait_stream(main)
-        b0, nb = blocks[k]
-        with torch.cuda.stream(side):
-            _wide_pass(W, b0, nb, n, d, h_state, *Qs[k % 2], side.cuda_stream,
-                       exclude=blocks[k - 1] if k > 0 else None)
-            done[k] = side.record_event()
-        if _GSW_DEBUG:
-            keep.extend([after, done[k]])
-        if _GSW_DEBUG in (2, 3):
-            main.wait_stream(side)
-
-    W.dbg = []
-    start = main.record_event()          # Y, its images and the centre are ready
-    issue_wide(0, start)
-    issue_wide(1, start)
-    for k, (b0, nb) in enumerate(blocks):
-        Q, Qr = Qs[k % 2]
-        if k > 0 and _GSW_DEBUG == 5:     # the correction on the side stream
-            side.wait_event(main.record_event())
-            p0, pb = blocks[k - 1]
-            N.call("dsvgd_gsw_prev_corr", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), N.ptr(W.mean), n,
-                   d, b0, nb, p0, pb, h_state.ptr, N.ptr(Q), W.ldy, N.ptr(Qr), side.cuda_stream)
-            done[k] = side.record_event()
-        main.wait_event(done.pop(k))
-        if k > 0 and _GSW_DEBUG != 5:
-            p0, pb = blocks[k - 1]
-            if _GSW_DEBUG == 6:       # the correction into a scratch copy (Q untouched)
-                if getattr(W, "Qd", None) is None:
-                    W.Qd, W.Qrd = torch.zeros_like(W.Q), torch.zeros_like(W.Qr)
-                Q_, Qr_ = W.Qd, W.Qrd
-            else:
-                Q_, Qr_ = Q, Qr
-            N.call("dsvgd_gsw_prev_corr", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), N.ptr(W.mean), n,
-                   d, b0, nb, p0, pb, h_state.ptr, N.ptr(Q_), W.ldy, N.ptr(Qr_), s)
-        if _GSW_DEBUG == 8:      # the sums each walk reads
-            W.dbg.append((k, Q[:nb].clone(), Qr[:nb].clone()))
-        walk(b0, nb, Q, Qr, s)
-        if k + 1 < len(blocks):
-            main.wait_event(done[k + 1])  # block k + 1's wide pass read these rows' old images
+    for b0, nb in blocks:
+        _wide_pass(W, b0, nb, n, d, h_state, W.Q, W.Qr, s)
+        walk(b0, nb, W.Q, W.Qr)
         W.images(b0, nb, s)
-        if k + 2 < len(blocks):
-            issue_wide(k + 2, main.record_event())
-    if caller is not None:
-        caller.wait_stream(main)
-    if _GSW_DEBUG:
-        torch.cuda.synchronize()
 
 
 def _blocked_sweep(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s):

@@ -371,19 +371,6 @@ int64_t dsvgd_gsw_block_rows(int64_t d, int score_kind);  /* 0 if d > 1024 */
  * the column loop.  Process-wide; returns the previous mask.  0 = normal. */
 int dsvgd_gsw_debug(int mask);
 int dsvgd_gs_mask(float* D, int64_t ldd, int64_t r0, int64_t B, void* stream);
-/* The pipelined wide sweep (block b + 1's wide pass runs while block b
- * walks): dsvgd_gs_mask_cols sets D[i][c0 + j] = +inf for i < B, j < nc (block
- * b's columns, left out of block b + 1's wide pass); after block b's walk,
- * dsvgd_gsw_prev_corr adds their terms at the moved positions to block b + 1's
- * sums: Q[i][c] += sum_j k_ij (x_j - center)[c], Q[i][dp + c] += sum_j k_ij
- * s_j[c], Qr[i] += sum_j k_ij, k_ij = exp(-|x_{r0+i} - x_{p0+j}|^2 / h), for
- * i < B, j < pB (explicit differences, j order).  The reference's in-place
- * order is unchanged (sampler.py:64-68). */
-int dsvgd_gs_mask_cols(float* D, int64_t ldd, int64_t B, int64_t c0, int64_t nc, void* stream);
-int dsvgd_gsw_prev_corr(const float* X, int64_t ldx, const float* S, int64_t lds,
-                        const float* center, int64_t n, int64_t d, int64_t r0, int64_t B,
-                        int64_t p0, int64_t pB, const dsvgd_select_state* st, float* Q, int64_t ldq,
-                        float* Qr, void* stream);
 int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y, int64_t ldy,
                           float* norms, const float* center, int64_t n, int64_t d, int64_t r0,
                           int64_t B, const dsvgd_select_state* st, float step, const float* Q,
