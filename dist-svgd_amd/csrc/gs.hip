@@ -726,215 +726,6 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
 
 using namespace dsvgd;
 
-
-// The walk with ONE wave (frozen or elementwise scores: score_kind 0, 1, 2).
-// The four-wave walk above spends ~0.6 us in each of its three barriers per
-// row with one workgroup alive on the chip; a single wave needs
-// none -- its LDS operations are in order -- and does the per-row work of the
-// four itself: (a) lane l takes moved row j = l / L, features [part dp / L,
-// +dp / L) (part = l % L, L = lanes per row: the largest power of two with
-// L B <= 64), the L partial sums meet by a fixed butterfly; (b) lane l keeps
-// the column quads q = l, l + 64, ... and adds k_j w_j[q] for j < i in j
-// order (k_j broadcast by v_readlane, its moved-row sum in the same order);
-// (c) the move and the elementwise score refresh of its columns.  Scores are
-// not kept in LDS: they are functions of the moved row, recomputed for the
-// block's stores.  LDS: the block's rows (old, then moved) and w_j.
-constexpr int kGsw1Q = kGswMaxD / 256;   // column quads per lane
-template <int L>
-__global__ __launch_bounds__(64) void gsw1_sweep_kernel(
-    float* __restrict__ X, int64_t ldx, float* __restrict__ S, int64_t lds, float* __restrict__ Y,
-    int64_t ldy, float* __restrict__ norms, const float* __restrict__ center, int64_t n, int d,
-    int dp, int64_t r0, int B, const dsvgd_select_state* __restrict__ st, float step,
-    const float* __restrict__ Q, int64_t ldq, const float* __restrict__ Qr,
-    const float* __restrict__ extra, int64_t lde, float* __restrict__ phi_out, int64_t ldphi,
-    int score_kind, const float* __restrict__ mu, const float* __restrict__ lam,
-    float score_scale) {
-  extern __shared__ __attribute__((aligned(16))) float gsw_smem[];
-  const int pitch = dp + 4;
-  float* xn = gsw_smem;                   // [B][pitch]: centred rows, old until moved
-  float* wn = xn + (int64_t)B * pitch;    // [B][dp]: w_j = s_j' - g (x_j' - c)
-  const int lane = threadIdx.x;
-  const int nq = dp >> 2;
-  const float inv_h = st->inv_h, g = 2.f * inv_h, scale = -inv_h * kLog2e;
-  const float inv_n = 1.f / (float)n;
-  for (int e = lane; e < B * nq; e += 64) {
-    const int i = e / nq, c4 = (e % nq) << 2;
-    *reinterpret_cast<f32x4*>(xn + i * pitch + c4) =
-        *reinterpret_cast<const f32x4*>(Y + (r0 + i) * ldy + c4);
-  }
-  // the lane's column quads q = lane + 64 u and their per-column constants
-  f32x4 cen[kGsw1Q], mu_c[kGsw1Q], lam_c[kGsw1Q];
-  f32x4 nq_x[kGsw1Q], nq_s[kGsw1Q], n_so[kGsw1Q], n_ex[kGsw1Q];
-  float nqr = 0.f;
-  auto col = [&](int u, int e) { return 4 * (lane + 64 * u) + e; };
-#pragma unroll
-  for (int u = 0; u < kGsw1Q; ++u)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int c = col(u, e);
-      const bool ok = c < d;
-      cen[u][e] = ok ? center[c] : 0.f;
-      mu_c[u][e] = (score_kind == 1 && ok) ? mu[c] : 0.f;
-      lam_c[u][e] = (score_kind == 1 && ok) ? lam[c] : 0.f;
-    }
-  auto prefetch = [&](int i) {
-    const int64_t gi = r0 + i;
-#pragma unroll
-    for (int u = 0; u < kGsw1Q; ++u)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int c = col(u, e);
-        const bool ok = c < d;
-        nq_x[u][e] = ok ? Q[i * ldq + c] : 0.f;
-        nq_s[u][e] = ok ? Q[i * ldq + dp + c] : 0.f;
-        n_so[u][e] = ok ? Y[gi * ldy + dp + c] : 0.f;
-        n_ex[u][e] = (ok && extra) ? extra[(int64_t)i * lde + c] : 0.f;
-      }
-    nqr = Qr[i];
-  };
-  prefetch(0);
-  __syncthreads();   // (one wave: orders the row loads before the walk)
-  const int jr = lane / L, part = lane % L;
-  const int fl = dp / L;                  // features per lane in the distance pass
-  for (int i = 0; i < B; ++i) {
-    f32x4 q_x[kGsw1Q], q_s[kGsw1Q], s_o[kGsw1Q], ex[kGsw1Q];
-#pragma unroll
-    for (int u = 0; u < kGsw1Q; ++u) {
-      q_x[u] = nq_x[u];
-      q_s[u] = nq_s[u];
-      s_o[u] = n_so[u];
-      ex[u] = n_ex[u];
-    }
-    const float qr = nqr;
-    if (i + 1 < B) prefetch(i + 1);
-    const float* xoi = xn + i * pitch;    // row i, still the old one
-    // (a) |x_i - x_j'|^2, j = jr < i
-    float dd = 0.f;
-    {
-      float sa = 0.f, sb = 0.f;
-      if (jr < i) {
-        const float* pa = xoi + part * fl;
-        const float* pb = xn + jr * pitch + part * fl;
-        auto acc4 = [&](const f32x4& va, const f32x4& vb) {
-          const float d0 = va[0] - vb[0], d1 = va[1] - vb[1], d2 = va[2] - vb[2], d3 = va[3] - vb[3];
-          sa = fmaf(d0, d0, fmaf(d2, d2, sa));
-          sb = fmaf(d1, d1, fmaf(d3, d3, sb));
-        };
-        int c = 0;
-        for (; c + 16 <= fl; c += 16) {
-          f32x4 va[4], vb[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            va[r] = *reinterpret_cast<const f32x4*>(pa + c + 4 * r);
-            vb[r] = *reinterpret_cast<const f32x4*>(pb + c + 4 * r);
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc4(va[r], vb[r]);
-        }
-        for (; c < fl; c += 4)
-          acc4(*reinterpret_cast<const f32x4*>(pa + c), *reinterpret_cast<const f32x4*>(pb + c));
-      }
-      dd = sa + sb;
-#pragma unroll
-      for (int o = 1; o < L; o <<= 1) dd += __shfl_xor(dd, o, 64);
-    }
-    const int kb = __builtin_bit_cast(int, (jr < i) ? __builtin_amdgcn_exp2f(dd * scale) : 0.f);
-    // (b) sum_{j<i} k_j w_j over the lane's quads, and sum_{j<i} k_j
-    f32x4 acc[kGsw1Q];
-#pragma unroll
-    for (int u = 0; u < kGsw1Q; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float rm = 0.f;
-    int j = 0;
-    for (; j + 4 <= i; j += 4) {
-      float kk[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        kk[r] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(kb, (j + r) * L));
-      rm += (kk[0] + kk[1]) + (kk[2] + kk[3]);
-#pragma unroll
-      for (int u = 0; u < kGsw1Q; ++u) {
-        if (64 * u >= nq) break;   // (uniform)
-        if (lane + 64 * u < nq) {
-          f32x4 wv[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            wv[r] = *reinterpret_cast<const f32x4*>(wn + (j + r) * dp + 4 * (lane + 64 * u));
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[u] += kk[r] * wv[r];
-        }
-      }
-    }
-    for (; j < i; ++j) {
-      const float k0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(kb, j * L));
-      rm += k0;
-#pragma unroll
-      for (int u = 0; u < kGsw1Q; ++u) {
-        if (64 * u >= nq) break;
-        if (lane + 64 * u < nq)
-          acc[u] += k0 * *reinterpret_cast<const f32x4*>(wn + j * dp + 4 * (lane + 64 * u));
-      }
-    }
-    // (c) the move of row i (its old values still in xn[i])
-    const float rtot = qr + rm;
-#pragma unroll
-    for (int u = 0; u < kGsw1Q; ++u) {
-      if (64 * u >= nq) break;
-      if (lane + 64 * u >= nq) continue;
-      const int c0 = 4 * (lane + 64 * u);
-      const f32x4 xo = *reinterpret_cast<const f32x4*>(xoi + c0);
-      f32x4 xcn, wv;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float p = inv_n * (((q_s[u][e] + s_o[u][e]) - g * q_x[u][e]) + acc[u][e] +
-                                 g * (rtot * xo[e])) + ex[u][e];
-        const int c = c0 + e;
-        if (phi_out && c < d) phi_out[(int64_t)i * ldphi + c] = p;
-        const float x = (xo[e] + cen[u][e]) + step * p;
-        const float xc = x - cen[u][e];
-        const float sv = (score_kind == 1 || score_kind == 2)
-                             ? gs_score(score_kind, x, mu_c[u][e], lam_c[u][e], score_scale)
-                             : s_o[u][e];
-        xcn[e] = c < d ? xc : 0.f;
-        wv[e] = c < d ? sv - g * xc : 0.f;
-      }
-      *reinterpret_cast<f32x4*>(xn + i * pitch + c0) = xcn;
-      *reinterpret_cast<f32x4*>(wn + i * dp + c0) = wv;
-    }
-  }
-  // the moved rows out: X, Y's centred row, with refreshed scores S and Y's
-  // score half (the same gs_score of the same moved value), then the norms
-  const bool refreshed = score_kind == 1 || score_kind == 2;
-  for (int i = 0; i < B; ++i) {
-    const int64_t gi = r0 + i;
-#pragma unroll
-    for (int u = 0; u < kGsw1Q; ++u)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int c = col(u, e);
-        if (c >= d) continue;
-        const float xc = xn[i * pitch + c];
-        const float x = xc + cen[u][e];
-        X[gi * ldx + c] = x;
-        Y[gi * ldy + c] = xc;
-        if (refreshed) {
-          const float sv = gs_score(score_kind, x, mu_c[u][e], lam_c[u][e], score_scale);
-          S[gi * lds + c] = sv;
-          Y[gi * ldy + dp + c] = sv;
-        }
-      }
-  }
-  for (int i = lane; i < B; i += 64) {
-    const float* pr = xn + i * pitch;
-    float s2a = 0.f, s2b = 0.f;
-    for (int c = 0; c < dp; c += 4) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(pr + c);
-      s2a = fmaf(v[0], v[0], fmaf(v[2], v[2], s2a));
-      s2b = fmaf(v[1], v[1], fmaf(v[3], v[3], s2b));
-    }
-    norms[r0 + i] = s2a + s2b;
-  }
-}
-
 extern "C" {
 
 int64_t dsvgd_gs_block_rows(void) { return kGsB; }
@@ -1030,33 +821,6 @@ int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y
                 "logreg data rows must be 16-byte aligned (ldxd % 4 == 0)");
   DSVGD_REQUIRE(!extra || lde >= d, "lde");
   DSVGD_REQUIRE(!phi_out || ldphi >= d, "ldphi");
-  if (score_kind != 3 && !(gsw_debug_mask() & 8)) {
-    // the one-wave walk (gsw_debug bit 8: the four-wave one, for A/B)
-    const size_t smem1 = sizeof(float) * (size_t)B * (2 * dp + 4);
-    int L = 1;
-    while (L < 8 && 2 * L * B <= 64) L *= 2;
-    const void* fn1 = L == 1   ? reinterpret_cast<const void*>(&gsw1_sweep_kernel<1>)
-                      : L == 2 ? reinterpret_cast<const void*>(&gsw1_sweep_kernel<2>)
-                      : L == 4 ? reinterpret_cast<const void*>(&gsw1_sweep_kernel<4>)
-                               : reinterpret_cast<const void*>(&gsw1_sweep_kernel<8>);
-    if (hipFuncSetAttribute(fn1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem1) !=
-        hipSuccess)
-      return fail_arg("gsw1_sweep: cannot reserve the walk's LDS");
-#define DSVGD_GSW1(LL)                                                                              \
-  hipLaunchKernelGGL(gsw1_sweep_kernel<LL>, dim3(1), dim3(64), smem1, (hipStream_t)stream, X, ldx, S, \
-                     lds, Y, ldy, norms, center, n, (int)d, (int)dp, r0, (int)B, st, step, Q, ldq,  \
-                     Qr, extra, lde, phi_out, ldphi, score_kind, mu, lam, score_scale)
-    if (L == 1)
-      DSVGD_GSW1(1);
-    else if (L == 2)
-      DSVGD_GSW1(2);
-    else if (L == 4)
-      DSVGD_GSW1(4);
-    else
-      DSVGD_GSW1(8);
-#undef DSVGD_GSW1
-    return check_launch("gsw1_sweep");
-  }
   const size_t smem =
       sizeof(float) * ((size_t)B * (dp + 4) + (size_t)B * dp * (score_kind != 0 ? 2 : 1) + 256 +
                        1024 + 16 + (score_kind == 3 ? kGswCoef : 0));

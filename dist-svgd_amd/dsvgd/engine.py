@@ -1014,25 +1014,6 @@ class _WideSweep(object):
 
 
 _WIDE = {}
-def _wide_pass(W, b0, nb, n, d, h_state, Q, Qr, s):
-    """Q = [K Xc | K S], Qr = K 1 of rows [b0, b0 + nb) against every row
-    except the block's own earlier ones."""
-    if W.gram_h2:
-        N.call("dsvgd_sqdist_h2", N.ptr(W.Yg), N.ptr(W.norms), b0, nb, n, d, N.ptr(W.D),
-               W.n_pad, 0, None, None, 0, N.ptr(W.rsc), s)
-    else:
-        N.call("dsvgd_sqdist", N.ptr(W.Y), W.ldy, N.ptr(W.norms), b0, nb, n, d, N.ptr(W.D),
-               W.n_pad, 0, None, None, s)
-    N.call("dsvgd_gs_mask", N.ptr(W.D), W.n_pad, b0, nb, s)
-    if W.phi_x3:
-        N.call("dsvgd_phi_mm_x3", N.ptr(W.D), W.n_pad, N.ptr(W.Yx3), W.ldy, b0, nb, n,
-               h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), 0, int(W.m16),
-               None, s)
-    else:
-        N.call("dsvgd_phi_mm", N.ptr(W.D), W.n_pad, N.ptr(W.Y), W.ldy, b0, nb, n,
-               h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), s)
-    N.call("dsvgd_phi_partial_reduce", N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), W.splits, nb,
-           2 * W.dp, N.ptr(Q), W.ldy, N.ptr(Qr), s)
 
 
 def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s):
@@ -1058,22 +1039,33 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
            W.Y.shape[0], N.ptr(W.Y), W.ldy, N.ptr(W.norms), s)
     W.images(0, W.n_pad, s)
     B = W.B
-    blocks = [(b0, min(B, rows.stop - b0)) for b0 in range(rows.start, rows.stop, B)]
-
-    def walk(b0, nb, Q, Qr):
+    for b0 in range(rows.start, rows.stop, B):
+        nb = min(B, rows.stop - b0)
         k0 = b0 - rows.start
+        if W.gram_h2:
+            N.call("dsvgd_sqdist_h2", N.ptr(W.Yg), N.ptr(W.norms), b0, nb, n, d, N.ptr(W.D),
+                   W.n_pad, 0, None, None, 0, N.ptr(W.rsc), s)
+        else:
+            N.call("dsvgd_sqdist", N.ptr(W.Y), W.ldy, N.ptr(W.norms), b0, nb, n, d, N.ptr(W.D),
+                   W.n_pad, 0, None, None, s)
+        N.call("dsvgd_gs_mask", N.ptr(W.D), W.n_pad, b0, nb, s)
+        if W.phi_x3:
+            N.call("dsvgd_phi_mm_x3", N.ptr(W.D), W.n_pad, N.ptr(W.Yx3), W.ldy, b0, nb, n,
+                   h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), 0, int(W.m16),
+                   None, s)
+        else:
+            N.call("dsvgd_phi_mm", N.ptr(W.D), W.n_pad, N.ptr(W.Y), W.ldy, b0, nb, n,
+                   h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), s)
+        N.call("dsvgd_phi_partial_reduce", N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), W.splits, nb,
+               2 * W.dp, N.ptr(W.Q), W.ldy, N.ptr(W.Qr), s)
         ex = N.ptr(extra[k0:k0 + nb]) if extra is not None else None
         po = N.ptr(phi_out[k0:k0 + nb]) if phi_out is not None else None
         N.call("dsvgd_gsw_block_sweep", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), N.ptr(W.Y), W.ldy,
-               N.ptr(W.norms), N.ptr(W.mean), n, d, b0, nb, h_state.ptr, float(step), N.ptr(Q),
-               W.ldy, N.ptr(Qr), ex, d, po, N.ld(phi_out) if phi_out is not None else d, sk,
+               N.ptr(W.norms), N.ptr(W.mean), n, d, b0, nb, h_state.ptr, float(step), N.ptr(W.Q),
+               W.ldy, N.ptr(W.Qr), ex, d, po, N.ld(phi_out) if phi_out is not None else d, sk,
                N.ptr(mu), N.ptr(lam), float(score_scale), N.ptr(xd),
                N.ld(xd) if xd is not None else d, N.ptr(td), td.numel() if td is not None else 0,
                s)
-
-    for b0, nb in blocks:
-        _wide_pass(W, b0, nb, n, d, h_state, W.Q, W.Qr, s)
-        walk(b0, nb, W.Q, W.Qr)
         W.images(b0, nb, s)
 
 

@@ -24,9 +24,6 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="D,E")
-    ap.add_argument("--walk", default="1",
-                    help="comma list of walks: 1 the one-wave walk (default), 4 the four-wave "
-                         "one (dsvgd_gsw_debug bit 8)")
     ap.add_argument("--rows-sample", type=int, default=2048,
                     help="rows of the per-row path to time (0: skip it)")
     args = ap.parse_args()
@@ -37,8 +34,7 @@ def main():
     # partition mode's exchange_scores=False; 2048 data rows = config D's
     # N_local at S = 8), scores scaled by N_global / N_local = 8
     shapes = {"D": (65536, 256, 16384), "E": (65536, 1024, 8192), "R": (16384, 256, 2048)}
-    for name, walk in [(a, int(b)) for a in args.only.split(",") for b in args.walk.split(",")]:
-        dsvgd._native.load().dsvgd_gsw_debug(8 if walk == 4 else 0)
+    for name in args.only.split(","):
         n, d, Ng = shapes[name]
         refresh = name == "R"
         x, t = synthetic_data(Ng, d - 1)
@@ -83,7 +79,7 @@ def main():
         sequential_sweep(Xb, Sb, range(n), eng.state, 1e-4, target=tgt, score_scale=scale)
         torch.cuda.synchronize()
         sweep_ms = 1e3 * (time.perf_counter() - t0)
-        print(json.dumps({"config": name, "walk": walk, "n": n, "d": d, "N_local": Ng,
+        print(json.dumps({"config": name, "n": n, "d": d, "N_local": Ng,
                           "scores": "refreshed (logreg)" if refresh else "frozen (all_scores)",
                           "order": "sequential",
                           "step_ms_blocked": blocked_ms, "sweep_only_ms_blocked": sweep_ms,

@@ -981,51 +981,3 @@ def test_predictive_prob_and_test_accuracy(n, d, Nt):
     agree = ((ref > 0.5) == (tt > 0))
     lo, hi = agree[sure].sum() / Nt, (agree[sure].sum() + (~sure).sum()) / Nt
     assert lo - 1e-12 <= acc <= hi + 1e-12
-
-
-@pytest.mark.parametrize("n,d,kind", [(4096, 256, "none"), (1100, 512, "gauss"),
-                                      (900, 1000, "gmm"), (700, 96, "none")])
-def test_one_wave_walk_matches_four_wave_walk(n, d, kind):
-    """The wide sweep's walk with ONE wave (csrc/gs.hip gsw1_sweep_kernel: no
-    barriers, frozen or elementwise scores; the default) against the
-    four-wave walk (dsvgd_gsw_debug bit 8) on the same sweep -- same terms,
-    different summation order -- and both against the fp64 sequential
-    restatement (reference order, sampler.py:64-68).  Block sizes 64 (d 96,
-    256), 32 (d 512) and 16 (d 1000; lanes per moved row 1, 2, 4)."""
-    from dsvgd import _native as N
-    from dsvgd.engine import SelectState, sequential_sweep
-    m = dsvgd()
-    lib = N.load()
-    rs = np.random.RandomState(n + 7 * d)
-    X0 = (0.7 * rs.randn(n, d)).astype(np.float32)
-    mu = rs.randn(d).astype(np.float32)
-    lam = rs.uniform(0.5, 2.0, d).astype(np.float32)
-    step = 0.05
-    tgt = {"gauss": lambda: m.targets.Gaussian(mu, lam), "none": lambda: None,
-           "gmm": m.targets.GaussianMixture1D}[kind]()
-    fn = {"gauss": lambda X: O.score_gaussian(X, mu, lam), "none": None, "gmm": O.score_gmm}[kind]
-    S0 = (fn(X0) if fn else rs.randn(n, d)).astype(np.float32)
-    h = 0.9 * d + 0.5
-    st = SelectState(DEV)
-    N.call("dsvgd_set_bandwidth", st.ptr, h, N.stream(DEV))
-    out = {}
-    old = lib.dsvgd_gsw_debug(0)
-    try:
-        for four in (False, True):
-            lib.dsvgd_gsw_debug(8 if four else 0)
-            Xg, Sg = gpu(X0), gpu(S0)
-            phi = torch.zeros(n, d, device=DEV)
-            sequential_sweep(Xg, Sg, range(n), st, step, target=tgt, phi_out=phi)
-            torch.cuda.synchronize()
-            out[four] = (Xg.cpu().numpy().astype(np.float64), Sg.cpu().numpy(), phi.cpu().numpy())
-    finally:
-        lib.dsvgd_gsw_debug(old)
-    ref, Sr, pr = O.sequential_sweep(X0, S0, h, range(n), step, score_fn=fn)
-    for four in (False, True):
-        e_phi = rel_err(out[four][2], pr)
-        record_parity(e_phi, walk="four" if four else "one")
-        assert e_phi < PHI_TOL, (four, e_phi)
-        assert abs_err(out[four][0], ref) < TRAJ_TOL
-        if fn:
-            assert np.abs(out[four][1] - Sr).max() <= 1e-5 * np.abs(Sr).max()
-    assert np.abs(out[True][0] - out[False][0]).max() <= 1e-5 * max(1.0, np.abs(ref).max())
