@@ -555,3 +555,50 @@ def test_target_fingerprint_of_device_tensors():
     assert dev.fingerprint() == host
     g = T.Gaussian(torch.zeros(3, device=DEV), torch.ones(3, device=DEV))
     assert g.fingerprint() == T.Gaussian(np.zeros(3), np.ones(3)).fingerprint()
+
+
+@pytest.mark.parametrize("load", ["torch", "scores"])
+def test_side_stream_work_beside_the_step(load):
+    """DistSampler overlaps the score all-reduce (a side stream) with the
+    distance / median stage (distsampler.py _compute, reference :160-170):
+    the step's kernels must give the same bits with other work running on
+    another stream.  One engine step (Gram + bracketed median + phi_mm) alone,
+    then again while a side stream runs torch GEMMs / elementwise kernels or
+    the logreg score kernels on other buffers -- phi and h bit-identical."""
+    m = dsvgd()
+    n, d = 16384, 256
+    g = torch.Generator(device="cpu").manual_seed(3)
+    X = (0.1 * torch.randn(n, d, generator=g)).to(DEV)
+    S = torch.randn(n, d, generator=g).to(DEV)
+    eng = m.PhiEngine(n, d, device=DEV)
+    side = torch.cuda.Stream(device=DEV)
+    A = torch.randn(4096, 4096, device=DEV)
+    if load == "scores":
+        x, t, _ = _data(N=4096, p=d - 1, n=8)
+        tgt = m.targets.LogisticRegression(x, t)
+        Xs = (0.1 * torch.randn(n, d, generator=g)).to(DEV)
+        Ss = torch.empty_like(Xs)
+
+    def step():
+        eng.pack(X, S)
+        eng.distances(median=True)
+        eng.median_bandwidth()
+        eng.direction(write_phi=True)
+
+    step()
+    torch.cuda.synchronize()
+    ref_phi, ref_h = eng.phi.clone(), eng.state.read()[1]
+    for rep in range(3):
+        side.wait_stream(torch.cuda.current_stream(DEV))
+        with torch.cuda.stream(side):
+            for _ in range(6):
+                if load == "torch":
+                    B = A @ A
+                    B.mul_(1e-3).add_(1.0)
+                else:
+                    tgt.score(Xs, Ss)
+        step()
+        torch.cuda.current_stream(DEV).wait_stream(side)
+        torch.cuda.synchronize()
+        assert eng.state.read()[1] == ref_h, rep
+        assert torch.equal(eng.phi, ref_phi), (rep, float((eng.phi - ref_phi).abs().max()))
