@@ -588,6 +588,9 @@ class PhiEngine(object):
         self._gparts = gparts(P.gram_parts)
         self._fbparts = gparts(P.fallback_parts)
         self.wmap = torch.tensor(P.tile_weights(), dtype=torch.uint8, device=dev).reshape(-1)
+        # rows of the FmtH2 B image the rank's products read (16-row K-steps;
+        # the image's byte offset of row r is 4 r ldy, like Y's)
+        self._yx_rows = P.image_rows()
         ldy = self.ldy
         # own direct product over the window: split-K slices into KY (the
         # fallback's whole-row phi_mm uses self.splits slices of the same KY)
@@ -690,8 +693,13 @@ class PhiEngine(object):
         colinv = N.ptr(self.yscale) + 4 * ldy
         with span(self.timer, "ysplit"):
             self._scales(ldy, self.yscale, s)
-            N.call("dsvgd_h2_ysplit", N.ptr(self.Y), ldy, self.n_pad, N.ptr(self.yscale),
-                   N.ptr(self.Yx), s)
+            # only the rows the rank's products read: its window, the high
+            # rank's antipodal block (the row half's columns); the transposed
+            # partials read the own rows, inside the window.  (The guard's
+            # fallback reads the FmtX3 image, made from Y.)
+            for r0, nr in self._yx_rows:
+                N.call("dsvgd_h2_ysplit", N.ptr(self.Y) + 4 * r0 * ldy, ldy, nr,
+                       N.ptr(self.yscale), N.ptr(self.Yx) + 4 * r0 * ldy, s)
         fork = torch.cuda.current_stream(self.device).record_event() \
             if self.WINDOW_SIDE_STREAM else None
         with span(self.timer, "phi_partials"):

@@ -126,6 +126,25 @@ class PairSplitPlan(object):
                     w[I][J] = wt
         return w
 
+    def image_rows(self):
+        """The interacting-set rows whose B image (Y's FmtH2 split) the
+        rank's phi products read, as sorted disjoint (start, length) ranges:
+        the window's columns (its own rows among them: the transposed
+        partials' B operand) and, for a high rank, the antipodal block (the
+        row half's columns)."""
+        spans = list(self.window_parts())
+        if self.row_half:
+            spans.append((self.row_half[2], self.row_half[3]))
+        spans.sort()
+        out = []
+        for a, ln in spans:
+            if out and a <= out[-1][0] + out[-1][1]:
+                end = max(out[-1][0] + out[-1][1], a + ln)
+                out[-1] = (out[-1][0], end - out[-1][0])
+            else:
+                out.append((a, ln))
+        return out
+
     def window_parts(self):
         """The own direct product's cyclic window as non-wrapping column ranges."""
         return _cyclic(self.window[0], self.window[1], self.n)

@@ -315,6 +315,18 @@ def test_pair_split_parts_meet_kernel_alignment(S, m):
             assert p["col0"] % 256 == 0 and p["cols"] % 256 == 0 and p["cols"] > 0
             assert p["col0"] + p["cols"] <= n
         assert P.window[0] % 16 == 0 and P.window[1] % 16 == 0 and 0 < P.window[1] <= n
+        # the imaged rows: 16-row aligned, disjoint, and they hold every
+        # column a product of this rank reads (window, row half, own rows)
+        rows_img = P.image_rows()
+        cover = np.zeros(n, bool)
+        for a, ln in rows_img:
+            assert a % 16 == 0 and ln % 16 == 0 and not cover[a:a + ln].any()
+            cover[a:a + ln] = True
+        for c0, ln in P.window_parts():
+            assert cover[c0:c0 + ln].all()
+        if P.row_half:
+            assert cover[P.row_half[2]:P.row_half[2] + P.row_half[3]].all()
+        assert cover[r * m:(r + 1) * m].all()
         if P.row_half:
             ro, nr, c0, nc = P.row_half
             assert ro % 128 == 0 and nr % 128 == 0 and c0 % 16 == 0 and nc % 16 == 0
