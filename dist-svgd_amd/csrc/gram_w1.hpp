@@ -29,8 +29,13 @@
 // size is 0 for tiles that are not stored (below the diagonal of the
 // symmetric layout, past the padded matrix): those stores are dropped by the
 // hardware, no branch in the epilogue.  Padding rows / columns get +inf
-// norms, so their entries come out +inf (skipped by the select), and the
-// diagonal is set to exactly 0 by a per-lane compare.
+// norms, so their entries come out +inf (skipped by the select).  The
+// diagonal: without the select accounting it is set to exactly 0 on the tiles
+// that hold it (a wave-uniform fix-up); with the bracket accounting it is
+// stored as computed -- |y_i|^2 + |y_i|^2 - 2 y_i.y_i, a rounding residue
+// ~2^-22 |y_i|^2, far below the bracket, so counted below it as an exact 0
+// would be -- and phi_mm skips it by index either way.  (A compare + select
+// per value cost two VALU and a VCC hazard nop on every value of every tile.)
 //
 // Limits (the host falls back to sqdist_x3w_kernel otherwise): FmtH2, the
 // none / bracket select modes, no mirror stores (layout 1 or a rectangle),
@@ -326,9 +331,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // per-slice copies (keeps the compiler from hoisting the row values
     // and products of them over the whole tile into SGPRs; not volatile: a
     // side-effecting asm would cut the K-step's scheduling region in two)
-    int tgv = tg[bi];
     float nrv = nr[bi], siv = si2[bi];
-    asm("" : "+v"(tgv), "+v"(nrv), "+v"(siv));
+    asm("" : "+v"(nrv), "+v"(siv));
     f32x4 v[2];
 #pragma unroll
     for (int gg = 0; gg < 2; ++gg) {
@@ -341,8 +345,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         // straight from the accumulator register (keeps the set in AGPRs)
         float a;
         asm("v_accvgpr_read_b32 %0, %1" : "=v"(a) : "a"(acc[S][bi][bj][4 * g + e]));
-        const float x = fmaxf(0.f, (nrv + cn[e]) - siv * (cs[e] * a));
-        v[gg][e] = (kBr && tgv == e + 8 * g + 32 * bj) ? 0.f : x;
+        v[gg][e] = fmaxf(0.f, (nrv + cn[e]) - siv * (cs[e] * a));
       }
       if constexpr (kBr) {
 #pragma unroll
@@ -415,14 +418,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     V8 (&a)[4][2] = af[KS & 1];  // this K-step's strip fragments (read last K-step)
     stage(nxt_st, (KS + 1) & 1);
     // epilogue operands of this slice (see slice())
-    int tgv = 0;
     float nrv = 0.f, siv = 0.f;
     f32x4 cn[2], cs[2], v[2];
     if constexpr (SL >= 0) {
-      tgv = tg[ebi];
       nrv = nr[ebi];
       siv = si2[ebi];
-      asm("" : "+v"(tgv), "+v"(nrv), "+v"(siv));
+      asm("" : "+v"(nrv), "+v"(siv));
 #pragma unroll
       for (int gg = 0; gg < 2; ++gg) {
         const int co = 32 * ebj + 4 * h + 8 * (2 * (SL & 1) + gg);
@@ -454,8 +455,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const int gg = grp >> 2, e = grp & 3, g = 2 * (SL & 1) + gg;
         float av;
         asm("v_accvgpr_read_b32 %0, %1" : "=v"(av) : "a"(acc[E][ebi][ebj][4 * g + e]));
-        const float x = fmaxf(0.f, (nrv + cn[gg][e]) - siv * (cs[gg][e] * av));
-        v[gg][e] = (kBr && tgv == e + 8 * g + 32 * ebj) ? 0.f : x;
+        v[gg][e] = fmaxf(0.f, (nrv + cn[gg][e]) - siv * (cs[gg][e] * av));
         if constexpr (kBr) {
           sw.add(v[gg][e]);
           // settle the per-lane counts here: left alone, the compiler defers
