@@ -109,17 +109,6 @@ struct GramUnitWalk {
 template <int DEPTH>
 struct GramSlotWriter : SlotWriterLdsT<DEPTH> {
   using B = SlotWriterLdsT<DEPTH>;
-  uint32_t bw = 0;   // wave-uniform below-count (the scalar unit's)
-  // as SlotWriterLdsT::add, but the below test's lane mask is counted on the
-  // scalar unit (one compare into an SGPR pair + s_bcnt1 + s_add) instead of
-  // a per-lane shift and add: one VALU less per value in an epilogue that
-  // shares its SIMD's issue slots with the MFMAs
-  __device__ __forceinline__ void add(float v) {
-    const uint32_t d = __float_as_uint(v) - B::klo;
-    bw += (uint32_t)__popcll(__ballot(d >= 0x80000000u));
-    B::stage[B::pos * 64] = v;
-    B::pos += d <= B::kspan ? 1u : 0u;
-  }
   // branch-free but for the uniform loop exit: inactive lanes' stores go out
   // of the slot's buffer range and are dropped (as are entries past cap)
   __device__ __forceinline__ void flush() {
@@ -139,7 +128,9 @@ struct GramSlotWriter : SlotWriterLdsT<DEPTH> {
   }
   __device__ __forceinline__ void finish(const SlotLayout& L, int64_t slot, bool weight2) {
     flush();
-    const uint32_t b = bw;
+    uint32_t b = B::below;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o, 64);
     // every lane stores the same words (no divergent branch)
     const uint32_t flag = weight2 ? DSVGD_SLOT_WEIGHT2 : 0u;
     L.cnt[slot] = (B::cnt < DSVGD_SLOT_WEIGHT2 ? B::cnt : DSVGD_SLOT_WEIGHT2 - 1u) | flag;
@@ -361,7 +352,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int e = 0; e < 4; ++e) sw.add(v[gg][e]);
         // settle the per-lane counts here: left alone, the compiler defers
         // the below-count sum to the tile's end and keeps all 128 keys live
-        asm("" : "+s"(sw.bw), "+v"(sw.pos));
+        asm("" : "+v"(sw.below), "+v"(sw.pos));
       }
     }
     store_slice(v, SL_);
@@ -469,7 +460,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           sw.add(v[gg][e]);
           // settle the per-lane counts here: left alone, the compiler defers
           // the below-count sum to the tile's end and keeps all 128 keys live
-          asm("" : "+s"(sw.bw), "+v"(sw.pos));
+          asm("" : "+v"(sw.below), "+v"(sw.pos));
         }
       }
       if (grp == 1) load_A(KS & 1, k + 2);
