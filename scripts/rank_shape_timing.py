@@ -42,19 +42,16 @@ def main():
     g = torch.Generator(device="cpu").manual_seed(0)
     X = (0.1 * torch.randn(n, d, generator=g)).cuda()
     runs = []
-    pfs = [None]
     for S in [int(v) for v in args.shards.split(",")]:
-        for pf in pfs:
-            for lay in (("rows", "pairs") if args.layout == "both" else (args.layout,)):
-                if lay == "rows":
-                    runs.append((S, lay, False, True, 0, pf))
-                elif S > 1 and dsvgd.PhiEngine.pair_split_ok(n, d, S):
-                    for side in args.side.split(","):
-                        for rest in args.rest.split(","):
-                            for fz in args.fwdz.split(","):
-                                runs.append((S, lay, bool(int(side)), bool(int(rest)), int(fz), pf))
-    lib = dsvgd._native.load()
-    for S, lay, side, rest, fz, pf in runs:
+        for lay in (("rows", "pairs") if args.layout == "both" else (args.layout,)):
+            if lay == "rows":
+                runs.append((S, lay, False, True, 0))
+            elif S > 1 and dsvgd.PhiEngine.pair_split_ok(n, d, S):
+                for side in args.side.split(","):
+                    for rest in args.rest.split(","):
+                        for fz in args.fwdz.split(","):
+                            runs.append((S, lay, bool(int(side)), bool(int(rest)), int(fz)))
+    for S, lay, side, rest, fz in runs:
         dsvgd.PhiEngine.WINDOW_SIDE_STREAM = side
         dsvgd.PhiEngine.REST_BESIDE = rest
         dsvgd.PhiEngine.FWD_ZSPLIT = fz or None
@@ -108,7 +105,7 @@ def main():
         st = {k: round(float(np.mean(v)), 3) for k, v in timer.summary().items()}
         print(json.dumps({"shards": S, "layout": lay + ("+side" if side else "")
                           + ("+rest" if lay == "pairs" and eng.plan is not None
-                             and eng.rest_beside else ""), "m": m, "pf": pf,
+                             and eng.rest_beside else ""), "m": m,
                           "fwd_z": getattr(eng, "fwd_z", None),
                           "row0": r * m, "N_local": per,
                           "ms_per_step_no_comm": e0.elapsed_time(e1) / args.steps,
