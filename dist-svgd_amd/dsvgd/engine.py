@@ -156,6 +156,12 @@ class PhiEngine(object):
     # workgroups x 4 = three full waves instead of 192 of 256), the slices
     # summed in order into the messages (dsvgd_phi_partial_reduce_blocks)
     FWD_ZSPLIT = None
+    # pair split, A/B overrides of the other products' split-K factors (None:
+    # chosen -- dsvgd_phi_splits for the window and the row half, the
+    # fill-the-CUs rule for the other transposed partials)
+    W_SPLITS = None
+    H_SPLITS = None
+    REST_SPLITS = None
 
     GEMMS = ("h2", "x3", "f32")
     DEFAULT_GEMM = "h2"
@@ -595,7 +601,7 @@ class PhiEngine(object):
         # own direct product over the window: split-K slices into KY (the
         # fallback's whole-row phi_mm uses self.splits slices of the same KY)
         wlen = P.window[1]
-        self.w_splits = int(lib.dsvgd_phi_splits(self.m, wlen, ldy))
+        self.w_splits = self.W_SPLITS or int(lib.dsvgd_phi_splits(self.m, wlen, ldy))
         need = max(self.w_splits, self.splits)
         if self.KY.shape[0] < need * self.m:
             self.KY = torch.empty(need * self.m, ldy, **f32)
@@ -603,7 +609,7 @@ class PhiEngine(object):
         # the high rank's row half: its own slices
         if P.row_half:
             ro, nr, c0, nc = P.row_half
-            self.h_splits = int(lib.dsvgd_phi_splits(nr, nc, ldy))
+            self.h_splits = self.H_SPLITS or int(lib.dsvgd_phi_splits(nr, nc, ldy))
             self.KYh = torch.empty(self.h_splits * nr, ldy, **f32)
             self.rsh = torch.empty(self.h_splits * lib.dsvgd_pad128(nr), **f32)
 
@@ -625,11 +631,13 @@ class PhiEngine(object):
                         if self.fwd_z > 1 else None)
         self.t_splits = []
         smax = 0
-        for q in P.sends:
+        for k, q in enumerate(P.sends):
             blocks = (ldy // 512) * (q["mo"] // 128)
             z = 1
             while blocks * z < 256 and q["krows"] // (2 * z) >= 1024:
                 z *= 2
+            if self.REST_SPLITS and k >= (nf if self.fwd_batched else 0):
+                z = self.REST_SPLITS
             self.t_splits.append(z)
             smax = max(smax, z * q["mo"]) if z > 1 else smax
         fwd_wg = nf * (self.m // 128) * (ldy // 512) if self.fwd_batched else 0

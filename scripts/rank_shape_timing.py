@@ -28,6 +28,9 @@ def main():
                     help="pairs: comma list of PhiEngine.WINDOW_SIDE_STREAM settings (0, 1)")
     ap.add_argument("--fwdz", default="0",
                     help="pairs: comma list of PhiEngine.FWD_ZSPLIT settings (0 = chosen, 1 = none)")
+    ap.add_argument("--set", action="append", default=[],
+                    help="pairs: NAME=v1,v2 sweeps a PhiEngine split override "
+                         "(W_SPLITS, H_SPLITS, REST_SPLITS; 0 = chosen)")
     ap.add_argument("--layout", default="both", choices=["rows", "pairs", "both"],
                     help="rows: the row-block layout; pairs: the pair-split layout (DESIGN.md 6; "
                          "the partials' exchange left out, their buffers zero)")
@@ -42,16 +45,25 @@ def main():
     g = torch.Generator(device="cpu").manual_seed(0)
     X = (0.1 * torch.randn(n, d, generator=g)).cuda()
     runs = []
+    overrides = [{}]
+    for spec in args.set:
+        k, vals = spec.split("=")
+        overrides = [dict(o, **{k: int(v)}) for o in overrides for v in vals.split(",")]
     for S in [int(v) for v in args.shards.split(",")]:
         for lay in (("rows", "pairs") if args.layout == "both" else (args.layout,)):
             if lay == "rows":
-                runs.append((S, lay, False, True, 0))
+                runs.append((S, lay, False, True, 0, {}))
             elif S > 1 and dsvgd.PhiEngine.pair_split_ok(n, d, S):
                 for side in args.side.split(","):
                     for rest in args.rest.split(","):
                         for fz in args.fwdz.split(","):
-                            runs.append((S, lay, bool(int(side)), bool(int(rest)), int(fz)))
-    for S, lay, side, rest, fz in runs:
+                            for ov in overrides:
+                                runs.append((S, lay, bool(int(side)), bool(int(rest)), int(fz),
+                                             ov))
+    for S, lay, side, rest, fz, *ovl in runs:
+        ov = ovl[0] if ovl else {}
+        for k in ("W_SPLITS", "H_SPLITS", "REST_SPLITS"):
+            setattr(dsvgd.PhiEngine, k, ov.get(k) or None)
         dsvgd.PhiEngine.WINDOW_SIDE_STREAM = side
         dsvgd.PhiEngine.REST_BESIDE = rest
         dsvgd.PhiEngine.FWD_ZSPLIT = fz or None
@@ -107,6 +119,9 @@ def main():
                           + ("+rest" if lay == "pairs" and eng.plan is not None
                              and eng.rest_beside else ""), "m": m,
                           "fwd_z": getattr(eng, "fwd_z", None),
+                          "w_splits": getattr(eng, "w_splits", None),
+                          "h_splits": getattr(eng, "h_splits", None),
+                          "t_splits": getattr(eng, "t_splits", None),
                           "row0": r * m, "N_local": per,
                           "ms_per_step_no_comm": e0.elapsed_time(e1) / args.steps,
                           "sym_layout": bool(eng.sym), "stages_ms": st}), flush=True)
