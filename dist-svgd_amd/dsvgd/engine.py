@@ -601,7 +601,7 @@ class PhiEngine(object):
         # own direct product over the window: split-K slices into KY (the
         # fallback's whole-row phi_mm uses self.splits slices of the same KY)
         wlen = P.window[1]
-        self.w_splits = self.W_SPLITS or int(lib.dsvgd_phi_splits(self.m, wlen, ldy))
+        self.w_splits = self.W_SPLITS or self.window_split(self.m, wlen, ldy)
         need = max(self.w_splits, self.splits)
         if self.KY.shape[0] < need * self.m:
             self.KY = torch.empty(need * self.m, ldy, **f32)
@@ -667,6 +667,20 @@ class PhiEngine(object):
         for a, q in zip(arr, parts):
             a.ky, a.rs, a.ldk, a.row_off, a.rows, a.splits = q
         self._phiparts = arr
+
+    @staticmethod
+    def window_split(m, wlen, ldy, cus=256, max_chain=16384):
+        """The own window's split-K factor: the smallest power of two whose
+        workgroups (m/128 row blocks x ldy/512 column blocks each) cover the
+        CUs once, with at most max_chain columns per slice (phi_splits'
+        precision bound) -- one wave of long slices rather than
+        dsvgd_phi_splits' two: half the slices to write and re-read in
+        phi_finish_parts (S = 8: 3.19 vs 3.25 ms, profiles/r13k)."""
+        wg = (m // 128) * max(1, ldy // 512)
+        z = 1
+        while (wg * z < cus or -(-wlen // z) > max_chain) and z < 64 and wlen // (2 * z) >= 1024:
+            z *= 2
+        return z
 
     @staticmethod
     def fill_split(wg, rows, cus=256, min_rows=1024):

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--set", action="append", default=[],
                     help="pairs: NAME=v1,v2 sweeps a PhiEngine split override "
                          "(W_SPLITS, H_SPLITS, REST_SPLITS; 0 = chosen)")
+    ap.add_argument("--mode", default="timer",
+                    help="comma list: timer (stage events), plain (no events), graph (the step "
+                         "captured as one HIP graph and replayed: the launch gaps' bound)")
     ap.add_argument("--layout", default="both", choices=["rows", "pairs", "both"],
                     help="rows: the row-block layout; pairs: the pair-split layout (DESIGN.md 6; "
                          "the partials' exchange left out, their buffers zero)")
@@ -95,7 +98,7 @@ def main():
         def step():
             with torch.cuda.device(0):
                 from dsvgd.engine import span
-                with span(timer, "scores"):
+                with span(eng.timer, "scores"):
                     tgt.score(X, Sx)          # all_scores: every particle on the local data
                 eng.pack(X, Sx)
                 eng.distances(median=True)
@@ -106,16 +109,28 @@ def main():
         for _ in range(2):
             step()
         torch.cuda.synchronize()
-        eng.timer = timer
-        timer.events.clear()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(args.steps):
-            step()
-        e1.record()
-        torch.cuda.synchronize()
-        st = {k: round(float(np.mean(v)), 3) for k, v in timer.summary().items()}
-        print(json.dumps({"shards": S, "layout": lay + ("+side" if side else "")
+        for mode in args.mode.split(","):
+          run = step
+          if mode == "timer":
+              eng.timer = timer
+              timer.events.clear()
+          else:
+              eng.timer = None
+          if mode == "graph":
+              from dsvgd.engine import StepGraph
+              run = StepGraph(step, torch.device("cuda:0"))
+              run()
+              run()
+              torch.cuda.synchronize()
+          e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+          e0.record()
+          for _ in range(args.steps):
+              run()
+          e1.record()
+          torch.cuda.synchronize()
+          st = ({k: round(float(np.mean(v)), 3) for k, v in timer.summary().items()}
+                if mode == "timer" else {})
+          print(json.dumps({"shards": S, "mode": mode, "layout": lay + ("+side" if side else "")
                           + ("+rest" if lay == "pairs" and eng.plan is not None
                              and eng.rest_beside else ""), "m": m,
                           "fwd_z": getattr(eng, "fwd_z", None),
@@ -125,6 +140,7 @@ def main():
                           "row0": r * m, "N_local": per,
                           "ms_per_step_no_comm": e0.elapsed_time(e1) / args.steps,
                           "sym_layout": bool(eng.sym), "stages_ms": st}), flush=True)
+          eng.timer = None
         del eng
         torch.cuda.empty_cache()
 
