@@ -246,6 +246,8 @@ def main(argv=None):
     ap.add_argument("--data-rows", type=int, default=16384, help="global data rows")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--breakdown", type=int, default=3,
+                    help="extra steps after the timed region with every stage's HIP events")
     ap.add_argument("--gemm", default="h2", choices=["h2", "x3", "f32"],
                     help="MFMA engine of the contractions (h2: fp16 split, the default)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -314,8 +316,11 @@ def main(argv=None):
     for _ in range(args.warmup):
         sampler.make_step(eps)
     torch.cuda.synchronize()
-    # per-stage HIP events ride along the timed steps (same stream as the kernels)
-    timer = StageTimer()
+    # phi_mm's HIP events ride along the timed steps (same stream as its
+    # kernels); every other stage's pair of stream markers would stall the
+    # queue between kernels (≈ 10 µs each, profiles/r13j), so the per-stage
+    # breakdown is timed on --breakdown extra steps after the timed region
+    timer = StageTimer(only={"phi_mm"})
     sampler.timer = timer
     barrier()
     torch.cuda.synchronize()
@@ -331,14 +336,21 @@ def main(argv=None):
                           device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
-    stages = {k: float(np.mean(v)) for k, v in timer.summary().items()}
+    ev = timer.summary().get("phi_mm") or [float("nan")]
+    phi_timed = gather_max({"phi_mm": float(np.mean(ev))}, world, args.backend, dev)
+    full = StageTimer()
+    sampler.timer = full
+    for _ in range(args.breakdown):
+        sampler.make_step(eps)
+    sampler.timer = None
+    stages = {k: float(np.mean(v)) for k, v in full.summary().items()}
     # N > 1: each stage's mean HIP-event time, max over ranks (the exchange
     # stages allgather_x / allreduce_scores / hist_allreduce included)
     stages = gather_max(stages, world, args.backend, dev)
     assert bool(torch.isfinite(sampler._work).all()), "non-finite particles"
 
     m = n // world
-    phi_ms = stages["phi_mm"]
+    phi_ms = phi_timed["phi_mm"]     # the timed region's own launches
     eng = sampler._engines[next(iter(sampler._engines))]
     gemm = eng.phi_gemm
     peak, peak_basis = engine_peak(gemm)
@@ -397,6 +409,8 @@ def main(argv=None):
                      "algorithmic_bytes": 4.0 * m * n + 4.0 * (n + 128) * 512,
                      "flop_per_launch": flops, "avg_launch_ms": phi_ms},
         "stages_ms": stages,
+        "stages_basis": "mean HIP-event time per step over %d steps after the timed region "
+                        "(phi_mm in roofline: the timed steps' own)" % args.breakdown,
         "passes": passes(eng, stages, m, n, d, per_data, args.gemm),
         "gemm": gemm,
         "step_6n2d_f32_mfma_frac": (6.0 * m * n * d) / (el / args.steps) / 1e12 / PEAK_FP32_MFMA_TFLOPS,
