@@ -327,6 +327,53 @@ __global__ __launch_bounds__(256) void rowsplit_h2_kernel(const float* __restric
   }
 }
 
+// rowscale_h2_kernel and rowsplit_h2_kernel<*, true> in one pass (the
+// logreg W image, rebuilt every step): one wave per row takes the row's
+// largest magnitude, its power-of-two scale (rscale, rinv), then splits the
+// row -- the second read hits the L1 / L2 lines the first one brought in.
+// Per 256-column chunk lane l holds K-step 16 q + l / 4, values 4 (l & 3) ..
+// +3: one 8-byte store per part into the row's 32-byte slot (halves swapped
+// on rows with bit 3 set, as rowsplit_h2_kernel).  Same bits as the two
+// kernels (same maxima, scales and splits).
+__global__ __launch_bounds__(256) void rowimage_h2_kernel(const float* __restrict__ A,
+                                                          int64_t lda, int64_t rows, int64_t cols,
+                                                          int64_t rows_pad, int64_t ksteps,
+                                                          float* __restrict__ rscale,
+                                                          float* __restrict__ rinv,
+                                                          _Float16* __restrict__ img) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= rows_pad) return;
+  const float* row = A + i * lda;
+  uint32_t m = 0u;
+  if (i < rows)
+    for (int64_t c = lane; c < cols; c += 64) m = max(m, abs_bits(row[c]));
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+  const float sc = pow2_scale(__uint_as_float(m));
+  if (lane == 0) {
+    rscale[i] = sc;
+    rinv[i] = pow2_inv(sc);
+  }
+  const int sw = (int)((i >> 3) & 1);
+  const int k0 = 4 * (lane & 3);
+  const int pos = (k0 < 8 ? 8 * sw : 8 * (sw ^ 1)) + (k0 & 7);
+  for (int64_t kb = lane >> 2; kb < ksteps; kb += 16) {
+    f16x4 h[2];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t c = kb * 16 + k0 + e;
+      const float a = (i < rows && c < cols) ? row[c] : 0.f;
+      _Float16 v[2];
+      split_fmt<FmtH2>(sc * a, v);
+      h[0][e] = v[0];
+      h[1][e] = v[1];
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      *reinterpret_cast<f16x4*>(img + ((kb * 2 + p) * rows_pad + i) * 16 + pos) = h[p];
+  }
+}
+
 // the partial maxima, then 4 words of range statistics (dsvgd_h2_colscale_guarded)
 size_t h2_colscale_ws_floats(int64_t rows, int64_t cols) {
   return (size_t)((rows + kScaleRows - 1) / kScaleRows) * (size_t)(cols < 1 ? 1 : cols) + 4;
@@ -402,6 +449,13 @@ int h2_rowsplit_rows_range(const float* A, int64_t lda, int64_t rows, int64_t co
                      dim3(256), 0, s, A, lda, rows, cols, rows_pad, ksteps, rscale,
                      (_Float16*)img, row_begin, nrows);
   return check_launch("rowsplit_h2(range)");
+}
+
+int h2_rowimage(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                int64_t kpad, float* rscale, float* rinv, void* img, hipStream_t s) {
+  hipLaunchKernelGGL(rowimage_h2_kernel, dim3((unsigned)((rows_pad + 3) / 4)), dim3(256), 0, s, A,
+                     lda, rows, cols, rows_pad, kpad / kX3Step, rscale, rinv, (_Float16*)img);
+  return check_launch("rowimage_h2");
 }
 
 int h2_rowscale(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
@@ -497,6 +551,16 @@ int dsvgd_h2_rowscale(const float* A, int64_t lda, int64_t rows, int64_t cols, i
   DSVGD_REQUIRE(A && rscale, "null pointer");
   DSVGD_REQUIRE(rows >= 0 && cols > 0 && rows <= rows_pad && lda >= cols, "sizes");
   return h2_rowscale(A, lda, rows, cols, rows_pad, rscale, rinv, (hipStream_t)stream);
+}
+
+int dsvgd_h2_rowimage(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                      int64_t kpad, float* rscale, float* rinv, void* img, void* stream) {
+  DSVGD_REQUIRE(A && rscale && rinv && img, "null pointer");
+  DSVGD_REQUIRE(rows >= 0 && cols > 0 && rows <= rows_pad && lda >= cols && kpad >= cols, "sizes");
+  DSVGD_REQUIRE(rows_pad > 0 && rows_pad % 16 == 0 && kpad % kX3Step == 0,
+                "rows_pad and kpad must be positive multiples of 16");
+  DSVGD_REQUIRE(((uintptr_t)img & 15) == 0, "16-byte alignment");
+  return h2_rowimage(A, lda, rows, cols, rows_pad, kpad, rscale, rinv, img, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -37,6 +37,8 @@ int h2_rowsplit_rows(const float* A, int64_t lda, int64_t rows, int64_t cols, in
                      int64_t kpad, const float* rscale, void* img, hipStream_t s);
 int h2_rowscale(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
                 float* rscale, float* rinv, hipStream_t s);
+int h2_rowimage(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                int64_t kpad, float* rscale, float* rinv, void* img, hipStream_t s);
 size_t h2_colscale_ws_floats(int64_t rows, int64_t cols);
 
 static int64_t nn_cols(int64_t w) {
@@ -553,10 +555,9 @@ static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float 
     float* rsw = (float*)(base + w.off_rsw);
     float* riw = (float*)(base + w.off_riw);
     float* sxd = (float*)(base + w.off_sxd);
-    // W = X[:, 1:] in place (the row image reads its unaligned rows through
-    // aligned 16-byte windows), one power-of-two scale per particle row
-    if ((rc = h2_rowscale(X + 1, ldx, n, p, w.n_pad, rsw, riw, s))) return rc;
-    if ((rc = h2_rowsplit_rows(X + 1, ldx, n, p, w.n_pad, w.pp, rsw, Wx, s))) return rc;
+    // W = X[:, 1:] in place, one power-of-two scale per particle row: scale
+    // and image in one pass (rowimage_h2_kernel)
+    if ((rc = h2_rowimage(X + 1, ldx, n, p, w.n_pad, w.pp, rsw, riw, Wx, s))) return rc;
     int blocks = 0;
     if ((rc = persistent_blocks(reinterpret_cast<const void*>(&logreg_z_x3p_kernel<FmtH2>),
                                 &blocks, 512)))

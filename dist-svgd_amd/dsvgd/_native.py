@@ -85,6 +85,7 @@ SIGNATURES = {
     "dsvgd_h2_rowsplit": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _p, _p, _p]),
     "dsvgd_h2_rowsplit_rows": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _p, _p, _p]),
     "dsvgd_h2_rowscale": (_int, [_p, _i64, _i64, _i64, _i64, _p, _p, _p]),
+    "dsvgd_h2_rowimage": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p]),
     "dsvgd_sqdist_h2": (_int, [_p, _p, _i64, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _int, _p,
                                _p]),
     "dsvgd_phi_mm_h2": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _int,

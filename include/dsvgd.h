@@ -343,6 +343,10 @@ int dsvgd_h2_rowsplit_rows_range(const float* A, int64_t lda, int64_t rows, int6
  * rowinv[i] = 1 / rowscale[i] (nullable), for i < rows_pad (1 past rows) */
 int dsvgd_h2_rowscale(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
                       float* rowscale, float* rowinv, void* stream);
+/* dsvgd_h2_rowscale (rowinv required) and dsvgd_h2_rowsplit_rows with those
+ * scales in one pass over A: the same bits (round 5; the logreg W image) */
+int dsvgd_h2_rowimage(const float* A, int64_t lda, int64_t rows, int64_t cols, int64_t rows_pad,
+                      int64_t kpad, float* rowscale, float* rowinv, void* img, void* stream);
 /* dsvgd_sqdist_x3 on the FmtH2 engine: Yg = dsvgd_h2_rowsplit_rows(Y, ldy,
  * n_pad, dp, n_pad + 256, dp, rowscale) with the per-row scales of Y's X half
  * (dsvgd_pack_h2's rowscale, or dsvgd_h2_rowscale; >= n_pad floats); same

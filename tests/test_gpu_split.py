@@ -424,3 +424,60 @@ def test_logreg_scores_general_labels(n, N):
         err[gemm] = float(np.abs(out.cpu().numpy() - ref).max() / np.abs(ref).max())
     record_parity(err["h2"], f32=err["f32"])
     assert err["h2"] <= 2.0 * err["f32"] + 1e-7 and err["h2"] < 1e-5, err
+
+
+@pytest.mark.parametrize("n,d,ties", [(65536, 256, False), (1000, 7, False), (4099, 33, True),
+                                      (3, 5, True)])
+def test_colcenter_is_the_lower_median_of_its_sample(n, d, ties):
+    """dsvgd_colcenter: per column the lower median of min(n, 1024) evenly
+    spaced rows (row k n / m) -- value-exact against numpy on the same
+    sample, ties (repeated values, signed zeros) included."""
+    from dsvgd import _native as N
+    rs = np.random.RandomState(n + d)
+    X = rs.randn(n, d).astype(np.float32)
+    if ties:
+        X = np.round(X * 2.0).astype(np.float32) / 2.0   # few distinct values, zeros of both signs
+        X[::3, 0] = -0.0
+    Xg = gpu(X)
+    mean = torch.full((d,), np.nan, device=DEV)
+    N.call("dsvgd_colcenter", N.ptr(Xg), d, n, d, N.ptr(mean), N.stream(0))
+    torch.cuda.synchronize()
+    m = min(n, 1024)
+    rows = (np.arange(m, dtype=np.int64) * n) // m
+    want = np.sort(X[rows], axis=0, kind="stable")[(m - 1) // 2]
+    got = mean.cpu().numpy()
+    assert np.array_equal(got, want), np.nonzero(got != want)
+
+
+@pytest.mark.parametrize("n,p,off", [(65536, 255, 1), (1000, 100, 1), (300, 64, 0), (17, 1023, 3)])
+def test_rowimage_equals_rowscale_then_rowsplit(n, p, off):
+    """dsvgd_h2_rowimage (the logreg W image in one pass) gives the same bits
+    as dsvgd_h2_rowscale + dsvgd_h2_rowsplit_rows: scales, inverses, image."""
+    from dsvgd import _native as N
+    lib = N.load()
+    rs = np.random.RandomState(n + p)
+    ld = off + p + 5
+    X = rs.randn(n, ld).astype(np.float32) * np.exp2(rs.randint(-20, 20, size=(n, 1))).astype(np.float32)
+    X[min(5, n - 1)] = 0.0      # a zero row: scale 1
+    Xg = gpu(X)
+    rows_pad = -(-n // 256) * 256
+    kpad = -(-p // 32) * 32
+    nb = lib.dsvgd_h2_image_bytes(rows_pad, kpad)
+    out = []
+    for fused in (False, True):
+        sc = torch.full((rows_pad,), -1.0, device=DEV)
+        inv = torch.full((rows_pad,), -1.0, device=DEV)
+        img = torch.full((nb // 2,), 7, dtype=torch.int16, device=DEV)
+        A = N.ptr(Xg) + 4 * off
+        if fused:
+            N.call("dsvgd_h2_rowimage", A, ld, n, p, rows_pad, kpad, N.ptr(sc), N.ptr(inv),
+                   N.ptr(img), N.stream(0))
+        else:
+            N.call("dsvgd_h2_rowscale", A, ld, n, p, rows_pad, N.ptr(sc), N.ptr(inv), N.stream(0))
+            N.call("dsvgd_h2_rowsplit_rows", A, ld, n, p, rows_pad, kpad, N.ptr(sc), N.ptr(img),
+                   N.stream(0))
+        torch.cuda.synchronize()
+        out.append((sc.cpu().numpy(), inv.cpu().numpy(), img.cpu().numpy()))
+    for a, b in zip(*out):
+        assert np.array_equal(a.view(np.uint32) if a.dtype == np.float32 else a,
+                              b.view(np.uint32) if b.dtype == np.float32 else b)
