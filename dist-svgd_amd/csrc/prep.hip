@@ -128,47 +128,31 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
 // The mean moves by (outlier) / n when one particle diverges, and every
 // other particle then sits that far from it (a particle 2^16 spreads away
 // costs the mean-centred Gram ~3e-4 of phi in fp32); the median of a sample
-// stays inside the bulk.  One block per column: the sample goes to LDS and
-// each thread ranks 4 of its values against all m (broadcast reads, two
-// barriers; a bitonic sort took 55 barriers, 22.8 µs per call at n = 65536,
-// profiles/r13j); the lower median is the value v_i with
-// #{v < v_i} <= (m - 1) / 2 < #{v <= v_i}, the first such i written
-// (deterministic among ties).
+// stays inside the bulk.  One block per column: the sample is bitonic-sorted
+// in LDS (deterministic, no data-dependent control flow).
 constexpr int kCenterRows = 1024;
 
 __global__ __launch_bounds__(256) void colcenter_kernel(const float* __restrict__ X, int64_t ldx,
                                                         int64_t n, float* __restrict__ center) {
   __shared__ float v[kCenterRows];
-  __shared__ int first;
   const int64_t c = blockIdx.x;
   const int m = (int)min(n, (int64_t)kCenterRows);
-  const int t = threadIdx.x;
-  for (int k = t; k < kCenterRows; k += 256)
+  for (int k = threadIdx.x; k < kCenterRows; k += 256)
     v[k] = k < m ? X[((int64_t)k * n / m) * ldx + c] : INFINITY;
-  if (t == 0) first = kCenterRows;
   __syncthreads();
-  float q[4];
-  int lt[4], le[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    q[u] = v[t + 256 * u];
-    lt[u] = 0;
-    le[u] = 0;
-  }
-  for (int j = 0; j < m; ++j) {
-    const float a = v[j];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      lt[u] += a < q[u];
-      le[u] += a <= q[u];
+  for (int size = 2; size <= kCenterRows; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < kCenterRows / 2; t += 256) {
+        const int i = 2 * t - (t & (stride - 1)), j = i + stride;
+        const float a = v[i], b = v[j];
+        if ((a > b) == ((i & size) == 0)) {
+          v[i] = b;
+          v[j] = a;
+        }
+      }
+      __syncthreads();
     }
-  }
-  const int k = (m - 1) / 2;
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
-    if (t + 256 * u < m && lt[u] <= k && k < le[u]) atomicMin(&first, t + 256 * u);
-  __syncthreads();
-  if (t == 0) center[c] = v[first < kCenterRows ? first : k];
+  if (threadIdx.x == 0) center[c] = v[(m - 1) / 2];
 }
 
 // ---------------------------------------------------------------- pack ----
