@@ -229,6 +229,10 @@ __global__ __launch_bounds__(256) void ysplit_kernel(const float* __restrict__ Y
   }
 }
 
+// the symmetric layout's phi_mm: 1 = one launch per row (DS 4), 0 = the
+// two-launch hybrid (DS 1 + DS 2); dsvgd_phi_set_symrow
+static int g_phi_symrow = 1;
+
 template <int TN, bool EXP, class F>
 int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy, int splits,
                  const dsvgd_select_state* st, float* C, int64_t ldc, float* rowsum, int64_t m,
@@ -250,6 +254,15 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
       hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F>), grid, dim3(512), 0, s, D, K,
                          Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0, 0, gate, gate_on);
   } else {  // FmtH2: the smaller stages fit a 3-stage ring
+    if (TN == 4 && EXP && sym && splits >= 2 && g_phi_symrow) {
+      // symmetric layout, each row's slices in ONE launch (phi_w1 DS 4):
+      // contiguous K ranges walked ascending, transposed K-steps first; the
+      // blocks of an XCD share a slice (xmap: 8 | row blocks x slices)
+      const bool xmap = grid.x == 1 && 8 % splits == 0 && (grid.y * splits) % 8 == 0;
+      launch_w1<4>(grid, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0,
+                   gate, gate_on, 0, 0, 0, xmap ? 1 : 0);
+      return check_launch("phi_w1_kernel(rows)");
+    }
     if (TN == 4 && EXP && sym && splits >= 2) {
       // symmetric layout split at each row block's diagonal tile: the
       // transposed K-steps (phi_w1 DS 1: the stored tiles transposed through
@@ -845,6 +858,12 @@ using namespace dsvgd;
 extern "C" {
 
 int64_t dsvgd_phi_splits(int64_t m, int64_t n, int64_t ldy) { return phi_splits(m, n, ldy); }
+
+int dsvgd_phi_set_symrow(int on) {
+  const int prev = g_phi_symrow;
+  g_phi_symrow = on ? 1 : 0;
+  return prev;
+}
 
 int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t row0,
                  int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,

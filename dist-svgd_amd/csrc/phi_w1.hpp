@@ -63,6 +63,13 @@ __device__ __forceinline__ f32x4 w1_load_nt(__amdgpu_buffer_rsrc_t r, int voff, 
 //     a panel-row boundary), and the image K-step of D row j is ks_begin + j/16
 //     (the owned rows' place in the interacting set): C = K(rows, cols)^T Y_rows,
 //     the partial a rank sends to the owner of those columns.
+//   DS 4: the symmetric layout's whole row in ONE launch: slice z of row
+//     block by takes the contiguous K range [z kchunk, +kchunk), walked
+//     ascending -- its transposed K-steps (left of the row block, as DS 1)
+//     first, then the plain ones (as DS 2).  Every block of a slice is at the
+//     same K-step at the same time whatever its row, and the blocks of one
+//     XCD share a slice (xmap), so the Yx K-steps they read are the same
+//     ones: one fetch per XCD instead of one per block walk.
 template <int DS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void phi_w1_kernel(
     const float* A, int64_t a_npad, const _Float16* Yx, int64_t ldy,
@@ -75,16 +82,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   using F = FmtH2;
   using V8 = F::V8;
   constexpr int P = PhiW1::P;
-  constexpr bool TR = DS == 1 || DS == 3;
-  __shared__ __attribute__((aligned(16))) char smem[PhiW1::kSmemBytes + (TR ? 4 * PhiW1::kScrBytes : 0)];
+  constexpr bool TRK = DS == 1 || DS == 3 || DS == 4;  // a transposed phase exists
+  __shared__ __attribute__((aligned(16))) char smem[PhiW1::kSmemBytes + (TRK ? 4 * PhiW1::kScrBytes : 0)];
   const int t = threadIdx.x, lane = t & 63, r = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   // DS 1 / 2: a row block's slices dispatched back to back, longest first
   // (the transposed part grows with the row, the plain part shrinks)
   const int64_t lin = (int64_t)blockIdx.z * gridDim.y + blockIdx.y;
-  const int64_t by = DS == 2 ? lin / gridDim.z
+  // DS 4 with xmap (t_per = 1; gridDim.x = 1, gridDim.z | 8, 8 | blocks):
+  // linear block id 8 q + x (x: the XCD it is dispatched to) -> slice x mod
+  // Z, row block (8 / Z) q + x / Z
+  const bool xm = DS == 4 && t_per == 1;
+  const int64_t lid = lin * gridDim.x + blockIdx.x;
+  const int64_t by = xm ? (lid >> 3) * (8 / gridDim.z) + (lid & 7) / gridDim.z
+                   : DS == 2 ? lin / gridDim.z
                    : DS == 1 ? (int64_t)gridDim.y - 1 - lin / gridDim.z : blockIdx.y;
-  const int64_t bz = (DS == 1 || DS == 2) ? lin % gridDim.z : blockIdx.z;
+  const int64_t bz = xm ? (lid & 7) % gridDim.z
+                   : (DS == 1 || DS == 2) ? lin % gridDim.z : blockIdx.z;
   // DS 3 batched over several column blocks of D (t_per > 0: t_per row
   // blocks of output per part; part q is D's column block (t_first + q) mod
   // t_nblk, its output t_ostride floats after part q - 1's; split-K slice z
@@ -93,7 +107,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int64_t tpart = tb ? by / t_per : 0;
   const int64_t byl = tb ? by % t_per : by;
   const int64_t i0 = byl * PhiW1::BM;
-  const int64_t c0 = (int64_t)blockIdx.x * PhiW1::BC + w * 128;
+  const int64_t c0 = (xm ? 0 : (int64_t)blockIdx.x * PhiW1::BC) + w * 128;
   // K-step k of this block is global K-step ks0 + kdir * k.  The symmetric
   // forms interleave the slices, slice z taking every Z-th K-step of its
   // range (DS 2 top-down from K, DS 1 up from 0): the blocks running together
@@ -117,6 +131,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     ks0 = (int)bz;
     nsteps = T > bz ? (T - (int)bz + Z - 1) / Z : 0;
   }
+  // DS 4: the slice's transposed K-steps [ks0, ksp), then the plain ones
+  // [ksp, ks0 + nsteps)
+  const int ksp = DS == 4 ? (int)min(max(kb0, i0), kend) / PhiW1::BJ : 0;
   if (tb) {   // batched DS 3: slice z of part q at (z * parts + q) t_ostride
     const int64_t at = ((int64_t)bz * (gridDim.y / t_per) + tpart) * t_ostride;
     C += at;
@@ -140,8 +157,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int aoff = x3_off(srow, shalf);       // this thread's 16 B of a part image row
   // diagonal: global row - the thread's first column at K-step 0, clamped to
   // int range (only |.| < 16 matters; DS 1 never meets it)
-  const int64_t dg = row0 + i0 + srow - 8 * shalf - (int64_t)ks0 * PhiW1::BJ;
-  const int qd0 = (int)max(min(dg, (int64_t)(1 << 30)), (int64_t)-(1 << 30));
+  auto diag0 = [&](int kfirst) {
+    const int64_t dg = row0 + i0 + srow - 8 * shalf - (int64_t)kfirst * PhiW1::BJ;
+    return (int)max(min(dg, (int64_t)(1 << 30)), (int64_t)-(1 << 30));
+  };
 
   f32x16 acc[4][4];
 #pragma unroll
@@ -155,7 +174,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // symmetric layout (m == n, row0 == 0): K-steps left of the block's
   // diagonal tile (DS 1) read the stored tile (J, I) transposed
   const int symI = tb ? (int)(((t_first + tpart) % t_nblk) * t_per + byl)
-                   : DS == 3 ? tcol0 + (int)by : sym ? (int)(i0 >> 7) : -1;
+                   : DS == 3 ? tcol0 + (int)by : (sym || DS == 4) ? (int)(i0 >> 7) : -1;
   const int64_t pcols = a_npad >> 4;
   // DS 1: lane (piece p = t >> 5, s = t & 31) loads rows i0 + 16 p + 8 (s & 1)
   // .. +7 of column j0 + (s >> 1): 32 contiguous bytes of panel I*8 + p
@@ -165,7 +184,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int sw_off = ((lane & 31) >> 1) * PhiW1::kScrLd + 16 * (lane >> 5) + 8 * (lane & 1);
   const int sr_off = 8 * shalf * PhiW1::kScrLd + (lane >> 1);
 
-  if (nsteps > 0) {
+  // one phase: nsteps K-steps from global K-step ks0 (stride kdir), all
+  // transposed (TR) or all plain
+  auto phase = [&](auto TR_, const int ks0, const int nsteps, const int qd0) {
+    constexpr bool TR = decltype(TR_)::value;
+    if (nsteps <= 0) return;
     V8 b[4][P];       // B fragments of the current K-step; column tile ni is
                       // reloaded for the next K-step right after its last MFMA
     f32x4 dr[4][2];   // D values: K-step k in dr[k & 3], loaded 3 K-steps ahead
@@ -318,6 +341,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       step(k + 7, smem + PhiW1::SA, smem, dr[0], dr[2], dr[1]);
       barrier();
     }
+  };
+  if constexpr (DS == 4) {
+    phase(std::true_type{}, ks0, ksp - ks0, 0);
+    phase(std::false_type{}, ksp, ks0 + nsteps - ksp, diag0(ksp));
+  } else {
+    phase(std::integral_constant<bool, DS == 1 || DS == 3>{}, ks0, nsteps, diag0(ks0));
   }
 
   // epilogue (nn_x3_kernel's): C = acc * colinv * 2^-15; row sums by column block 0
@@ -334,7 +363,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
     }
   const float v = rs + __shfl_xor(rs, 1, 64);
-  if (blockIdx.x == 0 && shalf == 0 && i0 + srow < m) rowsum[i0 + srow] = v * (1.f / F::kAScale);
+  if ((xm || blockIdx.x == 0) && shalf == 0 && i0 + srow < m) rowsum[i0 + srow] = v * (1.f / F::kAScale);
 }
 
 }  // namespace dsvgd

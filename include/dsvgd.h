@@ -233,6 +233,11 @@ int dsvgd_sqdist_x3(const void* Yg, const float* norms, int64_t row0, int64_t m,
  * dsvgd/distsampler.py:84-101.  dsvgd_phi_splits gives a slice count that
  * fills the 256 CUs (>= 2 blocks per CU) for an m-row block. */
 int64_t dsvgd_phi_splits(int64_t m, int64_t n, int64_t ldy);
+/* The symmetric layout's phi_mm form (A/B switch, returns the previous
+ * setting): 1 (default) = one launch, each row block's split-K slices walking
+ * contiguous K ranges ascending, transposed K-steps first (phi_w1 DS 4);
+ * 0 = two launches split at each row block's diagonal tile (DS 1 + DS 2). */
+int dsvgd_phi_set_symrow(int on);
 int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t row0,
                  int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
                  int64_t ldk, float* rowsum, void* stream);

@@ -313,13 +313,25 @@ def test_phi_full_size_sampled_rows():
     assert rel_err(got, ref) < PHI_TOL
 
 
-@pytest.mark.parametrize("n,d", [(4096, 1024), (8192, 256)])
-def test_phi_symmetric_hybrid_sampled_rows(n, d):
-    """The symmetric layout's phi_mm at split-K >= 2 is the hybrid (NNX3Tile on
-    each row block's transposed K-steps, phi_w1 on the rest, interleaved
-    slices): rows from every region of the triangle -- first and last row
-    blocks, block edges, the diagonal tiles -- vs fp64; d = 1024 runs four
-    column blocks per row block."""
+@pytest.mark.parametrize("symrow", [1, 0])
+@pytest.mark.parametrize("n,d", [(4096, 1024), (8192, 256), (4200, 256)])
+def test_phi_symmetric_hybrid_sampled_rows(n, d, symrow):
+    """The symmetric layout's phi_mm at split-K >= 2: one launch per row
+    (symrow = 1, phi_w1 DS 4: contiguous slices, transposed K-steps first,
+    slices mapped to XCDs when 8 | row blocks x slices) or the two-launch
+    hybrid (DS 1 + DS 2, interleaved slices): rows from every region of the
+    triangle -- first and last row blocks, block edges, the diagonal tiles --
+    vs fp64; d = 1024 runs four column blocks per row block (no XCD map),
+    n = 4200 a ragged last row block."""
+    from dsvgd import _native as N
+    prev = N.load().dsvgd_phi_set_symrow(symrow)
+    try:
+        _phi_symmetric_rows(n, d)
+    finally:
+        N.load().dsvgd_phi_set_symrow(prev)
+
+
+def _phi_symmetric_rows(n, d):
     rs = np.random.RandomState(n + d)
     X = (0.2 * rs.randn(n, d)).astype(np.float32)
     mu = rs.randn(d).astype(np.float32)
