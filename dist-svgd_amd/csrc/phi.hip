@@ -232,6 +232,12 @@ __global__ __launch_bounds__(256) void ysplit_kernel(const float* __restrict__ Y
 // the symmetric layout's phi_mm: 1 = one launch per row (DS 4), 0 = the
 // two-launch hybrid (DS 1 + DS 2); dsvgd_phi_set_symrow
 static int g_phi_symrow = 1;
+// DS 0 launches map their split-K slices to XCDs when the grid allows it
+// (phi_w1.hpp xmap); dsvgd_phi_set_xmap
+static int g_phi_xmap = 1;
+static int xmap_ok(dim3 g) {
+  return g_phi_xmap && g.x == 1 && g.z > 1 && 8 % g.z == 0 && ((int64_t)g.y * g.z) % 8 == 0;
+}
 
 template <int TN, bool EXP, class F>
 int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy, int splits,
@@ -258,7 +264,7 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
       // symmetric layout, each row's slices in ONE launch (phi_w1 DS 4):
       // contiguous K ranges walked ascending, transposed K-steps first; the
       // blocks of an XCD share a slice (xmap: 8 | row blocks x slices)
-      const bool xmap = grid.x == 1 && 8 % splits == 0 && (grid.y * splits) % 8 == 0;
+      const bool xmap = xmap_ok(grid);
       launch_w1<4>(grid, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0,
                    gate, gate_on, 0, 0, 0, xmap ? 1 : 0);
       return check_launch("phi_w1_kernel(rows)");
@@ -280,7 +286,7 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
     }
     if (TN == 4 && EXP && !sym) {
       launch_w1<0>(grid, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0,
-                   gate, gate_on);
+                   gate, gate_on, 0, 0, 0, xmap_ok(grid));
       return check_launch("phi_w1_kernel");
     }
     hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2>), grid,
@@ -859,6 +865,12 @@ extern "C" {
 
 int64_t dsvgd_phi_splits(int64_t m, int64_t n, int64_t ldy) { return phi_splits(m, n, ldy); }
 
+int dsvgd_phi_set_xmap(int on) {
+  const int prev = g_phi_xmap;
+  g_phi_xmap = on ? 1 : 0;
+  return prev;
+}
+
 int dsvgd_phi_set_symrow(int on) {
   const int prev = g_phi_symrow;
   g_phi_symrow = on ? 1 : 0;
@@ -993,7 +1005,7 @@ int dsvgd_phi_h2_window(const float* D, int64_t ldd, const void* Yh, int64_t ldy
   const dim3 grid((unsigned)(ldy / PhiW1::BC), (unsigned)(roundup(m, 128) / 128), (unsigned)splits);
   launch_w1<0>(grid, (hipStream_t)stream, D, n_pad, (const _Float16*)Yh, ldy, wlen, kchunk, st, KY,
                ldk, rowsum, m, row0, 0, colinv, 0, gate, gate_on, (int)(col0 / PhiW1::BJ),
-               (int)(n_pad / PhiW1::BJ), 0);
+               (int)(n_pad / PhiW1::BJ), 0, xmap_ok(grid));
   return check_launch("phi_w1_kernel(window)");
 }
 

@@ -89,10 +89,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // DS 1 / 2: a row block's slices dispatched back to back, longest first
   // (the transposed part grows with the row, the plain part shrinks)
   const int64_t lin = (int64_t)blockIdx.z * gridDim.y + blockIdx.y;
-  // DS 4 with xmap (t_per = 1; gridDim.x = 1, gridDim.z | 8, 8 | blocks):
-  // linear block id 8 q + x (x: the XCD it is dispatched to) -> slice x mod
-  // Z, row block (8 / Z) q + x / Z
-  const bool xm = DS == 4 && t_per == 1;
+  // DS 4 and DS 0 with xmap (t_per = 1; gridDim.x = 1, gridDim.z | 8, 8 |
+  // blocks): linear block id 8 q + x (x: the XCD it is dispatched to) ->
+  // slice x mod Z, row block (8 / Z) q + x / Z -- the blocks running on one
+  // XCD walk the same K range, so they read the same Yx K-steps
+  const bool xm = (DS == 4 || DS == 0) && t_per == 1;
   const int64_t lid = lin * gridDim.x + blockIdx.x;
   const int64_t by = xm ? (lid >> 3) * (8 / gridDim.z) + (lid & 7) / gridDim.z
                    : DS == 2 ? lin / gridDim.z

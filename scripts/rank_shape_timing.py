@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--mode", default="timer",
                     help="comma list: timer (stage events), plain (no events), graph (the step "
                          "captured as one HIP graph and replayed: the launch gaps' bound)")
+    ap.add_argument("--xmap", default="1",
+                    help="comma list of dsvgd_phi_set_xmap settings (slices mapped to XCDs)")
     ap.add_argument("--layout", default="both", choices=["rows", "pairs", "both"],
                     help="rows: the row-block layout; pairs: the pair-split layout (DESIGN.md 6; "
                          "the partials' exchange left out, their buffers zero)")
@@ -109,7 +111,9 @@ def main():
         for _ in range(2):
             step()
         torch.cuda.synchronize()
-        for mode in args.mode.split(","):
+        from dsvgd import _native as NX
+        for mode, xv in [(a, b) for a in args.mode.split(",") for b in args.xmap.split(",")]:
+          NX.load().dsvgd_phi_set_xmap(int(xv))
           run = step
           if mode == "timer":
               eng.timer = timer
@@ -130,7 +134,7 @@ def main():
           torch.cuda.synchronize()
           st = ({k: round(float(np.mean(v)), 3) for k, v in timer.summary().items()}
                 if mode == "timer" else {})
-          print(json.dumps({"shards": S, "mode": mode, "layout": lay + ("+side" if side else "")
+          print(json.dumps({"shards": S, "mode": mode, "xmap": int(xv), "layout": lay + ("+side" if side else "")
                           + ("+rest" if lay == "pairs" and eng.plan is not None
                              and eng.rest_beside else ""), "m": m,
                           "fwd_z": getattr(eng, "fwd_z", None),

@@ -39,9 +39,15 @@ def main():
         eng.step(X, S, h=None, write_phi=True)
         phis[mode] = eng.phi.clone()
     diff = float((phis[1] - phis[0]).abs().max() / phis[0].abs().max())
+    # forms: (symrow, xmap, splits)
+    forms = {"rows": (1, 1, eng.splits), "rows_noxmap": (1, 0, eng.splits),
+             "rows_z2": (1, 1, 2), "hybrid": (0, 1, eng.splits)}
+    base_splits = eng.splits
     for _ in range(args.rounds):
-        for mode in (1, 0):
-            lib.dsvgd_phi_set_symrow(mode)
+        for mode, (sr, xm, z) in forms.items():
+            lib.dsvgd_phi_set_symrow(sr)
+            lib.dsvgd_phi_set_xmap(xm)
+            eng.splits = z
             eng.step(X, S, h=None, write_phi=False)
             t = StageTimer(only={"phi_mm", "sqdist"})
             eng.timer = t
@@ -51,9 +57,11 @@ def main():
             sm = t.summary()
             out.setdefault(mode, []).append(float(np.mean(sm["phi_mm"])))
     lib.dsvgd_phi_set_symrow(1)
-    print(json.dumps({"n": n, "d": d, "splits": int(eng.splits), "sym": bool(eng.sym),
-                      "phi_mm_ms_rows(DS4)": out[1], "phi_mm_ms_hybrid(DS1+2)": out[0],
-                      "mean_rows": float(np.mean(out[1])), "mean_hybrid": float(np.mean(out[0])),
+    lib.dsvgd_phi_set_xmap(1)
+    eng.splits = base_splits
+    print(json.dumps({"n": n, "d": d, "splits": int(base_splits), "sym": bool(eng.sym),
+                      "phi_mm_ms": out,
+                      "mean": {k: float(np.mean(v)) for k, v in out.items()},
                       "phi_rel_diff_rows_vs_hybrid": diff}), flush=True)
 
 
