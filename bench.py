@@ -357,7 +357,11 @@ def main(argv=None):
     # the committed PMC summary is an N=1 profile: only quoted for the N=1 run
     # phi_mm is the NN tile with the fused exp (<TN, DMA, EXP=true, ..., Fmt>);
     # the logreg G.Xd launch is the same tile with EXP=false
-    knames = {"h2": (["_ZN5dsvgd13phi_w1_kernelILi1E", "_ZN5dsvgd13phi_w1_kernelILi2E"]
+    from dsvgd import _native as NL
+    symrow = NL.load().dsvgd_phi_set_symrow(1)       # read the form back (set returns it)
+    NL.load().dsvgd_phi_set_symrow(symrow)
+    knames = {"h2": ((["_ZN5dsvgd13phi_w1_kernelILi4E"] if symrow else
+                      ["_ZN5dsvgd13phi_w1_kernelILi1E", "_ZN5dsvgd13phi_w1_kernelILi2E"])
                      if eng.sym else ["_ZN5dsvgd13phi_w1_kernelILi0E"]),
               "x3": ["void dsvgd::nn_x3_kernel<4, true, true, true, 2, dsvgd::FmtX3,"],
               "f32": ["void dsvgd::nn_kernel<4, true,"]}[gemm]
@@ -387,9 +391,13 @@ def main(argv=None):
                    "n": n, "d": d, "N_global": Ng, "parallelism": "dp%d" % world,
                    "particles_per_gpu": m},
         "roofline": {"bound": "mfma",
-                     "kernel": {"h2": ("phi_mm (phi_w1_kernel<1> on each row block's "
-                                       "transposed K-steps + phi_w1_kernel<2> on the rest: one wave "
-                                       "per SIMD, FmtH2" if eng.sym
+                     "kernel": {"h2": (("phi_mm (phi_w1_kernel<4>: one launch, each row block's "
+                                        "split-K slices walking contiguous K ranges, its transposed "
+                                        "K-steps first, slices mapped to XCDs; one wave per SIMD, FmtH2"
+                                        if symrow else
+                                        "phi_mm (phi_w1_kernel<1> on each row block's "
+                                        "transposed K-steps + phi_w1_kernel<2> on the rest: one wave "
+                                        "per SIMD, FmtH2") if eng.sym
                                        else "phi_mm (phi_w1_kernel<0>: one wave per SIMD, FmtH2") +
                                       ": fp32-accurate 2-part fp16 split, 3 fp16 MFMA products "
                                       "per fp32 product; D layout %s)" % ("symmetric" if eng.sym

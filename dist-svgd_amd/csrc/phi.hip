@@ -232,11 +232,15 @@ __global__ __launch_bounds__(256) void ysplit_kernel(const float* __restrict__ Y
 // the symmetric layout's phi_mm: 1 = one launch per row (DS 4), 0 = the
 // two-launch hybrid (DS 1 + DS 2); dsvgd_phi_set_symrow
 static int g_phi_symrow = 1;
-// DS 0 launches map their split-K slices to XCDs when the grid allows it
-// (phi_w1.hpp xmap); dsvgd_phi_set_xmap
+// split-K slices mapped to XCDs when the grid allows it (phi_w1.hpp xmap):
+// 0 off, 1 DS 4 only (default), 2 DS 4 and DS 0; dsvgd_phi_set_xmap.  DS 4
+// without it: 11.44 vs 11.09 ms at S = 1; the S = 8 window with it: 3.03 /
+// 3.13 vs 3.01 / 3.02 ms (profiles/r13o) -- its slices' K ranges are short
+// enough to share the L2 either way
 static int g_phi_xmap = 1;
-static int xmap_ok(dim3 g) {
-  return g_phi_xmap && g.x == 1 && g.z > 1 && 8 % g.z == 0 && ((int64_t)g.y * g.z) % 8 == 0;
+static int xmap_ok(dim3 g, int level) {
+  return g_phi_xmap >= level && g.x == 1 && g.z > 1 && 8 % g.z == 0 &&
+         ((int64_t)g.y * g.z) % 8 == 0;
 }
 
 template <int TN, bool EXP, class F>
@@ -264,7 +268,7 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
       // symmetric layout, each row's slices in ONE launch (phi_w1 DS 4):
       // contiguous K ranges walked ascending, transposed K-steps first; the
       // blocks of an XCD share a slice (xmap: 8 | row blocks x slices)
-      const bool xmap = xmap_ok(grid);
+      const bool xmap = xmap_ok(grid, 1);
       launch_w1<4>(grid, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0,
                    gate, gate_on, 0, 0, 0, xmap ? 1 : 0);
       return check_launch("phi_w1_kernel(rows)");
@@ -286,7 +290,7 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
     }
     if (TN == 4 && EXP && !sym) {
       launch_w1<0>(grid, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0,
-                   gate, gate_on, 0, 0, 0, xmap_ok(grid));
+                   gate, gate_on, 0, 0, 0, xmap_ok(grid, 2));
       return check_launch("phi_w1_kernel");
     }
     hipLaunchKernelGGL((nn_x3_kernel<TN, TN != 1, EXP, false, 2, F, TN != 1 ? 3 : 2>), grid,
@@ -865,9 +869,9 @@ extern "C" {
 
 int64_t dsvgd_phi_splits(int64_t m, int64_t n, int64_t ldy) { return phi_splits(m, n, ldy); }
 
-int dsvgd_phi_set_xmap(int on) {
+int dsvgd_phi_set_xmap(int level) {
   const int prev = g_phi_xmap;
-  g_phi_xmap = on ? 1 : 0;
+  g_phi_xmap = level < 0 ? 0 : (level > 2 ? 2 : level);
   return prev;
 }
 
@@ -1005,7 +1009,7 @@ int dsvgd_phi_h2_window(const float* D, int64_t ldd, const void* Yh, int64_t ldy
   const dim3 grid((unsigned)(ldy / PhiW1::BC), (unsigned)(roundup(m, 128) / 128), (unsigned)splits);
   launch_w1<0>(grid, (hipStream_t)stream, D, n_pad, (const _Float16*)Yh, ldy, wlen, kchunk, st, KY,
                ldk, rowsum, m, row0, 0, colinv, 0, gate, gate_on, (int)(col0 / PhiW1::BJ),
-               (int)(n_pad / PhiW1::BJ), 0, xmap_ok(grid));
+               (int)(n_pad / PhiW1::BJ), 0, xmap_ok(grid, 2));
   return check_launch("phi_w1_kernel(window)");
 }
 

@@ -13,9 +13,10 @@ sys.path.insert(0, ROOT)
 
 
 def test_pmc_traffic_picks_phi_mm():
-    """The quoted traffic is phi_mm's: on the symmetric layout the sum of
-    phi_w1<1> (transposed K-steps) and phi_w1<2> (the rest) of the same step --
-    never a logreg launch -- and nothing when a launch of the pair is missing."""
+    """The quoted traffic is phi_mm's: on the symmetric layout phi_w1<4> (one
+    launch per row), or with the two-launch form the sum of phi_w1<1>
+    (transposed K-steps) and phi_w1<2> (the rest) of the same step -- never a
+    logreg launch -- and nothing when a launch of the pair is missing."""
     import bench
     summ = os.path.join(ROOT, "profiles", "latest_summary.json")
     if not os.path.exists(summ):
@@ -38,6 +39,9 @@ def test_pmc_traffic_picks_phi_mm():
         assert both == a + b
         assert src == os.path.join("profiles", "latest_summary.json")
     assert bench.pmc_traffic(["no-such-kernel"]) == (None, None)
+    w4 = "_ZN5dsvgd13phi_w1_kernelILi4E"   # the one-launch form (default since round 5)
+    c = per_launch(w4)
+    assert bench.pmc_traffic([w4])[0] == c
     lr = [k for k in ks if "logreg" in k and "hbm_bytes_per_launch" in ks[k]]
     if lr and a is not None:
         assert all(not k.startswith(w1) for k in lr)
