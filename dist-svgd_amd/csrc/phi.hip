@@ -869,6 +869,16 @@ extern "C" {
 
 int64_t dsvgd_phi_splits(int64_t m, int64_t n, int64_t ldy) { return phi_splits(m, n, ldy); }
 
+int64_t dsvgd_phi_splits_sym(int64_t n, int64_t ldy) {
+  int64_t s = phi_splits(n, n, ldy);
+  if (!g_phi_symrow) return s;
+  // the one-launch form: its slices' chains may reach 2 kMaxChain (as each
+  // launch of the hybrid's did), while the launch still fills the CUs twice
+  const int64_t n_pad = roundup(n, 128), blocks = (n_pad / 128) * (ldy % 512 == 0 ? ldy / 512 : 1);
+  while (s > 2 && n_pad / (s / 2) <= 2 * kMaxChain && blocks * (s / 2) >= 512) s /= 2;
+  return s;
+}
+
 int dsvgd_phi_set_xmap(int level) {
   const int prev = g_phi_xmap;
   g_phi_xmap = level < 0 ? 0 : (level > 2 ? 2 : level);

@@ -67,6 +67,7 @@ SIGNATURES = {
     "dsvgd_set_bandwidth": (_int, [_p, _f, _p]),
     "dsvgd_phi_splits": (_i64, [_i64, _i64, _i64]),
     "dsvgd_phi_set_symrow": (_int, [_int]),
+    "dsvgd_phi_splits_sym": (_i64, [_i64, _i64]),
     "dsvgd_phi_set_xmap": (_int, [_int]),
     "dsvgd_phi_mm": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p]),
     "dsvgd_phi_mm_gated": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p,

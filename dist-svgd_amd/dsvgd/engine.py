@@ -264,6 +264,9 @@ class PhiEngine(object):
         elif "h2" in (phi_gemm, gram_gemm):
             self.scale_ws = torch.empty(
                 max(1, lib.dsvgd_h2_colscale_workspace_floats(self.n_pad, self.ldy)), **f32)
+        if self.sym and phi_gemm == "h2":
+            # the one-launch form (phi_w1 DS 4) walks longer slices
+            self.splits = int(lib.dsvgd_phi_splits_sym(n, self.ldy))
         self.KY = torch.empty(self.splits * m, self.ldy, **f32)
         self.rowsum = torch.empty(self.splits * self.m_pad, **f32)
         self.mean = torch.empty(d, **f32)    # the packing centre (dsvgd_colcenter)

@@ -238,6 +238,11 @@ int64_t dsvgd_phi_splits(int64_t m, int64_t n, int64_t ldy);
  * contiguous K ranges ascending, transposed K-steps first (phi_w1 DS 4);
  * 0 = two launches split at each row block's diagonal tile (DS 1 + DS 2). */
 int dsvgd_phi_set_symrow(int on);
+/* The split-K slices of the symmetric layout's phi_mm (n x n, the engine's
+ * KY / rowsum hold this many): dsvgd_phi_splits, or with the one-launch form
+ * half as many while each fp32 chain stays within 2 x 16384 columns and the
+ * launch has >= 512 blocks (n = 65536, d = 256: 2). */
+int64_t dsvgd_phi_splits_sym(int64_t n, int64_t ldy);
 /* Map a phi_mm launch's split-K slices to XCDs (A/B switch, returns the
  * previous level): the blocks of one XCD then walk one K range and share its
  * Yx K-steps in their L2.  0 = off, 1 = the symmetric layout's one-launch
