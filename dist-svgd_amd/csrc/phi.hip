@@ -239,8 +239,7 @@ static int g_phi_symrow = 1;
 // enough to share the L2 either way
 static int g_phi_xmap = 1;
 static int xmap_ok(dim3 g, int level) {
-  return g_phi_xmap >= level && g.x == 1 && g.z > 1 && 8 % g.z == 0 &&
-         ((int64_t)g.y * g.z) % 8 == 0;
+  return g_phi_xmap >= level && g.z > 1 && 8 % g.z == 0 && ((int64_t)g.x * g.y * g.z) % 8 == 0;
 }
 
 template <int TN, bool EXP, class F>

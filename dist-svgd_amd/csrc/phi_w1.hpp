@@ -89,13 +89,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // DS 1 / 2: a row block's slices dispatched back to back, longest first
   // (the transposed part grows with the row, the plain part shrinks)
   const int64_t lin = (int64_t)blockIdx.z * gridDim.y + blockIdx.y;
-  // DS 4 and DS 0 with xmap (t_per = 1; gridDim.x = 1, gridDim.z | 8, 8 |
-  // blocks): linear block id 8 q + x (x: the XCD it is dispatched to) ->
-  // slice x mod Z, row block (8 / Z) q + x / Z -- the blocks running on one
-  // XCD walk the same K range, so they read the same Yx K-steps
+  // DS 4 and DS 0 with xmap (t_per = 1; gridDim.z | 8, 8 | blocks): linear
+  // block id 8 q + x (x: the XCD it is dispatched to) -> slice x mod Z, and
+  // u = (8 / Z) q + x / Z -> column block u mod gridDim.x, row block
+  // u / gridDim.x -- the blocks running on one XCD walk the same K range, so
+  // they read the same Yx K-steps
   const bool xm = (DS == 4 || DS == 0) && t_per == 1;
   const int64_t lid = lin * gridDim.x + blockIdx.x;
-  const int64_t by = xm ? (lid >> 3) * (8 / gridDim.z) + (lid & 7) / gridDim.z
+  const int64_t xu = (lid >> 3) * (8 / gridDim.z) + (lid & 7) / gridDim.z;
+  const int64_t cbx = xm ? xu % gridDim.x : blockIdx.x;
+  const int64_t by = xm ? xu / gridDim.x
                    : DS == 2 ? lin / gridDim.z
                    : DS == 1 ? (int64_t)gridDim.y - 1 - lin / gridDim.z : blockIdx.y;
   const int64_t bz = xm ? (lid & 7) % gridDim.z
@@ -108,7 +111,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int64_t tpart = tb ? by / t_per : 0;
   const int64_t byl = tb ? by % t_per : by;
   const int64_t i0 = byl * PhiW1::BM;
-  const int64_t c0 = (xm ? 0 : (int64_t)blockIdx.x * PhiW1::BC) + w * 128;
+  const int64_t c0 = cbx * PhiW1::BC + w * 128;
   // K-step k of this block is global K-step ks0 + kdir * k.  The symmetric
   // forms interleave the slices, slice z taking every Z-th K-step of its
   // range (DS 2 top-down from K, DS 1 up from 0): the blocks running together
@@ -364,7 +367,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
     }
   const float v = rs + __shfl_xor(rs, 1, 64);
-  if ((xm || blockIdx.x == 0) && shalf == 0 && i0 + srow < m) rowsum[i0 + srow] = v * (1.f / F::kAScale);
+  if (cbx == 0 && shalf == 0 && i0 + srow < m) rowsum[i0 + srow] = v * (1.f / F::kAScale);
 }
 
 }  // namespace dsvgd
