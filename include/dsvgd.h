@@ -246,8 +246,9 @@ int64_t dsvgd_phi_splits_sym(int64_t n, int64_t ldy);
 /* Map a phi_mm launch's split-K slices to XCDs (A/B switch, returns the
  * previous level): the blocks of one XCD then walk one K range and share its
  * Yx K-steps in their L2.  0 = off, 1 = the symmetric layout's one-launch
- * form only (default), 2 = also the full layout / window launches; grids
- * whose slice count divides 8 and whose block count 8 divides. */
+ * form only (default), 2 = also the full layout / window launches; grids of
+ * one column block whose slice count divides 8 and whose block count 8
+ * divides. */
 int dsvgd_phi_set_xmap(int level);
 int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t row0,
                  int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,

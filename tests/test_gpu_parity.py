@@ -332,8 +332,9 @@ def test_phi_symmetric_hybrid_sampled_rows(n, d, symrow):
     slices mapped to XCDs when 8 | row blocks x slices) or the two-launch
     hybrid (DS 1 + DS 2, interleaved slices): rows from every region of the
     triangle -- first and last row blocks, block edges, the diagonal tiles --
-    vs fp64; d = 1024 runs four column blocks per row block, n = 4200 a
-    ragged last row block (33 row blocks: the XCD map only with 8 slices)."""
+    vs fp64; d = 1024 runs four column blocks per row block (no XCD map),
+    n = 4200 a ragged last row block (33 row blocks: the map only with 8
+    slices)."""
     from dsvgd import _native as N
     prev = N.load().dsvgd_phi_set_symrow(symrow)
     try:
