@@ -232,6 +232,9 @@ __global__ __launch_bounds__(256) void ysplit_kernel(const float* __restrict__ Y
 // the symmetric layout's phi_mm: 1 = one launch per row (DS 4), 0 = the
 // two-launch hybrid (DS 1 + DS 2); dsvgd_phi_set_symrow
 static int g_phi_symrow = 1;
+// logreg's G . Xd (FmtH2, 256 columns) on phi_w1_kernel<0, 2, false> (1) or
+// the 8-wave 256-row NN tile (0); dsvgd_phi_set_gxd_w1
+static int g_gxd_w1 = 1;
 // split-K slices mapped to XCDs when the grid allows it (phi_w1.hpp xmap):
 // 0 off, 1 DS 4 only (default), 2 DS 4 and DS 0; dsvgd_phi_set_xmap.  DS 4
 // without it: 11.44 vs 11.09 ms at S = 1; the S = 8 window with it: 3.03 /
@@ -316,6 +319,17 @@ int nn_split_gemm(bool exp_, const float* A, int64_t K, const typename F::E* Yx,
   if (K * ldy * 2 * F::P >= ((int64_t)1 << 31) || K * 128 * 4 >= ((int64_t)1 << 31))
     return fail_arg("nn_x3: K x ldy too large for 32-bit buffer offsets");
   if (ldy % 128 != 0) return fail_arg("nn_x3: ldy must be a multiple of 128");
+  if constexpr (F::P == 2) {
+    if (!exp_ && ldy % 512 != 0 && ldy % 256 == 0 && g_gxd_w1) {
+      // G . Xd on phi_w1's shape: 128-row x 256-column blocks of four waves
+      // of 64 columns, B straight from the image, two blocks per CU
+      const int64_t kchunk = roundup((K + splits - 1) / splits, kX3Step);
+      const dim3 grid(ldy / 256, roundup(m, 128) / 128, splits);
+      hipLaunchKernelGGL((phi_w1_kernel<0, 2, false>), grid, dim3(PhiW1::kThreads), 0, s, A, K, Yx,
+                         ldy, K, kchunk, st, C, ldc, rowsum, m, row0, 0, colinv, 0, gate, gate_on);
+      return check_launch("phi_w1_kernel(G.Xd)");
+    }
+  }
   if (!exp_ && (m16 || F::P == 2) && ldy % 512 != 0 && ldy % 256 == 0) {
     // 256-row blocks x 256 columns (G . Xd): the A rows must exist up to a
     // multiple of 256 (the caller's panel layout; logreg pads n to 256)
@@ -880,6 +894,12 @@ int64_t dsvgd_phi_splits_sym(int64_t n, int64_t ldy) {
   const int64_t n_pad = roundup(n, 128), blocks = (n_pad / 128) * (ldy % 512 == 0 ? ldy / 512 : 1);
   while (s > 2 && n_pad / (s / 2) <= 2 * kMaxChain && blocks * (s / 2) >= 512) s /= 2;
   return s;
+}
+
+int dsvgd_phi_set_gxd_w1(int on) {
+  const int prev = g_gxd_w1;
+  g_gxd_w1 = on ? 1 : 0;
+  return prev;
 }
 
 int dsvgd_phi_set_xmap(int level) {

@@ -70,7 +70,11 @@ __device__ __forceinline__ f32x4 w1_load_nt(__amdgpu_buffer_rsrc_t r, int voff, 
 //     same K-step at the same time whatever its row, and the blocks of one
 //     XCD share a slice (xmap), so the Yx K-steps they read are the same
 //     ones: one fetch per XCD instead of one per block walk.
-template <int DS>
+// NI: 32-column tiles per wave (4: the 512-column block, one wave per SIMD;
+// 2: 256-column blocks of 64 columns per wave, 128 accumulators -- two
+// blocks per CU).  EXP = false: f = identity with the FmtH2 A scale (logreg
+// G . Xd, DS 0 only): no exp, no diagonal, no row sums, no select state.
+template <int DS, int NI = 4, bool EXP = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void phi_w1_kernel(
     const float* A, int64_t a_npad, const _Float16* Yx, int64_t ldy,
     int64_t K, int64_t kchunk, const dsvgd_select_state* __restrict__ st, float* __restrict__ C,
@@ -78,8 +82,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const float* __restrict__ colinv, int slice0, const float* __restrict__ gate, int gate_on,
     int ks_begin = 0, int ks_wrap = 0, int tcol0 = 0, int t_per = 0, int t_first = 0,
     int t_nblk = 1, int64_t t_ostride = 0) {
+  static_assert(NI == 4 || NI == 2, "NI: 4 or 2 column tiles per wave");
+  static_assert(EXP || DS == 0, "the identity form is DS 0 only");
+  const bool want_rs = EXP || rowsum != nullptr;   // (before the slice offset below)
   if (gate && ((*gate != 0.f) != (gate_on != 0))) return;  // the FmtH2 range guard (nn_x3_kernel)
   using F = FmtH2;
+  constexpr int BC = 4 * 32 * NI;   // block columns
   using V8 = F::V8;
   constexpr int P = PhiW1::P;
   constexpr bool TRK = DS == 1 || DS == 3 || DS == 4;  // a transposed phase exists
@@ -111,7 +119,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int64_t tpart = tb ? by / t_per : 0;
   const int64_t byl = tb ? by % t_per : by;
   const int64_t i0 = byl * PhiW1::BM;
-  const int64_t c0 = cbx * PhiW1::BC + w * 128;
+  const int64_t c0 = cbx * BC + w * 32 * NI;
   // K-step k of this block is global K-step ks0 + kdir * k.  The symmetric
   // forms interleave the slices, slice z taking every Z-th K-step of its
   // range (DS 2 top-down from K, DS 1 up from 0): the blocks running together
@@ -146,7 +154,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     C += (int64_t)(slice0 + bz) * m * ldc;
     rowsum += (int64_t)(slice0 + bz) * roundup128(m);
   }
-  const float scale = -st->inv_h * kLog2e;
+  const float scale = EXP ? -st->inv_h * kLog2e : 0.f;
 
   // D: the block's panel row; thread t stages row t >> 1, columns 8 (t & 1) .. +7
   const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc(
@@ -166,11 +174,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     return (int)max(min(dg, (int64_t)(1 << 30)), (int64_t)-(1 << 30));
   };
 
-  f32x16 acc[4][4];
+  f32x16 acc[4][NI];
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
+    for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[mi][ni][q] = 0.f;
   float rs = 0.f;
@@ -193,7 +201,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   auto phase = [&](auto TR_, const int ks0, const int nsteps, const int qd0) {
     constexpr bool TR = decltype(TR_)::value;
     if (nsteps <= 0) return;
-    V8 b[4][P];       // B fragments of the current K-step; column tile ni is
+    V8 b[NI][P];      // B fragments of the current K-step; column tile ni is
                       // reloaded for the next K-step right after its last MFMA
     f32x4 dr[4][2];   // D values: K-step k in dr[k & 3], loaded 3 K-steps ahead
     f32x4 tr[2];      // DS 1: K-step k+1's values, transposed during K-step k - 1
@@ -237,8 +245,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const float v = q < 4 ? d[0][q] : d[1][q - 4];
-        const float x = __builtin_amdgcn_exp2f(fmaf(v, scale, F::kAScaleLog2));
-        e[q] = (!TR && qd == q) ? 0.f : x;
+        const float x = EXP ? __builtin_amdgcn_exp2f(fmaf(v, scale, F::kAScaleLog2))
+                            : v * F::kAScale;   // G 2^15 (exact)
+        e[q] = (EXP && !TR && qd == q) ? 0.f : x;
       }
       const float s = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
       rs += k <= last ? s : 0.f;
@@ -269,7 +278,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       else
         stage(nxt, ds_, k + 1);
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
+      for (int ni = 0; ni < NI; ++ni) {
         // small terms first, as mfma_products
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) acc[mi][ni] = mfma_fmt<F>(a[mi][1], b[ni][0], acc[mi][ni]);
@@ -288,13 +297,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       // early among them, so its reads land before the closing barrier)
       __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
+      for (int i = 0; i < 4 * NI; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x002, kW1Sgb, 0);
       }
       __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
 #pragma unroll
-      for (int i = 0; i < 32; ++i) {
+      for (int i = 0; i < 8 * NI; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         if (TR && i == 1) __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
         if (TR && i >= 2 && i < 10) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
@@ -305,7 +314,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
     // prologue: B(0), D(0..2); A(0) -> stage 0 (DS 1: D(0), D(1) transposed)
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) loadB(ni, 0);
+    for (int ni = 0; ni < NI; ++ni) loadB(ni, 0);
     loadD(dr[0], 0);
     loadD(dr[1], 1);
     loadD(dr[2], 2);
@@ -357,7 +366,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
+    for (int ni = 0; ni < NI; ++ni) {
       const int64_t col = c0 + ni * 32 + r;
       const float cs = colinv[col] * (1.f / F::kAScale);
 #pragma unroll
@@ -366,8 +375,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (row < m) C[row * ldc + col] = acc[mi][ni][q] * cs;
       }
     }
-  const float v = rs + __shfl_xor(rs, 1, 64);
-  if (cbx == 0 && shalf == 0 && i0 + srow < m) rowsum[i0 + srow] = v * (1.f / F::kAScale);
+  // (the identity form keeps its row sums when asked for: with them dead
+  // the compiler's schedule of the unrolled loop spilled ~3700 registers)
+  {
+    const float v = rs + __shfl_xor(rs, 1, 64);
+    if (want_rs && cbx == 0 && shalf == 0 && i0 + srow < m)
+      rowsum[i0 + srow] = v * (1.f / F::kAScale);
+  }
 }
 
 }  // namespace dsvgd
