@@ -233,8 +233,11 @@ __global__ __launch_bounds__(256) void ysplit_kernel(const float* __restrict__ Y
 // two-launch hybrid (DS 1 + DS 2); dsvgd_phi_set_symrow
 static int g_phi_symrow = 1;
 // logreg's G . Xd (FmtH2, 256 columns) on phi_w1_kernel<0, 2, false> (1) or
-// the 8-wave 256-row NN tile (0); dsvgd_phi_set_gxd_w1
-static int g_gxd_w1 = 1;
+// the 8-wave 256-row NN tile (0, default: the phi_w1 shape measured slower,
+// scores 3.57 vs 3.38 ms at N = 16384, 0.58 vs 0.52 at 2048 -- with half
+// phi_mm's MFMAs per K-step its staging is no longer hidden; profiles/r13r);
+// dsvgd_phi_set_gxd_w1
+static int g_gxd_w1 = 0;
 // split-K slices mapped to XCDs when the grid allows it (phi_w1.hpp xmap):
 // 0 off, 1 DS 4 only (default), 2 DS 4 and DS 0; dsvgd_phi_set_xmap.  DS 4
 // without it: 11.44 vs 11.09 ms at S = 1; the S = 8 window with it: 3.03 /

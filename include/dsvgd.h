@@ -251,8 +251,9 @@ int64_t dsvgd_phi_splits_sym(int64_t n, int64_t ldy);
  * divides. */
 int dsvgd_phi_set_xmap(int level);
 /* logreg's G . Xd on the FmtH2 engine with 256 output columns (p <= 255):
- * phi_w1's one-wave-per-SIMD shape in 128 x 256 blocks (1, default) or the
- * 8-wave 256-row NN tile (0).  A/B switch; returns the previous setting. */
+ * phi_w1's one-wave-per-SIMD shape in 128 x 256 blocks (1; measured slower)
+ * or the 8-wave 256-row NN tile (0, default).  A/B switch; returns the
+ * previous setting. */
 int dsvgd_phi_set_gxd_w1(int on);
 int dsvgd_phi_mm(const float* D, int64_t ldd, const float* Y, int64_t ldy, int64_t row0,
                  int64_t m, int64_t n, const dsvgd_select_state* st, int64_t splits, float* KY,
