@@ -238,17 +238,17 @@ static int g_phi_symrow = 1;
 // phi_mm's MFMAs per K-step its staging is no longer hidden; profiles/r13r);
 // dsvgd_phi_set_gxd_w1
 static int g_gxd_w1 = 0;
-// split-K slices mapped to XCDs when the grid allows it (phi_w1.hpp xmap):
-// 0 off, 1 DS 4 only (default), 2 DS 4 and DS 0; dsvgd_phi_set_xmap.  DS 4
-// without it: 11.44 vs 11.09 ms at S = 1; the S = 8 window with it: 3.03 /
-// 3.13 vs 3.01 / 3.02 ms (profiles/r13o) -- its slices' K ranges are short
-// enough to share the L2 either way
+// split-K slices mapped to XCDs when the grid allows it (phi_w1.hpp xmap),
+// a bit mask: 1 DS 4 (default), 2 DS 0 (full layout, window), 4 the batched
+// DS 3 (forward partials); dsvgd_phi_set_xmap.  DS 4 without it: 11.44 vs
+// 11.09 ms at S = 1; the S = 8 window with it: 3.03 / 3.13 vs 3.01 / 3.02 ms
+// (profiles/r13o)
 static int g_phi_xmap = 1;
-static int xmap_ok(dim3 g, int level) {
+static int xmap_ok(dim3 g, int bit) {
   // one column block only: at d = 1024 (four) the map measured 45.4 vs 44.4
   // ms without it (profiles/r13q) -- there the blocks of a row sharing an
   // XCD's L2 for their D panels is what counts
-  return g_phi_xmap >= level && g.x == 1 && g.z > 1 && 8 % g.z == 0 &&
+  return (g_phi_xmap & bit) && g.x == 1 && g.z > 1 && 8 % g.z == 0 &&
          ((int64_t)g.y * g.z) % 8 == 0;
 }
 
@@ -905,9 +905,9 @@ int dsvgd_phi_set_gxd_w1(int on) {
   return prev;
 }
 
-int dsvgd_phi_set_xmap(int level) {
+int dsvgd_phi_set_xmap(int mask) {
   const int prev = g_phi_xmap;
-  g_phi_xmap = level < 0 ? 0 : (level > 2 ? 2 : level);
+  g_phi_xmap = mask & 7;
   return prev;
 }
 
@@ -1106,9 +1106,10 @@ int dsvgd_phi_h2_transposed_blocks_split(const float* D, int64_t ldd, const void
   DSVGD_REQUIRE(((uintptr_t)Yh & 15) == 0 && ((uintptr_t)D & 15) == 0, "16-byte alignment");
   const int64_t per = m / 128;
   const dim3 grid((unsigned)(ldy / PhiW1::BC), (unsigned)(per * count), (unsigned)zsplit);
+  // (tcol0 is unused by the batched form: 1 = its slices mapped to XCDs)
   launch_w1<3>(grid, (hipStream_t)stream, D, n_pad, (const _Float16*)Yh, ldy, m, m / zsplit, st, P, ldp,
                P + m * ldp, m, (int64_t)0, 0, colinv, 0, gate, gate_on, (int)(yrow0 / PhiW1::BJ), 0,
-               0, (int)per, (int)first, (int)nblocks, pstride);
+               xmap_ok(grid, 4), (int)per, (int)first, (int)nblocks, pstride);
   return check_launch("phi_w1_kernel(transposed blocks)");
 }
 

@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // u = (8 / Z) q + x / Z -> column block u mod gridDim.x, row block
   // u / gridDim.x -- the blocks running on one XCD walk the same K range, so
   // they read the same Yx K-steps
-  const bool xm = (DS == 4 || DS == 0) && t_per == 1;
+  const bool xm = ((DS == 4 || DS == 0) && t_per == 1) || (DS == 3 && t_per > 0 && tcol0 == 1);
   const int64_t lid = lin * gridDim.x + blockIdx.x;
   const int64_t xu = (lid >> 3) * (8 / gridDim.z) + (lid & 7) / gridDim.z;
   const int64_t cbx = xm ? xu % gridDim.x : blockIdx.x;

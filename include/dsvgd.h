@@ -244,12 +244,12 @@ int dsvgd_phi_set_symrow(int on);
  * launch has >= 512 blocks (n = 65536, d = 256: 2). */
 int64_t dsvgd_phi_splits_sym(int64_t n, int64_t ldy);
 /* Map a phi_mm launch's split-K slices to XCDs (A/B switch, returns the
- * previous level): the blocks of one XCD then walk one K range and share its
- * Yx K-steps in their L2.  0 = off, 1 = the symmetric layout's one-launch
- * form only (default), 2 = also the full layout / window launches; grids of
- * one column block whose slice count divides 8 and whose block count 8
- * divides. */
-int dsvgd_phi_set_xmap(int level);
+ * previous mask): the blocks of one XCD then walk one K range and share its
+ * Yx K-steps in their L2.  Bits: 1 = the symmetric layout's one-launch form
+ * (default), 2 = the full layout / window launches, 4 = the pair split's
+ * batched forward partials; grids of one column block whose slice count
+ * divides 8 and whose block count 8 divides. */
+int dsvgd_phi_set_xmap(int mask);
 /* logreg's G . Xd on the FmtH2 engine with 256 output columns (p <= 255):
  * phi_w1's one-wave-per-SIMD shape in 128 x 256 blocks (1; measured slower)
  * or the 8-wave 256-row NN tile (0, default).  A/B switch; returns the

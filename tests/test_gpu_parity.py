@@ -273,11 +273,11 @@ def test_direct_kernels_up_to_d64(n, d):
 
 
 @pytest.mark.parametrize("n,d,m,row0,xmap", [(4096, 256, 1024, 1024, 1), (16384, 96, 2048, 14336, 1),
-                                             (3000, 40, 1000, 1500, 1), (8192, 256, 2048, 4096, 2),
+                                             (3000, 40, 1000, 1500, 1), (8192, 256, 2048, 4096, 3),
                                              (8192, 256, 2048, 4096, 0)])
 def test_phi_row_block_split_k(n, d, m, row0, xmap):
     """A DistSampler rank's row block (non-symmetric D, split-K phi_mm); at
-    d = 256, m = 2048 the slices are mapped to XCDs (xmap 2) or not (0)."""
+    d = 256, m = 2048 the slices are mapped to XCDs (xmap mask 3) or not (0)."""
     from dsvgd import _native as N
     prev = N.load().dsvgd_phi_set_xmap(xmap)
     try:
