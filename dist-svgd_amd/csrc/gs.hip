@@ -299,11 +299,63 @@ __host__ __device__ inline int gsw_rows(int64_t dp, bool refreshed) {
 // D[i][r0 + j] = +inf for j < i < B (panel layout, row i of the block's D):
 // the pairs the walk takes with the moved rows
 __global__ void gs_mask_kernel(float* __restrict__ D, int64_t ldd, int64_t r0, int B) {
-  const int i = blockIdx.x, j = threadIdx.x;
-  if (j >= i || i >= B) return;
-  const int64_t col = r0 + j;
-  D[((int64_t)(i >> 7) * (ldd >> 4) + (col >> 4)) * kPanelElems + (i & 127) * 16 + (col & 15)] =
-      INFINITY;
+  const int i = blockIdx.x;
+  for (int j = threadIdx.x; j < i && i < B; j += blockDim.x) {
+    const int64_t col = r0 + j;
+    D[((int64_t)(i >> 7) * (ldd >> 4) + (col >> 4)) * kPanelElems + (i & 127) * 16 + (col & 15)] =
+        INFINITY;
+  }
+}
+
+// The grouped wide sweep's correction: the wide pass of a group of blocks
+// left every pair (i, j) with j < i inside the group out (dsvgd_gs_mask over
+// the group), so once a block has walked, the group's later rows [r0, r0 +
+// nr) (not moved yet) gain its pB rows [p0, p0 + pB) at their moved
+// positions: Q = [K Xc | K S] += k_ij (x_j' - c | s_j'), Qr += k_ij, k_ij =
+// exp(-|x_i - x_j'|^2 / h) by explicit differences (the walk's own form).
+// One workgroup per row i: wave w forms k_ij for j = w, w + 4, ... (lanes
+// over the features, a fixed butterfly), then thread t adds the j terms to
+// columns t, t + 256, ... in j order (deterministic).
+__global__ __launch_bounds__(256) void gsw_group_corr_kernel(
+    const float* __restrict__ X, int64_t ldx, const float* __restrict__ S, int64_t lds,
+    const float* __restrict__ center, int64_t d, int64_t dp, int64_t r0, int64_t p0, int pB,
+    const dsvgd_select_state* __restrict__ st, float* __restrict__ Q, int64_t ldq,
+    float* __restrict__ Qr) {
+  __shared__ float xi[kGswMaxD];
+  __shared__ float kv[kGsB];
+  const int i = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const float scale = -st->inv_h * kLog2e;
+  for (int64_t c = t; c < d; c += 256) xi[c] = X[(r0 + i) * ldx + c];
+  __syncthreads();
+  for (int j = w; j < pB; j += 4) {
+    const float* xj = X + (p0 + j) * ldx;
+    float a = 0.f;
+    for (int64_t c = lane; c < d; c += 64) {
+      const float df = xi[c] - xj[c];
+      a = fmaf(df, df, a);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    if (lane == 0) kv[j] = __builtin_amdgcn_exp2f(a * scale);
+  }
+  __syncthreads();
+  float* q = Q + (int64_t)i * ldq;
+  for (int64_t c = t; c < d; c += 256) {
+    const float cc = center[c];
+    float qx = 0.f, qs = 0.f;
+    for (int j = 0; j < pB; ++j) {
+      const float k = kv[j];
+      qx = fmaf(k, X[(p0 + j) * ldx + c] - cc, qx);
+      qs = fmaf(k, S[(p0 + j) * lds + c], qs);
+    }
+    q[c] += qx;
+    q[dp + c] += qs;
+  }
+  if (t == 0) {
+    float r = 0.f;
+    for (int j = 0; j < pB; ++j) r += kv[j];
+    Qr[i] += r;
+  }
 }
 
 // One workgroup of 256 threads walks rows [r0, r0 + B).  Q: [K Xc | K S] of
@@ -792,10 +844,26 @@ int64_t dsvgd_gsw_block_rows(int64_t d, int score_kind) {
 
 int dsvgd_gs_mask(float* D, int64_t ldd, int64_t r0, int64_t B, void* stream) {
   DSVGD_REQUIRE(D, "null pointer");
-  DSVGD_REQUIRE(B > 0 && B <= 128 && r0 >= 0 && r0 + B <= ldd && ldd % 128 == 0, "sizes");
-  hipLaunchKernelGGL(gs_mask_kernel, dim3((unsigned)B), dim3(128), 0, (hipStream_t)stream, D, ldd,
+  DSVGD_REQUIRE(B > 0 && B <= 1024 && r0 >= 0 && r0 + B <= ldd && ldd % 128 == 0, "sizes");
+  hipLaunchKernelGGL(gs_mask_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, D, ldd,
                      r0, (int)B);
   return check_launch("gs_mask");
+}
+
+int dsvgd_gsw_group_corr(const float* X, int64_t ldx, const float* S, int64_t lds,
+                         const float* center, int64_t n, int64_t d, int64_t r0, int64_t nr,
+                         int64_t p0, int64_t pB, const dsvgd_select_state* st, float* Q,
+                         int64_t ldq, float* Qr, void* stream) {
+  DSVGD_REQUIRE(X && S && center && st && Q && Qr, "null pointer");
+  const int64_t dp = roundup(d, 32);
+  DSVGD_REQUIRE(n > 0 && d > 0 && d <= kGswMaxD && ldx >= d && lds >= d && ldq >= 2 * dp,
+                "sizes (d <= 1024, ldq >= 2 roundup(d, 32))");
+  DSVGD_REQUIRE(nr > 0 && nr <= 65535 && r0 >= 0 && r0 + nr <= n && pB > 0 && pB <= kGsB &&
+                    p0 >= 0 && p0 + pB <= r0,
+                "rows: the later rows [r0, r0 + nr) after a block of at most 64 rows [p0, p0 + pB)");
+  hipLaunchKernelGGL(gsw_group_corr_kernel, dim3((unsigned)nr), dim3(256), 0, (hipStream_t)stream,
+                     X, ldx, S, lds, center, d, dp, r0, p0, (int)pB, st, Q, ldq, Qr);
+  return check_launch("gsw_group_corr");
 }
 
 int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y, int64_t ldy,

@@ -135,6 +135,8 @@ SIGNATURES = {
     "dsvgd_h2_rowsplit_rows_range": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _p, _p, _i64, _i64,
                                             _p]),
     "dsvgd_gs_mask": (_int, [_p, _i64, _i64, _i64, _p]),
+    "dsvgd_gsw_group_corr": (_int, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _i64,
+                                    _p, _p, _i64, _p, _p]),
     "dsvgd_gsw_block_sweep": (_int, [_p, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64,
                                      _p, _f, _p, _i64, _p, _p, _i64, _p, _i64, _int, _p, _p, _f,
                                      _p, _i64, _p, _i64, _p]),

@@ -998,10 +998,15 @@ class _WideSweep(object):
         self.ldy = lib.dsvgd_ldy(self.dp)
         # rows per block: the walk keeps x' and w (and, refreshed, s') in LDS
         self.B = int(lib.dsvgd_gsw_block_rows(d, kind))
+        # blocks per wide pass (GSW_GROUP): the group's rows in one pass, the
+        # earlier blocks' moved rows added after each walk (dsvgd_gsw_group_corr)
+        self.G = max(1, min(GSW_GROUP, 256 // self.B))
+        self.GB = self.G * self.B
+        gpad = -(-self.GB // 128) * 128
         self.Y = torch.zeros(self.n_pad + 128, self.ldy, **f32)
         self.norms = torch.zeros(self.n_pad + 128, **f32)
         self.mean = torch.empty(d, **f32)
-        self.D = torch.empty(128 * self.n_pad, **f32)
+        self.D = torch.empty(gpad * self.n_pad, **f32)
         split = gemm == "split"
         # phi_mm on FmtX3 (no scales: moved rows cannot leave a scale's window)
         self.phi_x3 = split and self.n_pad * self.ldy * 6 < (1 << 31)
@@ -1018,17 +1023,17 @@ class _WideSweep(object):
             self.rsc = torch.ones(self.n_pad + 128, **f32)
             self.Yg = torch.empty(lib.dsvgd_h2_image_bytes(self.gram_rows, self.dp) // 2,
                                   dtype=torch.int16, device=dev)
-        # split-K slices of the B-row wide pass: ldy / 512 column blocks per
-        # slice, so ~256 slices fill the CUs
-        cb = max(1, self.ldy // 512)
+        # split-K slices of the group's wide pass: ldy / 512 column blocks x
+        # 128-row tiles per slice, so ~256 blocks fill the CUs
+        cb = max(1, self.ldy // 512) * (gpad // 128)
         z = max(1, 256 // cb)
         while z > 1 and self.n_pad // z < 128:
             z //= 2
         self.splits = z
-        self.KY = torch.empty(z * self.B, self.ldy, **f32)
-        self.rowsum = torch.empty(z * 128, **f32)
-        self.Q = torch.empty(self.B, self.ldy, **f32)
-        self.Qr = torch.empty(128, **f32)
+        self.KY = torch.empty(z * self.GB, self.ldy, **f32)
+        self.rowsum = torch.empty(z * gpad, **f32)
+        self.Q = torch.empty(self.GB, self.ldy, **f32)
+        self.Qr = torch.empty(gpad, **f32)
 
     def images(self, r0, nr, s):
         """(Re)split rows [r0, r0 + nr) of Y into the engines' images (the
@@ -1052,6 +1057,8 @@ class _WideSweep(object):
 
 
 _WIDE = {}
+# blocks per wide pass of the wide Gauss-Seidel sweep (1: block after block)
+GSW_GROUP = 4
 
 
 def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s):
@@ -1062,7 +1069,7 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
     order (dsvgd_gsw_block_sweep) and the moved rows are re-split into the
     engines' images -- the same terms as the per-row path, in blocked order."""
     n, d = X.shape
-    key = (X.device, n, d, GSW_GEMM, kind != 0)
+    key = (X.device, n, d, GSW_GEMM, kind != 0, GSW_GROUP)
     W = _WIDE.get(key)
     if W is None:
         _WIDE.clear()
@@ -1076,35 +1083,45 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
     N.call("dsvgd_pack", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), 1.0, N.ptr(W.mean), n, d,
            W.Y.shape[0], N.ptr(W.Y), W.ldy, N.ptr(W.norms), s)
     W.images(0, W.n_pad, s)
-    B = W.B
-    for b0 in range(rows.start, rows.stop, B):
-        nb = min(B, rows.stop - b0)
-        k0 = b0 - rows.start
+    B, GB = W.B, W.GB
+    for g0 in range(rows.start, rows.stop, GB):
+        gn = min(GB, rows.stop - g0)
+        # the group's wide pass: every row against every row not moved before
+        # it, the group's own earlier pairs masked (the walks add the block's
+        # own, dsvgd_gsw_group_corr the earlier blocks' at their moved rows)
         if W.gram_h2:
-            N.call("dsvgd_sqdist_h2", N.ptr(W.Yg), N.ptr(W.norms), b0, nb, n, d, N.ptr(W.D),
+            N.call("dsvgd_sqdist_h2", N.ptr(W.Yg), N.ptr(W.norms), g0, gn, n, d, N.ptr(W.D),
                    W.n_pad, 0, None, None, 0, N.ptr(W.rsc), s)
         else:
-            N.call("dsvgd_sqdist", N.ptr(W.Y), W.ldy, N.ptr(W.norms), b0, nb, n, d, N.ptr(W.D),
+            N.call("dsvgd_sqdist", N.ptr(W.Y), W.ldy, N.ptr(W.norms), g0, gn, n, d, N.ptr(W.D),
                    W.n_pad, 0, None, None, s)
-        N.call("dsvgd_gs_mask", N.ptr(W.D), W.n_pad, b0, nb, s)
+        N.call("dsvgd_gs_mask", N.ptr(W.D), W.n_pad, g0, gn, s)
         if W.phi_x3:
-            N.call("dsvgd_phi_mm_x3", N.ptr(W.D), W.n_pad, N.ptr(W.Yx3), W.ldy, b0, nb, n,
+            N.call("dsvgd_phi_mm_x3", N.ptr(W.D), W.n_pad, N.ptr(W.Yx3), W.ldy, g0, gn, n,
                    h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), 0, int(W.m16),
                    None, s)
         else:
-            N.call("dsvgd_phi_mm", N.ptr(W.D), W.n_pad, N.ptr(W.Y), W.ldy, b0, nb, n,
+            N.call("dsvgd_phi_mm", N.ptr(W.D), W.n_pad, N.ptr(W.Y), W.ldy, g0, gn, n,
                    h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), s)
-        N.call("dsvgd_phi_partial_reduce", N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), W.splits, nb,
+        N.call("dsvgd_phi_partial_reduce", N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), W.splits, gn,
                2 * W.dp, N.ptr(W.Q), W.ldy, N.ptr(W.Qr), s)
-        ex = N.ptr(extra[k0:k0 + nb]) if extra is not None else None
-        po = N.ptr(phi_out[k0:k0 + nb]) if phi_out is not None else None
-        N.call("dsvgd_gsw_block_sweep", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), N.ptr(W.Y), W.ldy,
-               N.ptr(W.norms), N.ptr(W.mean), n, d, b0, nb, h_state.ptr, float(step), N.ptr(W.Q),
-               W.ldy, N.ptr(W.Qr), ex, d, po, N.ld(phi_out) if phi_out is not None else d, sk,
-               N.ptr(mu), N.ptr(lam), float(score_scale), N.ptr(xd),
-               N.ld(xd) if xd is not None else d, N.ptr(td), td.numel() if td is not None else 0,
-               s)
-        W.images(b0, nb, s)
+        for b0 in range(g0, g0 + gn, B):
+            nb = min(B, g0 + gn - b0)
+            k0, q0 = b0 - rows.start, b0 - g0
+            ex = N.ptr(extra[k0:k0 + nb]) if extra is not None else None
+            po = N.ptr(phi_out[k0:k0 + nb]) if phi_out is not None else None
+            N.call("dsvgd_gsw_block_sweep", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), N.ptr(W.Y),
+                   W.ldy, N.ptr(W.norms), N.ptr(W.mean), n, d, b0, nb, h_state.ptr, float(step),
+                   N.ptr(W.Q) + 4 * q0 * W.ldy, W.ldy, N.ptr(W.Qr) + 4 * q0, ex, d, po,
+                   N.ld(phi_out) if phi_out is not None else d, sk, N.ptr(mu), N.ptr(lam),
+                   float(score_scale), N.ptr(xd), N.ld(xd) if xd is not None else d, N.ptr(td),
+                   td.numel() if td is not None else 0, s)
+            W.images(b0, nb, s)
+            r1 = b0 + nb
+            if r1 < g0 + gn:   # the group's later rows gain this block at its moved rows
+                N.call("dsvgd_gsw_group_corr", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S),
+                       N.ptr(W.mean), n, d, r1, g0 + gn - r1, b0, nb, h_state.ptr,
+                       N.ptr(W.Q) + 4 * (r1 - g0) * W.ldy, W.ldy, N.ptr(W.Qr) + 4 * (r1 - g0), s)
 
 
 def _blocked_sweep(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s):

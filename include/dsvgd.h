@@ -397,6 +397,15 @@ int64_t dsvgd_gsw_block_rows(int64_t d, int score_kind);  /* 0 if d > 1024 */
  * the column loop.  Process-wide; returns the previous mask.  0 = normal. */
 int dsvgd_gsw_debug(int mask);
 int dsvgd_gs_mask(float* D, int64_t ldd, int64_t r0, int64_t B, void* stream);
+/* The grouped wide sweep (round 5): one wide pass for a group of blocks
+ * (dsvgd_gs_mask over the whole group, B <= 1024), then after each block's
+ * walk the group's later rows [r0, r0 + nr) gain that block's pB <= 64 moved
+ * rows [p0, p0 + pB): Q += k_ij (x_j' - c | s_j'), Qr += k_ij by explicit
+ * differences, j in order (Q, Qr: the later rows' first entries). */
+int dsvgd_gsw_group_corr(const float* X, int64_t ldx, const float* S, int64_t lds,
+                         const float* center, int64_t n, int64_t d, int64_t r0, int64_t nr,
+                         int64_t p0, int64_t pB, const dsvgd_select_state* st, float* Q,
+                         int64_t ldq, float* Qr, void* stream);
 int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y, int64_t ldy,
                           float* norms, const float* center, int64_t n, int64_t d, int64_t r0,
                           int64_t B, const dsvgd_select_state* st, float step, const float* Q,

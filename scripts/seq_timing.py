@@ -24,6 +24,9 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="D,E")
+    ap.add_argument("--group", default=None,
+                    help="comma list of engine.GSW_GROUP values: the blocked sweep alone "
+                         "timed for each (blocks per wide pass)")
     ap.add_argument("--rows-sample", type=int, default=2048,
                     help="rows of the per-row path to time (0: skip it)")
     args = ap.parse_args()
@@ -87,6 +90,29 @@ def main():
                           "per_row_ms_extrapolated": per_row_ms, "per_row_sample_rows": k,
                           "speedup_vs_per_row": per_row_ms / sweep_ms if per_row_ms else None}),
               flush=True)
+        if args.group:
+            import dsvgd.engine as E
+            res = {}
+            for gv in [int(v) for v in args.group.split(",")] * 2:
+                E.GSW_GROUP = gv
+                Xb, Sb = X.clone(), S0.clone()
+                sequential_sweep(Xb, Sb, range(0, 512), eng.state, 1e-4, target=tgt,
+                                 score_scale=scale)     # warm-up (buffers for this group)
+                Xb, Sb = X.clone(), S0.clone()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                sequential_sweep(Xb, Sb, range(n), eng.state, 1e-4, target=tgt, score_scale=scale)
+                torch.cuda.synchronize()
+                res.setdefault(gv, []).append(1e3 * (time.perf_counter() - t0))
+                res.setdefault("x_%d" % gv, Xb[::4096].cpu())
+            ref = res.pop("x_1", None)
+            out = {"config": name, "sweep_ms_by_group": {k: v for k, v in res.items()
+                                                         if not str(k).startswith("x_")}}
+            if ref is not None:
+                out["max_abs_diff_vs_group1"] = {k[2:]: float((v - ref).abs().max())
+                                                 for k, v in res.items() if str(k).startswith("x_")}
+            print(json.dumps(out), flush=True)
+            E.GSW_GROUP = 4
         del ds, eng
         torch.cuda.empty_cache()
 

@@ -380,12 +380,25 @@ def test_config_E_end_to_end_S8():
             eps * PHI_TOL * np.abs(ref).max() + 2 * np.spacing(np.abs(X1).astype(np.float32)).max()
 
 
-def test_sequential_wide_full_sweep_d256():
+@pytest.mark.parametrize("group", [4, 1])
+def test_sequential_wide_full_sweep_d256(group):
     """The reference's default Gauss-Seidel order at d > 64 (verdict r3 next
     #2): one full sweep of n = 16384 particles at d = 256 with frozen scores
-    (all_scores) through the wide blocked sweep (64-row blocks: an f32 MFMA
-    wide pass + a one-workgroup walk), every row against the fp64 sequential
-    restatement (O.sequential_sweep, pinned to the row-by-row loop on CPU)."""
+    (all_scores) through the wide blocked sweep (64-row blocks: a split-engine
+    wide pass per group of `group` blocks + a one-workgroup walk per block,
+    the group's earlier blocks added at their moved rows), every row against
+    the fp64 sequential restatement (O.sequential_sweep, pinned to the
+    row-by-row loop on CPU)."""
+    import dsvgd.engine as E
+    prev = E.GSW_GROUP
+    E.GSW_GROUP = group
+    try:
+        _wide_full_sweep_d256()
+    finally:
+        E.GSW_GROUP = prev
+
+
+def _wide_full_sweep_d256():
     from dsvgd import _native as N
     from dsvgd.engine import SelectState, sequential_sweep
     n, d, eps = 16384, 256, 1e-2
