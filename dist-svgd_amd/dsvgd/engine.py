@@ -1057,8 +1057,9 @@ class _WideSweep(object):
 
 
 _WIDE = {}
-# blocks per wide pass of the wide Gauss-Seidel sweep (1: block after block)
-GSW_GROUP = 4
+# blocks per wide pass of the wide Gauss-Seidel sweep (1: block after block;
+# config D sweep 278.7 / 253.0 / 256.2 ms at 1 / 2 / 4, profiles/r13u)
+GSW_GROUP = 2
 
 
 def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s):

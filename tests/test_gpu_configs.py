@@ -380,7 +380,7 @@ def test_config_E_end_to_end_S8():
             eps * PHI_TOL * np.abs(ref).max() + 2 * np.spacing(np.abs(X1).astype(np.float32)).max()
 
 
-@pytest.mark.parametrize("group", [4, 1])
+@pytest.mark.parametrize("group", [2, 4, 1])
 def test_sequential_wide_full_sweep_d256(group):
     """The reference's default Gauss-Seidel order at d > 64 (verdict r3 next
     #2): one full sweep of n = 16384 particles at d = 256 with frozen scores
