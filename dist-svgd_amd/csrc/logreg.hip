@@ -50,7 +50,7 @@ static int64_t nn_cols(int64_t w) {
 struct LogregWs {
   int64_t N, n_pad, N_pad, pp, ldb;
   size_t off_w, off_xd, off_t, off_g, off_gw, off_wx, off_xdx, off_xdy, off_rsw, off_riw, off_sxd,
-      off_sws, total;
+      off_sws, off_xdp, total;
 };
 
 // G . Xd (K = N data rows, 256-row blocks): split K so that a launch has
@@ -62,6 +62,9 @@ static int gxd_splits(int64_t n_pad, int64_t N_pad) {
   while (sp < kGxdMaxSplits && (n_pad / 256) * sp < 512 && N_pad / (2 * sp) >= 1024) sp *= 2;
   return sp;
 }
+
+// the FmtH2 score as one fused kernel (1) or Z + G . Xd (0); dsvgd_logreg_set_fused
+static int g_logreg_fused = 0;
 
 static LogregWs logreg_ws(int64_t n, int64_t N, int64_t p) {
   LogregWs w;
@@ -91,6 +94,8 @@ static LogregWs logreg_ws(int64_t n, int64_t N, int64_t p) {
   w.off_riw = take((size_t)w.n_pad);
   w.off_sxd = take((size_t)(2 * w.ldb + 3));
   w.off_sws = take(h2_colscale_ws_floats(w.N_pad, w.ldb));
+  // the fused score's column image of Xd, K order permuted (FmtH2, 4 B per entry)
+  w.off_xdp = take((size_t)w.N_pad * w.ldb);
   w.total = o;
   return w;
 }
@@ -273,6 +278,172 @@ __global__ __launch_bounds__(512, 1) void logreg_z_x3p_kernel(
     }
     ks = ksn;
     stage ^= 1;
+  }
+}
+
+// ---- the fused score (round 5): Z, sigma and G . Xd in one kernel ---------
+// Per block 128 particles (4 waves x 32); per wave the 32 particles' W image
+// fragments stay in registers (the B operand of Z^T = Xd W^T, 16 K-steps x
+// 2 parts at p <= 255) and their 32 x 256 G . Xd accumulators in AGPRs.  The
+// data go by in chunks of 32 rows, DMA'd to LDS one chunk ahead: the chunk's
+// row image (Z^T's A operand, shared by the 4 waves) and its 2 K-steps of
+// Xd's column image.  Z^T's C layout puts particle r in lane r & 31 and the
+// data rows 4h + 8g + e (g < 4, e < 4) in its registers: those 16 values,
+// sigma'd and split, ARE the A fragments of G . Xd for two 16-deep K-steps
+// when the column image stores each K-step's rows in the order
+// kFusedPerm (position 8h + j <-> row 4h + 8 (j >> 2) + (j & 3)) -- no G
+// in memory, no transpose.  G . Xd of chunk c - 1 runs beside Z of chunk c.
+__host__ __device__ constexpr int fused_perm(int p) { return 4 * (p >> 3) + 8 * ((p & 7) >> 2) + (p & 3); }
+
+// Yp[kstep][part][column][16 k]: ysplit_h2_kernel's image with position k of
+// each 16-row K-step holding row fused_perm(k)
+__global__ __launch_bounds__(256) void ysplit_h2_perm_kernel(const float* __restrict__ Y,
+                                                             int64_t ldy, int64_t ksteps,
+                                                             const float* __restrict__ colscale,
+                                                             _Float16* __restrict__ Yh) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= ksteps * ldy) return;
+  const int64_t kb = t / ldy, c = t % ldy;
+  const float sc = colscale[c];
+  f16x8 sp[2][2];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    _Float16 v[2];
+    split_fmt<FmtH2>(sc * Y[(kb * 16 + fused_perm(k)) * ldy + c], v);
+    sp[0][k >> 3][k & 7] = v[0];
+    sp[1][k >> 3][k & 7] = v[1];
+  }
+  const int sw = (int)((c >> 3) & 1);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    _Float16* dst = Yh + ((kb * 2 + p) * ldy + c) * 16;
+    *reinterpret_cast<f16x8*>(dst + 8 * sw) = sp[p][0];
+    *reinterpret_cast<f16x8*>(dst + 8 * (sw ^ 1)) = sp[p][1];
+  }
+}
+
+constexpr int kFusedRows = 128;   // particles per block
+constexpr int kFusedChunk = 32;   // data rows per chunk
+constexpr int kFusedKD = 16;      // K-steps over the weights (p <= 255)
+constexpr int kFusedCols = 256;   // G . Xd columns (ldb)
+constexpr int kFusedXdx = kFusedKD * 2 * kFusedChunk * 32;   // a chunk's row image (32 KiB)
+constexpr int kFusedXdp = 2 * 2 * kFusedCols * 32;           // its 2 K-steps of column image
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void logreg_fused_kernel(
+    const _Float16* __restrict__ Wx, int64_t n_img, const _Float16* __restrict__ Xdx,
+    int64_t N_img, const _Float16* __restrict__ Xdp, int nchunks,
+    const float* __restrict__ xinv, const float* __restrict__ rinv,
+    const float* __restrict__ colinv, float* __restrict__ GW, int64_t ldg, int64_t n) {
+  using V8 = FmtH2::V8;
+  __shared__ __attribute__((aligned(16))) char smem[2 * kFusedXdx + 2 * kFusedXdp];
+  char* const abuf = smem;                       // row image ring (chunk c in abuf[c & 1])
+  char* const xbuf = smem + 2 * kFusedXdx;       // column image ring (chunk c in xbuf[c & 1])
+  const int t = threadIdx.x, lane = t & 63, r = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int64_t p0 = (int64_t)blockIdx.x * kFusedRows + w * 32;
+  const __amdgpu_buffer_rsrc_t rW =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Wx, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rX =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Xdx, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rP =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Xdp, (short)0, 0x7fffffff, 0x00020000);
+  // the wave's W fragments: K-step k, part p -> lane (r, h): particle p0 + r
+  V8 wf[kFusedKD][2];
+#pragma unroll
+  for (int k = 0; k < kFusedKD; ++k)
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      wf[k][p] = __builtin_bit_cast(
+          V8, __builtin_amdgcn_raw_buffer_load_b128(
+                  rW, (int)(((int64_t)(k * 2 + p) * n_img) * 32 + x3_off((int)(p0 + r), h)), 0, 0));
+  const float zsc = kLog2e * (*xinv) * rinv[p0 + r];   // z = acc / (t_x s_i)
+  // LDS-DMA of chunk c's row image (into abuf[c & 1]) and column image (xbuf[c & 1]):
+  // 16-byte units u * 256 + t, wave-uniform LDS bases
+  auto dma_rows = [&](int c) {
+    char* dst = abuf + (c & 1) * kFusedXdx;
+    const int soff = c * kFusedChunk * 32;
+#pragma unroll
+    for (int u = 0; u < kFusedXdx / 4096; ++u) {
+      const int e = u * 256 + t, kp = e >> 6, within = e & 63;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rX, (__attribute__((address_space(3))) void*)(dst + (u * 256 + w * 64) * 16), 16,
+          (int)((int64_t)kp * N_img * 32 + within * 16), soff, 0, 0);
+    }
+  };
+  auto dma_cols = [&](int c) {
+    char* dst = xbuf + (c & 1) * kFusedXdp;
+    const int soff = c * kFusedXdp;
+#pragma unroll
+    for (int u = 0; u < kFusedXdp / 4096; ++u) {
+      const int e = u * 256 + t;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rP, (__attribute__((address_space(3))) void*)(dst + (u * 256 + w * 64) * 16), 16,
+          e * 16, soff, 0, 0);
+    }
+  };
+  auto barrier_dma = []() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  f32x16 acc[kFusedCols / 32];
+#pragma unroll
+  for (int ni = 0; ni < kFusedCols / 32; ++ni)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[ni][q] = 0.f;
+  V8 g[2][2];   // G of the previous chunk: K-step kk (data rows 16 kk ..), part
+  // G . Xd of the chunk whose G is in g, column image in xb
+  auto gxd = [&](const char* xb) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int ni = 0; ni < kFusedCols / 32; ++ni) {
+        const V8 bh = *reinterpret_cast<const V8*>(xb + (kk * 2 + 0) * kFusedCols * 32 + x3_off(ni * 32 + r, h));
+        const V8 bl = *reinterpret_cast<const V8*>(xb + (kk * 2 + 1) * kFusedCols * 32 + x3_off(ni * 32 + r, h));
+        acc[ni] = mfma_fmt<FmtH2>(g[kk][1], bh, acc[ni]);   // small terms first
+        acc[ni] = mfma_fmt<FmtH2>(g[kk][0], bl, acc[ni]);
+        acc[ni] = mfma_fmt<FmtH2>(g[kk][0], bh, acc[ni]);
+      }
+  };
+  dma_rows(0);
+  barrier_dma();
+  for (int c = 0; c < nchunks; ++c) {
+    if (c + 1 < nchunks) dma_rows(c + 1);
+    dma_cols(c);
+    // Z^T of chunk c (data rows x the wave's particles), two chains
+    const char* ab = abuf + (c & 1) * kFusedXdx;
+    f32x16 z0 = {}, z1 = {};
+#pragma unroll
+    for (int k = 0; k < kFusedKD; ++k) {
+      const V8 ah = *reinterpret_cast<const V8*>(ab + (k * 2 + 0) * kFusedChunk * 32 + x3_off(r, h));
+      const V8 al = *reinterpret_cast<const V8*>(ab + (k * 2 + 1) * kFusedChunk * 32 + x3_off(r, h));
+      f32x16& z = (k & 1) ? z1 : z0;
+      z = mfma_fmt<FmtH2>(al, wf[k][0], z);
+      z = mfma_fmt<FmtH2>(ah, wf[k][1], z);
+      z = mfma_fmt<FmtH2>(ah, wf[k][0], z);
+    }
+    // G . Xd of chunk c - 1 beside it
+    if (c > 0) gxd(xbuf + ((c - 1) & 1) * kFusedXdp);
+    // sigma(-z) -> the A fragments of chunk c's two K-steps (2^15 G, split)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float zz = (z0[q] + z1[q]) * zsc;
+      const float gv = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(zz)) * FmtH2::kAScale;
+      const _Float16 hi = (_Float16)gv;
+      g[q >> 3][0][q & 7] = hi;
+      g[q >> 3][1][q & 7] = (_Float16)(gv - (float)hi);
+    }
+    barrier_dma();
+  }
+  gxd(xbuf + ((nchunks - 1) & 1) * kFusedXdp);
+  // GW[i][c] = acc 2^-15 / s_c
+#pragma unroll
+  for (int ni = 0; ni < kFusedCols / 32; ++ni) {
+    const int col = ni * 32 + r;
+    const float cs = colinv[col] * (1.f / FmtH2::kAScale);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t i = p0 + c_row(q, lane);
+      if (i < n) GW[i * ldg + col] = acc[ni][q] * cs;
+    }
   }
 }
 
@@ -469,6 +640,12 @@ using namespace dsvgd;
 
 extern "C" {
 
+int dsvgd_logreg_set_fused(int on) {
+  const int prev = g_logreg_fused;
+  g_logreg_fused = on ? 1 : 0;
+  return prev;
+}
+
 size_t dsvgd_logreg_workspace_bytes(int64_t n, int64_t N, int64_t p) {
   return logreg_ws(n, N, p).total;
 }
@@ -528,7 +705,12 @@ static int logreg_prepare(const float* Xd, int64_t ldxd, const float* t, int64_t
     if ((rc = h2_rowsplit(Xdp, w.ldb, w.N_pad, w.pp, w.N_pad, w.pp, sxd + 2 * w.ldb,
                           P.base + w.off_xdx, s)))
       return rc;
-    return h2_ysplit(Xdp, w.ldb, w.N_pad, sxd, (_Float16*)(P.base + w.off_xdy), s);
+    if ((rc = h2_ysplit(Xdp, w.ldb, w.N_pad, sxd, (_Float16*)(P.base + w.off_xdy), s))) return rc;
+    // the fused score's column image: the same split, K order permuted
+    const int64_t th = (w.N_pad / 16) * w.ldb;
+    hipLaunchKernelGGL(ysplit_h2_perm_kernel, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, Xdp,
+                       w.ldb, w.N_pad / 16, sxd, (_Float16*)(P.base + w.off_xdp));
+    return check_launch("ysplit_h2_perm");
   }
   if (P.x3) {
     // the persistent 16x16x32 Z form reads unswizzled images
@@ -558,6 +740,18 @@ static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float 
     // W = X[:, 1:] in place, one power-of-two scale per particle row: scale
     // and image in one pass (rowimage_h2_kernel)
     if ((rc = h2_rowimage(X + 1, ldx, n, p, w.n_pad, w.pp, rsw, riw, Wx, s))) return rc;
+    if (g_logreg_fused && w.pp == kFusedKD * 16 && w.ldb == kFusedCols &&
+        w.N_pad % kFusedChunk == 0 && w.n_pad % kFusedRows == 0) {
+      hipLaunchKernelGGL(logreg_fused_kernel, dim3((unsigned)(w.n_pad / kFusedRows)), dim3(256), 0,
+                         s, (const _Float16*)Wx, w.n_pad, (const _Float16*)(base + w.off_xdx),
+                         w.N_pad, (const _Float16*)(base + w.off_xdp),
+                         (int)(w.N_pad / kFusedChunk), (const float*)(sxd + 2 * w.ldb + 1),
+                         (const float*)riw, (const float*)(sxd + w.ldb), GW, w.ldb, n);
+      if ((rc = check_launch("logreg_fused"))) return rc;
+      hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,
+                         w.ldb, scale, S, lds, 1);
+      return check_launch("logreg_finish");
+    }
     int blocks = 0;
     if ((rc = persistent_blocks(reinterpret_cast<const void*>(&logreg_z_x3p_kernel<FmtH2>),
                                 &blocks, 512)))

@@ -1,6 +1,8 @@
 """logreg scores at the headline (n = 65536, p = 255, N = 16384, and the S = 8
-shard N = 2048): G . Xd on phi_w1_kernel<0, 2, false> (dsvgd_phi_set_gxd_w1(1))
-against the 8-wave 256-row NN tile (0), alternating, HIP events."""
+shard N = 2048), an A/B switch on (1) and off (0), alternating, HIP events:
+--switch dsvgd_phi_set_gxd_w1 (G . Xd on phi_w1_kernel<0, 2, false>) or
+dsvgd_logreg_set_fused (the fused score kernel)."""
+import argparse
 import json
 import os
 import sys
@@ -14,6 +16,9 @@ import torch  # noqa: E402
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--switch", default="dsvgd_phi_set_gxd_w1")
+    args = ap.parse_args()
     import dsvgd
     from dsvgd import _native as N
     from bench import synthetic_data
@@ -27,7 +32,7 @@ def main():
         tgt = dsvgd.targets.LogisticRegression(x, t)
         S = {}
         for mode in (1, 0):
-            lib.dsvgd_phi_set_gxd_w1(mode)
+            getattr(lib, args.switch)(mode)
             Sx = torch.empty_like(X)
             tgt.score(X, Sx)
             S[mode] = Sx
@@ -35,7 +40,7 @@ def main():
         res = {1: [], 0: []}
         for _ in range(3):
             for mode in (1, 0):
-                lib.dsvgd_phi_set_gxd_w1(mode)
+                getattr(lib, args.switch)(mode)
                 Sx = torch.empty_like(X)
                 tgt.score(X, Sx)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -47,8 +52,8 @@ def main():
                 res[mode].append(e0.elapsed_time(e1) / 5)
         out[Ng] = {"w1_ms": res[1], "nn_ms": res[0], "mean_w1": float(np.mean(res[1])),
                    "mean_nn": float(np.mean(res[0])), "scores_rel_diff": rel}
-    lib.dsvgd_phi_set_gxd_w1(1)
-    print(json.dumps(out), flush=True)
+    getattr(lib, args.switch)(0)
+    print(json.dumps({"switch": args.switch, "by_N": out}), flush=True)
 
 
 if __name__ == "__main__":

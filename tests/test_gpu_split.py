@@ -481,3 +481,41 @@ def test_rowimage_equals_rowscale_then_rowsplit(n, p, off):
     for a, b in zip(*out):
         assert np.array_equal(a.view(np.uint32) if a.dtype == np.float32 else a,
                               b.view(np.uint32) if b.dtype == np.float32 else b)
+
+
+@pytest.mark.parametrize("n,N,labels", [(512, 16384, "pm1"), (1000, 1000, "pm1"), (4096, 8192, "general"),
+                                        (300, 129, "general"), (65536, 2048, "pm1")])
+def test_logreg_scores_fused(n, N, labels):
+    """The fused FmtH2 score (dsvgd_logreg_set_fused: Z, sigma and G . Xd in
+    one kernel, G in registers, the column image K-permuted) at p = 255
+    against fp64 and next to the two-GEMM path on the same inputs: particle
+    and data counts off the tiles (padding rows on both sides), +-1 and
+    general labels."""
+    from dsvgd import _native as N_
+    p = 255
+    rs = np.random.RandomState(n + 3 * N)
+    X = (rs.randn(n, p + 1) * 0.4).astype(np.float32)
+    xd = (rs.randn(N, p) / np.sqrt(p)).astype(np.float32)
+    t = (np.where(rs.randn(N) > 0, 1.0, -1.0) if labels == "pm1"
+         else rs.uniform(-3.0, 3.0, N)).astype(np.float32)
+    lib = N_.load()
+    out = {}
+    for fused in (1, 0):
+        prev = lib.dsvgd_logreg_set_fused(fused)
+        try:
+            o = torch.zeros(n, p + 1, device=DEV)
+            dsvgd().targets.LogisticRegression(xd, t, gemm="h2").score(gpu(X), o)
+            torch.cuda.synchronize()
+            out[fused] = o.cpu().numpy()
+        finally:
+            lib.dsvgd_logreg_set_fused(prev)
+    scale = None
+    if n * N <= 2 ** 27:
+        ref = O.score_logreg(X, xd, t)
+        scale = np.abs(ref).max()
+        e_f = float(np.abs(out[1] - ref).max() / scale)
+        e_2 = float(np.abs(out[0] - ref).max() / scale)
+        record_parity(e_f, two_gemm=e_2)
+        assert e_f < 1e-5 and e_f <= 2.0 * e_2 + 1e-7, (e_f, e_2)
+    d = float(np.abs(out[1] - out[0]).max() / np.abs(out[0]).max())
+    assert d < 2e-6, d
