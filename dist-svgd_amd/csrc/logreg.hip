@@ -403,26 +403,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         acc[ni] = mfma_fmt<FmtH2>(g[kk][0], bh, acc[ni]);
       }
   };
-  dma_rows(0);
-  barrier_dma();
-  for (int c = 0; c < nchunks; ++c) {
-    if (c + 1 < nchunks) dma_rows(c + 1);
+  // chunk c: the next chunk's rows and this chunk's columns DMA'd, Z^T of
+  // chunk c (two chains), G . Xd of chunk c - 1 beside it, then sigma(-z)
+  // into the A fragments of chunk c's two K-steps (2^15 G, split).  The
+  // first and last chunks are peeled so that the steady body is one basic
+  // block (the scheduler interleaves the two GEMMs only inside one)
+  auto chunk = [&](int c, auto NEXT_, auto PREV_) {
+    constexpr bool PREV = decltype(PREV_)::value;
+    if constexpr (decltype(NEXT_)::value) dma_rows(c + 1);
     dma_cols(c);
-    // Z^T of chunk c (data rows x the wave's particles), two chains
     const char* ab = abuf + (c & 1) * kFusedXdx;
+    const char* xp = xbuf + ((c - 1) & 1) * kFusedXdp;
+    // step s: Z^T's K-step s (A: the chunk's row image) and, beside it, G .
+    // Xd's (K-step s >> 3, column block s & 7) of chunk c - 1; the LDS
+    // fragments of step s + 1 are read while step s's MFMAs run
+    V8 fa[2][2], fb[2][2];
+    auto rd = [&](int st, int bi) {
+      fa[bi][0] = *reinterpret_cast<const V8*>(ab + (st * 2 + 0) * kFusedChunk * 32 + x3_off(r, h));
+      fa[bi][1] = *reinterpret_cast<const V8*>(ab + (st * 2 + 1) * kFusedChunk * 32 + x3_off(r, h));
+      if constexpr (PREV) {
+        const int kk = st >> 3, ni = st & 7;
+        fb[bi][0] = *reinterpret_cast<const V8*>(xp + (kk * 2 + 0) * kFusedCols * 32 + x3_off(ni * 32 + r, h));
+        fb[bi][1] = *reinterpret_cast<const V8*>(xp + (kk * 2 + 1) * kFusedCols * 32 + x3_off(ni * 32 + r, h));
+      }
+    };
     f32x16 z0 = {}, z1 = {};
+    rd(0, 0);
 #pragma unroll
-    for (int k = 0; k < kFusedKD; ++k) {
-      const V8 ah = *reinterpret_cast<const V8*>(ab + (k * 2 + 0) * kFusedChunk * 32 + x3_off(r, h));
-      const V8 al = *reinterpret_cast<const V8*>(ab + (k * 2 + 1) * kFusedChunk * 32 + x3_off(r, h));
-      f32x16& z = (k & 1) ? z1 : z0;
-      z = mfma_fmt<FmtH2>(al, wf[k][0], z);
-      z = mfma_fmt<FmtH2>(ah, wf[k][1], z);
-      z = mfma_fmt<FmtH2>(ah, wf[k][0], z);
+    for (int st = 0; st < kFusedKD; ++st) {
+      if (st + 1 < kFusedKD) rd(st + 1, (st + 1) & 1);
+      const V8 ah = fa[st & 1][0], al = fa[st & 1][1];
+      f32x16& z = (st & 1) ? z1 : z0;
+      z = mfma_fmt<FmtH2>(al, wf[st][0], z);
+      z = mfma_fmt<FmtH2>(ah, wf[st][1], z);
+      z = mfma_fmt<FmtH2>(ah, wf[st][0], z);
+      if constexpr (PREV) {
+        const int kk = st >> 3, ni = st & 7;
+        const V8 bh = fb[st & 1][0], bl = fb[st & 1][1];
+        acc[ni] = mfma_fmt<FmtH2>(g[kk][1], bh, acc[ni]);   // small terms first
+        acc[ni] = mfma_fmt<FmtH2>(g[kk][0], bl, acc[ni]);
+        acc[ni] = mfma_fmt<FmtH2>(g[kk][0], bh, acc[ni]);
+      }
     }
-    // G . Xd of chunk c - 1 beside it
-    if (c > 0) gxd(xbuf + ((c - 1) & 1) * kFusedXdp);
-    // sigma(-z) -> the A fragments of chunk c's two K-steps (2^15 G, split)
+    // order: the first step's reads, then per step the next step's reads
+    // ahead of this step's MFMAs (each read has a step of MFMAs to land)
+    __builtin_amdgcn_sched_group_barrier(0x100, PREV ? 4 : 2, 0);
+#pragma unroll
+    for (int st = 0; st < kFusedKD; ++st) {
+      if (st + 1 < kFusedKD) __builtin_amdgcn_sched_group_barrier(0x100, PREV ? 4 : 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, PREV ? 6 : 3, 0);
+    }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const float zz = (z0[q] + z1[q]) * zsc;
@@ -432,7 +462,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       g[q >> 3][1][q & 7] = (_Float16)(gv - (float)hi);
     }
     barrier_dma();
-  }
+  };
+  constexpr std::true_type yes{};
+  constexpr std::false_type no{};
+  dma_rows(0);
+  barrier_dma();
+  chunk(0, yes, no);                       // nchunks >= 2 (checked by the host)
+  for (int c = 1; c + 1 < nchunks; ++c) chunk(c, yes, yes);
+  chunk(nchunks - 1, no, yes);
   gxd(xbuf + ((nchunks - 1) & 1) * kFusedXdp);
   // GW[i][c] = acc 2^-15 / s_c
 #pragma unroll
@@ -741,7 +778,7 @@ static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float 
     // and image in one pass (rowimage_h2_kernel)
     if ((rc = h2_rowimage(X + 1, ldx, n, p, w.n_pad, w.pp, rsw, riw, Wx, s))) return rc;
     if (g_logreg_fused && w.pp == kFusedKD * 16 && w.ldb == kFusedCols &&
-        w.N_pad % kFusedChunk == 0 && w.n_pad % kFusedRows == 0) {
+        w.N_pad % kFusedChunk == 0 && w.N_pad >= 2 * kFusedChunk && w.n_pad % kFusedRows == 0) {
       hipLaunchKernelGGL(logreg_fused_kernel, dim3((unsigned)(w.n_pad / kFusedRows)), dim3(256), 0,
                          s, (const _Float16*)Wx, w.n_pad, (const _Float16*)(base + w.off_xdx),
                          w.N_pad, (const _Float16*)(base + w.off_xdp),

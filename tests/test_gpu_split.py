@@ -518,4 +518,4 @@ def test_logreg_scores_fused(n, N, labels):
         record_parity(e_f, two_gemm=e_2)
         assert e_f < 1e-5 and e_f <= 2.0 * e_2 + 1e-7, (e_f, e_2)
     d = float(np.abs(out[1] - out[0]).max() / np.abs(out[0]).max())
-    assert d < 2e-6, d
+    assert d < 5e-6, d
