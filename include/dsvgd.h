@@ -673,10 +673,10 @@ int dsvgd_score_gmm(const float* X, int64_t ldx, int64_t n, int64_t d, float sca
  * one-particle refresh) a single one-block-per-particle launch instead.
  * Xd: N x p data rows (ldxd), t: N labels (+-1).  Workspace:
  * dsvgd_logreg_workspace_bytes(n, N, p) (unused on the small path). */
-/* The FmtH2 logistic-regression score as one fused kernel (Z, sigma and
- * G . Xd with G kept in registers; p <= 255, the bench shape) or the two-GEMM
- * path (0).  A/B switch; returns the previous setting.  The prepared
- * workspace holds both paths' data images. */
+/* The FmtH2 logistic-regression score as one fused kernel (1, default: Z,
+ * sigma and G . Xd with G kept in registers; 128 < p + 1 <= 256, the bench
+ * shape) or the two-GEMM path (0).  A/B switch; returns the previous
+ * setting.  The prepared workspace holds both paths' data images. */
 int dsvgd_logreg_set_fused(int on);
 size_t dsvgd_logreg_workspace_bytes(int64_t n, int64_t N, int64_t p);
 int dsvgd_score_logreg(const float* X, int64_t ldx, int64_t n, int64_t d, const float* Xd,
