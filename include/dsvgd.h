@@ -674,8 +674,8 @@ int dsvgd_score_gmm(const float* X, int64_t ldx, int64_t n, int64_t d, float sca
  * Xd: N x p data rows (ldxd), t: N labels (+-1).  Workspace:
  * dsvgd_logreg_workspace_bytes(n, N, p) (unused on the small path). */
 /* The FmtH2 logistic-regression score as one fused kernel (1, default: Z,
- * sigma and G . Xd with G kept in registers; 128 < p + 1 <= 256, the bench
- * shape) or the two-GEMM path (0).  A/B switch; returns the previous
+ * sigma and G . Xd with G kept in registers; 224 < p <= 256 weights, the
+ * bench's p = 255) or the two-GEMM path (0).  A/B switch; returns the previous
  * setting.  The prepared workspace holds both paths' data images. */
 int dsvgd_logreg_set_fused(int on);
 size_t dsvgd_logreg_workspace_bytes(int64_t n, int64_t N, int64_t p);
