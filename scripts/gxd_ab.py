@@ -18,6 +18,8 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--switch", default="dsvgd_phi_set_gxd_w1")
+    ap.add_argument("--on", type=int, default=1, help="the switch value compared with --off")
+    ap.add_argument("--off", type=int, default=0)
     args = ap.parse_args()
     import dsvgd
     from dsvgd import _native as N
@@ -32,7 +34,7 @@ def main():
         tgt = dsvgd.targets.LogisticRegression(x, t)
         S = {}
         for mode in (1, 0):
-            getattr(lib, args.switch)(mode)
+            getattr(lib, args.switch)(args.on if mode else args.off)
             Sx = torch.empty_like(X)
             tgt.score(X, Sx)
             S[mode] = Sx
@@ -40,7 +42,7 @@ def main():
         res = {1: [], 0: []}
         for _ in range(3):
             for mode in (1, 0):
-                getattr(lib, args.switch)(mode)
+                getattr(lib, args.switch)(args.on if mode else args.off)
                 Sx = torch.empty_like(X)
                 tgt.score(X, Sx)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -52,7 +54,7 @@ def main():
                 res[mode].append(e0.elapsed_time(e1) / 5)
         out[Ng] = {"w1_ms": res[1], "nn_ms": res[0], "mean_w1": float(np.mean(res[1])),
                    "mean_nn": float(np.mean(res[0])), "scores_rel_diff": rel}
-    getattr(lib, args.switch)(0)
+    getattr(lib, args.switch)(args.off)
     print(json.dumps({"switch": args.switch, "by_N": out}), flush=True)
 
 
