@@ -331,10 +331,6 @@ constexpr int kFusedCols = 256;   // G . Xd columns (ldb)
 constexpr int kFusedXdx = kFusedKD * 2 * kFusedChunk * 32;   // a chunk's row image (32 KiB)
 constexpr int kFusedXdp = 2 * 2 * kFusedCols * 32;           // its 2 K-steps of column image
 
-// V = 2: sigma of chunk c - 1 in the first half of chunk c's steps (beside
-// Z^T's MFMAs), its G . Xd in the second half -- nothing but MFMAs' VALU
-// neighbours between the chunks
-template <int V = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void logreg_fused_kernel(
     const _Float16* __restrict__ Wx, int64_t n_img, const _Float16* __restrict__ Xdx,
     int64_t N_img, const _Float16* __restrict__ Xdp, int nchunks,
@@ -469,91 +465,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     barrier_dma();
   };
-  float zc[16];   // V = 2: the previous chunk's z (summed chains), sigma pending
-  auto sig = [&](int q) {
-    const float gv = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(zc[q] * zsc)) * FmtH2::kAScale;
-    const _Float16 hi = (_Float16)gv;
-    g[q >> 3][0][q & 7] = hi;
-    g[q >> 3][1][q & 7] = (_Float16)(gv - (float)hi);
-  };
-  auto chunk2 = [&](int c, auto NEXT_, auto PREV_) {
-    constexpr bool PREV = decltype(PREV_)::value;
-    if constexpr (decltype(NEXT_)::value) dma_rows(c + 1);
-    dma_cols(c);
-    const char* ab = abuf + (c & 1) * kFusedXdx;
-    const char* xp = xbuf + ((c - 1) & 1) * kFusedXdp;
-    V8 fa[2][2], fb[2][2][2];
-    auto rd = [&](int st, int bi) {
-      fa[bi][0] = *reinterpret_cast<const V8*>(ab + (st * 2 + 0) * kFusedChunk * 32 + x3_off(r, h));
-      fa[bi][1] = *reinterpret_cast<const V8*>(ab + (st * 2 + 1) * kFusedChunk * 32 + x3_off(r, h));
-      if (PREV && st >= 8) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int pr = 2 * (st - 8) + u, kk = pr >> 3, ni = pr & 7;
-          fb[bi][u][0] = *reinterpret_cast<const V8*>(xp + (kk * 2 + 0) * kFusedCols * 32 + x3_off(ni * 32 + r, h));
-          fb[bi][u][1] = *reinterpret_cast<const V8*>(xp + (kk * 2 + 1) * kFusedCols * 32 + x3_off(ni * 32 + r, h));
-        }
-      }
-    };
-    f32x16 z0 = {}, z1 = {};
-    rd(0, 0);
-#pragma unroll
-    for (int st = 0; st < kFusedKD; ++st) {
-      if (st + 1 < kFusedKD) rd(st + 1, (st + 1) & 1);
-      const V8 ah = fa[st & 1][0], al = fa[st & 1][1];
-      f32x16& z = (st & 1) ? z1 : z0;
-      z = mfma_fmt<FmtH2>(al, wf[st][0], z);
-      z = mfma_fmt<FmtH2>(ah, wf[st][1], z);
-      z = mfma_fmt<FmtH2>(ah, wf[st][0], z);
-      if (PREV && st < 8) {
-        sig(2 * st);
-        sig(2 * st + 1);
-      }
-      if (PREV && st >= 8) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int pr = 2 * (st - 8) + u, kk = pr >> 3, ni = pr & 7;
-          const V8 bh = fb[st & 1][u][0], bl = fb[st & 1][u][1];
-          acc[ni] = mfma_fmt<FmtH2>(g[kk][1], bh, acc[ni]);
-          acc[ni] = mfma_fmt<FmtH2>(g[kk][0], bl, acc[ni]);
-          acc[ni] = mfma_fmt<FmtH2>(g[kk][0], bh, acc[ni]);
-        }
-      }
-    }
-    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-#pragma unroll
-    for (int st = 0; st < kFusedKD; ++st) {
-      if (st + 1 < kFusedKD) {
-        if (PREV && st + 1 >= 8)
-          __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
-        else
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      }
-      if (PREV && st >= 8)
-        __builtin_amdgcn_sched_group_barrier(0x008, 9, 0);
-      else
-        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-      if (PREV && st < 8) __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
-    }
-#pragma unroll
-    for (int q = 0; q < 16; ++q) zc[q] = z0[q] + z1[q];
-    barrier_dma();
-  };
   constexpr std::true_type yes{};
   constexpr std::false_type no{};
   dma_rows(0);
   barrier_dma();
-  if constexpr (V == 2) {
-    chunk2(0, yes, no);
-    for (int c = 1; c + 1 < nchunks; ++c) chunk2(c, yes, yes);
-    chunk2(nchunks - 1, no, yes);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) sig(q);
-  } else {
-    chunk(0, yes, no);                     // nchunks >= 2 (checked by the host)
-    for (int c = 1; c + 1 < nchunks; ++c) chunk(c, yes, yes);
-    chunk(nchunks - 1, no, yes);
-  }
+  chunk(0, yes, no);                       // nchunks >= 2 (checked by the host)
+  for (int c = 1; c + 1 < nchunks; ++c) chunk(c, yes, yes);
+  chunk(nchunks - 1, no, yes);
   gxd(xbuf + ((nchunks - 1) & 1) * kFusedXdp);
   // GW[i][c] = acc 2^-15 / s_c
 #pragma unroll
@@ -763,7 +681,7 @@ extern "C" {
 
 int dsvgd_logreg_set_fused(int on) {
   const int prev = g_logreg_fused;
-  g_logreg_fused = on < 0 ? 0 : (on > 2 ? 2 : on);
+  g_logreg_fused = on ? 1 : 0;
   return prev;
 }
 
@@ -863,18 +781,11 @@ static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float 
     if ((rc = h2_rowimage(X + 1, ldx, n, p, w.n_pad, w.pp, rsw, riw, Wx, s))) return rc;
     if (g_logreg_fused && w.pp == kFusedKD * 16 && w.ldb == kFusedCols &&
         w.N_pad % kFusedChunk == 0 && w.N_pad >= 2 * kFusedChunk && w.n_pad % kFusedRows == 0) {
-      const dim3 fg((unsigned)(w.n_pad / kFusedRows));
-#define DSVGD_FUSED(V)                                                                           \
-  hipLaunchKernelGGL(logreg_fused_kernel<V>, fg, dim3(256), 0, s, (const _Float16*)Wx, w.n_pad,   \
-                     (const _Float16*)(base + w.off_xdx), w.N_pad,                                \
-                     (const _Float16*)(base + w.off_xdp), (int)(w.N_pad / kFusedChunk),          \
-                     (const float*)(sxd + 2 * w.ldb + 1), (const float*)riw,                      \
-                     (const float*)(sxd + w.ldb), GW, w.ldb, n)
-      if (g_logreg_fused == 2)
-        DSVGD_FUSED(2);
-      else
-        DSVGD_FUSED(1);
-#undef DSVGD_FUSED
+      hipLaunchKernelGGL(logreg_fused_kernel, dim3((unsigned)(w.n_pad / kFusedRows)), dim3(256), 0,
+                         s, (const _Float16*)Wx, w.n_pad, (const _Float16*)(base + w.off_xdx),
+                         w.N_pad, (const _Float16*)(base + w.off_xdp),
+                         (int)(w.N_pad / kFusedChunk), (const float*)(sxd + 2 * w.ldb + 1),
+                         (const float*)riw, (const float*)(sxd + w.ldb), GW, w.ldb, n);
       if ((rc = check_launch("logreg_fused"))) return rc;
       hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,
                          w.ldb, scale, S, lds, 1);
