@@ -179,3 +179,37 @@ def test_pair_split_declined_for_unaligned_half_block():
     cfg = dict(n=S * m, d=256, N=1024, eps=1e-3, seed=21, h=2.0 * 256 * 0.01 / 8.0,
                mode="all_scores", nrows=48, expect_plan=False)
     _check(S, cfg, _run(S, 29835, cfg))
+
+
+def test_xcd_slice_maps_give_identical_bits():
+    """The XCD slice maps (dsvgd_phi_set_xmap bits: 2 the window / row-half
+    DS 0 launches, 4 the batched forward partials) only change which block
+    runs which (row block, slice): one S = 8 rank's pair-split step at the
+    headline size (m = 8192: the forward partials batched and K-split) gives
+    the same bits -- its own rows' KY slices, row sums and every send
+    buffer -- with every map on and off."""
+    import dsvgd as m
+    from dsvgd import _native as N
+    n, d, S, r = 65536, 256, 8, 4
+    mm = n // S
+    rs = np.random.RandomState(7)
+    X = torch.tensor((0.1 * rs.randn(n, d)).astype(np.float32), device=DEV)
+    Sx = torch.tensor(rs.randn(n, d).astype(np.float32), device=DEV)
+    lib = N.load()
+    out = {}
+    for mask in (7, 0):
+        prev = lib.dsvgd_phi_set_xmap(mask)
+        try:
+            eng = m.PhiEngine(n, d, m=mm, row0=r * mm, device=DEV, pair_split=(r, S))
+            assert eng.plan is not None and eng.fwd_batched and eng.fwd_z > 1
+            for b in eng.recvbuf:
+                b.zero_()
+            eng.step(X, Sx, X_own=X[r * mm:(r + 1) * mm].clone(), h=2.0 * d, write_phi=True)
+            torch.cuda.synchronize()
+            out[mask] = ([eng.phi.clone()] + [b.clone() for b in eng.sendbuf])
+            del eng
+            torch.cuda.empty_cache()
+        finally:
+            lib.dsvgd_phi_set_xmap(prev)
+    for a, b in zip(out[7], out[0]):
+        assert torch.equal(a, b)
