@@ -1,7 +1,8 @@
 """The S = 1 distance Gram (n = 65536, d = 256, bracketed median accounting)
-with an A/B switch of the one-wave-per-SIMD Gram at --on and --off
-(default dsvgd_gram_set_packed 1 / 0), alternating, HIP events; D must come
-out bit-identical."""
+with an A/B switch of the one-wave-per-SIMD Gram at --on and --off,
+alternating, HIP events; D must come out bit-identical.  (profiles/r13ad: the
+switches dsvgd_gram_set_adepth and dsvgd_gram_set_packed of two builds since
+reverted.)"""
 import json
 import os
 import sys
@@ -17,7 +18,7 @@ import torch  # noqa: E402
 def main():
     import argparse
     ap = argparse.ArgumentParser()
-    ap.add_argument("--switch", default="dsvgd_gram_set_packed")
+    ap.add_argument("--switch", required=True, help="an int setter exported by the library")
     ap.add_argument("--on", type=int, default=1)
     ap.add_argument("--off", type=int, default=0)
     args = ap.parse_args()
