@@ -774,6 +774,176 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
   }
 }
 
+// ---- the incremental walk (dp <= 256, elementwise or frozen scores) -------
+// The same terms as gsw_sweep_kernel with the work per row moved OFF the
+// row-to-row path: when row j moves, every later row i of the block gets its
+// pair term at once -- k_ij = k(x_i, x_j') (x_i still the old row) into its
+// row sum, and k_ij w_j into its column accumulators -- so row i's phi is
+// ready when its turn comes (no distance phase, no column loop of its own).
+// Per row two barriers:
+//   A  thread c (column c): phi_j[c] from the wide pass's Q, the row's own
+//      accumulator and row sum, the move, w_j[c] = s_j'[c] - g (x_j'[c] - cen);
+//      the moved row into LDS;                                        (1)
+//   B  wave w, lane (r, q): row i = 16 w + r, features [64 q, 64 q + 64) of
+//      the old row in registers against the moved row from LDS, summed over
+//      the quad (DPP); k_ij for i > j into LDS at slot i - j - 1, the row sum
+//      r_i += k_ij;                                                   (2)
+//   C  thread c: acc[m] = acc[m + 1] + k_{j+1+m, j} w_j[c], m = 0 .. 62 --
+//      accumulator m belongs to row j + 1 + m, so the next row's is acc[0]
+//      (static register indices, no select chain).
+// Sums run over j in order (acc, r) and over the features in a fixed
+// order; the results differ from the four-wave walk's in rounding only.
+constexpr int kGsiMaxDp = 256;
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gsw_inc_kernel(
+    float* __restrict__ X, int64_t ldx, float* __restrict__ S, int64_t lds, float* __restrict__ Y,
+    int64_t ldy, float* __restrict__ norms, const float* __restrict__ center, int64_t n, int d,
+    int dp, int64_t r0, int B, const dsvgd_select_state* __restrict__ st, float step,
+    const float* __restrict__ Q, int64_t ldq, const float* __restrict__ Qr,
+    const float* __restrict__ extra, int64_t lde, float* __restrict__ phi_out, int64_t ldphi,
+    int score_kind, const float* __restrict__ mu, const float* __restrict__ lam,
+    float score_scale) {
+  extern __shared__ __attribute__((aligned(16))) float gsw_smem[];
+  const bool refreshed = score_kind != 0;
+  const int pitch = dp + 4;
+  float* xn = gsw_smem;                           // [B][pitch]: old rows, moved ones once moved
+  float* sn = xn + (int64_t)B * pitch;            // [B][dp] refreshed scores
+  float* kb = sn + (refreshed ? (int64_t)B * dp : 0);  // [64] k_{j+1+m, j}
+  float* rb = kb + 64;                            // [64] row sums over the moved rows
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int rr = lane >> 2, qq = lane & 3;        // phase B: row 16 w + rr, feature quarter qq
+  const int ib = 16 * w + rr;
+  const float inv_h = st->inv_h, g = 2.f * inv_h, scale = -inv_h * kLog2e;
+  const float inv_n = 1.f / (float)n;
+  const int c = t;
+  const bool cok = c < d;
+  for (int e = t; e < B * (dp >> 2); e += 256) {
+    const int i = e / (dp >> 2), c4 = (e % (dp >> 2)) << 2;
+    *reinterpret_cast<f32x4*>(xn + i * pitch + c4) =
+        *reinterpret_cast<const f32x4*>(Y + (r0 + i) * ldy + c4);
+  }
+  if (t < 64) rb[t] = 0.f;
+  // phase B's old row in registers (zero past dp and for rows >= B)
+  f32x4 xo[16];
+#pragma unroll
+  for (int f = 0; f < 16; ++f) {
+    const int cc = 64 * qq + 4 * f;
+    xo[f] = (ib < B && cc < dp) ? *reinterpret_cast<const f32x4*>(Y + (r0 + ib) * ldy + cc)
+                                : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const float cen = cok ? center[c] : 0.f;
+  const float mu_c = (score_kind == 1 && cok) ? mu[c] : 0.f;
+  const float lam_c = (score_kind == 1 && cok) ? lam[c] : 0.f;
+  float nq_x = 0.f, nq_s = 0.f, n_so = 0.f, n_ex = 0.f, nqr = 0.f;
+  auto prefetch = [&](int i) {
+    const int64_t gi = r0 + i;
+    nq_x = cok ? Q[i * ldq + c] : 0.f;
+    nq_s = cok ? Q[i * ldq + dp + c] : 0.f;
+    n_so = cok ? Y[gi * ldy + dp + c] : 0.f;
+    n_ex = (cok && extra) ? extra[(int64_t)i * lde + c] : 0.f;
+    nqr = Qr[i];
+  };
+  float acc[64];
+#pragma unroll
+  for (int m = 0; m < 64; ++m) acc[m] = 0.f;
+  float rsum = 0.f;   // phase B lanes: row ib's sum over the moved rows
+  prefetch(0);
+  __syncthreads();
+  for (int j = 0; j < B; ++j) {
+    // ---- A: row j's phi and move (column c) ----
+    const float q_x = nq_x, q_s = nq_s, s_o = n_so, ex = n_ex, qr = nqr;
+    if (j + 1 < B) prefetch(j + 1);
+    const float xc_o = cok ? xn[j * pitch + c] : 0.f;
+    const float rj = rb[j];
+    float wj = 0.f;
+    if (cok) {
+      float p = inv_n * (((q_s + s_o) - g * q_x) + acc[0] + g * ((qr + rj) * xc_o));
+      p += ex;
+      if (phi_out) phi_out[(int64_t)j * ldphi + c] = p;
+      const float x = (xc_o + cen) + step * p;
+      const float xc = x - cen;
+      xn[j * pitch + c] = xc;
+      float sv = s_o;
+      if (score_kind == 1 || score_kind == 2) {
+        sv = gs_score(score_kind, x, mu_c, lam_c, score_scale);
+        sn[j * dp + c] = sv;
+      }
+      wj = sv - g * xc;
+    }
+    gsw_barrier();                                                          // (1)
+    // ---- B: k(x_i, x_j') for the later rows i of this wave ----
+    {
+      const float* pm = xn + j * pitch + 64 * qq;
+      float da = 0.f, dbv = 0.f;
+#pragma unroll
+      for (int f = 0; f < 16; ++f) {
+        const int cc = 64 * qq + 4 * f;
+        const f32x4 v = cc < dp ? *reinterpret_cast<const f32x4*>(pm + 4 * f)
+                                : f32x4{0.f, 0.f, 0.f, 0.f};
+        const float d0 = xo[f][0] - v[0], d1 = xo[f][1] - v[1], d2 = xo[f][2] - v[2],
+                    d3 = xo[f][3] - v[3];
+        da = fmaf(d0, d0, fmaf(d2, d2, da));
+        dbv = fmaf(d1, d1, fmaf(d3, d3, dbv));
+      }
+      float dd = da + dbv;
+      dd += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                                          0, __builtin_bit_cast(int, dd), 0xB1, 0xF, 0xF, false));
+      dd += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                                          0, __builtin_bit_cast(int, dd), 0x4E, 0xF, 0xF, false));
+      const bool later = ib > j && ib < B;
+      const float k = later ? __builtin_amdgcn_exp2f(dd * scale) : 0.f;
+      rsum += k;
+      if (qq == 0 && ib > j) {
+        kb[ib - j - 1] = k;
+        rb[ib] = rsum;
+      }
+    }
+    gsw_barrier();                                                          // (2)
+    // ---- C: the later rows' accumulators gain k_ij w_j, shifted by one ----
+#pragma unroll
+    for (int m4 = 0; m4 < 16; ++m4) {
+      const f32x4 kv = *reinterpret_cast<const f32x4*>(kb + 4 * m4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = 4 * m4 + e;
+        if (m < 63) acc[m] = fmaf(kv[e], wj, acc[m + 1]);
+      }
+    }
+    acc[63] = 0.f;
+  }
+  __syncthreads();
+  for (int i = 0; i < B; ++i) {
+    const int64_t gi = r0 + i;
+    if (!cok) continue;
+    const float xc = xn[i * pitch + c];
+    X[gi * ldx + c] = xc + cen;
+    Y[gi * ldy + c] = xc;
+    if (refreshed) {
+      const float sv = sn[i * dp + c];
+      S[gi * lds + c] = sv;
+      Y[gi * ldy + dp + c] = sv;
+    }
+  }
+  {  // norms: four threads per row, a quarter of the features each (zero past d)
+    const int i = t >> 2, q4i = t & 3, q4 = dp >> 2;
+    float s2a = 0.f, s2b = 0.f;
+    if (i < B) {
+      const float* pr = xn + i * pitch + q4i * q4;
+      for (int cc = 0; cc < q4; cc += 4) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(pr + cc);
+        s2a = fmaf(v[0], v[0], fmaf(v[2], v[2], s2a));
+        s2b = fmaf(v[1], v[1], fmaf(v[3], v[3], s2b));
+      }
+    }
+    float s2 = s2a + s2b;
+    s2 += __shfl_xor(s2, 1, 64);
+    s2 += __shfl_xor(s2, 2, 64);
+    if (i < B && q4i == 0) norms[r0 + i] = s2;
+  }
+}
+
+// the incremental walk for the shapes it covers (A/B switch dsvgd_gsw_set_inc)
+static int g_gsw_inc = 1;
+
 }  // namespace dsvgd
 
 using namespace dsvgd;
@@ -837,6 +1007,12 @@ int dsvgd_gsw_debug(int mask) {
   return old;
 }
 
+int dsvgd_gsw_set_inc(int on) {
+  const int prev = g_gsw_inc;
+  g_gsw_inc = on ? 1 : 0;
+  return prev;
+}
+
 int64_t dsvgd_gsw_block_rows(int64_t d, int score_kind) {
   if (d <= 0 || d > kGswMaxD) return 0;
   return gsw_rows(roundup(d, 32), score_kind != 0);
@@ -889,6 +1065,17 @@ int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y
                 "logreg data rows must be 16-byte aligned (ldxd % 4 == 0)");
   DSVGD_REQUIRE(!extra || lde >= d, "lde");
   DSVGD_REQUIRE(!phi_out || ldphi >= d, "ldphi");
+  if (g_gsw_inc && dp <= kGsiMaxDp && score_kind != 3 && !(gsw_debug_mask() & 7)) {
+    const size_t smem_i =
+        sizeof(float) * ((size_t)B * (dp + 4) + (score_kind != 0 ? (size_t)B * dp : 0) + 128);
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gsw_inc_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem_i) != hipSuccess)
+      return fail_arg("gsw_inc: cannot reserve the walk's LDS");
+    hipLaunchKernelGGL(gsw_inc_kernel, dim3(1), dim3(256), smem_i, (hipStream_t)stream, X, ldx, S,
+                       lds, Y, ldy, norms, center, n, (int)d, (int)dp, r0, (int)B, st, step, Q, ldq,
+                       Qr, extra, lde, phi_out, ldphi, score_kind, mu, lam, score_scale);
+    return check_launch("gsw_inc");
+  }
   const size_t smem =
       sizeof(float) * ((size_t)B * (dp + 4) + (size_t)B * dp * (score_kind != 0 ? 2 : 1) + 256 +
                        1024 + 16 + (score_kind == 3 ? kGswCoef : 0));

@@ -69,6 +69,7 @@ SIGNATURES = {
     "dsvgd_phi_set_symrow": (_int, [_int]),
     "dsvgd_phi_splits_sym": (_i64, [_i64, _i64]),
     "dsvgd_phi_set_xmap": (_int, [_int]),
+    "dsvgd_gsw_set_inc": (_int, [_int]),
     "dsvgd_phi_set_gxd_w1": (_int, [_int]),
     "dsvgd_logreg_set_fused": (_int, [_int]),
     "dsvgd_phi_mm": (_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p]),

@@ -392,6 +392,12 @@ int dsvgd_sqdist_h2(const void* Yg, const float* norms, int64_t row0, int64_t m,
  * re-run per pair by distsampler.py:97-99), Y's row and norms[] kept current
  * (centre c = center, the packing centre of Y).  Any d <= 1024 for kind 3. */
 int64_t dsvgd_gsw_block_rows(int64_t d, int score_kind);  /* 0 if d > 1024 */
+/* The walk's form for roundup(d, 32) <= 256 and score_kind 0 .. 2 (A/B switch,
+ * returns the previous setting): 1 (default) = the incremental walk (each
+ * moved row's pair terms added to every later row of the block at once, two
+ * barriers per row, nothing per row on the path but the row's own phi);
+ * 0 = the four-wave walk (distances and the column loop per row). */
+int dsvgd_gsw_set_inc(int on);
 /* Timing probe of the walk (scripts/walk_probe.py; results are garbage while
  * set): bit 0 skips the next row's operand loads, bit 1 the distances, bit 2
  * the column loop.  Process-wide; returns the previous mask.  0 = normal. */

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--group", default=None,
                     help="comma list of engine.GSW_GROUP values: the blocked sweep alone "
                          "timed for each (blocks per wide pass)")
+    ap.add_argument("--inc", default=None,
+                    help="comma list of dsvgd_gsw_set_inc values (1: the incremental walk, "
+                         "0: the four-wave walk): the blocked sweep alone timed for each")
     ap.add_argument("--rows-sample", type=int, default=2048,
                     help="rows of the per-row path to time (0: skip it)")
     args = ap.parse_args()
@@ -113,6 +116,26 @@ def main():
                                                  for k, v in res.items() if str(k).startswith("x_")}
             print(json.dumps(out), flush=True)
             E.GSW_GROUP = 2
+        if args.inc:
+            from dsvgd import _native as NN
+            lib = NN.load()
+            res, xs = {}, {}
+            for v in [int(u) for u in args.inc.split(",")] * 2:
+                lib.dsvgd_gsw_set_inc(v)
+                Xb, Sb = X.clone(), S0.clone()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                sequential_sweep(Xb, Sb, range(n), eng.state, 1e-4, target=tgt, score_scale=scale)
+                torch.cuda.synchronize()
+                res.setdefault(v, []).append(1e3 * (time.perf_counter() - t0))
+                xs[v] = Xb
+            lib.dsvgd_gsw_set_inc(1)
+            out = {"config": name, "sweep_ms_by_inc": res}
+            if 0 in xs:
+                out["max_rel_diff_vs_inc0"] = {
+                    k: float((v - xs[0]).abs().max() / xs[0].abs().max()) for k, v in xs.items()}
+            print(json.dumps(out), flush=True)
+            del xs
         del ds, eng
         torch.cuda.empty_cache()
 

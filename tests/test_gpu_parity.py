@@ -451,6 +451,9 @@ def test_phi_row_split_matches_oracle(n, d, ldx):
                                              # the wide sweep (64 < d <= 1024, f32 MFMA wide pass)
                                              (1500, 128, 10, 700, "gauss"),
                                              (1200, 256, 0, 1200, "none"),
+                                             # the incremental walk's other shapes
+                                             (1100, 256, 5, 1000, "gmm"),
+                                             (900, 96, 0, 900, "gauss"),
                                              (800, 700, 50, 400, "gauss"),
                                              (600, 1024, 0, 300, "gmm"),
                                              # the logistic regression's score
@@ -517,6 +520,49 @@ def test_blocked_sweep_matches_oracle(n, d, lo, hi, kind):
             1e-5 * np.abs(S).max()
     # the per-row kernels on the same sweep (different summation order only)
     assert np.abs(out[False][0] - got).max() <= 1e-5 * max(1.0, np.abs(got).max())
+
+
+@pytest.mark.parametrize("n,d,lo,hi,kind", [(2000, 256, 0, 2000, "none"), (1500, 200, 31, 1400, "gauss"),
+                                             (700, 64 + 32, 0, 700, "gmm")])
+def test_incremental_walk_matches_four_wave_walk(n, d, lo, hi, kind):
+    """The incremental walk (dsvgd_gsw_set_inc(1): each moved row's pair terms
+    added to every later row of the block at once) and the four-wave walk
+    (per row: distances to the moved rows, then the column loop) move the same
+    rows to the same places up to rounding (different summation order),
+    with phi_out and extra rows."""
+    from dsvgd import _native as N
+    from dsvgd.engine import SelectState, sequential_sweep
+    m = dsvgd()
+    lib = N.load()
+    rs = np.random.RandomState(7 * n + d)
+    X0 = (0.6 * rs.randn(n, d)).astype(np.float32)
+    mu = rs.randn(d).astype(np.float32)
+    lam = rs.uniform(0.5, 2.0, d).astype(np.float32)
+    tgt = {"gauss": lambda: m.targets.Gaussian(mu, lam), "gmm": m.targets.GaussianMixture1D,
+           "none": lambda: None}[kind]()
+    S0 = rs.randn(n, d).astype(np.float32) if tgt is None else \
+        {"gauss": lambda: O.score_gaussian(X0, mu, lam), "gmm": lambda: O.score_gmm(X0)}[kind]().astype(np.float32)
+    st = SelectState(DEV)
+    N.call("dsvgd_set_bandwidth", st.ptr, 0.8 * d, N.stream(DEV))
+    extra = (0.01 * rs.randn(hi - lo, d)).astype(np.float32)
+    out = {}
+    prev = lib.dsvgd_gsw_set_inc(1)
+    try:
+        for inc in (1, 0):
+            lib.dsvgd_gsw_set_inc(inc)
+            Xg, Sg = gpu(X0), gpu(S0)
+            phi = torch.zeros(hi - lo, d, device=DEV)
+            sequential_sweep(Xg, Sg, range(lo, hi), st, 0.05, target=tgt, phi_out=phi,
+                             extra=gpu(extra))
+            torch.cuda.synchronize()
+            out[inc] = (Xg.cpu().numpy(), Sg.cpu().numpy(), phi.cpu().numpy())
+    finally:
+        lib.dsvgd_gsw_set_inc(prev)
+    (x1, s1, p1), (x0, s0, p0) = out[1], out[0]
+    assert np.array_equal(x1[:lo], X0[:lo]) and np.array_equal(x1[hi:], X0[hi:])
+    assert np.abs(p1 - p0).max() <= 1e-5 * np.abs(p0).max()
+    assert np.abs(x1 - x0).max() <= 1e-5 * max(1.0, np.abs(x0).max())
+    assert np.abs(s1 - s0).max() <= 1e-5 * max(1.0, np.abs(s0).max())
 
 
 def test_sampler_blocked_sweep_matches_reference(golden, monkeypatch):
