@@ -16,6 +16,7 @@ namespace dsvgd {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kWave = 64;
 constexpr float kLog2e = 1.4426950408889634f;

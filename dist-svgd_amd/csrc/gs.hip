@@ -804,7 +804,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     float score_scale) {
   extern __shared__ __attribute__((aligned(16))) float gsw_smem[];
   const bool refreshed = score_kind != 0;
-  const int pitch = dp + 4;
+  const int pitch = kGsiMaxDp + 4;                // zero past dp: phase B reads 256 features
   float* xn = gsw_smem;                           // [B][pitch]: old rows, moved ones once moved
   float* sn = xn + (int64_t)B * pitch;            // [B][dp] refreshed scores
   float* kb = sn + (refreshed ? (int64_t)B * dp : 0);  // [64] k_{j+1+m, j}
@@ -816,10 +816,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const float inv_n = 1.f / (float)n;
   const int c = t;
   const bool cok = c < d;
-  for (int e = t; e < B * (dp >> 2); e += 256) {
-    const int i = e / (dp >> 2), c4 = (e % (dp >> 2)) << 2;
+  for (int e = t; e < B * (kGsiMaxDp >> 2); e += 256) {
+    const int i = e / (kGsiMaxDp >> 2), c4 = (e % (kGsiMaxDp >> 2)) << 2;
     *reinterpret_cast<f32x4*>(xn + i * pitch + c4) =
-        *reinterpret_cast<const f32x4*>(Y + (r0 + i) * ldy + c4);
+        c4 < dp ? *reinterpret_cast<const f32x4*>(Y + (r0 + i) * ldy + c4)
+                : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   if (t < 64) rb[t] = 0.f;
   // phase B's old row in registers (zero past dp and for rows >= B)
@@ -852,7 +853,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // ---- A: row j's phi and move (column c) ----
     const float q_x = nq_x, q_s = nq_s, s_o = n_so, ex = n_ex, qr = nqr;
     if (j + 1 < B) prefetch(j + 1);
-    const float xc_o = cok ? xn[j * pitch + c] : 0.f;
+    const float xc_o = xn[j * pitch + c];   // (zero past dp)
     const float rj = rb[j];
     float wj = 0.f;
     if (cok) {
@@ -872,19 +873,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     gsw_barrier();                                                          // (1)
     // ---- B: k(x_i, x_j') for the later rows i of this wave ----
     {
-      const float* pm = xn + j * pitch + 64 * qq;
-      float da = 0.f, dbv = 0.f;
+      const float* pm = xn + j * pitch + 64 * qq;   // (zero past dp: pitch covers 256)
+      // feature pairs on the packed fp32 VALU, one v_pk_add + one v_pk_fma per
+      // two features (inline: the compiler's own packing added a v_mov per value)
+      f32x2 da = {0.f, 0.f}, dbv = {0.f, 0.f};
 #pragma unroll
       for (int f = 0; f < 16; ++f) {
-        const int cc = 64 * qq + 4 * f;
-        const f32x4 v = cc < dp ? *reinterpret_cast<const f32x4*>(pm + 4 * f)
-                                : f32x4{0.f, 0.f, 0.f, 0.f};
-        const float d0 = xo[f][0] - v[0], d1 = xo[f][1] - v[1], d2 = xo[f][2] - v[2],
-                    d3 = xo[f][3] - v[3];
-        da = fmaf(d0, d0, fmaf(d2, d2, da));
-        dbv = fmaf(d1, d1, fmaf(d3, d3, dbv));
+        const f32x4 v = *reinterpret_cast<const f32x4*>(pm + 4 * f);
+        const f32x2 x01 = {xo[f][0], xo[f][1]}, x23 = {xo[f][2], xo[f][3]};
+        const f32x2 v01 = {v[0], v[1]}, v23 = {v[2], v[3]};
+        f32x2 d01, d23;
+        asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d01) : "v"(x01), "v"(v01));
+        asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d23) : "v"(x23), "v"(v23));
+        asm("v_pk_fma_f32 %0, %1, %1, %0" : "+v"(da) : "v"(d01));
+        asm("v_pk_fma_f32 %0, %1, %1, %0" : "+v"(dbv) : "v"(d23));
       }
-      float dd = da + dbv;
+      float dd = (da.x + dbv.x) + (da.y + dbv.y);
       dd += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
                                           0, __builtin_bit_cast(int, dd), 0xB1, 0xF, 0xF, false));
       dd += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
@@ -905,7 +909,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int m = 4 * m4 + e;
-        if (m < 63) acc[m] = fmaf(kv[e], wj, acc[m + 1]);
+        // (inline: the compiler paired these shifted FMAs on the packed VALU
+        // at the cost of ~1.5 v_mov per value)
+        if (m < 63) asm("v_fma_f32 %0, %1, %2, %3" : "=v"(acc[m]) : "v"(kv[e]), "v"(wj), "v"(acc[m + 1]));
       }
     }
     acc[63] = 0.f;
@@ -1066,8 +1072,8 @@ int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y
   DSVGD_REQUIRE(!extra || lde >= d, "lde");
   DSVGD_REQUIRE(!phi_out || ldphi >= d, "ldphi");
   if (g_gsw_inc && dp <= kGsiMaxDp && score_kind != 3 && !(gsw_debug_mask() & 7)) {
-    const size_t smem_i =
-        sizeof(float) * ((size_t)B * (dp + 4) + (score_kind != 0 ? (size_t)B * dp : 0) + 128);
+    const size_t smem_i = sizeof(float) * ((size_t)B * (kGsiMaxDp + 4) +
+                                           (score_kind != 0 ? (size_t)B * dp : 0) + 128);
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gsw_inc_kernel),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem_i) != hipSuccess)
       return fail_arg("gsw_inc: cannot reserve the walk's LDS");
