@@ -30,6 +30,10 @@ def main():
     ap.add_argument("--inc", default=None,
                     help="comma list of dsvgd_gsw_set_inc values (1: the incremental walk, "
                          "0: the four-wave walk): the blocked sweep alone timed for each")
+    ap.add_argument("--ab", default=None,
+                    help="NAME=v1,v2: the blocked sweep alone timed for each value of the "
+                         "library switch NAME (e.g. dsvgd_gsw_set_corr_lds=1,0); the first "
+                         "value is restored after")
     ap.add_argument("--rows-sample", type=int, default=2048,
                     help="rows of the per-row path to time (0: skip it)")
     args = ap.parse_args()
@@ -116,12 +120,14 @@ def main():
                                                  for k, v in res.items() if str(k).startswith("x_")}
             print(json.dumps(out), flush=True)
             E.GSW_GROUP = 2
-        if args.inc:
+        if args.inc or args.ab:
             from dsvgd import _native as NN
             lib = NN.load()
+            sw, vals = ("dsvgd_gsw_set_inc", args.inc) if args.inc else args.ab.split("=")
+            vals = [int(u) for u in vals.split(",")]
             res, xs = {}, {}
-            for v in [int(u) for u in args.inc.split(",")] * 2:
-                lib.dsvgd_gsw_set_inc(v)
+            for v in vals * 2:
+                getattr(lib, sw)(v)
                 Xb, Sb = X.clone(), S0.clone()
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
@@ -129,11 +135,11 @@ def main():
                 torch.cuda.synchronize()
                 res.setdefault(v, []).append(1e3 * (time.perf_counter() - t0))
                 xs[v] = Xb
-            lib.dsvgd_gsw_set_inc(1)
-            out = {"config": name, "sweep_ms_by_inc": res}
-            if 0 in xs:
-                out["max_rel_diff_vs_inc0"] = {
-                    k: float((v - xs[0]).abs().max() / xs[0].abs().max()) for k, v in xs.items()}
+            getattr(lib, sw)(vals[0])
+            out = {"config": name, "switch": sw, "sweep_ms_by_value": res}
+            ref = xs[vals[-1]]
+            out["max_rel_diff_vs_last"] = {
+                k: float((v - ref).abs().max() / ref.abs().max()) for k, v in xs.items()}
             print(json.dumps(out), flush=True)
             del xs
         del ds, eng
