@@ -1117,12 +1117,15 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
                    N.ld(phi_out) if phi_out is not None else d, sk, N.ptr(mu), N.ptr(lam),
                    float(score_scale), N.ptr(xd), N.ld(xd) if xd is not None else d, N.ptr(td),
                    td.numel() if td is not None else 0, s)
-            W.images(b0, nb, s)
             r1 = b0 + nb
             if r1 < g0 + gn:   # the group's later rows gain this block at its moved rows
                 N.call("dsvgd_gsw_group_corr", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S),
                        N.ptr(W.mean), n, d, r1, g0 + gn - r1, b0, nb, h_state.ptr,
                        N.ptr(W.Q) + 4 * (r1 - g0) * W.ldy, W.ldy, N.ptr(W.Qr) + 4 * (r1 - g0), s)
+        # the group's moved rows into the images once, after its last walk:
+        # only the next groups' wide passes read them (the walks read Y, the
+        # correction X and S)
+        W.images(g0, gn, s)
 
 
 def _blocked_sweep(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s):
