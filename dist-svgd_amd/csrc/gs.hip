@@ -327,6 +327,66 @@ __global__ __launch_bounds__(256) void gsw_group_corr_kernel(
   const float scale = -st->inv_h * kLog2e;
   for (int64_t c = t; c < d; c += 256) xi[c] = X[(r0 + i) * ldx + c];
   __syncthreads();
+  if (d <= 256) {
+    // the same sums in the same order with every load of a loop issued
+    // before its first use (the general loops below wait on one L2 round
+    // trip per moved row: 28 us per 64-row correction at config D, r13ag)
+    float xv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xv[k] = lane + 64 * k < d ? xi[lane + 64 * k] : 0.f;
+    float xr[16][4];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+      const int j = w + 4 * jj;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = lane + 64 * k;
+        xr[jj][k] = (j < pB && c < d) ? X[(p0 + j) * ldx + c] : xv[k];
+      }
+    }
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+      const int j = w + 4 * jj;
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float df = xv[k] - xr[jj][k];
+        a = fmaf(df, df, a);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+      if (lane == 0 && j < pB) kv[j] = __builtin_amdgcn_exp2f(a * scale);
+    }
+    __syncthreads();
+    float* q = Q + (int64_t)i * ldq;
+    const int c = t;
+    if (c < d) {
+      const float cc = center[c];
+      float xa[kGsB], sa[kGsB];
+#pragma unroll
+      for (int j = 0; j < kGsB; ++j) {
+        xa[j] = j < pB ? X[(p0 + j) * ldx + c] : 0.f;
+        sa[j] = j < pB ? S[(p0 + j) * lds + c] : 0.f;
+      }
+      float qx = 0.f, qs = 0.f;
+#pragma unroll
+      for (int j = 0; j < kGsB; ++j) {
+        if (j < pB) {   // (not break: the loop must unroll)
+          const float k = kv[j];
+          qx = fmaf(k, xa[j] - cc, qx);
+          qs = fmaf(k, sa[j], qs);
+        }
+      }
+      q[c] += qx;
+      q[dp + c] += qs;
+    }
+    if (t == 0) {
+      float r = 0.f;
+      for (int j = 0; j < pB; ++j) r += kv[j];
+      Qr[i] += r;
+    }
+    return;
+  }
   for (int j = w; j < pB; j += 4) {
     const float* xj = X + (p0 + j) * ldx;
     float a = 0.f;
