@@ -1026,7 +1026,7 @@ class _WideSweep(object):
         # split-K slices of the group's wide pass: ldy / 512 column blocks x
         # 128-row tiles per slice, so ~256 blocks fill the CUs
         cb = max(1, self.ldy // 512) * (gpad // 128)
-        z = max(1, 256 // cb)
+        z = max(1, 256 // cb) if not GSW_SPLITS else GSW_SPLITS
         while z > 1 and self.n_pad // z < 128:
             z //= 2
         self.splits = z
@@ -1060,6 +1060,8 @@ _WIDE = {}
 # blocks per wide pass of the wide Gauss-Seidel sweep (1: block after block;
 # config D sweep 278.7 / 253.0 / 256.2 ms at 1 / 2 / 4, profiles/r13u)
 GSW_GROUP = 2
+# split-K slices of a group's wide pass (None: ~256 blocks; an A/B override)
+GSW_SPLITS = None
 
 
 def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s):
@@ -1070,7 +1072,7 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
     order (dsvgd_gsw_block_sweep) and the moved rows are re-split into the
     engines' images -- the same terms as the per-row path, in blocked order."""
     n, d = X.shape
-    key = (X.device, n, d, GSW_GEMM, kind != 0, GSW_GROUP)
+    key = (X.device, n, d, GSW_GEMM, kind != 0, GSW_GROUP, GSW_SPLITS)
     W = _WIDE.get(key)
     if W is None:
         _WIDE.clear()

@@ -34,6 +34,9 @@ def main():
                     help="NAME=v1,v2: the blocked sweep alone timed for each value of the "
                          "library switch NAME (e.g. dsvgd_gsw_set_corr_lds=1,0); the first "
                          "value is restored after")
+    ap.add_argument("--splits", default=None,
+                    help="comma list of engine.GSW_SPLITS values (0: chosen): the blocked "
+                         "sweep alone timed for each")
     ap.add_argument("--rows-sample", type=int, default=2048,
                     help="rows of the per-row path to time (0: skip it)")
     args = ap.parse_args()
@@ -120,6 +123,22 @@ def main():
                                                  for k, v in res.items() if str(k).startswith("x_")}
             print(json.dumps(out), flush=True)
             E.GSW_GROUP = 2
+        if args.splits:
+            import dsvgd.engine as E
+            res = {}
+            for zv in [int(v) for v in args.splits.split(",")] * 2:
+                E.GSW_SPLITS = zv or None
+                Xb, Sb = X.clone(), S0.clone()
+                sequential_sweep(Xb, Sb, range(0, 512), eng.state, 1e-4, target=tgt,
+                                 score_scale=scale)     # warm-up (this split count's buffers)
+                Xb, Sb = X.clone(), S0.clone()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                sequential_sweep(Xb, Sb, range(n), eng.state, 1e-4, target=tgt, score_scale=scale)
+                torch.cuda.synchronize()
+                res.setdefault(zv, []).append(1e3 * (time.perf_counter() - t0))
+            E.GSW_SPLITS = None
+            print(json.dumps({"config": name, "sweep_ms_by_splits": res}), flush=True)
         if args.inc or args.ab:
             from dsvgd import _native as NN
             lib = NN.load()
