@@ -854,6 +854,10 @@ __global__ __launch_bounds__(256) void gsw_sweep_kernel(
 // Sums run over j in order (acc, r) and over the features in a fixed
 // order; the results differ from the four-wave walk's in rounding only.
 constexpr int kGsiMaxDp = 256;
+// CPT columns per thread (roundup(d, 32) <= 256 CPT): phase B's rows get 4 CPT
+// lanes of 64 features each, so a wave holds 16 / CPT rows and a block at
+// most 64 / CPT (the host falls back to the four-wave walk above that).
+template <int CPT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gsw_inc_kernel(
     float* __restrict__ X, int64_t ldx, float* __restrict__ S, int64_t lds, float* __restrict__ Y,
     int64_t ldy, float* __restrict__ norms, const float* __restrict__ center, int64_t n, int d,
@@ -862,22 +866,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const float* __restrict__ extra, int64_t lde, float* __restrict__ phi_out, int64_t ldphi,
     int score_kind, const float* __restrict__ mu, const float* __restrict__ lam,
     float score_scale) {
+  constexpr int DPW = kGsiMaxDp * CPT;            // features a row carries in LDS
+  constexpr int LPR = 4 * CPT;                    // phase B lanes per row
+  constexpr int RPW = 64 / LPR;                   // rows per wave
+  constexpr int BMAX = 4 * RPW;                   // rows per block
   extern __shared__ __attribute__((aligned(16))) float gsw_smem[];
   const bool refreshed = score_kind != 0;
-  const int pitch = kGsiMaxDp + 4;                // zero past dp: phase B reads 256 features
+  const int pitch = DPW + 4;                      // zero past dp: phase B reads DPW features
   float* xn = gsw_smem;                           // [B][pitch]: old rows, moved ones once moved
   float* sn = xn + (int64_t)B * pitch;            // [B][dp] refreshed scores
   float* kb = sn + (refreshed ? (int64_t)B * dp : 0);  // [64] k_{j+1+m, j}
   float* rb = kb + 64;                            // [64] row sums over the moved rows
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int rr = lane >> 2, qq = lane & 3;        // phase B: row 16 w + rr, feature quarter qq
-  const int ib = 16 * w + rr;
+  const int rr = lane / LPR, qq = lane % LPR;     // phase B: row RPW w + rr, features 64 qq ..
+  const int ib = RPW * w + rr;
   const float inv_h = st->inv_h, g = 2.f * inv_h, scale = -inv_h * kLog2e;
   const float inv_n = 1.f / (float)n;
-  const int c = t;
-  const bool cok = c < d;
-  for (int e = t; e < B * (kGsiMaxDp >> 2); e += 256) {
-    const int i = e / (kGsiMaxDp >> 2), c4 = (e % (kGsiMaxDp >> 2)) << 2;
+  for (int e = t; e < B * (DPW >> 2); e += 256) {
+    const int i = e / (DPW >> 2), c4 = (e % (DPW >> 2)) << 2;
     *reinterpret_cast<f32x4*>(xn + i * pitch + c4) =
         c4 < dp ? *reinterpret_cast<const f32x4*>(Y + (r0 + i) * ldy + c4)
                 : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -891,49 +897,75 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     xo[f] = (ib < B && cc < dp) ? *reinterpret_cast<const f32x4*>(Y + (r0 + ib) * ldy + cc)
                                 : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const float cen = cok ? center[c] : 0.f;
-  const float mu_c = (score_kind == 1 && cok) ? mu[c] : 0.f;
-  const float lam_c = (score_kind == 1 && cok) ? lam[c] : 0.f;
-  float nq_x = 0.f, nq_s = 0.f, n_so = 0.f, n_ex = 0.f, nqr = 0.f;
+  // phase A / C columns c = t + 256 u
+  float cen[CPT], mu_c[CPT], lam_c[CPT];
+#pragma unroll
+  for (int u = 0; u < CPT; ++u) {
+    const int c = t + 256 * u;
+    cen[u] = c < d ? center[c] : 0.f;
+    mu_c[u] = (score_kind == 1 && c < d) ? mu[c] : 0.f;
+    lam_c[u] = (score_kind == 1 && c < d) ? lam[c] : 0.f;
+  }
+  float nq_x[CPT], nq_s[CPT], n_so[CPT], n_ex[CPT], nqr = 0.f;
   auto prefetch = [&](int i) {
     const int64_t gi = r0 + i;
-    nq_x = cok ? Q[i * ldq + c] : 0.f;
-    nq_s = cok ? Q[i * ldq + dp + c] : 0.f;
-    n_so = cok ? Y[gi * ldy + dp + c] : 0.f;
-    n_ex = (cok && extra) ? extra[(int64_t)i * lde + c] : 0.f;
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+      const int c = t + 256 * u;
+      const bool ok = c < d;
+      nq_x[u] = ok ? Q[i * ldq + c] : 0.f;
+      nq_s[u] = ok ? Q[i * ldq + dp + c] : 0.f;
+      n_so[u] = ok ? Y[gi * ldy + dp + c] : 0.f;
+      n_ex[u] = (ok && extra) ? extra[(int64_t)i * lde + c] : 0.f;
+    }
     nqr = Qr[i];
   };
-  float acc[64];
+  float acc[BMAX][CPT];
 #pragma unroll
-  for (int m = 0; m < 64; ++m) acc[m] = 0.f;
+  for (int m = 0; m < BMAX; ++m)
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) acc[m][u] = 0.f;
   float rsum = 0.f;   // phase B lanes: row ib's sum over the moved rows
   prefetch(0);
   __syncthreads();
   for (int j = 0; j < B; ++j) {
-    // ---- A: row j's phi and move (column c) ----
-    const float q_x = nq_x, q_s = nq_s, s_o = n_so, ex = n_ex, qr = nqr;
+    // ---- A: row j's phi and move (columns t + 256 u) ----
+    float q_x[CPT], q_s[CPT], s_o[CPT], ex[CPT];
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+      q_x[u] = nq_x[u];
+      q_s[u] = nq_s[u];
+      s_o[u] = n_so[u];
+      ex[u] = n_ex[u];
+    }
+    const float qr = nqr;
     if (j + 1 < B) prefetch(j + 1);
-    const float xc_o = xn[j * pitch + c];   // (zero past dp)
     const float rj = rb[j];
-    float wj = 0.f;
-    if (cok) {
-      float p = inv_n * (((q_s + s_o) - g * q_x) + acc[0] + g * ((qr + rj) * xc_o));
-      p += ex;
-      if (phi_out) phi_out[(int64_t)j * ldphi + c] = p;
-      const float x = (xc_o + cen) + step * p;
-      const float xc = x - cen;
-      xn[j * pitch + c] = xc;
-      float sv = s_o;
-      if (score_kind == 1 || score_kind == 2) {
-        sv = gs_score(score_kind, x, mu_c, lam_c, score_scale);
-        sn[j * dp + c] = sv;
+    float wj[CPT];
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+      const int c = t + 256 * u;
+      const float xc_o = xn[j * pitch + c];   // (zero past dp)
+      wj[u] = 0.f;
+      if (c < d) {
+        float p = inv_n * (((q_s[u] + s_o[u]) - g * q_x[u]) + acc[0][u] + g * ((qr + rj) * xc_o));
+        p += ex[u];
+        if (phi_out) phi_out[(int64_t)j * ldphi + c] = p;
+        const float x = (xc_o + cen[u]) + step * p;
+        const float xc = x - cen[u];
+        xn[j * pitch + c] = xc;
+        float sv = s_o[u];
+        if (score_kind == 1 || score_kind == 2) {
+          sv = gs_score(score_kind, x, mu_c[u], lam_c[u], score_scale);
+          sn[j * dp + c] = sv;
+        }
+        wj[u] = sv - g * xc;
       }
-      wj = sv - g * xc;
     }
     gsw_barrier();                                                          // (1)
     // ---- B: k(x_i, x_j') for the later rows i of this wave ----
     {
-      const float* pm = xn + j * pitch + 64 * qq;   // (zero past dp: pitch covers 256)
+      const float* pm = xn + j * pitch + 64 * qq;   // (zero past dp: pitch covers DPW)
       // feature pairs on the packed fp32 VALU, one v_pk_add + one v_pk_fma per
       // two features (inline: the compiler's own packing added a v_mov per value)
       f32x2 da = {0.f, 0.f}, dbv = {0.f, 0.f};
@@ -949,6 +981,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         asm("v_pk_fma_f32 %0, %1, %1, %0" : "+v"(dbv) : "v"(d23));
       }
       float dd = (da.x + dbv.x) + (da.y + dbv.y);
+      // the row's LPR lanes summed (every lane ends with the total)
+      if constexpr (LPR == 16) {   // one DPP row: rotations by 8, then 4
+        dd += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                                            0, __builtin_bit_cast(int, dd), 0x128, 0xF, 0xF, false));
+        dd += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                                            0, __builtin_bit_cast(int, dd), 0x124, 0xF, 0xF, false));
+      } else if constexpr (LPR == 8) {
+        dd += __shfl_xor(dd, 4, 64);
+      }
       dd += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
                                           0, __builtin_bit_cast(int, dd), 0xB1, 0xF, 0xF, false));
       dd += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
@@ -964,29 +1005,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     gsw_barrier();                                                          // (2)
     // ---- C: the later rows' accumulators gain k_ij w_j, shifted by one ----
 #pragma unroll
-    for (int m4 = 0; m4 < 16; ++m4) {
+    for (int m4 = 0; m4 < BMAX / 4; ++m4) {
       const f32x4 kv = *reinterpret_cast<const f32x4*>(kb + 4 * m4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int m = 4 * m4 + e;
         // (inline: the compiler paired these shifted FMAs on the packed VALU
         // at the cost of ~1.5 v_mov per value)
-        if (m < 63) asm("v_fma_f32 %0, %1, %2, %3" : "=v"(acc[m]) : "v"(kv[e]), "v"(wj), "v"(acc[m + 1]));
+#pragma unroll
+        for (int u = 0; u < CPT; ++u)
+          if (m < BMAX - 1)
+            asm("v_fma_f32 %0, %1, %2, %3" : "=v"(acc[m][u]) : "v"(kv[e]), "v"(wj[u]), "v"(acc[m + 1][u]));
       }
     }
-    acc[63] = 0.f;
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) acc[BMAX - 1][u] = 0.f;
   }
   __syncthreads();
   for (int i = 0; i < B; ++i) {
     const int64_t gi = r0 + i;
-    if (!cok) continue;
-    const float xc = xn[i * pitch + c];
-    X[gi * ldx + c] = xc + cen;
-    Y[gi * ldy + c] = xc;
-    if (refreshed) {
-      const float sv = sn[i * dp + c];
-      S[gi * lds + c] = sv;
-      Y[gi * ldy + dp + c] = sv;
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+      const int c = t + 256 * u;
+      if (c >= d) continue;
+      const float xc = xn[i * pitch + c];
+      X[gi * ldx + c] = xc + cen[u];
+      Y[gi * ldy + c] = xc;
+      if (refreshed) {
+        const float sv = sn[i * dp + c];
+        S[gi * lds + c] = sv;
+        Y[gi * ldy + dp + c] = sv;
+      }
     }
   }
   {  // norms: four threads per row, a quarter of the features each (zero past d)
@@ -1131,15 +1180,27 @@ int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y
                 "logreg data rows must be 16-byte aligned (ldxd % 4 == 0)");
   DSVGD_REQUIRE(!extra || lde >= d, "lde");
   DSVGD_REQUIRE(!phi_out || ldphi >= d, "ldphi");
-  if (g_gsw_inc && dp <= kGsiMaxDp && score_kind != 3 && !(gsw_debug_mask() & 7)) {
-    const size_t smem_i = sizeof(float) * ((size_t)B * (kGsiMaxDp + 4) +
+  const int cpt = dp <= kGsiMaxDp ? 1 : (dp <= 2 * kGsiMaxDp ? 2 : 4);
+  if (g_gsw_inc && score_kind != 3 && B <= 64 / cpt && !(gsw_debug_mask() & 7)) {
+    const size_t smem_i = sizeof(float) * ((size_t)B * (kGsiMaxDp * cpt + 4) +
                                            (score_kind != 0 ? (size_t)B * dp : 0) + 128);
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gsw_inc_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem_i) != hipSuccess)
+    const void* fn = cpt == 1   ? reinterpret_cast<const void*>(&gsw_inc_kernel<1>)
+                     : cpt == 2 ? reinterpret_cast<const void*>(&gsw_inc_kernel<2>)
+                                : reinterpret_cast<const void*>(&gsw_inc_kernel<4>);
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem_i) !=
+        hipSuccess)
       return fail_arg("gsw_inc: cannot reserve the walk's LDS");
-    hipLaunchKernelGGL(gsw_inc_kernel, dim3(1), dim3(256), smem_i, (hipStream_t)stream, X, ldx, S,
-                       lds, Y, ldy, norms, center, n, (int)d, (int)dp, r0, (int)B, st, step, Q, ldq,
-                       Qr, extra, lde, phi_out, ldphi, score_kind, mu, lam, score_scale);
+#define DSVGD_GSI(C)                                                                              \
+  hipLaunchKernelGGL(gsw_inc_kernel<C>, dim3(1), dim3(256), smem_i, (hipStream_t)stream, X, ldx, S, \
+                     lds, Y, ldy, norms, center, n, (int)d, (int)dp, r0, (int)B, st, step, Q, ldq,  \
+                     Qr, extra, lde, phi_out, ldphi, score_kind, mu, lam, score_scale)
+    if (cpt == 1)
+      DSVGD_GSI(1);
+    else if (cpt == 2)
+      DSVGD_GSI(2);
+    else
+      DSVGD_GSI(4);
+#undef DSVGD_GSI
     return check_launch("gsw_inc");
   }
   const size_t smem =

@@ -523,7 +523,11 @@ def test_blocked_sweep_matches_oracle(n, d, lo, hi, kind):
 
 
 @pytest.mark.parametrize("n,d,lo,hi,kind", [(2000, 256, 0, 2000, "none"), (1500, 200, 31, 1400, "gauss"),
-                                             (700, 64 + 32, 0, 700, "gmm")])
+                                             (700, 64 + 32, 0, 700, "gmm"),
+                                             # 2 and 4 columns per thread (16 / 32-row blocks)
+                                             (700, 512, 3, 650, "gauss"),
+                                             (600, 1024, 0, 600, "none"),
+                                             (500, 1000, 7, 480, "gmm")])
 def test_incremental_walk_matches_four_wave_walk(n, d, lo, hi, kind):
     """The incremental walk (dsvgd_gsw_set_inc(1): each moved row's pair terms
     added to every later row of the block at once) and the four-wave walk
