@@ -1000,7 +1000,11 @@ class _WideSweep(object):
         self.B = int(lib.dsvgd_gsw_block_rows(d, kind))
         # blocks per wide pass (GSW_GROUP): the group's rows in one pass, the
         # earlier blocks' moved rows added after each walk (dsvgd_gsw_group_corr)
-        self.G = max(1, min(GSW_GROUP, 256 // self.B))
+        # (None: about 128 rows per pass -- config D 2 x 64 rows, config E
+        # 8 x 16: 160 / 487 ms against 162.9 / 811 at 4 x 64 / 2 x 16,
+        # profiles/r13ak, r13ap, r13aq)
+        grp = GSW_GROUP if GSW_GROUP else max(1, 128 // self.B)
+        self.G = max(1, min(grp, 256 // self.B))
         self.GB = self.G * self.B
         gpad = -(-self.GB // 128) * 128
         self.Y = torch.zeros(self.n_pad + 128, self.ldy, **f32)
@@ -1058,8 +1062,9 @@ class _WideSweep(object):
 
 _WIDE = {}
 # blocks per wide pass of the wide Gauss-Seidel sweep (1: block after block;
-# config D sweep 278.7 / 253.0 / 256.2 ms at 1 / 2 / 4, profiles/r13u)
-GSW_GROUP = 2
+# config D sweep 278.7 / 253.0 / 256.2 ms at 1 / 2 / 4, profiles/r13u; None:
+# as many blocks as make about 128 rows)
+GSW_GROUP = None
 # split-K slices of a group's wide pass (None: ~256 blocks; an A/B override)
 GSW_SPLITS = None
 

@@ -122,7 +122,7 @@ def main():
                 out["max_abs_diff_vs_group1"] = {k[2:]: float((v - ref).abs().max())
                                                  for k, v in res.items() if str(k).startswith("x_")}
             print(json.dumps(out), flush=True)
-            E.GSW_GROUP = 2
+            E.GSW_GROUP = None
         if args.splits:
             import dsvgd.engine as E
             res = {}
