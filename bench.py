@@ -234,6 +234,33 @@ def gather_max(d, world, backend, dev):
     return {k: max(o.get(k, 0.0) for o in objs) for k in keys}
 
 
+EXCHANGE_STAGES = ("allgather_x", "allreduce_scores", "allgather_scores", "hist_allreduce",
+                   "partials_post", "partials_wait")
+
+
+def multi_gpu_report(sampler, eng, local_stages, world):
+    """N > 1: what ran, per rank -- whether the
+    pair-split layout engaged, its route probe's verdict and
+    its first-step check against the row-block layout (DistSampler), and
+    each rank's mean HIP-event time per step of every exchange stage (the
+    particle all-gather, the score all-reduce, the median's histogram
+    all-reduces, the pair split's partials post / join wait)."""
+    mine = {"rank": dist.get_rank(),
+            "pair_split": eng.plan is not None,
+            "route_probe_ok": sampler._routes_ok,
+            "exchange_ms": {k: local_stages[k] for k in EXCHANGE_STAGES if k in local_stages}}
+    ranks = [None] * world
+    dist.all_gather_object(ranks, mine)
+    ranks.sort(key=lambda r: r["rank"])
+    return {"backend": dist.get_backend(),
+            "world_size": dist.get_world_size(),
+            "pair_split_engaged": [r["pair_split"] for r in ranks],
+            "route_probe_ok": [r["route_probe_ok"] for r in ranks],
+            "pair_split_first_step_check": sampler.pair_split_check,
+            "pair_split_check_tol": sampler.PAIR_SPLIT_CHECK_TOL,
+            "exchange_ms_per_rank": [r["exchange_ms"] for r in ranks]}
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     ap = argparse.ArgumentParser()
@@ -343,10 +370,10 @@ def main(argv=None):
     for _ in range(args.breakdown):
         sampler.make_step(eps)
     sampler.timer = None
-    stages = {k: float(np.mean(v)) for k, v in full.summary().items()}
+    local_stages = {k: float(np.mean(v)) for k, v in full.summary().items()}
     # N > 1: each stage's mean HIP-event time, max over ranks (the exchange
     # stages allgather_x / allreduce_scores / hist_allreduce included)
-    stages = gather_max(stages, world, args.backend, dev)
+    stages = gather_max(local_stages, world, args.backend, dev)
     assert bool(torch.isfinite(sampler._work).all()), "non-finite particles"
 
     m = n // world
@@ -427,6 +454,8 @@ def main(argv=None):
                           "world_size_seen": dist.get_world_size() if world > 1 else 1,
                           "stages": "mean per step, max over ranks" if world > 1 else "mean per step"},
     }
+    if world > 1:
+        out["multi_gpu"] = multi_gpu_report(sampler, eng, local_stages, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, d, xl, tl, args.cpu_budget)
     if rank == 0:

@@ -1181,15 +1181,17 @@ int dsvgd_gsw_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, float* Y
   DSVGD_REQUIRE(!extra || lde >= d, "lde");
   DSVGD_REQUIRE(!phi_out || ldphi >= d, "ldphi");
   const int cpt = dp <= kGsiMaxDp ? 1 : (dp <= 2 * kGsiMaxDp ? 2 : 4);
-  if (g_gsw_inc && score_kind != 3 && B <= 64 / cpt && !(gsw_debug_mask() & 7)) {
-    const size_t smem_i = sizeof(float) * ((size_t)B * (kGsiMaxDp * cpt + 4) +
-                                           (score_kind != 0 ? (size_t)B * dp : 0) + 128);
-    const void* fn = cpt == 1   ? reinterpret_cast<const void*>(&gsw_inc_kernel<1>)
+  // the incremental walk (roundup(d, 32) <= 1024 at 1 / 2 / 4 columns per
+  // thread, B <= 64 / cpt rows); when its LDS cannot be reserved the
+  // four-wave walk below runs the block instead (slower, same results)
+  const size_t smem_i = sizeof(float) * ((size_t)B * (kGsiMaxDp * cpt + 4) +
+                                         (score_kind != 0 ? (size_t)B * dp : 0) + 128);
+  const void* fn_i = cpt == 1   ? reinterpret_cast<const void*>(&gsw_inc_kernel<1>)
                      : cpt == 2 ? reinterpret_cast<const void*>(&gsw_inc_kernel<2>)
                                 : reinterpret_cast<const void*>(&gsw_inc_kernel<4>);
-    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem_i) !=
-        hipSuccess)
-      return fail_arg("gsw_inc: cannot reserve the walk's LDS");
+  if (g_gsw_inc && score_kind != 3 && B <= 64 / cpt && !(gsw_debug_mask() & 7) &&
+      hipFuncSetAttribute(fn_i, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem_i) ==
+          hipSuccess) {
 #define DSVGD_GSI(C)                                                                              \
   hipLaunchKernelGGL(gsw_inc_kernel<C>, dim3(1), dim3(256), smem_i, (hipStream_t)stream, X, ldx, S, \
                      lds, Y, ldy, norms, center, n, (int)d, (int)dp, r0, (int)B, st, step, Q, ldq,  \

@@ -232,6 +232,8 @@ __global__ __launch_bounds__(256) void ysplit_kernel(const float* __restrict__ Y
 // the symmetric layout's phi_mm: 1 = one launch per row (DS 4), 0 = the
 // two-launch hybrid (DS 1 + DS 2); dsvgd_phi_set_symrow
 static int g_phi_symrow = 1;
+// at most this many columns per fp32 split-K accumulation chain (phi_splits)
+constexpr int64_t kMaxChain = 16384;
 // logreg's G . Xd (FmtH2, 256 columns) on phi_w1_kernel<0, 2, false> (1) or
 // the 8-wave 256-row NN tile (0, default: the phi_w1 shape measured slower,
 // scores 3.57 vs 3.38 ms at N = 16384, 0.58 vs 0.52 at 2048 -- with half
@@ -288,6 +290,12 @@ int launch_nn_x3(const float* D, int64_t K, const typename F::E* Yx, int64_t ldy
       // a per-wave LDS scratch) and the plain ones (DS 2); half the split-K
       // slices each
       const int sl = splits / 2;
+      // a slice of either launch spans up to K / sl columns: refuse slices
+      // sized for the one-launch form (symrow switched after the engine took
+      // dsvgd_phi_splits_sym) rather than run chains past 2 kMaxChain
+      if (K > 2 * kMaxChain * (int64_t)sl)
+        return fail_arg("phi_mm: the hybrid's split-K chains would exceed 2 x 16384 columns; "
+                        "size the slices with dsvgd_phi_splits_sym under the current symrow form");
       const dim3 g1(grid.x, grid.y, sl), g2(grid.x, grid.y, splits - sl);
       launch_w1<1>(g1, s, D, K, Yx, ldy, K, kchunk, st, C, ldc, rowsum, m, row0, sym, colinv, 0,
                    gate, gate_on);
@@ -866,7 +874,7 @@ int nn_gemm(bool exp_, const float* A, int64_t K, const float* B, int64_t ldb, i
 // slices summed in slice order by phi_finish cut that.  FmtH2 at n = 65536:
 // 5.2e-7 with 8192-long slices, 7.8e-7 with 16384 (shipped: half the
 // partials to write and re-read, S = 1 step -1.7 %; profiles/r5g/).
-constexpr int64_t kMaxChain = 16384;
+// (kMaxChain: defined with g_phi_symrow above)
 
 int64_t phi_splits(int64_t m, int64_t n, int64_t ldy) {
   const int64_t cols = ldy % 512 == 0 ? 512 : (ldy % 256 == 0 ? 256 : 128);
@@ -891,10 +899,14 @@ int64_t dsvgd_phi_splits(int64_t m, int64_t n, int64_t ldy) { return phi_splits(
 
 int64_t dsvgd_phi_splits_sym(int64_t n, int64_t ldy) {
   int64_t s = phi_splits(n, n, ldy);
-  if (!g_phi_symrow) return s;
+  // only the one-launch form (phi_w1 DS 4: symrow on, TN = 4, i.e. ldy a
+  // multiple of 512) takes the longer slices; the hybrid and the 8-wave
+  // symmetric tile give each of their launches half the slices, so halving
+  // them there would double their chains again
+  if (!g_phi_symrow || ldy % 512 != 0) return s;
   // the one-launch form: its slices' chains may reach 2 kMaxChain (as each
   // launch of the hybrid's did), while the launch still fills the CUs twice
-  const int64_t n_pad = roundup(n, 128), blocks = (n_pad / 128) * (ldy % 512 == 0 ? ldy / 512 : 1);
+  const int64_t n_pad = roundup(n, 128), blocks = (n_pad / 128) * (ldy / 512);
   while (s > 2 && n_pad / (s / 2) <= 2 * kMaxChain && blocks * (s / 2) >= 512) s /= 2;
   return s;
 }

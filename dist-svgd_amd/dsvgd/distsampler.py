@@ -297,6 +297,7 @@ class DistSampler(object):
                                                                median=self._rbf.median))
 
     _routes_ok = None    # the pair split's point-to-point routes, checked once
+    _probe_corrupt = False   # tests: this rank's probe sees a wrong payload
 
     def _pair_split_routes(self, m):
         """The pair split exchanges transposed partials point to point; before
@@ -310,12 +311,51 @@ class DistSampler(object):
             P = PairSplitPlan(self._rank, self._num_shards, m)
             self._routes_ok = exchange.probe_p2p([q["dest"] for q in P.sends],
                                                  [q["src"] for q in P.recvs], self._rank,
-                                                 self._device, self._group)
+                                                 self._device, self._group,
+                                                 _corrupt=self._probe_corrupt)
             if not self._routes_ok:
                 warnings.warn("DistSampler: the pair-split layout's point-to-point probe "
                               "failed on this process group; using the row-block layout",
                               RuntimeWarning, stacklevel=4)
         return self._routes_ok
+
+    # the pair split's first step, checked against the row-block layout:
+    # max |phi_pair - phi_rows| / max |phi_rows| over every rank's owned rows
+    # (None until that step ran; inf when the routes or the check failed)
+    pair_split_check = None
+    PAIR_SPLIT_CHECK_TOL = 1e-5    # north_star's per-step phi tolerance
+    _check_corrupt = False         # tests: spoil this rank's pair-split phi before the check
+
+    def _check_pair_split(self, eng, run, X_own, step):
+        """the pair split's first step is checked against the
+        row-block layout on the live backend.  The row-block engine computes
+        phi of the owned rows without moving them, then the pair split runs
+        its real step (partials posted point to point, kernels in flight,
+        joined, finished with the update); the two phis are compared on every
+        rank and the verdict (MAX of the errors) is shared.  Above the
+        tolerance -- a mis-routed or stale partial, on any rank -- the owned
+        rows are reset and moved by the row-block phi, and every rank keeps
+        the row-block layout from then on, with a warning."""
+        rows_eng = PhiEngine(eng.n, self._d, m=eng.m, row0=eng.row0, device=self._device)
+        rows_eng.timer = self.timer
+        rows_eng.sample_share = eng.sample_share
+        run(rows_eng, 0.0, True)          # the row-block phi; particles unmoved
+        X0 = X_own.clone()
+        run(eng, step, True)              # the pair split's step
+        ref = rows_eng.phi
+        if self._check_corrupt:            # tests: a partial gone wrong on this rank
+            eng.phi[0, 0] += 1e3 * float(ref.abs().max())
+        err = ((eng.phi - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).double()
+        err = float(exchange.all_reduce_max(err.reshape(1), self._group)[0])
+        self.pair_split_check = err
+        if not err <= self.PAIR_SPLIT_CHECK_TOL:     # (a NaN fails too)
+            X_own.copy_(X0)
+            X_own.add_(ref, alpha=step)
+            self._routes_ok = False
+            self._engines = {(eng.n, eng.m, False, False): rows_eng}
+            warnings.warn("DistSampler: the pair-split layout's first step differs from the "
+                          "row-block layout's by %.3g of max|phi| on this process group; using "
+                          "the row-block layout" % err, RuntimeWarning, stacklevel=4)
 
     def _engine(self, n_int, m, row0):
         """One engine per (interacting set, owned rows, median kind, layout);
@@ -400,19 +440,27 @@ class DistSampler(object):
 
         if jacobi:
             eng = self._engine(n_int, ue - us, us - lo)
-            eng.pack(Xi)                           # X half only: the scores are in flight
-            eng.distances(median=median)
-            if median:
-                eng.median_bandwidth(hook)
+
+            def run(e, step, write_phi):
+                e.pack(Xi)                         # X half only: the scores are in flight
+                e.distances(median=median)
+                if median:
+                    e.median_bandwidth(hook)
+                else:
+                    e.fixed_bandwidth(self._rbf.h)
+                if side is not main:
+                    main.wait_stream(side)
+                e.pack_scores(Si)                  # Si already carries the score scale
+                p2p = None
+                if e.plan is not None:
+                    p2p = lambda sends, recvs: exchange.exchange_p2p_async(sends, recvs,
+                                                                           self._group)
+                e.direction(X[us:ue], step, write_phi=write_phi, extra=w2g, p2p=p2p)
+
+            if eng.plan is not None and self.pair_split_check is None:
+                self._check_pair_split(eng, run, X[us:ue], step_size)
             else:
-                eng.fixed_bandwidth(self._rbf.h)
-            if side is not main:
-                main.wait_stream(side)
-            eng.pack_scores(Si)                    # Si already carries the score scale
-            p2p = None
-            if eng.plan is not None:
-                p2p = lambda sends, recvs: exchange.exchange_p2p_async(sends, recvs, self._group)
-            eng.direction(X[us:ue], step_size, write_phi=self.keep_phi, extra=w2g, p2p=p2p)
+                run(eng, step_size, self.keep_phi)
         else:
             if median:
                 eng = self._engine(n_int, ue - us, us - lo)

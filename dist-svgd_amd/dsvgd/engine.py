@@ -516,6 +516,18 @@ class PhiEngine(object):
                        float(step), ex, lde, phi, self.d, xo, ldx, N.ptr(self.KY),
                        self.KY.numel(), s)
             return
+        if self.sym and self.phi_gemm == "h2":
+            # the slices were sized for the symmetric phi_mm form in force at
+            # construction (dsvgd_phi_splits_sym: longer slices for the
+            # one-launch form only); if the form was switched since
+            # (dsvgd_phi_set_symrow), re-size them for the current one
+            want = int(N.load().dsvgd_phi_splits_sym(self.n, self.ldy))
+            if want != self.splits:
+                self.splits = want
+                self.KY = torch.empty(want * self.m, self.ldy, dtype=torch.float32,
+                                      device=self.device)
+                self.rowsum = torch.empty(want * self.m_pad, dtype=torch.float32,
+                                          device=self.device)
         if self.phi_gemm == "h2":
             # the range guard word of the scales: phi_mm_h2 runs while it
             # reads 0; otherwise the FmtX3 image and phi_mm_x3 behind it do,

@@ -49,6 +49,18 @@ def all_reduce_sum(t, group=None):
     t.copy_(h.to(t.device))
 
 
+def all_reduce_max(t, group=None):
+    """In-place MAX over ranks (device tensors on RCCL, host staging on
+    gloo); returns t."""
+    if t.is_cuda and not _is_gloo(group):
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        return t
+    h = t.detach().cpu()
+    dist.all_reduce(h, op=dist.ReduceOp.MAX, group=group)
+    t.copy_(h.to(t.device))
+    return t
+
+
 def ring_shift(send, recv, rank, size, group=None):
     """send -> rank+1, recv <- rank-1   [distsampler.py:131-150].
 
@@ -104,11 +116,11 @@ def probe_p2p(send_peers, recv_peers, rank, device, group=None, _corrupt=False):
     for _ in range(3):                     # work queued between the post and the join
         busy = torch.mm(busy, busy) * (1.0 / 256)
     join()
+    if _corrupt and rb:
+        rb[0][0] += 1.0            # a wrong payload: the comparison below must catch it
     ok = True
     for t, p in zip(rb, recv_peers):
         ok = ok and bool(torch.equal(t, ramp + tag(p, rank)))
-    if _corrupt:
-        ok = False
     flag = torch.tensor([1 if ok else 0], dtype=torch.int64,
                         device=device if not _is_gloo(group) else "cpu")
     dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)

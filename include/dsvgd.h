@@ -392,11 +392,15 @@ int dsvgd_sqdist_h2(const void* Yg, const float* norms, int64_t row0, int64_t m,
  * re-run per pair by distsampler.py:97-99), Y's row and norms[] kept current
  * (centre c = center, the packing centre of Y).  Any d <= 1024 for kind 3. */
 int64_t dsvgd_gsw_block_rows(int64_t d, int score_kind);  /* 0 if d > 1024 */
-/* The walk's form for roundup(d, 32) <= 256 and score_kind 0 .. 2 (A/B switch,
- * returns the previous setting): 1 (default) = the incremental walk (each
- * moved row's pair terms added to every later row of the block at once, two
- * barriers per row, nothing per row on the path but the row's own phi);
- * 0 = the four-wave walk (distances and the column loop per row). */
+/* The walk's form for score_kind 0 .. 2 (A/B switch, returns the previous
+ * setting): 1 (default) = the incremental walk (each moved row's pair terms
+ * added to every later row of the block at once, two barriers per row,
+ * nothing per row on the path but the row's own phi) for roundup(d, 32) <=
+ * 1024 -- 1, 2 or 4 columns per thread up to 256, 512, 1024, blocks of at
+ * most 64, 32, 16 rows (B <= 64 / columns per thread), about 132 KB of LDS
+ * at every shape; 0 = the four-wave walk (distances and the column loop per
+ * row).  Where the incremental walk's LDS cannot be reserved the call runs
+ * the four-wave walk (no error). */
 int dsvgd_gsw_set_inc(int on);
 /* Timing probe of the walk (scripts/walk_probe.py; results are garbage while
  * set): bit 0 skips the next row's operand loads, bit 1 the distances, bit 2

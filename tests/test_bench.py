@@ -96,11 +96,14 @@ def test_bench_self_launch_two_ranks_gloo():
 
 @pytest.mark.gpu
 def test_bench_two_ranks_gloo():
-    """2 ranks sharing cuda:0, gloo exchange: the N>1 timing/reporting path."""
+    """2 ranks sharing cuda:0, gloo exchange: the N>1 timing/reporting path,
+    at a shape where the pair-split layout applies (d = 256, m = 4096), with
+    the self-describing multi-GPU keys: the layout each
+    rank ran, the route probe, the first-step check, per-rank exchange times."""
     env = _env()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29763", "bench.py", "--gpus", "2",
-           "--steps", "2", "--warmup", "1", "--particles", "4096", "--dim", "64",
+           "--steps", "2", "--warmup", "1", "--particles", "8192", "--dim", "256",
            "--data-rows", "1024", "--backend", "gloo"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -108,8 +111,16 @@ def test_bench_two_ranks_gloo():
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["steps"] == 2
-    assert out["config"]["particles_per_gpu"] == 2048
+    assert out["config"]["particles_per_gpu"] == 4096
     assert out["value"] > 0 and out["ms_per_step"] > 0
-    assert abs(out["value"] - 4096 * 2 / (out["ms_per_step"] * 2e-3)) < 1e-6 * out["value"]
+    assert abs(out["value"] - 8192 * 2 / (out["ms_per_step"] * 2e-3)) < 1e-6 * out["value"]
+    mg = out["multi_gpu"]
+    assert mg["world_size"] == 2 and mg["backend"] == "gloo"
+    assert mg["pair_split_engaged"] == [True, True] and mg["route_probe_ok"] == [True, True]
+    assert mg["pair_split_first_step_check"] <= mg["pair_split_check_tol"] == 1e-5
+    assert len(mg["exchange_ms_per_rank"]) == 2
+    for ex in mg["exchange_ms_per_rank"]:
+        for k in ("allgather_x", "allreduce_scores", "hist_allreduce", "partials_wait"):
+            assert k in ex and ex[k] >= 0.0
     assert out["roofline"]["traffic"] is None   # N=1 PMC summary is not quoted at N>1
     assert "cpu_baseline" not in out

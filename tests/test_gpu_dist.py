@@ -507,6 +507,110 @@ def test_rccl_world1_exchange_primitives():
         assert a == b and np.isfinite(a) and a > 0, out["median_h"]
 
 
+def _nccl_pair_split_worker(port, q):
+    """Both ranks of an S = 2 pair-split plan as two engines in ONE process
+    on a one-rank RCCL group: every message of the plan goes rank 0 -> rank 0
+    through exchange_p2p_async (batch_isend_irecv on the process group's
+    stream), matched in the plan's order, so the real direction() path runs
+    on RCCL -- partials computed and posted, the own window's kernels
+    enqueued between the post and the join, the received partials summed by
+    phi_finish_parts after it."""
+    import os
+    import sys
+    import torch.distributed as dist
+    from conftest import PKG, ROOT
+    for p in (ROOT, PKG):
+        sys.path.insert(0, p)
+    import dsvgd as m
+    from dsvgd import exchange
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    S, mm, d = 2, 2048, 256
+    n = S * mm
+    h = 2.0 * d * 0.01 / 8.0
+    eps = 1e-3
+    rs = np.random.RandomState(41)
+    X0 = (0.1 * rs.randn(n, d)).astype(np.float32)
+    S0 = rs.randn(n, d).astype(np.float32)
+    X = torch.tensor(X0, device=dev)
+    Sc = torch.tensor(S0, device=dev)
+    engs = [m.PhiEngine(n, d, m=mm, row0=r * mm, device=dev, pair_split=(r, S)) for r in range(S)]
+    own = [X[r * mm:(r + 1) * mm].clone() for r in range(S)]
+    for e in engs:
+        assert e.plan is not None
+        for b in e.recvbuf:
+            b.fill_(float("nan"))
+        e.pack(X, Sc)
+        e.distances(median=False)
+        e.fixed_bandwidth(h)
+    # rank 1's partials first (its exchange captured, not run) ...
+    captured = {}
+
+    def capture(sends, recvs):
+        captured["sends"] = sends
+        return lambda: None
+    engs[1].direction(own[1].clone(), 0.0, write_phi=True, p2p=capture)
+    # ... then rank 0's real step: its sends to rank 1 land in rank 1's
+    # receive buffers, rank 1's sends to rank 0 in rank 0's, each pair of
+    # (send, receive) posted in the plan's order on the one RCCL rank
+    posted = {}
+
+    def self_peered(sends, recvs):
+        P0, P1 = engs[0].plan, engs[1].plan
+        to0 = [t for t, dst in captured["sends"] if dst == 0]
+        from0 = [b for b, q_ in zip(engs[1].recvbuf, P1.recvs) if q_["src"] == 0]
+        out0 = [t for t, dst in sends if dst == 1]
+        in0 = [t for t, src in recvs if src == 1]
+        assert len(to0) == len(in0) and len(out0) == len(from0)
+        sl = [(t, 0) for t in to0] + [(t, 0) for t in out0]
+        rl = [(t, 0) for t in in0] + [(t, 0) for t in from0]
+        assert all(a.numel() == b.numel() for (a, _), (b, _) in zip(sl, rl))
+        posted["messages"] = len(sl)
+        return exchange.exchange_p2p_async(sl, rl)
+    engs[0].direction(own[0], eps, write_phi=True, p2p=self_peered)
+    # rank 1 finishes with the partials rank 0 sent it (no exchange of its own)
+    engs[1].direction(own[1], eps, write_phi=True, p2p=None)
+    torch.cuda.synchronize()
+    out = {"messages": posted.get("messages", 0),
+           "phi": [e.phi.cpu().numpy() for e in engs], "X1": [o.cpu().numpy() for o in own],
+           "h": [e.state.read()[1] for e in engs], "X0": X0, "S0": S0, "eps": eps}
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put(out)
+
+
+def test_rccl_world1_pair_split_direction():
+    """the pair split's real direction() path with
+    exchange_p2p_async on RCCL (both ranks of an S = 2 plan in one process,
+    every message self-peered on a one-rank group; the own window's kernels
+    run between the post and the join): phi of both row blocks and their
+    update against the fp64 oracle (1e-5 max-normalised)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_pair_split_worker, args=(29652, q))
+    p.start()
+    out = q.get(timeout=240)
+    p.join(60)
+    assert p.exitcode == 0
+    assert out["messages"] == 2
+    X0, S0, eps = out["X0"].astype(np.float64), out["S0"].astype(np.float64), out["eps"]
+    h = out["h"][0]
+    assert out["h"][1] == h
+    mm = X0.shape[0] // 2
+    for r in range(2):
+        rows = np.arange(r * mm, (r + 1) * mm)
+        ref = O.phi(X0, S0, h, rows=rows)
+        e = np.abs(out["phi"][r] - ref).max() / np.abs(ref).max()
+        assert e < 1e-5, (r, e)
+        X1 = out["X1"][r].astype(np.float64)
+        tol = eps * 1e-5 * np.abs(ref).max() + 2 * np.spacing(np.abs(X1).astype(np.float32)).max()
+        assert np.abs(X1 - (X0[rows] + eps * ref)).max() <= tol
+
+
 @pytest.mark.parametrize("S", [2, 4, 8])
 @pytest.mark.parametrize("mode", ["partitions", "all_particles", "all_scores"])
 @pytest.mark.parametrize("order", ["jacobi", "sequential"])

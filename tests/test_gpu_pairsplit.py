@@ -62,6 +62,8 @@ def _worker(rank, S, port, cfg, q):
                            exchange_particles=True, exchange_scores=False,
                            include_wasserstein=False, order="jacobi")
     ds.keep_phi = True
+    ds._probe_corrupt = cfg.get("probe_corrupt") == rank
+    ds._check_corrupt = cfg.get("check_corrupt") == rank
     ds.make_step(eps)
     torch.cuda.synchronize()
     eng = next(iter(ds._engines.values()))
@@ -73,6 +75,7 @@ def _worker(rank, S, port, cfg, q):
     Si = ds._scores if cfg["mode"] == "all_scores" else ds._sbuf
     out = {"rows": s0 + rows, "h": eng.state.read()[1], "median": eng.state.read()[0],
            "plan": eng.plan is not None, "guard": eng.range_guard(),
+           "check": ds.pair_split_check, "engines": len(ds._engines),
            "scores": Si[torch.as_tensor(s0 + rows, device=DEV)].cpu().numpy(),
            "phi": eng.phi[ridx].cpu().numpy(), "X1": ds.particles[ridx].cpu().numpy()}
     q.put((rank, out))
@@ -110,6 +113,14 @@ def _check(S, cfg, res):
     want = cfg.get("expect_plan", True)
     assert all(o["plan"] == want for _, o in res), "pair-split layout engaged: %s, expected %s" % (
         [o["plan"] for _, o in res], want)
+    assert all(o["engines"] == 1 for _, o in res)
+    checks = [o["check"] for _, o in res]
+    if cfg.get("check_corrupt") is not None:      # the first step's check caught it everywhere
+        assert all(c is not None and c > PHI_TOL for c in checks), checks
+    elif want:                                    # the first step's check passed everywhere
+        assert all(c is not None and c <= PHI_TOL for c in checks), checks
+    else:                                         # declined or the probe failed: never checked
+        assert all(c is None for c in checks), checks
     assert all(o["h"] == h for _, o in res)
     if cfg["h"] == "median":
         assert all(o["median"] == med for _, o in res)
@@ -213,3 +224,25 @@ def test_xcd_slice_maps_give_identical_bits():
             lib.dsvgd_phi_set_xmap(prev)
     for a, b in zip(out[7], out[0]):
         assert torch.equal(a, b)
+
+
+def test_pair_split_failed_route_probe_keeps_row_blocks():
+    """one rank's route probe sees a wrong payload (the received
+    buffer spoiled before the comparison): every rank keeps the row-block
+    layout from the first step on, and the step still matches the oracle."""
+    S, m = 2, 2048
+    cfg = dict(n=S * m, d=256, N=1024, eps=1e-3, seed=31, h="median", mode="all_scores",
+               nrows=48, expect_plan=False, probe_corrupt=1)
+    _check(S, cfg, _run(S, 29837, cfg))
+
+
+def test_pair_split_first_step_check_falls_back():
+    """the pair split's first step is checked against the
+    row-block layout on every rank (DistSampler._check_pair_split).  With one
+    rank's pair-split phi spoiled the shared verdict fails on both ranks, the
+    owned rows are moved by the row-block phi instead (the update matches the
+    oracle) and the row-block engine is the only one kept."""
+    S, m = 2, 2048
+    cfg = dict(n=S * m, d=256, N=1024, eps=1e-3, seed=33, h="median", mode="all_scores",
+               nrows=48, expect_plan=False, check_corrupt=0)
+    _check(S, cfg, _run(S, 29839, cfg))
