@@ -307,6 +307,26 @@ __global__ void gs_mask_kernel(float* __restrict__ D, int64_t ldd, int64_t r0, i
   }
 }
 
+// D[i][c0 + j] = +inf for i < B, j < nc: the pipelined wide sweep's pass of
+// group g + 1 runs while group g walks, so it leaves group g's columns out
+// (dsvgd_gsw_group_corr adds them at their moved positions afterwards)
+__global__ void gs_mask_cols_kernel(float* __restrict__ D, int64_t ldd, int64_t c0, int64_t nc) {
+  const int i = blockIdx.x;
+  for (int64_t j = threadIdx.x; j < nc; j += blockDim.x) {
+    const int64_t col = c0 + j;
+    D[((int64_t)(i >> 7) * (ldd >> 4) + (col >> 4)) * kPanelElems + (i & 127) * 16 + (col & 15)] =
+        INFINITY;
+  }
+}
+
+// test hook: one wave holds the stream for ns nanoseconds (s_memrealtime:
+// 100 MHz), so that work queued on another stream is in flight when the
+// kernels behind it start (the pipelined sweep's forced-overlap test)
+__global__ void debug_spin_kernel(int64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
 // The grouped wide sweep's correction: the wide pass of a group of blocks
 // left every pair (i, j) with j < i inside the group out (dsvgd_gs_mask over
 // the group), so once a block has walked, the group's later rows [r0, r0 +
@@ -1139,6 +1159,21 @@ int dsvgd_gs_mask(float* D, int64_t ldd, int64_t r0, int64_t B, void* stream) {
   hipLaunchKernelGGL(gs_mask_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, D, ldd,
                      r0, (int)B);
   return check_launch("gs_mask");
+}
+
+int dsvgd_gs_mask_cols(float* D, int64_t ldd, int64_t B, int64_t c0, int64_t nc, void* stream) {
+  DSVGD_REQUIRE(D, "null pointer");
+  DSVGD_REQUIRE(B > 0 && B <= 1024 && c0 >= 0 && nc > 0 && c0 + nc <= ldd && ldd % 128 == 0,
+                "sizes");
+  hipLaunchKernelGGL(gs_mask_cols_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, D,
+                     ldd, c0, nc);
+  return check_launch("gs_mask_cols");
+}
+
+int dsvgd_debug_spin(int64_t ns, void* stream) {
+  DSVGD_REQUIRE(ns >= 0 && ns <= 1000000000, "0 <= ns <= 1 s");
+  hipLaunchKernelGGL(debug_spin_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ns / 10);
+  return check_launch("debug_spin");
 }
 
 int dsvgd_gsw_group_corr(const float* X, int64_t ldx, const float* S, int64_t lds,

@@ -14,6 +14,7 @@
 
 #include "gemm_tiles.hpp"
 #include "gemm_x3.hpp"
+#include "gram_rs.hpp"
 #include "gram_w1.hpp"
 #include "select.hpp"
 
@@ -459,6 +460,98 @@ __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
   }
 }
 
+// The one-kernel Gram units (128 x 256, four candidate slots each) run on
+// gram_rs_kernel (split roles: MFMA waves + epilogue waves, gram_rs.hpp;
+// default) or gram_w1_kernel (one wave per SIMD, the epilogue between the
+// MFMAs); the same arguments, units, slots and D bits.  dsvgd_gram_set_rs.
+static int g_gram_rs = 1;
+
+template <int SM, bool SY>
+int launch_gram_units(const _Float16* Yg, int64_t img, const float* norms, const float* rsc,
+                      int64_t row0, int64_t m, int64_t n, int64_t n_pad, int nk, float* D,
+                      dsvgd_select_state* st, float* cand, int64_t tot, int Tm, int Tc, int jp_off,
+                      int64_t base, int64_t ns_total, int w2all, const float* gate, hipStream_t s) {
+  int bw = 0, rc = 0;
+  if (g_gram_rs) {
+    // the A/B probe variants (gram_rs.hpp VAR) exist for the headline's form only
+    auto launch = [&](auto VAR_) {
+      constexpr int VAR = decltype(VAR_)::value;
+      int r = persistent_blocks(reinterpret_cast<const void*>(&gram_rs_kernel<SM, SY, 0, VAR>),
+                                &bw, GramRS::kThreads);
+      if (r) return r;
+      hipLaunchKernelGGL((gram_rs_kernel<SM, SY, 0, VAR>), dim3((unsigned)bw),
+                         dim3(GramRS::kThreads), 0, s, Yg, img, norms, rsc, row0, m, n, n_pad, nk,
+                         D, st, cand, tot, Tm, Tc, jp_off, base, ns_total, w2all, gate, W2Out{});
+      return check_launch("gram_rs");
+    };
+    const int var = g_gram_rs - 1;
+    if constexpr (SM == kSelBracket && SY) {
+      if (var == 4) return launch(std::integral_constant<int, 4>{});
+    }
+    return launch(std::integral_constant<int, 0>{});
+  }
+  if ((rc = persistent_blocks(reinterpret_cast<const void*>(&gram_w1_kernel<SM, SY>), &bw,
+                              GramW1::kThreads)))
+    return rc;
+  hipLaunchKernelGGL((gram_w1_kernel<SM, SY>), dim3((unsigned)bw), dim3(GramW1::kThreads), 0, s, Yg,
+                     img, norms, rsc, row0, m, n, n_pad, nk, D, st, cand, tot, Tm, Tc, jp_off, base,
+                     ns_total, w2all, gate);
+  return check_launch("gram_w1");
+}
+
+// ---- the W2 cost on the split-role Gram (dsvgd_w2_cost_h2) -----------------
+// One wave per image row: rows [0, n) hold Y - c, rows [n_pad, n_pad + m) X - c
+// (c: Y's robust centre), zero-padded to dp columns; norms[row] = |row|^2 and
+// rsc[row] = the row's FmtH2 power-of-two scale (1 for a zero or padding row).
+__global__ __launch_bounds__(256) void w2_pack_kernel(const float* __restrict__ X, int64_t ldx,
+                                                      int64_t m, const float* __restrict__ Y,
+                                                      int64_t ldy, int64_t n, int64_t n_pad,
+                                                      int64_t rows, int d, int dp,
+                                                      const float* __restrict__ center,
+                                                      float* __restrict__ Yc,
+                                                      float* __restrict__ norms,
+                                                      float* __restrict__ rsc) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* src = nullptr;
+  if (row < n)
+    src = Y + row * ldy;
+  else if (row >= n_pad && row - n_pad < m)
+    src = X + (row - n_pad) * ldx;
+  float s2 = 0.f, mx = 0.f;
+  for (int c = lane; c < dp; c += 64) {
+    const float v = (src && c < d) ? src[c] - center[c] : 0.f;
+    Yc[row * dp + c] = v;
+    s2 = fmaf(v, v, s2);
+    mx = fmaxf(mx, fabsf(v));
+  }
+  s2 = warp_sum(s2);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if (lane == 0) {
+    norms[row] = s2;
+    rsc[row] = pow2_scale(mx);
+  }
+}
+
+struct W2CostWs {
+  int64_t n_pad, m_pad, dp, img, off_c, off_y, off_n, off_s, off_g, bytes;
+  W2CostWs(int64_t m, int64_t n, int64_t d) {
+    n_pad = roundup(n, 256);   // whole 256-column unit pairs
+    m_pad = roundup(m, 128);
+    dp = roundup(d, 256);      // the Gram's 16-K-step epilogue
+    img = n_pad + m_pad + 256;
+    auto al = [](int64_t b) { return roundup(b, 256); };
+    off_c = 0;
+    off_y = al(off_c + 4 * dp);
+    off_n = al(off_y + 4 * img * dp);
+    off_s = al(off_n + 4 * img);
+    off_g = al(off_s + 4 * img);
+    bytes = al(off_g + 2 * 2 * img * dp);
+  }
+};
+
 // Yg's image rows per part: the padded matrix plus one 256-row tile of slack
 // (a row block's last 256-row tile may start anywhere below n)
 int64_t gram_img_rows(int64_t n) { return roundup(n, 128) + 256; }
@@ -511,10 +604,6 @@ int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, 
   int64_t ns_total = 0;
   for (int i = 0; i < np; ++i)
     ns_total += w1part(parts[i]) ? w1walk(parts[i]).total() * GramW1::kSlots : parts[i].total * 8;
-  int bw = 0;
-  if (w1ok && (rc = persistent_blocks(reinterpret_cast<const void*>(&gram_w1_kernel<SM, true>), &bw,
-                                      GramW1::kThreads)))
-    return rc;
   int64_t base = 0;
   for (int i = 0; i < np; ++i) {
     const Part& P = parts[i];
@@ -522,16 +611,15 @@ int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, 
     if (w1part(P)) {
       const GramUnitWalk wk = w1walk(P);
       const int64_t tot = wk.total();
-#define DSVGD_GW1(SY)                                                                             \
-  hipLaunchKernelGGL((gram_w1_kernel<SM, SY>), dim3((unsigned)bw), dim3(GramW1::kThreads), 0, s,  \
-                     (const _Float16*)Yg, img, norms, rsc, row0, m, n, n_pad, nk * KS, D, st,     \
-                     cand, tot, wk.Tm, wk.Tc, P.bj_off, base, ns_total)
-      if (P.sym)
-        DSVGD_GW1(true);
-      else
-        DSVGD_GW1(false);
-#undef DSVGD_GW1
-      if ((rc = check_launch("gram_w1"))) return rc;
+      if constexpr (F::P == 2) {
+        rc = P.sym ? launch_gram_units<SM, true>((const _Float16*)Yg, img, norms, rsc, row0, m, n,
+                                                 n_pad, nk * KS, D, st, cand, tot, wk.Tm, wk.Tc,
+                                                 P.bj_off, base, ns_total, 0, nullptr, s)
+                   : launch_gram_units<SM, false>((const _Float16*)Yg, img, norms, rsc, row0, m,
+                                                  n, n_pad, nk * KS, D, st, cand, tot, wk.Tm,
+                                                  wk.Tc, P.bj_off, base, ns_total, 0, nullptr, s);
+        if (rc) return rc;
+      }
       base += tot * GramW1::kSlots;
       continue;
     }
@@ -570,15 +658,9 @@ int launch_sqdist_h2_parts(const _Float16* Yg, const float* norms, int64_t row0,
   const int64_t img = gram_img_rows(n);
   constexpr int KS = kGramKS;
   const int nk = (int)(dp / kX3Step / KS);
-  int rc = 0, bs = 0, bw = 0, bg = 0;
+  int rc = 0, bs = 0;
   if ((rc = persistent_blocks(
            reinterpret_cast<const void*>(&sqdist_x3w_kernel<true, SM, false, F, KS>), &bs, 512)))
-    return rc;
-  if ((rc = persistent_blocks(reinterpret_cast<const void*>(&gram_w1_kernel<SM, false>), &bw,
-                              GramW1::kThreads)))
-    return rc;
-  if ((rc = persistent_blocks(reinterpret_cast<const void*>(&gram_w1_kernel<kSelNone, false>),
-                              &bg, GramW1::kThreads)))
     return rc;
   auto walk = [&](const dsvgd_gram_part& P) {
     return GramUnitWalk((int)(P.rows / 128), (int)(P.cols / 256), false);
@@ -608,18 +690,17 @@ int launch_sqdist_h2_parts(const _Float16* Yg, const float* norms, int64_t row0,
     const int64_t tot = wk.total();
     float* Dp = D + P.row_off * n_pad;  // panel rows of the part's strips
     if (P.kind == 0) {
-      hipLaunchKernelGGL((gram_w1_kernel<SM, false>), dim3((unsigned)bw), dim3(GramW1::kThreads), 0,
-                         s, Yg, img, norms, rsc, row0 + P.row_off, P.rows, n, n_pad, nk * KS, Dp,
-                         st, cand, tot, wk.Tm, wk.Tc, (int)(P.col0 / 256), base, ns_total,
-                         (int)P.weight2, (const float*)nullptr);
+      rc = launch_gram_units<SM, false>(Yg, img, norms, rsc, row0 + P.row_off, P.rows, n, n_pad,
+                                        nk * KS, Dp, st, cand, tot, wk.Tm, wk.Tc,
+                                        (int)(P.col0 / 256), base, ns_total, (int)P.weight2,
+                                        nullptr, s);
       base += tot * GramW1::kSlots;
     } else {
-      hipLaunchKernelGGL((gram_w1_kernel<kSelNone, false>), dim3((unsigned)bg),
-                         dim3(GramW1::kThreads), 0, s, Yg, img, norms, rsc, row0 + P.row_off,
-                         P.rows, n, n_pad, nk * KS, Dp, st, (float*)nullptr, tot, wk.Tm, wk.Tc,
-                         (int)(P.col0 / 256), (int64_t)0, (int64_t)0, 0, gate);
+      rc = launch_gram_units<kSelNone, false>(Yg, img, norms, rsc, row0 + P.row_off, P.rows, n,
+                                              n_pad, nk * KS, Dp, st, nullptr, tot, wk.Tm, wk.Tc,
+                                              (int)(P.col0 / 256), 0, 0, 0, gate, s);
     }
-    if ((rc = check_launch("gram_w1(part)"))) return rc;
+    if (rc) return rc;
   }
   return 0;
 }
@@ -846,6 +927,63 @@ int dsvgd_sqdist_h2(const void* Yg, const float* norms, int64_t row0, int64_t m,
       return launch_sqdist_x3<kSelBracket, FmtH2>(yg, norms, row0, m, n, d, D, st, cand, layout, s,
                                                   rowscale);
   }
+}
+
+size_t dsvgd_w2_cost_h2_workspace_bytes(int64_t m, int64_t n, int64_t d) {
+  if (m <= 0 || n <= 0 || d <= 0) return 0;
+  return (size_t)W2CostWs(m, n, d).bytes;
+}
+
+int dsvgd_w2_cost_h2(const float* X, int64_t ldx, int64_t m, const float* Y, int64_t ldy,
+                     int64_t n, int64_t d, float* C, int64_t ldc, void* ws, float tau,
+                     void* stream) {
+  DSVGD_REQUIRE(X && Y && C && ws, "null pointer");
+  DSVGD_REQUIRE(m > 0 && n > 0 && d > 0 && d <= 1024 && ldx >= d && ldy >= d, "sizes (d <= 1024)");
+  const W2CostWs w(m, n, d);
+  DSVGD_REQUIRE(ldc >= w.n_pad && ldc % 4 == 0 && ((uintptr_t)C & 15) == 0,
+                "C: ldc >= roundup(n, 256), a multiple of 4, 16-byte aligned rows");
+  DSVGD_REQUIRE(((uintptr_t)ws & 255) == 0, "workspace: 256-byte aligned");
+  DSVGD_REQUIRE(w.dp * w.img * 4 < ((int64_t)1 << 31) && 127 * ldc * 4 + 1024 < ((int64_t)1 << 31),
+                "too large for the Gram's 32-bit offsets");
+  DSVGD_REQUIRE(tau >= 0.f && tau <= 1.f, "tau in [0, 1]");
+  hipStream_t s = (hipStream_t)stream;
+  char* base = (char*)ws;
+  float* cen = (float*)(base + w.off_c);
+  float* Yc = (float*)(base + w.off_y);
+  float* nrm = (float*)(base + w.off_n);
+  float* rs = (float*)(base + w.off_s);
+  void* Yg = base + w.off_g;
+  int rc = dsvgd_colcenter(Y, ldy, n, d, cen, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(w2_pack_kernel, dim3((unsigned)((w.img + 3) / 4)), dim3(256), 0, s, X, ldx, m,
+                     Y, ldy, n, w.n_pad, w.img, (int)d, (int)w.dp, cen, Yc, nrm, rs);
+  if ((rc = check_launch("w2_pack"))) return rc;
+  if ((rc = dsvgd_h2_rowsplit_rows(Yc, w.dp, w.img, w.dp, w.img, w.dp, rs, Yg, stream))) return rc;
+  const GramUnitWalk wk((int)(w.m_pad / 128), (int)(w.n_pad / 256), false);
+  W2Out wo;
+  wo.X = X;
+  wo.Y = Y;
+  wo.ldx = ldx;
+  wo.ldy = ldy;
+  wo.ldc = ldc;
+  wo.d = (int)d;
+  wo.tau = tau;
+  int bw = 0;
+  if ((rc = persistent_blocks(reinterpret_cast<const void*>(&gram_rs_kernel<kSelNone, false, 1>),
+                              &bw, GramRS::kThreads)))
+    return rc;
+  hipLaunchKernelGGL((gram_rs_kernel<kSelNone, false, 1>), dim3((unsigned)bw),
+                     dim3(GramRS::kThreads), 0, s, (const _Float16*)Yg, w.img, nrm, rs, w.n_pad, m,
+                     n, w.n_pad, (int)(w.dp / 16), C, (dsvgd_select_state*)nullptr,
+                     (float*)nullptr, wk.total(), wk.Tm, wk.Tc, 0, (int64_t)0, (int64_t)0, 0,
+                     (const float*)nullptr, wo);
+  return check_launch("gram_rs(w2 cost)");
+}
+
+int dsvgd_gram_set_rs(int on) {
+  const int prev = g_gram_rs;
+  g_gram_rs = on < 0 ? 0 : (on > 5 ? 1 : on);
+  return prev;
 }
 
 int dsvgd_sqdist_h2_parts(const void* Yg, const float* norms, int64_t row0, int64_t m, int64_t n,

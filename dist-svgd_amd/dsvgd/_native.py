@@ -67,6 +67,7 @@ SIGNATURES = {
     "dsvgd_set_bandwidth": (_int, [_p, _f, _p]),
     "dsvgd_phi_splits": (_i64, [_i64, _i64, _i64]),
     "dsvgd_phi_set_symrow": (_int, [_int]),
+    "dsvgd_gram_set_rs": (_int, [_int]),
     "dsvgd_phi_splits_sym": (_i64, [_i64, _i64]),
     "dsvgd_phi_set_xmap": (_int, [_int]),
     "dsvgd_gsw_set_inc": (_int, [_int]),
@@ -111,6 +112,8 @@ SIGNATURES = {
                                     _p, _i64, _p, _i64, _int, _p, _p, _f, _p]),
     "dsvgd_w2_cost": (_int, [_p, _i64, _i64, _p, _i64, _i64, _i64, _p, _i64, _p]),
     "dsvgd_w2_workspace_bytes": (_c.c_size_t, [_i64, _i64]),
+    "dsvgd_w2_cost_h2_workspace_bytes": (_c.c_size_t, [_i64, _i64, _i64]),
+    "dsvgd_w2_cost_h2": (_int, [_p, _i64, _i64, _p, _i64, _i64, _i64, _p, _i64, _p, _c.c_float, _p]),
     "dsvgd_w2_assign": (_int, [_p, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p]),
     "dsvgd_w2_assign_warm": (_int, [_p, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p]),
     "dsvgd_w2_trace": (_i64, [_p, _i64]),
@@ -137,6 +140,8 @@ SIGNATURES = {
     "dsvgd_h2_rowsplit_rows_range": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _p, _p, _i64, _i64,
                                             _p]),
     "dsvgd_gs_mask": (_int, [_p, _i64, _i64, _i64, _p]),
+    "dsvgd_gs_mask_cols": (_int, [_p, _i64, _i64, _i64, _i64, _p]),
+    "dsvgd_debug_spin": (_int, [_i64, _p]),
     "dsvgd_gsw_group_corr": (_int, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _i64,
                                     _p, _p, _i64, _p, _p]),
     "dsvgd_gsw_block_sweep": (_int, [_p, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64,

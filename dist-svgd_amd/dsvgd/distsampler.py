@@ -339,7 +339,7 @@ class DistSampler(object):
         rows_eng = PhiEngine(eng.n, self._d, m=eng.m, row0=eng.row0, device=self._device)
         rows_eng.timer = self.timer
         rows_eng.sample_share = eng.sample_share
-        run(rows_eng, 0.0, True)          # the row-block phi; particles unmoved
+        run(rows_eng, 0.0, True, move=False)   # the row-block phi; particles unmoved
         X0 = X_own.clone()
         run(eng, step, True)              # the pair split's step
         ref = rows_eng.phi
@@ -441,7 +441,7 @@ class DistSampler(object):
         if jacobi:
             eng = self._engine(n_int, ue - us, us - lo)
 
-            def run(e, step, write_phi):
+            def run(e, step, write_phi, move=True):
                 e.pack(Xi)                         # X half only: the scores are in flight
                 e.distances(median=median)
                 if median:
@@ -455,7 +455,8 @@ class DistSampler(object):
                 if e.plan is not None:
                     p2p = lambda sends, recvs: exchange.exchange_p2p_async(sends, recvs,
                                                                            self._group)
-                e.direction(X[us:ue], step, write_phi=write_phi, extra=w2g, p2p=p2p)
+                e.direction(X[us:ue] if move else None, step, write_phi=write_phi, extra=w2g,
+                            p2p=p2p)
 
             if eng.plan is not None and self.pair_split_check is None:
                 self._check_pair_split(eng, run, X[us:ue], step_size)

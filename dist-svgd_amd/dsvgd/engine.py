@@ -1050,6 +1050,12 @@ class _WideSweep(object):
         self.rowsum = torch.empty(z * gpad, **f32)
         self.Q = torch.empty(self.GB, self.ldy, **f32)
         self.Qr = torch.empty(gpad, **f32)
+        # the pipelined sweep (GSW_PIPELINE): group g + 1's sums beside group
+        # g's, the norms snapshot its wide pass reads, its stream
+        self.Q2 = torch.empty(self.GB, self.ldy, **f32)
+        self.Qr2 = torch.empty(gpad, **f32)
+        self.norms_s = torch.empty_like(self.norms)
+        self.side = None
 
     def images(self, r0, nr, s):
         """(Re)split rows [r0, r0 + nr) of Y into the engines' images (the
@@ -1073,6 +1079,11 @@ class _WideSweep(object):
 
 
 _WIDE = {}
+# the pipelined wide sweep (round 6): group g + 1's wide pass on a second
+# stream while group g walks, group g's columns left out of it and added at
+# their moved positions by dsvgd_gsw_group_corr before g + 1 walks
+GSW_PIPELINE = True
+GSW_PIPE_SPIN_NS = 0   # tests: hold the walk's stream this long after each pass is posted
 # blocks per wide pass of the wide Gauss-Seidel sweep (1: block after block;
 # config D sweep 278.7 / 253.0 / 256.2 ms at 1 / 2 / 4, profiles/r13u; None:
 # as many blocks as make about 128 rows)
@@ -1104,6 +1115,11 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
            W.Y.shape[0], N.ptr(W.Y), W.ldy, N.ptr(W.norms), s)
     W.images(0, W.n_pad, s)
     B, GB = W.B, W.GB
+    groups = [(g0, min(GB, rows.stop - g0)) for g0 in range(rows.start, rows.stop, GB)]
+    if GSW_PIPELINE and len(groups) >= 2:
+        _pipelined_sweep_wide(W, X, S, groups, n, d, h_state, step, sk, mu, lam, xd, td,
+                              score_scale, phi_out, extra, rows.start, s)
+        return
     for g0 in range(rows.start, rows.stop, GB):
         gn = min(GB, rows.stop - g0)
         # the group's wide pass: every row against every row not moved before
@@ -1144,6 +1160,101 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
         # the group's moved rows into the images once, after its last walk:
         # only the next groups' wide passes read them (the walks read Y, the
         # correction X and S)
+        W.images(g0, gn, s)
+
+
+def _gsw_pass(W, g0, gn, n, d, h_state, norms, Q, Qr, s, exclude=None):
+    """The wide pass of the group's rows [g0, g0 + gn) against every row not
+    moved before them in the group (and, pipelined, not in the `exclude` =
+    (p0, pn) group walking beside it): Q = [K Xc | K S], Qr = K 1."""
+    if W.gram_h2:
+        N.call("dsvgd_sqdist_h2", N.ptr(W.Yg), N.ptr(norms), g0, gn, n, d, N.ptr(W.D),
+               W.n_pad, 0, None, None, 0, N.ptr(W.rsc), s)
+    else:
+        N.call("dsvgd_sqdist", N.ptr(W.Y), W.ldy, N.ptr(norms), g0, gn, n, d, N.ptr(W.D),
+               W.n_pad, 0, None, None, s)
+    N.call("dsvgd_gs_mask", N.ptr(W.D), W.n_pad, g0, gn, s)
+    if exclude is not None:
+        N.call("dsvgd_gs_mask_cols", N.ptr(W.D), W.n_pad, gn, exclude[0], exclude[1], s)
+    if W.phi_x3:
+        N.call("dsvgd_phi_mm_x3", N.ptr(W.D), W.n_pad, N.ptr(W.Yx3), W.ldy, g0, gn, n,
+               h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), 0, int(W.m16),
+               None, s)
+    else:
+        N.call("dsvgd_phi_mm", N.ptr(W.D), W.n_pad, N.ptr(W.Y), W.ldy, g0, gn, n,
+               h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), s)
+    N.call("dsvgd_phi_partial_reduce", N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), W.splits, gn,
+           2 * W.dp, N.ptr(Q), W.ldy, N.ptr(Qr), s)
+
+
+def _pipelined_sweep_wide(W, X, S, groups, n, d, h_state, step, sk, mu, lam, xd, td,
+                          score_scale, phi_out, extra, r_start, s):
+    """The wide blocked sweep with group g + 1's wide pass on a second stream
+    beside group g's walk.  What the two streams share, and why it is safe:
+
+      * the side stream alone writes D, KY, rowsum (its passes in order) and
+        the sums Qs[(g + 1) % 2]; the walk of g reads Qs[g % 2];
+      * the pass of g + 1 reads the images (Yg, rsc, Yx3) and a SNAPSHOT of
+        the norms taken after group g - 1's images were re-split: the walk of
+        g rewrites Y / norms / X rows of group g, the images of g are re-split
+        only after the pass of g + 1 is done (it masked those columns);
+      * before g + 1 walks, its sums gain group g's rows at their moved
+        positions (dsvgd_gsw_group_corr, block by block, on the walk's stream).
+
+    The same terms as the block-after-block sweep, in another order
+    (tests/test_gpu_parity.py: against the fp64 restatement, the overlap
+    forced)."""
+    dev = X.device
+    main = torch.cuda.current_stream(dev)
+    if W.side is None:
+        W.side = torch.cuda.Stream(device=dev)
+    side = W.side
+    B = W.B
+    Qs = ((W.Q, W.Qr), (W.Q2, W.Qr2))
+    done = [None] * len(groups)
+
+    def post(k):
+        g0, gn = groups[k]
+        W.norms_s.copy_(W.norms)          # on the walk's stream, after group k - 2's images
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            _gsw_pass(W, g0, gn, n, d, h_state, W.norms_s, *Qs[k % 2], side.cuda_stream,
+                      exclude=groups[k - 1] if k > 0 else None)
+            done[k] = side.record_event()
+
+    post(0)
+    for k, (g0, gn) in enumerate(groups):
+        Q, Qr = Qs[k % 2]
+        main.wait_event(done[k])
+        if k > 0:   # the previous group's moved rows, left out of this pass
+            p0, pn = groups[k - 1]
+            for b0 in range(p0, p0 + pn, B):
+                nb = min(B, p0 + pn - b0)
+                N.call("dsvgd_gsw_group_corr", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S),
+                       N.ptr(W.mean), n, d, g0, gn, b0, nb, h_state.ptr, N.ptr(Q), W.ldy,
+                       N.ptr(Qr), s)
+        if k + 1 < len(groups):
+            post(k + 1)
+            if GSW_PIPE_SPIN_NS:
+                N.call("dsvgd_debug_spin", int(GSW_PIPE_SPIN_NS), s)
+        for b0 in range(g0, g0 + gn, B):
+            nb = min(B, g0 + gn - b0)
+            k0, q0 = b0 - r_start, b0 - g0
+            ex = N.ptr(extra[k0:k0 + nb]) if extra is not None else None
+            po = N.ptr(phi_out[k0:k0 + nb]) if phi_out is not None else None
+            N.call("dsvgd_gsw_block_sweep", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S), N.ptr(W.Y),
+                   W.ldy, N.ptr(W.norms), N.ptr(W.mean), n, d, b0, nb, h_state.ptr, float(step),
+                   N.ptr(Q) + 4 * q0 * W.ldy, W.ldy, N.ptr(Qr) + 4 * q0, ex, d, po,
+                   N.ld(phi_out) if phi_out is not None else d, sk, N.ptr(mu), N.ptr(lam),
+                   float(score_scale), N.ptr(xd), N.ld(xd) if xd is not None else d, N.ptr(td),
+                   td.numel() if td is not None else 0, s)
+            r1 = b0 + nb
+            if r1 < g0 + gn:
+                N.call("dsvgd_gsw_group_corr", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S),
+                       N.ptr(W.mean), n, d, r1, g0 + gn - r1, b0, nb, h_state.ptr,
+                       N.ptr(Q) + 4 * (r1 - g0) * W.ldy, W.ldy, N.ptr(Qr) + 4 * (r1 - g0), s)
+        if k + 1 < len(groups):
+            main.wait_event(done[k + 1])  # the next pass has read this group's old images
         W.images(g0, gn, s)
 
 

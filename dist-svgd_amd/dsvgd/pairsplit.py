@@ -42,6 +42,10 @@ def _cyclic(c0, length, n):
 
 class PairSplitPlan(object):
     GRAM_RECT, GRAM_DIAG, GRAM_FALLBACK = 0, 1, 2
+    # the diagonal square as one full rectangle on the one-kernel Gram (both
+    # triangles computed, each entry counted once) instead of its upper tiles
+    # on the 8-wave kernel with mirror stores (round 6, A/B)
+    FULL_SQUARE = False
 
     @staticmethod
     def aligned(S, m):
@@ -75,7 +79,8 @@ class PairSplitPlan(object):
 
         # Gram parts (include/dsvgd.h dsvgd_gram_part): accounted, then the
         # fallback-only complement (the range guard's whole-row-block phi)
-        parts = [dict(row_off=0, rows=m, col0=r0, cols=m, kind=self.GRAM_DIAG, weight2=0)]
+        parts = [dict(row_off=0, rows=m, col0=r0, cols=m,
+                      kind=self.GRAM_RECT if self.FULL_SQUARE else self.GRAM_DIAG, weight2=0)]
         for c0, ln in _cyclic(r0 + m, self.window[1] - m, n):
             parts.append(dict(row_off=0, rows=m, col0=c0, cols=ln, kind=self.GRAM_RECT, weight2=1))
         if self.high:

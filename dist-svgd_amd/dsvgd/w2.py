@@ -33,13 +33,37 @@ class W2Term(object):
     # without, the cold one 3.95 vs 4.04 s (profiles/r11g/w2.log)
     KEEP = False
     THETA = 8.0   # eps divisor between phases (dsvgd_w2_set_theta)
+    # the cost matrix: "h2" on the split-role MFMA Gram with the near pairs
+    # recomputed exactly (dsvgd_w2_cost_h2), "exact" the explicit-difference
+    # VALU tiles (dsvgd_w2_cost), "auto" h2 from H2_MIN_ENTRIES entries on
+    # (smaller plans: the VALU tiles take microseconds) for 2 < d <= 1024
+    COST = "auto"
+    H2_MIN_ENTRIES = 1 << 22
+    # an entry is recomputed from explicit differences when its Gram form is
+    # below TAU (|x_i - c|^2 + |y_j - c|^2): there the form's error bound
+    # (~2^-21 of that sum) exceeds 2^-19 of the entry
+    TAU = 0.25
 
     def __init__(self, m, n, d, device, warm=True):
         if n % m:
             raise ValueError("W2 term needs n to be a multiple of m (n = R m)")
         self.m, self.n, self.d = m, n, d
         self.device = torch.device(device)
-        self.C = torch.empty((m, n), dtype=torch.float32, device=self.device)
+        lib = N.load()
+        mode = self.COST
+        if mode == "auto":
+            mode = "h2" if (m * n >= self.H2_MIN_ENTRIES and 2 < d <= 1024) else "exact"
+        self.cost = mode
+        if mode == "h2":
+            # whole 128-row x 256-column tiles are written (padding included)
+            self.ldc = -(-n // 256) * 256
+            self.C = torch.empty((-(-m // 128) * 128, self.ldc), dtype=torch.float32,
+                                 device=self.device)
+            nb = int(lib.dsvgd_w2_cost_h2_workspace_bytes(m, n, d))
+            self.cws = torch.empty(nb + 256, dtype=torch.uint8, device=self.device)
+        else:
+            self.ldc = n
+            self.C = torch.empty((m, n), dtype=torch.float32, device=self.device)
         nbytes = int(N.load().dsvgd_w2_workspace_bytes(m, n))
         self.ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
         self.assign = torch.empty(n, dtype=torch.int32, device=self.device)
@@ -53,19 +77,25 @@ class W2Term(object):
         previous particles Y (n, d).  Blocks until the auction has converged."""
         assert X.shape == (self.m, self.d) and Y.shape == (self.n, self.d)
         s = N.stream(self.device)
-        N.call("dsvgd_w2_cost", N.ptr(X), N.ld(X), self.m, N.ptr(Y), N.ld(Y), self.n, self.d,
-               N.ptr(self.C), self.n, s)
+        if self.cost == "h2":
+            ws = N.ptr(self.cws)
+            ws = (ws + 255) // 256 * 256
+            N.call("dsvgd_w2_cost_h2", N.ptr(X), N.ld(X), self.m, N.ptr(Y), N.ld(Y), self.n,
+                   self.d, N.ptr(self.C), self.ldc, ws, float(self.TAU), s)
+        else:
+            N.call("dsvgd_w2_cost", N.ptr(X), N.ld(X), self.m, N.ptr(Y), N.ld(Y), self.n, self.d,
+                   N.ptr(self.C), self.ldc, s)
         rounds = ctypes.c_int64(0)
         N.load().dsvgd_w2_set_keep(int(bool(self.KEEP)))    # returns the old setting
         N.load().dsvgd_w2_set_theta(float(self.THETA))
         if self.warm and self._solved and self.WARM_PHASES is None:
             # prev and out may alias: the plan is only written after the solve
-            N.call("dsvgd_w2_assign_warm", N.ptr(self.C), self.n, self.m, self.n,
+            N.call("dsvgd_w2_assign_warm", N.ptr(self.C), self.ldc, self.m, self.n,
                    N.ptr(self.ws), self.MAX_ROUNDS, N.ptr(self.assign), N.ptr(self.assign),
                    ctypes.addressof(rounds), s)
         else:
             warm = (self.WARM_PHASES or 0) if (self.warm and self._solved) else 0
-            N.call("dsvgd_w2_assign", N.ptr(self.C), self.n, self.m, self.n, N.ptr(self.ws),
+            N.call("dsvgd_w2_assign", N.ptr(self.C), self.ldc, self.m, self.n, N.ptr(self.ws),
                    self.MAX_ROUNDS, warm, N.ptr(self.assign), ctypes.addressof(rounds), s)
         self.rounds = int(rounds.value)
         self._solved = True

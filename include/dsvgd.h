@@ -238,6 +238,13 @@ int64_t dsvgd_phi_splits(int64_t m, int64_t n, int64_t ldy);
  * contiguous K ranges ascending, transposed K-steps first (phi_w1 DS 4);
  * 0 = two launches split at each row block's diagonal tile (DS 1 + DS 2). */
 int dsvgd_phi_set_symrow(int on);
+/* The one-kernel FmtH2 Gram units (dsvgd_sqdist_h2, dsvgd_sqdist_h2_parts):
+ * 1 (default) = gram_rs_kernel, split roles -- four waves issue only the
+ * MFMAs, four waves stage the strip image and write the previous tile's
+ * epilogue (D values, bracket accounting, stores) from an LDS hand-off;
+ * 0 = gram_w1_kernel, one wave per SIMD with the epilogue between its MFMAs.
+ * Identical D and candidates.  Returns the previous setting (A/B switch). */
+int dsvgd_gram_set_rs(int on);
 /* The split-K slices of the symmetric layout's phi_mm (n x n, the engine's
  * KY / rowsum hold this many): dsvgd_phi_splits, or with the one-launch form
  * half as many while each fp32 chain stays within 2 x 16384 columns and the
@@ -407,6 +414,14 @@ int dsvgd_gsw_set_inc(int on);
  * the column loop.  Process-wide; returns the previous mask.  0 = normal. */
 int dsvgd_gsw_debug(int mask);
 int dsvgd_gs_mask(float* D, int64_t ldd, int64_t r0, int64_t B, void* stream);
+/* D[i][c0 + j] = +inf for i < B (<= 1024), j < nc (panel layout): the
+ * pipelined wide sweep (round 6) leaves the group walking beside a wide pass
+ * out of that pass; dsvgd_gsw_group_corr adds its rows at their moved
+ * positions afterwards. */
+int dsvgd_gs_mask_cols(float* D, int64_t ldd, int64_t B, int64_t c0, int64_t nc, void* stream);
+/* Test hook: one wave holds `stream` for ns nanoseconds (the pipelined
+ * sweep's forced-overlap test). */
+int dsvgd_debug_spin(int64_t ns, void* stream);
 /* The grouped wide sweep (round 5): one wide pass for a group of blocks
  * (dsvgd_gs_mask over the whole group, B <= 1024), then after each block's
  * walk the group's later rows [r0, r0 + nr) gain that block's pB <= 64 moved
@@ -617,6 +632,20 @@ int dsvgd_gs_block_sweep(float* X, int64_t ldx, float* S, int64_t lds, int64_t n
  * (distsampler.py:107-114). */
 int dsvgd_w2_cost(const float* X, int64_t ldx, int64_t m, const float* Y, int64_t ldy, int64_t n,
                   int64_t d, float* C, int64_t ldc, void* stream);
+/* The same C on the FmtH2 split-role Gram (ABI 4, round 6): C_ij = |x_i -
+ * c|^2 + |y_j - c|^2 - 2 (x_i - c).(y_j - c) (c: Y's robust centre,
+ * dsvgd_colcenter) on the fp16 MFMAs, fp32-accurate per the FmtH2 bound
+ * (|error| ~ 2^-21 (|x_i - c|^2 + |y_j - c|^2)), and every entry below
+ * tau (|x_i - c|^2 + |y_j - c|^2) -- where that form cancels, e.g. a particle
+ * and its own previous position -- recomputed from explicit fp32
+ * differences in dsvgd_w2_cost's order (the same bits).  C needs
+ * roundup(m, 128) rows and ldc >= roundup(n, 256) (16-byte aligned rows;
+ * the padding is written); ws: dsvgd_w2_cost_h2_workspace_bytes, 256-byte
+ * aligned.  d <= 1024. */
+size_t dsvgd_w2_cost_h2_workspace_bytes(int64_t m, int64_t n, int64_t d);
+int dsvgd_w2_cost_h2(const float* X, int64_t ldx, int64_t m, const float* Y, int64_t ldy,
+                     int64_t n, int64_t d, float* C, int64_t ldc, void* ws, float tau,
+                     void* stream);
 /* Device workspace of dsvgd_w2_assign (32 n + 256 bytes). */
 size_t dsvgd_w2_workspace_bytes(int64_t m, int64_t n);
 /* assign[s] = column of slot s in an optimal plan (replaces scipy linprog,

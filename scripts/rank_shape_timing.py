@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--set", action="append", default=[],
                     help="pairs: NAME=v1,v2 sweeps a PhiEngine split override "
                          "(W_SPLITS, H_SPLITS, REST_SPLITS; 0 = chosen)")
+    ap.add_argument("--square", default=None,
+                    help="pairs: comma list of PairSplitPlan.FULL_SQUARE settings (0, 1)")
     ap.add_argument("--mode", default="timer",
                     help="comma list: timer (stage events), plain (no events), graph (the step "
                          "captured as one HIP graph and replayed: the launch gaps' bound)")
@@ -54,6 +56,8 @@ def main():
     for spec in args.set:
         k, vals = spec.split("=")
         overrides = [dict(o, **{k: int(v)}) for o in overrides for v in vals.split(",")]
+    if args.square:
+        overrides = [dict(o, FULL_SQUARE=int(v)) for o in overrides for v in args.square.split(",")]
     for S in [int(v) for v in args.shards.split(",")]:
         for lay in (("rows", "pairs") if args.layout == "both" else (args.layout,)):
             if lay == "rows":
@@ -69,6 +73,8 @@ def main():
         ov = ovl[0] if ovl else {}
         for k in ("W_SPLITS", "H_SPLITS", "REST_SPLITS"):
             setattr(dsvgd.PhiEngine, k, ov.get(k) or None)
+        from dsvgd.pairsplit import PairSplitPlan
+        PairSplitPlan.FULL_SQUARE = bool(ov.get("FULL_SQUARE", PairSplitPlan.FULL_SQUARE))
         dsvgd.PhiEngine.WINDOW_SIDE_STREAM = side
         dsvgd.PhiEngine.REST_BESIDE = rest
         dsvgd.PhiEngine.FWD_ZSPLIT = fz or None
@@ -143,7 +149,8 @@ def main():
                           "t_splits": getattr(eng, "t_splits", None),
                           "row0": r * m, "N_local": per,
                           "ms_per_step_no_comm": e0.elapsed_time(e1) / args.steps,
-                          "sym_layout": bool(eng.sym), "stages_ms": st}), flush=True)
+                          "sym_layout": bool(eng.sym), "full_square": bool(ov.get("FULL_SQUARE", 0)),
+                          "stages_ms": st}), flush=True)
           eng.timer = None
         del eng
         torch.cuda.empty_cache()

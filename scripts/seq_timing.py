@@ -37,6 +37,10 @@ def main():
     ap.add_argument("--splits", default=None,
                     help="comma list of engine.GSW_SPLITS values (0: chosen): the blocked "
                          "sweep alone timed for each")
+    ap.add_argument("--pipe", default=None,
+                    help="comma list of engine.GSW_PIPELINE values (1: the pipelined wide "
+                         "sweep, 0: block group after group): the blocked sweep alone timed "
+                         "for each, the results compared")
     ap.add_argument("--rows-sample", type=int, default=2048,
                     help="rows of the per-row path to time (0: skip it)")
     args = ap.parse_args()
@@ -123,6 +127,25 @@ def main():
                                                  for k, v in res.items() if str(k).startswith("x_")}
             print(json.dumps(out), flush=True)
             E.GSW_GROUP = None
+        if args.pipe:
+            import dsvgd.engine as E
+            res, xs = {}, {}
+            for pv in [int(v) for v in args.pipe.split(",")] * 2:
+                E.GSW_PIPELINE = bool(pv)
+                Xb, Sb = X.clone(), S0.clone()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                sequential_sweep(Xb, Sb, range(n), eng.state, 1e-4, target=tgt, score_scale=scale)
+                torch.cuda.synchronize()
+                res.setdefault(pv, []).append(1e3 * (time.perf_counter() - t0))
+                xs[pv] = Xb
+            vals = list(xs.values())
+            scale_x = float((vals[0] - X).abs().max())
+            print(json.dumps({"config": name, "sweep_ms_by_pipeline": res,
+                              "finite": [bool(torch.isfinite(v).all()) for v in vals],
+                              "max_abs_diff_between": float((vals[0] - vals[-1]).abs().max()),
+                              "max_abs_move": scale_x}), flush=True)
+            E.GSW_PIPELINE = True
         if args.splits:
             import dsvgd.engine as E
             res = {}

@@ -31,6 +31,21 @@ def case(m, n, d, kind, seed=0):
         P[:m] = X - 1e-3 * torch.randn(m, d, generator=g)
     X, P = X.cuda(), P.cuda()
     w = dsvgd.w2.W2Term(m, n, d, "cuda:0", warm=False)
+    # the cost matrix alone (the form W2Term chose), HIP events over 3 calls
+    from dsvgd import _native as N
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for it in range(2):
+        e0.record()
+        for _ in range(3):
+            if w.cost == "h2":
+                N.call("dsvgd_w2_cost_h2", N.ptr(X), d, m, N.ptr(P), d, n, d, N.ptr(w.C), w.ldc,
+                       (N.ptr(w.cws) + 255) // 256 * 256, float(w.TAU), N.stream(X.device))
+            else:
+                N.call("dsvgd_w2_cost", N.ptr(X), d, m, N.ptr(P), d, n, d, N.ptr(w.C), w.ldc,
+                       N.stream(X.device))
+        e1.record()
+        torch.cuda.synchronize()
+    cost_ms = e0.elapsed_time(e1) / 3
     w.grad(X, P, 1.0)
     torch.cuda.synchronize()
     t = time.perf_counter()
@@ -38,6 +53,7 @@ def case(m, n, d, kind, seed=0):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t) * 1e3
     out = {"m": m, "n": n, "d": d, "kind": kind, "ms": round(ms, 3), "rounds": w.rounds,
+           "cost_ms": round(cost_ms, 3),
            "us_per_round": round(ms * 1e3 / max(w.rounds, 1), 2)}
     # the next SVGD step: rows and columns both moved by a small step; warm
     # start from this solve's prices vs a cold solve of the same problem
@@ -65,6 +81,8 @@ def case(m, n, d, kind, seed=0):
             out["warm_vs_cold_grad_maxdiff"] = float((G - cold_plan).abs().max())
         if TRACE:
             out[key + "_next_profile"] = profile(ww.trace())
+        out["cost_form"] = ww.cost
+        out["_plan"] = ww.assign.clone()
     return out
 
 
@@ -98,6 +116,8 @@ def main():
                     help="comma list of W2Term.THETA settings to sweep on --shapes")
     ap.add_argument("--keep", default="0",
                     help="comma list of W2Term.KEEP settings to sweep on --shapes (1, 0)")
+    ap.add_argument("--cost", default="auto",
+                    help="comma list of W2Term.COST settings to sweep on --shapes (auto, h2, exact)")
     ap.add_argument("--warm-phases", default=None,
                     help="comma list of warm phase counts to sweep on --shapes (a = adaptive)")
     args = ap.parse_args()
@@ -114,11 +134,21 @@ def main():
                        if args.warm_phases else [dsvgd.w2.W2Term.WARM_PHASES]):
                 dsvgd.w2.W2Term.WARM_PHASES = ph
                 for sh in shapes:
-                    r = case(*sh)
-                    r["warm_phases"] = ph
-                    r["keep"] = keep
-                    r["theta"] = theta
-                    print(json.dumps(r), flush=True)
+                    plans = {}
+                    for cm in args.cost.split(","):
+                        dsvgd.w2.W2Term.COST = cm
+                        r = case(*sh)
+                        r["warm_phases"] = ph
+                        r["keep"] = keep
+                        r["theta"] = theta
+                        r["cost_mode"] = cm
+                        plans[cm] = r.pop("_plan")
+                        if len(plans) > 1:
+                            first = next(iter(plans.values()))
+                            r["plan_equal_to_" + next(iter(plans))] = bool(
+                                torch.equal(first, plans[cm]))
+                        print(json.dumps(r), flush=True)
+                    dsvgd.w2.W2Term.COST = "auto"
         return
     if args.lib:
         import dsvgd
@@ -140,7 +170,9 @@ def main():
     if args.big:
         shapes += [(8192, 65536, 256, "svgd"), (65536, 65536, 256, "svgd")]
     for s in shapes:
-        print(json.dumps(case(*s)), flush=True)
+        r = case(*s)
+        r.pop("_plan", None)
+        print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":

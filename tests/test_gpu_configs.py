@@ -398,6 +398,23 @@ def test_sequential_wide_full_sweep_d256(group):
         E.GSW_GROUP = prev
 
 
+@pytest.mark.parametrize("spin_ns", [0, 20000])
+def test_pipelined_sweep_forced_overlap(spin_ns):
+    """the pipelined wide sweep (engine.GSW_PIPELINE:
+    group g + 1's wide pass on a second stream beside group g's walk, group
+    g's columns masked out of it and added back at their moved positions)
+    with the overlap forced by construction -- the walk's stream held 20 us
+    after each pass is posted (dsvgd_debug_spin), so every pass runs beside a
+    walk -- against the fp64 sequential restatement, like the serial sweep."""
+    import dsvgd.engine as E
+    prev = (E.GSW_PIPELINE, E.GSW_PIPE_SPIN_NS)
+    E.GSW_PIPELINE, E.GSW_PIPE_SPIN_NS = True, spin_ns
+    try:
+        _wide_full_sweep_d256()
+    finally:
+        E.GSW_PIPELINE, E.GSW_PIPE_SPIN_NS = prev
+
+
 def _wide_full_sweep_d256():
     from dsvgd import _native as N
     from dsvgd.engine import SelectState, sequential_sweep

@@ -127,3 +127,49 @@ def test_gram_w1_sharded_counts_sum_to_whole():
     torch.cuda.synchronize()
     b = whole.state.bracket()
     assert tuple(got) == (b[2], b[3])
+
+
+@pytest.mark.parametrize("n,d,m,row0,median", [
+    (4200, 256, None, 0, True),     # symmetric, bracketed, ragged n
+    (1000, 256, None, 0, False),    # symmetric, no select (the diagonal fix-up)
+    (6000, 512, None, 0, True),     # dp = 512: K-steps past the epilogue's 16
+    (8192, 256, 4096, 4096, True),  # rectangle + mirrored square
+    (8000, 256, 2504, 2496, True),  # 16-aligned row block: one rectangle
+    (3000, 256, 1000, 1024, False),  # rectangles either side of the square
+    (65536, 256, None, 0, True),    # the headline Gram
+])
+def test_gram_rs_matches_gram_w1(n, d, m, row0, median):
+    """the split-role Gram (gram_rs_kernel: MFMA waves +
+    epilogue waves through an LDS hand-off, csrc/gram_rs.hpp) computes the
+    same D bits as the one-wave kernel (same fragments, products and order),
+    the same bracket counts and the same median; one selected per
+    dsvgd_gram_set_rs."""
+    from dsvgd import _native as N
+    lib = N.load()
+    rs = np.random.RandomState(n + d + 7)
+    X = gpu((0.1 * rs.randn(n, d)).astype(np.float32))
+    out = {}
+    prev = lib.dsvgd_gram_set_rs(1)
+    try:
+        for mode in (1, 0):
+            lib.dsvgd_gram_set_rs(mode)
+            eng = dsvgd().PhiEngine(n, d, m=m, row0=row0, device=DEV)
+            eng.pack(X)
+            if median:
+                eng.distances(median=True)
+                eng.median_bandwidth()
+            else:
+                eng.distances(median=False)
+            torch.cuda.synchronize()
+            # the stored tiles (the symmetric layout's lower ones are never written)
+            out[mode] = (eng.dense_D(padded=True).clone(), eng.state.read()[:2] if median else None,
+                         eng.state.bracket()[2:4] if median and eng.bracketed else None)
+            del eng
+            torch.cuda.empty_cache()
+    finally:
+        lib.dsvgd_gram_set_rs(prev)
+    assert torch.equal(out[1][0], out[0][0])
+    # (a row block's median needs the other blocks' counts: NaN on both sides)
+    assert np.array_equal(np.asarray(out[1][1], np.float64), np.asarray(out[0][1], np.float64),
+                          equal_nan=True)
+    assert out[1][2] == out[0][2]

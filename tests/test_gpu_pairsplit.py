@@ -230,7 +230,7 @@ def test_pair_split_failed_route_probe_keeps_row_blocks():
     """one rank's route probe sees a wrong payload (the received
     buffer spoiled before the comparison): every rank keeps the row-block
     layout from the first step on, and the step still matches the oracle."""
-    S, m = 2, 2048
+    S, m = 2, 4096     # m * n >= 2^24: the bracketed median, so the layout applies
     cfg = dict(n=S * m, d=256, N=1024, eps=1e-3, seed=31, h="median", mode="all_scores",
                nrows=48, expect_plan=False, probe_corrupt=1)
     _check(S, cfg, _run(S, 29837, cfg))
@@ -242,7 +242,7 @@ def test_pair_split_first_step_check_falls_back():
     rank's pair-split phi spoiled the shared verdict fails on both ranks, the
     owned rows are moved by the row-block phi instead (the update matches the
     oracle) and the row-block engine is the only one kept."""
-    S, m = 2, 2048
+    S, m = 2, 4096     # m * n >= 2^24: the bracketed median, so the layout applies
     cfg = dict(n=S * m, d=256, N=1024, eps=1e-3, seed=33, h="median", mode="all_scores",
                nrows=48, expect_plan=False, check_corrupt=0)
     _check(S, cfg, _run(S, 29839, cfg))

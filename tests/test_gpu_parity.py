@@ -835,6 +835,113 @@ def test_w2_errors():
         w.grad(X, bad, 1.0)
 
 
+# ---- the W2 cost on the MFMA Gram (dsvgd_w2_cost_h2) --
+def _w2_cost(X, P, form):
+    """C (m x n) from W2Term's cost form `form` ("h2" / "exact")."""
+    N = dsvgd()._native
+    W2 = dsvgd().w2.W2Term
+    old = W2.COST
+    W2.COST = form
+    try:
+        w = W2(X.shape[0], P.shape[0], X.shape[1], DEV)
+    finally:
+        W2.COST = old
+    Xg, Pg = gpu(X), gpu(P)
+    if form == "h2":
+        N.call("dsvgd_w2_cost_h2", N.ptr(Xg), X.shape[1], X.shape[0], N.ptr(Pg), P.shape[1],
+               P.shape[0], X.shape[1], N.ptr(w.C), w.ldc, (N.ptr(w.cws) + 255) // 256 * 256,
+               float(w.TAU), N.stream(torch.device(DEV)))
+    else:
+        N.call("dsvgd_w2_cost", N.ptr(Xg), X.shape[1], X.shape[0], N.ptr(Pg), P.shape[1],
+               P.shape[0], X.shape[1], N.ptr(w.C), w.ldc, N.stream(torch.device(DEV)))
+    torch.cuda.synchronize()
+    return w.C[:X.shape[0], :P.shape[0]].cpu().numpy()
+
+
+@pytest.mark.parametrize("m,n,d,kind", [(300, 900, 37, "random"), (1024, 1024, 256, "svgd"),
+                                        (512, 4096, 256, "svgd"), (250, 1000, 700, "random"),
+                                        (150, 300, 3, "near"), (2048, 2048, 64, "svgd")])
+def test_w2_cost_h2_matches_exact(m, n, d, kind):
+    """The Gram-form W2 cost on the split-role MFMA Gram against the
+    explicit-difference VALU tiles: every entry within 2e-5 of it (the FmtH2
+    bound, ~2^-19 of the entry where the form is kept), and the near pairs
+    -- a particle and its own previous position, the entries that decide an
+    SVGD plan -- recomputed to the same bits."""
+    rs = np.random.RandomState(m + n + d)
+    X = rs.randn(m, d).astype(np.float32)
+    P = rs.randn(n, d).astype(np.float32)
+    if kind == "svgd":
+        P[:m] = X - 1e-3 * rs.randn(m, d).astype(np.float32)
+    elif kind == "near":
+        P = (np.tile(X, (n // m + 1, 1))[:n] + 0.05 * rs.randn(n, d)).astype(np.float32)
+    Ch, Ce = _w2_cost(X, P, "h2"), _w2_cost(X, P, "exact")
+    assert np.isfinite(Ch).all()
+    rel = np.abs(Ch.astype(np.float64) - Ce) / np.maximum(Ce, 1e-30)
+    record_parity(float(rel.max()))
+    assert rel.max() < 2e-5, rel.max()
+    if kind == "svgd":
+        idx = np.arange(m)
+        np.testing.assert_array_equal(Ch[idx, idx], Ce[idx, idx])
+
+
+@pytest.mark.parametrize("name", W2_GOLDEN)
+def test_w2_h2_cost_golden_plans(golden, name):
+    """The golden LPs (reference linprog plans, near-tie sets included) on the
+    MFMA cost form (forced; W2Term takes it from 2^22 entries by default):
+    the same plans and gradients."""
+    W2 = dsvgd().w2.W2Term
+    old = W2.COST
+    W2.COST = "h2"
+    try:
+        g = golden(name)
+        G, plan, w = _w2_gpu(g["X"], g["P"], h=1.0)
+        assert w.cost == "h2"
+    finally:
+        W2.COST = old
+    err = abs_err(G, g["grad"]) / max(np.abs(g["grad"]).max(), 1e-30)
+    assert err < PHI_TOL, err
+    m = g["X"].shape[0]
+    np.testing.assert_array_equal(_row_sets(plan, m), _row_sets(O.w2_plan(O.w2_cost(g["X"], g["P"])), m))
+
+
+@pytest.mark.parametrize("m,n,d,near", [(256, 256, 16, None), (512, 1024, 8, None),
+                                        (2048, 2048, 64, None), (1024, 1024, 32, 0.05),
+                                        (1024, 4096, 8, 0.01), (512, 4096, 16, "svgd"),
+                                        (4096, 4096, 256, "svgd"), (2048, 16384, 256, "svgd")])
+def test_w2_h2_cost_same_plan_as_exact(m, n, d, near):
+    """Plans on the MFMA cost form == plans on the exact VALU cost form ==
+    scipy's assignment (up to 4096 x 4096), R = 1 .. 8, random and
+    SVGD-shaped (the owned rows' previous copies among the columns)."""
+    rs = np.random.RandomState(m + n + d + 3)
+    X = rs.randn(m, d).astype(np.float32)
+    if near is None:
+        P = rs.randn(n, d).astype(np.float32)
+    elif near == "svgd":
+        P = rs.randn(n, d).astype(np.float32)
+        P[:m] = X - 1e-3 * rs.randn(m, d).astype(np.float32)
+    else:
+        P = (np.tile(X, (n // m, 1)) + near * rs.randn(n, d)).astype(np.float32)
+    W2 = dsvgd().w2.W2Term
+    old = W2.COST
+    plans = {}
+    try:
+        for form in ("h2", "exact"):
+            W2.COST = form
+            G, plan, w = _w2_gpu(X, P, h=2.5)
+            assert w.cost == form
+            plans[form] = (plan, G)
+    finally:
+        W2.COST = old
+    np.testing.assert_array_equal(_row_sets(plans["h2"][0], m), _row_sets(plans["exact"][0], m))
+    # (the same row sets; the slots of a row may hold them in another order, so the
+    # gradient's sum over a row's columns may round differently in the last bits)
+    Gh, Ge = plans["h2"][1], plans["exact"][1]
+    assert np.abs(Gh - Ge).max() <= 1e-6 * np.abs(Ge).max()
+    if m * n <= 4096 * 4096 and d <= 64:
+        ref_plan = O.w2_plan(O.w2_cost(X, P))
+        np.testing.assert_array_equal(_row_sets(plans["h2"][0], m), _row_sets(ref_plan, m))
+
+
 # ------------------------------------------ DistSampler, 2 ranks, 1 GPU --
 def _dist_gpu_worker(rank, S, port, name, order, q, median=False):
     import os
