@@ -125,6 +125,23 @@ def pmc_traffic(kernel_prefixes):
     return total, os.path.relpath(path, ROOT)
 
 
+def pmc_mfma(prefix):
+    """MFMA-busy (SQ_VALU_MFMA_BUSY_CYCLES over the kernel's cycles x 1024
+    SIMDs) and the clock under load of the first kernel named `prefix` in the
+    committed PMC summary (scripts/pmc_summary.py "mfma" pass), or None."""
+    path = os.path.join(ROOT, "profiles", "latest_summary.json")
+    try:
+        with open(path) as f:
+            ks = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for name, v in ks.items():
+        if name.startswith(prefix) and "mfma_busy" in v:
+            return {"mfma_busy": v["mfma_busy"], "clock_ghz": v.get("clock_ghz"),
+                    "kernel": name, "source": os.path.relpath(path, ROOT)}
+    return None
+
+
 def passes(eng, stages, m, n, d, n_local, score_gemm):
     """The other passes of the step, each against its own bound (north_star:
     MFMA rate for the contractions, HBM GB/s for the distance and select
@@ -148,7 +165,9 @@ def passes(eng, stages, m, n, d, n_local, score_gemm):
                             "tflops_no_symmetry_credit": 2.0 * m * n * d / (t * 1e-3) / 1e12,
                             "d_bytes_written": d_bytes,
                             "write_gbs": d_bytes / (t * 1e-3) / 1e9,
-                            "frac_hbm": d_bytes / (t * 1e-3) / 1e9 / PEAK_HBM_GBS}
+                            "frac_hbm": d_bytes / (t * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                            "pmc": pmc_mfma("_ZN5dsvgd14gram_rs_kernelILi2ELb1E") or
+                            pmc_mfma("_ZN5dsvgd14gram_w1_kernelILi2ELb1E")}
     t = stages.get("radix_hist")
     if t:
         if eng.bracketed:
@@ -166,7 +185,8 @@ def passes(eng, stages, m, n, d, n_local, score_gemm):
     if t:
         tf = 4.0 * n * n_local * (d - 1) / (t * 1e-3) / 1e12
         peak = engine_peak(score_gemm)[0]
-        out["scores"] = {"ms": t, "bound": "mfma", "tflops": tf, "frac_mfma": tf / peak}
+        out["scores"] = {"ms": t, "bound": "mfma", "tflops": tf, "frac_mfma": tf / peak,
+                         "pmc": pmc_mfma("_ZN5dsvgd19logreg_fused_kernel")}
     return out
 
 
@@ -442,7 +462,9 @@ def main(argv=None):
                      "traffic": traffic,
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                      "algorithmic_bytes": 4.0 * m * n + 4.0 * (n + 128) * 512,
-                     "flop_per_launch": flops, "avg_launch_ms": phi_ms},
+                     "flop_per_launch": flops, "avg_launch_ms": phi_ms,
+                     # the committed N = 1 PMC pass of the same kernel (None at N > 1)
+                     "pmc": pmc_mfma(knames[0]) if world == 1 else None},
         "stages_ms": stages,
         "stages_basis": "mean HIP-event time per step over %d steps after the timed region "
                         "(phi_mm in roofline: the timed steps' own)" % args.breakdown,

@@ -16,10 +16,11 @@
 //     pipeline as gram_w1, so D is bit-identical) plus its B-fragment loads
 //     and LDS fragment reads; at the tile's end it writes its 128
 //     accumulators per lane to an LDS hand-off buffer (32 ds_write_b128,
-//     1 KiB each, conflict-free) and starts the next tile;
-//   * an E wave (waves 4-7) stages the strip's A image through LDS for every
-//     K-step (the loads gram_w1's four waves shared) and, during the next
-//     tile's 16 K-steps, runs the hand-off's epilogue one slice per K-step:
+//     1 KiB each, conflict-free) and starts the next tile.  The strip's A
+//     image reaches LDS by LDS-DMA the M waves issue two K-steps ahead (a
+//     3-stage ring);
+//   * an E wave (waves 4-7), during the next tile's 16 K-steps, runs the
+//     hand-off's epilogue one slice per K-step:
 //     the D value, the bracket accounting, the permlane pairing and the
 //     16-byte nt stores of gram_w1, reading the accumulators from LDS in the
 //     M wave's own lane layout.
@@ -29,9 +30,10 @@
 // longer stops the MFMAs.  M waves run at priority 1 (MI355X_MICROARCH.md
 // "static priority").
 //
-// LDS: 2 x 8 KiB A stages + 4 x 32 KiB hand-off + 2 KiB column data + 8 KiB
-// candidate stages (depth 8, flushed after every slice) = 154 KiB: one block
-// per CU.  Registers: <= 256 per wave (waves_per_eu 2): the M wave holds one
+// LDS: 3 x 8 KiB A stages + 4 x 32 KiB hand-off = 152 KiB: one block per CU.
+// The bracket's candidate stage reuses the hand-off chunks a slice has
+// already read (depth 128, one flush per tile instead of one per slice: the
+// per-slice flush's LDS read latency was most of the E wave's time).  Registers: <= 256 per wave (waves_per_eu 2): the M wave holds one
 // accumulator set (128), two fragment sets (64) and a two-deep B ring (32).
 //
 // Barriers: one per K-step (the A stage, as in gram_w1), plus two per tile
@@ -49,12 +51,10 @@ struct GramRS {
   static constexpr int SA = P * BM * 32;            // one K-step of the strip's image (8 KiB)
   static constexpr int kHWave = 128 * 64 * 4;       // one M wave's accumulators (32 KiB)
   static constexpr int kHOff = 3 * SA;               // 3 A stages, then the hand-off
-  static constexpr int kCandDepth = 8;
-  static constexpr int kCandOff = kHOff + 4 * kHWave;
-  static constexpr int kSmemBytes = kCandOff + 4 * 64 * kCandDepth * 4;
+  static constexpr int kSmemBytes = kHOff + 4 * kHWave;
   static constexpr int kSlots = 4;                  // candidate slots per unit (one per E wave)
 };
-static_assert(GramRS::kSmemBytes <= 160 * 1024, "gram_rs LDS");  // exactly 160 KiB
+static_assert(GramRS::kSmemBytes <= 160 * 1024, "gram_rs LDS");  // 152 KiB
 
 // OUT = 1: the W2 cost matrix (dsvgd_w2_cost_h2) -- D row-major with leading
 // dimension ldc instead of the panel layout, and every entry whose Gram form
@@ -67,11 +67,14 @@ struct W2Out {
   int64_t ldx = 0, ldy = 0, ldc = 0;
   int d = 0;
   float tau = 0.f;
+  int vec = 0;                // rows 16-byte aligned and d % 4 == 0: 16-byte loads
 };
 
-// VAR (a timing probe, dsvgd_gram_set_rs(5)): 4 = the E waves skip the
-// epilogue (D is not written) -- the MFMA waves' own rate
-template <int smode, bool SYM, int OUT = 0, int VAR = 0>
+// VAR (timing probes, dsvgd_gram_set_rs(5 / 6 / 7)): 4 = the E waves skip
+// the epilogue (D is not written) -- the MFMA waves' own rate; 8 = the M
+// waves skip the MFMAs (D is wrong) -- the epilogue waves' own rate; 16 = the
+// E waves at priority 1 instead of the M waves
+template <int smode, bool SYM, int OUT = 0, int VAR = 0, int KG = GramW1::kGroup>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gram_rs_kernel(
     const _Float16* __restrict__ Yg, int64_t img_rows, const float* __restrict__ norms,
     const float* __restrict__ rsc, int64_t row0, int64_t m, int64_t n, int64_t n_pad, int nk,
@@ -98,7 +101,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   SlotLayout sl(cand, ns_total, kBr ? st->cand_cap : 0);
   if (kBr) sl.publish(st, blockIdx.x);
 
-  GramUnitWalk walk(Tm, Tc, SYM);
+  GramUnitWalk walk(Tm, Tc, SYM, KG);
   // skipped units' slots are zeroed by the E waves only (one writer per slot)
   auto next_valid = [&](int64_t L, int& I, int& J2) -> int64_t {
     for (; L < hi; L += U) {
@@ -157,7 +160,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // for a stage never waits for an epilogue store.  A(k + 2) is issued at
     // the start of K-step k into the stage A(k - 1) left (read before the
     // last barrier), waited for at the barrier of K-step k + 1.
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (!(VAR & 16)) __builtin_amdgcn_s_setprio(1);
     const int vB = x3_off(r, h);
     const int voffA = (t >> 1) * 32 + (t & 1) * 16;
     const int voffA1 = voffA + (int)img_rows * 32;
@@ -216,7 +219,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           f32x16 c = (p == 0 && FIRST) ? f32x16{} : acc[bi][bj];
           const V8 bx = rb[KS & 1][bj][p == 1 ? 1 : 0];
           const V8 ax = a[bi][p == 0 ? 1 : 0];
-          acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bx, ax, c, 0, 0, 0);
+          if constexpr (VAR & 8)
+            acc[bi][bj] = c;
+          else
+            acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bx, ax, c, 0, 0, 0);
         }
         if (grp == 0) {
           load_B((KS + 1) & 1, k + 1);
@@ -295,9 +301,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   float pn[4], pr[4];
   f32x4 pcn[2][4], pcr[2][4];
   Unit pend = cur;
-  GramSlotWriter<GramRS::kCandDepth> sw;
-  float* const cstage =
-      reinterpret_cast<float*>(smem + GramRS::kCandOff) + w * 64 * GramRS::kCandDepth;
+  // the candidate stage is the hand-off region itself: slice SL has read
+  // chunks 2 SL, 2 SL + 1 (4 levels of 64 lanes each) and stages levels
+  // <= 8 SL + 7, so every level lands in an already-read chunk; one flush per
+  // tile, before X (where the M waves overwrite the region)
+  GramSlotWriter<128> sw;
+  float* const cstage = reinterpret_cast<float*>(hbuf);
   auto prefetch_epi = [&](const Unit& un) {
     const __amdgpu_buffer_rsrc_t rN =
         __builtin_amdgcn_make_buffer_rsrc((void*)norms, (short)0, 0x7fffffff, 0x00020000);
@@ -385,30 +394,54 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         if constexpr (kBr) sw.add(v[gg][e]);
       }
     if constexpr (OUT == 1) {
-      // near pairs: the explicit-difference cost (rare: a branch per slice)
-      bool any = false;
+      // near pairs: the explicit-difference cost, rare (the diagonal of an
+      // SVGD-shaped plan).  All lanes at once, each lane one of its entries
+      // per round (rounds = the most any lane has, 1 on the diagonal), the
+      // rows read 16 bytes at a time where aligned -- the same fmaf order
+      // as w2_cost_kernel either way.  (Per (g, e) entry with scalar loads
+      // this cost up to 8 serial 256-load chains per diagonal slice.)
+      uint32_t nm = 0u;
 #pragma unroll
       for (int gg = 0; gg < 2; ++gg)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) any |= v[gg][e] < wo.tau * (nrv + cnA[bj][g0 + gg][e]);
-      if (__ballot(any) != 0ull) {
+        for (int e = 0; e < 4; ++e)
+          nm |= v[gg][e] < wo.tau * (nrv + cnA[bj][g0 + gg][e]) ? 1u << (4 * gg + e) : 0u;
+      if (__ballot(nm != 0u) != 0ull) {
+        const int64_t i = ei0 + 32 * bi + r;
+        const float* xi = wo.X + i * wo.ldx;
+        while (__ballot(nm != 0u) != 0ull) {
+          const int b = nm ? __builtin_ctz(nm) : 0;
+          const int64_t j = ej0 + 32 * bj + 8 * (g0 + (b >> 2)) + 4 * h + (b & 3);
+          const float* yj = wo.Y + (nm ? j : 0) * wo.ldy;
+          float a = 0.f;
+          if (nm) {
+            if (wo.vec) {
+              const f32x4* x4 = reinterpret_cast<const f32x4*>(xi);
+              const f32x4* y4 = reinterpret_cast<const f32x4*>(yj);
+#pragma unroll 2
+              for (int k = 0; k < (wo.d >> 2); ++k) {
+                const f32x4 xa = x4[k], ya = y4[k];
 #pragma unroll
-        for (int gg = 0; gg < 2; ++gg)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (v[gg][e] < wo.tau * (nrv + cnA[bj][g0 + gg][e])) {
-              const int64_t i = ei0 + 32 * bi + r;
-              const int64_t j = ej0 + 32 * bj + 8 * (g0 + gg) + 4 * h + e;
-              const float* xi = wo.X + i * wo.ldx;
-              const float* yj = wo.Y + j * wo.ldy;
-              float a = 0.f;
-#pragma unroll 8
+                for (int c = 0; c < 4; ++c) {
+                  const float df = xa[c] - ya[c];
+                  a = fmaf(df, df, a);
+                }
+              }
+            } else {
+#pragma unroll 4
               for (int k = 0; k < wo.d; ++k) {
                 const float df = xi[k] - yj[k];
                 a = fmaf(df, df, a);
               }
-              v[gg][e] = a;
             }
+          }
+#pragma unroll
+          for (int gg = 0; gg < 2; ++gg)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (nm && b == 4 * gg + e) v[gg][e] = a;
+          nm &= nm - 1u;
+        }
       }
     }
     if (!kBr && ediag) {
@@ -419,7 +452,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int e = 0; e < 4; ++e)
           if (tgv == e + 8 * (g0 + gg) + 32 * bj) v[gg][e] = 0.f;
     }
-    if constexpr (kBr) sw.flush();
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const auto sv = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[0][e]),
@@ -444,6 +476,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
   };
 
+  if constexpr (VAR & 16) __builtin_amdgcn_s_setprio(1);
   barrier();  // the prologue's (the M waves' first A stage)
   bool epi = false;  // a tile's accumulators are in the hand-off buffer
   for (;;) {
@@ -461,13 +494,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     DSVGD_GRS_E(8) DSVGD_GRS_E(9) DSVGD_GRS_E(10) DSVGD_GRS_E(11)
     DSVGD_GRS_E(12) DSVGD_GRS_E(13) DSVGD_GRS_E(14) DSVGD_GRS_E(15)
 #undef DSVGD_GRS_E
+    if (kBr && epi) sw.flush4();  // the stage: before X
     for (int k = 16; k < nk; ++k) barrier();  // K-steps past the epilogue's 16 (dp > 256)
     // X: this tile's MFMAs are done, the previous tile's slices are read
     barrier();
     if (kBr && epi) sw.finish(sl, eslot, ew2);
     activate();
     if (kBr) {
-      sw = GramSlotWriter<GramRS::kCandDepth>{};
+      sw = GramSlotWriter<128>{};
       sw.begin(st, sl, eslot, cstage);
     }
     epi = true;
@@ -488,7 +522,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     DSVGD_GRS_D(12) DSVGD_GRS_D(13) DSVGD_GRS_D(14) DSVGD_GRS_D(15)
 #undef DSVGD_GRS_D
   }
-  if (kBr) sw.finish(sl, eslot, ew2);
+  if (kBr) {
+    sw.flush4();
+    sw.finish(sl, eslot, ew2);
+  }
 }
 
 }  // namespace dsvgd

@@ -74,9 +74,9 @@ struct GramUnitWalk {
   bool sym;
   int g = 0;
   int64_t goff = 0;
-  __host__ __device__ GramUnitWalk(int Tm_, int Tc_, bool sym_)
+  __host__ __device__ GramUnitWalk(int Tm_, int Tc_, bool sym_, int G_ = GramW1::kGroup)
       : Tm(Tm_), Tc(Tc_),
-        G(sym_ || Tm_ >= GramW1::kGroup ? GramW1::kGroup : (Tm_ > 0 ? Tm_ : 1)),
+        G(sym_ || Tm_ >= G_ ? G_ : (Tm_ > 0 ? Tm_ : 1)),
         ng((Tm_ + G - 1) / G), sym(sym_) {}
   __host__ __device__ int j0(int gg) const { return sym ? gg * (G / 2) : 0; }
   __host__ __device__ int64_t count(int gg) const {
@@ -123,6 +123,28 @@ struct GramSlotWriter : SlotWriterLdsT<DEPTH> {
       const float v = B::stage[k * 64];
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, act ? (int)(p * 4) : -1, 0, 0);
       B::cnt += (uint32_t)__popcll(bal);
+    }
+    B::pos = 0u;
+  }
+  // the same, four levels per round of LDS reads (gram_rs: one flush per tile
+  // over up to 128 levels, so the read latency is paid per four)
+  __device__ __forceinline__ void flush4() {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)B::dst, (short)0, (int)(B::cap * 4), 0x00020000);
+    for (uint32_t k0 = 0;; k0 += 4) {
+      if (__ballot(k0 < B::pos) == 0ull) break;
+      float v4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v4[i] = B::stage[(k0 + i) * 64];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool act = k0 + i < B::pos;
+        const uint64_t bal = __ballot(act);
+        const uint32_t p = B::cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v4[i]), rs, act ? (int)(p * 4) : -1, 0, 0);
+        B::cnt += (uint32_t)__popcll(bal);
+      }
     }
     B::pos = 0u;
   }

@@ -465,6 +465,11 @@ __global__ __launch_bounds__(512, 1) void sqdist_x3w_kernel(
 // default) or gram_w1_kernel (one wave per SIMD, the epilogue between the
 // MFMAs); the same arguments, units, slots and D bits.  dsvgd_gram_set_rs.
 static int g_gram_rs = 1;
+// strips per unit group of the split-role Gram's walk (GramUnitWalk G: the
+// strips whose image an XCD's L2 keeps while the column pairs stream past;
+// B is fetched once per group).  8 or 16, dsvgd_gram_set_group.
+static int g_gram_group = 8;
+static int gram_group() { return g_gram_rs ? g_gram_group : GramW1::kGroup; }
 
 template <int SM, bool SY>
 int launch_gram_units(const _Float16* Yg, int64_t img, const float* norms, const float* rsc,
@@ -476,17 +481,27 @@ int launch_gram_units(const _Float16* Yg, int64_t img, const float* norms, const
     // the A/B probe variants (gram_rs.hpp VAR) exist for the headline's form only
     auto launch = [&](auto VAR_) {
       constexpr int VAR = decltype(VAR_)::value;
-      int r = persistent_blocks(reinterpret_cast<const void*>(&gram_rs_kernel<SM, SY, 0, VAR>),
-                                &bw, GramRS::kThreads);
-      if (r) return r;
-      hipLaunchKernelGGL((gram_rs_kernel<SM, SY, 0, VAR>), dim3((unsigned)bw),
-                         dim3(GramRS::kThreads), 0, s, Yg, img, norms, rsc, row0, m, n, n_pad, nk,
-                         D, st, cand, tot, Tm, Tc, jp_off, base, ns_total, w2all, gate, W2Out{});
-      return check_launch("gram_rs");
+      auto go = [&](auto KG_) {
+        constexpr int KG = decltype(KG_)::value;
+        int r = persistent_blocks(
+            reinterpret_cast<const void*>(&gram_rs_kernel<SM, SY, 0, VAR, KG>), &bw,
+            GramRS::kThreads);
+        if (r) return r;
+        hipLaunchKernelGGL((gram_rs_kernel<SM, SY, 0, VAR, KG>), dim3((unsigned)bw),
+                           dim3(GramRS::kThreads), 0, s, Yg, img, norms, rsc, row0, m, n, n_pad,
+                           nk, D, st, cand, tot, Tm, Tc, jp_off, base, ns_total, w2all, gate,
+                           W2Out{});
+        return check_launch("gram_rs");
+      };
+      // (the caller's unit count came from the same group: gram_group())
+      return gram_group() == 16 ? go(std::integral_constant<int, 16>{})
+                                : go(std::integral_constant<int, 8>{});
     };
     const int var = g_gram_rs - 1;
     if constexpr (SM == kSelBracket && SY) {
       if (var == 4) return launch(std::integral_constant<int, 4>{});
+      if (var == 5) return launch(std::integral_constant<int, 8>{});
+      if (var == 6) return launch(std::integral_constant<int, 16>{});
     }
     return launch(std::integral_constant<int, 0>{});
   }
@@ -600,7 +615,9 @@ int launch_sqdist_x3(const typename F::E* Yg, const float* norms, int64_t row0, 
   const bool w1ok = F::P == 2 && SM != kSelHist && nk * KS % 16 == 0 && row0 % 16 == 0;
   auto w1part = [&](const Part& P) { return w1ok && !(P.sym && (sym ? layout : 0) == 0); };
   // every part spans the owned block's strips; its column pairs from bj_off
-  auto w1walk = [&](const Part& P) { return GramUnitWalk((int)(m_pad / 128), P.tc2, P.sym); };
+  auto w1walk = [&](const Part& P) {
+    return GramUnitWalk((int)(m_pad / 128), P.tc2, P.sym, gram_group());
+  };
   int64_t ns_total = 0;
   for (int i = 0; i < np; ++i)
     ns_total += w1part(parts[i]) ? w1walk(parts[i]).total() * GramW1::kSlots : parts[i].total * 8;
@@ -663,7 +680,7 @@ int launch_sqdist_h2_parts(const _Float16* Yg, const float* norms, int64_t row0,
            reinterpret_cast<const void*>(&sqdist_x3w_kernel<true, SM, false, F, KS>), &bs, 512)))
     return rc;
   auto walk = [&](const dsvgd_gram_part& P) {
-    return GramUnitWalk((int)(P.rows / 128), (int)(P.cols / 256), false);
+    return GramUnitWalk((int)(P.rows / 128), (int)(P.cols / 256), false, gram_group());
   };
   int64_t ns_total = 0;
   for (int i = 0; i < np; ++i) {
@@ -968,6 +985,10 @@ int dsvgd_w2_cost_h2(const float* X, int64_t ldx, int64_t m, const float* Y, int
   wo.ldc = ldc;
   wo.d = (int)d;
   wo.tau = tau;
+  wo.vec = (d % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)X & 15) == 0 &&
+            ((uintptr_t)Y & 15) == 0)
+               ? 1
+               : 0;
   int bw = 0;
   if ((rc = persistent_blocks(reinterpret_cast<const void*>(&gram_rs_kernel<kSelNone, false, 1>),
                               &bw, GramRS::kThreads)))
@@ -980,9 +1001,15 @@ int dsvgd_w2_cost_h2(const float* X, int64_t ldx, int64_t m, const float* Y, int
   return check_launch("gram_rs(w2 cost)");
 }
 
+int dsvgd_gram_set_group(int g) {
+  const int prev = g_gram_group;
+  g_gram_group = g == 16 ? 16 : 8;
+  return prev;
+}
+
 int dsvgd_gram_set_rs(int on) {
   const int prev = g_gram_rs;
-  g_gram_rs = on < 0 ? 0 : (on > 5 ? 1 : on);
+  g_gram_rs = on < 0 ? 0 : (on > 7 ? 1 : on);
   return prev;
 }
 

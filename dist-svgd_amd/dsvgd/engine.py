@@ -1082,7 +1082,11 @@ _WIDE = {}
 # the pipelined wide sweep (round 6): group g + 1's wide pass on a second
 # stream while group g walks, group g's columns left out of it and added at
 # their moved positions by dsvgd_gsw_group_corr before g + 1 walks
+# (d <= GSW_PIPELINE_MAX_D: config D sweep 136.4 vs 155.3 ms; at config E,
+# d = 1024, the extra whole-group corrections cost more than the overlap
+# saves, 536 vs 488 ms -- profiles/r14h)
 GSW_PIPELINE = True
+GSW_PIPELINE_MAX_D = 256
 GSW_PIPE_SPIN_NS = 0   # tests: hold the walk's stream this long after each pass is posted
 # blocks per wide pass of the wide Gauss-Seidel sweep (1: block after block;
 # config D sweep 278.7 / 253.0 / 256.2 ms at 1 / 2 / 4, profiles/r13u; None:
@@ -1116,7 +1120,7 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
     W.images(0, W.n_pad, s)
     B, GB = W.B, W.GB
     groups = [(g0, min(GB, rows.stop - g0)) for g0 in range(rows.start, rows.stop, GB)]
-    if GSW_PIPELINE and len(groups) >= 2:
+    if GSW_PIPELINE and d <= GSW_PIPELINE_MAX_D and len(groups) >= 2:
         _pipelined_sweep_wide(W, X, S, groups, n, d, h_state, step, sk, mu, lam, xd, td,
                               score_scale, phi_out, extra, rows.start, s)
         return

@@ -45,7 +45,7 @@ class PairSplitPlan(object):
     # the diagonal square as one full rectangle on the one-kernel Gram (both
     # triangles computed, each entry counted once) instead of its upper tiles
     # on the 8-wave kernel with mirror stores (round 6, A/B)
-    FULL_SQUARE = False
+    FULL_SQUARE = True
 
     @staticmethod
     def aligned(S, m):

@@ -240,11 +240,17 @@ int64_t dsvgd_phi_splits(int64_t m, int64_t n, int64_t ldy);
 int dsvgd_phi_set_symrow(int on);
 /* The one-kernel FmtH2 Gram units (dsvgd_sqdist_h2, dsvgd_sqdist_h2_parts):
  * 1 (default) = gram_rs_kernel, split roles -- four waves issue only the
- * MFMAs, four waves stage the strip image and write the previous tile's
- * epilogue (D values, bracket accounting, stores) from an LDS hand-off;
- * 0 = gram_w1_kernel, one wave per SIMD with the epilogue between its MFMAs.
- * Identical D and candidates.  Returns the previous setting (A/B switch). */
+ * MFMAs (and stage the strip image by LDS-DMA), four waves write the
+ * previous tile's epilogue (D values, bracket accounting, stores) from an
+ * LDS hand-off; 0 = gram_w1_kernel, one wave per SIMD with the epilogue
+ * between its MFMAs.  Identical D and candidates.  5, 6, 7: timing probes of
+ * the bracketed symmetric form only (5: no epilogue, 6: no MFMAs -- D wrong;
+ * 7: epilogue waves at priority 1).  Returns the previous setting. */
 int dsvgd_gram_set_rs(int on);
+/* Strips per unit group of the split-role Gram's walk (A/B switch, returns
+ * the previous setting): 8 (default) or 16.  Each group's strip images stay
+ * in an XCD's L2 while every column pair's image streams past once. */
+int dsvgd_gram_set_group(int g);
 /* The split-K slices of the symmetric layout's phi_mm (n x n, the engine's
  * KY / rowsum hold this many): dsvgd_phi_splits, or with the one-launch form
  * half as many while each fp32 chain stays within 2 x 16384 columns and the
