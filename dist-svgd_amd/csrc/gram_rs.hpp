@@ -73,7 +73,7 @@ struct W2Out {
 // VAR (timing probes, dsvgd_gram_set_rs(5 / 6 / 7)): 4 = the E waves skip
 // the epilogue (D is not written) -- the MFMA waves' own rate; 8 = the M
 // waves skip the MFMAs (D is wrong) -- the epilogue waves' own rate; 16 = the
-// E waves at priority 1 instead of the M waves
+// E waves at priority 1 instead of the M waves; 32 = barrier stamps (below)
 template <int smode, bool SYM, int OUT = 0, int VAR = 0, int KG = GramW1::kGroup>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gram_rs_kernel(
     const _Float16* __restrict__ Yg, int64_t img_rows, const float* __restrict__ norms,
@@ -139,10 +139,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
   const int pstride = (int)(img_rows * 32);  // bytes of one part of one image K-step
   // workgroup-wide: LDS writes landed, every wave past its LDS reads
-  auto barrier = []() {
+  // VAR & 32 (a timing probe): each wave of blocks 0-7 stamps the shader
+  // clock on arriving at and leaving every barrier into wo.X (int64
+  // [block][wave][512]); lane 0's vector store
+  int ev = 0;
+  auto stamp = [&]() {
+    if constexpr ((VAR & 32) != 0) {
+      const int64_t tnow = (int64_t)__builtin_amdgcn_s_memtime();
+      if (blockIdx.x < 8 && ev < 512 && lane == 0)
+        reinterpret_cast<int64_t*>(const_cast<float*>(wo.X))[(blockIdx.x * 8 + wv) * 512 + ev] = tnow;
+      ++ev;
+    }
+  };
+  auto barrier = [&]() {
+    stamp();
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    stamp();
   };
   float* const hbuf = reinterpret_cast<float*>(smem + GramRS::kHOff + w * GramRS::kHWave);
 

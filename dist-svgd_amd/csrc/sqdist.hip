@@ -469,6 +469,7 @@ static int g_gram_rs = 1;
 // strips whose image an XCD's L2 keeps while the column pairs stream past;
 // B is fetched once per group).  8 or 16, dsvgd_gram_set_group.
 static int g_gram_group = 8;
+static void* g_gram_stamps = nullptr;  // dsvgd_gram_debug_stamps (probe 8)
 static int gram_group() { return g_gram_rs ? g_gram_group : GramW1::kGroup; }
 
 template <int SM, bool SY>
@@ -487,10 +488,11 @@ int launch_gram_units(const _Float16* Yg, int64_t img, const float* norms, const
             reinterpret_cast<const void*>(&gram_rs_kernel<SM, SY, 0, VAR, KG>), &bw,
             GramRS::kThreads);
         if (r) return r;
+        W2Out wo{};
+        wo.X = (const float*)g_gram_stamps;
         hipLaunchKernelGGL((gram_rs_kernel<SM, SY, 0, VAR, KG>), dim3((unsigned)bw),
                            dim3(GramRS::kThreads), 0, s, Yg, img, norms, rsc, row0, m, n, n_pad,
-                           nk, D, st, cand, tot, Tm, Tc, jp_off, base, ns_total, w2all, gate,
-                           W2Out{});
+                           nk, D, st, cand, tot, Tm, Tc, jp_off, base, ns_total, w2all, gate, wo);
         return check_launch("gram_rs");
       };
       // (the caller's unit count came from the same group: gram_group())
@@ -502,6 +504,7 @@ int launch_gram_units(const _Float16* Yg, int64_t img, const float* norms, const
       if (var == 4) return launch(std::integral_constant<int, 4>{});
       if (var == 5) return launch(std::integral_constant<int, 8>{});
       if (var == 6) return launch(std::integral_constant<int, 16>{});
+      if (var == 7 && g_gram_stamps) return launch(std::integral_constant<int, 32>{});
     }
     return launch(std::integral_constant<int, 0>{});
   }
@@ -1001,6 +1004,11 @@ int dsvgd_w2_cost_h2(const float* X, int64_t ldx, int64_t m, const float* Y, int
   return check_launch("gram_rs(w2 cost)");
 }
 
+int dsvgd_gram_debug_stamps(void* buf) {
+  g_gram_stamps = buf;
+  return 0;
+}
+
 int dsvgd_gram_set_group(int g) {
   const int prev = g_gram_group;
   g_gram_group = g == 16 ? 16 : 8;
@@ -1009,7 +1017,7 @@ int dsvgd_gram_set_group(int g) {
 
 int dsvgd_gram_set_rs(int on) {
   const int prev = g_gram_rs;
-  g_gram_rs = on < 0 ? 0 : (on > 7 ? 1 : on);
+  g_gram_rs = on < 0 ? 0 : (on > 8 ? 1 : on);
   return prev;
 }
 

@@ -245,12 +245,16 @@ int dsvgd_phi_set_symrow(int on);
  * LDS hand-off; 0 = gram_w1_kernel, one wave per SIMD with the epilogue
  * between its MFMAs.  Identical D and candidates.  5, 6, 7: timing probes of
  * the bracketed symmetric form only (5: no epilogue, 6: no MFMAs -- D wrong;
- * 7: epilogue waves at priority 1).  Returns the previous setting. */
+ * 7: epilogue waves at priority 1; 8: barrier clock stamps into the buffer
+ * given to dsvgd_gram_debug_stamps).  Returns the previous setting. */
 int dsvgd_gram_set_rs(int on);
 /* Strips per unit group of the split-role Gram's walk (A/B switch, returns
  * the previous setting): 8 (default) or 16.  Each group's strip images stay
  * in an XCD's L2 while every column pair's image streams past once. */
 int dsvgd_gram_set_group(int g);
+/* Probe 8 of dsvgd_gram_set_rs: int64 [8 blocks][8 waves][512] shader-clock
+ * stamps, on arriving at and leaving each barrier (NULL: probe off). */
+int dsvgd_gram_debug_stamps(void* buf);
 /* The split-K slices of the symmetric layout's phi_mm (n x n, the engine's
  * KY / rowsum hold this many): dsvgd_phi_splits, or with the one-launch form
  * half as many while each fp32 chain stays within 2 x 16384 columns and the

@@ -77,7 +77,8 @@ def main(run, tag):
         for k, v in agg.items():
             key = "fetch_bytes_corrected" if cnt == "FETCH_SIZE" else "write_bytes"
             out["kernels"].setdefault(k, {})[key] = sum(v) / len(v)
-    mfma_pass(os.path.join(run, "mfma"), out["kernels"])
+    for sub in ("mfma", "pmcmfma"):
+        mfma_pass(os.path.join(run, sub), out["kernels"])
     for k, v in out["kernels"].items():
         if "fetch_bytes_corrected" in v or "write_bytes" in v:
             v["hbm_bytes_per_launch"] = v.get("fetch_bytes_corrected", 0) + v.get("write_bytes", 0)
