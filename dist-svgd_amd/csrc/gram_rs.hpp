@@ -51,10 +51,11 @@ struct GramRS {
   static constexpr int SA = P * BM * 32;            // one K-step of the strip's image (8 KiB)
   static constexpr int kHWave = 128 * 64 * 4;       // one M wave's accumulators (32 KiB)
   static constexpr int kHOff = 3 * SA;               // 3 A stages, then the hand-off
-  static constexpr int kSmemBytes = kHOff + 4 * kHWave;
+  static constexpr int kSOff = kHOff + 4 * kHWave;  // the last slice's candidate stage
+  static constexpr int kSmemBytes = kSOff + 4 * 64 * 8 * 4;
   static constexpr int kSlots = 4;                  // candidate slots per unit (one per E wave)
 };
-static_assert(GramRS::kSmemBytes <= 160 * 1024, "gram_rs LDS");  // 152 KiB
+static_assert(GramRS::kSmemBytes <= 160 * 1024, "gram_rs LDS");  // exactly 160 KiB
 
 // OUT = 1: the W2 cost matrix (dsvgd_w2_cost_h2) -- D row-major with leading
 // dimension ldc instead of the panel layout, and every entry whose Gram form
@@ -73,7 +74,8 @@ struct W2Out {
 // VAR (timing probes, dsvgd_gram_set_rs(5 / 6 / 7)): 4 = the E waves skip
 // the epilogue (D is not written) -- the MFMA waves' own rate; 8 = the M
 // waves skip the MFMAs (D is wrong) -- the epilogue waves' own rate; 16 = the
-// E waves at priority 1 instead of the M waves; 32 = barrier stamps (below)
+// E waves at priority 1 instead of the M waves; 32 = barrier stamps (below);
+// 64 = the M waves' B ring 4 deep (B two K-steps ahead)
 template <int smode, bool SYM, int OUT = 0, int VAR = 0, int KG = GramW1::kGroup>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gram_rs_kernel(
     const _Float16* __restrict__ Yg, int64_t img_rows, const float* __restrict__ norms,
@@ -183,7 +185,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           (void*)(Yg + ((int64_t)(un.J2 + jp_off) * 256 + 64 * w) * 16), (short)0, 0x7fffffff,
           0x00020000);
     };
-    V8 rb[2][2][2];  // [ring][bj][part]
+    // VAR & 64: a 4-deep ring, B issued two K-steps ahead (probe 9)
+    constexpr int kRB = (VAR & 64) ? 4 : 2;
+    V8 rb[kRB][2][2];  // [ring][bj][part]
     auto load_B = [&](int sb, int kk) {  // step kk's B (kk >= nk: the next unit's)
       const bool nx = kk >= nk;
       const int ks = nx ? (has_next ? kk - nk : nk - 1) : kk;
@@ -231,7 +235,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int qq = 0; qq < 3; ++qq) {
           const int idx = 3 * grp + qq, p = idx / 8, bi = (idx % 8) >> 1, bj = idx & 1;
           f32x16 c = (p == 0 && FIRST) ? f32x16{} : acc[bi][bj];
-          const V8 bx = rb[KS & 1][bj][p == 1 ? 1 : 0];
+          const V8 bx = rb[KS & (kRB - 1)][bj][p == 1 ? 1 : 0];
           const V8 ax = a[bi][p == 0 ? 1 : 0];
           if constexpr (VAR & 8)
             acc[bi][bj] = c;
@@ -239,13 +243,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bx, ax, c, 0, 0, 0);
         }
         if (grp == 0) {
-          load_B((KS + 1) & 1, k + 1);
+          if constexpr (kRB == 4)
+            load_B((KS + 2) & 3, k + 2);
+          else
+            load_B((KS + 1) & 1, k + 1);
           dma_A(k + 2, sD);
           sD = nxt3(sD);
         }
         if (grp == 3) {
           // A(k + 1)'s DMA (issued last K-step) landed: only this step's four
-          // B loads and two A DMAs are younger
+          // B loads and two A DMAs are younger (4-deep ring: the four of
+          // B(k + 2); B(k + 1), issued last step, older than A(k + 1)'s DMA,
+          // is waited for here too)
           __builtin_amdgcn_sched_barrier(0);
           asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
           barrier();
@@ -259,6 +268,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     dma_A(0, 0);
     dma_A(1, 1);
     load_B(0, 0);
+    if constexpr (kRB == 4) load_B(1, 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier();
     read_frags(af[0], smem);
@@ -321,6 +331,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // tile, before X (where the M waves overwrite the region)
   GramSlotWriter<128> sw;
   float* const cstage = reinterpret_cast<float*>(hbuf);
+  // slice 15 runs after X (the M waves already overwriting the hand-off):
+  // its candidates go to a stage of their own, depth 8
+  float* const sstage = reinterpret_cast<float*>(smem + GramRS::kSOff) + w * 64 * 8;
+  // the bracket is fixed for the launch: read once, not per tile
+  uint32_t klo0 = 0x7FFFFFFFu, kspan0 = 0u;
+  if constexpr (kBr) {
+    const float blo = st->lo, bhi = st->hi;
+    const bool ok = bhi >= blo && blo >= 0.f;  // as SlotWriterLdsT::begin
+    klo0 = ok ? __float_as_uint(blo) : 0x7FFFFFFFu;
+    kspan0 = ok ? __float_as_uint(bhi) - klo0 : 0u;
+  }
   auto prefetch_epi = [&](const Unit& un) {
     const __amdgpu_buffer_rsrc_t rN =
         __builtin_amdgcn_make_buffer_rsrc((void*)norms, (short)0, 0x7fffffff, 0x00020000);
@@ -506,21 +527,33 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     DSVGD_GRS_E(0) DSVGD_GRS_E(1) DSVGD_GRS_E(2) DSVGD_GRS_E(3)
     DSVGD_GRS_E(4) DSVGD_GRS_E(5) DSVGD_GRS_E(6) DSVGD_GRS_E(7)
     DSVGD_GRS_E(8) DSVGD_GRS_E(9) DSVGD_GRS_E(10) DSVGD_GRS_E(11)
-    DSVGD_GRS_E(12) DSVGD_GRS_E(13) DSVGD_GRS_E(14) DSVGD_GRS_E(15)
+    DSVGD_GRS_E(12) DSVGD_GRS_E(13) DSVGD_GRS_E(14)
 #undef DSVGD_GRS_E
-    if (kBr && epi) sw.flush4();  // the stage: before X
+    // K-step 15: the stage in the hand-off is flushed before X; slice 15
+    // (its values read at slice 14) runs after X beside the M waves'
+    // hand-off writes, its candidates in the stage of its own
+    barrier();
+    if (kBr && epi) {
+      sw.flush4();
+      sw.stage = sstage + lane;
+    }
     for (int k = 16; k < nk; ++k) barrier();  // K-steps past the epilogue's 16 (dp > 256)
-    // X: this tile's MFMAs are done, the previous tile's slices are read
+    // X: this tile's MFMAs are done, the previous tile's hand-off is read
+    barrier();
+    if (epi && !(VAR & 4)) slice(std::integral_constant<int, 15>{}, hv[1]);
+    // Y: the M waves' hand-off writes have landed
     barrier();
     if (kBr && epi) sw.finish(sl, eslot, ew2);
     activate();
     if (kBr) {
       sw = GramSlotWriter<128>{};
-      sw.begin(st, sl, eslot, cstage);
+      sw.klo = klo0;
+      sw.kspan = kspan0;
+      sw.dst = sl.data + eslot * sl.cap;
+      sw.cap = (uint32_t)sl.cap;
+      sw.stage = cstage + lane;
     }
     epi = true;
-    // Y: the M waves' hand-off writes have landed
-    barrier();
     read_h(0, hv[0]);
     if (!has_next) break;
     advance();

@@ -505,6 +505,7 @@ int launch_gram_units(const _Float16* Yg, int64_t img, const float* norms, const
       if (var == 5) return launch(std::integral_constant<int, 8>{});
       if (var == 6) return launch(std::integral_constant<int, 16>{});
       if (var == 7 && g_gram_stamps) return launch(std::integral_constant<int, 32>{});
+      if (var == 8) return launch(std::integral_constant<int, 64>{});
     }
     return launch(std::integral_constant<int, 0>{});
   }
@@ -1017,7 +1018,7 @@ int dsvgd_gram_set_group(int g) {
 
 int dsvgd_gram_set_rs(int on) {
   const int prev = g_gram_rs;
-  g_gram_rs = on < 0 ? 0 : (on > 8 ? 1 : on);
+  g_gram_rs = on < 0 ? 0 : (on > 9 ? 1 : on);
   return prev;
 }
 

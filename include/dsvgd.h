@@ -246,7 +246,8 @@ int dsvgd_phi_set_symrow(int on);
  * between its MFMAs.  Identical D and candidates.  5, 6, 7: timing probes of
  * the bracketed symmetric form only (5: no epilogue, 6: no MFMAs -- D wrong;
  * 7: epilogue waves at priority 1; 8: barrier clock stamps into the buffer
- * given to dsvgd_gram_debug_stamps).  Returns the previous setting. */
+ * given to dsvgd_gram_debug_stamps; 9: the MFMA waves' B ring 4 deep).
+ * Returns the previous setting. */
 int dsvgd_gram_set_rs(int on);
 /* Strips per unit group of the split-role Gram's walk (A/B switch, returns
  * the previous setting): 8 (default) or 16.  Each group's strip images stay

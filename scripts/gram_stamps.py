@@ -57,7 +57,26 @@ def main():
                     waitx.append(lev[u0 + 16] - arr[u0 + 16])
                     waity.append(lev[u0 + 17] - arr[u0 + 17])
                     tile.append(lev[u0 + 18] - lev[u0] if u0 + 18 < len(lev) else 0)
+        # per barrier index of a tile (B_0 .. B_15, X, Y): the median time from
+        # the previous barrier's release to this one's release, and the wait
+        seg = [[] for _ in range(18)]
+        wt = [[] for _ in range(18)]
+        for b in range(8):
+            for w in waves:
+                s = t[b, w]
+                nz = int(np.count_nonzero(s))
+                pairs = s[:nz - nz % 2].reshape(-1, 2)
+                arr, lev = pairs[:, 0], pairs[:, 1]
+                for u0 in range(1, len(pairs) - 18, 18):
+                    for i in range(18):
+                        seg[i].append(lev[u0 + i] - lev[u0 + i - 1])
+                        wt[i].append(lev[u0 + i] - arr[u0 + i])
         med = lambda v: float(np.median(v)) if len(v) else None  # noqa: E731
+        out[role + "_by_barrier"] = {"names": ["B%d" % i for i in range(16)] + ["X", "Y"],
+                                     "segment_median": [med(v) for v in seg],
+                                     "segment_mean": [float(np.mean(v)) if v else None for v in seg],
+                                     "wait_median": [med(v) for v in wt],
+                                     "wait_mean": [float(np.mean(v)) if v else None for v in wt]}
         out[role] = {"kstep_period": med(per), "kstep_wait": med(waitk),
                      "kstep_wait_p90": float(np.percentile(waitk, 90)) if waitk else None,
                      "x_wait": med(waitx), "y_wait": med(waity),
