@@ -342,23 +342,29 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     klo0 = ok ? __float_as_uint(blo) : 0x7FFFFFFFu;
     kspan0 = ok ? __float_as_uint(bhi) - klo0 : 0u;
   }
-  auto prefetch_epi = [&](const Unit& un) {
+  // in three parts (K-steps 8, 10, 12: one batch of 24 loads had the E wave
+  // arrive ~1600 cycles late at its barrier, profiles/r14n; each part, the
+  // previous slot's close (K-step 3) and the walk's advance (K-step 5) in a
+  // K-step of its own, where the wave has ~400 cycles of slack)
+  auto prefetch_epi = [&](const Unit& un, auto PART_) {
+    constexpr int PART = decltype(PART_)::value;
     const __amdgpu_buffer_rsrc_t rN =
         __builtin_amdgcn_make_buffer_rsrc((void*)norms, (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t rS =
         __builtin_amdgcn_make_buffer_rsrc((void*)rsc, (short)0, 0x7fffffff, 0x00020000);
-    pend = un;
-    const int64_t gj0 = (int64_t)(un.J2 + jp_off) * 256 + 64 * w;
+    if constexpr (PART == 0) {
+      pend = un;
 #pragma unroll
-    for (int bi = 0; bi < 4; ++bi) {
-      // rows past m read row 0's data (clamped); activate() masks them
-      const int64_t il = (int64_t)un.I * 128 + 32 * bi + r;
-      const int64_t gi = row0 + (il < m ? il : 0);
-      pn[bi] = norms[gi];
-      pr[bi] = rsc[gi];
-    }
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj)
+      for (int bi = 0; bi < 4; ++bi) {
+        // rows past m read row 0's data (clamped); activate() masks them
+        const int64_t il = (int64_t)un.I * 128 + 32 * bi + r;
+        const int64_t gi = row0 + (il < m ? il : 0);
+        pn[bi] = norms[gi];
+        pr[bi] = rsc[gi];
+      }
+    } else {
+      constexpr int bj = PART - 1;
+      const int64_t gj0 = (int64_t)(pend.J2 + jp_off) * 256 + 64 * w;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         // columns >= n read whatever lies there (the image's slack rows): masked below
@@ -366,6 +372,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         pcn[bj][g] = gw1_load(rN, c * 4, 0);
         pcr[bj][g] = gw1_load(rS, c * 4, 0);
       }
+    }
   };
   auto activate = [&]() {
     const Unit& un = pend;
@@ -381,16 +388,29 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       si2[bi] = 2.f * pow2_inv(ok ? pr[bi] : 1.f);
       tg[bi] = ok ? (int)(gi0 + 32 * bi + r - gj0) - 4 * h : (1 << 20);
     }
+    if (gj0 + 64 <= n) {  // (wave-uniform) every column of the tile is real
 #pragma unroll
-    for (int bj = 0; bj < 2; ++bj)
+      for (int bj = 0; bj < 2; ++bj)
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
+        for (int g = 0; g < 4; ++g)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const bool ok = gj0 + 32 * bj + 8 * g + 4 * h + e < n;
-          cnA[bj][g][e] = ok ? pcn[bj][g][e] : INFINITY;
-          csA[bj][g][e] = pow2_inv(ok ? pcr[bj][g][e] : 1.f);
-        }
+          for (int e = 0; e < 4; ++e) {
+            cnA[bj][g][e] = pcn[bj][g][e];
+            csA[bj][g][e] = pow2_inv(pcr[bj][g][e]);
+          }
+    } else {
+      const int nl = (int)(n - gj0);  // < 64
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool ok = 32 * bj + 8 * g + 4 * h + e < nl;
+            cnA[bj][g][e] = ok ? pcn[bj][g][e] : INFINITY;
+            csA[bj][g][e] = pow2_inv(ok ? pcr[bj][g][e] : 1.f);
+          }
+    }
     if constexpr (OUT == 1) {
       // rows I*128 .. +128 (the caller's C has roundup(m, 128) rows), the wave's 64 columns
       float* dt = D + (int64_t)un.I * 128 * wo.ldc + gj0;
@@ -514,15 +534,32 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if constexpr (VAR & 16) __builtin_amdgcn_s_setprio(1);
   barrier();  // the prologue's (the M waves' first A stage)
   bool epi = false;  // a tile's accumulators are in the hand-off buffer
+  // the previous tile's slot is closed (its last slice's stage flushed, the
+  // counts stored) after slice 3 of the next, and the walk advanced after
+  // slice 5 -- both off the hand-off, where the M waves wait for this wave
+  GramSlotWriter<128> sw_old;
+  int64_t eslot_old = 0;
+  bool ew2_old = false, old_pending = false, adv_pending = false;
   for (;;) {
     // K-step k: after its barrier, slice k of the handed-off tile with slice
-    // k + 1's values read ahead; the next tile's row / column data at k = 2
+    // k + 1's values read ahead; the next tile's row / column data at k = 8,
+    // 10, 12
 #define DSVGD_GRS_E(KK)                                                        \
-  if ((KK) == 2) prefetch_epi(cur);                                            \
+  if ((KK) == 8) prefetch_epi(cur, std::integral_constant<int, 0>{});        \
+  if ((KK) == 10) prefetch_epi(cur, std::integral_constant<int, 1>{});       \
+  if ((KK) == 12) prefetch_epi(cur, std::integral_constant<int, 2>{});       \
   barrier();                                                                   \
   if (epi && !(VAR & 4)) {                                                     \
     if ((KK) + 1 < 16) read_h((KK) + 1, hv[((KK) + 1) & 1]);                   \
     slice(std::integral_constant<int, KK>{}, hv[(KK) & 1]);                    \
+  }                                                                            \
+  if ((KK) == 3 && kBr && old_pending) {                                       \
+    sw_old.finish_tile(sl, eslot_old, ew2_old);                                \
+    old_pending = false;                                                       \
+  }                                                                            \
+  if ((KK) == 5 && adv_pending) {                                              \
+    advance();                                                                 \
+    adv_pending = false;                                                       \
   }
     DSVGD_GRS_E(0) DSVGD_GRS_E(1) DSVGD_GRS_E(2) DSVGD_GRS_E(3)
     DSVGD_GRS_E(4) DSVGD_GRS_E(5) DSVGD_GRS_E(6) DSVGD_GRS_E(7)
@@ -543,7 +580,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if (epi && !(VAR & 4)) slice(std::integral_constant<int, 15>{}, hv[1]);
     // Y: the M waves' hand-off writes have landed
     barrier();
-    if (kBr && epi) sw.finish(sl, eslot, ew2);
+    if (kBr && epi) {
+      sw_old = sw;
+      eslot_old = eslot;
+      ew2_old = ew2;
+      old_pending = true;
+    }
     activate();
     if (kBr) {
       sw = GramSlotWriter<128>{};
@@ -556,8 +598,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     epi = true;
     read_h(0, hv[0]);
     if (!has_next) break;
-    advance();
+    adv_pending = true;
   }
+  if (kBr && old_pending) sw_old.finish_tile(sl, eslot_old, ew2_old);
   // drain: the last tile's epilogue, with the M waves gone
   if constexpr (!(VAR & 4)) {
 #define DSVGD_GRS_D(KK)                                              \
@@ -569,10 +612,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     DSVGD_GRS_D(12) DSVGD_GRS_D(13) DSVGD_GRS_D(14) DSVGD_GRS_D(15)
 #undef DSVGD_GRS_D
   }
-  if (kBr) {
-    sw.flush4();
-    sw.finish(sl, eslot, ew2);
-  }
+  if (kBr) sw.finish_tile(sl, eslot, ew2);
 }
 
 }  // namespace dsvgd

@@ -148,6 +148,19 @@ struct GramSlotWriter : SlotWriterLdsT<DEPTH> {
     }
     B::pos = 0u;
   }
+  // finish() for a wave whose lanes saw at most 255 values each since begin
+  // (gram_rs: one tile, 128 per lane): the below count summed by eight
+  // ballots on the scalar unit instead of a six-step shuffle chain through
+  // the LDS crossbar, the stage flushed four levels per round
+  __device__ __forceinline__ void finish_tile(const SlotLayout& L, int64_t slot, bool weight2) {
+    flush4();
+    uint32_t b = 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b += (uint32_t)__popcll(__ballot((B::below >> k) & 1u)) << k;
+    const uint32_t flag = weight2 ? DSVGD_SLOT_WEIGHT2 : 0u;
+    L.cnt[slot] = (B::cnt < DSVGD_SLOT_WEIGHT2 ? B::cnt : DSVGD_SLOT_WEIGHT2 - 1u) | flag;
+    L.below[slot] = b;
+  }
   __device__ __forceinline__ void finish(const SlotLayout& L, int64_t slot, bool weight2) {
     flush();
     uint32_t b = B::below;
