@@ -40,6 +40,8 @@
 // around the hand-off (X: the E waves have read the previous tile's last
 // slice; Y: the M waves' writes have landed).
 #pragma once
+#include <cfloat>
+
 #include "gram_w1.hpp"
 
 namespace dsvgd {
@@ -69,6 +71,9 @@ struct W2Out {
   int d = 0;
   float tau = 0.f;
   int vec = 0;                // rows 16-byte aligned and d % 4 == 0: 16-byte loads
+  // stat[0]: the largest entry's bits, stat[1]: 1 if an entry is not finite
+  // (what w2_cmax_kernel finds in a pass over C; zeroed by the caller)
+  uint32_t* stat = nullptr;
 };
 
 // VAR (timing probes, dsvgd_gram_set_rs(5 / 6 / 7)): 4 = the E waves skip
@@ -316,6 +321,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // Each lane's columns are 32 bj + 8 g + 4 h + e (bj < 2, g < 4, e < 4): 32
   // per lane, kept in registers (no LDS column table).
   float nr[4], si2[4];
+  uint32_t vrow = 0u, vcol = 0u;  // OUT 1: the real rows (bit bi) / columns (16 bj + 4 g + e)
+  uint32_t cmx = 0u;              // OUT 1: the largest real entry's bits so far
+  bool cbad = false;
   int tg[4];
   f32x4 cnA[2][4], csA[2][4];
   __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc((void*)D, (short)0, 0, 0x00020000);
@@ -385,6 +393,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const int64_t il = (int64_t)un.I * 128 + 32 * bi + r;
       const bool ok = valid && il < m;
       nr[bi] = ok ? pn[bi] : INFINITY;
+      if constexpr (OUT == 1) vrow = bi == 0 ? (ok ? 1u : 0u) : (vrow | (ok ? 1u << bi : 0u));
       si2[bi] = 2.f * pow2_inv(ok ? pr[bi] : 1.f);
       tg[bi] = ok ? (int)(gi0 + 32 * bi + r - gj0) - 4 * h : (1 << 20);
     }
@@ -398,7 +407,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             cnA[bj][g][e] = pcn[bj][g][e];
             csA[bj][g][e] = pow2_inv(pcr[bj][g][e]);
           }
+      if constexpr (OUT == 1) vcol = ~0u;
     } else {
+      if constexpr (OUT == 1) vcol = 0u;
       const int nl = (int)(n - gj0);  // < 64
 #pragma unroll
       for (int bj = 0; bj < 2; ++bj)
@@ -409,6 +420,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             const bool ok = 32 * bj + 8 * g + 4 * h + e < nl;
             cnA[bj][g][e] = ok ? pcn[bj][g][e] : INFINITY;
             csA[bj][g][e] = pow2_inv(ok ? pcr[bj][g][e] : 1.f);
+            if constexpr (OUT == 1) vcol |= ok ? 1u << (16 * bj + 4 * g + e) : 0u;
           }
     }
     if constexpr (OUT == 1) {
@@ -498,6 +510,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           nm &= nm - 1u;
         }
       }
+    }
+    if constexpr (OUT == 1) {
+      // the largest real entry and the non-finite check (w2_cmax_kernel's)
+      const uint32_t rb = (vrow >> bi) & 1u;
+#pragma unroll
+      for (int gg = 0; gg < 2; ++gg)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool ok = (rb & (vcol >> (16 * bj + 4 * (g0 + gg) + e))) != 0u;
+          const float x = v[gg][e];
+          cmx = max(cmx, ok ? __float_as_uint(x) : 0u);
+          cbad |= ok && !(x >= 0.f && x <= FLT_MAX);
+        }
     }
     if (!kBr && ediag) {
       const int tgv = tg[bi];
@@ -601,6 +626,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     adv_pending = true;
   }
   if (kBr && old_pending) sw_old.finish_tile(sl, eslot_old, ew2_old);
+  auto publish_stat = [&]() {
+    if constexpr (OUT == 1) {
+      if (wo.stat) {
+        uint32_t mx = cmx;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+        const bool bad = __ballot(cbad) != 0ull;
+        if (lane == 0) {
+          atomicMax(wo.stat, mx);
+          if (bad) atomicOr(wo.stat + 1, 1u);
+        }
+      }
+    }
+  };
   // drain: the last tile's epilogue, with the M waves gone
   if constexpr (!(VAR & 4)) {
 #define DSVGD_GRS_D(KK)                                              \
@@ -613,6 +652,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #undef DSVGD_GRS_D
   }
   if (kBr) sw.finish_tile(sl, eslot, ew2);
+  publish_stat();
 }
 
 }  // namespace dsvgd

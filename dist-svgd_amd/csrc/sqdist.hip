@@ -957,7 +957,7 @@ size_t dsvgd_w2_cost_h2_workspace_bytes(int64_t m, int64_t n, int64_t d) {
 
 int dsvgd_w2_cost_h2(const float* X, int64_t ldx, int64_t m, const float* Y, int64_t ldy,
                      int64_t n, int64_t d, float* C, int64_t ldc, void* ws, float tau,
-                     void* stream) {
+                     uint32_t* cstat, void* stream) {
   DSVGD_REQUIRE(X && Y && C && ws, "null pointer");
   DSVGD_REQUIRE(m > 0 && n > 0 && d > 0 && d <= 1024 && ldx >= d && ldy >= d, "sizes (d <= 1024)");
   const W2CostWs w(m, n, d);
@@ -974,6 +974,8 @@ int dsvgd_w2_cost_h2(const float* X, int64_t ldx, int64_t m, const float* Y, int
   float* nrm = (float*)(base + w.off_n);
   float* rs = (float*)(base + w.off_s);
   void* Yg = base + w.off_g;
+  if (cstat && hipMemsetAsync(cstat, 0, 2 * sizeof(uint32_t), s) != hipSuccess)
+    return check_launch("w2 cost stat memset");
   int rc = dsvgd_colcenter(Y, ldy, n, d, cen, stream);
   if (rc) return rc;
   hipLaunchKernelGGL(w2_pack_kernel, dim3((unsigned)((w.img + 3) / 4)), dim3(256), 0, s, X, ldx, m,
@@ -989,6 +991,7 @@ int dsvgd_w2_cost_h2(const float* X, int64_t ldx, int64_t m, const float* Y, int
   wo.ldc = ldc;
   wo.d = (int)d;
   wo.tau = tau;
+  wo.stat = cstat;
   wo.vec = (d % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)X & 15) == 0 &&
             ((uintptr_t)Y & 15) == 0)
                ? 1

@@ -245,6 +245,14 @@ __global__ __launch_bounds__(256) void w2_cmax_kernel(const float* __restrict__ 
   if (bad) atomicExch(&ctl->done, 3);
 }
 
+// cmax and the bad-input flag from the cost kernel's own (dsvgd_w2_cost_h2 cstat)
+__global__ void w2_cstat_kernel(const uint32_t* __restrict__ cstat, W2Ctl* ctl) {
+  if (threadIdx.x == 0) {
+    ctl->cmax = __uint_as_float(cstat[0]);
+    if (cstat[1]) ctl->done = 3;
+  }
+}
+
 // Warm start, adaptive: how far the previous plan `prev` is from
 // complementary slackness under the new costs and the kept prices,
 //   viol = max_i [ max_j (-C_ij - p_j) - min_{slots s of i} (-C_i,prev[s] - p_prev[s]) ],
@@ -1393,25 +1401,37 @@ int dsvgd_w2_cost(const float* X, int64_t ldx, int64_t m, const float* Y, int64_
 
 static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
                      int64_t max_rounds, int warm_phases, const int32_t* prev, int32_t* assign,
-                     int64_t* rounds_out, void* stream);
+                     int64_t* rounds_out, void* stream, const uint32_t* cstat);
 
 int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
                     int64_t max_rounds, int warm_phases, int32_t* assign, int64_t* rounds_out,
                     void* stream) {
   DSVGD_REQUIRE(warm_phases >= 0, "warm_phases");
-  return w2_assign(C, ldc, m, n, ws, max_rounds, warm_phases, nullptr, assign, rounds_out, stream);
+  return w2_assign(C, ldc, m, n, ws, max_rounds, warm_phases, nullptr, assign, rounds_out, stream,
+                   nullptr);
 }
 
 int dsvgd_w2_assign_warm(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
                          int64_t max_rounds, const int32_t* prev_assign, int32_t* assign,
                          int64_t* rounds_out, void* stream) {
   DSVGD_REQUIRE(prev_assign, "null prev_assign");
-  return w2_assign(C, ldc, m, n, ws, max_rounds, -1, prev_assign, assign, rounds_out, stream);
+  return w2_assign(C, ldc, m, n, ws, max_rounds, -1, prev_assign, assign, rounds_out, stream,
+                   nullptr);
+}
+
+int dsvgd_w2_assign_stat(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
+                         int64_t max_rounds, int warm_phases, const int32_t* prev_assign,
+                         int32_t* assign, int64_t* rounds_out, const uint32_t* cstat,
+                         void* stream) {
+  DSVGD_REQUIRE(cstat, "null cstat");
+  DSVGD_REQUIRE(prev_assign || warm_phases >= 0, "warm_phases");
+  return w2_assign(C, ldc, m, n, ws, max_rounds, prev_assign ? -1 : warm_phases, prev_assign,
+                   assign, rounds_out, stream, cstat);
 }
 
 static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
                      int64_t max_rounds, int warm_phases, const int32_t* prev, int32_t* assign,
-                     int64_t* rounds_out, void* stream) {
+                     int64_t* rounds_out, void* stream, const uint32_t* cstat) {
   DSVGD_REQUIRE(C && ws && assign, "null pointer");
   DSVGD_REQUIRE(m > 0 && n > 0 && ldc >= n, "sizes");
   DSVGD_REQUIRE(n % m == 0, "n must be a multiple of m (n = R m slots)");
@@ -1432,8 +1452,12 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
         hipMemsetAsync((char*)ws + kW2CtlBytes + prices, 0, total_b - kW2CtlBytes - prices, s) !=
             hipSuccess)))
     return check_launch("w2 workspace memset");
-  const int cblocks = (int)std::min<int64_t>(4096, m * ((n + 2047) / 2048));
-  hipLaunchKernelGGL(w2_cmax_kernel, dim3(cblocks), dim3(256), 0, s, C, ldc, m, n, w.ctl);
+  if (cstat) {  // taken while the cost was written (dsvgd_w2_cost_h2)
+    hipLaunchKernelGGL(w2_cstat_kernel, dim3(1), dim3(64), 0, s, cstat, w.ctl);
+  } else {
+    const int cblocks = (int)std::min<int64_t>(4096, m * ((n + 2047) / 2048));
+    hipLaunchKernelGGL(w2_cmax_kernel, dim3(cblocks), dim3(256), 0, s, C, ldc, m, n, w.ctl);
+  }
   if (prev)
     hipLaunchKernelGGL(w2_violation_kernel, dim3((unsigned)std::min<int64_t>(1024, (m + 3) / 4)),
                        dim3(256), 0, s, C, ldc, m, n, n / m, prev, w);

@@ -115,9 +115,11 @@ SIGNATURES = {
     "dsvgd_w2_cost": (_int, [_p, _i64, _i64, _p, _i64, _i64, _i64, _p, _i64, _p]),
     "dsvgd_w2_workspace_bytes": (_c.c_size_t, [_i64, _i64]),
     "dsvgd_w2_cost_h2_workspace_bytes": (_c.c_size_t, [_i64, _i64, _i64]),
-    "dsvgd_w2_cost_h2": (_int, [_p, _i64, _i64, _p, _i64, _i64, _i64, _p, _i64, _p, _c.c_float, _p]),
+    "dsvgd_w2_cost_h2": (_int, [_p, _i64, _i64, _p, _i64, _i64, _i64, _p, _i64, _p, _c.c_float, _p,
+                                 _p]),
     "dsvgd_w2_assign": (_int, [_p, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p]),
     "dsvgd_w2_assign_warm": (_int, [_p, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p]),
+    "dsvgd_w2_assign_stat": (_int, [_p, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p, _p, _p]),
     "dsvgd_w2_trace": (_i64, [_p, _i64]),
     "dsvgd_w2_set_keep": (_int, [_int]),
     "dsvgd_w2_set_theta": (_f64, [_f64]),

@@ -61,6 +61,9 @@ class W2Term(object):
                                  device=self.device)
             nb = int(lib.dsvgd_w2_cost_h2_workspace_bytes(m, n, d))
             self.cws = torch.empty(nb + 256, dtype=torch.uint8, device=self.device)
+            # C's largest entry and finiteness, taken while the cost kernel
+            # writes C (the solve then skips its own pass over C for them)
+            self.cstat = torch.zeros(2, dtype=torch.int32, device=self.device)
         else:
             self.ldc = n
             self.C = torch.empty((m, n), dtype=torch.float32, device=self.device)
@@ -81,14 +84,21 @@ class W2Term(object):
             ws = N.ptr(self.cws)
             ws = (ws + 255) // 256 * 256
             N.call("dsvgd_w2_cost_h2", N.ptr(X), N.ld(X), self.m, N.ptr(Y), N.ld(Y), self.n,
-                   self.d, N.ptr(self.C), self.ldc, ws, float(self.TAU), s)
+                   self.d, N.ptr(self.C), self.ldc, ws, float(self.TAU), N.ptr(self.cstat), s)
         else:
             N.call("dsvgd_w2_cost", N.ptr(X), N.ld(X), self.m, N.ptr(Y), N.ld(Y), self.n, self.d,
                    N.ptr(self.C), self.ldc, s)
         rounds = ctypes.c_int64(0)
         N.load().dsvgd_w2_set_keep(int(bool(self.KEEP)))    # returns the old setting
         N.load().dsvgd_w2_set_theta(float(self.THETA))
-        if self.warm and self._solved and self.WARM_PHASES is None:
+        if self.cost == "h2":
+            warm_start = self.warm and self._solved and self.WARM_PHASES is None
+            warm = (self.WARM_PHASES or 0) if (self.warm and self._solved) else 0
+            N.call("dsvgd_w2_assign_stat", N.ptr(self.C), self.ldc, self.m, self.n,
+                   N.ptr(self.ws), self.MAX_ROUNDS, 0 if warm_start else warm,
+                   N.ptr(self.assign) if warm_start else None, N.ptr(self.assign),
+                   ctypes.addressof(rounds), N.ptr(self.cstat), s)
+        elif self.warm and self._solved and self.WARM_PHASES is None:
             # prev and out may alias: the plan is only written after the solve
             N.call("dsvgd_w2_assign_warm", N.ptr(self.C), self.ldc, self.m, self.n,
                    N.ptr(self.ws), self.MAX_ROUNDS, N.ptr(self.assign), N.ptr(self.assign),

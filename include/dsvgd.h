@@ -652,11 +652,13 @@ int dsvgd_w2_cost(const float* X, int64_t ldx, int64_t m, const float* Y, int64_
  * differences in dsvgd_w2_cost's order (the same bits).  C needs
  * roundup(m, 128) rows and ldc >= roundup(n, 256) (16-byte aligned rows;
  * the padding is written); ws: dsvgd_w2_cost_h2_workspace_bytes, 256-byte
- * aligned.  d <= 1024. */
+ * aligned.  d <= 1024.  cstat (NULL, or 2 device words): the largest entry
+ * of C (float bits) and a non-finite flag, taken while C is written --
+ * dsvgd_w2_assign_stat then skips its pass over C for them. */
 size_t dsvgd_w2_cost_h2_workspace_bytes(int64_t m, int64_t n, int64_t d);
 int dsvgd_w2_cost_h2(const float* X, int64_t ldx, int64_t m, const float* Y, int64_t ldy,
                      int64_t n, int64_t d, float* C, int64_t ldc, void* ws, float tau,
-                     void* stream);
+                     uint32_t* cstat, void* stream);
 /* Device workspace of dsvgd_w2_assign (32 n + 256 bytes). */
 size_t dsvgd_w2_workspace_bytes(int64_t m, int64_t n);
 /* assign[s] = column of slot s in an optimal plan (replaces scipy linprog,
@@ -678,6 +680,14 @@ int dsvgd_w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
 int dsvgd_w2_assign_warm(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
                          int64_t max_rounds, const int32_t* prev_assign, int32_t* assign,
                          int64_t* rounds_out, void* stream);
+/* dsvgd_w2_assign (prev_assign NULL, warm_phases as there) or
+ * dsvgd_w2_assign_warm (prev_assign set) with C's largest entry and
+ * finiteness taken from cstat (dsvgd_w2_cost_h2's) instead of a pass over C
+ * (round 6).  The same plan. */
+int dsvgd_w2_assign_stat(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws,
+                         int64_t max_rounds, int warm_phases, const int32_t* prev_assign,
+                         int32_t* assign, int64_t* rounds_out, const uint32_t* cstat,
+                         void* stream);
 /* Process-wide switch of the auction's phase keep (default 0): a new
  * epsilon phase, and dsvgd_w2_assign_warm's first phase with the previous
  * plan, keep every slot whose column still meets epsilon-complementary

@@ -39,7 +39,8 @@ def case(m, n, d, kind, seed=0):
         for _ in range(3):
             if w.cost == "h2":
                 N.call("dsvgd_w2_cost_h2", N.ptr(X), d, m, N.ptr(P), d, n, d, N.ptr(w.C), w.ldc,
-                       (N.ptr(w.cws) + 255) // 256 * 256, float(w.TAU), N.stream(X.device))
+                       (N.ptr(w.cws) + 255) // 256 * 256, float(w.TAU), N.ptr(w.cstat),
+                       N.stream(X.device))
             else:
                 N.call("dsvgd_w2_cost", N.ptr(X), d, m, N.ptr(P), d, n, d, N.ptr(w.C), w.ldc,
                        N.stream(X.device))

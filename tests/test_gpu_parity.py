@@ -850,12 +850,18 @@ def _w2_cost(X, P, form):
     if form == "h2":
         N.call("dsvgd_w2_cost_h2", N.ptr(Xg), X.shape[1], X.shape[0], N.ptr(Pg), P.shape[1],
                P.shape[0], X.shape[1], N.ptr(w.C), w.ldc, (N.ptr(w.cws) + 255) // 256 * 256,
-               float(w.TAU), N.stream(torch.device(DEV)))
+               float(w.TAU), N.ptr(w.cstat), N.stream(torch.device(DEV)))
     else:
         N.call("dsvgd_w2_cost", N.ptr(Xg), X.shape[1], X.shape[0], N.ptr(Pg), P.shape[1],
                P.shape[0], X.shape[1], N.ptr(w.C), w.ldc, N.stream(torch.device(DEV)))
     torch.cuda.synchronize()
-    return w.C[:X.shape[0], :P.shape[0]].cpu().numpy()
+    C = w.C[:X.shape[0], :P.shape[0]].cpu().numpy()
+    if form == "h2":
+        # the largest entry and the finite flag, taken while C was written
+        # (what the solve's own pass over C would find; dsvgd_w2_assign_stat)
+        st = w.cstat.cpu().numpy().view(np.uint32)
+        assert st[0] == C.max().view(np.uint32) and st[1] == 0, (st, C.max())
+    return C
 
 
 @pytest.mark.parametrize("m,n,d,kind", [(300, 900, 37, "random"), (1024, 1024, 256, "svgd"),
