@@ -74,6 +74,7 @@ struct W2Out {
   // stat[0]: the largest entry's bits, stat[1]: 1 if an entry is not finite
   // (what w2_cmax_kernel finds in a pass over C; zeroed by the caller)
   uint32_t* stat = nullptr;
+  int nt = 1;                 // C's stores non-temporal (dsvgd_w2_set_cost_nt)
 };
 
 // VAR (timing probes, dsvgd_gram_set_rs(5 / 6 / 7)): 4 = the E waves skip
@@ -545,9 +546,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const int row = 32 * bi + (lane & 15);
       const int col = 16 * (2 * bj + (SL & 1)) + 4 * h + 8 * ((lane >> 4) & 1);
       const int o0 = (int)((row * wo.ldc + col) * 4);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[0]), rD, o0, 0, 2);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[1]), rD,
-                                             o0 + (int)(16 * wo.ldc * 4), 0, 2);
+      // half-line pieces (the other 64 bytes of each row's line come one
+      // slice later): nt, or the default policy so the L2 merges the halves
+      // before they go out (dsvgd_w2_set_cost_nt, A/B)
+      if (wo.nt) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[0]), rD, o0, 0, 2);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[1]), rD,
+                                               o0 + (int)(16 * wo.ldc * 4), 0, 2);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[0]), rD, o0, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[1]), rD,
+                                               o0 + (int)(16 * wo.ldc * 4), 0, 0);
+      }
     } else {
       const int vo = (32 * bi + (lane & 15)) * 64 + 16 * h + 32 * ((lane >> 4) & 1);
       constexpr int so = (2 * bj + (SL & 1)) * kPanelElems * 4;

@@ -955,6 +955,13 @@ size_t dsvgd_w2_cost_h2_workspace_bytes(int64_t m, int64_t n, int64_t d) {
   return (size_t)W2CostWs(m, n, d).bytes;
 }
 
+static int g_w2_cost_nt = 1;
+int dsvgd_w2_set_cost_nt(int on) {
+  const int prev = g_w2_cost_nt;
+  g_w2_cost_nt = on ? 1 : 0;
+  return prev;
+}
+
 int dsvgd_w2_cost_h2(const float* X, int64_t ldx, int64_t m, const float* Y, int64_t ldy,
                      int64_t n, int64_t d, float* C, int64_t ldc, void* ws, float tau,
                      uint32_t* cstat, void* stream) {
@@ -992,6 +999,7 @@ int dsvgd_w2_cost_h2(const float* X, int64_t ldx, int64_t m, const float* Y, int
   wo.d = (int)d;
   wo.tau = tau;
   wo.stat = cstat;
+  wo.nt = g_w2_cost_nt;
   wo.vec = (d % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)X & 15) == 0 &&
             ((uintptr_t)Y & 15) == 0)
                ? 1

@@ -119,6 +119,7 @@ SIGNATURES = {
                                  _p]),
     "dsvgd_w2_assign": (_int, [_p, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p]),
     "dsvgd_w2_assign_warm": (_int, [_p, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p]),
+    "dsvgd_w2_set_cost_nt": (_int, [_int]),
     "dsvgd_w2_assign_stat": (_int, [_p, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p, _p, _p]),
     "dsvgd_w2_trace": (_i64, [_p, _i64]),
     "dsvgd_w2_set_keep": (_int, [_int]),

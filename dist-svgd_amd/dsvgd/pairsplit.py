@@ -44,8 +44,17 @@ class PairSplitPlan(object):
     GRAM_RECT, GRAM_DIAG, GRAM_FALLBACK = 0, 1, 2
     # the diagonal square as one full rectangle on the one-kernel Gram (both
     # triangles computed, each entry counted once) instead of its upper tiles
-    # on the 8-wave kernel with mirror stores (round 6, A/B)
-    FULL_SQUARE = True
+    # on the 8-wave kernel with mirror stores, from S = FULL_SQUARE_MIN_S
+    # ranks on (round 6: Gram stage at S = 8 0.525 vs 0.615 ms, S = 4 1.125
+    # vs 1.196; at S = 2 the square is half the rank's Gram and the mirror
+    # kernel's half of it wins, 2.39 vs 2.66 -- profiles/r14u, r13z).
+    # FULL_SQUARE: True / False forces it (A/B), None = by S.
+    FULL_SQUARE = None
+    FULL_SQUARE_MIN_S = 4
+
+    @classmethod
+    def full_square(cls, S):
+        return cls.FULL_SQUARE if cls.FULL_SQUARE is not None else S >= cls.FULL_SQUARE_MIN_S
 
     @staticmethod
     def aligned(S, m):
@@ -80,7 +89,8 @@ class PairSplitPlan(object):
         # Gram parts (include/dsvgd.h dsvgd_gram_part): accounted, then the
         # fallback-only complement (the range guard's whole-row-block phi)
         parts = [dict(row_off=0, rows=m, col0=r0, cols=m,
-                      kind=self.GRAM_RECT if self.FULL_SQUARE else self.GRAM_DIAG, weight2=0)]
+                      kind=self.GRAM_RECT if self.full_square(S) else self.GRAM_DIAG,
+                      weight2=0)]
         for c0, ln in _cyclic(r0 + m, self.window[1] - m, n):
             parts.append(dict(row_off=0, rows=m, col0=c0, cols=ln, kind=self.GRAM_RECT, weight2=1))
         if self.high:

@@ -655,6 +655,9 @@ int dsvgd_w2_cost(const float* X, int64_t ldx, int64_t m, const float* Y, int64_
  * aligned.  d <= 1024.  cstat (NULL, or 2 device words): the largest entry
  * of C (float bits) and a non-finite flag, taken while C is written --
  * dsvgd_w2_assign_stat then skips its pass over C for them. */
+/* A/B switch of dsvgd_w2_cost_h2's C stores (returns the previous): 1
+ * (default) non-temporal, 0 the default cache policy. */
+int dsvgd_w2_set_cost_nt(int on);
 size_t dsvgd_w2_cost_h2_workspace_bytes(int64_t m, int64_t n, int64_t d);
 int dsvgd_w2_cost_h2(const float* X, int64_t ldx, int64_t m, const float* Y, int64_t ldy,
                      int64_t n, int64_t d, float* C, int64_t ldc, void* ws, float tau,

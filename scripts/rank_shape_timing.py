@@ -74,7 +74,7 @@ def main():
         for k in ("W_SPLITS", "H_SPLITS", "REST_SPLITS"):
             setattr(dsvgd.PhiEngine, k, ov.get(k) or None)
         from dsvgd.pairsplit import PairSplitPlan
-        PairSplitPlan.FULL_SQUARE = bool(ov.get("FULL_SQUARE", PairSplitPlan.FULL_SQUARE))
+        PairSplitPlan.FULL_SQUARE = (bool(ov["FULL_SQUARE"]) if "FULL_SQUARE" in ov else None)
         dsvgd.PhiEngine.WINDOW_SIDE_STREAM = side
         dsvgd.PhiEngine.REST_BESIDE = rest
         dsvgd.PhiEngine.FWD_ZSPLIT = fz or None
@@ -149,7 +149,7 @@ def main():
                           "t_splits": getattr(eng, "t_splits", None),
                           "row0": r * m, "N_local": per,
                           "ms_per_step_no_comm": e0.elapsed_time(e1) / args.steps,
-                          "sym_layout": bool(eng.sym), "full_square": bool(ov.get("FULL_SQUARE", 0)),
+                          "sym_layout": bool(eng.sym), "full_square": bool(PairSplitPlan.full_square(S)),
                           "stages_ms": st}), flush=True)
           eng.timer = None
         del eng
