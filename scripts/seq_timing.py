@@ -41,6 +41,9 @@ def main():
                     help="comma list of engine.GSW_PIPELINE values (1: the pipelined wide "
                          "sweep, 0: block group after group): the blocked sweep alone timed "
                          "for each, the results compared")
+    ap.add_argument("--reserve", default=None,
+                    help="comma list of engine.GSW_SIDE_RESERVE values (CUs the pipelined "
+                         "sweep's side passes leave to the walk): the sweep timed for each")
     ap.add_argument("--rows-sample", type=int, default=2048,
                     help="rows of the per-row path to time (0: skip it)")
     args = ap.parse_args()
@@ -146,6 +149,25 @@ def main():
                               "max_abs_diff_between": float((vals[0] - vals[-1]).abs().max()),
                               "max_abs_move": scale_x}), flush=True)
             E.GSW_PIPELINE = True
+        if args.reserve:
+            import dsvgd.engine as E
+            res, xs = {}, {}
+            keep = E.GSW_SIDE_RESERVE
+            for rv in [int(v) for v in args.reserve.split(",")] * 2:
+                E.GSW_SIDE_RESERVE = rv
+                Xb, Sb = X.clone(), S0.clone()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                sequential_sweep(Xb, Sb, range(n), eng.state, 1e-4, target=tgt, score_scale=scale)
+                torch.cuda.synchronize()
+                res.setdefault(rv, []).append(1e3 * (time.perf_counter() - t0))
+                xs[rv] = Xb
+            vals = list(xs.values())
+            print(json.dumps({"config": name, "sweep_ms_by_side_reserve": res,
+                              "finite": [bool(torch.isfinite(v).all()) for v in vals],
+                              "max_abs_diff_between": float((vals[0] - vals[-1]).abs().max())}),
+                  flush=True)
+            E.GSW_SIDE_RESERVE = keep
         if args.splits:
             import dsvgd.engine as E
             res = {}
