@@ -33,8 +33,17 @@ int check_launch(const char* kernel) {
 // Grid of a persistent kernel: resident blocks per CU (occupancy of `fn` at
 // `threads` threads, no dynamic LDS) x CUs, a multiple of the 8 XCDs.
 // Cached per (kernel, device).
+// CUs a persistent launch leaves free (dsvgd_set_cu_reserve): the pipelined
+// Gauss-Seidel sweep's side-stream passes leave room for the walk beside them
+static int g_cu_reserve = 0;
+int set_cu_reserve(int cus) {
+  const int prev = g_cu_reserve;
+  g_cu_reserve = cus < 0 ? 0 : cus;
+  return prev;
+}
+
 int persistent_blocks(const void* fn, int* blocks, int threads) {
-  struct Entry { const void* fn; int dev; int blocks; };
+  struct Entry { const void* fn; int dev; int per_cu, cus; };
   static thread_local Entry cache[16];
   static thread_local int ncache = 0;
   int dev = 0;
@@ -42,20 +51,25 @@ int persistent_blocks(const void* fn, int* blocks, int threads) {
     set_error("hipGetDevice failed");
     return DSVGD_E_LAUNCH;
   }
-  for (int i = 0; i < ncache; ++i)
-    if (cache[i].fn == fn && cache[i].dev == dev) {
-      *blocks = cache[i].blocks;
-      return DSVGD_OK;
-    }
   int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
-    set_error("occupancy query failed");
-    return DSVGD_E_LAUNCH;
+  bool hit = false;
+  for (int i = 0; i < ncache && !hit; ++i)
+    if (cache[i].fn == fn && cache[i].dev == dev) {
+      per_cu = cache[i].per_cu;
+      cus = cache[i].cus;
+      hit = true;
+    }
+  if (!hit) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+      set_error("occupancy query failed");
+      return DSVGD_E_LAUNCH;
+    }
+    if (ncache < 16) cache[ncache++] = Entry{fn, dev, per_cu, cus};
   }
-  int b = (per_cu < 1 ? 1 : per_cu) * cus;
+  const int use = cus - g_cu_reserve >= 8 ? cus - g_cu_reserve : 8;
+  int b = (per_cu < 1 ? 1 : per_cu) * use;
   b = b >= 8 ? b / 8 * 8 : 8;
-  if (ncache < 16) cache[ncache++] = Entry{fn, dev, b};
   *blocks = b;
   return DSVGD_OK;
 }
@@ -521,5 +535,7 @@ int dsvgd_set_bandwidth(dsvgd_select_state* st, float h, void* stream) {
   hipLaunchKernelGGL(set_bandwidth_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, st, h);
   return check_launch("set_bandwidth");
 }
+
+int dsvgd_set_cu_reserve(int cus) { return dsvgd::set_cu_reserve(cus); }
 
 }  // extern "C"

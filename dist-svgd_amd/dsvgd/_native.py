@@ -69,6 +69,7 @@ SIGNATURES = {
     "dsvgd_phi_set_symrow": (_int, [_int]),
     "dsvgd_gram_set_rs": (_int, [_int]),
     "dsvgd_gram_set_group": (_int, [_int]),
+    "dsvgd_set_cu_reserve": (_int, [_int]),
     "dsvgd_gram_debug_stamps": (_int, [_p]),
     "dsvgd_phi_splits_sym": (_i64, [_i64, _i64]),
     "dsvgd_phi_set_xmap": (_int, [_int]),

@@ -1087,6 +1087,10 @@ _WIDE = {}
 # saves, 536 vs 488 ms -- profiles/r14h)
 GSW_PIPELINE = True
 GSW_PIPELINE_MAX_D = 256
+# CUs the side stream's passes leave free (dsvgd_set_cu_reserve, and the
+# phi_mm split-K slices cut by as many) so the walk -- one workgroup with
+# most of a CU's LDS -- starts beside them instead of after them
+GSW_SIDE_RESERVE = 8
 GSW_PIPE_SPIN_NS = 0   # tests: hold the walk's stream this long after each pass is posted
 # blocks per wide pass of the wide Gauss-Seidel sweep (1: block after block;
 # config D sweep 278.7 / 253.0 / 256.2 ms at 1 / 2 / 4, profiles/r13u; None:
@@ -1167,10 +1171,11 @@ def _blocked_sweep_wide(X, S, rows, h_state, step, kind, target, score_scale, ph
         W.images(g0, gn, s)
 
 
-def _gsw_pass(W, g0, gn, n, d, h_state, norms, Q, Qr, s, exclude=None):
+def _gsw_pass(W, g0, gn, n, d, h_state, norms, Q, Qr, s, exclude=None, splits=None):
     """The wide pass of the group's rows [g0, g0 + gn) against every row not
     moved before them in the group (and, pipelined, not in the `exclude` =
     (p0, pn) group walking beside it): Q = [K Xc | K S], Qr = K 1."""
+    z = splits or W.splits
     if W.gram_h2:
         N.call("dsvgd_sqdist_h2", N.ptr(W.Yg), N.ptr(norms), g0, gn, n, d, N.ptr(W.D),
                W.n_pad, 0, None, None, 0, N.ptr(W.rsc), s)
@@ -1182,12 +1187,12 @@ def _gsw_pass(W, g0, gn, n, d, h_state, norms, Q, Qr, s, exclude=None):
         N.call("dsvgd_gs_mask_cols", N.ptr(W.D), W.n_pad, gn, exclude[0], exclude[1], s)
     if W.phi_x3:
         N.call("dsvgd_phi_mm_x3", N.ptr(W.D), W.n_pad, N.ptr(W.Yx3), W.ldy, g0, gn, n,
-               h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), 0, int(W.m16),
+               h_state.ptr, z, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), 0, int(W.m16),
                None, s)
     else:
         N.call("dsvgd_phi_mm", N.ptr(W.D), W.n_pad, N.ptr(W.Y), W.ldy, g0, gn, n,
-               h_state.ptr, W.splits, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), s)
-    N.call("dsvgd_phi_partial_reduce", N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), W.splits, gn,
+               h_state.ptr, z, N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), s)
+    N.call("dsvgd_phi_partial_reduce", N.ptr(W.KY), W.ldy, N.ptr(W.rowsum), z, gn,
            2 * W.dp, N.ptr(Q), W.ldy, N.ptr(Qr), s)
 
 
@@ -1217,14 +1222,21 @@ def _pipelined_sweep_wide(W, X, S, groups, n, d, h_state, step, sk, mu, lam, xd,
     Qs = ((W.Q, W.Qr), (W.Q2, W.Qr2))
     done = [None] * len(groups)
 
+    lib = N.load()
+    zs = max(1, W.splits - GSW_SIDE_RESERVE) if W.splits > 2 * GSW_SIDE_RESERVE else W.splits
+
     def post(k):
         g0, gn = groups[k]
         W.norms_s.copy_(W.norms)          # on the walk's stream, after group k - 2's images
         side.wait_stream(main)
-        with torch.cuda.stream(side):
-            _gsw_pass(W, g0, gn, n, d, h_state, W.norms_s, *Qs[k % 2], side.cuda_stream,
-                      exclude=groups[k - 1] if k > 0 else None)
-            done[k] = side.record_event()
+        prev = lib.dsvgd_set_cu_reserve(GSW_SIDE_RESERVE)
+        try:
+            with torch.cuda.stream(side):
+                _gsw_pass(W, g0, gn, n, d, h_state, W.norms_s, *Qs[k % 2], side.cuda_stream,
+                          exclude=groups[k - 1] if k > 0 else None, splits=zs)
+                done[k] = side.record_event()
+        finally:
+            lib.dsvgd_set_cu_reserve(prev)
 
     post(0)
     for k, (g0, gn) in enumerate(groups):

@@ -249,6 +249,11 @@ int dsvgd_phi_set_symrow(int on);
  * given to dsvgd_gram_debug_stamps; 9: the MFMA waves' B ring 4 deep).
  * Returns the previous setting. */
 int dsvgd_gram_set_rs(int on);
+/* CUs the persistent launches issued after this call leave free (returns
+ * the previous; 0 = none): the pipelined Gauss-Seidel sweep sets it around
+ * its side-stream passes so the walk (one workgroup, most of a CU's LDS)
+ * finds a free CU beside them.  A launch-time host setting. */
+int dsvgd_set_cu_reserve(int cus);
 /* Strips per unit group of the split-role Gram's walk (A/B switch, returns
  * the previous setting): 8 (default) or 16.  Each group's strip images stay
  * in an XCD's L2 while every column pair's image streams past once. */

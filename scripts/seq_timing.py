@@ -44,6 +44,11 @@ def main():
     ap.add_argument("--reserve", default=None,
                     help="comma list of engine.GSW_SIDE_RESERVE values (CUs the pipelined "
                          "sweep's side passes leave to the walk): the sweep timed for each")
+    ap.add_argument("--graphs", type=int, default=0,
+                    help="1: also time DistSampler.make_step as the product runs it at S = 1 "
+                         "(captured as one HIP graph on the second call, replayed after)")
+    ap.add_argument("--pipe-max-d", type=int, default=None,
+                    help="engine.GSW_PIPELINE_MAX_D for the --pipe / --reserve runs")
     ap.add_argument("--rows-sample", type=int, default=2048,
                     help="rows of the per-row path to time (0: skip it)")
     args = ap.parse_args()
@@ -54,6 +59,9 @@ def main():
     # partition mode's exchange_scores=False; 2048 data rows = config D's
     # N_local at S = 8), scores scaled by N_global / N_local = 8
     shapes = {"D": (65536, 256, 16384), "E": (65536, 1024, 8192), "R": (16384, 256, 2048)}
+    if args.pipe_max_d is not None:
+        import dsvgd.engine as E
+        E.GSW_PIPELINE_MAX_D = args.pipe_max_d
     for name in args.only.split(","):
         n, d, Ng = shapes[name]
         refresh = name == "R"
@@ -73,6 +81,18 @@ def main():
         ds.make_step(1e-4)
         torch.cuda.synchronize()
         blocked_ms = 1e3 * (time.perf_counter() - t0)
+        graph_ms = None
+        if args.graphs:
+            ds.graphs = True
+            ds.make_step(1e-4)                  # eager (graphs start counting here)
+            ds.make_step(1e-4)                  # captured
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(2):
+                ds.make_step(1e-4)              # replayed
+            torch.cuda.synchronize()
+            graph_ms = 1e3 * (time.perf_counter() - t0) / 2
+            ds.graphs = False
         # the per-row kernels over a sample of rows, same scores and bandwidth
         eng = next(iter(ds._engines.values()))
         if refresh:     # the sweep's starting scores (the sampler keeps them internal)
@@ -102,7 +122,8 @@ def main():
         print(json.dumps({"config": name, "n": n, "d": d, "N_local": Ng,
                           "scores": "refreshed (logreg)" if refresh else "frozen (all_scores)",
                           "order": "sequential",
-                          "step_ms_blocked": blocked_ms, "sweep_only_ms_blocked": sweep_ms,
+                          "step_ms_blocked": blocked_ms, "step_ms_graph": graph_ms,
+                          "sweep_only_ms_blocked": sweep_ms,
                           "particle_updates_per_s": n / blocked_ms * 1e3,
                           "per_row_ms_extrapolated": per_row_ms, "per_row_sample_rows": k,
                           "speedup_vs_per_row": per_row_ms / sweep_ms if per_row_ms else None}),
@@ -159,8 +180,10 @@ def main():
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 sequential_sweep(Xb, Sb, range(n), eng.state, 1e-4, target=tgt, score_scale=scale)
+                th = time.perf_counter()        # the host's enqueue time of the sweep
                 torch.cuda.synchronize()
                 res.setdefault(rv, []).append(1e3 * (time.perf_counter() - t0))
+                res.setdefault("host_%d" % rv, []).append(1e3 * (th - t0))
                 xs[rv] = Xb
             vals = list(xs.values())
             print(json.dumps({"config": name, "sweep_ms_by_side_reserve": res,
