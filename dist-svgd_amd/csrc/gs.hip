@@ -342,7 +342,7 @@ __global__ __launch_bounds__(256) void gsw_group_corr_kernel(
     const dsvgd_select_state* __restrict__ st, float* __restrict__ Q, int64_t ldq,
     float* __restrict__ Qr) {
   __shared__ float xi[kGswMaxD];
-  __shared__ float kv[kGsB];
+  __shared__ float kv[2 * kGsB];   // up to two blocks of earlier rows (a group)
   const int i = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const float scale = -st->inv_h * kLog2e;
   for (int64_t c = t; c < d; c += 256) xi[c] = X[(r0 + i) * ldx + c];
@@ -350,51 +350,56 @@ __global__ __launch_bounds__(256) void gsw_group_corr_kernel(
   if (d <= 256) {
     // the same sums in the same order with every load of a loop issued
     // before its first use (the general loops below wait on one L2 round
-    // trip per moved row: 28 us per 64-row correction at config D, r13ag)
+    // trip per moved row: 28 us per 64-row correction at config D, r13ag);
+    // the earlier rows in halves of 64
     float xv[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) xv[k] = lane + 64 * k < d ? xi[lane + 64 * k] : 0.f;
-    float xr[16][4];
+    for (int hb = 0; hb < pB; hb += kGsB) {
+      float xr[16][4];
 #pragma unroll
-    for (int jj = 0; jj < 16; ++jj) {
-      const int j = w + 4 * jj;
+      for (int jj = 0; jj < 16; ++jj) {
+        const int j = hb + w + 4 * jj;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int c = lane + 64 * k;
-        xr[jj][k] = (j < pB && c < d) ? X[(p0 + j) * ldx + c] : xv[k];
-      }
-    }
-#pragma unroll
-    for (int jj = 0; jj < 16; ++jj) {
-      const int j = w + 4 * jj;
-      float a = 0.f;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float df = xv[k] - xr[jj][k];
-        a = fmaf(df, df, a);
+        for (int k = 0; k < 4; ++k) {
+          const int c = lane + 64 * k;
+          xr[jj][k] = (j < pB && c < d) ? X[(p0 + j) * ldx + c] : xv[k];
+        }
       }
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
-      if (lane == 0 && j < pB) kv[j] = __builtin_amdgcn_exp2f(a * scale);
+      for (int jj = 0; jj < 16; ++jj) {
+        const int j = hb + w + 4 * jj;
+        float a = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float df = xv[k] - xr[jj][k];
+          a = fmaf(df, df, a);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+        if (lane == 0 && j < pB) kv[j] = __builtin_amdgcn_exp2f(a * scale);
+      }
     }
     __syncthreads();
     float* q = Q + (int64_t)i * ldq;
     const int c = t;
     if (c < d) {
       const float cc = center[c];
-      float xa[kGsB], sa[kGsB];
-#pragma unroll
-      for (int j = 0; j < kGsB; ++j) {
-        xa[j] = j < pB ? X[(p0 + j) * ldx + c] : 0.f;
-        sa[j] = j < pB ? S[(p0 + j) * lds + c] : 0.f;
-      }
       float qx = 0.f, qs = 0.f;
+      for (int hb = 0; hb < pB; hb += kGsB) {
+        float xa[kGsB], sa[kGsB];
 #pragma unroll
-      for (int j = 0; j < kGsB; ++j) {
-        if (j < pB) {   // (not break: the loop must unroll)
-          const float k = kv[j];
-          qx = fmaf(k, xa[j] - cc, qx);
-          qs = fmaf(k, sa[j], qs);
+        for (int j = 0; j < kGsB; ++j) {
+          xa[j] = hb + j < pB ? X[(p0 + hb + j) * ldx + c] : 0.f;
+          sa[j] = hb + j < pB ? S[(p0 + hb + j) * lds + c] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < kGsB; ++j) {
+          if (hb + j < pB) {   // (not break: the loop must unroll)
+            const float k = kv[hb + j];
+            qx = fmaf(k, xa[j] - cc, qx);
+            qs = fmaf(k, sa[j], qs);
+          }
         }
       }
       q[c] += qx;
@@ -1184,9 +1189,9 @@ int dsvgd_gsw_group_corr(const float* X, int64_t ldx, const float* S, int64_t ld
   const int64_t dp = roundup(d, 32);
   DSVGD_REQUIRE(n > 0 && d > 0 && d <= kGswMaxD && ldx >= d && lds >= d && ldq >= 2 * dp,
                 "sizes (d <= 1024, ldq >= 2 roundup(d, 32))");
-  DSVGD_REQUIRE(nr > 0 && nr <= 65535 && r0 >= 0 && r0 + nr <= n && pB > 0 && pB <= kGsB &&
-                    p0 >= 0 && p0 + pB <= r0,
-                "rows: the later rows [r0, r0 + nr) after a block of at most 64 rows [p0, p0 + pB)");
+  DSVGD_REQUIRE(nr > 0 && nr <= 65535 && r0 >= 0 && r0 + nr <= n && pB > 0 &&
+                    pB <= 2 * kGsB && p0 >= 0 && p0 + pB <= r0,
+                "rows: the later rows [r0, r0 + nr) after at most 128 rows [p0, p0 + pB)");
   hipLaunchKernelGGL(gsw_group_corr_kernel, dim3((unsigned)nr), dim3(256), 0, (hipStream_t)stream,
                      X, ldx, S, lds, center, d, dp, r0, p0, (int)pB, st, Q, ldq, Qr);
   return check_launch("gsw_group_corr");

@@ -1204,14 +1204,18 @@ def _pipelined_sweep_wide(W, X, S, groups, n, d, h_state, step, sk, mu, lam, xd,
       * the side stream alone writes D, KY, rowsum (its passes in order) and
         the sums Qs[(g + 1) % 2]; the walk of g reads Qs[g % 2];
       * the pass of g + 1 reads the images (Yg, rsc, Yx3) and a SNAPSHOT of
-        the norms taken after group g - 1's images were re-split: the walk of
-        g rewrites Y / norms / X rows of group g, the images of g are re-split
-        only after the pass of g + 1 is done (it masked those columns);
+        the norms (norms_s), both refreshed on the side stream after the walk
+        of g - 1 (an event), behind the pass of g: the walk of g rewrites
+        Y / norms / X rows of group g, which the pass of g + 1 masks;
+      * the images of g are re-split on the side stream after the walk of g
+        and after the pass of g + 1 (stream order), before the pass of g + 2;
+        nothing on the walk's stream reads the images;
       * before g + 1 walks, its sums gain group g's rows at their moved
         positions (dsvgd_gsw_group_corr, block by block, on the walk's stream).
 
-    The same terms as the block-after-block sweep, in another order
-    (tests/test_gpu_parity.py: against the fp64 restatement, the overlap
+    So the walk's stream runs only the walks and the corrections.  The same
+    terms as the block-after-block sweep, in another order
+    (tests/test_gpu_configs.py: against the fp64 restatement, the overlap
     forced)."""
     dev = X.device
     main = torch.cuda.current_stream(dev)
@@ -1227,8 +1231,6 @@ def _pipelined_sweep_wide(W, X, S, groups, n, d, h_state, step, sk, mu, lam, xd,
 
     def post(k):
         g0, gn = groups[k]
-        W.norms_s.copy_(W.norms)          # on the walk's stream, after group k - 2's images
-        side.wait_stream(main)
         prev = lib.dsvgd_set_cu_reserve(GSW_SIDE_RESERVE)
         try:
             with torch.cuda.stream(side):
@@ -1238,14 +1240,19 @@ def _pipelined_sweep_wide(W, X, S, groups, n, d, h_state, step, sk, mu, lam, xd,
         finally:
             lib.dsvgd_set_cu_reserve(prev)
 
+    side.wait_stream(main)              # Y, its images, the norms of the sweep's start
+    with torch.cuda.stream(side):
+        W.norms_s.copy_(W.norms)
     post(0)
     for k, (g0, gn) in enumerate(groups):
         Q, Qr = Qs[k % 2]
         main.wait_event(done[k])
         if k > 0:   # the previous group's moved rows, left out of this pass
             p0, pn = groups[k - 1]
-            for b0 in range(p0, p0 + pn, B):
-                nb = min(B, p0 + pn - b0)
+            # (one launch for up to 128 of them, in row order)
+            step_rows = 128
+            for b0 in range(p0, p0 + pn, step_rows):
+                nb = min(step_rows, p0 + pn - b0)
                 N.call("dsvgd_gsw_group_corr", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S),
                        N.ptr(W.mean), n, d, g0, gn, b0, nb, h_state.ptr, N.ptr(Q), W.ldy,
                        N.ptr(Qr), s)
@@ -1269,9 +1276,14 @@ def _pipelined_sweep_wide(W, X, S, groups, n, d, h_state, step, sk, mu, lam, xd,
                 N.call("dsvgd_gsw_group_corr", N.ptr(X), N.ld(X), N.ptr(S), N.ld(S),
                        N.ptr(W.mean), n, d, r1, g0 + gn - r1, b0, nb, h_state.ptr,
                        N.ptr(Q) + 4 * (r1 - g0) * W.ldy, W.ldy, N.ptr(Qr) + 4 * (r1 - g0), s)
-        if k + 1 < len(groups):
-            main.wait_event(done[k + 1])  # the next pass has read this group's old images
-        W.images(g0, gn, s)
+        if k + 2 < len(groups):
+            # for the passes of g + 2 on: this group's images and the norms,
+            # on the side stream after this walk (and after the pass of g + 1)
+            side.wait_event(main.record_event())
+            with torch.cuda.stream(side):
+                W.images(g0, gn, side.cuda_stream)
+                W.norms_s.copy_(W.norms)
+    main.wait_stream(side)
 
 
 def _blocked_sweep(X, S, rows, h_state, step, kind, target, score_scale, phi_out, extra, s):

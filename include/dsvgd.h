@@ -440,9 +440,11 @@ int dsvgd_gs_mask_cols(float* D, int64_t ldd, int64_t B, int64_t c0, int64_t nc,
 int dsvgd_debug_spin(int64_t ns, void* stream);
 /* The grouped wide sweep (round 5): one wide pass for a group of blocks
  * (dsvgd_gs_mask over the whole group, B <= 1024), then after each block's
- * walk the group's later rows [r0, r0 + nr) gain that block's pB <= 64 moved
- * rows [p0, p0 + pB): Q += k_ij (x_j' - c | s_j'), Qr += k_ij by explicit
- * differences, j in order (Q, Qr: the later rows' first entries). */
+ * walk the group's later rows [r0, r0 + nr) gain that block's moved rows
+ * [p0, p0 + pB): Q += k_ij (x_j' - c | s_j'), Qr += k_ij by explicit
+ * differences, j in order (Q, Qr: the later rows' first entries).  pB <= 128
+ * (round 6: a whole 128-row group in one launch, the pipelined sweep's
+ * correction for the group walked beside its pass). */
 int dsvgd_gsw_group_corr(const float* X, int64_t ldx, const float* S, int64_t lds,
                          const float* center, int64_t n, int64_t d, int64_t r0, int64_t nr,
                          int64_t p0, int64_t pB, const dsvgd_select_state* st, float* Q,
