@@ -349,6 +349,101 @@ __global__ __launch_bounds__(256) void w2_violation_rows_kernel(const float* __r
   }
 }
 
+// Warm start at R = 1 (no price cache, keep off): the first round's bids and
+// the violation above from ONE pass over C.  Every slot is free in that round
+// and nothing is held, so w2_bid_kernel<2> would scan each whole row for its
+// best value, that value's column (the lowest on a tie) and the second best
+// value (a tie counts twice) -- exactly what the violation pass reads too,
+// minus the column and the second value.  This pass keeps all three per row
+// (w2_bid_first_kernel bids from them once w2_start_kernel has set eps from
+// the violation) and the violation, eight rows per block as in
+// w2_violation_rows_kernel.  Same values, same tie rule, so the same bids and
+// the same viol bits; the unfused order (violation pass, full-scan bid round)
+// stays behind dsvgd_w2_set_fuse_first(0).  Needs n % 4 == 0, ldc % 4 == 0,
+// C 16-byte aligned.  The row results go to the price cache's arrays, unused
+// at R = 1: best -> cbound, second -> ccost (as doubles), column -> ccol.
+__device__ __forceinline__ void top2_push(double x, int c, double& b1, int& j1, double& b2) {
+  const bool gt = x > b1;  // columns arrive in increasing order: a tie keeps the lower
+  b2 = fmax(b2, gt ? b1 : x);
+  j1 = gt ? c : j1;
+  b1 = gt ? x : b1;
+}
+__device__ __forceinline__ void top2_merge(double p1, int q1, double p2, double& b1, int& j1,
+                                           double& b2) {
+  const bool first = b1 > p1 || (b1 == p1 && j1 < q1);
+  b2 = fmax(first ? p1 : b1, fmax(b2, p2));
+  if (!first) {
+    b1 = p1;
+    j1 = q1;
+  }
+}
+__global__ __launch_bounds__(256) void w2_scan_first_kernel(const float* __restrict__ C,
+                                                            int64_t ldc, int64_t m, int64_t n,
+                                                            const int32_t* __restrict__ prev,
+                                                            W2Ws w) {
+  __shared__ double r1[4][kViolRows], r2[4][kViolRows];
+  __shared__ int rj[4][kViolRows];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t i0 = (int64_t)blockIdx.x * kViolRows;
+  const int nr = (int)min<int64_t>(kViolRows, m - i0);
+  double b1[kViolRows], b2[kViolRows];
+  int j1[kViolRows];
+#pragma unroll
+  for (int r = 0; r < kViolRows; ++r) {
+    b1[r] = b2[r] = -DBL_MAX;
+    j1[r] = INT32_MAX;
+  }
+  for (int64_t j = 4 * (int64_t)t; j < n; j += 1024) {
+    const double2 pa = *reinterpret_cast<const double2*>(w.price + j);
+    const double2 pb = *reinterpret_cast<const double2*>(w.price + j + 2);
+#pragma unroll
+    for (int r = 0; r < kViolRows; ++r) {
+      if (r < nr) {
+        const float4 c = *reinterpret_cast<const float4*>(C + (i0 + r) * ldc + j);
+        top2_push(-(double)c.x - pa.x, (int)j, b1[r], j1[r], b2[r]);
+        top2_push(-(double)c.y - pa.y, (int)j + 1, b1[r], j1[r], b2[r]);
+        top2_push(-(double)c.z - pb.x, (int)j + 2, b1[r], j1[r], b2[r]);
+        top2_push(-(double)c.w - pb.y, (int)j + 3, b1[r], j1[r], b2[r]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kViolRows; ++r) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double p1 = __shfl_xor(b1[r], o, 64), p2 = __shfl_xor(b2[r], o, 64);
+      const int q1 = __shfl_xor(j1[r], o, 64);
+      top2_merge(p1, q1, p2, b1[r], j1[r], b2[r]);
+    }
+    if (lane == 0) {
+      r1[wv][r] = b1[r];
+      r2[wv][r] = b2[r];
+      rj[wv][r] = j1[r];
+    }
+  }
+  __syncthreads();
+  if (wv == 0) {
+    double vmax = 0.0;
+    if (lane < nr) {
+      double a1 = r1[0][lane], a2 = r2[0][lane];
+      int aj = rj[0][lane];
+#pragma unroll
+      for (int q = 1; q < 4; ++q) top2_merge(r1[q][lane], rj[q][lane], r2[q][lane], a1, aj, a2);
+      const int64_t i = i0 + lane;
+      w.cbound[i] = a1;
+      reinterpret_cast<double*>(w.ccost)[i] = a2;
+      w.ccol[i] = aj;
+      const int64_t a = prev[i];
+      const double worst = (a >= 0 && a < n) ? -(double)C[i * ldc + a] - w.price[a] : -DBL_MAX;
+      vmax = fmax(vmax, a1 - worst);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) vmax = fmax(vmax, __shfl_xor(vmax, o, 64));
+    if (lane == 0 && vmax > 0.0)
+      atomicMax(&w.ctl->viol, (unsigned long long)__double_as_longlong(vmax));
+  }
+}
+
 // warm_phases > 0: the prices are the previous solve's (a nearby problem:
 // SVGD moves rows and columns by one step), so the auction starts only
 // warm_phases epsilon-scaling phases above eps_final instead of at cmax/theta;
@@ -1269,6 +1364,27 @@ __global__ __launch_bounds__(256) void w2_bid_kernel(const float* __restrict__ C
   }
 }
 
+// The first round of a fused R = 1 warm start (w2_scan_first_kernel): row i's
+// one slot bids for its best column with the row's best and second values,
+// as bid_from_best with u = 1 -- one thread per row, no scan.
+__global__ __launch_bounds__(256) void w2_bid_first_kernel(int64_t m, W2Ws w) {
+  const W2Ctl* ctl = w.ctl;
+  if (ctl->done || ctl->tail) return;  // (uniform) as w2_bid_kernel
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= m) return;
+  const int kj = w.ccol[i];
+  if (kj == INT32_MAX) return;
+  const double kv = w.cbound[i], vu1 = reinterpret_cast<const double*>(w.ccost)[i];
+  const double vref = (vu1 > -DBL_MAX) ? vu1 : kv;
+  const double inc = kv - vref + ctl->eps;
+  float f = (float)inc;
+  if ((double)f > inc) f = nextafterf(f, 0.f);  // round down: keeps eps-CS
+  if (!(f > 0.f)) f = FLT_MIN;
+  const unsigned long long key =
+      ((unsigned long long)__float_as_uint(f) << 32) | (unsigned long long)(uint32_t)i;
+  atomicMax(&w.bid[kj], key);
+}
+
 __device__ void w2_control(W2Ctl* ctl, int64_t n) {
   ctl->rounds += 1;
   ctl->fresh = 0;
@@ -1387,6 +1503,13 @@ static bool& w2_nohelp_flag() {
   return k;
 }
 
+// R = 1 warm starts: the violation and the first round's scans in one pass
+// (w2_scan_first_kernel; default on, dsvgd_w2_set_fuse_first)
+static bool& w2_fuse_first_flag() {
+  static bool k = true;
+  return k;
+}
+
 // eps divisor between phases (default kTheta; A/B: dsvgd_w2_set_theta)
 static double& w2_theta() {
   static double th = kTheta;
@@ -1420,6 +1543,12 @@ int64_t dsvgd_w2_tail_stats(int64_t* out) {
     for (int k = 0; k < 6; ++k) out[k] = w2_tail_stats()[k];
   }
   return 6;
+}
+
+int dsvgd_w2_set_fuse_first(int on) {
+  const int old = w2_fuse_first_flag() ? 1 : 0;
+  w2_fuse_first_flag() = on != 0;
+  return old;
 }
 
 int dsvgd_w2_set_tail_debug(int nohelp) {
@@ -1514,13 +1643,19 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
     const int cblocks = (int)std::min<int64_t>(4096, m * ((n + 2047) / 2048));
     hipLaunchKernelGGL(w2_cmax_kernel, dim3(cblocks), dim3(256), 0, s, C, ldc, m, n, w.ctl);
   }
-  if (prev && n % 4 == 0 && ldc % 4 == 0 && ((uintptr_t)C & 15) == 0)
+  const bool keep = w2_keep_flag();
+  const bool rows4 = n % 4 == 0 && ldc % 4 == 0 && ((uintptr_t)C & 15) == 0;
+  // R = 1 warm start: the violation and the first round's scans in one pass
+  bool fused_first = prev && rows4 && R == 1 && !keep && w2_fuse_first_flag();
+  if (fused_first)
+    hipLaunchKernelGGL(w2_scan_first_kernel, dim3((unsigned)((m + kViolRows - 1) / kViolRows)),
+                       dim3(256), 0, s, C, ldc, m, n, prev, w);
+  else if (prev && rows4)
     hipLaunchKernelGGL(w2_violation_rows_kernel, dim3((unsigned)((m + kViolRows - 1) / kViolRows)),
                        dim3(256), 0, s, C, ldc, m, n, n / m, prev, w);
   else if (prev)
     hipLaunchKernelGGL(w2_violation_kernel, dim3((unsigned)std::min<int64_t>(1024, (m + 3) / 4)),
                        dim3(256), 0, s, C, ldc, m, n, n / m, prev, w);
-  const bool keep = w2_keep_flag();
   if (prev && keep)
     hipLaunchKernelGGL(w2_load_prev_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n,
                        prev, w);
@@ -1554,6 +1689,14 @@ static int w2_assign(const float* C, int64_t ldc, int64_t m, int64_t n, void* ws
   int rc = check_launch("w2_start");
   if (rc) return rc;
   auto bid = [&]() {
+    if (fused_first) {  // round 1 from the scan pass's row results (R = 1: not cached)
+      hipLaunchKernelGGL(w2_bid_first_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s,
+                         m, w);
+      hipLaunchKernelGGL((w2_tail_kernel<2, false>), dim3(1 + kTailHelpers), dim3(kTailThreads),
+                         kTailLds, s, C, ldc, n, R, w);
+      fused_first = false;
+      return;
+    }
     if (cached) {
       hipLaunchKernelGGL(w2_bid_cached_kernel, gb, dim3(256), 0, s, C, ldc, m, n, R, w);
       hipLaunchKernelGGL((w2_tail_kernel<2, true>), dim3(1 + kTailHelpers), dim3(kTailThreads),

@@ -127,6 +127,7 @@ SIGNATURES = {
     "dsvgd_w2_set_theta": (_f64, [_f64]),
     "dsvgd_w2_tail_stats": (_i64, [_p]),
     "dsvgd_w2_set_tail_debug": (_int, [_int]),
+    "dsvgd_w2_set_fuse_first": (_int, [_int]),
     "dsvgd_w2_grad": (_int, [_p, _i64, _i64, _p, _i64, _i64, _i64, _p, _f, _p, _i64, _p]),
     "dsvgd_score_gaussian": (_int, [_p, _i64, _i64, _i64, _p, _p, _f, _p, _i64, _p]),
     "dsvgd_score_gmm": (_int, [_p, _i64, _i64, _i64, _f, _p, _i64, _p]),

@@ -718,6 +718,13 @@ int64_t dsvgd_w2_tail_stats(int64_t* out);
  * at once, so every tail stalls and hands its phase back to the bid rounds.
  * Returns the previous setting. */
 int dsvgd_w2_set_tail_debug(int nohelp);
+
+/* Process-wide switch (default 1): an R = 1 warm start (prev_assign given,
+ * keep off) takes the violation and its first round's row scans (best value,
+ * its column, second value) in one pass over C, and the first round bids from
+ * them; 0 runs the violation pass and a full-scan bid round (same bids, same
+ * plan; A/B).  Returns the previous setting. */
+int dsvgd_w2_set_fuse_first(int on);
 /* Progress of this host thread's last dsvgd_w2_assign: out[3k..3k+2] =
  * (rounds, epsilon phase, unassigned slots) at the k-th control readback
  * (every 16 rounds); copies min(count, cap) triples, returns count. */

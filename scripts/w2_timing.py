@@ -121,7 +121,12 @@ def main():
                     help="comma list of W2Term.COST settings to sweep on --shapes (auto, h2, exact)")
     ap.add_argument("--warm-phases", default=None,
                     help="comma list of warm phase counts to sweep on --shapes (a = adaptive)")
+    ap.add_argument("--fuse-first", type=int, default=1,
+                    help="R = 1 warm starts: violation + first-round scans in one pass "
+                         "(dsvgd_w2_set_fuse_first)")
     args = ap.parse_args()
+    from dsvgd import _native
+    _native.load().dsvgd_w2_set_fuse_first(args.fuse_first)
     global TRACE
     TRACE = args.trace
     if args.shapes:

@@ -777,6 +777,61 @@ def test_w2_warm_start_same_plan(m, n, d, step):
     record_parity(0.0, rounds_adaptive=plans[None][1], rounds_cold=plans[0][1])
 
 
+@pytest.mark.parametrize("m,d,step,cost,ties", [(1024, 32, 1e-2, "exact", False),
+                                                (512, 8, 0.3, "exact", False),
+                                                (400, 3, 1e-2, "exact", True),
+                                                (2048, 256, 1e-3, "h2", False),
+                                                (2048, 64, 1e-3, "h2", True)])
+def test_w2_fused_first_round_same_solve(m, d, step, cost, ties):
+    """An R = 1 warm start takes the violation and the first round's row
+    scans (best value, its column -- the lower on a tie --, second value) in
+    one pass over C and bids from them (dsvgd_w2_set_fuse_first): the same
+    plan slot for slot, the same round count and bit-identical prices and
+    gradient as the violation pass + full-scan bid round, and scipy's plan.
+    `ties`: previous particles duplicated in pairs, so rows see equal costs."""
+    lib = dsvgd()._native.load()
+    rs = np.random.RandomState(m + d + (7 if ties else 0))
+    X = rs.randn(m, d).astype(np.float32)
+    if ties:
+        P = np.repeat(rs.randn(m // 2, d).astype(np.float32), 2, axis=0)
+        X2 = X + np.float32(step) * rs.randn(m, d).astype(np.float32)
+        P2 = P.copy()
+    else:
+        P = X - 1e-3 * rs.randn(m, d).astype(np.float32)
+        X2 = (X + step * rs.randn(m, d)).astype(np.float32)
+        P2 = (P + step * rs.randn(m, d)).astype(np.float32)
+    W2 = dsvgd().w2.W2Term
+    out = {}
+    for fuse in (1, 0):
+        old_cost, W2.COST = W2.COST, cost
+        try:
+            w = W2(m, m, d, DEV, warm=True)
+        finally:
+            W2.COST = old_cost
+        assert w.cost == cost
+        prev = lib.dsvgd_w2_set_fuse_first(fuse)
+        try:
+            w.grad(gpu(X), gpu(P), 1.0)
+            G = w.grad(gpu(X2), gpu(P2), 1.0).cpu().numpy()
+        finally:
+            lib.dsvgd_w2_set_fuse_first(prev)
+        price = w.ws[256:256 + 8 * m].cpu().numpy().view(np.float64).copy()
+        out[fuse] = (w.plan(), w.rounds, price, G)
+    (p1, r1, q1, g1), (p0, r0, q0, g0) = out[1], out[0]
+    np.testing.assert_array_equal(p1, p0)
+    assert r1 == r0, (r1, r0)
+    np.testing.assert_array_equal(q1, q0)
+    np.testing.assert_array_equal(g1, g0)
+    C = O.w2_cost(X2, P2)
+    ref = O.w2_plan(C)
+    rows = np.arange(m)
+    if ties:  # several optimal plans: the cost must be optimal
+        assert C[rows, p1].sum() <= C[rows, ref].sum() * (1 + 1e-6)
+    else:
+        np.testing.assert_array_equal(p1, ref)
+    record_parity(0.0, rounds=r1)
+
+
 @pytest.mark.parametrize("m,n,d,pad", [(1, 1, 1, 0), (129, 127, 37, 3), (130, 300, 64, 0),
                                        (256, 1024, 256, 1), (77, 515, 5, 2)])
 def test_w2_cost_tiles(m, n, d, pad):
