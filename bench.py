@@ -263,10 +263,12 @@ def multi_gpu_report(sampler, eng, local_stages, world):
     pair-split layout engaged, its route probe's verdict and
     its first-step check against the row-block layout (DistSampler), and
     each rank's mean HIP-event time per step of every exchange stage (the
-    particle all-gather, the score all-reduce, the median's histogram
+    particle all-gather, the score all-reduce or, with gathered data, the
+    score all-gather, the median's histogram
     all-reduces, the pair split's partials post / join wait)."""
     mine = {"rank": dist.get_rank(),
             "pair_split": eng.plan is not None,
+            "gathered_data": bool(sampler._gdata),
             "route_probe_ok": sampler._routes_ok,
             "exchange_ms": {k: local_stages[k] for k in EXCHANGE_STAGES if k in local_stages}}
     ranks = [None] * world
@@ -275,6 +277,9 @@ def multi_gpu_report(sampler, eng, local_stages, world):
     return {"backend": dist.get_backend(),
             "world_size": dist.get_world_size(),
             "pair_split_engaged": [r["pair_split"] for r in ranks],
+            # all_scores as the own block's scores over every rank's data,
+            # all-gathered (DistSampler gather_data); False: the all-reduce
+            "scores_gathered_data": [r["gathered_data"] for r in ranks],
             "route_probe_ok": [r["route_probe_ok"] for r in ranks],
             "pair_split_first_step_check": sampler.pair_split_check,
             "pair_split_check_tol": sampler.PAIR_SPLIT_CHECK_TOL,

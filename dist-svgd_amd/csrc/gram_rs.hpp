@@ -75,6 +75,7 @@ struct W2Out {
   // (what w2_cmax_kernel finds in a pass over C; zeroed by the caller)
   uint32_t* stat = nullptr;
   int nt = 1;                 // C's stores non-temporal (dsvgd_w2_set_cost_nt)
+  int lines = 1;              // C's stores as whole 128-byte lines (dsvgd_w2_set_cost_lines)
 };
 
 // VAR (timing probes, dsvgd_gram_set_rs(5 / 6 / 7)): 4 = the E waves skip
@@ -543,20 +544,62 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if constexpr (OUT == 1) {
       // lane: row 32 bi + (lane & 15) (+16 for v[1]), columns 16 (2 bj + (SL & 1))
       // + 4 h + 8 ((lane >> 4) & 1) .. + 3 of the wave's 64
-      const int row = 32 * bi + (lane & 15);
-      const int col = 16 * (2 * bj + (SL & 1)) + 4 * h + 8 * ((lane >> 4) & 1);
-      const int o0 = (int)((row * wo.ldc + col) * 4);
-      // half-line pieces (the other 64 bytes of each row's line come one
-      // slice later): nt, or the default policy so the L2 merges the halves
-      // before they go out (dsvgd_w2_set_cost_nt, A/B)
-      if (wo.nt) {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[0]), rD, o0, 0, 2);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[1]), rD,
-                                               o0 + (int)(16 * wo.ldc * 4), 0, 2);
+      if (wo.lines && SL < 14) {
+        // full 128-byte lines (dsvgd_w2_set_cost_lines): a slice pair (even,
+        // odd) holds both 64-byte halves of the same 32 rows' lines.  Each
+        // slice parks its values in the hand-off chunks it has just read; the
+        // odd one then reads them back transposed -- lanes 2k and 2k + 1 (rows
+        // 2k', 2k' + 1) swap one chunk -- so that one store writes 8 even
+        // rows whole and the next 8 odd rows whole (was 16 half lines per
+        // store).  Slices 14 and 15 keep half lines: slice 15 runs after X,
+        // where the M waves overwrite the hand-off.
+        constexpr int ce = 4 * (2 * (SL >> 2) + ((SL >> 1) & 1));  // the even slice's chunks
+        constexpr int cs = ce + 2 * (SL & 1);                       // this slice's chunks
+        f32x4* const hb = reinterpret_cast<f32x4*>(hbuf);
+        hb[cs * 64 + lane] = v[0];
+        hb[(cs + 1) * 64 + lane] = v[1];
+        if constexpr ((SL & 1) == 1) {
+          asm volatile("" ::: "memory");
+          const bool ev = (lane & 1) == 0;
+          // the per-lane part of every line store's offset (row 2k' of the
+          // pair, columns 4 h + 8 ((lane >> 4) & 1) + 16 (lane & 1)); the
+          // slice's rows and columns go in the scalar offset
+          const int vl = (int)((((lane & 15) & ~1) * wo.ldc + 4 * h + 8 * ((lane >> 4) & 1) +
+                                16 * (lane & 1)) * 4);
+          const int xo = ev ? ce * 64 + lane : (ce + 2) * 64 + (lane ^ 1);
+          const int yo = ev ? ce * 64 + (lane ^ 1) : (ce + 2) * 64 + lane;
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            // X: row 2k' of the pair, Y: row 2k' + 1
+            const f32x4 X = hb[xo + 64 * q];
+            const f32x4 Y = hb[yo + 64 * q];
+            const int so = (int)((32 * bi + 16 * q) * wo.ldc * 4) + 128 * bj;
+            const int sy = so + (int)(wo.ldc * 4);
+            if (wo.nt) {
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, X), rD, vl, so, 2);
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, Y), rD, vl, sy, 2);
+            } else {
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, X), rD, vl, so, 0);
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, Y), rD, vl, sy, 0);
+            }
+          }
+        }
       } else {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[0]), rD, o0, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[1]), rD,
-                                               o0 + (int)(16 * wo.ldc * 4), 0, 0);
+        // half-line pieces (the other 64 bytes of each row's line come one
+        // slice later): nt, or the default policy so the L2 merges the halves
+        // before they go out (dsvgd_w2_set_cost_nt, A/B); the per-lane offset
+        // (row lane & 15, columns 4 h + 8 ((lane >> 4) & 1)) in a VGPR, the
+        // slice's rows and columns in the scalar offset
+        const int vh = (int)(((lane & 15) * wo.ldc + 4 * h + 8 * ((lane >> 4) & 1)) * 4);
+        const int s0 = (int)(32 * bi * wo.ldc * 4) + 64 * (2 * bj + (SL & 1));
+        const int s1 = s0 + (int)(16 * wo.ldc * 4);
+        if (wo.nt) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[0]), rD, vh, s0, 2);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[1]), rD, vh, s1, 2);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[0]), rD, vh, s0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[1]), rD, vh, s1, 0);
+        }
       }
     } else {
       const int vo = (32 * bi + (lane & 15)) * 64 + 16 * h + 32 * ((lane >> 4) & 1);

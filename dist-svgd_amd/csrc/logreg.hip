@@ -68,6 +68,19 @@ static int gxd_splits(int64_t n_pad, int64_t N_pad) {
 // G . Xd (0); dsvgd_logreg_set_fused
 static int g_logreg_fused = 1;
 
+// The fused score over data slices: a block is 128 particles, so a few
+// particles (a rank's own block in DistSampler's gathered-data all_scores:
+// m = 8192 at S = 8, 64 blocks) leave most CUs idle.  Split the data chunks
+// into Z slices (blocks (x, z)) until the launch covers the CUs, each slice
+// at least 16 chunks (512 data rows); logreg_finish adds the slices in order.
+// Z = 1 (the same launch and bits as before) whenever n fills the CUs alone.
+constexpr int kFusedMaxSplits = 8;
+static int fused_splits(int64_t n_pad, int64_t N_pad) {
+  int z = 1;
+  while (z < kFusedMaxSplits && (n_pad / 128) * z < 256 && (N_pad / 32) / (2 * z) >= 16) z *= 2;
+  return z;
+}
+
 static LogregWs logreg_ws(int64_t n, int64_t N, int64_t p) {
   LogregWs w;
   w.N = N;
@@ -85,7 +98,9 @@ static LogregWs logreg_ws(int64_t n, int64_t N, int64_t p) {
   w.off_xd = take((size_t)w.N_pad * w.ldb);
   w.off_t = take((size_t)w.N_pad);
   w.off_g = take((size_t)w.n_pad * w.N_pad);
-  w.off_gw = take((size_t)kGxdMaxSplits * w.n_pad * w.ldb);  // split-K slices of G . Xd
+  // split-K slices of G . Xd (two-GEMM path) or of the fused score
+  w.off_gw = take((size_t)std::max(kGxdMaxSplits, fused_splits(w.n_pad, w.N_pad)) * w.n_pad *
+                  w.ldb);
   // split images (bf16 x 3 = 6 B per element, counted in floats)
   w.off_wx = take((size_t)w.n_pad * w.pp * 3 / 2);
   w.off_xdx = take((size_t)w.N_pad * w.pp * 3 / 2);
@@ -335,7 +350,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const _Float16* __restrict__ Wx, int64_t n_img, const _Float16* __restrict__ Xdx,
     int64_t N_img, const _Float16* __restrict__ Xdp, int nchunks,
     const float* __restrict__ xinv, const float* __restrict__ rinv,
-    const float* __restrict__ colinv, float* __restrict__ GW, int64_t ldg, int64_t n) {
+    const float* __restrict__ colinv, float* __restrict__ GW, int64_t ldg, int64_t n,
+    int cpb) {
   using V8 = FmtH2::V8;
   __shared__ __attribute__((aligned(16))) char smem[2 * kFusedXdx + 2 * kFusedXdp];
   char* const abuf = smem;                       // row image ring (chunk c in abuf[c & 1])
@@ -467,12 +483,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   };
   constexpr std::true_type yes{};
   constexpr std::false_type no{};
-  dma_rows(0);
+  // data slice blockIdx.y: chunks [c0, c0 + cpb) (>= 2, checked by the host)
+  const int c0 = (int)blockIdx.y * cpb, c1 = min(nchunks, c0 + cpb);
+  GW += (int64_t)blockIdx.y * n * ldg;
+  dma_rows(c0);
   barrier_dma();
-  chunk(0, yes, no);                       // nchunks >= 2 (checked by the host)
-  for (int c = 1; c + 1 < nchunks; ++c) chunk(c, yes, yes);
-  chunk(nchunks - 1, no, yes);
-  gxd(xbuf + ((nchunks - 1) & 1) * kFusedXdp);
+  chunk(c0, yes, no);
+  for (int c = c0 + 1; c + 1 < c1; ++c) chunk(c, yes, yes);
+  chunk(c1 - 1, no, yes);
+  gxd(xbuf + ((c1 - 1) & 1) * kFusedXdp);
   // GW[i][c] = acc 2^-15 / s_c
 #pragma unroll
   for (int ni = 0; ni < kFusedCols / 32; ++ni) {
@@ -505,7 +524,7 @@ __global__ __launch_bounds__(256) void logreg_finish_kernel(const float* __restr
                                                             const float* __restrict__ GW,
                                                             int64_t ldg, float scale,
                                                             float* __restrict__ S, int64_t lds,
-                                                            int splits = 1) {
+                                                            int splits = 1, float pw = 1.f) {
   const int lane = threadIdx.x & 63;
   const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (j >= n) return;
@@ -517,9 +536,9 @@ __global__ __launch_bounds__(256) void logreg_finish_kernel(const float* __restr
   for (int64_t c = lane; c < p; c += 64) {
     float g = GW[j * ldg + c];
     for (int z = 1; z < splits; ++z) g += GW[(int64_t)z * n * ldg + j * ldg + c];  // slice order
-    S[j * lds + 1 + c] = scale * (g - a * x[1 + c]);
+    S[j * lds + 1 + c] = scale * (g - (pw * a) * x[1 + c]);  // pw = 1: the same fma as before
   }
-  if (lane == 0) S[j * lds] = scale * (-a + 0.5f * (float)p - 0.5f * a * w2);
+  if (lane == 0) S[j * lds] = scale * (pw * (-a + 0.5f * (float)p - 0.5f * a * w2));
 }
 
 
@@ -761,8 +780,10 @@ static int logreg_prepare(const float* Xd, int64_t ldxd, const float* t, int64_t
   return DSVGD_OK;
 }
 
+// pw: the prior's weight (1 = the reference's logp; DistSampler's gathered-data
+// all_scores passes S, the prior the reference's all-reduce sums S times)
 static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float scale, float* S,
-                       int64_t lds, const LogregPlan& P, hipStream_t s) {
+                       int64_t lds, const LogregPlan& P, hipStream_t s, float pw = 1.f) {
   const LogregWs& w = P.w;
   char* base = P.base;
   float* Xdp = (float*)(base + w.off_xd);
@@ -781,14 +802,17 @@ static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float 
     if ((rc = h2_rowimage(X + 1, ldx, n, p, w.n_pad, w.pp, rsw, riw, Wx, s))) return rc;
     if (g_logreg_fused && w.pp == kFusedKD * 16 && w.ldb == kFusedCols &&
         w.N_pad % kFusedChunk == 0 && w.N_pad >= 2 * kFusedChunk && w.n_pad % kFusedRows == 0) {
-      hipLaunchKernelGGL(logreg_fused_kernel, dim3((unsigned)(w.n_pad / kFusedRows)), dim3(256), 0,
-                         s, (const _Float16*)Wx, w.n_pad, (const _Float16*)(base + w.off_xdx),
-                         w.N_pad, (const _Float16*)(base + w.off_xdp),
-                         (int)(w.N_pad / kFusedChunk), (const float*)(sxd + 2 * w.ldb + 1),
-                         (const float*)riw, (const float*)(sxd + w.ldb), GW, w.ldb, n);
+      const int z = fused_splits(w.n_pad, w.N_pad);
+      const int nchunks = (int)(w.N_pad / kFusedChunk);
+      hipLaunchKernelGGL(logreg_fused_kernel, dim3((unsigned)(w.n_pad / kFusedRows), (unsigned)z),
+                         dim3(256), 0, s, (const _Float16*)Wx, w.n_pad,
+                         (const _Float16*)(base + w.off_xdx), w.N_pad,
+                         (const _Float16*)(base + w.off_xdp), nchunks,
+                         (const float*)(sxd + 2 * w.ldb + 1), (const float*)riw,
+                         (const float*)(sxd + w.ldb), GW, w.ldb, n, nchunks / z);
       if ((rc = check_launch("logreg_fused"))) return rc;
       hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,
-                         w.ldb, scale, S, lds, 1);
+                         w.ldb, scale, S, lds, z, pw);
       return check_launch("logreg_finish");
     }
     int blocks = 0;
@@ -836,7 +860,7 @@ static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float 
       return rc;
   }
   hipLaunchKernelGGL(logreg_finish_kernel, dim3((n + 3) / 4), dim3(256), 0, s, X, ldx, n, p, GW,
-                     w.ldb, scale, S, lds, splits);
+                     w.ldb, scale, S, lds, splits, pw);
   return check_launch("logreg_finish");
 }
 
@@ -896,6 +920,20 @@ int dsvgd_score_logreg_prepared(const float* X, int64_t ldx, int64_t n, int64_t 
                 "n <= 32 takes the one-block path: call dsvgd_score_logreg_engine");
   return logreg_step(X, ldx, n, d - 1, scale, S, lds,
                      logreg_plan(n, N, d - 1, workspace, engine), (hipStream_t)stream);
+}
+
+int dsvgd_score_logreg_prior(const float* X, int64_t ldx, int64_t n, int64_t d, int64_t N,
+                             float scale, float prior_weight, float* S, int64_t lds,
+                             void* workspace, int engine, void* stream) {
+  DSVGD_REQUIRE(X && S && workspace, "null pointer");
+  DSVGD_REQUIRE(n > 0 && d >= 2 && N > 0 && ldx >= d && lds >= d, "sizes");
+  DSVGD_REQUIRE(((uintptr_t)workspace & 255) == 0, "workspace must be 256-byte aligned");
+  DSVGD_REQUIRE(engine >= 0 && engine <= 2, "engine must be 0 (h2), 1 (x3) or 2 (f32)");
+  DSVGD_REQUIRE(!logreg_small(n, N, d - 1),
+                "n <= 32 takes the one-block path: call dsvgd_score_logreg_engine");
+  return logreg_step(X, ldx, n, d - 1, scale, S, lds,
+                     logreg_plan(n, N, d - 1, workspace, engine), (hipStream_t)stream,
+                     prior_weight);
 }
 
 size_t dsvgd_logreg_predict_workspace_bytes(int64_t n, int64_t Nt, int64_t p) {

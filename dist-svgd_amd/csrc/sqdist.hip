@@ -962,6 +962,13 @@ int dsvgd_w2_set_cost_nt(int on) {
   return prev;
 }
 
+static int g_w2_cost_lines = 1;
+int dsvgd_w2_set_cost_lines(int on) {
+  const int prev = g_w2_cost_lines;
+  g_w2_cost_lines = on ? 1 : 0;
+  return prev;
+}
+
 int dsvgd_w2_cost_h2(const float* X, int64_t ldx, int64_t m, const float* Y, int64_t ldy,
                      int64_t n, int64_t d, float* C, int64_t ldc, void* ws, float tau,
                      uint32_t* cstat, void* stream) {
@@ -1000,6 +1007,7 @@ int dsvgd_w2_cost_h2(const float* X, int64_t ldx, int64_t m, const float* Y, int
   wo.tau = tau;
   wo.stat = cstat;
   wo.nt = g_w2_cost_nt;
+  wo.lines = g_w2_cost_lines;
   wo.vec = (d % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)X & 15) == 0 &&
             ((uintptr_t)Y & 15) == 0)
                ? 1

@@ -121,6 +121,7 @@ SIGNATURES = {
     "dsvgd_w2_assign": (_int, [_p, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p]),
     "dsvgd_w2_assign_warm": (_int, [_p, _i64, _i64, _i64, _p, _i64, _p, _p, _p, _p]),
     "dsvgd_w2_set_cost_nt": (_int, [_int]),
+    "dsvgd_w2_set_cost_lines": (_int, [_int]),
     "dsvgd_w2_assign_stat": (_int, [_p, _i64, _i64, _i64, _p, _i64, _int, _p, _p, _p, _p, _p]),
     "dsvgd_w2_trace": (_i64, [_p, _i64]),
     "dsvgd_w2_set_keep": (_int, [_int]),
@@ -139,6 +140,8 @@ SIGNATURES = {
     "dsvgd_logreg_prepare": (_int, [_p, _i64, _p, _i64, _i64, _i64, _p, _int, _p]),
     "dsvgd_score_logreg_prepared": (_int, [_p, _i64, _i64, _i64, _i64, _f, _p, _i64, _p, _int,
                                            _p]),
+    "dsvgd_score_logreg_prior": (_int, [_p, _i64, _i64, _i64, _i64, _f, _f, _p, _i64, _p, _int,
+                                        _p]),
     "dsvgd_logreg_predict_workspace_bytes": (_c.c_size_t, [_i64, _i64, _i64]),
     "dsvgd_logreg_predict": (_int, [_p, _i64, _i64, _i64, _p, _i64, _i64, _p, _p, _p]),
     # the wide blocked Gauss-Seidel sweep (ABI 4)

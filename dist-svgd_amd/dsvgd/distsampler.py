@@ -41,6 +41,22 @@ checked once at the first step; a plain `logp` callable (which may close over
 rank-specific data, as logreg.py:68's `logp(rank, x)` can) keeps the
 redundant per-rank scoring.  `replicated=True` forces it, False disables it.
 
+Gathered data (all_scores with the built-in LogisticRegression target,
+`gather_data=None` = auto): the reference sums every rank's local-data score
+of ALL n particles with an all-reduce (distsampler.py:160-170), i.e. score_i
+= grad of the likelihood over all ranks' data + S x the prior (each rank's
+logp carries the prior once).  Here the ranks' data are all-gathered once (at
+the first step) and each rank scores only its OWN block over all of them with
+the prior weighted S (dsvgd_score_logreg_prior), and the score blocks are
+all-gathered -- north_star's "RCCL all-gather of particles and scores": the
+same scores to fp32 rounding, 1/S of the per-particle score work, an
+all-gather instead of an all-reduce (half the bytes), and the own block's
+scores need only the own rows, so they run while the particle all-gather is
+in flight (Jacobi: the gather on the side stream).  On when every rank's
+target is a LogisticRegression, m > LogisticRegression.SMALL_ROWS and the
+gathered data fit GATHER_DATA_MAX_BYTES; gather_data=False keeps the
+all-reduce, True requires the mode (ValueError where it cannot apply).
+
 Lagged modes (keyword `lagged`; the reference's notes.md:108-114, which
 describe them and time them at :134-135 but ship no code):
 
@@ -73,7 +89,7 @@ from . import _native as N
 from . import exchange
 from .engine import PhiEngine, SelectState, StepGraph, sequential_sweep, span
 from .kernels import resolve_kernel
-from .targets import BuiltinTarget, resolve_target
+from .targets import BuiltinTarget, LogisticRegression, resolve_target
 from .w2 import W2Term
 
 
@@ -82,12 +98,13 @@ class DistSampler(object):
     keep_phi = False  # Jacobi: also write phi of the owned rows to the engine's `phi` (tests)
     graphs = True  # S = 1, no W2, built-in target: replay each step as a HIP graph
     W2_WARN_ENTRIES = 1 << 24  # R > 1 plans this large warn at construction
+    GATHER_DATA_MAX_BYTES = 1 << 30  # gathered-data all_scores: all ranks' data, per rank
 
     def __init__(self, rank, num_shards, logp, kernel, particles,
                  N_local, N_global,
                  exchange_particles=True, exchange_scores=True, include_wasserstein=True,
                  *, order="sequential", device=None, group=None, replicated=None,
-                 lagged=None):
+                 lagged=None, gather_data=None):
         """Initializes a distributed SVGD sampler (distsampler.py:9-51)."""
         assert not (exchange_scores and not exchange_particles), \
             "must exchange particles to also exchange scores"
@@ -123,6 +140,14 @@ class DistSampler(object):
             self._replicated = None if (N_local == N_global and
                                         hasattr(self._target, "fingerprint")) else False
         self._rbf = resolve_kernel(kernel, self._d)
+        # gathered-data all_scores: decided at the first step (needs the group)
+        if gather_data not in (None, True, False):
+            raise ValueError("gather_data must be None, True or False")
+        self._gdata = False if (gather_data is False or not exchange_scores
+                                or num_shards == 1) else gather_data
+        if gather_data and not (exchange_scores and num_shards > 1):
+            raise ValueError("gather_data=True needs exchange_scores=True and num_shards > 1")
+        self._gtarget = None
 
         # NOTE: drops particles if not divisible by num_shards (as the reference)
         self._particles_per_shard = int(particles.shape[0] / self._num_shards)
@@ -280,8 +305,67 @@ class DistSampler(object):
         digest (one all_gather_object of a short string, first step only)."""
         import torch.distributed as dist
         fps = [None] * self._num_shards
-        dist.all_gather_object(fps, self._target.fingerprint(), group=self._group)
+        with torch.cuda.device(self._device):     # nccl stages the objects on the current device
+            dist.all_gather_object(fps, self._target.fingerprint(), group=self._group)
         self._replicated = all(f == fps[0] for f in fps)
+
+    def _resolve_gather_data(self):
+        """gather_data=None/True, first step: every rank's (x, t) gathered
+        once when every rank's target is a LogisticRegression (one
+        all_gather_object; all ranks decide alike from the same gathered
+        list); the gathered target scores the own block, prior weighted S."""
+        import torch.distributed as dist
+        m = self._particles_per_shard
+        tg = self._target
+        ok = (type(tg) is LogisticRegression and m > LogisticRegression.SMALL_ROWS
+              and not self._lagged and self._exchange_particles)
+        mine = (bool(ok), tg.x.cpu() if ok else None, tg.t.cpu() if ok else None,
+                tg.gemm if ok else None)
+        parts = [None] * self._num_shards
+        with torch.cuda.device(self._device):     # nccl stages the objects on the current device
+            dist.all_gather_object(parts, mine, group=self._group)
+        every = all(q[0] for q in parts) and len({q[3] for q in parts}) == 1
+        if every:
+            x = torch.cat([q[1] for q in parts])
+            t = torch.cat([q[2] for q in parts])
+            every = (x.numel() + t.numel()) * 4 <= self.GATHER_DATA_MAX_BYTES
+        if not every:
+            if self._gdata:
+                raise ValueError("gather_data=True: every rank needs a LogisticRegression "
+                                 "target (same engine), more than %d particles per rank and "
+                                 "at most GATHER_DATA_MAX_BYTES of data in all"
+                                 % LogisticRegression.SMALL_ROWS)
+            self._gdata = False
+            return
+        self._gtarget = LogisticRegression(x, t, gemm=parts[0][3])
+        self._gdata = True
+
+    def _gathered_scores(self, X, Si, jacobi):
+        """Gathered-data all_scores: the own block's scores over every
+        rank's data (prior x S) while the particle all-gather runs (Jacobi:
+        on the side stream), then the score blocks all-gathered (Jacobi: on
+        the side stream, joined before pack_scores)."""
+        S = self._num_shards
+        s, e = self._particle_start_idx, self._particle_end_idx
+        main = torch.cuda.current_stream(self._device)
+        side = main
+        if jacobi:
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=self._device)
+            side = self._side
+            side.wait_stream(main)             # the own rows' last update
+        with torch.cuda.stream(side):
+            with span(self.timer, "allgather_x"):
+                self._exchange_all_particles()
+        with span(self.timer, "scores"):   # own rows only: beside the gather
+            self._gtarget.score(X[s:e], Si[s:e], 1.0, prior_weight=float(S))
+        if side is not main:
+            main.wait_stream(side)             # the gathered particles
+            side.wait_stream(main)             # the own scores
+        with torch.cuda.stream(side):
+            with span(self.timer, "allgather_scores"):
+                self._gather_scores(Si)
+        return side
 
     # ------------------------------------------------------------ step --
     pair_split = True   # Jacobi with identical scores on every rank: the block-pair layout
@@ -411,15 +495,18 @@ class DistSampler(object):
         # stream: run beside the distance kernel they only time-slice the CUs
         # (measured: no gain), both being MFMA-bound.
         main = torch.cuda.current_stream(self._device)
-        with span(self.timer, "scores"):
-            if self._exchange_scores:
-                self._local_scores(X, Si)
-            elif self._replicated:                 # owned block only, gathered below
-                self._local_scores(X[s:e], Si[s:e], scale)
-            else:
-                self._local_scores(Xi, Si, scale)
         side = main
-        if (self._exchange_scores or self._replicated) and S > 1:
+        if self._gdata:
+            side = self._gathered_scores(X, Si, jacobi)
+        else:
+            with span(self.timer, "scores"):
+                if self._exchange_scores:
+                    self._local_scores(X, Si)
+                elif self._replicated:                 # owned block only, gathered below
+                    self._local_scores(X[s:e], Si[s:e], scale)
+                else:
+                    self._local_scores(Xi, Si, scale)
+        if (self._exchange_scores or self._replicated) and S > 1 and not self._gdata:
             if jacobi:
                 if self._side is None:
                     self._side = torch.cuda.Stream(device=self._device)
@@ -492,8 +579,12 @@ class DistSampler(object):
             self._check_group()
         if self._replicated is None:
             self._resolve_replicated()
+        if self._gdata is None or (self._gdata and self._gtarget is None):
+            self._resolve_gather_data()
         if S > 1:
-            if self._exchange_particles:
+            if self._gdata:
+                pass                       # in _compute, beside the own block's scores
+            elif self._exchange_particles:
                 with span(self.timer, "allgather_x"):
                     self._exchange_all_particles()
             elif self._lagged:

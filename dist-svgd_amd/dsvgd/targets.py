@@ -171,7 +171,10 @@ class LogisticRegression(BuiltinTarget):
             self._prepared.pop(k, None)
         return ws
 
-    def score(self, X, out, scale=1.0):
+    def score(self, X, out, scale=1.0, prior_weight=1.0):
+        """out = scale * grad log p(X); prior_weight != 1 weighs the prior
+        terms (DistSampler's gathered-data all_scores: the prior of S ranks'
+        logp, distsampler.py:160-170), on the prepared path only."""
         n, d = X.shape
         assert d == self.x.shape[1] + 1, "logreg target has d = 1 + p = %d" % (self.x.shape[1] + 1)
         xd, t = self._params(X.device)
@@ -188,6 +191,8 @@ class LogisticRegression(BuiltinTarget):
         eng = self.ENGINES[self.gemm]
         s = N.stream(X.device)
         if small:
+            if prior_weight != 1.0:
+                raise ValueError("prior_weight needs more than %d particles" % self.SMALL_ROWS)
             N.call("dsvgd_score_logreg_engine", N.ptr(X), N.ld(X), n, d, N.ptr(xd), N.ld(xd),
                    N.ptr(t), self.N, float(scale), N.ptr(out), N.ld(out), aligned, eng, s)
             return
@@ -200,6 +205,10 @@ class LogisticRegression(BuiltinTarget):
             if not torch.cuda.is_current_stream_capturing():
                 # later calls may come on other streams (the DistSampler side stream)
                 torch.cuda.current_stream(X.device).synchronize()
+        if prior_weight != 1.0:
+            N.call("dsvgd_score_logreg_prior", N.ptr(X), N.ld(X), n, d, self.N, float(scale),
+                   float(prior_weight), N.ptr(out), N.ld(out), aligned, eng, s)
+            return
         N.call("dsvgd_score_logreg_prepared", N.ptr(X), N.ld(X), n, d, self.N, float(scale),
                N.ptr(out), N.ld(out), aligned, eng, s)
 

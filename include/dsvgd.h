@@ -665,6 +665,12 @@ int dsvgd_w2_cost(const float* X, int64_t ldx, int64_t m, const float* Y, int64_
 /* A/B switch of dsvgd_w2_cost_h2's C stores (returns the previous): 1
  * (default) non-temporal, 0 the default cache policy. */
 int dsvgd_w2_set_cost_nt(int on);
+
+/* Process-wide A/B switch (default 1): dsvgd_w2_cost_h2 writes C in whole
+ * 128-byte row lines (two slices' values traded between lane pairs); 0 writes
+ * each slice's half lines as it goes.  Same C bits.  Returns the previous
+ * setting. */
+int dsvgd_w2_set_cost_lines(int on);
 size_t dsvgd_w2_cost_h2_workspace_bytes(int64_t m, int64_t n, int64_t d);
 int dsvgd_w2_cost_h2(const float* X, int64_t ldx, int64_t m, const float* Y, int64_t ldy,
                      int64_t n, int64_t d, float* C, int64_t ldc, void* ws, float tau,
@@ -774,6 +780,17 @@ int dsvgd_logreg_prepare(const float* Xd, int64_t ldxd, const float* t, int64_t 
 int dsvgd_score_logreg_prepared(const float* X, int64_t ldx, int64_t n, int64_t d, int64_t N,
                                 float scale, float* S, int64_t lds, void* workspace, int engine,
                                 void* stream);
+
+/* dsvgd_score_logreg_prepared with the prior weighted by prior_weight:
+ * S = scale * (sum over the data - prior_weight * grad of the prior terms).
+ * DistSampler's gathered-data all_scores mode scores its own particles over
+ * every rank's data with prior_weight = S, which is what the reference's
+ * all-reduce of S per-rank logp gradients sums to (distsampler.py:160-170:
+ * each rank's logp carries the prior once).  prior_weight = 1 gives exactly
+ * dsvgd_score_logreg_prepared's bits.  Replaces: the same call sites. */
+int dsvgd_score_logreg_prior(const float* X, int64_t ldx, int64_t n, int64_t d, int64_t N,
+                             float scale, float prior_weight, float* S, int64_t lds,
+                             void* workspace, int engine, void* stream);
 
 /* Posterior-predictive probability of the logistic-regression test set:
  * prob[q] = (1/n) sum_j sigma(xt_q . w_j), w_j = X[j][1:d] (no bias; alpha

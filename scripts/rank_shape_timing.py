@@ -41,6 +41,11 @@ def main():
     ap.add_argument("--layout", default="both", choices=["rows", "pairs", "both"],
                     help="rows: the row-block layout; pairs: the pair-split layout (DESIGN.md 6; "
                          "the partials' exchange left out, their buffers zero)")
+    ap.add_argument("--scores", default="gathered",
+                    help="comma list: gathered (DistSampler gather_data: the own m particles "
+                         "over all Ng data rows, prior x S; the score blocks' all-gather left "
+                         "out) | allreduce (all n particles over the rank's Ng / S rows; the "
+                         "all-reduce left out)")
     args = ap.parse_args()
     import dsvgd
     if args.lib:
@@ -69,8 +74,8 @@ def main():
                             for ov in overrides:
                                 runs.append((S, lay, bool(int(side)), bool(int(rest)), int(fz),
                                              ov))
-    for S, lay, side, rest, fz, *ovl in runs:
-        ov = ovl[0] if ovl else {}
+    runs = [rn + (sm,) for rn in runs for sm in args.scores.split(",")]
+    for S, lay, side, rest, fz, ov, smode in runs:
         for k in ("W_SPLITS", "H_SPLITS", "REST_SPLITS"):
             setattr(dsvgd.PhiEngine, k, ov.get(k) or None)
         from dsvgd.pairsplit import PairSplitPlan
@@ -80,7 +85,9 @@ def main():
         dsvgd.PhiEngine.FWD_ZSPLIT = fz or None
         m, r = n // S, S // 2          # a middle rank (a high one of the pair split)
         per = Ng // S
-        tgt = dsvgd.targets.LogisticRegression(x[r * per:(r + 1) * per], t[r * per:(r + 1) * per])
+        gathered = smode == "gathered" and S > 1
+        tgt = (dsvgd.targets.LogisticRegression(x, t) if gathered else
+               dsvgd.targets.LogisticRegression(x[r * per:(r + 1) * per], t[r * per:(r + 1) * per]))
         eng = dsvgd.PhiEngine(n, d, m=m, row0=r * m, device="cuda:0",
                               pair_split=(r, S) if lay == "pairs" else None)
         if eng.plan is not None:
@@ -100,6 +107,8 @@ def main():
                 sample[b:].copy_(full[b:])
             eng.sample_share = (r, S, gather)
         Sx = torch.empty_like(X)
+        if gathered:   # the other ranks' score blocks (the all-gather's) stand in
+            tgt.score(X, Sx, 1.0, prior_weight=float(S))
         Xo = X[r * m:(r + 1) * m].clone()
         timer = StageTimer()
 
@@ -107,7 +116,11 @@ def main():
             with torch.cuda.device(0):
                 from dsvgd.engine import span
                 with span(eng.timer, "scores"):
-                    tgt.score(X, Sx)          # all_scores: every particle on the local data
+                    if gathered:              # the own block over every rank's data
+                        tgt.score(X[r * m:(r + 1) * m], Sx[r * m:(r + 1) * m], 1.0,
+                                  prior_weight=float(S))
+                    else:                     # all_scores: every particle on the local data
+                        tgt.score(X, Sx)
                 eng.pack(X, Sx)
                 eng.distances(median=True)
                 # the other S-1 ranks' counts approximated by this rank's (x S):
@@ -148,6 +161,7 @@ def main():
                           "h_splits": getattr(eng, "h_splits", None),
                           "t_splits": getattr(eng, "t_splits", None),
                           "row0": r * m, "N_local": per,
+                          "scores": "gathered" if gathered else "allreduce",
                           "ms_per_step_no_comm": e0.elapsed_time(e1) / args.steps,
                           "sym_layout": bool(eng.sym), "full_square": bool(PairSplitPlan.full_square(S)),
                           "stages_ms": st}), flush=True)

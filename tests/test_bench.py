@@ -90,7 +90,10 @@ def test_bench_self_launch_two_ranks_gloo():
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["process_group"]["world_size_seen"] == 2
-    assert "allgather_x" in out["stages_ms"] and "allreduce_scores" in out["stages_ms"]
+    # all_scores with the logreg target: the own block's scores over the
+    # gathered data, the score blocks all-gathered (DistSampler gather_data)
+    assert "allgather_x" in out["stages_ms"] and "allgather_scores" in out["stages_ms"]
+    assert out["multi_gpu"]["scores_gathered_data"] == [True, True]
     assert "hist_allreduce" in out["stages_ms"]
 
 
@@ -118,9 +121,10 @@ def test_bench_two_ranks_gloo():
     assert mg["world_size"] == 2 and mg["backend"] == "gloo"
     assert mg["pair_split_engaged"] == [True, True] and mg["route_probe_ok"] == [True, True]
     assert mg["pair_split_first_step_check"] <= mg["pair_split_check_tol"] == 1e-5
+    assert mg["scores_gathered_data"] == [True, True]
     assert len(mg["exchange_ms_per_rank"]) == 2
     for ex in mg["exchange_ms_per_rank"]:
-        for k in ("allgather_x", "allreduce_scores", "hist_allreduce", "partials_wait"):
+        for k in ("allgather_x", "allgather_scores", "hist_allreduce", "partials_wait"):
             assert k in ex and ex[k] >= 0.0
     assert out["roofline"]["traffic"] is None   # N=1 PMC summary is not quoted at N>1
     assert "cpu_baseline" not in out

@@ -945,6 +945,26 @@ def test_w2_cost_h2_matches_exact(m, n, d, kind):
         np.testing.assert_array_equal(Ch[idx, idx], Ce[idx, idx])
 
 
+@pytest.mark.parametrize("m,n,d", [(1024, 1024, 256), (300, 900, 37), (2048, 4096, 64)])
+def test_w2_cost_h2_line_stores_identical(m, n, d):
+    """dsvgd_w2_set_cost_lines: C written as whole 128-byte row lines (two
+    slices' values traded between lane pairs) and as half lines -- the same
+    bits everywhere, ragged tiles included."""
+    lib = dsvgd()._native.load()
+    rs = np.random.RandomState(m + n + d + 5)
+    X = rs.randn(m, d).astype(np.float32)
+    P = rs.randn(n, d).astype(np.float32)
+    P[:min(m, n)] = X[:min(m, n)] - 1e-3 * rs.randn(min(m, n), d).astype(np.float32)
+    out = {}
+    for lines in (1, 0):
+        prev = lib.dsvgd_w2_set_cost_lines(lines)
+        try:
+            out[lines] = _w2_cost(X, P, "h2")
+        finally:
+            lib.dsvgd_w2_set_cost_lines(prev)
+    np.testing.assert_array_equal(out[1], out[0])
+
+
 @pytest.mark.parametrize("name", W2_GOLDEN)
 def test_w2_h2_cost_golden_plans(golden, name):
     """The golden LPs (reference linprog plans, near-tie sets included) on the

@@ -519,3 +519,35 @@ def test_logreg_scores_fused(n, N, labels):
         assert e_f < 1e-5 and e_f <= 2.0 * e_2 + 1e-7, (e_f, e_2)
     d = float(np.abs(out[1] - out[0]).max() / np.abs(out[0]).max())
     assert d < 5e-6, d
+
+
+@pytest.mark.parametrize("n,N,S,fused", [(512, 16384, 8, 1), (1000, 3000, 4, 1), (300, 700, 2, 0)])
+def test_logreg_scores_prior_weight(n, N, S, fused):
+    """dsvgd_score_logreg_prior: the prior terms weighted by S -- what the
+    reference's all_scores all-reduce of S per-rank logp gradients sums to
+    (distsampler.py:160-170) -- against fp64 (data term + S x prior), and
+    weight 1 bit-identical to dsvgd_score_logreg_prepared."""
+    from dsvgd import _native as N_
+    p = 255
+    rs = np.random.RandomState(n + N + S)
+    X = (rs.randn(n, p + 1) * 0.4).astype(np.float32)
+    xd = (rs.randn(N, p) / np.sqrt(p)).astype(np.float32)
+    t = np.where(rs.randn(N) > 0, 1.0, -1.0).astype(np.float32)
+    lib = N_.load()
+    prev = lib.dsvgd_logreg_set_fused(fused)
+    try:
+        tg = dsvgd().targets.LogisticRegression(xd, t, gemm="h2")
+        o1, ow, op = (torch.zeros(n, p + 1, device=DEV) for _ in range(3))
+        tg.score(gpu(X), o1)
+        tg.score(gpu(X), op, prior_weight=1.0 + 0.0 * S)      # the plain path
+        tg.score(gpu(X), ow, prior_weight=float(S))
+        torch.cuda.synchronize()
+    finally:
+        lib.dsvgd_logreg_set_fused(prev)
+    np.testing.assert_array_equal(o1.cpu().numpy(), op.cpu().numpy())
+    ref = O.score_logreg(X, xd, t)
+    prior = O.score_logreg(X, xd[:0], t[:0])              # no data: the prior terms alone
+    ref = ref + (S - 1) * prior
+    err = float(np.abs(ow.cpu().numpy() - ref).max() / np.abs(ref).max())
+    record_parity(err)
+    assert err < 1e-5, err

@@ -69,6 +69,7 @@ def test_meta_calls_without_gpu():
     assert lib.dsvgd_w2_tail_stats(stats) == 6
     assert lib.dsvgd_w2_set_tail_debug(1) == 0 and lib.dsvgd_w2_set_tail_debug(0) == 1
     assert lib.dsvgd_w2_set_fuse_first(0) == 1 and lib.dsvgd_w2_set_fuse_first(1) == 0
+    assert lib.dsvgd_w2_set_cost_lines(0) == 1 and lib.dsvgd_w2_set_cost_lines(1) == 0
     # argument validation returns an error code (no GPU work is enqueued)
     rc = lib.dsvgd_sqdist(None, 0, None, 0, 0, 0, 32, None, 128, 0, None, None, None)
     assert rc == -1 and b"null" in lib.dsvgd_last_error()
