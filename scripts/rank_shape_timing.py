@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--shards", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--lib", default=None, help="an A/B build of the library (make ab)")
-    ap.add_argument("--rest", default="1",
+    ap.add_argument("--rest", default="0",
                     help="pairs: comma list of PhiEngine.REST_BESIDE settings (1, 0)")
     ap.add_argument("--side", default="0",
                     help="pairs: comma list of PhiEngine.WINDOW_SIDE_STREAM settings (0, 1)")
