@@ -74,6 +74,7 @@ static int g_logreg_fused = 1;
 // into Z slices (blocks (x, z)) until the launch covers the CUs, each slice
 // at least 16 chunks (512 data rows); logreg_finish adds the slices in order.
 // Z = 1 (the same launch and bits as before) whenever n fills the CUs alone.
+// The slices are equal: N_pad is a multiple of 256 = 8 chunks and Z | 8.
 constexpr int kFusedMaxSplits = 8;
 static int fused_splits(int64_t n_pad, int64_t N_pad) {
   int z = 1;
