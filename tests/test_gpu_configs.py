@@ -404,6 +404,66 @@ def test_sequential_wide_full_sweep_d256(group):
         E.GSW_GROUP = prev
 
 
+@pytest.mark.parametrize("cfg,pipeline,h", [("D", True, 0.46), ("D", False, 0.46), ("D", True, 5.0),
+                                             ("E", True, 1.85)])
+def test_sequential_refreshed_scores_full_size(cfg, pipeline, h):
+    """the reference's default Gauss-Seidel order at the
+    full sizes of configs D and E -- D: n = 65536, d = 256, the logistic
+    regression on N = 16384 data rows; E: n = 65536, d = 1024 on N = 8192
+    (bench.py's synthetic data) -- the score refreshed in the walk after every
+    move (dsvgd/sampler.py:64-68), through the wide blocked sweep
+    (group-pipelined, engine.GSW_PIPELINE, and serial at D): a row range cut
+    off the block grid (several groups) against the fp64 sequential
+    restatement (O.sequential_sweep with the fp64 score), every moved row's
+    phi, position and refreshed score compared, the other rows untouched.
+    h = 0.46 / 1.85 is the median heuristic's value for these particles (K ~
+    1/n at the median distance); h = 5 makes every pair interact strongly (K
+    ~ e^-1).  The starting scores are the engine's fp32 scores of the
+    starting particles, handed to both sides as the same input (the score
+    kernel has its own full-size tests: test_config_D_bench_step,
+    test_config_E_logreg_scores)."""
+    import dsvgd.engine as E
+    from bench import synthetic_data
+    from dsvgd import _native as N
+    from dsvgd.engine import SelectState, sequential_sweep
+    n, d, Ng, count = {"D": (65536, 256, 16384, 1100), "E": (65536, 1024, 8192, 300)}[cfg]
+    eps = 1e-3
+    x, t = synthetic_data(Ng, d - 1)
+    X0 = (0.1 * np.random.RandomState(3).randn(n, d)).astype(np.float32)
+    tgt = dsvgd().targets.LogisticRegression(x, t)
+    Xg = gpu(X0)
+    Sg = torch.empty_like(Xg)
+    tgt.score(Xg, Sg)
+    torch.cuda.synchronize()
+    S0 = Sg.cpu().numpy()
+    lo = 32741
+    hi = lo + count
+    st = SelectState(DEV)
+    N.call("dsvgd_set_bandwidth", st.ptr, h, N.stream(DEV))
+    phi = torch.zeros(hi - lo, d, device=DEV)
+    prev = E.GSW_PIPELINE
+    E.GSW_PIPELINE = pipeline
+    try:
+        sequential_sweep(Xg, Sg, range(lo, hi), st, eps, target=tgt, phi_out=phi)
+        torch.cuda.synchronize()
+    finally:
+        E.GSW_PIPELINE = prev
+    xd64, t64 = x.astype(np.float64), t.astype(np.float64)
+    Xr, Sr, pr = O.sequential_sweep(X0, S0, h, range(lo, hi), eps,
+                                    score_fn=lambda R: O.score_logreg(R, xd64, t64))
+    got = Xg.cpu().numpy().astype(np.float64)
+    gs = Sg.cpu().numpy().astype(np.float64)
+    assert np.array_equal(got[:lo], X0[:lo]) and np.array_equal(got[hi:], X0[hi:])
+    assert np.array_equal(gs[:lo], S0[:lo]) and np.array_equal(gs[hi:], S0[hi:])
+    e_phi = rel_err(phi.cpu().numpy(), pr)
+    assert e_phi < PHI_TOL, e_phi
+    e_x = float(np.abs(got[lo:hi] - Xr[lo:hi]).max())
+    record_parity(e_phi, x_abs=e_x)
+    assert e_x < 1e-4, e_x
+    e_s = float(np.abs(gs[lo:hi] - Sr[lo:hi]).max() / np.abs(Sr[lo:hi]).max())
+    assert e_s < 1e-5, e_s
+
+
 @pytest.mark.parametrize("spin_ns", [0, 20000])
 def test_pipelined_sweep_forced_overlap(spin_ns):
     """the pipelined wide sweep (engine.GSW_PIPELINE:
