@@ -1,8 +1,11 @@
 """bench.py -- SVGD particle-updates/s at n=65536, d=256 (BASELINE.json metric).
 
 Workload (BASELINE.json configs[3]): dist-logreg via
-DistSampler, exchange=all_scores (all-gather of particles + all-reduce of the
-shard-local scores of all n particles), median-heuristic bandwidth, Jacobi
+DistSampler, exchange=all_scores (all-gather of particles + the scores of all
+n particles over all N data rows: at N > 1 by default each rank scores its own
+block over the once-gathered data and the score blocks are all-gathered --
+DistSampler gather_data, the same sums as the reference's all-reduce of the
+shard-local scores), median-heuristic bandwidth, Jacobi
 order, n = 65536 particles of d = 256 (p = 255 weights), N_global = 16384
 synthetic data rows sharded N/S, the n particles sharded n/S per GPU.
 One step = exchange + scores + median (exact radix select over n^2 distances)
