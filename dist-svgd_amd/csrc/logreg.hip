@@ -805,6 +805,8 @@ static int logreg_step(const float* X, int64_t ldx, int64_t n, int64_t p, float 
         w.N_pad % kFusedChunk == 0 && w.N_pad >= 2 * kFusedChunk && w.n_pad % kFusedRows == 0) {
       const int z = fused_splits(w.n_pad, w.N_pad);
       const int nchunks = (int)(w.N_pad / kFusedChunk);
+      // every slice takes nchunks / z >= 2 whole chunks (none dropped)
+      DSVGD_REQUIRE(nchunks % z == 0 && nchunks / z >= 2, "fused score: unequal data slices");
       hipLaunchKernelGGL(logreg_fused_kernel, dim3((unsigned)(w.n_pad / kFusedRows), (unsigned)z),
                          dim3(256), 0, s, (const _Float16*)Wx, w.n_pad,
                          (const _Float16*)(base + w.off_xdx), w.N_pad,
