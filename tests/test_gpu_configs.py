@@ -413,7 +413,7 @@ def test_sequential_refreshed_scores_full_size(cfg, pipeline, h):
     (bench.py's synthetic data) -- the score refreshed in the walk after every
     move (dsvgd/sampler.py:64-68), through the wide blocked sweep
     (group-pipelined, engine.GSW_PIPELINE, and serial at D): a row range cut
-    off the block grid (several groups) against the fp64 sequential
+    off the block grid (700 rows at D, several groups) against the fp64 sequential
     restatement (O.sequential_sweep with the fp64 score), every moved row's
     phi, position and refreshed score compared, the other rows untouched.
     h = 0.46 / 1.85 is the median heuristic's value for these particles (K ~
@@ -426,7 +426,7 @@ def test_sequential_refreshed_scores_full_size(cfg, pipeline, h):
     from bench import synthetic_data
     from dsvgd import _native as N
     from dsvgd.engine import SelectState, sequential_sweep
-    n, d, Ng, count = {"D": (65536, 256, 16384, 1100), "E": (65536, 1024, 8192, 300)}[cfg]
+    n, d, Ng, count = {"D": (65536, 256, 16384, 700), "E": (65536, 1024, 8192, 300)}[cfg]
     eps = 1e-3
     x, t = synthetic_data(Ng, d - 1)
     X0 = (0.1 * np.random.RandomState(3).randn(n, d)).astype(np.float32)
