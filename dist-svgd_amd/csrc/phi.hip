@@ -407,6 +407,50 @@ __global__ __launch_bounds__(256) void phi_finish_kernel(
   if (X) X[i * ldx + c] += step * p;
 }
 
+// phi_finish_kernel with four consecutive columns per thread (16-byte loads
+// and stores; every stride and base 16-byte aligned, d % 4 == 0): the same
+// per-element arithmetic in the same order, so the same bits.
+__global__ __launch_bounds__(256) void phi_finish4_kernel(
+    const float* __restrict__ KY, int64_t ldk, const float* __restrict__ rowsum, int splits,
+    const float* __restrict__ Y, int64_t ldy, int64_t row0, int64_t m, int64_t d4, int64_t dp,
+    const dsvgd_select_state* __restrict__ st, float inv_n, float step,
+    const float* __restrict__ extra, int64_t lde, float* __restrict__ phi, int64_t ldphi,
+    float* __restrict__ X, int64_t ldx) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= m * d4) return;
+  const int64_t i = t / d4, c = (t % d4) * 4;
+  const float two_inv_h = 2.f * st->inv_h;
+  const int64_t mp = roundup128(m);
+  f32x4 kx = {0.f, 0.f, 0.f, 0.f}, ks = {0.f, 0.f, 0.f, 0.f};
+  float r = 0.f;
+  for (int z = 0; z < splits; ++z) {
+    const float* ky = KY + (int64_t)z * m * ldk + i * ldk;
+    kx += *reinterpret_cast<const f32x4*>(ky + c);
+    ks += *reinterpret_cast<const f32x4*>(ky + dp + c);
+    r += rowsum[(int64_t)z * mp + i];
+  }
+  const float* yi = Y + (row0 + i) * ldy;
+  const f32x4 yx = *reinterpret_cast<const f32x4*>(yi + c);
+  const f32x4 ys = *reinterpret_cast<const f32x4*>(yi + dp + c);
+  const f32x4 ex = extra ? *reinterpret_cast<const f32x4*>(extra + i * lde + c)
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 p;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    // + the self term k_ii (s_i + 2/h (x_i - x_i)) = s_i, excluded from phi_mm
+    float q = inv_n * ((ys[e] + ks[e]) + two_inv_h * (r * yx[e] - kx[e]));
+    if (extra) q += ex[e];
+    p[e] = q;
+  }
+  if (phi) *reinterpret_cast<f32x4*>(phi + i * ldphi + c) = p;
+  if (X) {
+    f32x4 x = *reinterpret_cast<const f32x4*>(X + i * ldx + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] += step * p[e];
+    *reinterpret_cast<f32x4*>(X + i * ldx + c) = x;
+  }
+}
+
 // ---- split-K partials summed (dsvgd_phi_h2_transposed, the wide sweep) ---
 // out[i][c] = sum_z P[z][i][c], out_rs[i] = sum_z rs[z][i] in a fixed order:
 // a workgroup takes 256 / G float4 positions; its G thread groups (G = the
@@ -1204,6 +1248,15 @@ int dsvgd_phi_finish_parts(const float* KY, int64_t ldk, const float* rowsum, in
   return check_launch("phi_finish_parts");
 }
 
+// A/B switch (default 1): dsvgd_phi_finish on four columns per thread where
+// the layout allows (phi_finish4_kernel, the same bits)
+static int g_phi_finish_vec = 1;
+int dsvgd_phi_set_finish_vec(int on) {
+  const int prev = g_phi_finish_vec;
+  g_phi_finish_vec = on ? 1 : 0;
+  return prev;
+}
+
 int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t splits,
                      const float* Y, int64_t ldy, int64_t row0, int64_t m, int64_t d, int64_t dp,
                      const dsvgd_select_state* st, float inv_n, float step, const float* extra,
@@ -1215,6 +1268,16 @@ int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t 
   DSVGD_REQUIRE(m > 0 && d > 0 && dp >= d && ldk >= 2 * dp && ldy >= 2 * dp, "sizes");
   DSVGD_REQUIRE(!phi || ldphi >= d, "ldphi");
   DSVGD_REQUIRE(!X || ldx >= d, "ldx");
+  auto a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  if (g_phi_finish_vec && d % 4 == 0 && dp % 4 == 0 && ldk % 4 == 0 && ldy % 4 == 0 &&
+      a16(KY) && a16(Y) && (!extra || (lde % 4 == 0 && a16(extra))) &&
+      (!phi || (ldphi % 4 == 0 && a16(phi))) && (!X || (ldx % 4 == 0 && a16(X)))) {
+    const int64_t d4 = d / 4;
+    hipLaunchKernelGGL(phi_finish4_kernel, dim3((unsigned)((m * d4 + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, KY, ldk, rowsum, (int)splits, Y, ldy, row0, m, d4,
+                       dp, st, inv_n, step, extra, lde, phi, ldphi, X, ldx);
+    return check_launch("phi_finish4");
+  }
   hipLaunchKernelGGL(phi_finish_kernel, dim3((m * d + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, KY, ldk, rowsum, (int)splits, Y, ldy, row0, m, d, dp,
                      st, inv_n, step, extra, lde, phi, ldphi, X, ldx);

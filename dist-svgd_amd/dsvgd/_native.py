@@ -67,6 +67,7 @@ SIGNATURES = {
     "dsvgd_set_bandwidth": (_int, [_p, _f, _p]),
     "dsvgd_phi_splits": (_i64, [_i64, _i64, _i64]),
     "dsvgd_phi_set_symrow": (_int, [_int]),
+    "dsvgd_phi_set_finish_vec": (_int, [_int]),
     "dsvgd_gram_set_rs": (_int, [_int]),
     "dsvgd_gram_set_group": (_int, [_int]),
     "dsvgd_set_cu_reserve": (_int, [_int]),

@@ -582,6 +582,11 @@ int dsvgd_phi_finish(const float* KY, int64_t ldk, const float* rowsum, int64_t 
                      const dsvgd_select_state* st, float inv_n, float step, const float* extra,
                      int64_t lde, float* phi, int64_t ldphi, float* X, int64_t ldx,
                      void* stream);
+/* Process-wide A/B switch (default 1): dsvgd_phi_finish takes four columns
+ * per thread (16-byte accesses) when d, dp and every leading dimension are
+ * multiples of 4 and every base is 16-byte aligned; 0 keeps one element per
+ * thread.  Same bits.  Returns the previous setting. */
+int dsvgd_phi_set_finish_vec(int on);
 
 /* d <= 64 (used for d <= 2): phi (and the optional X update) straight from the pairwise form
  * phi_i = inv_n sum_j k_ij (s_j + (2/h)(x_i - x_j)) on the VALU -- the

@@ -1243,3 +1243,45 @@ def test_predictive_prob_and_test_accuracy(n, d, Nt):
     agree = ((ref > 0.5) == (tt > 0))
     lo, hi = agree[sure].sum() / Nt, (agree[sure].sum() + (~sure).sum()) / Nt
     assert lo - 1e-12 <= acc <= hi + 1e-12
+
+
+@pytest.mark.parametrize("m,d,dp,splits,extra,off", [(1000, 256, 256, 2, False, 0),
+                                                       (513, 64, 64, 3, True, 0),
+                                                       (300, 36, 64, 1, True, 0),
+                                                       (200, 256, 256, 2, False, 1)])
+def test_phi_finish_vec_same_bits(m, d, dp, splits, extra, off):
+    """dsvgd_phi_set_finish_vec: four columns per thread (16-byte accesses)
+    gives the same phi and the same updated X bits as one element per thread
+    (the split-K partials summed in slice order, the self term, extra rows);
+    off = 1 misaligns X so the call falls back to the scalar kernel."""
+    from dsvgd import _native as N
+    from dsvgd.engine import SelectState
+    dsvgd()
+    lib = N.load()
+    g = torch.Generator(device="cpu").manual_seed(m + d)
+    ldk, ldy, row0 = 2 * dp, 2 * dp, 7
+    mp = (m + 127) // 128 * 128
+    KY = torch.randn(splits * m * ldk, generator=g).to(DEV)
+    rs = torch.rand(splits * mp, generator=g).to(DEV)
+    Y = torch.randn((row0 + m) * ldy, generator=g).to(DEV)
+    ex = torch.randn(m * d, generator=g).to(DEV) if extra else None
+    X0 = torch.randn(m * d + 4, generator=g).to(DEV)
+    st = SelectState(DEV)
+    N.call("dsvgd_set_bandwidth", st.ptr, 3.7, N.stream(DEV))
+    out = {}
+    prev = lib.dsvgd_phi_set_finish_vec(1)
+    try:
+        for vec in (1, 0):
+            lib.dsvgd_phi_set_finish_vec(vec)
+            phi = torch.empty(m * d, device=DEV)
+            X = X0.clone()
+            Xv = X[off:off + m * d]
+            N.call("dsvgd_phi_finish", N.ptr(KY), ldk, N.ptr(rs), splits, N.ptr(Y), ldy, row0, m,
+                   d, dp, st.ptr, 1.0 / 4096, 0.01, N.ptr(ex) if extra else None, d, N.ptr(phi), d,
+                   N.ptr(Xv), d, N.stream(DEV))
+            torch.cuda.synchronize()
+            out[vec] = (phi.cpu(), X.cpu())
+    finally:
+        lib.dsvgd_phi_set_finish_vec(prev)
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    assert bool(torch.isfinite(out[1][0]).all())
