@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/r16h
+OUT=gpurun_out/${TAG:-r16h}
 mkdir -p $OUT
 timeout -k 10 400 python bench.py --steps 10 --warmup 3 > $OUT/bench.log 2>&1 || { tail -20 $OUT/bench.log; exit 1; }
 grep "^{" $OUT/bench.log | cut -c1-200
