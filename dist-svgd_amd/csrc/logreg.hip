@@ -530,6 +530,32 @@ __global__ __launch_bounds__(256) void logreg_finish_kernel(const float* __restr
   const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (j >= n) return;
   const float* x = X + j * ldx;
+  if (p <= 256) {
+    // every load of the row issued before the norm's reduction (a lane's
+    // columns lane + 64 u in registers); the same sums in the same order
+    float xv[4], gv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t c = lane + 64 * u;
+      xv[u] = c < p ? x[1 + c] : 0.f;
+      gv[u] = c < p ? GW[j * ldg + c] : 0.f;
+    }
+    const float a = expf(x[0]);
+    for (int z = 1; z < splits; ++z)  // slice order
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (lane + 64 * u < p) gv[u] += GW[(int64_t)z * n * ldg + j * ldg + lane + 64 * u];
+    float w2 = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (lane + 64 * u < p) w2 = fmaf(xv[u], xv[u], w2);
+    w2 = warp_sum(w2);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (lane + 64 * u < p) S[j * lds + 1 + lane + 64 * u] = scale * (gv[u] - (pw * a) * xv[u]);
+    if (lane == 0) S[j * lds] = scale * (pw * (-a + 0.5f * (float)p - 0.5f * a * w2));
+    return;
+  }
   const float a = expf(x[0]);
   float w2 = 0.f;
   for (int64_t c = lane; c < p; c += 64) w2 = fmaf(x[1 + c], x[1 + c], w2);
