@@ -345,6 +345,42 @@ __global__ __launch_bounds__(256) void rowimage_h2_kernel(const float* __restric
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= rows_pad) return;
   const float* row = A + i * lda;
+  const int sw = (int)((i >> 3) & 1);
+  const int k0 = 4 * (lane & 3);
+  const int pos = (k0 < 8 ? 8 * sw : 8 * (sw ^ 1)) + (k0 & 7);
+  if (ksteps <= 16) {
+    // one K-step per lane (kb = lane / 4: columns 4 lane .. 4 lane + 3): the
+    // row read once, every load before the maximum's reduction (the same
+    // maximum, scale and splits)
+    const int64_t kb = lane >> 2;
+    float a[4];
+    uint32_t m = 0u;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t c = kb * 16 + k0 + e;
+      a[e] = (kb < ksteps && i < rows && c < cols) ? row[c] : 0.f;
+      m = max(m, abs_bits(a[e]));
+    }
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    const float sc = pow2_scale(__uint_as_float(m));
+    if (lane == 0) {
+      rscale[i] = sc;
+      rinv[i] = pow2_inv(sc);
+    }
+    if (kb >= ksteps) return;
+    f16x4 h[2];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      _Float16 v[2];
+      split_fmt<FmtH2>(sc * a[e], v);
+      h[0][e] = v[0];
+      h[1][e] = v[1];
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      *reinterpret_cast<f16x4*>(img + ((kb * 2 + p) * rows_pad + i) * 16 + pos) = h[p];
+    return;
+  }
   uint32_t m = 0u;
   if (i < rows)
     for (int64_t c = lane; c < cols; c += 64) m = max(m, abs_bits(row[c]));
@@ -354,9 +390,6 @@ __global__ __launch_bounds__(256) void rowimage_h2_kernel(const float* __restric
     rscale[i] = sc;
     rinv[i] = pow2_inv(sc);
   }
-  const int sw = (int)((i >> 3) & 1);
-  const int k0 = 4 * (lane & 3);
-  const int pos = (k0 < 8 ? 8 * sw : 8 * (sw ^ 1)) + (k0 & 7);
   for (int64_t kb = lane >> 2; kb < ksteps; kb += 16) {
     f16x4 h[2];
 #pragma unroll
